@@ -1,0 +1,187 @@
+"""bench.py -- headline benchmark: full incompressible-flow time steps of the lid-driven
+cavity (BASELINE.json metric "cell-updates/sec (MLUPS) + Poisson iters/sec, 4096^2 grid at
+1/2/4/8 GPUs").
+
+A "step" = one FluidSolver::Solve loop body (/root/reference/SRC/FluidSolver.cpp:546-560):
+RHS (K1) -> Helmholtz u, v (K2 sweeps to rtol) -> divergence (K3) -> Poisson (K4 sweeps to
+rtol 1e-8, warm start) -> correction + min/max (K5), on the 4096^2 cavity (fp64, Re 1000,
+dt = 1/(8n)), inputs resident in HBM.  N > 1: x-slabs, one rank per GPU, RCCL halos
+(strong scaling: the global grid is fixed).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--re 1000] [--no-cpu]
+  (N > 1 under torch.distributed.run; RANK / WORLD_SIZE / LOCAL_RANK from the env)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+POISSON_BYTES_PER_CELL = 24  # read phi, read rhs, write phi
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--re", type=float, default=1000.0)
+    ap.add_argument("--rtol", type=float, default=1e-8)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-sweeps", type=int, default=3)
+    return ap.parse_args()
+
+
+def cpu_baseline(n, re, dt, it_phi, it_v, sweeps):
+    """The oracle (CPU restatement, 1 thread) on a bounded sample of the same workload:
+    one K1 + K3 + K5 pass and `sweeps` Poisson / Helmholtz red-black sweeps on the full
+    n^2 grid; a full step is extrapolated with the GPU run's own sweep counts."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    from oracle import OGrid  # CPU baseline leg only
+
+    g = OGrid.rectangle(n, n)
+    N = g.N
+    rng = np.random.default_rng(0)
+    u, v, phi = rng.uniform(-1, 1, N), rng.uniform(-1, 1, N), rng.uniform(-1, 1, N)
+    cu, cv = np.zeros(N), np.zeros(N)
+    t0 = time.perf_counter()
+    gx, gy = g.grad_phi(phi)
+    ru, rv, cu, cv = g.rhs_velocity(dt, re, u, v, gx, gy, cu, cv)
+    t_k1 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    rp = g.divergence(dt, u, v)
+    g.correct(dt, u, v, phi)
+    t_k35 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    p = phi
+    for _ in range(sweeps):
+        p, _ = g.rbsor_sweep(p, rp, float(rp.mean()), 1.9)
+    t_ps = (time.perf_counter() - t0) / sweeps
+    t0 = time.perf_counter()
+    a, b = u, v
+    for _ in range(max(1, sweeps // 2)):
+        a, b, _ = g.helm_sweep(dt / (2 * re), a, b, ru, rv, 1.0)
+    t_hs = (time.perf_counter() - t0) / max(1, sweeps // 2)
+    t_step = t_k1 + t_k35 + it_phi * t_ps + it_v * t_hs
+    return {
+        "value": N / t_step / 1e6, "unit": "MLUPS", "cores": 1, "kind": "port",
+        "sample": (f"oracle (C restatement, 1 thread) on the {n}^2 grid: K1+K3+K5 once ({t_k1 + t_k35:.2f} s), "
+                   f"{sweeps} Poisson RB-SOR sweeps ({t_ps:.3f} s each), {max(1, sweeps // 2)} Helmholtz "
+                   f"sweeps ({t_hs:.3f} s each); step time extrapolated with the GPU run's average "
+                   f"{it_phi:.0f} Poisson + {it_v:.0f} Helmholtz sweeps/step = {t_step:.1f} s/step"),
+        "poisson_sweeps_per_s": 1.0 / t_ps,
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        world = max(world, 1)
+    import torch
+    import torch.distributed as dist
+
+    import navierstokessolver_amd as nsa
+
+    nccl_id = None
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        idt = torch.zeros(nsa._lib.lib().ns_nccl_id_size(), dtype=torch.uint8)
+        if rank == 0:
+            import ctypes
+            buf = ctypes.create_string_buffer(idt.numel())
+            nsa._lib.check(nsa._lib.lib().ns_nccl_get_id(buf))
+            idt = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
+        dist.broadcast(idt, 0)
+        nccl_id = bytes(idt.tolist())
+
+    n, re = args.n, args.re
+    dt = 1.0 / (8 * n)
+    torch.cuda.set_device(local)
+    solver = nsa.GpuSolver(nsa.cavity(n), dt, re, rtol=args.rtol, device=local, timing=True,
+                           rank=rank, nranks=world, nccl_id=nccl_id)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        solver.step()
+    barrier()
+    t0 = time.perf_counter()
+    stats = [solver.step() for _ in range(args.steps)]
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    K = args.steps
+    cells = n * n
+    sweeps = sum(s["it_phi"] for s in stats)
+    hsweeps = sum(s["it_u"] for s in stats)
+    kms = sum(s["t_poisson_kernel_ms"] for s in stats)
+    kn = sum(s["n_poisson_kernels"] for s in stats)
+    avg_kernel_s = kms / kn / 1e3 if kn else float("nan")
+    local_cells = (solver.i1 - solver.i0) * n
+    achieved = POISSON_BYTES_PER_CELL * local_cells / avg_kernel_s / 1e9
+    value = cells * K / elapsed / 1e6
+
+    if rank != 0:
+        return
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(prof):
+        try:
+            d = json.load(open(prof))
+            if d.get("n") == n and d.get("kernel_bytes_per_launch"):
+                traffic = d["kernel_bytes_per_launch"]
+        except Exception:
+            traffic = None
+    line = {
+        "metric": "cell-updates/sec (MLUPS) + Poisson iters/sec, 4096^2 grid at 1/2/4/8 GPUs",
+        "value": value,
+        "unit": "MLUPS",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (lid-driven cavity from rest, no input files)",
+        "config": {"workload": f"{n}x{n} lid-driven cavity, Re={re:g}, dt=1/{8 * n}, fp64, RB-SOR Poisson "
+                               f"+ RB-GS Helmholtz to rtol {args.rtol:g}",
+                   "nx": n, "ny": n, "re": re, "dt": dt, "parallelism": f"x-slab x{world}"},
+        "poisson_sweeps_per_s": sweeps / elapsed,
+        "poisson_glups": cells * sweeps / elapsed / 1e9,
+        "poisson_sweeps_per_step": sweeps / K,
+        "helmholtz_sweeps_per_step": hsweeps / K,
+        "roofline": {"bound": "hbm", "kernel": "k_rb_sweep<32,128,Poisson> (K4)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic, "avg_kernel_us": avg_kernel_s * 1e6,
+                     "bytes_per_launch": POISSON_BYTES_PER_CELL * local_cells},
+    }
+    if world == 1 and not args.no_cpu:
+        try:
+            line["cpu_baseline"] = cpu_baseline(n, re, dt, sweeps / K, hsweeps / K, args.cpu_sweeps)
+        except Exception as e:  # the baseline must never hide the GPU line
+            line["cpu_baseline"] = {"error": repr(e)}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

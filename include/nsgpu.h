@@ -1,0 +1,168 @@
+/*
+ * nsgpu.h -- C-ABI of libnsgpu.so, the MI355X (gfx950) implementation of the
+ * shivams15/navierstokessolver hot path: FluidSolver::Solve's
+ * advect / diffuse / project time step and its pressure-Poisson solve.
+ *
+ * Plain C types only (no torch / HIP types), so the reference-side host code
+ * (navierstokessolver_amd/host/FluidSolver.cpp, ctypes in Python, ...) can bind
+ * it directly.  Each entry point names the reference interface it replaces
+ * (/root/reference/SRC/<file>:<line>).
+ *
+ * Conventions
+ *   - every call returns 0 on success and a negative NS_E* code on failure;
+ *     ns_last_error() holds the message (thread-local).  Nothing throws or aborts.
+ *   - the caller owns all host buffers; the library copies them.
+ *   - one host thread drives one ns_solver (handles are not thread-safe).
+ *   - fields are exchanged in the reference's compact cell-id order
+ *     (i outer / x, j inner / y: Grid.cpp:149-162).  With nranks > 1 each rank
+ *     exchanges its own x-slab (global rows ns_slab_range()).
+ *   - all state lives in HBM; ns_step() synchronises with the host once per
+ *     residual check and once at the end of the step (its ns_stats), mirroring
+ *     the reference's per-step printf (FluidSolver.cpp:554-560).
+ */
+#ifndef NSGPU_H
+#define NSGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NSGPU_ABI_VERSION 1
+
+typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm */
+
+/* status codes */
+#define NS_OK        0
+#define NS_EINVAL   -1  /* bad argument / unsupported configuration */
+#define NS_EHIP     -2  /* HIP runtime failure */
+#define NS_ERCCL    -3  /* RCCL failure */
+#define NS_ENOMEM   -4
+#define NS_EDIVERGE -5  /* non-finite values / solver did not converge */
+
+/* boundary-condition types: bcTypes, Grid.h:6 */
+#define NS_BC_INLET_UNI       0
+#define NS_BC_INLET_PARABOLIC 1  /* rejected: empty ghost constant in the reference (FluidSolver.cpp:86-87,171) */
+#define NS_BC_WALL            2
+#define NS_BC_PRESSURE        3  /* rejected: no ghost stencil in the reference (FluidSolver.cpp:150,168) */
+#define NS_BC_NEUMANN         4
+
+/* Poisson solvers */
+#define NS_POISSON_RBSOR  0  /* fused red-black SOR, one HBM pass per sweep (default) */
+#define NS_POISSON_JACOBI 1  /* weighted Jacobi (ping-pong) */
+
+/* One boundary edge of the polygon (Edge, Grid.h:20-26). */
+typedef struct ns_edge {
+    int32_t nx, ny;   /* outward normal, one of (+-1,0),(0,+-1) */
+    int32_t type;     /* NS_BC_* */
+    double  info;     /* bcInfo: wall tangential speed / inlet speed */
+} ns_edge;
+
+/* Grid geometry (replaces the Grid object FluidSolver reads, Grid.h:42-69).
+ * This version accepts rectangular domains: cell_id == NULL and the four
+ * sides W,E,S,N each covered by exactly one edge (found by its normal). */
+typedef struct ns_grid_desc {
+    int32_t nx, ny;           /* cells in x and y (Grid::hx.size(), hy.size()) */
+    const double* hx;         /* nx spacings (Grid::hx) */
+    const double* hy;         /* ny spacings (Grid::hy) */
+    int32_t n_edges;
+    const ns_edge* edges;     /* Grid::edges, in vertex order */
+    const int32_t* cell_id;   /* nx*ny ids or -1 (outside); NULL = full rectangle */
+} ns_grid_desc;
+
+typedef struct ns_params {
+    double  dt;               /* FluidSolver::dt */
+    double  re;               /* FluidSolver::re */
+    int32_t poisson;          /* NS_POISSON_* */
+    double  rtol;             /* relative residual tolerance of each solve (reference: 1e-8, FluidSolver.cpp:68,80) */
+    int32_t max_iters;        /* sweep cap per solve (0 = 200000) */
+    double  omega;            /* Poisson SOR/Jacobi weight (0 = automatic) */
+    double  omega_v;          /* Helmholtz SOR weight (0 = 1.0) */
+    int32_t check_every;      /* sweeps between residual checks (0 = automatic) */
+    int32_t device;           /* HIP device ordinal (-1 = current / LOCAL_RANK) */
+    int32_t timing;           /* 1 = time every Poisson sweep kernel with HIP events */
+    /* x-slab decomposition over ranks (one process per GPU) */
+    int32_t rank, nranks;
+    const void* nccl_id;      /* 128-byte ncclUniqueId from rank 0 (NULL if nranks == 1) */
+} ns_params;
+
+/* Per-step result (the reference prints iter, umin, umax, vmin, vmax: FluidSolver.cpp:559-560). */
+typedef struct ns_stats {
+    double  umin, umax, vmin, vmax;
+    int32_t it_u, it_v, it_phi;      /* sweeps used by the two Helmholtz solves and the Poisson solve */
+    double  res_u, res_v, res_phi;   /* final relative residuals (of the input of the last sweep) */
+    double  t_poisson_kernel_ms;     /* sum of Poisson sweep-kernel durations (timing == 1) */
+    int32_t n_poisson_kernels;       /* number of Poisson sweep kernels timed */
+    int32_t n_checks;                /* residual checks (host syncs) in the step */
+} ns_stats;
+
+/* device arrays addressable by ns_get_array / ns_set_array */
+#define NS_ARR_U     0  /* u (u* between K2 and K5) */
+#define NS_ARR_V     1
+#define NS_ARR_PHI   2
+#define NS_ARR_CU    3  /* convective derivative of the previous step (convectiveDer_u0) */
+#define NS_ARR_CV    4
+#define NS_ARR_RU    5  /* RHS_u */
+#define NS_ARR_RV    6
+#define NS_ARR_RPHI  7  /* RHS_phi (div u* / dt, before mean removal) */
+#define NS_ARR_TMP   8  /* Jacobi ping-pong partner */
+#define NS_NUM_ARR   9
+
+/* kernels addressable by ns_kernel */
+#define NS_K_RHS        1  /* K1 rhs_velocity            (ConstructRHS_V, FluidSolver.cpp:327-363) */
+#define NS_K_HELMHOLTZ  2  /* K2 helmholtz sweep x iters  (KSPSolve(uSolver) x2, :547-548) */
+#define NS_K_DIV        3  /* K3 divergence + sums        (ConstructRHS_phi, :365-378) */
+#define NS_K_POISSON    4  /* K4 Poisson sweep x iters    (KSPSolve(phiSolver), :551) */
+#define NS_K_CORRECT    5  /* K5 correct + min/max        (CorrectVelocities, :512-534) */
+#define NS_K_HELM_SOLVE 6  /* converged Helmholtz solve   (:547-548) */
+#define NS_K_POIS_SOLVE 7  /* converged Poisson solve incl. null-space removal (:550-551) */
+#define NS_K_RESIDUAL   8  /* Poisson residual ||rhs - mean - L phi||^2 -> out[0] (no update) */
+
+/* ---- lifecycle: FluidSolver(char*, Grid*) = SolverInitialize + SolverSetup (FluidSolver.cpp:8-58) ---- */
+int  ns_create(const ns_grid_desc* grid, const ns_params* params, ns_solver** out);
+void ns_destroy(ns_solver* s);
+
+/* ---- one full time step: the body of FluidSolver::Solve's loop (FluidSolver.cpp:546-560) ---- */
+int  ns_step(ns_solver* s, ns_stats* out);
+
+/* ---- state access (host buffers, local slab, compact-id order) ---- */
+int  ns_get_fields(ns_solver* s, double* u, double* v, double* phi);
+int  ns_set_fields(ns_solver* s, const double* u, const double* v, const double* phi,
+                   const double* cu0, const double* cv0);
+int  ns_get_array(ns_solver* s, int which, double* host);
+int  ns_set_array(ns_solver* s, int which, const double* host);
+
+/* ---- individual kernels (tests and bench) ----
+ * out (may be NULL) receives kernel-specific scalars:
+ *   NS_K_HELMHOLTZ / NS_K_POISSON: out[0] = residual^2 of the last sweep's input
+ *   NS_K_DIV:     out[0] = sum rhs, out[1] = sum rhs^2
+ *   NS_K_CORRECT: out[0..3] = umin, umax, vmin, vmax
+ *   NS_K_*_SOLVE: out[0] = sweeps used, out[1] = final relative residual
+ *   NS_K_RESIDUAL: out[0] = residual^2 */
+int  ns_kernel(ns_solver* s, int which, int iters, double* out);
+
+/* Fill phi and rhs_phi with reproducible uniform [-1,1) values generated on the
+ * device (splitmix64 of (seed, global cell)), rhs mean-removed: the sweep benchmark input. */
+int  ns_fill_random(ns_solver* s, uint64_t seed);
+
+/* Time `iters` Poisson sweep kernels (after `warmup`) with HIP events on the
+ * solver's stream: out[0] = average kernel ms, out[1] = total ms. */
+int  ns_time_poisson(ns_solver* s, int warmup, int iters, double* out);
+
+/* ---- host-side helpers (no GPU needed) ---- */
+/* the x-slab [i0, i1) of `rank` out of `nranks` for nx cells */
+int  ns_slab_range(int32_t nx, int32_t nranks, int32_t rank, int32_t* i0, int32_t* i1);
+/* size in bytes of an ncclUniqueId, and produce one (rank 0 only; needs RCCL, no GPU) */
+int  ns_nccl_id_size(void);
+int  ns_nccl_get_id(void* out128);
+/* device bytes one solver allocates for this grid */
+int64_t ns_device_bytes(int32_t nx_local, int32_t ny);
+/* version / last error */
+int  ns_abi_version(void);
+const char* ns_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NSGPU_H */

@@ -1,0 +1,72 @@
+// ns_internal.h -- shared between the gfx950 kernels (ns_kernels.hip) and the
+// C-ABI / orchestration layer (ns_solver.cpp).  Not installed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace nsg {
+
+constexpr int HALO = 2;  // ghost rows per side of every field (K1's MUSCL stencil is radius 2)
+
+// Geometry of one x-slab.  Fields are (nxl + 2*HALO) rows of ld doubles, j contiguous;
+// pointers handed to kernels point at local row 0.  Global row = i0 + local row.
+struct Geo {
+    int nx, ny;       // global cells
+    int i0, nxl;      // slab start (global) and local rows
+    int ld;           // row stride in doubles (ny rounded up to 32)
+    // rectangle sides 0=W,1=E,2=S,3=N: velocity ghost q_g = neu ? q : -q + c[d]
+    // (EvaluateGhostStencil_V, FluidSolver.cpp:166-173; constants :89-96)
+    int neu[4];
+    double c0[4], c1[4];
+    int enx[4], eny[4];  // outward normal of the edge on that side
+};
+
+// 1-D coefficient tables (global index) built once from hx, hy (ConstructLHS, FluidSolver.cpp:113-131)
+struct Coef {
+    const double *hx, *hy;          // spacings
+    const double *pw, *pe, *ps, *pn; // 2/(h (h+h_nb)) toward an existing neighbour, 0 at the boundary
+    const double *bx, *by;          // Helmholtz Dirichlet boundary-face diagonal term 2/h^2 (0 inside)
+};
+
+struct Partials {
+    double* p;      // per-block partials
+    int n;          // number of blocks written
+};
+
+// ---- launchers (all asynchronous on `st`) ----
+// K1: rhs_velocity (ConstructRHS_V); partials (sum ru^2, sum rv^2) per block
+int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
+               const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st);
+// K2: fused red-black SOR sweep of (I - a L_V) on u and v; residual^2 partials (u, v) if part != null
+int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, double* u, double* v,
+                      const double* ru, const double* rv, double* part, hipStream_t st);
+// K3: divergence / dt  + partial sums (sum, sum^2)
+int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* rp,
+               double* part, hipStream_t st);
+// K4: fused red-black SOR Poisson sweep (in place); residual^2 partials of the input iterate
+int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, double* phi, const double* rp,
+                      const double* shift, double* part, hipStream_t st);
+// K4 Jacobi: out = in + w (b - shift - L in)/diag
+int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* in, double* out,
+                       const double* rp, const double* shift, double* part, hipStream_t st);
+// residual only
+int launch_pois_residual(const Geo& g, const Coef& c, const double* phi, const double* rp,
+                         const double* shift, double* part, hipStream_t st);
+// K5: u = u* - dt grad phi ; min/max partials (4 per block)
+int launch_correct(const Geo& g, const Coef& c, double dt, double* u, double* v, const double* phi,
+                   double* part, hipStream_t st);
+// reductions: sum `nv` interleaved values over n partials (p[k*nv + v]) -> out[v]
+void launch_reduce_sum(const double* p, int n, int nv, double* out, hipStream_t st);
+// min/max: partials are (umin, -umax, vmin, -vmax) per block -> out[4] = mins of each
+void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t st);
+// Poisson prep: from sums (S, S2) and N -> shift = S/N, out[1] = S2 - S^2/N (= ||b||^2)
+void launch_finish_mean(const double* sums, double ncells, double* shift_and_bn2, hipStream_t st);
+// (sum f, sum f^2) partials over own cells
+int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st);
+// random fill of phi, rhs (sweep benchmark input)
+void launch_fill_random(const Geo& g, double* phi, double* rp, uint64_t seed, hipStream_t st);
+
+// max partials any launcher writes for this geometry
+int max_partials(const Geo& g);
+
+}  // namespace nsg

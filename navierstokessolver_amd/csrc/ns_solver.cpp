@@ -1,0 +1,700 @@
+// ns_solver.cpp -- C-ABI (include/nsgpu.h) and time-step orchestration of libnsgpu.so.
+//
+// One ns_solver = one x-slab on one MI355X: all fields resident in HBM, one HIP
+// stream, and (nranks > 1) one RCCL communicator whose neighbour send/recv pairs
+// move contiguous ghost rows over xGMI.  The step mirrors FluidSolver::Solve's
+// loop body (/root/reference/SRC/FluidSolver.cpp:546-560):
+//   K1 rhs -> K2 Helmholtz sweeps (u, v) -> K3 div -> null-space mean -> K4
+//   Poisson sweeps -> K5 correct + min/max.
+// The reference's Krylov solves (GMRES+ILU, BCGSL+BJacobi, rtol 1e-8,
+// FluidSolver.cpp:61-82) are replaced by red-black SOR sweeps run to the same
+// relative-residual tolerance, checked every few sweeps from a fused residual.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/nsgpu.h"
+#include "ns_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+#define HIPCHK(x)                                                                        \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) {                                                          \
+            set_err("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return NS_EHIP;                                                              \
+        }                                                                                \
+    } while (0)
+
+#define NCCLCHK(x)                                                                          \
+    do {                                                                                    \
+        ncclResult_t r_ = (x);                                                              \
+        if (r_ != ncclSuccess) {                                                            \
+            set_err("%s failed: %s (%s:%d)", #x, ncclGetErrorString(r_), __FILE__, __LINE__); \
+            return NS_ERCCL;                                                                \
+        }                                                                                   \
+    } while (0)
+
+#define CHK(x)                 \
+    do {                       \
+        int rc_ = (x);         \
+        if (rc_ != 0) return rc_; \
+    } while (0)
+
+// device scalar slots
+enum {
+    S_DIVSUM = 0,   // 2: sum rhs, sum rhs^2
+    S_SHIFT = 2,    // 2: mean, ||rhs - mean||^2
+    S_HBN = 4,      // 2: ||ru||^2, ||rv||^2
+    S_RES = 6,      // 2: residual^2 (u, v) or (phi, -)
+    S_MM = 8,       // 4: umin, -umax, vmin, -vmax
+    S_AUX = 12,     // 4
+    S_NUM = 16
+};
+
+}  // namespace
+
+struct ns_solver {
+    nsg::Geo g{};
+    nsg::Coef c{};
+    int device = 0;
+    hipStream_t st = nullptr;
+    double dt = 0, re = 0, rtol = 1e-8, omega = 0, omega_v = 1.0;
+    int poisson = NS_POISSON_RBSOR, max_iters = 200000, check_every = 0, timing = 0;
+    double* base = nullptr;      // all fields
+    size_t plane = 0;            // doubles per field plane
+    double* arr[NS_NUM_ARR] = {};  // pointer to local row 0 of each field
+    double* coef = nullptr;      // device coefficient tables
+    double* part = nullptr;      // per-block partials
+    double* scal = nullptr;      // device scalars
+    double* hs = nullptr;        // pinned host mirror of scal
+    int rank = 0, nranks = 1;
+    ncclComm_t comm = nullptr;
+    double ncells = 0;           // global cell count
+    std::vector<hipEvent_t> ev;  // timing events (pairs)
+    int helm_batch0 = 4, pois_batch0 = 8;
+};
+
+namespace {
+
+int halo(ns_solver* s, std::initializer_list<double*> fields, int w) {
+    if (s->nranks == 1) return 0;
+    const size_t cnt = (size_t)w * s->g.ld;
+    const int ld = s->g.ld, nxl = s->g.nxl;
+    NCCLCHK(ncclGroupStart());
+    for (double* f : fields) {
+        if (s->rank > 0) {
+            NCCLCHK(ncclSend(f, cnt, ncclDouble, s->rank - 1, s->comm, s->st));
+            NCCLCHK(ncclRecv(f - (ptrdiff_t)w * ld, cnt, ncclDouble, s->rank - 1, s->comm, s->st));
+        }
+        if (s->rank < s->nranks - 1) {
+            NCCLCHK(ncclSend(f + (ptrdiff_t)(nxl - w) * ld, cnt, ncclDouble, s->rank + 1, s->comm, s->st));
+            NCCLCHK(ncclRecv(f + (ptrdiff_t)nxl * ld, cnt, ncclDouble, s->rank + 1, s->comm, s->st));
+        }
+    }
+    NCCLCHK(ncclGroupEnd());
+    return 0;
+}
+
+int allreduce(ns_solver* s, double* d, int n, ncclRedOp_t op) {
+    if (s->nranks == 1) return 0;
+    NCCLCHK(ncclAllReduce(d, d, n, ncclDouble, op, s->comm, s->st));
+    return 0;
+}
+
+// copy all device scalars to the host and wait: the only host syncs of a step
+int fetch(ns_solver* s) {
+    HIPCHK(hipMemcpyAsync(s->hs, s->scal, S_NUM * sizeof(double), hipMemcpyDeviceToHost, s->st));
+    HIPCHK(hipStreamSynchronize(s->st));
+    return 0;
+}
+
+int ensure_events(ns_solver* s, size_t n) {
+    while (s->ev.size() < n) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        s->ev.push_back(e);
+    }
+    return 0;
+}
+
+int next_batch(int prev_batch, double prev_r2, int prev_at, double r2, int at, double tol2, int cap) {
+    // geometric model of the residual contraction between two checks
+    if (prev_r2 > 0 && r2 > 0 && r2 < prev_r2 && at > prev_at) {
+        const double rate = std::log(r2 / prev_r2) / (double)(at - prev_at);  // < 0
+        const double need = std::log(tol2 / r2) / rate;
+        int b = (int)std::ceil(need) + 1;
+        b = std::max(b, 2);
+        b = std::min(b, std::max(64, 4 * prev_batch));
+        return std::min(b, cap);
+    }
+    return std::min(std::max(prev_batch, 2) * 2, cap);
+}
+
+// ---------------- Helmholtz (I - a L_V) u* = RHS_u, v* likewise (KSPSolve(uSolver), FluidSolver.cpp:547-548)
+// Initial guess u^n (in place): converged solution is the same; fewer sweeps than the reference's zero guess.
+int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
+    const double alpha = s->dt / (2 * s->re);
+    double* u = s->arr[NS_ARR_U];
+    double* v = s->arr[NS_ARR_V];
+    const double tol2 = s->rtol * s->rtol;
+    int sweeps = 0, batch = s->helm_batch0, prev_at = -1;
+    double prev_r2 = -1;
+    for (;;) {
+        const int n = std::min(batch, s->max_iters - sweeps);
+        int nb = 0;
+        for (int k = 0; k < n; k++) {
+            CHK(halo(s, {u, v}, 2));
+            nb = nsg::launch_helm_sweep(s->g, s->c, alpha, s->omega_v, u, v, s->arr[NS_ARR_RU], s->arr[NS_ARR_RV],
+                                        k == n - 1 ? s->part : nullptr, s->st);
+        }
+        sweeps += n;
+        nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_RES, s->st);
+        CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
+        CHK(fetch(s));
+        const double r2u = s->hs[S_RES], r2v = s->hs[S_RES + 1];
+        const double bu = s->hs[S_HBN], bv = s->hs[S_HBN + 1];
+        const bool ok = (r2u <= tol2 * bu || r2u == 0.0) && (r2v <= tol2 * bv || r2v == 0.0);
+        *resu = bu > 0 ? std::sqrt(r2u / bu) : std::sqrt(r2u);
+        *resv = bv > 0 ? std::sqrt(r2v / bv) : std::sqrt(r2v);
+        if (!std::isfinite(r2u) || !std::isfinite(r2v)) { set_err("Helmholtz residual is not finite"); *its = sweeps; return NS_EDIVERGE; }
+        if (ok || sweeps >= s->max_iters) break;
+        const double r2 = std::max(r2u / std::max(bu, 1e-300), r2v / std::max(bv, 1e-300));
+        const int nbatch = next_batch(batch, prev_r2, prev_at, r2, sweeps - 1, tol2, s->max_iters);
+        prev_r2 = r2;
+        prev_at = sweeps - 1;
+        batch = nbatch;
+    }
+    *its = sweeps;
+    return 0;
+}
+
+// ---------------- Poisson L phi = rhs - mean  (MatNullSpaceRemove + KSPSolve(phiSolver), FluidSolver.cpp:550-551)
+// Warm start from phi^{n-1} (KSPSetInitialGuessNonzero, :54).  Expects S_SHIFT set.
+int pois_solve(ns_solver* s, int* its, double* res, ns_stats* stt) {
+    const double tol2 = s->rtol * s->rtol;
+    int sweeps = 0, batch = s->pois_batch0, prev_at = -1;
+    double prev_r2 = -1;
+    const double* shift = s->scal + S_SHIFT;
+    double tms = 0.0;
+    int tn = 0, nchk = 0;
+    for (;;) {
+        const int n = std::min(batch, s->max_iters - sweeps);
+        if (s->timing) CHK(ensure_events(s, 2 * (size_t)n));
+        int nb = 0;
+        for (int k = 0; k < n; k++) {
+            double* part = k == n - 1 ? s->part : nullptr;
+            CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
+            if (s->timing) HIPCHK(hipEventRecord(s->ev[2 * k], s->st));
+            if (s->poisson == NS_POISSON_JACOBI) {
+                nb = nsg::launch_pois_jacobi(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP],
+                                             s->arr[NS_ARR_RPHI], shift, part ? part : s->part, s->st);
+                std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
+            } else {
+                nb = nsg::launch_pois_rbsor(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], shift,
+                                            part, s->st);
+            }
+            if (s->timing) HIPCHK(hipEventRecord(s->ev[2 * k + 1], s->st));
+        }
+        sweeps += n;
+        nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
+        CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
+        CHK(fetch(s));
+        nchk++;
+        if (s->timing) {
+            for (int k = 0; k < n; k++) {
+                float ms = 0.f;
+                HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
+                tms += ms;
+            }
+            tn += n;
+        }
+        const double r2 = s->hs[S_RES], b2 = s->hs[S_SHIFT + 1];
+        *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
+        if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = sweeps; return NS_EDIVERGE; }
+        if (r2 <= tol2 * b2 || r2 == 0.0 || sweeps >= s->max_iters) break;
+        const double rr = r2 / b2;
+        const int nbatch = next_batch(batch, prev_r2, prev_at, rr, sweeps - 1, tol2, s->max_iters);
+        prev_r2 = rr;
+        prev_at = sweeps - 1;
+        batch = nbatch;
+    }
+    *its = sweeps;
+    if (stt) {
+        stt->t_poisson_kernel_ms += tms;
+        stt->n_poisson_kernels += tn;
+        stt->n_checks += nchk;
+    }
+    return 0;
+}
+
+// K3 + null-space mean
+int divergence(ns_solver* s) {
+    const int nb = nsg::launch_div(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_RPHI],
+                                   s->part, s->st);
+    nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_DIVSUM, s->st);
+    CHK(allreduce(s, s->scal + S_DIVSUM, 2, ncclSum));
+    nsg::launch_finish_mean(s->scal + S_DIVSUM, s->ncells, s->scal + S_SHIFT, s->st);
+    return 0;
+}
+
+// sums of an arbitrary RHS_phi -> null-space shift (standalone solves / sweep benchmark)
+int rhs_mean(ns_solver* s) {
+    const int nb = nsg::launch_sums(s->g, s->arr[NS_ARR_RPHI], s->part, s->st);
+    nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_DIVSUM, s->st);
+    CHK(allreduce(s, s->scal + S_DIVSUM, 2, ncclSum));
+    nsg::launch_finish_mean(s->scal + S_DIVSUM, s->ncells, s->scal + S_SHIFT, s->st);
+    return 0;
+}
+
+// ||RHS_u||^2, ||RHS_v||^2 of arbitrary RHS arrays (standalone Helmholtz solve)
+int helm_bnorm(ns_solver* s) {
+    int nb = nsg::launch_sums(s->g, s->arr[NS_ARR_RU], s->part, s->st);
+    nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_AUX, s->st);
+    nb = nsg::launch_sums(s->g, s->arr[NS_ARR_RV], s->part, s->st);
+    nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_AUX + 2, s->st);
+    CHK(allreduce(s, s->scal + S_AUX, 4, ncclSum));
+    HIPCHK(hipMemcpyAsync(s->scal + S_HBN, s->scal + S_AUX + 1, sizeof(double), hipMemcpyDeviceToDevice, s->st));
+    HIPCHK(hipMemcpyAsync(s->scal + S_HBN + 1, s->scal + S_AUX + 3, sizeof(double), hipMemcpyDeviceToDevice, s->st));
+    return 0;
+}
+
+int rhs(ns_solver* s) {
+    const int nb = nsg::launch_rhs(s->g, s->c, s->dt, s->re, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_PHI],
+                                   s->arr[NS_ARR_CU], s->arr[NS_ARR_CV], s->arr[NS_ARR_RU], s->arr[NS_ARR_RV],
+                                   s->part, s->st);
+    nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_HBN, s->st);
+    CHK(allreduce(s, s->scal + S_HBN, 2, ncclSum));
+    return 0;
+}
+
+int correct(ns_solver* s) {
+    const int nb = nsg::launch_correct(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_PHI],
+                                       s->part, s->st);
+    nsg::launch_reduce_min(s->part, nb, 4, s->scal + S_MM, s->st);
+    CHK(allreduce(s, s->scal + S_MM, 4, ncclMin));
+    return 0;
+}
+
+int check_arr(ns_solver* s, int which) {
+    if (!s) { set_err("null solver"); return NS_EINVAL; }
+    if (which < 0 || which >= NS_NUM_ARR) { set_err("bad array index %d", which); return NS_EINVAL; }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ns_last_error(void) { return g_err.c_str(); }
+int ns_abi_version(void) { return NSGPU_ABI_VERSION; }
+
+int ns_slab_range(int32_t nx, int32_t nranks, int32_t rank, int32_t* i0, int32_t* i1) {
+    if (nx <= 0 || nranks <= 0 || rank < 0 || rank >= nranks) { set_err("bad slab arguments"); return NS_EINVAL; }
+    const int base = nx / nranks, rem = nx % nranks;
+    const int a = rank * base + std::min(rank, rem);
+    *i0 = a;
+    *i1 = a + base + (rank < rem ? 1 : 0);
+    return 0;
+}
+
+int ns_nccl_id_size(void) { return (int)sizeof(ncclUniqueId); }
+
+int ns_nccl_get_id(void* out) {
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    std::memcpy(out, &id, sizeof id);
+    return 0;
+}
+
+int64_t ns_device_bytes(int32_t nxl, int32_t ny) {
+    const int64_t ld = ((int64_t)ny + 31) / 32 * 32;
+    return (int64_t)NS_NUM_ARR * (nxl + 2 * nsg::HALO) * ld * 8;
+}
+
+int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
+    if (!gd || !p || !out) { set_err("null argument"); return NS_EINVAL; }
+    *out = nullptr;
+    if (gd->cell_id) {
+        set_err("non-rectangular domains (cell_id mask) are not supported by this build");
+        return NS_EINVAL;
+    }
+    if (gd->nx < 2 || gd->ny < 2) { set_err("one-cell-thick geometry is not supported (FluidSolver.cpp:470-477)"); return NS_EINVAL; }
+    if (!gd->hx || !gd->hy) { set_err("hx/hy missing"); return NS_EINVAL; }
+    if (!(p->dt > 0)) { set_err("Time step should be positive"); return NS_EINVAL; }
+    if (!(p->re > 0)) { set_err("Reynolds number should be positive"); return NS_EINVAL; }
+    if (p->nranks < 1 || p->rank < 0 || p->rank >= p->nranks) { set_err("bad rank/nranks"); return NS_EINVAL; }
+    if (p->nranks > 1 && !p->nccl_id) { set_err("nranks > 1 needs an ncclUniqueId"); return NS_EINVAL; }
+    if (p->poisson != NS_POISSON_RBSOR && p->poisson != NS_POISSON_JACOBI) { set_err("unknown Poisson solver %d", p->poisson); return NS_EINVAL; }
+
+    nsg::Geo g{};
+    g.nx = gd->nx;
+    g.ny = gd->ny;
+    g.ld = (gd->ny + 31) / 32 * 32;
+    int32_t i0, i1;
+    if (ns_slab_range(gd->nx, p->nranks, p->rank, &i0, &i1)) return NS_EINVAL;
+    g.i0 = i0;
+    g.nxl = i1 - i0;
+    if (p->nranks > 1 && g.nxl < 2 * nsg::HALO) {
+        set_err("slab of %d rows is thinner than the %d-row halo exchange", g.nxl, 2 * nsg::HALO);
+        return NS_EINVAL;
+    }
+    // sides from edge normals (a rectangle: Grid.cpp:35-63 gives one edge per side)
+    const int snx[4] = {-1, 1, 0, 0}, sny[4] = {0, 0, -1, 1};
+    int side_edge[4] = {-1, -1, -1, -1};
+    for (int e = 0; e < gd->n_edges; e++) {
+        const ns_edge& E = gd->edges[e];
+        for (int k = 0; k < 4; k++)
+            if (E.nx == snx[k] && E.ny == sny[k]) {
+                if (side_edge[k] >= 0) { set_err("side %d has more than one edge: not a rectangle", k); return NS_EINVAL; }
+                side_edge[k] = e;
+            }
+    }
+    for (int k = 0; k < 4; k++) {
+        if (side_edge[k] < 0) { set_err("side %d has no edge: not a rectangle", k); return NS_EINVAL; }
+        const ns_edge& E = gd->edges[side_edge[k]];
+        g.enx[k] = E.nx;
+        g.eny[k] = E.ny;
+        g.c0[k] = g.c1[k] = 0.0;
+        g.neu[k] = 0;
+        // ConstructGhostStencils (FluidSolver.cpp:84-103)
+        if (E.type == NS_BC_INLET_UNI) {
+            if (E.nx == 0) g.c1[k] = 2 * E.info; else g.c0[k] = 2 * E.info;
+        } else if (E.type == NS_BC_WALL) {
+            if (E.nx != 0) g.c1[k] = 2 * E.info; else g.c0[k] = 2 * E.info;
+        } else if (E.type == NS_BC_NEUMANN) {
+            set_err("NEUMANN outflow edges are not supported by this build's Poisson kernels");
+            return NS_EINVAL;
+        } else {
+            set_err("edge %d: boundary condition type %d is not supported (INLET_PARABOLIC / PRESSURE / unset "
+                    "have no ghost stencil in the reference)", side_edge[k], E.type);
+            return NS_EINVAL;
+        }
+    }
+
+    ns_solver* s = new ns_solver();
+    s->g = g;
+    s->dt = p->dt;
+    s->re = p->re;
+    s->rtol = p->rtol > 0 ? p->rtol : 1e-8;
+    s->poisson = p->poisson;
+    s->max_iters = p->max_iters > 0 ? p->max_iters : 200000;
+    const int nmax = std::max(gd->nx, gd->ny);
+    const double pi = 3.14159265358979323846;
+    s->omega = p->omega > 0 ? p->omega
+                            : (p->poisson == NS_POISSON_RBSOR ? 2.0 / (1.0 + std::sin(pi / nmax)) : 0.9);
+    s->omega_v = p->omega_v > 0 ? p->omega_v : 1.0;
+    s->check_every = p->check_every;
+    if (p->check_every > 0) s->pois_batch0 = s->helm_batch0 = p->check_every;
+    s->timing = p->timing;
+    s->rank = p->rank;
+    s->nranks = p->nranks;
+    s->ncells = (double)gd->nx * (double)gd->ny;
+
+    auto fail = [&](int rc) { ns_destroy(s); return rc; };
+    int dev = p->device;
+    if (dev < 0) {
+        const char* lr = getenv("LOCAL_RANK");
+        dev = lr ? atoi(lr) : 0;
+    }
+    s->device = dev;
+    if (hipSetDevice(dev) != hipSuccess) { set_err("hipSetDevice(%d) failed", dev); return fail(NS_EHIP); }
+    if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); return fail(NS_EHIP); }
+
+    s->plane = (size_t)(g.nxl + 2 * nsg::HALO) * g.ld;
+    if (hipMalloc(&s->base, s->plane * NS_NUM_ARR * sizeof(double)) != hipSuccess) {
+        set_err("hipMalloc of %zu bytes failed", s->plane * NS_NUM_ARR * sizeof(double));
+        return fail(NS_ENOMEM);
+    }
+    if (hipMemsetAsync(s->base, 0, s->plane * NS_NUM_ARR * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
+    for (int k = 0; k < NS_NUM_ARR; k++) s->arr[k] = s->base + k * s->plane + (size_t)nsg::HALO * g.ld;
+
+    // coefficient tables (ConstructLHS, FluidSolver.cpp:113-131)
+    const int nx = g.nx, ny = g.ny;
+    std::vector<double> h(3 * nx + 3 * ny + nx + ny, 0.0);
+    double *pw = h.data(), *pe = pw + nx, *bx = pe + nx, *ps = bx + nx, *pn = ps + ny, *by = pn + ny;
+    double *hx = by + ny, *hy = hx + nx;
+    for (int i = 0; i < nx; i++) {
+        const double a = gd->hx[i];
+        if (!(a > 0)) { set_err("hx[%d] = %g is not positive", i, a); return fail(NS_EINVAL); }
+        hx[i] = a;
+        pw[i] = i > 0 ? 2.0 / (a * (a + gd->hx[i - 1])) : 0.0;
+        pe[i] = i < nx - 1 ? 2.0 / (a * (a + gd->hx[i + 1])) : 0.0;
+        bx[i] = (i == 0 ? 2.0 / (a * a) : 0.0) + (i == nx - 1 ? 2.0 / (a * a) : 0.0);
+    }
+    for (int j = 0; j < ny; j++) {
+        const double a = gd->hy[j];
+        if (!(a > 0)) { set_err("hy[%d] = %g is not positive", j, a); return fail(NS_EINVAL); }
+        hy[j] = a;
+        ps[j] = j > 0 ? 2.0 / (a * (a + gd->hy[j - 1])) : 0.0;
+        pn[j] = j < ny - 1 ? 2.0 / (a * (a + gd->hy[j + 1])) : 0.0;
+        by[j] = (j == 0 ? 2.0 / (a * a) : 0.0) + (j == ny - 1 ? 2.0 / (a * a) : 0.0);
+    }
+    if (hipMalloc(&s->coef, h.size() * sizeof(double)) != hipSuccess) { set_err("hipMalloc coef failed"); return fail(NS_ENOMEM); }
+    if (hipMemcpy(s->coef, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) { set_err("coef upload failed"); return fail(NS_EHIP); }
+    {
+        double* d = s->coef;
+        s->c.pw = d; s->c.pe = d + nx; s->c.bx = d + 2 * nx;
+        s->c.ps = d + 3 * nx; s->c.pn = d + 3 * nx + ny; s->c.by = d + 3 * nx + 2 * ny;
+        s->c.hx = d + 3 * nx + 3 * ny; s->c.hy = d + 4 * nx + 3 * ny;
+    }
+    const int np = nsg::max_partials(g);
+    if (hipMalloc(&s->part, (size_t)np * 4 * sizeof(double)) != hipSuccess) { set_err("hipMalloc partials failed"); return fail(NS_ENOMEM); }
+    if (hipMalloc(&s->scal, S_NUM * sizeof(double)) != hipSuccess) { set_err("hipMalloc scalars failed"); return fail(NS_ENOMEM); }
+    if (hipMemsetAsync(s->scal, 0, S_NUM * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
+    if (hipHostMalloc(&s->hs, S_NUM * sizeof(double), hipHostMallocDefault) != hipSuccess) { set_err("hipHostMalloc failed"); return fail(NS_ENOMEM); }
+
+    if (s->nranks > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, p->nccl_id, sizeof id);
+        ncclResult_t r = ncclCommInitRank(&s->comm, s->nranks, id, s->rank);
+        if (r != ncclSuccess) { set_err("ncclCommInitRank: %s", ncclGetErrorString(r)); return fail(NS_ERCCL); }
+    }
+    if (hipStreamSynchronize(s->st) != hipSuccess) { set_err("sync failed"); return fail(NS_EHIP); }
+    *out = s;
+    return 0;
+}
+
+void ns_destroy(ns_solver* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    if (s->st) (void)hipStreamSynchronize(s->st);
+    if (s->comm) (void)ncclCommDestroy(s->comm);
+    for (auto e : s->ev) (void)hipEventDestroy(e);
+    if (s->base) (void)hipFree(s->base);
+    if (s->coef) (void)hipFree(s->coef);
+    if (s->part) (void)hipFree(s->part);
+    if (s->scal) (void)hipFree(s->scal);
+    if (s->hs) (void)hipHostFree(s->hs);
+    if (s->st) (void)hipStreamDestroy(s->st);
+    delete s;
+}
+
+int ns_step(ns_solver* s, ns_stats* out) {
+    if (!s) { set_err("null solver"); return NS_EINVAL; }
+    ns_stats st{};
+    HIPCHK(hipSetDevice(s->device));
+    // ghost rows for K1: u, v width 2 (MUSCL), phi width 1 (grad phi^{n-1} on walls)
+    CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
+    CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
+    CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
+    CHK(helm_solve(s, &st.it_u, &st.res_u, &st.res_v));            // KSPSolve(uSolver) x2 (:547-548)
+    st.it_v = st.it_u;
+    CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
+    CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
+    CHK(pois_solve(s, &st.it_phi, &st.res_phi, &st));              // KSPSolve(phiSolver)  (:551)
+    CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
+    CHK(correct(s));                                               // CorrectVelocities    (:552)
+    CHK(fetch(s));                                                 // VecMin/VecMax        (:554-557)
+    st.umin = s->hs[S_MM];
+    st.umax = -s->hs[S_MM + 1];
+    st.vmin = s->hs[S_MM + 2];
+    st.vmax = -s->hs[S_MM + 3];
+    if (out) *out = st;
+    if (!std::isfinite(st.umin) || !std::isfinite(st.umax) || !std::isfinite(st.vmin) || !std::isfinite(st.vmax)) {
+        set_err("velocity field is not finite after the step (scheme diverged; see SURVEY.md section 5 on CFL)");
+        return NS_EDIVERGE;
+    }
+    return 0;
+}
+
+int ns_get_array(ns_solver* s, int which, double* host) {
+    CHK(check_arr(s, which));
+    HIPCHK(hipSetDevice(s->device));
+    HIPCHK(hipMemcpy2DAsync(host, (size_t)s->g.ny * 8, s->arr[which], (size_t)s->g.ld * 8, (size_t)s->g.ny * 8,
+                            s->g.nxl, hipMemcpyDeviceToHost, s->st));
+    HIPCHK(hipStreamSynchronize(s->st));
+    return 0;
+}
+
+int ns_set_array(ns_solver* s, int which, const double* host) {
+    CHK(check_arr(s, which));
+    HIPCHK(hipSetDevice(s->device));
+    HIPCHK(hipMemcpy2DAsync(s->arr[which], (size_t)s->g.ld * 8, host, (size_t)s->g.ny * 8, (size_t)s->g.ny * 8,
+                            s->g.nxl, hipMemcpyHostToDevice, s->st));
+    // keep the derived scalars consistent with an injected right-hand side
+    if (which == NS_ARR_RPHI) CHK(rhs_mean(s));
+    if (which == NS_ARR_RU || which == NS_ARR_RV) CHK(helm_bnorm(s));
+    HIPCHK(hipStreamSynchronize(s->st));
+    return 0;
+}
+
+int ns_get_fields(ns_solver* s, double* u, double* v, double* phi) {
+    if (u) CHK(ns_get_array(s, NS_ARR_U, u));
+    if (v) CHK(ns_get_array(s, NS_ARR_V, v));
+    if (phi) CHK(ns_get_array(s, NS_ARR_PHI, phi));
+    return 0;
+}
+
+int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* phi, const double* cu0,
+                  const double* cv0) {
+    if (u) CHK(ns_set_array(s, NS_ARR_U, u));
+    if (v) CHK(ns_set_array(s, NS_ARR_V, v));
+    if (phi) CHK(ns_set_array(s, NS_ARR_PHI, phi));
+    if (cu0) CHK(ns_set_array(s, NS_ARR_CU, cu0));
+    if (cv0) CHK(ns_set_array(s, NS_ARR_CV, cv0));
+    return 0;
+}
+
+int ns_kernel(ns_solver* s, int which, int iters, double* out) {
+    if (!s) { set_err("null solver"); return NS_EINVAL; }
+    HIPCHK(hipSetDevice(s->device));
+    const double alpha = s->dt / (2 * s->re);
+    switch (which) {
+    case NS_K_RHS:
+        CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
+        CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
+        CHK(rhs(s));
+        CHK(fetch(s));
+        if (out) { out[0] = s->hs[S_HBN]; out[1] = s->hs[S_HBN + 1]; }
+        return 0;
+    case NS_K_HELMHOLTZ: {
+        int nb = 0;
+        for (int k = 0; k < iters; k++) {
+            CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
+            nb = nsg::launch_helm_sweep(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
+                                        s->arr[NS_ARR_RU], s->arr[NS_ARR_RV], k == iters - 1 ? s->part : nullptr, s->st);
+        }
+        if (iters > 0) {
+            nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_RES, s->st);
+            CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
+        }
+        CHK(fetch(s));
+        if (out) { out[0] = s->hs[S_RES]; out[1] = s->hs[S_RES + 1]; }
+        return 0;
+    }
+    case NS_K_DIV:
+        CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
+        CHK(divergence(s));
+        CHK(fetch(s));
+        if (out) { out[0] = s->hs[S_DIVSUM]; out[1] = s->hs[S_DIVSUM + 1]; }
+        return 0;
+    case NS_K_POISSON: {
+        int nb = 0;
+        for (int k = 0; k < iters; k++) {
+            double* part = k == iters - 1 ? s->part : nullptr;
+            CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
+            if (s->poisson == NS_POISSON_JACOBI) {
+                nb = nsg::launch_pois_jacobi(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP],
+                                             s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, s->part, s->st);
+                std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
+            } else {
+                nb = nsg::launch_pois_rbsor(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI],
+                                            s->scal + S_SHIFT, part, s->st);
+            }
+        }
+        if (iters > 0) {
+            nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
+            CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
+        }
+        CHK(fetch(s));
+        if (out) out[0] = s->hs[S_RES];
+        return 0;
+    }
+    case NS_K_CORRECT:
+        CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
+        CHK(correct(s));
+        CHK(fetch(s));
+        if (out) { out[0] = s->hs[S_MM]; out[1] = -s->hs[S_MM + 1]; out[2] = s->hs[S_MM + 2]; out[3] = -s->hs[S_MM + 3]; }
+        return 0;
+    case NS_K_HELM_SOLVE: {
+        int its = 0;
+        double ru = 0, rv = 0;
+        CHK(helm_bnorm(s));
+        CHK(helm_solve(s, &its, &ru, &rv));
+        if (out) { out[0] = its; out[1] = std::max(ru, rv); }
+        return 0;
+    }
+    case NS_K_POIS_SOLVE: {
+        int its = 0;
+        double r = 0;
+        CHK(rhs_mean(s));
+        CHK(pois_solve(s, &its, &r, nullptr));
+        if (out) { out[0] = its; out[1] = r; }
+        return 0;
+    }
+    case NS_K_RESIDUAL: {
+        CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
+        const int nb = nsg::launch_pois_residual(s->g, s->c, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI],
+                                                 s->scal + S_SHIFT, s->part, s->st);
+        nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_AUX, s->st);
+        CHK(allreduce(s, s->scal + S_AUX, 1, ncclSum));
+        CHK(fetch(s));
+        if (out) out[0] = s->hs[S_AUX];
+        return 0;
+    }
+    default:
+        set_err("unknown kernel %d", which);
+        return NS_EINVAL;
+    }
+}
+
+int ns_fill_random(ns_solver* s, uint64_t seed) {
+    if (!s) { set_err("null solver"); return NS_EINVAL; }
+    HIPCHK(hipSetDevice(s->device));
+    nsg::launch_fill_random(s->g, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], seed, s->st);
+    CHK(rhs_mean(s));  // the random rhs's mean becomes the Poisson shift (null-space removal)
+    HIPCHK(hipStreamSynchronize(s->st));
+    return 0;
+}
+
+int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
+    if (!s || iters <= 0) { set_err("bad arguments"); return NS_EINVAL; }
+    HIPCHK(hipSetDevice(s->device));
+    CHK(ensure_events(s, 2 * (size_t)iters));
+    for (int k = 0; k < warmup; k++) {
+        CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
+        if (s->poisson == NS_POISSON_JACOBI) {
+            nsg::launch_pois_jacobi(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP], s->arr[NS_ARR_RPHI],
+                                    s->scal + S_SHIFT, s->part, s->st);
+            std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
+        } else {
+            nsg::launch_pois_rbsor(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,
+                                   nullptr, s->st);
+        }
+    }
+    for (int k = 0; k < iters; k++) {
+        CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
+        HIPCHK(hipEventRecord(s->ev[2 * k], s->st));
+        if (s->poisson == NS_POISSON_JACOBI) {
+            nsg::launch_pois_jacobi(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP], s->arr[NS_ARR_RPHI],
+                                    s->scal + S_SHIFT, s->part, s->st);
+            std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
+        } else {
+            nsg::launch_pois_rbsor(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,
+                                   k == iters - 1 ? s->part : nullptr, s->st);
+        }
+        HIPCHK(hipEventRecord(s->ev[2 * k + 1], s->st));
+    }
+    HIPCHK(hipStreamSynchronize(s->st));
+    double tot = 0.0;
+    for (int k = 0; k < iters; k++) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
+        tot += ms;
+    }
+    float span = 0.f;
+    HIPCHK(hipEventElapsedTime(&span, s->ev[0], s->ev[2 * iters - 1]));
+    if (out) { out[0] = tot / iters; out[1] = tot; out[2] = span; }
+    return 0;
+}
+
+}  // extern "C"

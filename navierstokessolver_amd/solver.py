@@ -1,0 +1,114 @@
+"""Python handle over one ns_solver (libnsgpu.so).  Plumbing for tests and bench.py;
+the reference-compatible host API is the C++ Grid / FluidSolver in host/."""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass
+class Edge:
+    """One polygon edge (Edge, /root/reference/SRC/Grid.h:20-26)."""
+    nx: int
+    ny: int
+    type: int = L.NS_BC_WALL
+    info: float = 0.0
+
+
+@dataclass
+class GridSpec:
+    """Geometry handed to ns_create: spacings plus edges (a rectangle)."""
+    hx: np.ndarray
+    hy: np.ndarray
+    edges: list = field(default_factory=list)
+
+    @property
+    def nx(self):
+        return len(self.hx)
+
+    @property
+    def ny(self):
+        return len(self.hy)
+
+
+def _dptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+class GpuSolver:
+    """One x-slab (the whole grid when nranks == 1) resident on one MI355X."""
+
+    def __init__(self, grid: GridSpec, dt: float, re: float, *, poisson=L.NS_POISSON_RBSOR, rtol=1e-8,
+                 max_iters=0, omega=0.0, omega_v=0.0, check_every=0, device=-1, timing=False,
+                 rank=0, nranks=1, nccl_id: bytes | None = None):
+        self.grid = grid
+        self.hx = np.ascontiguousarray(grid.hx, dtype=np.float64)
+        self.hy = np.ascontiguousarray(grid.hy, dtype=np.float64)
+        self._edges = (L.NsEdge * len(grid.edges))(*[L.NsEdge(e.nx, e.ny, e.type, e.info) for e in grid.edges])
+        desc = L.NsGridDesc(self.hx.size, self.hy.size, _dptr(self.hx), _dptr(self.hy), len(grid.edges),
+                            self._edges, None)
+        self._nccl = ctypes.create_string_buffer(nccl_id, len(nccl_id)) if nccl_id else None
+        prm = L.NsParams(dt, re, poisson, rtol, max_iters, omega, omega_v, check_every, device,
+                         1 if timing else 0, rank, nranks,
+                         ctypes.cast(self._nccl, ctypes.c_void_p) if self._nccl is not None else None)
+        h = ctypes.c_void_p()
+        L.check(L.lib().ns_create(ctypes.byref(desc), ctypes.byref(prm), ctypes.byref(h)))
+        self._h = h
+        self.dt, self.re = dt, re
+        self.rank, self.nranks = rank, nranks
+        self.i0, self.i1 = L.slab_range(self.hx.size, nranks, rank)
+        self.shape = (self.i1 - self.i0, self.hy.size)
+
+    # ---- lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib().ns_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- stepping
+    def step(self) -> dict:
+        st = L.NsStats()
+        L.check(L.lib().ns_step(self._h, ctypes.byref(st)))
+        return st.as_dict()
+
+    # ---- state
+    def get(self, which: int) -> np.ndarray:
+        out = np.empty(self.shape, dtype=np.float64)
+        L.check(L.lib().ns_get_array(self._h, which, _dptr(out)))
+        return out
+
+    def set(self, which: int, a) -> None:
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(self.shape))
+        L.check(L.lib().ns_set_array(self._h, which, _dptr(a)))
+
+    def fields(self):
+        return self.get(L.NS_ARR_U), self.get(L.NS_ARR_V), self.get(L.NS_ARR_PHI)
+
+    def kernel(self, which: int, iters: int = 1) -> np.ndarray:
+        out = np.zeros(8, dtype=np.float64)
+        L.check(L.lib().ns_kernel(self._h, which, iters, _dptr(out)))
+        return out
+
+    def fill_random(self, seed: int = 0x5EED) -> None:
+        L.check(L.lib().ns_fill_random(self._h, seed))
+
+    def time_poisson(self, warmup: int, iters: int):
+        out = np.zeros(3, dtype=np.float64)
+        L.check(L.lib().ns_time_poisson(self._h, warmup, iters, _dptr(out)))
+        return {"avg_ms": out[0], "total_ms": out[1], "span_ms": out[2]}

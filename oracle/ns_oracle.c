@@ -1,0 +1,874 @@
+/*
+ * ns_oracle.c -- CPU restatement of the reference hot path (TEST INFRASTRUCTURE).
+ * See ns_oracle.h for provenance and the rules on who may call this code.
+ * Citations: /root/reference/SRC/<file>:<line>.
+ */
+#include "ns_oracle.h"
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static char og_err[512];
+const char* og_last_error(void) { return og_err; }
+static void set_err(const char* fmt, ...) {
+    va_list ap; va_start(ap, fmt); vsnprintf(og_err, sizeof og_err, fmt, ap); va_end(ap);
+}
+
+#define TOL 1e-8 /* Grid.h:7 */
+static int equals_(double a, double b) { return fabs(a - b) > TOL ? 0 : 1; } /* Grid.cpp:292 */
+
+typedef struct {
+    int nx, ny;     /* normal (Grid.cpp:40-61) */
+    double loc[3];  /* Grid.cpp:36-59 */
+    int btype;
+    double binfo;
+    double c[2];    /* ghost[0].constant, FluidSolver.cpp:89-96 */
+} og_edge;
+
+struct og_grid {
+    int nx, ny, N;
+    double *hx, *hy;
+    double *xc, *yc;     /* by compact id */
+    int *id;             /* nx*ny, i*ny+j */
+    int *tag;            /* nx*ny*4: W,E,S,N edge index or -1 (Grid.h:33) */
+    int *ci, *cj;        /* id -> (i,j) */
+    int ne;
+    og_edge* e;
+};
+
+static inline int IDX(const og_grid* g, int i, int j) { return i * g->ny + j; }
+/* Grid::inDomain Grid.cpp:214-218 */
+static inline int in_dom(const og_grid* g, int i, int j) {
+    if (i < 0 || i >= g->nx || j < 0 || j >= g->ny) return 0;
+    return g->id[IDX(g, i, j)] >= 0;
+}
+static inline int CID(const og_grid* g, int i, int j) { return g->id[IDX(g, i, j)]; }
+static inline int TAG(const og_grid* g, int i, int j, int k) { return g->tag[4 * IDX(g, i, j) + k]; }
+
+void og_grid_free(og_grid* g) {
+    if (!g) return;
+    free(g->hx); free(g->hy); free(g->xc); free(g->yc); free(g->id); free(g->tag);
+    free(g->ci); free(g->cj); free(g->e); free(g);
+}
+int og_grid_N(const og_grid* g) { return g->N; }
+int og_grid_nx(const og_grid* g) { return g->nx; }
+int og_grid_ny(const og_grid* g) { return g->ny; }
+
+void og_grid_info(const og_grid* g, double* hx, double* hy, int* id, int* tag, double* xc, double* yc) {
+    if (hx) memcpy(hx, g->hx, sizeof(double) * g->nx);
+    if (hy) memcpy(hy, g->hy, sizeof(double) * g->ny);
+    if (id) memcpy(id, g->id, sizeof(int) * g->nx * g->ny);
+    if (tag) memcpy(tag, g->tag, sizeof(int) * 4 * g->nx * g->ny);
+    if (xc) memcpy(xc, g->xc, sizeof(double) * g->N);
+    if (yc) memcpy(yc, g->yc, sizeof(double) * g->N);
+}
+
+/* GenerateFaces' per-direction loop, Grid.cpp:78-120.  Returns count or -1. */
+static int gen_faces(double start, int ns, const double* spec, double** F, double** H) {
+    int cap = 64, n = 0;
+    double* f = malloc(sizeof(double) * (cap + 1));
+    double* h = malloc(sizeof(double) * cap);
+    f[0] = start;
+    double hh = 0.0;
+    for (int s = 0; s < ns; s++) {
+        double a = spec[4 * s + 0], b = spec[4 * s + 1], cnt = spec[4 * s + 2], r = spec[4 * s + 3];
+        if (!equals_(a, f[n]) || (n == 0 && cnt <= 0)) goto bad;
+        if (r > 0) {
+            if (cnt <= 0) cnt = ceil(log((b - a) * (r - 1) / hh + 1) / log(r));
+            hh = (b - a) * (r - 1) / (pow(r, cnt) - 1);
+        } else if (r == -1) {
+            if (cnt <= 0) cnt = ceil((b - a) / hh);
+            hh = (b - a) / cnt;
+        } else goto bad;
+        double x = a;
+        for (int j = 0; j < cnt; j++) { /* int vs double compare, Grid.cpp:91,97 */
+            if (n + 1 >= cap) {
+                cap *= 2;
+                f = realloc(f, sizeof(double) * (cap + 1));
+                h = realloc(h, sizeof(double) * cap);
+            }
+            x += hh;
+            f[n + 1] = x; h[n] = hh; n++;
+            if (r > 0) hh *= r;
+        }
+    }
+    *F = f; *H = h;
+    return n;
+bad:
+    free(f); free(h);
+    return -1;
+}
+
+og_grid* og_grid_polygon(int nv, const double* vx, const double* vy, int nsx, const double* xspec,
+                         int nsy, const double* yspec, const int* btype, const double* binfo) {
+    og_grid* g = calloc(1, sizeof *g);
+    double xr0 = 1e15, xr1 = -1e15, yr0 = 1e15, yr1 = -1e15;
+    g->ne = nv;
+    g->e = calloc(nv, sizeof(og_edge));
+    /* GenerateEdges Grid.cpp:28-72 (polygon closed back to vertex 0) */
+    for (int k = 0; k < nv; k++) {
+        double x0 = vx[k], y0 = vy[k], x1 = vx[(k + 1) % nv], y1 = vy[(k + 1) % nv];
+        og_edge* e = &g->e[k];
+        if (x1 == x0) {
+            e->loc[0] = x1;
+            if (y1 > y0) { e->loc[1] = y0; e->loc[2] = y1; e->nx = -1; xr0 = x1 < xr0 ? x1 : xr0; }
+            else         { e->loc[2] = y0; e->loc[1] = y1; e->nx = 1;  xr1 = x1 > xr1 ? x1 : xr1; }
+        } else if (y1 == y0) {
+            e->loc[0] = y1;
+            if (x1 > x0) { e->loc[1] = x0; e->loc[2] = x1; e->ny = 1;  yr1 = y1 > yr1 ? y1 : yr1; }
+            else         { e->loc[2] = x0; e->loc[1] = x1; e->ny = -1; yr0 = y1 < yr0 ? y1 : yr0; }
+        } else { set_err("Edges should be parallel to the x-axis or y-axis"); og_grid_free(g); return NULL; }
+    }
+    double *X, *Y;
+    int nx = gen_faces(xr0, nsx, xspec, &X, &g->hx);
+    if (nx < 0) { set_err("Invalid specification for number of cells"); og_grid_free(g); return NULL; }
+    int ny = gen_faces(yr0, nsy, yspec, &Y, &g->hy);
+    if (ny < 0) { free(X); set_err("Invalid specification for number of cells"); og_grid_free(g); return NULL; }
+    if (!equals_(xr1, X[nx]) || !equals_(yr1, Y[ny])) { /* Grid.cpp:122-125 */
+        free(X); free(Y); set_err("Invalid specification for number of cells"); og_grid_free(g); return NULL;
+    }
+    g->nx = nx; g->ny = ny;
+    g->id = malloc(sizeof(int) * nx * ny);
+    g->tag = malloc(sizeof(int) * 4 * nx * ny);
+    /* GenerateCells + Cleanup + Interior, Grid.cpp:131-185 */
+    int n = 0;
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < ny; j++) {
+            double X0 = X[i], X1 = X[i + 1], Y0 = Y[j], Y1 = Y[j + 1];
+            double cx = 0.5 * (X0 + X1), cy = 0.5 * (Y0 + Y1);
+            int* t = &g->tag[4 * (i * ny + j)];
+            t[0] = t[1] = t[2] = t[3] = -1;
+            int intersect = 0;
+            for (int k = 0; k < nv; k++) {
+                const og_edge* e = &g->e[k];
+                if (e->nx != 0) {
+                    if (cy > e->loc[1] && cy < e->loc[2]) {
+                        if (e->loc[0] > cx) intersect++;
+                        if (e->nx == -1 && equals_(X0, e->loc[0])) t[0] = k;
+                        if (e->nx == 1 && equals_(X1, e->loc[0])) t[1] = k;
+                    }
+                } else {
+                    if (cx > e->loc[1] && cx < e->loc[2]) {
+                        if (e->ny == -1 && equals_(Y0, e->loc[0])) t[2] = k;
+                        if (e->ny == 1 && equals_(Y1, e->loc[0])) t[3] = k;
+                    }
+                }
+            }
+            g->id[i * ny + j] = (intersect % 2) ? n++ : -1;
+        }
+    g->N = n;
+    g->xc = malloc(sizeof(double) * n); g->yc = malloc(sizeof(double) * n);
+    g->ci = malloc(sizeof(int) * n); g->cj = malloc(sizeof(int) * n);
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < ny; j++) {
+            int c = g->id[i * ny + j];
+            if (c < 0) continue;
+            g->xc[c] = 0.5 * (X[i] + X[i + 1]); g->yc[c] = 0.5 * (Y[j] + Y[j + 1]);
+            g->ci[c] = i; g->cj[c] = j;
+        }
+    free(X); free(Y);
+    /* BCs + ConstructGhostStencils FluidSolver.cpp:84-103 */
+    for (int k = 0; k < nv; k++) {
+        og_edge* e = &g->e[k];
+        e->btype = btype[k]; e->binfo = binfo[k];
+        e->c[0] = e->c[1] = 0.0;
+        if (e->btype == OG_INLET_UNI) {
+            if (e->nx == 0) e->c[1] = 2 * e->binfo; else e->c[0] = 2 * e->binfo;
+        } else if (e->btype == OG_WALL) {
+            if (e->nx != 0) e->c[1] = 2 * e->binfo; else e->c[0] = 2 * e->binfo;
+        } else if (e->btype != OG_NEUMANN) {
+            /* INLET_PARABOLIC / unset read an empty constant vector (UB,
+             * FluidSolver.cpp:86-87,171); PRESSURE has no ghost (:150,168). */
+            set_err("edge %d: unsupported boundary condition type %d", k, e->btype);
+            og_grid_free(g); return NULL;
+        }
+    }
+    /* one-cell-thick geometry would index j-1 = -1 (FluidSolver.cpp:470-477) */
+    for (int c = 0; c < n; c++) {
+        int i = g->ci[c], j = g->cj[c];
+        if ((!in_dom(g, i, j + 1) && !in_dom(g, i, j - 1)) || (!in_dom(g, i + 1, j) && !in_dom(g, i - 1, j))) {
+            set_err("one-cell-thick geometry at cell (%d,%d) is not supported", i, j);
+            og_grid_free(g); return NULL;
+        }
+    }
+    return g;
+}
+
+/* ---------------------------------------------------------------------- */
+/* ghosts: EvaluateGhostStencil_V / _P, FluidSolver.cpp:166-181            */
+
+static inline double ghost_v(const og_grid* g, const double* q, int i, int j, int e, int d) {
+    const og_edge* E = &g->e[e];
+    double r = 0.0;
+    if (E->btype == OG_NEUMANN) { r += 1.0 * q[CID(g, i, j)]; r += 0.0; }
+    else { r += -1.0 * q[CID(g, i, j)]; r += E->c[d]; }
+    return r;
+}
+static inline double ghost_p(const og_grid* g, const double* p, int i, int j, int e) {
+    const og_edge* E = &g->e[e];
+    double r = 0.0;
+    if (E->btype == OG_NEUMANN) {
+        r += 2.5 * p[CID(g, i, j)];
+        r += -2.0 * p[CID(g, i - E->nx, j - E->ny)];
+        r += 0.5 * p[CID(g, i - 2 * E->nx, j - 2 * E->ny)];
+    } else r += 1.0 * p[CID(g, i, j)];
+    return r;
+}
+
+/* minmode FluidSolver.cpp:671-674 */
+static inline double minmode(double a, double b) {
+    if (a * b > 0) return a * fmin(1.0, fabs(b / a));
+    return 0;
+}
+
+/* SlopeLimiter FluidSolver.cpp:283-325 */
+static void slope(const og_grid* g, const double* u, const double* v, int i, int j, int d, double* s) {
+    const double* h = d == 0 ? g->hx : g->hy;
+    int c = CID(g, i, j);
+    double a0, a1, b0, b1;
+    if (d == 0) {
+        if (in_dom(g, i + 1, j)) {
+            a0 = 2 * (u[CID(g, i + 1, j)] - u[c]) / (h[i + 1] + h[i]);
+            a1 = 2 * (v[CID(g, i + 1, j)] - v[c]) / (h[i + 1] + h[i]);
+        } else {
+            a0 = (ghost_v(g, u, i, j, TAG(g, i, j, 1), 0) - u[c]) / h[i];
+            a1 = (ghost_v(g, v, i, j, TAG(g, i, j, 1), 1) - v[c]) / h[i];
+        }
+        if (in_dom(g, i - 1, j)) {
+            b0 = 2 * (u[c] - u[CID(g, i - 1, j)]) / (h[i - 1] + h[i]);
+            b1 = 2 * (v[c] - v[CID(g, i - 1, j)]) / (h[i - 1] + h[i]);
+        } else {
+            b0 = (u[c] - ghost_v(g, u, i, j, TAG(g, i, j, 0), 0)) / h[i];
+            b1 = (v[c] - ghost_v(g, v, i, j, TAG(g, i, j, 0), 1)) / h[i];
+        }
+    } else {
+        if (in_dom(g, i, j + 1)) {
+            a0 = 2 * (u[CID(g, i, j + 1)] - u[c]) / (h[j + 1] + h[j]);
+            a1 = 2 * (v[CID(g, i, j + 1)] - v[c]) / (h[j + 1] + h[j]);
+        } else {
+            a0 = (ghost_v(g, u, i, j, TAG(g, i, j, 3), 0) - u[c]) / h[j];
+            a1 = (ghost_v(g, v, i, j, TAG(g, i, j, 3), 1) - v[c]) / h[j];
+        }
+        if (in_dom(g, i, j - 1)) {
+            b0 = 2 * (u[c] - u[CID(g, i, j - 1)]) / (h[j - 1] + h[j]);
+            b1 = 2 * (v[c] - v[CID(g, i, j - 1)]) / (h[j - 1] + h[j]);
+        } else {
+            b0 = (u[c] - ghost_v(g, u, i, j, TAG(g, i, j, 2), 0)) / h[j];
+            b1 = (v[c] - ghost_v(g, v, i, j, TAG(g, i, j, 2), 1)) / h[j];
+        }
+    }
+    s[0] = minmode(a0, b0);
+    s[1] = minmode(a1, b1);
+}
+
+static inline double fnn(double l, double r) { return 0.5 * (l * l + r * r - fabs(l + r) * (r - l)); }
+static inline double fuv(double u1, double v1, double u2, double v2) {
+    return 0.5 * (u1 * v1 + u2 * v2 - 0.5 * fabs(v1 + v2) * (u2 - u1) - 0.5 * fabs(u2 + u1) * (v2 - v1));
+}
+
+/* ConvectiveFlux FluidSolver.cpp:205-281 */
+static void conv_flux(const og_grid* g, const double* u, const double* v, int i, int j, double* C) {
+    const double *hx = g->hx, *hy = g->hy;
+    int c = CID(g, i, j);
+    double SL[2], sl[2], u1, u2, v1, v2;
+    slope(g, u, v, i, j, 0, SL);
+    u2 = u[c] - hx[i] / 2 * SL[0];
+    v2 = v[c] - hx[i] / 2 * SL[1];
+    if (TAG(g, i, j, 0) == -1) {
+        slope(g, u, v, i - 1, j, 0, sl);
+        u1 = u[CID(g, i - 1, j)] + hx[i - 1] / 2 * sl[0];
+        v1 = v[CID(g, i - 1, j)] + hx[i - 1] / 2 * sl[1];
+    } else {
+        u1 = 0.5 * (u[c] + ghost_v(g, u, i, j, TAG(g, i, j, 0), 0));
+        v1 = 0.5 * (v[c] + ghost_v(g, v, i, j, TAG(g, i, j, 0), 1));
+    }
+    C[0] = fnn(u1, u2);
+    C[1] = fuv(u1, v1, u2, v2);
+    u1 = u[c] + hx[i] / 2 * SL[0];
+    v1 = v[c] + hx[i] / 2 * SL[1];
+    if (TAG(g, i, j, 1) == -1) {
+        slope(g, u, v, i + 1, j, 0, sl);
+        u2 = u[CID(g, i + 1, j)] - hx[i + 1] / 2 * sl[0];
+        v2 = v[CID(g, i + 1, j)] - hx[i + 1] / 2 * sl[1];
+    } else {
+        u2 = 0.5 * (u[c] + ghost_v(g, u, i, j, TAG(g, i, j, 1), 0));
+        v2 = 0.5 * (v[c] + ghost_v(g, v, i, j, TAG(g, i, j, 1), 1));
+    }
+    C[2] = fnn(u1, u2);
+    C[3] = fuv(u1, v1, u2, v2);
+    slope(g, u, v, i, j, 1, SL);
+    u2 = u[c] - hy[j] / 2 * SL[0];
+    v2 = v[c] - hy[j] / 2 * SL[1];
+    if (TAG(g, i, j, 2) == -1) {
+        slope(g, u, v, i, j - 1, 1, sl);
+        u1 = u[CID(g, i, j - 1)] + hy[j - 1] / 2 * sl[0];
+        v1 = v[CID(g, i, j - 1)] + hy[j - 1] / 2 * sl[1];
+    } else {
+        u1 = 0.5 * (u[c] + ghost_v(g, u, i, j, TAG(g, i, j, 2), 0));
+        v1 = 0.5 * (v[c] + ghost_v(g, v, i, j, TAG(g, i, j, 2), 1));
+    }
+    C[5] = fnn(v1, v2);
+    C[4] = fuv(u1, v1, u2, v2);
+    u1 = u[c] + hy[j] / 2 * SL[0];
+    v1 = v[c] + hy[j] / 2 * SL[1];
+    if (TAG(g, i, j, 3) == -1) {
+        slope(g, u, v, i, j + 1, 1, sl);
+        u2 = u[CID(g, i, j + 1)] - hy[j + 1] / 2 * sl[0];
+        v2 = v[CID(g, i, j + 1)] - hy[j + 1] / 2 * sl[1];
+    } else {
+        u2 = 0.5 * (u[c] + ghost_v(g, u, i, j, TAG(g, i, j, 3), 0));
+        v2 = 0.5 * (v[c] + ghost_v(g, v, i, j, TAG(g, i, j, 3), 1));
+    }
+    C[7] = fnn(v1, v2);
+    C[6] = fuv(u1, v1, u2, v2);
+}
+
+/* DiffusiveFlux FluidSolver.cpp:183-203 */
+static void diff_flux(const og_grid* g, double re, const double* q, int i, int j, int d, double* D) {
+    const double *hx = g->hx, *hy = g->hy;
+    int c = CID(g, i, j);
+    if (in_dom(g, i - 1, j)) D[0] = (1 / re) * (q[c] - q[CID(g, i - 1, j)]) / (hx[i] + hx[i - 1]);
+    else D[0] = (0.5 / re / hx[i]) * (q[c] - ghost_v(g, q, i, j, TAG(g, i, j, 0), d));
+    if (in_dom(g, i + 1, j)) D[1] = (1 / re) * (q[CID(g, i + 1, j)] - q[c]) / (hx[i] + hx[i + 1]);
+    else D[1] = -(0.5 / re / hx[i]) * (q[c] - ghost_v(g, q, i, j, TAG(g, i, j, 1), d));
+    if (in_dom(g, i, j - 1)) D[2] = (1 / re) * (q[c] - q[CID(g, i, j - 1)]) / (hy[j] + hy[j - 1]);
+    else D[2] = (0.5 / re / hy[j]) * (q[c] - ghost_v(g, q, i, j, TAG(g, i, j, 2), d));
+    if (in_dom(g, i, j + 1)) D[3] = (1 / re) * (q[CID(g, i, j + 1)] - q[c]) / (hy[j] + hy[j + 1]);
+    else D[3] = -(0.5 / re / hy[j]) * (q[c] - ghost_v(g, q, i, j, TAG(g, i, j, 3), d));
+}
+
+/* ApplyBoundaryConditions FluidSolver.cpp:458-510 */
+static void apply_bc(const og_grid* g, double dt, double re, int i, int j, const double* gx,
+                     const double* gy, double* ru, double* rv) {
+    const double *hx = g->hx, *hy = g->hy;
+    int c = CID(g, i, j);
+    int calc = 0;
+    double w, W, D = 0.0;
+    for (int k = 0; k < 4; k++) {
+        int t = TAG(g, i, j, k);
+        if (t == -1) continue;
+        const og_edge* e = &g->e[t];
+        if (!calc) {
+            if (e->nx != 0) {
+                if (!in_dom(g, i, j + 1)) D = 2.0 * (gx[c] - gx[CID(g, i, j - 1)]) / (hy[j] + hy[j - 1]);
+                else if (!in_dom(g, i, j - 1)) D = 2.0 * (gx[CID(g, i, j + 1)] - gx[c]) / (hy[j] + hy[j + 1]);
+                else D = gx[CID(g, i, j + 1)] / (hy[j] + hy[j + 1]) - gx[CID(g, i, j - 1)] / (hy[j] + hy[j - 1])
+                         - gx[c] * (1 / (hy[j] + hy[j + 1]) - 1 / (hy[j] + hy[j - 1]));
+            } else {
+                if (!in_dom(g, i + 1, j)) D = 2.0 * (gy[c] - gy[CID(g, i - 1, j)]) / (hx[i] + hx[i - 1]);
+                else if (!in_dom(g, i - 1, j)) D = 2.0 * (gy[CID(g, i + 1, j)] - gy[c]) / (hx[i] + hx[i + 1]);
+                else D = gy[CID(g, i + 1, j)] / (hx[i] + hx[i + 1]) - gy[CID(g, i - 1, j)] / (hx[i] + hx[i - 1])
+                         - gy[c] * (1 / (hx[i] + hx[i + 1]) - 1 / (hx[i] + hx[i - 1]));
+            }
+            calc = 1;
+        }
+        if (e->btype == OG_NEUMANN) {
+            if (e->nx != 0) {
+                w = dt * e->nx * hx[i] * D;
+                W = dt * (0.5 / re / pow(hx[i], 2)) * w;
+                rv[c] += W;
+            } else {
+                w = dt * e->ny * hy[j] * D;
+                W = dt * (0.5 / re / pow(hy[j], 2)) * w;
+                ru[c] += W;
+            }
+        } else {
+            if (e->nx != 0) {
+                W = dt * (0.5 / re / pow(hx[i], 2)) * e->c[0];
+                ru[c] += W;
+                w = 2 * dt * (gy[c] + e->nx * hx[i] * D / 2);
+                W = dt * (0.5 / re / pow(hx[i], 2)) * (e->c[1] + w);
+                rv[c] += W;
+            } else {
+                W = dt * (0.5 / re / pow(hy[j], 2)) * e->c[1];
+                rv[c] += W;
+                w = 2 * dt * (gx[c] + e->ny * hy[j] * D / 2);
+                W = dt * (0.5 / re / pow(hy[j], 2)) * (e->c[0] + w);
+                ru[c] += W;
+            }
+        }
+    }
+}
+
+/* ConstructRHS_V FluidSolver.cpp:327-363 */
+void og_rhs_velocity(const og_grid* g, double dt, double re, const double* u, const double* v,
+                     const double* gx, const double* gy, double* cu, double* cv, double* ru, double* rv) {
+    const double *hx = g->hx, *hy = g->hy;
+    /* VecSet(0) ; VecAXPY(1, u) ; VecAXPY(0.5dt, conv0)  (:335-340) */
+    for (int c = 0; c < g->N; c++) {
+        ru[c] = 0.0 + 1.0 * u[c]; ru[c] += 0.5 * dt * cu[c];
+        rv[c] = 0.0 + 1.0 * v[c]; rv[c] += 0.5 * dt * cv[c];
+    }
+    double D[4], C[8], val;
+    for (int i = 0; i < g->nx; i++)
+        for (int j = 0; j < g->ny; j++) {
+            int c = CID(g, i, j);
+            if (c < 0) continue;
+            diff_flux(g, re, u, i, j, 0, D);
+            val = dt * ((D[1] - D[0]) / hx[i] + (D[3] - D[2]) / hy[j]);
+            ru[c] += val;
+            diff_flux(g, re, v, i, j, 1, D);
+            val = dt * ((D[1] - D[0]) / hx[i] + (D[3] - D[2]) / hy[j]);
+            rv[c] += val;
+            conv_flux(g, u, v, i, j, C);
+            val = (C[2] - C[0]) / hx[i] + (C[6] - C[4]) / hy[j];
+            cu[c] = val;
+            val *= -1.5 * dt;
+            ru[c] += val;
+            val = (C[3] - C[1]) / hx[i] + (C[7] - C[5]) / hy[j];
+            cv[c] = val;
+            val *= -1.5 * dt;
+            rv[c] += val;
+            apply_bc(g, dt, re, i, j, gx, gy, ru, rv);
+        }
+}
+
+/* face interpolation used by Div_V and GradP (FluidSolver.cpp:390-412, 429-451) */
+static inline double face_w(const og_grid* g, const double* q, int i, int j) {
+    double r = g->hx[i] / (g->hx[i - 1] + g->hx[i]);
+    return q[CID(g, i - 1, j)] * r + q[CID(g, i, j)] * (1 - r);
+}
+static inline double face_e(const og_grid* g, const double* q, int i, int j) {
+    double r = g->hx[i] / (g->hx[i + 1] + g->hx[i]);
+    return q[CID(g, i + 1, j)] * r + q[CID(g, i, j)] * (1 - r);
+}
+static inline double face_s(const og_grid* g, const double* q, int i, int j) {
+    double r = g->hy[j] / (g->hy[j - 1] + g->hy[j]);
+    return q[CID(g, i, j - 1)] * r + q[CID(g, i, j)] * (1 - r);
+}
+static inline double face_n(const og_grid* g, const double* q, int i, int j) {
+    double r = g->hy[j] / (g->hy[j + 1] + g->hy[j]);
+    return q[CID(g, i, j + 1)] * r + q[CID(g, i, j)] * (1 - r);
+}
+
+/* Div_V FluidSolver.cpp:380-418 */
+static double div_v(const og_grid* g, const double* u, const double* v, int i, int j) {
+    int c = CID(g, i, j);
+    double V0 = TAG(g, i, j, 0) == -1 ? face_w(g, u, i, j) : 0.5 * (u[c] + ghost_v(g, u, i, j, TAG(g, i, j, 0), 0));
+    double V1 = TAG(g, i, j, 1) == -1 ? face_e(g, u, i, j) : 0.5 * (u[c] + ghost_v(g, u, i, j, TAG(g, i, j, 1), 0));
+    double V2 = TAG(g, i, j, 2) == -1 ? face_s(g, v, i, j) : 0.5 * (v[c] + ghost_v(g, v, i, j, TAG(g, i, j, 2), 1));
+    double V3 = TAG(g, i, j, 3) == -1 ? face_n(g, v, i, j) : 0.5 * (v[c] + ghost_v(g, v, i, j, TAG(g, i, j, 3), 1));
+    return (V1 - V0) / g->hx[i] + (V3 - V2) / g->hy[j];
+}
+
+void og_divergence(const og_grid* g, double dt, const double* us, const double* vs, double* rhs) {
+    for (int c = 0; c < g->N; c++) rhs[c] = div_v(g, us, vs, g->ci[c], g->cj[c]) / dt;
+}
+
+/* GradP FluidSolver.cpp:420-456 */
+static void grad_p(const og_grid* g, const double* p, int i, int j, double* gr) {
+    int c = CID(g, i, j);
+    double V0 = TAG(g, i, j, 0) == -1 ? face_w(g, p, i, j) : 0.5 * (p[c] + ghost_p(g, p, i, j, TAG(g, i, j, 0)));
+    double V1 = TAG(g, i, j, 1) == -1 ? face_e(g, p, i, j) : 0.5 * (p[c] + ghost_p(g, p, i, j, TAG(g, i, j, 1)));
+    double V2 = TAG(g, i, j, 2) == -1 ? face_s(g, p, i, j) : 0.5 * (p[c] + ghost_p(g, p, i, j, TAG(g, i, j, 2)));
+    double V3 = TAG(g, i, j, 3) == -1 ? face_n(g, p, i, j) : 0.5 * (p[c] + ghost_p(g, p, i, j, TAG(g, i, j, 3)));
+    gr[0] = (V1 - V0) / g->hx[i];
+    gr[1] = (V3 - V2) / g->hy[j];
+}
+
+void og_grad_phi(const og_grid* g, const double* phi, double* gx, double* gy) {
+    double gr[2];
+    for (int c = 0; c < g->N; c++) {
+        grad_p(g, phi, g->ci[c], g->cj[c], gr);
+        gx[c] = gr[0]; gy[c] = gr[1];
+    }
+}
+
+/* CorrectVelocities FluidSolver.cpp:512-534 */
+void og_correct(const og_grid* g, double dt, const double* us, const double* vs, const double* phi,
+                double* u, double* v, double* gx, double* gy) {
+    double gr[2];
+    for (int c = 0; c < g->N; c++) {
+        grad_p(g, phi, g->ci[c], g->cj[c], gr);
+        gx[c] = gr[0]; gy[c] = gr[1];
+        u[c] = us[c] - dt * gr[0];
+        v[c] = vs[c] - dt * gr[1];
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* operators, ConstructLHS FluidSolver.cpp:105-145 + AddGhostStencils :147-164 */
+
+static const int NXk[4] = {-1, 1, 0, 0}, NYk[4] = {0, 0, -1, 1};
+
+static inline double face_w8(const og_grid* g, int i, int j, int k, int nb) {
+    /* nb: neighbour weight 2/(h(h+h_nb)); else boundary weight 1/h^2 (:119-126) */
+    if (NXk[k] != 0) return nb ? 2.0 / (g->hx[i] * (g->hx[i] + g->hx[i + NXk[k]])) : 1.0 / pow(g->hx[i], 2);
+    return nb ? 2.0 / (g->hy[j] * (g->hy[j] + g->hy[j + NYk[k]])) : 1.0 / pow(g->hy[j], 2);
+}
+
+void og_apply_poisson(const og_grid* g, const double* p, double* out) {
+    for (int c = 0; c < g->N; c++) {
+        int i = g->ci[c], j = g->cj[c];
+        double s = 0.0;
+        for (int k = 0; k < 4; k++) {
+            int ii = i + NXk[k], jj = j + NYk[k];
+            if (in_dom(g, ii, jj)) s += face_w8(g, i, j, k, 1) * (p[CID(g, ii, jj)] - p[c]);
+            else s += face_w8(g, i, j, k, 0) * (ghost_p(g, p, i, j, TAG(g, i, j, k)) - p[c]);
+        }
+        out[c] = s;
+    }
+}
+
+/* L_V q without the ghost constants (those go to the RHS, :495-506) */
+static void apply_lv(const og_grid* g, const double* q, double* out) {
+    for (int c = 0; c < g->N; c++) {
+        int i = g->ci[c], j = g->cj[c];
+        double s = 0.0;
+        for (int k = 0; k < 4; k++) {
+            int ii = i + NXk[k], jj = j + NYk[k];
+            if (in_dom(g, ii, jj)) s += face_w8(g, i, j, k, 1) * (q[CID(g, ii, jj)] - q[c]);
+            else {
+                double wself = g->e[TAG(g, i, j, k)].btype == OG_NEUMANN ? 1.0 : -1.0;
+                s += face_w8(g, i, j, k, 0) * (wself * q[c] - q[c]);
+            }
+        }
+        out[c] = s;
+    }
+}
+
+void og_apply_helmholtz(const og_grid* g, double alpha, const double* q, double* out) {
+    apply_lv(g, q, out);
+    for (int c = 0; c < g->N; c++) out[c] = q[c] - alpha * out[c];
+}
+
+void og_pressure(const og_grid* g, double alpha, const double* phi, double* P) {
+    og_apply_poisson(g, phi, P);
+    for (int c = 0; c < g->N; c++) P[c] = phi[c] - alpha * P[c];
+}
+
+/* diagonal of the operators (for the Jacobi preconditioner / sweeps) */
+static void diag_poisson(const og_grid* g, double* d) {
+    for (int c = 0; c < g->N; c++) {
+        int i = g->ci[c], j = g->cj[c];
+        double s = 0.0;
+        for (int k = 0; k < 4; k++) {
+            int ii = i + NXk[k], jj = j + NYk[k];
+            if (in_dom(g, ii, jj)) s -= face_w8(g, i, j, k, 1);
+            else if (g->e[TAG(g, i, j, k)].btype == OG_NEUMANN) s += 1.5 * face_w8(g, i, j, k, 0);
+        }
+        d[c] = s;
+    }
+}
+static void diag_helmholtz(const og_grid* g, double alpha, double* d) {
+    for (int c = 0; c < g->N; c++) {
+        int i = g->ci[c], j = g->cj[c];
+        double s = 0.0;
+        for (int k = 0; k < 4; k++) {
+            int ii = i + NXk[k], jj = j + NYk[k];
+            if (in_dom(g, ii, jj)) s -= face_w8(g, i, j, k, 1);
+            else if (g->e[TAG(g, i, j, k)].btype != OG_NEUMANN) s -= 2.0 * face_w8(g, i, j, k, 0);
+        }
+        d[c] = 1.0 - alpha * s;
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* GPU-path sweeps restated (rectangle, Dirichlet-type faces): Poisson
+ *   (L phi)_c = cW phi_W + cE phi_E + cS phi_S + cN phi_N + d phi_c,
+ *   cX = 2/(h (h + h_nb)) if the neighbour exists else 0, d = -(cW+cE+cS+cN).
+ * This is ConstructLHS's matrix for wall/inlet faces, whose phi ghost = phi_c
+ * makes each boundary face contribute 0 (FluidSolver.cpp:124-131,159-163). */
+
+static int rect_dirichlet(const og_grid* g) {
+    if (g->N != g->nx * g->ny) return 0;
+    for (int k = 0; k < g->ne; k++) if (g->e[k].btype == OG_NEUMANN) return 0;
+    return 1;
+}
+
+static inline void pcoef(const og_grid* g, int i, int j, double* cw, double* ce, double* cs, double* cn) {
+    const double *hx = g->hx, *hy = g->hy;
+    *cw = i > 0 ? 2.0 / (hx[i] * (hx[i] + hx[i - 1])) : 0.0;
+    *ce = i < g->nx - 1 ? 2.0 / (hx[i] * (hx[i] + hx[i + 1])) : 0.0;
+    *cs = j > 0 ? 2.0 / (hy[j] * (hy[j] + hy[j - 1])) : 0.0;
+    *cn = j < g->ny - 1 ? 2.0 / (hy[j] * (hy[j] + hy[j + 1])) : 0.0;
+}
+
+static inline double lap_rect(const og_grid* g, const double* p, int i, int j) {
+    int ny = g->ny;
+    double cw, ce, cs, cn;
+    pcoef(g, i, j, &cw, &ce, &cs, &cn);
+    double c0 = p[i * ny + j];
+    double s = -(cw + ce + cs + cn) * c0;
+    if (i > 0) s += cw * p[(i - 1) * ny + j];
+    if (i < g->nx - 1) s += ce * p[(i + 1) * ny + j];
+    if (j > 0) s += cs * p[i * ny + j - 1];
+    if (j < ny - 1) s += cn * p[i * ny + j + 1];
+    return s;
+}
+
+double og_poisson_jacobi_sweep(const og_grid* g, const double* in, double* out, const double* b,
+                               double shift, double omega) {
+    if (!rect_dirichlet(g)) { set_err("sweeps need a rectangle with Dirichlet-type faces"); return -1; }
+    double r2 = 0.0;
+    for (int i = 0; i < g->nx; i++)
+        for (int j = 0; j < g->ny; j++) {
+            double cw, ce, cs, cn;
+            pcoef(g, i, j, &cw, &ce, &cs, &cn);
+            double d = -(cw + ce + cs + cn);
+            int c = i * g->ny + j;
+            double r = (b[c] - shift) - lap_rect(g, in, i, j);
+            r2 += r * r;
+            out[c] = in[c] + omega * r / d;
+        }
+    return r2;
+}
+
+double og_poisson_rbsor_sweep(const og_grid* g, double* p, const double* b, double shift, double omega) {
+    if (!rect_dirichlet(g)) { set_err("sweeps need a rectangle with Dirichlet-type faces"); return -1; }
+    double r2 = 0.0;
+    for (int i = 0; i < g->nx; i++)
+        for (int j = 0; j < g->ny; j++) {
+            double r = (b[i * g->ny + j] - shift) - lap_rect(g, p, i, j);
+            r2 += r * r;
+        }
+    for (int color = 0; color < 2; color++)
+        for (int i = 0; i < g->nx; i++)
+            for (int j = (i + color) & 1; j < g->ny; j += 2) {
+                double cw, ce, cs, cn;
+                pcoef(g, i, j, &cw, &ce, &cs, &cn);
+                double d = -(cw + ce + cs + cn);
+                int c = i * g->ny + j;
+                double r = (b[c] - shift) - lap_rect(g, p, i, j);
+                p[c] += omega * r / d;
+            }
+    return r2;
+}
+
+/* Helmholtz (I - a L_V): Dirichlet boundary faces add 2/h^2 to -L_V's diagonal */
+static inline double helm_rect(const og_grid* g, double a, const double* q, int i, int j, double* diag) {
+    const double *hx = g->hx, *hy = g->hy;
+    int ny = g->ny;
+    double cw, ce, cs, cn;
+    pcoef(g, i, j, &cw, &ce, &cs, &cn);
+    double bx = (i == 0 ? 2.0 / (hx[i] * hx[i]) : 0.0) + (i == g->nx - 1 ? 2.0 / (hx[i] * hx[i]) : 0.0);
+    double by = (j == 0 ? 2.0 / (hy[j] * hy[j]) : 0.0) + (j == ny - 1 ? 2.0 / (hy[j] * hy[j]) : 0.0);
+    double d = 1.0 + a * (cw + ce + cs + cn + bx + by);
+    *diag = d;
+    double s = d * q[i * ny + j];
+    if (i > 0) s -= a * cw * q[(i - 1) * ny + j];
+    if (i < g->nx - 1) s -= a * ce * q[(i + 1) * ny + j];
+    if (j > 0) s -= a * cs * q[i * ny + j - 1];
+    if (j < ny - 1) s -= a * cn * q[i * ny + j + 1];
+    return s;
+}
+
+double og_helmholtz_rbsor_sweep(const og_grid* g, double a, double* u, double* v, const double* ru,
+                                const double* rv, double omega) {
+    if (!rect_dirichlet(g)) { set_err("sweeps need a rectangle with Dirichlet-type faces"); return -1; }
+    double r2 = 0.0, d;
+    for (int i = 0; i < g->nx; i++)
+        for (int j = 0; j < g->ny; j++) {
+            int c = i * g->ny + j;
+            double r1 = ru[c] - helm_rect(g, a, u, i, j, &d);
+            double r2v = rv[c] - helm_rect(g, a, v, i, j, &d);
+            r2 += r1 * r1 + r2v * r2v;
+        }
+    for (int color = 0; color < 2; color++)
+        for (int i = 0; i < g->nx; i++)
+            for (int j = (i + color) & 1; j < g->ny; j += 2) {
+                int c = i * g->ny + j;
+                double r1 = ru[c] - helm_rect(g, a, u, i, j, &d);
+                u[c] += omega * r1 / d;
+                double r2v = rv[c] - helm_rect(g, a, v, i, j, &d);
+                v[c] += omega * r2v / d;
+            }
+    return r2;
+}
+
+/* ---------------------------------------------------------------------- */
+/* Krylov solves (the oracle's stand-in for PETSc's KSPs; converged tight)  */
+
+typedef void (*op_fn)(const og_grid*, double, const double*, double*);
+
+static double dot(int n, const double* a, const double* b) {
+    double s = 0.0;
+    for (int k = 0; k < n; k++) s += a[k] * b[k];
+    return s;
+}
+
+static void op_helm(const og_grid* g, double a, const double* x, double* y) { og_apply_helmholtz(g, a, x, y); }
+static void op_pois(const og_grid* g, double a, const double* x, double* y) { (void)a; og_apply_poisson(g, x, y); }
+
+/* PCG on the area-scaled symmetric system  S A x = S b  (S = diag(hx_i hy_j)),
+ * symmetric for Helmholtz always and for Poisson without Neumann faces.
+ * proj: remove the (scaled) null space component -- constants. */
+static int pcg(const og_grid* g, op_fn A, double a, const double* b, double* x, const double* dg,
+               double sgn, int proj, double rtol, int maxit) {
+    int n = g->N;
+    double *r = malloc(sizeof(double) * n), *z = malloc(sizeof(double) * n);
+    double *p = malloc(sizeof(double) * n), *q = malloc(sizeof(double) * n), *S = malloc(sizeof(double) * n);
+    for (int c = 0; c < n; c++) S[c] = sgn * g->hx[g->ci[c]] * g->hy[g->cj[c]];
+    /* r = S(b - A x) */
+    A(g, a, x, q);
+    double bn = 0.0;
+    for (int c = 0; c < n; c++) { r[c] = S[c] * (b[c] - q[c]); bn += (S[c] * b[c]) * (S[c] * b[c]); }
+    if (proj) {
+        double m = 0.0, mb = 0.0;
+        for (int c = 0; c < n; c++) { m += r[c]; mb += S[c] * b[c]; }
+        m /= n; mb /= n;
+        for (int c = 0; c < n; c++) r[c] -= m;
+        bn = 0.0;
+        for (int c = 0; c < n; c++) bn += (S[c] * b[c] - mb) * (S[c] * b[c] - mb);
+    }
+    bn = sqrt(bn);
+    int it = 0;
+    if (bn == 0.0) { free(r); free(z); free(p); free(q); free(S); return 0; }
+    for (int c = 0; c < n; c++) z[c] = r[c] / (S[c] * dg[c]);
+    memcpy(p, z, sizeof(double) * n);
+    double rz = dot(n, r, z);
+    while (it < maxit) {
+        if (sqrt(dot(n, r, r)) <= rtol * bn) break;
+        A(g, a, p, q);
+        for (int c = 0; c < n; c++) q[c] *= S[c];
+        double al = rz / dot(n, p, q);
+        for (int c = 0; c < n; c++) { x[c] += al * p[c]; r[c] -= al * q[c]; }
+        for (int c = 0; c < n; c++) z[c] = r[c] / (S[c] * dg[c]);
+        double rz2 = dot(n, r, z);
+        double be = rz2 / rz;
+        rz = rz2;
+        for (int c = 0; c < n; c++) p[c] = z[c] + be * p[c];
+        it++;
+    }
+    free(r); free(z); free(p); free(q); free(S);
+    return it;
+}
+
+/* Jacobi-right-preconditioned BiCGStab (Poisson with Neumann faces), mean-projected residual */
+static int bicgstab(const og_grid* g, op_fn A, double a, const double* b, double* x, const double* dg,
+                    int proj, double rtol, int maxit) {
+    int n = g->N;
+    double *r = malloc(sizeof(double) * n), *r0 = malloc(sizeof(double) * n), *p = malloc(sizeof(double) * n);
+    double *v = malloc(sizeof(double) * n), *s = malloc(sizeof(double) * n), *t = malloc(sizeof(double) * n);
+    double *ph = malloc(sizeof(double) * n), *sh = malloc(sizeof(double) * n);
+    A(g, a, x, t);
+    for (int c = 0; c < n; c++) r[c] = b[c] - t[c];
+    if (proj) { double m = 0; for (int c = 0; c < n; c++) m += r[c]; m /= n; for (int c = 0; c < n; c++) r[c] -= m; }
+    double bn = sqrt(dot(n, b, b));
+    memcpy(r0, r, sizeof(double) * n);
+    double rho = 1, al = 1, om = 1;
+    memset(v, 0, sizeof(double) * n); memset(p, 0, sizeof(double) * n);
+    int it = 0;
+    if (bn == 0.0) goto done;
+    while (it < maxit) {
+        if (sqrt(dot(n, r, r)) <= rtol * bn) break;
+        double rho1 = dot(n, r0, r);
+        if (rho1 == 0.0) break;
+        double be = (rho1 / rho) * (al / om);
+        rho = rho1;
+        for (int c = 0; c < n; c++) p[c] = r[c] + be * (p[c] - om * v[c]);
+        for (int c = 0; c < n; c++) ph[c] = p[c] / dg[c];
+        A(g, a, ph, v);
+        al = rho / dot(n, r0, v);
+        for (int c = 0; c < n; c++) s[c] = r[c] - al * v[c];
+        for (int c = 0; c < n; c++) sh[c] = s[c] / dg[c];
+        A(g, a, sh, t);
+        om = dot(n, t, s) / dot(n, t, t);
+        for (int c = 0; c < n; c++) { x[c] += al * ph[c] + om * sh[c]; r[c] = s[c] - om * t[c]; }
+        if (proj) { double m = 0; for (int c = 0; c < n; c++) m += r[c]; m /= n; for (int c = 0; c < n; c++) r[c] -= m; }
+        it++;
+    }
+done:
+    free(r); free(r0); free(p); free(v); free(s); free(t); free(ph); free(sh);
+    return it;
+}
+
+int og_solve_helmholtz(const og_grid* g, double alpha, const double* rhs, double* x, double rtol, int maxit) {
+    double* d = malloc(sizeof(double) * g->N);
+    diag_helmholtz(g, alpha, d);
+    int it = pcg(g, op_helm, alpha, rhs, x, d, 1.0, 0, rtol, maxit);
+    free(d);
+    return it;
+}
+
+int og_solve_poisson(const og_grid* g, double* rhs, double* x, double rtol, int maxit) {
+    int n = g->N;
+    /* MatNullSpaceRemove(NSP, RHS_phi) FluidSolver.cpp:550: subtract the plain mean */
+    double m = 0.0;
+    for (int c = 0; c < n; c++) m += rhs[c];
+    m /= n;
+    for (int c = 0; c < n; c++) rhs[c] -= m;
+    double* d = malloc(sizeof(double) * n);
+    diag_poisson(g, d);
+    int neu = 0;
+    for (int k = 0; k < g->ne; k++) neu |= g->e[k].btype == OG_NEUMANN;
+    int it = neu ? bicgstab(g, op_pois, 0.0, rhs, x, d, 1, rtol, maxit)
+                 : pcg(g, op_pois, 0.0, rhs, x, d, -1.0, 1, rtol, maxit);
+    free(d);
+    return it;
+}
+
+/* ---------------------------------------------------------------------- */
+/* time stepper, FluidSolver::Solve FluidSolver.cpp:536-567                */
+
+struct og_solver {
+    og_grid* g;
+    double dt, re, rtol;
+    double *u, *v, *phi, *cu, *cv, *gx, *gy, *ru, *rv, *us, *vs, *rp;
+};
+
+og_solver* og_solver_new(og_grid* g, double dt, double re, double rtol) {
+    og_solver* s = calloc(1, sizeof *s);
+    s->g = g; s->dt = dt; s->re = re; s->rtol = rtol;
+    int n = g->N;
+    double** arr[] = {&s->u, &s->v, &s->phi, &s->cu, &s->cv, &s->gx, &s->gy, &s->ru, &s->rv, &s->us, &s->vs, &s->rp};
+    for (unsigned k = 0; k < sizeof arr / sizeof arr[0]; k++) *arr[k] = calloc(n, sizeof(double));
+    return s;
+}
+
+void og_solver_free(og_solver* s) {
+    if (!s) return;
+    double* arr[] = {s->u, s->v, s->phi, s->cu, s->cv, s->gx, s->gy, s->ru, s->rv, s->us, s->vs, s->rp};
+    for (unsigned k = 0; k < sizeof arr / sizeof arr[0]; k++) free(arr[k]);
+    free(s);
+}
+
+int og_solver_step(og_solver* s, double* mm, int* its) {
+    const og_grid* g = s->g;
+    int n = g->N, maxit = 100000;
+    double alpha = s->dt / (2 * s->re);
+    og_rhs_velocity(g, s->dt, s->re, s->u, s->v, s->gx, s->gy, s->cu, s->cv, s->ru, s->rv);
+    /* KSPSolve(uSolver, ...) x2 with zero initial guess (:547-548) */
+    memset(s->us, 0, sizeof(double) * n);
+    memset(s->vs, 0, sizeof(double) * n);
+    int iu = og_solve_helmholtz(g, alpha, s->ru, s->us, s->rtol, maxit);
+    int iv = og_solve_helmholtz(g, alpha, s->rv, s->vs, s->rtol, maxit);
+    og_divergence(g, s->dt, s->us, s->vs, s->rp);
+    int ip = og_solve_poisson(g, s->rp, s->phi, s->rtol, maxit); /* warm start (:54) */
+    og_correct(g, s->dt, s->us, s->vs, s->phi, s->u, s->v, s->gx, s->gy);
+    double umin = s->u[0], umax = s->u[0], vmin = s->v[0], vmax = s->v[0];
+    for (int c = 1; c < n; c++) {
+        umin = fmin(umin, s->u[c]); umax = fmax(umax, s->u[c]);
+        vmin = fmin(vmin, s->v[c]); vmax = fmax(vmax, s->v[c]);
+    }
+    if (mm) { mm[0] = umin; mm[1] = umax; mm[2] = vmin; mm[3] = vmax; }
+    if (its) { its[0] = iu; its[1] = iv; its[2] = ip; }
+    return (iu >= maxit || iv >= maxit || ip >= maxit) ? 1 : 0;
+}
+
+void og_solver_get(const og_solver* s, double* u, double* v, double* phi, double* cu, double* cv,
+                   double* gx, double* gy) {
+    size_t b = sizeof(double) * s->g->N;
+    if (u) memcpy(u, s->u, b);
+    if (v) memcpy(v, s->v, b);
+    if (phi) memcpy(phi, s->phi, b);
+    if (cu) memcpy(cu, s->cu, b);
+    if (cv) memcpy(cv, s->cv, b);
+    if (gx) memcpy(gx, s->gx, b);
+    if (gy) memcpy(gy, s->gy, b);
+}
+
+void og_solver_set(og_solver* s, const double* u, const double* v, const double* phi, const double* cu,
+                   const double* cv, const double* gx, const double* gy) {
+    size_t b = sizeof(double) * s->g->N;
+    if (u) memcpy(s->u, u, b);
+    if (v) memcpy(s->v, v, b);
+    if (phi) memcpy(s->phi, phi, b);
+    if (cu) memcpy(s->cu, cu, b);
+    if (cv) memcpy(s->cv, cv, b);
+    if (gx) memcpy(s->gx, gx, b);
+    if (gy) memcpy(s->gy, gy, b);
+}

@@ -1,0 +1,90 @@
+"""The C-ABI library loads and exports every symbol include/nsgpu.h declares;
+host-side helpers that need no GPU (slab decomposition, sizes, ABI layout)."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+import navierstokessolver_amd as nsa
+from navierstokessolver_amd import _lib as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = L.lib()
+    names = L.header_functions()
+    assert len(names) >= 15, names
+    for n in names:
+        assert hasattr(lib, n), f"libnsgpu.so does not export {n}"
+    assert set(names) == set(L.SIGNATURES), "ctypes signatures out of sync with include/nsgpu.h"
+    assert lib.ns_abi_version() == 1
+
+
+def test_lib_is_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", L.LIB_PATH], capture_output=True,
+                         text=True).stdout + subprocess.run(
+        ["strings", L.LIB_PATH], capture_output=True, text=True).stdout
+    assert "gfx950" in out
+
+
+def _c_sizes():
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "nsgpu.h"
+int main(void){
+ printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(ns_edge), sizeof(ns_grid_desc), sizeof(ns_params),
+        sizeof(ns_stats), offsetof(ns_params, nccl_id), offsetof(ns_stats, t_poisson_kernel_ms),
+        offsetof(ns_grid_desc, cell_id));
+ return 0;}
+'''
+    exe = "/tmp/ns_abi_sizes"
+    subprocess.run(["gcc", "-x", "c", "-I", os.path.join(ROOT, "include"), "-o", exe, "-"], input=src, text=True,
+                   check=True)
+    return [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
+
+
+def test_ctypes_struct_layout_matches_c():
+    c = _c_sizes()
+    py = [ctypes.sizeof(L.NsEdge), ctypes.sizeof(L.NsGridDesc), ctypes.sizeof(L.NsParams),
+          ctypes.sizeof(L.NsStats), L.NsParams.nccl_id.offset, L.NsStats.t_poisson_kernel_ms.offset,
+          L.NsGridDesc.cell_id.offset]
+    assert c == py
+
+
+@pytest.mark.parametrize("nx,p", [(4096, 1), (4096, 2), (4096, 8), (8192, 8), (1000, 7), (130, 3)])
+def test_slab_ranges_partition_the_grid(nx, p):
+    ranges = [nsa.slab_range(nx, p, r) for r in range(p)]
+    assert ranges[0][0] == 0 and ranges[-1][1] == nx
+    for (a0, a1), (b0, b1) in zip(ranges, ranges[1:]):
+        assert a1 == b0
+    sizes = [b - a for a, b in ranges]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_bad_slab_arguments_rejected():
+    with pytest.raises(nsa.NsError):
+        nsa.slab_range(100, 4, 4)
+    with pytest.raises(nsa.NsError):
+        nsa.slab_range(0, 1, 0)
+
+
+def test_device_bytes():
+    # 9 planes of (rows + 4 halo) x ld doubles
+    assert L.lib().ns_device_bytes(4096, 4096) == 9 * 4100 * 4096 * 8
+    assert L.lib().ns_device_bytes(10, 33) == 9 * 14 * 64 * 8
+
+
+def test_nccl_unique_id_size():
+    assert L.lib().ns_nccl_id_size() == 128
+
+
+def test_constants_match_header():
+    txt = open(L.HEADER).read()
+    import re
+    for name in ["NS_OK", "NS_EINVAL", "NS_BC_WALL", "NS_BC_NEUMANN", "NS_POISSON_JACOBI", "NS_ARR_RPHI",
+                 "NS_NUM_ARR", "NS_K_RESIDUAL", "NS_K_POIS_SOLVE"]:
+        m = re.search(rf"#define {name}\s+(-?\d+)", txt)
+        assert m and int(m.group(1)) == getattr(L, name), name

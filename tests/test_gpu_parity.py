@@ -1,0 +1,219 @@
+"""GPU parity: every kernel of the time step and the full step against the oracle
+(oracle/ns_oracle.c, the CPU restatement of /root/reference/SRC/FluidSolver.cpp).
+
+Tolerances (written per test):
+  * single kernels (K1, K3, K5, one K2/K4 sweep): max |gpu - oracle| <= 1e-12 * max|oracle|
+    (fp64 both sides; differences are FMA contraction / division rounding only);
+  * converged solves: <= 1e-7 relative (GPU rtol 1e-11 vs oracle rtol 1e-13);
+  * full time steps at the reference's rtol 1e-8: max|du|, max|dv| <= 1e-6 (SURVEY.md 8(c):
+    rtol 1e-8 moves u, v by ~8e-8 after 200 steps at 128^2); phi compared modulo its mean.
+"""
+import numpy as np
+import pytest
+
+from conftest import KNOWN_TRACE_128, printed_equal
+from oracle import OGrid, OSolver
+
+pytestmark = pytest.mark.gpu
+
+BC_CAVITY = [(2, 0.0), (2, 1.0), (2, 0.0), (2, 0.0)]
+BC_FLOW = [(0, 1.0), (2, 0.0), (0, 1.0), (2, 0.5)]   # inlet W, moving wall N, inlet-as-outlet E, moving wall S
+
+
+def pair(nsa, nx, ny, dt, re, bc=BC_CAVITY, xratio=-1, yratio=-1, **kw):
+    og = OGrid.rectangle(nx, ny, bc=bc, xratio=xratio, yratio=yratio)
+    gs = nsa.GpuSolver(nsa.rectangle(nx, ny, bc=bc, xratio=xratio, yratio=yratio), dt, re, **kw)
+    return og, gs
+
+
+def rel(a, b):
+    return np.max(np.abs(np.asarray(a).ravel() - np.asarray(b).ravel())) / max(np.max(np.abs(b)), 1e-300)
+
+
+def rand(rng, n, scale=1.0):
+    return scale * rng.uniform(-1, 1, n)
+
+
+GEOMS = [(24, 24, -1, -1, BC_CAVITY), (20, 33, -1, -1, BC_FLOW), (17, 16, 1.07, 0.95, BC_CAVITY),
+         (64, 64, -1, -1, BC_FLOW)]
+
+
+@pytest.mark.parametrize("nx,ny,xr,yr,bc", GEOMS)
+def test_k1_rhs_velocity(gpu, nx, ny, xr, yr, bc):
+    rng = np.random.default_rng(1)
+    dt, re = 1e-3, 250.0
+    og, gs = pair(gpu, nx, ny, dt, re, bc, xr, yr)
+    N = nx * ny
+    u, v, phi, cu, cv = (rand(rng, N) for _ in range(5))
+    for a, x in ((gpu.NS_ARR_U, u), (gpu.NS_ARR_V, v), (gpu.NS_ARR_PHI, phi), (gpu.NS_ARR_CU, cu), (gpu.NS_ARR_CV, cv)):
+        gs.set(a, x)
+    sums = gs.kernel(gpu.NS_K_RHS)
+    gx, gy = og.grad_phi(phi)
+    ru, rv, cu1, cv1 = og.rhs_velocity(dt, re, u, v, gx, gy, cu, cv)
+    assert rel(gs.get(gpu.NS_ARR_RU), ru) <= 1e-12
+    assert rel(gs.get(gpu.NS_ARR_RV), rv) <= 1e-12
+    assert rel(gs.get(gpu.NS_ARR_CU), cu1) <= 1e-12
+    assert rel(gs.get(gpu.NS_ARR_CV), cv1) <= 1e-12
+    assert abs(sums[0] - np.sum(ru * ru)) <= 1e-11 * np.sum(ru * ru)
+
+
+@pytest.mark.parametrize("nx,ny,xr,yr,bc", GEOMS)
+def test_k3_divergence(gpu, nx, ny, xr, yr, bc):
+    rng = np.random.default_rng(2)
+    dt = 1.0 / 512
+    og, gs = pair(gpu, nx, ny, dt, 100.0, bc, xr, yr)
+    u, v = rand(rng, nx * ny), rand(rng, nx * ny)
+    gs.set(gpu.NS_ARR_U, u); gs.set(gpu.NS_ARR_V, v)
+    sums = gs.kernel(gpu.NS_K_DIV)
+    ref = og.divergence(dt, u, v)
+    assert rel(gs.get(gpu.NS_ARR_RPHI), ref) <= 1e-12
+    assert abs(sums[0] - ref.sum()) <= 1e-9 * np.abs(ref).sum()
+    assert abs(sums[1] - (ref * ref).sum()) <= 1e-11 * (ref * ref).sum()
+
+
+@pytest.mark.parametrize("nx,ny,xr,yr,bc", GEOMS)
+def test_k5_correct(gpu, nx, ny, xr, yr, bc):
+    rng = np.random.default_rng(3)
+    dt = 1.0 / 256
+    og, gs = pair(gpu, nx, ny, dt, 100.0, bc, xr, yr)
+    us, vs, phi = (rand(rng, nx * ny) for _ in range(3))
+    gs.set(gpu.NS_ARR_U, us); gs.set(gpu.NS_ARR_V, vs); gs.set(gpu.NS_ARR_PHI, phi)
+    mm = gs.kernel(gpu.NS_K_CORRECT)
+    u, v, _, _ = og.correct(dt, us, vs, phi)
+    assert rel(gs.get(gpu.NS_ARR_U), u) <= 1e-12
+    assert rel(gs.get(gpu.NS_ARR_V), v) <= 1e-12
+    np.testing.assert_allclose(mm[:4], [u.min(), u.max(), v.min(), v.max()], rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("nx,ny", [(24, 24), (37, 130), (130, 40), (256, 256)])
+def test_k4_rbsor_sweeps(gpu, nx, ny):
+    """Fused red-black SOR sweeps == the oracle's two-colour sweep (tile seams included)."""
+    rng = np.random.default_rng(4)
+    og, gs = pair(gpu, nx, ny, 1e-3, 100.0, omega=1.7)
+    phi, b = rand(rng, nx * ny), rand(rng, nx * ny, 50.0)
+    gs.set(gpu.NS_ARR_PHI, phi); gs.set(gpu.NS_ARR_RPHI, b)
+    shift = b.mean()
+    p = phi.copy()
+    for k in range(3):
+        p, r2 = og.rbsor_sweep(p, b, shift, 1.7)
+    out = gs.kernel(gpu.NS_K_POISSON, 3)
+    assert rel(gs.get(gpu.NS_ARR_PHI), p) <= 1e-12
+    assert abs(out[0] - r2) <= 1e-10 * r2        # residual of the last sweep's input
+
+
+@pytest.mark.parametrize("nx,ny", [(24, 24), (37, 130), (256, 256)])
+def test_k4_jacobi_sweeps(gpu, nx, ny):
+    rng = np.random.default_rng(5)
+    og, gs = pair(gpu, nx, ny, 1e-3, 100.0, poisson=gpu.NS_POISSON_JACOBI, omega=0.8)
+    phi, b = rand(rng, nx * ny), rand(rng, nx * ny, 50.0)
+    gs.set(gpu.NS_ARR_PHI, phi); gs.set(gpu.NS_ARR_RPHI, b)
+    p = phi.copy()
+    for k in range(4):
+        p, r2 = og.jacobi_sweep(p, b, b.mean(), 0.8)
+    out = gs.kernel(gpu.NS_K_POISSON, 4)
+    assert rel(gs.get(gpu.NS_ARR_PHI), p) <= 1e-12
+    assert abs(out[0] - r2) <= 1e-10 * r2
+
+
+@pytest.mark.parametrize("nx,ny,xr", [(24, 24, -1), (37, 130, -1), (40, 33, 1.05)])
+def test_k2_helmholtz_sweeps(gpu, nx, ny, xr):
+    rng = np.random.default_rng(6)
+    dt, re = 1.0 / 64, 10.0   # alpha/h^2 ~ O(1): a non-trivial operator
+    og, gs = pair(gpu, nx, ny, dt, re, xratio=xr)
+    alpha = dt / (2 * re)
+    u, v, ru, rv = (rand(rng, nx * ny) for _ in range(4))
+    for a, x in ((gpu.NS_ARR_U, u), (gpu.NS_ARR_V, v), (gpu.NS_ARR_RU, ru), (gpu.NS_ARR_RV, rv)):
+        gs.set(a, x)
+    uu, vv = u.copy(), v.copy()
+    for k in range(2):
+        uu, vv, r2 = og.helm_sweep(alpha, uu, vv, ru, rv, 1.0)
+    out = gs.kernel(gpu.NS_K_HELMHOLTZ, 2)
+    assert rel(gs.get(gpu.NS_ARR_U), uu) <= 1e-12
+    assert rel(gs.get(gpu.NS_ARR_V), vv) <= 1e-12
+    assert abs(out[0] + out[1] - r2) <= 1e-10 * r2
+
+
+def test_converged_solves(gpu):
+    rng = np.random.default_rng(7)
+    n, dt, re = 48, 1.0 / 128, 50.0
+    og, gs = pair(gpu, n, n, dt, re, rtol=1e-11)
+    alpha = dt / (2 * re)
+    ru, rv = rand(rng, n * n), rand(rng, n * n)
+    gs.set(gpu.NS_ARR_U, np.zeros(n * n)); gs.set(gpu.NS_ARR_V, np.zeros(n * n))
+    gs.set(gpu.NS_ARR_RU, ru); gs.set(gpu.NS_ARR_RV, rv)
+    its, res = gs.kernel(gpu.NS_K_HELM_SOLVE)[:2]
+    assert res <= 1e-11 and its > 0
+    xu, _ = og.solve_helmholtz(alpha, ru)
+    assert rel(gs.get(gpu.NS_ARR_U), xu) <= 1e-9
+    b = rand(rng, n * n, 100.0)
+    gs.set(gpu.NS_ARR_PHI, np.zeros(n * n)); gs.set(gpu.NS_ARR_RPHI, b)
+    its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+    assert res <= 1e-11
+    xp, _ = og.solve_poisson(b)
+    g = gs.get(gpu.NS_ARR_PHI).ravel()
+    assert rel(g - g.mean(), xp - xp.mean()) <= 1e-8
+
+
+@pytest.mark.parametrize("n,steps,re,bc", [(16, 12, 100.0, BC_CAVITY), (32, 20, 400.0, BC_CAVITY),
+                                           (40, 15, 100.0, BC_FLOW)])
+def test_full_steps_vs_oracle(gpu, n, steps, re, bc):
+    dt = 1.0 / (8 * n)
+    og, gs = pair(gpu, n, n, dt, re, bc)
+    osv = OSolver(og, dt, re, rtol=1e-13)
+    for k in range(steps):
+        st = gs.step()
+        mm, _ = osv.step()
+        np.testing.assert_allclose([st["umin"], st["umax"], st["vmin"], st["vmax"]], mm, atol=1e-6)
+    ref = osv.get()
+    u, v, phi = gs.fields()
+    assert np.max(np.abs(u.ravel() - ref["u"])) <= 1e-6
+    assert np.max(np.abs(v.ravel() - ref["v"])) <= 1e-6
+    p = phi.ravel() - phi.mean()
+    q = ref["phi"] - ref["phi"].mean()
+    assert np.linalg.norm(p - q) <= 1e-5 * np.linalg.norm(q)
+
+
+def test_full_steps_tight_rtol(gpu):
+    """At rtol 1e-12 the GPU step converges onto the oracle's discrete solution."""
+    n, steps, re = 32, 10, 100.0
+    dt = 1.0 / (8 * n)
+    og, gs = pair(gpu, n, n, dt, re, rtol=1e-12)
+    osv = OSolver(og, dt, re, rtol=1e-13)
+    for k in range(steps):
+        gs.step()
+        osv.step()
+    ref = osv.get()
+    u, v, _ = gs.fields()
+    assert np.max(np.abs(u.ravel() - ref["u"])) <= 1e-9
+    assert np.max(np.abs(v.ravel() - ref["v"])) <= 1e-9
+
+
+def test_known_answer_trace_128(gpu):
+    """The reference's printed monitor for the 128^2 Re=100 cavity, at rtol 1e-8."""
+    n = 128
+    gs = gpu.GpuSolver(gpu.cavity(n), 1.0 / 1024, 100.0)
+    for it in range(1, 201):
+        st = gs.step()
+        if it in KNOWN_TRACE_128:
+            got = (st["umin"], st["umax"], st["vmin"], st["vmax"])
+            assert all(printed_equal(a, b) for a, b in zip(got, KNOWN_TRACE_128[it])), (it, got)
+
+
+def test_random_fill_and_timing(gpu):
+    n = 512
+    gs = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0)
+    gs.fill_random(0x5EED)
+    phi = gs.get(gpu.NS_ARR_PHI); b = gs.get(gpu.NS_ARR_RPHI)
+    assert -1 <= phi.min() < -0.99 and 0.99 < phi.max() < 1
+    assert abs(b.mean()) < 0.01
+    t = gs.time_poisson(2, 5)
+    assert t["avg_ms"] > 0
+
+
+def test_bad_configs_fail_loudly(gpu):
+    with pytest.raises(gpu.NsError):
+        gpu.GpuSolver(gpu.rectangle(8, 8, bc=[(1, 1.0), (2, 0.0), (2, 0.0), (2, 0.0)]), 1e-3, 100.0)
+    with pytest.raises(gpu.NsError):
+        gpu.GpuSolver(gpu.rectangle(8, 8, bc=[(3, 1.0), (2, 0.0), (2, 0.0), (2, 0.0)]), 1e-3, 100.0)
+    with pytest.raises(gpu.NsError):
+        gpu.GpuSolver(gpu.cavity(8), -1.0, 100.0)

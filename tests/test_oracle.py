@@ -1,0 +1,117 @@
+"""The oracle (oracle/ns_oracle.c) against the reference's known answers and its own
+internal consistency.  Pinning: SURVEY.md section 6 / 8(c) known-answer trace."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import KNOWN_TRACE_128, printed_equal
+from oracle import OGrid, OSolver
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.mark.slow
+def test_known_answer_trace_128_cavity():
+    """128^2, Re 100, dt 1/1024, 200 steps: every printed monitor line of SURVEY.md section 6."""
+    g = OGrid.rectangle(128, 128)
+    s = OSolver(g, 1.0 / 1024, 100.0, rtol=1e-10)
+    for it in range(1, 201):
+        mm, _ = s.step()
+        if it in KNOWN_TRACE_128:
+            assert all(printed_equal(a, b) for a, b in zip(mm, KNOWN_TRACE_128[it])), (it, mm)
+
+
+def test_grid_matches_reference_conventions():
+    # cavity vertices clockwise: edges left(-1,0), top(0,1), right(1,0), bottom(0,-1) (Grid.cpp:28-72)
+    g = OGrid.rectangle(6, 4)
+    assert g.N == 24 and g.nx == 6 and g.ny == 4
+    assert np.array_equal(g.id, np.arange(24))                 # id = i*ny + j (Grid.cpp:149-162)
+    tag = g.tag.reshape(6, 4, 4)
+    assert (tag[0, :, 0] == 0).all() and (tag[:, 3, 3] == 1).all()
+    assert (tag[5, :, 1] == 2).all() and (tag[:, 0, 2] == 3).all()
+    assert (tag[1:-1, 1:-1] == -1).all()
+    np.testing.assert_allclose(g.xc.reshape(6, 4)[:, 0], (np.arange(6) + 0.5) / 6)
+
+
+def test_l_shaped_polygon_has_compact_ids_and_reentrant_tags():
+    # L-shape, clockwise from the origin: 6 edges
+    v = [(0, 0), (0, 2), (1, 2), (1, 1), (2, 1), (2, 0)]
+    bc = [(2, 0.0)] * 6
+    g = OGrid(v, [[0, 2, 8, -1]], [[0, 2, 8, -1]], bc)
+    assert g.N == 64 - 16
+    ids = g.id.reshape(8, 8)
+    assert (ids[4:, 4:] == -1).all()
+    assert sorted(ids[ids >= 0].tolist()) == list(range(48))
+
+
+def test_invalid_grids_rejected():
+    with pytest.raises(ValueError):   # counter-clockwise vertex list
+        OGrid([(0, 0), (1, 0), (1, 1), (0, 1)], [[0, 1, 4, -1]], [[0, 1, 4, -1]], [(2, 0)] * 4)
+    with pytest.raises(ValueError):   # unsupported BC (INLET_PARABOLIC)
+        OGrid.rectangle(4, 4, bc=[(1, 1.0), (2, 0), (2, 0), (2, 0)])
+
+
+def _poisson_setup(n=24, seed=0):
+    g = OGrid.rectangle(n, n)
+    rng = np.random.default_rng(seed)
+    b = rng.uniform(-1, 1, g.N)
+    return g, b, b.mean()
+
+
+def test_sweep_residual_is_true_residual_of_input():
+    g, b, m = _poisson_setup()
+    phi = np.random.default_rng(1).uniform(-1, 1, g.N)
+    r = (b - m) - g.apply_poisson(phi)
+    _, r2 = g.rbsor_sweep(phi, b, m, 1.5)
+    _, r2j = g.jacobi_sweep(phi, b, m, 0.8)
+    assert abs(r2 - (r * r).sum()) <= 1e-9 * (r * r).sum()
+    assert abs(r2j - (r * r).sum()) <= 1e-9 * (r * r).sum()
+
+
+def test_rbsor_converges_to_krylov_solution():
+    g, b, m = _poisson_setup(32)
+    x, _ = g.solve_poisson(b)
+    p = np.zeros(g.N)
+    om = 2 / (1 + np.sin(np.pi / 32))
+    for _ in range(400):
+        p, r2 = g.rbsor_sweep(p, b, m, om)
+    assert np.sqrt(r2) <= 1e-9 * np.linalg.norm(b - m)
+    np.testing.assert_allclose(p - p.mean(), x - x.mean(), atol=1e-9 * np.abs(x).max())
+
+
+def test_helmholtz_sweep_converges_to_krylov_solution():
+    g = OGrid.rectangle(20, 28, xratio=1.04)
+    rng = np.random.default_rng(3)
+    ru, rv = rng.uniform(-1, 1, g.N), rng.uniform(-1, 1, g.N)
+    alpha = 0.01
+    xu, _ = g.solve_helmholtz(alpha, ru)
+    u, v = np.zeros(g.N), np.zeros(g.N)
+    for _ in range(300):
+        u, v, r2 = g.helm_sweep(alpha, u, v, ru, rv, 1.0)
+    np.testing.assert_allclose(u, xu, atol=1e-10)
+    np.testing.assert_allclose(g.apply_helmholtz(alpha, u), ru, atol=1e-9)
+
+
+def test_operators_annihilate_constants():
+    g = OGrid.rectangle(10, 7, xratio=1.1, yratio=0.9)
+    assert np.abs(g.apply_poisson(np.full(g.N, 3.0))).max() < 1e-9
+    # wall / inlet phi ghost = phi (FluidSolver.cpp:87-88): constant phi has zero gradient
+    gx, gy = g.grad_phi(np.full(g.N, 2.0))
+    assert np.abs(gx).max() == 0 and np.abs(gy).max() == 0
+
+
+def test_golden_fixtures_reproduced():
+    """Committed oracle fixtures (tests/golden/make_golden.py) -- guards the restatement."""
+    idx = json.load(open(os.path.join(GOLD, "index.json")))
+    for case in idx["cases"]:
+        d = np.load(os.path.join(GOLD, case["file"]))
+        g = OGrid.rectangle(case["nx"], case["ny"], bc=case["bc"], xratio=case["xratio"], yratio=case["yratio"])
+        s = OSolver(g, case["dt"], case["re"], rtol=1e-13)
+        for k in range(case["steps"]):
+            mm, _ = s.step()
+            np.testing.assert_allclose(mm, d["mm"][k], rtol=0, atol=1e-11)
+        st = s.get()
+        np.testing.assert_allclose(st["u"], d["u"], rtol=0, atol=1e-11)
+        np.testing.assert_allclose(st["v"], d["v"], rtol=0, atol=1e-11)
