@@ -106,8 +106,10 @@ typedef struct ns_stats {
 #define NS_ARR_RU    5  /* RHS_u */
 #define NS_ARR_RV    6
 #define NS_ARR_RPHI  7  /* RHS_phi (div u* / dt, before mean removal) */
-#define NS_ARR_TMP   8  /* Jacobi ping-pong partner */
-#define NS_NUM_ARR   9
+#define NS_ARR_TMP   8  /* Poisson sweep ping-pong partner */
+#define NS_ARR_TMPU  9  /* Helmholtz sweep ping-pong partners */
+#define NS_ARR_TMPV 10
+#define NS_NUM_ARR  11
 
 /* kernels addressable by ns_kernel */
 #define NS_K_RHS        1  /* K1 rhs_velocity            (ConstructRHS_V, FluidSolver.cpp:327-363) */

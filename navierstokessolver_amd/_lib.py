@@ -19,8 +19,8 @@ NS_OK, NS_EINVAL, NS_EHIP, NS_ERCCL, NS_ENOMEM, NS_EDIVERGE = 0, -1, -2, -3, -4,
 NS_BC_INLET_UNI, NS_BC_INLET_PARABOLIC, NS_BC_WALL, NS_BC_PRESSURE, NS_BC_NEUMANN = 0, 1, 2, 3, 4
 NS_POISSON_RBSOR, NS_POISSON_JACOBI = 0, 1
 (NS_ARR_U, NS_ARR_V, NS_ARR_PHI, NS_ARR_CU, NS_ARR_CV, NS_ARR_RU, NS_ARR_RV, NS_ARR_RPHI,
- NS_ARR_TMP) = range(9)
-NS_NUM_ARR = 9
+ NS_ARR_TMP, NS_ARR_TMPU, NS_ARR_TMPV) = range(11)
+NS_NUM_ARR = 11
 (NS_K_RHS, NS_K_HELMHOLTZ, NS_K_DIV, NS_K_POISSON, NS_K_CORRECT, NS_K_HELM_SOLVE,
  NS_K_POIS_SOLVE, NS_K_RESIDUAL) = range(1, 9)
 

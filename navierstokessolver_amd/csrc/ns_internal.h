@@ -37,15 +37,16 @@ struct Partials {
 // K1: rhs_velocity (ConstructRHS_V); partials (sum ru^2, sum rv^2) per block
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
                const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st);
-// K2: fused red-black SOR sweep of (I - a L_V) on u and v; residual^2 partials (u, v) if part != null
-int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, double* u, double* v,
-                      const double* ru, const double* rv, double* part, hipStream_t st);
+// K2: fused red-black SOR sweep of (I - a L_V) on u and v, (u,v) -> (uo,vo);
+//     residual^2 partials (u, v) of the input if part != null
+int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                      double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st);
 // K3: divergence / dt  + partial sums (sum, sum^2)
 int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* rp,
                double* part, hipStream_t st);
-// K4: fused red-black SOR Poisson sweep (in place); residual^2 partials of the input iterate
-int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, double* phi, const double* rp,
-                      const double* shift, double* part, hipStream_t st);
+// K4: fused red-black SOR Poisson sweep phi -> out; residual^2 partials of the input iterate
+int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                      const double* rp, const double* shift, double* part, hipStream_t st);
 // K4 Jacobi: out = in + w (b - shift - L in)/diag
 int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* in, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st);

@@ -351,6 +351,9 @@ __global__ __launch_bounds__(256) void k_correct(Geo g, Coef c, double dt, doubl
 // neighbouring tiles -- identical arithmetic, so the result is exactly a
 // red-black SOR sweep), then the black cells of the tile, and writes the tile
 // once: one HBM pass per full sweep (24 B/cell Poisson, 48 B/cell u+v).
+// Out of place (ping-pong): an in-place sweep would let a late tile stage a
+// ring that an early tile already overwrote -- chaotic relaxation, which is
+// nondeterministic and diverges at omega ~ 2.
 // With RES the true residual of the input iterate is accumulated from the
 // staged old values at no extra traffic.
 //
@@ -372,7 +375,8 @@ struct Op {
 };
 
 struct SweepArgs {
-    double* q[2];
+    const double* q[2];   // input iterate (read only: tiles never see each other's writes)
+    double* qo[2];        // output iterate (ping-pong partner)
     const double* b[2];
     const double* shift;  // Poisson: device mean of rhs (null-space removal), else null
     double alpha, omega;
@@ -479,7 +483,7 @@ __global__ __launch_bounds__(256) void k_rb_sweep(SweepArgs A) {
         const int li = li0 + r, j = j0 + cc;
         if (li >= g.nxl || j >= g.ny) continue;
 #pragma unroll
-        for (int f = 0; f < NF; f++) A.q[f][(ptrdiff_t)li * ld + j] = sq[f][r + 2][cc + 2];
+        for (int f = 0; f < NF; f++) A.qo[f][(ptrdiff_t)li * ld + j] = sq[f][r + 2][cc + 2];
     }
     if (RES) block_reduce_sum<NF>(res, A.part + NF * blockIdx.x);
 }
@@ -647,10 +651,11 @@ static SweepArgs make_args(const Geo& g, const Coef& c, int TI, int TJ) {
     return a;
 }
 
-int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, double* phi, const double* rp,
-                      const double* shift, double* part, hipStream_t st) {
+int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                      const double* rp, const double* shift, double* part, hipStream_t st) {
     SweepArgs a = make_args(g, c, PTI, PTJ);
     a.q[0] = phi; a.q[1] = nullptr;
+    a.qo[0] = out; a.qo[1] = nullptr;
     a.b[0] = rp; a.b[1] = nullptr;
     a.shift = shift;
     a.omega = omega;
@@ -661,10 +666,11 @@ int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, double* phi, co
     return a.ntiles;
 }
 
-int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, double* u, double* v,
-                      const double* ru, const double* rv, double* part, hipStream_t st) {
+int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                      double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st) {
     SweepArgs a = make_args(g, c, HTI, HTJ);
     a.q[0] = u; a.q[1] = v;
+    a.qo[0] = uo; a.qo[1] = vo;
     a.b[0] = ru; a.b[1] = rv;
     a.shift = nullptr;
     a.omega = omega;

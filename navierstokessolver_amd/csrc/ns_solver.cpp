@@ -136,6 +136,29 @@ int ensure_events(ns_solver* s, size_t n) {
     return 0;
 }
 
+// one Helmholtz sweep U,V -> TMPU,TMPV, then swap so NS_ARR_U/V stay "current"
+int helm_sweep(ns_solver* s, double alpha, double* part) {
+    const int nb = nsg::launch_helm_sweep(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
+                                          s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
+                                          s->arr[NS_ARR_RV], part, s->st);
+    std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
+    std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
+    return nb;
+}
+
+// one Poisson sweep PHI -> TMP (RB-SOR or Jacobi), then swap
+int pois_sweep(ns_solver* s, double* part) {
+    int nb;
+    if (s->poisson == NS_POISSON_JACOBI)
+        nb = nsg::launch_pois_jacobi(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP],
+                                     s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, part ? part : s->part, s->st);
+    else
+        nb = nsg::launch_pois_rbsor(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP],
+                                    s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, part, s->st);
+    std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
+    return nb;
+}
+
 int next_batch(int prev_batch, double prev_r2, int prev_at, double r2, int at, double tol2, int cap) {
     // geometric model of the residual contraction between two checks
     if (prev_r2 > 0 && r2 > 0 && r2 < prev_r2 && at > prev_at) {
@@ -153,8 +176,6 @@ int next_batch(int prev_batch, double prev_r2, int prev_at, double r2, int at, d
 // Initial guess u^n (in place): converged solution is the same; fewer sweeps than the reference's zero guess.
 int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
     const double alpha = s->dt / (2 * s->re);
-    double* u = s->arr[NS_ARR_U];
-    double* v = s->arr[NS_ARR_V];
     const double tol2 = s->rtol * s->rtol;
     int sweeps = 0, batch = s->helm_batch0, prev_at = -1;
     double prev_r2 = -1;
@@ -162,9 +183,8 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         const int n = std::min(batch, s->max_iters - sweeps);
         int nb = 0;
         for (int k = 0; k < n; k++) {
-            CHK(halo(s, {u, v}, 2));
-            nb = nsg::launch_helm_sweep(s->g, s->c, alpha, s->omega_v, u, v, s->arr[NS_ARR_RU], s->arr[NS_ARR_RV],
-                                        k == n - 1 ? s->part : nullptr, s->st);
+            CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
+            nb = helm_sweep(s, alpha, k == n - 1 ? s->part : nullptr);
         }
         sweeps += n;
         nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_RES, s->st);
@@ -193,7 +213,6 @@ int pois_solve(ns_solver* s, int* its, double* res, ns_stats* stt) {
     const double tol2 = s->rtol * s->rtol;
     int sweeps = 0, batch = s->pois_batch0, prev_at = -1;
     double prev_r2 = -1;
-    const double* shift = s->scal + S_SHIFT;
     double tms = 0.0;
     int tn = 0, nchk = 0;
     for (;;) {
@@ -204,14 +223,7 @@ int pois_solve(ns_solver* s, int* its, double* res, ns_stats* stt) {
             double* part = k == n - 1 ? s->part : nullptr;
             CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
             if (s->timing) HIPCHK(hipEventRecord(s->ev[2 * k], s->st));
-            if (s->poisson == NS_POISSON_JACOBI) {
-                nb = nsg::launch_pois_jacobi(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP],
-                                             s->arr[NS_ARR_RPHI], shift, part ? part : s->part, s->st);
-                std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
-            } else {
-                nb = nsg::launch_pois_rbsor(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], shift,
-                                            part, s->st);
-            }
+            nb = pois_sweep(s, part);
             if (s->timing) HIPCHK(hipEventRecord(s->ev[2 * k + 1], s->st));
         }
         sweeps += n;
@@ -570,8 +582,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         int nb = 0;
         for (int k = 0; k < iters; k++) {
             CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
-            nb = nsg::launch_helm_sweep(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
-                                        s->arr[NS_ARR_RU], s->arr[NS_ARR_RV], k == iters - 1 ? s->part : nullptr, s->st);
+            nb = helm_sweep(s, alpha, k == iters - 1 ? s->part : nullptr);
         }
         if (iters > 0) {
             nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_RES, s->st);
@@ -592,14 +603,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         for (int k = 0; k < iters; k++) {
             double* part = k == iters - 1 ? s->part : nullptr;
             CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
-            if (s->poisson == NS_POISSON_JACOBI) {
-                nb = nsg::launch_pois_jacobi(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP],
-                                             s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, s->part, s->st);
-                std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
-            } else {
-                nb = nsg::launch_pois_rbsor(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI],
-                                            s->scal + S_SHIFT, part, s->st);
-            }
+            nb = pois_sweep(s, part);
         }
         if (iters > 0) {
             nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
@@ -662,26 +666,12 @@ int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
     CHK(ensure_events(s, 2 * (size_t)iters));
     for (int k = 0; k < warmup; k++) {
         CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
-        if (s->poisson == NS_POISSON_JACOBI) {
-            nsg::launch_pois_jacobi(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP], s->arr[NS_ARR_RPHI],
-                                    s->scal + S_SHIFT, s->part, s->st);
-            std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
-        } else {
-            nsg::launch_pois_rbsor(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,
-                                   nullptr, s->st);
-        }
+        pois_sweep(s, nullptr);
     }
     for (int k = 0; k < iters; k++) {
         CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
         HIPCHK(hipEventRecord(s->ev[2 * k], s->st));
-        if (s->poisson == NS_POISSON_JACOBI) {
-            nsg::launch_pois_jacobi(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP], s->arr[NS_ARR_RPHI],
-                                    s->scal + S_SHIFT, s->part, s->st);
-            std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
-        } else {
-            nsg::launch_pois_rbsor(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,
-                                   k == iters - 1 ? s->part : nullptr, s->st);
-        }
+        pois_sweep(s, k == iters - 1 ? s->part : nullptr);
         HIPCHK(hipEventRecord(s->ev[2 * k + 1], s->st));
     }
     HIPCHK(hipStreamSynchronize(s->st));
