@@ -51,6 +51,7 @@ typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm
 /* Poisson solvers */
 #define NS_POISSON_RBSOR  0  /* fused red-black SOR, one HBM pass per sweep (default) */
 #define NS_POISSON_JACOBI 1  /* weighted Jacobi (ping-pong) */
+#define NS_POISSON_MG     2  /* geometric multigrid V-cycles, RB Gauss-Seidel smoother (default) */
 
 /* One boundary edge of the polygon (Edge, Grid.h:20-26). */
 typedef struct ns_edge {
@@ -85,12 +86,15 @@ typedef struct ns_params {
     /* x-slab decomposition over ranks (one process per GPU) */
     int32_t rank, nranks;
     const void* nccl_id;      /* 128-byte ncclUniqueId from rank 0 (NULL if nranks == 1) */
+    /* multigrid (NS_POISSON_MG): smoothing sweeps per level before / after the coarse
+     * correction, and sweeps of the coarsest solve (0 = defaults 2 / 2 / automatic) */
+    int32_t mg_pre, mg_post, mg_coarse_iters;
 } ns_params;
 
 /* Per-step result (the reference prints iter, umin, umax, vmin, vmax: FluidSolver.cpp:559-560). */
 typedef struct ns_stats {
     double  umin, umax, vmin, vmax;
-    int32_t it_u, it_v, it_phi;      /* sweeps used by the two Helmholtz solves and the Poisson solve */
+    int32_t it_u, it_v, it_phi;      /* sweeps of the Helmholtz solves; Poisson sweeps (RB-SOR / Jacobi) or V-cycles (MG) */
     double  res_u, res_v, res_phi;   /* final relative residuals (of the input of the last sweep) */
     double  t_poisson_kernel_ms;     /* sum of Poisson sweep-kernel durations (timing == 1) */
     int32_t n_poisson_kernels;       /* number of Poisson sweep kernels timed */

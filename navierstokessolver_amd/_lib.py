@@ -17,7 +17,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "nsgpu.h")
 # ---- constants mirrored from include/nsgpu.h (checked by tests/test_abi.py) ----
 NS_OK, NS_EINVAL, NS_EHIP, NS_ERCCL, NS_ENOMEM, NS_EDIVERGE = 0, -1, -2, -3, -4, -5
 NS_BC_INLET_UNI, NS_BC_INLET_PARABOLIC, NS_BC_WALL, NS_BC_PRESSURE, NS_BC_NEUMANN = 0, 1, 2, 3, 4
-NS_POISSON_RBSOR, NS_POISSON_JACOBI = 0, 1
+NS_POISSON_RBSOR, NS_POISSON_JACOBI, NS_POISSON_MG = 0, 1, 2
 (NS_ARR_U, NS_ARR_V, NS_ARR_PHI, NS_ARR_CU, NS_ARR_CV, NS_ARR_RU, NS_ARR_RV, NS_ARR_RPHI,
  NS_ARR_TMP, NS_ARR_TMPU, NS_ARR_TMPV) = range(11)
 NS_NUM_ARR = 11
@@ -42,7 +42,8 @@ class NsParams(ctypes.Structure):
                 ("rtol", ctypes.c_double), ("max_iters", ctypes.c_int32), ("omega", ctypes.c_double),
                 ("omega_v", ctypes.c_double), ("check_every", ctypes.c_int32),
                 ("device", ctypes.c_int32), ("timing", ctypes.c_int32),
-                ("rank", ctypes.c_int32), ("nranks", ctypes.c_int32), ("nccl_id", ctypes.c_void_p)]
+                ("rank", ctypes.c_int32), ("nranks", ctypes.c_int32), ("nccl_id", ctypes.c_void_p),
+                ("mg_pre", ctypes.c_int32), ("mg_post", ctypes.c_int32), ("mg_coarse_iters", ctypes.c_int32)]
 
 
 class NsStats(ctypes.Structure):

@@ -13,7 +13,7 @@ constexpr int HALO = 2;  // ghost rows per side of every field (K1's MUSCL stenc
 struct Geo {
     int nx, ny;       // global cells
     int i0, nxl;      // slab start (global) and local rows
-    int ld;           // row stride in doubles (ny rounded up to 32)
+    int ld;           // row stride in doubles (ny rounded up to 128: one streaming strip = 1 KiB per wave)
     // rectangle sides 0=W,1=E,2=S,3=N: velocity ghost q_g = neu ? q : -q + c[d]
     // (EvaluateGhostStencil_V, FluidSolver.cpp:166-173; constants :89-96)
     int neu[4];
@@ -38,7 +38,7 @@ struct Partials {
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
                const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st);
 // K2: fused red-black SOR sweep of (I - a L_V) on u and v, (u,v) -> (uo,vo);
-//     residual^2 partials (u, v) of the input if part != null
+//     residual^2 partials of the input if part != null: u at part[0..n), v at part[n..2n), n returned
 int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
                       double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st);
 // K3: divergence / dt  + partial sums (sum, sum^2)
@@ -50,6 +50,13 @@ int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* p
 // K4 Jacobi: out = in + w (b - shift - L in)/diag
 int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* in, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st);
+// A/B reference: LDS-tiled fused sweeps (first version)
+int launch_pois_rbsor_tiled(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                            const double* rp, const double* shift, double* part, hipStream_t st);
+int launch_pois_jacobi_tiled(const Geo& g, const Coef& c, double omega, const double* in, double* out,
+                             const double* rp, const double* shift, double* part, hipStream_t st);
+// rows per streaming strip (tuning knob)
+void set_strip_rows(int L);
 // residual only
 int launch_pois_residual(const Geo& g, const Coef& c, const double* phi, const double* rp,
                          const double* shift, double* part, hipStream_t st);
@@ -66,6 +73,15 @@ void launch_finish_mean(const double* sums, double ncells, double* shift_and_bn2
 int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st);
 // random fill of phi, rhs (sweep benchmark input)
 void launch_fill_random(const Geo& g, double* phi, double* rp, uint64_t seed, hipStream_t st);
+
+// multigrid transfers (K4 MG): fine residual -> coarse rhs (+ coarse phi := 0, partials of r^2 over
+// fine cells); fine phi += bilinear(coarse correction); coarsest solve in one workgroup's LDS
+int launch_restrict(const Geo& gf, const Coef& cf, const double* phi, const double* b, const double* shift,
+                    const Geo& gc, const Coef& cc, double* bc, double* pc, double* part, hipStream_t st);
+void launch_prolong(const Geo& gf, double* phi, const Geo& gc, const double* ec, hipStream_t st);
+size_t coarse_lds_bytes(const Geo& g);
+int launch_coarse_lds(const Geo& g, const Coef& c, double* phi, const double* b, double omega, int iters,
+                      hipStream_t st);
 
 // max partials any launcher writes for this geometry
 int max_partials(const Geo& g);

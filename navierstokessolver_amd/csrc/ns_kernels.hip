@@ -16,6 +16,8 @@
 // No MFMA: every kernel is a stencil far below the fp64 VALU ridge point; HBM bound.
 #include "ns_internal.h"
 
+#include <algorithm>
+
 namespace nsg {
 
 // ---------------------------------------------------------------- helpers
@@ -532,6 +534,278 @@ __global__ __launch_bounds__(256) void k_jacobi(SweepArgs A, const double* __res
     if (A.part) block_reduce_sum<1>(res, A.part + blockIdx.x);
 }
 
+// ------------------------------------------------ K2 / K4: register-streaming sweep
+// One wave owns a strip of rows [ib, ib+L) x 128 loaded columns [jb-2, jb+126)
+// (2 per lane, double2 = 16 B/lane loads: 1 KiB per wave-instruction) and walks
+// it along i with a 3-row window in registers.  Strips overlap by 2 columns on
+// each side: lane 0's and lane 63's cells only feed their neighbours, so every
+// j-neighbour a written cell needs is in an adjacent lane (cross-lane shuffle) --
+// no halo loads, no halo registers -- and each strip writes 124 columns.
+// Red-black: while row r arrives, row r-1 gets its red update (old neighbours)
+// and row r-2 its black update (red neighbours) and is stored: one read of phi
+// and b and one write of phi per cell and sweep (24 B/cell).  Jacobi: row r-1 is
+// relaxed from old rows r-2..r and stored.  Rows are prefetched D ahead.
+// Out of place (in -> out): strips never observe each other's writes.
+constexpr int SW = 124;   // written columns per strip
+constexpr int SD = 4;     // rows in flight per wave
+
+struct StreamArgs {
+    const double* in;
+    double* out;
+    const double* b;
+    const double* shift;              // Poisson: device mean of b (null-space removal), else null
+    const double *cw, *ce, *bx;       // per global row: weights toward i-1 / i+1, Helmholtz wall term
+    const double *cs, *cn, *by;       // per column
+    double alpha, omega;
+    int nx, ny, i0, nxl, ld;
+    int nsj, nsi, L;                  // strips along j, along i, rows per strip
+    double* part;                     // one residual partial per strip
+};
+
+// diagonal of the operator at a cell from its row / column coefficient sums
+template <int OP>
+__device__ __forceinline__ double diag(double rowd, double cold, double alpha) {
+    return OP == 0 ? -(rowd + cold) : 1.0 + alpha * (rowd + cold);
+}
+
+// relaxed value q + w (b - A q), w = omega / diag; `res` = b - A q of the input values
+// (OP 0: Poisson L, OP 1: Helmholtz I - a L_V)
+template <int OP>
+__device__ __forceinline__ double relax(double q, double xm, double xp, double ym, double yp, double b, double cw,
+                                        double ce, double cs, double cn, double dg, double w, double alpha,
+                                        double& res) {
+    const double s = cw * xm + ce * xp + cs * ym + cn * yp;
+    const double aq = OP == 0 ? s + dg * q : dg * q - alpha * s;
+    res = b - aq;
+    return q + w * res;
+}
+
+// per-lane cache of diag and omega/diag for the two columns, refreshed only when the
+// row's coefficient sum changes (boundary rows, stretched grids): one division per
+// cell on the first row instead of one per update
+template <int OP>
+struct DiagCache {
+    double rowd = -1.0, d0 = 0, d1 = 0, w0 = 0, w1 = 0;
+    __device__ __forceinline__ void at(double rd, double cd0, double cd1, double alpha, double omega) {
+        if (rd != rowd) {
+            rowd = rd;
+            d0 = diag<OP>(rd, cd0, alpha);
+            d1 = diag<OP>(rd, cd1, alpha);
+            w0 = omega / d0;
+            w1 = omega / d1;
+        }
+    }
+};
+
+template <int OP, bool RB, bool RES>
+__global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int nstr = a.nsj * a.nsi;
+    const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    double res = 0.0;
+    if (wid < nstr) {
+        const int si = wid / a.nsj, sj = wid - si * a.nsj;
+        const int jb = sj * SW, ib = si * a.L;
+        const int ie = min(ib + a.L, a.nxl);
+        const int ny = a.ny, ld = a.ld;
+        const int c0 = jb - 2 + 2 * lane, c1 = c0 + 1;
+        const int lc = min(max(c0, 0), ld - 2);                 // clamped 16-B aligned pair
+        const bool v0 = c0 >= 0 && c0 < ny, v1 = c1 >= 0 && c1 < ny;   // cells inside the domain
+        const bool wr = lane >= 1 && lane <= 62 && c0 < ny;      // this lane's pair is written
+        const bool o0 = wr && v0, o1 = wr && v1;                 // ... and counts in the residual
+        const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
+        const double cs0 = a.cs[k0], cn0 = a.cn[k0], cd0 = cs0 + cn0 + (OP == 1 ? a.by[k0] : 0.0);
+        const double cs1 = a.cs[k1], cn1 = a.cn[k1], cd1 = cs1 + cn1 + (OP == 1 ? a.by[k1] : 0.0);
+        const double shift = (OP == 0 && a.shift) ? a.shift[0] : 0.0;
+        const double alpha = a.alpha, omega = a.omega;
+        const int rlo = -HALO, rhi = a.nxl + HALO - 1;
+
+        // one row of phi (row r) and of b (row r-1), per lane
+        double2 Q[SD], QB[SD];
+        auto load = [&](int slot_r, double2& p, double2& bb) {
+            const int lp = min(max(slot_r, rlo), rhi), lb = min(max(slot_r - 1, rlo), rhi);
+            p = *reinterpret_cast<const double2*>(a.in + (ptrdiff_t)lp * ld + lc);
+            bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
+        };
+
+        double2 P0 = {0, 0}, P1 = {0, 0}, P2 = {0, 0}, R0 = {0, 0}, R1 = {0, 0}, R2 = {0, 0};
+        double2 Bm = {0, 0}, Bk = {0, 0};
+
+        DiagCache<OP> dm, dk;   // red-stage row m / black-stage row k
+        auto step = [&](const double2 p, const double2 bb, int r) {
+            P0 = P1; P1 = P2; P2 = p;
+            Bk = Bm;
+            Bm = make_double2(bb.x - shift, bb.y - shift);
+            const int m = r - 1, gim = a.i0 + m;
+            double2 Rn = P1;
+            if (m >= ib - 1 && m <= ie) {
+                double lf = __shfl_up(P1.y, 1, 64), rt = __shfl_down(P1.x, 1, 64);
+                const int gc = min(max(gim, 0), a.nx - 1);
+                const double cw = a.cw[gc], ce = a.ce[gc];
+                dm.at(cw + ce + (OP == 1 ? a.bx[gc] : 0.0), cd0, cd1, alpha, omega);
+                double r0, r1;
+                if (RES && m >= ib && m < ie) {
+                    relax<OP>(P1.x, P0.x, P2.x, lf, P1.y, Bm.x, cw, ce, cs0, cn0, dm.d0, dm.w0, alpha, r0);
+                    relax<OP>(P1.y, P0.y, P2.y, P1.x, rt, Bm.y, cw, ce, cs1, cn1, dm.d1, dm.w1, alpha, r1);
+                    res += (o0 ? r0 * r0 : 0.0) + (o1 ? r1 * r1 : 0.0);
+                }
+                if (!RB) {
+                    if (m >= ib && m < ie) {
+                        double2 o = P1;
+                        if (v0) o.x = relax<OP>(P1.x, P0.x, P2.x, lf, P1.y, Bm.x, cw, ce, cs0, cn0, dm.d0, dm.w0, alpha, r0);
+                        if (v1) o.y = relax<OP>(P1.y, P0.y, P2.y, P1.x, rt, Bm.y, cw, ce, cs1, cn1, dm.d1, dm.w1, alpha, r1);
+                        if (wr) *reinterpret_cast<double2*>(a.out + (ptrdiff_t)m * ld + c0) = o;
+                    }
+                } else if (gim >= 0 && gim < a.nx) {
+                    if ((gim & 1) == 0) {  // red = (gi + j) even = c0
+                        if (v0) Rn.x = relax<OP>(P1.x, P0.x, P2.x, lf, P1.y, Bm.x, cw, ce, cs0, cn0, dm.d0, dm.w0, alpha, r0);
+                    } else {               // red = c1
+                        if (v1) Rn.y = relax<OP>(P1.y, P0.y, P2.y, P1.x, rt, Bm.y, cw, ce, cs1, cn1, dm.d1, dm.w1, alpha, r1);
+                    }
+                }
+            }
+            if (RB) {
+                R0 = R1; R1 = R2; R2 = Rn;
+                const int k = r - 2, gik = a.i0 + k;
+                if (k >= ib && k < ie) {
+                    const double lf = __shfl_up(R1.y, 1, 64), rt = __shfl_down(R1.x, 1, 64);
+                    const double cw = a.cw[gik], ce = a.ce[gik];
+                    dk.at(cw + ce + (OP == 1 ? a.bx[gik] : 0.0), cd0, cd1, alpha, omega);
+                    double2 o = R1;
+                    double rr;
+                    if ((gik & 1) == 0) {  // black = c1
+                        if (v1) o.y = relax<OP>(R1.y, R0.y, R2.y, R1.x, rt, Bk.y, cw, ce, cs1, cn1, dk.d1, dk.w1, alpha, rr);
+                    } else {               // black = c0
+                        if (v0) o.x = relax<OP>(R1.x, R0.x, R2.x, lf, R1.y, Bk.x, cw, ce, cs0, cn0, dk.d0, dk.w0, alpha, rr);
+                    }
+                    if (wr) *reinterpret_cast<double2*>(a.out + (ptrdiff_t)k * ld + c0) = o;
+                }
+            }
+        };
+
+        // rows ib-2 .. ie+1 (RB) / ib-1 .. ie (Jacobi); SD rows in flight
+        const int r0 = RB ? ib - 2 : ib - 1, r1 = RB ? ie + 1 : ie;
+#pragma unroll
+        for (int q = 0; q < SD; q++) load(r0 + q, Q[q], QB[q]);
+        for (int r = r0; r <= r1; r += SD) {
+#pragma unroll
+            for (int q = 0; q < SD; q++) {
+                if (r + q <= r1) step(Q[q], QB[q], r + q);
+                load(r + q + SD, Q[q], QB[q]);
+            }
+        }
+    }
+    if (RES) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
+        if (lane == 0 && wid < nstr) a.part[wid] = res;
+    }
+}
+
+// ------------------------------------------------ K4 multigrid transfer kernels
+// Cell-centred geometric multigrid for L phi = b (the Poisson solve of
+// FluidSolver.cpp:551): each coarse cell is the union of 2 x 2 fine cells, the
+// coarse operator is ConstructLHS's stencil rediscretised on the coarse spacings
+// (hx_c = hx_2I + hx_2I+1), restriction is the area-weighted average of the fine
+// residuals and prolongation is bilinear (9/16, 3/16, 3/16, 1/16; a missing coarse
+// neighbour at a wall is replaced by the parent -- the zero-flux reflection).
+// Both transfers are one HBM pass over the fine level (16 B/cell and 24 B/cell).
+
+// residual b - shift - L phi at fine cell (li, j)
+__device__ __forceinline__ double pois_residual(const Geo& g, const Coef& c, const double* phi, const double* b,
+                                                double shift, int li, int j) {
+    const int gi = g.i0 + li, ld = g.ld;
+    const double cw = c.pw[gi], ce = c.pe[gi], cs = c.ps[j], cn = c.pn[j];
+    const double q = ldf(phi, ld, li, j);
+    const double s = cw * ldf(phi, ld, li - 1, j) + ce * ldf(phi, ld, li + 1, j) +
+                     cs * ldf(phi, ld, li, max(j - 1, 0)) + cn * ldf(phi, ld, li, min(j + 1, g.ny - 1));
+    const double dg = -((cw + ce) + (cs + cn));
+    return (ldf(b, ld, li, j) - shift) - (s + dg * q);
+}
+
+// fine residual -> coarse rhs (area-weighted average), coarse phi := 0; partials of sum r^2 (fine)
+__global__ __launch_bounds__(256) void k_restrict(Geo gf, Coef cf, const double* __restrict__ phi,
+                                                  const double* __restrict__ b, const double* __restrict__ shiftp,
+                                                  Geo gc, Coef cc, double* __restrict__ bc, double* __restrict__ pc,
+                                                  double* __restrict__ part) {
+    const int J = blockIdx.x * 64 + threadIdx.x;
+    const int I = blockIdx.y * 4 + threadIdx.y;
+    double acc[1] = {0.0};
+    if (J < gc.ny && I < gc.nxl) {
+        const double shift = shiftp ? shiftp[0] : 0.0;
+        double sum = 0.0;
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const int li = 2 * I + a, j = 2 * J + q;
+                const double r = pois_residual(gf, cf, phi, b, shift, li, j);
+                sum += (cf.hx[gf.i0 + li] * cf.hy[j]) * r;
+                acc[0] += r * r;
+            }
+        const int gI = gc.i0 + I;
+        bc[(ptrdiff_t)I * gc.ld + J] = sum / (cc.hx[gI] * cc.hy[J]);
+        pc[(ptrdiff_t)I * gc.ld + J] = 0.0;
+    }
+    block_reduce_sum<1>(acc, part + (blockIdx.x + gridDim.x * blockIdx.y));
+}
+
+// fine phi += bilinear interpolation of the coarse correction
+__global__ __launch_bounds__(256) void k_prolong(Geo gf, double* __restrict__ phi, Geo gc,
+                                                 const double* __restrict__ ec) {
+    const int j = blockIdx.x * 64 + threadIdx.x;
+    const int li = blockIdx.y * 4 + threadIdx.y;
+    if (j >= gf.ny || li >= gf.nxl) return;
+    const int I = li >> 1, Jc = j >> 1;
+    const int In = (li & 1) ? I + 1 : I - 1;        // coarse row on this child's side
+    const int Jn = (j & 1) ? Jc + 1 : Jc - 1;
+    const int gIn = gc.i0 + In;
+    const int Iu = (gIn >= 0 && gIn < gc.nx) ? In : I;       // wall: reflect onto the parent
+    const int Ju = (Jn >= 0 && Jn < gc.ny) ? Jn : Jc;
+    const double e = (9.0 * ldf(ec, gc.ld, I, Jc) + 3.0 * ldf(ec, gc.ld, Iu, Jc) + 3.0 * ldf(ec, gc.ld, I, Ju) +
+                      ldf(ec, gc.ld, Iu, Ju)) * 0.0625;
+    phi[(ptrdiff_t)li * gf.ld + j] += e;
+}
+
+// coarsest level, whole grid resident in one workgroup's LDS: `iters` red-black SOR
+// sweeps in place (barrier between colours), phi starts at 0
+__global__ __launch_bounds__(1024) void k_coarse_lds(Geo g, Coef c, double* __restrict__ phi,
+                                                     const double* __restrict__ b, double omega, int iters) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int nx = g.nx, ny = g.ny, n = nx * ny;
+    double* sp = lds;
+    double* sb = lds + n;
+    double* cw = sb + n;
+    double* ce = cw + nx;
+    double* cs = ce + nx;
+    double* cn = cs + ny;
+    for (int k = threadIdx.x; k < n; k += 1024) {
+        const int i = k / ny, j = k - i * ny;
+        sp[k] = ldf(phi, g.ld, i, j);
+        sb[k] = ldf(b, g.ld, i, j);
+    }
+    for (int k = threadIdx.x; k < nx; k += 1024) { cw[k] = c.pw[k]; ce[k] = c.pe[k]; }
+    for (int k = threadIdx.x; k < ny; k += 1024) { cs[k] = c.ps[k]; cn[k] = c.pn[k]; }
+    __syncthreads();
+    for (int it = 0; it < iters; it++)
+        for (int color = 0; color < 2; color++) {
+            for (int k = threadIdx.x; k < n; k += 1024) {
+                const int i = k / ny, j = k - i * ny;
+                if (((i + j) & 1) != color) continue;
+                const double q = sp[k];
+                const double s = cw[i] * sp[k - (i > 0 ? ny : 0)] + ce[i] * sp[k + (i < nx - 1 ? ny : 0)] +
+                                 cs[j] * sp[k - (j > 0 ? 1 : 0)] + cn[j] * sp[k + (j < ny - 1 ? 1 : 0)];
+                const double dg = -((cw[i] + ce[i]) + (cs[j] + cn[j]));
+                sp[k] = q + omega * (sb[k] - (s + dg * q)) / dg;
+            }
+            __syncthreads();
+        }
+    for (int k = threadIdx.x; k < n; k += 1024) {
+        const int i = k / ny, j = k - i * ny;
+        phi[(ptrdiff_t)i * g.ld + j] = sp[k];
+    }
+}
+
 // ---------------------------------------------------------------- reductions
 __global__ __launch_bounds__(1024) void k_reduce_sum(const double* __restrict__ p, int n, int nv,
                                                      double* __restrict__ out) {
@@ -610,8 +884,9 @@ static inline dim3 cell_grid(const Geo& g) { return dim3((g.ny + 63) / 64, (g.nx
 int max_partials(const Geo& g) {
     const dim3 cg = cell_grid(g);
     int n = (int)(cg.x * cg.y) * 4;
-    const int tiles = ((g.nxl + 7) / 8) * ((g.ny + 63) / 64) * 2;  // generous bound over sweep tilings
-    return n > tiles ? n : tiles;
+    const int tiles = ((g.nxl + 7) / 8) * ((g.ny + 63) / 64) * 2;   // tiled sweeps
+    const int strips = ((g.nxl + 3) / 4) * ((g.ny + 123) / 124) * 2;  // streaming sweeps, strip rows >= 4
+    return std::max(n, std::max(tiles, strips));
 }
 
 }  // namespace nsg
@@ -640,7 +915,7 @@ int launch_correct(const Geo& g, const Coef& c, double dt, double* u, double* v,
 }
 
 // Poisson tile: 32 x 128 (73 KB LDS, 2 workgroups / CU); Helmholtz u+v tile: 16 x 128.
-constexpr int PTI = 32, PTJ = 128, HTI = 16, HTJ = 128, JTI = 16, JTJ = 128;
+constexpr int PTI = 32, PTJ = 128, JTI = 16, JTJ = 128;
 
 static SweepArgs make_args(const Geo& g, const Coef& c, int TI, int TJ) {
     SweepArgs a{};
@@ -651,7 +926,51 @@ static SweepArgs make_args(const Geo& g, const Coef& c, int TI, int TJ) {
     return a;
 }
 
+static int g_strip_rows = 64;
+void set_strip_rows(int L) { if (L >= 4) g_strip_rows = L & ~1; }
+
+static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, double* out, const double* b,
+                              const double* shift, double alpha, double omega, double* part, bool helm) {
+    StreamArgs a{};
+    a.in = in; a.out = out; a.b = b; a.shift = shift;
+    a.cw = c.pw; a.ce = c.pe; a.bx = c.bx; a.cs = c.ps; a.cn = c.pn; a.by = c.by;
+    (void)helm;
+    a.alpha = alpha; a.omega = omega;
+    a.nx = g.nx; a.ny = g.ny; a.i0 = g.i0; a.nxl = g.nxl; a.ld = g.ld;
+    a.L = g_strip_rows;
+    a.nsj = (g.ny + SW - 1) / SW;
+    a.nsi = (g.nxl + a.L - 1) / a.L;
+    a.part = part;
+    return a;
+}
+
+template <int OP, bool RB>
+static int launch_stream(const StreamArgs& a, hipStream_t st) {
+    const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
+    if (a.part) hipLaunchKernelGGL((k_sweep<OP, RB, true>), dim3(nblk), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_sweep<OP, RB, false>), dim3(nblk), dim3(256), 0, st, a);
+    return nstr;
+}
+
 int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                      const double* rp, const double* shift, double* part, hipStream_t st) {
+    return launch_stream<0, true>(stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false), st);
+}
+
+int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* in, double* out, const double* rp,
+                       const double* shift, double* part, hipStream_t st) {
+    return launch_stream<0, false>(stream_args(g, c, in, out, rp, shift, 0.0, omega, part, false), st);
+}
+
+int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                      double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st) {
+    // u and v are independent systems with the same operator: two streaming passes
+    const int n = launch_stream<1, true>(stream_args(g, c, u, uo, ru, nullptr, alpha, omega, part, true), st);
+    launch_stream<1, true>(stream_args(g, c, v, vo, rv, nullptr, alpha, omega, part ? part + n : nullptr, true), st);
+    return n;
+}
+
+int launch_pois_rbsor_tiled(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                       const double* rp, const double* shift, double* part, hipStream_t st) {
     SweepArgs a = make_args(g, c, PTI, PTJ);
     a.q[0] = phi; a.q[1] = nullptr;
@@ -666,23 +985,8 @@ int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* p
     return a.ntiles;
 }
 
-int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
-                      double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st) {
-    SweepArgs a = make_args(g, c, HTI, HTJ);
-    a.q[0] = u; a.q[1] = v;
-    a.qo[0] = uo; a.qo[1] = vo;
-    a.b[0] = ru; a.b[1] = rv;
-    a.shift = nullptr;
-    a.omega = omega;
-    a.alpha = alpha;
-    a.part = part;
-    if (part) hipLaunchKernelGGL((k_rb_sweep<HTI, HTJ, 1, 2, true>), dim3(a.ntiles), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_rb_sweep<HTI, HTJ, 1, 2, false>), dim3(a.ntiles), dim3(256), 0, st, a);
-    return a.ntiles;
-}
-
-int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* in, double* out, const double* rp,
-                       const double* shift, double* part, hipStream_t st) {
+int launch_pois_jacobi_tiled(const Geo& g, const Coef& c, double omega, const double* in, double* out,
+                             const double* rp, const double* shift, double* part, hipStream_t st) {
     SweepArgs a = make_args(g, c, JTI, JTJ);
     a.b[0] = rp;
     a.shift = shift;
@@ -701,6 +1005,32 @@ int launch_pois_residual(const Geo& g, const Coef& c, const double* phi, const d
     a.part = part;
     hipLaunchKernelGGL((k_jacobi<JTI, JTJ>), dim3(a.ntiles), dim3(256), 0, st, a, phi, (double*)nullptr, 0);
     return a.ntiles;
+}
+
+int launch_restrict(const Geo& gf, const Coef& cf, const double* phi, const double* b, const double* shift,
+                    const Geo& gc, const Coef& cc, double* bc, double* pc, double* part, hipStream_t st) {
+    const dim3 cg = cell_grid(gc);
+    hipLaunchKernelGGL(k_restrict, cg, dim3(64, 4), 0, st, gf, cf, phi, b, shift, gc, cc, bc, pc, part);
+    return (int)(cg.x * cg.y);
+}
+
+void launch_prolong(const Geo& gf, double* phi, const Geo& gc, const double* ec, hipStream_t st) {
+    hipLaunchKernelGGL(k_prolong, cell_grid(gf), dim3(64, 4), 0, st, gf, phi, gc, ec);
+}
+
+size_t coarse_lds_bytes(const Geo& g) { return sizeof(double) * (2 * (size_t)g.nx * g.ny + 2 * g.nx + 2 * g.ny); }
+
+int launch_coarse_lds(const Geo& g, const Coef& c, double* phi, const double* b, double omega, int iters,
+                      hipStream_t st) {
+    const size_t bytes = coarse_lds_bytes(g);
+    if (bytes > 160 * 1024 || g.nxl != g.nx) return -1;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_coarse_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_coarse_lds, dim3(1), dim3(1024), bytes, st, g, c, phi, b, omega, iters);
+    return 0;
 }
 
 void launch_reduce_sum(const double* p, int n, int nv, double* out, hipStream_t st) {

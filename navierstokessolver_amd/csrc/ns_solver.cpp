@@ -72,6 +72,16 @@ enum {
 
 }  // namespace
 
+// one multigrid level (level 0 = the solver's own PHI / TMP / RPHI arrays)
+struct MgLevel {
+    nsg::Geo g{};
+    nsg::Coef c{};
+    double *phi = nullptr, *tmp = nullptr, *b = nullptr;  // current iterate, ping-pong partner, rhs
+    double* mem = nullptr;                               // planes (levels >= 1)
+    double* coef = nullptr;                              // coefficient tables (levels >= 1)
+    std::vector<double> hx, hy;                          // host spacings
+};
+
 struct ns_solver {
     nsg::Geo g{};
     nsg::Coef c{};
@@ -91,14 +101,19 @@ struct ns_solver {
     double ncells = 0;           // global cell count
     std::vector<hipEvent_t> ev;  // timing events (pairs)
     int helm_batch0 = 4, pois_batch0 = 8;
+    int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
+    std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
+    int mg_pre = 2, mg_post = 2, mg_coarse_iters = 0;
+    double mg_omega_c = 1.0, mg_omega_s = 1.0;
+    bool mg_coarse_lds = false;
 };
 
 namespace {
 
-int halo(ns_solver* s, std::initializer_list<double*> fields, int w) {
+int halo_g(ns_solver* s, const nsg::Geo& g, std::initializer_list<double*> fields, int w) {
     if (s->nranks == 1) return 0;
-    const size_t cnt = (size_t)w * s->g.ld;
-    const int ld = s->g.ld, nxl = s->g.nxl;
+    const size_t cnt = (size_t)w * g.ld;
+    const int ld = g.ld, nxl = g.nxl;
     NCCLCHK(ncclGroupStart());
     for (double* f : fields) {
         if (s->rank > 0) {
@@ -113,6 +128,8 @@ int halo(ns_solver* s, std::initializer_list<double*> fields, int w) {
     NCCLCHK(ncclGroupEnd());
     return 0;
 }
+
+int halo(ns_solver* s, std::initializer_list<double*> fields, int w) { return halo_g(s, s->g, fields, w); }
 
 int allreduce(ns_solver* s, double* d, int n, ncclRedOp_t op) {
     if (s->nranks == 1) return 0;
@@ -149,7 +166,14 @@ int helm_sweep(ns_solver* s, double alpha, double* part) {
 // one Poisson sweep PHI -> TMP (RB-SOR or Jacobi), then swap
 int pois_sweep(ns_solver* s, double* part) {
     int nb;
-    if (s->poisson == NS_POISSON_JACOBI)
+    if (s->tiled) {
+        if (s->poisson == NS_POISSON_JACOBI)
+            nb = nsg::launch_pois_jacobi_tiled(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP],
+                                               s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, part ? part : s->part, s->st);
+        else
+            nb = nsg::launch_pois_rbsor_tiled(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP],
+                                              s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, part, s->st);
+    } else if (s->poisson == NS_POISSON_JACOBI)
         nb = nsg::launch_pois_jacobi(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP],
                                      s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, part ? part : s->part, s->st);
     else
@@ -187,7 +211,8 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
             nb = helm_sweep(s, alpha, k == n - 1 ? s->part : nullptr);
         }
         sweeps += n;
-        nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_RES, s->st);
+        nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
+        nsg::launch_reduce_sum(s->part + nb, nb, 1, s->scal + S_RES + 1, s->st);
         CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
         CHK(fetch(s));
         const double r2u = s->hs[S_RES], r2v = s->hs[S_RES + 1];
@@ -255,6 +280,182 @@ int pois_solve(ns_solver* s, int* its, double* res, ns_stats* stt) {
         stt->n_poisson_kernels += tn;
         stt->n_checks += nchk;
     }
+    return 0;
+}
+
+// ---------------- multigrid Poisson solve (V-cycles; smoother = the streaming RB sweep)
+MgLevel& level(ns_solver* s, int l) {
+    MgLevel& L = s->lv[l];
+    if (l == 0) { L.phi = s->arr[NS_ARR_PHI]; L.tmp = s->arr[NS_ARR_TMP]; L.b = s->arr[NS_ARR_RPHI]; }
+    return L;
+}
+
+int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
+    MgLevel& L = level(s, l);
+    for (int k = 0; k < n; k++) {
+        CHK(halo_g(s, L.g, {L.phi}, 2));
+        const bool t = s->timing && l == 0;
+        if (t) HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st));
+        nsg::launch_pois_rbsor(L.g, L.c, s->mg_omega_s, L.phi, L.tmp, L.b, l == 0 ? s->scal + S_SHIFT : nullptr,
+                               nullptr, s->st);
+        if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn) + 1], s->st)); (*tn)++; }
+        std::swap(L.phi, L.tmp);
+        if (l == 0) { s->arr[NS_ARR_PHI] = L.phi; s->arr[NS_ARR_TMP] = L.tmp; }
+    }
+    return 0;
+}
+
+int mg_coarse(ns_solver* s) {
+    MgLevel& L = level(s, (int)s->lv.size() - 1);
+    if (s->mg_coarse_lds) {
+        if (nsg::launch_coarse_lds(L.g, L.c, L.phi, L.b, s->mg_omega_c, s->mg_coarse_iters, s->st) != 0) {
+            set_err("coarse LDS solve does not fit");
+            return NS_EINVAL;
+        }
+        return 0;
+    }
+    for (int k = 0; k < s->mg_coarse_iters; k++) {
+        CHK(halo_g(s, L.g, {L.phi}, 2));
+        nsg::launch_pois_rbsor(L.g, L.c, s->mg_omega_c, L.phi, L.tmp, L.b, nullptr, nullptr, s->st);
+        std::swap(L.phi, L.tmp);
+    }
+    return 0;
+}
+
+int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
+    const double tol2 = s->rtol * s->rtol;
+    const int nl = (int)s->lv.size();
+    const int maxc = std::min(s->max_iters, 1000);
+    int cycles = 0, tn = 0, nchk = 0;
+    double tms = 0.0;
+    const int per_cycle = s->mg_pre + s->mg_post;
+    for (;;) {
+        if (s->timing) CHK(ensure_events(s, 2 * (size_t)(tn + per_cycle)));
+        const int ev0 = 0;
+        bool done = false;
+        for (int l = 0; l < nl - 1 && !done; l++) {
+            CHK(mg_smooth(s, l, s->mg_pre, &tn, ev0));
+            MgLevel& F = level(s, l);
+            MgLevel& C = level(s, l + 1);
+            CHK(halo_g(s, F.g, {F.phi}, 1));
+            const int nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, l == 0 ? s->scal + S_SHIFT : nullptr, C.g, C.c,
+                                                C.b, C.phi, s->part, s->st);
+            CHK(halo_g(s, C.g, {C.b}, 1));
+            if (l == 0) {
+                // fine residual after pre-smoothing: the convergence test (one host sync per cycle)
+                nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
+                CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
+                CHK(fetch(s));
+                nchk++;
+                if (s->timing) {
+                    for (int k = 0; k < tn; k++) {
+                        float ms = 0.f;
+                        HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
+                        tms += ms;
+                    }
+                    if (stt) stt->n_poisson_kernels += tn;
+                    tn = 0;
+                }
+                const double r2 = s->hs[S_RES], b2 = s->hs[S_SHIFT + 1];
+                *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
+                if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = cycles; return NS_EDIVERGE; }
+                if (r2 <= tol2 * b2 || r2 == 0.0 || cycles >= maxc) done = true;
+            }
+        }
+        if (done) break;
+        CHK(mg_coarse(s));
+        for (int l = nl - 2; l >= 0; l--) {
+            MgLevel& F = level(s, l);
+            MgLevel& C = level(s, l + 1);
+            CHK(halo_g(s, C.g, {C.phi}, 1));
+            nsg::launch_prolong(F.g, F.phi, C.g, C.phi, s->st);
+            CHK(mg_smooth(s, l, s->mg_post, &tn, ev0));
+        }
+        cycles++;
+    }
+    *its = cycles;
+    if (stt) {
+        stt->t_poisson_kernel_ms += tms;
+        stt->n_checks += nchk;
+    }
+    return 0;
+}
+
+// coefficient tables of one level: [pw pe bx | ps pn by | hx hy]  (ConstructLHS, FluidSolver.cpp:113-131)
+std::vector<double> coef_tables(const std::vector<double>& hx, const std::vector<double>& hy) {
+    const int nx = (int)hx.size(), ny = (int)hy.size();
+    std::vector<double> h(4 * (size_t)nx + 4 * (size_t)ny, 0.0);
+    double *pw = h.data(), *pe = pw + nx, *bx = pe + nx, *ps = bx + nx, *pn = ps + ny, *by = pn + ny;
+    double *hxo = by + ny, *hyo = hxo + nx;
+    for (int i = 0; i < nx; i++) {
+        const double a = hx[i];
+        hxo[i] = a;
+        pw[i] = i > 0 ? 2.0 / (a * (a + hx[i - 1])) : 0.0;
+        pe[i] = i < nx - 1 ? 2.0 / (a * (a + hx[i + 1])) : 0.0;
+        bx[i] = (i == 0 ? 2.0 / (a * a) : 0.0) + (i == nx - 1 ? 2.0 / (a * a) : 0.0);
+    }
+    for (int j = 0; j < ny; j++) {
+        const double a = hy[j];
+        hyo[j] = a;
+        ps[j] = j > 0 ? 2.0 / (a * (a + hy[j - 1])) : 0.0;
+        pn[j] = j < ny - 1 ? 2.0 / (a * (a + hy[j + 1])) : 0.0;
+        by[j] = (j == 0 ? 2.0 / (a * a) : 0.0) + (j == ny - 1 ? 2.0 / (a * a) : 0.0);
+    }
+    return h;
+}
+
+nsg::Coef coef_view(double* d, int nx, int ny) {
+    nsg::Coef c{};
+    c.pw = d; c.pe = d + nx; c.bx = d + 2 * nx;
+    c.ps = d + 3 * nx; c.pn = d + 3 * nx + ny; c.by = d + 3 * nx + 2 * ny;
+    c.hx = d + 3 * nx + 3 * ny; c.hy = d + 4 * nx + 3 * ny;
+    return c;
+}
+
+// multigrid hierarchy: halve while every level stays even and (multi-rank) slabs keep >= 4 rows;
+// stop at the first level small enough for the single-workgroup LDS coarse solve
+int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector<double>& hy0) {
+    MgLevel L0;
+    L0.g = s->g;
+    L0.c = s->c;
+    L0.hx = hx0;
+    L0.hy = hy0;
+    s->lv.push_back(L0);
+    const size_t lds_cap = 128 * 1024;
+    for (;;) {
+        const MgLevel& F = s->lv.back();
+        const nsg::Geo& gf = F.g;
+        if (s->nranks == 1 && s->lv.size() > 1 && nsg::coarse_lds_bytes(gf) <= lds_cap) break;
+        if (gf.nx % 2 || gf.ny % 2 || gf.nxl % 2 || gf.i0 % 2) break;
+        nsg::Geo gc = gf;
+        gc.nx /= 2; gc.ny /= 2; gc.i0 /= 2; gc.nxl /= 2;
+        gc.ld = (gc.ny + 127) / 128 * 128;
+        if (gc.nx < 2 || gc.ny < 2) break;
+        if (s->nranks > 1 && gc.nxl < 4) break;
+        MgLevel C;
+        C.g = gc;
+        C.hx.resize(gc.nx);
+        C.hy.resize(gc.ny);
+        for (int i = 0; i < gc.nx; i++) C.hx[i] = F.hx[2 * i] + F.hx[2 * i + 1];
+        for (int j = 0; j < gc.ny; j++) C.hy[j] = F.hy[2 * j] + F.hy[2 * j + 1];
+        const std::vector<double> t = coef_tables(C.hx, C.hy);
+        HIPCHK(hipMalloc(&C.coef, t.size() * sizeof(double)));
+        HIPCHK(hipMemcpy(C.coef, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+        C.c = coef_view(C.coef, gc.nx, gc.ny);
+        const size_t plane = (size_t)(gc.nxl + 2 * nsg::HALO) * gc.ld;
+        HIPCHK(hipMalloc(&C.mem, 3 * plane * sizeof(double)));
+        HIPCHK(hipMemsetAsync(C.mem, 0, 3 * plane * sizeof(double), s->st));
+        C.phi = C.mem + (size_t)nsg::HALO * gc.ld;
+        C.tmp = C.phi + plane;
+        C.b = C.tmp + plane;
+        s->lv.push_back(C);
+    }
+    const nsg::Geo& gc = s->lv.back().g;
+    const int nc = std::max(gc.nx, gc.ny);
+    const double pi = 3.14159265358979323846;
+    s->mg_omega_c = 2.0 / (1.0 + std::sin(pi / nc));
+    s->mg_coarse_iters = 2 * nc + 10;
+    s->mg_coarse_lds = s->nranks == 1 && s->lv.size() > 1 && nsg::coarse_lds_bytes(gc) <= lds_cap;
     return 0;
 }
 
@@ -338,7 +539,7 @@ int ns_nccl_get_id(void* out) {
 }
 
 int64_t ns_device_bytes(int32_t nxl, int32_t ny) {
-    const int64_t ld = ((int64_t)ny + 31) / 32 * 32;
+    const int64_t ld = ((int64_t)ny + 127) / 128 * 128;
     return (int64_t)NS_NUM_ARR * (nxl + 2 * nsg::HALO) * ld * 8;
 }
 
@@ -355,12 +556,15 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (!(p->re > 0)) { set_err("Reynolds number should be positive"); return NS_EINVAL; }
     if (p->nranks < 1 || p->rank < 0 || p->rank >= p->nranks) { set_err("bad rank/nranks"); return NS_EINVAL; }
     if (p->nranks > 1 && !p->nccl_id) { set_err("nranks > 1 needs an ncclUniqueId"); return NS_EINVAL; }
-    if (p->poisson != NS_POISSON_RBSOR && p->poisson != NS_POISSON_JACOBI) { set_err("unknown Poisson solver %d", p->poisson); return NS_EINVAL; }
+    if (p->poisson != NS_POISSON_RBSOR && p->poisson != NS_POISSON_JACOBI && p->poisson != NS_POISSON_MG) {
+        set_err("unknown Poisson solver %d", p->poisson);
+        return NS_EINVAL;
+    }
 
     nsg::Geo g{};
     g.nx = gd->nx;
     g.ny = gd->ny;
-    g.ld = (gd->ny + 31) / 32 * 32;
+    g.ld = (gd->ny + 127) / 128 * 128;
     int32_t i0, i1;
     if (ns_slab_range(gd->nx, p->nranks, p->rank, &i0, &i1)) return NS_EINVAL;
     g.i0 = i0;
@@ -412,11 +616,13 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     const int nmax = std::max(gd->nx, gd->ny);
     const double pi = 3.14159265358979323846;
     s->omega = p->omega > 0 ? p->omega
-                            : (p->poisson == NS_POISSON_RBSOR ? 2.0 / (1.0 + std::sin(pi / nmax)) : 0.9);
+                            : (p->poisson != NS_POISSON_JACOBI ? 2.0 / (1.0 + std::sin(pi / nmax)) : 0.9);
     s->omega_v = p->omega_v > 0 ? p->omega_v : 1.0;
     s->check_every = p->check_every;
     if (p->check_every > 0) s->pois_batch0 = s->helm_batch0 = p->check_every;
     s->timing = p->timing;
+    if (const char* e = getenv("NSGPU_SWEEP")) s->tiled = std::strcmp(e, "tiled") == 0;
+    if (const char* e = getenv("NSGPU_STRIP_ROWS")) nsg::set_strip_rows(atoi(e));
     s->rank = p->rank;
     s->nranks = p->nranks;
     s->ncells = (double)gd->nx * (double)gd->ny;
@@ -440,33 +646,23 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     for (int k = 0; k < NS_NUM_ARR; k++) s->arr[k] = s->base + k * s->plane + (size_t)nsg::HALO * g.ld;
 
     // coefficient tables (ConstructLHS, FluidSolver.cpp:113-131)
-    const int nx = g.nx, ny = g.ny;
-    std::vector<double> h(3 * nx + 3 * ny + nx + ny, 0.0);
-    double *pw = h.data(), *pe = pw + nx, *bx = pe + nx, *ps = bx + nx, *pn = ps + ny, *by = pn + ny;
-    double *hx = by + ny, *hy = hx + nx;
-    for (int i = 0; i < nx; i++) {
-        const double a = gd->hx[i];
-        if (!(a > 0)) { set_err("hx[%d] = %g is not positive", i, a); return fail(NS_EINVAL); }
-        hx[i] = a;
-        pw[i] = i > 0 ? 2.0 / (a * (a + gd->hx[i - 1])) : 0.0;
-        pe[i] = i < nx - 1 ? 2.0 / (a * (a + gd->hx[i + 1])) : 0.0;
-        bx[i] = (i == 0 ? 2.0 / (a * a) : 0.0) + (i == nx - 1 ? 2.0 / (a * a) : 0.0);
-    }
-    for (int j = 0; j < ny; j++) {
-        const double a = gd->hy[j];
-        if (!(a > 0)) { set_err("hy[%d] = %g is not positive", j, a); return fail(NS_EINVAL); }
-        hy[j] = a;
-        ps[j] = j > 0 ? 2.0 / (a * (a + gd->hy[j - 1])) : 0.0;
-        pn[j] = j < ny - 1 ? 2.0 / (a * (a + gd->hy[j + 1])) : 0.0;
-        by[j] = (j == 0 ? 2.0 / (a * a) : 0.0) + (j == ny - 1 ? 2.0 / (a * a) : 0.0);
-    }
-    if (hipMalloc(&s->coef, h.size() * sizeof(double)) != hipSuccess) { set_err("hipMalloc coef failed"); return fail(NS_ENOMEM); }
-    if (hipMemcpy(s->coef, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) { set_err("coef upload failed"); return fail(NS_EHIP); }
+    std::vector<double> hx0(gd->hx, gd->hx + g.nx), hy0(gd->hy, gd->hy + g.ny);
+    for (int i = 0; i < g.nx; i++)
+        if (!(hx0[i] > 0)) { set_err("hx[%d] = %g is not positive", i, hx0[i]); return fail(NS_EINVAL); }
+    for (int j = 0; j < g.ny; j++)
+        if (!(hy0[j] > 0)) { set_err("hy[%d] = %g is not positive", j, hy0[j]); return fail(NS_EINVAL); }
     {
-        double* d = s->coef;
-        s->c.pw = d; s->c.pe = d + nx; s->c.bx = d + 2 * nx;
-        s->c.ps = d + 3 * nx; s->c.pn = d + 3 * nx + ny; s->c.by = d + 3 * nx + 2 * ny;
-        s->c.hx = d + 3 * nx + 3 * ny; s->c.hy = d + 4 * nx + 3 * ny;
+        const std::vector<double> h = coef_tables(hx0, hy0);
+        if (hipMalloc(&s->coef, h.size() * sizeof(double)) != hipSuccess) { set_err("hipMalloc coef failed"); return fail(NS_ENOMEM); }
+        if (hipMemcpy(s->coef, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) { set_err("coef upload failed"); return fail(NS_EHIP); }
+        s->c = coef_view(s->coef, g.nx, g.ny);
+    }
+    if (s->poisson == NS_POISSON_MG) {
+        if (p->mg_pre > 0) s->mg_pre = p->mg_pre;
+        if (p->mg_post > 0) s->mg_post = p->mg_post;
+        if (int rc = build_levels(s, hx0, hy0)) return fail(rc);
+        if (p->mg_coarse_iters > 0) s->mg_coarse_iters = p->mg_coarse_iters;
+        if (s->lv.size() < 2) s->poisson = NS_POISSON_RBSOR;  // nothing to coarsen: plain RB-SOR
     }
     const int np = nsg::max_partials(g);
     if (hipMalloc(&s->part, (size_t)np * 4 * sizeof(double)) != hipSuccess) { set_err("hipMalloc partials failed"); return fail(NS_ENOMEM); }
@@ -491,6 +687,10 @@ void ns_destroy(ns_solver* s) {
     if (s->st) (void)hipStreamSynchronize(s->st);
     if (s->comm) (void)ncclCommDestroy(s->comm);
     for (auto e : s->ev) (void)hipEventDestroy(e);
+    for (size_t l = 1; l < s->lv.size(); l++) {
+        if (s->lv[l].mem) (void)hipFree(s->lv[l].mem);
+        if (s->lv[l].coef) (void)hipFree(s->lv[l].coef);
+    }
     if (s->base) (void)hipFree(s->base);
     if (s->coef) (void)hipFree(s->coef);
     if (s->part) (void)hipFree(s->part);
@@ -508,11 +708,14 @@ int ns_step(ns_solver* s, ns_stats* out) {
     CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
     CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
     CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
+    CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 1));       // rhs ghost rows: the fused sweep's ring reds
     CHK(helm_solve(s, &st.it_u, &st.res_u, &st.res_v));            // KSPSolve(uSolver) x2 (:547-548)
     st.it_v = st.it_u;
     CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
-    CHK(pois_solve(s, &st.it_phi, &st.res_phi, &st));              // KSPSolve(phiSolver)  (:551)
+    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 1));
+    if (s->poisson == NS_POISSON_MG) CHK(pois_solve_mg(s, &st.it_phi, &st.res_phi, &st));  // KSPSolve(phiSolver) (:551)
+    else CHK(pois_solve(s, &st.it_phi, &st.res_phi, &st));
     CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
     CHK(correct(s));                                               // CorrectVelocities    (:552)
     CHK(fetch(s));                                                 // VecMin/VecMax        (:554-557)
@@ -580,12 +783,14 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         return 0;
     case NS_K_HELMHOLTZ: {
         int nb = 0;
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 1));
         for (int k = 0; k < iters; k++) {
             CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
             nb = helm_sweep(s, alpha, k == iters - 1 ? s->part : nullptr);
         }
         if (iters > 0) {
-            nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_RES, s->st);
+            nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
+            nsg::launch_reduce_sum(s->part + nb, nb, 1, s->scal + S_RES + 1, s->st);
             CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
         }
         CHK(fetch(s));
@@ -600,6 +805,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         return 0;
     case NS_K_POISSON: {
         int nb = 0;
+        CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 1));
         for (int k = 0; k < iters; k++) {
             double* part = k == iters - 1 ? s->part : nullptr;
             CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
@@ -623,6 +829,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         int its = 0;
         double ru = 0, rv = 0;
         CHK(helm_bnorm(s));
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 1));
         CHK(helm_solve(s, &its, &ru, &rv));
         if (out) { out[0] = its; out[1] = std::max(ru, rv); }
         return 0;
@@ -631,7 +838,9 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         int its = 0;
         double r = 0;
         CHK(rhs_mean(s));
-        CHK(pois_solve(s, &its, &r, nullptr));
+        CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 1));
+        if (s->poisson == NS_POISSON_MG) CHK(pois_solve_mg(s, &its, &r, nullptr));
+        else CHK(pois_solve(s, &its, &r, nullptr));
         if (out) { out[0] = its; out[1] = r; }
         return 0;
     }
@@ -656,6 +865,7 @@ int ns_fill_random(ns_solver* s, uint64_t seed) {
     HIPCHK(hipSetDevice(s->device));
     nsg::launch_fill_random(s->g, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], seed, s->st);
     CHK(rhs_mean(s));  // the random rhs's mean becomes the Poisson shift (null-space removal)
+    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 1));
     HIPCHK(hipStreamSynchronize(s->st));
     return 0;
 }

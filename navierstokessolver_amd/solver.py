@@ -42,9 +42,9 @@ def _dptr(a):
 class GpuSolver:
     """One x-slab (the whole grid when nranks == 1) resident on one MI355X."""
 
-    def __init__(self, grid: GridSpec, dt: float, re: float, *, poisson=L.NS_POISSON_RBSOR, rtol=1e-8,
+    def __init__(self, grid: GridSpec, dt: float, re: float, *, poisson=L.NS_POISSON_MG, rtol=1e-8,
                  max_iters=0, omega=0.0, omega_v=0.0, check_every=0, device=-1, timing=False,
-                 rank=0, nranks=1, nccl_id: bytes | None = None):
+                 rank=0, nranks=1, nccl_id: bytes | None = None, mg_pre=0, mg_post=0, mg_coarse_iters=0):
         self.grid = grid
         self.hx = np.ascontiguousarray(grid.hx, dtype=np.float64)
         self.hy = np.ascontiguousarray(grid.hy, dtype=np.float64)
@@ -54,7 +54,8 @@ class GpuSolver:
         self._nccl = ctypes.create_string_buffer(nccl_id, len(nccl_id)) if nccl_id else None
         prm = L.NsParams(dt, re, poisson, rtol, max_iters, omega, omega_v, check_every, device,
                          1 if timing else 0, rank, nranks,
-                         ctypes.cast(self._nccl, ctypes.c_void_p) if self._nccl is not None else None)
+                         ctypes.cast(self._nccl, ctypes.c_void_p) if self._nccl is not None else None,
+                         mg_pre, mg_post, mg_coarse_iters)
         h = ctypes.c_void_p()
         L.check(L.lib().ns_create(ctypes.byref(desc), ctypes.byref(prm), ctypes.byref(h)))
         self._h = h

@@ -241,3 +241,35 @@ def test_sweeps_deterministic_and_exact_with_many_tiles(gpu):
     for _ in range(3):
         p, _ = og.rbsor_sweep(p, b, b.mean(), 1.99)
     assert rel(runs[0], p) <= 1e-12
+
+
+@pytest.mark.parametrize("nx,ny", [(64, 64), (96, 160), (100, 60), (33, 47), (256, 512)])
+def test_mg_poisson_solve_matches_oracle(gpu, nx, ny):
+    """Multigrid V-cycles converge to the oracle's Krylov solution (odd sizes: RB-SOR fallback)."""
+    rng = np.random.default_rng(11)
+    og, gs = pair(gpu, nx, ny, 1e-3, 100.0, poisson=gpu.NS_POISSON_MG, rtol=1e-11)
+    b = rand(rng, nx * ny, 100.0)
+    gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny)); gs.set(gpu.NS_ARR_RPHI, b)
+    its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+    assert res <= 1e-11
+    if nx % 2 == 0 and ny % 2 == 0:
+        assert its <= 30, its          # V-cycles, not sweeps
+    xp, _ = og.solve_poisson(b)
+    g = gs.get(gpu.NS_ARR_PHI).ravel()
+    assert rel(g - g.mean(), xp - xp.mean()) <= 1e-8
+
+
+@pytest.mark.parametrize("solver", ["rbsor", "jacobi_small"])
+def test_full_steps_other_poisson_solvers(gpu, solver):
+    n, steps, re = 16 if solver == "jacobi_small" else 32, 8, 100.0
+    dt = 1.0 / (8 * n)
+    kw = dict(poisson=gpu.NS_POISSON_RBSOR) if solver == "rbsor" else dict(poisson=gpu.NS_POISSON_JACOBI, omega=0.9)
+    og, gs = pair(gpu, n, n, dt, re, **kw)
+    osv = OSolver(og, dt, re, rtol=1e-13)
+    for k in range(steps):
+        gs.step()
+        osv.step()
+    ref = osv.get()
+    u, v, _ = gs.fields()
+    assert np.max(np.abs(u.ravel() - ref["u"])) <= 1e-6
+    assert np.max(np.abs(v.ravel() - ref["v"])) <= 1e-6
