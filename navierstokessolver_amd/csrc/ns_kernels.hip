@@ -926,8 +926,17 @@ static SweepArgs make_args(const Geo& g, const Coef& c, int TI, int TJ) {
     return a;
 }
 
-static int g_strip_rows = 64;
-void set_strip_rows(int L) { if (L >= 4) g_strip_rows = L & ~1; }
+static int g_strip_rows = 0;  // 0 = adaptive
+void set_strip_rows(int L) { g_strip_rows = L >= 4 ? (L & ~1) : 0; }
+
+// rows per strip (measured, tools/sweep_levels.py): 16 while that still gives >= 2048
+// waves (4096^2, 2048^2), else 4 -- coarse multigrid levels are latency-bound and need
+// every wave they can get
+static int strip_rows(const Geo& g) {
+    if (g_strip_rows) return g_strip_rows;
+    const long nsj = (g.ny + SW - 1) / SW;
+    return nsj * ((g.nxl + 15) / 16) >= 2048 ? 16 : 4;
+}
 
 static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, double* out, const double* b,
                               const double* shift, double alpha, double omega, double* part, bool helm) {
@@ -937,7 +946,7 @@ static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, dou
     (void)helm;
     a.alpha = alpha; a.omega = omega;
     a.nx = g.nx; a.ny = g.ny; a.i0 = g.i0; a.nxl = g.nxl; a.ld = g.ld;
-    a.L = g_strip_rows;
+    a.L = strip_rows(g);
     a.nsj = (g.ny + SW - 1) / SW;
     a.nsi = (g.nxl + a.L - 1) / a.L;
     a.part = part;

@@ -100,7 +100,7 @@ struct ns_solver {
     ncclComm_t comm = nullptr;
     double ncells = 0;           // global cell count
     std::vector<hipEvent_t> ev;  // timing events (pairs)
-    int helm_batch0 = 4, pois_batch0 = 8;
+    int helm_batch0 = 3, pois_batch0 = 8;
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
     int mg_pre = 2, mg_post = 2, mg_coarse_iters = 0;
@@ -203,17 +203,25 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
     const double tol2 = s->rtol * s->rtol;
     int sweeps = 0, batch = s->helm_batch0, prev_at = -1;
     double prev_r2 = -1;
+    double* p0 = s->part + 2 * (size_t)nsg::max_partials(s->g) / 2;  // second half: first-sweep residuals
     for (;;) {
         const int n = std::min(batch, s->max_iters - sweeps);
         int nb = 0;
+        const bool first = sweeps == 0 && n > 1;
         for (int k = 0; k < n; k++) {
             CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
-            nb = helm_sweep(s, alpha, k == n - 1 ? s->part : nullptr);
+            double* part = k == n - 1 ? s->part : (first && k == 0 ? p0 : nullptr);
+            nb = helm_sweep(s, alpha, part);
         }
         sweeps += n;
         nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
         nsg::launch_reduce_sum(s->part + nb, nb, 1, s->scal + S_RES + 1, s->st);
+        if (first) {
+            nsg::launch_reduce_sum(p0, nb, 1, s->scal + S_AUX, s->st);
+            nsg::launch_reduce_sum(p0 + nb, nb, 1, s->scal + S_AUX + 1, s->st);
+        }
         CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
+        if (first) CHK(allreduce(s, s->scal + S_AUX, 2, ncclSum));
         CHK(fetch(s));
         const double r2u = s->hs[S_RES], r2v = s->hs[S_RES + 1];
         const double bu = s->hs[S_HBN], bv = s->hs[S_HBN + 1];
@@ -223,6 +231,10 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         if (!std::isfinite(r2u) || !std::isfinite(r2v)) { set_err("Helmholtz residual is not finite"); *its = sweeps; return NS_EDIVERGE; }
         if (ok || sweeps >= s->max_iters) break;
         const double r2 = std::max(r2u / std::max(bu, 1e-300), r2v / std::max(bv, 1e-300));
+        if (first) {  // residual of the initial guess (input of sweep 1) -> contraction rate
+            prev_r2 = std::max(s->hs[S_AUX] / std::max(bu, 1e-300), s->hs[S_AUX + 1] / std::max(bv, 1e-300));
+            prev_at = 0;
+        }
         const int nbatch = next_batch(batch, prev_r2, prev_at, r2, sweeps - 1, tol2, s->max_iters);
         prev_r2 = r2;
         prev_at = sweeps - 1;
@@ -421,7 +433,7 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
     L0.hx = hx0;
     L0.hy = hy0;
     s->lv.push_back(L0);
-    const size_t lds_cap = 128 * 1024;
+    const size_t lds_cap = 24 * 1024;   // coarsest <= ~32 x 32: the single-workgroup solve stays ~10 us
     for (;;) {
         const MgLevel& F = s->lv.back();
         const nsg::Geo& gf = F.g;
@@ -617,7 +629,16 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     const double pi = 3.14159265358979323846;
     s->omega = p->omega > 0 ? p->omega
                             : (p->poisson != NS_POISSON_JACOBI ? 2.0 / (1.0 + std::sin(pi / nmax)) : 0.9);
-    s->omega_v = p->omega_v > 0 ? p->omega_v : 1.0;
+    {
+        // Helmholtz SOR weight: (I - a L_V) has Jacobi spectral radius
+        // rho = 2a(1/hx^2 + 1/hy^2) / (1 + 2a(1/hx^2 + 1/hy^2) + ...) <= that ratio on the finest spacing;
+        // optimal SOR omega = 2 / (1 + sqrt(1 - rho^2))
+        const double a = p->dt / (2 * p->re);
+        const double hxm = *std::min_element(gd->hx, gd->hx + gd->nx), hym = *std::min_element(gd->hy, gd->hy + gd->ny);
+        const double t = 2 * a * (1 / (hxm * hxm) + 1 / (hym * hym));
+        const double rho = t / (1 + t);
+        s->omega_v = p->omega_v > 0 ? p->omega_v : 2.0 / (1.0 + std::sqrt(1.0 - rho * rho));
+    }
     s->check_every = p->check_every;
     if (p->check_every > 0) s->pois_batch0 = s->helm_batch0 = p->check_every;
     s->timing = p->timing;
