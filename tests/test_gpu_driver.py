@@ -1,0 +1,80 @@
+"""End to end through the drop-in boundary on the GPU: the repo's ns_main and the
+reference's own MAIN_Solver.cpp (compiled unchanged against include/, binary
+ref_main_link built where /root/reference exists) read the reference's two input files,
+print the reference's monitor and write FlowData_<iter>.csv; all checked against the oracle.
+Tolerances: monitor = printf("%lf") digits (last-digit flip allowed); CSV = 6 significant
+digits (ostream default, half-unit 5e-6 relative) plus the rtol-1e-8 solve difference
+(~1e-7) -> 1e-5 relative + 1e-6 absolute."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import printed_equal
+from oracle import OGrid, OSolver
+
+pytestmark = pytest.mark.gpu
+HOST = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "navierstokessolver_amd", "host")
+
+N, RE, STEPS, SAVE = 32, 100.0, 20, 10
+DT = 1.0 / (8 * N)
+
+
+def write_inputs(d):
+    (d / "grid").write_text(f"Vertices {{\n0 0\n0 1\n1 1\n1 0\n}}\nNx {{\n0 1 {N} -1\n}}\nNy {{\n0 1 {N} -1\n}}\n")
+    (d / "sim").write_text(f"BC {{\n2 0\n2 1\n2 0\n2 0\n}}\ndt {DT!r}\nfinal_time {STEPS * DT!r}\nre {RE!r}\nsaveIter {SAVE}\n")
+
+
+@pytest.fixture(scope="module")
+def oracle_run():
+    og = OGrid.rectangle(N, N)
+    s = OSolver(og, DT, RE, rtol=1e-13)
+    trace, snaps = [], {}
+    for it in range(1, STEPS + 1):
+        mm, _ = s.step()
+        trace.append(mm)
+        if it % SAVE == 0:
+            st = s.get()
+            snaps[it] = (st["u"], st["v"], og.pressure(DT / (2 * RE), st["phi"]))
+    return og, trace, snaps
+
+
+@pytest.mark.parametrize("exe", ["ns_main", "ref_main_link"])
+def test_driver_matches_oracle(tmp_path, exe, oracle_run):
+    path = os.path.join(HOST, exe)
+    if not os.path.exists(path):
+        pytest.skip(f"{exe} not built (ref_main_link needs /root/reference at build time)")
+    write_inputs(tmp_path)
+    out = subprocess.run([path, "grid", "sim"], capture_output=True, text=True, cwd=tmp_path, timeout=120).stdout
+    assert "Solver Setup Complete!" in out and "Solution Complete!" in out, out[-2000:]
+    lines = [l for l in out.splitlines() if l and l[0].isdigit()]
+    assert len(lines) == STEPS
+    og, trace, snaps = oracle_run
+    for k, l in enumerate(lines):
+        f = l.split("\t")
+        assert int(f[0]) == k + 1
+        assert all(printed_equal(float(a), b) for a, b in zip(f[1:5], trace[k])), (l, trace[k])
+    assert out.count("iter\tumin") == 2   # header every 10 steps
+    for it, (u, v, p) in snaps.items():
+        d = np.loadtxt(tmp_path / f"FlowData_{it}.csv", delimiter=",", skiprows=1)
+        assert d.shape == (N * N + 4 * N, 6)      # one row per cell + one per boundary face
+        cells = d[np.isin(np.arange(len(d)), _cell_rows())]
+        np.testing.assert_allclose(cells[:, 0], og.xc, atol=1e-6)
+        np.testing.assert_allclose(cells[:, 3], u, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(cells[:, 4], v, rtol=1e-5, atol=1e-6)
+        pc = cells[:, 5] - cells[:, 5].mean()
+        np.testing.assert_allclose(pc, p - p.mean(), rtol=0, atol=1e-5 * np.abs(p).max())
+        top = d[np.isclose(d[:, 1], 1.0)]
+        np.testing.assert_allclose(top[:, 3], 1.0, atol=1e-6)   # lid face value u = b (ghost -u + 2b)
+    assert (tmp_path / "CellCenters.csv").exists()
+
+
+def _cell_rows():
+    # rows are written cell by cell (i outer, j inner), each followed by its boundary faces
+    rows, r = [], 0
+    for i in range(N):
+        for j in range(N):
+            rows.append(r)
+            r += 1 + (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1)
+    return rows
