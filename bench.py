@@ -95,15 +95,11 @@ def main():
 
     nccl_id = None
     if world > 1:
+        # gloo carries only the bootstrap (RCCL unique id), the barrier and the timing max;
+        # the data path (ghost rows, residual / mean / min-max reductions) is RCCL in libnsgpu.so
+        from navierstokessolver_amd.dist import nccl_id as make_nccl_id
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        idt = torch.zeros(nsa._lib.lib().ns_nccl_id_size(), dtype=torch.uint8)
-        if rank == 0:
-            import ctypes
-            buf = ctypes.create_string_buffer(idt.numel())
-            nsa._lib.check(nsa._lib.lib().ns_nccl_get_id(buf))
-            idt = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
-        dist.broadcast(idt, 0)
-        nccl_id = bytes(idt.tolist())
+        nccl_id = make_nccl_id(dist)
 
     n, re = args.n, args.re
     dt = 1.0 / (8 * n)

@@ -72,6 +72,18 @@ typedef struct ns_grid_desc {
     const int32_t* cell_id;   /* nx*ny ids or -1 (outside); NULL = full rectangle */
 } ns_grid_desc;
 
+/* Optional host-side transport for the x-slab exchanges (tests, or clusters without
+ * RCCL): the library stages ghost rows through pinned host memory and calls these.
+ * exchange: send_lo goes to rank-1, send_hi to rank+1; recv_lo is filled from rank-1,
+ *           recv_hi from rank+1 (NULL where there is no neighbour); count doubles each.
+ * allreduce: in place over n doubles, op 0 = sum, 1 = min.  Both return 0 on success. */
+typedef struct ns_host_transport {
+    void* user;
+    int (*exchange)(void* user, const double* send_lo, const double* send_hi, double* recv_lo, double* recv_hi,
+                    int64_t count);
+    int (*allreduce)(void* user, double* buf, int32_t n, int32_t op);
+} ns_host_transport;
+
 typedef struct ns_params {
     double  dt;               /* FluidSolver::dt */
     double  re;               /* FluidSolver::re */
@@ -89,6 +101,7 @@ typedef struct ns_params {
     /* multigrid (NS_POISSON_MG): smoothing sweeps per level before / after the coarse
      * correction, and sweeps of the coarsest solve (0 = defaults 2 / 2 / automatic) */
     int32_t mg_pre, mg_post, mg_coarse_iters;
+    const ns_host_transport* host_transport;  /* NULL = RCCL (nranks > 1) */
 } ns_params;
 
 /* Per-step result (the reference prints iter, umin, umax, vmin, vmax: FluidSolver.cpp:559-560). */

@@ -37,13 +37,25 @@ class NsGridDesc(ctypes.Structure):
                 ("cell_id", ctypes.POINTER(ctypes.c_int32))]
 
 
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                               ctypes.POINTER(ctypes.c_double), ctypes.c_int64)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int32,
+                                ctypes.c_int32)
+
+
+class NsHostTransport(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("exchange", EXCHANGE_FN), ("allreduce", ALLREDUCE_FN)]
+
+
 class NsParams(ctypes.Structure):
     _fields_ = [("dt", ctypes.c_double), ("re", ctypes.c_double), ("poisson", ctypes.c_int32),
                 ("rtol", ctypes.c_double), ("max_iters", ctypes.c_int32), ("omega", ctypes.c_double),
                 ("omega_v", ctypes.c_double), ("check_every", ctypes.c_int32),
                 ("device", ctypes.c_int32), ("timing", ctypes.c_int32),
                 ("rank", ctypes.c_int32), ("nranks", ctypes.c_int32), ("nccl_id", ctypes.c_void_p),
-                ("mg_pre", ctypes.c_int32), ("mg_post", ctypes.c_int32), ("mg_coarse_iters", ctypes.c_int32)]
+                ("mg_pre", ctypes.c_int32), ("mg_post", ctypes.c_int32), ("mg_coarse_iters", ctypes.c_int32),
+                ("host_transport", ctypes.POINTER(NsHostTransport))]
 
 
 class NsStats(ctypes.Structure):

@@ -106,21 +106,53 @@ struct ns_solver {
     int mg_pre = 2, mg_post = 2, mg_coarse_iters = 0;
     double mg_omega_c = 1.0, mg_omega_s = 1.0;
     bool mg_coarse_lds = false;
+    ns_host_transport ht{};      // host transport (ht.exchange != NULL) instead of RCCL
+    double* stage = nullptr;     // pinned staging for the host transport
+    size_t stage_n = 0;
 };
 
 namespace {
 
+int ensure_stage(ns_solver* s, size_t n) {
+    if (s->stage_n >= n) return 0;
+    if (s->stage) HIPCHK(hipHostFree(s->stage));
+    s->stage = nullptr;
+    HIPCHK(hipHostMalloc(&s->stage, n * sizeof(double), hipHostMallocDefault));
+    s->stage_n = n;
+    return 0;
+}
+
+// ghost rows of width w (contiguous: w * ld doubles) to / from the x-neighbours
 int halo_g(ns_solver* s, const nsg::Geo& g, std::initializer_list<double*> fields, int w) {
     if (s->nranks == 1) return 0;
     const size_t cnt = (size_t)w * g.ld;
     const int ld = g.ld, nxl = g.nxl;
+    const bool lo = s->rank > 0, hi = s->rank < s->nranks - 1;
+    if (s->ht.exchange) {
+        CHK(ensure_stage(s, 4 * cnt));
+        double *slo = s->stage, *shi = slo + cnt, *rlo = shi + cnt, *rhi = rlo + cnt;
+        for (double* f : fields) {
+            if (lo) HIPCHK(hipMemcpyAsync(slo, f, cnt * 8, hipMemcpyDeviceToHost, s->st));
+            if (hi) HIPCHK(hipMemcpyAsync(shi, f + (ptrdiff_t)(nxl - w) * ld, cnt * 8, hipMemcpyDeviceToHost, s->st));
+            HIPCHK(hipStreamSynchronize(s->st));
+            if (s->ht.exchange(s->ht.user, lo ? slo : nullptr, hi ? shi : nullptr, lo ? rlo : nullptr,
+                               hi ? rhi : nullptr, (int64_t)cnt) != 0) {
+                set_err("host transport exchange failed");
+                return NS_ERCCL;
+            }
+            if (lo) HIPCHK(hipMemcpyAsync(f - (ptrdiff_t)w * ld, rlo, cnt * 8, hipMemcpyHostToDevice, s->st));
+            if (hi) HIPCHK(hipMemcpyAsync(f + (ptrdiff_t)nxl * ld, rhi, cnt * 8, hipMemcpyHostToDevice, s->st));
+            HIPCHK(hipStreamSynchronize(s->st));
+        }
+        return 0;
+    }
     NCCLCHK(ncclGroupStart());
     for (double* f : fields) {
-        if (s->rank > 0) {
+        if (lo) {
             NCCLCHK(ncclSend(f, cnt, ncclDouble, s->rank - 1, s->comm, s->st));
             NCCLCHK(ncclRecv(f - (ptrdiff_t)w * ld, cnt, ncclDouble, s->rank - 1, s->comm, s->st));
         }
-        if (s->rank < s->nranks - 1) {
+        if (hi) {
             NCCLCHK(ncclSend(f + (ptrdiff_t)(nxl - w) * ld, cnt, ncclDouble, s->rank + 1, s->comm, s->st));
             NCCLCHK(ncclRecv(f + (ptrdiff_t)nxl * ld, cnt, ncclDouble, s->rank + 1, s->comm, s->st));
         }
@@ -133,6 +165,17 @@ int halo(ns_solver* s, std::initializer_list<double*> fields, int w) { return ha
 
 int allreduce(ns_solver* s, double* d, int n, ncclRedOp_t op) {
     if (s->nranks == 1) return 0;
+    if (s->ht.allreduce) {
+        CHK(ensure_stage(s, 64));
+        HIPCHK(hipMemcpyAsync(s->stage, d, n * 8, hipMemcpyDeviceToHost, s->st));
+        HIPCHK(hipStreamSynchronize(s->st));
+        if (s->ht.allreduce(s->ht.user, s->stage, n, op == ncclMin ? 1 : 0) != 0) {
+            set_err("host transport allreduce failed");
+            return NS_ERCCL;
+        }
+        HIPCHK(hipMemcpyAsync(d, s->stage, n * 8, hipMemcpyHostToDevice, s->st));
+        return 0;
+    }
     NCCLCHK(ncclAllReduce(d, d, n, ncclDouble, op, s->comm, s->st));
     return 0;
 }
@@ -567,7 +610,10 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (!(p->dt > 0)) { set_err("Time step should be positive"); return NS_EINVAL; }
     if (!(p->re > 0)) { set_err("Reynolds number should be positive"); return NS_EINVAL; }
     if (p->nranks < 1 || p->rank < 0 || p->rank >= p->nranks) { set_err("bad rank/nranks"); return NS_EINVAL; }
-    if (p->nranks > 1 && !p->nccl_id) { set_err("nranks > 1 needs an ncclUniqueId"); return NS_EINVAL; }
+    if (p->nranks > 1 && !p->nccl_id && !(p->host_transport && p->host_transport->exchange && p->host_transport->allreduce)) {
+        set_err("nranks > 1 needs an ncclUniqueId or a host transport");
+        return NS_EINVAL;
+    }
     if (p->poisson != NS_POISSON_RBSOR && p->poisson != NS_POISSON_JACOBI && p->poisson != NS_POISSON_MG) {
         set_err("unknown Poisson solver %d", p->poisson);
         return NS_EINVAL;
@@ -691,7 +737,9 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (hipMemsetAsync(s->scal, 0, S_NUM * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     if (hipHostMalloc(&s->hs, S_NUM * sizeof(double), hipHostMallocDefault) != hipSuccess) { set_err("hipHostMalloc failed"); return fail(NS_ENOMEM); }
 
-    if (s->nranks > 1) {
+    if (s->nranks > 1 && p->host_transport && p->host_transport->exchange) {
+        s->ht = *p->host_transport;
+    } else if (s->nranks > 1) {
         ncclUniqueId id;
         std::memcpy(&id, p->nccl_id, sizeof id);
         ncclResult_t r = ncclCommInitRank(&s->comm, s->nranks, id, s->rank);
@@ -717,6 +765,7 @@ void ns_destroy(ns_solver* s) {
     if (s->part) (void)hipFree(s->part);
     if (s->scal) (void)hipFree(s->scal);
     if (s->hs) (void)hipHostFree(s->hs);
+    if (s->stage) (void)hipHostFree(s->stage);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
 }

@@ -44,7 +44,8 @@ class GpuSolver:
 
     def __init__(self, grid: GridSpec, dt: float, re: float, *, poisson=L.NS_POISSON_MG, rtol=1e-8,
                  max_iters=0, omega=0.0, omega_v=0.0, check_every=0, device=-1, timing=False,
-                 rank=0, nranks=1, nccl_id: bytes | None = None, mg_pre=0, mg_post=0, mg_coarse_iters=0):
+                 rank=0, nranks=1, nccl_id: bytes | None = None, mg_pre=0, mg_post=0, mg_coarse_iters=0,
+                 host_transport=None):
         self.grid = grid
         self.hx = np.ascontiguousarray(grid.hx, dtype=np.float64)
         self.hy = np.ascontiguousarray(grid.hy, dtype=np.float64)
@@ -55,7 +56,9 @@ class GpuSolver:
         prm = L.NsParams(dt, re, poisson, rtol, max_iters, omega, omega_v, check_every, device,
                          1 if timing else 0, rank, nranks,
                          ctypes.cast(self._nccl, ctypes.c_void_p) if self._nccl is not None else None,
-                         mg_pre, mg_post, mg_coarse_iters)
+                         mg_pre, mg_post, mg_coarse_iters,
+                         ctypes.pointer(host_transport.struct) if host_transport is not None else None)
+        self._transport = host_transport  # keep the callbacks alive
         h = ctypes.c_void_p()
         L.check(L.lib().ns_create(ctypes.byref(desc), ctypes.byref(prm), ctypes.byref(h)))
         self._h = h

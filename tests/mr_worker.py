@@ -1,0 +1,53 @@
+"""Worker for tests/test_gpu_multirank.py (launched by torch.distributed.run, 2 ranks).
+Runs `steps` cavity steps on an x-slab per rank (both ranks on GPU 0), gathers u, v, phi
+on rank 0 and saves them.  --transport host | rccl."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np
+import torch
+import torch.distributed as dist
+
+import navierstokessolver_amd as nsa
+from navierstokessolver_amd.dist import TorchHostTransport, nccl_id
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--xport", default="host")
+ap.add_argument("--size", type=int, default=64)
+ap.add_argument("--size-y", type=int, default=0)
+ap.add_argument("--nsteps", type=int, default=10)
+ap.add_argument("--solver", type=int, default=nsa.NS_POISSON_MG)
+ap.add_argument("--tol", type=float, default=1e-10)
+ap.add_argument("--output", required=True)
+a = ap.parse_args()
+dist.init_process_group("gloo")
+rank, world = dist.get_rank(), dist.get_world_size()
+n, ny = a.size, a.size_y or a.size
+kw = dict(rank=rank, nranks=world, device=0, poisson=a.solver, rtol=a.tol)
+if a.xport == "host":
+    kw["host_transport"] = TorchHostTransport(dist)
+else:
+    kw["nccl_id"] = nccl_id(dist)
+status = "ok"
+try:
+    gs = nsa.GpuSolver(nsa.rectangle(n, ny), 1.0 / (8 * n), 100.0, **kw)
+    mm = [list(gs.step().values())[:7] for _ in range(a.nsteps)]
+    u, v, phi = gs.fields()
+except Exception as e:  # report, don't hang the other rank
+    status = f"error: {e}"
+    u = v = phi = np.zeros((1, ny))
+    mm = []
+parts = [None] * world
+dist.all_gather_object(parts, (status, u, v, phi, mm))
+if rank == 0:
+    st = [p[0] for p in parts]
+    if all(s == "ok" for s in st):
+        np.savez(a.output, u=np.concatenate([p[1] for p in parts]), v=np.concatenate([p[2] for p in parts]),
+                 phi=np.concatenate([p[3] for p in parts]), mm=np.array(parts[0][4]), status="ok")
+    else:
+        np.savez(a.output, status="; ".join(st))
+dist.barrier()
+dist.destroy_process_group()
