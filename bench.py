@@ -35,49 +35,27 @@ def parse():
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-sweeps", type=int, default=3)
     return ap.parse_args()
 
 
-def cpu_baseline(n, re, dt, it_phi, it_v, sweeps):
-    """The oracle (CPU restatement, 1 thread) on a bounded sample of the same workload:
-    one K1 + K3 + K5 pass and `sweeps` Poisson / Helmholtz red-black sweeps on the full
-    n^2 grid; a full step is extrapolated with the GPU run's own sweep counts."""
+def cpu_baseline(n, re, dt, omega_v):
+    """The oracle (CPU restatement, 1 thread) running the SAME algorithm as the GPU path
+    (RB-SOR Helmholtz to rtol, multigrid Poisson to rtol 1e-8) for one full time step of
+    the same n^2 cavity (the first step from rest: a bounded sample, ~10-30 s)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
-    from oracle import OGrid  # CPU baseline leg only
+    from oracle import OGrid, OSolver  # CPU baseline leg only
 
     g = OGrid.rectangle(n, n)
-    N = g.N
-    rng = np.random.default_rng(0)
-    u, v, phi = rng.uniform(-1, 1, N), rng.uniform(-1, 1, N), rng.uniform(-1, 1, N)
-    cu, cv = np.zeros(N), np.zeros(N)
+    s = OSolver(g, dt, re, rtol=1e-8)
+    s.use_gpu_algorithm(omega_v)
     t0 = time.perf_counter()
-    gx, gy = g.grad_phi(phi)
-    ru, rv, cu, cv = g.rhs_velocity(dt, re, u, v, gx, gy, cu, cv)
-    t_k1 = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    rp = g.divergence(dt, u, v)
-    g.correct(dt, u, v, phi)
-    t_k35 = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    p = phi
-    for _ in range(sweeps):
-        p, _ = g.rbsor_sweep(p, rp, float(rp.mean()), 1.9)
-    t_ps = (time.perf_counter() - t0) / sweeps
-    t0 = time.perf_counter()
-    a, b = u, v
-    for _ in range(max(1, sweeps // 2)):
-        a, b, _ = g.helm_sweep(dt / (2 * re), a, b, ru, rv, 1.0)
-    t_hs = (time.perf_counter() - t0) / max(1, sweeps // 2)
-    t_step = t_k1 + t_k35 + it_phi * t_ps + it_v * t_hs
+    _, its = s.step()
+    t = time.perf_counter() - t0
     return {
-        "value": N / t_step / 1e6, "unit": "MLUPS", "cores": 1, "kind": "port",
-        "sample": (f"oracle (C restatement, 1 thread) on the {n}^2 grid: K1+K3+K5 once ({t_k1 + t_k35:.2f} s), "
-                   f"{sweeps} Poisson RB-SOR sweeps ({t_ps:.3f} s each), {max(1, sweeps // 2)} Helmholtz "
-                   f"sweeps ({t_hs:.3f} s each); step time extrapolated with the GPU run's average "
-                   f"{it_phi:.0f} Poisson + {it_v:.0f} Helmholtz sweeps/step = {t_step:.1f} s/step"),
-        "poisson_sweeps_per_s": 1.0 / t_ps,
+        "value": g.N / t / 1e6, "unit": "MLUPS", "cores": 1, "kind": "port",
+        "sample": (f"one full time step (step 1 from rest) of the {n}^2 cavity in the oracle's C restatement "
+                   f"(oracle/ns_oracle.c), same algorithm as the GPU (MG Poisson: {its[2]} V-cycles, RB-SOR "
+                   f"Helmholtz: {its[0]} sweeps), 1 thread: {t:.1f} s"),
     }
 
 
@@ -126,7 +104,7 @@ def main():
 
     K = args.steps
     cells = n * n
-    sweeps = sum(s["it_phi"] for s in stats)
+    cycles = sum(s["it_phi"] for s in stats)
     hsweeps = sum(s["it_u"] for s in stats)
     kms = sum(s["t_poisson_kernel_ms"] for s in stats)
     kn = sum(s["n_poisson_kernels"] for s in stats)
@@ -159,21 +137,22 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (lid-driven cavity from rest, no input files)",
-        "config": {"workload": f"{n}x{n} lid-driven cavity, Re={re:g}, dt=1/{8 * n}, fp64, RB-SOR Poisson "
-                               f"+ RB-GS Helmholtz to rtol {args.rtol:g}",
+        "config": {"workload": f"{n}x{n} lid-driven cavity, Re={re:g}, dt=1/{8 * n}, fp64, multigrid Poisson "
+                               f"(RB-GS smoother) + RB-SOR Helmholtz, both to rtol {args.rtol:g}",
                    "nx": n, "ny": n, "re": re, "dt": dt, "parallelism": f"x-slab x{world}"},
-        "poisson_sweeps_per_s": sweeps / elapsed,
-        "poisson_glups": cells * sweeps / elapsed / 1e9,
-        "poisson_sweeps_per_step": sweeps / K,
+        "poisson_vcycles_per_s": cycles / elapsed,
+        "poisson_vcycles_per_step": cycles / K,
+        "poisson_fine_sweeps_per_s": kn / elapsed,
+        "poisson_fine_sweep_glups": local_cells * world * kn / elapsed / 1e9,
         "helmholtz_sweeps_per_step": hsweeps / K,
-        "roofline": {"bound": "hbm", "kernel": "k_rb_sweep<32,128,Poisson> (K4)",
+        "roofline": {"bound": "hbm", "kernel": "k_sweep<Poisson,RB> (K4 multigrid smoother, finest level)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "avg_kernel_us": avg_kernel_s * 1e6,
                      "bytes_per_launch": POISSON_BYTES_PER_CELL * local_cells},
     }
     if world == 1 and not args.no_cpu:
         try:
-            line["cpu_baseline"] = cpu_baseline(n, re, dt, sweeps / K, hsweeps / K, args.cpu_sweeps)
+            line["cpu_baseline"] = cpu_baseline(n, re, dt, solver.omega_v)
         except Exception as e:  # the baseline must never hide the GPU line
             line["cpu_baseline"] = {"error": repr(e)}
     print(json.dumps(line), flush=True)

@@ -161,6 +161,11 @@ int  ns_set_array(ns_solver* s, int which, const double* host);
  *   NS_K_RESIDUAL: out[0] = residual^2 */
 int  ns_kernel(ns_solver* s, int which, int iters, double* out);
 
+/* Multigrid transfers alone (tests): op 0 = restriction of the current residual
+ * rhs_phi - mean - L phi into `coarse` (nx/2 x ny/2, host, the slab's coarse rows);
+ * op 1 = prolongation: phi += bilinear(`coarse`).  Needs NS_POISSON_MG with >= 2 levels. */
+int  ns_mg_transfer(ns_solver* s, int op, double* coarse);
+
 /* Fill phi and rhs_phi with reproducible uniform [-1,1) values generated on the
  * device (splitmix64 of (seed, global cell)), rhs mean-removed: the sweep benchmark input. */
 int  ns_fill_random(ns_solver* s, uint64_t seed);

@@ -81,6 +81,7 @@ SIGNATURES = {
     "ns_set_array": (ctypes.c_int, [_P, ctypes.c_int, _D]),
     "ns_kernel": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _D]),
     "ns_fill_random": (ctypes.c_int, [_P, ctypes.c_uint64]),
+    "ns_mg_transfer": (ctypes.c_int, [_P, ctypes.c_int, _D]),
     "ns_time_poisson": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _D]),
     "ns_slab_range": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                      ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),

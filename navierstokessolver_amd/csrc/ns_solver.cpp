@@ -930,6 +930,28 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
     }
 }
 
+int ns_mg_transfer(ns_solver* s, int op, double* coarse) {
+    if (!s || !coarse || s->poisson != NS_POISSON_MG || s->lv.size() < 2) {
+        set_err("ns_mg_transfer needs a multigrid solver with at least two levels");
+        return NS_EINVAL;
+    }
+    HIPCHK(hipSetDevice(s->device));
+    MgLevel& F = level(s, 0);
+    MgLevel& C = level(s, 1);
+    const size_t w = (size_t)C.g.ny * 8;
+    if (op == 0) {
+        CHK(halo_g(s, F.g, {F.phi}, 1));
+        nsg::launch_restrict(F.g, F.c, F.phi, F.b, s->scal + S_SHIFT, C.g, C.c, C.b, C.phi, s->part, s->st);
+        HIPCHK(hipMemcpy2DAsync(coarse, w, C.b, (size_t)C.g.ld * 8, w, C.g.nxl, hipMemcpyDeviceToHost, s->st));
+    } else {
+        HIPCHK(hipMemcpy2DAsync(C.phi, (size_t)C.g.ld * 8, coarse, w, w, C.g.nxl, hipMemcpyHostToDevice, s->st));
+        CHK(halo_g(s, C.g, {C.phi}, 1));
+        nsg::launch_prolong(F.g, F.phi, C.g, C.phi, s->st);
+    }
+    HIPCHK(hipStreamSynchronize(s->st));
+    return 0;
+}
+
 int ns_fill_random(ns_solver* s, uint64_t seed) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));

@@ -65,6 +65,13 @@ class GpuSolver:
         self.dt, self.re = dt, re
         self.rank, self.nranks = rank, nranks
         self.i0, self.i1 = L.slab_range(self.hx.size, nranks, rank)
+        # the Helmholtz SOR weight libnsgpu.so derives (ns_create): 2 / (1 + sqrt(1 - rho^2))
+        if omega_v > 0:
+            self.omega_v = omega_v
+        else:
+            t = dt / re * (1 / self.hx.min() ** 2 + 1 / self.hy.min() ** 2)
+            rho = t / (1 + t)
+            self.omega_v = 2 / (1 + (1 - rho * rho) ** 0.5)
         self.shape = (self.i1 - self.i0, self.hy.size)
 
     # ---- lifecycle
@@ -108,6 +115,15 @@ class GpuSolver:
         out = np.zeros(8, dtype=np.float64)
         L.check(L.lib().ns_kernel(self._h, which, iters, _dptr(out)))
         return out
+
+    def mg_restrict(self) -> np.ndarray:
+        out = np.zeros((self.shape[0] // 2, self.shape[1] // 2))
+        L.check(L.lib().ns_mg_transfer(self._h, 0, _dptr(out)))
+        return out
+
+    def mg_prolong(self, coarse) -> None:
+        c = np.ascontiguousarray(np.asarray(coarse, dtype=np.float64).reshape(self.shape[0] // 2, self.shape[1] // 2))
+        L.check(L.lib().ns_mg_transfer(self._h, 1, _dptr(c)))
 
     def fill_random(self, seed: int = 0x5EED) -> None:
         L.check(L.lib().ns_fill_random(self._h, seed))

@@ -802,11 +802,172 @@ int og_solve_poisson(const og_grid* g, double* rhs, double* x, double rtol, int 
 }
 
 /* ---------------------------------------------------------------------- */
+/* geometric multigrid (rectangle, Dirichlet-type faces)                   */
+
+static void coef1(int n, const double* h, double* cm, double* cp) {
+    for (int i = 0; i < n; i++) {
+        cm[i] = i > 0 ? 2.0 / (h[i] * (h[i] + h[i - 1])) : 0.0;
+        cp[i] = i < n - 1 ? 2.0 / (h[i] * (h[i] + h[i + 1])) : 0.0;
+    }
+}
+
+typedef struct {
+    int nx, ny;
+    double *hx, *hy, *cw, *ce, *cs, *cn, *x, *b;
+} mg_level;
+
+static double lap_at(const mg_level* L, const double* p, int i, int j) {
+    const int ny = L->ny;
+    const double q = p[i * ny + j];
+    const double s = L->cw[i] * p[(i > 0 ? i - 1 : i) * ny + j] + L->ce[i] * p[(i < L->nx - 1 ? i + 1 : i) * ny + j] +
+                     L->cs[j] * p[i * ny + (j > 0 ? j - 1 : j)] + L->cn[j] * p[i * ny + (j < ny - 1 ? j + 1 : j)];
+    const double dg = -((L->cw[i] + L->ce[i]) + (L->cs[j] + L->cn[j]));
+    return s + dg * q;
+}
+
+/* one red-black sweep in place (red = (i+j) even first) */
+static void mg_rb(const mg_level* L, double* p, const double* b, double shift, double omega) {
+    for (int color = 0; color < 2; color++)
+        for (int i = 0; i < L->nx; i++)
+            for (int j = (i + color) & 1; j < L->ny; j += 2) {
+                const double dg = -((L->cw[i] + L->ce[i]) + (L->cs[j] + L->cn[j]));
+                const double r = (b[i * L->ny + j] - shift) - lap_at(L, p, i, j);
+                p[i * L->ny + j] += omega * r / dg;
+            }
+}
+
+static double mg_restrict_lv(const mg_level* F, const double* phi, const double* b, double shift, const mg_level* C,
+                             double* bc) {
+    double r2 = 0.0;
+    for (int I = 0; I < C->nx; I++)
+        for (int J = 0; J < C->ny; J++) {
+            double sum = 0.0;
+            for (int a = 0; a < 2; a++)
+                for (int q = 0; q < 2; q++) {
+                    const int i = 2 * I + a, j = 2 * J + q;
+                    const double r = (b[i * F->ny + j] - shift) - lap_at(F, phi, i, j);
+                    sum += (F->hx[i] * F->hy[j]) * r;
+                    r2 += r * r;
+                }
+            bc[I * C->ny + J] = sum / (C->hx[I] * C->hy[J]);
+        }
+    return r2;
+}
+
+void og_mg_prolong(int nx, int ny, const double* ec, double* phi) {
+    const int cnx = nx / 2, cny = ny / 2;
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < ny; j++) {
+            const int I = i >> 1, J = j >> 1;
+            int In = (i & 1) ? I + 1 : I - 1, Jn = (j & 1) ? J + 1 : J - 1;
+            if (In < 0 || In >= cnx) In = I;   /* wall: reflect onto the parent */
+            if (Jn < 0 || Jn >= cny) Jn = J;
+            phi[i * ny + j] += (9.0 * ec[I * cny + J] + 3.0 * ec[In * cny + J] + 3.0 * ec[I * cny + Jn] +
+                                ec[In * cny + Jn]) * 0.0625;
+        }
+}
+
+static mg_level* mg_build(int nx, int ny, const double* hx, const double* hy, int* nlev) {
+    int cap = 32, n = 0;
+    mg_level* L = calloc(cap, sizeof(mg_level));
+    for (;;) {
+        mg_level* l = &L[n];
+        l->nx = nx; l->ny = ny;
+        l->hx = malloc(sizeof(double) * nx); l->hy = malloc(sizeof(double) * ny);
+        if (n == 0) { memcpy(l->hx, hx, sizeof(double) * nx); memcpy(l->hy, hy, sizeof(double) * ny); }
+        else {
+            for (int i = 0; i < nx; i++) l->hx[i] = L[n - 1].hx[2 * i] + L[n - 1].hx[2 * i + 1];
+            for (int j = 0; j < ny; j++) l->hy[j] = L[n - 1].hy[2 * j] + L[n - 1].hy[2 * j + 1];
+        }
+        l->cw = malloc(sizeof(double) * nx); l->ce = malloc(sizeof(double) * nx);
+        l->cs = malloc(sizeof(double) * ny); l->cn = malloc(sizeof(double) * ny);
+        coef1(nx, l->hx, l->cw, l->ce);
+        coef1(ny, l->hy, l->cs, l->cn);
+        l->x = calloc((size_t)nx * ny, sizeof(double));
+        l->b = calloc((size_t)nx * ny, sizeof(double));
+        n++;
+        /* same rule as the GPU hierarchy: stop at <= 32 x 32 once coarsened, or at odd sizes */
+        const size_t lds = sizeof(double) * (2 * (size_t)nx * ny + 2 * nx + 2 * ny);
+        if ((n > 1 && lds <= 24 * 1024) || nx % 2 || ny % 2 || nx / 2 < 2 || ny / 2 < 2 || n == cap) break;
+        nx /= 2; ny /= 2;
+    }
+    *nlev = n;
+    return L;
+}
+
+static void mg_free(mg_level* L, int n) {
+    for (int k = 0; k < n; k++) {
+        free(L[k].hx); free(L[k].hy); free(L[k].cw); free(L[k].ce); free(L[k].cs); free(L[k].cn);
+        free(L[k].x); free(L[k].b);
+    }
+    free(L);
+}
+
+void og_mg_restrict(int nx, int ny, const double* hx, const double* hy, const double* phi, const double* b,
+                    double shift, double* bc) {
+    int n;
+    mg_level* L = mg_build(nx, ny, hx, hy, &n);
+    mg_level F = L[0];
+    mg_level C = {0};
+    C.nx = nx / 2; C.ny = ny / 2;
+    C.hx = malloc(sizeof(double) * C.nx); C.hy = malloc(sizeof(double) * C.ny);
+    for (int i = 0; i < C.nx; i++) C.hx[i] = hx[2 * i] + hx[2 * i + 1];
+    for (int j = 0; j < C.ny; j++) C.hy[j] = hy[2 * j] + hy[2 * j + 1];
+    mg_restrict_lv(&F, phi, b, shift, &C, bc);
+    free(C.hx); free(C.hy);
+    mg_free(L, n);
+}
+
+int og_mg_solve(const og_grid* g, double* rhs, double* x, double rtol, int pre, int post, int maxcycles) {
+    if (!rect_dirichlet(g)) { set_err("multigrid needs a rectangle with Dirichlet-type faces"); return -1; }
+    const int N = g->N;
+    double m = 0.0, b2 = 0.0;
+    for (int c = 0; c < N; c++) m += rhs[c];
+    m /= N;
+    for (int c = 0; c < N; c++) { rhs[c] -= m; b2 += rhs[c] * rhs[c]; }
+    int nl;
+    mg_level* L = mg_build(g->nx, g->ny, g->hx, g->hy, &nl);
+    if (nl < 2) { mg_free(L, nl); set_err("grid cannot be coarsened"); return -1; }
+    const mg_level* Lc = &L[nl - 1];
+    const int nc = Lc->nx > Lc->ny ? Lc->nx : Lc->ny;
+    const double omc = 2.0 / (1.0 + sin(3.14159265358979323846 / nc));
+    const int itc = 2 * nc + 10;
+    int cycles = 0;
+    for (;;) {
+        /* down */
+        double* xf = x;
+        const double* bf = rhs;
+        int done = 0;
+        for (int l = 0; l < nl - 1; l++) {
+            for (int k = 0; k < pre; k++) mg_rb(&L[l], xf, bf, 0.0, 1.0);
+            const double r2 = mg_restrict_lv(&L[l], xf, bf, 0.0, &L[l + 1], L[l + 1].b);
+            memset(L[l + 1].x, 0, sizeof(double) * (size_t)L[l + 1].nx * L[l + 1].ny);
+            if (l == 0 && (r2 <= rtol * rtol * b2 || r2 == 0.0 || cycles >= maxcycles)) { done = 1; break; }
+            xf = L[l + 1].x;
+            bf = L[l + 1].b;
+        }
+        if (done) break;
+        for (int k = 0; k < itc; k++) mg_rb(Lc, L[nl - 1].x, L[nl - 1].b, 0.0, omc);
+        for (int l = nl - 2; l >= 0; l--) {
+            double* xl = l == 0 ? x : L[l].x;
+            const double* bl = l == 0 ? rhs : L[l].b;
+            og_mg_prolong(L[l].nx, L[l].ny, L[l + 1].x, xl);
+            for (int k = 0; k < post; k++) mg_rb(&L[l], xl, bl, 0.0, 1.0);
+        }
+        cycles++;
+    }
+    mg_free(L, nl);
+    return cycles;
+}
+
+/* ---------------------------------------------------------------------- */
 /* time stepper, FluidSolver::Solve FluidSolver.cpp:536-567                */
 
 struct og_solver {
     og_grid* g;
     double dt, re, rtol;
+    int gpu_alg;
+    double omega_v;
     double *u, *v, *phi, *cu, *cv, *gx, *gy, *ru, *rv, *us, *vs, *rp;
 };
 
@@ -817,6 +978,11 @@ og_solver* og_solver_new(og_grid* g, double dt, double re, double rtol) {
     double** arr[] = {&s->u, &s->v, &s->phi, &s->cu, &s->cv, &s->gx, &s->gy, &s->ru, &s->rv, &s->us, &s->vs, &s->rp};
     for (unsigned k = 0; k < sizeof arr / sizeof arr[0]; k++) *arr[k] = calloc(n, sizeof(double));
     return s;
+}
+
+void og_solver_set_algorithm(og_solver* s, int gpu_algorithm, double omega_v) {
+    s->gpu_alg = gpu_algorithm;
+    s->omega_v = omega_v;
 }
 
 void og_solver_free(og_solver* s) {
@@ -831,13 +997,38 @@ int og_solver_step(og_solver* s, double* mm, int* its) {
     int n = g->N, maxit = 100000;
     double alpha = s->dt / (2 * s->re);
     og_rhs_velocity(g, s->dt, s->re, s->u, s->v, s->gx, s->gy, s->cu, s->cv, s->ru, s->rv);
-    /* KSPSolve(uSolver, ...) x2 with zero initial guess (:547-548) */
-    memset(s->us, 0, sizeof(double) * n);
-    memset(s->vs, 0, sizeof(double) * n);
-    int iu = og_solve_helmholtz(g, alpha, s->ru, s->us, s->rtol, maxit);
-    int iv = og_solve_helmholtz(g, alpha, s->rv, s->vs, s->rtol, maxit);
-    og_divergence(g, s->dt, s->us, s->vs, s->rp);
-    int ip = og_solve_poisson(g, s->rp, s->phi, s->rtol, maxit); /* warm start (:54) */
+    int iu, iv, ip;
+    if (s->gpu_alg) {
+        /* the GPU path's algorithm: RB-SOR Helmholtz from u^n, checked every sweep; MG Poisson */
+        memcpy(s->us, s->u, sizeof(double) * n);
+        memcpy(s->vs, s->v, sizeof(double) * n);
+        double bu = dot(n, s->ru, s->ru), bv = dot(n, s->rv, s->rv), r2;
+        iu = 0;
+        do {
+            double* tu = malloc(sizeof(double) * n);
+            double* tv = malloc(sizeof(double) * n);
+            og_apply_helmholtz(g, alpha, s->us, tu);
+            og_apply_helmholtz(g, alpha, s->vs, tv);
+            double ru2 = 0, rv2 = 0;
+            for (int c = 0; c < n; c++) { ru2 += (s->ru[c] - tu[c]) * (s->ru[c] - tu[c]); rv2 += (s->rv[c] - tv[c]) * (s->rv[c] - tv[c]); }
+            free(tu); free(tv);
+            if ((ru2 <= s->rtol * s->rtol * bu || ru2 == 0) && (rv2 <= s->rtol * s->rtol * bv || rv2 == 0)) break;
+            r2 = og_helmholtz_rbsor_sweep(g, alpha, s->us, s->vs, s->ru, s->rv, s->omega_v);
+            (void)r2;
+            iu++;
+        } while (iu < maxit);
+        iv = iu;
+        og_divergence(g, s->dt, s->us, s->vs, s->rp);
+        ip = og_mg_solve(g, s->rp, s->phi, s->rtol, 2, 2, 1000);
+    } else {
+        /* KSPSolve(uSolver, ...) x2 with zero initial guess (:547-548) */
+        memset(s->us, 0, sizeof(double) * n);
+        memset(s->vs, 0, sizeof(double) * n);
+        iu = og_solve_helmholtz(g, alpha, s->ru, s->us, s->rtol, maxit);
+        iv = og_solve_helmholtz(g, alpha, s->rv, s->vs, s->rtol, maxit);
+        og_divergence(g, s->dt, s->us, s->vs, s->rp);
+        ip = og_solve_poisson(g, s->rp, s->phi, s->rtol, maxit); /* warm start (:54) */
+    }
     og_correct(g, s->dt, s->us, s->vs, s->phi, s->u, s->v, s->gx, s->gy);
     double umin = s->u[0], umax = s->u[0], vmin = s->v[0], vmax = s->v[0];
     for (int c = 1; c < n; c++) {

@@ -98,9 +98,25 @@ int og_solve_helmholtz(const og_grid* g, double alpha, const double* rhs, double
 /* removes the null-space (plain mean) from rhs in place first (FluidSolver.cpp:550) */
 int og_solve_poisson(const og_grid* g, double* rhs, double* x, double rtol, int maxit);
 
+/* ---- geometric multigrid (the GPU path's Poisson solver, restated for parity and as
+ *      the same-algorithm CPU baseline).  Rectangles with Dirichlet-type faces. ---- */
+/* fine residual (b - shift - L phi) -> coarse rhs, area-weighted average of each 2x2 block */
+void og_mg_restrict(int nx, int ny, const double* hx, const double* hy, const double* phi, const double* b,
+                    double shift, double* bc);
+/* phi (nx x ny) += bilinear prolongation of the coarse correction ec (nx/2 x ny/2) */
+void og_mg_prolong(int nx, int ny, const double* ec, double* phi);
+/* V-cycle solve of L x = rhs - mean(rhs) (rhs is mean-removed in place): RB Gauss-Seidel
+ * smoothing (pre/post sweeps), coarsening while both sizes are even down to <= 32 x 32,
+ * coarsest level by red-black SOR; stops when the residual after pre-smoothing is
+ * <= rtol * ||rhs||.  Returns V-cycles. */
+int og_mg_solve(const og_grid* g, double* rhs, double* x, double rtol, int pre, int post, int maxcycles);
+
 /* ---- full time stepper (FluidSolver::Solve, FluidSolver.cpp:536-567) ---- */
 og_solver* og_solver_new(og_grid* g, double dt, double re, double rtol);
 void og_solver_free(og_solver* s);
+/* algorithm: 0 = Krylov solves (the reference's kind, default); 1 = the GPU path's
+ * algorithm (red-black SOR Helmholtz with omega_v, multigrid Poisson) */
+void og_solver_set_algorithm(og_solver* s, int gpu_algorithm, double omega_v);
 /* one time step; mm = {umin, umax, vmin, vmax}; its = {it_u, it_v, it_phi} */
 int  og_solver_step(og_solver* s, double* mm, int* its);
 /* get / set state: u, v, phi, cu0, cv0, gx, gy (divPhi) -- any pointer may be NULL */

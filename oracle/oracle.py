@@ -36,6 +36,10 @@ _SIG = {
     "og_helmholtz_rbsor_sweep": (ctypes.c_double, [_P, ctypes.c_double, _D, _D, _D, _D, ctypes.c_double]),
     "og_solve_helmholtz": (ctypes.c_int, [_P, ctypes.c_double, _D, _D, ctypes.c_double, ctypes.c_int]),
     "og_solve_poisson": (ctypes.c_int, [_P, _D, _D, ctypes.c_double, ctypes.c_int]),
+    "og_mg_restrict": (None, [ctypes.c_int, ctypes.c_int, _D, _D, _D, _D, ctypes.c_double, _D]),
+    "og_mg_prolong": (None, [ctypes.c_int, ctypes.c_int, _D, _D]),
+    "og_mg_solve": (ctypes.c_int, [_P, _D, _D, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "og_solver_set_algorithm": (None, [_P, ctypes.c_int, ctypes.c_double]),
     "og_solver_new": (_P, [_P, ctypes.c_double, ctypes.c_double, ctypes.c_double]),
     "og_solver_free": (None, [_P]),
     "og_solver_step": (ctypes.c_int, [_P, _D, _I]),
@@ -162,6 +166,24 @@ class OGrid:
         it = lib().og_solve_helmholtz(self.h, alpha, _d(_f(rhs)), _d(x), rtol, maxit)
         return x, it
 
+    def mg_restrict(self, phi, b, shift):
+        bc = np.zeros((self.nx // 2) * (self.ny // 2))
+        lib().og_mg_restrict(self.nx, self.ny, _d(self.hx), _d(self.hy), _d(_f(phi)), _d(_f(b)), shift, _d(bc))
+        return bc
+
+    def mg_prolong(self, phi, ec):
+        p = _f(phi).copy()
+        lib().og_mg_prolong(self.nx, self.ny, _d(_f(ec)), _d(p))
+        return p
+
+    def mg_solve(self, rhs, x0=None, rtol=1e-10, pre=2, post=2, maxcycles=1000):
+        b = _f(rhs).copy()
+        x = self.z() if x0 is None else _f(x0).copy()
+        cyc = lib().og_mg_solve(self.h, _d(b), _d(x), rtol, pre, post, maxcycles)
+        if cyc < 0:
+            raise ValueError(lib().og_last_error().decode())
+        return x, cyc
+
     def solve_poisson(self, rhs, x0=None, rtol=1e-13, maxit=100000):
         b = _f(rhs).copy()
         x = self.z() if x0 is None else _f(x0).copy()
@@ -182,6 +204,10 @@ class OSolver:
             lib().og_solver_free(self.h)
         except Exception:
             pass
+
+    def use_gpu_algorithm(self, omega_v):
+        """RB-SOR Helmholtz + multigrid Poisson (the GPU path's algorithm; CPU baseline)."""
+        lib().og_solver_set_algorithm(self.h, 1, omega_v)
 
     def step(self):
         mm = np.zeros(4)

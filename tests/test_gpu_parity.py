@@ -273,3 +273,31 @@ def test_full_steps_other_poisson_solvers(gpu, solver):
     u, v, _ = gs.fields()
     assert np.max(np.abs(u.ravel() - ref["u"])) <= 1e-6
     assert np.max(np.abs(v.ravel() - ref["v"])) <= 1e-6
+
+
+@pytest.mark.parametrize("nx,ny,xr,yr", [(64, 64, -1, -1), (96, 40, 1.03, -1), (260, 130, -1, 0.99)])
+def test_mg_restrict_and_prolong_match_oracle(gpu, nx, ny, xr, yr):
+    rng = np.random.default_rng(13)
+    og, gs = pair(gpu, nx, ny, 1e-3, 100.0, BC_CAVITY, xr, yr, poisson=gpu.NS_POISSON_MG)
+    phi, b = rand(rng, nx * ny), rand(rng, nx * ny, 10.0)
+    gs.set(gpu.NS_ARR_PHI, phi); gs.set(gpu.NS_ARR_RPHI, b)
+    bc = gs.mg_restrict()
+    ref = og.mg_restrict(phi, b, b.mean())
+    assert rel(bc, ref) <= 1e-12
+    ec = rand(rng, (nx // 2) * (ny // 2))
+    gs.mg_prolong(ec)
+    assert rel(gs.get(gpu.NS_ARR_PHI), og.mg_prolong(phi, ec)) <= 1e-13
+
+
+def test_mg_step_algorithm_matches_oracle_mg(gpu):
+    """Same algorithm on both sides (MG Poisson + RB-SOR Helmholtz): the CPU baseline leg."""
+    n, re, steps = 64, 100.0, 8
+    dt = 1.0 / (8 * n)
+    og, gs = pair(gpu, n, n, dt, re, rtol=1e-10)
+    osv = OSolver(og, dt, re, rtol=1e-10)
+    osv.use_gpu_algorithm(1.0)
+    for _ in range(steps):
+        gs.step(); osv.step()
+    u, v, _ = gs.fields()
+    ref = osv.get()
+    assert np.max(np.abs(u.ravel() - ref["u"])) <= 1e-8
