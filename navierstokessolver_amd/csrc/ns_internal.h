@@ -6,7 +6,7 @@
 
 namespace nsg {
 
-constexpr int HALO = 2;  // ghost rows per side of every field (K1's MUSCL stencil is radius 2)
+constexpr int HALO = 4;  // ghost rows per side: K1's MUSCL stencil (2) and the 2-sweep pass's cone (4)
 
 // Geometry of one x-slab.  Fields are (nxl + 2*HALO) rows of ld doubles, j contiguous;
 // pointers handed to kernels point at local row 0.  Global row = i0 + local row.
@@ -50,6 +50,12 @@ int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* p
 // K4 Jacobi: out = in + w (b - shift - L in)/diag
 int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* in, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st);
+// two red-black sweeps in one HBM pass (temporal blocking): same results as two calls above;
+// residual partials (if part) are of the input iterate
+int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                       const double* rp, const double* shift, double* part, hipStream_t st);
+int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                       double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st);
 // A/B reference: LDS-tiled fused sweeps (first version)
 int launch_pois_rbsor_tiled(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                             const double* rp, const double* shift, double* part, hipStream_t st);
@@ -61,8 +67,8 @@ void set_strip_rows(int L);
 int launch_pois_residual(const Geo& g, const Coef& c, const double* phi, const double* rp,
                          const double* shift, double* part, hipStream_t st);
 // K5: u = u* - dt grad phi ; min/max partials (4 per block)
-int launch_correct(const Geo& g, const Coef& c, double dt, double* u, double* v, const double* phi,
-                   double* part, hipStream_t st);
+int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, const double* vs, double* u, double* v,
+                   const double* phi, double* part, hipStream_t st);
 // reductions: sum `nv` interleaved values over n partials (p[k*nv + v]) -> out[v]
 void launch_reduce_sum(const double* p, int n, int nv, double* out, hipStream_t st);
 // min/max: partials are (umin, -umax, vmin, -vmax) per block -> out[4] = mins of each

@@ -323,8 +323,9 @@ __global__ __launch_bounds__(256) void k_div(Geo g, Coef c, double dt, const dou
 
 // ---------------------------------------------------------------- K5
 // CorrectVelocities (FluidSolver.cpp:512-534): u = u* - dt dphi/dx, v = v* - dt dphi/dy,
-// in place; fused VecMin/VecMax partials (:554-557) as (umin, -umax, vmin, -vmax).
-__global__ __launch_bounds__(256) void k_correct(Geo g, Coef c, double dt, double* __restrict__ u,
+// out of place; fused VecMin/VecMax partials (:554-557) as (umin, -umax, vmin, -vmax).
+__global__ __launch_bounds__(256) void k_correct(Geo g, Coef c, double dt, const double* __restrict__ us,
+                                                 const double* __restrict__ vs, double* __restrict__ u,
                                                  double* __restrict__ v, const double* __restrict__ phi,
                                                  double* __restrict__ part) {
     const int j = blockIdx.x * 64 + threadIdx.x;
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(256) void k_correct(Geo g, Coef c, double dt, doubl
         double gx, gy;
         grad_phi(g, c, phi, li, j, gx, gy);
         const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
-        const double un = u[o] - dt * gx, vn = v[o] - dt * gy;
+        const double un = us[o] - dt * gx, vn = vs[o] - dt * gy;
         u[o] = un;
         v[o] = vn;
         // NaN-propagating min so a blown-up step is visible in the stats
@@ -597,11 +598,30 @@ struct DiagCache {
     }
 };
 
+// per-wave LDS copy of the row coefficients (cw, ce, cw + ce [+ bx]) for rows ib-4 .. ib+L+3:
+// read with a wave-uniform address (broadcast) instead of a global load on every row's
+// critical path (hipcc cannot prove the tables read-only against the `out` stores)
+constexpr int RC_MAX = 72;  // L <= 64
+template <int OP>
+__device__ __forceinline__ void stage_rows(const StreamArgs& a, double (*rc)[3], int ib, int lane) {
+    for (int t = lane; t < a.L + 8 && t < RC_MAX; t += 64) {
+        const int gi = min(max(a.i0 + ib - 4 + t, 0), a.nx - 1);
+        const double cw = a.cw[gi], ce = a.ce[gi];
+        rc[t][0] = cw;
+        rc[t][1] = ce;
+        rc[t][2] = cw + ce + (OP == 1 ? a.bx[gi] : 0.0);
+    }
+}
+
 template <int OP, bool RB, bool RES>
 __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
+    __shared__ double rcs[4][RC_MAX][3];
     const int lane = threadIdx.x & 63;
     const int nstr = a.nsj * a.nsi;
     const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    double (*rc)[3] = rcs[threadIdx.x >> 6];
+    if (wid < nstr) stage_rows<OP>(a, rc, (wid / a.nsj) * a.L, lane);
+    __syncthreads();
     double res = 0.0;
     if (wid < nstr) {
         const int si = wid / a.nsj, sj = wid - si * a.nsj;
@@ -640,9 +660,9 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
             double2 Rn = P1;
             if (m >= ib - 1 && m <= ie) {
                 double lf = __shfl_up(P1.y, 1, 64), rt = __shfl_down(P1.x, 1, 64);
-                const int gc = min(max(gim, 0), a.nx - 1);
-                const double cw = a.cw[gc], ce = a.ce[gc];
-                dm.at(cw + ce + (OP == 1 ? a.bx[gc] : 0.0), cd0, cd1, alpha, omega);
+                const double* rw = rc[m - ib + 4];
+                const double cw = rw[0], ce = rw[1];
+                dm.at(rw[2], cd0, cd1, alpha, omega);
                 double r0, r1;
                 if (RES && m >= ib && m < ie) {
                     relax<OP>(P1.x, P0.x, P2.x, lf, P1.y, Bm.x, cw, ce, cs0, cn0, dm.d0, dm.w0, alpha, r0);
@@ -669,8 +689,9 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
                 const int k = r - 2, gik = a.i0 + k;
                 if (k >= ib && k < ie) {
                     const double lf = __shfl_up(R1.y, 1, 64), rt = __shfl_down(R1.x, 1, 64);
-                    const double cw = a.cw[gik], ce = a.ce[gik];
-                    dk.at(cw + ce + (OP == 1 ? a.bx[gik] : 0.0), cd0, cd1, alpha, omega);
+                    const double* rw = rc[k - ib + 4];
+                    const double cw = rw[0], ce = rw[1];
+                    dk.at(rw[2], cd0, cd1, alpha, omega);
                     double2 o = R1;
                     double rr;
                     if ((gik & 1) == 0) {  // black = c1
@@ -692,6 +713,132 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
             for (int q = 0; q < SD; q++) {
                 if (r + q <= r1) step(Q[q], QB[q], r + q);
                 load(r + q + SD, Q[q], QB[q]);
+            }
+        }
+    }
+    if (RES) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
+        if (lane == 0 && wid < nstr) a.part[wid] = res;
+    }
+}
+
+// ------------------------------------------------ K2 / K4: two sweeps per HBM pass
+// Temporal blocking of k_sweep<RB>: the row pipeline carries four stages -- red of
+// sweep 1 at row r-1, black 1 at r-2, red 2 at r-3, black 2 at r-4 -- so one read of
+// phi and b and one write of phi give two full red-black sweeps.  The dependency cone
+// widens by one cell per half-sweep, so strips overlap by 4 columns on each side
+// (128 loaded, 120 written) and read rows ib-4 .. ie+3.  Every value is computed with
+// the same arithmetic as two k_sweep launches (bit-identical).
+constexpr int SW2 = 120;
+constexpr int SD2 = 3;
+
+template <int OP, bool RES>
+__global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
+    __shared__ double rcs[4][RC_MAX][3];
+    const int lane = threadIdx.x & 63;
+    const int nstr = a.nsj * a.nsi;
+    const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    double (*rc)[3] = rcs[threadIdx.x >> 6];
+    if (wid < nstr) stage_rows<OP>(a, rc, (wid / a.nsj) * a.L, lane);
+    __syncthreads();
+    double res = 0.0;
+    if (wid < nstr) {
+        const int si = wid / a.nsj, sj = wid - si * a.nsj;
+        const int jb = sj * SW2, ib = si * a.L;
+        const int ie = min(ib + a.L, a.nxl);
+        const int ny = a.ny, ld = a.ld;
+        const int c0 = jb - 4 + 2 * lane, c1 = c0 + 1;
+        const int lc = min(max(c0, 0), ld - 2);
+        const bool v0 = c0 >= 0 && c0 < ny, v1 = c1 >= 0 && c1 < ny;
+        const bool wr = lane >= 2 && lane <= 61 && c0 < ny;
+        const bool o0 = wr && v0, o1 = wr && v1;
+        const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
+        const double cs0 = a.cs[k0], cn0 = a.cn[k0], cd0 = cs0 + cn0 + (OP == 1 ? a.by[k0] : 0.0);
+        const double cs1 = a.cs[k1], cn1 = a.cn[k1], cd1 = cs1 + cn1 + (OP == 1 ? a.by[k1] : 0.0);
+        const double shift = (OP == 0 && a.shift) ? a.shift[0] : 0.0;
+        const double alpha = a.alpha, omega = a.omega;
+        const int rlo = -HALO, rhi = a.nxl + HALO - 1;
+
+        double2 Q[SD2], QB[SD2];
+        auto load = [&](int slot_r, double2& p, double2& bb) {
+            const int lp = min(max(slot_r, rlo), rhi), lb = min(max(slot_r - 1, rlo), rhi);
+            p = *reinterpret_cast<const double2*>(a.in + (ptrdiff_t)lp * ld + lc);
+            bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
+        };
+        // windows (3 rows each) of the four stages' inputs, rhs rows r-1 .. r-4
+        double2 P0 = {0, 0}, P1 = {0, 0}, P2 = {0, 0};     // old:           rows r-2 .. r
+        double2 A0 = {0, 0}, A1 = {0, 0}, A2 = {0, 0};     // after red 1:   rows r-3 .. r-1
+        double2 C0 = {0, 0}, C1 = {0, 0}, C2 = {0, 0};     // after black 1: rows r-4 .. r-2
+        double2 E0 = {0, 0}, E1 = {0, 0}, E2 = {0, 0};     // after red 2:   rows r-5 .. r-3
+        double2 B1 = {0, 0}, B2 = {0, 0}, B3 = {0, 0}, B4 = {0, 0};
+        DiagCache<OP> d1, d2, d3, d4;
+
+        // one colour update of row `row` (window W0 above, W1 the row, W2 below); colour
+        // parity: update c0 when (gi + c0) % 2 == par
+        auto half = [&](const double2& W0, const double2& W1, const double2& W2, const double2& B, int row, int par,
+                        DiagCache<OP>& dc) -> double2 {
+            double2 o = W1;
+            const int gi = a.i0 + row;
+            if (gi < 0 || gi >= a.nx) return o;
+            const double lf = __shfl_up(W1.y, 1, 64), rt = __shfl_down(W1.x, 1, 64);
+            const double* rw = rc[row - ib + 4];
+            const double cw = rw[0], ce = rw[1];
+            dc.at(rw[2], cd0, cd1, alpha, omega);
+            double rr;
+            if ((gi & 1) == par) {
+                if (v0) o.x = relax<OP>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, dc.d0, dc.w0, alpha, rr);
+            } else {
+                if (v1) o.y = relax<OP>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, dc.d1, dc.w1, alpha, rr);
+            }
+            return o;
+        };
+
+        auto step = [&](const double2 p, const double2 bb, int r) {
+            P0 = P1; P1 = P2; P2 = p;
+            B4 = B3; B3 = B2; B2 = B1;
+            B1 = make_double2(bb.x - shift, bb.y - shift);
+            // stage 1: red of sweep 1 at m = r-1 (+ residual of the input)
+            const int m = r - 1;
+            double2 n1 = P1;
+            if (m >= ib - 3 && m <= ie + 2) {
+                if (RES && m >= ib && m < ie) {
+                    const double lf = __shfl_up(P1.y, 1, 64), rt = __shfl_down(P1.x, 1, 64);
+                    const double* rw = rc[m - ib + 4];
+                    const double cw = rw[0], ce = rw[1];
+                    d1.at(rw[2], cd0, cd1, alpha, omega);
+                    double r0, r1;
+                    relax<OP>(P1.x, P0.x, P2.x, lf, P1.y, B1.x, cw, ce, cs0, cn0, d1.d0, d1.w0, alpha, r0);
+                    relax<OP>(P1.y, P0.y, P2.y, P1.x, rt, B1.y, cw, ce, cs1, cn1, d1.d1, d1.w1, alpha, r1);
+                    res += (o0 ? r0 * r0 : 0.0) + (o1 ? r1 * r1 : 0.0);
+                }
+                n1 = half(P0, P1, P2, B1, m, 0, d1);
+            }
+            A0 = A1; A1 = A2; A2 = n1;
+            // stage 2: black of sweep 1 at r-2
+            double2 n2 = A1;
+            if (r - 2 >= ib - 2 && r - 2 <= ie + 1) n2 = half(A0, A1, A2, B2, r - 2, 1, d2);
+            C0 = C1; C1 = C2; C2 = n2;
+            // stage 3: red of sweep 2 at r-3
+            double2 n3 = C1;
+            if (r - 3 >= ib - 1 && r - 3 <= ie) n3 = half(C0, C1, C2, B3, r - 3, 0, d3);
+            E0 = E1; E1 = E2; E2 = n3;
+            // stage 4: black of sweep 2 at r-4, stored
+            const int k = r - 4;
+            if (k >= ib && k < ie) {
+                const double2 o = half(E0, E1, E2, B4, k, 1, d4);
+                if (wr) *reinterpret_cast<double2*>(a.out + (ptrdiff_t)k * ld + c0) = o;
+            }
+        };
+
+        const int r0 = ib - 4, r1 = ie + 3;
+#pragma unroll
+        for (int q = 0; q < SD2; q++) load(r0 + q, Q[q], QB[q]);
+        for (int r = r0; r <= r1; r += SD2) {
+#pragma unroll
+            for (int q = 0; q < SD2; q++) {
+                if (r + q <= r1) step(Q[q], QB[q], r + q);
+                load(r + q + SD2, Q[q], QB[q]);
             }
         }
     }
@@ -885,7 +1032,7 @@ int max_partials(const Geo& g) {
     const dim3 cg = cell_grid(g);
     int n = (int)(cg.x * cg.y) * 4;
     const int tiles = ((g.nxl + 7) / 8) * ((g.ny + 63) / 64) * 2;   // tiled sweeps
-    const int strips = ((g.nxl + 3) / 4) * ((g.ny + 123) / 124) * 2;  // streaming sweeps, strip rows >= 4
+    const int strips = ((g.nxl + 3) / 4) * ((g.ny + 119) / 120) * 2;  // streaming sweeps, strip rows >= 4
     return std::max(n, std::max(tiles, strips));
 }
 
@@ -907,10 +1054,10 @@ int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const do
     return (int)(cg.x * cg.y);
 }
 
-int launch_correct(const Geo& g, const Coef& c, double dt, double* u, double* v, const double* phi, double* part,
-                   hipStream_t st) {
+int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, const double* vs, double* u, double* v,
+                   const double* phi, double* part, hipStream_t st) {
     const dim3 cg = cell_grid(g);
-    hipLaunchKernelGGL(k_correct, cg, dim3(64, 4), 0, st, g, c, dt, u, v, phi, part);
+    hipLaunchKernelGGL(k_correct, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part);
     return (int)(cg.x * cg.y);
 }
 
@@ -927,7 +1074,7 @@ static SweepArgs make_args(const Geo& g, const Coef& c, int TI, int TJ) {
 }
 
 static int g_strip_rows = 0;  // 0 = adaptive
-void set_strip_rows(int L) { g_strip_rows = L >= 4 ? (L & ~1) : 0; }
+void set_strip_rows(int L) { g_strip_rows = L >= 4 ? (std::min(L, 64) & ~1) : 0; }
 
 // rows per strip (measured, tools/sweep_levels.py): 16 while that still gives >= 2048
 // waves (4096^2, 2048^2), else 4 -- coarse multigrid levels are latency-bound and need
@@ -964,6 +1111,31 @@ static int launch_stream(const StreamArgs& a, hipStream_t st) {
 int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                       const double* rp, const double* shift, double* part, hipStream_t st) {
     return launch_stream<0, true>(stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false), st);
+}
+
+// two fused red-black sweeps: strips of 120 written columns; 32 rows per strip while that
+// still gives >= 2048 waves (fewer re-read rows: ib-4 .. ie+3), else 8
+template <int OP>
+static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st) {
+    a.nsj = (g.ny + SW2 - 1) / SW2;
+    a.L = g_strip_rows ? g_strip_rows : (a.nsj * ((g.nxl + 31) / 32) >= 2048 ? 32 : 8);
+    a.nsi = (g.nxl + a.L - 1) / a.L;
+    const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
+    if (a.part) hipLaunchKernelGGL((k_sweep2<OP, true>), dim3(nblk), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_sweep2<OP, false>), dim3(nblk), dim3(256), 0, st, a);
+    return nstr;
+}
+
+int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                       const double* rp, const double* shift, double* part, hipStream_t st) {
+    return launch_stream2<0>(stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false), g, st);
+}
+
+int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                       double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st) {
+    const int n = launch_stream2<1>(stream_args(g, c, u, uo, ru, nullptr, alpha, omega, part, true), g, st);
+    launch_stream2<1>(stream_args(g, c, v, vo, rv, nullptr, alpha, omega, part ? part + n : nullptr, true), g, st);
+    return n;
 }
 
 int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* in, double* out, const double* rp,

@@ -100,7 +100,7 @@ struct ns_solver {
     ncclComm_t comm = nullptr;
     double ncells = 0;           // global cell count
     std::vector<hipEvent_t> ev;  // timing events (pairs)
-    int helm_batch0 = 3, pois_batch0 = 8;
+    int helm_batch0 = 4, pois_batch0 = 8;
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
     int mg_pre = 2, mg_post = 2, mg_coarse_iters = 0;
@@ -206,6 +206,37 @@ int helm_sweep(ns_solver* s, double alpha, double* part) {
     return nb;
 }
 
+// two Helmholtz sweeps in one pass (temporal blocking), then swap
+int helm_sweep2(ns_solver* s, double alpha, double* part) {
+    const int nb = nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
+                                           s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
+                                           s->arr[NS_ARR_RV], part, s->st);
+    std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
+    std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
+    return nb;
+}
+
+// `n` Helmholtz sweeps: pairs in one pass each (ghost width 4), a single sweep for an odd
+// remainder.  Residual partials of the LAST launch's input go to `part_last`, of the first
+// launch's input to `part_first` (either may be null).  Returns the last launch's partial
+// count; *last_w = sweeps in the last launch.
+int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* part_last, int* nb_first,
+                int* last_w) {
+    int nb = 0, k = 0, launch = 0;
+    while (k < n) {
+        const int w = (n - k >= 2 && !s->tiled) ? 2 : 1;
+        const bool last = k + w >= n;
+        double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
+        CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2 * w));
+        nb = w == 2 ? helm_sweep2(s, alpha, part) : helm_sweep(s, alpha, part);
+        if (launch == 0 && nb_first) *nb_first = nb;
+        if (last) *last_w = w;
+        k += w;
+        launch++;
+    }
+    return nb;
+}
+
 // one Poisson sweep PHI -> TMP (RB-SOR or Jacobi), then swap
 int pois_sweep(ns_solver* s, double* part) {
     int nb;
@@ -249,19 +280,16 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
     double* p0 = s->part + 2 * (size_t)nsg::max_partials(s->g) / 2;  // second half: first-sweep residuals
     for (;;) {
         const int n = std::min(batch, s->max_iters - sweeps);
-        int nb = 0;
-        const bool first = sweeps == 0 && n > 1;
-        for (int k = 0; k < n; k++) {
-            CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
-            double* part = k == n - 1 ? s->part : (first && k == 0 ? p0 : nullptr);
-            nb = helm_sweep(s, alpha, part);
-        }
+        const bool first = sweeps == 0 && n > 2;
+        int nb0 = 0, lw = 1;
+        const int nb = helm_sweeps(s, alpha, n, first ? p0 : nullptr, s->part, &nb0, &lw);
+        (void)nb0;
         sweeps += n;
         nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
         nsg::launch_reduce_sum(s->part + nb, nb, 1, s->scal + S_RES + 1, s->st);
         if (first) {
-            nsg::launch_reduce_sum(p0, nb, 1, s->scal + S_AUX, s->st);
-            nsg::launch_reduce_sum(p0 + nb, nb, 1, s->scal + S_AUX + 1, s->st);
+            nsg::launch_reduce_sum(p0, nb0, 1, s->scal + S_AUX, s->st);
+            nsg::launch_reduce_sum(p0 + nb0, nb0, 1, s->scal + S_AUX + 1, s->st);
         }
         CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
         if (first) CHK(allreduce(s, s->scal + S_AUX, 2, ncclSum));
@@ -278,10 +306,10 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
             prev_r2 = std::max(s->hs[S_AUX] / std::max(bu, 1e-300), s->hs[S_AUX + 1] / std::max(bv, 1e-300));
             prev_at = 0;
         }
-        const int nbatch = next_batch(batch, prev_r2, prev_at, r2, sweeps - 1, tol2, s->max_iters);
+        const int nbatch = next_batch(batch, prev_r2, prev_at, r2, sweeps - lw, tol2, s->max_iters);
         prev_r2 = r2;
-        prev_at = sweeps - 1;
-        batch = nbatch;
+        prev_at = sweeps - lw;
+        batch = nbatch + (nbatch & 1);  // even batches: whole 2-sweep passes
     }
     *its = sweeps;
     return 0;
@@ -347,15 +375,18 @@ MgLevel& level(ns_solver* s, int l) {
 
 int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
     MgLevel& L = level(s, l);
-    for (int k = 0; k < n; k++) {
-        CHK(halo_g(s, L.g, {L.phi}, 2));
+    for (int k = 0; k < n;) {
+        const int w = (n - k >= 2 && !s->tiled) ? 2 : 1;   // two sweeps per HBM pass where possible
+        CHK(halo_g(s, L.g, {L.phi}, 2 * w));
         const bool t = s->timing && l == 0;
         if (t) HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st));
-        nsg::launch_pois_rbsor(L.g, L.c, s->mg_omega_s, L.phi, L.tmp, L.b, l == 0 ? s->scal + S_SHIFT : nullptr,
-                               nullptr, s->st);
+        const double* sh = l == 0 ? s->scal + S_SHIFT : nullptr;
+        if (w == 2) nsg::launch_pois_rbsor2(L.g, L.c, s->mg_omega_s, L.phi, L.tmp, L.b, sh, nullptr, s->st);
+        else nsg::launch_pois_rbsor(L.g, L.c, s->mg_omega_s, L.phi, L.tmp, L.b, sh, nullptr, s->st);
         if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn) + 1], s->st)); (*tn)++; }
         std::swap(L.phi, L.tmp);
         if (l == 0) { s->arr[NS_ARR_PHI] = L.phi; s->arr[NS_ARR_TMP] = L.tmp; }
+        k += w;
     }
     return 0;
 }
@@ -395,7 +426,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
             CHK(halo_g(s, F.g, {F.phi}, 1));
             const int nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, l == 0 ? s->scal + S_SHIFT : nullptr, C.g, C.c,
                                                 C.b, C.phi, s->part, s->st);
-            CHK(halo_g(s, C.g, {C.b}, 1));
+            CHK(halo_g(s, C.g, {C.b}, 3));
             if (l == 0) {
                 // fine residual after pre-smoothing: the convergence test (one host sync per cycle)
                 nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
@@ -554,9 +585,12 @@ int rhs(ns_solver* s) {
     return 0;
 }
 
+// u^{n+1} = u* - dt grad phi into the ping-pong partners (no in-place read/write hazard)
 int correct(ns_solver* s) {
-    const int nb = nsg::launch_correct(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_PHI],
-                                       s->part, s->st);
+    const int nb = nsg::launch_correct(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
+                                       s->arr[NS_ARR_TMPV], s->arr[NS_ARR_PHI], s->part, s->st);
+    std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
+    std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
     nsg::launch_reduce_min(s->part, nb, 4, s->scal + S_MM, s->st);
     CHK(allreduce(s, s->scal + S_MM, 4, ncclMin));
     return 0;
@@ -689,7 +723,10 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (p->check_every > 0) s->pois_batch0 = s->helm_batch0 = p->check_every;
     s->timing = p->timing;
     if (const char* e = getenv("NSGPU_SWEEP")) s->tiled = std::strcmp(e, "tiled") == 0;
-    if (const char* e = getenv("NSGPU_STRIP_ROWS")) nsg::set_strip_rows(atoi(e));
+    {
+        const char* e = getenv("NSGPU_STRIP_ROWS");  // tuning override; unset = adaptive
+        nsg::set_strip_rows(e ? atoi(e) : 0);
+    }
     s->rank = p->rank;
     s->nranks = p->nranks;
     s->ncells = (double)gd->nx * (double)gd->ny;
@@ -778,12 +815,14 @@ int ns_step(ns_solver* s, ns_stats* out) {
     CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
     CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
     CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
-    CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 1));       // rhs ghost rows: the fused sweep's ring reds
+    // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
+    // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
+    CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 3));       // rhs ghost rows: the fused sweep's ring reds
     CHK(helm_solve(s, &st.it_u, &st.res_u, &st.res_v));            // KSPSolve(uSolver) x2 (:547-548)
     st.it_v = st.it_u;
     CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
-    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 1));
+    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 3));
     if (s->poisson == NS_POISSON_MG) CHK(pois_solve_mg(s, &st.it_phi, &st.res_phi, &st));  // KSPSolve(phiSolver) (:551)
     else CHK(pois_solve(s, &st.it_phi, &st.res_phi, &st));
     CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
@@ -852,9 +891,15 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         if (out) { out[0] = s->hs[S_HBN]; out[1] = s->hs[S_HBN + 1]; }
         return 0;
     case NS_K_HELMHOLTZ: {
+        // (iters-1)/2 two-sweep passes, then single sweeps; the residual is of the last sweep's input
         int nb = 0;
-        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 1));
-        for (int k = 0; k < iters; k++) {
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 3));
+        const int pairs = iters > 0 ? (iters - 1) / 2 : 0;
+        for (int k = 0; k < pairs; k++) {
+            CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 4));
+            helm_sweep2(s, alpha, nullptr);
+        }
+        for (int k = 2 * pairs; k < iters; k++) {
             CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
             nb = helm_sweep(s, alpha, k == iters - 1 ? s->part : nullptr);
         }
@@ -875,8 +920,15 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         return 0;
     case NS_K_POISSON: {
         int nb = 0;
-        CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 1));
-        for (int k = 0; k < iters; k++) {
+        CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 3));
+        const int pairs = (s->poisson != NS_POISSON_JACOBI && !s->tiled && iters > 0) ? (iters - 1) / 2 : 0;
+        for (int k = 0; k < pairs; k++) {
+            CHK(halo(s, {s->arr[NS_ARR_PHI]}, 4));
+            nsg::launch_pois_rbsor2(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP], s->arr[NS_ARR_RPHI],
+                                    s->scal + S_SHIFT, nullptr, s->st);
+            std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
+        }
+        for (int k = 2 * pairs; k < iters; k++) {
             double* part = k == iters - 1 ? s->part : nullptr;
             CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
             nb = pois_sweep(s, part);
@@ -899,7 +951,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         int its = 0;
         double ru = 0, rv = 0;
         CHK(helm_bnorm(s));
-        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 1));
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 3));
         CHK(helm_solve(s, &its, &ru, &rv));
         if (out) { out[0] = its; out[1] = std::max(ru, rv); }
         return 0;
@@ -908,7 +960,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         int its = 0;
         double r = 0;
         CHK(rhs_mean(s));
-        CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 1));
+        CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 3));
         if (s->poisson == NS_POISSON_MG) CHK(pois_solve_mg(s, &its, &r, nullptr));
         else CHK(pois_solve(s, &its, &r, nullptr));
         if (out) { out[0] = its; out[1] = r; }
@@ -957,7 +1009,7 @@ int ns_fill_random(ns_solver* s, uint64_t seed) {
     HIPCHK(hipSetDevice(s->device));
     nsg::launch_fill_random(s->g, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], seed, s->st);
     CHK(rhs_mean(s));  // the random rhs's mean becomes the Poisson shift (null-space removal)
-    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 1));
+    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 3));
     HIPCHK(hipStreamSynchronize(s->st));
     return 0;
 }
@@ -966,14 +1018,24 @@ int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
     if (!s || iters <= 0) { set_err("bad arguments"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
     CHK(ensure_events(s, 2 * (size_t)iters));
-    for (int k = 0; k < warmup; k++) {
-        CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
-        pois_sweep(s, nullptr);
-    }
+    // NSGPU_TIME_PAIRS=1: time the two-sweep (temporally blocked) pass instead of a single sweep
+    const bool pairs = getenv("NSGPU_TIME_PAIRS") && s->poisson != NS_POISSON_JACOBI;
+    auto one = [&](double* part) -> int {
+        if (!pairs) {
+            CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
+            pois_sweep(s, part);
+            return 0;
+        }
+        CHK(halo(s, {s->arr[NS_ARR_PHI]}, 4));
+        nsg::launch_pois_rbsor2(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP], s->arr[NS_ARR_RPHI],
+                                s->scal + S_SHIFT, part, s->st);
+        std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
+        return 0;
+    };
+    for (int k = 0; k < warmup; k++) CHK(one(nullptr));
     for (int k = 0; k < iters; k++) {
-        CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
         HIPCHK(hipEventRecord(s->ev[2 * k], s->st));
-        pois_sweep(s, k == iters - 1 ? s->part : nullptr);
+        CHK(one(k == iters - 1 ? s->part : nullptr));
         HIPCHK(hipEventRecord(s->ev[2 * k + 1], s->st));
     }
     HIPCHK(hipStreamSynchronize(s->st));
