@@ -26,6 +26,8 @@ struct Coef {
     const double *hx, *hy;          // spacings
     const double *pw, *pe, *ps, *pn; // 2/(h (h+h_nb)) toward an existing neighbour, 0 at the boundary
     const double *bx, *by;          // Helmholtz Dirichlet boundary-face diagonal term 2/h^2 (0 inside)
+    const double *rhx, *rhy;        // 1/h
+    const double *rsx, *rsy;        // 2/(h_{i-1} + h_i) at index i (n+1 entries; 0 at both ends)
 };
 
 struct Partials {
@@ -80,14 +82,23 @@ int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st);
 // random fill of phi, rhs (sweep benchmark input)
 void launch_fill_random(const Geo& g, double* phi, double* rp, uint64_t seed, hipStream_t st);
 
+
+// the multigrid coarsening rule shared by the global hierarchy, the LDS V-cycle and the
+// oracle (og_mg_solve): halve while both sizes are even, >= 4, and the level has > 16 cells
+__host__ __device__ inline bool mg_can_coarsen(int nx, int ny) {
+    return nx % 2 == 0 && ny % 2 == 0 && nx >= 4 && ny >= 4 && nx * ny > 16;
+}
+
 // multigrid transfers (K4 MG): fine residual -> coarse rhs (+ coarse phi := 0, partials of r^2 over
-// fine cells); fine phi += bilinear(coarse correction); coarsest solve in one workgroup's LDS
+// fine cells); fine phi += bilinear(coarse correction)
 int launch_restrict(const Geo& gf, const Coef& cf, const double* phi, const double* b, const double* shift,
                     const Geo& gc, const Coef& cc, double* bc, double* pc, double* part, hipStream_t st);
 void launch_prolong(const Geo& gf, double* phi, const Geo& gc, const double* ec, hipStream_t st);
-size_t coarse_lds_bytes(const Geo& g);
-int launch_coarse_lds(const Geo& g, const Coef& c, double* phi, const double* b, double omega, int iters,
-                      hipStream_t st);
+
+// coarse levels as one LDS-resident V-cycle (single rank): level g and its 2x coarsenings
+size_t coarse_vcycle_bytes(const Geo& g);
+int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double* b, int cycles, int pre, int post,
+                         int citers, double comega, hipStream_t st);
 
 // max partials any launcher writes for this geometry
 int max_partials(const Geo& g);

@@ -16,6 +16,11 @@
 // No MFMA: every kernel is a stencil far below the fp64 VALU ridge point; HBM bound.
 #include "ns_internal.h"
 
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+
 #include <algorithm>
 
 namespace nsg {
@@ -120,8 +125,25 @@ __device__ __forceinline__ void grad_phi(const Geo& g, const Coef& c, const doub
 // ConstructRHS_V (FluidSolver.cpp:327-363): one thread per cell.  MUSCL needs
 // the neighbour's slope, so the stencil reaches 2 cells along each axis.
 // grad phi^{n-1} (divPhi) is recomputed from phi^{n-1} on the fly for boundary
-// cells -- bit-identical to the stored divPhi of the reference (GradP of the
-// same phi) and it saves a 16 B/cell state array.
+// cells -- the reference's stored divPhi is GradP of the same phi -- saving a
+// 16 B/cell state array.  Divisions by spacings use reciprocal tables (1/h,
+// 2/(h+h_nb)); minmode(a,b) = a*min(1,|b/a|) is evaluated as "the smaller of the two
+// (same sign)", its exact value, without the division.
+
+// minmode without the division: for a*b > 0, a*min(1, |b/a|) = (|b| < |a| ? b : a)
+__device__ __forceinline__ double minmode_nd(double a, double b) {
+    return (a * b > 0) ? (fabs(b) < fabs(a) ? b : a) : 0.0;
+}
+
+// SlopeLimiter component along one axis: forward difference a (2(qp-qc)/(h+hp) or
+// (gp-qc)/h at a wall), backward difference b; rsp / rsm = 2/(h+h_nb), rh = 1/h
+__device__ __forceinline__ double slope_r(double qc, double qp, double qm, bool hp, bool hm, double rh, double rsp,
+                                         double rsm, double gp, double gm) {
+    const double a = hp ? (qp - qc) * rsp : (gp - qc) * rh;
+    const double b = hm ? (qc - qm) * rsm : (qc - gm) * rh;
+    return minmode_nd(a, b);
+}
+
 __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
                                              const double* __restrict__ v, const double* __restrict__ phi,
                                              double* __restrict__ cu, double* __restrict__ cv,
@@ -135,11 +157,14 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
         const bool hW = gi > 0, hWW = gi > 1, hE = gi < nx - 1, hEE = gi < nx - 2;
         const bool hS = j > 0, hSS = j > 1, hN = j < ny - 1, hNN = j < ny - 2;
         const double hx = c.hx[gi], hy = c.hy[j];
-        const double hxW = hW ? c.hx[gi - 1] : 0.0, hxWW = hWW ? c.hx[gi - 2] : 0.0;
-        const double hxE = hE ? c.hx[gi + 1] : 0.0, hxEE = hEE ? c.hx[gi + 2] : 0.0;
-        const double hyS = hS ? c.hy[j - 1] : 0.0, hySS = hSS ? c.hy[j - 2] : 0.0;
-        const double hyN = hN ? c.hy[j + 1] : 0.0, hyNN = hNN ? c.hy[j + 2] : 0.0;
-        (void)hxWW; (void)hxEE; (void)hySS; (void)hyNN;
+        const double hxW = hW ? c.hx[gi - 1] : 0.0, hxE = hE ? c.hx[gi + 1] : 0.0;
+        const double hyS = hS ? c.hy[j - 1] : 0.0, hyN = hN ? c.hy[j + 1] : 0.0;
+        // reciprocals: 1/h of the cell and its neighbours, 2/(h+h') of each face
+        const double rx = c.rhx[gi], ry = c.rhy[j];
+        const double rxW = hW ? c.rhx[gi - 1] : 0.0, rxE = hE ? c.rhx[gi + 1] : 0.0;
+        const double ryS = hS ? c.rhy[j - 1] : 0.0, ryN = hN ? c.rhy[j + 1] : 0.0;
+        const double sxW = c.rsx[gi], sxE = c.rsx[gi + 1], sxWW = hW ? c.rsx[gi - 1] : 0.0, sxEE = hE ? c.rsx[gi + 2] : 0.0;
+        const double syS = c.rsy[j], syN = c.rsy[j + 1], sySS = hS ? c.rsy[j - 1] : 0.0, syNN = hN ? c.rsy[j + 2] : 0.0;
 
         const double uc = ldf(u, ld, li, j), vc = ldf(v, ld, li, j);
         const double uW = hW ? ldf(u, ld, li - 1, j) : 0.0, vW = hW ? ldf(v, ld, li - 1, j) : 0.0;
@@ -151,36 +176,37 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
         const double uSS = hSS ? ldf(u, ld, li, j - 2) : 0.0, vSS = hSS ? ldf(v, ld, li, j - 2) : 0.0;
         const double uNN = hNN ? ldf(u, ld, li, j + 2) : 0.0, vNN = hNN ? ldf(v, ld, li, j + 2) : 0.0;
 
-        // ---- DiffusiveFlux (FluidSolver.cpp:183-203) for u (d=0) and v (d=1)
+        // ---- DiffusiveFlux (FluidSolver.cpp:183-203) for u (d=0) and v (d=1); (1/re)/(h+h') = (0.5/re) * 2/(h+h')
+        const double hre = 0.5 / re;
         double ru_ = 0.0 + 1.0 * uc, rv_ = 0.0 + 1.0 * vc;    // VecSet + VecAXPY(1, u) (:335-338)
         ru_ += 0.5 * dt * cu[(ptrdiff_t)li * ld + j];           // VecAXPY(0.5dt, conv0) (:339-340)
         rv_ += 0.5 * dt * cv[(ptrdiff_t)li * ld + j];
         {
             double D0, D1, D2, D3;
-            D0 = hW ? (1 / re) * (uc - uW) / (hx + hxW) : (0.5 / re / hx) * (uc - ghost_v(g, uc, 0, 0));
-            D1 = hE ? (1 / re) * (uE - uc) / (hx + hxE) : -(0.5 / re / hx) * (uc - ghost_v(g, uc, 1, 0));
-            D2 = hS ? (1 / re) * (uc - uS) / (hy + hyS) : (0.5 / re / hy) * (uc - ghost_v(g, uc, 2, 0));
-            D3 = hN ? (1 / re) * (uN - uc) / (hy + hyN) : -(0.5 / re / hy) * (uc - ghost_v(g, uc, 3, 0));
-            ru_ += dt * ((D1 - D0) / hx + (D3 - D2) / hy);
-            D0 = hW ? (1 / re) * (vc - vW) / (hx + hxW) : (0.5 / re / hx) * (vc - ghost_v(g, vc, 0, 1));
-            D1 = hE ? (1 / re) * (vE - vc) / (hx + hxE) : -(0.5 / re / hx) * (vc - ghost_v(g, vc, 1, 1));
-            D2 = hS ? (1 / re) * (vc - vS) / (hy + hyS) : (0.5 / re / hy) * (vc - ghost_v(g, vc, 2, 1));
-            D3 = hN ? (1 / re) * (vN - vc) / (hy + hyN) : -(0.5 / re / hy) * (vc - ghost_v(g, vc, 3, 1));
-            rv_ += dt * ((D1 - D0) / hx + (D3 - D2) / hy);
+            D0 = hW ? hre * (uc - uW) * sxW : hre * rx * (uc - ghost_v(g, uc, 0, 0));
+            D1 = hE ? hre * (uE - uc) * sxE : -hre * rx * (uc - ghost_v(g, uc, 1, 0));
+            D2 = hS ? hre * (uc - uS) * syS : hre * ry * (uc - ghost_v(g, uc, 2, 0));
+            D3 = hN ? hre * (uN - uc) * syN : -hre * ry * (uc - ghost_v(g, uc, 3, 0));
+            ru_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
+            D0 = hW ? hre * (vc - vW) * sxW : hre * rx * (vc - ghost_v(g, vc, 0, 1));
+            D1 = hE ? hre * (vE - vc) * sxE : -hre * rx * (vc - ghost_v(g, vc, 1, 1));
+            D2 = hS ? hre * (vc - vS) * syS : hre * ry * (vc - ghost_v(g, vc, 2, 1));
+            D3 = hN ? hre * (vN - vc) * syN : -hre * ry * (vc - ghost_v(g, vc, 3, 1));
+            rv_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
         }
 
         // ---- ConvectiveFlux (FluidSolver.cpp:205-281)
         double C[8];
         {
             // x slopes of the cell and of its W/E neighbours (each needs its own ghosts at the wall)
-            const double sxu = slope1(uc, uE, uW, hE, hW, hx, hxE, hxW, ghost_v(g, uc, 1, 0), ghost_v(g, uc, 0, 0));
-            const double sxv = slope1(vc, vE, vW, hE, hW, hx, hxE, hxW, ghost_v(g, vc, 1, 1), ghost_v(g, vc, 0, 1));
+            const double sxu = slope_r(uc, uE, uW, hE, hW, rx, sxE, sxW, ghost_v(g, uc, 1, 0), ghost_v(g, uc, 0, 0));
+            const double sxv = slope_r(vc, vE, vW, hE, hW, rx, sxE, sxW, ghost_v(g, vc, 1, 1), ghost_v(g, vc, 0, 1));
             double u1, v1, u2, v2;
             u2 = uc - hx / 2 * sxu;
             v2 = vc - hx / 2 * sxv;
             if (hW) {
-                const double su = slope1(uW, uc, uWW, true, hWW, hxW, hx, hxWW, 0.0, ghost_v(g, uW, 0, 0));
-                const double sv = slope1(vW, vc, vWW, true, hWW, hxW, hx, hxWW, 0.0, ghost_v(g, vW, 0, 1));
+                const double su = slope_r(uW, uc, uWW, true, hWW, rxW, sxW, sxWW, 0.0, ghost_v(g, uW, 0, 0));
+                const double sv = slope_r(vW, vc, vWW, true, hWW, rxW, sxW, sxWW, 0.0, ghost_v(g, vW, 0, 1));
                 u1 = uW + hxW / 2 * su;
                 v1 = vW + hxW / 2 * sv;
             } else {
@@ -192,8 +218,8 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
             u1 = uc + hx / 2 * sxu;
             v1 = vc + hx / 2 * sxv;
             if (hE) {
-                const double su = slope1(uE, uEE, uc, hEE, true, hxE, hxEE, hx, ghost_v(g, uE, 1, 0), 0.0);
-                const double sv = slope1(vE, vEE, vc, hEE, true, hxE, hxEE, hx, ghost_v(g, vE, 1, 1), 0.0);
+                const double su = slope_r(uE, uEE, uc, hEE, true, rxE, sxEE, sxE, ghost_v(g, uE, 1, 0), 0.0);
+                const double sv = slope_r(vE, vEE, vc, hEE, true, rxE, sxEE, sxE, ghost_v(g, vE, 1, 1), 0.0);
                 u2 = uE - hxE / 2 * su;
                 v2 = vE - hxE / 2 * sv;
             } else {
@@ -203,13 +229,13 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
             C[2] = fnn(u1, u2);
             C[3] = fuv(u1, v1, u2, v2);
 
-            const double syu = slope1(uc, uN, uS, hN, hS, hy, hyN, hyS, ghost_v(g, uc, 3, 0), ghost_v(g, uc, 2, 0));
-            const double syv = slope1(vc, vN, vS, hN, hS, hy, hyN, hyS, ghost_v(g, vc, 3, 1), ghost_v(g, vc, 2, 1));
+            const double syu = slope_r(uc, uN, uS, hN, hS, ry, syN, syS, ghost_v(g, uc, 3, 0), ghost_v(g, uc, 2, 0));
+            const double syv = slope_r(vc, vN, vS, hN, hS, ry, syN, syS, ghost_v(g, vc, 3, 1), ghost_v(g, vc, 2, 1));
             u2 = uc - hy / 2 * syu;
             v2 = vc - hy / 2 * syv;
             if (hS) {
-                const double su = slope1(uS, uc, uSS, true, hSS, hyS, hy, hySS, 0.0, ghost_v(g, uS, 2, 0));
-                const double sv = slope1(vS, vc, vSS, true, hSS, hyS, hy, hySS, 0.0, ghost_v(g, vS, 2, 1));
+                const double su = slope_r(uS, uc, uSS, true, hSS, ryS, syS, sySS, 0.0, ghost_v(g, uS, 2, 0));
+                const double sv = slope_r(vS, vc, vSS, true, hSS, ryS, syS, sySS, 0.0, ghost_v(g, vS, 2, 1));
                 u1 = uS + hyS / 2 * su;
                 v1 = vS + hyS / 2 * sv;
             } else {
@@ -221,8 +247,8 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
             u1 = uc + hy / 2 * syu;
             v1 = vc + hy / 2 * syv;
             if (hN) {
-                const double su = slope1(uN, uNN, uc, hNN, true, hyN, hyNN, hy, ghost_v(g, uN, 3, 0), 0.0);
-                const double sv = slope1(vN, vNN, vc, hNN, true, hyN, hyNN, hy, ghost_v(g, vN, 3, 1), 0.0);
+                const double su = slope_r(uN, uNN, uc, hNN, true, ryN, syNN, syN, ghost_v(g, uN, 3, 0), 0.0);
+                const double sv = slope_r(vN, vNN, vc, hNN, true, ryN, syNN, syN, ghost_v(g, vN, 3, 1), 0.0);
                 u2 = uN - hyN / 2 * su;
                 v2 = vN - hyN / 2 * sv;
             } else {
@@ -232,10 +258,10 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
             C[7] = fnn(v1, v2);
             C[6] = fuv(u1, v1, u2, v2);
         }
-        double val = (C[2] - C[0]) / hx + (C[6] - C[4]) / hy;   // (:352-355)
+        double val = (C[2] - C[0]) * rx + (C[6] - C[4]) * ry;   // (:352-355)
         cu[(ptrdiff_t)li * ld + j] = val;
         ru_ += val * (-1.5 * dt);
-        val = (C[3] - C[1]) / hx + (C[7] - C[5]) / hy;          // (:356-359)
+        val = (C[3] - C[1]) * rx + (C[7] - C[5]) * ry;          // (:356-359)
         cv[(ptrdiff_t)li * ld + j] = val;
         rv_ += val * (-1.5 * dt);
 
@@ -640,10 +666,15 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
         const double alpha = a.alpha, omega = a.omega;
         const int rlo = -HALO, rhi = a.nxl + HALO - 1;
 
-        // one row of phi (row r) and of b (row r-1), per lane
+        // one row of phi (row r) and of b (row r-1), per lane.  Rows no stage reads -- phi
+        // past r1 (the prefetch overrun) and b before the first red / relaxed row -- are
+        // clamped onto a row this wave fetches anyway: a cache hit instead of an HBM row,
+        // with no branch in the load pipeline.
         double2 Q[SD], QB[SD];
+        const int r1 = RB ? ie + 1 : ie;
+        const int blo = max(RB ? ib - 1 : ib, rlo), phi_hi = min(r1, rhi);
         auto load = [&](int slot_r, double2& p, double2& bb) {
-            const int lp = min(max(slot_r, rlo), rhi), lb = min(max(slot_r - 1, rlo), rhi);
+            const int lp = min(max(slot_r, rlo), phi_hi), lb = min(max(slot_r - 1, blo), rhi);
             p = *reinterpret_cast<const double2*>(a.in + (ptrdiff_t)lp * ld + lc);
             bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
         };
@@ -705,7 +736,7 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
         };
 
         // rows ib-2 .. ie+1 (RB) / ib-1 .. ie (Jacobi); SD rows in flight
-        const int r0 = RB ? ib - 2 : ib - 1, r1 = RB ? ie + 1 : ie;
+        const int r0 = RB ? ib - 2 : ib - 1;
 #pragma unroll
         for (int q = 0; q < SD; q++) load(r0 + q, Q[q], QB[q]);
         for (int r = r0; r <= r1; r += SD) {
@@ -761,8 +792,12 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
         const int rlo = -HALO, rhi = a.nxl + HALO - 1;
 
         double2 Q[SD2], QB[SD2];
+        // phi rows ib-4 .. ie+3 and b rows ib-3 .. ie+2 (the first red stage's) are read;
+        // the rest are clamped onto fetched rows (see k_sweep)
+        const int r0 = ib - 4, r1 = ie + 3;
+        const int blo = max(ib - 3, rlo), phi_hi = min(r1, rhi);
         auto load = [&](int slot_r, double2& p, double2& bb) {
-            const int lp = min(max(slot_r, rlo), rhi), lb = min(max(slot_r - 1, rlo), rhi);
+            const int lp = min(max(slot_r, rlo), phi_hi), lb = min(max(slot_r - 1, blo), rhi);
             p = *reinterpret_cast<const double2*>(a.in + (ptrdiff_t)lp * ld + lc);
             bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
         };
@@ -831,7 +866,6 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
             }
         };
 
-        const int r0 = ib - 4, r1 = ie + 3;
 #pragma unroll
         for (int q = 0; q < SD2; q++) load(r0 + q, Q[q], QB[q]);
         for (int r = r0; r <= r1; r += SD2) {
@@ -914,42 +948,146 @@ __global__ __launch_bounds__(256) void k_prolong(Geo gf, double* __restrict__ ph
     phi[(ptrdiff_t)li * gf.ld + j] += e;
 }
 
-// coarsest level, whole grid resident in one workgroup's LDS: `iters` red-black SOR
-// sweeps in place (barrier between colours), phi starts at 0
-__global__ __launch_bounds__(1024) void k_coarse_lds(Geo g, Coef c, double* __restrict__ phi,
-                                                     const double* __restrict__ b, double omega, int iters) {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int nx = g.nx, ny = g.ny, n = nx * ny;
-    double* sp = lds;
-    double* sb = lds + n;
-    double* cw = sb + n;
-    double* ce = cw + nx;
-    double* cs = ce + nx;
-    double* cn = cs + ny;
-    for (int k = threadIdx.x; k < n; k += 1024) {
-        const int i = k / ny, j = k - i * ny;
-        sp[k] = ldf(phi, g.ld, i, j);
-        sb[k] = ldf(b, g.ld, i, j);
-    }
-    for (int k = threadIdx.x; k < nx; k += 1024) { cw[k] = c.pw[k]; ce[k] = c.pe[k]; }
-    for (int k = threadIdx.x; k < ny; k += 1024) { cs[k] = c.ps[k]; cn[k] = c.pn[k]; }
-    __syncthreads();
-    for (int it = 0; it < iters; it++)
+// ------------------------------------------------ K4 coarse levels: a whole V-cycle in LDS
+// Levels from the coarsest global one (<= 64 x 64) down to <= 4 x 4 live in one
+// workgroup's LDS; one launch runs `cycles` V-cycles over them (RB Gauss-Seidel
+// smoothing, the same area-weighted restriction / bilinear prolongation as
+// k_restrict / k_prolong, RB-SOR on the last level).  Replaces ~6 launches per level
+// that are pure launch latency at these sizes.  Single rank (the level is whole).
+constexpr int LV_MAX = 8;
+
+struct LdsLv {
+    int nx, ny, phi, b, cw, ce, cs, cn, hx, hy;  // offsets in doubles
+};
+
+__device__ __forceinline__ double lv_lap(const double* L, const LdsLv& v, int i, int j) {
+    const int ny = v.ny, k = i * ny + j;
+    const double* p = L + v.phi;
+    const double s = L[v.cw + i] * p[k - (i > 0 ? ny : 0)] + L[v.ce + i] * p[k + (i < v.nx - 1 ? ny : 0)] +
+                     L[v.cs + j] * p[k - (j > 0 ? 1 : 0)] + L[v.cn + j] * p[k + (j < ny - 1 ? 1 : 0)];
+    const double dg = -((L[v.cw + i] + L[v.ce + i]) + (L[v.cs + j] + L[v.cn + j]));
+    return s + dg * p[k];
+}
+
+__device__ __forceinline__ void lv_rb(double* L, const LdsLv& v, double omega, int sweeps) {
+    for (int s = 0; s < sweeps; s++)
         for (int color = 0; color < 2; color++) {
-            for (int k = threadIdx.x; k < n; k += 1024) {
-                const int i = k / ny, j = k - i * ny;
-                if (((i + j) & 1) != color) continue;
-                const double q = sp[k];
-                const double s = cw[i] * sp[k - (i > 0 ? ny : 0)] + ce[i] * sp[k + (i < nx - 1 ? ny : 0)] +
-                                 cs[j] * sp[k - (j > 0 ? 1 : 0)] + cn[j] * sp[k + (j < ny - 1 ? 1 : 0)];
-                const double dg = -((cw[i] + ce[i]) + (cs[j] + cn[j]));
-                sp[k] = q + omega * (sb[k] - (s + dg * q)) / dg;
+            const bool even = (v.ny & 1) == 0;
+            const int cnt = even ? v.nx * v.ny / 2 : v.nx * v.ny;
+            for (int t = threadIdx.x; t < cnt; t += blockDim.x) {
+                // even ny: the t-th cell of this colour in row-major order; odd ny (last
+                // level only): every cell, filtered by colour
+                const int k = even ? 2 * t : t;
+                int i = k / v.ny, j = k - i * v.ny;
+                if (even) j += ((i + j + color) & 1);
+                else if ((i + j + color) & 1) continue;
+                const int c = i * v.ny + j;
+                const double dg = -((L[v.cw + i] + L[v.ce + i]) + (L[v.cs + j] + L[v.cn + j]));
+                const double r = L[v.b + c] - lv_lap(L, v, i, j);
+                L[v.phi + c] += omega * r / dg;
             }
             __syncthreads();
         }
-    for (int k = threadIdx.x; k < n; k += 1024) {
-        const int i = k / ny, j = k - i * ny;
-        phi[(ptrdiff_t)i * g.ld + j] = sp[k];
+}
+
+__global__ __launch_bounds__(256) void k_coarse_vcycle(Geo g, Coef c, double* __restrict__ phi,
+                                                       const double* __restrict__ b, int cycles, int pre, int post,
+                                                       int citers, double comega) {
+    extern __shared__ __attribute__((aligned(16))) double L[];
+    __shared__ LdsLv lv[LV_MAX];
+    __shared__ int nlev;
+    if (threadIdx.x == 0) {
+        int off = 0, nx = g.nx, ny = g.ny, k = 0;
+        for (;;) {
+            LdsLv& v = lv[k];
+            v.nx = nx; v.ny = ny;
+            v.phi = off; off += nx * ny;
+            v.b = off; off += nx * ny;
+            v.cw = off; off += nx; v.ce = off; off += nx; v.hx = off; off += nx;
+            v.cs = off; off += ny; v.cn = off; off += ny; v.hy = off; off += ny;
+            off = (off + 1) & ~1;
+            k++;
+            if (k == LV_MAX || !mg_can_coarsen(nx, ny)) break;
+            nx /= 2; ny /= 2;
+        }
+        nlev = k;
+    }
+    __syncthreads();
+    const int nl = nlev;
+    // level 0: the global coarsest level's phi, b and spacings
+    {
+        const LdsLv v = lv[0];
+        for (int t = threadIdx.x; t < v.nx * v.ny; t += blockDim.x) {
+            const int i = t / v.ny, j = t - i * v.ny;
+            L[v.phi + t] = ldf(phi, g.ld, i, j);
+            L[v.b + t] = ldf(b, g.ld, i, j);
+        }
+        for (int t = threadIdx.x; t < v.nx; t += blockDim.x) L[v.hx + t] = c.hx[t];
+        for (int t = threadIdx.x; t < v.ny; t += blockDim.x) L[v.hy + t] = c.hy[t];
+    }
+    __syncthreads();
+    // coarser spacings (sums of children) and every level's ConstructLHS weights
+    for (int k = 0; k < nl; k++) {
+        const LdsLv v = lv[k];
+        if (k > 0) {
+            const LdsLv f = lv[k - 1];
+            for (int t = threadIdx.x; t < v.nx; t += blockDim.x) L[v.hx + t] = L[f.hx + 2 * t] + L[f.hx + 2 * t + 1];
+            for (int t = threadIdx.x; t < v.ny; t += blockDim.x) L[v.hy + t] = L[f.hy + 2 * t] + L[f.hy + 2 * t + 1];
+            __syncthreads();
+        }
+        for (int t = threadIdx.x; t < v.nx; t += blockDim.x) {
+            const double h = L[v.hx + t];
+            L[v.cw + t] = t > 0 ? 2.0 / (h * (h + L[v.hx + t - 1])) : 0.0;
+            L[v.ce + t] = t < v.nx - 1 ? 2.0 / (h * (h + L[v.hx + t + 1])) : 0.0;
+        }
+        for (int t = threadIdx.x; t < v.ny; t += blockDim.x) {
+            const double h = L[v.hy + t];
+            L[v.cs + t] = t > 0 ? 2.0 / (h * (h + L[v.hy + t - 1])) : 0.0;
+            L[v.cn + t] = t < v.ny - 1 ? 2.0 / (h * (h + L[v.hy + t + 1])) : 0.0;
+        }
+        __syncthreads();
+    }
+    for (int cyc = 0; cyc < cycles; cyc++) {
+        for (int k = 0; k < nl - 1; k++) {
+            const LdsLv f = lv[k], v = lv[k + 1];
+            lv_rb(L, f, 1.0, pre);
+            for (int t = threadIdx.x; t < v.nx * v.ny; t += blockDim.x) {
+                const int I = t / v.ny, J = t - I * v.ny;
+                double sum = 0.0;
+                for (int a = 0; a < 2; a++)
+                    for (int q = 0; q < 2; q++) {
+                        const int i = 2 * I + a, j = 2 * J + q;
+                        const double r = L[f.b + i * f.ny + j] - lv_lap(L, f, i, j);
+                        sum += (L[f.hx + i] * L[f.hy + j]) * r;
+                    }
+                L[v.b + t] = sum / (L[v.hx + I] * L[v.hy + J]);
+                L[v.phi + t] = 0.0;
+            }
+            __syncthreads();
+        }
+        lv_rb(L, lv[nl - 1], comega, citers);
+        for (int k = nl - 2; k >= 0; k--) {
+            const LdsLv f = lv[k], v = lv[k + 1];
+            for (int t = threadIdx.x; t < f.nx * f.ny; t += blockDim.x) {
+                const int i = t / f.ny, j = t - i * f.ny;
+                const int I = i >> 1, J = j >> 1;
+                int In = (i & 1) ? I + 1 : I - 1, Jn = (j & 1) ? J + 1 : J - 1;
+                if (In < 0 || In >= v.nx) In = I;
+                if (Jn < 0 || Jn >= v.ny) Jn = J;
+                const double* e = L + v.phi;
+                L[f.phi + t] += (9.0 * e[I * v.ny + J] + 3.0 * e[In * v.ny + J] + 3.0 * e[I * v.ny + Jn] +
+                                 e[In * v.ny + Jn]) * 0.0625;
+            }
+            __syncthreads();
+            lv_rb(L, f, 1.0, post);
+        }
+    }
+    {
+        const LdsLv v = lv[0];
+        for (int t = threadIdx.x; t < v.nx * v.ny; t += blockDim.x) {
+            const int i = t / v.ny, j = t - i * v.ny;
+            phi[(ptrdiff_t)i * g.ld + j] = L[v.phi + t];
+        }
     }
 }
 
@@ -1076,13 +1214,33 @@ static SweepArgs make_args(const Geo& g, const Coef& c, int TI, int TJ) {
 static int g_strip_rows = 0;  // 0 = adaptive
 void set_strip_rows(int L) { g_strip_rows = L >= 4 ? (std::min(L, 64) & ~1) : 0; }
 
-// rows per strip (measured, tools/sweep_levels.py): 16 while that still gives >= 2048
-// waves (4096^2, 2048^2), else 4 -- coarse multigrid levels are latency-bound and need
-// every wave they can get
-static int strip_rows(const Geo& g) {
+// waves of kernel `k` (256-thread workgroups) the whole chip holds at once
+static long resident_waves(const void* k) {
+    static std::mutex mu;
+    static std::map<const void*, long> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(k);
+    if (it != cache.end()) return it->second;
+    int nb = 0, dev = 0, cus = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const long cap = std::max(1L, (long)nb * 4 * cus);
+    cache[k] = cap;
+    if (getenv("NSGPU_VERBOSE")) fprintf(stderr, "nsgpu: %p holds %d blocks/CU x %d CUs\n", k, nb, cus);
+    return cap;
+}
+
+// rows per strip: the fewest rows (re-read halo rows cost (rows + halo) / rows of the
+// traffic) such that every strip is resident in ONE round -- a second, partial round of
+// the same length runs with the chip mostly idle.  lmin: below it the halo re-reads
+// dominate (coarse multigrid levels are latency-bound and want short strips).
+static int strip_rows(int nxl, long nsj, long cap, int lmin) {
     if (g_strip_rows) return g_strip_rows;
-    const long nsj = (g.ny + SW - 1) / SW;
-    return nsj * ((g.nxl + 15) / 16) >= 2048 ? 16 : 4;
+    const long nsi = std::max(1L, cap / nsj);
+    int L = (int)((nxl + nsi - 1) / nsi);
+    L = (L + 1) & ~1;
+    return std::min(std::max(L, lmin), 64);
 }
 
 static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, double* out, const double* b,
@@ -1093,15 +1251,16 @@ static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, dou
     (void)helm;
     a.alpha = alpha; a.omega = omega;
     a.nx = g.nx; a.ny = g.ny; a.i0 = g.i0; a.nxl = g.nxl; a.ld = g.ld;
-    a.L = strip_rows(g);
     a.nsj = (g.ny + SW - 1) / SW;
-    a.nsi = (g.nxl + a.L - 1) / a.L;
     a.part = part;
     return a;
 }
 
 template <int OP, bool RB>
-static int launch_stream(const StreamArgs& a, hipStream_t st) {
+static int launch_stream(StreamArgs a, hipStream_t st) {
+    const long cap = resident_waves(a.part ? (const void*)k_sweep<OP, RB, true> : (const void*)k_sweep<OP, RB, false>);
+    a.L = strip_rows(a.nxl, a.nsj, cap, 4);
+    a.nsi = (a.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
     if (a.part) hipLaunchKernelGGL((k_sweep<OP, RB, true>), dim3(nblk), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_sweep<OP, RB, false>), dim3(nblk), dim3(256), 0, st, a);
@@ -1113,12 +1272,12 @@ int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* p
     return launch_stream<0, true>(stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false), st);
 }
 
-// two fused red-black sweeps: strips of 120 written columns; 32 rows per strip while that
-// still gives >= 2048 waves (fewer re-read rows: ib-4 .. ie+3), else 8
+// two fused red-black sweeps: strips of 120 written columns reading rows ib-4 .. ie+3
 template <int OP>
 static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st) {
     a.nsj = (g.ny + SW2 - 1) / SW2;
-    a.L = g_strip_rows ? g_strip_rows : (a.nsj * ((g.nxl + 31) / 32) >= 2048 ? 32 : 8);
+    const long cap = resident_waves(a.part ? (const void*)k_sweep2<OP, true> : (const void*)k_sweep2<OP, false>);
+    a.L = strip_rows(a.nxl, a.nsj, cap, 16);
     a.nsi = (g.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
     if (a.part) hipLaunchKernelGGL((k_sweep2<OP, true>), dim3(nblk), dim3(256), 0, st, a);
@@ -1199,18 +1358,28 @@ void launch_prolong(const Geo& gf, double* phi, const Geo& gc, const double* ec,
     hipLaunchKernelGGL(k_prolong, cell_grid(gf), dim3(64, 4), 0, st, gf, phi, gc, ec);
 }
 
-size_t coarse_lds_bytes(const Geo& g) { return sizeof(double) * (2 * (size_t)g.nx * g.ny + 2 * g.nx + 2 * g.ny); }
+size_t coarse_vcycle_bytes(const Geo& g) {
+    size_t off = 0;
+    int nx = g.nx, ny = g.ny;
+    for (int k = 0; k < LV_MAX; k++) {
+        off += 2 * (size_t)nx * ny + 3 * (size_t)nx + 3 * (size_t)ny;
+        off = (off + 1) & ~(size_t)1;
+        if (!mg_can_coarsen(nx, ny)) break;
+        nx /= 2; ny /= 2;
+    }
+    return off * sizeof(double);
+}
 
-int launch_coarse_lds(const Geo& g, const Coef& c, double* phi, const double* b, double omega, int iters,
-                      hipStream_t st) {
-    const size_t bytes = coarse_lds_bytes(g);
-    if (bytes > 160 * 1024 || g.nxl != g.nx) return -1;
+int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double* b, int cycles, int pre, int post,
+                         int citers, double comega, hipStream_t st) {
+    const size_t bytes = coarse_vcycle_bytes(g);
+    if (bytes > 150 * 1024 || g.nxl != g.nx) return -1;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_coarse_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_coarse_vcycle, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k_coarse_lds, dim3(1), dim3(1024), bytes, st, g, c, phi, b, omega, iters);
+    hipLaunchKernelGGL(k_coarse_vcycle, dim3(1), dim3(256), bytes, st, g, c, phi, b, cycles, pre, post, citers, comega);
     return 0;
 }
 

@@ -376,7 +376,11 @@ MgLevel& level(ns_solver* s, int l) {
 int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
     MgLevel& L = level(s, l);
     for (int k = 0; k < n;) {
-        const int w = (n - k >= 2 && !s->tiled) ? 2 : 1;   // two sweeps per HBM pass where possible
+        // two sweeps per HBM pass on the HBM-bound levels (>= 2048^2 local cells); the coarser
+        // ones are latency-bound and the fused pass's deeper row pipeline only costs there
+        // (tools/sweep_levels2.py: 512^2 9.5 us/sweep fused vs 8.1 single)
+        const bool big = (long)L.g.nxl * L.g.ny >= 2048L * 2048L;
+        const int w = (n - k >= 2 && !s->tiled && big) ? 2 : 1;
         CHK(halo_g(s, L.g, {L.phi}, 2 * w));
         const bool t = s->timing && l == 0;
         if (t) HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st));
@@ -394,8 +398,9 @@ int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
 int mg_coarse(ns_solver* s) {
     MgLevel& L = level(s, (int)s->lv.size() - 1);
     if (s->mg_coarse_lds) {
-        if (nsg::launch_coarse_lds(L.g, L.c, L.phi, L.b, s->mg_omega_c, s->mg_coarse_iters, s->st) != 0) {
-            set_err("coarse LDS solve does not fit");
+        if (nsg::launch_coarse_vcycle(L.g, L.c, L.phi, L.b, 1, s->mg_pre, s->mg_post, s->mg_coarse_iters,
+                                      s->mg_omega_c, s->st) != 0) {
+            set_err("coarse LDS V-cycle does not fit");
             return NS_EINVAL;
         }
         return 0;
@@ -470,9 +475,14 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
 // coefficient tables of one level: [pw pe bx | ps pn by | hx hy]  (ConstructLHS, FluidSolver.cpp:113-131)
 std::vector<double> coef_tables(const std::vector<double>& hx, const std::vector<double>& hy) {
     const int nx = (int)hx.size(), ny = (int)hy.size();
-    std::vector<double> h(4 * (size_t)nx + 4 * (size_t)ny, 0.0);
+    std::vector<double> h(6 * (size_t)nx + 6 * (size_t)ny + 2, 0.0);
     double *pw = h.data(), *pe = pw + nx, *bx = pe + nx, *ps = bx + nx, *pn = ps + ny, *by = pn + ny;
     double *hxo = by + ny, *hyo = hxo + nx;
+    double *rhx = hyo + ny, *rhy = rhx + nx, *rsx = rhy + ny, *rsy = rsx + nx + 1;
+    for (int i = 0; i < nx; i++) rhx[i] = 1.0 / hx[i];
+    for (int j = 0; j < ny; j++) rhy[j] = 1.0 / hy[j];
+    for (int i = 1; i < nx; i++) rsx[i] = 2.0 / (hx[i - 1] + hx[i]);
+    for (int j = 1; j < ny; j++) rsy[j] = 2.0 / (hy[j - 1] + hy[j]);
     for (int i = 0; i < nx; i++) {
         const double a = hx[i];
         hxo[i] = a;
@@ -495,6 +505,8 @@ nsg::Coef coef_view(double* d, int nx, int ny) {
     c.pw = d; c.pe = d + nx; c.bx = d + 2 * nx;
     c.ps = d + 3 * nx; c.pn = d + 3 * nx + ny; c.by = d + 3 * nx + 2 * ny;
     c.hx = d + 3 * nx + 3 * ny; c.hy = d + 4 * nx + 3 * ny;
+    c.rhx = d + 4 * nx + 4 * ny; c.rhy = d + 5 * nx + 4 * ny;
+    c.rsx = d + 5 * nx + 5 * ny; c.rsy = d + 6 * nx + 5 * ny + 1;
     return c;
 }
 
@@ -507,16 +519,15 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
     L0.hx = hx0;
     L0.hy = hy0;
     s->lv.push_back(L0);
-    const size_t lds_cap = 24 * 1024;   // coarsest <= ~32 x 32: the single-workgroup solve stays ~10 us
+    const size_t lds_cap = 150 * 1024;  // single rank: stop at the first level whose LDS V-cycle fits (<= ~64^2)
     for (;;) {
         const MgLevel& F = s->lv.back();
         const nsg::Geo& gf = F.g;
-        if (s->nranks == 1 && s->lv.size() > 1 && nsg::coarse_lds_bytes(gf) <= lds_cap) break;
-        if (gf.nx % 2 || gf.ny % 2 || gf.nxl % 2 || gf.i0 % 2) break;
+        if (s->nranks == 1 && s->lv.size() > 1 && nsg::coarse_vcycle_bytes(gf) <= lds_cap) break;
+        if (!nsg::mg_can_coarsen(gf.nx, gf.ny) || gf.nxl % 2 || gf.i0 % 2) break;
         nsg::Geo gc = gf;
         gc.nx /= 2; gc.ny /= 2; gc.i0 /= 2; gc.nxl /= 2;
         gc.ld = (gc.ny + 127) / 128 * 128;
-        if (gc.nx < 2 || gc.ny < 2) break;
         if (s->nranks > 1 && gc.nxl < 4) break;
         MgLevel C;
         C.g = gc;
@@ -537,11 +548,16 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
         s->lv.push_back(C);
     }
     const nsg::Geo& gc = s->lv.back().g;
-    const int nc = std::max(gc.nx, gc.ny);
+    s->mg_coarse_lds = s->nranks == 1 && s->lv.size() > 1 && nsg::coarse_vcycle_bytes(gc) <= lds_cap;
+    // coarsest relaxation: on the last LDS level (<= 4x4 after the in-LDS coarsening) when the
+    // LDS V-cycle is used, else on gc itself by distributed sweeps
+    int ncx = gc.nx, ncy = gc.ny;
+    if (s->mg_coarse_lds)
+        while (nsg::mg_can_coarsen(ncx, ncy)) { ncx /= 2; ncy /= 2; }
+    const int nc = std::max(ncx, ncy);
     const double pi = 3.14159265358979323846;
     s->mg_omega_c = 2.0 / (1.0 + std::sin(pi / nc));
     s->mg_coarse_iters = 2 * nc + 10;
-    s->mg_coarse_lds = s->nranks == 1 && s->lv.size() > 1 && nsg::coarse_lds_bytes(gc) <= lds_cap;
     return 0;
 }
 

@@ -886,9 +886,9 @@ static mg_level* mg_build(int nx, int ny, const double* hx, const double* hy, in
         l->x = calloc((size_t)nx * ny, sizeof(double));
         l->b = calloc((size_t)nx * ny, sizeof(double));
         n++;
-        /* same rule as the GPU hierarchy: stop at <= 32 x 32 once coarsened, or at odd sizes */
-        const size_t lds = sizeof(double) * (2 * (size_t)nx * ny + 2 * nx + 2 * ny);
-        if ((n > 1 && lds <= 24 * 1024) || nx % 2 || ny % 2 || nx / 2 < 2 || ny / 2 < 2 || n == cap) break;
+        /* same rule as the GPU hierarchy (global levels + the LDS V-cycle, mg_can_coarsen in
+         * ns_internal.h): halve while both sizes are even, >= 4, and the level has > 16 cells */
+        if (nx % 2 || ny % 2 || nx < 4 || ny < 4 || nx * ny <= 16 || n == cap) break;
         nx /= 2; ny /= 2;
     }
     *nlev = n;

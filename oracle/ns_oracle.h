@@ -106,8 +106,8 @@ void og_mg_restrict(int nx, int ny, const double* hx, const double* hy, const do
 /* phi (nx x ny) += bilinear prolongation of the coarse correction ec (nx/2 x ny/2) */
 void og_mg_prolong(int nx, int ny, const double* ec, double* phi);
 /* V-cycle solve of L x = rhs - mean(rhs) (rhs is mean-removed in place): RB Gauss-Seidel
- * smoothing (pre/post sweeps), coarsening while both sizes are even down to <= 32 x 32,
- * coarsest level by red-black SOR; stops when the residual after pre-smoothing is
+ * smoothing (pre/post sweeps), coarsening while both sizes are even, >= 4 and > 16 cells,
+ * coarsest level by red-black SOR (2n+10 iterations at the optimal omega); stops when the residual after pre-smoothing is
  * <= rtol * ||rhs||.  Returns V-cycles. */
 int og_mg_solve(const og_grid* g, double* rhs, double* x, double rtol, int pre, int post, int maxcycles);
 
