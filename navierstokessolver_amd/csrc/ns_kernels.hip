@@ -148,11 +148,11 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
                                              const double* __restrict__ v, const double* __restrict__ phi,
                                              double* __restrict__ cu, double* __restrict__ cv,
                                              double* __restrict__ ru, double* __restrict__ rv,
-                                             double* __restrict__ part) {
+                                             double* __restrict__ part, int rows) {
     const int j = blockIdx.x * 64 + threadIdx.x;
-    const int li = blockIdx.y * 4 + threadIdx.y;
+    const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
     double acc[2] = {0.0, 0.0};
-    if (j < g.ny && li < g.nxl) {
+    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
         const int gi = g.i0 + li, ld = g.ld, nx = g.nx, ny = g.ny;
         const bool hW = gi > 0, hWW = gi > 1, hE = gi < nx - 1, hEE = gi < nx - 2;
         const bool hS = j > 0, hSS = j > 1, hN = j < ny - 1, hNN = j < ny - 2;
@@ -311,8 +311,8 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
         }
         ru[(ptrdiff_t)li * ld + j] = ru_;
         rv[(ptrdiff_t)li * ld + j] = rv_;
-        acc[0] = ru_ * ru_;
-        acc[1] = rv_ * rv_;
+        acc[0] += ru_ * ru_;
+        acc[1] += rv_ * rv_;
     }
     block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
 }
@@ -322,11 +322,11 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
 // block partials of (sum rhs, sum rhs^2) for the null-space mean (:550) and ||b||.
 __global__ __launch_bounds__(256) void k_div(Geo g, Coef c, double dt, const double* __restrict__ u,
                                              const double* __restrict__ v, double* __restrict__ rp,
-                                             double* __restrict__ part) {
+                                             double* __restrict__ part, int rows) {
     const int j = blockIdx.x * 64 + threadIdx.x;
-    const int li = blockIdx.y * 4 + threadIdx.y;
+    const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
     double acc[2] = {0.0, 0.0};
-    if (j < g.ny && li < g.nxl) {
+    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
         const int gi = g.i0 + li, ld = g.ld;
         const double uc = ldf(u, ld, li, j), vc = ldf(v, ld, li, j);
         const double hx = c.hx[gi], hy = c.hy[j];
@@ -341,8 +341,8 @@ __global__ __launch_bounds__(256) void k_div(Geo g, Coef c, double dt, const dou
         else V3 = 0.5 * (vc + ghost_v(g, vc, 3, 1));
         const double val = ((V1 - V0) / hx + (V3 - V2) / hy) / dt;
         rp[(ptrdiff_t)li * ld + j] = val;
-        acc[0] = val;
-        acc[1] = val * val;
+        acc[0] += val;
+        acc[1] += val * val;
     }
     block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
 }
@@ -353,11 +353,11 @@ __global__ __launch_bounds__(256) void k_div(Geo g, Coef c, double dt, const dou
 __global__ __launch_bounds__(256) void k_correct(Geo g, Coef c, double dt, const double* __restrict__ us,
                                                  const double* __restrict__ vs, double* __restrict__ u,
                                                  double* __restrict__ v, const double* __restrict__ phi,
-                                                 double* __restrict__ part) {
+                                                 double* __restrict__ part, int rows) {
     const int j = blockIdx.x * 64 + threadIdx.x;
-    const int li = blockIdx.y * 4 + threadIdx.y;
+    const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
     double acc[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
-    if (j < g.ny && li < g.nxl) {
+    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
         double gx, gy;
         grad_phi(g, c, phi, li, j, gx, gy);
         const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
@@ -365,10 +365,10 @@ __global__ __launch_bounds__(256) void k_correct(Geo g, Coef c, double dt, const
         u[o] = un;
         v[o] = vn;
         // NaN-propagating min so a blown-up step is visible in the stats
-        acc[0] = un != un ? -INFINITY : un;
-        acc[1] = un != un ? -INFINITY : -un;
-        acc[2] = vn != vn ? -INFINITY : vn;
-        acc[3] = vn != vn ? -INFINITY : -vn;
+        acc[0] = fmin(acc[0], un != un ? -INFINITY : un);
+        acc[1] = fmin(acc[1], un != un ? -INFINITY : -un);
+        acc[2] = fmin(acc[2], vn != vn ? -INFINITY : vn);
+        acc[3] = fmin(acc[3], vn != vn ? -INFINITY : -vn);
     }
     block_reduce_min<4>(acc, part + 4 * (blockIdx.x + gridDim.x * blockIdx.y));
 }
@@ -908,11 +908,11 @@ __device__ __forceinline__ double pois_residual(const Geo& g, const Coef& c, con
 __global__ __launch_bounds__(256) void k_restrict(Geo gf, Coef cf, const double* __restrict__ phi,
                                                   const double* __restrict__ b, const double* __restrict__ shiftp,
                                                   Geo gc, Coef cc, double* __restrict__ bc, double* __restrict__ pc,
-                                                  double* __restrict__ part) {
+                                                  double* __restrict__ part, int rows) {
     const int J = blockIdx.x * 64 + threadIdx.x;
-    const int I = blockIdx.y * 4 + threadIdx.y;
+    const int Iend = min((int)(blockIdx.y + 1) * 4 * rows, gc.nxl);
     double acc[1] = {0.0};
-    if (J < gc.ny && I < gc.nxl) {
+    for (int I = blockIdx.y * 4 * rows + threadIdx.y; I < Iend && J < gc.ny; I += 4) {
         const double shift = shiftp ? shiftp[0] : 0.0;
         double sum = 0.0;
 #pragma unroll
@@ -933,10 +933,11 @@ __global__ __launch_bounds__(256) void k_restrict(Geo gf, Coef cf, const double*
 
 // fine phi += bilinear interpolation of the coarse correction
 __global__ __launch_bounds__(256) void k_prolong(Geo gf, double* __restrict__ phi, Geo gc,
-                                                 const double* __restrict__ ec) {
+                                                 const double* __restrict__ ec, int rows) {
     const int j = blockIdx.x * 64 + threadIdx.x;
-    const int li = blockIdx.y * 4 + threadIdx.y;
-    if (j >= gf.ny || li >= gf.nxl) return;
+    const int lend = min((int)(blockIdx.y + 1) * 4 * rows, gf.nxl);
+    if (j >= gf.ny) return;
+    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend; li += 4) {
     const int I = li >> 1, Jc = j >> 1;
     const int In = (li & 1) ? I + 1 : I - 1;        // coarse row on this child's side
     const int Jn = (j & 1) ? Jc + 1 : Jc - 1;
@@ -946,6 +947,7 @@ __global__ __launch_bounds__(256) void k_prolong(Geo gf, double* __restrict__ ph
     const double e = (9.0 * ldf(ec, gc.ld, I, Jc) + 3.0 * ldf(ec, gc.ld, Iu, Jc) + 3.0 * ldf(ec, gc.ld, I, Ju) +
                       ldf(ec, gc.ld, Iu, Ju)) * 0.0625;
     phi[(ptrdiff_t)li * gf.ld + j] += e;
+    }
 }
 
 // ------------------------------------------------ K4 coarse levels: a whole V-cycle in LDS
@@ -955,10 +957,20 @@ __global__ __launch_bounds__(256) void k_prolong(Geo gf, double* __restrict__ ph
 // k_restrict / k_prolong, RB-SOR on the last level).  Replaces ~6 launches per level
 // that are pure launch latency at these sizes.  Single rank (the level is whole).
 constexpr int LV_MAX = 8;
+constexpr int CV_THREADS = 1024;
 
 struct LdsLv {
-    int nx, ny, phi, b, cw, ce, cs, cn, hx, hy;  // offsets in doubles
+    int nx, ny, phi, b, idg, cw, ce, cs, cn, hx, hy;  // offsets in doubles
+    float rny;                                          // 1/ny for the index split
 };
+
+// k -> (k / ny, k % ny) without an integer division: float estimate + one correction
+__device__ __forceinline__ void lv_split(const LdsLv& v, int k, int& i, int& j) {
+    i = __float2int_rz(__int2float_rn(k) * v.rny);
+    j = k - i * v.ny;
+    if (j < 0) { i--; j += v.ny; }
+    else if (j >= v.ny) { i++; j -= v.ny; }
+}
 
 __device__ __forceinline__ double lv_lap(const double* L, const LdsLv& v, int i, int j) {
     const int ny = v.ny, k = i * ny + j;
@@ -970,91 +982,106 @@ __device__ __forceinline__ double lv_lap(const double* L, const LdsLv& v, int i,
 }
 
 __device__ __forceinline__ void lv_rb(double* L, const LdsLv& v, double omega, int sweeps) {
+    const bool even = (v.ny & 1) == 0;
+    const int cnt = even ? v.nx * v.ny / 2 : v.nx * v.ny;
     for (int s = 0; s < sweeps; s++)
         for (int color = 0; color < 2; color++) {
-            const bool even = (v.ny & 1) == 0;
-            const int cnt = even ? v.nx * v.ny / 2 : v.nx * v.ny;
-            for (int t = threadIdx.x; t < cnt; t += blockDim.x) {
+            for (int t = threadIdx.x; t < cnt; t += CV_THREADS) {
                 // even ny: the t-th cell of this colour in row-major order; odd ny (last
                 // level only): every cell, filtered by colour
-                const int k = even ? 2 * t : t;
-                int i = k / v.ny, j = k - i * v.ny;
+                int i, j;
+                lv_split(v, even ? 2 * t : t, i, j);
                 if (even) j += ((i + j + color) & 1);
                 else if ((i + j + color) & 1) continue;
                 const int c = i * v.ny + j;
-                const double dg = -((L[v.cw + i] + L[v.ce + i]) + (L[v.cs + j] + L[v.cn + j]));
                 const double r = L[v.b + c] - lv_lap(L, v, i, j);
-                L[v.phi + c] += omega * r / dg;
+                L[v.phi + c] += omega * r * L[v.idg + c];
             }
             __syncthreads();
         }
 }
 
-__global__ __launch_bounds__(256) void k_coarse_vcycle(Geo g, Coef c, double* __restrict__ phi,
-                                                       const double* __restrict__ b, int cycles, int pre, int post,
-                                                       int citers, double comega) {
+// LDS footprint (doubles) of the levels from (nx, ny) down; fills lv when non-null
+__host__ __device__ inline int lv_layout(int nx, int ny, LdsLv* lv, int* nlev) {
+    int off = 0, k = 0;
+    for (;;) {
+        if (lv) {
+            LdsLv& v = lv[k];
+            v.nx = nx; v.ny = ny; v.rny = 1.0f / (float)ny;
+            v.phi = off; v.b = off + nx * ny; v.idg = off + 2 * nx * ny;
+            v.cw = off + 3 * nx * ny; v.ce = v.cw + nx; v.hx = v.ce + nx;
+            v.cs = v.hx + nx; v.cn = v.cs + ny; v.hy = v.cn + ny;
+        }
+        off += 3 * nx * ny + 3 * nx + 3 * ny;
+        off = (off + 1) & ~1;
+        k++;
+        if (k == LV_MAX || !mg_can_coarsen(nx, ny)) break;
+        nx /= 2; ny /= 2;
+    }
+    if (nlev) *nlev = k;
+    return off;
+}
+
+__global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, double* __restrict__ phi,
+                                                              const double* __restrict__ b, int cycles, int pre,
+                                                              int post, int citers, double comega) {
     extern __shared__ __attribute__((aligned(16))) double L[];
     __shared__ LdsLv lv[LV_MAX];
     __shared__ int nlev;
-    if (threadIdx.x == 0) {
-        int off = 0, nx = g.nx, ny = g.ny, k = 0;
-        for (;;) {
-            LdsLv& v = lv[k];
-            v.nx = nx; v.ny = ny;
-            v.phi = off; off += nx * ny;
-            v.b = off; off += nx * ny;
-            v.cw = off; off += nx; v.ce = off; off += nx; v.hx = off; off += nx;
-            v.cs = off; off += ny; v.cn = off; off += ny; v.hy = off; off += ny;
-            off = (off + 1) & ~1;
-            k++;
-            if (k == LV_MAX || !mg_can_coarsen(nx, ny)) break;
-            nx /= 2; ny /= 2;
-        }
-        nlev = k;
-    }
+    if (threadIdx.x == 0) lv_layout(g.nx, g.ny, lv, &nlev);
     __syncthreads();
     const int nl = nlev;
     // level 0: the global coarsest level's phi, b and spacings
     {
         const LdsLv v = lv[0];
-        for (int t = threadIdx.x; t < v.nx * v.ny; t += blockDim.x) {
-            const int i = t / v.ny, j = t - i * v.ny;
+        for (int t = threadIdx.x; t < v.nx * v.ny; t += CV_THREADS) {
+            int i, j;
+            lv_split(v, t, i, j);
             L[v.phi + t] = ldf(phi, g.ld, i, j);
             L[v.b + t] = ldf(b, g.ld, i, j);
         }
-        for (int t = threadIdx.x; t < v.nx; t += blockDim.x) L[v.hx + t] = c.hx[t];
-        for (int t = threadIdx.x; t < v.ny; t += blockDim.x) L[v.hy + t] = c.hy[t];
+        for (int t = threadIdx.x; t < v.nx; t += CV_THREADS) L[v.hx + t] = c.hx[t];
+        for (int t = threadIdx.x; t < v.ny; t += CV_THREADS) L[v.hy + t] = c.hy[t];
     }
     __syncthreads();
-    // coarser spacings (sums of children) and every level's ConstructLHS weights
+    // coarser spacings (sums of children), every level's ConstructLHS weights and 1/diag
     for (int k = 0; k < nl; k++) {
         const LdsLv v = lv[k];
         if (k > 0) {
             const LdsLv f = lv[k - 1];
-            for (int t = threadIdx.x; t < v.nx; t += blockDim.x) L[v.hx + t] = L[f.hx + 2 * t] + L[f.hx + 2 * t + 1];
-            for (int t = threadIdx.x; t < v.ny; t += blockDim.x) L[v.hy + t] = L[f.hy + 2 * t] + L[f.hy + 2 * t + 1];
+            for (int t = threadIdx.x; t < v.nx; t += CV_THREADS) L[v.hx + t] = L[f.hx + 2 * t] + L[f.hx + 2 * t + 1];
+            for (int t = threadIdx.x; t < v.ny; t += CV_THREADS) L[v.hy + t] = L[f.hy + 2 * t] + L[f.hy + 2 * t + 1];
             __syncthreads();
         }
-        for (int t = threadIdx.x; t < v.nx; t += blockDim.x) {
+        for (int t = threadIdx.x; t < v.nx; t += CV_THREADS) {
             const double h = L[v.hx + t];
             L[v.cw + t] = t > 0 ? 2.0 / (h * (h + L[v.hx + t - 1])) : 0.0;
             L[v.ce + t] = t < v.nx - 1 ? 2.0 / (h * (h + L[v.hx + t + 1])) : 0.0;
         }
-        for (int t = threadIdx.x; t < v.ny; t += blockDim.x) {
+        for (int t = threadIdx.x; t < v.ny; t += CV_THREADS) {
             const double h = L[v.hy + t];
             L[v.cs + t] = t > 0 ? 2.0 / (h * (h + L[v.hy + t - 1])) : 0.0;
             L[v.cn + t] = t < v.ny - 1 ? 2.0 / (h * (h + L[v.hy + t + 1])) : 0.0;
         }
         __syncthreads();
+        for (int t = threadIdx.x; t < v.nx * v.ny; t += CV_THREADS) {
+            int i, j;
+            lv_split(v, t, i, j);
+            L[v.idg + t] = -1.0 / ((L[v.cw + i] + L[v.ce + i]) + (L[v.cs + j] + L[v.cn + j]));
+        }
     }
+    __syncthreads();
     for (int cyc = 0; cyc < cycles; cyc++) {
         for (int k = 0; k < nl - 1; k++) {
             const LdsLv f = lv[k], v = lv[k + 1];
             lv_rb(L, f, 1.0, pre);
-            for (int t = threadIdx.x; t < v.nx * v.ny; t += blockDim.x) {
-                const int I = t / v.ny, J = t - I * v.ny;
+            for (int t = threadIdx.x; t < v.nx * v.ny; t += CV_THREADS) {
+                int I, J;
+                lv_split(v, t, I, J);
                 double sum = 0.0;
+#pragma unroll
                 for (int a = 0; a < 2; a++)
+#pragma unroll
                     for (int q = 0; q < 2; q++) {
                         const int i = 2 * I + a, j = 2 * J + q;
                         const double r = L[f.b + i * f.ny + j] - lv_lap(L, f, i, j);
@@ -1068,8 +1095,9 @@ __global__ __launch_bounds__(256) void k_coarse_vcycle(Geo g, Coef c, double* __
         lv_rb(L, lv[nl - 1], comega, citers);
         for (int k = nl - 2; k >= 0; k--) {
             const LdsLv f = lv[k], v = lv[k + 1];
-            for (int t = threadIdx.x; t < f.nx * f.ny; t += blockDim.x) {
-                const int i = t / f.ny, j = t - i * f.ny;
+            for (int t = threadIdx.x; t < f.nx * f.ny; t += CV_THREADS) {
+                int i, j;
+                lv_split(f, t, i, j);
                 const int I = i >> 1, J = j >> 1;
                 int In = (i & 1) ? I + 1 : I - 1, Jn = (j & 1) ? J + 1 : J - 1;
                 if (In < 0 || In >= v.nx) In = I;
@@ -1084,8 +1112,9 @@ __global__ __launch_bounds__(256) void k_coarse_vcycle(Geo g, Coef c, double* __
     }
     {
         const LdsLv v = lv[0];
-        for (int t = threadIdx.x; t < v.nx * v.ny; t += blockDim.x) {
-            const int i = t / v.ny, j = t - i * v.ny;
+        for (int t = threadIdx.x; t < v.nx * v.ny; t += CV_THREADS) {
+            int i, j;
+            lv_split(v, t, i, j);
             phi[(ptrdiff_t)i * g.ld + j] = L[v.phi + t];
         }
     }
@@ -1133,14 +1162,15 @@ __global__ void k_finish_mean(const double* __restrict__ sums, double n, double*
 }
 
 // (sum f, sum f^2) block partials over the slab's own cells
-__global__ __launch_bounds__(256) void k_sums(Geo g, const double* __restrict__ f, double* __restrict__ part) {
+__global__ __launch_bounds__(256) void k_sums(Geo g, const double* __restrict__ f, double* __restrict__ part,
+                                              int rows) {
     const int j = blockIdx.x * 64 + threadIdx.x;
-    const int li = blockIdx.y * 4 + threadIdx.y;
+    const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
     double acc[2] = {0.0, 0.0};
-    if (j < g.ny && li < g.nxl) {
+    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
         const double x = ldf(f, g.ld, li, j);
-        acc[0] = x;
-        acc[1] = x * x;
+        acc[0] += x;
+        acc[1] += x * x;
     }
     block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
 }
@@ -1166,6 +1196,16 @@ __global__ void k_fill_random(Geo g, double* phi, double* rp, uint64_t seed) {
 // ---------------------------------------------------------------- launchers
 static inline dim3 cell_grid(const Geo& g) { return dim3((g.ny + 63) / 64, (g.nxl + 3) / 4); }
 
+// cell kernels walk `rows` 4-row groups per 64 x 4 block: one block reduction (and one
+// partial) per 64 x 4*rows cells instead of per 256; still >= 2048 blocks per launch
+static inline int cell_rows(const Geo& g) {
+    const long blocks = (long)((g.ny + 63) / 64) * ((g.nxl + 3) / 4);
+    return (int)std::min(16L, std::max(1L, blocks / 2048));
+}
+static inline dim3 cell_grid(const Geo& g, int rows) {
+    return dim3((g.ny + 63) / 64, (g.nxl + 4 * rows - 1) / (4 * rows));
+}
+
 int max_partials(const Geo& g) {
     const dim3 cg = cell_grid(g);
     int n = (int)(cg.x * cg.y) * 4;
@@ -1180,22 +1220,25 @@ namespace nsg {
 
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
                const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st) {
-    const dim3 cg = cell_grid(g);
-    hipLaunchKernelGGL(k_rhs, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part);
+    const int rows = cell_rows(g);
+    const dim3 cg = cell_grid(g, rows);
+    hipLaunchKernelGGL(k_rhs, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
     return (int)(cg.x * cg.y);
 }
 
 int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* rp, double* part,
                hipStream_t st) {
-    const dim3 cg = cell_grid(g);
-    hipLaunchKernelGGL(k_div, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part);
+    const int rows = cell_rows(g);
+    const dim3 cg = cell_grid(g, rows);
+    hipLaunchKernelGGL(k_div, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part, rows);
     return (int)(cg.x * cg.y);
 }
 
 int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, const double* vs, double* u, double* v,
                    const double* phi, double* part, hipStream_t st) {
-    const dim3 cg = cell_grid(g);
-    hipLaunchKernelGGL(k_correct, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part);
+    const int rows = cell_rows(g);
+    const dim3 cg = cell_grid(g, rows);
+    hipLaunchKernelGGL(k_correct, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part, rows);
     return (int)(cg.x * cg.y);
 }
 
@@ -1349,26 +1392,18 @@ int launch_pois_residual(const Geo& g, const Coef& c, const double* phi, const d
 
 int launch_restrict(const Geo& gf, const Coef& cf, const double* phi, const double* b, const double* shift,
                     const Geo& gc, const Coef& cc, double* bc, double* pc, double* part, hipStream_t st) {
-    const dim3 cg = cell_grid(gc);
-    hipLaunchKernelGGL(k_restrict, cg, dim3(64, 4), 0, st, gf, cf, phi, b, shift, gc, cc, bc, pc, part);
+    const int rows = cell_rows(gc);
+    const dim3 cg = cell_grid(gc, rows);
+    hipLaunchKernelGGL(k_restrict, cg, dim3(64, 4), 0, st, gf, cf, phi, b, shift, gc, cc, bc, pc, part, rows);
     return (int)(cg.x * cg.y);
 }
 
 void launch_prolong(const Geo& gf, double* phi, const Geo& gc, const double* ec, hipStream_t st) {
-    hipLaunchKernelGGL(k_prolong, cell_grid(gf), dim3(64, 4), 0, st, gf, phi, gc, ec);
+    const int rows = cell_rows(gf);
+    hipLaunchKernelGGL(k_prolong, cell_grid(gf, rows), dim3(64, 4), 0, st, gf, phi, gc, ec, rows);
 }
 
-size_t coarse_vcycle_bytes(const Geo& g) {
-    size_t off = 0;
-    int nx = g.nx, ny = g.ny;
-    for (int k = 0; k < LV_MAX; k++) {
-        off += 2 * (size_t)nx * ny + 3 * (size_t)nx + 3 * (size_t)ny;
-        off = (off + 1) & ~(size_t)1;
-        if (!mg_can_coarsen(nx, ny)) break;
-        nx /= 2; ny /= 2;
-    }
-    return off * sizeof(double);
-}
+size_t coarse_vcycle_bytes(const Geo& g) { return sizeof(double) * (size_t)lv_layout(g.nx, g.ny, nullptr, nullptr); }
 
 int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double* b, int cycles, int pre, int post,
                          int citers, double comega, hipStream_t st) {
@@ -1379,7 +1414,8 @@ int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double*
         (void)hipFuncSetAttribute((const void*)k_coarse_vcycle, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k_coarse_vcycle, dim3(1), dim3(256), bytes, st, g, c, phi, b, cycles, pre, post, citers, comega);
+    hipLaunchKernelGGL(k_coarse_vcycle, dim3(1), dim3(CV_THREADS), bytes, st, g, c, phi, b, cycles, pre, post, citers,
+                       comega);
     return 0;
 }
 
@@ -1393,8 +1429,9 @@ void launch_finish_mean(const double* sums, double ncells, double* out, hipStrea
     hipLaunchKernelGGL(k_finish_mean, dim3(1), dim3(1), 0, st, sums, ncells, out);
 }
 int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st) {
-    const dim3 cg = cell_grid(g);
-    hipLaunchKernelGGL(k_sums, cg, dim3(64, 4), 0, st, g, f, part);
+    const int rows = cell_rows(g);
+    const dim3 cg = cell_grid(g, rows);
+    hipLaunchKernelGGL(k_sums, cg, dim3(64, 4), 0, st, g, f, part, rows);
     return (int)(cg.x * cg.y);
 }
 void launch_fill_random(const Geo& g, double* phi, double* rp, uint64_t seed, hipStream_t st) {
