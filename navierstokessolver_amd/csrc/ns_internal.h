@@ -6,7 +6,8 @@
 
 namespace nsg {
 
-constexpr int HALO = 4;  // ghost rows per side: K1's MUSCL stencil (2) and the 2-sweep pass's cone (4)
+constexpr int HALO = 5;  // ghost rows per side: K1's MUSCL stencil (2), the 2-sweep pass's cone (4),
+                         // the 2-sweep pass with fused restriction (5)
 
 // Geometry of one x-slab.  Fields are (nxl + 2*HALO) rows of ld doubles, j contiguous;
 // pointers handed to kernels point at local row 0.  Global row = i0 + local row.
@@ -94,6 +95,13 @@ __host__ __device__ inline bool mg_can_coarsen(int nx, int ny) {
 int launch_restrict(const Geo& gf, const Coef& cf, const double* phi, const double* b, const double* shift,
                     const Geo& gc, const Coef& cc, double* bc, double* pc, double* part, hipStream_t st);
 void launch_prolong(const Geo& gf, double* phi, const Geo& gc, const double* ec, hipStream_t st);
+
+// the last pre-smoothing pass with the restriction fused in: two RB sweeps of phi -> out,
+// then the residual of `out` restricted to the coarse rhs bc (+ coarse phi pc := 0) and
+// partials of r^2 over the fine cells (the MG convergence check); needs 5 ghost rows
+int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                                const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
+                                double* part, hipStream_t st);
 
 // coarse levels as one LDS-resident V-cycle (single rank): level g and its 2x coarsenings
 size_t coarse_vcycle_bytes(const Geo& g);

@@ -587,6 +587,10 @@ struct StreamArgs {
     int nx, ny, i0, nxl, ld;
     int nsj, nsi, L;                  // strips along j, along i, rows per strip
     double* part;                     // one residual partial per strip
+    // fused restriction (k_sweep2<.., XR>): spacings, coarse rhs / phi and their stride
+    const double *hx, *hy;
+    double *bc, *pc;
+    int ldc;
 };
 
 // diagonal of the operator at a cell from its row / column coefficient sums
@@ -607,45 +611,53 @@ __device__ __forceinline__ double relax(double q, double xm, double xp, double y
     return q + w * res;
 }
 
-// per-lane cache of diag and omega/diag for the two columns, refreshed only when the
-// row's coefficient sum changes (boundary rows, stretched grids): one division per
-// cell on the first row instead of one per update
+// 1/x to within an ulp without a division: v_rcp_f64 + two Newton steps
+__device__ __forceinline__ double rcp_nr(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-x, y, 1.0);
+    return fma(y, e, y);
+}
+
+// diag and omega/diag of a row's two columns, recomputed per use (no division, and no
+// registers held across the row pipeline: the stages of k_sweep2 would need 40 VGPRs
+// to cache them)
 template <int OP>
 struct DiagCache {
-    double rowd = -1.0, d0 = 0, d1 = 0, w0 = 0, w1 = 0;
+    double d0, d1, w0, w1;
     __device__ __forceinline__ void at(double rd, double cd0, double cd1, double alpha, double omega) {
-        if (rd != rowd) {
-            rowd = rd;
-            d0 = diag<OP>(rd, cd0, alpha);
-            d1 = diag<OP>(rd, cd1, alpha);
-            w0 = omega / d0;
-            w1 = omega / d1;
-        }
+        d0 = diag<OP>(rd, cd0, alpha);
+        d1 = diag<OP>(rd, cd1, alpha);
+        w0 = omega * rcp_nr(d0);
+        w1 = omega * rcp_nr(d1);
     }
 };
 
-// per-wave LDS copy of the row coefficients (cw, ce, cw + ce [+ bx]) for rows ib-4 .. ib+L+3:
+// per-wave LDS copy of the row coefficients (cw, ce, cw + ce [+ bx], hx) for rows ib-5 .. ib+L+4:
 // read with a wave-uniform address (broadcast) instead of a global load on every row's
 // critical path (hipcc cannot prove the tables read-only against the `out` stores)
-constexpr int RC_MAX = 72;  // L <= 64
+constexpr int RC_OFF = 5;            // table row of strip row ib
+constexpr int RC_MAX = 64 + 2 * RC_OFF;  // L <= 64
 template <int OP>
-__device__ __forceinline__ void stage_rows(const StreamArgs& a, double (*rc)[3], int ib, int lane) {
-    for (int t = lane; t < a.L + 8 && t < RC_MAX; t += 64) {
-        const int gi = min(max(a.i0 + ib - 4 + t, 0), a.nx - 1);
+__device__ __forceinline__ void stage_rows(const StreamArgs& a, double (*rc)[4], int ib, int lane) {
+    for (int t = lane; t < a.L + 2 * RC_OFF && t < RC_MAX; t += 64) {
+        const int gi = min(max(a.i0 + ib - RC_OFF + t, 0), a.nx - 1);
         const double cw = a.cw[gi], ce = a.ce[gi];
         rc[t][0] = cw;
         rc[t][1] = ce;
         rc[t][2] = cw + ce + (OP == 1 ? a.bx[gi] : 0.0);
+        rc[t][3] = a.hx ? a.hx[gi] : 0.0;
     }
 }
 
 template <int OP, bool RB, bool RES>
 __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
-    __shared__ double rcs[4][RC_MAX][3];
+    __shared__ double rcs[4][RC_MAX][4];
     const int lane = threadIdx.x & 63;
     const int nstr = a.nsj * a.nsi;
     const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-    double (*rc)[3] = rcs[threadIdx.x >> 6];
+    double (*rc)[4] = rcs[threadIdx.x >> 6];
     if (wid < nstr) stage_rows<OP>(a, rc, (wid / a.nsj) * a.L, lane);
     __syncthreads();
     double res = 0.0;
@@ -691,7 +703,7 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
             double2 Rn = P1;
             if (m >= ib - 1 && m <= ie) {
                 double lf = __shfl_up(P1.y, 1, 64), rt = __shfl_down(P1.x, 1, 64);
-                const double* rw = rc[m - ib + 4];
+                const double* rw = rc[m - ib + RC_OFF];
                 const double cw = rw[0], ce = rw[1];
                 dm.at(rw[2], cd0, cd1, alpha, omega);
                 double r0, r1;
@@ -720,7 +732,7 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
                 const int k = r - 2, gik = a.i0 + k;
                 if (k >= ib && k < ie) {
                     const double lf = __shfl_up(R1.y, 1, 64), rt = __shfl_down(R1.x, 1, 64);
-                    const double* rw = rc[k - ib + 4];
+                    const double* rw = rc[k - ib + RC_OFF];
                     const double cw = rw[0], ce = rw[1];
                     dk.at(rw[2], cd0, cd1, alpha, omega);
                     double2 o = R1;
@@ -761,28 +773,37 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
 // widens by one cell per half-sweep, so strips overlap by 4 columns on each side
 // (128 loaded, 120 written) and read rows ib-4 .. ie+3.  Every value is computed with
 // the same arithmetic as two k_sweep launches (bit-identical).
+//
+// XR (the last pre-smoothing pass of a V-cycle): a fifth stage at row r-5 takes the
+// residual of the finished values and restricts it (k_restrict's area-weighted 2 x 2
+// sum, same order) into the coarse rhs, so the restriction costs no HBM pass of its
+// own.  The cone grows by one more cell: rows ib-5 .. ie+4, 116 written columns, and
+// the black-2 stage also runs (unstored) on rows ib-1 and ie.
 constexpr int SW2 = 120;
+constexpr int SW2X = 116;
 constexpr int SD2 = 3;
 
-template <int OP, bool RES>
+template <int OP, bool RES, bool XR>
 __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
-    __shared__ double rcs[4][RC_MAX][3];
+    constexpr int EXT = XR ? 1 : 0;
+    constexpr int SWc = XR ? SW2X : SW2;
+    __shared__ double rcs[4][RC_MAX][4];
     const int lane = threadIdx.x & 63;
     const int nstr = a.nsj * a.nsi;
     const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-    double (*rc)[3] = rcs[threadIdx.x >> 6];
+    double (*rc)[4] = rcs[threadIdx.x >> 6];
     if (wid < nstr) stage_rows<OP>(a, rc, (wid / a.nsj) * a.L, lane);
     __syncthreads();
     double res = 0.0;
     if (wid < nstr) {
         const int si = wid / a.nsj, sj = wid - si * a.nsj;
-        const int jb = sj * SW2, ib = si * a.L;
+        const int jb = sj * SWc, ib = si * a.L;
         const int ie = min(ib + a.L, a.nxl);
         const int ny = a.ny, ld = a.ld;
-        const int c0 = jb - 4 + 2 * lane, c1 = c0 + 1;
+        const int c0 = jb - 4 - 2 * EXT + 2 * lane, c1 = c0 + 1;
         const int lc = min(max(c0, 0), ld - 2);
         const bool v0 = c0 >= 0 && c0 < ny, v1 = c1 >= 0 && c1 < ny;
-        const bool wr = lane >= 2 && lane <= 61 && c0 < ny;
+        const bool wr = lane >= 2 + EXT && lane <= 61 - EXT && c0 < ny;
         const bool o0 = wr && v0, o1 = wr && v1;
         const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
         const double cs0 = a.cs[k0], cn0 = a.cn[k0], cd0 = cs0 + cn0 + (OP == 1 ? a.by[k0] : 0.0);
@@ -792,32 +813,36 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
         const int rlo = -HALO, rhi = a.nxl + HALO - 1;
 
         double2 Q[SD2], QB[SD2];
-        // phi rows ib-4 .. ie+3 and b rows ib-3 .. ie+2 (the first red stage's) are read;
-        // the rest are clamped onto fetched rows (see k_sweep)
-        const int r0 = ib - 4, r1 = ie + 3;
-        const int blo = max(ib - 3, rlo), phi_hi = min(r1, rhi);
+        // phi rows ib-4-EXT .. ie+3+EXT and b rows ib-3-EXT .. ie+2+EXT (the first red
+        // stage's) are read; the rest are clamped onto fetched rows (see k_sweep)
+        const int r0 = ib - 4 - EXT, r1 = ie + 3 + EXT;
+        const int blo = max(ib - 3 - EXT, rlo), phi_hi = min(r1, rhi);
         auto load = [&](int slot_r, double2& p, double2& bb) {
             const int lp = min(max(slot_r, rlo), phi_hi), lb = min(max(slot_r - 1, blo), rhi);
             p = *reinterpret_cast<const double2*>(a.in + (ptrdiff_t)lp * ld + lc);
             bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
         };
-        // windows (3 rows each) of the four stages' inputs, rhs rows r-1 .. r-4
+        // windows (3 rows each) of the stages' inputs, rhs rows r-1 .. r-5
         double2 P0 = {0, 0}, P1 = {0, 0}, P2 = {0, 0};     // old:           rows r-2 .. r
         double2 A0 = {0, 0}, A1 = {0, 0}, A2 = {0, 0};     // after red 1:   rows r-3 .. r-1
         double2 C0 = {0, 0}, C1 = {0, 0}, C2 = {0, 0};     // after black 1: rows r-4 .. r-2
         double2 E0 = {0, 0}, E1 = {0, 0}, E2 = {0, 0};     // after red 2:   rows r-5 .. r-3
-        double2 B1 = {0, 0}, B2 = {0, 0}, B3 = {0, 0}, B4 = {0, 0};
-        DiagCache<OP> d1, d2, d3, d4;
+        double2 F0 = {0, 0}, F1 = {0, 0}, F2 = {0, 0};     // after black 2: rows r-6 .. r-4 (XR)
+        double2 B1 = {0, 0}, B2 = {0, 0}, B3 = {0, 0}, B4 = {0, 0}, B5 = {0, 0};
+        DiagCache<OP> dc;
+        // XR: this lane's column spacings, the even row's partial sum and spacing
+        const double hy0 = XR ? a.hy[k0] : 0.0, hy1 = XR ? a.hy[k1] : 0.0;
+        double xs = 0.0, hxe = 0.0;
 
         // one colour update of row `row` (window W0 above, W1 the row, W2 below); colour
         // parity: update c0 when (gi + c0) % 2 == par
-        auto half = [&](const double2& W0, const double2& W1, const double2& W2, const double2& B, int row, int par,
-                        DiagCache<OP>& dc) -> double2 {
+        auto half = [&](const double2& W0, const double2& W1, const double2& W2, const double2& B, int row,
+                        int par) -> double2 {
             double2 o = W1;
             const int gi = a.i0 + row;
             if (gi < 0 || gi >= a.nx) return o;
             const double lf = __shfl_up(W1.y, 1, 64), rt = __shfl_down(W1.x, 1, 64);
-            const double* rw = rc[row - ib + 4];
+            const double* rw = rc[row - ib + RC_OFF];
             const double cw = rw[0], ce = rw[1];
             dc.at(rw[2], cd0, cd1, alpha, omega);
             double rr;
@@ -831,38 +856,67 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
 
         auto step = [&](const double2 p, const double2 bb, int r) {
             P0 = P1; P1 = P2; P2 = p;
-            B4 = B3; B3 = B2; B2 = B1;
+            B5 = B4; B4 = B3; B3 = B2; B2 = B1;
             B1 = make_double2(bb.x - shift, bb.y - shift);
             // stage 1: red of sweep 1 at m = r-1 (+ residual of the input)
             const int m = r - 1;
             double2 n1 = P1;
-            if (m >= ib - 3 && m <= ie + 2) {
+            if (m >= ib - 3 - EXT && m <= ie + 2 + EXT) {
                 if (RES && m >= ib && m < ie) {
                     const double lf = __shfl_up(P1.y, 1, 64), rt = __shfl_down(P1.x, 1, 64);
-                    const double* rw = rc[m - ib + 4];
+                    const double* rw = rc[m - ib + RC_OFF];
                     const double cw = rw[0], ce = rw[1];
-                    d1.at(rw[2], cd0, cd1, alpha, omega);
+                    dc.at(rw[2], cd0, cd1, alpha, omega);
                     double r0, r1;
-                    relax<OP>(P1.x, P0.x, P2.x, lf, P1.y, B1.x, cw, ce, cs0, cn0, d1.d0, d1.w0, alpha, r0);
-                    relax<OP>(P1.y, P0.y, P2.y, P1.x, rt, B1.y, cw, ce, cs1, cn1, d1.d1, d1.w1, alpha, r1);
+                    relax<OP>(P1.x, P0.x, P2.x, lf, P1.y, B1.x, cw, ce, cs0, cn0, dc.d0, dc.w0, alpha, r0);
+                    relax<OP>(P1.y, P0.y, P2.y, P1.x, rt, B1.y, cw, ce, cs1, cn1, dc.d1, dc.w1, alpha, r1);
                     res += (o0 ? r0 * r0 : 0.0) + (o1 ? r1 * r1 : 0.0);
                 }
-                n1 = half(P0, P1, P2, B1, m, 0, d1);
+                n1 = half(P0, P1, P2, B1, m, 0);
             }
             A0 = A1; A1 = A2; A2 = n1;
             // stage 2: black of sweep 1 at r-2
             double2 n2 = A1;
-            if (r - 2 >= ib - 2 && r - 2 <= ie + 1) n2 = half(A0, A1, A2, B2, r - 2, 1, d2);
+            if (r - 2 >= ib - 2 - EXT && r - 2 <= ie + 1 + EXT) n2 = half(A0, A1, A2, B2, r - 2, 1);
             C0 = C1; C1 = C2; C2 = n2;
             // stage 3: red of sweep 2 at r-3
             double2 n3 = C1;
-            if (r - 3 >= ib - 1 && r - 3 <= ie) n3 = half(C0, C1, C2, B3, r - 3, 0, d3);
+            if (r - 3 >= ib - 1 - EXT && r - 3 <= ie + EXT) n3 = half(C0, C1, C2, B3, r - 3, 0);
             E0 = E1; E1 = E2; E2 = n3;
-            // stage 4: black of sweep 2 at r-4, stored
+            // stage 4: black of sweep 2 at r-4, stored on the strip's rows
             const int k = r - 4;
-            if (k >= ib && k < ie) {
-                const double2 o = half(E0, E1, E2, B4, k, 1, d4);
-                if (wr) *reinterpret_cast<double2*>(a.out + (ptrdiff_t)k * ld + c0) = o;
+            double2 n4 = E1;
+            if (k >= ib - EXT && k < ie + EXT) {
+                n4 = half(E0, E1, E2, B4, k, 1);
+                if (k >= ib && k < ie && wr) *reinterpret_cast<double2*>(a.out + (ptrdiff_t)k * ld + c0) = n4;
+            }
+            if (XR) {
+                // stage 5: residual of the finished row r-5, restricted in row pairs
+                F0 = F1; F1 = F2; F2 = n4;
+                const int m5 = r - 5;
+                if (m5 >= ib && m5 < ie) {
+                    const double lf = __shfl_up(F1.y, 1, 64), rt = __shfl_down(F1.x, 1, 64);
+                    const double* rw = rc[m5 - ib + RC_OFF];
+                    const double cw = rw[0], ce = rw[1], hxr = rw[3];
+                    dc.at(rw[2], cd0, cd1, alpha, omega);
+                    double r0, r1;
+                    relax<OP>(F1.x, F0.x, F2.x, lf, F1.y, B5.x, cw, ce, cs0, cn0, dc.d0, 0.0, alpha, r0);
+                    relax<OP>(F1.y, F0.y, F2.y, F1.x, rt, B5.y, cw, ce, cs1, cn1, dc.d1, 0.0, alpha, r1);
+                    res += (o0 ? r0 * r0 : 0.0) + (o1 ? r1 * r1 : 0.0);
+                    if (((a.i0 + m5) & 1) == 0) {
+                        xs = (hxr * hy0) * r0;
+                        xs = xs + (hxr * hy1) * r1;
+                        hxe = hxr;
+                    } else {
+                        xs = xs + (hxr * hy0) * r0;
+                        xs = xs + (hxr * hy1) * r1;
+                        if (wr) {
+                            const ptrdiff_t o = (ptrdiff_t)(m5 >> 1) * a.ldc + (c0 >> 1);
+                            a.bc[o] = xs / ((hxe + hxr) * (hy0 + hy1));
+                            a.pc[o] = 0.0;
+                        }
+                    }
+                }
             }
         };
 
@@ -876,7 +930,7 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
             }
         }
     }
-    if (RES) {
+    if (RES || XR) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
         if (lane == 0 && wid < nstr) a.part[wid] = res;
@@ -1210,7 +1264,7 @@ int max_partials(const Geo& g) {
     const dim3 cg = cell_grid(g);
     int n = (int)(cg.x * cg.y) * 4;
     const int tiles = ((g.nxl + 7) / 8) * ((g.ny + 63) / 64) * 2;   // tiled sweeps
-    const int strips = ((g.nxl + 3) / 4) * ((g.ny + 119) / 120) * 2;  // streaming sweeps, strip rows >= 4
+    const int strips = ((g.nxl + 3) / 4) * ((g.ny + 115) / 116) * 2;  // streaming sweeps, strip rows >= 4
     return std::max(n, std::max(tiles, strips));
 }
 
@@ -1319,12 +1373,26 @@ int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* p
 template <int OP>
 static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st) {
     a.nsj = (g.ny + SW2 - 1) / SW2;
-    const long cap = resident_waves(a.part ? (const void*)k_sweep2<OP, true> : (const void*)k_sweep2<OP, false>);
+    const long cap =
+        resident_waves(a.part ? (const void*)k_sweep2<OP, true, false> : (const void*)k_sweep2<OP, false, false>);
     a.L = strip_rows(a.nxl, a.nsj, cap, 16);
     a.nsi = (g.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
-    if (a.part) hipLaunchKernelGGL((k_sweep2<OP, true>), dim3(nblk), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_sweep2<OP, false>), dim3(nblk), dim3(256), 0, st, a);
+    if (a.part) hipLaunchKernelGGL((k_sweep2<OP, true, false>), dim3(nblk), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_sweep2<OP, false, false>), dim3(nblk), dim3(256), 0, st, a);
+    return nstr;
+}
+
+int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                                const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
+                                double* part, hipStream_t st) {
+    StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
+    a.hx = c.hx; a.hy = c.hy; a.bc = bc; a.pc = pc; a.ldc = gc.ld;
+    a.nsj = (g.ny + SW2X - 1) / SW2X;
+    a.L = strip_rows(a.nxl, a.nsj, resident_waves((const void*)k_sweep2<0, false, true>), 16);
+    a.nsi = (g.nxl + a.L - 1) / a.L;
+    const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
+    hipLaunchKernelGGL((k_sweep2<0, false, true>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 

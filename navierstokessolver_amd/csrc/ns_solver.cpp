@@ -102,6 +102,8 @@ struct ns_solver {
     std::vector<hipEvent_t> ev;  // timing events (pairs)
     int helm_batch0 = 4, pois_batch0 = 8;
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
+    int fuse_restrict = 1;       // NSGPU_FUSED_RESTRICT=0: separate k_restrict pass (A/B)
+    long pair_min_cells = 2048L * 2048L;   // NSGPU_PAIR_MIN_CELLS: smallest level smoothed in 2-sweep passes
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
     int mg_pre = 2, mg_post = 2, mg_coarse_iters = 0;
     double mg_omega_c = 1.0, mg_omega_s = 1.0;
@@ -373,14 +375,25 @@ MgLevel& level(ns_solver* s, int l) {
     return L;
 }
 
+// levels whose smoothing runs as two-sweep passes: the HBM-bound ones (>= 2048^2 local
+// cells); the coarser ones are latency-bound and the fused pass's deeper row pipeline only
+// costs there (tools/sweep_levels2.py: 512^2 9.5 us/sweep fused vs 8.1 single)
+bool pair_level(const ns_solver* s, int l) {
+    const nsg::Geo& g = s->lv[l].g;
+    if (s->tiled || (s->nranks > 1 && g.nxl < nsg::HALO)) return false;   // ghost rows come from ONE neighbour
+    return (long)g.nxl * g.ny >= s->pair_min_cells;
+}
+
+// the last two pre-smoothing sweeps of level l carry the restriction (k_sweep2<XR>);
+// NSGPU_FUSED_RESTRICT=0 keeps the separate k_restrict pass (A/B and tests)
+bool fused_restrict(const ns_solver* s, int l) {
+    return s->fuse_restrict && pair_level(s, l) && s->mg_pre >= 2 && s->mg_pre % 2 == 0;
+}
+
 int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
     MgLevel& L = level(s, l);
     for (int k = 0; k < n;) {
-        // two sweeps per HBM pass on the HBM-bound levels (>= 2048^2 local cells); the coarser
-        // ones are latency-bound and the fused pass's deeper row pipeline only costs there
-        // (tools/sweep_levels2.py: 512^2 9.5 us/sweep fused vs 8.1 single)
-        const bool big = (long)L.g.nxl * L.g.ny >= 2048L * 2048L;
-        const int w = (n - k >= 2 && !s->tiled && big) ? 2 : 1;
+        const int w = (n - k >= 2 && pair_level(s, l)) ? 2 : 1;   // two sweeps per HBM pass
         CHK(halo_g(s, L.g, {L.phi}, 2 * w));
         const bool t = s->timing && l == 0;
         if (t) HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st));
@@ -425,13 +438,24 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
         const int ev0 = 0;
         bool done = false;
         for (int l = 0; l < nl - 1 && !done; l++) {
-            CHK(mg_smooth(s, l, s->mg_pre, &tn, ev0));
             MgLevel& F = level(s, l);
             MgLevel& C = level(s, l + 1);
-            CHK(halo_g(s, F.g, {F.phi}, 1));
-            const int nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, l == 0 ? s->scal + S_SHIFT : nullptr, C.g, C.c,
-                                                C.b, C.phi, s->part, s->st);
-            CHK(halo_g(s, C.g, {C.b}, 3));
+            const double* sh = l == 0 ? s->scal + S_SHIFT : nullptr;
+            int nb;
+            if (fused_restrict(s, l)) {
+                // last two pre-smoothing sweeps + residual + restriction in one HBM pass
+                CHK(mg_smooth(s, l, s->mg_pre - 2, &tn, ev0));
+                CHK(halo_g(s, F.g, {F.phi}, 5));
+                nb = nsg::launch_pois_rbsor2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, C.g, C.b, C.phi,
+                                                      s->part, s->st);
+                std::swap(F.phi, F.tmp);
+                if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
+            } else {
+                CHK(mg_smooth(s, l, s->mg_pre, &tn, ev0));
+                CHK(halo_g(s, F.g, {F.phi}, 1));
+                nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, sh, C.g, C.c, C.b, C.phi, s->part, s->st);
+            }
+            CHK(halo_g(s, C.g, {C.b}, 4));
             if (l == 0) {
                 // fine residual after pre-smoothing: the convergence test (one host sync per cycle)
                 nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
@@ -739,6 +763,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (p->check_every > 0) s->pois_batch0 = s->helm_batch0 = p->check_every;
     s->timing = p->timing;
     if (const char* e = getenv("NSGPU_SWEEP")) s->tiled = std::strcmp(e, "tiled") == 0;
+    if (const char* e = getenv("NSGPU_FUSED_RESTRICT")) s->fuse_restrict = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     {
         const char* e = getenv("NSGPU_STRIP_ROWS");  // tuning override; unset = adaptive
         nsg::set_strip_rows(e ? atoi(e) : 0);
@@ -838,7 +864,7 @@ int ns_step(ns_solver* s, ns_stats* out) {
     st.it_v = st.it_u;
     CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
-    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 3));
+    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
     if (s->poisson == NS_POISSON_MG) CHK(pois_solve_mg(s, &st.it_phi, &st.res_phi, &st));  // KSPSolve(phiSolver) (:551)
     else CHK(pois_solve(s, &st.it_phi, &st.res_phi, &st));
     CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
@@ -936,7 +962,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         return 0;
     case NS_K_POISSON: {
         int nb = 0;
-        CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 3));
+        CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
         const int pairs = (s->poisson != NS_POISSON_JACOBI && !s->tiled && iters > 0) ? (iters - 1) / 2 : 0;
         for (int k = 0; k < pairs; k++) {
             CHK(halo(s, {s->arr[NS_ARR_PHI]}, 4));
@@ -976,7 +1002,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         int its = 0;
         double r = 0;
         CHK(rhs_mean(s));
-        CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 3));
+        CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
         if (s->poisson == NS_POISSON_MG) CHK(pois_solve_mg(s, &its, &r, nullptr));
         else CHK(pois_solve(s, &its, &r, nullptr));
         if (out) { out[0] = its; out[1] = r; }
@@ -1025,7 +1051,7 @@ int ns_fill_random(ns_solver* s, uint64_t seed) {
     HIPCHK(hipSetDevice(s->device));
     nsg::launch_fill_random(s->g, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], seed, s->st);
     CHK(rhs_mean(s));  // the random rhs's mean becomes the Poisson shift (null-space removal)
-    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 3));
+    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
     HIPCHK(hipStreamSynchronize(s->st));
     return 0;
 }

@@ -22,7 +22,7 @@ def launch(tmp_path, *args, port=29561):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(HERE, "mr_worker.py"),
            "--output", str(out), *args]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ))
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     return dict(np.load(out, allow_pickle=False))
 
@@ -34,9 +34,14 @@ def single(n, ny, steps, poisson, rtol):
     return u, v, phi, np.array(mm)
 
 
-@pytest.mark.parametrize("poisson,n,ny", [(nsa.NS_POISSON_RBSOR, 48, 40), (nsa.NS_POISSON_MG, 64, 64),
-                                          (nsa.NS_POISSON_MG, 130, 96)])
-def test_two_slabs_host_transport_match_single_rank(tmp_path, poisson, n, ny):
+@pytest.mark.parametrize("poisson,n,ny,pairs", [(nsa.NS_POISSON_RBSOR, 48, 40, False), (nsa.NS_POISSON_MG, 64, 64, False),
+                                                (nsa.NS_POISSON_MG, 130, 96, False),
+                                                (nsa.NS_POISSON_MG, 128, 96, True)])
+def test_two_slabs_host_transport_match_single_rank(tmp_path, monkeypatch, poisson, n, ny, pairs):
+    """pairs: every level smoothed by two-sweep passes with the fused restriction (5 ghost rows),
+    the path 4096^2 production runs take on their finest levels."""
+    if pairs:
+        monkeypatch.setenv("NSGPU_PAIR_MIN_CELLS", "0")
     steps, rtol = 6, 1e-11
     r = launch(tmp_path, "--xport", "host", "--size", str(n), "--size-y", str(ny), "--nsteps", str(steps),
                "--solver", str(poisson), "--tol", str(rtol))
