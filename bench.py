@@ -23,7 +23,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-POISSON_BYTES_PER_CELL = 24  # read phi, read rhs, write phi
+# the timed kernel: the finest level's first post-smoothing pass (k_sweep2 FUSE_P) --
+# bilinear prolongation of the coarse correction + two red-black sweeps in one HBM pass.
+# Algorithmic bytes per cell: read phi 8, read rhs 8, write phi 8, read the coarse
+# correction 8/4 (24 B/cell per sweep for an unfused sweep)
+ROOFLINE_KERNEL = "k_sweep2<Poisson, FUSE_P> (finest post-smoothing pass: prolongation + 2 RB sweeps)"
+PASS_BYTES_PER_CELL = 26
+SWEEP_BYTES_PER_CELL = 24
 
 
 def parse():
@@ -38,7 +44,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(n, re, dt, omega_v):
+def cpu_baseline(n, re, dt, omega_v, omega_mg):
     """The oracle (CPU restatement, 1 thread) running the SAME algorithm as the GPU path
     (RB-SOR Helmholtz to rtol, multigrid Poisson to rtol 1e-8) for one full time step of
     the same n^2 cavity (the first step from rest: a bounded sample, ~10-30 s)."""
@@ -47,7 +53,7 @@ def cpu_baseline(n, re, dt, omega_v):
 
     g = OGrid.rectangle(n, n)
     s = OSolver(g, dt, re, rtol=1e-8)
-    s.use_gpu_algorithm(omega_v)
+    s.use_gpu_algorithm(omega_v, omega_mg)
     t0 = time.perf_counter()
     _, its = s.step()
     t = time.perf_counter() - t0
@@ -110,7 +116,9 @@ def main():
     kn = sum(s["n_poisson_kernels"] for s in stats)
     avg_kernel_s = kms / kn / 1e3 if kn else float("nan")
     local_cells = (solver.i1 - solver.i0) * n
-    achieved = POISSON_BYTES_PER_CELL * local_cells / avg_kernel_s / 1e9
+    achieved = PASS_BYTES_PER_CELL * local_cells / avg_kernel_s / 1e9
+    # finest-level sweeps: V(2,2) per cycle + the 2 pre-smoothing sweeps of the converged check
+    fine_sweeps = 4 * cycles + 2 * K
     value = cells * K / elapsed / 1e6
 
     if rank != 0:
@@ -120,7 +128,7 @@ def main():
     if os.path.exists(prof):
         try:
             d = json.load(open(prof))
-            if d.get("n") == n and d.get("kernel_bytes_per_launch"):
+            if d.get("n") == n and d.get("kernel") == ROOFLINE_KERNEL and d.get("kernel_bytes_per_launch"):
                 traffic = d["kernel_bytes_per_launch"]
         except Exception:
             traffic = None
@@ -142,17 +150,19 @@ def main():
                    "nx": n, "ny": n, "re": re, "dt": dt, "parallelism": f"x-slab x{world}"},
         "poisson_vcycles_per_s": cycles / elapsed,
         "poisson_vcycles_per_step": cycles / K,
-        "poisson_fine_sweeps_per_s": kn / elapsed,
-        "poisson_fine_sweep_glups": local_cells * world * kn / elapsed / 1e9,
+        "poisson_fine_sweeps_per_s": fine_sweeps / elapsed,
+        "poisson_fine_sweeps_per_step": fine_sweeps / K,
         "helmholtz_sweeps_per_step": hsweeps / K,
-        "roofline": {"bound": "hbm", "kernel": "k_sweep<Poisson,RB> (K4 multigrid smoother, finest level)",
+        "roofline": {"bound": "hbm", "kernel": ROOFLINE_KERNEL,
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "avg_kernel_us": avg_kernel_s * 1e6,
-                     "bytes_per_launch": POISSON_BYTES_PER_CELL * local_cells},
+                     "traffic": traffic, "avg_kernel_us": avg_kernel_s * 1e6, "launches_timed": kn,
+                     "bytes_per_launch": PASS_BYTES_PER_CELL * local_cells,
+                     # two sweeps per pass: the rate an unfused sweep (24 B/cell) would need to match
+                     "sweep_equivalent_GBs": 2 * SWEEP_BYTES_PER_CELL * local_cells / avg_kernel_s / 1e9},
     }
     if world == 1 and not args.no_cpu:
         try:
-            line["cpu_baseline"] = cpu_baseline(n, re, dt, solver.omega_v)
+            line["cpu_baseline"] = cpu_baseline(n, re, dt, solver.omega_v, solver.mg_omega)
         except Exception as e:  # the baseline must never hide the GPU line
             line["cpu_baseline"] = {"error": repr(e)}
     print(json.dumps(line), flush=True)

@@ -102,6 +102,8 @@ typedef struct ns_params {
      * correction, and sweeps of the coarsest solve (0 = defaults 2 / 2 / automatic) */
     int32_t mg_pre, mg_post, mg_coarse_iters;
     const ns_host_transport* host_transport;  /* NULL = RCCL (nranks > 1) */
+    double mg_omega;          /* over-relaxation of the red-black smoother (0 = default 1.1:
+                               * 4.1 vs 4.6 V-cycles per step at 4096^2, tools/mg_params_sweep.py) */
 } ns_params;
 
 /* Per-step result (the reference prints iter, umin, umax, vmin, vmax: FluidSolver.cpp:559-560). */

@@ -55,7 +55,7 @@ class NsParams(ctypes.Structure):
                 ("device", ctypes.c_int32), ("timing", ctypes.c_int32),
                 ("rank", ctypes.c_int32), ("nranks", ctypes.c_int32), ("nccl_id", ctypes.c_void_p),
                 ("mg_pre", ctypes.c_int32), ("mg_post", ctypes.c_int32), ("mg_coarse_iters", ctypes.c_int32),
-                ("host_transport", ctypes.POINTER(NsHostTransport))]
+                ("host_transport", ctypes.POINTER(NsHostTransport)), ("mg_omega", ctypes.c_double)]
 
 
 class NsStats(ctypes.Structure):

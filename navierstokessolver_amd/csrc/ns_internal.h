@@ -54,7 +54,8 @@ int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* p
 int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* in, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st);
 // two red-black sweeps in one HBM pass (temporal blocking): same results as two calls above;
-// residual partials (if part) are of the input iterate
+// residual partials (if part) are of the OUTPUT iterate, and then 5 ghost rows are read
+// (4 without)
 int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st);
 int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
@@ -103,10 +104,16 @@ int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const
                                 const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
                                 double* part, hipStream_t st);
 
+// the first post-smoothing pass with the prolongation fused in: phi + P(ec) enters two RB
+// sweeps -> out (phi itself is not modified); needs 5 ghost rows of phi, 3 of ec
+int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                               const double* rp, const double* shift, const Geo& gc, const double* ec,
+                               hipStream_t st);
+
 // coarse levels as one LDS-resident V-cycle (single rank): level g and its 2x coarsenings
 size_t coarse_vcycle_bytes(const Geo& g);
 int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double* b, int cycles, int pre, int post,
-                         int citers, double comega, hipStream_t st);
+                         int citers, double comega, double somega, hipStream_t st);
 
 // max partials any launcher writes for this geometry
 int max_partials(const Geo& g);

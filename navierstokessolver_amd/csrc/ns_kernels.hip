@@ -587,10 +587,13 @@ struct StreamArgs {
     int nx, ny, i0, nxl, ld;
     int nsj, nsi, L;                  // strips along j, along i, rows per strip
     double* part;                     // one residual partial per strip
-    // fused restriction (k_sweep2<.., XR>): spacings, coarse rhs / phi and their stride
+    // fused restriction (k_sweep2 FUSE_R): spacings, coarse rhs / phi and their stride;
+    // fused prolongation (FUSE_P): the coarse correction ec, its global size and first row
     const double *hx, *hy;
     double *bc, *pc;
     int ldc;
+    const double* ec;
+    int ncx, ncy, ci0;
 };
 
 // diagonal of the operator at a cell from its row / column coefficient sums
@@ -774,19 +777,29 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
 // (128 loaded, 120 written) and read rows ib-4 .. ie+3.  Every value is computed with
 // the same arithmetic as two k_sweep launches (bit-identical).
 //
-// XR (the last pre-smoothing pass of a V-cycle): a fifth stage at row r-5 takes the
-// residual of the finished values and restricts it (k_restrict's area-weighted 2 x 2
-// sum, same order) into the coarse rhs, so the restriction costs no HBM pass of its
-// own.  The cone grows by one more cell: rows ib-5 .. ie+4, 116 written columns, and
-// the black-2 stage also runs (unstored) on rows ib-1 and ie.
+// RES: a fifth stage at row r-5 takes the residual of the finished values (partials of
+// r^2 per strip: the solver's convergence check sees the pass's OUTPUT, not its input).
+// The cone grows by one more cell: rows ib-5 .. ie+4, 116 written columns, and the
+// black-2 stage also runs (unstored) on rows ib-1 and ie.
+// FUSE_R (the last pre-smoothing pass of a V-cycle): the same fifth stage, and the
+// residual restricted (k_restrict's area-weighted 2 x 2 sum, same order) into the coarse
+// rhs, so the restriction costs no HBM pass of its own.
+// FUSE_P (the first post-smoothing pass): every phi row entering the pipeline gets the
+// bilinear prolongation of the coarse correction added (k_prolong's formula): coarse
+// rows I = r/2 and its neighbour row are loaded with the row, coarse columns J +- 1
+// come from the adjacent lanes (the outermost lanes' missing neighbours fall outside
+// the written cone of the same 116-column layout).
 constexpr int SW2 = 120;
 constexpr int SW2X = 116;
 constexpr int SD2 = 3;
+constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2;
 
-template <int OP, bool RES, bool XR>
+template <int OP, bool RES, int FUSE>
 __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
-    constexpr int EXT = XR ? 1 : 0;
-    constexpr int SWc = XR ? SW2X : SW2;
+    constexpr bool XR = FUSE == FUSE_R, XP = FUSE == FUSE_P;
+    constexpr bool R5 = RES || XR;                 // the fifth (output residual) stage
+    constexpr int EXT = (R5 || XP) ? 1 : 0;
+    constexpr int SWc = EXT ? SW2X : SW2;
     __shared__ double rcs[4][RC_MAX][4];
     const int lane = threadIdx.x & 63;
     const int nstr = a.nsj * a.nsi;
@@ -812,15 +825,27 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
         const double alpha = a.alpha, omega = a.omega;
         const int rlo = -HALO, rhi = a.nxl + HALO - 1;
 
-        double2 Q[SD2], QB[SD2];
+        double2 Q[SD2], QB[SD2], QE[SD2];
         // phi rows ib-4-EXT .. ie+3+EXT and b rows ib-3-EXT .. ie+2+EXT (the first red
         // stage's) are read; the rest are clamped onto fetched rows (see k_sweep)
         const int r0 = ib - 4 - EXT, r1 = ie + 3 + EXT;
         const int blo = max(ib - 3 - EXT, rlo), phi_hi = min(r1, rhi);
-        auto load = [&](int slot_r, double2& p, double2& bb) {
+        // FUSE_P: this lane's coarse column (its pair c0, c1 = 2J, 2J+1) and whether J -+ 1
+        // exist (a missing one is replaced by J: the wall reflection of k_prolong)
+        const int Jc = c0 >> 1;
+        const int Jl = XP ? min(max(Jc, 0), a.ncy - 1) : 0;
+        const bool jm_ok = Jc - 1 >= 0, jp_ok = Jc + 1 < a.ncy;
+        auto load = [&](int slot_r, double2& p, double2& bb, double2& ee) {
             const int lp = min(max(slot_r, rlo), phi_hi), lb = min(max(slot_r - 1, blo), rhi);
             p = *reinterpret_cast<const double2*>(a.in + (ptrdiff_t)lp * ld + lc);
             bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
+            if (XP) {
+                const int I = lp >> 1;                      // floor, also for ghost rows
+                int In = (lp & 1) ? I + 1 : I - 1;
+                if (a.ci0 + In < 0 || a.ci0 + In >= a.ncx) In = I;
+                ee.x = a.ec[(ptrdiff_t)I * a.ldc + Jl];
+                ee.y = a.ec[(ptrdiff_t)In * a.ldc + Jl];
+            }
         };
         // windows (3 rows each) of the stages' inputs, rhs rows r-1 .. r-5
         double2 P0 = {0, 0}, P1 = {0, 0}, P2 = {0, 0};     // old:           rows r-2 .. r
@@ -854,26 +879,23 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
             return o;
         };
 
-        auto step = [&](const double2 p, const double2 bb, int r) {
+        auto step = [&](double2 p, const double2 bb, const double2 ee, int r) {
+            if (XP) {
+                // phi += P(e): e(I, J) = ee.x, e(In, J) = ee.y, column neighbours from lanes -+ 1
+                double m0 = __shfl_up(ee.x, 1, 64), m1 = __shfl_up(ee.y, 1, 64);
+                double q0 = __shfl_down(ee.x, 1, 64), q1 = __shfl_down(ee.y, 1, 64);
+                if (!jm_ok) { m0 = ee.x; m1 = ee.y; }
+                if (!jp_ok) { q0 = ee.x; q1 = ee.y; }
+                p.x += (9.0 * ee.x + 3.0 * ee.y + 3.0 * m0 + m1) * 0.0625;
+                p.y += (9.0 * ee.x + 3.0 * ee.y + 3.0 * q0 + q1) * 0.0625;
+            }
             P0 = P1; P1 = P2; P2 = p;
             B5 = B4; B4 = B3; B3 = B2; B2 = B1;
             B1 = make_double2(bb.x - shift, bb.y - shift);
-            // stage 1: red of sweep 1 at m = r-1 (+ residual of the input)
+            // stage 1: red of sweep 1 at m = r-1
             const int m = r - 1;
             double2 n1 = P1;
-            if (m >= ib - 3 - EXT && m <= ie + 2 + EXT) {
-                if (RES && m >= ib && m < ie) {
-                    const double lf = __shfl_up(P1.y, 1, 64), rt = __shfl_down(P1.x, 1, 64);
-                    const double* rw = rc[m - ib + RC_OFF];
-                    const double cw = rw[0], ce = rw[1];
-                    dc.at(rw[2], cd0, cd1, alpha, omega);
-                    double r0, r1;
-                    relax<OP>(P1.x, P0.x, P2.x, lf, P1.y, B1.x, cw, ce, cs0, cn0, dc.d0, dc.w0, alpha, r0);
-                    relax<OP>(P1.y, P0.y, P2.y, P1.x, rt, B1.y, cw, ce, cs1, cn1, dc.d1, dc.w1, alpha, r1);
-                    res += (o0 ? r0 * r0 : 0.0) + (o1 ? r1 * r1 : 0.0);
-                }
-                n1 = half(P0, P1, P2, B1, m, 0);
-            }
+            if (m >= ib - 3 - EXT && m <= ie + 2 + EXT) n1 = half(P0, P1, P2, B1, m, 0);
             A0 = A1; A1 = A2; A2 = n1;
             // stage 2: black of sweep 1 at r-2
             double2 n2 = A1;
@@ -890,8 +912,8 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
                 n4 = half(E0, E1, E2, B4, k, 1);
                 if (k >= ib && k < ie && wr) *reinterpret_cast<double2*>(a.out + (ptrdiff_t)k * ld + c0) = n4;
             }
-            if (XR) {
-                // stage 5: residual of the finished row r-5, restricted in row pairs
+            if (R5) {
+                // stage 5: residual of the finished row r-5 (FUSE_R: restricted in row pairs)
                 F0 = F1; F1 = F2; F2 = n4;
                 const int m5 = r - 5;
                 if (m5 >= ib && m5 < ie) {
@@ -903,7 +925,8 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
                     relax<OP>(F1.x, F0.x, F2.x, lf, F1.y, B5.x, cw, ce, cs0, cn0, dc.d0, 0.0, alpha, r0);
                     relax<OP>(F1.y, F0.y, F2.y, F1.x, rt, B5.y, cw, ce, cs1, cn1, dc.d1, 0.0, alpha, r1);
                     res += (o0 ? r0 * r0 : 0.0) + (o1 ? r1 * r1 : 0.0);
-                    if (((a.i0 + m5) & 1) == 0) {
+                    if (!XR) {
+                    } else if (((a.i0 + m5) & 1) == 0) {
                         xs = (hxr * hy0) * r0;
                         xs = xs + (hxr * hy1) * r1;
                         hxe = hxr;
@@ -921,16 +944,16 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
         };
 
 #pragma unroll
-        for (int q = 0; q < SD2; q++) load(r0 + q, Q[q], QB[q]);
+        for (int q = 0; q < SD2; q++) load(r0 + q, Q[q], QB[q], QE[q]);
         for (int r = r0; r <= r1; r += SD2) {
 #pragma unroll
             for (int q = 0; q < SD2; q++) {
-                if (r + q <= r1) step(Q[q], QB[q], r + q);
-                load(r + q + SD2, Q[q], QB[q]);
+                if (r + q <= r1) step(Q[q], QB[q], QE[q], r + q);
+                load(r + q + SD2, Q[q], QB[q], QE[q]);
             }
         }
     }
-    if (RES || XR) {
+    if (R5) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
         if (lane == 0 && wid < nstr) a.part[wid] = res;
@@ -1078,7 +1101,7 @@ __host__ __device__ inline int lv_layout(int nx, int ny, LdsLv* lv, int* nlev) {
 
 __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, double* __restrict__ phi,
                                                               const double* __restrict__ b, int cycles, int pre,
-                                                              int post, int citers, double comega) {
+                                                              int post, int citers, double comega, double somega) {
     extern __shared__ __attribute__((aligned(16))) double L[];
     __shared__ LdsLv lv[LV_MAX];
     __shared__ int nlev;
@@ -1128,7 +1151,7 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, dou
     for (int cyc = 0; cyc < cycles; cyc++) {
         for (int k = 0; k < nl - 1; k++) {
             const LdsLv f = lv[k], v = lv[k + 1];
-            lv_rb(L, f, 1.0, pre);
+            lv_rb(L, f, somega, pre);
             for (int t = threadIdx.x; t < v.nx * v.ny; t += CV_THREADS) {
                 int I, J;
                 lv_split(v, t, I, J);
@@ -1161,7 +1184,7 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, dou
                                  e[In * v.ny + Jn]) * 0.0625;
             }
             __syncthreads();
-            lv_rb(L, f, 1.0, post);
+            lv_rb(L, f, somega, post);
         }
     }
     {
@@ -1369,17 +1392,18 @@ int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* p
     return launch_stream<0, true>(stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false), st);
 }
 
-// two fused red-black sweeps: strips of 120 written columns reading rows ib-4 .. ie+3
+// two fused red-black sweeps: strips of 120 written columns reading rows ib-4 .. ie+3;
+// with the output residual (part != null) 116 columns, rows ib-5 .. ie+4
 template <int OP>
 static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st) {
-    a.nsj = (g.ny + SW2 - 1) / SW2;
-    const long cap =
-        resident_waves(a.part ? (const void*)k_sweep2<OP, true, false> : (const void*)k_sweep2<OP, false, false>);
+    a.nsj = a.part ? (g.ny + SW2X - 1) / SW2X : (g.ny + SW2 - 1) / SW2;
+    const long cap = resident_waves(a.part ? (const void*)k_sweep2<OP, true, FUSE_NONE>
+                                           : (const void*)k_sweep2<OP, false, FUSE_NONE>);
     a.L = strip_rows(a.nxl, a.nsj, cap, 16);
     a.nsi = (g.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
-    if (a.part) hipLaunchKernelGGL((k_sweep2<OP, true, false>), dim3(nblk), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_sweep2<OP, false, false>), dim3(nblk), dim3(256), 0, st, a);
+    if (a.part) hipLaunchKernelGGL((k_sweep2<OP, true, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_sweep2<OP, false, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 
@@ -1389,10 +1413,23 @@ int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const
     StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
     a.hx = c.hx; a.hy = c.hy; a.bc = bc; a.pc = pc; a.ldc = gc.ld;
     a.nsj = (g.ny + SW2X - 1) / SW2X;
-    a.L = strip_rows(a.nxl, a.nsj, resident_waves((const void*)k_sweep2<0, false, true>), 16);
+    a.L = strip_rows(a.nxl, a.nsj, resident_waves((const void*)k_sweep2<0, false, FUSE_R>), 16);
     a.nsi = (g.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
-    hipLaunchKernelGGL((k_sweep2<0, false, true>), dim3(nblk), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_sweep2<0, false, FUSE_R>), dim3(nblk), dim3(256), 0, st, a);
+    return nstr;
+}
+
+int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                               const double* rp, const double* shift, const Geo& gc, const double* ec,
+                               hipStream_t st) {
+    StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, nullptr, false);
+    a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0;
+    a.nsj = (g.ny + SW2X - 1) / SW2X;
+    a.L = strip_rows(a.nxl, a.nsj, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 16);
+    a.nsi = (g.nxl + a.L - 1) / a.L;
+    const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
+    hipLaunchKernelGGL((k_sweep2<0, false, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 
@@ -1474,7 +1511,7 @@ void launch_prolong(const Geo& gf, double* phi, const Geo& gc, const double* ec,
 size_t coarse_vcycle_bytes(const Geo& g) { return sizeof(double) * (size_t)lv_layout(g.nx, g.ny, nullptr, nullptr); }
 
 int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double* b, int cycles, int pre, int post,
-                         int citers, double comega, hipStream_t st) {
+                         int citers, double comega, double somega, hipStream_t st) {
     const size_t bytes = coarse_vcycle_bytes(g);
     if (bytes > 150 * 1024 || g.nxl != g.nx) return -1;
     static bool attr = false;
@@ -1483,7 +1520,7 @@ int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double*
         attr = true;
     }
     hipLaunchKernelGGL(k_coarse_vcycle, dim3(1), dim3(CV_THREADS), bytes, st, g, c, phi, b, cycles, pre, post, citers,
-                       comega);
+                       comega, somega);
     return 0;
 }
 

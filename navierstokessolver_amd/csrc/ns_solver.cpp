@@ -101,12 +101,16 @@ struct ns_solver {
     double ncells = 0;           // global cell count
     std::vector<hipEvent_t> ev;  // timing events (pairs)
     int helm_batch0 = 4, pois_batch0 = 8;
+    int helm_next = 4;           // first Helmholtz batch of the next step (adaptive unless check_every)
+    int helm_adapt = 1;
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
     int fuse_restrict = 1;       // NSGPU_FUSED_RESTRICT=0: separate k_restrict pass (A/B)
+    int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
+    int verbose = 0;             // NSGPU_VERBOSE=1: solver residual histories on stderr
     long pair_min_cells = 2048L * 2048L;   // NSGPU_PAIR_MIN_CELLS: smallest level smoothed in 2-sweep passes
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
     int mg_pre = 2, mg_post = 2, mg_coarse_iters = 0;
-    double mg_omega_c = 1.0, mg_omega_s = 1.0;
+    double mg_omega_c = 1.0, mg_omega_s = 1.1;
     bool mg_coarse_lds = false;
     ns_host_transport ht{};      // host transport (ht.exchange != NULL) instead of RCCL
     double* stage = nullptr;     // pinned staging for the host transport
@@ -218,21 +222,26 @@ int helm_sweep2(ns_solver* s, double alpha, double* part) {
     return nb;
 }
 
-// `n` Helmholtz sweeps: pairs in one pass each (ghost width 4), a single sweep for an odd
-// remainder.  Residual partials of the LAST launch's input go to `part_last`, of the first
-// launch's input to `part_first` (either may be null).  Returns the last launch's partial
-// count; *last_w = sweeps in the last launch.
+// `n` Helmholtz sweeps: pairs in one pass each (ghost width 4, 5 with a residual), a single
+// sweep for an odd remainder.  Residual partials of the LAST launch go to `part_last`, of the
+// first launch to `part_first` (either may be null): a pair reports the residual of its
+// output, a single sweep that of its input.  Returns the last launch's partial count;
+// *first_at / *last_at = the sweep count the reported residuals belong to.
 int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* part_last, int* nb_first,
-                int* last_w) {
+                int* first_at, int* last_at) {
     int nb = 0, k = 0, launch = 0;
     while (k < n) {
         const int w = (n - k >= 2 && !s->tiled) ? 2 : 1;
         const bool last = k + w >= n;
         double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
-        CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2 * w));
+        CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, w == 2 ? (part ? 5 : 4) : 2));
         nb = w == 2 ? helm_sweep2(s, alpha, part) : helm_sweep(s, alpha, part);
-        if (launch == 0 && nb_first) *nb_first = nb;
-        if (last) *last_w = w;
+        const int at = w == 2 ? k + 2 : k;
+        if (launch == 0) {
+            if (nb_first) *nb_first = nb;
+            if (first_at) *first_at = at;
+        }
+        if (last) *last_at = at;
         k += w;
         launch++;
     }
@@ -277,15 +286,19 @@ int next_batch(int prev_batch, double prev_r2, int prev_at, double r2, int at, d
 int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
     const double alpha = s->dt / (2 * s->re);
     const double tol2 = s->rtol * s->rtol;
-    int sweeps = 0, batch = s->helm_batch0, prev_at = -1;
+    // first batch: what the previous step needed (consecutive steps converge alike), so a
+    // step normally costs one residual check
+    int sweeps = 0, batch = s->helm_next, prev_at = -1;
     double prev_r2 = -1;
-    double* p0 = s->part + 2 * (size_t)nsg::max_partials(s->g) / 2;  // second half: first-sweep residuals
+    double first_r2 = -1, last_r2 = -1;   // max over u, v of r^2 / ||b||^2
+    int first_at = 0, last_at = 0;
+    double* p0 = s->part + 2 * (size_t)nsg::max_partials(s->g) / 2;  // second half: first-launch residuals
     for (;;) {
         const int n = std::min(batch, s->max_iters - sweeps);
         const bool first = sweeps == 0 && n > 2;
-        int nb0 = 0, lw = 1;
-        const int nb = helm_sweeps(s, alpha, n, first ? p0 : nullptr, s->part, &nb0, &lw);
-        (void)nb0;
+        int nb0 = 0, at0 = 0, at = 0;
+        const int nb = helm_sweeps(s, alpha, n, first ? p0 : nullptr, s->part, &nb0, &at0, &at);
+        at += sweeps;
         sweeps += n;
         nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
         nsg::launch_reduce_sum(s->part + nb, nb, 1, s->scal + S_RES + 1, s->st);
@@ -302,18 +315,39 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         *resu = bu > 0 ? std::sqrt(r2u / bu) : std::sqrt(r2u);
         *resv = bv > 0 ? std::sqrt(r2v / bv) : std::sqrt(r2v);
         if (!std::isfinite(r2u) || !std::isfinite(r2v)) { set_err("Helmholtz residual is not finite"); *its = sweeps; return NS_EDIVERGE; }
-        if (ok || sweeps >= s->max_iters) break;
-        const double r2 = std::max(r2u / std::max(bu, 1e-300), r2v / std::max(bv, 1e-300));
-        if (first) {  // residual of the initial guess (input of sweep 1) -> contraction rate
-            prev_r2 = std::max(s->hs[S_AUX] / std::max(bu, 1e-300), s->hs[S_AUX + 1] / std::max(bv, 1e-300));
-            prev_at = 0;
+        if (s->verbose) {
+            if (first)
+                fprintf(stderr, "nsgpu helmholtz: after %d sweeps rel. residual u %.3e v %.3e\n", at0,
+                        std::sqrt(s->hs[S_AUX] / std::max(bu, 1e-300)), std::sqrt(s->hs[S_AUX + 1] / std::max(bv, 1e-300)));
+            fprintf(stderr, "nsgpu helmholtz: after %d sweeps rel. residual u %.3e v %.3e\n", at, *resu, *resv);
         }
-        const int nbatch = next_batch(batch, prev_r2, prev_at, r2, sweeps - lw, tol2, s->max_iters);
+        const double r2 = std::max(r2u / std::max(bu, 1e-300), r2v / std::max(bv, 1e-300));
+        if (first) {
+            first_r2 = std::max(s->hs[S_AUX] / std::max(bu, 1e-300), s->hs[S_AUX + 1] / std::max(bv, 1e-300));
+            first_at = at0;
+        }
+        last_r2 = r2;
+        last_at = at;
+        if (ok || sweeps >= s->max_iters) break;
+        if (first) {  // residual after the first launch -> contraction rate
+            prev_r2 = std::max(s->hs[S_AUX] / std::max(bu, 1e-300), s->hs[S_AUX + 1] / std::max(bv, 1e-300));
+            prev_at = at0;
+        }
+        const int nbatch = next_batch(batch, prev_r2, prev_at, r2, at, tol2, s->max_iters) - (sweeps - at);
         prev_r2 = r2;
-        prev_at = sweeps - lw;
-        batch = nbatch + (nbatch & 1);  // even batches: whole 2-sweep passes
+        prev_at = at;
+        batch = std::max(nbatch + (nbatch & 1), 2);  // even batches: whole 2-sweep passes
     }
     *its = sweeps;
+    // next step's first batch: the sweeps this step's measured contraction says suffice
+    // (from the first launch's residual), else the sweeps it took
+    int need = sweeps;
+    if (s->helm_adapt && first_r2 > 0 && last_r2 > 0 && last_r2 < first_r2 && last_at > first_at) {
+        const double rate = std::log(last_r2 / first_r2) / (double)(last_at - first_at);
+        const double more = std::log(tol2 / first_r2) / rate;
+        if (std::isfinite(more)) need = std::min(sweeps, first_at + std::max(0, (int)std::ceil(more)));
+    }
+    s->helm_next = s->helm_adapt ? std::max(2, need + (need & 1)) : s->helm_batch0;
     return 0;
 }
 
@@ -390,6 +424,12 @@ bool fused_restrict(const ns_solver* s, int l) {
     return s->fuse_restrict && pair_level(s, l) && s->mg_pre >= 2 && s->mg_pre % 2 == 0;
 }
 
+// the prolongation rides on the first two post-smoothing sweeps (k_sweep2 FUSE_P);
+// NSGPU_FUSED_PROLONG=0 keeps the separate k_prolong pass
+bool fused_prolong(const ns_solver* s, int l) {
+    return s->fuse_prolong && pair_level(s, l) && s->mg_post >= 2;
+}
+
 int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
     MgLevel& L = level(s, l);
     for (int k = 0; k < n;) {
@@ -412,7 +452,7 @@ int mg_coarse(ns_solver* s) {
     MgLevel& L = level(s, (int)s->lv.size() - 1);
     if (s->mg_coarse_lds) {
         if (nsg::launch_coarse_vcycle(L.g, L.c, L.phi, L.b, 1, s->mg_pre, s->mg_post, s->mg_coarse_iters,
-                                      s->mg_omega_c, s->st) != 0) {
+                                      s->mg_omega_c, s->mg_omega_s, s->st) != 0) {
             set_err("coarse LDS V-cycle does not fit");
             return NS_EINVAL;
         }
@@ -473,6 +513,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
                 }
                 const double r2 = s->hs[S_RES], b2 = s->hs[S_SHIFT + 1];
                 *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
+                if (s->verbose) fprintf(stderr, "nsgpu poisson: cycle %d rel. residual after pre-smoothing %.3e\n", cycles, *res);
                 if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = cycles; return NS_EDIVERGE; }
                 if (r2 <= tol2 * b2 || r2 == 0.0 || cycles >= maxc) done = true;
             }
@@ -482,9 +523,23 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
         for (int l = nl - 2; l >= 0; l--) {
             MgLevel& F = level(s, l);
             MgLevel& C = level(s, l + 1);
-            CHK(halo_g(s, C.g, {C.phi}, 1));
-            nsg::launch_prolong(F.g, F.phi, C.g, C.phi, s->st);
-            CHK(mg_smooth(s, l, s->mg_post, &tn, ev0));
+            if (fused_prolong(s, l)) {
+                // prolongation + the first two post-smoothing sweeps in one HBM pass
+                CHK(halo_g(s, C.g, {C.phi}, 3));
+                CHK(halo_g(s, F.g, {F.phi}, 5));
+                const bool t = s->timing && l == 0;
+                if (t) HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn)], s->st));
+                nsg::launch_pois_rbsor2_prolong(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b,
+                                                l == 0 ? s->scal + S_SHIFT : nullptr, C.g, C.phi, s->st);
+                if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn) + 1], s->st)); tn++; }
+                std::swap(F.phi, F.tmp);
+                if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
+                CHK(mg_smooth(s, l, s->mg_post - 2, &tn, ev0));
+            } else {
+                CHK(halo_g(s, C.g, {C.phi}, 1));
+                nsg::launch_prolong(F.g, F.phi, C.g, C.phi, s->st);
+                CHK(mg_smooth(s, l, s->mg_post, &tn, ev0));
+            }
         }
         cycles++;
     }
@@ -761,9 +816,13 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     }
     s->check_every = p->check_every;
     if (p->check_every > 0) s->pois_batch0 = s->helm_batch0 = p->check_every;
+    s->helm_next = s->helm_batch0;
+    s->helm_adapt = p->check_every <= 0;
     s->timing = p->timing;
     if (const char* e = getenv("NSGPU_SWEEP")) s->tiled = std::strcmp(e, "tiled") == 0;
     if (const char* e = getenv("NSGPU_FUSED_RESTRICT")) s->fuse_restrict = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     {
         const char* e = getenv("NSGPU_STRIP_ROWS");  // tuning override; unset = adaptive
@@ -805,6 +864,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     }
     if (s->poisson == NS_POISSON_MG) {
         if (p->mg_pre > 0) s->mg_pre = p->mg_pre;
+        if (p->mg_omega > 0) s->mg_omega_s = p->mg_omega;
+        if (const char* e = getenv("NSGPU_MG_OMEGA")) s->mg_omega_s = std::atof(e);   // smoother over-relaxation (A/B)
         if (p->mg_post > 0) s->mg_post = p->mg_post;
         if (int rc = build_levels(s, hx0, hy0)) return fail(rc);
         if (p->mg_coarse_iters > 0) s->mg_coarse_iters = p->mg_coarse_iters;
@@ -859,7 +920,7 @@ int ns_step(ns_solver* s, ns_stats* out) {
     CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
     // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
-    CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 3));       // rhs ghost rows: the fused sweep's ring reds
+    CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));       // rhs ghost rows: a checked pair pass reads ib-4
     CHK(helm_solve(s, &st.it_u, &st.res_u, &st.res_v));            // KSPSolve(uSolver) x2 (:547-548)
     st.it_v = st.it_u;
     CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
@@ -935,7 +996,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
     case NS_K_HELMHOLTZ: {
         // (iters-1)/2 two-sweep passes, then single sweeps; the residual is of the last sweep's input
         int nb = 0;
-        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 3));
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
         const int pairs = iters > 0 ? (iters - 1) / 2 : 0;
         for (int k = 0; k < pairs; k++) {
             CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 4));
@@ -993,7 +1054,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         int its = 0;
         double ru = 0, rv = 0;
         CHK(helm_bnorm(s));
-        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 3));
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
         CHK(helm_solve(s, &its, &ru, &rv));
         if (out) { out[0] = its; out[1] = std::max(ru, rv); }
         return 0;
@@ -1068,7 +1129,7 @@ int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
             pois_sweep(s, part);
             return 0;
         }
-        CHK(halo(s, {s->arr[NS_ARR_PHI]}, 4));
+        CHK(halo(s, {s->arr[NS_ARR_PHI]}, part ? 5 : 4));
         nsg::launch_pois_rbsor2(s->g, s->c, s->omega, s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP], s->arr[NS_ARR_RPHI],
                                 s->scal + S_SHIFT, part, s->st);
         std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);

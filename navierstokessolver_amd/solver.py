@@ -3,6 +3,7 @@ the reference-compatible host API is the C++ Grid / FluidSolver in host/."""
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -45,7 +46,7 @@ class GpuSolver:
     def __init__(self, grid: GridSpec, dt: float, re: float, *, poisson=L.NS_POISSON_MG, rtol=1e-8,
                  max_iters=0, omega=0.0, omega_v=0.0, check_every=0, device=-1, timing=False,
                  rank=0, nranks=1, nccl_id: bytes | None = None, mg_pre=0, mg_post=0, mg_coarse_iters=0,
-                 host_transport=None):
+                 host_transport=None, mg_omega=0.0):
         self.grid = grid
         self.hx = np.ascontiguousarray(grid.hx, dtype=np.float64)
         self.hy = np.ascontiguousarray(grid.hy, dtype=np.float64)
@@ -57,7 +58,8 @@ class GpuSolver:
                          1 if timing else 0, rank, nranks,
                          ctypes.cast(self._nccl, ctypes.c_void_p) if self._nccl is not None else None,
                          mg_pre, mg_post, mg_coarse_iters,
-                         ctypes.pointer(host_transport.struct) if host_transport is not None else None)
+                         ctypes.pointer(host_transport.struct) if host_transport is not None else None,
+                         mg_omega)
         self._transport = host_transport  # keep the callbacks alive
         h = ctypes.c_void_p()
         L.check(L.lib().ns_create(ctypes.byref(desc), ctypes.byref(prm), ctypes.byref(h)))
@@ -73,6 +75,8 @@ class GpuSolver:
             rho = t / (1 + t)
             self.omega_v = 2 / (1 + (1 - rho * rho) ** 0.5)
         self.shape = (self.i1 - self.i0, self.hy.size)
+        # the multigrid smoother's over-relaxation (ns_create: 1.1 unless given; NSGPU_MG_OMEGA wins)
+        self.mg_omega = float(os.environ.get("NSGPU_MG_OMEGA", mg_omega if mg_omega > 0 else 1.1))
 
     # ---- lifecycle
     def close(self):

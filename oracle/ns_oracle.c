@@ -919,6 +919,11 @@ void og_mg_restrict(int nx, int ny, const double* hx, const double* hy, const do
 }
 
 int og_mg_solve(const og_grid* g, double* rhs, double* x, double rtol, int pre, int post, int maxcycles) {
+    return og_mg_solve_w(g, rhs, x, rtol, pre, post, maxcycles, 1.0);
+}
+
+int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre, int post, int maxcycles,
+                  double omega) {
     if (!rect_dirichlet(g)) { set_err("multigrid needs a rectangle with Dirichlet-type faces"); return -1; }
     const int N = g->N;
     double m = 0.0, b2 = 0.0;
@@ -939,7 +944,7 @@ int og_mg_solve(const og_grid* g, double* rhs, double* x, double rtol, int pre, 
         const double* bf = rhs;
         int done = 0;
         for (int l = 0; l < nl - 1; l++) {
-            for (int k = 0; k < pre; k++) mg_rb(&L[l], xf, bf, 0.0, 1.0);
+            for (int k = 0; k < pre; k++) mg_rb(&L[l], xf, bf, 0.0, omega);
             const double r2 = mg_restrict_lv(&L[l], xf, bf, 0.0, &L[l + 1], L[l + 1].b);
             memset(L[l + 1].x, 0, sizeof(double) * (size_t)L[l + 1].nx * L[l + 1].ny);
             if (l == 0 && (r2 <= rtol * rtol * b2 || r2 == 0.0 || cycles >= maxcycles)) { done = 1; break; }
@@ -952,7 +957,7 @@ int og_mg_solve(const og_grid* g, double* rhs, double* x, double rtol, int pre, 
             double* xl = l == 0 ? x : L[l].x;
             const double* bl = l == 0 ? rhs : L[l].b;
             og_mg_prolong(L[l].nx, L[l].ny, L[l + 1].x, xl);
-            for (int k = 0; k < post; k++) mg_rb(&L[l], xl, bl, 0.0, 1.0);
+            for (int k = 0; k < post; k++) mg_rb(&L[l], xl, bl, 0.0, omega);
         }
         cycles++;
     }
@@ -967,7 +972,7 @@ struct og_solver {
     og_grid* g;
     double dt, re, rtol;
     int gpu_alg;
-    double omega_v;
+    double omega_v, omega_mg;
     double *u, *v, *phi, *cu, *cv, *gx, *gy, *ru, *rv, *us, *vs, *rp;
 };
 
@@ -980,9 +985,10 @@ og_solver* og_solver_new(og_grid* g, double dt, double re, double rtol) {
     return s;
 }
 
-void og_solver_set_algorithm(og_solver* s, int gpu_algorithm, double omega_v) {
+void og_solver_set_algorithm(og_solver* s, int gpu_algorithm, double omega_v, double omega_mg) {
     s->gpu_alg = gpu_algorithm;
     s->omega_v = omega_v;
+    s->omega_mg = omega_mg;
 }
 
 void og_solver_free(og_solver* s) {
@@ -1019,7 +1025,7 @@ int og_solver_step(og_solver* s, double* mm, int* its) {
         } while (iu < maxit);
         iv = iu;
         og_divergence(g, s->dt, s->us, s->vs, s->rp);
-        ip = og_mg_solve(g, s->rp, s->phi, s->rtol, 2, 2, 1000);
+        ip = og_mg_solve_w(g, s->rp, s->phi, s->rtol, 2, 2, 1000, s->omega_mg);
     } else {
         /* KSPSolve(uSolver, ...) x2 with zero initial guess (:547-548) */
         memset(s->us, 0, sizeof(double) * n);

@@ -110,13 +110,17 @@ void og_mg_prolong(int nx, int ny, const double* ec, double* phi);
  * coarsest level by red-black SOR (2n+10 iterations at the optimal omega); stops when the residual after pre-smoothing is
  * <= rtol * ||rhs||.  Returns V-cycles. */
 int og_mg_solve(const og_grid* g, double* rhs, double* x, double rtol, int pre, int post, int maxcycles);
+/* the same with the smoother over-relaxed by omega (the GPU path's default is 1.1) */
+int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre, int post, int maxcycles,
+                  double omega);
 
 /* ---- full time stepper (FluidSolver::Solve, FluidSolver.cpp:536-567) ---- */
 og_solver* og_solver_new(og_grid* g, double dt, double re, double rtol);
 void og_solver_free(og_solver* s);
 /* algorithm: 0 = Krylov solves (the reference's kind, default); 1 = the GPU path's
- * algorithm (red-black SOR Helmholtz with omega_v, multigrid Poisson) */
-void og_solver_set_algorithm(og_solver* s, int gpu_algorithm, double omega_v);
+ * algorithm (red-black SOR Helmholtz with omega_v, multigrid Poisson V(2,2) with the
+ * red-black smoother over-relaxed by omega_mg) */
+void og_solver_set_algorithm(og_solver* s, int gpu_algorithm, double omega_v, double omega_mg);
 /* one time step; mm = {umin, umax, vmin, vmax}; its = {it_u, it_v, it_phi} */
 int  og_solver_step(og_solver* s, double* mm, int* its);
 /* get / set state: u, v, phi, cu0, cv0, gx, gy (divPhi) -- any pointer may be NULL */

@@ -39,7 +39,9 @@ _SIG = {
     "og_mg_restrict": (None, [ctypes.c_int, ctypes.c_int, _D, _D, _D, _D, ctypes.c_double, _D]),
     "og_mg_prolong": (None, [ctypes.c_int, ctypes.c_int, _D, _D]),
     "og_mg_solve": (ctypes.c_int, [_P, _D, _D, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
-    "og_solver_set_algorithm": (None, [_P, ctypes.c_int, ctypes.c_double]),
+    "og_mg_solve_w": (ctypes.c_int, [_P, _D, _D, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_double]),
+    "og_solver_set_algorithm": (None, [_P, ctypes.c_int, ctypes.c_double, ctypes.c_double]),
     "og_solver_new": (_P, [_P, ctypes.c_double, ctypes.c_double, ctypes.c_double]),
     "og_solver_free": (None, [_P]),
     "og_solver_step": (ctypes.c_int, [_P, _D, _I]),
@@ -176,10 +178,10 @@ class OGrid:
         lib().og_mg_prolong(self.nx, self.ny, _d(_f(ec)), _d(p))
         return p
 
-    def mg_solve(self, rhs, x0=None, rtol=1e-10, pre=2, post=2, maxcycles=1000):
+    def mg_solve(self, rhs, x0=None, rtol=1e-10, pre=2, post=2, maxcycles=1000, omega=1.0):
         b = _f(rhs).copy()
         x = self.z() if x0 is None else _f(x0).copy()
-        cyc = lib().og_mg_solve(self.h, _d(b), _d(x), rtol, pre, post, maxcycles)
+        cyc = lib().og_mg_solve_w(self.h, _d(b), _d(x), rtol, pre, post, maxcycles, omega)
         if cyc < 0:
             raise ValueError(lib().og_last_error().decode())
         return x, cyc
@@ -205,9 +207,9 @@ class OSolver:
         except Exception:
             pass
 
-    def use_gpu_algorithm(self, omega_v):
+    def use_gpu_algorithm(self, omega_v, omega_mg=1.1):
         """RB-SOR Helmholtz + multigrid Poisson (the GPU path's algorithm; CPU baseline)."""
-        lib().og_solver_set_algorithm(self.h, 1, omega_v)
+        lib().og_solver_set_algorithm(self.h, 1, omega_v, omega_mg)
 
     def step(self):
         mm = np.zeros(4)

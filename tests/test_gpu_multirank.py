@@ -52,6 +52,9 @@ def test_two_slabs_host_transport_match_single_rank(tmp_path, monkeypatch, poiss
     assert np.max(np.abs(r["u"] - u)) <= tol
     assert np.max(np.abs(r["v"] - v)) <= tol
     np.testing.assert_allclose(r["mm"][:, :4], mm[:, :4], atol=tol)
+    # Helmholtz sweeps per step: the slabs' residual checks see the same residual as the
+    # whole grid (a stale ghost row shows up as a solve that never reaches its tolerance)
+    assert np.max(np.abs(r["mm"][:, 4] - mm[:, 4])) <= 2, (r["mm"][:, 4], mm[:, 4])
 
 
 def test_rccl_two_ranks_one_gpu_probe(tmp_path):

@@ -332,24 +332,27 @@ def test_two_sweep_pass_equals_two_sweeps(gpu, nx, ny, op):
 
 
 @pytest.mark.parametrize("nx,ny", [(256, 192), (96, 160)])
-def test_fused_restriction_pass_matches_separate_restrict(gpu, monkeypatch, nx, ny):
-    """The last pre-smoothing pass with the restriction fused in (k_sweep2<XR>) gives the same
-    V-cycles as two sweeps + k_restrict, and the oracle's solution.  NSGPU_PAIR_MIN_CELLS=0
-    makes every level use the two-sweep passes (production: levels >= 2048^2 only)."""
+def test_fused_transfer_passes_match_separate_transfers(gpu, monkeypatch, nx, ny):
+    """The last pre-smoothing pass with the restriction fused in (k_sweep2 FUSE_R) and the first
+    post-smoothing pass with the prolongation fused in (FUSE_P) give the same V-cycles as
+    sweeps + k_restrict / k_prolong, and the oracle's solution.  NSGPU_PAIR_MIN_CELLS=0 makes
+    every level use the two-sweep passes (production: levels >= 2048^2 only)."""
     rng = np.random.default_rng(23)
     b = rand(rng, nx * ny, 100.0)
     out = {}
     monkeypatch.setenv("NSGPU_PAIR_MIN_CELLS", "0")
-    for fused in ("1", "0"):
-        monkeypatch.setenv("NSGPU_FUSED_RESTRICT", fused)
+    for fr, fp in (("1", "1"), ("0", "0"), ("1", "0"), ("0", "1")):
+        monkeypatch.setenv("NSGPU_FUSED_RESTRICT", fr)
+        monkeypatch.setenv("NSGPU_FUSED_PROLONG", fp)
         og, gs = pair(gpu, nx, ny, 1e-3, 100.0, poisson=gpu.NS_POISSON_MG, rtol=1e-11)
         gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny)); gs.set(gpu.NS_ARR_RPHI, b)
         its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
-        out[fused] = (its, res, gs.get(gpu.NS_ARR_PHI).ravel())
+        out[fr + fp] = (its, res, gs.get(gpu.NS_ARR_PHI).ravel())
         gs.close()
-    assert out["1"][0] == out["0"][0]
-    assert out["1"][1] <= 1e-11
-    assert rel(out["1"][2], out["0"][2]) <= 1e-12
+    for k in ("11", "10", "01"):
+        assert out[k][0] == out["00"][0], (k, out[k][0], out["00"][0])
+        assert out[k][1] <= 1e-11
+        assert rel(out[k][2], out["00"][2]) <= 1e-12
     xp, _ = og.solve_poisson(b)
-    g = out["1"][2]
+    g = out["11"][2]
     assert rel(g - g.mean(), xp - xp.mean()) <= 1e-8
