@@ -80,6 +80,14 @@ struct MgLevel {
     double* mem = nullptr;                               // planes (levels >= 1)
     double* coef = nullptr;                              // coefficient tables (levels >= 1)
     std::vector<double> hx, hy;                          // host spacings
+    int minrows = 0;                                     // fewest rows any rank holds of this level
+    // coarse-level agglomeration (nranks > 1): a replicated level lives WHOLE on every rank
+    // (g.i0 = 0, g.nxl = g.nx) and is smoothed with no exchange.  The first replicated level
+    // is reached from the last distributed one through this rank's slab of it (gs) and
+    // gathered (every rank's rows si0[q] .. si0[q] + sn[q]) after the restriction.
+    bool repl = false;
+    nsg::Geo gs{};
+    std::vector<int> si0, sn;
 };
 
 struct ns_solver {
@@ -128,43 +136,70 @@ int ensure_stage(ns_solver* s, size_t n) {
     return 0;
 }
 
-// ghost rows of width w (contiguous: w * ld doubles) to / from the x-neighbours
-int halo_g(ns_solver* s, const nsg::Geo& g, std::initializer_list<double*> fields, int w) {
+// one ghost-row request: `w` rows (contiguous: w * ld doubles) of field f on level geometry g
+struct HaloReq {
+    const nsg::Geo* g;
+    double* f;
+    int w;
+};
+
+// ghost rows to / from the x-neighbours; every request of the list goes in ONE RCCL group
+// (one latency for all of them)
+int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq) {
     if (s->nranks == 1) return 0;
-    const size_t cnt = (size_t)w * g.ld;
-    const int ld = g.ld, nxl = g.nxl;
     const bool lo = s->rank > 0, hi = s->rank < s->nranks - 1;
     if (s->ht.exchange) {
-        CHK(ensure_stage(s, 4 * cnt));
-        double *slo = s->stage, *shi = slo + cnt, *rlo = shi + cnt, *rhi = rlo + cnt;
-        for (double* f : fields) {
+        for (int k = 0; k < nreq; k++) {
+            const HaloReq& q = reqs[k];
+            const size_t cnt = (size_t)q.w * q.g->ld;
+            const int ld = q.g->ld, nxl = q.g->nxl;
+            double* f = q.f;
+            CHK(ensure_stage(s, 4 * cnt));
+            double *slo = s->stage, *shi = slo + cnt, *rlo = shi + cnt, *rhi = rlo + cnt;
             if (lo) HIPCHK(hipMemcpyAsync(slo, f, cnt * 8, hipMemcpyDeviceToHost, s->st));
-            if (hi) HIPCHK(hipMemcpyAsync(shi, f + (ptrdiff_t)(nxl - w) * ld, cnt * 8, hipMemcpyDeviceToHost, s->st));
+            if (hi) HIPCHK(hipMemcpyAsync(shi, f + (ptrdiff_t)(nxl - q.w) * ld, cnt * 8, hipMemcpyDeviceToHost, s->st));
             HIPCHK(hipStreamSynchronize(s->st));
             if (s->ht.exchange(s->ht.user, lo ? slo : nullptr, hi ? shi : nullptr, lo ? rlo : nullptr,
                                hi ? rhi : nullptr, (int64_t)cnt) != 0) {
                 set_err("host transport exchange failed");
                 return NS_ERCCL;
             }
-            if (lo) HIPCHK(hipMemcpyAsync(f - (ptrdiff_t)w * ld, rlo, cnt * 8, hipMemcpyHostToDevice, s->st));
+            if (lo) HIPCHK(hipMemcpyAsync(f - (ptrdiff_t)q.w * ld, rlo, cnt * 8, hipMemcpyHostToDevice, s->st));
             if (hi) HIPCHK(hipMemcpyAsync(f + (ptrdiff_t)nxl * ld, rhi, cnt * 8, hipMemcpyHostToDevice, s->st));
             HIPCHK(hipStreamSynchronize(s->st));
         }
         return 0;
     }
     NCCLCHK(ncclGroupStart());
-    for (double* f : fields) {
+    for (int k = 0; k < nreq; k++) {
+        const HaloReq& q = reqs[k];
+        const size_t cnt = (size_t)q.w * q.g->ld;
+        const int ld = q.g->ld, nxl = q.g->nxl;
+        double* f = q.f;
         if (lo) {
             NCCLCHK(ncclSend(f, cnt, ncclDouble, s->rank - 1, s->comm, s->st));
-            NCCLCHK(ncclRecv(f - (ptrdiff_t)w * ld, cnt, ncclDouble, s->rank - 1, s->comm, s->st));
+            NCCLCHK(ncclRecv(f - (ptrdiff_t)q.w * ld, cnt, ncclDouble, s->rank - 1, s->comm, s->st));
         }
         if (hi) {
-            NCCLCHK(ncclSend(f + (ptrdiff_t)(nxl - w) * ld, cnt, ncclDouble, s->rank + 1, s->comm, s->st));
+            NCCLCHK(ncclSend(f + (ptrdiff_t)(nxl - q.w) * ld, cnt, ncclDouble, s->rank + 1, s->comm, s->st));
             NCCLCHK(ncclRecv(f + (ptrdiff_t)nxl * ld, cnt, ncclDouble, s->rank + 1, s->comm, s->st));
         }
     }
     NCCLCHK(ncclGroupEnd());
     return 0;
+}
+
+int halo_reqs(ns_solver* s, std::initializer_list<HaloReq> reqs) {
+    return halo_reqs(s, reqs.begin(), (int)reqs.size());
+}
+
+int halo_g(ns_solver* s, const nsg::Geo& g, std::initializer_list<double*> fields, int w) {
+    if (s->nranks == 1) return 0;
+    HaloReq r[4];
+    int n = 0;
+    for (double* f : fields)
+        if (n < 4) r[n++] = HaloReq{&g, f, w};
+    return halo_reqs(s, r, n);
 }
 
 int halo(ns_solver* s, std::initializer_list<double*> fields, int w) { return halo_g(s, s->g, fields, w); }
@@ -409,13 +444,23 @@ MgLevel& level(ns_solver* s, int l) {
     return L;
 }
 
+// ghost rows of level l (nothing to exchange on a replicated level)
+int halo_l(ns_solver* s, int l, std::initializer_list<double*> fields, int w) {
+    if (s->lv[l].repl) return 0;
+    return halo_g(s, s->lv[l].g, fields, w);
+}
+
 // levels whose smoothing runs as two-sweep passes: the HBM-bound ones (>= 2048^2 local
 // cells); the coarser ones are latency-bound and the fused pass's deeper row pipeline only
-// costs there (tools/sweep_levels2.py: 512^2 9.5 us/sweep fused vs 8.1 single)
+// costs there (tools/sweep_levels2.py: 512^2 9.5 us/sweep fused vs 8.1 single).  A
+// distributed level always pairs (one exchange per two sweeps) when every rank's slab can
+// feed the 5-row ghost exchange from ONE neighbour -- decided on the global minimum, so
+// every rank makes the same choice (the exchange sizes must match).
 bool pair_level(const ns_solver* s, int l) {
-    const nsg::Geo& g = s->lv[l].g;
-    if (s->tiled || (s->nranks > 1 && g.nxl < nsg::HALO)) return false;   // ghost rows come from ONE neighbour
-    return (long)g.nxl * g.ny >= s->pair_min_cells;
+    const MgLevel& L = s->lv[l];
+    if (s->tiled) return false;
+    if (s->nranks > 1 && !L.repl) return L.minrows >= nsg::HALO;
+    return (long)L.g.nxl * L.g.ny >= s->pair_min_cells;
 }
 
 // the last two pre-smoothing sweeps of level l carry the restriction (k_sweep2<XR>);
@@ -430,11 +475,62 @@ bool fused_prolong(const ns_solver* s, int l) {
     return s->fuse_prolong && pair_level(s, l) && s->mg_post >= 2;
 }
 
+// level l+1 as level l's restriction target / prolongation source: the first replicated
+// level is seen through this rank's slab of it (rows gs.i0 .. of the whole level)
+struct CoarseView {
+    nsg::Geo g;
+    double *b, *phi;
+    bool gather;   // the distributed -> replicated transition
+};
+CoarseView coarse_view(ns_solver* s, int l) {
+    const MgLevel& F = s->lv[l];
+    MgLevel& C = s->lv[l + 1];
+    if (C.repl && !F.repl) {
+        const ptrdiff_t off = (ptrdiff_t)C.gs.i0 * C.g.ld;
+        return CoarseView{C.gs, C.b + off, C.phi + off, true};
+    }
+    return CoarseView{C.g, C.b, C.phi, false};
+}
+
+// agglomeration: every rank's slab of the first replicated level's rhs to every rank, and
+// that level's iterate zeroed whole (the restriction zeroed only this rank's rows).  RCCL:
+// one group of point-to-point copies (slabs may differ by a row, so not ncclAllGather);
+// host transport: an exact sum-allreduce of the level with every foreign row zeroed.
+int gather_level(ns_solver* s, MgLevel& C) {
+    const size_t ld = C.g.ld;
+    HIPCHK(hipMemsetAsync(C.phi - (ptrdiff_t)nsg::HALO * ld, 0,
+                          (size_t)(C.g.nx + 2 * nsg::HALO) * ld * sizeof(double), s->st));
+    if (s->ht.allreduce) {
+        const size_t n = (size_t)C.g.nx * ld;
+        if (n > (size_t)INT32_MAX) { set_err("agglomerated level too large for the host transport"); return NS_EINVAL; }
+        CHK(ensure_stage(s, n));
+        HIPCHK(hipMemcpyAsync(s->stage, C.b, n * 8, hipMemcpyDeviceToHost, s->st));
+        HIPCHK(hipStreamSynchronize(s->st));
+        const size_t r0 = (size_t)C.gs.i0 * ld, r1 = r0 + (size_t)C.gs.nxl * ld;
+        std::fill(s->stage, s->stage + r0, 0.0);
+        std::fill(s->stage + r1, s->stage + n, 0.0);
+        if (s->ht.allreduce(s->ht.user, s->stage, (int32_t)n, 0) != 0) {
+            set_err("host transport allreduce failed");
+            return NS_ERCCL;
+        }
+        HIPCHK(hipMemcpyAsync(C.b, s->stage, n * 8, hipMemcpyHostToDevice, s->st));
+        return 0;
+    }
+    NCCLCHK(ncclGroupStart());
+    for (int q = 0; q < s->nranks; q++) {
+        if (q == s->rank) continue;
+        NCCLCHK(ncclSend(C.b + (ptrdiff_t)C.gs.i0 * ld, (size_t)C.gs.nxl * ld, ncclDouble, q, s->comm, s->st));
+        NCCLCHK(ncclRecv(C.b + (ptrdiff_t)C.si0[q] * ld, (size_t)C.sn[q] * ld, ncclDouble, q, s->comm, s->st));
+    }
+    NCCLCHK(ncclGroupEnd());
+    return 0;
+}
+
 int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
     MgLevel& L = level(s, l);
     for (int k = 0; k < n;) {
         const int w = (n - k >= 2 && pair_level(s, l)) ? 2 : 1;   // two sweeps per HBM pass
-        CHK(halo_g(s, L.g, {L.phi}, 2 * w));
+        CHK(halo_l(s, l, {L.phi}, 2 * w));
         const bool t = s->timing && l == 0;
         if (t) HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st));
         const double* sh = l == 0 ? s->scal + S_SHIFT : nullptr;
@@ -449,7 +545,8 @@ int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
 }
 
 int mg_coarse(ns_solver* s) {
-    MgLevel& L = level(s, (int)s->lv.size() - 1);
+    const int l = (int)s->lv.size() - 1;
+    MgLevel& L = level(s, l);
     if (s->mg_coarse_lds) {
         if (nsg::launch_coarse_vcycle(L.g, L.c, L.phi, L.b, 1, s->mg_pre, s->mg_post, s->mg_coarse_iters,
                                       s->mg_omega_c, s->mg_omega_s, s->st) != 0) {
@@ -459,7 +556,7 @@ int mg_coarse(ns_solver* s) {
         return 0;
     }
     for (int k = 0; k < s->mg_coarse_iters; k++) {
-        CHK(halo_g(s, L.g, {L.phi}, 2));
+        CHK(halo_l(s, l, {L.phi}, 2));
         nsg::launch_pois_rbsor(L.g, L.c, s->mg_omega_c, L.phi, L.tmp, L.b, nullptr, nullptr, s->st);
         std::swap(L.phi, L.tmp);
     }
@@ -480,22 +577,22 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
         for (int l = 0; l < nl - 1 && !done; l++) {
             MgLevel& F = level(s, l);
             MgLevel& C = level(s, l + 1);
+            const CoarseView cv = coarse_view(s, l);
             const double* sh = l == 0 ? s->scal + S_SHIFT : nullptr;
             int nb;
             if (fused_restrict(s, l)) {
                 // last two pre-smoothing sweeps + residual + restriction in one HBM pass
                 CHK(mg_smooth(s, l, s->mg_pre - 2, &tn, ev0));
-                CHK(halo_g(s, F.g, {F.phi}, 5));
-                nb = nsg::launch_pois_rbsor2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, C.g, C.b, C.phi,
-                                                      s->part, s->st);
+                CHK(halo_l(s, l, {F.phi}, 5));
+                nb = nsg::launch_pois_rbsor2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b,
+                                                      cv.phi, s->part, s->st);
                 std::swap(F.phi, F.tmp);
                 if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
             } else {
                 CHK(mg_smooth(s, l, s->mg_pre, &tn, ev0));
-                CHK(halo_g(s, F.g, {F.phi}, 1));
-                nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, sh, C.g, C.c, C.b, C.phi, s->part, s->st);
+                CHK(halo_l(s, l, {F.phi}, 1));
+                nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, sh, cv.g, C.c, cv.b, cv.phi, s->part, s->st);
             }
-            CHK(halo_g(s, C.g, {C.b}, 4));
             if (l == 0) {
                 // fine residual after pre-smoothing: the convergence test (one host sync per cycle)
                 nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
@@ -517,27 +614,34 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
                 if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = cycles; return NS_EDIVERGE; }
                 if (r2 <= tol2 * b2 || r2 == 0.0 || cycles >= maxc) done = true;
             }
+            if (done) break;
+            if (cv.gather) CHK(gather_level(s, C));
+            else CHK(halo_l(s, l + 1, {C.b}, 4));
         }
         if (done) break;
         CHK(mg_coarse(s));
         for (int l = nl - 2; l >= 0; l--) {
             MgLevel& F = level(s, l);
             MgLevel& C = level(s, l + 1);
+            const CoarseView cv = coarse_view(s, l);
             if (fused_prolong(s, l)) {
-                // prolongation + the first two post-smoothing sweeps in one HBM pass
-                CHK(halo_g(s, C.g, {C.phi}, 3));
-                CHK(halo_g(s, F.g, {F.phi}, 5));
+                // prolongation + the first two post-smoothing sweeps in one HBM pass; the coarse
+                // and fine ghost rows travel in one group
+                if (!F.repl) {
+                    if (cv.gather || C.repl) CHK(halo_l(s, l, {F.phi}, 5));
+                    else CHK(halo_reqs(s, {HaloReq{&C.g, C.phi, 3}, HaloReq{&F.g, F.phi, 5}}));
+                }
                 const bool t = s->timing && l == 0;
                 if (t) HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn)], s->st));
                 nsg::launch_pois_rbsor2_prolong(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b,
-                                                l == 0 ? s->scal + S_SHIFT : nullptr, C.g, C.phi, s->st);
+                                                l == 0 ? s->scal + S_SHIFT : nullptr, cv.g, cv.phi, s->st);
                 if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn) + 1], s->st)); tn++; }
                 std::swap(F.phi, F.tmp);
                 if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
                 CHK(mg_smooth(s, l, s->mg_post - 2, &tn, ev0));
             } else {
-                CHK(halo_g(s, C.g, {C.phi}, 1));
-                nsg::launch_prolong(F.g, F.phi, C.g, C.phi, s->st);
+                if (!cv.gather) CHK(halo_l(s, l + 1, {C.phi}, 1));
+                nsg::launch_prolong(F.g, F.phi, cv.g, cv.phi, s->st);
                 CHK(mg_smooth(s, l, s->mg_post, &tn, ev0));
             }
         }
@@ -589,26 +693,63 @@ nsg::Coef coef_view(double* d, int nx, int ny) {
     return c;
 }
 
-// multigrid hierarchy: halve while every level stays even and (multi-rank) slabs keep >= 4 rows;
-// stop at the first level small enough for the single-workgroup LDS coarse solve
+// multigrid hierarchy: halve while every level stays even; stop at the first level small
+// enough for the single-workgroup LDS coarse solve.  With nranks > 1 the first coarse level
+// of <= agg_cells cells (NSGPU_AGG_CELLS, default 1024^2; 0 = never), or whose slabs would
+// drop below 8 rows on some rank, is agglomerated: it and every coarser level live whole on
+// every rank (the single-rank hierarchy from there down, LDS coarse solve included), so the
+// latency-bound coarse levels cost no exchanges.  Every decision is made from all ranks'
+// slab ranges, so every rank builds the same hierarchy.
 int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector<double>& hy0) {
     MgLevel L0;
     L0.g = s->g;
     L0.c = s->c;
     L0.hx = hx0;
     L0.hy = hy0;
+    std::vector<int> ri0(s->nranks), rn(s->nranks);
+    for (int q = 0; q < s->nranks; q++) {
+        int32_t a, b;
+        ns_slab_range(s->g.nx, s->nranks, q, &a, &b);
+        ri0[q] = a;
+        rn[q] = b - a;
+    }
+    L0.minrows = *std::min_element(rn.begin(), rn.end());
     s->lv.push_back(L0);
-    const size_t lds_cap = 150 * 1024;  // single rank: stop at the first level whose LDS V-cycle fits (<= ~64^2)
+    long agg_cells = 1024L * 1024L;
+    if (const char* e = getenv("NSGPU_AGG_CELLS")) agg_cells = std::atol(e);
+    const int agg_min_rows = 8;
+    const size_t lds_cap = 150 * 1024;  // stop at the first whole level whose LDS V-cycle fits (<= ~64^2)
     for (;;) {
         const MgLevel& F = s->lv.back();
         const nsg::Geo& gf = F.g;
-        if (s->nranks == 1 && s->lv.size() > 1 && nsg::coarse_vcycle_bytes(gf) <= lds_cap) break;
-        if (!nsg::mg_can_coarsen(gf.nx, gf.ny) || gf.nxl % 2 || gf.i0 % 2) break;
+        const bool whole = s->nranks == 1 || F.repl;
+        if (whole && s->lv.size() > 1 && nsg::coarse_vcycle_bytes(gf) <= lds_cap) break;
+        if (!nsg::mg_can_coarsen(gf.nx, gf.ny)) break;
         nsg::Geo gc = gf;
-        gc.nx /= 2; gc.ny /= 2; gc.i0 /= 2; gc.nxl /= 2;
+        gc.nx /= 2; gc.ny /= 2;
         gc.ld = (gc.ny + 127) / 128 * 128;
-        if (s->nranks > 1 && gc.nxl < 4) break;
+        bool repl = F.repl;
+        int minrows = gc.nx;
+        if (whole) { gc.i0 = 0; gc.nxl = gc.nx; }
+        else {
+            bool even = true;
+            for (int q = 0; q < s->nranks; q++) even = even && ri0[q] % 2 == 0 && rn[q] % 2 == 0;
+            if (!even) break;   // a slab edge would split a coarse cell
+            for (int q = 0; q < s->nranks; q++) { ri0[q] /= 2; rn[q] /= 2; }
+            minrows = *std::min_element(rn.begin(), rn.end());
+            gc.i0 /= 2; gc.nxl /= 2;
+            repl = agg_cells > 0 && ((long)gc.nx * gc.ny <= agg_cells || minrows < agg_min_rows);
+            if (!repl && minrows < 4) break;
+        }
         MgLevel C;
+        C.repl = repl && s->nranks > 1;
+        if (C.repl && !F.repl) {
+            C.gs = gc;
+            C.si0 = ri0;
+            C.sn = rn;
+        }
+        if (C.repl) { gc.i0 = 0; gc.nxl = gc.nx; minrows = gc.nx; }
+        C.minrows = minrows;
         C.g = gc;
         C.hx.resize(gc.nx);
         C.hy.resize(gc.ny);
@@ -626,10 +767,18 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
         C.b = C.tmp + plane;
         s->lv.push_back(C);
     }
-    const nsg::Geo& gc = s->lv.back().g;
-    s->mg_coarse_lds = s->nranks == 1 && s->lv.size() > 1 && nsg::coarse_vcycle_bytes(gc) <= lds_cap;
+    const MgLevel& last = s->lv.back();
+    const nsg::Geo& gc = last.g;
+    s->mg_coarse_lds = (s->nranks == 1 || last.repl) && s->lv.size() > 1 && nsg::coarse_vcycle_bytes(gc) <= lds_cap;
+    if (s->verbose && s->rank == 0) {
+        for (size_t l = 0; l < s->lv.size(); l++)
+            fprintf(stderr, "nsgpu mg level %zu: %d x %d%s, rows/rank >= %d, %s\n", l, s->lv[l].g.nx, s->lv[l].g.ny,
+                    s->lv[l].repl ? " (replicated)" : "", s->lv[l].minrows,
+                    pair_level(s, (int)l) ? "2-sweep passes" : "single sweeps");
+        fprintf(stderr, "nsgpu mg coarse solve: %s\n", s->mg_coarse_lds ? "LDS V-cycle" : "sweeps");
+    }
     // coarsest relaxation: on the last LDS level (<= 4x4 after the in-LDS coarsening) when the
-    // LDS V-cycle is used, else on gc itself by distributed sweeps
+    // LDS V-cycle is used, else on gc itself by (distributed) sweeps
     int ncx = gc.nx, ncy = gc.ny;
     if (s->mg_coarse_lds)
         while (nsg::mg_can_coarsen(ncx, ncy)) { ncx /= 2; ncy /= 2; }
@@ -914,9 +1063,9 @@ int ns_step(ns_solver* s, ns_stats* out) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     ns_stats st{};
     HIPCHK(hipSetDevice(s->device));
-    // ghost rows for K1: u, v width 2 (MUSCL), phi width 1 (grad phi^{n-1} on walls)
-    CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
-    CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
+    // ghost rows for K1 (one exchange group): u, v width 2 (MUSCL), phi width 1 (grad phi^{n-1} on walls)
+    CHK(halo_reqs(s, {HaloReq{&s->g, s->arr[NS_ARR_U], 2}, HaloReq{&s->g, s->arr[NS_ARR_V], 2},
+                      HaloReq{&s->g, s->arr[NS_ARR_PHI], 1}}));
     CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
     // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
@@ -1093,15 +1242,24 @@ int ns_mg_transfer(ns_solver* s, int op, double* coarse) {
     HIPCHK(hipSetDevice(s->device));
     MgLevel& F = level(s, 0);
     MgLevel& C = level(s, 1);
+    const CoarseView cv = coarse_view(s, 0);   // this rank's coarse rows (a slab of a replicated level)
     const size_t w = (size_t)C.g.ny * 8;
     if (op == 0) {
         CHK(halo_g(s, F.g, {F.phi}, 1));
-        nsg::launch_restrict(F.g, F.c, F.phi, F.b, s->scal + S_SHIFT, C.g, C.c, C.b, C.phi, s->part, s->st);
-        HIPCHK(hipMemcpy2DAsync(coarse, w, C.b, (size_t)C.g.ld * 8, w, C.g.nxl, hipMemcpyDeviceToHost, s->st));
+        nsg::launch_restrict(F.g, F.c, F.phi, F.b, s->scal + S_SHIFT, cv.g, C.c, cv.b, cv.phi, s->part, s->st);
+        HIPCHK(hipMemcpy2DAsync(coarse, w, cv.b, (size_t)C.g.ld * 8, w, cv.g.nxl, hipMemcpyDeviceToHost, s->st));
     } else {
-        HIPCHK(hipMemcpy2DAsync(C.phi, (size_t)C.g.ld * 8, coarse, w, w, C.g.nxl, hipMemcpyHostToDevice, s->st));
-        CHK(halo_g(s, C.g, {C.phi}, 1));
-        nsg::launch_prolong(F.g, F.phi, C.g, C.phi, s->st);
+        HIPCHK(hipMemcpy2DAsync(cv.phi, (size_t)C.g.ld * 8, coarse, w, w, cv.g.nxl, hipMemcpyHostToDevice, s->st));
+        if (cv.gather) {
+            // the prolongation reads the neighbours' coarse rows too: gather them (the gather
+            // moves b, so stage phi through it)
+            HIPCHK(hipMemcpyAsync(C.b, C.phi, (size_t)C.g.nx * C.g.ld * 8, hipMemcpyDeviceToDevice, s->st));
+            CHK(gather_level(s, C));
+            HIPCHK(hipMemcpyAsync(C.phi, C.b, (size_t)C.g.nx * C.g.ld * 8, hipMemcpyDeviceToDevice, s->st));
+        } else {
+            CHK(halo_g(s, C.g, {C.phi}, 1));
+        }
+        nsg::launch_prolong(F.g, F.phi, cv.g, cv.phi, s->st);
     }
     HIPCHK(hipStreamSynchronize(s->st));
     return 0;

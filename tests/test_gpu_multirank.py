@@ -17,9 +17,9 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def launch(tmp_path, *args, port=29561):
+def launch(tmp_path, *args, port=29561, nproc=2):
     out = tmp_path / "r.npz"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(HERE, "mr_worker.py"),
            "--output", str(out), *args]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ))
@@ -34,17 +34,28 @@ def single(n, ny, steps, poisson, rtol):
     return u, v, phi, np.array(mm)
 
 
-@pytest.mark.parametrize("poisson,n,ny,pairs", [(nsa.NS_POISSON_RBSOR, 48, 40, False), (nsa.NS_POISSON_MG, 64, 64, False),
-                                                (nsa.NS_POISSON_MG, 130, 96, False),
-                                                (nsa.NS_POISSON_MG, 128, 96, True)])
-def test_two_slabs_host_transport_match_single_rank(tmp_path, monkeypatch, poisson, n, ny, pairs):
+@pytest.mark.parametrize("poisson,n,ny,pairs,agg,nproc", [
+    (nsa.NS_POISSON_RBSOR, 48, 40, False, None, 2),
+    (nsa.NS_POISSON_MG, 64, 64, False, None, 2),
+    (nsa.NS_POISSON_MG, 130, 96, False, None, 2),
+    (nsa.NS_POISSON_MG, 128, 96, True, None, 2),
+    (nsa.NS_POISSON_MG, 128, 96, True, "0", 2),
+    (nsa.NS_POISSON_MG, 256, 128, False, "2048", 4),
+    (nsa.NS_POISSON_MG, 264, 160, True, "4096", 3),
+])
+def test_slabs_host_transport_match_single_rank(tmp_path, monkeypatch, poisson, n, ny, pairs, agg, nproc):
     """pairs: every level smoothed by two-sweep passes with the fused restriction (5 ghost rows),
-    the path 4096^2 production runs take on their finest levels."""
+    the path 4096^2 production runs take on their finest levels.  agg: NSGPU_AGG_CELLS, the
+    coarse-level agglomeration threshold (None = default 1024^2: every coarse level of these
+    grids is replicated; "0" = never, the distributed coarse solve; "2048" = distributed levels
+    down to 2048 cells, then the gather onto every rank)."""
     if pairs:
         monkeypatch.setenv("NSGPU_PAIR_MIN_CELLS", "0")
+    if agg is not None:
+        monkeypatch.setenv("NSGPU_AGG_CELLS", agg)
     steps, rtol = 6, 1e-11
     r = launch(tmp_path, "--xport", "host", "--size", str(n), "--size-y", str(ny), "--nsteps", str(steps),
-               "--solver", str(poisson), "--tol", str(rtol))
+               "--solver", str(poisson), "--tol", str(rtol), nproc=nproc, port=29561 + nproc)
     assert str(r["status"]) == "ok", r["status"]
     u, v, phi, mm = single(n, ny, steps, poisson, rtol)
     assert r["u"].shape == u.shape
@@ -55,6 +66,9 @@ def test_two_slabs_host_transport_match_single_rank(tmp_path, monkeypatch, poiss
     # Helmholtz sweeps per step: the slabs' residual checks see the same residual as the
     # whole grid (a stale ghost row shows up as a solve that never reaches its tolerance)
     assert np.max(np.abs(r["mm"][:, 4] - mm[:, 4])) <= 2, (r["mm"][:, 4], mm[:, 4])
+    if poisson == nsa.NS_POISSON_MG and agg != "0" and n % nproc == 0 and (n // nproc) % 2 == 0:
+        # agglomerated: the same hierarchy as one rank, so the same V-cycle count per step
+        assert np.max(np.abs(r["mm"][:, 6] - mm[:, 6])) <= 1, (r["mm"][:, 6], mm[:, 6])
 
 
 def test_rccl_two_ranks_one_gpu_probe(tmp_path):
