@@ -110,6 +110,15 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
                                const double* rp, const double* shift, const Geo& gc, const double* ec,
                                hipStream_t st);
 
+// the same two passes as LDS-tiled kernels for the latency-bound small levels (one load
+// round per pass instead of a row pipeline); same results
+int launch_pois_tile2_restrict(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                               const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
+                               double* part, hipStream_t st);
+int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                              const double* rp, const double* shift, const Geo& gc, const double* ec,
+                              hipStream_t st);
+
 // coarse levels as one LDS-resident V-cycle (single rank): level g and its 2x coarsenings
 size_t coarse_vcycle_bytes(const Geo& g);
 int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double* b, int cycles, int pre, int post,

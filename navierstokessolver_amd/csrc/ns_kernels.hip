@@ -960,6 +960,173 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
     }
 }
 
+// ------------------------------------------------ K4 small levels: LDS-tiled fused passes
+// The multigrid levels below the streaming kernels' range (< 2048^2 cells: 1024^2 .. 128^2
+// at 4096^2) are latency-bound: a row pipeline of L rows costs L dependent steps whatever
+// the level's size.  Here one 256-thread workgroup owns a TT x TT output tile, stages phi
+// and b over the tile plus the dependency cone in LDS with ONE round of loads, and runs the
+// four half-sweeps of two red-black sweeps there (red, black, red, black; the updated
+// region shrinks by one cell per half-sweep):
+//   FUSE_R (cone 5): + the residual of the finished tile, restricted to the coarse rhs
+//                    (+ coarse phi := 0) and r^2 partials -- k_sweep2<XR>'s pass;
+//   FUSE_P (cone 4): every staged phi gets the bilinear prolongation of the coarse
+//                    correction first -- k_sweep2<FUSE_P>'s pass.
+// Same arithmetic as k_sweep2 (relax<0>, the Newton reciprocal of the diagonal, the
+// restriction's summation order), so the two are interchangeable level by level.
+constexpr int TT = 32;
+
+template <int FUSE>
+__global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
+    constexpr bool XR = FUSE == FUSE_R, XP = FUSE == FUSE_P;
+    constexpr int R = XR ? 5 : 4;
+    constexpr int E = TT + 2 * R;
+    constexpr int NQ = (E * E + 255) / 256;     // staged cells per thread
+    constexpr int CE = E / 2 + 3;                // XP: staged coarse rows / columns
+    constexpr int NC = (CE * CE + 255) / 256;
+    __shared__ double sp[E][E];
+    __shared__ double sb[E][E];
+    __shared__ double rw[E][4];   // per staged row: cw, ce, cw + ce, hx
+    __shared__ double cl[E][4];   // per staged column: cs, cn, cs + cn, hy
+    __shared__ double se[XP ? CE : 1][XP ? CE : 1];
+    const int t = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int ti = t / tiles_j, tj = t - ti * tiles_j;
+    const int li0 = ti * TT, j0 = tj * TT;
+    const int ld = a.ld, ny = a.ny;
+    const int rlo = -HALO, rhi = a.nxl + HALO - 1;
+    // every global load first (one latency for the whole stage-in): phi and b over the cone,
+    // the row / column coefficients, and (XP) the coarse correction over its parent rows
+    // Ilo-1 .. (whole level: ci0 = 0; rows clamped into the allocation -- a clamped row only
+    // feeds cells outside the cone)
+    double pv[NQ], bv[NQ], ev[NC];
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const int q = threadIdx.x + 256 * k;
+        if (q < E * E) {
+            const int r = q / E, cc = q - r * E;
+            const int li = min(max(li0 - R + r, rlo), rhi);
+            const int j = min(max(j0 - R + cc, 0), ny - 1);
+            pv[k] = a.in[(ptrdiff_t)li * ld + j];
+            bv[k] = a.b[(ptrdiff_t)li * ld + j];
+        }
+    }
+    const int Ilo = ((li0 - R) >> 1) - 1, Jlo = max(((j0 - R) >> 1) - 1, 0);
+    if (XP) {
+#pragma unroll
+        for (int k = 0; k < NC; k++) {
+            const int q = threadIdx.x + 256 * k;
+            if (q < CE * CE) {
+                const int r = q / CE, cc = q - r * CE;
+                const int I = min(max(Ilo + r, -HALO), a.ncx + HALO - 1);
+                const int J = min(Jlo + cc, a.ncy - 1);
+                ev[k] = a.ec[(ptrdiff_t)I * a.ldc + J];
+            }
+        }
+    }
+    double c4[4] = {0.0, 0.0, 0.0, 0.0};
+    if (threadIdx.x < E) {
+        const int gi = min(max(a.i0 + li0 - R + (int)threadIdx.x, 0), a.nx - 1);
+        c4[0] = a.cw[gi]; c4[1] = a.ce[gi]; c4[3] = XR ? a.hx[gi] : 0.0;
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + E) {
+        const int j = min(max(j0 - R + (int)threadIdx.x - 64, 0), ny - 1);
+        c4[0] = a.cs[j]; c4[1] = a.cn[j]; c4[3] = XR ? a.hy[j] : 0.0;
+    }
+    const double shift = a.shift ? a.shift[0] : 0.0;
+    if (threadIdx.x < E) {
+        rw[threadIdx.x][0] = c4[0]; rw[threadIdx.x][1] = c4[1]; rw[threadIdx.x][2] = c4[0] + c4[1];
+        rw[threadIdx.x][3] = c4[3];
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + E) {
+        const int q = threadIdx.x - 64;
+        cl[q][0] = c4[0]; cl[q][1] = c4[1]; cl[q][2] = c4[0] + c4[1]; cl[q][3] = c4[3];
+    }
+    if (XP) {
+#pragma unroll
+        for (int k = 0; k < NC; k++) {
+            const int q = threadIdx.x + 256 * k;
+            if (q < CE * CE) se[q / CE][q - (q / CE) * CE] = ev[k];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const int q = threadIdx.x + 256 * k;
+        if (q < E * E) {
+            const int r = q / E, cc = q - r * E;
+            double p = pv[k];
+            if (XP) {
+                // phi += P(e) (k_prolong / k_sweep2<FUSE_P>: the row's coarse row I and its
+                // neighbour In on the child's side, the wall reflecting onto the parent)
+                const int li = min(max(li0 - R + r, rlo), rhi);
+                const int j = min(max(j0 - R + cc, 0), ny - 1);
+                const int I = li >> 1, Jc = j >> 1;
+                int In = (li & 1) ? I + 1 : I - 1;
+                if (a.ci0 + In < 0 || a.ci0 + In >= a.ncx) In = I;
+                int Jn = (j & 1) ? Jc + 1 : Jc - 1;
+                if (Jn < 0 || Jn >= a.ncy) Jn = Jc;
+                const int i1 = I - Ilo, i2 = In - Ilo, k1 = Jc - Jlo, k2 = Jn - Jlo;
+                p += (9.0 * se[i1][k1] + 3.0 * se[i2][k1] + 3.0 * se[i1][k2] + se[i2][k2]) * 0.0625;
+            }
+            sp[r][cc] = p;
+            sb[r][cc] = bv[k] - shift;
+        }
+    }
+    __syncthreads();
+    const double omega = a.omega;
+    const int gib = a.i0 + li0 - R, jb = j0 - R;   // global row / column of staged (0, 0)
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+        const int par = h & 1;              // red ((gi + j) even), black, red, black
+        const int W = E - 2 - 2 * h;         // the half-sweep's region: [h+1, E-2-h]^2
+        const int hw = W / 2;
+        for (int q = threadIdx.x; q < W * hw; q += 256) {
+            const int r = h + 1 + q / hw;
+            const int gi = gib + r;
+            const int cc = h + 1 + 2 * (q - (q / hw) * hw) + ((par + gi + jb + h + 1) & 1);
+            const int j = jb + cc;
+            if (gi < 0 || gi >= a.nx || j < 0 || j >= ny) continue;
+            const double dg = diag<0>(rw[r][2], cl[cc][2], 0.0), w = omega * rcp_nr(dg);
+            double rr;
+            sp[r][cc] = relax<0>(sp[r][cc], sp[r - 1][cc], sp[r + 1][cc], sp[r][cc - 1], sp[r][cc + 1], sb[r][cc],
+                                 rw[r][0], rw[r][1], cl[cc][0], cl[cc][1], dg, w, 0.0, rr);
+        }
+        __syncthreads();
+    }
+    double res = 0.0;
+    for (int q = threadIdx.x; q < TT * TT; q += 256) {
+        const int r = R + q / TT, cc = R + (q & (TT - 1));
+        const int li = li0 + r - R, j = j0 + cc - R;
+        if (li >= a.nxl || j >= ny) continue;
+        a.out[(ptrdiff_t)li * ld + j] = sp[r][cc];
+        if (XR) {
+            const double dg = diag<0>(rw[r][2], cl[cc][2], 0.0);
+            double rr;
+            relax<0>(sp[r][cc], sp[r - 1][cc], sp[r + 1][cc], sp[r][cc - 1], sp[r][cc + 1], sb[r][cc], rw[r][0],
+                     rw[r][1], cl[cc][0], cl[cc][1], dg, 0.0, 0.0, rr);
+            res += rr * rr;
+            sb[r][cc] = rr;   // this cell's own b is no longer needed
+        }
+    }
+    if (XR) {
+        __syncthreads();
+        // one coarse cell per thread: k_restrict's area-weighted sum, same order
+        const int Ic = threadIdx.x / (TT / 2), Jc = threadIdx.x - Ic * (TT / 2);
+        const int li = li0 + 2 * Ic, j = j0 + 2 * Jc;
+        if (li < a.nxl && j < ny) {
+            const int r = R + 2 * Ic, cc = R + 2 * Jc;
+            double xs = (rw[r][3] * cl[cc][3]) * sb[r][cc];
+            xs = xs + (rw[r][3] * cl[cc + 1][3]) * sb[r][cc + 1];
+            xs = xs + (rw[r + 1][3] * cl[cc][3]) * sb[r + 1][cc];
+            xs = xs + (rw[r + 1][3] * cl[cc + 1][3]) * sb[r + 1][cc + 1];
+            const ptrdiff_t o = (ptrdiff_t)(li >> 1) * a.ldc + (j >> 1);
+            a.bc[o] = xs / ((rw[r][3] + rw[r + 1][3]) * (cl[cc][3] + cl[cc + 1][3]));
+            a.pc[o] = 0.0;
+        }
+        if (a.part) {
+            double x[1] = {res};
+            block_reduce_sum<1>(x, a.part + blockIdx.x);
+        }
+    }
+}
+
 // ------------------------------------------------ K4 multigrid transfer kernels
 // Cell-centred geometric multigrid for L phi = b (the Poisson solve of
 // FluidSolver.cpp:551): each coarse cell is the union of 2 x 2 fine cells, the
@@ -1078,6 +1245,41 @@ __device__ __forceinline__ void lv_rb(double* L, const LdsLv& v, double omega, i
         }
 }
 
+// the coarsest level's RB-SOR solve (citers sweeps): when it has <= 64 cells of a colour,
+// wave 0 alone runs it -- its lanes' LDS accesses stay in program order, so a wave barrier
+// (no workgroup barrier) separates the half-sweeps: 2 * citers workgroup barriers saved
+__device__ __forceinline__ void lv_rb_last(double* L, const LdsLv& v, double omega, int sweeps) {
+    const bool even = (v.ny & 1) == 0;
+    const int cnt = even ? v.nx * v.ny / 2 : v.nx * v.ny;
+    if (cnt > 64) {
+        lv_rb(L, v, omega, sweeps);
+        return;
+    }
+    if (threadIdx.x < 64) {
+        const int t = threadIdx.x;
+        int i = 0, j = 0;
+        if (t < cnt) lv_split(v, even ? 2 * t : t, i, j);
+        for (int s = 0; s < sweeps; s++)
+            for (int color = 0; color < 2; color++) {
+                if (t < cnt) {
+                    int jj = j;
+                    bool on = true;
+                    if (even) jj += ((i + j + color) & 1);
+                    else on = ((i + j + color) & 1) == 0;
+                    if (on) {
+                        const int c = i * v.ny + jj;
+                        const double r = L[v.b + c] - lv_lap(L, v, i, jj);
+                        L[v.phi + c] += omega * r * L[v.idg + c];
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+    }
+    __syncthreads();
+}
+
 // LDS footprint (doubles) of the levels from (nx, ny) down; fills lv when non-null
 __host__ __device__ inline int lv_layout(int nx, int ny, LdsLv* lv, int* nlev) {
     int off = 0, k = 0;
@@ -1169,7 +1371,7 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, dou
             }
             __syncthreads();
         }
-        lv_rb(L, lv[nl - 1], comega, citers);
+        lv_rb_last(L, lv[nl - 1], comega, citers);
         for (int k = nl - 2; k >= 0; k--) {
             const LdsLv f = lv[k], v = lv[k + 1];
             for (int t = threadIdx.x; t < f.nx * f.ny; t += CV_THREADS) {
@@ -1431,6 +1633,27 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
     hipLaunchKernelGGL((k_sweep2<0, false, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
+}
+
+// the LDS-tiled versions of the two launchers above (small levels); TT x TT tiles
+int launch_pois_tile2_restrict(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                               const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
+                               double* part, hipStream_t st) {
+    StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
+    a.hx = c.hx; a.hy = c.hy; a.bc = bc; a.pc = pc; a.ldc = gc.ld;
+    const int tj = (g.ny + TT - 1) / TT, ntiles = tj * ((g.nxl + TT - 1) / TT);
+    hipLaunchKernelGGL(k_tile2<FUSE_R>, dim3(ntiles), dim3(256), 0, st, a, tj);
+    return ntiles;
+}
+
+int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                              const double* rp, const double* shift, const Geo& gc, const double* ec,
+                              hipStream_t st) {
+    StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, nullptr, false);
+    a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0;
+    const int tj = (g.ny + TT - 1) / TT, ntiles = tj * ((g.nxl + TT - 1) / TT);
+    hipLaunchKernelGGL(k_tile2<FUSE_P>, dim3(ntiles), dim3(256), 0, st, a, tj);
+    return ntiles;
 }
 
 int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,

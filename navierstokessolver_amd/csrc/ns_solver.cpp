@@ -114,6 +114,7 @@ struct ns_solver {
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
     int fuse_restrict = 1;       // NSGPU_FUSED_RESTRICT=0: separate k_restrict pass (A/B)
     int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
+    int tile_small = 1;          // NSGPU_TILE_SMALL=0: no LDS-tiled fused passes on small levels (A/B)
     int verbose = 0;             // NSGPU_VERBOSE=1: solver residual histories on stderr
     long pair_min_cells = 2048L * 2048L;   // NSGPU_PAIR_MIN_CELLS: smallest level smoothed in 2-sweep passes
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
@@ -463,16 +464,25 @@ bool pair_level(const ns_solver* s, int l) {
     return (long)L.g.nxl * L.g.ny >= s->pair_min_cells;
 }
 
-// the last two pre-smoothing sweeps of level l carry the restriction (k_sweep2<XR>);
-// NSGPU_FUSED_RESTRICT=0 keeps the separate k_restrict pass (A/B and tests)
-bool fused_restrict(const ns_solver* s, int l) {
-    return s->fuse_restrict && pair_level(s, l) && s->mg_pre >= 2 && s->mg_pre % 2 == 0;
+// the smaller (latency-bound) levels that live whole on this rank run their fused passes as
+// LDS-tiled kernels (k_tile2); NSGPU_TILE_SMALL=0 keeps single streaming sweeps + separate
+// transfers there (A/B)
+bool tile_level(const ns_solver* s, int l) {
+    const MgLevel& L = s->lv[l];
+    if (s->tiled || !s->tile_small || pair_level(s, l)) return false;
+    return s->nranks == 1 || L.repl;
 }
 
-// the prolongation rides on the first two post-smoothing sweeps (k_sweep2 FUSE_P);
+// the last two pre-smoothing sweeps of level l carry the restriction (k_sweep2<XR> /
+// k_tile2<FUSE_R>); NSGPU_FUSED_RESTRICT=0 keeps the separate k_restrict pass (A/B and tests)
+bool fused_restrict(const ns_solver* s, int l) {
+    return s->fuse_restrict && (pair_level(s, l) || tile_level(s, l)) && s->mg_pre >= 2 && s->mg_pre % 2 == 0;
+}
+
+// the prolongation rides on the first two post-smoothing sweeps (k_sweep2 / k_tile2 FUSE_P);
 // NSGPU_FUSED_PROLONG=0 keeps the separate k_prolong pass
 bool fused_prolong(const ns_solver* s, int l) {
-    return s->fuse_prolong && pair_level(s, l) && s->mg_post >= 2;
+    return s->fuse_prolong && (pair_level(s, l) || tile_level(s, l)) && s->mg_post >= 2;
 }
 
 // level l+1 as level l's restriction target / prolongation source: the first replicated
@@ -584,8 +594,8 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
                 // last two pre-smoothing sweeps + residual + restriction in one HBM pass
                 CHK(mg_smooth(s, l, s->mg_pre - 2, &tn, ev0));
                 CHK(halo_l(s, l, {F.phi}, 5));
-                nb = nsg::launch_pois_rbsor2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b,
-                                                      cv.phi, s->part, s->st);
+                nb = (tile_level(s, l) ? nsg::launch_pois_tile2_restrict : nsg::launch_pois_rbsor2_restrict)(
+                    F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b, cv.phi, s->part, s->st);
                 std::swap(F.phi, F.tmp);
                 if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
             } else {
@@ -633,8 +643,9 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
                 }
                 const bool t = s->timing && l == 0;
                 if (t) HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn)], s->st));
-                nsg::launch_pois_rbsor2_prolong(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b,
-                                                l == 0 ? s->scal + S_SHIFT : nullptr, cv.g, cv.phi, s->st);
+                (tile_level(s, l) ? nsg::launch_pois_tile2_prolong : nsg::launch_pois_rbsor2_prolong)(
+                    F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, l == 0 ? s->scal + S_SHIFT : nullptr, cv.g, cv.phi,
+                    s->st);
                 if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn) + 1], s->st)); tn++; }
                 std::swap(F.phi, F.tmp);
                 if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
@@ -774,7 +785,7 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
         for (size_t l = 0; l < s->lv.size(); l++)
             fprintf(stderr, "nsgpu mg level %zu: %d x %d%s, rows/rank >= %d, %s\n", l, s->lv[l].g.nx, s->lv[l].g.ny,
                     s->lv[l].repl ? " (replicated)" : "", s->lv[l].minrows,
-                    pair_level(s, (int)l) ? "2-sweep passes" : "single sweeps");
+                    pair_level(s, (int)l) ? "2-sweep passes" : (tile_level(s, (int)l) ? "LDS-tiled passes" : "single sweeps"));
         fprintf(stderr, "nsgpu mg coarse solve: %s\n", s->mg_coarse_lds ? "LDS V-cycle" : "sweeps");
     }
     // coarsest relaxation: on the last LDS level (<= 4x4 after the in-LDS coarsening) when the
@@ -971,6 +982,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_SWEEP")) s->tiled = std::strcmp(e, "tiled") == 0;
     if (const char* e = getenv("NSGPU_FUSED_RESTRICT")) s->fuse_restrict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     {

@@ -356,3 +356,32 @@ def test_fused_transfer_passes_match_separate_transfers(gpu, monkeypatch, nx, ny
     xp, _ = og.solve_poisson(b)
     g = out["11"][2]
     assert rel(g - g.mean(), xp - xp.mean()) <= 1e-8
+
+
+@pytest.mark.parametrize("nx,ny", [(256, 192), (100, 68), (96, 160)])
+def test_tiled_small_level_passes_match_streaming(gpu, monkeypatch, nx, ny):
+    """The LDS-tiled fused passes of the small levels (k_tile2: two sweeps + residual +
+    restriction; prolongation + two sweeps) give the same V-cycles as the streaming fused
+    passes (k_sweep2, NSGPU_PAIR_MIN_CELLS=0) and as single sweeps + separate transfers
+    (NSGPU_TILE_SMALL=0): same cycle count, same iterate to 1e-12 (same arithmetic), and the
+    oracle's solution.  Partial tiles: 100 x 68."""
+    rng = np.random.default_rng(29)
+    b = rand(rng, nx * ny, 100.0)
+    out = {}
+    for mode, env in (("tile", {}), ("stream", {"NSGPU_PAIR_MIN_CELLS": "0"}), ("single", {"NSGPU_TILE_SMALL": "0"})):
+        for k in ("NSGPU_PAIR_MIN_CELLS", "NSGPU_TILE_SMALL"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        og, gs = pair(gpu, nx, ny, 1e-3, 100.0, poisson=gpu.NS_POISSON_MG, rtol=1e-11)
+        gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny)); gs.set(gpu.NS_ARR_RPHI, b)
+        its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+        out[mode] = (its, res, gs.get(gpu.NS_ARR_PHI).ravel())
+        gs.close()
+    for k in ("stream", "single"):
+        assert out[k][0] == out["tile"][0], (k, out[k][0], out["tile"][0])
+        assert rel(out[k][2], out["tile"][2]) <= 1e-12
+    assert out["tile"][1] <= 1e-11
+    xp, _ = og.solve_poisson(b)
+    g = out["tile"][2]
+    assert rel(g - g.mean(), xp - xp.mean()) <= 1e-8
