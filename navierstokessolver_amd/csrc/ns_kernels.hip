@@ -18,6 +18,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 
@@ -144,6 +145,188 @@ __device__ __forceinline__ double slope_r(double qc, double qp, double qm, bool 
     return minmode_nd(a, b);
 }
 
+// the ApplyBoundaryConditions terms of cell (li, j) added to its RHS (no-op off the walls)
+__device__ __forceinline__ void rhs_bc(const Geo& g, const Coef& c, double dt, double re,
+                                       const double* __restrict__ phi, int li, int j, double& ru_, double& rv_) {
+    const int gi = g.i0 + li, nx = g.nx, ny = g.ny;
+    const bool hW = gi > 0, hE = gi < nx - 1, hS = j > 0, hN = j < ny - 1;
+    if (!hW || !hE || !hS || !hN) {
+        const double hx = c.hx[gi], hy = c.hy[j];
+        const double hxW = hW ? c.hx[gi - 1] : 0.0, hxE = hE ? c.hx[gi + 1] : 0.0;
+        const double hyS = hS ? c.hy[j - 1] : 0.0, hyN = hN ? c.hy[j + 1] : 0.0;
+        const int first = !hW ? 0 : (!hE ? 1 : (!hS ? 2 : 3));
+        double gxc, gyc;
+        grad_phi(g, c, phi, li, j, gxc, gyc);
+        double D;
+        if (first < 2) {  // vertical edge: D = d/dy of (dphi/dx) along the wall (:469-473)
+            double gxn = 0.0, gxs = 0.0, dum;
+            if (hN) grad_phi(g, c, phi, li, j + 1, gxn, dum);
+            if (hS) grad_phi(g, c, phi, li, j - 1, gxs, dum);
+            if (!hN) D = 2.0 * (gxc - gxs) / (hy + hyS);
+            else if (!hS) D = 2.0 * (gxn - gxc) / (hy + hyN);
+            else D = gxn / (hy + hyN) - gxs / (hy + hyS) - gxc * (1 / (hy + hyN) - 1 / (hy + hyS));
+        } else {          // horizontal edge: D = d/dx of (dphi/dy) (:474-478)
+            double gye = 0.0, gyw = 0.0, dum;
+            if (hE) grad_phi(g, c, phi, li + 1, j, dum, gye);
+            if (hW) grad_phi(g, c, phi, li - 1, j, dum, gyw);
+            if (!hE) D = 2.0 * (gyc - gyw) / (hx + hxW);
+            else if (!hW) D = 2.0 * (gye - gyc) / (hx + hxE);
+            else D = gye / (hx + hxE) - gyw / (hx + hxW) - gyc * (1 / (hx + hxE) - 1 / (hx + hxW));
+        }
+        const bool bnd[4] = {!hW, !hE, !hS, !hN};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (!bnd[k]) continue;
+            double w, W;
+            if (g.neu[k]) {
+                if (k < 2) { w = dt * g.enx[k] * hx * D; W = dt * (0.5 / re / (hx * hx)) * w; rv_ += W; }
+                else       { w = dt * g.eny[k] * hy * D; W = dt * (0.5 / re / (hy * hy)) * w; ru_ += W; }
+            } else if (k < 2) {
+                W = dt * (0.5 / re / (hx * hx)) * g.c0[k];
+                ru_ += W;
+                w = 2 * dt * (gyc + g.enx[k] * hx * D / 2);
+                W = dt * (0.5 / re / (hx * hx)) * (g.c1[k] + w);
+                rv_ += W;
+            } else {
+                W = dt * (0.5 / re / (hy * hy)) * g.c1[k];
+                rv_ += W;
+                w = 2 * dt * (gxc + g.eny[k] * hy * D / 2);
+                W = dt * (0.5 / re / (hy * hy)) * (g.c0[k] + w);
+                ru_ += W;
+            }
+        }
+    }
+}
+
+// one cell of ConstructRHS_V (FluidSolver.cpp:327-363): u / v values at offsets (di, dj)
+// come from U(di, dj) / V(di, dj) (global loads or an LDS tile); cu0 / cv0 are the previous
+// step's convective derivatives; returns the new ones (cun, cvn) and the RHS (ru_, rv_).
+// grad phi^{n-1} (divPhi) is recomputed from phi^{n-1} on the fly for boundary cells -- the
+// reference's stored divPhi is GradP of the same phi -- saving a 16 B/cell state array.
+// X(t, d) / Y(t, d): spacing table t (0: h, 1: 1/h, 2: 2/(h_{k-1} + h_k)) at row gi + d /
+// column j + d (global tables or an LDS copy)
+template <bool BC = true, class FU, class FV, class FX, class FY>
+__device__ __forceinline__ void rhs_cell(const Geo& g, const Coef& c, double dt, double re, FU&& U, FV&& V,
+                                         FX&& X, FY&& Y, const double* __restrict__ phi, int li, int j,
+                                         double cu0, double cv0, double& cun, double& cvn, double& ru_,
+                                         double& rv_) {
+    const int gi = g.i0 + li, nx = g.nx, ny = g.ny;
+    const bool hW = gi > 0, hWW = gi > 1, hE = gi < nx - 1, hEE = gi < nx - 2;
+    const bool hS = j > 0, hSS = j > 1, hN = j < ny - 1, hNN = j < ny - 2;
+    const double hx = X(0, 0), hy = Y(0, 0);
+    const double hxW = hW ? X(0, -1) : 0.0, hxE = hE ? X(0, 1) : 0.0;
+    const double hyS = hS ? Y(0, -1) : 0.0, hyN = hN ? Y(0, 1) : 0.0;
+    // reciprocals: 1/h of the cell and its neighbours, 2/(h+h') of each face
+    const double rx = X(1, 0), ry = Y(1, 0);
+    const double rxW = hW ? X(1, -1) : 0.0, rxE = hE ? X(1, 1) : 0.0;
+    const double ryS = hS ? Y(1, -1) : 0.0, ryN = hN ? Y(1, 1) : 0.0;
+    const double sxW = X(2, 0), sxE = X(2, 1), sxWW = hW ? X(2, -1) : 0.0, sxEE = hE ? X(2, 2) : 0.0;
+    const double syS = Y(2, 0), syN = Y(2, 1), sySS = hS ? Y(2, -1) : 0.0, syNN = hN ? Y(2, 2) : 0.0;
+
+    const double uc = U(0, 0), vc = V(0, 0);
+    const double uW = hW ? U(-1, 0) : 0.0, vW = hW ? V(-1, 0) : 0.0;
+    const double uE = hE ? U(1, 0) : 0.0, vE = hE ? V(1, 0) : 0.0;
+    const double uS = hS ? U(0, -1) : 0.0, vS = hS ? V(0, -1) : 0.0;
+    const double uN = hN ? U(0, 1) : 0.0, vN = hN ? V(0, 1) : 0.0;
+    const double uWW = hWW ? U(-2, 0) : 0.0, vWW = hWW ? V(-2, 0) : 0.0;
+    const double uEE = hEE ? U(2, 0) : 0.0, vEE = hEE ? V(2, 0) : 0.0;
+    const double uSS = hSS ? U(0, -2) : 0.0, vSS = hSS ? V(0, -2) : 0.0;
+    const double uNN = hNN ? U(0, 2) : 0.0, vNN = hNN ? V(0, 2) : 0.0;
+
+    // ---- DiffusiveFlux (FluidSolver.cpp:183-203) for u (d=0) and v (d=1); (1/re)/(h+h') = (0.5/re) * 2/(h+h')
+    const double hre = 0.5 / re;
+    ru_ = 0.0 + 1.0 * uc;                                   // VecSet + VecAXPY(1, u) (:335-338)
+    rv_ = 0.0 + 1.0 * vc;
+    ru_ += 0.5 * dt * cu0;                                  // VecAXPY(0.5dt, conv0) (:339-340)
+    rv_ += 0.5 * dt * cv0;
+    {
+        double D0, D1, D2, D3;
+        D0 = hW ? hre * (uc - uW) * sxW : hre * rx * (uc - ghost_v(g, uc, 0, 0));
+        D1 = hE ? hre * (uE - uc) * sxE : -hre * rx * (uc - ghost_v(g, uc, 1, 0));
+        D2 = hS ? hre * (uc - uS) * syS : hre * ry * (uc - ghost_v(g, uc, 2, 0));
+        D3 = hN ? hre * (uN - uc) * syN : -hre * ry * (uc - ghost_v(g, uc, 3, 0));
+        ru_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
+        D0 = hW ? hre * (vc - vW) * sxW : hre * rx * (vc - ghost_v(g, vc, 0, 1));
+        D1 = hE ? hre * (vE - vc) * sxE : -hre * rx * (vc - ghost_v(g, vc, 1, 1));
+        D2 = hS ? hre * (vc - vS) * syS : hre * ry * (vc - ghost_v(g, vc, 2, 1));
+        D3 = hN ? hre * (vN - vc) * syN : -hre * ry * (vc - ghost_v(g, vc, 3, 1));
+        rv_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
+    }
+
+    // ---- ConvectiveFlux (FluidSolver.cpp:205-281)
+    double C[8];
+    {
+        // x slopes of the cell and of its W/E neighbours (each needs its own ghosts at the wall)
+        const double sxu = slope_r(uc, uE, uW, hE, hW, rx, sxE, sxW, ghost_v(g, uc, 1, 0), ghost_v(g, uc, 0, 0));
+        const double sxv = slope_r(vc, vE, vW, hE, hW, rx, sxE, sxW, ghost_v(g, vc, 1, 1), ghost_v(g, vc, 0, 1));
+        double u1, v1, u2, v2;
+        u2 = uc - hx / 2 * sxu;
+        v2 = vc - hx / 2 * sxv;
+        if (hW) {
+            const double su = slope_r(uW, uc, uWW, true, hWW, rxW, sxW, sxWW, 0.0, ghost_v(g, uW, 0, 0));
+            const double sv = slope_r(vW, vc, vWW, true, hWW, rxW, sxW, sxWW, 0.0, ghost_v(g, vW, 0, 1));
+            u1 = uW + hxW / 2 * su;
+            v1 = vW + hxW / 2 * sv;
+        } else {
+            u1 = 0.5 * (uc + ghost_v(g, uc, 0, 0));
+            v1 = 0.5 * (vc + ghost_v(g, vc, 0, 1));
+        }
+        C[0] = fnn(u1, u2);
+        C[1] = fuv(u1, v1, u2, v2);
+        u1 = uc + hx / 2 * sxu;
+        v1 = vc + hx / 2 * sxv;
+        if (hE) {
+            const double su = slope_r(uE, uEE, uc, hEE, true, rxE, sxEE, sxE, ghost_v(g, uE, 1, 0), 0.0);
+            const double sv = slope_r(vE, vEE, vc, hEE, true, rxE, sxEE, sxE, ghost_v(g, vE, 1, 1), 0.0);
+            u2 = uE - hxE / 2 * su;
+            v2 = vE - hxE / 2 * sv;
+        } else {
+            u2 = 0.5 * (uc + ghost_v(g, uc, 1, 0));
+            v2 = 0.5 * (vc + ghost_v(g, vc, 1, 1));
+        }
+        C[2] = fnn(u1, u2);
+        C[3] = fuv(u1, v1, u2, v2);
+
+        const double syu = slope_r(uc, uN, uS, hN, hS, ry, syN, syS, ghost_v(g, uc, 3, 0), ghost_v(g, uc, 2, 0));
+        const double syv = slope_r(vc, vN, vS, hN, hS, ry, syN, syS, ghost_v(g, vc, 3, 1), ghost_v(g, vc, 2, 1));
+        u2 = uc - hy / 2 * syu;
+        v2 = vc - hy / 2 * syv;
+        if (hS) {
+            const double su = slope_r(uS, uc, uSS, true, hSS, ryS, syS, sySS, 0.0, ghost_v(g, uS, 2, 0));
+            const double sv = slope_r(vS, vc, vSS, true, hSS, ryS, syS, sySS, 0.0, ghost_v(g, vS, 2, 1));
+            u1 = uS + hyS / 2 * su;
+            v1 = vS + hyS / 2 * sv;
+        } else {
+            u1 = 0.5 * (uc + ghost_v(g, uc, 2, 0));
+            v1 = 0.5 * (vc + ghost_v(g, vc, 2, 1));
+        }
+        C[5] = fnn(v1, v2);
+        C[4] = fuv(u1, v1, u2, v2);
+        u1 = uc + hy / 2 * syu;
+        v1 = vc + hy / 2 * syv;
+        if (hN) {
+            const double su = slope_r(uN, uNN, uc, hNN, true, ryN, syNN, syN, ghost_v(g, uN, 3, 0), 0.0);
+            const double sv = slope_r(vN, vNN, vc, hNN, true, ryN, syNN, syN, ghost_v(g, vN, 3, 1), 0.0);
+            u2 = uN - hyN / 2 * su;
+            v2 = vN - hyN / 2 * sv;
+        } else {
+            u2 = 0.5 * (uc + ghost_v(g, uc, 3, 0));
+            v2 = 0.5 * (vc + ghost_v(g, vc, 3, 1));
+        }
+        C[7] = fnn(v1, v2);
+        C[6] = fuv(u1, v1, u2, v2);
+    }
+    double val = (C[2] - C[0]) * rx + (C[6] - C[4]) * ry;   // (:352-355)
+    cun = val;
+    ru_ += val * (-1.5 * dt);
+    val = (C[3] - C[1]) * rx + (C[7] - C[5]) * ry;          // (:356-359)
+    cvn = val;
+    rv_ += val * (-1.5 * dt);
+
+    // ---- ApplyBoundaryConditions (FluidSolver.cpp:458-510), boundary cells only
+    if (BC) rhs_bc(g, c, dt, re, phi, li, j, ru_, rv_);
+}
+
 __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
                                              const double* __restrict__ v, const double* __restrict__ phi,
                                              double* __restrict__ cu, double* __restrict__ cv,
@@ -153,168 +336,155 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
     const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
     double acc[2] = {0.0, 0.0};
     for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
-        const int gi = g.i0 + li, ld = g.ld, nx = g.nx, ny = g.ny;
-        const bool hW = gi > 0, hWW = gi > 1, hE = gi < nx - 1, hEE = gi < nx - 2;
-        const bool hS = j > 0, hSS = j > 1, hN = j < ny - 1, hNN = j < ny - 2;
-        const double hx = c.hx[gi], hy = c.hy[j];
-        const double hxW = hW ? c.hx[gi - 1] : 0.0, hxE = hE ? c.hx[gi + 1] : 0.0;
-        const double hyS = hS ? c.hy[j - 1] : 0.0, hyN = hN ? c.hy[j + 1] : 0.0;
-        // reciprocals: 1/h of the cell and its neighbours, 2/(h+h') of each face
-        const double rx = c.rhx[gi], ry = c.rhy[j];
-        const double rxW = hW ? c.rhx[gi - 1] : 0.0, rxE = hE ? c.rhx[gi + 1] : 0.0;
-        const double ryS = hS ? c.rhy[j - 1] : 0.0, ryN = hN ? c.rhy[j + 1] : 0.0;
-        const double sxW = c.rsx[gi], sxE = c.rsx[gi + 1], sxWW = hW ? c.rsx[gi - 1] : 0.0, sxEE = hE ? c.rsx[gi + 2] : 0.0;
-        const double syS = c.rsy[j], syN = c.rsy[j + 1], sySS = hS ? c.rsy[j - 1] : 0.0, syNN = hN ? c.rsy[j + 2] : 0.0;
-
-        const double uc = ldf(u, ld, li, j), vc = ldf(v, ld, li, j);
-        const double uW = hW ? ldf(u, ld, li - 1, j) : 0.0, vW = hW ? ldf(v, ld, li - 1, j) : 0.0;
-        const double uE = hE ? ldf(u, ld, li + 1, j) : 0.0, vE = hE ? ldf(v, ld, li + 1, j) : 0.0;
-        const double uS = hS ? ldf(u, ld, li, j - 1) : 0.0, vS = hS ? ldf(v, ld, li, j - 1) : 0.0;
-        const double uN = hN ? ldf(u, ld, li, j + 1) : 0.0, vN = hN ? ldf(v, ld, li, j + 1) : 0.0;
-        const double uWW = hWW ? ldf(u, ld, li - 2, j) : 0.0, vWW = hWW ? ldf(v, ld, li - 2, j) : 0.0;
-        const double uEE = hEE ? ldf(u, ld, li + 2, j) : 0.0, vEE = hEE ? ldf(v, ld, li + 2, j) : 0.0;
-        const double uSS = hSS ? ldf(u, ld, li, j - 2) : 0.0, vSS = hSS ? ldf(v, ld, li, j - 2) : 0.0;
-        const double uNN = hNN ? ldf(u, ld, li, j + 2) : 0.0, vNN = hNN ? ldf(v, ld, li, j + 2) : 0.0;
-
-        // ---- DiffusiveFlux (FluidSolver.cpp:183-203) for u (d=0) and v (d=1); (1/re)/(h+h') = (0.5/re) * 2/(h+h')
-        const double hre = 0.5 / re;
-        double ru_ = 0.0 + 1.0 * uc, rv_ = 0.0 + 1.0 * vc;    // VecSet + VecAXPY(1, u) (:335-338)
-        ru_ += 0.5 * dt * cu[(ptrdiff_t)li * ld + j];           // VecAXPY(0.5dt, conv0) (:339-340)
-        rv_ += 0.5 * dt * cv[(ptrdiff_t)li * ld + j];
-        {
-            double D0, D1, D2, D3;
-            D0 = hW ? hre * (uc - uW) * sxW : hre * rx * (uc - ghost_v(g, uc, 0, 0));
-            D1 = hE ? hre * (uE - uc) * sxE : -hre * rx * (uc - ghost_v(g, uc, 1, 0));
-            D2 = hS ? hre * (uc - uS) * syS : hre * ry * (uc - ghost_v(g, uc, 2, 0));
-            D3 = hN ? hre * (uN - uc) * syN : -hre * ry * (uc - ghost_v(g, uc, 3, 0));
-            ru_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
-            D0 = hW ? hre * (vc - vW) * sxW : hre * rx * (vc - ghost_v(g, vc, 0, 1));
-            D1 = hE ? hre * (vE - vc) * sxE : -hre * rx * (vc - ghost_v(g, vc, 1, 1));
-            D2 = hS ? hre * (vc - vS) * syS : hre * ry * (vc - ghost_v(g, vc, 2, 1));
-            D3 = hN ? hre * (vN - vc) * syN : -hre * ry * (vc - ghost_v(g, vc, 3, 1));
-            rv_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
-        }
-
-        // ---- ConvectiveFlux (FluidSolver.cpp:205-281)
-        double C[8];
-        {
-            // x slopes of the cell and of its W/E neighbours (each needs its own ghosts at the wall)
-            const double sxu = slope_r(uc, uE, uW, hE, hW, rx, sxE, sxW, ghost_v(g, uc, 1, 0), ghost_v(g, uc, 0, 0));
-            const double sxv = slope_r(vc, vE, vW, hE, hW, rx, sxE, sxW, ghost_v(g, vc, 1, 1), ghost_v(g, vc, 0, 1));
-            double u1, v1, u2, v2;
-            u2 = uc - hx / 2 * sxu;
-            v2 = vc - hx / 2 * sxv;
-            if (hW) {
-                const double su = slope_r(uW, uc, uWW, true, hWW, rxW, sxW, sxWW, 0.0, ghost_v(g, uW, 0, 0));
-                const double sv = slope_r(vW, vc, vWW, true, hWW, rxW, sxW, sxWW, 0.0, ghost_v(g, vW, 0, 1));
-                u1 = uW + hxW / 2 * su;
-                v1 = vW + hxW / 2 * sv;
-            } else {
-                u1 = 0.5 * (uc + ghost_v(g, uc, 0, 0));
-                v1 = 0.5 * (vc + ghost_v(g, vc, 0, 1));
-            }
-            C[0] = fnn(u1, u2);
-            C[1] = fuv(u1, v1, u2, v2);
-            u1 = uc + hx / 2 * sxu;
-            v1 = vc + hx / 2 * sxv;
-            if (hE) {
-                const double su = slope_r(uE, uEE, uc, hEE, true, rxE, sxEE, sxE, ghost_v(g, uE, 1, 0), 0.0);
-                const double sv = slope_r(vE, vEE, vc, hEE, true, rxE, sxEE, sxE, ghost_v(g, vE, 1, 1), 0.0);
-                u2 = uE - hxE / 2 * su;
-                v2 = vE - hxE / 2 * sv;
-            } else {
-                u2 = 0.5 * (uc + ghost_v(g, uc, 1, 0));
-                v2 = 0.5 * (vc + ghost_v(g, vc, 1, 1));
-            }
-            C[2] = fnn(u1, u2);
-            C[3] = fuv(u1, v1, u2, v2);
-
-            const double syu = slope_r(uc, uN, uS, hN, hS, ry, syN, syS, ghost_v(g, uc, 3, 0), ghost_v(g, uc, 2, 0));
-            const double syv = slope_r(vc, vN, vS, hN, hS, ry, syN, syS, ghost_v(g, vc, 3, 1), ghost_v(g, vc, 2, 1));
-            u2 = uc - hy / 2 * syu;
-            v2 = vc - hy / 2 * syv;
-            if (hS) {
-                const double su = slope_r(uS, uc, uSS, true, hSS, ryS, syS, sySS, 0.0, ghost_v(g, uS, 2, 0));
-                const double sv = slope_r(vS, vc, vSS, true, hSS, ryS, syS, sySS, 0.0, ghost_v(g, vS, 2, 1));
-                u1 = uS + hyS / 2 * su;
-                v1 = vS + hyS / 2 * sv;
-            } else {
-                u1 = 0.5 * (uc + ghost_v(g, uc, 2, 0));
-                v1 = 0.5 * (vc + ghost_v(g, vc, 2, 1));
-            }
-            C[5] = fnn(v1, v2);
-            C[4] = fuv(u1, v1, u2, v2);
-            u1 = uc + hy / 2 * syu;
-            v1 = vc + hy / 2 * syv;
-            if (hN) {
-                const double su = slope_r(uN, uNN, uc, hNN, true, ryN, syNN, syN, ghost_v(g, uN, 3, 0), 0.0);
-                const double sv = slope_r(vN, vNN, vc, hNN, true, ryN, syNN, syN, ghost_v(g, vN, 3, 1), 0.0);
-                u2 = uN - hyN / 2 * su;
-                v2 = vN - hyN / 2 * sv;
-            } else {
-                u2 = 0.5 * (uc + ghost_v(g, uc, 3, 0));
-                v2 = 0.5 * (vc + ghost_v(g, vc, 3, 1));
-            }
-            C[7] = fnn(v1, v2);
-            C[6] = fuv(u1, v1, u2, v2);
-        }
-        double val = (C[2] - C[0]) * rx + (C[6] - C[4]) * ry;   // (:352-355)
-        cu[(ptrdiff_t)li * ld + j] = val;
-        ru_ += val * (-1.5 * dt);
-        val = (C[3] - C[1]) * rx + (C[7] - C[5]) * ry;          // (:356-359)
-        cv[(ptrdiff_t)li * ld + j] = val;
-        rv_ += val * (-1.5 * dt);
-
-        // ---- ApplyBoundaryConditions (FluidSolver.cpp:458-510), boundary cells only
-        if (!hW || !hE || !hS || !hN) {
-            const int first = !hW ? 0 : (!hE ? 1 : (!hS ? 2 : 3));
-            double gxc, gyc;
-            grad_phi(g, c, phi, li, j, gxc, gyc);
-            double D;
-            if (first < 2) {  // vertical edge: D = d/dy of (dphi/dx) along the wall (:469-473)
-                double gxn = 0.0, gxs = 0.0, dum;
-                if (hN) grad_phi(g, c, phi, li, j + 1, gxn, dum);
-                if (hS) grad_phi(g, c, phi, li, j - 1, gxs, dum);
-                if (!hN) D = 2.0 * (gxc - gxs) / (hy + hyS);
-                else if (!hS) D = 2.0 * (gxn - gxc) / (hy + hyN);
-                else D = gxn / (hy + hyN) - gxs / (hy + hyS) - gxc * (1 / (hy + hyN) - 1 / (hy + hyS));
-            } else {          // horizontal edge: D = d/dx of (dphi/dy) (:474-478)
-                double gye = 0.0, gyw = 0.0, dum;
-                if (hE) grad_phi(g, c, phi, li + 1, j, dum, gye);
-                if (hW) grad_phi(g, c, phi, li - 1, j, dum, gyw);
-                if (!hE) D = 2.0 * (gyc - gyw) / (hx + hxW);
-                else if (!hW) D = 2.0 * (gye - gyc) / (hx + hxE);
-                else D = gye / (hx + hxE) - gyw / (hx + hxW) - gyc * (1 / (hx + hxE) - 1 / (hx + hxW));
-            }
-            const bool bnd[4] = {!hW, !hE, !hS, !hN};
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (!bnd[k]) continue;
-                double w, W;
-                if (g.neu[k]) {
-                    if (k < 2) { w = dt * g.enx[k] * hx * D; W = dt * (0.5 / re / (hx * hx)) * w; rv_ += W; }
-                    else       { w = dt * g.eny[k] * hy * D; W = dt * (0.5 / re / (hy * hy)) * w; ru_ += W; }
-                } else if (k < 2) {
-                    W = dt * (0.5 / re / (hx * hx)) * g.c0[k];
-                    ru_ += W;
-                    w = 2 * dt * (gyc + g.enx[k] * hx * D / 2);
-                    W = dt * (0.5 / re / (hx * hx)) * (g.c1[k] + w);
-                    rv_ += W;
-                } else {
-                    W = dt * (0.5 / re / (hy * hy)) * g.c1[k];
-                    rv_ += W;
-                    w = 2 * dt * (gxc + g.eny[k] * hy * D / 2);
-                    W = dt * (0.5 / re / (hy * hy)) * (g.c0[k] + w);
-                    ru_ += W;
-                }
-            }
-        }
-        ru[(ptrdiff_t)li * ld + j] = ru_;
-        rv[(ptrdiff_t)li * ld + j] = rv_;
+        const int ld = g.ld;
+        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+        auto U = [&](int di, int dj) { return ldf(u, ld, li + di, j + dj); };
+        auto V = [&](int di, int dj) { return ldf(v, ld, li + di, j + dj); };
+        const int gi = g.i0 + li;
+        auto X = [&](int t, int d) { return (t == 0 ? c.hx : t == 1 ? c.rhx : c.rsx)[gi + d]; };
+        auto Y = [&](int t, int d) { return (t == 0 ? c.hy : t == 1 ? c.rhy : c.rsy)[j + d]; };
+        double cun, cvn, ru_, rv_;
+        rhs_cell(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
+        cu[o] = cun;
+        cv[o] = cvn;
+        ru[o] = ru_;
+        rv[o] = rv_;
         acc[0] += ru_ * ru_;
         acc[1] += rv_ * rv_;
     }
     block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
+}
+
+// K1 with everything staged in LDS: a 256-thread workgroup owns RT x 64 cells and loads u, v
+// over them plus the MUSCL stencil's 2-cell ring, cu0 / cv0, and the tile's spacing tables
+// in ONE round of coalesced loads (the global-load version fetches every u / v value ~13
+// times through L1/L2 and reloads ~30 table entries per cell); the cell loop then reads
+// LDS only.  Same per-cell arithmetic (rhs_cell).
+constexpr int RT = 16;
+__global__ __launch_bounds__(256) void k_rhs_lds(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
+                                                 const double* __restrict__ v, const double* __restrict__ phi,
+                                                 double* __restrict__ cu, double* __restrict__ cv,
+                                                 double* __restrict__ ru, double* __restrict__ rv,
+                                                 double* __restrict__ part) {
+    constexpr int EI = RT + 4, EJ = 64 + 4;
+    __shared__ double su[EI][EJ], sv[EI][EJ];
+    __shared__ double scu[RT][64], scv[RT][64];
+    __shared__ double tx[3][RT + 4], ty[3][64 + 4];   // tables at rows gi-1 .. / columns j-1 ..
+    const int tj = blockIdx.x, ti = blockIdx.y;
+    const int li0 = ti * RT, j0 = tj * 64, ld = g.ld;
+    const int tid = threadIdx.x + 64 * threadIdx.y;
+    // stage rows li0-2 .. li0+RT+1, columns j0-2 .. j0+65 (clamped into the field; a clamped
+    // value is never used: the stencil reads past a wall only through its ghost formula)
+    constexpr int NQ = (EI * EJ + 255) / 256, NC = (RT * 64) / 256;
+    double pu[NQ], pv[NQ], pc[NC], pd[NC];
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const int q = tid + 256 * k;
+        if (q < EI * EJ) {
+            const int r = q / EJ, cc = q - r * EJ;
+            const int li = min(max(li0 - 2 + r, -HALO), g.nxl + HALO - 1);
+            const int j = min(max(j0 - 2 + cc, 0), g.ny - 1);
+            pu[k] = ldf(u, ld, li, j);
+            pv[k] = ldf(v, ld, li, j);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NC; k++) {
+        const int q = tid + 256 * k, r = q >> 6, cc = q & 63;
+        const int li = min(li0 + r, g.nxl - 1), j = min(j0 + cc, g.ny - 1);
+        pc[k] = ldf(cu, ld, li, j);
+        pd[k] = ldf(cv, ld, li, j);
+    }
+    // spacing tables: entries q < NTX are rows (table q / (RT+4)), the rest columns
+    constexpr int NTX = 3 * (RT + 4), NT = NTX + 3 * 68;
+    auto table = [&](int q) {
+        if (q < NTX) {
+            const int t = q / (RT + 4), k = q - t * (RT + 4);
+            const int gi = min(max(g.i0 + li0 - 1 + k, 0), g.nx);   // rsx has nx + 1 entries
+            return t == 0 ? c.hx[min(gi, g.nx - 1)] : t == 1 ? c.rhx[min(gi, g.nx - 1)] : c.rsx[gi];
+        }
+        const int t = (q - NTX) / 68, k = q - NTX - t * 68;
+        const int j = min(max(j0 - 1 + k, 0), g.ny);
+        return t == 0 ? c.hy[min(j, g.ny - 1)] : t == 1 ? c.rhy[min(j, g.ny - 1)] : c.rsy[j];
+    };
+    const double tv0 = table(tid), tv1 = tid + 256 < NT ? table(tid + 256) : 0.0;
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const int q = tid + 256 * k;
+        if (q < EI * EJ) {
+            const int r = q / EJ, cc = q - r * EJ;
+            su[r][cc] = pu[k];
+            sv[r][cc] = pv[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NC; k++) {
+        const int q = tid + 256 * k;
+        scu[q >> 6][q & 63] = pc[k];
+        scv[q >> 6][q & 63] = pd[k];
+    }
+    auto put = [&](int q, double x) {
+        if (q < NTX) tx[q / (RT + 4)][q % (RT + 4)] = x;
+        else ty[(q - NTX) / 68][(q - NTX) % 68] = x;
+    };
+    put(tid, tv0);
+    if (tid + 256 < NT) put(tid + 256, tv1);
+    __syncthreads();
+    double acc[2] = {0.0, 0.0};
+    const int j = j0 + threadIdx.x;
+    const int lend = min(li0 + RT, g.nxl);
+    // one wave = one row (blockDim.x == 64): the row index is wave-uniform
+    for (int li = __builtin_amdgcn_readfirstlane(li0 + (int)threadIdx.y); li < lend && j < g.ny; li += 4) {
+        const int R = li - li0 + 2, C = threadIdx.x + 2;
+        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+        auto U = [&](int di, int dj) { return su[R + di][C + dj]; };
+        auto V = [&](int di, int dj) { return sv[R + di][C + dj]; };
+        auto X = [&](int t, int d) { return tx[t][R - 1 + d]; };
+        auto Y = [&](int t, int d) { return ty[t][C - 1 + d]; };
+        double cun, cvn, ru_, rv_;
+        rhs_cell<false>(g, c, dt, re, U, V, X, Y, phi, li, j, scu[R - 2][C - 2], scv[R - 2][C - 2], cun, cvn, ru_,
+                        rv_);
+        cu[o] = cun;
+        cv[o] = cvn;
+        ru[o] = ru_;
+        rv[o] = rv_;
+        const int gi = g.i0 + li;
+        if (gi > 0 && gi < g.nx - 1 && j > 0 && j < g.ny - 1) {   // wall cells: k_rhs_bc
+            acc[0] += ru_ * ru_;
+            acc[1] += rv_ * rv_;
+        }
+    }
+    block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
+}
+
+// the wall cells' ApplyBoundaryConditions terms (rhs_bc) on top of k_rhs_lds's values -- the
+// same additions in the same order as the fused k_rhs -- plus their ||RHS||^2 partials.  Out
+// of the main kernel because the wall branch (three grad phi evaluations) would cost it ~40
+// VGPRs (197 -> 153) for 0.05 % of the cells.  Thread k: the slab's column j = 0 / ny-1
+// cells (2 nxl), then the W / E wall rows if this slab holds them (ny - 2 each).
+__global__ __launch_bounds__(256) void k_rhs_bc(Geo g, Coef c, double dt, double re, const double* __restrict__ phi,
+                                                double* __restrict__ ru, double* __restrict__ rv,
+                                                double* __restrict__ part) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const bool wrow = g.i0 == 0, erow = g.i0 + g.nxl == g.nx;
+    int li = -1, j = 0;
+    if (k < 2 * g.nxl) { li = k >> 1; j = (k & 1) ? g.ny - 1 : 0; }
+    else {
+        int q = k - 2 * g.nxl;
+        if (wrow) { if (q < g.ny - 2) { li = 0; j = q + 1; } q -= g.ny - 2; }
+        if (li < 0 && erow && q >= 0 && q < g.ny - 2) { li = g.nxl - 1; j = q + 1; }
+    }
+    double acc[2] = {0.0, 0.0};
+    if (li >= 0) {
+        const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
+        double ru_ = ru[o], rv_ = rv[o];
+        rhs_bc(g, c, dt, re, phi, li, j, ru_, rv_);
+        ru[o] = ru_;
+        rv[o] = rv_;
+        acc[0] = ru_ * ru_;
+        acc[1] = rv_ * rv_;
+    }
+    block_reduce_sum<2>(acc, part + 2 * blockIdx.x);
 }
 
 // ---------------------------------------------------------------- K3
@@ -1499,6 +1669,15 @@ namespace nsg {
 
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
                const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st) {
+    const char* e = getenv("NSGPU_RHS");   // NSGPU_RHS=global: the global-load K1 (A/B)
+    if (!(e && std::strcmp(e, "global") == 0)) {
+        const dim3 grid((g.ny + 63) / 64, (g.nxl + RT - 1) / RT);
+        hipLaunchKernelGGL(k_rhs_lds, grid, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part);
+        const int nb = (int)(grid.x * grid.y);
+        const int nbc = (2 * g.nxl + 2 * g.ny + 255) / 256;
+        hipLaunchKernelGGL(k_rhs_bc, dim3(nbc), dim3(256), 0, st, g, c, dt, re, phi, ru, rv, part + 2 * nb);
+        return nb + nbc;
+    }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
     hipLaunchKernelGGL(k_rhs, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);

@@ -35,7 +35,7 @@ def rand(rng, n, scale=1.0):
 
 
 GEOMS = [(24, 24, -1, -1, BC_CAVITY), (20, 33, -1, -1, BC_FLOW), (17, 16, 1.07, 0.95, BC_CAVITY),
-         (64, 64, -1, -1, BC_FLOW)]
+         (64, 64, -1, -1, BC_FLOW), (100, 130, 1.01, -1, BC_FLOW)]
 
 
 @pytest.mark.parametrize("nx,ny,xr,yr,bc", GEOMS)
@@ -385,3 +385,27 @@ def test_tiled_small_level_passes_match_streaming(gpu, monkeypatch, nx, ny):
     xp, _ = og.solve_poisson(b)
     g = out["tile"][2]
     assert rel(g - g.mean(), xp - xp.mean()) <= 1e-8
+
+
+@pytest.mark.parametrize("nx,ny,xr,yr,bc", [(300, 200, 1.002, 0.998, BC_FLOW), (37, 70, -1, -1, BC_CAVITY)])
+def test_k1_lds_equals_global_kernel(gpu, monkeypatch, nx, ny, xr, yr, bc):
+    """K1 staged in LDS (k_rhs_lds + the wall-cell kernel k_rhs_bc) = the global-load K1
+    (NSGPU_RHS=global): same per-cell source (rhs_cell / rhs_bc); the compiler's FMA
+    contraction differs between the two kernels, so equal to 1e-14 relative, not bit for bit."""
+    rng = np.random.default_rng(31)
+    dt, re = 1e-3, 250.0
+    N = nx * ny
+    ins = [rand(rng, N) for _ in range(5)]
+    outs = []
+    for mode in ("lds", "global"):
+        if mode == "global":
+            monkeypatch.setenv("NSGPU_RHS", "global")
+        _, gs = pair(gpu, nx, ny, dt, re, bc, xr, yr)
+        for a, x in zip((gpu.NS_ARR_U, gpu.NS_ARR_V, gpu.NS_ARR_PHI, gpu.NS_ARR_CU, gpu.NS_ARR_CV), ins):
+            gs.set(a, x)
+        sums = gs.kernel(gpu.NS_K_RHS)
+        outs.append([gs.get(a) for a in (gpu.NS_ARR_RU, gpu.NS_ARR_RV, gpu.NS_ARR_CU, gpu.NS_ARR_CV)] + [sums[:2]])
+        gs.close()
+    for a, b in zip(outs[0][:4], outs[1][:4]):
+        assert rel(a, b) <= 1e-14
+    np.testing.assert_allclose(outs[0][4], outs[1][4], rtol=1e-13)
