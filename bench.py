@@ -23,12 +23,19 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-# the timed kernel: the finest level's first post-smoothing pass (k_sweep2 FUSE_P) --
-# bilinear prolongation of the coarse correction + two red-black sweeps in one HBM pass.
-# Algorithmic bytes per cell: read phi 8, read rhs 8, write phi 8, read the coarse
-# correction 8/4 (24 B/cell per sweep for an unfused sweep)
-ROOFLINE_KERNEL = "k_sweep2<Poisson, FUSE_P> (finest post-smoothing pass: prolongation + 2 RB sweeps)"
-PASS_BYTES_PER_CELL = 26
+# the finest multigrid level's two passes per V-cycle, timed with HIP events on the solver's
+# stream around every launch in the timed region (ns_params.timing).  Algorithmic bytes per
+# cell (24 B/cell for one unfused sweep: read phi, read b, write phi):
+#   restriction pass (k_sweep2 FUSE_R): two RB sweeps + residual + restriction:
+#       read phi 8 + read b 8 + write phi 8 + write the coarse rhs and phi 2 x 8 / 4  = 28
+#   prolongation pass (k_sweep2 FUSE_P): prolongation + two RB sweeps:
+#       read phi 8 + read b 8 + write phi 8 + read the coarse correction 8 / 4         = 26
+# The one with the larger total time per step is `roofline` (the dominant kernel).
+KERNELS = {
+    "restrict": ("k_sweep2<Poisson, FUSE_R> (finest pre-smoothing pass: 2 RB sweeps + residual + restriction)", 28),
+    "prolong": ("k_sweep2<Poisson, FUSE_P> (finest post-smoothing pass: prolongation + 2 RB sweeps)", 26),
+}
+JACOBI_LABEL = "k_sweep<Poisson, Jacobi> (one weighted-Jacobi sweep, the north star's roofline kernel)"
 SWEEP_BYTES_PER_CELL = 24
 
 
@@ -112,26 +119,47 @@ def main():
     cells = n * n
     cycles = sum(s["it_phi"] for s in stats)
     hsweeps = sum(s["it_u"] for s in stats)
-    kms = sum(s["t_poisson_kernel_ms"] for s in stats)
-    kn = sum(s["n_poisson_kernels"] for s in stats)
-    avg_kernel_s = kms / kn / 1e3 if kn else float("nan")
     local_cells = (solver.i1 - solver.i0) * n
-    achieved = PASS_BYTES_PER_CELL * local_cells / avg_kernel_s / 1e9
+    timed = {"prolong": (sum(s["t_poisson_kernel_ms"] for s in stats), sum(s["n_poisson_kernels"] for s in stats)),
+             "restrict": (sum(s["t_restrict_kernel_ms"] for s in stats), sum(s["n_restrict_kernels"] for s in stats))}
     # finest-level sweeps: V(2,2) per cycle + the 2 pre-smoothing sweeps of the converged check
     fine_sweeps = 4 * cycles + 2 * K
     value = cells * K / elapsed / 1e6
 
+    # the north star's roofline kernel: one Jacobi sweep of this rank's slab (random phi, b;
+    # 10 warm-up + 50 timed launches, HIP events), single rank only
+    jacobi = None
+    if world == 1:
+        js = nsa.GpuSolver(nsa.cavity(n), dt, re, poisson=nsa.NS_POISSON_JACOBI, omega=1.0, device=local)
+        js.fill_random(0x5EED)
+        t = js.time_poisson(10, 50)
+        js.close()
+        jacobi = t["avg_ms"] * 1e-3
     if rank != 0:
         return
-    traffic = None
+    traffic = {}
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(prof):
         try:
             d = json.load(open(prof))
-            if d.get("n") == n and d.get("kernel") == ROOFLINE_KERNEL and d.get("kernel_bytes_per_launch"):
-                traffic = d["kernel_bytes_per_launch"]
+            if d.get("n") == n:
+                traffic = {k: v.get("kernel_bytes_per_launch") for k, v in d.get("kernels", {}).items()}
         except Exception:
-            traffic = None
+            traffic = {}
+
+    def roof(key, label, bpc, avg_s, launches):
+        achieved = bpc * local_cells / avg_s / 1e9
+        return {"bound": "hbm", "kernel": label, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get(key), "avg_kernel_us": avg_s * 1e6,
+                "launches_timed": launches, "bytes_per_launch": bpc * local_cells, "bytes_per_cell": bpc}
+
+    kern = {}
+    for key, (label, bpc) in KERNELS.items():
+        ms, cnt = timed[key]
+        if cnt:
+            kern[key] = roof(key, label, bpc, ms / cnt / 1e3, cnt)
+            kern[key]["ms_per_step"] = ms / K
+    dominant = max(kern, key=lambda k: kern[k]["ms_per_step"]) if kern else None
     line = {
         "metric": "cell-updates/sec (MLUPS) + Poisson iters/sec, 4096^2 grid at 1/2/4/8 GPUs",
         "value": value,
@@ -153,13 +181,11 @@ def main():
         "poisson_fine_sweeps_per_s": fine_sweeps / elapsed,
         "poisson_fine_sweeps_per_step": fine_sweeps / K,
         "helmholtz_sweeps_per_step": hsweeps / K,
-        "roofline": {"bound": "hbm", "kernel": ROOFLINE_KERNEL,
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "avg_kernel_us": avg_kernel_s * 1e6, "launches_timed": kn,
-                     "bytes_per_launch": PASS_BYTES_PER_CELL * local_cells,
-                     # two sweeps per pass: the rate an unfused sweep (24 B/cell) would need to match
-                     "sweep_equivalent_GBs": 2 * SWEEP_BYTES_PER_CELL * local_cells / avg_kernel_s / 1e9},
+        "roofline": kern.get(dominant),
+        "kernels": dict(kern),
     }
+    if jacobi is not None:
+        line["kernels"]["jacobi_sweep"] = roof("jacobi_sweep", JACOBI_LABEL, SWEEP_BYTES_PER_CELL, jacobi, 50)
     if world == 1 and not args.no_cpu:
         try:
             line["cpu_baseline"] = cpu_baseline(n, re, dt, solver.omega_v, solver.mg_omega)

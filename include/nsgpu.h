@@ -111,9 +111,12 @@ typedef struct ns_stats {
     double  umin, umax, vmin, vmax;
     int32_t it_u, it_v, it_phi;      /* sweeps of the Helmholtz solves; Poisson sweeps (RB-SOR / Jacobi) or V-cycles (MG) */
     double  res_u, res_v, res_phi;   /* final relative residuals (of the input of the last sweep) */
-    double  t_poisson_kernel_ms;     /* sum of Poisson sweep-kernel durations (timing == 1) */
+    double  t_poisson_kernel_ms;     /* sum of Poisson sweep-kernel durations (timing == 1; multigrid: the
+                                      * finest level's sweeps and prolongation passes) */
     int32_t n_poisson_kernels;       /* number of Poisson sweep kernels timed */
     int32_t n_checks;                /* residual checks (host syncs) in the step */
+    double  t_restrict_kernel_ms;    /* multigrid: sum of the finest level's restriction-pass durations (timing == 1) */
+    int32_t n_restrict_kernels;      /* number of those passes timed */
 } ns_stats;
 
 /* device arrays addressable by ns_get_array / ns_set_array */

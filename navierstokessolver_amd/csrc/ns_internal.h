@@ -43,7 +43,8 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
 // K2: fused red-black SOR sweep of (I - a L_V) on u and v, (u,v) -> (uo,vo);
 //     residual^2 partials of the input if part != null: u at part[0..n), v at part[n..2n), n returned
 int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
-                      double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st);
+                      double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st,
+                      int which = 3);
 // K3: divergence / dt  + partial sums (sum, sum^2)
 int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* rp,
                double* part, hipStream_t st);
@@ -59,7 +60,8 @@ int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* 
 int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st);
 int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
-                       double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st);
+                       double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st,
+                       int which = 3);
 // A/B reference: LDS-tiled fused sweeps (first version)
 int launch_pois_rbsor_tiled(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                             const double* rp, const double* shift, double* part, hipStream_t st);

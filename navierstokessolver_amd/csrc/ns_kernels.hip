@@ -764,6 +764,7 @@ struct StreamArgs {
     int ldc;
     const double* ec;
     int ncx, ncy, ci0;
+    int nt;                           // non-temporal output stores
 };
 
 // diagonal of the operator at a cell from its row / column coefficient sums
@@ -782,6 +783,16 @@ __device__ __forceinline__ double relax(double q, double xm, double xp, double y
     const double aq = OP == 0 ? s + dg * q : dg * q - alpha * s;
     res = b - aq;
     return q + w * res;
+}
+
+// Streamed field stores bypass the Infinity Cache (non-temporal): the 256 MiB die cache then
+// keeps what the NEXT pass re-reads -- the rhs b, read by every sweep of a solve -- instead
+// of filling with this pass's output (tools/membw2.hip, 4096^2 2-read + 1-write stream:
+// 5.3 TB/s with plain stores, 6.8-7.5 TB/s with nt stores).  NSGPU_NT_STORES=0: plain (A/B).
+typedef double nsd2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_stream(double* p, double2 v, bool nt) {
+    if (nt) __builtin_nontemporal_store(nsd2{v.x, v.y}, reinterpret_cast<nsd2*>(p));
+    else *reinterpret_cast<double2*>(p) = v;
 }
 
 // 1/x to within an ulp without a division: v_rcp_f64 + two Newton steps
@@ -890,7 +901,7 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
                         double2 o = P1;
                         if (v0) o.x = relax<OP>(P1.x, P0.x, P2.x, lf, P1.y, Bm.x, cw, ce, cs0, cn0, dm.d0, dm.w0, alpha, r0);
                         if (v1) o.y = relax<OP>(P1.y, P0.y, P2.y, P1.x, rt, Bm.y, cw, ce, cs1, cn1, dm.d1, dm.w1, alpha, r1);
-                        if (wr) *reinterpret_cast<double2*>(a.out + (ptrdiff_t)m * ld + c0) = o;
+                        if (wr) st_stream(a.out + (ptrdiff_t)m * ld + c0, o, a.nt);
                     }
                 } else if (gim >= 0 && gim < a.nx) {
                     if ((gim & 1) == 0) {  // red = (gi + j) even = c0
@@ -915,7 +926,7 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
                     } else {               // black = c0
                         if (v0) o.x = relax<OP>(R1.x, R0.x, R2.x, lf, R1.y, Bk.x, cw, ce, cs0, cn0, dk.d0, dk.w0, alpha, rr);
                     }
-                    if (wr) *reinterpret_cast<double2*>(a.out + (ptrdiff_t)k * ld + c0) = o;
+                    if (wr) st_stream(a.out + (ptrdiff_t)k * ld + c0, o, a.nt);
                 }
             }
         };
@@ -1080,7 +1091,7 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
             double2 n4 = E1;
             if (k >= ib - EXT && k < ie + EXT) {
                 n4 = half(E0, E1, E2, B4, k, 1);
-                if (k >= ib && k < ie && wr) *reinterpret_cast<double2*>(a.out + (ptrdiff_t)k * ld + c0) = n4;
+                if (k >= ib && k < ie && wr) st_stream(a.out + (ptrdiff_t)k * ld + c0, n4, a.nt);
             }
             if (R5) {
                 // stage 5: residual of the finished row r-5 (FUSE_R: restricted in row pairs)
@@ -1754,15 +1765,20 @@ static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, dou
     a.nx = g.nx; a.ny = g.ny; a.i0 = g.i0; a.nxl = g.nxl; a.ld = g.ld;
     a.nsj = (g.ny + SW - 1) / SW;
     a.part = part;
+    const char* e = getenv("NSGPU_NT_STORES");
+    a.nt = e ? std::atoi(e) != 0 : 1;
     return a;
 }
 
+// count_only: return the strip (= partial) count a launch with residual would have, launch nothing
 template <int OP, bool RB>
-static int launch_stream(StreamArgs a, hipStream_t st) {
+static int launch_stream(StreamArgs a, hipStream_t st, bool count_only = false) {
+    if (count_only) a.part = reinterpret_cast<double*>(1);
     const long cap = resident_waves(a.part ? (const void*)k_sweep<OP, RB, true> : (const void*)k_sweep<OP, RB, false>);
     a.L = strip_rows(a.nxl, a.nsj, cap, 4);
     a.nsi = (a.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
+    if (count_only) return nstr;
     if (a.part) hipLaunchKernelGGL((k_sweep<OP, RB, true>), dim3(nblk), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_sweep<OP, RB, false>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
@@ -1776,13 +1792,15 @@ int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* p
 // two fused red-black sweeps: strips of 120 written columns reading rows ib-4 .. ie+3;
 // with the output residual (part != null) 116 columns, rows ib-5 .. ie+4
 template <int OP>
-static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st) {
+static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st, bool count_only = false) {
+    if (count_only) a.part = reinterpret_cast<double*>(1);
     a.nsj = a.part ? (g.ny + SW2X - 1) / SW2X : (g.ny + SW2 - 1) / SW2;
     const long cap = resident_waves(a.part ? (const void*)k_sweep2<OP, true, FUSE_NONE>
                                            : (const void*)k_sweep2<OP, false, FUSE_NONE>);
     a.L = strip_rows(a.nxl, a.nsj, cap, 16);
     a.nsi = (g.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
+    if (count_only) return nstr;
     if (a.part) hipLaunchKernelGGL((k_sweep2<OP, true, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_sweep2<OP, false, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
@@ -1841,9 +1859,16 @@ int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* 
 }
 
 int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
-                       double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st) {
-    const int n = launch_stream2<1>(stream_args(g, c, u, uo, ru, nullptr, alpha, omega, part, true), g, st);
-    launch_stream2<1>(stream_args(g, c, v, vo, rv, nullptr, alpha, omega, part ? part + n : nullptr, true), g, st);
+                       double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st,
+                       int which) {
+    int n = 0;
+    if (which & 1) n = launch_stream2<1>(stream_args(g, c, u, uo, ru, nullptr, alpha, omega, part, true), g, st);
+    if (which & 2) {
+        StreamArgs a = stream_args(g, c, v, vo, rv, nullptr, alpha, omega, nullptr, true);
+        if (!(which & 1)) n = launch_stream2<1>(a, g, st, true);   // strip count only
+        a.part = part ? part + n : nullptr;
+        n = launch_stream2<1>(a, g, st);
+    }
     return n;
 }
 
@@ -1853,10 +1878,17 @@ int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* 
 }
 
 int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
-                      double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st) {
+                      double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st,
+                      int which) {
     // u and v are independent systems with the same operator: two streaming passes
-    const int n = launch_stream<1, true>(stream_args(g, c, u, uo, ru, nullptr, alpha, omega, part, true), st);
-    launch_stream<1, true>(stream_args(g, c, v, vo, rv, nullptr, alpha, omega, part ? part + n : nullptr, true), st);
+    int n = 0;
+    if (which & 1) n = launch_stream<1, true>(stream_args(g, c, u, uo, ru, nullptr, alpha, omega, part, true), st);
+    if (which & 2) {
+        StreamArgs a = stream_args(g, c, v, vo, rv, nullptr, alpha, omega, nullptr, true);
+        if (!(which & 1)) n = launch_stream<1, true>(a, st, true);   // strip count only
+        a.part = part ? part + n : nullptr;
+        n = launch_stream<1, true>(a, st);
+    }
     return n;
 }
 

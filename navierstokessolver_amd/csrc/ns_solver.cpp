@@ -108,6 +108,7 @@ struct ns_solver {
     ncclComm_t comm = nullptr;
     double ncells = 0;           // global cell count
     std::vector<hipEvent_t> ev;  // timing events (pairs)
+    std::vector<char> evtag;     // per pair: 0 = sweep / prolongation pass, 1 = restriction pass
     int helm_batch0 = 4, pois_batch0 = 8;
     int helm_next = 4;           // first Helmholtz batch of the next step (adaptive unless check_every)
     int helm_adapt = 1;
@@ -115,6 +116,7 @@ struct ns_solver {
     int fuse_restrict = 1;       // NSGPU_FUSED_RESTRICT=0: separate k_restrict pass (A/B)
     int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
     int tile_small = 1;          // NSGPU_TILE_SMALL=0: no LDS-tiled fused passes on small levels (A/B)
+    int helm_split = 1;          // NSGPU_HELM_SPLIT=0: u and v pass by pass (A/B)
     int verbose = 0;             // NSGPU_VERBOSE=1: solver residual histories on stderr
     long pair_min_cells = 2048L * 2048L;   // NSGPU_PAIR_MIN_CELLS: smallest level smoothed in 2-sweep passes
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
@@ -235,26 +237,28 @@ int ensure_events(ns_solver* s, size_t n) {
         HIPCHK(hipEventCreate(&e));
         s->ev.push_back(e);
     }
+    if (s->evtag.size() < n / 2 + 1) s->evtag.resize(n / 2 + 1, 0);
     return 0;
 }
 
-// one Helmholtz sweep U,V -> TMPU,TMPV, then swap so NS_ARR_U/V stay "current"
-int helm_sweep(ns_solver* s, double alpha, double* part) {
+// Helmholtz sweeps of the fields in `which` (1 = u, 2 = v, 3 = both): U,V -> TMPU,TMPV, then
+// swap so NS_ARR_U/V stay "current".  Partials: u at part[0, nb), v at part[nb, 2 nb).
+int helm_sweep(ns_solver* s, double alpha, double* part, int which = 3) {
     const int nb = nsg::launch_helm_sweep(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
                                           s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
-                                          s->arr[NS_ARR_RV], part, s->st);
-    std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
-    std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
+                                          s->arr[NS_ARR_RV], part, s->st, which);
+    if (which & 1) std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
+    if (which & 2) std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
     return nb;
 }
 
 // two Helmholtz sweeps in one pass (temporal blocking), then swap
-int helm_sweep2(ns_solver* s, double alpha, double* part) {
+int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3) {
     const int nb = nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
                                            s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
-                                           s->arr[NS_ARR_RV], part, s->st);
-    std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
-    std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
+                                           s->arr[NS_ARR_RV], part, s->st, which);
+    if (which & 1) std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
+    if (which & 2) std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
     return nb;
 }
 
@@ -263,23 +267,33 @@ int helm_sweep2(ns_solver* s, double alpha, double* part) {
 // first launch to `part_first` (either may be null): a pair reports the residual of its
 // output, a single sweep that of its input.  Returns the last launch's partial count;
 // *first_at / *last_at = the sweep count the reported residuals belong to.
+// Single rank: all of u's passes, then all of v's (helm_split): each field's rhs is then the
+// only re-read stream of its passes and can stay in the Infinity Cache (the outputs are
+// non-temporal stores).  Multi-rank: u and v pass by pass, their ghost rows in one exchange.
 int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* part_last, int* nb_first,
                 int* first_at, int* last_at) {
-    int nb = 0, k = 0, launch = 0;
-    while (k < n) {
-        const int w = (n - k >= 2 && !s->tiled) ? 2 : 1;
-        const bool last = k + w >= n;
-        double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
-        CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, w == 2 ? (part ? 5 : 4) : 2));
-        nb = w == 2 ? helm_sweep2(s, alpha, part) : helm_sweep(s, alpha, part);
-        const int at = w == 2 ? k + 2 : k;
-        if (launch == 0) {
-            if (nb_first) *nb_first = nb;
-            if (first_at) *first_at = at;
+    int nb = 0;
+    const bool split = s->helm_split && s->nranks == 1;
+    for (int which : {split ? 1 : 3, split ? 2 : 0}) {
+        if (!which) break;
+        int k = 0, launch = 0;
+        while (k < n) {
+            const int w = (n - k >= 2 && !s->tiled) ? 2 : 1;
+            const bool last = k + w >= n;
+            double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
+            const int hw = w == 2 ? (part ? 5 : 4) : 2;
+            if (which == 3) CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, hw));
+            else CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
+            nb = w == 2 ? helm_sweep2(s, alpha, part, which) : helm_sweep(s, alpha, part, which);
+            const int at = w == 2 ? k + 2 : k;
+            if (launch == 0) {
+                if (nb_first) *nb_first = nb;
+                if (first_at) *first_at = at;
+            }
+            if (last) *last_at = at;
+            k += w;
+            launch++;
         }
-        if (last) *last_at = at;
-        k += w;
-        launch++;
     }
     return nb;
 }
@@ -542,7 +556,7 @@ int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
         const int w = (n - k >= 2 && pair_level(s, l)) ? 2 : 1;   // two sweeps per HBM pass
         CHK(halo_l(s, l, {L.phi}, 2 * w));
         const bool t = s->timing && l == 0;
-        if (t) HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st));
+        if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st)); s->evtag[ev0 + *tn] = 0; }
         const double* sh = l == 0 ? s->scal + S_SHIFT : nullptr;
         if (w == 2) nsg::launch_pois_rbsor2(L.g, L.c, s->mg_omega_s, L.phi, L.tmp, L.b, sh, nullptr, s->st);
         else nsg::launch_pois_rbsor(L.g, L.c, s->mg_omega_s, L.phi, L.tmp, L.b, sh, nullptr, s->st);
@@ -581,7 +595,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     double tms = 0.0;
     const int per_cycle = s->mg_pre + s->mg_post;
     for (;;) {
-        if (s->timing) CHK(ensure_events(s, 2 * (size_t)(tn + per_cycle)));
+        if (s->timing) CHK(ensure_events(s, 2 * (size_t)(tn + per_cycle + 2)));
         const int ev0 = 0;
         bool done = false;
         for (int l = 0; l < nl - 1 && !done; l++) {
@@ -594,8 +608,11 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
                 // last two pre-smoothing sweeps + residual + restriction in one HBM pass
                 CHK(mg_smooth(s, l, s->mg_pre - 2, &tn, ev0));
                 CHK(halo_l(s, l, {F.phi}, 5));
+                const bool t = s->timing && l == 0;
+                if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn)], s->st)); s->evtag[ev0 + tn] = 1; }
                 nb = (tile_level(s, l) ? nsg::launch_pois_tile2_restrict : nsg::launch_pois_rbsor2_restrict)(
                     F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b, cv.phi, s->part, s->st);
+                if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn) + 1], s->st)); tn++; }
                 std::swap(F.phi, F.tmp);
                 if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
             } else {
@@ -613,9 +630,13 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
                     for (int k = 0; k < tn; k++) {
                         float ms = 0.f;
                         HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
-                        tms += ms;
+                        if (s->evtag[k]) {
+                            if (stt) { stt->t_restrict_kernel_ms += ms; stt->n_restrict_kernels++; }
+                        } else {
+                            tms += ms;
+                            if (stt) stt->n_poisson_kernels++;
+                        }
                     }
-                    if (stt) stt->n_poisson_kernels += tn;
                     tn = 0;
                 }
                 const double r2 = s->hs[S_RES], b2 = s->hs[S_SHIFT + 1];
@@ -642,7 +663,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
                     else CHK(halo_reqs(s, {HaloReq{&C.g, C.phi, 3}, HaloReq{&F.g, F.phi, 5}}));
                 }
                 const bool t = s->timing && l == 0;
-                if (t) HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn)], s->st));
+                if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn)], s->st)); s->evtag[ev0 + tn] = 0; }
                 (tile_level(s, l) ? nsg::launch_pois_tile2_prolong : nsg::launch_pois_rbsor2_prolong)(
                     F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, l == 0 ? s->scal + S_SHIFT : nullptr, cv.g, cv.phi,
                     s->st);
@@ -983,6 +1004,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_FUSED_RESTRICT")) s->fuse_restrict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_HELM_SPLIT")) s->helm_split = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     {

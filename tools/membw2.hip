@@ -1,0 +1,82 @@
+// membw2.hip -- ceiling study for the 2-read + 1-write fp64 stream (24 B/cell) of the sweeps:
+// unrolled grid-stride (U independent 16-B loads of each input in flight per lane), with and
+// without non-temporal loads / stores, at 4096^2 (402 MB, partly Infinity-Cache resident) and
+// 8192^2 (1.6 GB, HBM).  hipcc --offload-arch=gfx950 -O3 -o tools/membw2 tools/membw2.hip
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+template <int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void k_flat(const double2* __restrict__ a, const double2* __restrict__ b,
+                                              double2* __restrict__ c, size_t n2) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i0 = blockIdx.x * 256 + threadIdx.x; i0 < n2; i0 += stride * U) {
+        double2 x[U], y[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const size_t i = i0 + k * stride;
+            if (i < n2) {
+                if (NTL) {
+                    x[k].x = __builtin_nontemporal_load(&a[i].x); x[k].y = __builtin_nontemporal_load(&a[i].y);
+                    y[k].x = __builtin_nontemporal_load(&b[i].x); y[k].y = __builtin_nontemporal_load(&b[i].y);
+                } else { x[k] = a[i]; y[k] = b[i]; }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const size_t i = i0 + k * stride;
+            if (i < n2) {
+                const double2 r = make_double2(x[k].x + 0.5 * y[k].x, x[k].y + 0.5 * y[k].y);
+                if (NTS) { __builtin_nontemporal_store(r.x, &c[i].x); __builtin_nontemporal_store(r.y, &c[i].y); }
+                else c[i] = r;
+            }
+        }
+    }
+}
+
+// copy (1R + 1W) for reference against the guide's 6.3 TB/s
+template <int U>
+__global__ __launch_bounds__(256) void k_copy(const double2* __restrict__ a, double2* __restrict__ c, size_t n2) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i0 = blockIdx.x * 256 + threadIdx.x; i0 < n2; i0 += stride * U) {
+        double2 x[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) { const size_t i = i0 + k * stride; if (i < n2) x[k] = a[i]; }
+#pragma unroll
+        for (int k = 0; k < U; k++) { const size_t i = i0 + k * stride; if (i < n2) c[i] = x[k]; }
+    }
+}
+
+int main(int argc, char** argv) {
+    for (int n : {4096, 8192}) {
+        const size_t N = (size_t)n * n;
+        double *a, *b, *c;
+        hipMalloc(&a, N * 8); hipMalloc(&b, N * 8); hipMalloc(&c, N * 8);
+        hipMemset(a, 0, N * 8); hipMemset(b, 0, N * 8); hipMemset(c, 0, N * 8);
+        hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+        auto timeit = [&](auto launch, const std::string& name, double bytes_per_cell) {
+            for (int w = 0; w < 5; w++) launch();
+            std::vector<float> ts;
+            for (int it = 0; it < 20; it++) {
+                hipEventRecord(e0); launch(); hipEventRecord(e1); hipEventSynchronize(e1);
+                float ms; hipEventElapsedTime(&ms, e0, e1); ts.push_back(ms);
+            }
+            std::sort(ts.begin(), ts.end());
+            printf("n=%d %-34s median %8.1f us  %7.1f GB/s\n", n, name.c_str(), ts[10] * 1e3,
+                   bytes_per_cell * N / (ts[10] * 1e-3) / 1e9);
+        };
+        for (int g : {1024, 2048, 4096}) {
+            auto G = std::to_string(g);
+            timeit([&] { hipLaunchKernelGGL((k_flat<1, false, false>), dim3(g), dim3(256), 0, 0, (const double2*)a, (const double2*)b, (double2*)c, N / 2); }, "2R1W U1 grid=" + G, 24);
+            timeit([&] { hipLaunchKernelGGL((k_flat<4, false, false>), dim3(g), dim3(256), 0, 0, (const double2*)a, (const double2*)b, (double2*)c, N / 2); }, "2R1W U4 grid=" + G, 24);
+            timeit([&] { hipLaunchKernelGGL((k_flat<4, false, true>), dim3(g), dim3(256), 0, 0, (const double2*)a, (const double2*)b, (double2*)c, N / 2); }, "2R1W U4 ntstore grid=" + G, 24);
+            timeit([&] { hipLaunchKernelGGL((k_flat<4, true, true>), dim3(g), dim3(256), 0, 0, (const double2*)a, (const double2*)b, (double2*)c, N / 2); }, "2R1W U4 ntload+ntstore grid=" + G, 24);
+            timeit([&] { hipLaunchKernelGGL((k_copy<4>), dim3(g), dim3(256), 0, 0, (const double2*)a, (double2*)c, N / 2); }, "copy U4 grid=" + G, 16);
+        }
+        hipFree(a); hipFree(b); hipFree(c);
+    }
+    return 0;
+}
