@@ -765,6 +765,7 @@ struct StreamArgs {
     const double* ec;
     int ncx, ncy, ci0;
     int nt;                           // non-temporal output stores
+    int alt;                          // alternate strips walk upwards
 };
 
 // diagonal of the operator at a cell from its row / column coefficient sums
@@ -975,12 +976,190 @@ constexpr int SW2X = 116;
 constexpr int SD2 = 3;
 constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2;
 
-template <int OP, bool RES, int FUSE>
-__global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
+// one strip of k_sweep2, walked downwards (DIR = 1) or upwards (DIR = -1); returns the
+// strip's residual partial (R5)
+// (two instantiations: runtime window selects would cost ~50 VGPRs)
+template <int OP, bool RES, int FUSE, int DIR>
+__device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double (*rc)[4], int wid, int lane) {
     constexpr bool XR = FUSE == FUSE_R, XP = FUSE == FUSE_P;
-    constexpr bool R5 = RES || XR;                 // the fifth (output residual) stage
+    constexpr bool R5 = RES || XR;
     constexpr int EXT = (R5 || XP) ? 1 : 0;
     constexpr int SWc = EXT ? SW2X : SW2;
+    double res = 0.0;
+    const int si = wid / a.nsj, sj = wid - si * a.nsj;
+    const int jb = sj * SWc, ib = si * a.L;
+    const int ie = min(ib + a.L, a.nxl);
+    const int ny = a.ny, ld = a.ld;
+    const int c0 = jb - 4 - 2 * EXT + 2 * lane, c1 = c0 + 1;
+    const int lc = min(max(c0, 0), ld - 2);
+    const bool v0 = c0 >= 0 && c0 < ny, v1 = c1 >= 0 && c1 < ny;
+    const bool wr = lane >= 2 + EXT && lane <= 61 - EXT && c0 < ny;
+    const bool o0 = wr && v0, o1 = wr && v1;
+    const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
+    const double cs0 = a.cs[k0], cn0 = a.cn[k0], cd0 = cs0 + cn0 + (OP == 1 ? a.by[k0] : 0.0);
+    const double cs1 = a.cs[k1], cn1 = a.cn[k1], cd1 = cs1 + cn1 + (OP == 1 ? a.by[k1] : 0.0);
+    const double shift = (OP == 0 && a.shift) ? a.shift[0] : 0.0;
+    const double alpha = a.alpha, omega = a.omega;
+    const int rlo = -HALO, rhi = a.nxl + HALO - 1;
+
+    double2 Q[SD2], QB[SD2], QE[SD2];
+    // phi rows ib-4-EXT .. ie+3+EXT and b rows ib-3-EXT .. ie+2+EXT (the first red
+    // stage's) are read; the rest are clamped onto fetched rows (see k_sweep)
+    const int r0 = ib - 4 - EXT, r1 = ie + 3 + EXT;
+    // DIR < 0 walks the strip upwards: the prefetch overrun and the rows before the first
+    // red stage's are then at the other end
+    const int phi_lo = DIR > 0 ? rlo : max(r0, rlo), phi_hi = DIR > 0 ? min(r1, rhi) : rhi;
+    const int b_lo = DIR > 0 ? max(ib - 3 - EXT, rlo) : rlo, b_hi = DIR > 0 ? rhi : min(ie + 2 + EXT, rhi);
+    // FUSE_P: this lane's coarse column (its pair c0, c1 = 2J, 2J+1) and whether J -+ 1
+    // exist (a missing one is replaced by J: the wall reflection of k_prolong)
+    const int Jc = c0 >> 1;
+    const int Jl = XP ? min(max(Jc, 0), a.ncy - 1) : 0;
+    const bool jm_ok = Jc - 1 >= 0, jp_ok = Jc + 1 < a.ncy;
+    auto load = [&](int slot_r, double2& p, double2& bb, double2& ee) {
+        const int lp = min(max(slot_r, phi_lo), phi_hi), lb = min(max(slot_r - DIR, b_lo), b_hi);
+        p = *reinterpret_cast<const double2*>(a.in + (ptrdiff_t)lp * ld + lc);
+        bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
+        if (XP) {
+            const int I = lp >> 1;                      // floor, also for ghost rows
+            int In = (lp & 1) ? I + 1 : I - 1;
+            if (a.ci0 + In < 0 || a.ci0 + In >= a.ncx) In = I;
+            ee.x = a.ec[(ptrdiff_t)I * a.ldc + Jl];
+            ee.y = a.ec[(ptrdiff_t)In * a.ldc + Jl];
+        }
+    };
+    // windows (3 rows each) of the stages' inputs, rhs rows r-1 .. r-5
+    double2 P0 = {0, 0}, P1 = {0, 0}, P2 = {0, 0};     // old:           rows r-2 .. r
+    double2 A0 = {0, 0}, A1 = {0, 0}, A2 = {0, 0};     // after red 1:   rows r-3 .. r-1
+    double2 C0 = {0, 0}, C1 = {0, 0}, C2 = {0, 0};     // after black 1: rows r-4 .. r-2
+    double2 E0 = {0, 0}, E1 = {0, 0}, E2 = {0, 0};     // after red 2:   rows r-5 .. r-3
+    double2 F0 = {0, 0}, F1 = {0, 0}, F2 = {0, 0};     // after black 2: rows r-6 .. r-4 (XR)
+    double2 B1 = {0, 0}, B2 = {0, 0}, B3 = {0, 0}, B4 = {0, 0}, B5 = {0, 0};
+    DiagCache<OP> dc;
+    // XR: this lane's column spacings, the even row's partial sum and spacing
+    const double hy0 = XR ? a.hy[k0] : 0.0, hy1 = XR ? a.hy[k1] : 0.0;
+    double xs = 0.0, hxe = 0.0, ro0 = 0.0, ro1 = 0.0, hxo = 0.0;
+
+    // one colour update of row `row` (window W0 above, W1 the row, W2 below); colour
+    // parity: update c0 when (gi + c0) % 2 == par
+    auto half = [&](const double2& W0, const double2& W1, const double2& W2, const double2& B, int row,
+                    int par) -> double2 {
+        double2 o = W1;
+        const int gi = a.i0 + row;
+        if (gi < 0 || gi >= a.nx) return o;
+        const double lf = __shfl_up(W1.y, 1, 64), rt = __shfl_down(W1.x, 1, 64);
+        const double* rw = rc[row - ib + RC_OFF];
+        const double cw = rw[0], ce = rw[1];
+        dc.at(rw[2], cd0, cd1, alpha, omega);
+        double rr;
+        if ((gi & 1) == par) {
+            if (v0) o.x = relax<OP>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, dc.d0, dc.w0, alpha, rr);
+        } else {
+            if (v1) o.y = relax<OP>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, dc.d1, dc.w1, alpha, rr);
+        }
+        return o;
+    };
+
+    auto step = [&](double2 p, const double2 bb, const double2 ee, int r) {
+        if (XP) {
+            // phi += P(e): e(I, J) = ee.x, e(In, J) = ee.y, column neighbours from lanes -+ 1
+            double m0 = __shfl_up(ee.x, 1, 64), m1 = __shfl_up(ee.y, 1, 64);
+            double q0 = __shfl_down(ee.x, 1, 64), q1 = __shfl_down(ee.y, 1, 64);
+            if (!jm_ok) { m0 = ee.x; m1 = ee.y; }
+            if (!jp_ok) { q0 = ee.x; q1 = ee.y; }
+            p.x += (9.0 * ee.x + 3.0 * ee.y + 3.0 * m0 + m1) * 0.0625;
+            p.y += (9.0 * ee.x + 3.0 * ee.y + 3.0 * q0 + q1) * 0.0625;
+        }
+        P0 = P1; P1 = P2; P2 = p;
+        B5 = B4; B4 = B3; B3 = B2; B2 = B1;
+        B1 = make_double2(bb.x - shift, bb.y - shift);
+        // stage 1: red of sweep 1 at m = r-1
+        // (windows run oldest -> newest; half() wants rows i-1, i, i+1: swapped when DIR < 0)
+        const int m = r - DIR;
+        double2 n1 = P1;
+        if (m >= ib - 3 - EXT && m <= ie + 2 + EXT) n1 = DIR > 0 ? half(P0, P1, P2, B1, m, 0) : half(P2, P1, P0, B1, m, 0);
+        A0 = A1; A1 = A2; A2 = n1;
+        // stage 2: black of sweep 1 at r-2
+        double2 n2 = A1;
+        const int m2 = r - 2 * DIR;
+        if (m2 >= ib - 2 - EXT && m2 <= ie + 1 + EXT) n2 = DIR > 0 ? half(A0, A1, A2, B2, m2, 1) : half(A2, A1, A0, B2, m2, 1);
+        C0 = C1; C1 = C2; C2 = n2;
+        // stage 3: red of sweep 2 at r-3
+        double2 n3 = C1;
+        const int m3 = r - 3 * DIR;
+        if (m3 >= ib - 1 - EXT && m3 <= ie + EXT) n3 = DIR > 0 ? half(C0, C1, C2, B3, m3, 0) : half(C2, C1, C0, B3, m3, 0);
+        E0 = E1; E1 = E2; E2 = n3;
+        // stage 4: black of sweep 2 at r-4, stored on the strip's rows
+        const int k = r - 4 * DIR;
+        double2 n4 = E1;
+        if (k >= ib - EXT && k < ie + EXT) {
+            n4 = DIR > 0 ? half(E0, E1, E2, B4, k, 1) : half(E2, E1, E0, B4, k, 1);
+            if (k >= ib && k < ie && wr) st_stream(a.out + (ptrdiff_t)k * ld + c0, n4, a.nt);
+        }
+        if (R5) {
+            // stage 5: residual of the finished row r-5 (FUSE_R: restricted in row pairs)
+            F0 = F1; F1 = F2; F2 = n4;
+            const int m5 = r - 5 * DIR;
+            const double2 Fm = DIR > 0 ? F0 : F2, Fp = DIR > 0 ? F2 : F0;   // rows m5 - 1, m5 + 1
+            if (m5 >= ib && m5 < ie) {
+                const double lf = __shfl_up(F1.y, 1, 64), rt = __shfl_down(F1.x, 1, 64);
+                const double* rw = rc[m5 - ib + RC_OFF];
+                const double cw = rw[0], ce = rw[1], hxr = rw[3];
+                dc.at(rw[2], cd0, cd1, alpha, omega);
+                double r0, r1;
+                relax<OP>(F1.x, Fm.x, Fp.x, lf, F1.y, B5.x, cw, ce, cs0, cn0, dc.d0, 0.0, alpha, r0);
+                relax<OP>(F1.y, Fm.y, Fp.y, F1.x, rt, B5.y, cw, ce, cs1, cn1, dc.d1, 0.0, alpha, r1);
+                res += (o0 ? r0 * r0 : 0.0) + (o1 ? r1 * r1 : 0.0);
+                if (!XR) {
+                } else if (DIR < 0) {
+                    // upwards: the odd row of a pair arrives first; the sum keeps k_restrict's
+                    // order (even row, then odd row)
+                    if ((a.i0 + m5) & 1) {
+                        ro0 = r0; ro1 = r1; hxo = hxr;
+                    } else {
+                        xs = (hxr * hy0) * r0;
+                        xs = xs + (hxr * hy1) * r1;
+                        xs = xs + (hxo * hy0) * ro0;
+                        xs = xs + (hxo * hy1) * ro1;
+                        if (wr) {
+                            const ptrdiff_t o = (ptrdiff_t)(m5 >> 1) * a.ldc + (c0 >> 1);
+                            a.bc[o] = xs / ((hxr + hxo) * (hy0 + hy1));
+                            a.pc[o] = 0.0;
+                        }
+                    }
+                } else if (((a.i0 + m5) & 1) == 0) {
+                    xs = (hxr * hy0) * r0;
+                    xs = xs + (hxr * hy1) * r1;
+                    hxe = hxr;
+                } else {
+                    xs = xs + (hxr * hy0) * r0;
+                    xs = xs + (hxr * hy1) * r1;
+                    if (wr) {
+                        const ptrdiff_t o = (ptrdiff_t)(m5 >> 1) * a.ldc + (c0 >> 1);
+                        a.bc[o] = xs / ((hxe + hxr) * (hy0 + hy1));
+                        a.pc[o] = 0.0;
+                    }
+                }
+            }
+        }
+    };
+
+    const int rs = DIR > 0 ? r0 : r1, nr = r1 - r0 + 1;
+#pragma unroll
+    for (int q = 0; q < SD2; q++) load(rs + DIR * q, Q[q], QB[q], QE[q]);
+    for (int t = 0; t < nr; t += SD2) {
+#pragma unroll
+        for (int q = 0; q < SD2; q++) {
+            if (t + q < nr) step(Q[q], QB[q], QE[q], rs + DIR * (t + q));
+            load(rs + DIR * (t + q + SD2), Q[q], QB[q], QE[q]);
+        }
+    }
+    return res;
+}
+
+template <int OP, bool RES, int FUSE>
+__global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
+    constexpr bool XR = FUSE == FUSE_R;
+    constexpr bool R5 = RES || XR;                 // the fifth (output residual) stage
     __shared__ double rcs[4][RC_MAX][4];
     const int lane = threadIdx.x & 63;
     const int nstr = a.nsj * a.nsi;
@@ -990,149 +1169,12 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
     __syncthreads();
     double res = 0.0;
     if (wid < nstr) {
-        const int si = wid / a.nsj, sj = wid - si * a.nsj;
-        const int jb = sj * SWc, ib = si * a.L;
-        const int ie = min(ib + a.L, a.nxl);
-        const int ny = a.ny, ld = a.ld;
-        const int c0 = jb - 4 - 2 * EXT + 2 * lane, c1 = c0 + 1;
-        const int lc = min(max(c0, 0), ld - 2);
-        const bool v0 = c0 >= 0 && c0 < ny, v1 = c1 >= 0 && c1 < ny;
-        const bool wr = lane >= 2 + EXT && lane <= 61 - EXT && c0 < ny;
-        const bool o0 = wr && v0, o1 = wr && v1;
-        const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
-        const double cs0 = a.cs[k0], cn0 = a.cn[k0], cd0 = cs0 + cn0 + (OP == 1 ? a.by[k0] : 0.0);
-        const double cs1 = a.cs[k1], cn1 = a.cn[k1], cd1 = cs1 + cn1 + (OP == 1 ? a.by[k1] : 0.0);
-        const double shift = (OP == 0 && a.shift) ? a.shift[0] : 0.0;
-        const double alpha = a.alpha, omega = a.omega;
-        const int rlo = -HALO, rhi = a.nxl + HALO - 1;
-
-        double2 Q[SD2], QB[SD2], QE[SD2];
-        // phi rows ib-4-EXT .. ie+3+EXT and b rows ib-3-EXT .. ie+2+EXT (the first red
-        // stage's) are read; the rest are clamped onto fetched rows (see k_sweep)
-        const int r0 = ib - 4 - EXT, r1 = ie + 3 + EXT;
-        const int blo = max(ib - 3 - EXT, rlo), phi_hi = min(r1, rhi);
-        // FUSE_P: this lane's coarse column (its pair c0, c1 = 2J, 2J+1) and whether J -+ 1
-        // exist (a missing one is replaced by J: the wall reflection of k_prolong)
-        const int Jc = c0 >> 1;
-        const int Jl = XP ? min(max(Jc, 0), a.ncy - 1) : 0;
-        const bool jm_ok = Jc - 1 >= 0, jp_ok = Jc + 1 < a.ncy;
-        auto load = [&](int slot_r, double2& p, double2& bb, double2& ee) {
-            const int lp = min(max(slot_r, rlo), phi_hi), lb = min(max(slot_r - 1, blo), rhi);
-            p = *reinterpret_cast<const double2*>(a.in + (ptrdiff_t)lp * ld + lc);
-            bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
-            if (XP) {
-                const int I = lp >> 1;                      // floor, also for ghost rows
-                int In = (lp & 1) ? I + 1 : I - 1;
-                if (a.ci0 + In < 0 || a.ci0 + In >= a.ncx) In = I;
-                ee.x = a.ec[(ptrdiff_t)I * a.ldc + Jl];
-                ee.y = a.ec[(ptrdiff_t)In * a.ldc + Jl];
-            }
-        };
-        // windows (3 rows each) of the stages' inputs, rhs rows r-1 .. r-5
-        double2 P0 = {0, 0}, P1 = {0, 0}, P2 = {0, 0};     // old:           rows r-2 .. r
-        double2 A0 = {0, 0}, A1 = {0, 0}, A2 = {0, 0};     // after red 1:   rows r-3 .. r-1
-        double2 C0 = {0, 0}, C1 = {0, 0}, C2 = {0, 0};     // after black 1: rows r-4 .. r-2
-        double2 E0 = {0, 0}, E1 = {0, 0}, E2 = {0, 0};     // after red 2:   rows r-5 .. r-3
-        double2 F0 = {0, 0}, F1 = {0, 0}, F2 = {0, 0};     // after black 2: rows r-6 .. r-4 (XR)
-        double2 B1 = {0, 0}, B2 = {0, 0}, B3 = {0, 0}, B4 = {0, 0}, B5 = {0, 0};
-        DiagCache<OP> dc;
-        // XR: this lane's column spacings, the even row's partial sum and spacing
-        const double hy0 = XR ? a.hy[k0] : 0.0, hy1 = XR ? a.hy[k1] : 0.0;
-        double xs = 0.0, hxe = 0.0;
-
-        // one colour update of row `row` (window W0 above, W1 the row, W2 below); colour
-        // parity: update c0 when (gi + c0) % 2 == par
-        auto half = [&](const double2& W0, const double2& W1, const double2& W2, const double2& B, int row,
-                        int par) -> double2 {
-            double2 o = W1;
-            const int gi = a.i0 + row;
-            if (gi < 0 || gi >= a.nx) return o;
-            const double lf = __shfl_up(W1.y, 1, 64), rt = __shfl_down(W1.x, 1, 64);
-            const double* rw = rc[row - ib + RC_OFF];
-            const double cw = rw[0], ce = rw[1];
-            dc.at(rw[2], cd0, cd1, alpha, omega);
-            double rr;
-            if ((gi & 1) == par) {
-                if (v0) o.x = relax<OP>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, dc.d0, dc.w0, alpha, rr);
-            } else {
-                if (v1) o.y = relax<OP>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, dc.d1, dc.w1, alpha, rr);
-            }
-            return o;
-        };
-
-        auto step = [&](double2 p, const double2 bb, const double2 ee, int r) {
-            if (XP) {
-                // phi += P(e): e(I, J) = ee.x, e(In, J) = ee.y, column neighbours from lanes -+ 1
-                double m0 = __shfl_up(ee.x, 1, 64), m1 = __shfl_up(ee.y, 1, 64);
-                double q0 = __shfl_down(ee.x, 1, 64), q1 = __shfl_down(ee.y, 1, 64);
-                if (!jm_ok) { m0 = ee.x; m1 = ee.y; }
-                if (!jp_ok) { q0 = ee.x; q1 = ee.y; }
-                p.x += (9.0 * ee.x + 3.0 * ee.y + 3.0 * m0 + m1) * 0.0625;
-                p.y += (9.0 * ee.x + 3.0 * ee.y + 3.0 * q0 + q1) * 0.0625;
-            }
-            P0 = P1; P1 = P2; P2 = p;
-            B5 = B4; B4 = B3; B3 = B2; B2 = B1;
-            B1 = make_double2(bb.x - shift, bb.y - shift);
-            // stage 1: red of sweep 1 at m = r-1
-            const int m = r - 1;
-            double2 n1 = P1;
-            if (m >= ib - 3 - EXT && m <= ie + 2 + EXT) n1 = half(P0, P1, P2, B1, m, 0);
-            A0 = A1; A1 = A2; A2 = n1;
-            // stage 2: black of sweep 1 at r-2
-            double2 n2 = A1;
-            if (r - 2 >= ib - 2 - EXT && r - 2 <= ie + 1 + EXT) n2 = half(A0, A1, A2, B2, r - 2, 1);
-            C0 = C1; C1 = C2; C2 = n2;
-            // stage 3: red of sweep 2 at r-3
-            double2 n3 = C1;
-            if (r - 3 >= ib - 1 - EXT && r - 3 <= ie + EXT) n3 = half(C0, C1, C2, B3, r - 3, 0);
-            E0 = E1; E1 = E2; E2 = n3;
-            // stage 4: black of sweep 2 at r-4, stored on the strip's rows
-            const int k = r - 4;
-            double2 n4 = E1;
-            if (k >= ib - EXT && k < ie + EXT) {
-                n4 = half(E0, E1, E2, B4, k, 1);
-                if (k >= ib && k < ie && wr) st_stream(a.out + (ptrdiff_t)k * ld + c0, n4, a.nt);
-            }
-            if (R5) {
-                // stage 5: residual of the finished row r-5 (FUSE_R: restricted in row pairs)
-                F0 = F1; F1 = F2; F2 = n4;
-                const int m5 = r - 5;
-                if (m5 >= ib && m5 < ie) {
-                    const double lf = __shfl_up(F1.y, 1, 64), rt = __shfl_down(F1.x, 1, 64);
-                    const double* rw = rc[m5 - ib + RC_OFF];
-                    const double cw = rw[0], ce = rw[1], hxr = rw[3];
-                    dc.at(rw[2], cd0, cd1, alpha, omega);
-                    double r0, r1;
-                    relax<OP>(F1.x, F0.x, F2.x, lf, F1.y, B5.x, cw, ce, cs0, cn0, dc.d0, 0.0, alpha, r0);
-                    relax<OP>(F1.y, F0.y, F2.y, F1.x, rt, B5.y, cw, ce, cs1, cn1, dc.d1, 0.0, alpha, r1);
-                    res += (o0 ? r0 * r0 : 0.0) + (o1 ? r1 * r1 : 0.0);
-                    if (!XR) {
-                    } else if (((a.i0 + m5) & 1) == 0) {
-                        xs = (hxr * hy0) * r0;
-                        xs = xs + (hxr * hy1) * r1;
-                        hxe = hxr;
-                    } else {
-                        xs = xs + (hxr * hy0) * r0;
-                        xs = xs + (hxr * hy1) * r1;
-                        if (wr) {
-                            const ptrdiff_t o = (ptrdiff_t)(m5 >> 1) * a.ldc + (c0 >> 1);
-                            a.bc[o] = xs / ((hxe + hxr) * (hy0 + hy1));
-                            a.pc[o] = 0.0;
-                        }
-                    }
-                }
-            }
-        };
-
-#pragma unroll
-        for (int q = 0; q < SD2; q++) load(r0 + q, Q[q], QB[q], QE[q]);
-        for (int r = r0; r <= r1; r += SD2) {
-#pragma unroll
-            for (int q = 0; q < SD2; q++) {
-                if (r + q <= r1) step(Q[q], QB[q], QE[q], r + q);
-                load(r + q + SD2, Q[q], QB[q], QE[q]);
-            }
-        }
+        // alternate strips walk in opposite directions (a.alt): the halo rows two strips
+        // share are then read by both at about the same time -- an L2 hit for the second --
+        // instead of at opposite ends of the kernel (each row band read twice from HBM)
+        const int si = wid / a.nsj;
+        if (a.alt && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1>(a, rc, wid, lane);
+        else res = sweep2_strip<OP, RES, FUSE, 1>(a, rc, wid, lane);
     }
     if (R5) {
 #pragma unroll
@@ -1767,6 +1809,8 @@ static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, dou
     a.part = part;
     const char* e = getenv("NSGPU_NT_STORES");
     a.nt = e ? std::atoi(e) != 0 : 1;
+    const char* e2 = getenv("NSGPU_ALT_DIR");   // NSGPU_ALT_DIR=0: every strip walks downwards (A/B)
+    a.alt = e2 ? std::atoi(e2) != 0 : 1;
     return a;
 }
 
