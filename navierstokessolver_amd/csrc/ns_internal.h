@@ -83,6 +83,8 @@ void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t 
 void launch_finish_mean(const double* sums, double ncells, double* shift_and_bn2, hipStream_t st);
 // (sum f, sum f^2) partials over own cells
 int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st);
+// out = a x + b y over the slab's own cells
+void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st);
 // random fill of phi, rhs (sweep benchmark input)
 void launch_fill_random(const Geo& g, double* phi, double* rp, uint64_t seed, hipStream_t st);
 

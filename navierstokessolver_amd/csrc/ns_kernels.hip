@@ -1695,6 +1695,16 @@ __global__ void k_fill_random(Geo g, double* phi, double* rp, uint64_t seed) {
     rp[(ptrdiff_t)li * g.ld + j] = 2.0 * ((b >> 11) * s) - 1.0;
 }
 
+// out = a x + b y over the slab's own cells (the Poisson initial-guess extrapolation)
+__global__ __launch_bounds__(256) void k_axpby(Geo g, double a, const double* __restrict__ x, double b,
+                                               const double* __restrict__ y, double* __restrict__ out) {
+    const int j = blockIdx.x * 64 + threadIdx.x;
+    const int li = blockIdx.y * 4 + threadIdx.y;
+    if (j >= g.ny || li >= g.nxl) return;
+    const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
+    out[o] = a * x[o] + b * y[o];
+}
+
 // ---------------------------------------------------------------- launchers
 static inline dim3 cell_grid(const Geo& g) { return dim3((g.ny + 63) / 64, (g.nxl + 3) / 4); }
 
@@ -2016,6 +2026,9 @@ int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st) {
     const dim3 cg = cell_grid(g, rows);
     hipLaunchKernelGGL(k_sums, cg, dim3(64, 4), 0, st, g, f, part, rows);
     return (int)(cg.x * cg.y);
+}
+void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_axpby, cell_grid(g), dim3(64, 4), 0, st, g, a, x, b, y, out);
 }
 void launch_fill_random(const Geo& g, double* phi, double* rp, uint64_t seed, hipStream_t st) {
     hipLaunchKernelGGL(k_fill_random, cell_grid(g), dim3(64, 4), 0, st, g, phi, rp, seed);

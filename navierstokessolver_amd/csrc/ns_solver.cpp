@@ -117,6 +117,10 @@ struct ns_solver {
     int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
     int tile_small = 1;          // NSGPU_TILE_SMALL=0: no LDS-tiled fused passes on small levels (A/B)
     int helm_split = 1;          // NSGPU_HELM_SPLIT=0: u and v pass by pass (A/B)
+    int phi_extrap = 1;          // NSGPU_PHI_EXTRAP=0: Poisson initial guess phi^{n-1} (A/B)
+    double* phim = nullptr;      // phi^{n-2} (the extrapolation's second point; rotates with PHI / TMP)
+    double* phim_mem = nullptr;  // the extra plane's allocation
+    bool phim_valid = false;
     int verbose = 0;             // NSGPU_VERBOSE=1: solver residual histories on stderr
     long pair_min_cells = 2048L * 2048L;   // NSGPU_PAIR_MIN_CELLS: smallest level smoothed in 2-sweep passes
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
@@ -821,6 +825,26 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
     return 0;
 }
 
+// Poisson initial guess: the reference warm-starts from phi^{n-1} (KSPSetInitialGuessNonzero,
+// FluidSolver.cpp:54); here from the linear extrapolation 2 phi^{n-1} - phi^{n-2}, which is
+// O(dt^2) closer to phi^n (the converged answer is the same: both solve to rtol).  The
+// three planes PHI (phi^{n-1}), phim (phi^{n-2}) and TMP rotate: no copies.
+int extrapolate_phi(ns_solver* s) {
+    if (!s->phim) return 0;
+    if (!s->phim_valid) {
+        HIPCHK(hipMemcpyAsync(s->phim - (size_t)nsg::HALO * s->g.ld, s->arr[NS_ARR_PHI] - (size_t)nsg::HALO * s->g.ld,
+                              s->plane * sizeof(double), hipMemcpyDeviceToDevice, s->st));
+        s->phim_valid = true;
+        return 0;
+    }
+    nsg::launch_axpby(s->g, 2.0, s->arr[NS_ARR_PHI], -1.0, s->phim, s->arr[NS_ARR_TMP], s->st);
+    double* prev = s->arr[NS_ARR_PHI];
+    s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
+    s->arr[NS_ARR_TMP] = s->phim;
+    s->phim = prev;
+    return 0;
+}
+
 // K3 + null-space mean
 int divergence(ns_solver* s) {
     const int nb = nsg::launch_div(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_RPHI],
@@ -1005,6 +1029,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_SPLIT")) s->helm_split = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     {
@@ -1032,6 +1057,11 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     }
     if (hipMemsetAsync(s->base, 0, s->plane * NS_NUM_ARR * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     for (int k = 0; k < NS_NUM_ARR; k++) s->arr[k] = s->base + k * s->plane + (size_t)nsg::HALO * g.ld;
+    if (s->phi_extrap) {
+        if (hipMalloc(&s->phim_mem, s->plane * sizeof(double)) != hipSuccess) { set_err("hipMalloc phim failed"); return fail(NS_ENOMEM); }
+        if (hipMemsetAsync(s->phim_mem, 0, s->plane * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
+        s->phim = s->phim_mem + (size_t)nsg::HALO * g.ld;
+    }
 
     // coefficient tables (ConstructLHS, FluidSolver.cpp:113-131)
     std::vector<double> hx0(gd->hx, gd->hx + g.nx), hy0(gd->hy, gd->hy + g.ny);
@@ -1084,6 +1114,7 @@ void ns_destroy(ns_solver* s) {
         if (s->lv[l].coef) (void)hipFree(s->lv[l].coef);
     }
     if (s->base) (void)hipFree(s->base);
+    if (s->phim_mem) (void)hipFree(s->phim_mem);
     if (s->coef) (void)hipFree(s->coef);
     if (s->part) (void)hipFree(s->part);
     if (s->scal) (void)hipFree(s->scal);
@@ -1109,6 +1140,7 @@ int ns_step(ns_solver* s, ns_stats* out) {
     CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
     CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
+    CHK(extrapolate_phi(s));
     if (s->poisson == NS_POISSON_MG) CHK(pois_solve_mg(s, &st.it_phi, &st.res_phi, &st));  // KSPSolve(phiSolver) (:551)
     else CHK(pois_solve(s, &st.it_phi, &st.res_phi, &st));
     CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
@@ -1142,6 +1174,7 @@ int ns_set_array(ns_solver* s, int which, const double* host) {
                             s->g.nxl, hipMemcpyHostToDevice, s->st));
     // keep the derived scalars consistent with an injected right-hand side
     if (which == NS_ARR_RPHI) CHK(rhs_mean(s));
+    if (which == NS_ARR_PHI || which == NS_ARR_TMP) s->phim_valid = false;
     if (which == NS_ARR_RU || which == NS_ARR_RV) CHK(helm_bnorm(s));
     HIPCHK(hipStreamSynchronize(s->st));
     return 0;
