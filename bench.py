@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--time-every", type=int, default=3,
+                    help="HIP-event kernel timing on every k-th timed step (each event pair costs a few us of "
+                         "GPU idle; 0 = none)")
     return ap.parse_args()
 
 
@@ -107,7 +110,11 @@ def main():
         solver.step()
     barrier()
     t0 = time.perf_counter()
-    stats = [solver.step() for _ in range(args.steps)]
+    stats = []
+    for k in range(args.steps):
+        if args.time_every != 1:
+            solver.set_timing(args.time_every > 0 and k % args.time_every == 0)
+        stats.append(solver.step())
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:

@@ -150,6 +150,9 @@ void ns_destroy(ns_solver* s);
 /* ---- one full time step: the body of FluidSolver::Solve's loop (FluidSolver.cpp:546-560) ---- */
 int  ns_step(ns_solver* s, ns_stats* out);
 
+/* per-kernel HIP-event timing (ns_params.timing) switched on / off between steps */
+int  ns_set_timing(ns_solver* s, int on);
+
 /* ---- state access (host buffers, local slab, compact-id order) ---- */
 int  ns_get_fields(ns_solver* s, double* u, double* v, double* phi);
 int  ns_set_fields(ns_solver* s, const double* u, const double* v, const double* phi,

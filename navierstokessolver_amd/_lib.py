@@ -84,6 +84,7 @@ SIGNATURES = {
     "ns_fill_random": (ctypes.c_int, [_P, ctypes.c_uint64]),
     "ns_mg_transfer": (ctypes.c_int, [_P, ctypes.c_int, _D]),
     "ns_time_poisson": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _D]),
+    "ns_set_timing": (ctypes.c_int, [_P, ctypes.c_int]),
     "ns_slab_range": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                      ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     "ns_nccl_id_size": (ctypes.c_int, []),

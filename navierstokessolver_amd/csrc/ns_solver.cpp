@@ -118,6 +118,8 @@ struct ns_solver {
     int tile_small = 1;          // NSGPU_TILE_SMALL=0: no LDS-tiled fused passes on small levels (A/B)
     int helm_split = 1;          // NSGPU_HELM_SPLIT=0: u and v pass by pass (A/B)
     int phi_extrap = 1;          // NSGPU_PHI_EXTRAP=0: Poisson initial guess phi^{n-1} (A/B)
+    int mg_predict = 1;          // NSGPU_MG_PREDICT=0: a residual check (host sync) after every V-cycle
+    double mg_rate2 = 0.0;       // last measured per-cycle contraction of ||r||^2
     double* phim = nullptr;      // phi^{n-2} (the extrapolation's second point; rotates with PHI / TMP)
     double* phim_mem = nullptr;  // the extra plane's allocation
     bool phim_valid = false;
@@ -598,6 +600,11 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     int cycles = 0, tn = 0, nchk = 0;
     double tms = 0.0;
     const int per_cycle = s->mg_pre + s->mg_post;
+    // residual checks (host syncs): after cycle 0, then where the contraction rate (measured
+    // between this solve's checks, else the previous solve's) predicts convergence -- the
+    // cycles in between run without a host round trip
+    int next_chk = 0, prev_c = -1;
+    double prev_rr = -1.0;
     for (;;) {
         if (s->timing) CHK(ensure_events(s, 2 * (size_t)(tn + per_cycle + 2)));
         const int ev0 = 0;
@@ -624,8 +631,8 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
                 CHK(halo_l(s, l, {F.phi}, 1));
                 nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, sh, cv.g, C.c, cv.b, cv.phi, s->part, s->st);
             }
-            if (l == 0) {
-                // fine residual after pre-smoothing: the convergence test (one host sync per cycle)
+            if (l == 0 && (cycles >= next_chk || cycles >= maxc)) {
+                // fine residual after pre-smoothing: the convergence test (a host sync)
                 nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
                 CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
                 CHK(fetch(s));
@@ -648,6 +655,25 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
                 if (s->verbose) fprintf(stderr, "nsgpu poisson: cycle %d rel. residual after pre-smoothing %.3e\n", cycles, *res);
                 if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = cycles; return NS_EDIVERGE; }
                 if (r2 <= tol2 * b2 || r2 == 0.0 || cycles >= maxc) done = true;
+                else if (s->mg_predict) {
+                    const double rr = r2 / b2;
+                    double rate = s->mg_rate2;   // per-cycle contraction of r^2
+                    if (prev_rr > 0 && rr < prev_rr && cycles > prev_c)
+                        rate = std::pow(rr / prev_rr, 1.0 / (cycles - prev_c));
+                    int need = 1;
+                    if (rate > 0 && rate < 0.5) {
+                        s->mg_rate2 = rate;
+                        // one check BEFORE the predicted converged cycle: a slower-than-predicted
+                        // contraction then costs a check, never a wasted V-cycle
+                        need = (int)std::ceil(std::log(tol2 / rr) / std::log(rate)) - 1;
+                        need = std::min(std::max(need, 1), 8);
+                    }
+                    prev_rr = rr;
+                    prev_c = cycles;
+                    next_chk = cycles + need;
+                } else {
+                    next_chk = cycles + 1;
+                }
             }
             if (done) break;
             if (cv.gather) CHK(gather_level(s, C));
@@ -1030,6 +1056,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_SPLIT")) s->helm_split = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_MG_PREDICT")) s->mg_predict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     {
@@ -1155,6 +1182,12 @@ int ns_step(ns_solver* s, ns_stats* out) {
         set_err("velocity field is not finite after the step (scheme diverged; see SURVEY.md section 5 on CFL)");
         return NS_EDIVERGE;
     }
+    return 0;
+}
+
+int ns_set_timing(ns_solver* s, int on) {
+    if (!s) { set_err("null solver"); return NS_EINVAL; }
+    s->timing = on ? 1 : 0;
     return 0;
 }
 

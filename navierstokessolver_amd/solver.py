@@ -129,6 +129,9 @@ class GpuSolver:
         c = np.ascontiguousarray(np.asarray(coarse, dtype=np.float64).reshape(self.shape[0] // 2, self.shape[1] // 2))
         L.check(L.lib().ns_mg_transfer(self._h, 1, _dptr(c)))
 
+    def set_timing(self, on: bool) -> None:
+        L.check(L.lib().ns_set_timing(self._h, 1 if on else 0))
+
     def fill_random(self, seed: int = 0x5EED) -> None:
         L.check(L.lib().ns_fill_random(self._h, seed))
 
