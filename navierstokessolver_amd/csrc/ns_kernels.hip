@@ -766,6 +766,7 @@ struct StreamArgs {
     int ncx, ncy, ci0;
     int nt;                           // non-temporal output stores
     int alt;                          // alternate strips walk upwards
+    int ntl;                          // non-temporal iterate loads
 };
 
 // diagonal of the operator at a cell from its row / column coefficient sums
@@ -791,6 +792,14 @@ __device__ __forceinline__ double relax(double q, double xm, double xp, double y
 // of filling with this pass's output (tools/membw2.hip, 4096^2 2-read + 1-write stream:
 // 5.3 TB/s with plain stores, 6.8-7.5 TB/s with nt stores).  NSGPU_NT_STORES=0: plain (A/B).
 typedef double nsd2 __attribute__((ext_vector_type(2)));
+// the iterate's loads may be non-temporal too (NSGPU_NT_LOADS=1, A/B): it is read once per pass
+__device__ __forceinline__ double2 ld_stream(const double* p, int nt) {
+    if (nt > 0) {
+        const nsd2 v = __builtin_nontemporal_load(reinterpret_cast<const nsd2*>(p));
+        return make_double2(v.x, v.y);
+    }
+    return *reinterpret_cast<const double2*>(p);
+}
 __device__ __forceinline__ void st_stream(double* p, double2 v, bool nt) {
     if (nt) __builtin_nontemporal_store(nsd2{v.x, v.y}, reinterpret_cast<nsd2*>(p));
     else *reinterpret_cast<double2*>(p) = v;
@@ -872,7 +881,7 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
         const int blo = max(RB ? ib - 1 : ib, rlo), phi_hi = min(r1, rhi);
         auto load = [&](int slot_r, double2& p, double2& bb) {
             const int lp = min(max(slot_r, rlo), phi_hi), lb = min(max(slot_r - 1, blo), rhi);
-            p = *reinterpret_cast<const double2*>(a.in + (ptrdiff_t)lp * ld + lc);
+            p = ld_stream(a.in + (ptrdiff_t)lp * ld + lc, a.ntl);
             bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
         };
 
@@ -1017,7 +1026,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     const bool jm_ok = Jc - 1 >= 0, jp_ok = Jc + 1 < a.ncy;
     auto load = [&](int slot_r, double2& p, double2& bb, double2& ee) {
         const int lp = min(max(slot_r, phi_lo), phi_hi), lb = min(max(slot_r - DIR, b_lo), b_hi);
-        p = *reinterpret_cast<const double2*>(a.in + (ptrdiff_t)lp * ld + lc);
+        p = ld_stream(a.in + (ptrdiff_t)lp * ld + lc, a.ntl);
         bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
         if (XP) {
             const int I = lp >> 1;                      // floor, also for ghost rows
@@ -1821,6 +1830,8 @@ static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, dou
     a.nt = e ? std::atoi(e) != 0 : 1;
     const char* e2 = getenv("NSGPU_ALT_DIR");   // NSGPU_ALT_DIR=0: every strip walks downwards (A/B)
     a.alt = e2 ? std::atoi(e2) != 0 : 1;
+    const char* e3 = getenv("NSGPU_NT_LOADS");
+    a.ntl = e3 ? std::atoi(e3) : -1;   // -1: per kernel (the prolongation pass only)
     return a;
 }
 
@@ -1878,6 +1889,9 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
                                hipStream_t st) {
     StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, nullptr, false);
     a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0;
+    // the iterate streamed non-temporally here: 113 -> 101 us at 4096^2 (b and the coarse
+    // correction keep the Infinity Cache); neutral-to-worse in the other passes
+    if (a.ntl < 0) a.ntl = 1;
     a.nsj = (g.ny + SW2X - 1) / SW2X;
     a.L = strip_rows(a.nxl, a.nsj, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 16);
     a.nsi = (g.nxl + a.L - 1) / a.L;
