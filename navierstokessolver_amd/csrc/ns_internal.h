@@ -29,6 +29,9 @@ struct Coef {
     const double *bx, *by;          // Helmholtz Dirichlet boundary-face diagonal term 2/h^2 (0 inside)
     const double *rhx, *rhy;        // 1/h
     const double *rsx, *rsy;        // 2/(h_{i-1} + h_i) at index i (n+1 entries; 0 at both ends)
+    // face interpolation weights of Div_V / GradP (FluidSolver.cpp:389-414, 429-452):
+    // r = h_i / (h_nb + h_i) toward the lower (fw, fs) and upper (fe, fn) neighbour, 0 at a wall
+    const double *fwx, *fex, *fsy, *fny;
 };
 
 struct Partials {

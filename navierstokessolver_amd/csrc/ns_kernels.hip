@@ -960,6 +960,152 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
     }
 }
 
+// ------------------------------------------------ K3 / K5 as streaming strips
+// The same strip walk as k_sweep (128 loaded columns, 124 written, 2 per lane, x-neighbours
+// from a 3-row register window, y-neighbours by cross-lane shuffle, rows prefetched SD ahead):
+// every value is loaded once instead of ~3 times through L1/L2, and the face weights
+// r = h / (h_nb + h) come from tables (the same values Div_V / GradP compute).
+//   K3 (k_div_s):     rhs_phi = div(u*) / dt, + per-strip (sum, sum^2)     (FluidSolver.cpp:365-418)
+//   K5 (k_correct_s): u = u* - dt dphi/dx, v = v* - dt dphi/dy, + per-strip min/max (:420-456, 512-534)
+struct CellStreamArgs {
+    Geo g;
+    Coef c;
+    double dt;
+    const double *a0, *a1, *a2;   // K3: u, v, -;  K5: phi, u*, v*
+    double *o0, *o1;              // K3: rhs_phi, -;  K5: u, v
+    double* part;
+    int nsj, nsi, L;
+};
+
+// one face value along a line: interior r-weighted interpolation, or the wall's (q + ghost)/2
+__device__ __forceinline__ double face_val(double q, double qn, bool has, double r, double ghost) {
+    return has ? qn * r + q * (1 - r) : 0.5 * (q + ghost);
+}
+
+template <int K>   // 3: divergence, 5: correction
+__global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
+    const Geo& g = A.g;
+    const Coef& c = A.c;
+    const int lane = threadIdx.x & 63;
+    const int nstr = A.nsj * A.nsi;
+    const int wid = __builtin_amdgcn_readfirstlane(xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (int)(threadIdx.x >> 6));
+    double acc[4] = {0.0, 0.0, INFINITY, INFINITY};   // K3: sum, sum^2; K5: (umin, -umax, vmin, -vmax)
+    if (K == 5) acc[0] = acc[1] = INFINITY;
+    if (wid < nstr) {
+        const int si = wid / A.nsj, sj = wid - si * A.nsj;
+        const int jb = sj * SW, ib = si * A.L, ie = min(ib + A.L, g.nxl);
+        const int ny = g.ny, ld = g.ld;
+        const int c0 = jb - 2 + 2 * lane, c1 = c0 + 1;
+        const int lc = min(max(c0, 0), ld - 2);
+        const bool v0 = c0 >= 0 && c0 < ny, v1 = c1 >= 0 && c1 < ny;
+        const bool wr = lane >= 1 && lane <= 62 && c0 < ny;
+        const bool o0 = wr && v0, o1 = wr && v1;
+        const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
+        const double hy0 = c.hy[k0], hy1 = c.hy[k1];
+        const double fs0 = c.fsy[k0], fn0 = c.fny[k0], fs1 = c.fsy[k1], fn1 = c.fny[k1];
+        const bool s0 = c0 > 0, n0 = c0 < ny - 1, s1 = c1 > 0, n1 = c1 < ny - 1;
+        const int rlo = -HALO, rhi = g.nxl + HALO - 1;
+        // window field (K3: u; K5: phi) at rows ib-1 .. ie, row fields (K3: v; K5: u*, v*) at
+        // row r-1 when row r arrives (prefetch overruns clamped onto fetched rows)
+        double2 W0 = {0, 0}, W1 = {0, 0}, W2 = {0, 0};
+        double2 Q[SD], X[SD], Y[SD];
+        auto load = [&](int r, double2& q, double2& x, double2& y) {
+            const int lw = min(max(r, max(ib - 1, rlo)), min(ie, rhi));
+            const int lr = min(max(r - 1, ib), ie - 1);
+            q = *reinterpret_cast<const double2*>(A.a0 + (ptrdiff_t)lw * ld + lc);
+            if (K == 3) {
+                x = *reinterpret_cast<const double2*>(A.a1 + (ptrdiff_t)lr * ld + lc);
+            } else {
+                x = *reinterpret_cast<const double2*>(A.a1 + (ptrdiff_t)lr * ld + lc);
+                y = *reinterpret_cast<const double2*>(A.a2 + (ptrdiff_t)lr * ld + lc);
+            }
+        };
+        auto step = [&](const double2 q, const double2 x, const double2 y, int r) {
+            W0 = W1; W1 = W2; W2 = q;
+            const int m = r - 1;
+            if (m < ib || m >= ie) return;
+            const int gi = g.i0 + m;
+            const bool hW = gi > 0, hE = gi < g.nx - 1;
+            const double hx = c.hx[gi], fw = c.fwx[gi], fe = c.fex[gi];
+            if (K == 3) {
+                // Div_V: u faces along x from the window, v faces along y from the lanes
+                const double2 vv = x;
+                const double vs0 = __shfl_up(vv.y, 1, 64), vn1 = __shfl_down(vv.x, 1, 64);
+                double val[2];
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    const double uc = e ? W1.y : W1.x, uw = e ? W0.y : W0.x, ue = e ? W2.y : W2.x;
+                    const double vc = e ? vv.y : vv.x, vs = e ? vv.x : vs0, vn = e ? vn1 : vv.y;
+                    const double V0 = face_val(uc, uw, hW, fw, ghost_v(g, uc, 0, 0));
+                    const double V1 = face_val(uc, ue, hE, fe, ghost_v(g, uc, 1, 0));
+                    const double V2 = face_val(vc, vs, e ? s1 : s0, e ? fs1 : fs0, ghost_v(g, vc, 2, 1));
+                    const double V3 = face_val(vc, vn, e ? n1 : n0, e ? fn1 : fn0, ghost_v(g, vc, 3, 1));
+                    val[e] = ((V1 - V0) / hx + (V3 - V2) / (e ? hy1 : hy0)) / A.dt;
+                }
+                if (wr) {   // (an odd ny's last pair: column ny is row padding, left untouched)
+                    if (v1) st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(val[0], val[1]), false);
+                    else A.o0[(ptrdiff_t)m * ld + c0] = val[0];
+                }
+                if (o0) { acc[0] += val[0]; acc[1] += val[0] * val[0]; }
+                if (o1) { acc[0] += val[1]; acc[1] += val[1] * val[1]; }
+            } else {
+                // GradP (phi ghost = phi at every face of this build: 0.5 (p + p)) and the correction
+                const double ps0 = __shfl_up(W1.y, 1, 64), pn1 = __shfl_down(W1.x, 1, 64);
+                double un[2], vn[2];
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    const double pc = e ? W1.y : W1.x, pw = e ? W0.y : W0.x, pe = e ? W2.y : W2.x;
+                    const double ps = e ? W1.x : ps0, pn = e ? pn1 : W1.y;
+                    const double V0 = face_val(pc, pw, hW, fw, pc);
+                    const double V1 = face_val(pc, pe, hE, fe, pc);
+                    const double V2 = face_val(pc, ps, e ? s1 : s0, e ? fs1 : fs0, pc);
+                    const double V3 = face_val(pc, pn, e ? n1 : n0, e ? fn1 : fn0, pc);
+                    const double gx = (V1 - V0) / hx, gy = (V3 - V2) / (e ? hy1 : hy0);
+                    un[e] = (e ? x.y : x.x) - A.dt * gx;
+                    vn[e] = (e ? y.y : y.x) - A.dt * gy;
+                }
+                if (wr && v1) {
+                    st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(un[0], un[1]), false);
+                    st_stream(A.o1 + (ptrdiff_t)m * ld + c0, make_double2(vn[0], vn[1]), false);
+                } else if (wr) {
+                    A.o0[(ptrdiff_t)m * ld + c0] = un[0];
+                    A.o1[(ptrdiff_t)m * ld + c0] = vn[0];
+                }
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    if (!(e ? o1 : o0)) continue;
+                    // NaN-propagating min so a blown-up step is visible in the stats
+                    acc[0] = fmin(acc[0], un[e] != un[e] ? -INFINITY : un[e]);
+                    acc[1] = fmin(acc[1], un[e] != un[e] ? -INFINITY : -un[e]);
+                    acc[2] = fmin(acc[2], vn[e] != vn[e] ? -INFINITY : vn[e]);
+                    acc[3] = fmin(acc[3], vn[e] != vn[e] ? -INFINITY : -vn[e]);
+                }
+            }
+        };
+        const int r0 = ib - 1, r1 = ie;
+#pragma unroll
+        for (int q = 0; q < SD; q++) load(r0 + q, Q[q], X[q], Y[q]);
+        for (int r = r0; r <= r1; r += SD) {
+#pragma unroll
+            for (int q = 0; q < SD; q++) {
+                if (r + q <= r1) step(Q[q], X[q], Y[q], r + q);
+                load(r + q + SD, Q[q], X[q], Y[q]);
+            }
+        }
+    }
+    constexpr int NV = K == 3 ? 2 : 4;
+#pragma unroll
+    for (int k = 0; k < NV; k++)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const double o = __shfl_xor(acc[k], off, 64);
+            acc[k] = K == 3 ? acc[k] + o : fmin(acc[k], o);
+        }
+    if (lane == 0 && wid < nstr)
+#pragma unroll
+        for (int k = 0; k < NV; k++) A.part[NV * wid + k] = acc[k];
+}
+
 // ------------------------------------------------ K2 / K4: two sweeps per HBM pass
 // Temporal blocking of k_sweep<RB>: the row pipeline carries four stages -- red of
 // sweep 1 at row r-1, black 1 at r-2, red 2 at r-3, black 2 at r-4 -- so one read of
@@ -1756,8 +1902,31 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
     return (int)(cg.x * cg.y);
 }
 
+static long resident_waves(const void* k);
+static int strip_rows(int nxl, long nsj, long cap, int lmin);
+
+template <int K>
+static int launch_cell_s(CellStreamArgs A, hipStream_t st) {
+    A.nsj = (A.g.ny + SW - 1) / SW;
+    A.L = strip_rows(A.g.nxl, A.nsj, resident_waves((const void*)k_cell_s<K>), 4);
+    A.nsi = (A.g.nxl + A.L - 1) / A.L;
+    const int nstr = A.nsj * A.nsi;
+    hipLaunchKernelGGL(k_cell_s<K>, dim3((nstr + 3) / 4), dim3(256), 0, st, A);
+    return nstr;
+}
+
+static bool cell_streaming() {
+    const char* e = getenv("NSGPU_CELL");   // NSGPU_CELL=grid: the thread-per-cell K3 / K5 (A/B)
+    return !(e && std::strcmp(e, "grid") == 0);
+}
+
 int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* rp, double* part,
                hipStream_t st) {
+    if (cell_streaming()) {
+        CellStreamArgs A{};
+        A.g = g; A.c = c; A.dt = dt; A.a0 = u; A.a1 = v; A.o0 = rp; A.part = part;
+        return launch_cell_s<3>(A, st);
+    }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
     hipLaunchKernelGGL(k_div, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part, rows);
@@ -1766,6 +1935,11 @@ int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const do
 
 int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, const double* vs, double* u, double* v,
                    const double* phi, double* part, hipStream_t st) {
+    if (cell_streaming()) {
+        CellStreamArgs A{};
+        A.g = g; A.c = c; A.dt = dt; A.a0 = phi; A.a1 = us; A.a2 = vs; A.o0 = u; A.o1 = v; A.part = part;
+        return launch_cell_s<5>(A, st);
+    }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
     hipLaunchKernelGGL(k_correct, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part, rows);

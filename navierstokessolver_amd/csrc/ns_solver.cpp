@@ -720,10 +720,20 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
 // coefficient tables of one level: [pw pe bx | ps pn by | hx hy]  (ConstructLHS, FluidSolver.cpp:113-131)
 std::vector<double> coef_tables(const std::vector<double>& hx, const std::vector<double>& hy) {
     const int nx = (int)hx.size(), ny = (int)hy.size();
-    std::vector<double> h(6 * (size_t)nx + 6 * (size_t)ny + 2, 0.0);
+    std::vector<double> h(8 * (size_t)nx + 8 * (size_t)ny + 2, 0.0);
     double *pw = h.data(), *pe = pw + nx, *bx = pe + nx, *ps = bx + nx, *pn = ps + ny, *by = pn + ny;
     double *hxo = by + ny, *hyo = hxo + nx;
     double *rhx = hyo + ny, *rhy = rhx + nx, *rsx = rhy + ny, *rsy = rsx + nx + 1;
+    double *fwx = rsy + ny + 1, *fex = fwx + nx, *fsy = fex + nx, *fny = fsy + ny;
+    // Div_V / GradP face weights r = h / (h_nb + h) (FluidSolver.cpp:389-414, 429-452)
+    for (int i = 0; i < nx; i++) {
+        fwx[i] = i > 0 ? hx[i] / (hx[i - 1] + hx[i]) : 0.0;
+        fex[i] = i < nx - 1 ? hx[i] / (hx[i + 1] + hx[i]) : 0.0;
+    }
+    for (int j = 0; j < ny; j++) {
+        fsy[j] = j > 0 ? hy[j] / (hy[j - 1] + hy[j]) : 0.0;
+        fny[j] = j < ny - 1 ? hy[j] / (hy[j + 1] + hy[j]) : 0.0;
+    }
     for (int i = 0; i < nx; i++) rhx[i] = 1.0 / hx[i];
     for (int j = 0; j < ny; j++) rhy[j] = 1.0 / hy[j];
     for (int i = 1; i < nx; i++) rsx[i] = 2.0 / (hx[i - 1] + hx[i]);
@@ -752,6 +762,7 @@ nsg::Coef coef_view(double* d, int nx, int ny) {
     c.hx = d + 3 * nx + 3 * ny; c.hy = d + 4 * nx + 3 * ny;
     c.rhx = d + 4 * nx + 4 * ny; c.rhy = d + 5 * nx + 4 * ny;
     c.rsx = d + 5 * nx + 5 * ny; c.rsy = d + 6 * nx + 5 * ny + 1;
+    c.fwx = d + 6 * nx + 6 * ny + 2; c.fex = c.fwx + nx; c.fsy = c.fex + nx; c.fny = c.fsy + ny;
     return c;
 }
 

@@ -409,3 +409,31 @@ def test_k1_lds_equals_global_kernel(gpu, monkeypatch, nx, ny, xr, yr, bc):
     for a, b in zip(outs[0][:4], outs[1][:4]):
         assert rel(a, b) <= 1e-14
     np.testing.assert_allclose(outs[0][4], outs[1][4], rtol=1e-13)
+
+
+@pytest.mark.parametrize("nx,ny,xr,yr,bc", [(300, 201, 1.002, 0.998, BC_FLOW), (130, 256, -1, -1, BC_CAVITY),
+                                            (37, 70, 1.05, -1, BC_CAVITY)])
+def test_streaming_k3_k5_equal_grid_kernels(gpu, monkeypatch, nx, ny, xr, yr, bc):
+    """K3 / K5 as streaming strips (k_cell_s) = the thread-per-cell kernels (NSGPU_CELL=grid):
+    same face weights and divisions, so equal to 1e-14 (FMA contraction may differ); same
+    reductions; odd ny (the last pair's padding column) included."""
+    rng = np.random.default_rng(37)
+    dt = 1e-3
+    N = nx * ny
+    u, v, phi = (rand(rng, N) for _ in range(3))
+    outs = []
+    for mode in ("stream", "grid"):
+        if mode == "grid":
+            monkeypatch.setenv("NSGPU_CELL", "grid")
+        _, gs = pair(gpu, nx, ny, dt, 100.0, bc, xr, yr)
+        gs.set(gpu.NS_ARR_U, u); gs.set(gpu.NS_ARR_V, v); gs.set(gpu.NS_ARR_PHI, phi)
+        sums = gs.kernel(gpu.NS_K_DIV)[:2]
+        rp = gs.get(gpu.NS_ARR_RPHI)
+        mm = gs.kernel(gpu.NS_K_CORRECT)[:4]
+        outs.append((rp, sums, mm, gs.get(gpu.NS_ARR_U), gs.get(gpu.NS_ARR_V)))
+        gs.close()
+    a, b = outs
+    assert rel(a[0], b[0]) <= 1e-14
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-12, atol=1e-12 * np.abs(b[1]).max())
+    np.testing.assert_array_equal(a[2], b[2]) if rel(a[3], b[3]) == 0 else np.testing.assert_allclose(a[2], b[2], rtol=1e-14)
+    assert rel(a[3], b[3]) <= 1e-14 and rel(a[4], b[4]) <= 1e-14
