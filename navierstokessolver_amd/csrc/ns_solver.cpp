@@ -791,7 +791,9 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
     long agg_cells = 1024L * 1024L;
     if (const char* e = getenv("NSGPU_AGG_CELLS")) agg_cells = std::atol(e);
     const int agg_min_rows = 8;
-    const size_t lds_cap = 150 * 1024;  // stop at the first whole level whose LDS V-cycle fits (<= ~64^2)
+    // stop at the first whole level whose LDS V-cycle fits (<= ~64^2); NSGPU_LDS_CAP (bytes) for A/B
+    size_t lds_cap = 150 * 1024;
+    if (const char* e = getenv("NSGPU_LDS_CAP")) lds_cap = std::min<size_t>(std::atol(e), 150 * 1024);
     for (;;) {
         const MgLevel& F = s->lv.back();
         const nsg::Geo& gf = F.g;
