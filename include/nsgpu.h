@@ -46,7 +46,9 @@ typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm
 #define NS_BC_INLET_PARABOLIC 1  /* rejected: empty ghost constant in the reference (FluidSolver.cpp:86-87,171) */
 #define NS_BC_WALL            2
 #define NS_BC_PRESSURE        3  /* rejected: no ghost stencil in the reference (FluidSolver.cpp:150,168) */
-#define NS_BC_NEUMANN         4
+#define NS_BC_NEUMANN         4  /* outflow: velocity ghost q, phi ghost 2.5 phi_0 - 2 phi_1 + 0.5 phi_2
+                                    (FluidSolver.cpp:98-101); needs NS_POISSON_MG, whose hierarchy then
+                                    preconditions a BiCGStab solve of the true Poisson matrix */
 
 /* Poisson solvers */
 #define NS_POISSON_RBSOR  0  /* fused red-black SOR, one HBM pass per sweep (default) */

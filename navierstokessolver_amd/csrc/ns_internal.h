@@ -9,9 +9,26 @@ namespace nsg {
 constexpr int HALO = 5;  // ghost rows per side: K1's MUSCL stencil (2), the 2-sweep pass's cone (4),
                          // the 2-sweep pass with fused restriction (5)
 
+// Non-rectangular domains (polygons with holes / steps, Grid.cpp:131-185): one int32 code per
+// cell of the bounding box, in a plane laid out like the fields (halo rows included):
+//   FC_IN set = the cell is in the domain; bits 5k..5k+4 = the boundary edge on face k
+//   (0 W, 1 E, 2 S, 3 N; Cell::edges, Grid.h:33) or FC_INT if the neighbour is in the domain.
+constexpr int FC_IN = 1 << 20;
+constexpr int FC_INT = 31;
+constexpr int MAX_EDGES = 31;
+__host__ __device__ inline int fc_edge(int code, int k) { return (code >> (5 * k)) & 31; }
+// one polygon edge on the device: ghost stencils of ConstructGhostStencils (FluidSolver.cpp:84-103)
+struct EdgeDev {
+    int neu;            // NEUMANN outflow (velocity ghost q, phi ghost 2.5/-2/0.5)
+    int enx, eny;       // outward normal
+    double c0, c1;      // velocity ghost constants (u, v) of walls / inlets
+};
+
 // Geometry of one x-slab.  Fields are (nxl + 2*HALO) rows of ld doubles, j contiguous;
 // pointers handed to kernels point at local row 0.  Global row = i0 + local row.
 struct Geo {
+    const int32_t* fc = nullptr;   // masked domains: topology codes at local row 0 (null: rectangle)
+    const EdgeDev* et = nullptr;   // masked domains: edge table
     int nx, ny;       // global cells
     int i0, nxl;      // slab start (global) and local rows
     int ld;           // row stride in doubles (ny rounded up to 128: one streaming strip = 1 KiB per wave)
@@ -130,6 +147,28 @@ int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const d
 size_t coarse_vcycle_bytes(const Geo& g);
 int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double* b, int cycles, int pre, int post,
                          int citers, double comega, double somega, hipStream_t st);
+
+// NEUMANN outflow Poisson (BiCGStab on the true operator, right-preconditioned by one
+// wall-closure V-cycle; ns_solver.cpp pois_solve_krylov).  Device scalar slots:
+enum { KS_RHO = 0, KS_ALPHA, KS_OMEGA, KS_BETA, KS_MEAN, KS_SUMR0, KS_BRK, KS_D = 8, KS_NUM = 16 };
+// scalar stages (k_bicg_scal) and vector modes (k_bicg_vec)
+enum { KSC_INIT = 0, KSC_RHO, KSC_ALPHA, KSC_MEAN, KSC_OMEGA };
+enum { KV_INIT = 0, KV_P, KV_V, KV_T, KV_X };
+struct KrylovArgs {
+    Geo g;
+    double *x, *r, *r0, *p, *v, *s, *t, *ph, *sh;
+    const double *b, *shift, *sc;
+    double* part;
+    int rows;
+};
+// y = A x with A the reference's Poisson matrix incl. NEUMANN outflow rows; partials
+// (sum y, sum q*y) per block (q may be null); returns the partial count
+int launch_pois_apply(const Geo& g, const Coef& c, const double* x, double* y, const double* q, double* part,
+                      hipStream_t st);
+// one fused BiCGStab vector update (KV_*); 3 partials per block for KV_INIT / KV_T / KV_X
+int launch_bicg_vec(int mode, KrylovArgs a, hipStream_t st);
+// the scalar recurrences (KSC_*) from reduced sums d
+void launch_bicg_scal(int stage, const double* d, double n, double* sc, hipStream_t st);
 
 // max partials any launcher writes for this geometry
 int max_partials(const Geo& g);

@@ -103,7 +103,15 @@ __device__ __forceinline__ void block_reduce_min(double (&x)[NV], double* out) {
 }
 
 // ------------------------------------------------ grad phi (GradP, FluidSolver.cpp:420-456)
-// Dirichlet-type faces only (phi ghost = phi, FluidSolver.cpp:87-88): boundary face value = phi_c.
+// phi ghost (EvaluateGhostStencil_P, :175-181; stencils :87-88, :98-101): walls / inlets
+// phi_c (face value 0.5 (p + p)); a NEUMANN outflow side 2.5 phi_c - 2 phi_1 + 0.5 phi_2
+// with phi_1, phi_2 the next two cells inward (the side's slab rows / columns; nx, ny >= 3)
+__device__ __forceinline__ double ghost_p(const Geo& g, const double* phi, int li, int j, int side, double pc) {
+    if (!g.neu[side]) return pc;
+    const int di = side == 0 ? 1 : (side == 1 ? -1 : 0), dj = side == 2 ? 1 : (side == 3 ? -1 : 0);
+    return 2.5 * pc - 2.0 * ldf(phi, g.ld, li + di, j + dj) + 0.5 * ldf(phi, g.ld, li + 2 * di, j + 2 * dj);
+}
+
 __device__ __forceinline__ void grad_phi(const Geo& g, const Coef& c, const double* phi, int li, int j,
                                          double& gx, double& gy) {
     const int gi = g.i0 + li, ld = g.ld;
@@ -111,13 +119,13 @@ __device__ __forceinline__ void grad_phi(const Geo& g, const Coef& c, const doub
     const double hx = c.hx[gi], hy = c.hy[j];
     double V0, V1, V2, V3, r;
     if (gi > 0) { r = hx / (c.hx[gi - 1] + hx); V0 = ldf(phi, ld, li - 1, j) * r + pc * (1 - r); }
-    else V0 = 0.5 * (pc + pc);
+    else V0 = 0.5 * (pc + ghost_p(g, phi, li, j, 0, pc));
     if (gi < g.nx - 1) { r = hx / (c.hx[gi + 1] + hx); V1 = ldf(phi, ld, li + 1, j) * r + pc * (1 - r); }
-    else V1 = 0.5 * (pc + pc);
+    else V1 = 0.5 * (pc + ghost_p(g, phi, li, j, 1, pc));
     if (j > 0) { r = hy / (c.hy[j - 1] + hy); V2 = ldf(phi, ld, li, j - 1) * r + pc * (1 - r); }
-    else V2 = 0.5 * (pc + pc);
+    else V2 = 0.5 * (pc + ghost_p(g, phi, li, j, 2, pc));
     if (j < g.ny - 1) { r = hy / (c.hy[j + 1] + hy); V3 = ldf(phi, ld, li, j + 1) * r + pc * (1 - r); }
-    else V3 = 0.5 * (pc + pc);
+    else V3 = 0.5 * (pc + ghost_p(g, phi, li, j, 3, pc));
     gx = (V1 - V0) / hx;
     gy = (V3 - V2) / hy;
 }
@@ -1049,7 +1057,8 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                 if (o0) { acc[0] += val[0]; acc[1] += val[0] * val[0]; }
                 if (o1) { acc[0] += val[1]; acc[1] += val[1] * val[1]; }
             } else {
-                // GradP (phi ghost = phi at every face of this build: 0.5 (p + p)) and the correction
+                // GradP (phi ghost = phi at wall / inlet faces: 0.5 (p + p); a NEUMANN side's
+                // extrapolated ghost goes through k_correct) and the correction
                 const double ps0 = __shfl_up(W1.y, 1, 64), pn1 = __shfl_down(W1.x, 1, 64);
                 double un[2], vn[2];
 #pragma unroll
@@ -1860,6 +1869,116 @@ __global__ __launch_bounds__(256) void k_axpby(Geo g, double a, const double* __
     out[o] = a * x[o] + b * y[o];
 }
 
+// ------------------------------------------------ NEUMANN outflow: BiCGStab pieces
+// With an outflow side the Poisson matrix is no longer the wall-closure L the smoothers
+// relax: AddGhostStencils (FluidSolver.cpp:147-163) adds, per outflow face, w (ghost_p - x_c)
+// with w = 1/h^2 (:124-127) and the ghost 2.5 x_c - 2 x_1 + 0.5 x_2 (:98-101) -- a row that
+// reaches two cells inward and is not diagonally dominant.  The solver then runs BiCGStab on
+// the true operator (the reference's KSPBCGSL, :73-82), right-preconditioned by one V-cycle
+// of the wall-closure multigrid (ns_solver.cpp pois_solve_krylov).
+//
+// y = A x over own cells; block partials (sum y, sum q*y) (q may be null)
+__global__ __launch_bounds__(256) void k_pois_apply(Geo g, Coef c, const double* __restrict__ x,
+                                                    double* __restrict__ y, const double* __restrict__ q,
+                                                    double* __restrict__ part, int rows) {
+    const int j = blockIdx.x * 64 + threadIdx.x;
+    const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
+    double acc[2] = {0.0, 0.0};
+    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
+        const int gi = g.i0 + li, ld = g.ld;
+        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+        const double xc = x[o], hx = c.hx[gi], hy = c.hy[j];
+        double s = 0.0;
+        if (gi > 0) s += c.pw[gi] * (x[o - ld] - xc);
+        else if (g.neu[0]) s += (ghost_p(g, x, li, j, 0, xc) - xc) / (hx * hx);
+        if (gi < g.nx - 1) s += c.pe[gi] * (x[o + ld] - xc);
+        else if (g.neu[1]) s += (ghost_p(g, x, li, j, 1, xc) - xc) / (hx * hx);
+        if (j > 0) s += c.ps[j] * (x[o - 1] - xc);
+        else if (g.neu[2]) s += (ghost_p(g, x, li, j, 2, xc) - xc) / (hy * hy);
+        if (j < g.ny - 1) s += c.pn[j] * (x[o + 1] - xc);
+        else if (g.neu[3]) s += (ghost_p(g, x, li, j, 3, xc) - xc) / (hy * hy);
+        y[o] = s;
+        acc[0] += s;
+        if (q) acc[1] += q[o] * s;
+    }
+    block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
+}
+
+// BiCGStab vector updates; coefficients from the device scalars k_bicg_scal leaves in sc,
+// each fused with the dot products the next scalar stage needs (block partials, 3 per block):
+//   KV_INIT: r = (b - shift) - (y - mean_y), r0 = r, p = v = 0     partials (r.r, r0.r, sum r)
+//   KV_P:    p = r + beta (p - omega v)
+//   KV_V:    v = y - mean_y (in place), s = r - alpha v
+//   KV_T:    t = y - mean_y (in place)                             partials (t.s, t.t, -)
+//   KV_X:    x += alpha ph + omega sh, r = s - omega t             partials (r.r, r0.r, sum r)
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_bicg_vec(KrylovArgs a) {
+    const Geo& g = a.g;
+    const int j = blockIdx.x * 64 + threadIdx.x;
+    const int lend = min((int)(blockIdx.y + 1) * 4 * a.rows, g.nxl);
+    double acc[3] = {0.0, 0.0, 0.0};
+    const double alpha = a.sc[KS_ALPHA], beta = a.sc[KS_BETA], omega = a.sc[KS_OMEGA], my = a.sc[KS_MEAN];
+    const double shift = a.shift ? a.shift[0] : 0.0;
+    for (int li = blockIdx.y * 4 * a.rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
+        const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
+        if (MODE == KV_INIT) {
+            const double r = (a.b[o] - shift) - (a.v[o] - my);
+            a.r[o] = r; a.r0[o] = r; a.p[o] = 0.0; a.v[o] = 0.0;
+            acc[0] += r * r; acc[1] += r * r; acc[2] += r;
+        } else if (MODE == KV_P) {
+            a.p[o] = a.r[o] + beta * (a.p[o] - omega * a.v[o]);
+        } else if (MODE == KV_V) {
+            const double v = a.v[o] - my;
+            a.v[o] = v;
+            a.s[o] = a.r[o] - alpha * v;
+        } else if (MODE == KV_T) {
+            const double t = a.t[o] - my;
+            a.t[o] = t;
+            acc[0] += t * a.s[o]; acc[1] += t * t;
+        } else {
+            a.x[o] += alpha * a.ph[o] + omega * a.sh[o];
+            const double r = a.s[o] - omega * a.t[o];
+            a.r[o] = r;
+            acc[0] += r * r; acc[1] += a.r0[o] * r; acc[2] += r;
+        }
+    }
+    if (MODE == KV_INIT || MODE == KV_T || MODE == KV_X)
+        block_reduce_sum<3>(acc, a.part + 3 * (blockIdx.x + gridDim.x * blockIdx.y));
+}
+
+// the scalar recurrences of BiCGStab on one thread; d = the stage's reduced sums
+//   KSC_RHO  (d = r.r, r0.r, sum r):   beta = (rho1/rho)(alpha/omega), rho = rho1
+//   KSC_ALPHA (d = sum y, r0.y):       mean_y, alpha = rho / (r0.y - mean_y sum r0)
+//   KSC_MEAN  (d = sum y):             mean_y
+//   KSC_OMEGA (d = t.s, t.t):          omega = t.s / t.t
+__global__ void k_bicg_scal(int stage, const double* __restrict__ d, double n, double* __restrict__ sc) {
+    // a breakdown (a zero or non-finite denominator) zeroes the coefficient -- the vector
+    // updates then leave x untouched -- and raises KS_BRK; the host restarts from x
+    auto guard = [&](double v) {
+        if (!isfinite(v)) { sc[KS_BRK] = 1.0; return 0.0; }
+        return v;
+    };
+    if (stage == KSC_INIT) {
+        sc[KS_RHO] = 1.0; sc[KS_ALPHA] = 1.0; sc[KS_OMEGA] = 1.0; sc[KS_SUMR0] = d[2]; sc[KS_BRK] = 0.0;
+    } else if (stage == KSC_RHO) {
+        const double rho1 = d[1];
+        sc[KS_BETA] = guard((rho1 / sc[KS_RHO]) * (sc[KS_ALPHA] / sc[KS_OMEGA]));
+        if (rho1 == 0.0) sc[KS_BRK] = 1.0;
+        sc[KS_RHO] = rho1;
+    } else if (stage == KSC_ALPHA) {
+        const double m = d[0] / n;
+        sc[KS_MEAN] = m;
+        sc[KS_ALPHA] = guard(sc[KS_RHO] / (d[1] - m * sc[KS_SUMR0]));
+    } else if (stage == KSC_MEAN) {
+        sc[KS_MEAN] = d[0] / n;
+    } else {
+        const double om = d[1] > 0.0 ? d[0] / d[1] : 0.0;
+        sc[KS_OMEGA] = guard(om);
+        if (om == 0.0) sc[KS_BRK] = 1.0;
+    }
+}
+
 // ---------------------------------------------------------------- launchers
 static inline dim3 cell_grid(const Geo& g) { return dim3((g.ny + 63) / 64, (g.nxl + 3) / 4); }
 
@@ -1933,9 +2052,35 @@ int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const do
     return (int)(cg.x * cg.y);
 }
 
+int launch_pois_apply(const Geo& g, const Coef& c, const double* x, double* y, const double* q, double* part,
+                      hipStream_t st) {
+    const int rows = cell_rows(g);
+    const dim3 cg = cell_grid(g, rows);
+    hipLaunchKernelGGL(k_pois_apply, cg, dim3(64, 4), 0, st, g, c, x, y, q, part, rows);
+    return (int)(cg.x * cg.y);
+}
+
+int launch_bicg_vec(int mode, KrylovArgs a, hipStream_t st) {
+    a.rows = cell_rows(a.g);
+    const dim3 cg = cell_grid(a.g, a.rows);
+    switch (mode) {
+        case KV_INIT: hipLaunchKernelGGL(k_bicg_vec<KV_INIT>, cg, dim3(64, 4), 0, st, a); break;
+        case KV_P: hipLaunchKernelGGL(k_bicg_vec<KV_P>, cg, dim3(64, 4), 0, st, a); break;
+        case KV_V: hipLaunchKernelGGL(k_bicg_vec<KV_V>, cg, dim3(64, 4), 0, st, a); break;
+        case KV_T: hipLaunchKernelGGL(k_bicg_vec<KV_T>, cg, dim3(64, 4), 0, st, a); break;
+        default: hipLaunchKernelGGL(k_bicg_vec<KV_X>, cg, dim3(64, 4), 0, st, a); break;
+    }
+    return (int)(cg.x * cg.y);
+}
+
+void launch_bicg_scal(int stage, const double* d, double n, double* sc, hipStream_t st) {
+    hipLaunchKernelGGL(k_bicg_scal, dim3(1), dim3(1), 0, st, stage, d, n, sc);
+}
+
 int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, const double* vs, double* u, double* v,
                    const double* phi, double* part, hipStream_t st) {
-    if (cell_streaming()) {
+    // (a NEUMANN side's phi ghost reaches two cells inward: the grid kernel's grad_phi)
+    if (cell_streaming() && !(g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3])) {
         CellStreamArgs A{};
         A.g = g; A.c = c; A.dt = dt; A.a0 = phi; A.a1 = us; A.a2 = vs; A.o0 = u; A.o1 = v; A.part = part;
         return launch_cell_s<5>(A, st);

@@ -129,6 +129,12 @@ struct ns_solver {
     int mg_pre = 2, mg_post = 2, mg_coarse_iters = 0;
     double mg_omega_c = 1.0, mg_omega_s = 1.1;
     bool mg_coarse_lds = false;
+    // NEUMANN outflow (pois_solve_krylov): BiCGStab planes r, r0, p, v, s, t, ph, sh, scratch
+    // (null without an outflow side) and the recurrence scalars
+    double* kv[9] = {};
+    double* kv_mem = nullptr;
+    double* ksc = nullptr;
+    bool pc_active = false;      // inside mg_precond: level 0 has no mean shift, no timing
     ns_host_transport ht{};      // host transport (ht.exchange != NULL) instead of RCCL
     double* stage = nullptr;     // pinned staging for the host transport
     size_t stage_n = 0;
@@ -459,6 +465,9 @@ int pois_solve(ns_solver* s, int* its, double* res, ns_stats* stt) {
 }
 
 // ---------------- multigrid Poisson solve (V-cycles; smoother = the streaming RB sweep)
+// the finest level's rhs shift (the null-space mean); none while preconditioning
+const double* shift0(const ns_solver* s) { return s->pc_active ? nullptr : s->scal + S_SHIFT; }
+
 MgLevel& level(ns_solver* s, int l) {
     MgLevel& L = s->lv[l];
     if (l == 0) { L.phi = s->arr[NS_ARR_PHI]; L.tmp = s->arr[NS_ARR_TMP]; L.b = s->arr[NS_ARR_RPHI]; }
@@ -561,9 +570,9 @@ int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
     for (int k = 0; k < n;) {
         const int w = (n - k >= 2 && pair_level(s, l)) ? 2 : 1;   // two sweeps per HBM pass
         CHK(halo_l(s, l, {L.phi}, 2 * w));
-        const bool t = s->timing && l == 0;
+        const bool t = s->timing && l == 0 && !s->pc_active;
         if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st)); s->evtag[ev0 + *tn] = 0; }
-        const double* sh = l == 0 ? s->scal + S_SHIFT : nullptr;
+        const double* sh = l == 0 ? shift0(s) : nullptr;
         if (w == 2) nsg::launch_pois_rbsor2(L.g, L.c, s->mg_omega_s, L.phi, L.tmp, L.b, sh, nullptr, s->st);
         else nsg::launch_pois_rbsor(L.g, L.c, s->mg_omega_s, L.phi, L.tmp, L.b, sh, nullptr, s->st);
         if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn) + 1], s->st)); (*tn)++; }
@@ -593,9 +602,75 @@ int mg_coarse(ns_solver* s) {
     return 0;
 }
 
+// one V-cycle (pre-smoothing + restriction down to the coarsest level, the coarse solve,
+// prolongation + post-smoothing back up).  `check(nb)` runs after the finest level's
+// restriction pass (r^2 partials of the finest residual in s->part, nb of them) and returns
+// 1 to end the solve there, 0 to go on, < 0 on error; the preconditioner passes none.
+template <class Check>
+int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
+    const int nl = (int)s->lv.size();
+    *done = false;
+    for (int l = 0; l < nl - 1; l++) {
+        MgLevel& F = level(s, l);
+        MgLevel& C = level(s, l + 1);
+        const CoarseView cv = coarse_view(s, l);
+        const double* sh = l == 0 ? shift0(s) : nullptr;
+        int nb;
+        if (fused_restrict(s, l)) {
+            // last two pre-smoothing sweeps + residual + restriction in one HBM pass
+            CHK(mg_smooth(s, l, s->mg_pre - 2, tn, ev0));
+            CHK(halo_l(s, l, {F.phi}, 5));
+            const bool t = s->timing && l == 0 && !s->pc_active;
+            if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st)); s->evtag[ev0 + *tn] = 1; }
+            nb = (tile_level(s, l) ? nsg::launch_pois_tile2_restrict : nsg::launch_pois_rbsor2_restrict)(
+                F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b, cv.phi, s->part, s->st);
+            if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn) + 1], s->st)); (*tn)++; }
+            std::swap(F.phi, F.tmp);
+            if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
+        } else {
+            CHK(mg_smooth(s, l, s->mg_pre, tn, ev0));
+            CHK(halo_l(s, l, {F.phi}, 1));
+            nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, sh, cv.g, C.c, cv.b, cv.phi, s->part, s->st);
+        }
+        if (l == 0) {
+            const int rc = check(nb);
+            if (rc < 0) return rc;
+            if (rc > 0) { *done = true; return 0; }
+        }
+        if (cv.gather) CHK(gather_level(s, C));
+        else CHK(halo_l(s, l + 1, {C.b}, 4));
+    }
+    CHK(mg_coarse(s));
+    for (int l = nl - 2; l >= 0; l--) {
+        MgLevel& F = level(s, l);
+        MgLevel& C = level(s, l + 1);
+        const CoarseView cv = coarse_view(s, l);
+        if (fused_prolong(s, l)) {
+            // prolongation + the first two post-smoothing sweeps in one HBM pass; the coarse
+            // and fine ghost rows travel in one group
+            if (!F.repl) {
+                if (cv.gather || C.repl) CHK(halo_l(s, l, {F.phi}, 5));
+                else CHK(halo_reqs(s, {HaloReq{&C.g, C.phi, 3}, HaloReq{&F.g, F.phi, 5}}));
+            }
+            const bool t = s->timing && l == 0 && !s->pc_active;
+            if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st)); s->evtag[ev0 + *tn] = 0; }
+            (tile_level(s, l) ? nsg::launch_pois_tile2_prolong : nsg::launch_pois_rbsor2_prolong)(
+                F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, l == 0 ? shift0(s) : nullptr, cv.g, cv.phi, s->st);
+            if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn) + 1], s->st)); (*tn)++; }
+            std::swap(F.phi, F.tmp);
+            if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
+            CHK(mg_smooth(s, l, s->mg_post - 2, tn, ev0));
+        } else {
+            if (!cv.gather) CHK(halo_l(s, l + 1, {C.phi}, 1));
+            nsg::launch_prolong(F.g, F.phi, cv.g, cv.phi, s->st);
+            CHK(mg_smooth(s, l, s->mg_post, tn, ev0));
+        }
+    }
+    return 0;
+}
+
 int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     const double tol2 = s->rtol * s->rtol;
-    const int nl = (int)s->lv.size();
     const int maxc = std::min(s->max_iters, 1000);
     int cycles = 0, tn = 0, nchk = 0;
     double tms = 0.0;
@@ -605,108 +680,57 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     // cycles in between run without a host round trip
     int next_chk = 0, prev_c = -1;
     double prev_rr = -1.0;
+    auto check = [&](int nb) -> int {
+        if (!(cycles >= next_chk || cycles >= maxc)) return 0;
+        // fine residual after pre-smoothing: the convergence test (a host sync)
+        nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
+        CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
+        CHK(fetch(s));
+        nchk++;
+        if (s->timing) {
+            for (int k = 0; k < tn; k++) {
+                float ms = 0.f;
+                HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
+                if (s->evtag[k]) {
+                    if (stt) { stt->t_restrict_kernel_ms += ms; stt->n_restrict_kernels++; }
+                } else {
+                    tms += ms;
+                    if (stt) stt->n_poisson_kernels++;
+                }
+            }
+            tn = 0;
+        }
+        const double r2 = s->hs[S_RES], b2 = s->hs[S_SHIFT + 1];
+        *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
+        if (s->verbose) fprintf(stderr, "nsgpu poisson: cycle %d rel. residual after pre-smoothing %.3e\n", cycles, *res);
+        if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = cycles; return NS_EDIVERGE; }
+        if (r2 <= tol2 * b2 || r2 == 0.0 || cycles >= maxc) return 1;
+        if (s->mg_predict) {
+            const double rr = r2 / b2;
+            double rate = s->mg_rate2;   // per-cycle contraction of r^2
+            if (prev_rr > 0 && rr < prev_rr && cycles > prev_c)
+                rate = std::pow(rr / prev_rr, 1.0 / (cycles - prev_c));
+            int need = 1;
+            if (rate > 0 && rate < 0.5) {
+                s->mg_rate2 = rate;
+                // one check BEFORE the predicted converged cycle: a slower-than-predicted
+                // contraction then costs a check, never a wasted V-cycle
+                need = (int)std::ceil(std::log(tol2 / rr) / std::log(rate)) - 1;
+                need = std::min(std::max(need, 1), 8);
+            }
+            prev_rr = rr;
+            prev_c = cycles;
+            next_chk = cycles + need;
+        } else {
+            next_chk = cycles + 1;
+        }
+        return 0;
+    };
     for (;;) {
         if (s->timing) CHK(ensure_events(s, 2 * (size_t)(tn + per_cycle + 2)));
-        const int ev0 = 0;
         bool done = false;
-        for (int l = 0; l < nl - 1 && !done; l++) {
-            MgLevel& F = level(s, l);
-            MgLevel& C = level(s, l + 1);
-            const CoarseView cv = coarse_view(s, l);
-            const double* sh = l == 0 ? s->scal + S_SHIFT : nullptr;
-            int nb;
-            if (fused_restrict(s, l)) {
-                // last two pre-smoothing sweeps + residual + restriction in one HBM pass
-                CHK(mg_smooth(s, l, s->mg_pre - 2, &tn, ev0));
-                CHK(halo_l(s, l, {F.phi}, 5));
-                const bool t = s->timing && l == 0;
-                if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn)], s->st)); s->evtag[ev0 + tn] = 1; }
-                nb = (tile_level(s, l) ? nsg::launch_pois_tile2_restrict : nsg::launch_pois_rbsor2_restrict)(
-                    F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b, cv.phi, s->part, s->st);
-                if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn) + 1], s->st)); tn++; }
-                std::swap(F.phi, F.tmp);
-                if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
-            } else {
-                CHK(mg_smooth(s, l, s->mg_pre, &tn, ev0));
-                CHK(halo_l(s, l, {F.phi}, 1));
-                nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, sh, cv.g, C.c, cv.b, cv.phi, s->part, s->st);
-            }
-            if (l == 0 && (cycles >= next_chk || cycles >= maxc)) {
-                // fine residual after pre-smoothing: the convergence test (a host sync)
-                nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
-                CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
-                CHK(fetch(s));
-                nchk++;
-                if (s->timing) {
-                    for (int k = 0; k < tn; k++) {
-                        float ms = 0.f;
-                        HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
-                        if (s->evtag[k]) {
-                            if (stt) { stt->t_restrict_kernel_ms += ms; stt->n_restrict_kernels++; }
-                        } else {
-                            tms += ms;
-                            if (stt) stt->n_poisson_kernels++;
-                        }
-                    }
-                    tn = 0;
-                }
-                const double r2 = s->hs[S_RES], b2 = s->hs[S_SHIFT + 1];
-                *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
-                if (s->verbose) fprintf(stderr, "nsgpu poisson: cycle %d rel. residual after pre-smoothing %.3e\n", cycles, *res);
-                if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = cycles; return NS_EDIVERGE; }
-                if (r2 <= tol2 * b2 || r2 == 0.0 || cycles >= maxc) done = true;
-                else if (s->mg_predict) {
-                    const double rr = r2 / b2;
-                    double rate = s->mg_rate2;   // per-cycle contraction of r^2
-                    if (prev_rr > 0 && rr < prev_rr && cycles > prev_c)
-                        rate = std::pow(rr / prev_rr, 1.0 / (cycles - prev_c));
-                    int need = 1;
-                    if (rate > 0 && rate < 0.5) {
-                        s->mg_rate2 = rate;
-                        // one check BEFORE the predicted converged cycle: a slower-than-predicted
-                        // contraction then costs a check, never a wasted V-cycle
-                        need = (int)std::ceil(std::log(tol2 / rr) / std::log(rate)) - 1;
-                        need = std::min(std::max(need, 1), 8);
-                    }
-                    prev_rr = rr;
-                    prev_c = cycles;
-                    next_chk = cycles + need;
-                } else {
-                    next_chk = cycles + 1;
-                }
-            }
-            if (done) break;
-            if (cv.gather) CHK(gather_level(s, C));
-            else CHK(halo_l(s, l + 1, {C.b}, 4));
-        }
+        CHK(mg_vcycle(s, &tn, 0, check, &done));
         if (done) break;
-        CHK(mg_coarse(s));
-        for (int l = nl - 2; l >= 0; l--) {
-            MgLevel& F = level(s, l);
-            MgLevel& C = level(s, l + 1);
-            const CoarseView cv = coarse_view(s, l);
-            if (fused_prolong(s, l)) {
-                // prolongation + the first two post-smoothing sweeps in one HBM pass; the coarse
-                // and fine ghost rows travel in one group
-                if (!F.repl) {
-                    if (cv.gather || C.repl) CHK(halo_l(s, l, {F.phi}, 5));
-                    else CHK(halo_reqs(s, {HaloReq{&C.g, C.phi, 3}, HaloReq{&F.g, F.phi, 5}}));
-                }
-                const bool t = s->timing && l == 0;
-                if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn)], s->st)); s->evtag[ev0 + tn] = 0; }
-                (tile_level(s, l) ? nsg::launch_pois_tile2_prolong : nsg::launch_pois_rbsor2_prolong)(
-                    F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, l == 0 ? s->scal + S_SHIFT : nullptr, cv.g, cv.phi,
-                    s->st);
-                if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + tn) + 1], s->st)); tn++; }
-                std::swap(F.phi, F.tmp);
-                if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
-                CHK(mg_smooth(s, l, s->mg_post - 2, &tn, ev0));
-            } else {
-                if (!cv.gather) CHK(halo_l(s, l + 1, {C.phi}, 1));
-                nsg::launch_prolong(F.g, F.phi, cv.g, cv.phi, s->st);
-                CHK(mg_smooth(s, l, s->mg_post, &tn, ev0));
-            }
-        }
         cycles++;
     }
     *its = cycles;
@@ -717,8 +741,127 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     return 0;
 }
 
+// ---------------- NEUMANN outflow: BiCGStab on the reference's Poisson matrix
+// With an outflow side the matrix (ConstructLHS + AddGhostStencils, FluidSolver.cpp:105-163)
+// has rows the red-black smoothers cannot relax (2.5/-2/0.5 ghost, :98-101: not diagonally
+// dominant, and coupling a cell to a same-colour cell two rows inward).  The solve is then
+// the reference's own method class -- BiCGStab (KSPBCGSL, :73-82) -- on the true matrix,
+// right-preconditioned by ONE V-cycle of the wall-closure multigrid (the smoothers' operator:
+// outflow faces treated like walls).  The singular system (constant null space, :142-144) is
+// solved as P A x = P (b - mean b) with P the mean projection: every residual is kept
+// mean-free, as MatNullSpaceRemove does to the reference's Krylov vectors.  All recurrence
+// scalars live on the device (k_bicg_scal); one host sync per iteration reads ||r||^2.
+
+// z = M^-1 q: one V-cycle of the wall-closure multigrid from z = 0 with level-0 rhs q (no
+// mean shift).  Level 0 is re-pointed at (z, scratch, q) and restored afterwards; the cycle's
+// ping-pong may leave the result in either buffer, so z / scratch are swapped to match.
+int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch) {
+    double* sv[3] = {s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP], s->arr[NS_ARR_RPHI]};
+    HIPCHK(hipMemsetAsync(z - (ptrdiff_t)nsg::HALO * s->g.ld, 0, s->plane * sizeof(double), s->st));
+    CHK(halo(s, {q}, 5));
+    s->arr[NS_ARR_PHI] = z;
+    s->arr[NS_ARR_TMP] = scratch;
+    s->arr[NS_ARR_RPHI] = q;
+    s->pc_active = true;
+    int tn = 0;
+    bool done = false;
+    const int rc = mg_vcycle(s, &tn, 0, [](int) { return 0; }, &done);
+    s->pc_active = false;
+    // (level 0's own pointer: a single-level hierarchy relaxes it in mg_coarse, which does not
+    // track the swaps in s->arr)
+    if (s->lv[0].phi != z) std::swap(z, scratch);
+    s->arr[NS_ARR_PHI] = sv[0];
+    s->arr[NS_ARR_TMP] = sv[1];
+    s->arr[NS_ARR_RPHI] = sv[2];
+    return rc;
+}
+
+int pois_solve_krylov(ns_solver* s, int* its, double* res, ns_stats* stt) {
+    const double tol2 = s->rtol * s->rtol;
+    const int maxit = std::min(s->max_iters, 5000);
+    double** K = s->kv;   // r, r0, p, v, s, t, ph, sh, scratch
+    nsg::KrylovArgs a{};
+    a.g = s->g;
+    a.x = s->arr[NS_ARR_PHI];
+    a.r = K[0]; a.r0 = K[1]; a.p = K[2]; a.v = K[3]; a.s = K[4]; a.t = K[5];
+    a.b = s->arr[NS_ARR_RPHI];
+    a.shift = s->scal + S_SHIFT;
+    a.sc = s->ksc;
+    a.part = s->part;
+    double* d = s->ksc + nsg::KS_D;
+    const double n = s->ncells;
+    auto reduce = [&](int nb, int nv) -> int {
+        nsg::launch_reduce_sum(s->part, nb, nv, d, s->st);
+        return allreduce(s, d, nv, ncclSum);
+    };
+    auto apply = [&](double* x, double* y, const double* q) -> int {
+        CHK(halo(s, {x}, 1));
+        const int nb = nsg::launch_pois_apply(s->g, s->c, x, y, q, s->part, s->st);
+        return reduce(nb, 2);
+    };
+    // r = P(b - mean b - A x), r0 = r, p = v = 0 (also the restart after a breakdown)
+    auto init = [&]() -> int {
+        CHK(apply(a.x, a.v, nullptr));
+        nsg::launch_bicg_scal(nsg::KSC_MEAN, d, n, s->ksc, s->st);
+        CHK(reduce(nsg::launch_bicg_vec(nsg::KV_INIT, a, s->st), 3));
+        nsg::launch_bicg_scal(nsg::KSC_INIT, d, n, s->ksc, s->st);
+        return 0;
+    };
+    CHK(init());
+    int it = 0, nchk = 0, restarts = 0;
+    for (;;) {
+        // ||r||^2 and the breakdown flag to the host: the convergence test (KSPSolve's rtol on
+        // ||b - mean||)
+        HIPCHK(hipMemcpyAsync(s->scal + S_AUX, d, sizeof(double), hipMemcpyDeviceToDevice, s->st));
+        HIPCHK(hipMemcpyAsync(s->scal + S_AUX + 1, s->ksc + nsg::KS_BRK, sizeof(double), hipMemcpyDeviceToDevice, s->st));
+        if (s->verbose) HIPCHK(hipMemcpyAsync(s->scal + S_AUX + 2, s->ksc + nsg::KS_ALPHA, 2 * sizeof(double), hipMemcpyDeviceToDevice, s->st));
+        CHK(fetch(s));
+        nchk++;
+        const double r2 = s->hs[S_AUX], b2 = s->hs[S_SHIFT + 1];
+        *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
+        if (s->verbose)
+            fprintf(stderr, "nsgpu poisson (bicgstab): it %d rel. residual %.3e (alpha %.3e omega %.3e%s)\n", it, *res,
+                    s->hs[S_AUX + 2], s->hs[S_AUX + 3], s->hs[S_AUX + 1] != 0.0 ? ", breakdown: restart" : "");
+        if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = it; return NS_EDIVERGE; }
+        if (r2 <= tol2 * b2 || r2 == 0.0 || it >= maxit) break;
+        if (s->hs[S_AUX + 1] != 0.0) {
+            if (++restarts > 50) { set_err("BiCGStab broke down 50 times"); *its = it; return NS_EDIVERGE; }
+            CHK(init());
+            continue;
+        }
+        nsg::launch_bicg_scal(nsg::KSC_RHO, d, n, s->ksc, s->st);        // beta, rho
+        nsg::launch_bicg_vec(nsg::KV_P, a, s->st);                        // p = r + beta (p - omega v)
+        CHK(mg_precond(s, a.p, s->kv[6], s->kv[8]));                      // ph = M^-1 p
+        a.ph = s->kv[6];
+        CHK(apply(a.ph, a.v, a.r0));                                      // y = A ph, r0.y
+        nsg::launch_bicg_scal(nsg::KSC_ALPHA, d, n, s->ksc, s->st);      // mean y, alpha
+        nsg::launch_bicg_vec(nsg::KV_V, a, s->st);                        // v = P y, s = r - alpha v
+        CHK(mg_precond(s, a.s, s->kv[7], s->kv[8]));                      // sh = M^-1 s
+        a.sh = s->kv[7];
+        CHK(apply(a.sh, a.t, nullptr));                                   // y = A sh
+        nsg::launch_bicg_scal(nsg::KSC_MEAN, d, n, s->ksc, s->st);
+        CHK(reduce(nsg::launch_bicg_vec(nsg::KV_T, a, s->st), 3));       // t = P y; t.s, t.t (3-wide partials)
+        nsg::launch_bicg_scal(nsg::KSC_OMEGA, d, n, s->ksc, s->st);
+        CHK(reduce(nsg::launch_bicg_vec(nsg::KV_X, a, s->st), 3));       // x, r; r.r, r0.r, sum r
+        it++;
+    }
+    *its = it;
+    if (stt) stt->n_checks += nchk;
+    return 0;
+}
+
+int pois_solve_any(ns_solver* s, int* its, double* res, ns_stats* stt) {
+    if (s->kv[0]) return pois_solve_krylov(s, its, res, stt);
+    if (s->poisson == NS_POISSON_MG) return pois_solve_mg(s, its, res, stt);
+    return pois_solve(s, its, res, stt);
+}
+
 // coefficient tables of one level: [pw pe bx | ps pn by | hx hy]  (ConstructLHS, FluidSolver.cpp:113-131)
-std::vector<double> coef_tables(const std::vector<double>& hx, const std::vector<double>& hy) {
+// neu[side]: a NEUMANN outflow side, whose velocity ghost q (:98) adds no Helmholtz wall term
+std::vector<double> coef_tables(const std::vector<double>& hx, const std::vector<double>& hy,
+                                const int* neu = nullptr) {
+    const int nz[4] = {0, 0, 0, 0};
+    if (!neu) neu = nz;
     const int nx = (int)hx.size(), ny = (int)hy.size();
     std::vector<double> h(8 * (size_t)nx + 8 * (size_t)ny + 2, 0.0);
     double *pw = h.data(), *pe = pw + nx, *bx = pe + nx, *ps = bx + nx, *pn = ps + ny, *by = pn + ny;
@@ -743,14 +886,14 @@ std::vector<double> coef_tables(const std::vector<double>& hx, const std::vector
         hxo[i] = a;
         pw[i] = i > 0 ? 2.0 / (a * (a + hx[i - 1])) : 0.0;
         pe[i] = i < nx - 1 ? 2.0 / (a * (a + hx[i + 1])) : 0.0;
-        bx[i] = (i == 0 ? 2.0 / (a * a) : 0.0) + (i == nx - 1 ? 2.0 / (a * a) : 0.0);
+        bx[i] = (i == 0 && !neu[0] ? 2.0 / (a * a) : 0.0) + (i == nx - 1 && !neu[1] ? 2.0 / (a * a) : 0.0);
     }
     for (int j = 0; j < ny; j++) {
         const double a = hy[j];
         hyo[j] = a;
         ps[j] = j > 0 ? 2.0 / (a * (a + hy[j - 1])) : 0.0;
         pn[j] = j < ny - 1 ? 2.0 / (a * (a + hy[j + 1])) : 0.0;
-        by[j] = (j == 0 ? 2.0 / (a * a) : 0.0) + (j == ny - 1 ? 2.0 / (a * a) : 0.0);
+        by[j] = (j == 0 && !neu[2] ? 2.0 / (a * a) : 0.0) + (j == ny - 1 && !neu[3] ? 2.0 / (a * a) : 0.0);
     }
     return h;
 }
@@ -1028,8 +1171,18 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         } else if (E.type == NS_BC_WALL) {
             if (E.nx != 0) g.c1[k] = 2 * E.info; else g.c0[k] = 2 * E.info;
         } else if (E.type == NS_BC_NEUMANN) {
-            set_err("NEUMANN outflow edges are not supported by this build's Poisson kernels");
-            return NS_EINVAL;
+            // outflow: velocity ghost q, phi ghost 2.5 phi_0 - 2 phi_1 + 0.5 phi_2 (:98-101);
+            // the Poisson solve becomes BiCGStab on the true matrix (pois_solve_krylov)
+            g.neu[k] = 1;
+            if ((k < 2 ? gd->nx : gd->ny) < 3) {
+                set_err("a NEUMANN side needs >= 3 cells along its normal (its phi ghost reaches 2 inward)");
+                return NS_EINVAL;
+            }
+            if (p->poisson != NS_POISSON_MG) {
+                set_err("NEUMANN outflow edges need the multigrid-preconditioned Krylov Poisson solve "
+                        "(NS_POISSON_MG): the RB-SOR / Jacobi sweeps cannot relax the outflow rows");
+                return NS_EINVAL;
+            }
         } else {
             set_err("edge %d: boundary condition type %d is not supported (INLET_PARABOLIC / PRESSURE / unset "
                     "have no ghost stencil in the reference)", side_edge[k], E.type);
@@ -1110,7 +1263,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     for (int j = 0; j < g.ny; j++)
         if (!(hy0[j] > 0)) { set_err("hy[%d] = %g is not positive", j, hy0[j]); return fail(NS_EINVAL); }
     {
-        const std::vector<double> h = coef_tables(hx0, hy0);
+        const std::vector<double> h = coef_tables(hx0, hy0, g.neu);
         if (hipMalloc(&s->coef, h.size() * sizeof(double)) != hipSuccess) { set_err("hipMalloc coef failed"); return fail(NS_ENOMEM); }
         if (hipMemcpy(s->coef, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) { set_err("coef upload failed"); return fail(NS_EHIP); }
         s->c = coef_view(s->coef, g.nx, g.ny);
@@ -1123,6 +1276,16 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (int rc = build_levels(s, hx0, hy0)) return fail(rc);
         if (p->mg_coarse_iters > 0) s->mg_coarse_iters = p->mg_coarse_iters;
         if (s->lv.size() < 2) s->poisson = NS_POISSON_RBSOR;  // nothing to coarsen: plain RB-SOR
+    }
+    if (g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3]) {
+        // BiCGStab planes (the preconditioner is the hierarchy above; with a single level its
+        // coarse relaxation -- 2n+10 SOR sweeps from zero -- is the preconditioner)
+        const size_t nk = sizeof(s->kv) / sizeof(s->kv[0]);
+        if (hipMalloc(&s->kv_mem, nk * s->plane * sizeof(double)) != hipSuccess) { set_err("hipMalloc Krylov planes failed"); return fail(NS_ENOMEM); }
+        if (hipMemsetAsync(s->kv_mem, 0, nk * s->plane * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
+        for (size_t k = 0; k < nk; k++) s->kv[k] = s->kv_mem + k * s->plane + (size_t)nsg::HALO * g.ld;
+        if (hipMalloc(&s->ksc, nsg::KS_NUM * sizeof(double)) != hipSuccess) { set_err("hipMalloc failed"); return fail(NS_ENOMEM); }
+        if (hipMemsetAsync(s->ksc, 0, nsg::KS_NUM * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     }
     const int np = nsg::max_partials(g);
     if (hipMalloc(&s->part, (size_t)np * 4 * sizeof(double)) != hipSuccess) { set_err("hipMalloc partials failed"); return fail(NS_ENOMEM); }
@@ -1155,6 +1318,8 @@ void ns_destroy(ns_solver* s) {
     }
     if (s->base) (void)hipFree(s->base);
     if (s->phim_mem) (void)hipFree(s->phim_mem);
+    if (s->kv_mem) (void)hipFree(s->kv_mem);
+    if (s->ksc) (void)hipFree(s->ksc);
     if (s->coef) (void)hipFree(s->coef);
     if (s->part) (void)hipFree(s->part);
     if (s->scal) (void)hipFree(s->scal);
@@ -1181,8 +1346,7 @@ int ns_step(ns_solver* s, ns_stats* out) {
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
     CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
     CHK(extrapolate_phi(s));
-    if (s->poisson == NS_POISSON_MG) CHK(pois_solve_mg(s, &st.it_phi, &st.res_phi, &st));  // KSPSolve(phiSolver) (:551)
-    else CHK(pois_solve(s, &st.it_phi, &st.res_phi, &st));
+    CHK(pois_solve_any(s, &st.it_phi, &st.res_phi, &st));         // KSPSolve(phiSolver)  (:551)
     CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
     CHK(correct(s));                                               // CorrectVelocities    (:552)
     CHK(fetch(s));                                                 // VecMin/VecMax        (:554-557)
@@ -1284,6 +1448,10 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         if (out) { out[0] = s->hs[S_DIVSUM]; out[1] = s->hs[S_DIVSUM + 1]; }
         return 0;
     case NS_K_POISSON: {
+        if (s->kv[0]) {
+            set_err("NS_K_POISSON sweeps relax the wall-closure operator; with a NEUMANN side use NS_K_POIS_SOLVE");
+            return NS_EINVAL;
+        }
         int nb = 0;
         CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
         const int pairs = (s->poisson != NS_POISSON_JACOBI && !s->tiled && iters > 0) ? (iters - 1) / 2 : 0;
@@ -1326,12 +1494,15 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         double r = 0;
         CHK(rhs_mean(s));
         CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
-        if (s->poisson == NS_POISSON_MG) CHK(pois_solve_mg(s, &its, &r, nullptr));
-        else CHK(pois_solve(s, &its, &r, nullptr));
+        CHK(pois_solve_any(s, &its, &r, nullptr));
         if (out) { out[0] = its; out[1] = r; }
         return 0;
     }
     case NS_K_RESIDUAL: {
+        if (s->kv[0]) {
+            set_err("NS_K_RESIDUAL is the wall-closure residual; not defined with a NEUMANN side");
+            return NS_EINVAL;
+        }
         CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
         const int nb = nsg::launch_pois_residual(s->g, s->c, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI],
                                                  s->scal + S_SHIFT, s->part, s->st);

@@ -737,43 +737,102 @@ static int pcg(const og_grid* g, op_fn A, double a, const double* b, double* x, 
     return it;
 }
 
-/* Jacobi-right-preconditioned BiCGStab (Poisson with Neumann faces), mean-projected residual */
-static int bicgstab(const og_grid* g, op_fn A, double a, const double* b, double* x, const double* dg,
-                    int proj, double rtol, int maxit) {
-    int n = g->N;
-    double *r = malloc(sizeof(double) * n), *r0 = malloc(sizeof(double) * n), *p = malloc(sizeof(double) * n);
-    double *v = malloc(sizeof(double) * n), *s = malloc(sizeof(double) * n), *t = malloc(sizeof(double) * n);
-    double *ph = malloc(sizeof(double) * n), *sh = malloc(sizeof(double) * n);
-    A(g, a, x, t);
-    for (int c = 0; c < n; c++) r[c] = b[c] - t[c];
-    if (proj) { double m = 0; for (int c = 0; c < n; c++) m += r[c]; m /= n; for (int c = 0; c < n; c++) r[c] -= m; }
-    double bn = sqrt(dot(n, b, b));
-    memcpy(r0, r, sizeof(double) * n);
-    double rho = 1, al = 1, om = 1;
-    memset(v, 0, sizeof(double) * n); memset(p, 0, sizeof(double) * n);
-    int it = 0;
-    if (bn == 0.0) goto done;
-    while (it < maxit) {
-        if (sqrt(dot(n, r, r)) <= rtol * bn) break;
-        double rho1 = dot(n, r0, r);
-        if (rho1 == 0.0) break;
-        double be = (rho1 / rho) * (al / om);
-        rho = rho1;
-        for (int c = 0; c < n; c++) p[c] = r[c] + be * (p[c] - om * v[c]);
-        for (int c = 0; c < n; c++) ph[c] = p[c] / dg[c];
-        A(g, a, ph, v);
-        al = rho / dot(n, r0, v);
-        for (int c = 0; c < n; c++) s[c] = r[c] - al * v[c];
-        for (int c = 0; c < n; c++) sh[c] = s[c] / dg[c];
-        A(g, a, sh, t);
-        om = dot(n, t, s) / dot(n, t, t);
-        for (int c = 0; c < n; c++) { x[c] += al * ph[c] + om * sh[c]; r[c] = s[c] - om * t[c]; }
-        if (proj) { double m = 0; for (int c = 0; c < n; c++) m += r[c]; m /= n; for (int c = 0; c < n; c++) r[c] -= m; }
-        it++;
+/* One row of the assembled Poisson matrix LHS_phi (ConstructLHS FluidSolver.cpp:105-131 with
+ * AddGhostStencils :147-163): (col, val) pairs, at most 1 + 4 * 3. */
+static int poisson_row(const og_grid* g, int c, int* col, double* val) {
+    int i = g->ci[c], j = g->cj[c], m = 0;
+    double dg = 0.0;
+    for (int k = 0; k < 4; k++) {
+        int ii = i + NXk[k], jj = j + NYk[k];
+        if (in_dom(g, ii, jj)) {
+            double w = face_w8(g, i, j, k, 1);
+            col[m] = CID(g, ii, jj); val[m++] = w; dg -= w;
+        } else {
+            double w = face_w8(g, i, j, k, 0);
+            const og_edge* E = &g->e[TAG(g, i, j, k)];
+            if (E->btype == OG_NEUMANN) {   /* ghost 2.5 p_c - 2 p_1 + 0.5 p_2 (:98-101) */
+                dg += 2.5 * w;
+                col[m] = CID(g, i - E->nx, j - E->ny); val[m++] = -2.0 * w;
+                col[m] = CID(g, i - 2 * E->nx, j - 2 * E->ny); val[m++] = 0.5 * w;
+            } else dg += w;                 /* ghost p_c */
+            dg -= w;
+        }
     }
-done:
-    free(r); free(r0); free(p); free(v); free(s); free(t); free(ph); free(sh);
-    return it;
+    col[m] = c; val[m++] = dg;
+    return m;
+}
+
+/* NEUMANN outflow sides make LHS_phi non-symmetric and not diagonally dominant; Krylov
+ * iterations with a Jacobi preconditioner stall or diverge on it, so the oracle solves it
+ * DIRECTLY: P A x = P b (P = mean projection, the null-space handling of :142-144, 550) is
+ * A x = P b + c 1 for a scalar c.  With row z of A replaced by e_z (x_z = 0; the constant
+ * null space pinned) the banded matrix Abar is regular, x = x1 + c x2 for Abar x1 = (P b)',
+ * Abar x2 = 1' (row z zeroed), and c follows from the dropped row z.  z must carry a nonzero
+ * entry of A's LEFT null vector, which with an outflow side lives next to the outflow (in 1-D
+ * it is (.., 0, -1/2, 1) on the last two cells): z = the first cell with a NEUMANN face.
+ * Banded Gaussian elimination with partial pivoting; returns 1 (one "iteration"), -1 if
+ * singular. */
+static int neu_direct(const og_grid* g, const double* b, double* x) {
+    const int n = g->N;
+    int col[16], kl = 0;
+    double val[16];
+    for (int c = 0; c < n; c++) {
+        int m = poisson_row(g, c, col, val);
+        for (int q = 0; q < m; q++) kl = abs(col[q] - c) > kl ? abs(col[q] - c) : kl;
+    }
+    int z = 0;
+    for (int c = n - 1; c >= 0; c--)
+        for (int k = 0; k < 4; k++) {
+            int e = in_dom(g, g->ci[c] + NXk[k], g->cj[c] + NYk[k]) ? -1 : TAG(g, g->ci[c], g->cj[c], k);
+            if (e >= 0 && g->e[e].btype == OG_NEUMANN) z = c;
+        }
+    const int ku = kl, W = 2 * kl + ku + 1;
+    double* ab = calloc((size_t)n * W, sizeof(double));
+    double *f1 = malloc(sizeof(double) * n), *f2 = malloc(sizeof(double) * n);
+#define AB(r, cc) ab[(size_t)(r) * W + ((cc) - (r) + kl)]
+    for (int c = 0; c < n; c++) {
+        if (c == z) { AB(z, z) = 1.0; f1[z] = 0.0; f2[z] = 0.0; continue; }
+        int m = poisson_row(g, c, col, val);
+        for (int q = 0; q < m; q++) AB(c, col[q]) += val[q];
+        f1[c] = b[c]; f2[c] = 1.0;
+    }
+    int rc = 1;
+    for (int k = 0; k < n && rc > 0; k++) {
+        int last = k + kl < n - 1 ? k + kl : n - 1, hi = k + kl + ku < n - 1 ? k + kl + ku : n - 1, p = k;
+        for (int r = k + 1; r <= last; r++) if (fabs(AB(r, k)) > fabs(AB(p, k))) p = r;
+        if (AB(p, k) == 0.0) { rc = -1; break; }
+        if (p != k) {
+            for (int cc = k; cc <= hi; cc++) { double t = AB(k, cc); AB(k, cc) = AB(p, cc); AB(p, cc) = t; }
+            double t = f1[k]; f1[k] = f1[p]; f1[p] = t;
+            t = f2[k]; f2[k] = f2[p]; f2[p] = t;
+        }
+        for (int r = k + 1; r <= last; r++) {
+            double fct = AB(r, k) / AB(k, k);
+            if (fct == 0.0) continue;
+            AB(r, k) = 0.0;
+            for (int cc = k + 1; cc <= hi; cc++) AB(r, cc) -= fct * AB(k, cc);
+            f1[r] -= fct * f1[k];
+            f2[r] -= fct * f2[k];
+        }
+    }
+    if (rc > 0) {
+        for (int k = n - 1; k >= 0; k--) {
+            int hi = k + kl + ku < n - 1 ? k + kl + ku : n - 1;
+            double s1 = f1[k], s2 = f2[k];
+            for (int cc = k + 1; cc <= hi; cc++) { s1 -= AB(k, cc) * f1[cc]; s2 -= AB(k, cc) * f2[cc]; }
+            f1[k] = s1 / AB(k, k);
+            f2[k] = s2 / AB(k, k);
+        }
+        /* the dropped row z: a_z . (x1 + c x2) - c = (P b)_z */
+        int m = poisson_row(g, z, col, val);
+        double a1 = 0.0, a2 = 0.0;
+        for (int q = 0; q < m; q++) { a1 += val[q] * f1[col[q]]; a2 += val[q] * f2[col[q]]; }
+        double cc = (b[z] - a1) / (a2 - 1.0);
+        for (int c = 0; c < n; c++) x[c] = f1[c] + cc * f2[c];
+    }
+#undef AB
+    free(ab); free(f1); free(f2);
+    return rc;
 }
 
 int og_solve_helmholtz(const og_grid* g, double alpha, const double* rhs, double* x, double rtol, int maxit) {
@@ -795,8 +854,7 @@ int og_solve_poisson(const og_grid* g, double* rhs, double* x, double rtol, int 
     diag_poisson(g, d);
     int neu = 0;
     for (int k = 0; k < g->ne; k++) neu |= g->e[k].btype == OG_NEUMANN;
-    int it = neu ? bicgstab(g, op_pois, 0.0, rhs, x, d, 1, rtol, maxit)
-                 : pcg(g, op_pois, 0.0, rhs, x, d, -1.0, 1, rtol, maxit);
+    int it = neu ? neu_direct(g, rhs, x) : pcg(g, op_pois, 0.0, rhs, x, d, -1.0, 1, rtol, maxit);
     free(d);
     return it;
 }

@@ -22,6 +22,7 @@ ap.add_argument("--nsteps", type=int, default=10)
 ap.add_argument("--solver", type=int, default=nsa.NS_POISSON_MG)
 ap.add_argument("--tol", type=float, default=1e-10)
 ap.add_argument("--output", required=True)
+ap.add_argument("--bc", default="", help="edge BCs W,N,E,S as type:info,... (default: the cavity)")
 ap.add_argument("--stats-only", action="store_true", help="gather only the per-step stats (large grids)")
 a = ap.parse_args()
 dist.init_process_group("gloo")
@@ -34,7 +35,8 @@ else:
     kw["nccl_id"] = nccl_id(dist)
 status = "ok"
 try:
-    gs = nsa.GpuSolver(nsa.rectangle(n, ny), 1.0 / (8 * n), 100.0, **kw)
+    bc = [(int(t), float(i)) for t, i in (e.split(":") for e in a.bc.split(","))] if a.bc else None
+    gs = nsa.GpuSolver(nsa.rectangle(n, ny, bc=bc), 1.0 / (8 * n), 100.0, **kw)
     mm = [list(gs.step().values())[:7] for _ in range(a.nsteps)]
     u, v, phi = (np.zeros((1, ny)),) * 3 if a.stats_only else gs.fields()
 except Exception as e:  # report, don't hang the other rank

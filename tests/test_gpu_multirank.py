@@ -27,8 +27,8 @@ def launch(tmp_path, *args, port=29561, nproc=2):
     return dict(np.load(out, allow_pickle=False))
 
 
-def single(n, ny, steps, poisson, rtol):
-    gs = nsa.GpuSolver(nsa.rectangle(n, ny), 1.0 / (8 * n), 100.0, poisson=poisson, rtol=rtol, device=0)
+def single(n, ny, steps, poisson, rtol, bc=None):
+    gs = nsa.GpuSolver(nsa.rectangle(n, ny, bc=bc), 1.0 / (8 * n), 100.0, poisson=poisson, rtol=rtol, device=0)
     mm = [list(gs.step().values())[:7] for _ in range(steps)]
     u, v, phi = gs.fields()
     return u, v, phi, np.array(mm)
@@ -69,6 +69,27 @@ def test_slabs_host_transport_match_single_rank(tmp_path, monkeypatch, poisson, 
     if poisson == nsa.NS_POISSON_MG and agg != "0" and n % nproc == 0 and (n // nproc) % 2 == 0:
         # agglomerated: the same hierarchy as one rank, so the same V-cycle count per step
         assert np.max(np.abs(r["mm"][:, 6] - mm[:, 6])) <= 1, (r["mm"][:, 6], mm[:, 6])
+
+
+@pytest.mark.parametrize("bc,nproc", [
+    ([(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0)], 2),    # channel: inlet W, outflow E (the last slab)
+    ([(4, 0.0), (2, 0.0), (0, -1.0), (2, 0.0)], 3),   # reversed: outflow W (the first slab)
+    ([(2, 0.0), (4, 0.0), (2, 0.0), (0, 1.0)], 2),    # outflow N: inside every slab's rows
+])
+def test_neumann_outflow_slabs_match_single_rank(tmp_path, bc, nproc):
+    """NEUMANN outflow (BiCGStab + V-cycle preconditioner): ghost rows before every operator
+    application and preconditioner, and every dot product all-reduced -- the slabs converge
+    to the single-rank solution."""
+    n, ny, steps, rtol = 96, 64, 5, 1e-11
+    spec = ",".join(f"{t}:{i}" for t, i in bc)
+    r = launch(tmp_path, "--xport", "host", "--size", str(n), "--size-y", str(ny), "--nsteps", str(steps),
+               "--solver", str(nsa.NS_POISSON_MG), "--tol", str(rtol), "--bc", spec, nproc=nproc,
+               port=29581 + nproc)
+    assert str(r["status"]) == "ok", r["status"]
+    u, v, phi, mm = single(n, ny, steps, nsa.NS_POISSON_MG, rtol, bc)
+    assert np.max(np.abs(r["u"] - u)) <= 1e-8
+    assert np.max(np.abs(r["v"] - v)) <= 1e-8
+    np.testing.assert_allclose(r["mm"][:, :4], mm[:, :4], atol=1e-8)
 
 
 def test_rccl_two_ranks_one_gpu_probe(tmp_path):

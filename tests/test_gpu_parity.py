@@ -18,6 +18,9 @@ pytestmark = pytest.mark.gpu
 
 BC_CAVITY = [(2, 0.0), (2, 1.0), (2, 0.0), (2, 0.0)]
 BC_FLOW = [(0, 1.0), (2, 0.0), (0, 1.0), (2, 0.5)]   # inlet W, moving wall N, inlet-as-outlet E, moving wall S
+BC_CHANNEL = [(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0)]  # inlet W, walls N / S, NEUMANN outflow E
+BC_OUT_N = [(2, 0.0), (4, 0.0), (2, 0.5), (0, 1.0)]    # inflow from S, outflow N, moving wall E
+BC_OUT_WS = [(4, 0.0), (0, -0.5), (0, -1.0), (4, 0.0)]  # inflow N / E, outflow W and S (a corner)
 
 
 def pair(nsa, nx, ny, dt, re, bc=BC_CAVITY, xratio=-1, yratio=-1, **kw):
@@ -35,7 +38,8 @@ def rand(rng, n, scale=1.0):
 
 
 GEOMS = [(24, 24, -1, -1, BC_CAVITY), (20, 33, -1, -1, BC_FLOW), (17, 16, 1.07, 0.95, BC_CAVITY),
-         (64, 64, -1, -1, BC_FLOW), (100, 130, 1.01, -1, BC_FLOW)]
+         (64, 64, -1, -1, BC_FLOW), (100, 130, 1.01, -1, BC_FLOW), (40, 24, -1, -1, BC_CHANNEL),
+         (33, 70, 1.03, 0.97, BC_OUT_N), (30, 26, -1, -1, BC_OUT_WS)]
 
 
 @pytest.mark.parametrize("nx,ny,xr,yr,bc", GEOMS)
@@ -171,6 +175,55 @@ def test_full_steps_vs_oracle(gpu, n, steps, re, bc):
     p = phi.ravel() - phi.mean()
     q = ref["phi"] - ref["phi"].mean()
     assert np.linalg.norm(p - q) <= 1e-5 * np.linalg.norm(q)
+
+
+@pytest.mark.parametrize("nx,ny,bc", [(40, 24, BC_CHANNEL), (64, 64, BC_CHANNEL), (24, 48, BC_OUT_N),
+                                      (30, 26, BC_OUT_WS), (33, 20, BC_CHANNEL)])
+def test_neumann_outflow_poisson_solve(gpu, nx, ny, bc):
+    """NEUMANN outflow: the Poisson matrix gains the 2.5 / -2 / 0.5 ghost rows
+    (FluidSolver.cpp:98-101, 147-163); the GPU's BiCGStab (V-cycle preconditioned; a single
+    level for the odd 33 x 20) reaches the oracle's BiCGStab solution of the same
+    mean-projected system.  Tolerance: 1e-8 relative, phi modulo its mean."""
+    rng = np.random.default_rng(11)
+    og, gs = pair(gpu, nx, ny, 1.0 / 256, 100.0, bc, rtol=1e-12)
+    b = rand(rng, nx * ny, 100.0)
+    gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny)); gs.set(gpu.NS_ARR_RPHI, b)
+    its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+    assert res <= 1e-12 and 0 < its < 200
+    xp, _ = og.solve_poisson(b)   # the oracle solves the outflow system directly
+    g = gs.get(gpu.NS_ARR_PHI).ravel()
+    err = float(rel(g - g.mean(), xp - xp.mean()))
+    assert err <= 1e-8, (err, its)
+    with pytest.raises(gpu.NsError):
+        gs.kernel(gpu.NS_K_POISSON, 1)   # the smoother's sweeps are not the outflow operator
+
+
+@pytest.mark.parametrize("nx,ny,steps,re,bc", [(40, 24, 20, 100.0, BC_CHANNEL), (32, 32, 12, 400.0, BC_OUT_N),
+                                               (30, 26, 10, 100.0, BC_OUT_WS)])
+def test_neumann_outflow_full_steps(gpu, nx, ny, steps, re, bc):
+    """Channel-type flows with NEUMANN outflow sides, full steps at the reference's rtol 1e-8
+    against the oracle's converged steps: max|du|, max|dv| <= 1e-6 (as for the cavity)."""
+    dt = 1.0 / (8 * max(nx, ny))
+    og, gs = pair(gpu, nx, ny, dt, re, bc)
+    osv = OSolver(og, dt, re, rtol=1e-13)
+    for k in range(steps):
+        st = gs.step()
+        mm, _ = osv.step()
+        np.testing.assert_allclose([st["umin"], st["umax"], st["vmin"], st["vmax"]], mm, atol=1e-6)
+    ref = osv.get()
+    u, v, phi = gs.fields()
+    du = float(np.max(np.abs(u.ravel() - ref["u"])))
+    dv = float(np.max(np.abs(v.ravel() - ref["v"])))
+    assert du <= 1e-6 and dv <= 1e-6, (du, dv)
+    p = phi.ravel() - phi.mean()
+    q = ref["phi"] - ref["phi"].mean()
+    ep = float(np.linalg.norm(p - q) / np.linalg.norm(q))
+    assert ep <= 1e-5, ep
+
+
+def test_neumann_needs_multigrid(gpu):
+    with pytest.raises(gpu.NsError):
+        gpu.GpuSolver(gpu.rectangle(16, 16, bc=BC_CHANNEL), 1e-3, 100.0, poisson=gpu.NS_POISSON_RBSOR)
 
 
 def test_full_steps_tight_rtol(gpu):
