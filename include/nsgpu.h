@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define NSGPU_ABI_VERSION 1
+#define NSGPU_ABI_VERSION 2   /* 2: ns_grid_desc.face_edge (non-rectangular domains) */
 
 typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm */
 
@@ -63,8 +63,11 @@ typedef struct ns_edge {
 } ns_edge;
 
 /* Grid geometry (replaces the Grid object FluidSolver reads, Grid.h:42-69).
- * This version accepts rectangular domains: cell_id == NULL and the four
- * sides W,E,S,N each covered by exactly one edge (found by its normal). */
+ * Rectangle: cell_id == face_edge == NULL and the four sides W,E,S,N each covered by
+ * exactly one edge (found by its normal) -- the streaming / multigrid fast path.
+ * Any other polygon (steps, holes, split sides; Grid.cpp:131-185): cell_id and
+ * face_edge describe it cell by cell over the nx*ny bounding box; the time step then
+ * runs the masked kernels and Jacobi-preconditioned BiCGStab solves. */
 typedef struct ns_grid_desc {
     int32_t nx, ny;           /* cells in x and y (Grid::hx.size(), hy.size()) */
     const double* hx;         /* nx spacings (Grid::hx) */
@@ -72,6 +75,8 @@ typedef struct ns_grid_desc {
     int32_t n_edges;
     const ns_edge* edges;     /* Grid::edges, in vertex order */
     const int32_t* cell_id;   /* nx*ny ids or -1 (outside); NULL = full rectangle */
+    const int32_t* face_edge; /* nx*ny*4: boundary edge on the W,E,S,N face or -1 (Cell::edges, Grid.h:33);
+                                 required with cell_id */
 } ns_grid_desc;
 
 /* Optional host-side transport for the x-slab exchanges (tests, or clusters without

@@ -34,7 +34,7 @@ class NsGridDesc(ctypes.Structure):
     _fields_ = [("nx", ctypes.c_int32), ("ny", ctypes.c_int32),
                 ("hx", ctypes.POINTER(ctypes.c_double)), ("hy", ctypes.POINTER(ctypes.c_double)),
                 ("n_edges", ctypes.c_int32), ("edges", ctypes.POINTER(NsEdge)),
-                ("cell_id", ctypes.POINTER(ctypes.c_int32))]
+                ("cell_id", ctypes.POINTER(ctypes.c_int32)), ("face_edge", ctypes.POINTER(ctypes.c_int32))]
 
 
 EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),

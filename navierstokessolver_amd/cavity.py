@@ -28,6 +28,51 @@ def rectangle(nx, ny, lx=1.0, ly=1.0, bc=None, xratio=-1, yratio=-1) -> GridSpec
     return GridSpec(geometric_spacing(0.0, lx, nx, xratio), geometric_spacing(0.0, ly, ny, yratio), edges)
 
 
+TOL = 1e-8   # Grid.h:7
+
+
+def polygon(vertices, hx, hy, bc) -> GridSpec:
+    """An axis-parallel polygon over the cells of spacings hx, hy (starting at its lowest
+    x / y), classified as Grid.cpp does: edges and outward normals from consecutive vertices
+    (Grid.cpp:28-72), a cell is inside if a ray from its centre towards +x crosses an odd
+    number of vertical edges, and a cell face lying on an edge (within TOL, Grid.cpp:292)
+    is tagged with that edge -- the last one in vertex order wins (Grid.cpp:131-185).
+    bc: (type, info) per edge, in vertex order.  A full rectangle of four edges comes back
+    without a mask (the fast path)."""
+    V = [(float(x), float(y)) for x, y in vertices]
+    if len(bc) != len(V):
+        raise ValueError("one (type, info) pair per edge")
+    xlo, ylo = min(x for x, _ in V), min(y for _, y in V)
+    X = xlo + np.concatenate([[0.0], np.cumsum(hx)])
+    Y = ylo + np.concatenate([[0.0], np.cumsum(hy)])
+    xc, yc = 0.5 * (X[:-1] + X[1:]), 0.5 * (Y[:-1] + Y[1:])
+    nx, ny = len(hx), len(hy)
+    cross = np.zeros((nx, ny), dtype=np.int64)
+    tag = -np.ones((nx, ny, 4), dtype=np.int32)
+    edges = []
+    for k, (a, b) in enumerate(zip(V, V[1:] + V[:1])):
+        if b[0] == a[0]:
+            enx, eny, pos, lo, hi = (-1 if b[1] > a[1] else 1), 0, b[0], min(a[1], b[1]), max(a[1], b[1])
+            rows = (yc > lo) & (yc < hi)
+            cross += np.outer(pos > xc, rows)
+            face = X[:-1] if enx == -1 else X[1:]
+            tag[np.outer(np.abs(face - pos) <= TOL, rows), 0 if enx == -1 else 1] = k
+        elif b[1] == a[1]:
+            enx, eny, pos, lo, hi = 0, (1 if b[0] > a[0] else -1), b[1], min(a[0], b[0]), max(a[0], b[0])
+            cols = (xc > lo) & (xc < hi)
+            face = Y[:-1] if eny == -1 else Y[1:]
+            tag[np.outer(cols, np.abs(face - pos) <= TOL), 2 if eny == -1 else 3] = k
+        else:
+            raise ValueError("Edges should be parallel to the x-axis or y-axis")
+        edges.append(Edge(enx, eny, int(bc[k][0]), float(bc[k][1])))
+    inside = cross % 2 == 1
+    if inside.all() and len(V) == 4:
+        return GridSpec(np.asarray(hx, dtype=np.float64), np.asarray(hy, dtype=np.float64), edges)
+    cell_id = np.where(inside, np.cumsum(inside.ravel()).reshape(nx, ny) - 1, -1).astype(np.int32)
+    return GridSpec(np.asarray(hx, dtype=np.float64), np.asarray(hy, dtype=np.float64), edges,
+                    cell_id.ravel(), tag.ravel())
+
+
 def cavity(n, lid=1.0) -> GridSpec:
     return rectangle(n, n, bc=[(L.NS_BC_WALL, 0.0), (L.NS_BC_WALL, lid), (L.NS_BC_WALL, 0.0), (L.NS_BC_WALL, 0.0)])
 

@@ -103,8 +103,9 @@ void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t 
 void launch_finish_mean(const double* sums, double ncells, double* shift_and_bn2, hipStream_t st);
 // (sum f, sum f^2) partials over own cells
 int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st);
-// out = a x + b y over the slab's own cells
-void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st);
+// out = a x + b y (+ c z if z) over the slab's own cells
+void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st,
+                  double c = 0.0, const double* z = nullptr);
 // random fill of phi, rhs (sweep benchmark input)
 void launch_fill_random(const Geo& g, double* phi, double* rp, uint64_t seed, hipStream_t st);
 
@@ -161,10 +162,13 @@ struct KrylovArgs {
     double* part;
     int rows;
 };
-// y = A x with A the reference's Poisson matrix incl. NEUMANN outflow rows; partials
+// y = A x with A the reference's Poisson matrix (op 0, NEUMANN outflow rows included) or its
+// Helmholtz matrix I - alpha L_V (op 1), on a rectangle or a masked domain; partials
 // (sum y, sum q*y) per block (q may be null); returns the partial count
-int launch_pois_apply(const Geo& g, const Coef& c, const double* x, double* y, const double* q, double* part,
-                      hipStream_t st);
+int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double* x, double* y, const double* q,
+                 double* part, hipStream_t st);
+// z = q / diag(A) (Jacobi preconditioner of the masked-domain solves)
+void launch_diag_pc(int op, const Geo& g, const Coef& c, double alpha, const double* q, double* z, hipStream_t st);
 // one fused BiCGStab vector update (KV_*); 3 partials per block for KV_INIT / KV_T / KV_X
 int launch_bicg_vec(int mode, KrylovArgs a, hipStream_t st);
 // the scalar recurrences (KSC_*) from reduced sums d

@@ -102,30 +102,76 @@ __device__ __forceinline__ void block_reduce_min(double (&x)[NV], double* out) {
         }
 }
 
+// ------------------------------------------------ cell topology: rectangle or masked polygon
+// The reference's existence tests (Grid::inDomain, Cell::edges[k] == -1) and ghost stencils
+// (EvaluateGhostStencil_V/_P, FluidSolver.cpp:166-181) seen from cell (li, j):
+//   in(di, dj)          the cell at that offset is in the domain;
+//   gv(di, dj, k, q, d) the velocity ghost across face k of the cell at (di, dj), value q;
+//   edge(k)             the edge on face k of this cell (ApplyBoundaryConditions).
+// TopoRect folds to bound checks on the compile-time offsets and per-side constants (the
+// rectangle kernels compile to what they were); TopoMask reads the int32 topology plane
+// (FC_*) and the edge table of a non-rectangular domain.
+struct TopoRect {
+    const Geo& g;
+    int gi, j;
+    __device__ __forceinline__ TopoRect(const Geo& g_, int li, int j_) : g(g_), gi(g_.i0 + li), j(j_) {}
+    __device__ __forceinline__ bool cell() const { return true; }
+    __device__ __forceinline__ bool in(int di, int dj) const {
+        if (dj == 0) return di < 0 ? gi + di >= 0 : gi + di < g.nx;
+        if (di == 0) return dj < 0 ? j + dj >= 0 : j + dj < g.ny;
+        return gi + di >= 0 && gi + di < g.nx && j + dj >= 0 && j + dj < g.ny;
+    }
+    __device__ __forceinline__ double gv(int, int, int k, double q, int d) const { return ghost_v(g, q, k, d); }
+    __device__ __forceinline__ EdgeDev edge(int k) const { return EdgeDev{g.neu[k], g.enx[k], g.eny[k], g.c0[k], g.c1[k]}; }
+};
+struct TopoMask {
+    const Geo& g;
+    int li, j, code;
+    __device__ __forceinline__ int at(int di, int dj) const {
+        const int jj = j + dj;
+        return (jj >= 0 && jj < g.ny) ? g.fc[(ptrdiff_t)(li + di) * g.ld + jj] : 0;
+    }
+    __device__ __forceinline__ TopoMask(const Geo& g_, int li_, int j_) : g(g_), li(li_), j(j_), code(0) { code = at(0, 0); }
+    __device__ __forceinline__ bool cell() const { return (code & FC_IN) != 0; }
+    __device__ __forceinline__ bool in(int di, int dj) const { return (at(di, dj) & FC_IN) != 0; }
+    __device__ __forceinline__ double gv(int di, int dj, int k, double q, int d) const {
+        const EdgeDev& E = g.et[fc_edge(di == 0 && dj == 0 ? code : at(di, dj), k)];
+        return E.neu ? q : (-q + (d == 0 ? E.c0 : E.c1));
+    }
+    __device__ __forceinline__ EdgeDev edge(int k) const { return g.et[fc_edge(code, k)]; }
+};
+
 // ------------------------------------------------ grad phi (GradP, FluidSolver.cpp:420-456)
 // phi ghost (EvaluateGhostStencil_P, :175-181; stencils :87-88, :98-101): walls / inlets
-// phi_c (face value 0.5 (p + p)); a NEUMANN outflow side 2.5 phi_c - 2 phi_1 + 0.5 phi_2
-// with phi_1, phi_2 the next two cells inward (the side's slab rows / columns; nx, ny >= 3)
+// phi_c (face value 0.5 (p + p)); a NEUMANN outflow face 2.5 phi_c - 2 phi_1 + 0.5 phi_2
+// with phi_1, phi_2 the next two cells inward along the edge normal (slab rows / columns)
+__device__ __forceinline__ double ghost_p_e(const Geo& g, const EdgeDev& E, const double* phi, int li, int j,
+                                            double pc) {
+    if (!E.neu) return pc;
+    return 2.5 * pc - 2.0 * ldf(phi, g.ld, li - E.enx, j - E.eny) + 0.5 * ldf(phi, g.ld, li - 2 * E.enx, j - 2 * E.eny);
+}
 __device__ __forceinline__ double ghost_p(const Geo& g, const double* phi, int li, int j, int side, double pc) {
     if (!g.neu[side]) return pc;
     const int di = side == 0 ? 1 : (side == 1 ? -1 : 0), dj = side == 2 ? 1 : (side == 3 ? -1 : 0);
     return 2.5 * pc - 2.0 * ldf(phi, g.ld, li + di, j + dj) + 0.5 * ldf(phi, g.ld, li + 2 * di, j + 2 * dj);
 }
 
+template <class T = TopoRect>
 __device__ __forceinline__ void grad_phi(const Geo& g, const Coef& c, const double* phi, int li, int j,
                                          double& gx, double& gy) {
+    const T t(g, li, j);
     const int gi = g.i0 + li, ld = g.ld;
     const double pc = ldf(phi, ld, li, j);
     const double hx = c.hx[gi], hy = c.hy[j];
     double V0, V1, V2, V3, r;
-    if (gi > 0) { r = hx / (c.hx[gi - 1] + hx); V0 = ldf(phi, ld, li - 1, j) * r + pc * (1 - r); }
-    else V0 = 0.5 * (pc + ghost_p(g, phi, li, j, 0, pc));
-    if (gi < g.nx - 1) { r = hx / (c.hx[gi + 1] + hx); V1 = ldf(phi, ld, li + 1, j) * r + pc * (1 - r); }
-    else V1 = 0.5 * (pc + ghost_p(g, phi, li, j, 1, pc));
-    if (j > 0) { r = hy / (c.hy[j - 1] + hy); V2 = ldf(phi, ld, li, j - 1) * r + pc * (1 - r); }
-    else V2 = 0.5 * (pc + ghost_p(g, phi, li, j, 2, pc));
-    if (j < g.ny - 1) { r = hy / (c.hy[j + 1] + hy); V3 = ldf(phi, ld, li, j + 1) * r + pc * (1 - r); }
-    else V3 = 0.5 * (pc + ghost_p(g, phi, li, j, 3, pc));
+    if (t.in(-1, 0)) { r = hx / (c.hx[gi - 1] + hx); V0 = ldf(phi, ld, li - 1, j) * r + pc * (1 - r); }
+    else V0 = 0.5 * (pc + ghost_p_e(g, t.edge(0), phi, li, j, pc));
+    if (t.in(1, 0)) { r = hx / (c.hx[gi + 1] + hx); V1 = ldf(phi, ld, li + 1, j) * r + pc * (1 - r); }
+    else V1 = 0.5 * (pc + ghost_p_e(g, t.edge(1), phi, li, j, pc));
+    if (t.in(0, -1)) { r = hy / (c.hy[j - 1] + hy); V2 = ldf(phi, ld, li, j - 1) * r + pc * (1 - r); }
+    else V2 = 0.5 * (pc + ghost_p_e(g, t.edge(2), phi, li, j, pc));
+    if (t.in(0, 1)) { r = hy / (c.hy[j + 1] + hy); V3 = ldf(phi, ld, li, j + 1) * r + pc * (1 - r); }
+    else V3 = 0.5 * (pc + ghost_p_e(g, t.edge(3), phi, li, j, pc));
     gx = (V1 - V0) / hx;
     gy = (V3 - V2) / hy;
 }
@@ -154,29 +200,31 @@ __device__ __forceinline__ double slope_r(double qc, double qp, double qm, bool 
 }
 
 // the ApplyBoundaryConditions terms of cell (li, j) added to its RHS (no-op off the walls)
+template <class T = TopoRect>
 __device__ __forceinline__ void rhs_bc(const Geo& g, const Coef& c, double dt, double re,
                                        const double* __restrict__ phi, int li, int j, double& ru_, double& rv_) {
-    const int gi = g.i0 + li, nx = g.nx, ny = g.ny;
-    const bool hW = gi > 0, hE = gi < nx - 1, hS = j > 0, hN = j < ny - 1;
+    const T t(g, li, j);
+    const int gi = g.i0 + li;
+    const bool hW = t.in(-1, 0), hE = t.in(1, 0), hS = t.in(0, -1), hN = t.in(0, 1);
     if (!hW || !hE || !hS || !hN) {
         const double hx = c.hx[gi], hy = c.hy[j];
         const double hxW = hW ? c.hx[gi - 1] : 0.0, hxE = hE ? c.hx[gi + 1] : 0.0;
         const double hyS = hS ? c.hy[j - 1] : 0.0, hyN = hN ? c.hy[j + 1] : 0.0;
         const int first = !hW ? 0 : (!hE ? 1 : (!hS ? 2 : 3));
         double gxc, gyc;
-        grad_phi(g, c, phi, li, j, gxc, gyc);
+        grad_phi<T>(g, c, phi, li, j, gxc, gyc);
         double D;
         if (first < 2) {  // vertical edge: D = d/dy of (dphi/dx) along the wall (:469-473)
             double gxn = 0.0, gxs = 0.0, dum;
-            if (hN) grad_phi(g, c, phi, li, j + 1, gxn, dum);
-            if (hS) grad_phi(g, c, phi, li, j - 1, gxs, dum);
+            if (hN) grad_phi<T>(g, c, phi, li, j + 1, gxn, dum);
+            if (hS) grad_phi<T>(g, c, phi, li, j - 1, gxs, dum);
             if (!hN) D = 2.0 * (gxc - gxs) / (hy + hyS);
             else if (!hS) D = 2.0 * (gxn - gxc) / (hy + hyN);
             else D = gxn / (hy + hyN) - gxs / (hy + hyS) - gxc * (1 / (hy + hyN) - 1 / (hy + hyS));
         } else {          // horizontal edge: D = d/dx of (dphi/dy) (:474-478)
             double gye = 0.0, gyw = 0.0, dum;
-            if (hE) grad_phi(g, c, phi, li + 1, j, dum, gye);
-            if (hW) grad_phi(g, c, phi, li - 1, j, dum, gyw);
+            if (hE) grad_phi<T>(g, c, phi, li + 1, j, dum, gye);
+            if (hW) grad_phi<T>(g, c, phi, li - 1, j, dum, gyw);
             if (!hE) D = 2.0 * (gyc - gyw) / (hx + hxW);
             else if (!hW) D = 2.0 * (gye - gyc) / (hx + hxE);
             else D = gye / (hx + hxE) - gyw / (hx + hxW) - gyc * (1 / (hx + hxE) - 1 / (hx + hxW));
@@ -185,21 +233,22 @@ __device__ __forceinline__ void rhs_bc(const Geo& g, const Coef& c, double dt, d
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (!bnd[k]) continue;
+            const EdgeDev E = t.edge(k);
             double w, W;
-            if (g.neu[k]) {
-                if (k < 2) { w = dt * g.enx[k] * hx * D; W = dt * (0.5 / re / (hx * hx)) * w; rv_ += W; }
-                else       { w = dt * g.eny[k] * hy * D; W = dt * (0.5 / re / (hy * hy)) * w; ru_ += W; }
+            if (E.neu) {
+                if (k < 2) { w = dt * E.enx * hx * D; W = dt * (0.5 / re / (hx * hx)) * w; rv_ += W; }
+                else       { w = dt * E.eny * hy * D; W = dt * (0.5 / re / (hy * hy)) * w; ru_ += W; }
             } else if (k < 2) {
-                W = dt * (0.5 / re / (hx * hx)) * g.c0[k];
+                W = dt * (0.5 / re / (hx * hx)) * E.c0;
                 ru_ += W;
-                w = 2 * dt * (gyc + g.enx[k] * hx * D / 2);
-                W = dt * (0.5 / re / (hx * hx)) * (g.c1[k] + w);
+                w = 2 * dt * (gyc + E.enx * hx * D / 2);
+                W = dt * (0.5 / re / (hx * hx)) * (E.c1 + w);
                 rv_ += W;
             } else {
-                W = dt * (0.5 / re / (hy * hy)) * g.c1[k];
+                W = dt * (0.5 / re / (hy * hy)) * E.c1;
                 rv_ += W;
-                w = 2 * dt * (gxc + g.eny[k] * hy * D / 2);
-                W = dt * (0.5 / re / (hy * hy)) * (g.c0[k] + w);
+                w = 2 * dt * (gxc + E.eny * hy * D / 2);
+                W = dt * (0.5 / re / (hy * hy)) * (E.c0 + w);
                 ru_ += W;
             }
         }
@@ -213,14 +262,17 @@ __device__ __forceinline__ void rhs_bc(const Geo& g, const Coef& c, double dt, d
 // reference's stored divPhi is GradP of the same phi -- saving a 16 B/cell state array.
 // X(t, d) / Y(t, d): spacing table t (0: h, 1: 1/h, 2: 2/(h_{k-1} + h_k)) at row gi + d /
 // column j + d (global tables or an LDS copy)
-template <bool BC = true, class FU, class FV, class FX, class FY>
+template <bool BC = true, class T = TopoRect, class FU, class FV, class FX, class FY>
 __device__ __forceinline__ void rhs_cell(const Geo& g, const Coef& c, double dt, double re, FU&& U, FV&& V,
                                          FX&& X, FY&& Y, const double* __restrict__ phi, int li, int j,
                                          double cu0, double cv0, double& cun, double& cvn, double& ru_,
                                          double& rv_) {
-    const int gi = g.i0 + li, nx = g.nx, ny = g.ny;
-    const bool hW = gi > 0, hWW = gi > 1, hE = gi < nx - 1, hEE = gi < nx - 2;
-    const bool hS = j > 0, hSS = j > 1, hN = j < ny - 1, hNN = j < ny - 2;
+    const T t(g, li, j);
+    // existence (Grid::inDomain / Cell::edges, which agree on a consistent polygon); a masked
+    // domain's second neighbour only counts behind an existing first one (SlopeLimiter of the
+    // neighbour reads it only then)
+    const bool hW = t.in(-1, 0), hWW = hW && t.in(-2, 0), hE = t.in(1, 0), hEE = hE && t.in(2, 0);
+    const bool hS = t.in(0, -1), hSS = hS && t.in(0, -2), hN = t.in(0, 1), hNN = hN && t.in(0, 2);
     const double hx = X(0, 0), hy = Y(0, 0);
     const double hxW = hW ? X(0, -1) : 0.0, hxE = hE ? X(0, 1) : 0.0;
     const double hyS = hS ? Y(0, -1) : 0.0, hyN = hN ? Y(0, 1) : 0.0;
@@ -249,15 +301,15 @@ __device__ __forceinline__ void rhs_cell(const Geo& g, const Coef& c, double dt,
     rv_ += 0.5 * dt * cv0;
     {
         double D0, D1, D2, D3;
-        D0 = hW ? hre * (uc - uW) * sxW : hre * rx * (uc - ghost_v(g, uc, 0, 0));
-        D1 = hE ? hre * (uE - uc) * sxE : -hre * rx * (uc - ghost_v(g, uc, 1, 0));
-        D2 = hS ? hre * (uc - uS) * syS : hre * ry * (uc - ghost_v(g, uc, 2, 0));
-        D3 = hN ? hre * (uN - uc) * syN : -hre * ry * (uc - ghost_v(g, uc, 3, 0));
+        D0 = hW ? hre * (uc - uW) * sxW : hre * rx * (uc - t.gv(0, 0, 0, uc, 0));
+        D1 = hE ? hre * (uE - uc) * sxE : -hre * rx * (uc - t.gv(0, 0, 1, uc, 0));
+        D2 = hS ? hre * (uc - uS) * syS : hre * ry * (uc - t.gv(0, 0, 2, uc, 0));
+        D3 = hN ? hre * (uN - uc) * syN : -hre * ry * (uc - t.gv(0, 0, 3, uc, 0));
         ru_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
-        D0 = hW ? hre * (vc - vW) * sxW : hre * rx * (vc - ghost_v(g, vc, 0, 1));
-        D1 = hE ? hre * (vE - vc) * sxE : -hre * rx * (vc - ghost_v(g, vc, 1, 1));
-        D2 = hS ? hre * (vc - vS) * syS : hre * ry * (vc - ghost_v(g, vc, 2, 1));
-        D3 = hN ? hre * (vN - vc) * syN : -hre * ry * (vc - ghost_v(g, vc, 3, 1));
+        D0 = hW ? hre * (vc - vW) * sxW : hre * rx * (vc - t.gv(0, 0, 0, vc, 1));
+        D1 = hE ? hre * (vE - vc) * sxE : -hre * rx * (vc - t.gv(0, 0, 1, vc, 1));
+        D2 = hS ? hre * (vc - vS) * syS : hre * ry * (vc - t.gv(0, 0, 2, vc, 1));
+        D3 = hN ? hre * (vN - vc) * syN : -hre * ry * (vc - t.gv(0, 0, 3, vc, 1));
         rv_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
     }
 
@@ -265,61 +317,61 @@ __device__ __forceinline__ void rhs_cell(const Geo& g, const Coef& c, double dt,
     double C[8];
     {
         // x slopes of the cell and of its W/E neighbours (each needs its own ghosts at the wall)
-        const double sxu = slope_r(uc, uE, uW, hE, hW, rx, sxE, sxW, ghost_v(g, uc, 1, 0), ghost_v(g, uc, 0, 0));
-        const double sxv = slope_r(vc, vE, vW, hE, hW, rx, sxE, sxW, ghost_v(g, vc, 1, 1), ghost_v(g, vc, 0, 1));
+        const double sxu = slope_r(uc, uE, uW, hE, hW, rx, sxE, sxW, t.gv(0, 0, 1, uc, 0), t.gv(0, 0, 0, uc, 0));
+        const double sxv = slope_r(vc, vE, vW, hE, hW, rx, sxE, sxW, t.gv(0, 0, 1, vc, 1), t.gv(0, 0, 0, vc, 1));
         double u1, v1, u2, v2;
         u2 = uc - hx / 2 * sxu;
         v2 = vc - hx / 2 * sxv;
         if (hW) {
-            const double su = slope_r(uW, uc, uWW, true, hWW, rxW, sxW, sxWW, 0.0, ghost_v(g, uW, 0, 0));
-            const double sv = slope_r(vW, vc, vWW, true, hWW, rxW, sxW, sxWW, 0.0, ghost_v(g, vW, 0, 1));
+            const double su = slope_r(uW, uc, uWW, true, hWW, rxW, sxW, sxWW, 0.0, t.gv(-1, 0, 0, uW, 0));
+            const double sv = slope_r(vW, vc, vWW, true, hWW, rxW, sxW, sxWW, 0.0, t.gv(-1, 0, 0, vW, 1));
             u1 = uW + hxW / 2 * su;
             v1 = vW + hxW / 2 * sv;
         } else {
-            u1 = 0.5 * (uc + ghost_v(g, uc, 0, 0));
-            v1 = 0.5 * (vc + ghost_v(g, vc, 0, 1));
+            u1 = 0.5 * (uc + t.gv(0, 0, 0, uc, 0));
+            v1 = 0.5 * (vc + t.gv(0, 0, 0, vc, 1));
         }
         C[0] = fnn(u1, u2);
         C[1] = fuv(u1, v1, u2, v2);
         u1 = uc + hx / 2 * sxu;
         v1 = vc + hx / 2 * sxv;
         if (hE) {
-            const double su = slope_r(uE, uEE, uc, hEE, true, rxE, sxEE, sxE, ghost_v(g, uE, 1, 0), 0.0);
-            const double sv = slope_r(vE, vEE, vc, hEE, true, rxE, sxEE, sxE, ghost_v(g, vE, 1, 1), 0.0);
+            const double su = slope_r(uE, uEE, uc, hEE, true, rxE, sxEE, sxE, t.gv(1, 0, 1, uE, 0), 0.0);
+            const double sv = slope_r(vE, vEE, vc, hEE, true, rxE, sxEE, sxE, t.gv(1, 0, 1, vE, 1), 0.0);
             u2 = uE - hxE / 2 * su;
             v2 = vE - hxE / 2 * sv;
         } else {
-            u2 = 0.5 * (uc + ghost_v(g, uc, 1, 0));
-            v2 = 0.5 * (vc + ghost_v(g, vc, 1, 1));
+            u2 = 0.5 * (uc + t.gv(0, 0, 1, uc, 0));
+            v2 = 0.5 * (vc + t.gv(0, 0, 1, vc, 1));
         }
         C[2] = fnn(u1, u2);
         C[3] = fuv(u1, v1, u2, v2);
 
-        const double syu = slope_r(uc, uN, uS, hN, hS, ry, syN, syS, ghost_v(g, uc, 3, 0), ghost_v(g, uc, 2, 0));
-        const double syv = slope_r(vc, vN, vS, hN, hS, ry, syN, syS, ghost_v(g, vc, 3, 1), ghost_v(g, vc, 2, 1));
+        const double syu = slope_r(uc, uN, uS, hN, hS, ry, syN, syS, t.gv(0, 0, 3, uc, 0), t.gv(0, 0, 2, uc, 0));
+        const double syv = slope_r(vc, vN, vS, hN, hS, ry, syN, syS, t.gv(0, 0, 3, vc, 1), t.gv(0, 0, 2, vc, 1));
         u2 = uc - hy / 2 * syu;
         v2 = vc - hy / 2 * syv;
         if (hS) {
-            const double su = slope_r(uS, uc, uSS, true, hSS, ryS, syS, sySS, 0.0, ghost_v(g, uS, 2, 0));
-            const double sv = slope_r(vS, vc, vSS, true, hSS, ryS, syS, sySS, 0.0, ghost_v(g, vS, 2, 1));
+            const double su = slope_r(uS, uc, uSS, true, hSS, ryS, syS, sySS, 0.0, t.gv(0, -1, 2, uS, 0));
+            const double sv = slope_r(vS, vc, vSS, true, hSS, ryS, syS, sySS, 0.0, t.gv(0, -1, 2, vS, 1));
             u1 = uS + hyS / 2 * su;
             v1 = vS + hyS / 2 * sv;
         } else {
-            u1 = 0.5 * (uc + ghost_v(g, uc, 2, 0));
-            v1 = 0.5 * (vc + ghost_v(g, vc, 2, 1));
+            u1 = 0.5 * (uc + t.gv(0, 0, 2, uc, 0));
+            v1 = 0.5 * (vc + t.gv(0, 0, 2, vc, 1));
         }
         C[5] = fnn(v1, v2);
         C[4] = fuv(u1, v1, u2, v2);
         u1 = uc + hy / 2 * syu;
         v1 = vc + hy / 2 * syv;
         if (hN) {
-            const double su = slope_r(uN, uNN, uc, hNN, true, ryN, syNN, syN, ghost_v(g, uN, 3, 0), 0.0);
-            const double sv = slope_r(vN, vNN, vc, hNN, true, ryN, syNN, syN, ghost_v(g, vN, 3, 1), 0.0);
+            const double su = slope_r(uN, uNN, uc, hNN, true, ryN, syNN, syN, t.gv(0, 1, 3, uN, 0), 0.0);
+            const double sv = slope_r(vN, vNN, vc, hNN, true, ryN, syNN, syN, t.gv(0, 1, 3, vN, 1), 0.0);
             u2 = uN - hyN / 2 * su;
             v2 = vN - hyN / 2 * sv;
         } else {
-            u2 = 0.5 * (uc + ghost_v(g, uc, 3, 0));
-            v2 = 0.5 * (vc + ghost_v(g, vc, 3, 1));
+            u2 = 0.5 * (uc + t.gv(0, 0, 3, uc, 0));
+            v2 = 0.5 * (vc + t.gv(0, 0, 3, vc, 1));
         }
         C[7] = fnn(v1, v2);
         C[6] = fuv(u1, v1, u2, v2);
@@ -332,9 +384,10 @@ __device__ __forceinline__ void rhs_cell(const Geo& g, const Coef& c, double dt,
     rv_ += val * (-1.5 * dt);
 
     // ---- ApplyBoundaryConditions (FluidSolver.cpp:458-510), boundary cells only
-    if (BC) rhs_bc(g, c, dt, re, phi, li, j, ru_, rv_);
+    if (BC) rhs_bc<T>(g, c, dt, re, phi, li, j, ru_, rv_);
 }
 
+template <class T>
 __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
                                              const double* __restrict__ v, const double* __restrict__ phi,
                                              double* __restrict__ cu, double* __restrict__ cv,
@@ -346,13 +399,14 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
     for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
         const int ld = g.ld;
         const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+        if (!T(g, li, j).cell()) continue;   // outside a masked domain: stays 0
         auto U = [&](int di, int dj) { return ldf(u, ld, li + di, j + dj); };
         auto V = [&](int di, int dj) { return ldf(v, ld, li + di, j + dj); };
         const int gi = g.i0 + li;
         auto X = [&](int t, int d) { return (t == 0 ? c.hx : t == 1 ? c.rhx : c.rsx)[gi + d]; };
         auto Y = [&](int t, int d) { return (t == 0 ? c.hy : t == 1 ? c.rhy : c.rsy)[j + d]; };
         double cun, cvn, ru_, rv_;
-        rhs_cell(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
+        rhs_cell<true, T>(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
         cu[o] = cun;
         cv[o] = cvn;
         ru[o] = ru_;
@@ -498,6 +552,7 @@ __global__ __launch_bounds__(256) void k_rhs_bc(Geo g, Coef c, double dt, double
 // ---------------------------------------------------------------- K3
 // ConstructRHS_phi / Div_V (FluidSolver.cpp:365-418): rhs = div(u*)/dt, plus
 // block partials of (sum rhs, sum rhs^2) for the null-space mean (:550) and ||b||.
+template <class T>
 __global__ __launch_bounds__(256) void k_div(Geo g, Coef c, double dt, const double* __restrict__ u,
                                              const double* __restrict__ v, double* __restrict__ rp,
                                              double* __restrict__ part, int rows) {
@@ -505,18 +560,20 @@ __global__ __launch_bounds__(256) void k_div(Geo g, Coef c, double dt, const dou
     const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
     double acc[2] = {0.0, 0.0};
     for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
+        const T t(g, li, j);
+        if (!t.cell()) continue;
         const int gi = g.i0 + li, ld = g.ld;
         const double uc = ldf(u, ld, li, j), vc = ldf(v, ld, li, j);
         const double hx = c.hx[gi], hy = c.hy[j];
         double V0, V1, V2, V3, r;
-        if (gi > 0) { r = hx / (c.hx[gi - 1] + hx); V0 = ldf(u, ld, li - 1, j) * r + uc * (1 - r); }
-        else V0 = 0.5 * (uc + ghost_v(g, uc, 0, 0));
-        if (gi < g.nx - 1) { r = hx / (c.hx[gi + 1] + hx); V1 = ldf(u, ld, li + 1, j) * r + uc * (1 - r); }
-        else V1 = 0.5 * (uc + ghost_v(g, uc, 1, 0));
-        if (j > 0) { r = hy / (c.hy[j - 1] + hy); V2 = ldf(v, ld, li, j - 1) * r + vc * (1 - r); }
-        else V2 = 0.5 * (vc + ghost_v(g, vc, 2, 1));
-        if (j < g.ny - 1) { r = hy / (c.hy[j + 1] + hy); V3 = ldf(v, ld, li, j + 1) * r + vc * (1 - r); }
-        else V3 = 0.5 * (vc + ghost_v(g, vc, 3, 1));
+        if (t.in(-1, 0)) { r = hx / (c.hx[gi - 1] + hx); V0 = ldf(u, ld, li - 1, j) * r + uc * (1 - r); }
+        else V0 = 0.5 * (uc + t.gv(0, 0, 0, uc, 0));
+        if (t.in(1, 0)) { r = hx / (c.hx[gi + 1] + hx); V1 = ldf(u, ld, li + 1, j) * r + uc * (1 - r); }
+        else V1 = 0.5 * (uc + t.gv(0, 0, 1, uc, 0));
+        if (t.in(0, -1)) { r = hy / (c.hy[j - 1] + hy); V2 = ldf(v, ld, li, j - 1) * r + vc * (1 - r); }
+        else V2 = 0.5 * (vc + t.gv(0, 0, 2, vc, 1));
+        if (t.in(0, 1)) { r = hy / (c.hy[j + 1] + hy); V3 = ldf(v, ld, li, j + 1) * r + vc * (1 - r); }
+        else V3 = 0.5 * (vc + t.gv(0, 0, 3, vc, 1));
         const double val = ((V1 - V0) / hx + (V3 - V2) / hy) / dt;
         rp[(ptrdiff_t)li * ld + j] = val;
         acc[0] += val;
@@ -528,6 +585,7 @@ __global__ __launch_bounds__(256) void k_div(Geo g, Coef c, double dt, const dou
 // ---------------------------------------------------------------- K5
 // CorrectVelocities (FluidSolver.cpp:512-534): u = u* - dt dphi/dx, v = v* - dt dphi/dy,
 // out of place; fused VecMin/VecMax partials (:554-557) as (umin, -umax, vmin, -vmax).
+template <class T>
 __global__ __launch_bounds__(256) void k_correct(Geo g, Coef c, double dt, const double* __restrict__ us,
                                                  const double* __restrict__ vs, double* __restrict__ u,
                                                  double* __restrict__ v, const double* __restrict__ phi,
@@ -536,8 +594,9 @@ __global__ __launch_bounds__(256) void k_correct(Geo g, Coef c, double dt, const
     const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
     double acc[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
     for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
+        if (!T(g, li, j).cell()) continue;
         double gx, gy;
-        grad_phi(g, c, phi, li, j, gx, gy);
+        grad_phi<T>(g, c, phi, li, j, gx, gy);
         const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
         const double un = us[o] - dt * gx, vn = vs[o] - dt * gy;
         u[o] = un;
@@ -1859,124 +1918,17 @@ __global__ void k_fill_random(Geo g, double* phi, double* rp, uint64_t seed) {
     rp[(ptrdiff_t)li * g.ld + j] = 2.0 * ((b >> 11) * s) - 1.0;
 }
 
-// out = a x + b y over the slab's own cells (the Poisson initial-guess extrapolation)
+// out = a x + b y (+ c z) over the slab's own cells (the Poisson initial-guess extrapolation)
 __global__ __launch_bounds__(256) void k_axpby(Geo g, double a, const double* __restrict__ x, double b,
-                                               const double* __restrict__ y, double* __restrict__ out) {
+                                               const double* __restrict__ y, double c, const double* __restrict__ z,
+                                               double* __restrict__ out) {
     const int j = blockIdx.x * 64 + threadIdx.x;
     const int li = blockIdx.y * 4 + threadIdx.y;
     if (j >= g.ny || li >= g.nxl) return;
     const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
-    out[o] = a * x[o] + b * y[o];
-}
-
-// ------------------------------------------------ NEUMANN outflow: BiCGStab pieces
-// With an outflow side the Poisson matrix is no longer the wall-closure L the smoothers
-// relax: AddGhostStencils (FluidSolver.cpp:147-163) adds, per outflow face, w (ghost_p - x_c)
-// with w = 1/h^2 (:124-127) and the ghost 2.5 x_c - 2 x_1 + 0.5 x_2 (:98-101) -- a row that
-// reaches two cells inward and is not diagonally dominant.  The solver then runs BiCGStab on
-// the true operator (the reference's KSPBCGSL, :73-82), right-preconditioned by one V-cycle
-// of the wall-closure multigrid (ns_solver.cpp pois_solve_krylov).
-//
-// y = A x over own cells; block partials (sum y, sum q*y) (q may be null)
-__global__ __launch_bounds__(256) void k_pois_apply(Geo g, Coef c, const double* __restrict__ x,
-                                                    double* __restrict__ y, const double* __restrict__ q,
-                                                    double* __restrict__ part, int rows) {
-    const int j = blockIdx.x * 64 + threadIdx.x;
-    const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
-    double acc[2] = {0.0, 0.0};
-    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
-        const int gi = g.i0 + li, ld = g.ld;
-        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
-        const double xc = x[o], hx = c.hx[gi], hy = c.hy[j];
-        double s = 0.0;
-        if (gi > 0) s += c.pw[gi] * (x[o - ld] - xc);
-        else if (g.neu[0]) s += (ghost_p(g, x, li, j, 0, xc) - xc) / (hx * hx);
-        if (gi < g.nx - 1) s += c.pe[gi] * (x[o + ld] - xc);
-        else if (g.neu[1]) s += (ghost_p(g, x, li, j, 1, xc) - xc) / (hx * hx);
-        if (j > 0) s += c.ps[j] * (x[o - 1] - xc);
-        else if (g.neu[2]) s += (ghost_p(g, x, li, j, 2, xc) - xc) / (hy * hy);
-        if (j < g.ny - 1) s += c.pn[j] * (x[o + 1] - xc);
-        else if (g.neu[3]) s += (ghost_p(g, x, li, j, 3, xc) - xc) / (hy * hy);
-        y[o] = s;
-        acc[0] += s;
-        if (q) acc[1] += q[o] * s;
-    }
-    block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
-}
-
-// BiCGStab vector updates; coefficients from the device scalars k_bicg_scal leaves in sc,
-// each fused with the dot products the next scalar stage needs (block partials, 3 per block):
-//   KV_INIT: r = (b - shift) - (y - mean_y), r0 = r, p = v = 0     partials (r.r, r0.r, sum r)
-//   KV_P:    p = r + beta (p - omega v)
-//   KV_V:    v = y - mean_y (in place), s = r - alpha v
-//   KV_T:    t = y - mean_y (in place)                             partials (t.s, t.t, -)
-//   KV_X:    x += alpha ph + omega sh, r = s - omega t             partials (r.r, r0.r, sum r)
-
-template <int MODE>
-__global__ __launch_bounds__(256) void k_bicg_vec(KrylovArgs a) {
-    const Geo& g = a.g;
-    const int j = blockIdx.x * 64 + threadIdx.x;
-    const int lend = min((int)(blockIdx.y + 1) * 4 * a.rows, g.nxl);
-    double acc[3] = {0.0, 0.0, 0.0};
-    const double alpha = a.sc[KS_ALPHA], beta = a.sc[KS_BETA], omega = a.sc[KS_OMEGA], my = a.sc[KS_MEAN];
-    const double shift = a.shift ? a.shift[0] : 0.0;
-    for (int li = blockIdx.y * 4 * a.rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
-        const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
-        if (MODE == KV_INIT) {
-            const double r = (a.b[o] - shift) - (a.v[o] - my);
-            a.r[o] = r; a.r0[o] = r; a.p[o] = 0.0; a.v[o] = 0.0;
-            acc[0] += r * r; acc[1] += r * r; acc[2] += r;
-        } else if (MODE == KV_P) {
-            a.p[o] = a.r[o] + beta * (a.p[o] - omega * a.v[o]);
-        } else if (MODE == KV_V) {
-            const double v = a.v[o] - my;
-            a.v[o] = v;
-            a.s[o] = a.r[o] - alpha * v;
-        } else if (MODE == KV_T) {
-            const double t = a.t[o] - my;
-            a.t[o] = t;
-            acc[0] += t * a.s[o]; acc[1] += t * t;
-        } else {
-            a.x[o] += alpha * a.ph[o] + omega * a.sh[o];
-            const double r = a.s[o] - omega * a.t[o];
-            a.r[o] = r;
-            acc[0] += r * r; acc[1] += a.r0[o] * r; acc[2] += r;
-        }
-    }
-    if (MODE == KV_INIT || MODE == KV_T || MODE == KV_X)
-        block_reduce_sum<3>(acc, a.part + 3 * (blockIdx.x + gridDim.x * blockIdx.y));
-}
-
-// the scalar recurrences of BiCGStab on one thread; d = the stage's reduced sums
-//   KSC_RHO  (d = r.r, r0.r, sum r):   beta = (rho1/rho)(alpha/omega), rho = rho1
-//   KSC_ALPHA (d = sum y, r0.y):       mean_y, alpha = rho / (r0.y - mean_y sum r0)
-//   KSC_MEAN  (d = sum y):             mean_y
-//   KSC_OMEGA (d = t.s, t.t):          omega = t.s / t.t
-__global__ void k_bicg_scal(int stage, const double* __restrict__ d, double n, double* __restrict__ sc) {
-    // a breakdown (a zero or non-finite denominator) zeroes the coefficient -- the vector
-    // updates then leave x untouched -- and raises KS_BRK; the host restarts from x
-    auto guard = [&](double v) {
-        if (!isfinite(v)) { sc[KS_BRK] = 1.0; return 0.0; }
-        return v;
-    };
-    if (stage == KSC_INIT) {
-        sc[KS_RHO] = 1.0; sc[KS_ALPHA] = 1.0; sc[KS_OMEGA] = 1.0; sc[KS_SUMR0] = d[2]; sc[KS_BRK] = 0.0;
-    } else if (stage == KSC_RHO) {
-        const double rho1 = d[1];
-        sc[KS_BETA] = guard((rho1 / sc[KS_RHO]) * (sc[KS_ALPHA] / sc[KS_OMEGA]));
-        if (rho1 == 0.0) sc[KS_BRK] = 1.0;
-        sc[KS_RHO] = rho1;
-    } else if (stage == KSC_ALPHA) {
-        const double m = d[0] / n;
-        sc[KS_MEAN] = m;
-        sc[KS_ALPHA] = guard(sc[KS_RHO] / (d[1] - m * sc[KS_SUMR0]));
-    } else if (stage == KSC_MEAN) {
-        sc[KS_MEAN] = d[0] / n;
-    } else {
-        const double om = d[1] > 0.0 ? d[0] / d[1] : 0.0;
-        sc[KS_OMEGA] = guard(om);
-        if (om == 0.0) sc[KS_BRK] = 1.0;
-    }
+    double r = a * x[o] + b * y[o];
+    if (z) r += c * z[o];
+    out[o] = r;
 }
 
 // ---------------------------------------------------------------- launchers
@@ -2007,6 +1959,12 @@ namespace nsg {
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
                const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st) {
     const char* e = getenv("NSGPU_RHS");   // NSGPU_RHS=global: the global-load K1 (A/B)
+    if (g.fc) {   // masked domain: the grid kernel with the polygon's topology
+        const int rows = cell_rows(g);
+        const dim3 cg = cell_grid(g, rows);
+        hipLaunchKernelGGL(k_rhs<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
+        return (int)(cg.x * cg.y);
+    }
     if (!(e && std::strcmp(e, "global") == 0)) {
         const dim3 grid((g.ny + 63) / 64, (g.nxl + RT - 1) / RT);
         hipLaunchKernelGGL(k_rhs_lds, grid, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part);
@@ -2017,7 +1975,7 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
     }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
-    hipLaunchKernelGGL(k_rhs, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
+    hipLaunchKernelGGL(k_rhs<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
     return (int)(cg.x * cg.y);
 }
 
@@ -2041,23 +1999,35 @@ static bool cell_streaming() {
 
 int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* rp, double* part,
                hipStream_t st) {
-    if (cell_streaming()) {
+    if (cell_streaming() && !g.fc) {
         CellStreamArgs A{};
         A.g = g; A.c = c; A.dt = dt; A.a0 = u; A.a1 = v; A.o0 = rp; A.part = part;
         return launch_cell_s<3>(A, st);
     }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
-    hipLaunchKernelGGL(k_div, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part, rows);
+    if (g.fc) hipLaunchKernelGGL(k_div<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part, rows);
+    else hipLaunchKernelGGL(k_div<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part, rows);
     return (int)(cg.x * cg.y);
 }
 
-int launch_pois_apply(const Geo& g, const Coef& c, const double* x, double* y, const double* q, double* part,
-                      hipStream_t st) {
+int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double* x, double* y, const double* q,
+                 double* part, hipStream_t st) {
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
-    hipLaunchKernelGGL(k_pois_apply, cg, dim3(64, 4), 0, st, g, c, x, y, q, part, rows);
+    if (op == 0 && g.fc) hipLaunchKernelGGL((k_apply<0, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
+    else if (op == 0) hipLaunchKernelGGL((k_apply<0, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
+    else if (g.fc) hipLaunchKernelGGL((k_apply<1, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
+    else hipLaunchKernelGGL((k_apply<1, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
     return (int)(cg.x * cg.y);
+}
+
+void launch_diag_pc(int op, const Geo& g, const Coef& c, double alpha, const double* q, double* z, hipStream_t st) {
+    const dim3 cg = cell_grid(g);
+    if (op == 0 && g.fc) hipLaunchKernelGGL((k_diag_pc<0, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
+    else if (op == 0) hipLaunchKernelGGL((k_diag_pc<0, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
+    else if (g.fc) hipLaunchKernelGGL((k_diag_pc<1, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
+    else hipLaunchKernelGGL((k_diag_pc<1, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
 }
 
 int launch_bicg_vec(int mode, KrylovArgs a, hipStream_t st) {
@@ -2080,14 +2050,15 @@ void launch_bicg_scal(int stage, const double* d, double n, double* sc, hipStrea
 int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, const double* vs, double* u, double* v,
                    const double* phi, double* part, hipStream_t st) {
     // (a NEUMANN side's phi ghost reaches two cells inward: the grid kernel's grad_phi)
-    if (cell_streaming() && !(g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3])) {
+    if (cell_streaming() && !g.fc && !(g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3])) {
         CellStreamArgs A{};
         A.g = g; A.c = c; A.dt = dt; A.a0 = phi; A.a1 = us; A.a2 = vs; A.o0 = u; A.o1 = v; A.part = part;
         return launch_cell_s<5>(A, st);
     }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
-    hipLaunchKernelGGL(k_correct, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part, rows);
+    if (g.fc) hipLaunchKernelGGL(k_correct<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part, rows);
+    else hipLaunchKernelGGL(k_correct<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part, rows);
     return (int)(cg.x * cg.y);
 }
 
@@ -2360,8 +2331,9 @@ int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st) {
     hipLaunchKernelGGL(k_sums, cg, dim3(64, 4), 0, st, g, f, part, rows);
     return (int)(cg.x * cg.y);
 }
-void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(k_axpby, cell_grid(g), dim3(64, 4), 0, st, g, a, x, b, y, out);
+void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st,
+                  double c, const double* z) {
+    hipLaunchKernelGGL(k_axpby, cell_grid(g), dim3(64, 4), 0, st, g, a, x, b, y, c, z, out);
 }
 void launch_fill_random(const Geo& g, double* phi, double* rp, uint64_t seed, hipStream_t st) {
     hipLaunchKernelGGL(k_fill_random, cell_grid(g), dim3(64, 4), 0, st, g, phi, rp, seed);

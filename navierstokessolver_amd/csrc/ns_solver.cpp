@@ -117,12 +117,13 @@ struct ns_solver {
     int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
     int tile_small = 1;          // NSGPU_TILE_SMALL=0: no LDS-tiled fused passes on small levels (A/B)
     int helm_split = 1;          // NSGPU_HELM_SPLIT=0: u and v pass by pass (A/B)
-    int phi_extrap = 1;          // NSGPU_PHI_EXTRAP=0: Poisson initial guess phi^{n-1} (A/B)
+    int phi_extrap = 1;          // Poisson initial guess: NSGPU_PHI_EXTRAP=0 phi^{n-1}, 1 linear, 2 quadratic (A/B)
     int mg_predict = 1;          // NSGPU_MG_PREDICT=0: a residual check (host sync) after every V-cycle
     double mg_rate2 = 0.0;       // last measured per-cycle contraction of ||r||^2
     double* phim = nullptr;      // phi^{n-2} (the extrapolation's second point; rotates with PHI / TMP)
-    double* phim_mem = nullptr;  // the extra plane's allocation
-    bool phim_valid = false;
+    double* phim2 = nullptr;     // phi^{n-3} (quadratic extrapolation only)
+    double* phim_mem = nullptr;  // the extra planes' allocation
+    int phim_valid = 0;          // history planes holding data (0 after a reset / an injected phi)
     int verbose = 0;             // NSGPU_VERBOSE=1: solver residual histories on stderr
     long pair_min_cells = 2048L * 2048L;   // NSGPU_PAIR_MIN_CELLS: smallest level smoothed in 2-sweep passes
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
@@ -135,6 +136,8 @@ struct ns_solver {
     double* kv_mem = nullptr;
     double* ksc = nullptr;
     bool pc_active = false;      // inside mg_precond: level 0 has no mean shift, no timing
+    int32_t* fc_mem = nullptr;   // masked domain: topology plane (g.fc) and edge table (g.et)
+    nsg::EdgeDev* et_mem = nullptr;
     ns_host_transport ht{};      // host transport (ht.exchange != NULL) instead of RCCL
     double* stage = nullptr;     // pinned staging for the host transport
     size_t stage_n = 0;
@@ -343,10 +346,34 @@ int next_batch(int prev_batch, double prev_r2, int prev_at, double r2, int at, d
     return std::min(std::max(prev_batch, 2) * 2, cap);
 }
 
+struct KrylovSolve {
+    int op;
+    double alpha;
+    bool mg;
+    double* x;
+    const double* b;
+    const double* shift;
+    double b2;
+    const char* name;
+};
+
+int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res);
+
 // ---------------- Helmholtz (I - a L_V) u* = RHS_u, v* likewise (KSPSolve(uSolver), FluidSolver.cpp:547-548)
 // Initial guess u^n (in place): converged solution is the same; fewer sweeps than the reference's zero guess.
 int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
     const double alpha = s->dt / (2 * s->re);
+    if (s->g.fc) {
+        // masked domain: u then v, each a Jacobi-preconditioned BiCGStab on I - alpha L_V
+        CHK(fetch(s));   // ||RHS_u||^2, ||RHS_v||^2
+        int iu = 0, iv = 0;
+        const KrylovSolve ku{1, alpha, false, s->arr[NS_ARR_U], s->arr[NS_ARR_RU], nullptr, s->hs[S_HBN], "helmholtz u"};
+        CHK(bicgstab(s, ku, &iu, resu));
+        const KrylovSolve kw{1, alpha, false, s->arr[NS_ARR_V], s->arr[NS_ARR_RV], nullptr, s->hs[S_HBN + 1], "helmholtz v"};
+        CHK(bicgstab(s, kw, &iv, resv));
+        *its = std::max(iu, iv);
+        return 0;
+    }
     const double tol2 = s->rtol * s->rtol;
     // first batch: what the previous step needed (consecutive steps converge alike), so a
     // step normally costs one residual check
@@ -776,30 +803,43 @@ int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch) {
     return rc;
 }
 
-int pois_solve_krylov(ns_solver* s, int* its, double* res, ns_stats* stt) {
+// One BiCGStab solve A x = b - shift on this solver's planes (x updated in place).
+//   op 0: the Poisson matrix (NEUMANN outflow rows / a masked domain), solved as
+//         P A x = P (b - shift) with P the mean projection over the domain's cells;
+//   op 1: the Helmholtz matrix I - alpha L_V of a masked domain (regular: no projection).
+// Preconditioner: one wall-closure multigrid V-cycle (mg) or diag(A)^-1 (masked domains,
+// whose operators the rectangle hierarchy does not represent).  b2 = ||b - shift||^2 (host)
+// for the relative test; `name` labels the verbose history.
+int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
     const double tol2 = s->rtol * s->rtol;
-    const int maxit = std::min(s->max_iters, 5000);
+    const int maxit = std::min(s->max_iters, ks.mg ? 5000 : 100000);
     double** K = s->kv;   // r, r0, p, v, s, t, ph, sh, scratch
     nsg::KrylovArgs a{};
     a.g = s->g;
-    a.x = s->arr[NS_ARR_PHI];
+    a.x = ks.x;
     a.r = K[0]; a.r0 = K[1]; a.p = K[2]; a.v = K[3]; a.s = K[4]; a.t = K[5];
-    a.b = s->arr[NS_ARR_RPHI];
-    a.shift = s->scal + S_SHIFT;
+    a.b = ks.b;
+    a.shift = ks.shift;
     a.sc = s->ksc;
     a.part = s->part;
     double* d = s->ksc + nsg::KS_D;
-    const double n = s->ncells;
+    // the projection's cell count (k_bicg_scal: mean = sum / n); infinite = no projection
+    const double n = ks.op == 0 ? s->ncells : INFINITY;
     auto reduce = [&](int nb, int nv) -> int {
         nsg::launch_reduce_sum(s->part, nb, nv, d, s->st);
         return allreduce(s, d, nv, ncclSum);
     };
     auto apply = [&](double* x, double* y, const double* q) -> int {
         CHK(halo(s, {x}, 1));
-        const int nb = nsg::launch_pois_apply(s->g, s->c, x, y, q, s->part, s->st);
+        const int nb = nsg::launch_apply(ks.op, s->g, s->c, ks.alpha, x, y, q, s->part, s->st);
         return reduce(nb, 2);
     };
-    // r = P(b - mean b - A x), r0 = r, p = v = 0 (also the restart after a breakdown)
+    auto precond = [&](double* q, int k) -> int {   // K[k] = M^-1 q
+        if (ks.mg) return mg_precond(s, q, s->kv[k], s->kv[8]);
+        nsg::launch_diag_pc(ks.op, s->g, s->c, ks.alpha, q, s->kv[k], s->st);
+        return 0;
+    };
+    // r = P(b - shift - A x), r0 = r, p = v = 0 (also the restart after a breakdown)
     auto init = [&]() -> int {
         CHK(apply(a.x, a.v, nullptr));
         nsg::launch_bicg_scal(nsg::KSC_MEAN, d, n, s->ksc, s->st);
@@ -808,35 +848,33 @@ int pois_solve_krylov(ns_solver* s, int* its, double* res, ns_stats* stt) {
         return 0;
     };
     CHK(init());
-    int it = 0, nchk = 0, restarts = 0;
+    int it = 0, restarts = 0;
     for (;;) {
-        // ||r||^2 and the breakdown flag to the host: the convergence test (KSPSolve's rtol on
-        // ||b - mean||)
+        // ||r||^2 and the breakdown flag to the host: the convergence test (KSPSolve's rtol)
         HIPCHK(hipMemcpyAsync(s->scal + S_AUX, d, sizeof(double), hipMemcpyDeviceToDevice, s->st));
         HIPCHK(hipMemcpyAsync(s->scal + S_AUX + 1, s->ksc + nsg::KS_BRK, sizeof(double), hipMemcpyDeviceToDevice, s->st));
         if (s->verbose) HIPCHK(hipMemcpyAsync(s->scal + S_AUX + 2, s->ksc + nsg::KS_ALPHA, 2 * sizeof(double), hipMemcpyDeviceToDevice, s->st));
         CHK(fetch(s));
-        nchk++;
-        const double r2 = s->hs[S_AUX], b2 = s->hs[S_SHIFT + 1];
+        const double r2 = s->hs[S_AUX], b2 = ks.b2;
         *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
         if (s->verbose)
-            fprintf(stderr, "nsgpu poisson (bicgstab): it %d rel. residual %.3e (alpha %.3e omega %.3e%s)\n", it, *res,
-                    s->hs[S_AUX + 2], s->hs[S_AUX + 3], s->hs[S_AUX + 1] != 0.0 ? ", breakdown: restart" : "");
-        if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = it; return NS_EDIVERGE; }
+            fprintf(stderr, "nsgpu %s (bicgstab): it %d rel. residual %.3e (alpha %.3e omega %.3e%s)\n", ks.name, it,
+                    *res, s->hs[S_AUX + 2], s->hs[S_AUX + 3], s->hs[S_AUX + 1] != 0.0 ? ", breakdown: restart" : "");
+        if (!std::isfinite(r2)) { set_err("%s residual is not finite", ks.name); *its = it; return NS_EDIVERGE; }
         if (r2 <= tol2 * b2 || r2 == 0.0 || it >= maxit) break;
         if (s->hs[S_AUX + 1] != 0.0) {
-            if (++restarts > 50) { set_err("BiCGStab broke down 50 times"); *its = it; return NS_EDIVERGE; }
+            if (++restarts > 50) { set_err("BiCGStab (%s) broke down 50 times", ks.name); *its = it; return NS_EDIVERGE; }
             CHK(init());
             continue;
         }
         nsg::launch_bicg_scal(nsg::KSC_RHO, d, n, s->ksc, s->st);        // beta, rho
         nsg::launch_bicg_vec(nsg::KV_P, a, s->st);                        // p = r + beta (p - omega v)
-        CHK(mg_precond(s, a.p, s->kv[6], s->kv[8]));                      // ph = M^-1 p
+        CHK(precond(a.p, 6));                                             // ph = M^-1 p
         a.ph = s->kv[6];
         CHK(apply(a.ph, a.v, a.r0));                                      // y = A ph, r0.y
         nsg::launch_bicg_scal(nsg::KSC_ALPHA, d, n, s->ksc, s->st);      // mean y, alpha
         nsg::launch_bicg_vec(nsg::KV_V, a, s->st);                        // v = P y, s = r - alpha v
-        CHK(mg_precond(s, a.s, s->kv[7], s->kv[8]));                      // sh = M^-1 s
+        CHK(precond(a.s, 7));                                             // sh = M^-1 s
         a.sh = s->kv[7];
         CHK(apply(a.sh, a.t, nullptr));                                   // y = A sh
         nsg::launch_bicg_scal(nsg::KSC_MEAN, d, n, s->ksc, s->st);
@@ -846,12 +884,18 @@ int pois_solve_krylov(ns_solver* s, int* its, double* res, ns_stats* stt) {
         it++;
     }
     *its = it;
-    if (stt) stt->n_checks += nchk;
     return 0;
 }
 
 int pois_solve_any(ns_solver* s, int* its, double* res, ns_stats* stt) {
-    if (s->kv[0]) return pois_solve_krylov(s, its, res, stt);
+    if (s->kv[0]) {
+        CHK(fetch(s));   // ||b - mean||^2 for the relative test
+        const KrylovSolve ks{0, 0.0, !s->g.fc, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,
+                             s->hs[S_SHIFT + 1], "poisson"};
+        const int rc = bicgstab(s, ks, its, res);
+        if (stt) stt->n_checks += *its + 1;
+        return rc;
+    }
     if (s->poisson == NS_POISSON_MG) return pois_solve_mg(s, its, res, stt);
     return pois_solve(s, its, res, stt);
 }
@@ -1013,16 +1057,33 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
 // three planes PHI (phi^{n-1}), phim (phi^{n-2}) and TMP rotate: no copies.
 int extrapolate_phi(ns_solver* s) {
     if (!s->phim) return 0;
-    if (!s->phim_valid) {
-        HIPCHK(hipMemcpyAsync(s->phim - (size_t)nsg::HALO * s->g.ld, s->arr[NS_ARR_PHI] - (size_t)nsg::HALO * s->g.ld,
-                              s->plane * sizeof(double), hipMemcpyDeviceToDevice, s->st));
-        s->phim_valid = true;
+    const size_t back = (size_t)nsg::HALO * s->g.ld;
+    if (s->phim_valid == 0) {
+        HIPCHK(hipMemcpyAsync(s->phim - back, s->arr[NS_ARR_PHI] - back, s->plane * sizeof(double),
+                              hipMemcpyDeviceToDevice, s->st));
+        s->phim_valid = 1;
         return 0;
     }
-    nsg::launch_axpby(s->g, 2.0, s->arr[NS_ARR_PHI], -1.0, s->phim, s->arr[NS_ARR_TMP], s->st);
     double* prev = s->arr[NS_ARR_PHI];
+    if (s->phi_extrap >= 2 && s->phim_valid >= 2) {
+        // 3 phi^{n-1} - 3 phi^{n-2} + phi^{n-3}
+        nsg::launch_axpby(s->g, 3.0, prev, -3.0, s->phim, s->arr[NS_ARR_TMP], s->st, 1.0, s->phim2);
+        s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
+        s->arr[NS_ARR_TMP] = s->phim2;
+        s->phim2 = s->phim;
+        s->phim = prev;
+        return 0;
+    }
+    nsg::launch_axpby(s->g, 2.0, prev, -1.0, s->phim, s->arr[NS_ARR_TMP], s->st);
     s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
-    s->arr[NS_ARR_TMP] = s->phim;
+    if (s->phi_extrap >= 2) {
+        // keep phi^{n-2} as the quadratic's third point; the spare plane becomes scratch
+        s->arr[NS_ARR_TMP] = s->phim2;
+        s->phim2 = s->phim;
+        s->phim_valid = 2;
+    } else {
+        s->arr[NS_ARR_TMP] = s->phim;
+    }
     s->phim = prev;
     return 0;
 }
@@ -1117,10 +1178,8 @@ int64_t ns_device_bytes(int32_t nxl, int32_t ny) {
 int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (!gd || !p || !out) { set_err("null argument"); return NS_EINVAL; }
     *out = nullptr;
-    if (gd->cell_id) {
-        set_err("non-rectangular domains (cell_id mask) are not supported by this build");
-        return NS_EINVAL;
-    }
+    const bool masked = gd->cell_id != nullptr;
+    if (masked && !gd->face_edge) { set_err("a cell_id mask needs face_edge (the cells' boundary edges, Grid.h:33)"); return NS_EINVAL; }
     if (gd->nx < 2 || gd->ny < 2) { set_err("one-cell-thick geometry is not supported (FluidSolver.cpp:470-477)"); return NS_EINVAL; }
     if (!gd->hx || !gd->hy) { set_err("hx/hy missing"); return NS_EINVAL; }
     if (!(p->dt > 0)) { set_err("Time step should be positive"); return NS_EINVAL; }
@@ -1147,46 +1206,100 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         set_err("slab of %d rows is thinner than the %d-row halo exchange", g.nxl, 2 * nsg::HALO);
         return NS_EINVAL;
     }
-    // sides from edge normals (a rectangle: Grid.cpp:35-63 gives one edge per side)
-    const int snx[4] = {-1, 1, 0, 0}, sny[4] = {0, 0, -1, 1};
-    int side_edge[4] = {-1, -1, -1, -1};
-    for (int e = 0; e < gd->n_edges; e++) {
+    // ConstructGhostStencils (FluidSolver.cpp:84-103) of one edge
+    auto edge_dev = [&](int e, nsg::EdgeDev* D) -> int {
         const ns_edge& E = gd->edges[e];
-        for (int k = 0; k < 4; k++)
-            if (E.nx == snx[k] && E.ny == sny[k]) {
-                if (side_edge[k] >= 0) { set_err("side %d has more than one edge: not a rectangle", k); return NS_EINVAL; }
-                side_edge[k] = e;
-            }
-    }
-    for (int k = 0; k < 4; k++) {
-        if (side_edge[k] < 0) { set_err("side %d has no edge: not a rectangle", k); return NS_EINVAL; }
-        const ns_edge& E = gd->edges[side_edge[k]];
-        g.enx[k] = E.nx;
-        g.eny[k] = E.ny;
-        g.c0[k] = g.c1[k] = 0.0;
-        g.neu[k] = 0;
-        // ConstructGhostStencils (FluidSolver.cpp:84-103)
+        *D = nsg::EdgeDev{0, E.nx, E.ny, 0.0, 0.0};
         if (E.type == NS_BC_INLET_UNI) {
-            if (E.nx == 0) g.c1[k] = 2 * E.info; else g.c0[k] = 2 * E.info;
+            if (E.nx == 0) D->c1 = 2 * E.info; else D->c0 = 2 * E.info;
         } else if (E.type == NS_BC_WALL) {
-            if (E.nx != 0) g.c1[k] = 2 * E.info; else g.c0[k] = 2 * E.info;
+            if (E.nx != 0) D->c1 = 2 * E.info; else D->c0 = 2 * E.info;
         } else if (E.type == NS_BC_NEUMANN) {
             // outflow: velocity ghost q, phi ghost 2.5 phi_0 - 2 phi_1 + 0.5 phi_2 (:98-101);
-            // the Poisson solve becomes BiCGStab on the true matrix (pois_solve_krylov)
-            g.neu[k] = 1;
-            if ((k < 2 ? gd->nx : gd->ny) < 3) {
-                set_err("a NEUMANN side needs >= 3 cells along its normal (its phi ghost reaches 2 inward)");
-                return NS_EINVAL;
-            }
-            if (p->poisson != NS_POISSON_MG) {
+            // the Poisson solve becomes BiCGStab on the true matrix (pois_solve_any)
+            D->neu = 1;
+            if (!masked && p->poisson != NS_POISSON_MG) {
                 set_err("NEUMANN outflow edges need the multigrid-preconditioned Krylov Poisson solve "
                         "(NS_POISSON_MG): the RB-SOR / Jacobi sweeps cannot relax the outflow rows");
                 return NS_EINVAL;
             }
         } else {
             set_err("edge %d: boundary condition type %d is not supported (INLET_PARABOLIC / PRESSURE / unset "
-                    "have no ghost stencil in the reference)", side_edge[k], E.type);
+                    "have no ghost stencil in the reference)", e, E.type);
             return NS_EINVAL;
+        }
+        return 0;
+    };
+    std::vector<nsg::EdgeDev> etab(nsg::MAX_EDGES + 1, nsg::EdgeDev{0, 0, 0, 0.0, 0.0});  // [31]: interior faces
+    if (masked) {
+        if (gd->n_edges > nsg::MAX_EDGES) { set_err("more than %d polygon edges", nsg::MAX_EDGES); return NS_EINVAL; }
+        for (int e = 0; e < gd->n_edges; e++)
+            if (int rc = edge_dev(e, &etab[e])) return rc;
+    } else {
+        // sides from edge normals (a rectangle: Grid.cpp:35-63 gives one edge per side)
+        const int snx[4] = {-1, 1, 0, 0}, sny[4] = {0, 0, -1, 1};
+        int side_edge[4] = {-1, -1, -1, -1};
+        for (int e = 0; e < gd->n_edges; e++) {
+            const ns_edge& E = gd->edges[e];
+            for (int k = 0; k < 4; k++)
+                if (E.nx == snx[k] && E.ny == sny[k]) {
+                    if (side_edge[k] >= 0) { set_err("side %d has more than one edge: not a rectangle (pass cell_id / face_edge)", k); return NS_EINVAL; }
+                    side_edge[k] = e;
+                }
+        }
+        for (int k = 0; k < 4; k++) {
+            if (side_edge[k] < 0) { set_err("side %d has no edge: not a rectangle", k); return NS_EINVAL; }
+            nsg::EdgeDev D;
+            if (int rc = edge_dev(side_edge[k], &D)) return rc;
+            g.enx[k] = D.enx;
+            g.eny[k] = D.eny;
+            g.c0[k] = D.c0;
+            g.c1[k] = D.c1;
+            g.neu[k] = D.neu;
+            if (D.neu && (k < 2 ? gd->nx : gd->ny) < 3) {
+                set_err("a NEUMANN side needs >= 3 cells along its normal (its phi ghost reaches 2 inward)");
+                return NS_EINVAL;
+            }
+        }
+    }
+
+    // masked domain: the topology plane (this slab's rows and HALO ghost rows on each side)
+    // and the global in-domain cell count
+    std::vector<int32_t> fch;
+    long nin = (long)gd->nx * gd->ny;
+    if (masked) {
+        const int nx = gd->nx, ny = gd->ny;
+        auto inside = [&](int i, int j) { return i >= 0 && i < nx && j >= 0 && j < ny && gd->cell_id[(size_t)i * ny + j] >= 0; };
+        nin = 0;
+        for (size_t c = 0; c < (size_t)nx * ny; c++) nin += gd->cell_id[c] >= 0;
+        if (nin == 0) { set_err("the cell_id mask holds no cell"); return NS_EINVAL; }
+        fch.assign((size_t)(g.nxl + 2 * nsg::HALO) * g.ld, 0);
+        const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
+        for (int li = -nsg::HALO; li < g.nxl + nsg::HALO; li++) {
+            const int i = g.i0 + li;
+            if (i < 0 || i >= nx) continue;
+            for (int j = 0; j < ny; j++) {
+                if (!inside(i, j)) continue;
+                int code = nsg::FC_IN;
+                for (int k = 0; k < 4; k++) {
+                    const int t = gd->face_edge[((size_t)i * ny + j) * 4 + k];
+                    const bool nb = inside(i + di[k], j + dj[k]);
+                    // Grid::inDomain and Cell::edges must agree (the reference mixes both tests)
+                    if (nb == (t >= 0) || t >= gd->n_edges) {
+                        set_err("cell (%d,%d) face %d: edge tag %d disagrees with the domain mask", i, j, k, t);
+                        return NS_EINVAL;
+                    }
+                    code |= (nb ? nsg::FC_INT : t) << (5 * k);
+                    if (!nb && etab[t].neu) {   // the outflow phi ghost's two inward cells
+                        const int a1 = i - etab[t].enx, b1 = j - etab[t].eny;
+                        if (!inside(a1, b1) || !inside(a1 - etab[t].enx, b1 - etab[t].eny)) {
+                            set_err("cell (%d,%d): a NEUMANN face needs two cells inward (FluidSolver.cpp:100)", i, j);
+                            return NS_EINVAL;
+                        }
+                    }
+                }
+                fch[(size_t)(li + nsg::HALO) * g.ld + j] = code;
+            }
         }
     }
 
@@ -1221,7 +1334,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_SPLIT")) s->helm_split = std::atoi(e) != 0;
-    if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = getenv("NSGPU_MG_PREDICT")) s->mg_predict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
@@ -1231,7 +1344,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     }
     s->rank = p->rank;
     s->nranks = p->nranks;
-    s->ncells = (double)gd->nx * (double)gd->ny;
+    s->ncells = (double)nin;
 
     auto fail = [&](int rc) { ns_destroy(s); return rc; };
     int dev = p->device;
@@ -1251,9 +1364,20 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (hipMemsetAsync(s->base, 0, s->plane * NS_NUM_ARR * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     for (int k = 0; k < NS_NUM_ARR; k++) s->arr[k] = s->base + k * s->plane + (size_t)nsg::HALO * g.ld;
     if (s->phi_extrap) {
-        if (hipMalloc(&s->phim_mem, s->plane * sizeof(double)) != hipSuccess) { set_err("hipMalloc phim failed"); return fail(NS_ENOMEM); }
-        if (hipMemsetAsync(s->phim_mem, 0, s->plane * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
+        const size_t np = s->phi_extrap >= 2 ? 2 : 1;
+        if (hipMalloc(&s->phim_mem, np * s->plane * sizeof(double)) != hipSuccess) { set_err("hipMalloc phim failed"); return fail(NS_ENOMEM); }
+        if (hipMemsetAsync(s->phim_mem, 0, np * s->plane * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
         s->phim = s->phim_mem + (size_t)nsg::HALO * g.ld;
+        if (np == 2) s->phim2 = s->phim + s->plane;
+    }
+
+    if (masked) {
+        if (hipMalloc(&s->fc_mem, fch.size() * sizeof(int32_t)) != hipSuccess ||
+            hipMalloc(&s->et_mem, etab.size() * sizeof(nsg::EdgeDev)) != hipSuccess) { set_err("hipMalloc topology failed"); return fail(NS_ENOMEM); }
+        if (hipMemcpy(s->fc_mem, fch.data(), fch.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(s->et_mem, etab.data(), etab.size() * sizeof(nsg::EdgeDev), hipMemcpyHostToDevice) != hipSuccess) { set_err("topology upload failed"); return fail(NS_EHIP); }
+        s->g.fc = s->fc_mem + (size_t)nsg::HALO * g.ld;
+        s->g.et = s->et_mem;
     }
 
     // coefficient tables (ConstructLHS, FluidSolver.cpp:113-131)
@@ -1268,7 +1392,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (hipMemcpy(s->coef, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) { set_err("coef upload failed"); return fail(NS_EHIP); }
         s->c = coef_view(s->coef, g.nx, g.ny);
     }
-    if (s->poisson == NS_POISSON_MG) {
+    if (s->poisson == NS_POISSON_MG && !masked) {
         if (p->mg_pre > 0) s->mg_pre = p->mg_pre;
         if (p->mg_omega > 0) s->mg_omega_s = p->mg_omega;
         if (const char* e = getenv("NSGPU_MG_OMEGA")) s->mg_omega_s = std::atof(e);   // smoother over-relaxation (A/B)
@@ -1277,9 +1401,9 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (p->mg_coarse_iters > 0) s->mg_coarse_iters = p->mg_coarse_iters;
         if (s->lv.size() < 2) s->poisson = NS_POISSON_RBSOR;  // nothing to coarsen: plain RB-SOR
     }
-    if (g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3]) {
-        // BiCGStab planes (the preconditioner is the hierarchy above; with a single level its
-        // coarse relaxation -- 2n+10 SOR sweeps from zero -- is the preconditioner)
+    if (masked || g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3]) {
+        // BiCGStab planes (outflow rectangle: the preconditioner is the hierarchy above -- with a
+        // single level its coarse relaxation, 2n+10 SOR sweeps from zero; masked domain: Jacobi)
         const size_t nk = sizeof(s->kv) / sizeof(s->kv[0]);
         if (hipMalloc(&s->kv_mem, nk * s->plane * sizeof(double)) != hipSuccess) { set_err("hipMalloc Krylov planes failed"); return fail(NS_ENOMEM); }
         if (hipMemsetAsync(s->kv_mem, 0, nk * s->plane * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
@@ -1319,6 +1443,8 @@ void ns_destroy(ns_solver* s) {
     if (s->base) (void)hipFree(s->base);
     if (s->phim_mem) (void)hipFree(s->phim_mem);
     if (s->kv_mem) (void)hipFree(s->kv_mem);
+    if (s->fc_mem) (void)hipFree(s->fc_mem);
+    if (s->et_mem) (void)hipFree(s->et_mem);
     if (s->ksc) (void)hipFree(s->ksc);
     if (s->coef) (void)hipFree(s->coef);
     if (s->part) (void)hipFree(s->part);
@@ -1384,7 +1510,7 @@ int ns_set_array(ns_solver* s, int which, const double* host) {
                             s->g.nxl, hipMemcpyHostToDevice, s->st));
     // keep the derived scalars consistent with an injected right-hand side
     if (which == NS_ARR_RPHI) CHK(rhs_mean(s));
-    if (which == NS_ARR_PHI || which == NS_ARR_TMP) s->phim_valid = false;
+    if (which == NS_ARR_PHI || which == NS_ARR_TMP) s->phim_valid = 0;
     if (which == NS_ARR_RU || which == NS_ARR_RV) CHK(helm_bnorm(s));
     HIPCHK(hipStreamSynchronize(s->st));
     return 0;
@@ -1420,6 +1546,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         if (out) { out[0] = s->hs[S_HBN]; out[1] = s->hs[S_HBN + 1]; }
         return 0;
     case NS_K_HELMHOLTZ: {
+        if (s->g.fc) { set_err("NS_K_HELMHOLTZ sweeps are rectangle-only; use NS_K_HELM_SOLVE on a masked domain"); return NS_EINVAL; }
         // (iters-1)/2 two-sweep passes, then single sweeps; the residual is of the last sweep's input
         int nb = 0;
         CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
@@ -1449,7 +1576,8 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         return 0;
     case NS_K_POISSON: {
         if (s->kv[0]) {
-            set_err("NS_K_POISSON sweeps relax the wall-closure operator; with a NEUMANN side use NS_K_POIS_SOLVE");
+            set_err("NS_K_POISSON sweeps relax the rectangle's wall-closure operator; with a NEUMANN side or a "
+                    "masked domain use NS_K_POIS_SOLVE");
             return NS_EINVAL;
         }
         int nb = 0;
@@ -1500,7 +1628,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
     }
     case NS_K_RESIDUAL: {
         if (s->kv[0]) {
-            set_err("NS_K_RESIDUAL is the wall-closure residual; not defined with a NEUMANN side");
+            set_err("NS_K_RESIDUAL is the rectangle's wall-closure residual; not defined with a NEUMANN side or a mask");
             return NS_EINVAL;
         }
         CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
@@ -1551,6 +1679,7 @@ int ns_mg_transfer(ns_solver* s, int op, double* coarse) {
 
 int ns_fill_random(ns_solver* s, uint64_t seed) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
+    if (s->g.fc) { set_err("ns_fill_random (the sweep benchmark input) is rectangle-only"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
     nsg::launch_fill_random(s->g, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], seed, s->st);
     CHK(rhs_mean(s));  // the random rhs's mean becomes the Poisson shift (null-space removal)
@@ -1561,6 +1690,7 @@ int ns_fill_random(ns_solver* s, uint64_t seed) {
 
 int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
     if (!s || iters <= 0) { set_err("bad arguments"); return NS_EINVAL; }
+    if (s->kv[0]) { set_err("ns_time_poisson times the rectangle's sweeps (no NEUMANN side, no mask)"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
     CHK(ensure_events(s, 2 * (size_t)iters));
     // NSGPU_TIME_PAIRS=1: time the two-sweep (temporally blocked) pass instead of a single sweep

@@ -159,6 +159,7 @@ FluidSolver::FluidSolver(char* fname, Grid* g) : grid(g) {
     gd.n_edges = (int32_t)m.edges.size();
     gd.edges = m.edges.data();
     gd.cell_id = grid->isRectangle() ? nullptr : grid->cellIds().data();
+    gd.face_edge = grid->isRectangle() ? nullptr : grid->faceEdges().data();
     ns_params pr{};
     pr.dt = m.p.dt;
     pr.re = m.p.re;
@@ -195,6 +196,7 @@ void write_flow_csv(int iter, Grid& g, double dt, double re, const vector<double
     const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
     for (int i = 0; i < nx; i++)
         for (int j = 0; j < ny; j++) {
+            if (!g.inDomain(i, j)) continue;   // a polygon's bounding-box cells outside the domain
             const size_t c = id(i, j);
             double lap = 0.0, dg = 0.0;
             for (int k = 0; k < 4; k++) {

@@ -22,10 +22,22 @@ class Edge:
 
 @dataclass
 class GridSpec:
-    """Geometry handed to ns_create: spacings plus edges (a rectangle)."""
+    """Geometry handed to ns_create: spacings plus edges.  A rectangle leaves cell_id /
+    face_edge None; any other polygon (cavity.polygon) carries the bounding box's
+    compact ids (-1 outside; Grid.cpp:149-162) and per-cell boundary-edge tags (W,E,S,N;
+    Cell::edges, Grid.h:33)."""
     hx: np.ndarray
     hy: np.ndarray
     edges: list = field(default_factory=list)
+    cell_id: np.ndarray | None = None
+    face_edge: np.ndarray | None = None
+
+    @property
+    def mask(self):
+        """nx x ny booleans: the cells inside the domain (all of them for a rectangle)."""
+        if self.cell_id is None:
+            return np.ones((self.nx, self.ny), dtype=bool)
+        return np.asarray(self.cell_id).reshape(self.nx, self.ny) >= 0
 
     @property
     def nx(self):
@@ -51,8 +63,15 @@ class GpuSolver:
         self.hx = np.ascontiguousarray(grid.hx, dtype=np.float64)
         self.hy = np.ascontiguousarray(grid.hy, dtype=np.float64)
         self._edges = (L.NsEdge * len(grid.edges))(*[L.NsEdge(e.nx, e.ny, e.type, e.info) for e in grid.edges])
+        ip = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        self._cid = self._ftag = None
+        if grid.cell_id is not None:
+            self._cid = np.ascontiguousarray(grid.cell_id, dtype=np.int32)
+            self._ftag = np.ascontiguousarray(grid.face_edge, dtype=np.int32)
+            assert self._cid.size == self.hx.size * self.hy.size and self._ftag.size == 4 * self._cid.size
         desc = L.NsGridDesc(self.hx.size, self.hy.size, _dptr(self.hx), _dptr(self.hy), len(grid.edges),
-                            self._edges, None)
+                            self._edges, ip(self._cid) if self._cid is not None else None,
+                            ip(self._ftag) if self._ftag is not None else None)
         self._nccl = ctypes.create_string_buffer(nccl_id, len(nccl_id)) if nccl_id else None
         prm = L.NsParams(dt, re, poisson, rtol, max_iters, omega, omega_v, check_every, device,
                          1 if timing else 0, rank, nranks,

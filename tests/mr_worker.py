@@ -23,6 +23,7 @@ ap.add_argument("--solver", type=int, default=nsa.NS_POISSON_MG)
 ap.add_argument("--tol", type=float, default=1e-10)
 ap.add_argument("--output", required=True)
 ap.add_argument("--bc", default="", help="edge BCs W,N,E,S as type:info,... (default: the cavity)")
+ap.add_argument("--poly", default="", help="a tests/polygons.py geometry instead of the rectangle")
 ap.add_argument("--stats-only", action="store_true", help="gather only the per-step stats (large grids)")
 a = ap.parse_args()
 dist.init_process_group("gloo")
@@ -36,7 +37,17 @@ else:
 status = "ok"
 try:
     bc = [(int(t), float(i)) for t, i in (e.split(":") for e in a.bc.split(","))] if a.bc else None
-    gs = nsa.GpuSolver(nsa.rectangle(n, ny, bc=bc), 1.0 / (8 * n), 100.0, **kw)
+    if a.poly:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle import OGrid   # the geometry's spacings (a test helper, not the solve)
+        from polygons import ALL
+        P = ALL[a.poly]
+        og = OGrid(P["vertices"], P["xspec"], P["yspec"], P["bc"])
+        n, ny = og.nx, og.ny
+        grid = nsa.polygon(P["vertices"], og.hx, og.hy, P["bc"])
+    else:
+        grid = nsa.rectangle(n, ny, bc=bc)
+    gs = nsa.GpuSolver(grid, 1.0 / (8 * n), 100.0, **kw)
     mm = [list(gs.step().values())[:7] for _ in range(a.nsteps)]
     u, v, phi = (np.zeros((1, ny)),) * 3 if a.stats_only else gs.fields()
 except Exception as e:  # report, don't hang the other rank

@@ -19,7 +19,7 @@ def test_library_exports_every_header_symbol():
     for n in names:
         assert hasattr(lib, n), f"libnsgpu.so does not export {n}"
     assert set(names) == set(L.SIGNATURES), "ctypes signatures out of sync with include/nsgpu.h"
-    assert lib.ns_abi_version() == 1
+    assert lib.ns_abi_version() == 2
 
 
 def test_lib_is_gfx950_code_object():
@@ -35,9 +35,9 @@ def _c_sizes():
 #include <stddef.h>
 #include "nsgpu.h"
 int main(void){
- printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(ns_edge), sizeof(ns_grid_desc), sizeof(ns_params),
+ printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(ns_edge), sizeof(ns_grid_desc), sizeof(ns_params),
         sizeof(ns_stats), offsetof(ns_params, nccl_id), offsetof(ns_stats, t_poisson_kernel_ms),
-        offsetof(ns_grid_desc, cell_id));
+        offsetof(ns_grid_desc, cell_id), offsetof(ns_grid_desc, face_edge));
  return 0;}
 '''
     exe = "/tmp/ns_abi_sizes"
@@ -50,7 +50,7 @@ def test_ctypes_struct_layout_matches_c():
     c = _c_sizes()
     py = [ctypes.sizeof(L.NsEdge), ctypes.sizeof(L.NsGridDesc), ctypes.sizeof(L.NsParams),
           ctypes.sizeof(L.NsStats), L.NsParams.nccl_id.offset, L.NsStats.t_poisson_kernel_ms.offset,
-          L.NsGridDesc.cell_id.offset]
+          L.NsGridDesc.cell_id.offset, L.NsGridDesc.face_edge.offset]
     assert c == py
 
 

@@ -1,0 +1,127 @@
+"""Non-rectangular domains on the GPU (cell_id / face_edge masks):
+every kernel of the step and the full step against the oracle, which restates the
+reference's general polygon code (Grid.cpp:131-185, FluidSolver.cpp with inDomain /
+Cell::edges tests).  GPU fields are bounding-box planes (zero outside the domain); the
+oracle's are compact vectors in the reference's id order -- plane.ravel()[mask].
+
+Tolerances (per test): single kernels 1e-12 relative; converged solves 1e-8 (phi modulo
+its mean); full steps at the reference's rtol 1e-8: max|du|, max|dv| <= 1e-6."""
+import numpy as np
+import pytest
+
+from oracle import OGrid, OSolver
+from polygons import ALL
+
+pytestmark = pytest.mark.gpu
+
+
+def pair(gpu, name, dt, re, **kw):
+    P = ALL[name]
+    og = OGrid(P["vertices"], P["xspec"], P["yspec"], P["bc"])
+    gs = gpu.GpuSolver(gpu.polygon(P["vertices"], og.hx, og.hy, P["bc"]), dt, re, **kw)
+    return og, gs, gs.grid.mask.ravel()
+
+
+def plane(m, x):
+    p = np.zeros(m.size)
+    p[m] = x
+    return p
+
+
+def rel(a, b):
+    return float(np.max(np.abs(np.asarray(a).ravel() - np.asarray(b).ravel())) / max(np.max(np.abs(b)), 1e-300))
+
+
+@pytest.mark.parametrize("name", sorted(ALL))
+def test_mask_k1_rhs_velocity(gpu, name):
+    rng = np.random.default_rng(21)
+    dt, re = 1e-3, 250.0
+    og, gs, m = pair(gpu, name, dt, re)
+    u, v, phi, cu, cv = (rng.uniform(-1, 1, og.N) for _ in range(5))
+    for a, x in ((gpu.NS_ARR_U, u), (gpu.NS_ARR_V, v), (gpu.NS_ARR_PHI, phi), (gpu.NS_ARR_CU, cu),
+                 (gpu.NS_ARR_CV, cv)):
+        gs.set(a, plane(m, x))
+    sums = gs.kernel(gpu.NS_K_RHS)
+    gx, gy = og.grad_phi(phi)
+    ru, rv, cu1, cv1 = og.rhs_velocity(dt, re, u, v, gx, gy, cu, cv)
+    for a, ref in ((gpu.NS_ARR_RU, ru), (gpu.NS_ARR_RV, rv), (gpu.NS_ARR_CU, cu1), (gpu.NS_ARR_CV, cv1)):
+        got = gs.get(a).ravel()
+        err = rel(got[m], ref)
+        assert err <= 1e-12, (a, err)
+        assert not np.any(got[~m]), "cells outside the domain must stay 0"
+    assert abs(sums[0] - np.sum(ru * ru)) <= 1e-11 * np.sum(ru * ru)
+
+
+@pytest.mark.parametrize("name", sorted(ALL))
+def test_mask_k3_k5(gpu, name):
+    rng = np.random.default_rng(22)
+    dt = 1.0 / 512
+    og, gs, m = pair(gpu, name, dt, 100.0)
+    us, vs, phi = (rng.uniform(-1, 1, og.N) for _ in range(3))
+    gs.set(gpu.NS_ARR_U, plane(m, us)); gs.set(gpu.NS_ARR_V, plane(m, vs))
+    sums = gs.kernel(gpu.NS_K_DIV)
+    ref = og.divergence(dt, us, vs)
+    err = rel(gs.get(gpu.NS_ARR_RPHI).ravel()[m], ref)
+    assert err <= 1e-12, err
+    assert abs(sums[0] - ref.sum()) <= 1e-9 * np.abs(ref).sum()
+    gs.set(gpu.NS_ARR_PHI, plane(m, phi))
+    mm = gs.kernel(gpu.NS_K_CORRECT)
+    u, v, _, _ = og.correct(dt, us, vs, phi)
+    eu, ev = rel(gs.get(gpu.NS_ARR_U).ravel()[m], u), rel(gs.get(gpu.NS_ARR_V).ravel()[m], v)
+    assert eu <= 1e-12 and ev <= 1e-12, (eu, ev)
+    np.testing.assert_allclose(mm[:4], [u.min(), u.max(), v.min(), v.max()], rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("name", sorted(ALL))
+def test_mask_converged_solves(gpu, name):
+    """Jacobi-preconditioned BiCGStab (Helmholtz u; Poisson with the mean projection) against
+    the oracle's converged solves."""
+    rng = np.random.default_rng(23)
+    dt, re = 1.0 / 128, 50.0
+    og, gs, m = pair(gpu, name, dt, re, rtol=1e-12)
+    alpha = dt / (2 * re)
+    ru, rv = rng.uniform(-1, 1, og.N), rng.uniform(-1, 1, og.N)
+    gs.set(gpu.NS_ARR_U, np.zeros(m.size)); gs.set(gpu.NS_ARR_V, np.zeros(m.size))
+    gs.set(gpu.NS_ARR_RU, plane(m, ru)); gs.set(gpu.NS_ARR_RV, plane(m, rv))
+    its, res = gs.kernel(gpu.NS_K_HELM_SOLVE)[:2]
+    assert res <= 1e-12 and its > 0
+    xu, _ = og.solve_helmholtz(alpha, ru)
+    err = rel(gs.get(gpu.NS_ARR_U).ravel()[m], xu)
+    assert err <= 1e-9, err
+    b = rng.uniform(-100, 100, og.N)
+    gs.set(gpu.NS_ARR_PHI, np.zeros(m.size)); gs.set(gpu.NS_ARR_RPHI, plane(m, b))
+    its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+    assert res <= 1e-12, (its, res)
+    xp, _ = og.solve_poisson(b)
+    g = gs.get(gpu.NS_ARR_PHI).ravel()[m]
+    err = rel(g - g.mean(), xp - xp.mean())
+    assert err <= 1e-8, (err, its)
+
+
+@pytest.mark.parametrize("name,steps,re", [("step", 15, 100.0), ("lshape", 12, 400.0), ("split", 10, 100.0),
+                                           ("uchannel", 10, 100.0)])
+def test_mask_full_steps_vs_oracle(gpu, name, steps, re):
+    P = ALL[name]
+    n = max(P["xspec"][-1][2], P["yspec"][-1][2])
+    dt = 1.0 / (16 * n)
+    og, gs, m = pair(gpu, name, dt, re)
+    osv = OSolver(og, dt, re, rtol=1e-13)
+    for _ in range(steps):
+        st = gs.step()
+        mm, _ = osv.step()
+        np.testing.assert_allclose([st["umin"], st["umax"], st["vmin"], st["vmax"]], mm, atol=1e-6)
+    ref = osv.get()
+    u, v, phi = (a.ravel() for a in gs.fields())
+    du, dv = float(np.max(np.abs(u[m] - ref["u"]))), float(np.max(np.abs(v[m] - ref["v"])))
+    assert du <= 1e-6 and dv <= 1e-6, (du, dv)
+    assert not np.any(u[~m]) and not np.any(v[~m])
+    p, q = phi[m] - phi[m].mean(), ref["phi"] - ref["phi"].mean()
+    ep = float(np.linalg.norm(p - q) / np.linalg.norm(q))
+    assert ep <= 1e-5, ep
+
+
+def test_mask_rectangle_only_entry_points_fail_loudly(gpu):
+    og, gs, m = pair(gpu, "lshape", 1e-3, 100.0)
+    for k in (gpu.NS_K_HELMHOLTZ, gpu.NS_K_POISSON, gpu.NS_K_RESIDUAL):
+        with pytest.raises(gpu.NsError):
+            gs.kernel(k, 1)

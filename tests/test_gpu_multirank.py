@@ -92,6 +92,27 @@ def test_neumann_outflow_slabs_match_single_rank(tmp_path, bc, nproc):
     np.testing.assert_allclose(r["mm"][:, :4], mm[:, :4], atol=1e-8)
 
 
+@pytest.mark.parametrize("poly,nproc", [("step", 2), ("uchannel", 3)])
+def test_masked_domain_slabs_match_single_rank(tmp_path, poly, nproc):
+    """Non-rectangular domain on x-slabs: the topology plane carries its ghost rows from the
+    global mask, the Krylov solves all-reduce every dot product."""
+    from oracle import OGrid
+    from polygons import ALL
+    P = ALL[poly]
+    og = OGrid(P["vertices"], P["xspec"], P["yspec"], P["bc"])
+    steps, rtol = 5, 1e-11
+    r = launch(tmp_path, "--xport", "host", "--poly", poly, "--nsteps", str(steps), "--tol", str(rtol),
+               nproc=nproc, port=29591 + nproc)
+    assert str(r["status"]) == "ok", r["status"]
+    gs = nsa.GpuSolver(nsa.polygon(P["vertices"], og.hx, og.hy, P["bc"]), 1.0 / (8 * og.nx), 100.0, rtol=rtol,
+                       device=0)
+    mm = np.array([list(gs.step().values())[:7] for _ in range(steps)])
+    u, v, _ = gs.fields()
+    du, dv = float(np.max(np.abs(r["u"] - u))), float(np.max(np.abs(r["v"] - v)))
+    assert du <= 1e-8 and dv <= 1e-8, (du, dv)
+    np.testing.assert_allclose(r["mm"][:, :4], mm[:, :4], atol=1e-8)
+
+
 def test_rccl_two_ranks_one_gpu_probe(tmp_path):
     """RCCL usually rejects two ranks on one device; record what it does (never fails the suite
     unless RCCL ran and produced a wrong answer)."""
