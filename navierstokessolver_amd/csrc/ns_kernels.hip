@@ -1931,6 +1931,156 @@ __global__ __launch_bounds__(256) void k_axpby(Geo g, double a, const double* __
     out[o] = r;
 }
 
+// ------------------------------------------------ NEUMANN outflow: BiCGStab pieces
+// With an outflow side the Poisson matrix is no longer the wall-closure L the smoothers
+// relax: AddGhostStencils (FluidSolver.cpp:147-163) adds, per outflow face, w (ghost_p - x_c)
+// with w = 1/h^2 (:124-127) and the ghost 2.5 x_c - 2 x_1 + 0.5 x_2 (:98-101) -- a row that
+// reaches two cells inward and is not diagonally dominant.  The solver then runs BiCGStab on
+// the true operator (the reference's KSPBCGSL, :73-82), right-preconditioned by one V-cycle
+// of the wall-closure multigrid (ns_solver.cpp pois_solve_krylov).
+//
+// y = A x over own cells; block partials (sum y, sum q*y) (q may be null).
+// OP 0: the Poisson matrix LHS_phi (ConstructLHS + AddGhostStencils, :105-163);
+// OP 1: the Helmholtz matrix (I - alpha L_V) (:140-141) with L_V's boundary faces
+//       w (wself q_c - q_c), wself = 1 (NEUMANN) / -1 (walls, inlets; ghost[0].weights, :87-99).
+template <int OP, class T>
+__global__ __launch_bounds__(256) void k_apply(Geo g, Coef c, double alpha, const double* __restrict__ x,
+                                               double* __restrict__ y, const double* __restrict__ q,
+                                               double* __restrict__ part, int rows) {
+    const int j = blockIdx.x * 64 + threadIdx.x;
+    const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
+    double acc[2] = {0.0, 0.0};
+    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
+        const T t(g, li, j);
+        const int gi = g.i0 + li, ld = g.ld;
+        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+        if (!t.cell()) { y[o] = 0.0; continue; }
+        const double xc = x[o], hx = c.hx[gi], hy = c.hy[j];
+        const double w2[4] = {1.0 / (hx * hx), 1.0 / (hx * hx), 1.0 / (hy * hy), 1.0 / (hy * hy)};
+        const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
+        const double pn[4] = {c.pw[gi], c.pe[gi], c.ps[j], c.pn[j]};
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (t.in(di[k], dj[k])) {
+                s += pn[k] * (x[o + di[k] * ld + dj[k]] - xc);
+            } else {
+                const EdgeDev E = t.edge(k);
+                if (OP == 0) s += E.neu ? (ghost_p_e(g, E, x, li, j, xc) - xc) * w2[k] : 0.0;
+                else s += E.neu ? 0.0 : -2.0 * xc * w2[k];
+            }
+        }
+        const double val = OP == 0 ? s : xc - alpha * s;
+        y[o] = val;
+        acc[0] += val;
+        if (q) acc[1] += q[o] * val;
+    }
+    block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
+}
+
+// z = q / diag(A) (the Jacobi preconditioner of the masked-domain Krylov solves; the
+// outflow rows' diagonal -(sum p) + 1.5 w, oracle diag_poisson / diag_helmholtz)
+template <int OP, class T>
+__global__ __launch_bounds__(256) void k_diag_pc(Geo g, Coef c, double alpha, const double* __restrict__ qv,
+                                                 double* __restrict__ z) {
+    const int j = blockIdx.x * 64 + threadIdx.x;
+    const int li = blockIdx.y * 4 + threadIdx.y;
+    if (j >= g.ny || li >= g.nxl) return;
+    const T t(g, li, j);
+    const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
+    if (!t.cell()) { z[o] = 0.0; return; }
+    const int gi = g.i0 + li;
+    const double hx = c.hx[gi], hy = c.hy[j];
+    const double w2[4] = {1.0 / (hx * hx), 1.0 / (hx * hx), 1.0 / (hy * hy), 1.0 / (hy * hy)};
+    const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
+    const double pn[4] = {c.pw[gi], c.pe[gi], c.ps[j], c.pn[j]};
+    double d = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (t.in(di[k], dj[k])) d -= pn[k];
+        else if (OP == 0) d += t.edge(k).neu ? 1.5 * w2[k] : 0.0;
+        else d -= t.edge(k).neu ? 0.0 : 2.0 * w2[k];
+    }
+    if (OP == 1) d = 1.0 - alpha * d;
+    z[o] = d != 0.0 ? qv[o] / d : qv[o];
+}
+
+// BiCGStab vector updates; coefficients from the device scalars k_bicg_scal leaves in sc,
+// each fused with the dot products the next scalar stage needs (block partials, 3 per block):
+//   KV_INIT: r = (b - shift) - (y - mean_y), r0 = r, p = v = 0     partials (r.r, r0.r, sum r)
+//   KV_P:    p = r + beta (p - omega v)
+//   KV_V:    v = y - mean_y (in place), s = r - alpha v
+//   KV_T:    t = y - mean_y (in place)                             partials (t.s, t.t, -)
+//   KV_X:    x += alpha ph + omega sh, r = s - omega t             partials (r.r, r0.r, sum r)
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_bicg_vec(KrylovArgs a) {
+    const Geo& g = a.g;
+    const int j = blockIdx.x * 64 + threadIdx.x;
+    const int lend = min((int)(blockIdx.y + 1) * 4 * a.rows, g.nxl);
+    double acc[3] = {0.0, 0.0, 0.0};
+    const double alpha = a.sc[KS_ALPHA], beta = a.sc[KS_BETA], omega = a.sc[KS_OMEGA], my = a.sc[KS_MEAN];
+    const double shift = a.shift ? a.shift[0] : 0.0;
+    for (int li = blockIdx.y * 4 * a.rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
+        const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
+        if (g.fc && !(g.fc[o] & FC_IN)) continue;   // outside a masked domain: every vector stays 0
+        if (MODE == KV_INIT) {
+            const double r = (a.b[o] - shift) - (a.v[o] - my);
+            a.r[o] = r; a.r0[o] = r; a.p[o] = 0.0; a.v[o] = 0.0;
+            acc[0] += r * r; acc[1] += r * r; acc[2] += r;
+        } else if (MODE == KV_P) {
+            a.p[o] = a.r[o] + beta * (a.p[o] - omega * a.v[o]);
+        } else if (MODE == KV_V) {
+            const double v = a.v[o] - my;
+            a.v[o] = v;
+            a.s[o] = a.r[o] - alpha * v;
+        } else if (MODE == KV_T) {
+            const double t = a.t[o] - my;
+            a.t[o] = t;
+            acc[0] += t * a.s[o]; acc[1] += t * t;
+        } else {
+            a.x[o] += alpha * a.ph[o] + omega * a.sh[o];
+            const double r = a.s[o] - omega * a.t[o];
+            a.r[o] = r;
+            acc[0] += r * r; acc[1] += a.r0[o] * r; acc[2] += r;
+        }
+    }
+    if (MODE == KV_INIT || MODE == KV_T || MODE == KV_X)
+        block_reduce_sum<3>(acc, a.part + 3 * (blockIdx.x + gridDim.x * blockIdx.y));
+}
+
+// the scalar recurrences of BiCGStab on one thread; d = the stage's reduced sums
+//   KSC_RHO  (d = r.r, r0.r, sum r):   beta = (rho1/rho)(alpha/omega), rho = rho1
+//   KSC_ALPHA (d = sum y, r0.y):       mean_y, alpha = rho / (r0.y - mean_y sum r0)
+//   KSC_MEAN  (d = sum y):             mean_y
+//   KSC_OMEGA (d = t.s, t.t):          omega = t.s / t.t
+__global__ void k_bicg_scal(int stage, const double* __restrict__ d, double n, double* __restrict__ sc) {
+    // a breakdown (a zero or non-finite denominator) zeroes the coefficient -- the vector
+    // updates then leave x untouched -- and raises KS_BRK; the host restarts from x
+    auto guard = [&](double v) {
+        if (!isfinite(v)) { sc[KS_BRK] = 1.0; return 0.0; }
+        return v;
+    };
+    if (stage == KSC_INIT) {
+        sc[KS_RHO] = 1.0; sc[KS_ALPHA] = 1.0; sc[KS_OMEGA] = 1.0; sc[KS_SUMR0] = d[2]; sc[KS_BRK] = 0.0;
+    } else if (stage == KSC_RHO) {
+        const double rho1 = d[1];
+        sc[KS_BETA] = guard((rho1 / sc[KS_RHO]) * (sc[KS_ALPHA] / sc[KS_OMEGA]));
+        if (rho1 == 0.0) sc[KS_BRK] = 1.0;
+        sc[KS_RHO] = rho1;
+    } else if (stage == KSC_ALPHA) {
+        const double m = d[0] / n;
+        sc[KS_MEAN] = m;
+        sc[KS_ALPHA] = guard(sc[KS_RHO] / (d[1] - m * sc[KS_SUMR0]));
+    } else if (stage == KSC_MEAN) {
+        sc[KS_MEAN] = d[0] / n;
+    } else {
+        const double om = d[1] > 0.0 ? d[0] / d[1] : 0.0;
+        sc[KS_OMEGA] = guard(om);
+        if (om == 0.0) sc[KS_BRK] = 1.0;
+    }
+}
+
 // ---------------------------------------------------------------- launchers
 static inline dim3 cell_grid(const Geo& g) { return dim3((g.ny + 63) / 64, (g.nxl + 3) / 4); }
 

@@ -117,11 +117,15 @@ struct ns_solver {
     int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
     int tile_small = 1;          // NSGPU_TILE_SMALL=0: no LDS-tiled fused passes on small levels (A/B)
     int helm_split = 1;          // NSGPU_HELM_SPLIT=0: u and v pass by pass (A/B)
-    int phi_extrap = 1;          // Poisson initial guess: NSGPU_PHI_EXTRAP=0 phi^{n-1}, 1 linear, 2 quadratic (A/B)
+    int phi_extrap = 2;          // Poisson initial guess: NSGPU_PHI_EXTRAP=0 phi^{n-1}, 1 linear, 2 quadratic (default)
     int mg_predict = 1;          // NSGPU_MG_PREDICT=0: a residual check (host sync) after every V-cycle
     double mg_rate2 = 0.0;       // last measured per-cycle contraction of ||r||^2
     double* phim = nullptr;      // phi^{n-2} (the extrapolation's second point; rotates with PHI / TMP)
     double* phim2 = nullptr;     // phi^{n-3} (quadratic extrapolation only)
+    // NSGPU_HELM_EXTRAP=1 (A/B): Helmholtz initial guess 2 u*^n - u*^{n-1} instead of u^n
+    int helm_extrap = 0;
+    double *usm = nullptr, *vsm = nullptr, *usm_mem = nullptr;   // u*^{n-1}, v*^{n-1}
+    int us_valid = 0;            // 0: no u* kept; 1: TMPU/TMPV hold u*^n; 2: and usm/vsm u*^{n-1}
     double* phim_mem = nullptr;  // the extra planes' allocation
     int phim_valid = 0;          // history planes holding data (0 after a reset / an injected phi)
     int verbose = 0;             // NSGPU_VERBOSE=1: solver residual histories on stderr
@@ -1088,6 +1092,20 @@ int extrapolate_phi(ns_solver* s) {
     return 0;
 }
 
+// Helmholtz initial guess (NSGPU_HELM_EXTRAP=1): the linear extrapolation 2 u*^n - u*^{n-1} of the
+// previous steps' Helmholtz solutions into U (u^n is no longer needed once K1 has run).  u*^n
+// sits in TMPU / TMPV (correct() leaves it there); the planes rotate, no copies.
+int helm_guess(ns_solver* s) {
+    if (!s->helm_extrap || s->us_valid == 0) return 0;
+    if (s->us_valid >= 2) {
+        nsg::launch_axpby(s->g, 2.0, s->arr[NS_ARR_TMPU], -1.0, s->usm, s->arr[NS_ARR_U], s->st);
+        nsg::launch_axpby(s->g, 2.0, s->arr[NS_ARR_TMPV], -1.0, s->vsm, s->arr[NS_ARR_V], s->st);
+    }
+    std::swap(s->usm, s->arr[NS_ARR_TMPU]);
+    std::swap(s->vsm, s->arr[NS_ARR_TMPV]);
+    return 0;
+}
+
 // K3 + null-space mean
 int divergence(ns_solver* s) {
     const int nb = nsg::launch_div(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_RPHI],
@@ -1334,6 +1352,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_SPLIT")) s->helm_split = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_HELM_EXTRAP")) s->helm_extrap = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = getenv("NSGPU_MG_PREDICT")) s->mg_predict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
@@ -1371,6 +1390,12 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (np == 2) s->phim2 = s->phim + s->plane;
     }
 
+    if (s->helm_extrap) {
+        if (hipMalloc(&s->usm_mem, 2 * s->plane * sizeof(double)) != hipSuccess) { set_err("hipMalloc u* history failed"); return fail(NS_ENOMEM); }
+        if (hipMemsetAsync(s->usm_mem, 0, 2 * s->plane * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
+        s->usm = s->usm_mem + (size_t)nsg::HALO * g.ld;
+        s->vsm = s->usm + s->plane;
+    }
     if (masked) {
         if (hipMalloc(&s->fc_mem, fch.size() * sizeof(int32_t)) != hipSuccess ||
             hipMalloc(&s->et_mem, etab.size() * sizeof(nsg::EdgeDev)) != hipSuccess) { set_err("hipMalloc topology failed"); return fail(NS_ENOMEM); }
@@ -1443,6 +1468,7 @@ void ns_destroy(ns_solver* s) {
     if (s->base) (void)hipFree(s->base);
     if (s->phim_mem) (void)hipFree(s->phim_mem);
     if (s->kv_mem) (void)hipFree(s->kv_mem);
+    if (s->usm_mem) (void)hipFree(s->usm_mem);
     if (s->fc_mem) (void)hipFree(s->fc_mem);
     if (s->et_mem) (void)hipFree(s->et_mem);
     if (s->ksc) (void)hipFree(s->ksc);
@@ -1465,9 +1491,11 @@ int ns_step(ns_solver* s, ns_stats* out) {
     CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
     // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
+    CHK(helm_guess(s));
     CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));       // rhs ghost rows: a checked pair pass reads ib-4
     CHK(helm_solve(s, &st.it_u, &st.res_u, &st.res_v));            // KSPSolve(uSolver) x2 (:547-548)
     st.it_v = st.it_u;
+    if (s->helm_extrap) s->us_valid = std::min(s->us_valid + 1, 2);  // correct() leaves u* in TMPU/TMPV
     CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
     CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
@@ -1511,6 +1539,7 @@ int ns_set_array(ns_solver* s, int which, const double* host) {
     // keep the derived scalars consistent with an injected right-hand side
     if (which == NS_ARR_RPHI) CHK(rhs_mean(s));
     if (which == NS_ARR_PHI || which == NS_ARR_TMP) s->phim_valid = 0;
+    s->us_valid = 0;
     if (which == NS_ARR_RU || which == NS_ARR_RV) CHK(helm_bnorm(s));
     HIPCHK(hipStreamSynchronize(s->st));
     return 0;
@@ -1535,6 +1564,7 @@ int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* 
 
 int ns_kernel(ns_solver* s, int which, int iters, double* out) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
+    s->us_valid = 0;   // standalone kernels may overwrite the kept u*
     HIPCHK(hipSetDevice(s->device));
     const double alpha = s->dt / (2 * s->re);
     switch (which) {
