@@ -106,6 +106,11 @@ int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st);
 // out = a x + b y (+ c z if z) over the slab's own cells
 void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st,
                   double c = 0.0, const double* z = nullptr);
+// stretched grids: partials of sum_c A_c b_c, then b_c -= m / A_c with m = (sab - shift * area) / n
+// and kshift = the shift that leaves b - kshift mean-free (the Krylov solves)
+int launch_area_sum(const Geo& g, const Coef& c, const double* b, double* part, hipStream_t st);
+void launch_area_fix(const Geo& g, const Coef& c, double* b, const double* sab, const double* shift, double area,
+                     double inv_area, double n, double* kshift, hipStream_t st);
 // random fill of phi, rhs (sweep benchmark input)
 void launch_fill_random(const Geo& g, double* phi, double* rp, uint64_t seed, hipStream_t st);
 

@@ -2081,6 +2081,39 @@ __global__ void k_bicg_scal(int stage, const double* __restrict__ d, double n, d
     }
 }
 
+// ------------------------------------------------ stretched grids: a consistent Poisson rhs
+// The Poisson operator conserves area-weighted sums (sum_c A_c (L phi)_c = 0 at walls and
+// inlets), so L phi = b is solvable only if sum_c A_c b_c = 0.  div(u*) satisfies that, but the
+// reference's PLAIN mean removal (MatNullSpaceRemove, FluidSolver.cpp:550) breaks it on a
+// stretched grid and leaves its Krylov solve an inconsistent system.  The oracle's PCG
+// converges to the area-projected solution (b - shift) - m / A_c with
+// m = sum_c A_c (b_c - shift) / N; these two passes move the rhs there (in place; the shift
+// stays the plain mean), so every solver sees a consistent system with that same solution.
+__global__ __launch_bounds__(256) void k_area_sum(Geo g, Coef c, const double* __restrict__ b,
+                                                  double* __restrict__ part, int rows) {
+    const int j = blockIdx.x * 64 + threadIdx.x;
+    const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
+    double acc[1] = {0.0};
+    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4)
+        acc[0] += (c.hx[g.i0 + li] * c.hy[j]) * b[(ptrdiff_t)li * g.ld + j];   // 0 outside a mask
+    block_reduce_sum<1>(acc, part + (blockIdx.x + gridDim.x * blockIdx.y));
+}
+// b_c -= m / A_c, m = (sum A b - shift * sum A) / N from the reduced sum sab and the shift;
+// kshift = shift + mean(b - shift) afterwards = shift - m sum(1/A) / N (the mean-free shift of
+// the Krylov solves; the plain mean of b - shift was 0 before the fix)
+__global__ __launch_bounds__(256) void k_area_fix(Geo g, Coef c, double* __restrict__ b,
+                                                  const double* __restrict__ sab, const double* __restrict__ shift,
+                                                  double area, double inv_area, double n, double* __restrict__ kshift) {
+    const int j = blockIdx.x * 64 + threadIdx.x;
+    const int li = blockIdx.y * 4 + threadIdx.y;
+    const double m = (sab[0] - shift[0] * area) / n;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && threadIdx.y == 0) kshift[0] = shift[0] - m * inv_area / n;
+    if (j >= g.ny || li >= g.nxl) return;
+    const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
+    if (g.fc && !(g.fc[o] & FC_IN)) return;
+    b[o] -= m * (c.rhx[g.i0 + li] * c.rhy[j]);
+}
+
 // ---------------------------------------------------------------- launchers
 static inline dim3 cell_grid(const Geo& g) { return dim3((g.ny + 63) / 64, (g.nxl + 3) / 4); }
 
@@ -2484,6 +2517,16 @@ int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st) {
 void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st,
                   double c, const double* z) {
     hipLaunchKernelGGL(k_axpby, cell_grid(g), dim3(64, 4), 0, st, g, a, x, b, y, c, z, out);
+}
+int launch_area_sum(const Geo& g, const Coef& c, const double* b, double* part, hipStream_t st) {
+    const int rows = cell_rows(g);
+    const dim3 cg = cell_grid(g, rows);
+    hipLaunchKernelGGL(k_area_sum, cg, dim3(64, 4), 0, st, g, c, b, part, rows);
+    return (int)(cg.x * cg.y);
+}
+void launch_area_fix(const Geo& g, const Coef& c, double* b, const double* sab, const double* shift, double area,
+                     double inv_area, double n, double* kshift, hipStream_t st) {
+    hipLaunchKernelGGL(k_area_fix, cell_grid(g), dim3(64, 4), 0, st, g, c, b, sab, shift, area, inv_area, n, kshift);
 }
 void launch_fill_random(const Geo& g, double* phi, double* rp, uint64_t seed, hipStream_t st) {
     hipLaunchKernelGGL(k_fill_random, cell_grid(g), dim3(64, 4), 0, st, g, phi, rp, seed);

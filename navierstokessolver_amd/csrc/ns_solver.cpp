@@ -67,7 +67,8 @@ enum {
     S_RES = 6,      // 2: residual^2 (u, v) or (phi, -)
     S_MM = 8,       // 4: umin, -umax, vmin, -vmax
     S_AUX = 12,     // 4
-    S_NUM = 16
+    S_KSHIFT = 16,  // 1: the Krylov solves' shift after consistent_rhs (see there)
+    S_NUM = 18
 };
 
 }  // namespace
@@ -140,6 +141,9 @@ struct ns_solver {
     double* kv_mem = nullptr;
     double* ksc = nullptr;
     bool pc_active = false;      // inside mg_precond: level 0 has no mean shift, no timing
+    bool consist = false;        // stretched grid, no outflow: consistent_rhs() before every Poisson solve
+    double area = 0.0;           // sum of the domain's cell areas
+    double inv_area = 0.0;       // sum of their reciprocals
     int32_t* fc_mem = nullptr;   // masked domain: topology plane (g.fc) and edge table (g.et)
     nsg::EdgeDev* et_mem = nullptr;
     ns_host_transport ht{};      // host transport (ht.exchange != NULL) instead of RCCL
@@ -864,7 +868,11 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
         if (s->verbose)
             fprintf(stderr, "nsgpu %s (bicgstab): it %d rel. residual %.3e (alpha %.3e omega %.3e%s)\n", ks.name, it,
                     *res, s->hs[S_AUX + 2], s->hs[S_AUX + 3], s->hs[S_AUX + 1] != 0.0 ? ", breakdown: restart" : "");
-        if (!std::isfinite(r2)) { set_err("%s residual is not finite", ks.name); *its = it; return NS_EDIVERGE; }
+        if (!std::isfinite(r2) || (b2 > 0 && r2 > 1e16 * b2)) {
+            set_err("%s (BiCGStab) diverged: relative residual %g after %d iterations", ks.name, *res, it);
+            *its = it;
+            return NS_EDIVERGE;
+        }
         if (r2 <= tol2 * b2 || r2 == 0.0 || it >= maxit) break;
         if (s->hs[S_AUX + 1] != 0.0) {
             if (++restarts > 50) { set_err("BiCGStab (%s) broke down 50 times", ks.name); *its = it; return NS_EDIVERGE; }
@@ -894,8 +902,8 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
 int pois_solve_any(ns_solver* s, int* its, double* res, ns_stats* stt) {
     if (s->kv[0]) {
         CHK(fetch(s));   // ||b - mean||^2 for the relative test
-        const KrylovSolve ks{0, 0.0, !s->g.fc, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,
-                             s->hs[S_SHIFT + 1], "poisson"};
+        const KrylovSolve ks{0, 0.0, !s->g.fc, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI],
+                             s->scal + (s->consist ? S_KSHIFT : S_SHIFT), s->hs[S_SHIFT + 1], "poisson"};
         const int rc = bicgstab(s, ks, its, res);
         if (stt) stt->n_checks += *its + 1;
         return rc;
@@ -1103,6 +1111,21 @@ int helm_guess(ns_solver* s) {
     }
     std::swap(s->usm, s->arr[NS_ARR_TMPU]);
     std::swap(s->vsm, s->arr[NS_ARR_TMPV]);
+    return 0;
+}
+
+// stretched grid without an outflow side: move rhs_phi onto the consistent system the oracle's
+// PCG solves (k_area_fix); a no-op elsewhere (uniform grids: sum A b = A sum b = 0 already).
+// The multigrid keeps subtracting the plain mean S_SHIFT (b' = b - shift is the consistent rhs);
+// the Krylov solves project residuals onto mean-free vectors, so they subtract S_KSHIFT = shift +
+// mean(b'), which leaves the same solution and a mean-free initial residual.
+int consistent_rhs(ns_solver* s) {
+    if (!s->consist) return 0;
+    const int nb = nsg::launch_area_sum(s->g, s->c, s->arr[NS_ARR_RPHI], s->part, s->st);
+    nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_AUX, s->st);
+    CHK(allreduce(s, s->scal + S_AUX, 1, ncclSum));
+    nsg::launch_area_fix(s->g, s->c, s->arr[NS_ARR_RPHI], s->scal + S_AUX, s->scal + S_SHIFT, s->area, s->inv_area,
+                         s->ncells, s->scal + S_KSHIFT, s->st);
     return 0;
 }
 
@@ -1364,6 +1387,24 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     s->rank = p->rank;
     s->nranks = p->nranks;
     s->ncells = (double)nin;
+    {
+        // a stretched grid (Grid.cpp ratio > 0) with no outflow edge needs the consistent rhs
+        bool stretched = false, outflow = false;
+        for (int i = 1; i < gd->nx; i++) stretched |= std::fabs(gd->hx[i] - gd->hx[0]) > 1e-12 * gd->hx[0];
+        for (int j = 1; j < gd->ny; j++) stretched |= std::fabs(gd->hy[j] - gd->hy[0]) > 1e-12 * gd->hy[0];
+        for (int e = 0; e < gd->n_edges; e++) outflow |= gd->edges[e].type == NS_BC_NEUMANN;
+        s->consist = stretched && !outflow;
+        if (const char* e = getenv("NSGPU_CONSISTENT_RHS")) s->consist = s->consist && std::atoi(e) != 0;
+        double a = 0.0, ia = 0.0;
+        for (int i = 0; i < gd->nx; i++)
+            for (int j = 0; j < gd->ny; j++)
+                if (!masked || gd->cell_id[(size_t)i * gd->ny + j] >= 0) {
+                    a += gd->hx[i] * gd->hy[j];
+                    ia += 1.0 / (gd->hx[i] * gd->hy[j]);
+                }
+        s->area = a;
+        s->inv_area = ia;
+    }
 
     auto fail = [&](int rc) { ns_destroy(s); return rc; };
     int dev = p->device;
@@ -1498,6 +1539,7 @@ int ns_step(ns_solver* s, ns_stats* out) {
     if (s->helm_extrap) s->us_valid = std::min(s->us_valid + 1, 2);  // correct() leaves u* in TMPU/TMPV
     CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
+    CHK(consistent_rhs(s));                                        // stretched grids only
     CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
     CHK(extrapolate_phi(s));
     CHK(pois_solve_any(s, &st.it_phi, &st.res_phi, &st));         // KSPSolve(phiSolver)  (:551)
@@ -1651,6 +1693,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         int its = 0;
         double r = 0;
         CHK(rhs_mean(s));
+        CHK(consistent_rhs(s));
         CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
         CHK(pois_solve_any(s, &its, &r, nullptr));
         if (out) { out[0] = its; out[1] = r; }

@@ -21,4 +21,6 @@ UCHAN = dict(vertices=[(0, 0), (0, 1), (1.5, 1), (1.5, 0), (1, 0), (1, 0.5), (0.
              xspec=[[0, 0.5, 10, 1.05], [0.5, 1.0, 12, -1], [1.0, 1.5, 10, 0.95]], yspec=[[0, 1, 24, -1]],
              bc=[(WALL, 0.0), (WALL, 0.0), (WALL, 0.0), (WALL, 0.0), (NEUMANN, 0.0), (WALL, 0.0), (WALL, 0.0),
                  (INLET, 1.0)])
-ALL = {"step": STEP, "lshape": LSHAPE, "split": SPLIT, "uchannel": UCHAN}
+# the L-shaped cavity on a stretched grid (walls only: the area-consistent Poisson rhs)
+LSHAPE_S = dict(LSHAPE, xspec=[[0, 0.5, 12, 1.04], [0.5, 1, 12, 0.96]], yspec=[[0, 0.5, 10, 0.95], [0.5, 1, 14, -1]])
+ALL = {"step": STEP, "lshape": LSHAPE, "split": SPLIT, "uchannel": UCHAN, "lshape_s": LSHAPE_S}

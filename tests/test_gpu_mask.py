@@ -99,7 +99,7 @@ def test_mask_converged_solves(gpu, name):
 
 
 @pytest.mark.parametrize("name,steps,re", [("step", 15, 100.0), ("lshape", 12, 400.0), ("split", 10, 100.0),
-                                           ("uchannel", 10, 100.0)])
+                                           ("uchannel", 10, 100.0), ("lshape_s", 10, 200.0)])
 def test_mask_full_steps_vs_oracle(gpu, name, steps, re):
     P = ALL[name]
     n = max(P["xspec"][-1][2], P["yspec"][-1][2])
