@@ -30,10 +30,13 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level 
 #       read phi 8 + read b 8 + write phi 8 + write the coarse rhs and phi 2 x 8 / 4  = 28
 #   prolongation pass (k_sweep2 FUSE_P): prolongation + two RB sweeps:
 #       read phi 8 + read b 8 + write phi 8 + read the coarse correction 8 / 4         = 26
-# The one with the larger total time per step is `roofline` (the dominant kernel).
+# and the Helmholtz solve's passes (K2, single rank: one velocity component per pass):
+#   Helmholtz pass (k_sweep2<Helmholtz>): two RB-SOR sweeps: read q 8 + read b 8 + write q 8 = 24
+# The one with the largest total time per step is `roofline` (the dominant kernel).
 KERNELS = {
     "restrict": ("k_sweep2<Poisson, FUSE_R> (finest pre-smoothing pass: 2 RB sweeps + residual + restriction)", 28),
     "prolong": ("k_sweep2<Poisson, FUSE_P> (finest post-smoothing pass: prolongation + 2 RB sweeps)", 26),
+    "helmholtz": ("k_sweep2<Helmholtz> (2 RB-SOR sweeps of one velocity component of (I - a L_V) u* = RHS)", 24),
 }
 JACOBI_LABEL = "k_sweep<Poisson, Jacobi> (one weighted-Jacobi sweep, the north star's roofline kernel)"
 SWEEP_BYTES_PER_CELL = 24
@@ -42,8 +45,8 @@ SWEEP_BYTES_PER_CELL = 24
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--rtol", type=float, default=1e-8)
@@ -123,12 +126,15 @@ def main():
         elapsed = float(t.item())
 
     K = args.steps
+    timed_steps = K if args.time_every == 1 else (sum(1 for k in range(K) if k % args.time_every == 0)
+                                                   if args.time_every > 0 else 0)
     cells = n * n
     cycles = sum(s["it_phi"] for s in stats)
     hsweeps = sum(s["it_u"] for s in stats)
     local_cells = (solver.i1 - solver.i0) * n
     timed = {"prolong": (sum(s["t_poisson_kernel_ms"] for s in stats), sum(s["n_poisson_kernels"] for s in stats)),
-             "restrict": (sum(s["t_restrict_kernel_ms"] for s in stats), sum(s["n_restrict_kernels"] for s in stats))}
+             "restrict": (sum(s["t_restrict_kernel_ms"] for s in stats), sum(s["n_restrict_kernels"] for s in stats)),
+             "helmholtz": (sum(s["t_helm_kernel_ms"] for s in stats), sum(s["n_helm_kernels"] for s in stats))}
     # finest-level sweeps: V(2,2) per cycle + the 2 pre-smoothing sweeps of the converged check
     fine_sweeps = 4 * cycles + 2 * K
     value = cells * K / elapsed / 1e6
@@ -165,7 +171,8 @@ def main():
         ms, cnt = timed[key]
         if cnt:
             kern[key] = roof(key, label, bpc, ms / cnt / 1e3, cnt)
-            kern[key]["ms_per_step"] = ms / K
+            # (launches are timed on every --time-every'th step: scale to all K steps)
+            kern[key]["ms_per_step"] = ms / max(1, timed_steps)
     dominant = max(kern, key=lambda k: kern[k]["ms_per_step"]) if kern else None
     line = {
         "metric": "cell-updates/sec (MLUPS) + Poisson iters/sec, 4096^2 grid at 1/2/4/8 GPUs",

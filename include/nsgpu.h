@@ -124,6 +124,9 @@ typedef struct ns_stats {
     int32_t n_checks;                /* residual checks (host syncs) in the step */
     double  t_restrict_kernel_ms;    /* multigrid: sum of the finest level's restriction-pass durations (timing == 1) */
     int32_t n_restrict_kernels;      /* number of those passes timed */
+    double  t_helm_kernel_ms;        /* single rank: sum of the two-sweep Helmholtz pass durations (one velocity
+                                        component each, K2; timing == 1) */
+    int32_t n_helm_kernels;          /* number of those passes timed */
 } ns_stats;
 
 /* device arrays addressable by ns_get_array / ns_set_array */

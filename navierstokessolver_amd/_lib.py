@@ -64,7 +64,8 @@ class NsStats(ctypes.Structure):
                 ("it_phi", ctypes.c_int32), ("res_u", ctypes.c_double), ("res_v", ctypes.c_double),
                 ("res_phi", ctypes.c_double), ("t_poisson_kernel_ms", ctypes.c_double),
                 ("n_poisson_kernels", ctypes.c_int32), ("n_checks", ctypes.c_int32),
-                ("t_restrict_kernel_ms", ctypes.c_double), ("n_restrict_kernels", ctypes.c_int32)]
+                ("t_restrict_kernel_ms", ctypes.c_double), ("n_restrict_kernels", ctypes.c_int32),
+                ("t_helm_kernel_ms", ctypes.c_double), ("n_helm_kernels", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

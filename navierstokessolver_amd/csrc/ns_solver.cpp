@@ -110,6 +110,8 @@ struct ns_solver {
     double ncells = 0;           // global cell count
     std::vector<hipEvent_t> ev;  // timing events (pairs)
     std::vector<char> evtag;     // per pair: 0 = sweep / prolongation pass, 1 = restriction pass
+    std::vector<hipEvent_t> hev; // Helmholtz pass timing events (pairs; timing == 1, single rank)
+    int hn = 0;                  // Helmholtz pairs recorded this step
     int helm_batch0 = 4, pois_batch0 = 8;
     int helm_next = 4;           // first Helmholtz batch of the next step (adaptive unless check_every)
     int helm_adapt = 1;
@@ -277,9 +279,24 @@ int helm_sweep(ns_solver* s, double alpha, double* part, int which = 3) {
 
 // two Helmholtz sweeps in one pass (temporal blocking), then swap
 int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3) {
+    // timing: one-component passes only (the bench's 24 B/cell roofline figure)
+    const bool t = s->timing && which != 3;
+    if (t) {
+        if (s->hev.size() < 2 * (size_t)(s->hn + 1)) {
+            const size_t old = s->hev.size();
+            s->hev.resize(2 * (size_t)(s->hn + 8));
+            for (size_t k = old; k < s->hev.size(); k++)
+                if (hipEventCreate(&s->hev[k]) != hipSuccess) { set_err("hipEventCreate failed"); return -1; }
+        }
+        if (hipEventRecord(s->hev[2 * s->hn], s->st) != hipSuccess) { set_err("hipEventRecord failed"); return -1; }
+    }
     const int nb = nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
                                            s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
                                            s->arr[NS_ARR_RV], part, s->st, which);
+    if (t) {
+        if (hipEventRecord(s->hev[2 * s->hn + 1], s->st) != hipSuccess) { set_err("hipEventRecord failed"); return -1; }
+        s->hn++;
+    }
     if (which & 1) std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
     if (which & 2) std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
     return nb;
@@ -308,6 +325,7 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
             if (which == 3) CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, hw));
             else CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
             nb = w == 2 ? helm_sweep2(s, alpha, part, which) : helm_sweep(s, alpha, part, which);
+            if (nb < 0) return NS_EHIP;
             const int at = w == 2 ? k + 2 : k;
             if (launch == 0) {
                 if (nb_first) *nb_first = nb;
@@ -1502,6 +1520,7 @@ void ns_destroy(ns_solver* s) {
     if (s->st) (void)hipStreamSynchronize(s->st);
     if (s->comm) (void)ncclCommDestroy(s->comm);
     for (auto e : s->ev) (void)hipEventDestroy(e);
+    for (auto e : s->hev) (void)hipEventDestroy(e);
     for (size_t l = 1; l < s->lv.size(); l++) {
         if (s->lv[l].mem) (void)hipFree(s->lv[l].mem);
         if (s->lv[l].coef) (void)hipFree(s->lv[l].coef);
@@ -1534,8 +1553,16 @@ int ns_step(ns_solver* s, ns_stats* out) {
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
     CHK(helm_guess(s));
     CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));       // rhs ghost rows: a checked pair pass reads ib-4
+    s->hn = 0;
     CHK(helm_solve(s, &st.it_u, &st.res_u, &st.res_v));            // KSPSolve(uSolver) x2 (:547-548)
     st.it_v = st.it_u;
+    for (int k = 0; k < s->hn; k++) {   // (helm_solve's last residual check synchronised the stream)
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, s->hev[2 * k], s->hev[2 * k + 1]));
+        st.t_helm_kernel_ms += ms;
+        st.n_helm_kernels++;
+    }
+    s->hn = 0;
     if (s->helm_extrap) s->us_valid = std::min(s->us_valid + 1, 2);  // correct() leaves u* in TMPU/TMPV
     CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)

@@ -1,15 +1,18 @@
 #!/bin/bash
 # Kernel trace + HBM PMC passes of the bench workload (run on the GPU box from the repo root):
-#   bash tools/profile_round.sh <outdir>
-# writes <outdir>/trace (kernel trace + stats), <outdir>/fetch, <outdir>/write (PMC), and
-# profiles/pmc_traffic.json (per-kernel HBM bytes, read by bench.py).  Each rocprofv3 run is its
-# own pass (--pmc never combined with the runtime/sys trace domains).
+#   bash tools/profile_round.sh <outdir under gpurun_out/>
+# writes <outdir>/trace (kernel trace + stats), <outdir>/fetch, <outdir>/write (PMC),
+# <outdir>/per_step_summary.txt and <outdir>/pmc_traffic.json (per-kernel HBM bytes; copy it to
+# profiles/pmc_traffic.json, which bench.py reads for each kernel's roofline.traffic).  Each
+# rocprofv3 run is its own pass (--pmc never combined with the runtime/sys trace domains).
 set -e
 out=${1:-gpurun_out/prof}
 export TMPDIR=/tmp
 mkdir -p $out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu > $out/trace.log 2>&1
+python3 tools/trace_summary.py $(find $out/trace -name "*kernel_trace.csv" | head -1) 13 > $out/per_step_summary.txt
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu > $out/fetch.log 2>&1
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu > $out/write.log 2>&1
-python3 tools/pmc_summarize.py 4096 $out/fetch $out/write profiles/pmc_traffic.json \
-  'restrict=k_sweep2<0, false, 1>=28' 'prolong=k_sweep2<0, false, 2>=26' 'jacobi_sweep=k_sweep<0, false=24'
+python3 tools/pmc_summarize.py 4096 $out/fetch $out/write $out/pmc_traffic.json \
+  'restrict=k_sweep2<0, false, 1>=28' 'prolong=k_sweep2<0, false, 2>=26' 'jacobi_sweep=k_sweep<0, false=24' \
+  'helmholtz=k_sweep2<1, =24'
