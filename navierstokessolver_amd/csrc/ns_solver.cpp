@@ -115,6 +115,7 @@ struct ns_solver {
     int helm_batch0 = 4, pois_batch0 = 8;
     int helm_next = 4;           // first Helmholtz batch of the next step (adaptive unless check_every)
     int helm_adapt = 1;
+    int helm_probe = 0;          // steps since the Helmholtz first-pass residual was last sampled
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
     int fuse_restrict = 1;       // NSGPU_FUSED_RESTRICT=0: separate k_restrict pass (A/B)
     int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
@@ -404,13 +405,17 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
     // first batch: what the previous step needed (consecutive steps converge alike), so a
     // step normally costs one residual check
     int sweeps = 0, batch = s->helm_next, prev_at = -1;
+    const int n0 = batch;
     double prev_r2 = -1;
     double first_r2 = -1, last_r2 = -1;   // max over u, v of r^2 / ||b||^2
     int first_at = 0, last_at = 0;
     double* p0 = s->part + 2 * (size_t)nsg::max_partials(s->g) / 2;  // second half: first-launch residuals
     for (;;) {
         const int n = std::min(batch, s->max_iters - sweeps);
-        const bool first = sweeps == 0 && n > 2;
+        // the first pass's residual (a fifth pipeline stage: +20 % on that pass) feeds the next
+        // step's batch prediction; consecutive steps converge alike, so it is sampled on every
+        // 8th step only (and whenever the predicted batch fell short: see below)
+        const bool first = sweeps == 0 && n > 2 && (s->helm_probe == 0 || !s->helm_adapt);
         int nb0 = 0, at0 = 0, at = 0;
         const int nb = helm_sweeps(s, alpha, n, first ? p0 : nullptr, s->part, &nb0, &at0, &at);
         at += sweeps;
@@ -463,6 +468,8 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         if (std::isfinite(more)) need = std::min(sweeps, first_at + std::max(0, (int)std::ceil(more)));
     }
     s->helm_next = s->helm_adapt ? std::max(2, need + (need & 1)) : s->helm_batch0;
+    // probe again in 8 steps, or on the next step if this one needed more than one batch
+    s->helm_probe = (sweeps > n0) ? 0 : (s->helm_probe + 1) % 8;
     return 0;
 }
 

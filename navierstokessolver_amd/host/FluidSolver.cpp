@@ -199,18 +199,27 @@ void write_flow_csv(int iter, Grid& g, double dt, double re, const vector<double
             if (!g.inDomain(i, j)) continue;   // a polygon's bounding-box cells outside the domain
             const size_t c = id(i, j);
             double lap = 0.0, dg = 0.0;
+            const int32_t* t = &g.faceEdges()[c * 4];
             for (int k = 0; k < 4; k++) {
                 const int ii = i + di[k], jj = j + dj[k];
                 if (g.inDomain(ii, jj)) {
                     const double w = di[k] ? 2.0 / (g.hx[i] * (g.hx[i] + g.hx[ii])) : 2.0 / (g.hy[j] * (g.hy[j] + g.hy[jj]));
                     lap += w * phi[id(ii, jj)];
                     dg -= w;
+                } else if (t[k] >= 0) {
+                    // LHS_phi's ghost row (AddGhostStencils, FluidSolver.cpp:147-163): w (ghost - phi_c),
+                    // 0 at walls / inlets, the 2.5/-2/0.5 extrapolation at a NEUMANN face
+                    const Stencil& sp = g.edges[t[k]].ghost[1];
+                    double gp = 0.0;
+                    for (size_t q = 0; q < sp.weights.size(); q++)
+                        gp += sp.weights[q] * phi[id(i + sp.support[q][0], j + sp.support[q][1])];
+                    const double w = di[k] ? 1.0 / (g.hx[i] * g.hx[i]) : 1.0 / (g.hy[j] * g.hy[j]);
+                    lap += w * (gp - phi[c]);
                 }
             }
             lap += dg * phi[c];
             const double xc = g.centerX(i), yc = g.centerY(j);
             fs << xc << "," << yc << "," << 0.0 << "," << u[c] << "," << v[c] << "," << phi[c] + (-a) * lap << endl;
-            const int32_t* t = &g.faceEdges()[c * 4];
             for (int k = 0; k < 4; k++) {
                 if (t[k] < 0) continue;
                 const Edge& e = g.edges[t[k]];

@@ -78,3 +78,61 @@ def _cell_rows():
             rows.append(r)
             r += 1 + (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1)
     return rows
+
+
+# ---- a backward-facing step with an inlet and a NEUMANN outflow (tests/polygons.py STEP):
+# the host Grid classifies the polygon, FluidSolver hands libnsgpu.so the mask, the export
+# includes the outflow's ghost rows in L phi (MatMult(LHS_phi), FluidSolver.cpp:579)
+from polygons import STEP  # noqa: E402
+
+PSTEPS, PSAVE = 12, 6
+
+
+def write_polygon_inputs(d, P, dt):
+    verts = "\n".join(f"{x} {y}" for x, y in P["vertices"])
+    seg = lambda spec: "\n".join(" ".join(str(v) for v in s) for s in spec)
+    (d / "grid").write_text(f"Vertices {{\n{verts}\n}}\nNx {{\n{seg(P['xspec'])}\n}}\nNy {{\n{seg(P['yspec'])}\n}}\n")
+    bc = "\n".join(f"{t} {i}" for t, i in P["bc"])
+    (d / "sim").write_text(f"BC {{\n{bc}\n}}\ndt {dt!r}\nfinal_time {PSTEPS * dt!r}\nre {RE!r}\nsaveIter {PSAVE}\n")
+
+
+@pytest.mark.parametrize("exe", ["ns_main", "ref_main_link"])
+def test_driver_polygon_outflow_matches_oracle(tmp_path, exe):
+    path = os.path.join(HOST, exe)
+    if not os.path.exists(path):
+        pytest.skip(f"{exe} not built (ref_main_link needs /root/reference at build time)")
+    P = STEP
+    dt = 1.0 / 512
+    write_polygon_inputs(tmp_path, P, dt)
+    out = subprocess.run([path, "grid", "sim"], capture_output=True, text=True, cwd=tmp_path, timeout=120).stdout
+    assert "Solver Setup Complete!" in out and "Solution Complete!" in out, out[-2000:]
+    lines = [l for l in out.splitlines() if l and l[0].isdigit()]
+    assert len(lines) == PSTEPS
+    og = OGrid(P["vertices"], P["xspec"], P["yspec"], P["bc"])
+    osv = OSolver(og, dt, RE, rtol=1e-13)
+    tags = og.tag.reshape(og.nx, og.ny, 4)
+    ids = og.id.reshape(og.nx, og.ny)
+    rows, r = [], 0          # each in-domain cell's row, then one row per boundary face
+    for i in range(og.nx):
+        for j in range(og.ny):
+            if ids[i, j] < 0:
+                continue
+            rows.append(r)
+            r += 1 + int((tags[i, j] >= 0).sum())
+    for it in range(1, PSTEPS + 1):
+        mm, _ = osv.step()
+        f = lines[it - 1].split("\t")
+        assert all(printed_equal(float(a), b) for a, b in zip(f[1:5], mm)), (lines[it - 1], mm)
+        if it % PSAVE:
+            continue
+        st = osv.get()
+        d = np.loadtxt(tmp_path / f"FlowData_{it}.csv", delimiter=",", skiprows=1)
+        assert d.shape == (r, 6)
+        cells = d[rows]
+        np.testing.assert_allclose(cells[:, 0], og.xc, atol=1e-5)   # 6 significant digits, x up to 2
+        np.testing.assert_allclose(cells[:, 1], og.yc, atol=1e-5)
+        np.testing.assert_allclose(cells[:, 3], st["u"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(cells[:, 4], st["v"], rtol=1e-5, atol=1e-6)
+        p = og.pressure(dt / (2 * RE), st["phi"])
+        pc = cells[:, 5] - cells[:, 5].mean()
+        np.testing.assert_allclose(pc, p - p.mean(), rtol=0, atol=1e-5 * np.abs(p).max())
