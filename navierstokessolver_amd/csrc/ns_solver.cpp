@@ -144,6 +144,7 @@ struct ns_solver {
     double* kv_mem = nullptr;
     double* ksc = nullptr;
     bool pc_active = false;      // inside mg_precond: level 0 has no mean shift, no timing
+    bool krylov_mg = false;      // the Poisson BiCGStab is preconditioned by a V-cycle (else Jacobi)
     bool consist = false;        // stretched grid, no outflow: consistent_rhs() before every Poisson solve
     double area = 0.0;           // sum of the domain's cell areas
     double inv_area = 0.0;       // sum of their reciprocals
@@ -927,7 +928,7 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
 int pois_solve_any(ns_solver* s, int* its, double* res, ns_stats* stt) {
     if (s->kv[0]) {
         CHK(fetch(s));   // ||b - mean||^2 for the relative test
-        const KrylovSolve ks{0, 0.0, !s->g.fc, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI],
+        const KrylovSolve ks{0, 0.0, s->krylov_mg, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI],
                              s->scal + (s->consist ? S_KSHIFT : S_SHIFT), s->hs[S_SHIFT + 1], "poisson"};
         const int rc = bicgstab(s, ks, its, res);
         if (stt) stt->n_checks += *its + 1;
@@ -1025,6 +1026,8 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
         if (whole && s->lv.size() > 1 && nsg::coarse_vcycle_bytes(gf) <= lds_cap) break;
         if (!nsg::mg_can_coarsen(gf.nx, gf.ny)) break;
         nsg::Geo gc = gf;
+        gc.fc = nullptr;   // coarse levels are whole boxes (a masked domain's fictitious-domain V-cycle)
+        gc.et = nullptr;
         gc.nx /= 2; gc.ny /= 2;
         gc.ld = (gc.ny + 127) / 128 * 128;
         bool repl = F.repl;
@@ -1483,7 +1486,13 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (hipMemcpy(s->coef, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) { set_err("coef upload failed"); return fail(NS_EHIP); }
         s->c = coef_view(s->coef, g.nx, g.ny);
     }
-    if (s->poisson == NS_POISSON_MG && !masked) {
+    // a masked domain's Poisson preconditioner: one V-cycle of the BOUNDING BOX's wall-closure
+    // multigrid (a fictitious-domain preconditioner: the rhs is 0 outside the domain, the
+    // outside values of the result are ignored by the masked operator), unless
+    // NSGPU_MASK_PC=jacobi
+    bool mask_mg = true;
+    if (const char* e = getenv("NSGPU_MASK_PC")) mask_mg = std::strcmp(e, "jacobi") != 0;
+    if (s->poisson == NS_POISSON_MG && (!masked || mask_mg)) {
         if (p->mg_pre > 0) s->mg_pre = p->mg_pre;
         if (p->mg_omega > 0) s->mg_omega_s = p->mg_omega;
         if (const char* e = getenv("NSGPU_MG_OMEGA")) s->mg_omega_s = std::atof(e);   // smoother over-relaxation (A/B)
@@ -1491,6 +1500,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (int rc = build_levels(s, hx0, hy0)) return fail(rc);
         if (p->mg_coarse_iters > 0) s->mg_coarse_iters = p->mg_coarse_iters;
         if (s->lv.size() < 2) s->poisson = NS_POISSON_RBSOR;  // nothing to coarsen: plain RB-SOR
+        s->krylov_mg = true;
     }
     if (masked || g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3]) {
         // BiCGStab planes (outflow rectangle: the preconditioner is the hierarchy above -- with a
