@@ -121,6 +121,7 @@ struct ns_solver {
     int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
     int tile_small = 1;          // NSGPU_TILE_SMALL=0: no LDS-tiled fused passes on small levels (A/B)
     int helm_split = 1;          // NSGPU_HELM_SPLIT=0: u and v pass by pass (A/B)
+    int helm_ns = 2;             // Helmholtz sweeps per pass on one slab (NSGPU_HELM_NS: 2, 3, 4)
     int phi_extrap = 2;          // Poisson initial guess: NSGPU_PHI_EXTRAP=0 phi^{n-1}, 1 linear, 2 quadratic (default)
     int mg_predict = 1;          // NSGPU_MG_PREDICT=0: a residual check (host sync) after every V-cycle
     double mg_rate2 = 0.0;       // last measured per-cycle contraction of ||r||^2
@@ -280,7 +281,7 @@ int helm_sweep(ns_solver* s, double alpha, double* part, int which = 3) {
 }
 
 // two Helmholtz sweeps in one pass (temporal blocking), then swap
-int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3) {
+int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3, int ns = 2) {
     // timing: one-component passes only (the bench's 24 B/cell roofline figure)
     const bool t = s->timing && which != 3;
     if (t) {
@@ -292,9 +293,18 @@ int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3) {
         }
         if (hipEventRecord(s->hev[2 * s->hn], s->st) != hipSuccess) { set_err("hipEventRecord failed"); return -1; }
     }
-    const int nb = nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
-                                           s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
-                                           s->arr[NS_ARR_RV], part, s->st, which);
+    int nb;
+    if (ns > 2) {   // ns sweeps of one component in one pass (single slab)
+        const bool u = which == 1;
+        nb = nsg::launch_helm_sweepN(ns, s->g, s->c, alpha, s->omega_v, s->arr[u ? NS_ARR_U : NS_ARR_V],
+                                     s->arr[u ? NS_ARR_TMPU : NS_ARR_TMPV], s->arr[u ? NS_ARR_RU : NS_ARR_RV], part,
+                                     s->st, !u);
+        if (nb < 0) { set_err("k_sweepN: %d sweeps per pass need a single slab", ns); return -1; }
+    } else {
+        nb = nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
+                                     s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
+                                     s->arr[NS_ARR_RV], part, s->st, which);
+    }
     if (t) {
         if (hipEventRecord(s->hev[2 * s->hn + 1], s->st) != hipSuccess) { set_err("hipEventRecord failed"); return -1; }
         s->hn++;
@@ -320,15 +330,17 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
         if (!which) break;
         int k = 0, launch = 0;
         while (k < n) {
-            const int w = (n - k >= 2 && !s->tiled) ? 2 : 1;
+            // sweeps per pass: up to helm_ns (NSGPU_HELM_NS) on one slab, pairs otherwise
+            const int wmax = s->tiled ? 1 : (split ? s->helm_ns : 2);
+            const int w = std::min(wmax, n - k);
             const bool last = k + w >= n;
             double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
             const int hw = w == 2 ? (part ? 5 : 4) : 2;
             if (which == 3) CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, hw));
-            else CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
-            nb = w == 2 ? helm_sweep2(s, alpha, part, which) : helm_sweep(s, alpha, part, which);
+            else if (w <= 2) CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
+            nb = w >= 2 ? helm_sweep2(s, alpha, part, which, w) : helm_sweep(s, alpha, part, which);
             if (nb < 0) return NS_EHIP;
-            const int at = w == 2 ? k + 2 : k;
+            const int at = w >= 2 ? k + w : k;   // a multi-sweep pass reports its output's residual
             if (launch == 0) {
                 if (nb_first) *nb_first = nb;
                 if (first_at) *first_at = at;
@@ -1403,6 +1415,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_SPLIT")) s->helm_split = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_HELM_NS")) s->helm_ns = std::max(2, std::min(4, std::atoi(e)));
     if (const char* e = getenv("NSGPU_HELM_EXTRAP")) s->helm_extrap = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = getenv("NSGPU_MG_PREDICT")) s->mg_predict = std::atoi(e) != 0;

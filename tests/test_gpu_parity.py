@@ -408,6 +408,30 @@ def test_two_sweep_pass_equals_two_sweeps(gpu, nx, ny, op):
         assert rel(gs.get(gpu.NS_ARR_V), vv) <= 1e-12
 
 
+@pytest.mark.parametrize("ns", [3, 4])
+@pytest.mark.parametrize("nx,ny", [(300, 200), (1030, 260), (64, 700)])
+def test_multi_sweep_helmholtz_pass_equals_pairs(gpu, monkeypatch, nx, ny, ns):
+    """k_sweepN (ns red-black sweeps of one velocity component per HBM pass, one slab) gives the
+    same iterate as two-sweep passes -- bit for bit -- and the same output residual.  Fixed work:
+    8 sweeps per component (check_every 8, max_iters 8, an unreachable rtol)."""
+    rng = np.random.default_rng(31)
+    dt, re = 1.0 / 64, 10.0
+    u, v, ru, rv = (rand(rng, nx * ny) for _ in range(4))
+    out = {}
+    for k in (2, ns):
+        monkeypatch.setenv("NSGPU_HELM_NS", str(k))
+        gs = gpu.GpuSolver(gpu.rectangle(nx, ny, bc=BC_FLOW), dt, re, omega_v=1.1, check_every=8, max_iters=8,
+                           rtol=1e-30)
+        for a, x in ((gpu.NS_ARR_U, u), (gpu.NS_ARR_V, v), (gpu.NS_ARR_RU, ru), (gpu.NS_ARR_RV, rv)):
+            gs.set(a, x)
+        its, res = gs.kernel(gpu.NS_K_HELM_SOLVE)[:2]
+        assert its == 8
+        out[k] = (gs.get(gpu.NS_ARR_U), gs.get(gpu.NS_ARR_V), res)
+        gs.close()
+    assert np.array_equal(out[2][0], out[ns][0]) and np.array_equal(out[2][1], out[ns][1])
+    assert out[2][2] == out[ns][2]
+
+
 @pytest.mark.parametrize("nx,ny", [(256, 192), (96, 160)])
 def test_fused_transfer_passes_match_separate_transfers(gpu, monkeypatch, nx, ny):
     """The last pre-smoothing pass with the restriction fused in (k_sweep2 FUSE_R) and the first
