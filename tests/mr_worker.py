@@ -23,6 +23,7 @@ ap.add_argument("--solver", type=int, default=nsa.NS_POISSON_MG)
 ap.add_argument("--tol", type=float, default=1e-10)
 ap.add_argument("--output", required=True)
 ap.add_argument("--bc", default="", help="edge BCs W,N,E,S as type:info,... (default: the cavity)")
+ap.add_argument("--ratio", type=float, default=-1.0, help="geometric x and y spacing ratio (Grid.cpp)")
 ap.add_argument("--poly", default="", help="a tests/polygons.py geometry instead of the rectangle")
 ap.add_argument("--stats-only", action="store_true", help="gather only the per-step stats (large grids)")
 a = ap.parse_args()
@@ -46,7 +47,7 @@ try:
         n, ny = og.nx, og.ny
         grid = nsa.polygon(P["vertices"], og.hx, og.hy, P["bc"])
     else:
-        grid = nsa.rectangle(n, ny, bc=bc)
+        grid = nsa.rectangle(n, ny, bc=bc, xratio=a.ratio, yratio=a.ratio)
     gs = nsa.GpuSolver(grid, 1.0 / (8 * n), 100.0, **kw)
     mm = [list(gs.step().values())[:7] for _ in range(a.nsteps)]
     u, v, phi = (np.zeros((1, ny)),) * 3 if a.stats_only else gs.fields()

@@ -113,6 +113,21 @@ def test_masked_domain_slabs_match_single_rank(tmp_path, poly, nproc):
     np.testing.assert_allclose(r["mm"][:, :4], mm[:, :4], atol=1e-8)
 
 
+def test_stretched_slabs_match_single_rank(tmp_path):
+    """Stretched cavity on 2 slabs: the consistent Poisson rhs (area-weighted sums all-reduced)
+    and the multigrid on non-uniform spacing give the single-rank answer."""
+    n, ny, steps, rtol, ratio = 96, 64, 5, 1e-11, 1.01
+    r = launch(tmp_path, "--xport", "host", "--size", str(n), "--size-y", str(ny), "--nsteps", str(steps),
+               "--tol", str(rtol), "--ratio", str(ratio), nproc=2, port=29601)
+    assert str(r["status"]) == "ok", r["status"]
+    gs = nsa.GpuSolver(nsa.rectangle(n, ny, xratio=ratio, yratio=ratio), 1.0 / (8 * n), 100.0, rtol=rtol, device=0)
+    mm = np.array([list(gs.step().values())[:7] for _ in range(steps)])
+    assert np.all(mm[:, 6] < 100), mm[:, 6]   # V-cycles per step: converging, not stalled
+    u, v, _ = gs.fields()
+    du, dv = float(np.max(np.abs(r["u"] - u))), float(np.max(np.abs(r["v"] - v)))
+    assert du <= 1e-8 and dv <= 1e-8, (du, dv)
+
+
 def test_rccl_two_ranks_one_gpu_probe(tmp_path):
     """RCCL usually rejects two ranks on one device; record what it does (never fails the suite
     unless RCCL ran and produced a wrong answer)."""
