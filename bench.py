@@ -38,8 +38,11 @@ KERNELS = {
     "prolong": ("k_sweep2<Poisson, FUSE_P> (finest post-smoothing pass: prolongation + 2 RB sweeps)", 26),
     "helmholtz": ("k_sweep2<Helmholtz> (2 RB-SOR sweeps of one velocity component of (I - a L_V) u* = RHS)", 24),
 }
-JACOBI_LABEL = "k_sweep<Poisson, Jacobi> (one weighted-Jacobi sweep, the north star's roofline kernel)"
+JACOBI_LABEL = "k_jacobi_s<double> (one weighted-Jacobi sweep of the Poisson operator, the north star's roofline kernel)"
 SWEEP_BYTES_PER_CELL = 24
+# configs[4]'s fp32-field Jacobi sweep: read phi 4 + read b 4 + write phi 4 (fp64 arithmetic / residual)
+JACOBI32_LABEL = "k_jacobi_s<float> (one Jacobi sweep on fp32 phi, b; fp64 arithmetic and residual: configs[4])"
+SWEEP32_BYTES_PER_CELL = 12
 
 
 def parse():
@@ -141,13 +144,18 @@ def main():
 
     # the north star's roofline kernel: one Jacobi sweep of this rank's slab (random phi, b;
     # 10 warm-up + 50 timed launches, HIP events), single rank only
-    jacobi = None
+    jacobi = jacobi32 = None
     if world == 1:
         js = nsa.GpuSolver(nsa.cavity(n), dt, re, poisson=nsa.NS_POISSON_JACOBI, omega=1.0, device=local)
         js.fill_random(0x5EED)
         t = js.time_poisson(10, 50)
-        js.close()
         jacobi = t["avg_ms"] * 1e-3
+        try:
+            js.fill_random(0x5EED)
+            jacobi32 = js.time_poisson_fp32(10, 50)["avg_ms"] * 1e-3
+        except AttributeError:   # a library without the fp32 sweep (A/B against an older build)
+            jacobi32 = None
+        js.close()
     if rank != 0:
         return
     traffic = {}
@@ -200,6 +208,9 @@ def main():
     }
     if jacobi is not None:
         line["kernels"]["jacobi_sweep"] = roof("jacobi_sweep", JACOBI_LABEL, SWEEP_BYTES_PER_CELL, jacobi, 50)
+    if jacobi32 is not None:
+        line["kernels"]["jacobi_sweep_fp32"] = roof("jacobi_sweep_fp32", JACOBI32_LABEL, SWEEP32_BYTES_PER_CELL,
+                                                    jacobi32, 50)
     if world == 1 and not args.no_cpu:
         try:
             line["cpu_baseline"] = cpu_baseline(n, re, dt, solver.omega_v, solver.mg_omega)

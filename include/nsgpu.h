@@ -152,6 +152,8 @@ typedef struct ns_stats {
 #define NS_K_HELM_SOLVE 6  /* converged Helmholtz solve   (:547-548) */
 #define NS_K_POIS_SOLVE 7  /* converged Poisson solve incl. null-space removal (:550-551) */
 #define NS_K_RESIDUAL   8  /* Poisson residual ||rhs - mean - L phi||^2 -> out[0] (no update) */
+#define NS_K_POISSON32  9  /* K4 Jacobi x iters on fp32 copies of phi, rhs_phi (fp64 arithmetic and residual,
+                              SURVEY.md 8(d) C5); phi <- the fp32 result widened */
 
 /* ---- lifecycle: FluidSolver(char*, Grid*) = SolverInitialize + SolverSetup (FluidSolver.cpp:8-58) ---- */
 int  ns_create(const ns_grid_desc* grid, const ns_params* params, ns_solver** out);
@@ -191,6 +193,11 @@ int  ns_fill_random(ns_solver* s, uint64_t seed);
 /* Time `iters` Poisson sweep kernels (after `warmup`) with HIP events on the
  * solver's stream: out[0] = average kernel ms, out[1] = total ms. */
 int  ns_time_poisson(ns_solver* s, int warmup, int iters, double* out);
+
+/* The same for the fp32-field Jacobi sweep (12 B/cell; configs[4]: "fp32 fields + fp64
+ * Poisson residual"): phi and rhs_phi are copied to fp32 planes first (allocated on first
+ * use, 3 x 4 B/cell); out[0..2] as above, out[3] = residual^2 of the last sweep's input. */
+int  ns_time_poisson_fp32(ns_solver* s, int warmup, int iters, double* out);
 
 /* ---- host-side helpers (no GPU needed) ---- */
 /* the x-slab [i0, i1) of `rank` out of `nranks` for nx cells */

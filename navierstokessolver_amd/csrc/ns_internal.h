@@ -74,6 +74,12 @@ int launch_pois_rbsor(const Geo& g, const Coef& c, double omega, const double* p
 // K4 Jacobi: out = in + w (b - shift - L in)/diag
 int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* in, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st);
+// K4 Jacobi on fp32 fields (rows of g.ld floats), fp64 arithmetic and residual partials
+int launch_pois_jacobi32(const Geo& g, const Coef& c, double omega, const float* in, float* out, const float* rp,
+                         const double* shift, double* part, hipStream_t st);
+// the slab's own rows fp64 -> fp32 and back
+void launch_to_f32(const Geo& g, const double* src, float* dst, hipStream_t st);
+void launch_to_f64(const Geo& g, const float* src, double* dst, hipStream_t st);
 // two red-black sweeps in one HBM pass (temporal blocking): same results as two calls above;
 // residual partials (if part) are of the OUTPUT iterate, and then 5 ghost rows are read
 // (4 without)

@@ -1027,6 +1027,189 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
     }
 }
 
+// ------------------------------------------------ K4 Jacobi, branch-free streaming sweep
+// The Jacobi sweep on fp64 fields (the north star's roofline kernel) and on fp32 fields
+// (configs[4]: "fp32 fields + fp64 Poisson residual", SURVEY.md 8(d) C5: 12 B/cell).  Every
+// cell's update and residual are computed in fp64 from the widened values; only the new
+// iterate is rounded (fp32), and the residual norm is summed in fp64.  The strip walk of
+// k_sweep<Jacobi> with 16 B per lane per row (fp64: 2 columns, 124 written per strip; fp32:
+// 4 columns, 248), but the row loop is branch-free: every step computes, and a lane that
+// must not write (a halo lane, a column past ny, a pipeline-fill or tail row) stores through
+// a buffer resource at an out-of-range offset, which the hardware drops.  With the stores in
+// branches the compiler's vmcnt accounting assumed the fewest issued operations at each
+// join and waited for nearly every prefetched row.  fp32 rows are ld floats long (the fp64
+// planes' ld), so a ghost row exchange is ld/2 doubles.
+typedef unsigned nsu4 __attribute__((ext_vector_type(4)));
+typedef unsigned nsu2 __attribute__((ext_vector_type(2)));
+constexpr unsigned OOB = 0xFFFFFFF0u;
+
+// A copy the compiler cannot coalesce away.  A row window (rows r-2, r-1, r) that takes the
+// freshly consumed prefetch slot by plain assignment ends up sharing the slot's register;
+// the slot's next load must then land elsewhere, and the loop latch moves it back -- a move
+// that waits for the in-flight load, which cut the effective prefetch depth to ~1 row.
+// Copying into the window at consumption time (when the value has arrived anyway) frees
+// the slot's register for its next load.
+__device__ __forceinline__ nsu4 vcopy(const nsu4 x) {
+    nsu4 y;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(y.x) : "v"(x.x));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(y.y) : "v"(x.y));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(y.z) : "v"(x.z));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(y.w) : "v"(x.w));
+    return y;
+}
+__device__ __forceinline__ double2 vcopy(const double2 x) {
+    const nsu4 y = vcopy((nsu4){(unsigned)__double2loint(x.x), (unsigned)__double2hiint(x.x),
+                                (unsigned)__double2loint(x.y), (unsigned)__double2hiint(x.y)});
+    return make_double2(__hiloint2double((int)y.y, (int)y.x), __hiloint2double((int)y.w, (int)y.z));
+}
+
+template <class T> struct Lane16;
+template <> struct Lane16<float> {
+    static constexpr int V = 4;
+    __device__ static double get(const nsu4& u, int q) { return (double)__uint_as_float(u[q]); }
+    __device__ static void put(nsu4& u, int q, double x) { u[q] = __float_as_uint((float)x); }
+};
+template <> struct Lane16<double> {
+    static constexpr int V = 2;
+    __device__ static double get(const nsu4& u, int q) { return __hiloint2double((int)u[2 * q + 1], (int)u[2 * q]); }
+    __device__ static void put(nsu4& u, int q, double x) {
+        u[2 * q] = (unsigned)__double2loint(x);
+        u[2 * q + 1] = (unsigned)__double2hiint(x);
+    }
+};
+
+template <class T>
+struct JacobiArgs {
+    const T* in;
+    T* out;
+    const T* b;
+    const double* shift;
+    const double *cw, *ce, *cs, *cn;
+    double omega;
+    int nx, ny, i0, nxl, ld;          // ld in elements
+    int nsj, nsi, L;
+    double* part;
+};
+
+template <class T, bool RES, bool NT>
+__global__ __launch_bounds__(256) void k_jacobi_s(JacobiArgs<T> a) {
+    constexpr int V = Lane16<T>::V, SWV = 62 * V;
+    __shared__ double rcs[4][RC_MAX][3];
+    const int lane = threadIdx.x & 63;
+    const int nstr = a.nsj * a.nsi;
+    const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    double (*rc)[3] = rcs[threadIdx.x >> 6];
+    if (wid < nstr) {
+        const int ib = (wid / a.nsj) * a.L;
+        for (int t = lane; t < a.L + 2 * RC_OFF && t < RC_MAX; t += 64) {
+            const int gi = min(max(a.i0 + ib - RC_OFF + t, 0), a.nx - 1);
+            const double cw = a.cw[gi], ce = a.ce[gi];
+            rc[t][0] = cw;
+            rc[t][1] = ce;
+            rc[t][2] = cw + ce;
+        }
+    }
+    __syncthreads();
+    double res = 0.0;
+    if (wid < nstr) {
+        const int si = wid / a.nsj, sj = wid - si * a.nsj;
+        const int jb = sj * SWV, ib = si * a.L;
+        const int ie = min(ib + a.L, a.nxl);
+        const int ny = a.ny, ld = a.ld;
+        const int c0 = jb - V + V * lane;
+        const int lc = min(max(c0, 0), ld - V);
+        const bool wr = lane >= 1 && lane <= 62 && c0 < ny;
+        double cs[V], cn[V];
+        bool in[V];
+#pragma unroll
+        for (int q = 0; q < V; q++) {
+            const int c = c0 + q, k = min(max(c, 0), ny - 1);
+            in[q] = c >= 0 && c < ny;
+            cs[q] = a.cs[k];
+            cn[q] = a.cn[k];
+        }
+        const double shift = a.shift ? a.shift[0] : 0.0;
+        const double omega = a.omega;
+        const int rlo = -HALO, rhi = a.nxl + HALO - 1;
+        const int r1 = ie, blo = max(ib, rlo), phi_hi = min(r1, rhi);
+        // the output plane (ghost rows included) as a buffer: offsets past its end are dropped
+        const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
+            a.out - (ptrdiff_t)HALO * ld, (short)0, (int)((unsigned)(a.nxl + 2 * HALO) * ld * (unsigned)sizeof(T)),
+            0x00020000);
+        nsu4 Q[SD], QB[SD];
+        auto load = [&](int slot_r, nsu4& p, nsu4& bb) {
+            const int lp = min(max(slot_r, rlo), phi_hi), lb = min(max(slot_r - 1, blo), rhi);
+            p = *reinterpret_cast<const nsu4*>(a.in + (ptrdiff_t)lp * ld + lc);
+            bb = *reinterpret_cast<const nsu4*>(a.b + (ptrdiff_t)lb * ld + lc);
+        };
+        nsu4 P0 = {0, 0, 0, 0}, P1 = {0, 0, 0, 0}, P2 = {0, 0, 0, 0};
+        double dg[V], wq[V], rd_last = -1.0;
+        auto step = [&](const nsu4 p, const nsu4 bb, int r) {
+            P0 = P1; P1 = P2; P2 = vcopy(p);
+            const int m = r - 1;
+            const bool live = m >= ib && m < ie;
+            const double* rw = rc[min(max(m - ib + RC_OFF, 0), RC_MAX - 1)];
+            const double cw = rw[0], ce = rw[1], rd = rw[2];
+            double xm[V], xq[V], xp[V], bq[V];
+#pragma unroll
+            for (int q = 0; q < V; q++) {
+                xm[q] = Lane16<T>::get(P0, q);
+                xq[q] = Lane16<T>::get(P1, q);
+                xp[q] = Lane16<T>::get(P2, q);
+                bq[q] = Lane16<T>::get(bb, q);
+            }
+            const double lf = __shfl_up(xq[V - 1], 1, 64), rt = __shfl_down(xq[0], 1, 64);
+            if (rd != rd_last) {   // the diagonal's row part repeats on a uniform grid
+#pragma unroll
+                for (int q = 0; q < V; q++) {
+                    dg[q] = diag<0>(rd, cs[q] + cn[q], 0.0);
+                    wq[q] = omega * rcp_nr(dg[q]);
+                }
+                rd_last = rd;
+            }
+            nsu4 o;
+#pragma unroll
+            for (int q = 0; q < V; q++) {
+                const double ym = q == 0 ? lf : xq[q - 1], yp = q == V - 1 ? rt : xq[q + 1];
+                double rr;
+                const double v = relax<0>(xq[q], xm[q], xp[q], ym, yp, bq[q] - shift, cw, ce, cs[q], cn[q], dg[q],
+                                          wq[q], 0.0, rr);
+                Lane16<T>::put(o, q, in[q] ? v : xq[q]);
+                if (RES) res += (live && wr && in[q]) ? rr * rr : 0.0;
+            }
+            const unsigned off =
+                (live && wr) ? ((unsigned)(m + HALO) * (unsigned)ld + (unsigned)c0) * (unsigned)sizeof(T) : OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(o, out, (int)off, 0, NT ? 2 : 0);
+        };
+        const int r0 = ib - 1;
+#pragma unroll
+        for (int q = 0; q < SD; q++) {
+            load(r0 + q, Q[q], QB[q]);
+            asm volatile("" ::: "memory");   // keep the slots' issue order (the loop's vmcnt bookkeeping)
+        }
+        for (int r = r0; r <= r1; r += SD) {
+#pragma unroll
+            for (int q = 0; q < SD; q++) {
+                step(Q[q], QB[q], r + q);       // rows past r1: computed, not stored
+                load(r + q + SD, Q[q], QB[q]);
+            }
+        }
+    }
+    if (RES) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
+        if (lane == 0 && wid < nstr) a.part[wid] = res;
+    }
+}
+
+// fp64 <-> fp32 copies of a slab's own rows (fp32 rows: ld floats)
+__global__ __launch_bounds__(256) void k_to_f32(const double* __restrict__ src, float* __restrict__ dst, long n) {
+    for (long k = (long)blockIdx.x * 256 + threadIdx.x; k < n; k += (long)gridDim.x * 256) dst[k] = (float)src[k];
+}
+__global__ __launch_bounds__(256) void k_to_f64(const float* __restrict__ src, double* __restrict__ dst, long n) {
+    for (long k = (long)blockIdx.x * 256 + threadIdx.x; k < n; k += (long)gridDim.x * 256) dst[k] = (double)src[k];
+}
+
 // ------------------------------------------------ K3 / K5 as streaming strips
 // The same strip walk as k_sweep (128 loaded columns, 124 written, 2 per lane, x-neighbours
 // from a 3-row register window, y-neighbours by cross-lane shuffle, rows prefetched SD ahead):
@@ -1198,6 +1381,9 @@ constexpr int SW2 = 120;
 constexpr int SW2X = 116;
 constexpr int SD2 = 3;
 constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2;
+#ifndef XR_BUF
+#define XR_BUF 0   // FUSE_R's coarse stores through buffers too (1: 172 VGPRs, 2 waves/SIMD, slower)
+#endif
 
 // one strip of k_sweep2, walked downwards (DIR = 1) or upwards (DIR = -1); returns the
 // strip's residual partial (R5)
@@ -1208,6 +1394,10 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     constexpr bool R5 = RES || XR;
     constexpr int EXT = (R5 || XP) ? 1 : 0;
     constexpr int SWc = EXT ? SW2X : SW2;
+    // BF: the branch-free row loop (buffer stores, no tail guard; Helmholtz 95 -> 88 us, FUSE_P
+    // 107 -> 104 us at 4096^2).  FUSE_R keeps plain stores: its deeper pipeline needed 172 VGPRs
+    // (2 waves/SIMD, 112 -> 160 us), and at 3 waves it spilled and still lost 3 us
+    constexpr bool BF = !XR;
     double res = 0.0;
     const int si = wid / a.nsj, sj = wid - si * a.nsj;
     const int jb = sj * SWc, ib = si * a.L;
@@ -1225,6 +1415,19 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     const double alpha = a.alpha, omega = a.omega;
     const int rlo = -HALO, rhi = a.nxl + HALO - 1;
 
+    // stores go through buffer resources based at this strip's first rows (wave-uniform,
+    // 32-bit offsets): a lane / row that must not write gets an out-of-range offset, so the
+    // row loop has no memory operation inside a branch (k_jacobi_s explains why that matters)
+    const int rb = __builtin_amdgcn_readfirstlane(ib - 1 - EXT);
+    const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + (ptrdiff_t)rb * ld, (short)0, (int)((unsigned)(a.L + 2 * EXT + 2) * ld * 8u), 0x00020000);
+    const int rbc = __builtin_amdgcn_readfirstlane(ib >> 1);
+    const __amdgpu_buffer_rsrc_t bco = __builtin_amdgcn_make_buffer_rsrc(
+        XR ? a.bc + (ptrdiff_t)rbc * a.ldc : a.out, (short)0, XR ? (int)((unsigned)((a.L >> 1) + 2) * a.ldc * 8u) : 0,
+        0x00020000);
+    const __amdgpu_buffer_rsrc_t pco = __builtin_amdgcn_make_buffer_rsrc(
+        XR ? a.pc + (ptrdiff_t)rbc * a.ldc : a.out, (short)0, XR ? (int)((unsigned)((a.L >> 1) + 2) * a.ldc * 8u) : 0,
+        0x00020000);
     double2 Q[SD2], QB[SD2], QE[SD2];
     // phi rows ib-4-EXT .. ie+3+EXT and b rows ib-3-EXT .. ie+2+EXT (the first red
     // stage's) are read; the rest are clamped onto fetched rows (see k_sweep)
@@ -1240,7 +1443,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     const bool jm_ok = Jc - 1 >= 0, jp_ok = Jc + 1 < a.ncy;
     auto load = [&](int slot_r, double2& p, double2& bb, double2& ee) {
         const int lp = min(max(slot_r, phi_lo), phi_hi), lb = min(max(slot_r - DIR, b_lo), b_hi);
-        p = ld_stream(a.in + (ptrdiff_t)lp * ld + lc, a.ntl);
+        p = ld_stream(a.in + (ptrdiff_t)lp * ld + lc, XP ? 1 : 0);   // compile-time policy: no branch
         bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
         if (XP) {
             const int I = lp >> 1;                      // floor, also for ghost rows
@@ -1295,7 +1498,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
             p.x += (9.0 * ee.x + 3.0 * ee.y + 3.0 * m0 + m1) * 0.0625;
             p.y += (9.0 * ee.x + 3.0 * ee.y + 3.0 * q0 + q1) * 0.0625;
         }
-        P0 = P1; P1 = P2; P2 = p;
+        P0 = P1; P1 = P2; P2 = (XP || !BF) ? p : vcopy(p);   // (XP: p is already a new value)
         B5 = B4; B4 = B3; B3 = B2; B2 = B1;
         B1 = make_double2(bb.x - shift, bb.y - shift);
         // stage 1: red of sweep 1 at m = r-1
@@ -1317,10 +1520,20 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
         // stage 4: black of sweep 2 at r-4, stored on the strip's rows
         const int k = r - 4 * DIR;
         double2 n4 = E1;
-        if (k >= ib - EXT && k < ie + EXT) {
-            n4 = DIR > 0 ? half(E0, E1, E2, B4, k, 1) : half(E2, E1, E0, B4, k, 1);
-            if (k >= ib && k < ie && wr) st_stream(a.out + (ptrdiff_t)k * ld + c0, n4, a.nt);
+        if (!BF) {
+            if (k >= ib - EXT && k < ie + EXT) {
+                n4 = DIR > 0 ? half(E0, E1, E2, B4, k, 1) : half(E2, E1, E0, B4, k, 1);
+                if (k >= ib && k < ie && wr) st_stream(a.out + (ptrdiff_t)k * ld + c0, n4, a.nt);
+            }
+        } else {
+            if (k >= ib - EXT && k < ie + EXT) n4 = DIR > 0 ? half(E0, E1, E2, B4, k, 1) : half(E2, E1, E0, B4, k, 1);
+            const unsigned off = (k >= ib && k < ie && wr) ? ((unsigned)(k - rb) * (unsigned)ld + (unsigned)c0) * 8u : OOB;
+            const nsu4 d = {(unsigned)__double2loint(n4.x), (unsigned)__double2hiint(n4.x),
+                            (unsigned)__double2loint(n4.y), (unsigned)__double2hiint(n4.y)};
+            __builtin_amdgcn_raw_buffer_store_b128(d, out, (int)off, 0, 2);
         }
+        unsigned coff = OOB;   // XR: the coarse cell this step completes (else dropped)
+        double cval = 0.0;
         if (R5) {
             // stage 5: residual of the finished row r-5 (FUSE_R: restricted in row pairs)
             F0 = F1; F1 = F2; F2 = n4;
@@ -1346,7 +1559,10 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
                         xs = xs + (hxr * hy1) * r1;
                         xs = xs + (hxo * hy0) * ro0;
                         xs = xs + (hxo * hy1) * ro1;
-                        if (wr) {
+                        if (XR_BUF) {
+                            if (wr) coff = ((unsigned)((m5 >> 1) - rbc) * (unsigned)a.ldc + (unsigned)(c0 >> 1)) * 8u;
+                            cval = xs / ((hxr + hxo) * (hy0 + hy1));
+                        } else if (wr) {
                             const ptrdiff_t o = (ptrdiff_t)(m5 >> 1) * a.ldc + (c0 >> 1);
                             a.bc[o] = xs / ((hxr + hxo) * (hy0 + hy1));
                             a.pc[o] = 0.0;
@@ -1359,7 +1575,10 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
                 } else {
                     xs = xs + (hxr * hy0) * r0;
                     xs = xs + (hxr * hy1) * r1;
-                    if (wr) {
+                    if (XR_BUF) {
+                        if (wr) coff = ((unsigned)((m5 >> 1) - rbc) * (unsigned)a.ldc + (unsigned)(c0 >> 1)) * 8u;
+                        cval = xs / ((hxe + hxr) * (hy0 + hy1));
+                    } else if (wr) {
                         const ptrdiff_t o = (ptrdiff_t)(m5 >> 1) * a.ldc + (c0 >> 1);
                         a.bc[o] = xs / ((hxe + hxr) * (hy0 + hy1));
                         a.pc[o] = 0.0;
@@ -1367,15 +1586,23 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
                 }
             }
         }
+        if (XR && XR_BUF) {
+            __builtin_amdgcn_raw_buffer_store_b64(
+                (nsu2){(unsigned)__double2loint(cval), (unsigned)__double2hiint(cval)}, bco, (int)coff, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64((nsu2){0u, 0u}, pco, (int)coff, 0, 0);
+        }
     };
 
     const int rs = DIR > 0 ? r0 : r1, nr = r1 - r0 + 1;
 #pragma unroll
-    for (int q = 0; q < SD2; q++) load(rs + DIR * q, Q[q], QB[q], QE[q]);
+    for (int q = 0; q < SD2; q++) {
+        load(rs + DIR * q, Q[q], QB[q], QE[q]);
+        if (BF) asm volatile("" ::: "memory");   // keep the slots' issue order (the loop's vmcnt bookkeeping)
+    }
     for (int t = 0; t < nr; t += SD2) {
 #pragma unroll
         for (int q = 0; q < SD2; q++) {
-            if (t + q < nr) step(Q[q], QB[q], QE[q], rs + DIR * (t + q));
+            if (BF || t + q < nr) step(Q[q], QB[q], QE[q], rs + DIR * (t + q));   // (BF: steps past the strip store nothing)
             load(rs + DIR * (t + q + SD2), Q[q], QB[q], QE[q]);
         }
     }
@@ -2583,9 +2810,54 @@ int launch_helm_sweepN(int ns, const Geo& g, const Coef& c, double alpha, double
     return -1;
 }
 
+// -1 if the plane does not fit the kernel's 32-bit buffer offsets
+template <class T>
+static int launch_jacobi_s(const Geo& g, const Coef& c, double omega, const T* in, T* out, const T* rp,
+                           const double* shift, double* part, hipStream_t st) {
+    if ((size_t)(g.nxl + 2 * HALO) * g.ld * sizeof(T) >= (size_t)OOB) return -1;
+    JacobiArgs<T> a{};
+    a.in = in; a.out = out; a.b = rp; a.shift = shift;
+    a.cw = c.pw; a.ce = c.pe; a.cs = c.ps; a.cn = c.pn;
+    a.omega = omega;
+    a.nx = g.nx; a.ny = g.ny; a.i0 = g.i0; a.nxl = g.nxl; a.ld = g.ld;
+    constexpr int SWV = 62 * Lane16<T>::V;
+    a.nsj = (g.ny + SWV - 1) / SWV;
+    a.part = part;
+    const char* e = getenv("NSGPU_NT_STORES");
+    const bool nt = e ? std::atoi(e) != 0 : true;
+    const void* k = part ? (nt ? (const void*)k_jacobi_s<T, true, true> : (const void*)k_jacobi_s<T, true, false>)
+                         : (nt ? (const void*)k_jacobi_s<T, false, true> : (const void*)k_jacobi_s<T, false, false>);
+    a.L = strip_rows(a.nxl, a.nsj, resident_waves(k), 4);
+    a.nsi = (a.nxl + a.L - 1) / a.L;
+    const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
+    void* args[] = {&a};
+    if (hipLaunchKernel(k, dim3(nblk), dim3(256), args, 0, st) != hipSuccess) return -1;
+    return nstr;
+}
+
 int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* in, double* out, const double* rp,
                        const double* shift, double* part, hipStream_t st) {
+    // the branch-free streaming sweep; NSGPU_JACOBI_SWEEP=0, or a plane past 4 GiB: k_sweep<Jacobi>
+    static const int js = getenv("NSGPU_JACOBI_SWEEP") ? std::atoi(getenv("NSGPU_JACOBI_SWEEP")) : 1;
+    if (js) {
+        const int n = launch_jacobi_s<double>(g, c, omega, in, out, rp, shift, part, st);
+        if (n >= 0) return n;
+    }
     return launch_stream<0, false>(stream_args(g, c, in, out, rp, shift, 0.0, omega, part, false), st);
+}
+
+int launch_pois_jacobi32(const Geo& g, const Coef& c, double omega, const float* in, float* out, const float* rp,
+                         const double* shift, double* part, hipStream_t st) {
+    return launch_jacobi_s<float>(g, c, omega, in, out, rp, shift, part, st);
+}
+
+void launch_to_f32(const Geo& g, const double* src, float* dst, hipStream_t st) {
+    const long n = (long)g.nxl * g.ld;
+    hipLaunchKernelGGL(k_to_f32, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, st, src, dst, n);
+}
+void launch_to_f64(const Geo& g, const float* src, double* dst, hipStream_t st) {
+    const long n = (long)g.nxl * g.ld;
+    hipLaunchKernelGGL(k_to_f64, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, st, src, dst, n);
 }
 
 int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,

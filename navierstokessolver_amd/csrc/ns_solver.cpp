@@ -132,6 +132,8 @@ struct ns_solver {
     double *usm = nullptr, *vsm = nullptr, *usm_mem = nullptr;   // u*^{n-1}, v*^{n-1}
     int us_valid = 0;            // 0: no u* kept; 1: TMPU/TMPV hold u*^n; 2: and usm/vsm u*^{n-1}
     double* phim_mem = nullptr;  // the extra planes' allocation
+    float* f32_mem = nullptr;    // fp32-field sweep planes (configs[4]), allocated on first use
+    float* f32[3] = {};          // phi, its ping-pong partner, rhs_phi (rows of g.ld floats)
     int phim_valid = 0;          // history planes holding data (0 after a reset / an injected phi)
     int verbose = 0;             // NSGPU_VERBOSE=1: solver residual histories on stderr
     long pair_min_cells = 2048L * 2048L;   // NSGPU_PAIR_MIN_CELLS: smallest level smoothed in 2-sweep passes
@@ -371,6 +373,45 @@ int pois_sweep(ns_solver* s, double* part) {
                                     s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, part, s->st);
     std::swap(s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP]);
     return nb;
+}
+
+// fp32-field planes (phi, partner, rhs), zeroed once: the ghost rows and the row padding stay finite
+int ensure_f32(ns_solver* s) {
+    if (s->f32_mem) return 0;
+    if (hipMalloc(&s->f32_mem, 3 * s->plane * sizeof(float)) != hipSuccess) {
+        set_err("hipMalloc of the fp32 planes failed");
+        return NS_ENOMEM;
+    }
+    HIPCHK(hipMemsetAsync(s->f32_mem, 0, 3 * s->plane * sizeof(float), s->st));
+    for (int k = 0; k < 3; k++) s->f32[k] = s->f32_mem + k * s->plane + (size_t)nsg::HALO * s->g.ld;
+    return 0;
+}
+
+// the fp32 planes seen as rows of g.ld / 2 doubles (the ghost-row exchange moves doubles)
+nsg::Geo f32_view(const ns_solver* s) {
+    nsg::Geo v = s->g;
+    v.ld = s->g.ld / 2;
+    return v;
+}
+
+// one fp32-field Jacobi sweep f32[0] -> f32[1] (residual partials of the input), then swap
+int pois_sweep32(ns_solver* s, double* part, int* nb) {
+    const nsg::Geo v = f32_view(s);
+    CHK(halo_g(s, v, {reinterpret_cast<double*>(s->f32[0])}, 1));
+    *nb = nsg::launch_pois_jacobi32(s->g, s->c, s->omega, s->f32[0], s->f32[1], s->f32[2], s->scal + S_SHIFT,
+                                    part ? part : s->part, s->st);
+    if (*nb < 0) { set_err("fp32 Jacobi sweep: launch failed or plane past 4 GiB"); return NS_EINVAL; }
+    std::swap(s->f32[0], s->f32[1]);
+    return 0;
+}
+
+// phi, rhs_phi -> the fp32 planes
+int to_f32(ns_solver* s) {
+    CHK(ensure_f32(s));
+    nsg::launch_to_f32(s->g, s->arr[NS_ARR_PHI], s->f32[0], s->st);
+    nsg::launch_to_f32(s->g, s->arr[NS_ARR_RPHI], s->f32[2], s->st);
+    HIPCHK(hipGetLastError());
+    return 0;
 }
 
 int next_batch(int prev_batch, double prev_r2, int prev_at, double r2, int at, double tol2, int cap) {
@@ -1559,6 +1600,7 @@ void ns_destroy(ns_solver* s) {
     if (s->phim_mem) (void)hipFree(s->phim_mem);
     if (s->kv_mem) (void)hipFree(s->kv_mem);
     if (s->usm_mem) (void)hipFree(s->usm_mem);
+    if (s->f32_mem) (void)hipFree(s->f32_mem);
     if (s->fc_mem) (void)hipFree(s->fc_mem);
     if (s->et_mem) (void)hipFree(s->et_mem);
     if (s->ksc) (void)hipFree(s->ksc);
@@ -1770,6 +1812,20 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         if (out) out[0] = s->hs[S_AUX];
         return 0;
     }
+    case NS_K_POISSON32: {
+        if (s->kv[0]) { set_err("NS_K_POISSON32 sweeps the rectangle's wall-closure operator (no NEUMANN side, no mask)"); return NS_EINVAL; }
+        int nb = 0;
+        CHK(to_f32(s));
+        for (int k = 0; k < iters; k++) CHK(pois_sweep32(s, k == iters - 1 ? s->part : nullptr, &nb));
+        nsg::launch_to_f64(s->g, s->f32[0], s->arr[NS_ARR_PHI], s->st);
+        if (iters > 0) {
+            nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
+            CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
+        }
+        CHK(fetch(s));
+        if (out) out[0] = s->hs[S_RES];
+        return 0;
+    }
     default:
         set_err("unknown kernel %d", which);
         return NS_EINVAL;
@@ -1853,6 +1909,34 @@ int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
     float span = 0.f;
     HIPCHK(hipEventElapsedTime(&span, s->ev[0], s->ev[2 * iters - 1]));
     if (out) { out[0] = tot / iters; out[1] = tot; out[2] = span; }
+    return 0;
+}
+
+int ns_time_poisson_fp32(ns_solver* s, int warmup, int iters, double* out) {
+    if (!s || iters <= 0) { set_err("bad arguments"); return NS_EINVAL; }
+    if (s->kv[0]) { set_err("ns_time_poisson_fp32 times the rectangle's sweeps (no NEUMANN side, no mask)"); return NS_EINVAL; }
+    HIPCHK(hipSetDevice(s->device));
+    CHK(ensure_events(s, 2 * (size_t)iters));
+    CHK(to_f32(s));
+    int nb = 0;
+    for (int k = 0; k < warmup; k++) CHK(pois_sweep32(s, nullptr, &nb));
+    for (int k = 0; k < iters; k++) {
+        HIPCHK(hipEventRecord(s->ev[2 * k], s->st));
+        CHK(pois_sweep32(s, nullptr, &nb));
+        HIPCHK(hipEventRecord(s->ev[2 * k + 1], s->st));
+    }
+    nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
+    CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
+    CHK(fetch(s));
+    double tot = 0.0;
+    for (int k = 0; k < iters; k++) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
+        tot += ms;
+    }
+    float span = 0.f;
+    HIPCHK(hipEventElapsedTime(&span, s->ev[0], s->ev[2 * iters - 1]));
+    if (out) { out[0] = tot / iters; out[1] = tot; out[2] = span; out[3] = s->hs[S_RES]; }
     return 0;
 }
 

@@ -158,3 +158,10 @@ class GpuSolver:
         out = np.zeros(3, dtype=np.float64)
         L.check(L.lib().ns_time_poisson(self._h, warmup, iters, _dptr(out)))
         return {"avg_ms": out[0], "total_ms": out[1], "span_ms": out[2]}
+
+    def time_poisson_fp32(self, warmup: int, iters: int):
+        """Jacobi sweeps on fp32 copies of phi, rhs_phi (configs[4]); also the fp64-summed
+        residual^2 of the last sweep's input."""
+        out = np.zeros(4, dtype=np.float64)
+        L.check(L.lib().ns_time_poisson_fp32(self._h, warmup, iters, _dptr(out)))
+        return {"avg_ms": out[0], "total_ms": out[1], "span_ms": out[2], "res2": out[3]}

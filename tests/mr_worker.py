@@ -25,6 +25,8 @@ ap.add_argument("--output", required=True)
 ap.add_argument("--bc", default="", help="edge BCs W,N,E,S as type:info,... (default: the cavity)")
 ap.add_argument("--ratio", type=float, default=-1.0, help="geometric x and y spacing ratio (Grid.cpp)")
 ap.add_argument("--poly", default="", help="a tests/polygons.py geometry instead of the rectangle")
+ap.add_argument("--sweep32", type=int, default=0,
+                help="instead of time steps: K fp32-field Jacobi sweeps (NS_K_POISSON32) of the random input")
 ap.add_argument("--stats-only", action="store_true", help="gather only the per-step stats (large grids)")
 a = ap.parse_args()
 dist.init_process_group("gloo")
@@ -48,8 +50,14 @@ try:
         grid = nsa.polygon(P["vertices"], og.hx, og.hy, P["bc"])
     else:
         grid = nsa.rectangle(n, ny, bc=bc, xratio=a.ratio, yratio=a.ratio)
+    if a.sweep32:
+        kw.update(poisson=nsa.NS_POISSON_JACOBI, omega=0.8)
     gs = nsa.GpuSolver(grid, 1.0 / (8 * n), 100.0, **kw)
-    mm = [list(gs.step().values())[:7] for _ in range(a.nsteps)]
+    if a.sweep32:
+        gs.fill_random(0x5EED)
+        mm = [list(gs.kernel(nsa.NS_K_POISSON32, a.sweep32)[:1])]
+    else:
+        mm = [list(gs.step().values())[:7] for _ in range(a.nsteps)]
     u, v, phi = (np.zeros((1, ny)),) * 3 if a.stats_only else gs.fields()
 except Exception as e:  # report, don't hang the other rank
     status = f"error: {e}"

@@ -128,6 +128,22 @@ def test_stretched_slabs_match_single_rank(tmp_path):
     assert du <= 1e-8 and dv <= 1e-8, (du, dv)
 
 
+@pytest.mark.parametrize("n,ny,nproc", [(64, 600, 2), (90, 250, 3)])
+def test_fp32_jacobi_slabs_match_single_rank(tmp_path, n, ny, nproc):
+    """fp32-field Jacobi sweeps (configs[4]) on slabs: the float ghost rows travel as ld/2
+    doubles; every cell's update is decomposition-independent, so phi is bit-identical."""
+    k = 7
+    r = launch(tmp_path, "--xport", "host", "--size", str(n), "--size-y", str(ny), "--sweep32", str(k),
+               nproc=nproc, port=29611 + nproc)
+    assert str(r["status"]) == "ok", r["status"]
+    gs = nsa.GpuSolver(nsa.rectangle(n, ny), 1.0 / (8 * n), 100.0, poisson=nsa.NS_POISSON_JACOBI, omega=0.8, device=0)
+    gs.fill_random(0x5EED)
+    res = gs.kernel(nsa.NS_K_POISSON32, k)[0]
+    phi = gs.fields()[2]
+    assert np.array_equal(r["phi"], phi)
+    assert abs(r["mm"][0, 0] - res) <= 1e-12 * res
+
+
 def test_rccl_two_ranks_one_gpu_probe(tmp_path):
     """RCCL usually rejects two ranks on one device; record what it does (never fails the suite
     unless RCCL ran and produced a wrong answer)."""

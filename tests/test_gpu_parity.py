@@ -119,6 +119,32 @@ def test_k4_jacobi_sweeps(gpu, nx, ny):
     assert abs(out[0] - r2) <= 1e-10 * r2
 
 
+@pytest.mark.parametrize("nx,ny,xr", [(24, 24, -1), (37, 130, -1), (256, 256, -1), (70, 1000, -1), (40, 5, -1),
+                                       (33, 300, 1.02)])
+def test_k4_jacobi_fp32_fields(gpu, nx, ny, xr):
+    """configs[4]'s fp32-field Jacobi sweep (NS_K_POISSON32): phi, b stored as floats, each
+    update and the residual in fp64.  Tolerances: vs the oracle's fp64 sweep with the iterate
+    rounded to fp32 after every sweep (the same arithmetic), <= 1e-6 relative (a few fp32 ulps
+    where FMA contraction flips a rounding); vs the plain fp64 sweeps <= 1e-5 relative (the
+    fp32-field bound; SURVEY.md 8(c) allows 1e-4)."""
+    rng = np.random.default_rng(15)
+    og, gs = pair(gpu, nx, ny, 1e-3, 100.0, xratio=xr, yratio=xr, poisson=gpu.NS_POISSON_JACOBI, omega=0.8)
+    phi, b = rand(rng, nx * ny), rand(rng, nx * ny, 50.0)
+    gs.set(gpu.NS_ARR_PHI, phi); gs.set(gpu.NS_ARR_RPHI, b)
+    f32 = lambda a: np.asarray(a, dtype=np.float32).astype(np.float64)
+    b32, p32, p64 = f32(b), f32(phi), phi.copy()
+    for k in range(5):
+        p, r2 = og.jacobi_sweep(p32, b32, b.mean(), 0.8)
+        p32 = f32(p)
+        p64, _ = og.jacobi_sweep(p64, b, b.mean(), 0.8)
+    out = gs.kernel(gpu.NS_K_POISSON32, 5)
+    got = gs.get(gpu.NS_ARR_PHI)
+    assert np.array_equal(got, f32(got))                 # the result is the fp32 iterate
+    assert rel(got, p32) <= 1e-6
+    assert rel(got, p64) <= 1e-5
+    assert abs(out[0] - r2) <= 1e-6 * r2                 # fp64-summed residual of the last input
+
+
 @pytest.mark.parametrize("nx,ny,xr", [(24, 24, -1), (37, 130, -1), (40, 33, 1.05)])
 def test_k2_helmholtz_sweeps(gpu, nx, ny, xr):
     rng = np.random.default_rng(6)
