@@ -100,6 +100,9 @@ int launch_pois_jacobi_tiled(const Geo& g, const Coef& c, double omega, const do
                              const double* rp, const double* shift, double* part, hipStream_t st);
 // rows per streaming strip (tuning knob)
 void set_strip_rows(int L);
+// strip subset of the following two-sweep pass launches (k_sweep2): 0 all, 1 the strips
+// whose read cone lies inside the slab, 2 the others (exchange / compute overlap)
+void set_strip_phase(int phase);
 // residual only
 int launch_pois_residual(const Geo& g, const Coef& c, const double* phi, const double* rp,
                          const double* shift, double* part, hipStream_t st);

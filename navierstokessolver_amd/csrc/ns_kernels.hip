@@ -834,6 +834,9 @@ struct StreamArgs {
     int nt;                           // non-temporal output stores
     int alt;                          // alternate strips walk upwards
     int ntl;                          // non-temporal iterate loads
+    // strip subset of this launch (k_sweep2; exchange / compute overlap): launch strip-row k
+    // is strip row k if k < slo, else shi0 + (k - slo); nrun strip rows in all
+    int slo, shi0, nrun;
 };
 
 // diagonal of the operator at a cell from its row / column coefficient sums
@@ -1615,24 +1618,26 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
     constexpr bool R5 = RES || XR;                 // the fifth (output residual) stage
     __shared__ double rcs[4][RC_MAX][4];
     const int lane = threadIdx.x & 63;
-    const int nstr = a.nsj * a.nsi;
-    const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    const int nstr = a.nsj * a.nrun;
+    const int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
     double (*rc)[4] = rcs[threadIdx.x >> 6];
-    if (wid < nstr) stage_rows<OP>(a, rc, (wid / a.nsj) * a.L, lane);
+    // this wave's strip (row si of the slab's strips): the launch may cover a subset of them
+    const int run = w / a.nsj, si = run < a.slo ? run : a.shi0 + (run - a.slo);
+    const int wid = si * a.nsj + (w - run * a.nsj);
+    if (w < nstr) stage_rows<OP>(a, rc, si * a.L, lane);
     __syncthreads();
     double res = 0.0;
-    if (wid < nstr) {
+    if (w < nstr) {
         // alternate strips walk in opposite directions (a.alt): the halo rows two strips
         // share are then read by both at about the same time -- an L2 hit for the second --
         // instead of at opposite ends of the kernel (each row band read twice from HBM)
-        const int si = wid / a.nsj;
         if (a.alt && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1>(a, rc, wid, lane);
         else res = sweep2_strip<OP, RES, FUSE, 1>(a, rc, wid, lane);
     }
     if (R5) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
-        if (lane == 0 && wid < nstr) a.part[wid] = res;
+        if (lane == 0 && w < nstr) a.part[wid] = res;
     }
 }
 
@@ -2675,6 +2680,25 @@ static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, dou
     return a;
 }
 
+// Exchange / compute overlap (multi-rank): the solver launches a pass twice, first the
+// strips whose rows (and read cone of `depth` rows) lie inside the slab -- while the ghost
+// rows are still in flight on the comm stream -- then, after the exchange, the edge strips.
+static int g_phase = 0;   // 0: all strips, 1: interior, 2: edges
+void set_strip_phase(int phase) { g_phase = phase; }
+
+// the strip subset of the current phase (k_sweep2 launchers); returns the workgroup count
+// (0: nothing to launch)
+static int apply_phase(StreamArgs& a, int depth) {
+    a.slo = a.nsi; a.shi0 = 0; a.nrun = a.nsi;
+    if (g_phase) {
+        const int sa = (depth + a.L - 1) / a.L;                  // first strip clear of the low ghosts
+        const int sb = std::max(sa, (a.nxl - depth) / a.L);      // strips [sa, sb) are interior
+        if (g_phase == 1) { a.slo = 0; a.shi0 = sa; a.nrun = sb - sa; }
+        else { a.slo = sa; a.shi0 = sb; a.nrun = sa + (a.nsi - sb); }
+    }
+    return (a.nsj * a.nrun + 3) / 4;
+}
+
 // count_only: return the strip (= partial) count a launch with residual would have, launch nothing
 template <int OP, bool RB>
 static int launch_stream(StreamArgs a, hipStream_t st, bool count_only = false) {
@@ -2704,8 +2728,8 @@ static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st, bool count
                                            : (const void*)k_sweep2<OP, false, FUSE_NONE>);
     a.L = strip_rows(a.nxl, a.nsj, cap, 16);
     a.nsi = (g.nxl + a.L - 1) / a.L;
-    const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
-    if (count_only) return nstr;
+    const int nstr = a.nsj * a.nsi, nblk = apply_phase(a, a.part ? 5 : 4);
+    if (count_only || !nblk) return nstr;
     if (a.part) hipLaunchKernelGGL((k_sweep2<OP, true, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_sweep2<OP, false, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
@@ -2719,8 +2743,8 @@ int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const
     a.nsj = (g.ny + SW2X - 1) / SW2X;
     a.L = strip_rows(a.nxl, a.nsj, resident_waves((const void*)k_sweep2<0, false, FUSE_R>), 16);
     a.nsi = (g.nxl + a.L - 1) / a.L;
-    const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
-    hipLaunchKernelGGL((k_sweep2<0, false, FUSE_R>), dim3(nblk), dim3(256), 0, st, a);
+    const int nstr = a.nsj * a.nsi, nblk = apply_phase(a, 5);
+    if (nblk) hipLaunchKernelGGL((k_sweep2<0, false, FUSE_R>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 
@@ -2735,8 +2759,8 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
     a.nsj = (g.ny + SW2X - 1) / SW2X;
     a.L = strip_rows(a.nxl, a.nsj, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 16);
     a.nsi = (g.nxl + a.L - 1) / a.L;
-    const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
-    hipLaunchKernelGGL((k_sweep2<0, false, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
+    const int nstr = a.nsj * a.nsi, nblk = apply_phase(a, 5);
+    if (nblk) hipLaunchKernelGGL((k_sweep2<0, false, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 

@@ -137,6 +137,11 @@ struct ns_solver {
     int phim_valid = 0;          // history planes holding data (0 after a reset / an injected phi)
     int verbose = 0;             // NSGPU_VERBOSE=1: solver residual histories on stderr
     long pair_min_cells = 2048L * 2048L;   // NSGPU_PAIR_MIN_CELLS: smallest level smoothed in 2-sweep passes
+    // multi-rank: ghost-row exchanges of the two-sweep passes run on a comm stream while the
+    // pass's interior strips run (NSGPU_OVERLAP=0: exchange, then the whole pass)
+    int overlap = 1;
+    hipStream_t cst = nullptr;
+    hipEvent_t xev[2] = {nullptr, nullptr};
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
     int mg_pre = 2, mg_post = 2, mg_coarse_iters = 0;
     double mg_omega_c = 1.0, mg_omega_s = 1.1;
@@ -178,7 +183,8 @@ struct HaloReq {
 
 // ghost rows to / from the x-neighbours; every request of the list goes in ONE RCCL group
 // (one latency for all of them)
-int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq) {
+int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs = nullptr) {
+    if (!xs) xs = s->st;
     if (s->nranks == 1) return 0;
     const bool lo = s->rank > 0, hi = s->rank < s->nranks - 1;
     if (s->ht.exchange) {
@@ -189,17 +195,17 @@ int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq) {
             double* f = q.f;
             CHK(ensure_stage(s, 4 * cnt));
             double *slo = s->stage, *shi = slo + cnt, *rlo = shi + cnt, *rhi = rlo + cnt;
-            if (lo) HIPCHK(hipMemcpyAsync(slo, f, cnt * 8, hipMemcpyDeviceToHost, s->st));
-            if (hi) HIPCHK(hipMemcpyAsync(shi, f + (ptrdiff_t)(nxl - q.w) * ld, cnt * 8, hipMemcpyDeviceToHost, s->st));
-            HIPCHK(hipStreamSynchronize(s->st));
+            if (lo) HIPCHK(hipMemcpyAsync(slo, f, cnt * 8, hipMemcpyDeviceToHost, xs));
+            if (hi) HIPCHK(hipMemcpyAsync(shi, f + (ptrdiff_t)(nxl - q.w) * ld, cnt * 8, hipMemcpyDeviceToHost, xs));
+            HIPCHK(hipStreamSynchronize(xs));
             if (s->ht.exchange(s->ht.user, lo ? slo : nullptr, hi ? shi : nullptr, lo ? rlo : nullptr,
                                hi ? rhi : nullptr, (int64_t)cnt) != 0) {
                 set_err("host transport exchange failed");
                 return NS_ERCCL;
             }
-            if (lo) HIPCHK(hipMemcpyAsync(f - (ptrdiff_t)q.w * ld, rlo, cnt * 8, hipMemcpyHostToDevice, s->st));
-            if (hi) HIPCHK(hipMemcpyAsync(f + (ptrdiff_t)nxl * ld, rhi, cnt * 8, hipMemcpyHostToDevice, s->st));
-            HIPCHK(hipStreamSynchronize(s->st));
+            if (lo) HIPCHK(hipMemcpyAsync(f - (ptrdiff_t)q.w * ld, rlo, cnt * 8, hipMemcpyHostToDevice, xs));
+            if (hi) HIPCHK(hipMemcpyAsync(f + (ptrdiff_t)nxl * ld, rhi, cnt * 8, hipMemcpyHostToDevice, xs));
+            HIPCHK(hipStreamSynchronize(xs));
         }
         return 0;
     }
@@ -210,16 +216,44 @@ int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq) {
         const int ld = q.g->ld, nxl = q.g->nxl;
         double* f = q.f;
         if (lo) {
-            NCCLCHK(ncclSend(f, cnt, ncclDouble, s->rank - 1, s->comm, s->st));
-            NCCLCHK(ncclRecv(f - (ptrdiff_t)q.w * ld, cnt, ncclDouble, s->rank - 1, s->comm, s->st));
+            NCCLCHK(ncclSend(f, cnt, ncclDouble, s->rank - 1, s->comm, xs));
+            NCCLCHK(ncclRecv(f - (ptrdiff_t)q.w * ld, cnt, ncclDouble, s->rank - 1, s->comm, xs));
         }
         if (hi) {
-            NCCLCHK(ncclSend(f + (ptrdiff_t)(nxl - q.w) * ld, cnt, ncclDouble, s->rank + 1, s->comm, s->st));
-            NCCLCHK(ncclRecv(f + (ptrdiff_t)nxl * ld, cnt, ncclDouble, s->rank + 1, s->comm, s->st));
+            NCCLCHK(ncclSend(f + (ptrdiff_t)(nxl - q.w) * ld, cnt, ncclDouble, s->rank + 1, s->comm, xs));
+            NCCLCHK(ncclRecv(f + (ptrdiff_t)nxl * ld, cnt, ncclDouble, s->rank + 1, s->comm, xs));
         }
     }
     NCCLCHK(ncclGroupEnd());
     return 0;
+}
+
+// A two-sweep pass whose ghost rows must be exchanged first: the pass's interior strips (their
+// read cone inside the slab) are launched on the compute stream, the exchange runs on the comm
+// stream meanwhile, and the edge strips follow once it is done (nsg::set_strip_phase).  Every
+// RCCL call stays totally ordered across streams: the exchange waits for everything before the
+// pass, and everything after it waits for the exchange.  `launch` launches the pass (k_sweep2
+// launchers only) and returns its partial count or < 0.
+int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs);
+template <class F>
+int overlapped(ns_solver* s, const HaloReq* reqs, int nreq, F&& launch) {
+    if (s->nranks == 1 || !s->overlap || !s->cst) {
+        CHK(halo_reqs(s, reqs, nreq, s->st));
+        return launch();
+    }
+    HIPCHK(hipEventRecord(s->xev[0], s->st));
+    nsg::set_strip_phase(1);
+    int n = launch();
+    nsg::set_strip_phase(0);
+    if (n < 0) return n;
+    HIPCHK(hipStreamWaitEvent(s->cst, s->xev[0], 0));
+    CHK(halo_reqs(s, reqs, nreq, s->cst));
+    HIPCHK(hipEventRecord(s->xev[1], s->cst));
+    HIPCHK(hipStreamWaitEvent(s->st, s->xev[1], 0));
+    nsg::set_strip_phase(2);
+    n = launch();
+    nsg::set_strip_phase(0);
+    return n;
 }
 
 int halo_reqs(ns_solver* s, std::initializer_list<HaloReq> reqs) {
@@ -338,10 +372,23 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
             const bool last = k + w >= n;
             double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
             const int hw = w == 2 ? (part ? 5 : 4) : 2;
-            if (which == 3) CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, hw));
-            else if (w <= 2) CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
-            nb = w >= 2 ? helm_sweep2(s, alpha, part, which, w) : helm_sweep(s, alpha, part, which);
-            if (nb < 0) return NS_EHIP;
+            if (which == 3 && w == 2 && !s->tiled) {
+                // multi-rank pair pass: u and v ghost rows in one exchange, overlapped
+                const HaloReq r[2] = {{&s->g, s->arr[NS_ARR_U], hw}, {&s->g, s->arr[NS_ARR_V], hw}};
+                nb = overlapped(s, r, 2, [&]() {
+                    return nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
+                                                   s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
+                                                   s->arr[NS_ARR_RV], part, s->st, 3);
+                });
+                if (nb < 0) return nb;
+                std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
+                std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
+            } else {
+                if (which == 3) CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, hw));
+                else if (w <= 2) CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
+                nb = w >= 2 ? helm_sweep2(s, alpha, part, which, w) : helm_sweep(s, alpha, part, which);
+                if (nb < 0) return NS_EHIP;
+            }
             const int at = w >= 2 ? k + w : k;   // a multi-sweep pass reports its output's residual
             if (launch == 0) {
                 if (nb_first) *nb_first = nb;
@@ -733,11 +780,23 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
         if (fused_restrict(s, l)) {
             // last two pre-smoothing sweeps + residual + restriction in one HBM pass
             CHK(mg_smooth(s, l, s->mg_pre - 2, tn, ev0));
-            CHK(halo_l(s, l, {F.phi}, 5));
             const bool t = s->timing && l == 0 && !s->pc_active;
             if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st)); s->evtag[ev0 + *tn] = 1; }
-            nb = (tile_level(s, l) ? nsg::launch_pois_tile2_restrict : nsg::launch_pois_rbsor2_restrict)(
-                F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b, cv.phi, s->part, s->st);
+            if (tile_level(s, l)) {
+                CHK(halo_l(s, l, {F.phi}, 5));
+                nb = nsg::launch_pois_tile2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b, cv.phi,
+                                                     s->part, s->st);
+            } else if (F.repl) {
+                nb = nsg::launch_pois_rbsor2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b,
+                                                      cv.phi, s->part, s->st);
+            } else {
+                const HaloReq r[1] = {{&F.g, F.phi, 5}};
+                nb = overlapped(s, r, 1, [&]() {
+                    return nsg::launch_pois_rbsor2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g,
+                                                            cv.b, cv.phi, s->part, s->st);
+                });
+                if (nb < 0) return nb;
+            }
             if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn) + 1], s->st)); (*tn)++; }
             std::swap(F.phi, F.tmp);
             if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
@@ -762,14 +821,25 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
         if (fused_prolong(s, l)) {
             // prolongation + the first two post-smoothing sweeps in one HBM pass; the coarse
             // and fine ghost rows travel in one group
-            if (!F.repl) {
+            const bool t = s->timing && l == 0 && !s->pc_active;
+            const double* shp = l == 0 ? shift0(s) : nullptr;
+            auto pass = [&]() {
+                return (tile_level(s, l) ? nsg::launch_pois_tile2_prolong : nsg::launch_pois_rbsor2_prolong)(
+                    F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, shp, cv.g, cv.phi, s->st);
+            };
+            if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st)); s->evtag[ev0 + *tn] = 0; }
+            if (F.repl) {
+                pass();
+            } else if (tile_level(s, l)) {
                 if (cv.gather || C.repl) CHK(halo_l(s, l, {F.phi}, 5));
                 else CHK(halo_reqs(s, {HaloReq{&C.g, C.phi, 3}, HaloReq{&F.g, F.phi, 5}}));
+                pass();
+            } else {
+                // (the coarse ghost rows are read by the edge strips only)
+                const HaloReq r[2] = {{&F.g, F.phi, 5}, {&C.g, C.phi, 3}};
+                const int n = overlapped(s, r, (cv.gather || C.repl) ? 1 : 2, pass);
+                if (n < 0) return n;
             }
-            const bool t = s->timing && l == 0 && !s->pc_active;
-            if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st)); s->evtag[ev0 + *tn] = 0; }
-            (tile_level(s, l) ? nsg::launch_pois_tile2_prolong : nsg::launch_pois_rbsor2_prolong)(
-                F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, l == 0 ? shift0(s) : nullptr, cv.g, cv.phi, s->st);
             if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn) + 1], s->st)); (*tn)++; }
             std::swap(F.phi, F.tmp);
             if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
@@ -1497,6 +1567,16 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     s->device = dev;
     if (hipSetDevice(dev) != hipSuccess) { set_err("hipSetDevice(%d) failed", dev); return fail(NS_EHIP); }
     if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); return fail(NS_EHIP); }
+    if (p->nranks > 1) {
+        const char* ov = getenv("NSGPU_OVERLAP");
+        s->overlap = ov ? std::atoi(ov) != 0 : 1;
+        if (hipStreamCreateWithFlags(&s->cst, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&s->xev[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s->xev[1], hipEventDisableTiming) != hipSuccess) {
+            set_err("comm stream / event create failed");
+            return fail(NS_EHIP);
+        }
+    }
 
     s->plane = (size_t)(g.nxl + 2 * nsg::HALO) * g.ld;
     if (hipMalloc(&s->base, s->plane * NS_NUM_ARR * sizeof(double)) != hipSuccess) {
@@ -1609,6 +1689,10 @@ void ns_destroy(ns_solver* s) {
     if (s->scal) (void)hipFree(s->scal);
     if (s->hs) (void)hipHostFree(s->hs);
     if (s->stage) (void)hipHostFree(s->stage);
+    if (s->cst) (void)hipStreamSynchronize(s->cst);
+    for (auto e : s->xev)
+        if (e) (void)hipEventDestroy(e);
+    if (s->cst) (void)hipStreamDestroy(s->cst);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
 }
