@@ -1,0 +1,76 @@
+"""GPU parity at BASELINE.json's own sizes (configs[1] 2048^2, configs[2] 4096^2, configs[4]
+16384^2), where the small-grid tests of test_gpu_parity.py do not reach:
+
+  * full time steps vs the oracle (oracle/ns_oracle.c running the same multigrid + RB-SOR
+    algorithm, oracle/oracle.py OSolver.use_gpu_algorithm), both solves to rtol 1e-12 so the
+    two converged answers differ only by solver round-off: max |du|, |dv| <= 1e-9, the
+    monitor (umin, umax, vmin, vmax) to 1e-9 (tolerances written per test);
+  * the fp32-field Jacobi sweep (configs[4]) against the fp64 sweep kernel on the same random
+    input: every value is a float32, and the difference is fp32 rounding only (<= 1e-5
+    relative after 5 sweeps);
+  * the x-slab path at 4096^2 (2 ranks, host transport, production hierarchy: levels 0-1
+    distributed, 2-6 replicated): the per-step monitor equals the single-rank run to 1e-12.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import OGrid, OSolver
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("n,steps", [(2048, 3), (4096, 1)])
+def test_cavity_steps_vs_oracle_at_config_size(gpu, n, steps):
+    dt, re, rtol = 1.0 / (8 * n), 1000.0, 1e-12
+    gs = gpu.GpuSolver(gpu.cavity(n), dt, re, rtol=rtol)
+    og = OGrid.rectangle(n, n)
+    osv = OSolver(og, dt, re, rtol=rtol)
+    osv.use_gpu_algorithm(gs.omega_v, gs.mg_omega)
+    for _ in range(steps):
+        st = gs.step()
+        mm, _ = osv.step()
+        assert np.allclose([st["umin"], st["umax"], st["vmin"], st["vmax"]], mm, rtol=0, atol=1e-9)
+        assert st["res_phi"] <= rtol and max(st["res_u"], st["res_v"]) <= rtol
+    ref = osv.get()
+    u, v, _ = gs.fields()
+    assert np.max(np.abs(u.ravel() - ref["u"])) <= 1e-9
+    assert np.max(np.abs(v.ravel() - ref["v"])) <= 1e-9
+    assert abs(np.max(u) - 1.0) <= 1.0     # the lid drives the flow; nothing blew up
+
+
+@pytest.mark.parametrize("n", [4096, 16384])
+def test_fp32_sweeps_at_config_size(gpu, n):
+    k = 5
+    a = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0, poisson=gpu.NS_POISSON_JACOBI, omega=1.0)
+    a.fill_random(0x5EED)
+    r64 = a.kernel(gpu.NS_K_POISSON, k)[0]
+    p64 = a.get(gpu.NS_ARR_PHI)
+    a.fill_random(0x5EED)
+    r32 = a.kernel(gpu.NS_K_POISSON32, k)[0]
+    p32 = a.get(gpu.NS_ARR_PHI)
+    a.close()
+    assert np.array_equal(p32, p32.astype(np.float32).astype(np.float64))
+    assert np.max(np.abs(p32 - p64)) <= 1e-5 * np.max(np.abs(p64))
+    assert abs(r32 - r64) <= 1e-5 * r64
+
+
+def test_slabs_at_config_size(tmp_path, gpu):
+    n, steps = 4096, 2
+    out = tmp_path / "r.npz"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29671", os.path.join(HERE, "mr_worker.py"),
+           "--output", str(out), "--xport", "host", "--size", str(n), "--nsteps", str(steps),
+           "--solver", str(gpu.NS_POISSON_MG), "--tol", "1e-8", "--stats-only"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ))
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    r = dict(np.load(out, allow_pickle=False))
+    assert str(r["status"]) == "ok", r["status"]
+    gs = gpu.GpuSolver(gpu.rectangle(n, n), 1.0 / (8 * n), 100.0, rtol=1e-8)
+    mm = np.array([list(gs.step().values())[:7] for _ in range(steps)])
+    assert np.max(np.abs(r["mm"][:, :4] - mm[:, :4])) <= 1e-12
+    assert np.array_equal(r["mm"][:, 4:], mm[:, 4:])       # same sweep / V-cycle counts
