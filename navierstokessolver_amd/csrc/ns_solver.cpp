@@ -87,6 +87,9 @@ struct MgLevel {
     // is reached from the last distributed one through this rank's slab of it (gs) and
     // gathered (every rank's rows si0[q] .. si0[q] + sn[q]) after the restriction.
     bool repl = false;
+    // multi-rank: the rhs ghost rows are owed -- they travel with the level's next overlapped
+    // FUSE_R exchange instead of in an exchange round of their own (flush_b otherwise)
+    bool b_pend = false;
     nsg::Geo gs{};
     std::vector<int> si0, sn;
 };
@@ -140,6 +143,7 @@ struct ns_solver {
     // multi-rank: ghost-row exchanges of the two-sweep passes run on a comm stream while the
     // pass's interior strips run (NSGPU_OVERLAP=0: exchange, then the whole pass)
     int overlap = 1;
+    int helm_b_pend = 0;          // RHS_u / RHS_v ghost rows owed to the first Helmholtz pair pass
     hipStream_t cst = nullptr;
     hipEvent_t xev[2] = {nullptr, nullptr};
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
@@ -373,9 +377,13 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
             double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
             const int hw = w == 2 ? (part ? 5 : 4) : 2;
             if (which == 3 && w == 2 && !s->tiled) {
-                // multi-rank pair pass: u and v ghost rows in one exchange, overlapped
-                const HaloReq r[2] = {{&s->g, s->arr[NS_ARR_U], hw}, {&s->g, s->arr[NS_ARR_V], hw}};
-                nb = overlapped(s, r, 2, [&]() {
+                // multi-rank pair pass: u and v ghost rows in one exchange, overlapped (the rhs
+                // ghost rows ride along on the solve's first pass)
+                const HaloReq r[4] = {{&s->g, s->arr[NS_ARR_U], hw}, {&s->g, s->arr[NS_ARR_V], hw},
+                                      {&s->g, s->arr[NS_ARR_RU], 4}, {&s->g, s->arr[NS_ARR_RV], 4}};
+                const int nr = s->helm_b_pend ? 4 : 2;
+                s->helm_b_pend = 0;
+                nb = overlapped(s, r, nr, [&]() {
                     return nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
                                                    s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
                                                    s->arr[NS_ARR_RV], part, s->st, 3);
@@ -384,6 +392,10 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                 std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
                 std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
             } else {
+                if (s->helm_b_pend) {
+                    s->helm_b_pend = 0;
+                    CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
+                }
                 if (which == 3) CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, hw));
                 else if (w <= 2) CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
                 nb = w >= 2 ? helm_sweep2(s, alpha, part, which, w) : helm_sweep(s, alpha, part, which);
@@ -641,6 +653,14 @@ int halo_l(ns_solver* s, int l, std::initializer_list<double*> fields, int w) {
     return halo_g(s, s->lv[l].g, fields, w);
 }
 
+// the rhs ghost rows of level l, if still owed (MgLevel::b_pend)
+int flush_b(ns_solver* s, int l) {
+    MgLevel& L = level(s, l);
+    if (!L.b_pend) return 0;
+    L.b_pend = false;
+    return halo_l(s, l, {L.b}, 4);
+}
+
 // levels whose smoothing runs as two-sweep passes: the HBM-bound ones (>= 2048^2 local
 // cells); the coarser ones are latency-bound and the fused pass's deeper row pipeline only
 // costs there (tools/sweep_levels2.py: 512^2 9.5 us/sweep fused vs 8.1 single).  A
@@ -728,6 +748,7 @@ int gather_level(ns_solver* s, MgLevel& C) {
 
 int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
     MgLevel& L = level(s, l);
+    if (n > 0) CHK(flush_b(s, l));
     for (int k = 0; k < n;) {
         const int w = (n - k >= 2 && pair_level(s, l)) ? 2 : 1;   // two sweeps per HBM pass
         CHK(halo_l(s, l, {L.phi}, 2 * w));
@@ -747,6 +768,7 @@ int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
 int mg_coarse(ns_solver* s) {
     const int l = (int)s->lv.size() - 1;
     MgLevel& L = level(s, l);
+    CHK(flush_b(s, l));
     if (s->mg_coarse_lds) {
         if (nsg::launch_coarse_vcycle(L.g, L.c, L.phi, L.b, 1, s->mg_pre, s->mg_post, s->mg_coarse_iters,
                                       s->mg_omega_c, s->mg_omega_s, s->st) != 0) {
@@ -783,6 +805,7 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
             const bool t = s->timing && l == 0 && !s->pc_active;
             if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st)); s->evtag[ev0 + *tn] = 1; }
             if (tile_level(s, l)) {
+                CHK(flush_b(s, l));
                 CHK(halo_l(s, l, {F.phi}, 5));
                 nb = nsg::launch_pois_tile2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b, cv.phi,
                                                      s->part, s->st);
@@ -790,8 +813,11 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
                 nb = nsg::launch_pois_rbsor2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b,
                                                       cv.phi, s->part, s->st);
             } else {
-                const HaloReq r[1] = {{&F.g, F.phi, 5}};
-                nb = overlapped(s, r, 1, [&]() {
+                // (the level's rhs ghost rows ride along when owed)
+                const HaloReq r[2] = {{&F.g, F.phi, 5}, {&F.g, F.b, 4}};
+                const int nr = F.b_pend ? 2 : 1;
+                F.b_pend = false;
+                nb = overlapped(s, r, nr, [&]() {
                     return nsg::launch_pois_rbsor2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g,
                                                             cv.b, cv.phi, s->part, s->st);
                 });
@@ -802,6 +828,7 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
             if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
         } else {
             CHK(mg_smooth(s, l, s->mg_pre, tn, ev0));
+            CHK(flush_b(s, l));
             CHK(halo_l(s, l, {F.phi}, 1));
             nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, sh, cv.g, C.c, cv.b, cv.phi, s->part, s->st);
         }
@@ -811,6 +838,8 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
             if (rc > 0) { *done = true; return 0; }
         }
         if (cv.gather) CHK(gather_level(s, C));
+        else if (s->nranks > 1 && s->overlap && s->cst && !C.repl && fused_restrict(s, l + 1) && !tile_level(s, l + 1))
+            C.b_pend = true;   // sent with level l+1's FUSE_R exchange
         else CHK(halo_l(s, l + 1, {C.b}, 4));
     }
     CHK(mg_coarse(s));
@@ -1708,7 +1737,10 @@ int ns_step(ns_solver* s, ns_stats* out) {
     // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
     CHK(helm_guess(s));
-    CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));       // rhs ghost rows: a checked pair pass reads ib-4
+    // rhs ghost rows (a checked pair pass reads ib-5): multi-rank pair passes take them with
+    // their first overlapped exchange
+    if (s->nranks > 1 && s->overlap && s->cst && !s->g.fc && !s->tiled) s->helm_b_pend = 1;
+    else CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
     s->hn = 0;
     CHK(helm_solve(s, &st.it_u, &st.res_u, &st.res_v));            // KSPSolve(uSolver) x2 (:547-548)
     st.it_v = st.it_u;
@@ -1723,7 +1755,11 @@ int ns_step(ns_solver* s, ns_stats* out) {
     CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
     CHK(consistent_rhs(s));                                        // stretched grids only
-    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
+    // rhs_phi ghost rows: with the multigrid's first overlapped FUSE_R exchange when it has one
+    if (s->nranks > 1 && s->overlap && s->cst && s->poisson == NS_POISSON_MG && !s->kv[0] && !s->lv.empty() &&
+        !s->lv[0].repl && fused_restrict(s, 0) && !tile_level(s, 0))
+        level(s, 0).b_pend = true;
+    else CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
     CHK(extrapolate_phi(s));
     CHK(pois_solve_any(s, &st.it_phi, &st.res_phi, &st));         // KSPSolve(phiSolver)  (:551)
     CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
