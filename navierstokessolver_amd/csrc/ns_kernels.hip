@@ -422,17 +422,35 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
 // in ONE round of coalesced loads (the global-load version fetches every u / v value ~13
 // times through L1/L2 and reloads ~30 table entries per cell); the cell loop then reads
 // LDS only.  Same per-cell arithmetic (rhs_cell).
+// exchange / compute overlap (set_strip_phase): 0 all strips / tiles, 1 those whose read cone
+// lies inside the slab, 2 the others
+static int g_phase = 0;
+
+// the row-block subset of phase g_phase for blocks of `rows` rows (n of them) reading `depth`
+// rows beyond their own: launch block k is block k if k < *lo, else *hi0 + (k - *lo); returns
+// how many blocks the launch covers
+static int phase_range(int nxl, int rows, int n, int depth, int* lo, int* hi0) {
+    *lo = n; *hi0 = 0;
+    if (!g_phase) return n;
+    const int sa = std::min(n, (depth + rows - 1) / rows);        // first block clear of the low ghosts
+    const int sb = std::max(sa, std::min(n, (nxl - depth) / rows));   // blocks [sa, sb) are interior
+    if (g_phase == 1) { *lo = 0; *hi0 = sa; return sb - sa; }
+    *lo = sa; *hi0 = sb;
+    return sa + (n - sb);
+}
+__device__ __forceinline__ int phase_block(int k, int lo, int hi0) { return k < lo ? k : hi0 + (k - lo); }
+
 constexpr int RT = 16;
 __global__ __launch_bounds__(256) void k_rhs_lds(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
                                                  const double* __restrict__ v, const double* __restrict__ phi,
                                                  double* __restrict__ cu, double* __restrict__ cv,
                                                  double* __restrict__ ru, double* __restrict__ rv,
-                                                 double* __restrict__ part) {
+                                                 double* __restrict__ part, int tlo, int thi0) {
     constexpr int EI = RT + 4, EJ = 64 + 4;
     __shared__ double su[EI][EJ], sv[EI][EJ];
     __shared__ double scu[RT][64], scv[RT][64];
     __shared__ double tx[3][RT + 4], ty[3][64 + 4];   // tables at rows gi-1 .. / columns j-1 ..
-    const int tj = blockIdx.x, ti = blockIdx.y;
+    const int tj = blockIdx.x, ti = phase_block(blockIdx.y, tlo, thi0);
     const int li0 = ti * RT, j0 = tj * 64, ld = g.ld;
     const int tid = threadIdx.x + 64 * threadIdx.y;
     // stage rows li0-2 .. li0+RT+1, columns j0-2 .. j0+65 (clamped into the field; a clamped
@@ -516,7 +534,7 @@ __global__ __launch_bounds__(256) void k_rhs_lds(Geo g, Coef c, double dt, doubl
             acc[1] += rv_ * rv_;
         }
     }
-    block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
+    block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * ti));
 }
 
 // the wall cells' ApplyBoundaryConditions terms (rhs_bc) on top of k_rhs_lds's values -- the
@@ -1228,6 +1246,7 @@ struct CellStreamArgs {
     double *o0, *o1;              // K3: rhs_phi, -;  K5: u, v
     double* part;
     int nsj, nsi, L;
+    int slo, shi0, nrun;          // strip-row subset of this launch (phase_range)
 };
 
 // one face value along a line: interior r-weighted interpolation, or the wall's (q + ghost)/2
@@ -1240,11 +1259,13 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
     const Geo& g = A.g;
     const Coef& c = A.c;
     const int lane = threadIdx.x & 63;
-    const int nstr = A.nsj * A.nsi;
-    const int wid = __builtin_amdgcn_readfirstlane(xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (int)(threadIdx.x >> 6));
+    const int nstr = A.nsj * A.nrun;
+    const int w = __builtin_amdgcn_readfirstlane(xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (int)(threadIdx.x >> 6));
+    const int run = w / A.nsj;
+    const int wid = phase_block(run, A.slo, A.shi0) * A.nsj + (w - run * A.nsj);   // the strip (partial slot)
     double acc[4] = {0.0, 0.0, INFINITY, INFINITY};   // K3: sum, sum^2; K5: (umin, -umax, vmin, -vmax)
     if (K == 5) acc[0] = acc[1] = INFINITY;
-    if (wid < nstr) {
+    if (w < nstr) {
         const int si = wid / A.nsj, sj = wid - si * A.nsj;
         const int jb = sj * SW, ib = si * A.L, ie = min(ib + A.L, g.nxl);
         const int ny = g.ny, ld = g.ld;
@@ -1355,7 +1376,7 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
             const double o = __shfl_xor(acc[k], off, 64);
             acc[k] = K == 3 ? acc[k] + o : fmin(acc[k], o);
         }
-    if (lane == 0 && wid < nstr)
+    if (lane == 0 && w < nstr)
 #pragma unroll
         for (int k = 0; k < NV; k++) A.part[NV * wid + k] = acc[k];
 }
@@ -2514,23 +2535,33 @@ namespace nsg {
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
                const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st) {
     const char* e = getenv("NSGPU_RHS");   // NSGPU_RHS=global: the global-load K1 (A/B)
+    // (the grid kernels cannot split: the interior phase launches nothing, the edge phase all;
+    // K1 updates cu / cv in place, so no cell may run twice)
     if (g.fc) {   // masked domain: the grid kernel with the polygon's topology
         const int rows = cell_rows(g);
         const dim3 cg = cell_grid(g, rows);
-        hipLaunchKernelGGL(k_rhs<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
+        if (g_phase != 1)
+            hipLaunchKernelGGL(k_rhs<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
         return (int)(cg.x * cg.y);
     }
     if (!(e && std::strcmp(e, "global") == 0)) {
-        const dim3 grid((g.ny + 63) / 64, (g.nxl + RT - 1) / RT);
-        hipLaunchKernelGGL(k_rhs_lds, grid, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part);
-        const int nb = (int)(grid.x * grid.y);
+        const int nti = (g.nxl + RT - 1) / RT;
+        int tlo, thi0;
+        const int nrun = phase_range(g.nxl, RT, nti, 2, &tlo, &thi0);   // MUSCL: rows li0-2 .. li0+RT+1
+        const int nb = ((g.ny + 63) / 64) * nti;
+        if (nrun > 0)
+            hipLaunchKernelGGL(k_rhs_lds, dim3((g.ny + 63) / 64, nrun), dim3(64, 4), 0, st, g, c, dt, re, u, v, phi,
+                               cu, cv, ru, rv, part, tlo, thi0);
         const int nbc = (2 * g.nxl + 2 * g.ny + 255) / 256;
-        hipLaunchKernelGGL(k_rhs_bc, dim3(nbc), dim3(256), 0, st, g, c, dt, re, phi, ru, rv, part + 2 * nb);
+        // the wall terms read phi's ghost rows: with the edge phase
+        if (g_phase != 1)
+            hipLaunchKernelGGL(k_rhs_bc, dim3(nbc), dim3(256), 0, st, g, c, dt, re, phi, ru, rv, part + 2 * nb);
         return nb + nbc;
     }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
-    hipLaunchKernelGGL(k_rhs<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
+    if (g_phase != 1)
+        hipLaunchKernelGGL(k_rhs<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
     return (int)(cg.x * cg.y);
 }
 
@@ -2543,7 +2574,8 @@ static int launch_cell_s(CellStreamArgs A, hipStream_t st) {
     A.L = strip_rows(A.g.nxl, A.nsj, resident_waves((const void*)k_cell_s<K>), 4);
     A.nsi = (A.g.nxl + A.L - 1) / A.L;
     const int nstr = A.nsj * A.nsi;
-    hipLaunchKernelGGL(k_cell_s<K>, dim3((nstr + 3) / 4), dim3(256), 0, st, A);
+    A.nrun = phase_range(A.g.nxl, A.L, A.nsi, 1, &A.slo, &A.shi0);   // window rows ib-1 .. ie
+    if (A.nrun > 0) hipLaunchKernelGGL(k_cell_s<K>, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), 0, st, A);
     return nstr;
 }
 
@@ -2561,6 +2593,7 @@ int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const do
     }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
+    if (g_phase == 1) return (int)(cg.x * cg.y);   // (cannot split: all with the edge phase)
     if (g.fc) hipLaunchKernelGGL(k_div<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part, rows);
     else hipLaunchKernelGGL(k_div<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part, rows);
     return (int)(cg.x * cg.y);
@@ -2612,6 +2645,7 @@ int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, con
     }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
+    if (g_phase == 1) return (int)(cg.x * cg.y);   // (cannot split: all with the edge phase)
     if (g.fc) hipLaunchKernelGGL(k_correct<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part, rows);
     else hipLaunchKernelGGL(k_correct<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part, rows);
     return (int)(cg.x * cg.y);
@@ -2683,19 +2717,12 @@ static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, dou
 // Exchange / compute overlap (multi-rank): the solver launches a pass twice, first the
 // strips whose rows (and read cone of `depth` rows) lie inside the slab -- while the ghost
 // rows are still in flight on the comm stream -- then, after the exchange, the edge strips.
-static int g_phase = 0;   // 0: all strips, 1: interior, 2: edges
 void set_strip_phase(int phase) { g_phase = phase; }
 
 // the strip subset of the current phase (k_sweep2 launchers); returns the workgroup count
 // (0: nothing to launch)
 static int apply_phase(StreamArgs& a, int depth) {
-    a.slo = a.nsi; a.shi0 = 0; a.nrun = a.nsi;
-    if (g_phase) {
-        const int sa = (depth + a.L - 1) / a.L;                  // first strip clear of the low ghosts
-        const int sb = std::max(sa, (a.nxl - depth) / a.L);      // strips [sa, sb) are interior
-        if (g_phase == 1) { a.slo = 0; a.shi0 = sa; a.nrun = sb - sa; }
-        else { a.slo = sa; a.shi0 = sb; a.nrun = sa + (a.nsi - sb); }
-    }
+    a.nrun = phase_range(a.nxl, a.L, a.nsi, depth, &a.slo, &a.shi0);
     return (a.nsj * a.nrun + 3) / 4;
 }
 

@@ -1310,9 +1310,14 @@ int consistent_rhs(ns_solver* s) {
 }
 
 // K3 + null-space mean
+// K3 with the u*, v* ghost rows, overlapped with the interior strips
 int divergence(ns_solver* s) {
-    const int nb = nsg::launch_div(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_RPHI],
-                                   s->part, s->st);
+    const HaloReq r[2] = {{&s->g, s->arr[NS_ARR_U], 1}, {&s->g, s->arr[NS_ARR_V], 1}};
+    const int nb = overlapped(s, r, 2, [&]() {
+        return nsg::launch_div(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_RPHI], s->part,
+                               s->st);
+    });
+    if (nb < 0) return nb;
     nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_DIVSUM, s->st);
     CHK(allreduce(s, s->scal + S_DIVSUM, 2, ncclSum));
     nsg::launch_finish_mean(s->scal + S_DIVSUM, s->ncells, s->scal + S_SHIFT, s->st);
@@ -1340,19 +1345,30 @@ int helm_bnorm(ns_solver* s) {
     return 0;
 }
 
+// K1 with its ghost rows (u, v width 2: MUSCL; phi width 1: grad phi^{n-1} on walls) in one
+// exchange group, overlapped with the interior tiles
 int rhs(ns_solver* s) {
-    const int nb = nsg::launch_rhs(s->g, s->c, s->dt, s->re, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_PHI],
-                                   s->arr[NS_ARR_CU], s->arr[NS_ARR_CV], s->arr[NS_ARR_RU], s->arr[NS_ARR_RV],
-                                   s->part, s->st);
+    const HaloReq r[3] = {{&s->g, s->arr[NS_ARR_U], 2}, {&s->g, s->arr[NS_ARR_V], 2}, {&s->g, s->arr[NS_ARR_PHI], 1}};
+    const int nb = overlapped(s, r, 3, [&]() {
+        return nsg::launch_rhs(s->g, s->c, s->dt, s->re, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_PHI],
+                               s->arr[NS_ARR_CU], s->arr[NS_ARR_CV], s->arr[NS_ARR_RU], s->arr[NS_ARR_RV], s->part,
+                               s->st);
+    });
+    if (nb < 0) return nb;
     nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_HBN, s->st);
     CHK(allreduce(s, s->scal + S_HBN, 2, ncclSum));
     return 0;
 }
 
 // u^{n+1} = u* - dt grad phi into the ping-pong partners (no in-place read/write hazard)
+// (K5 with phi's ghost rows, overlapped with the interior strips)
 int correct(ns_solver* s) {
-    const int nb = nsg::launch_correct(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
-                                       s->arr[NS_ARR_TMPV], s->arr[NS_ARR_PHI], s->part, s->st);
+    const HaloReq r[1] = {{&s->g, s->arr[NS_ARR_PHI], 1}};
+    const int nb = overlapped(s, r, 1, [&]() {
+        return nsg::launch_correct(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
+                                   s->arr[NS_ARR_TMPV], s->arr[NS_ARR_PHI], s->part, s->st);
+    });
+    if (nb < 0) return nb;
     std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
     std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
     nsg::launch_reduce_min(s->part, nb, 4, s->scal + S_MM, s->st);
@@ -1730,9 +1746,6 @@ int ns_step(ns_solver* s, ns_stats* out) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     ns_stats st{};
     HIPCHK(hipSetDevice(s->device));
-    // ghost rows for K1 (one exchange group): u, v width 2 (MUSCL), phi width 1 (grad phi^{n-1} on walls)
-    CHK(halo_reqs(s, {HaloReq{&s->g, s->arr[NS_ARR_U], 2}, HaloReq{&s->g, s->arr[NS_ARR_V], 2},
-                      HaloReq{&s->g, s->arr[NS_ARR_PHI], 1}}));
     CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
     // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
@@ -1752,7 +1765,6 @@ int ns_step(ns_solver* s, ns_stats* out) {
     }
     s->hn = 0;
     if (s->helm_extrap) s->us_valid = std::min(s->us_valid + 1, 2);  // correct() leaves u* in TMPU/TMPV
-    CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
     CHK(consistent_rhs(s));                                        // stretched grids only
     // rhs_phi ghost rows: with the multigrid's first overlapped FUSE_R exchange when it has one
@@ -1762,7 +1774,6 @@ int ns_step(ns_solver* s, ns_stats* out) {
     else CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
     CHK(extrapolate_phi(s));
     CHK(pois_solve_any(s, &st.it_phi, &st.res_phi, &st));         // KSPSolve(phiSolver)  (:551)
-    CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
     CHK(correct(s));                                               // CorrectVelocities    (:552)
     CHK(fetch(s));                                                 // VecMin/VecMax        (:554-557)
     st.umin = s->hs[S_MM];
@@ -1830,8 +1841,6 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
     const double alpha = s->dt / (2 * s->re);
     switch (which) {
     case NS_K_RHS:
-        CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
-        CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
         CHK(rhs(s));
         CHK(fetch(s));
         if (out) { out[0] = s->hs[S_HBN]; out[1] = s->hs[S_HBN + 1]; }
@@ -1860,7 +1869,6 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         return 0;
     }
     case NS_K_DIV:
-        CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 1));
         CHK(divergence(s));
         CHK(fetch(s));
         if (out) { out[0] = s->hs[S_DIVSUM]; out[1] = s->hs[S_DIVSUM + 1]; }
@@ -1894,7 +1902,6 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         return 0;
     }
     case NS_K_CORRECT:
-        CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));
         CHK(correct(s));
         CHK(fetch(s));
         if (out) { out[0] = s->hs[S_MM]; out[1] = -s->hs[S_MM + 1]; out[2] = s->hs[S_MM + 2]; out[3] = -s->hs[S_MM + 3]; }
