@@ -128,6 +128,7 @@ struct ns_solver {
     int phi_extrap = 2;          // Poisson initial guess: NSGPU_PHI_EXTRAP=0 phi^{n-1}, 1 linear, 2 quadratic (default)
     int mg_predict = 1;          // NSGPU_MG_PREDICT=0: a residual check (host sync) after every V-cycle
     double mg_rate2 = 0.0;       // last measured per-cycle contraction of ||r||^2
+    int mg_hist[4] = {-1, -1, -1, -1};   // V-cycles the last four solves converged at (first check)
     double* phim = nullptr;      // phi^{n-2} (the extrapolation's second point; rotates with PHI / TMP)
     double* phim2 = nullptr;     // phi^{n-3} (quadratic extrapolation only)
     // NSGPU_HELM_EXTRAP=1 (A/B): Helmholtz initial guess 2 u*^n - u*^{n-1} instead of u^n
@@ -891,7 +892,15 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     // residual checks (host syncs): after cycle 0, then where the contraction rate (measured
     // between this solve's checks, else the previous solve's) predicts convergence -- the
     // cycles in between run without a host round trip
+    // the first check: at the fewest V-cycles any of the last four solves converged at (consecutive
+    // steps converge alike, so the check after cycle 0 would only measure a rate already known;
+    // a solve converging earlier than all four costs at most that many partial cycles)
     int next_chk = 0, prev_c = -1;
+    if (s->mg_predict && s->mg_rate2 > 0) {
+        int m = 1 << 30;
+        for (int h : s->mg_hist) m = std::min(m, h);
+        if (m > 0) next_chk = m;
+    }
     double prev_rr = -1.0;
     auto check = [&](int nb) -> int {
         if (!(cycles >= next_chk || cycles >= maxc)) return 0;
@@ -947,6 +956,15 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
         cycles++;
     }
     *its = cycles;
+    // history: the cycle count this solve needed -- one fewer when its only check came with a
+    // full cycle's contraction to spare (the earlier check point would have passed too)
+    int need = cycles;
+    if (nchk == 1 && cycles > 0 && s->mg_rate2 > 0) {
+        const double rr = s->hs[S_RES] / std::max(s->hs[S_SHIFT + 1], 1e-300);
+        if (rr / s->mg_rate2 <= tol2) need = cycles - 1;
+    }
+    for (int k = 3; k > 0; k--) s->mg_hist[k] = s->mg_hist[k - 1];
+    s->mg_hist[0] = need;
     if (stt) {
         stt->t_poisson_kernel_ms += tms;
         stt->n_checks += nchk;
@@ -1811,6 +1829,8 @@ int ns_set_array(ns_solver* s, int which, const double* host) {
     // keep the derived scalars consistent with an injected right-hand side
     if (which == NS_ARR_RPHI) CHK(rhs_mean(s));
     if (which == NS_ARR_PHI || which == NS_ARR_TMP) s->phim_valid = 0;
+    if (which == NS_ARR_PHI || which == NS_ARR_TMP || which == NS_ARR_RPHI)
+        for (int& h : s->mg_hist) h = -1;   // an injected state: no cycle-count history
     s->us_valid = 0;
     if (which == NS_ARR_RU || which == NS_ARR_RV) CHK(helm_bnorm(s));
     HIPCHK(hipStreamSynchronize(s->st));
