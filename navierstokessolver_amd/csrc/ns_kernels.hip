@@ -1063,6 +1063,8 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
 typedef unsigned nsu4 __attribute__((ext_vector_type(4)));
 typedef unsigned nsu2 __attribute__((ext_vector_type(2)));
 constexpr unsigned OOB = 0xFFFFFFF0u;
+// (the streamed stores are nt: sc1 write-through lost the Infinity-Cache reuse -- Jacobi 73 ->
+// 88 us -- and sc1 nt measured the same as nt)
 
 // A copy the compiler cannot coalesce away.  A row window (rows r-2, r-1, r) that takes the
 // freshly consumed prefetch slot by plain assignment ends up sharing the slot's register;

@@ -147,6 +147,8 @@ struct ns_solver {
     int helm_b_pend = 0;          // RHS_u / RHS_v ghost rows owed to the first Helmholtz pair pass
     hipStream_t cst = nullptr;
     hipEvent_t xev[2] = {nullptr, nullptr};
+    hipEvent_t fev = nullptr;     // fetch_begin / fetch_end: the scalars' copy to the host is done
+    int extrap_pending = 0;       // ns_step: the phi extrapolation waits to hide a host sync
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
     int mg_pre = 2, mg_post = 2, mg_coarse_iters = 0;
     double mg_omega_c = 1.0, mg_omega_s = 1.1;
@@ -299,6 +301,19 @@ int fetch(ns_solver* s) {
     HIPCHK(hipStreamSynchronize(s->st));
     return 0;
 }
+
+// the same in two halves: work enqueued between them (independent of the scalars) keeps the
+// GPU busy while the host waits for the copy and decides what to launch next
+int fetch_begin(ns_solver* s) {
+    HIPCHK(hipMemcpyAsync(s->hs, s->scal, S_NUM * sizeof(double), hipMemcpyDeviceToHost, s->st));
+    HIPCHK(hipEventRecord(s->fev, s->st));
+    return 0;
+}
+int fetch_end(ns_solver* s) {
+    HIPCHK(hipEventSynchronize(s->fev));
+    return 0;
+}
+int extrapolate_phi(ns_solver* s);
 
 int ensure_events(ns_solver* s, size_t n) {
     while (s->ev.size() < n) {
@@ -542,7 +557,14 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         }
         CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
         if (first) CHK(allreduce(s, s->scal + S_AUX, 2, ncclSum));
-        CHK(fetch(s));
+        CHK(fetch_begin(s));
+        if (s->extrap_pending) {
+            // the Poisson initial guess does not depend on u*: it runs on the GPU while the
+            // host waits for this check
+            s->extrap_pending = 0;
+            CHK(extrapolate_phi(s));
+        }
+        CHK(fetch_end(s));
         const double r2u = s->hs[S_RES], r2v = s->hs[S_RES + 1];
         const double bu = s->hs[S_HBN], bv = s->hs[S_HBN + 1];
         const bool ok = (r2u <= tol2 * bu || r2u == 0.0) && (r2v <= tol2 * bv || r2v == 0.0);
@@ -1630,6 +1652,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     s->device = dev;
     if (hipSetDevice(dev) != hipSuccess) { set_err("hipSetDevice(%d) failed", dev); return fail(NS_EHIP); }
     if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); return fail(NS_EHIP); }
+    if (hipEventCreateWithFlags(&s->fev, hipEventDisableTiming) != hipSuccess) { set_err("event create failed"); return fail(NS_EHIP); }
     if (p->nranks > 1) {
         const char* ov = getenv("NSGPU_OVERLAP");
         s->overlap = ov ? std::atoi(ov) != 0 : 1;
@@ -1755,6 +1778,7 @@ void ns_destroy(ns_solver* s) {
     if (s->cst) (void)hipStreamSynchronize(s->cst);
     for (auto e : s->xev)
         if (e) (void)hipEventDestroy(e);
+    if (s->fev) (void)hipEventDestroy(s->fev);
     if (s->cst) (void)hipStreamDestroy(s->cst);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
@@ -1773,7 +1797,9 @@ int ns_step(ns_solver* s, ns_stats* out) {
     if (s->nranks > 1 && s->overlap && s->cst && !s->g.fc && !s->tiled) s->helm_b_pend = 1;
     else CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
     s->hn = 0;
+    s->extrap_pending = s->phim ? 1 : 0;
     CHK(helm_solve(s, &st.it_u, &st.res_u, &st.res_v));            // KSPSolve(uSolver) x2 (:547-548)
+    if (s->extrap_pending) { s->extrap_pending = 0; CHK(extrapolate_phi(s)); }
     st.it_v = st.it_u;
     for (int k = 0; k < s->hn; k++) {   // (helm_solve's last residual check synchronised the stream)
         float ms = 0.f;
@@ -1790,7 +1816,6 @@ int ns_step(ns_solver* s, ns_stats* out) {
         !s->lv[0].repl && fused_restrict(s, 0) && !tile_level(s, 0))
         level(s, 0).b_pend = true;
     else CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
-    CHK(extrapolate_phi(s));
     CHK(pois_solve_any(s, &st.it_phi, &st.res_phi, &st));         // KSPSolve(phiSolver)  (:551)
     CHK(correct(s));                                               // CorrectVelocities    (:552)
     CHK(fetch(s));                                                 // VecMin/VecMax        (:554-557)
