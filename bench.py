@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--sync-monitor", action="store_true",
+                    help="ns_step (host sync at every step's end) instead of ns_step_async")
     ap.add_argument("--time-every", type=int, default=3,
                     help="HIP-event kernel timing on every k-th timed step (each event pair costs a few us of "
                          "GPU idle; 0 = none)")
@@ -112,15 +114,23 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    # ns_step_async: each step's min/max monitor arrives with the next step (FluidSolver.cpp:554-560
+    # prints every step; the values are the same, one call later), so the host enqueues step k+1's
+    # K1 while step k's K5 runs instead of waiting for it; the last step's monitor is fetched
+    # (ns_monitor) inside the timed region.  --sync-monitor: ns_step, one host sync at each step's end.
+    step = solver.step if args.sync_monitor else solver.step_async
     for _ in range(args.warmup):
-        solver.step()
+        step()
+    if not args.sync_monitor:
+        solver.monitor()
     barrier()
     t0 = time.perf_counter()
     stats = []
     for k in range(args.steps):
         if args.time_every != 1:
             solver.set_timing(args.time_every > 0 and k % args.time_every == 0)
-        stats.append(solver.step())
+        stats.append(step())
+    last_monitor = stats[-1] if args.sync_monitor else dict(zip(("umin", "umax", "vmin", "vmax"), solver.monitor()))
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -197,7 +207,9 @@ def main():
         "data": "synthetic (lid-driven cavity from rest, no input files)",
         "config": {"workload": f"{n}x{n} lid-driven cavity, Re={re:g}, dt=1/{8 * n}, fp64, multigrid Poisson "
                                f"(RB-GS smoother) + RB-SOR Helmholtz, both to rtol {args.rtol:g}",
-                   "nx": n, "ny": n, "re": re, "dt": dt, "parallelism": f"x-slab x{world}"},
+                   "nx": n, "ny": n, "re": re, "dt": dt, "parallelism": f"x-slab x{world}",
+                   "step_api": "ns_step" if args.sync_monitor else "ns_step_async"},
+        "monitor_last_step": {k: last_monitor[k] for k in ("umin", "umax", "vmin", "vmax")},
         "poisson_vcycles_per_s": cycles / elapsed,
         "poisson_vcycles_per_step": cycles / K,
         "poisson_fine_sweeps_per_s": fine_sweeps / elapsed,

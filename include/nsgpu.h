@@ -161,6 +161,12 @@ void ns_destroy(ns_solver* s);
 
 /* ---- one full time step: the body of FluidSolver::Solve's loop (FluidSolver.cpp:546-560) ---- */
 int  ns_step(ns_solver* s, ns_stats* out);
+/* the same step without its closing host sync: out's umin..vmax are the PREVIOUS
+ * ns_step_async's min/max (NaN on the first), so a caller printing them per step prints the
+ * reference's monitor sequence one step late; ns_monitor waits for the latest step's.
+ * The host can enqueue the next step while this one's last kernels run. */
+int  ns_step_async(ns_solver* s, ns_stats* out);
+int  ns_monitor(ns_solver* s, double* mm /* [4]: umin, umax, vmin, vmax */);
 
 /* per-kernel HIP-event timing (ns_params.timing) switched on / off between steps */
 int  ns_set_timing(ns_solver* s, int on);

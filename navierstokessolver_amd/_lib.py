@@ -77,6 +77,8 @@ SIGNATURES = {
     "ns_create": (ctypes.c_int, [ctypes.POINTER(NsGridDesc), ctypes.POINTER(NsParams), ctypes.POINTER(_P)]),
     "ns_destroy": (None, [_P]),
     "ns_step": (ctypes.c_int, [_P, ctypes.POINTER(NsStats)]),
+    "ns_step_async": (ctypes.c_int, [_P, ctypes.POINTER(NsStats)]),
+    "ns_monitor": (ctypes.c_int, [_P, _D]),
     "ns_get_fields": (ctypes.c_int, [_P, _D, _D, _D]),
     "ns_set_fields": (ctypes.c_int, [_P, _D, _D, _D, _D, _D]),
     "ns_get_array": (ctypes.c_int, [_P, ctypes.c_int, _D]),

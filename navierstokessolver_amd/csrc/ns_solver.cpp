@@ -10,6 +10,7 @@
 // FluidSolver.cpp:61-82) are replaced by red-black SOR sweeps run to the same
 // relative-residual tolerance, checked every few sweeps from a fused residual.
 #include <rccl/rccl.h>
+#include <limits>
 
 #include <algorithm>
 #include <cmath>
@@ -124,6 +125,11 @@ struct ns_solver {
     int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
     int tile_small = 1;          // NSGPU_TILE_SMALL=0: no LDS-tiled fused passes on small levels (A/B)
     int helm_split = 1;          // NSGPU_HELM_SPLIT=0: u and v pass by pass (A/B)
+    // NSGPU_HELM_CONC=1 (single rank, split): v's passes on a second stream, concurrent with
+    // u's, so each chain's dependent-kernel boundaries (launch + drain) overlap the other's work
+    int helm_conc = 0;
+    hipStream_t st2 = nullptr;
+    hipEvent_t cev[2] = {nullptr, nullptr};
     int helm_ns = 2;             // Helmholtz sweeps per pass on one slab (NSGPU_HELM_NS: 2, 3, 4)
     int phi_extrap = 2;          // Poisson initial guess: NSGPU_PHI_EXTRAP=0 phi^{n-1}, 1 linear, 2 quadratic (default)
     int mg_predict = 1;          // NSGPU_MG_PREDICT=0: a residual check (host sync) after every V-cycle
@@ -148,6 +154,11 @@ struct ns_solver {
     hipStream_t cst = nullptr;
     hipEvent_t xev[2] = {nullptr, nullptr};
     hipEvent_t fev = nullptr;     // fetch_begin / fetch_end: the scalars' copy to the host is done
+    // ns_step_async: the step's min/max travel to mm_host behind the step's last kernel (mev);
+    // read by the next ns_step_async (after that step's first host sync) or by ns_monitor
+    double* mm_host = nullptr;
+    hipEvent_t mev = nullptr;
+    int mm_pending = 0;
     int extrap_pending = 0;       // ns_step: the phi extrapolation waits to hide a host sync
     std::vector<MgLevel> lv;     // multigrid hierarchy (NS_POISSON_MG)
     int mg_pre = 2, mg_post = 2, mg_coarse_iters = 0;
@@ -382,8 +393,25 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                 int* first_at, int* last_at) {
     int nb = 0;
     const bool split = s->helm_split && s->nranks == 1;
+    const bool conc = split && s->helm_conc && !s->tiled;
+    hipStream_t main_st = s->st;
+    struct Restore {   // an error return inside v's chain leaves the main stream current
+        ns_solver* s; hipStream_t st;
+        ~Restore() { s->st = st; }
+    } restore{s, main_st};
+    if (conc) {
+        if (!s->st2) {
+            HIPCHK(hipStreamCreateWithFlags(&s->st2, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&s->cev[0], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&s->cev[1], hipEventDisableTiming));
+        }
+        // fork: v's chain starts from the same point as u's
+        HIPCHK(hipEventRecord(s->cev[0], s->st));
+        HIPCHK(hipStreamWaitEvent(s->st2, s->cev[0], 0));
+    }
     for (int which : {split ? 1 : 3, split ? 2 : 0}) {
         if (!which) break;
+        if (conc && which == 2) s->st = s->st2;   // v's launches (and their timing events) on st2
         int k = 0, launch = 0;
         while (k < n) {
             // sweeps per pass: up to helm_ns (NSGPU_HELM_NS) on one slab, pairs otherwise
@@ -426,6 +454,12 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
             k += w;
             launch++;
         }
+    }
+    if (conc) {
+        // join: everything after the solve (the residual reductions) waits for v's chain
+        s->st = main_st;
+        HIPCHK(hipEventRecord(s->cev[1], s->st2));
+        HIPCHK(hipStreamWaitEvent(s->st, s->cev[1], 0));
     }
     return nb;
 }
@@ -1611,6 +1645,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_SPLIT")) s->helm_split = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_HELM_CONC")) s->helm_conc = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_NS")) s->helm_ns = std::max(2, std::min(4, std::atoi(e)));
     if (const char* e = getenv("NSGPU_HELM_EXTRAP")) s->helm_extrap = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(2, std::atoi(e)));
@@ -1756,6 +1791,12 @@ void ns_destroy(ns_solver* s) {
     (void)hipSetDevice(s->device);
     if (s->st) (void)hipStreamSynchronize(s->st);
     if (s->comm) (void)ncclCommDestroy(s->comm);
+    if (s->st2) (void)hipStreamSynchronize(s->st2);
+    if (s->mev) (void)hipEventDestroy(s->mev);
+    if (s->mm_host) (void)hipHostFree(s->mm_host);
+    for (auto e : s->cev)
+        if (e) (void)hipEventDestroy(e);
+    if (s->st2) (void)hipStreamDestroy(s->st2);
     for (auto e : s->ev) (void)hipEventDestroy(e);
     for (auto e : s->hev) (void)hipEventDestroy(e);
     for (size_t l = 1; l < s->lv.size(); l++) {
@@ -1784,10 +1825,8 @@ void ns_destroy(ns_solver* s) {
     delete s;
 }
 
-int ns_step(ns_solver* s, ns_stats* out) {
-    if (!s) { set_err("null solver"); return NS_EINVAL; }
-    ns_stats st{};
-    HIPCHK(hipSetDevice(s->device));
+// the step up to CorrectVelocities (its min/max reduced into scal[S_MM], not yet fetched)
+static int step_body(ns_solver* s, ns_stats& st) {
     CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
     // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
@@ -1818,17 +1857,73 @@ int ns_step(ns_solver* s, ns_stats* out) {
     else CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
     CHK(pois_solve_any(s, &st.it_phi, &st.res_phi, &st));         // KSPSolve(phiSolver)  (:551)
     CHK(correct(s));                                               // CorrectVelocities    (:552)
+    return 0;
+}
+
+static int check_monitor(const ns_stats& st) {
+    if (!std::isfinite(st.umin) || !std::isfinite(st.umax) || !std::isfinite(st.vmin) || !std::isfinite(st.vmax)) {
+        set_err("velocity field is not finite after the step (scheme diverged; see SURVEY.md section 5 on CFL)");
+        return NS_EDIVERGE;
+    }
+    return 0;
+}
+
+int ns_step(ns_solver* s, ns_stats* out) {
+    if (!s) { set_err("null solver"); return NS_EINVAL; }
+    ns_stats st{};
+    HIPCHK(hipSetDevice(s->device));
+    if (s->mm_pending) HIPCHK(hipEventSynchronize(s->mev));   // (an ns_step_async before: its copy lands first)
+    s->mm_pending = 0;
+    CHK(step_body(s, st));
     CHK(fetch(s));                                                 // VecMin/VecMax        (:554-557)
     st.umin = s->hs[S_MM];
     st.umax = -s->hs[S_MM + 1];
     st.vmin = s->hs[S_MM + 2];
     st.vmax = -s->hs[S_MM + 3];
     if (out) *out = st;
-    if (!std::isfinite(st.umin) || !std::isfinite(st.umax) || !std::isfinite(st.vmin) || !std::isfinite(st.vmax)) {
-        set_err("velocity field is not finite after the step (scheme diverged; see SURVEY.md section 5 on CFL)");
-        return NS_EDIVERGE;
+    return check_monitor(st);
+}
+
+// The same step without the host sync at its end (the reference prints min/max every step:
+// FluidSolver.cpp:554-560).  Each step's min/max are copied to pinned memory behind its last
+// kernel; they are returned by the NEXT call (the monitor one step late: the same printed
+// sequence) or by ns_monitor.  The host is back to launch the next step's K1 while K5 runs.
+int ns_step_async(ns_solver* s, ns_stats* out) {
+    if (!s) { set_err("null solver"); return NS_EINVAL; }
+    ns_stats st{};
+    HIPCHK(hipSetDevice(s->device));
+    if (!s->mm_host) {
+        HIPCHK(hipHostMalloc(&s->mm_host, 4 * sizeof(double), hipHostMallocDefault));
+        HIPCHK(hipEventCreateWithFlags(&s->mev, hipEventDisableTiming));
+        for (int k = 0; k < 4; k++) s->mm_host[k] = std::numeric_limits<double>::quiet_NaN();
     }
-    return 0;
+    CHK(step_body(s, st));   // (its residual checks synchronised the stream: the previous copy has landed)
+    const bool prev = s->mm_pending != 0;
+    if (prev) HIPCHK(hipEventSynchronize(s->mev));
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    st.umin = prev ? s->mm_host[0] : nan;
+    st.umax = prev ? -s->mm_host[1] : nan;
+    st.vmin = prev ? s->mm_host[2] : nan;
+    st.vmax = prev ? -s->mm_host[3] : nan;
+    HIPCHK(hipMemcpyAsync(s->mm_host, s->scal + S_MM, 4 * sizeof(double), hipMemcpyDeviceToHost, s->st));
+    HIPCHK(hipEventRecord(s->mev, s->st));
+    s->mm_pending = 1;
+    if (out) *out = st;
+    return prev ? check_monitor(st) : 0;
+}
+
+int ns_monitor(ns_solver* s, double* mm) {
+    if (!s || !mm) { set_err("null argument"); return NS_EINVAL; }
+    if (!s->mm_pending) { set_err("ns_monitor: no ns_step_async since the last ns_step / ns_monitor"); return NS_EINVAL; }
+    HIPCHK(hipSetDevice(s->device));
+    HIPCHK(hipEventSynchronize(s->mev));
+    s->mm_pending = 0;
+    ns_stats st{};
+    st.umin = mm[0] = s->mm_host[0];
+    st.umax = mm[1] = -s->mm_host[1];
+    st.vmin = mm[2] = s->mm_host[2];
+    st.vmax = mm[3] = -s->mm_host[3];
+    return check_monitor(st);
 }
 
 int ns_set_timing(ns_solver* s, int on) {

@@ -121,6 +121,18 @@ class GpuSolver:
         L.check(L.lib().ns_step(self._h, ctypes.byref(st)))
         return st.as_dict()
 
+    def step_async(self) -> dict:
+        """ns_step_async: one step without the closing host sync; umin..vmax are the previous
+        step_async's monitor values (NaN on the first), monitor() returns the latest."""
+        st = L.NsStats()
+        L.check(L.lib().ns_step_async(self._h, ctypes.byref(st)))
+        return st.as_dict()
+
+    def monitor(self) -> tuple:
+        mm = np.empty(4, dtype=np.float64)
+        L.check(L.lib().ns_monitor(self._h, _dptr(mm)))
+        return tuple(float(x) for x in mm)
+
     # ---- state
     def get(self, which: int) -> np.ndarray:
         out = np.empty(self.shape, dtype=np.float64)

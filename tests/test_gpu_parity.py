@@ -564,3 +564,52 @@ def test_streaming_k3_k5_equal_grid_kernels(gpu, monkeypatch, nx, ny, xr, yr, bc
     np.testing.assert_allclose(a[1], b[1], rtol=1e-12, atol=1e-12 * np.abs(b[1]).max())
     np.testing.assert_array_equal(a[2], b[2]) if rel(a[3], b[3]) == 0 else np.testing.assert_allclose(a[2], b[2], rtol=1e-14)
     assert rel(a[3], b[3]) <= 1e-14 and rel(a[4], b[4]) <= 1e-14
+
+
+def test_step_async_equals_step(gpu):
+    """ns_step_async is ns_step without the closing host sync: the same fields bit for bit, and
+    its monitor values are the previous step's (ns_monitor returns the latest)."""
+    n, dt, re = 96, 1.0 / 768, 400.0
+    a = gpu.GpuSolver(gpu.cavity(n), dt, re)
+    b = gpu.GpuSolver(gpu.cavity(n), dt, re)
+    sync = [a.step() for _ in range(6)]
+    lag = [b.step_async() for _ in range(6)]
+    assert all(np.isnan(lag[0][k]) for k in ("umin", "umax", "vmin", "vmax"))
+    for k in range(1, 6):
+        assert [lag[k][q] for q in ("umin", "umax", "vmin", "vmax")] == \
+               [sync[k - 1][q] for q in ("umin", "umax", "vmin", "vmax")], k
+        assert (lag[k]["it_u"], lag[k]["it_phi"]) == (sync[k]["it_u"], sync[k]["it_phi"])
+    assert b.monitor() == (sync[5]["umin"], sync[5]["umax"], sync[5]["vmin"], sync[5]["vmax"])
+    with pytest.raises(gpu.NsError):
+        b.monitor()   # nothing pending
+    for x, y in zip(a.fields(), b.fields()):
+        assert np.array_equal(x, y)
+    # a synchronous step after async ones continues the same trajectory
+    assert a.step()["umax"] == b.step()["umax"]
+
+
+def test_known_answer_trace_128_async(gpu):
+    """The reference's printed 128^2 monitor through ns_step_async (one step late)."""
+    n = 128
+    gs = gpu.GpuSolver(gpu.cavity(n), 1.0 / 1024, 100.0)
+    for it in range(1, 202):
+        st = gs.step_async() if it <= 200 else None
+        got = gs.monitor() if it == 201 else (st["umin"], st["umax"], st["vmin"], st["vmax"])
+        if it - 1 in KNOWN_TRACE_128:
+            assert all(printed_equal(x, y) for x, y in zip(got, KNOWN_TRACE_128[it - 1])), (it - 1, got)
+
+
+def test_concurrent_helmholtz_streams_bit_identical(gpu, monkeypatch):
+    """NSGPU_HELM_CONC=1 (v's passes on a second stream, concurrent with u's) gives the same
+    steps bit for bit."""
+    n, dt, re = 160, 1.0 / 1280, 1000.0
+    out = {}
+    for conc in ("0", "1"):
+        monkeypatch.setenv("NSGPU_HELM_CONC", conc)
+        gs = gpu.GpuSolver(gpu.cavity(n), dt, re)
+        st = [gs.step() for _ in range(4)]
+        out[conc] = (st, gs.fields())
+        gs.close()
+    assert [s["umax"] for s in out["0"][0]] == [s["umax"] for s in out["1"][0]]
+    for x, y in zip(out["0"][1], out["1"][1]):
+        assert np.array_equal(x, y)
