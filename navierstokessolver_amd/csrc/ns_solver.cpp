@@ -130,6 +130,11 @@ struct ns_solver {
     int helm_conc = 0;
     hipStream_t st2 = nullptr;
     hipEvent_t cev[2] = {nullptr, nullptr};
+    // NSGPU_EXTRAP_CONC (single rank): the phi extrapolation (HBM-bound) on st2 alongside K1
+    // (fp64-issue-bound) instead of under the Helmholtz check's host wait: K1 258 -> 317 us,
+    // the extrapolation 83 -> 247 us, +0.2 % on the step; off, so the kernel profile stays readable
+    int extrap_conc = 0;
+    hipEvent_t xev2[2] = {nullptr, nullptr};
     int helm_ns = 2;             // Helmholtz sweeps per pass on one slab (NSGPU_HELM_NS: 2, 3, 4)
     int phi_extrap = 2;          // Poisson initial guess: NSGPU_PHI_EXTRAP=0 phi^{n-1}, 1 linear, 2 quadratic (default)
     int mg_predict = 1;          // NSGPU_MG_PREDICT=0: a residual check (host sync) after every V-cycle
@@ -325,6 +330,14 @@ int fetch_end(ns_solver* s) {
     return 0;
 }
 int extrapolate_phi(ns_solver* s);
+// the second stream (NSGPU_HELM_CONC, NSGPU_EXTRAP_CONC) and its fork / join events
+int ensure_st2(ns_solver* s) {
+    if (s->st2) return 0;
+    HIPCHK(hipStreamCreateWithFlags(&s->st2, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&s->cev[0], &s->cev[1], &s->xev2[0], &s->xev2[1]})
+        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return 0;
+}
 
 int ensure_events(ns_solver* s, size_t n) {
     while (s->ev.size() < n) {
@@ -400,11 +413,7 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
         ~Restore() { s->st = st; }
     } restore{s, main_st};
     if (conc) {
-        if (!s->st2) {
-            HIPCHK(hipStreamCreateWithFlags(&s->st2, hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&s->cev[0], hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&s->cev[1], hipEventDisableTiming));
-        }
+        CHK(ensure_st2(s));
         // fork: v's chain starts from the same point as u's
         HIPCHK(hipEventRecord(s->cev[0], s->st));
         HIPCHK(hipStreamWaitEvent(s->st2, s->cev[0], 0));
@@ -1646,6 +1655,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_SPLIT")) s->helm_split = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_CONC")) s->helm_conc = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_EXTRAP_CONC")) s->extrap_conc = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_NS")) s->helm_ns = std::max(2, std::min(4, std::atoi(e)));
     if (const char* e = getenv("NSGPU_HELM_EXTRAP")) s->helm_extrap = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(2, std::atoi(e)));
@@ -1794,7 +1804,7 @@ void ns_destroy(ns_solver* s) {
     if (s->st2) (void)hipStreamSynchronize(s->st2);
     if (s->mev) (void)hipEventDestroy(s->mev);
     if (s->mm_host) (void)hipHostFree(s->mm_host);
-    for (auto e : s->cev)
+    for (auto e : {s->cev[0], s->cev[1], s->xev2[0], s->xev2[1]})
         if (e) (void)hipEventDestroy(e);
     if (s->st2) (void)hipStreamDestroy(s->st2);
     for (auto e : s->ev) (void)hipEventDestroy(e);
@@ -1827,7 +1837,24 @@ void ns_destroy(ns_solver* s) {
 
 // the step up to CorrectVelocities (its min/max reduced into scal[S_MM], not yet fetched)
 static int step_body(ns_solver* s, ns_stats& st) {
+    // single rank: the Poisson initial guess (phi extrapolation: reads PHI and the history
+    // planes, writes TMP, which nothing reads before the Poisson solve) runs on st2 next to
+    // K1, which only reads PHI; the compute stream joins it after the Helmholtz solve
+    const bool xconc = s->extrap_conc && s->nranks == 1 && s->phim;
+    if (xconc) {
+        CHK(ensure_st2(s));
+        HIPCHK(hipEventRecord(s->xev2[0], s->st));
+    }
     CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
+    if (xconc) {   // (after K1's launch: it took the pre-rotation PHI pointer)
+        HIPCHK(hipStreamWaitEvent(s->st2, s->xev2[0], 0));
+        hipStream_t main_st = s->st;
+        s->st = s->st2;
+        const int rc = extrapolate_phi(s);
+        s->st = main_st;
+        CHK(rc);
+        HIPCHK(hipEventRecord(s->xev2[1], s->st2));
+    }
     // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
     CHK(helm_guess(s));
@@ -1836,9 +1863,10 @@ static int step_body(ns_solver* s, ns_stats& st) {
     if (s->nranks > 1 && s->overlap && s->cst && !s->g.fc && !s->tiled) s->helm_b_pend = 1;
     else CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
     s->hn = 0;
-    s->extrap_pending = s->phim ? 1 : 0;
+    s->extrap_pending = s->phim && !xconc ? 1 : 0;
     CHK(helm_solve(s, &st.it_u, &st.res_u, &st.res_v));            // KSPSolve(uSolver) x2 (:547-548)
     if (s->extrap_pending) { s->extrap_pending = 0; CHK(extrapolate_phi(s)); }
+    if (xconc) HIPCHK(hipStreamWaitEvent(s->st, s->xev2[1], 0));
     st.it_v = st.it_u;
     for (int k = 0; k < s->hn; k++) {   // (helm_solve's last residual check synchronised the stream)
         float ms = 0.f;
