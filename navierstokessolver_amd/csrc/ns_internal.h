@@ -100,6 +100,10 @@ int launch_pois_jacobi_tiled(const Geo& g, const Coef& c, double omega, const do
                              const double* rp, const double* shift, double* part, hipStream_t st);
 // rows per streaming strip (tuning knob)
 void set_strip_rows(int L);
+// the next kernel launch records a, b at its begin / end (hipExtLaunchKernel); pending() clears
+// the request and says whether no launch took it
+void time_next_launch(hipEvent_t a, hipEvent_t b);
+bool time_next_launch_pending();
 // strip subset of the following two-sweep pass launches (k_sweep2): 0 all, 1 the strips
 // whose read cone lies inside the slab, 2 the others (exchange / compute overlap)
 void set_strip_phase(int phase);

@@ -15,6 +15,7 @@
 //   K5 correct        40 B  CorrectVelocities / GradP (:420-456,512-534) + min/max (:554-557)
 // No MFMA: every kernel is a stencil far below the fp64 VALU ridge point; HBM bound.
 #include "ns_internal.h"
+#include <hip/hip_ext.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -2551,6 +2552,35 @@ int max_partials(const Geo& g) {
 
 namespace nsg {
 
+// Kernel timing with the dispatch's own timestamps: time_next_launch(a, b) makes the next launch
+// go through hipExtLaunchKernel with start / stop events a, b, which the runtime stamps at the
+// kernel's begin and end (the same interval rocprofv3's kernel trace reports).  HIP marker
+// events recorded around a launch also count its dispatch latency (~3 us at 4096^2).
+static thread_local hipEvent_t g_tev[2] = {nullptr, nullptr};
+void time_next_launch(hipEvent_t a, hipEvent_t b) { g_tev[0] = a; g_tev[1] = b; }
+bool time_next_launch_pending() {
+    const bool p = g_tev[0] != nullptr;
+    g_tev[0] = g_tev[1] = nullptr;
+    return p;
+}
+#define NS_LAUNCH(kern, grid, block, shmem, st, ...)                                                     \
+    do {                                                                                              \
+        if (::nsg::g_tev[0]) {                                                                        \
+            hipExtLaunchKernelGGL(kern, grid, block, shmem, st, ::nsg::g_tev[0], ::nsg::g_tev[1], 0, __VA_ARGS__); \
+            ::nsg::g_tev[0] = ::nsg::g_tev[1] = nullptr;                                              \
+        } else {                                                                                      \
+            hipLaunchKernelGGL(kern, grid, block, shmem, st, __VA_ARGS__);                            \
+        }                                                                                             \
+    } while (0)
+static hipError_t launch_raw(const void* k, dim3 grid, dim3 block, void** args, size_t shmem, hipStream_t st) {
+    if (g_tev[0]) {
+        const hipError_t e = hipExtLaunchKernel(k, grid, block, args, shmem, st, g_tev[0], g_tev[1], 0);
+        g_tev[0] = g_tev[1] = nullptr;
+        return e;
+    }
+    return hipLaunchKernel(k, grid, block, args, shmem, st);
+}
+
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
                const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st) {
     const char* e = getenv("NSGPU_RHS");   // NSGPU_RHS=global: the global-load K1 (A/B)
@@ -2560,7 +2590,7 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         const int rows = cell_rows(g);
         const dim3 cg = cell_grid(g, rows);
         if (g_phase != 1)
-            hipLaunchKernelGGL(k_rhs<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
+            NS_LAUNCH(k_rhs<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
         return (int)(cg.x * cg.y);
     }
     if (!(e && std::strcmp(e, "global") == 0)) {
@@ -2569,18 +2599,18 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         const int nrun = phase_range(g.nxl, RT, nti, 2, &tlo, &thi0);   // MUSCL: rows li0-2 .. li0+RT+1
         const int nb = ((g.ny + 63) / 64) * nti;
         if (nrun > 0)
-            hipLaunchKernelGGL(k_rhs_lds, dim3((g.ny + 63) / 64, nrun), dim3(64, 4), 0, st, g, c, dt, re, u, v, phi,
+            NS_LAUNCH(k_rhs_lds, dim3((g.ny + 63) / 64, nrun), dim3(64, 4), 0, st, g, c, dt, re, u, v, phi,
                                cu, cv, ru, rv, part, tlo, thi0);
         const int nbc = (2 * g.nxl + 2 * g.ny + 255) / 256;
         // the wall terms read phi's ghost rows: with the edge phase
         if (g_phase != 1)
-            hipLaunchKernelGGL(k_rhs_bc, dim3(nbc), dim3(256), 0, st, g, c, dt, re, phi, ru, rv, part + 2 * nb);
+            NS_LAUNCH(k_rhs_bc, dim3(nbc), dim3(256), 0, st, g, c, dt, re, phi, ru, rv, part + 2 * nb);
         return nb + nbc;
     }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
     if (g_phase != 1)
-        hipLaunchKernelGGL(k_rhs<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
+        NS_LAUNCH(k_rhs<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
     return (int)(cg.x * cg.y);
 }
 
@@ -2594,7 +2624,7 @@ static int launch_cell_s(CellStreamArgs A, hipStream_t st) {
     A.nsi = (A.g.nxl + A.L - 1) / A.L;
     const int nstr = A.nsj * A.nsi;
     A.nrun = phase_range(A.g.nxl, A.L, A.nsi, 1, &A.slo, &A.shi0);   // window rows ib-1 .. ie
-    if (A.nrun > 0) hipLaunchKernelGGL(k_cell_s<K>, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), 0, st, A);
+    if (A.nrun > 0) NS_LAUNCH(k_cell_s<K>, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), 0, st, A);
     return nstr;
 }
 
@@ -2613,8 +2643,8 @@ int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const do
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
     if (g_phase == 1) return (int)(cg.x * cg.y);   // (cannot split: all with the edge phase)
-    if (g.fc) hipLaunchKernelGGL(k_div<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part, rows);
-    else hipLaunchKernelGGL(k_div<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part, rows);
+    if (g.fc) NS_LAUNCH(k_div<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part, rows);
+    else NS_LAUNCH(k_div<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, u, v, rp, part, rows);
     return (int)(cg.x * cg.y);
 }
 
@@ -2622,36 +2652,36 @@ int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double
                  double* part, hipStream_t st) {
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
-    if (op == 0 && g.fc) hipLaunchKernelGGL((k_apply<0, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
-    else if (op == 0) hipLaunchKernelGGL((k_apply<0, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
-    else if (g.fc) hipLaunchKernelGGL((k_apply<1, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
-    else hipLaunchKernelGGL((k_apply<1, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
+    if (op == 0 && g.fc) NS_LAUNCH((k_apply<0, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
+    else if (op == 0) NS_LAUNCH((k_apply<0, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
+    else if (g.fc) NS_LAUNCH((k_apply<1, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
+    else NS_LAUNCH((k_apply<1, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
     return (int)(cg.x * cg.y);
 }
 
 void launch_diag_pc(int op, const Geo& g, const Coef& c, double alpha, const double* q, double* z, hipStream_t st) {
     const dim3 cg = cell_grid(g);
-    if (op == 0 && g.fc) hipLaunchKernelGGL((k_diag_pc<0, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
-    else if (op == 0) hipLaunchKernelGGL((k_diag_pc<0, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
-    else if (g.fc) hipLaunchKernelGGL((k_diag_pc<1, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
-    else hipLaunchKernelGGL((k_diag_pc<1, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
+    if (op == 0 && g.fc) NS_LAUNCH((k_diag_pc<0, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
+    else if (op == 0) NS_LAUNCH((k_diag_pc<0, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
+    else if (g.fc) NS_LAUNCH((k_diag_pc<1, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
+    else NS_LAUNCH((k_diag_pc<1, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
 }
 
 int launch_bicg_vec(int mode, KrylovArgs a, hipStream_t st) {
     a.rows = cell_rows(a.g);
     const dim3 cg = cell_grid(a.g, a.rows);
     switch (mode) {
-        case KV_INIT: hipLaunchKernelGGL(k_bicg_vec<KV_INIT>, cg, dim3(64, 4), 0, st, a); break;
-        case KV_P: hipLaunchKernelGGL(k_bicg_vec<KV_P>, cg, dim3(64, 4), 0, st, a); break;
-        case KV_V: hipLaunchKernelGGL(k_bicg_vec<KV_V>, cg, dim3(64, 4), 0, st, a); break;
-        case KV_T: hipLaunchKernelGGL(k_bicg_vec<KV_T>, cg, dim3(64, 4), 0, st, a); break;
-        default: hipLaunchKernelGGL(k_bicg_vec<KV_X>, cg, dim3(64, 4), 0, st, a); break;
+        case KV_INIT: NS_LAUNCH(k_bicg_vec<KV_INIT>, cg, dim3(64, 4), 0, st, a); break;
+        case KV_P: NS_LAUNCH(k_bicg_vec<KV_P>, cg, dim3(64, 4), 0, st, a); break;
+        case KV_V: NS_LAUNCH(k_bicg_vec<KV_V>, cg, dim3(64, 4), 0, st, a); break;
+        case KV_T: NS_LAUNCH(k_bicg_vec<KV_T>, cg, dim3(64, 4), 0, st, a); break;
+        default: NS_LAUNCH(k_bicg_vec<KV_X>, cg, dim3(64, 4), 0, st, a); break;
     }
     return (int)(cg.x * cg.y);
 }
 
 void launch_bicg_scal(int stage, const double* d, double n, double* sc, hipStream_t st) {
-    hipLaunchKernelGGL(k_bicg_scal, dim3(1), dim3(1), 0, st, stage, d, n, sc);
+    NS_LAUNCH(k_bicg_scal, dim3(1), dim3(1), 0, st, stage, d, n, sc);
 }
 
 int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, const double* vs, double* u, double* v,
@@ -2665,8 +2695,8 @@ int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, con
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
     if (g_phase == 1) return (int)(cg.x * cg.y);   // (cannot split: all with the edge phase)
-    if (g.fc) hipLaunchKernelGGL(k_correct<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part, rows);
-    else hipLaunchKernelGGL(k_correct<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part, rows);
+    if (g.fc) NS_LAUNCH(k_correct<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part, rows);
+    else NS_LAUNCH(k_correct<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, us, vs, u, v, phi, part, rows);
     return (int)(cg.x * cg.y);
 }
 
@@ -2754,8 +2784,8 @@ static int launch_stream(StreamArgs a, hipStream_t st, bool count_only = false) 
     a.nsi = (a.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
     if (count_only) return nstr;
-    if (a.part) hipLaunchKernelGGL((k_sweep<OP, RB, true>), dim3(nblk), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_sweep<OP, RB, false>), dim3(nblk), dim3(256), 0, st, a);
+    if (a.part) NS_LAUNCH((k_sweep<OP, RB, true>), dim3(nblk), dim3(256), 0, st, a);
+    else NS_LAUNCH((k_sweep<OP, RB, false>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 
@@ -2776,8 +2806,8 @@ static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st, bool count
     a.nsi = (g.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = apply_phase(a, a.part ? 5 : 4);
     if (count_only || !nblk) return nstr;
-    if (a.part) hipLaunchKernelGGL((k_sweep2<OP, true, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_sweep2<OP, false, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
+    if (a.part) NS_LAUNCH((k_sweep2<OP, true, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
+    else NS_LAUNCH((k_sweep2<OP, false, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 
@@ -2790,7 +2820,7 @@ int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const
     a.L = strip_rows(a.nxl, a.nsj, resident_waves((const void*)k_sweep2<0, false, FUSE_R>), 16);
     a.nsi = (g.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = apply_phase(a, 5);
-    if (nblk) hipLaunchKernelGGL((k_sweep2<0, false, FUSE_R>), dim3(nblk), dim3(256), 0, st, a);
+    if (nblk) NS_LAUNCH((k_sweep2<0, false, FUSE_R>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 
@@ -2806,7 +2836,7 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
     a.L = strip_rows(a.nxl, a.nsj, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 16);
     a.nsi = (g.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = apply_phase(a, 5);
-    if (nblk) hipLaunchKernelGGL((k_sweep2<0, false, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
+    if (nblk) NS_LAUNCH((k_sweep2<0, false, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 
@@ -2817,7 +2847,7 @@ int launch_pois_tile2_restrict(const Geo& g, const Coef& c, double omega, const 
     StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
     a.hx = c.hx; a.hy = c.hy; a.bc = bc; a.pc = pc; a.ldc = gc.ld;
     const int tj = (g.ny + TT - 1) / TT, ntiles = tj * ((g.nxl + TT - 1) / TT);
-    hipLaunchKernelGGL(k_tile2<FUSE_R>, dim3(ntiles), dim3(256), 0, st, a, tj);
+    NS_LAUNCH(k_tile2<FUSE_R>, dim3(ntiles), dim3(256), 0, st, a, tj);
     return ntiles;
 }
 
@@ -2827,7 +2857,7 @@ int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const d
     StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, nullptr, false);
     a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0;
     const int tj = (g.ny + TT - 1) / TT, ntiles = tj * ((g.nxl + TT - 1) / TT);
-    hipLaunchKernelGGL(k_tile2<FUSE_P>, dim3(ntiles), dim3(256), 0, st, a, tj);
+    NS_LAUNCH(k_tile2<FUSE_P>, dim3(ntiles), dim3(256), 0, st, a, tj);
     return ntiles;
 }
 
@@ -2862,8 +2892,8 @@ static int launch_streamN(StreamArgs a, const Geo& g, hipStream_t st, bool count
     a.nsi = (g.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
     if (count_only) return nstr;
-    if (a.part) hipLaunchKernelGGL((k_sweepN<OP, NS, true>), dim3(nblk), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_sweepN<OP, NS, false>), dim3(nblk), dim3(256), 0, st, a);
+    if (a.part) NS_LAUNCH((k_sweepN<OP, NS, true>), dim3(nblk), dim3(256), 0, st, a);
+    else NS_LAUNCH((k_sweepN<OP, NS, false>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 
@@ -2901,7 +2931,7 @@ static int launch_jacobi_s(const Geo& g, const Coef& c, double omega, const T* i
     a.nsi = (a.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
     void* args[] = {&a};
-    if (hipLaunchKernel(k, dim3(nblk), dim3(256), args, 0, st) != hipSuccess) return -1;
+    if (launch_raw(k, dim3(nblk), dim3(256), args, 0, st) != hipSuccess) return -1;
     return nstr;
 }
 
@@ -2923,11 +2953,11 @@ int launch_pois_jacobi32(const Geo& g, const Coef& c, double omega, const float*
 
 void launch_to_f32(const Geo& g, const double* src, float* dst, hipStream_t st) {
     const long n = (long)g.nxl * g.ld;
-    hipLaunchKernelGGL(k_to_f32, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, st, src, dst, n);
+    NS_LAUNCH(k_to_f32, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, st, src, dst, n);
 }
 void launch_to_f64(const Geo& g, const float* src, double* dst, hipStream_t st) {
     const long n = (long)g.nxl * g.ld;
-    hipLaunchKernelGGL(k_to_f64, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, st, src, dst, n);
+    NS_LAUNCH(k_to_f64, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0, st, src, dst, n);
 }
 
 int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
@@ -2955,8 +2985,8 @@ int launch_pois_rbsor_tiled(const Geo& g, const Coef& c, double omega, const dou
     a.omega = omega;
     a.alpha = 0.0;
     a.part = part;
-    if (part) hipLaunchKernelGGL((k_rb_sweep<PTI, PTJ, 0, 1, true>), dim3(a.ntiles), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_rb_sweep<PTI, PTJ, 0, 1, false>), dim3(a.ntiles), dim3(256), 0, st, a);
+    if (part) NS_LAUNCH((k_rb_sweep<PTI, PTJ, 0, 1, true>), dim3(a.ntiles), dim3(256), 0, st, a);
+    else NS_LAUNCH((k_rb_sweep<PTI, PTJ, 0, 1, false>), dim3(a.ntiles), dim3(256), 0, st, a);
     return a.ntiles;
 }
 
@@ -2967,7 +2997,7 @@ int launch_pois_jacobi_tiled(const Geo& g, const Coef& c, double omega, const do
     a.shift = shift;
     a.omega = omega;
     a.part = part;
-    hipLaunchKernelGGL((k_jacobi<JTI, JTJ>), dim3(a.ntiles), dim3(256), 0, st, a, in, out, 1);
+    NS_LAUNCH((k_jacobi<JTI, JTJ>), dim3(a.ntiles), dim3(256), 0, st, a, in, out, 1);
     return a.ntiles;
 }
 
@@ -2978,7 +3008,7 @@ int launch_pois_residual(const Geo& g, const Coef& c, const double* phi, const d
     a.shift = shift;
     a.omega = 0.0;
     a.part = part;
-    hipLaunchKernelGGL((k_jacobi<JTI, JTJ>), dim3(a.ntiles), dim3(256), 0, st, a, phi, (double*)nullptr, 0);
+    NS_LAUNCH((k_jacobi<JTI, JTJ>), dim3(a.ntiles), dim3(256), 0, st, a, phi, (double*)nullptr, 0);
     return a.ntiles;
 }
 
@@ -2986,13 +3016,13 @@ int launch_restrict(const Geo& gf, const Coef& cf, const double* phi, const doub
                     const Geo& gc, const Coef& cc, double* bc, double* pc, double* part, hipStream_t st) {
     const int rows = cell_rows(gc);
     const dim3 cg = cell_grid(gc, rows);
-    hipLaunchKernelGGL(k_restrict, cg, dim3(64, 4), 0, st, gf, cf, phi, b, shift, gc, cc, bc, pc, part, rows);
+    NS_LAUNCH(k_restrict, cg, dim3(64, 4), 0, st, gf, cf, phi, b, shift, gc, cc, bc, pc, part, rows);
     return (int)(cg.x * cg.y);
 }
 
 void launch_prolong(const Geo& gf, double* phi, const Geo& gc, const double* ec, hipStream_t st) {
     const int rows = cell_rows(gf);
-    hipLaunchKernelGGL(k_prolong, cell_grid(gf, rows), dim3(64, 4), 0, st, gf, phi, gc, ec, rows);
+    NS_LAUNCH(k_prolong, cell_grid(gf, rows), dim3(64, 4), 0, st, gf, phi, gc, ec, rows);
 }
 
 size_t coarse_vcycle_bytes(const Geo& g) { return sizeof(double) * (size_t)lv_layout(g.nx, g.ny, nullptr, nullptr); }
@@ -3006,42 +3036,42 @@ int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double*
         (void)hipFuncSetAttribute((const void*)k_coarse_vcycle, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k_coarse_vcycle, dim3(1), dim3(CV_THREADS), bytes, st, g, c, phi, b, cycles, pre, post, citers,
+    NS_LAUNCH(k_coarse_vcycle, dim3(1), dim3(CV_THREADS), bytes, st, g, c, phi, b, cycles, pre, post, citers,
                        comega, somega);
     return 0;
 }
 
 void launch_reduce_sum(const double* p, int n, int nv, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(k_reduce_sum, dim3(1), dim3(1024), 0, st, p, n, nv, out);
+    NS_LAUNCH(k_reduce_sum, dim3(1), dim3(1024), 0, st, p, n, nv, out);
 }
 void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(k_reduce_min, dim3(1), dim3(1024), 0, st, p, n, nv, out);
+    NS_LAUNCH(k_reduce_min, dim3(1), dim3(1024), 0, st, p, n, nv, out);
 }
 void launch_finish_mean(const double* sums, double ncells, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(k_finish_mean, dim3(1), dim3(1), 0, st, sums, ncells, out);
+    NS_LAUNCH(k_finish_mean, dim3(1), dim3(1), 0, st, sums, ncells, out);
 }
 int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st) {
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
-    hipLaunchKernelGGL(k_sums, cg, dim3(64, 4), 0, st, g, f, part, rows);
+    NS_LAUNCH(k_sums, cg, dim3(64, 4), 0, st, g, f, part, rows);
     return (int)(cg.x * cg.y);
 }
 void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st,
                   double c, const double* z) {
-    hipLaunchKernelGGL(k_axpby, cell_grid(g), dim3(64, 4), 0, st, g, a, x, b, y, c, z, out);
+    NS_LAUNCH(k_axpby, cell_grid(g), dim3(64, 4), 0, st, g, a, x, b, y, c, z, out);
 }
 int launch_area_sum(const Geo& g, const Coef& c, const double* b, double* part, hipStream_t st) {
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
-    hipLaunchKernelGGL(k_area_sum, cg, dim3(64, 4), 0, st, g, c, b, part, rows);
+    NS_LAUNCH(k_area_sum, cg, dim3(64, 4), 0, st, g, c, b, part, rows);
     return (int)(cg.x * cg.y);
 }
 void launch_area_fix(const Geo& g, const Coef& c, double* b, const double* sab, const double* shift, double area,
                      double inv_area, double n, double* kshift, hipStream_t st) {
-    hipLaunchKernelGGL(k_area_fix, cell_grid(g), dim3(64, 4), 0, st, g, c, b, sab, shift, area, inv_area, n, kshift);
+    NS_LAUNCH(k_area_fix, cell_grid(g), dim3(64, 4), 0, st, g, c, b, sab, shift, area, inv_area, n, kshift);
 }
 void launch_fill_random(const Geo& g, double* phi, double* rp, uint64_t seed, hipStream_t st) {
-    hipLaunchKernelGGL(k_fill_random, cell_grid(g), dim3(64, 4), 0, st, g, phi, rp, seed);
+    NS_LAUNCH(k_fill_random, cell_grid(g), dim3(64, 4), 0, st, g, phi, rp, seed);
 }
 
 }  // namespace nsg

@@ -127,6 +127,7 @@ struct ns_solver {
     int helm_split = 1;          // NSGPU_HELM_SPLIT=0: u and v pass by pass (A/B)
     // NSGPU_HELM_CONC=1 (single rank, split): v's passes on a second stream, concurrent with
     // u's, so each chain's dependent-kernel boundaries (launch + drain) overlap the other's work
+    int ext_timing = 1;          // NSGPU_EXT_TIMING=0: marker events around timed launches (t_begin)
     int helm_conc = 0;
     hipStream_t st2 = nullptr;
     hipEvent_t cev[2] = {nullptr, nullptr};
@@ -330,6 +331,30 @@ int fetch_end(ns_solver* s) {
     return 0;
 }
 int extrapolate_phi(ns_solver* s);
+
+// A timed kernel call.  One rank: the call is a single launch, timed by the dispatch's own
+// begin / end stamps (hipExtLaunchKernel's events: the interval rocprofv3's kernel trace
+// reports).  Multi-rank calls (exchanges, split launches) and NSGPU_EXT_TIMING=0: marker
+// events around the call, which also count the launch's dispatch latency.
+int t_begin(ns_solver* s, hipEvent_t a, hipEvent_t b) {
+    if (s->nranks == 1 && s->ext_timing) {
+        nsg::time_next_launch(a, b);
+        return 0;
+    }
+    HIPCHK(hipEventRecord(a, s->st));
+    return 0;
+}
+int t_end(ns_solver* s, hipEvent_t a, hipEvent_t b) {
+    if (s->nranks == 1 && s->ext_timing) {
+        if (nsg::time_next_launch_pending()) {   // the call launched no kernel: an empty interval
+            HIPCHK(hipEventRecord(a, s->st));
+            HIPCHK(hipEventRecord(b, s->st));
+        }
+        return 0;
+    }
+    HIPCHK(hipEventRecord(b, s->st));
+    return 0;
+}
 // the second stream (NSGPU_HELM_CONC, NSGPU_EXTRAP_CONC) and its fork / join events
 int ensure_st2(ns_solver* s) {
     if (s->st2) return 0;
@@ -371,7 +396,7 @@ int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3, int ns 
             for (size_t k = old; k < s->hev.size(); k++)
                 if (hipEventCreate(&s->hev[k]) != hipSuccess) { set_err("hipEventCreate failed"); return -1; }
         }
-        if (hipEventRecord(s->hev[2 * s->hn], s->st) != hipSuccess) { set_err("hipEventRecord failed"); return -1; }
+        if (t_begin(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]) != 0) return -1;
     }
     int nb;
     if (ns > 2) {   // ns sweeps of one component in one pass (single slab)
@@ -386,7 +411,7 @@ int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3, int ns 
                                      s->arr[NS_ARR_RV], part, s->st, which);
     }
     if (t) {
-        if (hipEventRecord(s->hev[2 * s->hn + 1], s->st) != hipSuccess) { set_err("hipEventRecord failed"); return -1; }
+        if (t_end(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]) != 0) return -1;
         s->hn++;
     }
     if (which & 1) std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
@@ -667,9 +692,9 @@ int pois_solve(ns_solver* s, int* its, double* res, ns_stats* stt) {
         for (int k = 0; k < n; k++) {
             double* part = k == n - 1 ? s->part : nullptr;
             CHK(halo(s, {s->arr[NS_ARR_PHI]}, 2));
-            if (s->timing) HIPCHK(hipEventRecord(s->ev[2 * k], s->st));
+            if (s->timing) CHK(t_begin(s, s->ev[2 * k], s->ev[2 * k + 1]));
             nb = pois_sweep(s, part);
-            if (s->timing) HIPCHK(hipEventRecord(s->ev[2 * k + 1], s->st));
+            if (s->timing) CHK(t_end(s, s->ev[2 * k], s->ev[2 * k + 1]));
         }
         sweeps += n;
         nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
@@ -819,11 +844,11 @@ int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
         const int w = (n - k >= 2 && pair_level(s, l)) ? 2 : 1;   // two sweeps per HBM pass
         CHK(halo_l(s, l, {L.phi}, 2 * w));
         const bool t = s->timing && l == 0 && !s->pc_active;
-        if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st)); s->evtag[ev0 + *tn] = 0; }
+        if (t) { CHK(t_begin(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); s->evtag[ev0 + *tn] = 0; }
         const double* sh = l == 0 ? shift0(s) : nullptr;
         if (w == 2) nsg::launch_pois_rbsor2(L.g, L.c, s->mg_omega_s, L.phi, L.tmp, L.b, sh, nullptr, s->st);
         else nsg::launch_pois_rbsor(L.g, L.c, s->mg_omega_s, L.phi, L.tmp, L.b, sh, nullptr, s->st);
-        if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn) + 1], s->st)); (*tn)++; }
+        if (t) { CHK(t_end(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); (*tn)++; }
         std::swap(L.phi, L.tmp);
         if (l == 0) { s->arr[NS_ARR_PHI] = L.phi; s->arr[NS_ARR_TMP] = L.tmp; }
         k += w;
@@ -869,7 +894,7 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
             // last two pre-smoothing sweeps + residual + restriction in one HBM pass
             CHK(mg_smooth(s, l, s->mg_pre - 2, tn, ev0));
             const bool t = s->timing && l == 0 && !s->pc_active;
-            if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st)); s->evtag[ev0 + *tn] = 1; }
+            if (t) { CHK(t_begin(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); s->evtag[ev0 + *tn] = 1; }
             if (tile_level(s, l)) {
                 CHK(flush_b(s, l));
                 CHK(halo_l(s, l, {F.phi}, 5));
@@ -889,7 +914,7 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
                 });
                 if (nb < 0) return nb;
             }
-            if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn) + 1], s->st)); (*tn)++; }
+            if (t) { CHK(t_end(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); (*tn)++; }
             std::swap(F.phi, F.tmp);
             if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
         } else {
@@ -922,7 +947,7 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
                 return (tile_level(s, l) ? nsg::launch_pois_tile2_prolong : nsg::launch_pois_rbsor2_prolong)(
                     F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, shp, cv.g, cv.phi, s->st);
             };
-            if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn)], s->st)); s->evtag[ev0 + *tn] = 0; }
+            if (t) { CHK(t_begin(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); s->evtag[ev0 + *tn] = 0; }
             if (F.repl) {
                 pass();
             } else if (tile_level(s, l)) {
@@ -935,7 +960,7 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
                 const int n = overlapped(s, r, (cv.gather || C.repl) ? 1 : 2, pass);
                 if (n < 0) return n;
             }
-            if (t) { HIPCHK(hipEventRecord(s->ev[2 * (ev0 + *tn) + 1], s->st)); (*tn)++; }
+            if (t) { CHK(t_end(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); (*tn)++; }
             std::swap(F.phi, F.tmp);
             if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
             CHK(mg_smooth(s, l, s->mg_post - 2, tn, ev0));
@@ -1655,6 +1680,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_SPLIT")) s->helm_split = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_CONC")) s->helm_conc = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_EXT_TIMING")) s->ext_timing = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_EXTRAP_CONC")) s->extrap_conc = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_NS")) s->helm_ns = std::max(2, std::min(4, std::atoi(e)));
     if (const char* e = getenv("NSGPU_HELM_EXTRAP")) s->helm_extrap = std::atoi(e) != 0;
@@ -2190,9 +2216,9 @@ int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
     };
     for (int k = 0; k < warmup; k++) CHK(one(nullptr));
     for (int k = 0; k < iters; k++) {
-        HIPCHK(hipEventRecord(s->ev[2 * k], s->st));
+        CHK(t_begin(s, s->ev[2 * k], s->ev[2 * k + 1]));
         CHK(one(k == iters - 1 ? s->part : nullptr));
-        HIPCHK(hipEventRecord(s->ev[2 * k + 1], s->st));
+        CHK(t_end(s, s->ev[2 * k], s->ev[2 * k + 1]));
     }
     HIPCHK(hipStreamSynchronize(s->st));
     double tot = 0.0;
@@ -2216,9 +2242,9 @@ int ns_time_poisson_fp32(ns_solver* s, int warmup, int iters, double* out) {
     int nb = 0;
     for (int k = 0; k < warmup; k++) CHK(pois_sweep32(s, nullptr, &nb));
     for (int k = 0; k < iters; k++) {
-        HIPCHK(hipEventRecord(s->ev[2 * k], s->st));
+        CHK(t_begin(s, s->ev[2 * k], s->ev[2 * k + 1]));
         CHK(pois_sweep32(s, nullptr, &nb));
-        HIPCHK(hipEventRecord(s->ev[2 * k + 1], s->st));
+        CHK(t_end(s, s->ev[2 * k], s->ev[2 * k + 1]));
     }
     nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
     CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));

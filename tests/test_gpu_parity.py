@@ -630,3 +630,24 @@ def test_side_stream_extrapolation_bit_identical(gpu, monkeypatch, bc):
     assert [(s["it_u"], s["it_phi"]) for s in out["0"][0]] == [(s["it_u"], s["it_phi"]) for s in out["1"][0]]
     for x, y in zip(out["0"][1], out["1"][1]):
         assert np.array_equal(x, y)
+
+
+def test_dispatch_stamped_kernel_timing(gpu, monkeypatch):
+    """Timed launches use hipExtLaunchKernel's begin / end stamps (the kernel's own interval,
+    what rocprofv3 reports); NSGPU_EXT_TIMING=0 brackets them with marker events, which also
+    count the dispatch latency.  Both are positive; the dispatch-stamped interval is not longer;
+    step timings stay positive and per-pass."""
+    n = 1024
+    avg = {}
+    for ext in ("1", "0"):
+        monkeypatch.setenv("NSGPU_EXT_TIMING", ext)
+        js = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0, poisson=gpu.NS_POISSON_JACOBI, omega=1.0)
+        js.fill_random(0x5EED)
+        avg[ext] = min(js.time_poisson(5, 20)["avg_ms"] for _ in range(3))
+        js.close()
+        gs = gpu.GpuSolver(gpu.cavity(2 * n), 1.0 / (16 * n), 1000.0, timing=True)
+        st = [gs.step() for _ in range(3)]
+        assert all(s["n_helm_kernels"] > 0 and s["t_helm_kernel_ms"] > 0 for s in st)
+        assert all(s["n_restrict_kernels"] > 0 and s["t_restrict_kernel_ms"] > 0 for s in st)
+        gs.close()
+    assert 0 < avg["1"] <= avg["0"] * 1.02, avg
