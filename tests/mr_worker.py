@@ -28,6 +28,8 @@ ap.add_argument("--poly", default="", help="a tests/polygons.py geometry instead
 ap.add_argument("--sweep32", type=int, default=0,
                 help="instead of time steps: K fp32-field Jacobi sweeps (NS_K_POISSON32) of the random input")
 ap.add_argument("--stats-only", action="store_true", help="gather only the per-step stats (large grids)")
+ap.add_argument("--async-steps", action="store_true",
+                help="ns_step_async (monitor one call late, realigned here) instead of ns_step")
 a = ap.parse_args()
 dist.init_process_group("gloo")
 rank, world = dist.get_rank(), dist.get_world_size()
@@ -56,6 +58,11 @@ try:
     if a.sweep32:
         gs.fill_random(0x5EED)
         mm = [list(gs.kernel(nsa.NS_K_POISSON32, a.sweep32)[:1])]
+    elif a.async_steps:
+        mm = [list(gs.step_async().values())[:7] for _ in range(a.nsteps)]
+        last = list(gs.monitor())
+        for k in range(a.nsteps):   # step k's monitor arrived with step k + 1 (the last via ns_monitor)
+            mm[k][:4] = mm[k + 1][:4] if k + 1 < a.nsteps else last
     else:
         mm = [list(gs.step().values())[:7] for _ in range(a.nsteps)]
     u, v, phi = (np.zeros((1, ny)),) * 3 if a.stats_only else gs.fields()

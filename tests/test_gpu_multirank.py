@@ -174,3 +174,14 @@ def test_rccl_two_ranks_one_gpu_probe(tmp_path):
         pytest.skip(f"RCCL refused: {r['status']}")
     u, v, phi, mm = single(48, 40, 4, nsa.NS_POISSON_RBSOR, 1e-10)
     assert np.max(np.abs(r["u"] - u)) <= 1e-9
+
+
+def test_async_steps_on_slabs_match_sync(tmp_path):
+    """ns_step_async on 2 slabs (host transport): the same fields and, realigned by one call,
+    the same min/max monitor and iteration counts as ns_step -- bit for bit."""
+    args = ["--xport", "host", "--size", "128", "--size-y", "96", "--nsteps", "5", "--tol", "1e-10"]
+    a = launch(tmp_path, *args, port=29651)
+    b = launch(tmp_path, *args, "--async-steps", port=29653)
+    assert str(a["status"]) == "ok" and str(b["status"]) == "ok", (a["status"], b["status"])
+    for k in ("u", "v", "phi", "mm"):
+        assert np.array_equal(a[k], b[k]), k
