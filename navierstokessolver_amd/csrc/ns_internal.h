@@ -115,6 +115,8 @@ int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, con
                    const double* phi, double* part, hipStream_t st);
 // reductions: sum `nv` interleaved values over n partials (p[k*nv + v]) -> out[v]
 void launch_reduce_sum(const double* p, int n, int nv, double* out, hipStream_t st);
+// nseg contiguous segments of n partials -> out[0..nseg) (k_reduce_sum's order per segment)
+void launch_reduce_sum_segs(const double* p, int n, int nseg, double* out, hipStream_t st);
 // min/max: partials are (umin, -umax, vmin, -vmax) per block -> out[4] = mins of each
 void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t st);
 // Poisson prep: from sums (S, S2) and N -> shift = S/N, out[1] = S2 - S^2/N (= ||b||^2)

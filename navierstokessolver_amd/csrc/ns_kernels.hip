@@ -2276,6 +2276,26 @@ __global__ __launch_bounds__(1024) void k_reduce_sum(const double* __restrict__ 
     }
 }
 
+// nseg contiguous segments of n partials -> out[seg]: one launch instead of nseg, each segment
+// summed exactly as k_reduce_sum (nv = 1) sums it
+__global__ __launch_bounds__(1024) void k_reduce_sum_segs(const double* __restrict__ p, int n, int nseg,
+                                                          double* __restrict__ out) {
+    __shared__ double sh[1024];
+    for (int g = 0; g < nseg; g++) {
+        const double* q = p + (size_t)g * n;
+        double s = 0.0;
+        for (int k = threadIdx.x; k < n; k += 1024) s += q[k];
+        sh[threadIdx.x] = s;
+        __syncthreads();
+        for (int w = 512; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[g] = sh[0];
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(1024) void k_reduce_min(const double* __restrict__ p, int n, int nv,
                                                      double* __restrict__ out) {
     __shared__ double sh[1024];
@@ -3043,6 +3063,9 @@ int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double*
 
 void launch_reduce_sum(const double* p, int n, int nv, double* out, hipStream_t st) {
     NS_LAUNCH(k_reduce_sum, dim3(1), dim3(1024), 0, st, p, n, nv, out);
+}
+void launch_reduce_sum_segs(const double* p, int n, int nseg, double* out, hipStream_t st) {
+    NS_LAUNCH(k_reduce_sum_segs, dim3(1), dim3(1024), 0, st, p, n, nseg, out);
 }
 void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t st) {
     NS_LAUNCH(k_reduce_min, dim3(1), dim3(1024), 0, st, p, n, nv, out);

@@ -617,12 +617,8 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         const int nb = helm_sweeps(s, alpha, n, first ? p0 : nullptr, s->part, &nb0, &at0, &at);
         at += sweeps;
         sweeps += n;
-        nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
-        nsg::launch_reduce_sum(s->part + nb, nb, 1, s->scal + S_RES + 1, s->st);
-        if (first) {
-            nsg::launch_reduce_sum(p0, nb0, 1, s->scal + S_AUX, s->st);
-            nsg::launch_reduce_sum(p0 + nb0, nb0, 1, s->scal + S_AUX + 1, s->st);
-        }
+        nsg::launch_reduce_sum_segs(s->part, nb, 2, s->scal + S_RES, s->st);          // u, v
+        if (first) nsg::launch_reduce_sum_segs(p0, nb0, 2, s->scal + S_AUX, s->st);
         CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
         if (first) CHK(allreduce(s, s->scal + S_AUX, 2, ncclSum));
         CHK(fetch_begin(s));
@@ -2054,8 +2050,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
             nb = helm_sweep(s, alpha, k == iters - 1 ? s->part : nullptr);
         }
         if (iters > 0) {
-            nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
-            nsg::launch_reduce_sum(s->part + nb, nb, 1, s->scal + S_RES + 1, s->st);
+            nsg::launch_reduce_sum_segs(s->part, nb, 2, s->scal + S_RES, s->st);
             CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
         }
         CHK(fetch(s));
