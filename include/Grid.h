@@ -5,11 +5,15 @@
 // types and the bcTypes enum the reference's FluidSolver reads.
 //
 // Differences by design (DESIGN.md "Host boundary"):
-//   * the mesh is also kept in compact form (cell-id plane + 4 face tags per
-//     cell, ~20 B/cell) which is what FluidSolver hands to libnsgpu.so;
+//   * the mesh is also kept in compact form, which is what FluidSolver hands to
+//     libnsgpu.so: a polygon keeps a cell-id plane + 4 face tags per cell (~20 B/cell);
+//     a rectangle (4 edges: every cell inside) keeps nothing per cell -- its ids
+//     (i*ny + j) and face tags (the side's edge) are answered by cellId() / faceEdge();
 //   * the per-cell `cells` table of the reference (~190 B/cell) is only
-//     materialised up to NS_GRID_CELLS_MAX cells (default 2^26); above that it
-//     stays empty and `inDomain` answers from the compact plane.
+//     materialised up to NS_GRID_CELLS_MAX cells (default 2^22 = 2048^2, ~0.8 GB);
+//     above that it stays empty and `inDomain` answers from the compact form;
+//   * CellCenters.csv (Grid.cpp:221-231) is skipped when the driver was started with
+//     -no_export (ns_export_files, set by PetscInitialize).
 #ifndef NS_AMD_GRID_H
 #define NS_AMD_GRID_H
 
@@ -67,9 +71,19 @@ public:
     // ---- compact form used by FluidSolver / libnsgpu.so ----
     int nxCells() const { return (int)hx.size(); }
     int nyCells() const { return (int)hy.size(); }
-    const vector<int32_t>& cellIds() const { return id_; }       // i*ny + j -> id or -1
-    const vector<int32_t>& faceEdges() const { return tag_; }    // (i*ny + j)*4 + k -> edge or -1
+    // polygon only (empty for a rectangle): i*ny + j -> id or -1; (i*ny + j)*4 + k -> edge or -1
+    const vector<int32_t>& cellIds() const { return id_; }
+    const vector<int32_t>& faceEdges() const { return tag_; }
     bool isRectangle() const { return rect_; }
+    // any domain: compact id of cell (i, j) or -1; boundary edge on face k (W, E, S, N) or -1
+    int32_t cellId(int i, int j) const {
+        return rect_ ? (int32_t)((size_t)i * nyCells() + j) : id_[(size_t)i * nyCells() + j];
+    }
+    int32_t faceEdge(int i, int j, int k) const {
+        if (!rect_) return tag_[((size_t)i * nyCells() + j) * 4 + k];
+        const bool onside = k == 0 ? i == 0 : k == 1 ? i == nxCells() - 1 : k == 2 ? j == 0 : j == nyCells() - 1;
+        return onside ? side_[k] : -1;
+    }
     double centerX(int i) const { return 0.5 * (X[i] + X[i + 1]); }
     double centerY(int j) const { return 0.5 * (Y[j] + Y[j + 1]); }
 
@@ -79,6 +93,7 @@ private:
     double arlo_ = 1E15, arhi_ = -1E15;
     vector<int32_t> id_, tag_;
     bool rect_ = false;
+    int32_t side_[4] = {-1, -1, -1, -1};   // rectangle: the edge on the W, E, S, N side
     bool readFile(ifstream& in);
     bool buildEdges();
     bool buildFaces();
@@ -88,5 +103,8 @@ private:
 };
 
 bool equals(double a, double b);
+
+// false: skip CellCenters.csv and FlowData_<iter>.csv (the -no_export option)
+extern bool ns_export_files;
 
 #endif

@@ -13,9 +13,13 @@
  *     ns_last_error() holds the message (thread-local).  Nothing throws or aborts.
  *   - the caller owns all host buffers; the library copies them.
  *   - one host thread drives one ns_solver (handles are not thread-safe).
- *   - fields are exchanged in the reference's compact cell-id order
- *     (i outer / x, j inner / y: Grid.cpp:149-162).  With nranks > 1 each rank
- *     exchanges its own x-slab (global rows ns_slab_range()).
+ *   - ns_get_fields / ns_set_fields exchange fields in the reference's compact
+ *     cell-id order (the PETSc Vec of FluidSolver.h:6-18; ids i outer / x, j inner / y,
+ *     cells outside the polygon skipped: Grid.cpp:149-162).  With nranks > 1 each rank
+ *     exchanges its own x-slab: the compact ids ns_local_cells() names, i.e. the
+ *     domain's cells in global rows ns_slab_range().  ns_get_array / ns_set_array copy
+ *     the slab's nx_local x ny bounding-box plane instead (the same thing for a
+ *     rectangle; 0 outside a polygon).
  *   - all state lives in HBM; ns_step() synchronises with the host once per
  *     residual check and once at the end of the step (its ns_stats), mirroring
  *     the reference's per-step printf (FluidSolver.cpp:554-560).
@@ -29,7 +33,8 @@
 extern "C" {
 #endif
 
-#define NSGPU_ABI_VERSION 2   /* 2: ns_grid_desc.face_edge (non-rectangular domains) */
+#define NSGPU_ABI_VERSION 3   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
+                                 3: ns_get/set_fields in compact-id order on polygons, ns_local_cells */
 
 typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm */
 
@@ -171,10 +176,15 @@ int  ns_monitor(ns_solver* s, double* mm /* [4]: umin, umax, vmin, vmax */);
 /* per-kernel HIP-event timing (ns_params.timing) switched on / off between steps */
 int  ns_set_timing(ns_solver* s, int on);
 
-/* ---- state access (host buffers, local slab, compact-id order) ---- */
+/* ---- state access (host buffers, local slab) ----
+ * ns_get_fields / ns_set_fields: compact-id order (prevField->u, v, phi and
+ * convectiveDer_u0 / _v0, FluidSolver.h:6-18 / FluidSolver.cpp:40-43), `count` doubles each
+ * as ns_local_cells reports; element k is the cell with compact id first_id + k.
+ * ns_get_array / ns_set_array: the slab's nx_local x ny bounding-box plane of any NS_ARR_*. */
 int  ns_get_fields(ns_solver* s, double* u, double* v, double* phi);
 int  ns_set_fields(ns_solver* s, const double* u, const double* v, const double* phi,
                    const double* cu0, const double* cv0);
+int  ns_local_cells(ns_solver* s, int64_t* first_id, int64_t* count);
 int  ns_get_array(ns_solver* s, int which, double* host);
 int  ns_set_array(ns_solver* s, int which, const double* host);
 

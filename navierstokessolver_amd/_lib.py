@@ -81,6 +81,7 @@ SIGNATURES = {
     "ns_monitor": (ctypes.c_int, [_P, _D]),
     "ns_get_fields": (ctypes.c_int, [_P, _D, _D, _D]),
     "ns_set_fields": (ctypes.c_int, [_P, _D, _D, _D, _D, _D]),
+    "ns_local_cells": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "ns_get_array": (ctypes.c_int, [_P, ctypes.c_int, _D]),
     "ns_set_array": (ctypes.c_int, [_P, ctypes.c_int, _D]),
     "ns_kernel": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _D]),

@@ -185,6 +185,11 @@ struct ns_solver {
     ns_host_transport ht{};      // host transport (ht.exchange != NULL) instead of RCCL
     double* stage = nullptr;     // pinned staging for the host transport
     size_t stage_n = 0;
+    // masked domain: this slab's bounding-box cells -> compact cell id - cid0 (-1 outside), so
+    // ns_get_fields / ns_set_fields speak the reference's compact Vec order (Grid.cpp:149-162)
+    std::vector<int32_t> cid;
+    int64_t cid0 = 0, ncid = 0;  // first compact id of the slab and its in-domain cell count
+    std::vector<double> hbuf;    // host bounding-box staging for that gather / scatter
 };
 
 namespace {
@@ -1646,6 +1651,30 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
 
     ns_solver* s = new ns_solver();
     s->g = g;
+    if (masked) {
+        // compact ids of this slab (i outer, j inner: ids increase along the slab's rows)
+        const int32_t* c = gd->cell_id + (size_t)g.i0 * gd->ny;
+        const size_t n = (size_t)g.nxl * gd->ny;
+        s->cid.assign(c, c + n);
+        int64_t lo = -1, cnt = 0;
+        for (size_t k = 0; k < n; k++)
+            if (c[k] >= 0) {
+                if (lo < 0) lo = c[k];
+                cnt++;
+            }
+        s->cid0 = lo < 0 ? 0 : lo;
+        s->ncid = cnt;
+        for (size_t k = 0; k < n; k++) {
+            if (c[k] < 0) continue;
+            const int64_t r = c[k] - s->cid0;
+            if (r < 0 || r >= cnt) {
+                set_err("cell_id is not the compact i-outer / j-inner numbering of Grid.cpp:149-162 (id %d)", c[k]);
+                delete s;
+                return NS_EINVAL;
+            }
+            s->cid[k] = (int32_t)r;
+        }
+    }
     s->dt = p->dt;
     s->re = p->re;
     s->rtol = p->rtol > 0 ? p->rtol : 1e-8;
@@ -2007,20 +2036,49 @@ int ns_set_array(ns_solver* s, int which, const double* host) {
     return 0;
 }
 
+// the reference's compact Vec order (prevField->u, v, phi: FluidSolver.h:6-18, ids from
+// Grid.cpp:149-162): a rectangle's compact order IS the bounding-box plane; a masked domain's
+// fields are gathered / scattered through the slab's id map (cells outside stay exactly 0)
+static int get_compact(ns_solver* s, int which, double* out) {
+    if (s->cid.empty()) return ns_get_array(s, which, out);
+    s->hbuf.resize(s->cid.size());
+    CHK(ns_get_array(s, which, s->hbuf.data()));
+    for (size_t k = 0; k < s->cid.size(); k++)
+        if (s->cid[k] >= 0) out[s->cid[k]] = s->hbuf[k];
+    return 0;
+}
+
+static int set_compact(ns_solver* s, int which, const double* in) {
+    if (s->cid.empty()) return ns_set_array(s, which, in);
+    s->hbuf.assign(s->cid.size(), 0.0);
+    for (size_t k = 0; k < s->cid.size(); k++)
+        if (s->cid[k] >= 0) s->hbuf[k] = in[s->cid[k]];
+    return ns_set_array(s, which, s->hbuf.data());
+}
+
+int ns_local_cells(ns_solver* s, int64_t* first_id, int64_t* count) {
+    if (!s) { set_err("null solver"); return NS_EINVAL; }
+    if (first_id) *first_id = s->cid.empty() ? (int64_t)s->g.i0 * s->g.ny : s->cid0;
+    if (count) *count = s->cid.empty() ? (int64_t)s->g.nxl * s->g.ny : s->ncid;
+    return 0;
+}
+
 int ns_get_fields(ns_solver* s, double* u, double* v, double* phi) {
-    if (u) CHK(ns_get_array(s, NS_ARR_U, u));
-    if (v) CHK(ns_get_array(s, NS_ARR_V, v));
-    if (phi) CHK(ns_get_array(s, NS_ARR_PHI, phi));
+    if (!s) { set_err("null solver"); return NS_EINVAL; }
+    if (u) CHK(get_compact(s, NS_ARR_U, u));
+    if (v) CHK(get_compact(s, NS_ARR_V, v));
+    if (phi) CHK(get_compact(s, NS_ARR_PHI, phi));
     return 0;
 }
 
 int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* phi, const double* cu0,
                   const double* cv0) {
-    if (u) CHK(ns_set_array(s, NS_ARR_U, u));
-    if (v) CHK(ns_set_array(s, NS_ARR_V, v));
-    if (phi) CHK(ns_set_array(s, NS_ARR_PHI, phi));
-    if (cu0) CHK(ns_set_array(s, NS_ARR_CU, cu0));
-    if (cv0) CHK(ns_set_array(s, NS_ARR_CV, cv0));
+    if (!s) { set_err("null solver"); return NS_EINVAL; }
+    if (u) CHK(set_compact(s, NS_ARR_U, u));
+    if (v) CHK(set_compact(s, NS_ARR_V, v));
+    if (phi) CHK(set_compact(s, NS_ARR_PHI, phi));
+    if (cu0) CHK(set_compact(s, NS_ARR_CU, cu0));
+    if (cv0) CHK(set_compact(s, NS_ARR_CV, cv0));
     return 0;
 }
 

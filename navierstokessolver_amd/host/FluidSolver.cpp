@@ -45,6 +45,7 @@ PetscErrorCode PetscInitialize(int* argc, char*** argv, const char*, const char*
             g_opt.device = std::atoi(next());
         } else if (!std::strcmp(a, "-no_export")) {
             g_opt.do_export = false;
+            ns_export_files = false;   // CellCenters.csv too (Grid.cpp)
         } else {
             keep.push_back((*argv)[k]);  // positional arguments (grid file, sim file) stay
         }
@@ -199,7 +200,7 @@ void write_flow_csv(int iter, Grid& g, double dt, double re, const vector<double
             if (!g.inDomain(i, j)) continue;   // a polygon's bounding-box cells outside the domain
             const size_t c = id(i, j);
             double lap = 0.0, dg = 0.0;
-            const int32_t* t = &g.faceEdges()[c * 4];
+            const int32_t t[4] = {g.faceEdge(i, j, 0), g.faceEdge(i, j, 1), g.faceEdge(i, j, 2), g.faceEdge(i, j, 3)};
             for (int k = 0; k < 4; k++) {
                 const int ii = i + di[k], jj = j + dj[k];
                 if (g.inDomain(ii, jj)) {
@@ -243,7 +244,7 @@ void FluidSolver::Solve() {
     Impl& m = *impl_;
     cout << "Initiating Solver..\n";
     const size_t n = (size_t)m.nx * m.ny;
-    vector<double> u(n), v(n), phi(n);
+    vector<double> u, v, phi;   // host copies for the export only (allocated on the first one)
     int iter = 1;
     do {
         ns_stats st{};
@@ -255,7 +256,10 @@ void FluidSolver::Solve() {
         printf("%d\t%lf\t%lf\t%lf\t%lf\n", iter, st.umin, st.umax, st.vmin, st.vmax);
         if (g_opt.do_export && m.p.saveIter > 0 && iter % m.p.saveIter == 0) {
             fflush(stdout);
-            if (ns_get_fields(m.gpu, u.data(), v.data(), phi.data()) == 0)
+            if (u.empty()) u.resize(n), v.resize(n), phi.resize(n);
+            // the bounding-box planes (the export's stencil walks (i, j) neighbours)
+            if (ns_get_array(m.gpu, NS_ARR_U, u.data()) == 0 && ns_get_array(m.gpu, NS_ARR_V, v.data()) == 0 &&
+                ns_get_array(m.gpu, NS_ARR_PHI, phi.data()) == 0)
                 write_flow_csv(iter, *grid, m.p.dt, m.p.re, u, v, phi);
         }
         iter++;

@@ -14,6 +14,8 @@
 
 bool equals(double a, double b) { return std::fabs(a - b) <= TOL; }
 
+bool ns_export_files = true;
+
 namespace {
 
 // read "{ row ; row ; ... }" where each row fills up to `width` numbers (missing
@@ -137,44 +139,61 @@ bool Grid::buildFaces() {
 
 // GenerateCells + Cleanup + Interior (Grid.cpp:131-185): ray cast along +x counts
 // crossings of vertical edges; faces lying on an edge get that edge's index.
+// A 4-edge polygon is a rectangle (every cell inside, ids i*ny + j, each side one edge):
+// nothing is stored per cell, cellId() / faceEdge() answer from the side table.
 void Grid::classify() {
     cout << "Generating Cells...\n";
     const int nx = nxCells(), ny = nyCells();
-    id_.assign((size_t)nx * ny, -1);
-    tag_.assign((size_t)nx * ny * 4, -1);
     const int ne = (int)edges.size();
-    int n = 0;
-    for (int i = 0; i < nx; i++) {
-        const double xw = X[i], xe = X[i + 1], xc = 0.5 * (xw + xe);
-        for (int j = 0; j < ny; j++) {
-            const double ys = Y[j], yn = Y[j + 1], yc = 0.5 * (ys + yn);
-            int32_t* t = &tag_[((size_t)i * ny + j) * 4];
-            int crossings = 0;
-            for (int k = 0; k < ne; k++) {
-                const Edge& e = edges[k];
-                if (e.nx != 0) {
-                    if (!(yc > e.loc[1] && yc < e.loc[2])) continue;
-                    if (e.loc[0] > xc) crossings++;
-                    if (e.nx == -1 && equals(xw, e.loc[0])) t[0] = k;
-                    if (e.nx == 1 && equals(xe, e.loc[0])) t[1] = k;
-                } else {
-                    if (!(xc > e.loc[1] && xc < e.loc[2])) continue;
-                    if (e.ny == -1 && equals(ys, e.loc[0])) t[2] = k;
-                    if (e.ny == 1 && equals(yn, e.loc[0])) t[3] = k;
+    if (ne == 4) {
+        rect_ = true;
+        N = nx * ny;
+        const int snx[4] = {-1, 1, 0, 0}, sny[4] = {0, 0, -1, 1};
+        for (int k = 0; k < ne; k++)
+            for (int f = 0; f < 4; f++)
+                if (edges[k].nx == snx[f] && edges[k].ny == sny[f]) side_[f] = k;
+        // the aspect-ratio range of the cells: min / max of (xe - xw) / (yn - ys) (monotone
+        // in each factor, so the extremes pair the extreme widths and heights)
+        double dxlo = 1E300, dxhi = -1E300, dylo = 1E300, dyhi = -1E300;
+        for (int i = 0; i < nx; i++) dxlo = std::min(dxlo, X[i + 1] - X[i]), dxhi = std::max(dxhi, X[i + 1] - X[i]);
+        for (int j = 0; j < ny; j++) dylo = std::min(dylo, Y[j + 1] - Y[j]), dyhi = std::max(dyhi, Y[j + 1] - Y[j]);
+        arlo_ = dxlo / dyhi;
+        arhi_ = dxhi / dylo;
+    } else {
+        id_.assign((size_t)nx * ny, -1);
+        tag_.assign((size_t)nx * ny * 4, -1);
+        int n = 0;
+        for (int i = 0; i < nx; i++) {
+            const double xw = X[i], xe = X[i + 1], xc = 0.5 * (xw + xe);
+            for (int j = 0; j < ny; j++) {
+                const double ys = Y[j], yn = Y[j + 1], yc = 0.5 * (ys + yn);
+                int32_t* t = &tag_[((size_t)i * ny + j) * 4];
+                int crossings = 0;
+                for (int k = 0; k < ne; k++) {
+                    const Edge& e = edges[k];
+                    if (e.nx != 0) {
+                        if (!(yc > e.loc[1] && yc < e.loc[2])) continue;
+                        if (e.loc[0] > xc) crossings++;
+                        if (e.nx == -1 && equals(xw, e.loc[0])) t[0] = k;
+                        if (e.nx == 1 && equals(xe, e.loc[0])) t[1] = k;
+                    } else {
+                        if (!(xc > e.loc[1] && xc < e.loc[2])) continue;
+                        if (e.ny == -1 && equals(ys, e.loc[0])) t[2] = k;
+                        if (e.ny == 1 && equals(yn, e.loc[0])) t[3] = k;
+                    }
+                }
+                if (crossings % 2) {
+                    id_[(size_t)i * ny + j] = n++;
+                    const double ar = (xe - xw) / (yn - ys);
+                    arlo_ = std::min(arlo_, ar);
+                    arhi_ = std::max(arhi_, ar);
                 }
             }
-            if (crossings % 2) {
-                id_[(size_t)i * ny + j] = n++;
-                const double ar = (xe - xw) / (yn - ys);
-                arlo_ = std::min(arlo_, ar);
-                arhi_ = std::max(arhi_, ar);
-            }
         }
+        N = n;
     }
-    N = n;
-    rect_ = (N == nx * ny) && edges.size() == 4;
     const char* cap = getenv("NS_GRID_CELLS_MAX");
-    const long long cellsMax = cap ? atoll(cap) : (1LL << 26);
+    const long long cellsMax = cap ? atoll(cap) : (1LL << 22);
     if ((long long)nx * ny > cellsMax) return;  // compact form only
     cells.assign(nx, vector<Cell>(ny));
     for (int i = 0; i < nx; i++)
@@ -184,9 +203,8 @@ void Grid::classify() {
             c.Y = {Y[j], Y[j + 1]};
             c.x = 0.5 * (X[i] + X[i + 1]);
             c.y = 0.5 * (Y[j] + Y[j + 1]);
-            c.id = id_[(size_t)i * ny + j];
-            const int32_t* t = &tag_[((size_t)i * ny + j) * 4];
-            c.edges = {t[0], t[1], t[2], t[3]};
+            c.id = cellId(i, j);
+            c.edges = {faceEdge(i, j, 0), faceEdge(i, j, 1), faceEdge(i, j, 2), faceEdge(i, j, 3)};
         }
 }
 
@@ -215,14 +233,15 @@ void Grid::ShowEdges(bool BC) {
 
 bool Grid::inDomain(int i, int j) {
     if (i < 0 || j < 0 || i >= nxCells() || j >= nyCells()) return false;
-    return id_[(size_t)i * nyCells() + j] >= 0;
+    return cellId(i, j) >= 0;
 }
 
 void Grid::writeCentres() {
+    if (!ns_export_files) return;   // -no_export
     ofstream out{"CellCenters.csv"};
     const int nx = nxCells(), ny = nyCells();
-    if (id_.empty()) return;
+    if (!setup) return;   // (the reference writes an empty file when setup failed)
     for (int i = 0; i < nx; i++)
         for (int j = 0; j < ny; j++)
-            if (id_[(size_t)i * ny + j] != -1) out << centerX(i) << "," << centerY(j) << endl;
+            if (cellId(i, j) != -1) out << centerX(i) << "," << centerY(j) << "\n";
 }

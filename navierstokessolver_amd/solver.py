@@ -144,7 +144,31 @@ class GpuSolver:
         L.check(L.lib().ns_set_array(self._h, which, _dptr(a)))
 
     def fields(self):
+        """u, v, phi as the slab's nx_local x ny bounding-box planes (ns_get_array)."""
         return self.get(L.NS_ARR_U), self.get(L.NS_ARR_V), self.get(L.NS_ARR_PHI)
+
+    def local_cells(self) -> tuple:
+        """(first compact id, count) of this slab's in-domain cells (ns_local_cells)."""
+        a, n = ctypes.c_int64(), ctypes.c_int64()
+        L.check(L.lib().ns_local_cells(self._h, ctypes.byref(a), ctypes.byref(n)))
+        return a.value, n.value
+
+    def fields_compact(self):
+        """u, v, phi in the reference's compact Vec order (ns_get_fields; Grid.cpp:149-162)."""
+        n = self.local_cells()[1]
+        u, v, p = (np.empty(n) for _ in range(3))
+        L.check(L.lib().ns_get_fields(self._h, _dptr(u), _dptr(v), _dptr(p)))
+        return u, v, p
+
+    def set_fields_compact(self, u=None, v=None, phi=None, cu0=None, cv0=None) -> None:
+        """ns_set_fields: any of u, v, phi, convectiveDer_u0 / _v0 in compact Vec order."""
+        n = self.local_cells()[1]
+        keep = [None if a is None else np.ascontiguousarray(np.asarray(a, dtype=np.float64).ravel())
+                for a in (u, v, phi, cu0, cv0)]
+        for a in keep:
+            if a is not None and a.size != n:
+                raise ValueError(f"compact field of {a.size} values; this slab holds {n} cells")
+        L.check(L.lib().ns_set_fields(self._h, *[None if a is None else _dptr(a) for a in keep]))
 
     def kernel(self, which: int, iters: int = 1) -> np.ndarray:
         out = np.zeros(8, dtype=np.float64)

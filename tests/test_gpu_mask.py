@@ -125,3 +125,36 @@ def test_mask_rectangle_only_entry_points_fail_loudly(gpu):
     for k in (gpu.NS_K_HELMHOLTZ, gpu.NS_K_POISSON, gpu.NS_K_RESIDUAL):
         with pytest.raises(gpu.NsError):
             gs.kernel(k, 1)
+
+
+@pytest.mark.parametrize("name", ["lshape", "step"])
+def test_mask_compact_fields_through_the_c_abi(gpu, name):
+    """ns_set_fields / ns_get_fields speak the reference's compact Vec order (FluidSolver.h:6-18,
+    ids from Grid.cpp:149-162): the oracle's state after a few steps goes in as compact N-vectors,
+    both sides step on, and the compact vectors that come back are compared with the oracle's
+    directly (no bounding-box plane in between).  Tolerance: the full-step bar, 1e-6."""
+    P = ALL[name]
+    n = max(P["xspec"][-1][2], P["yspec"][-1][2])
+    dt, re = 1.0 / (16 * n), 200.0
+    og, gs, m = pair(gpu, name, dt, re)
+    assert gs.local_cells() == (0, og.N)
+    osv = OSolver(og, dt, re, rtol=1e-13)
+    for _ in range(4):
+        osv.step()
+    ref = osv.get()
+    gs.set_fields_compact(ref["u"], ref["v"], ref["phi"], ref["cu"], ref["cv"])
+    u, v, phi = gs.fields_compact()
+    assert u.shape == (og.N,)
+    np.testing.assert_array_equal(u, ref["u"])     # a plain round trip is exact
+    np.testing.assert_array_equal(phi, ref["phi"])
+    assert not np.any(gs.get(gpu.NS_ARR_U).ravel()[~m]), "cells outside the domain must stay 0"
+    for _ in range(3):
+        st = gs.step()
+        mm, _ = osv.step()
+        np.testing.assert_allclose([st["umin"], st["umax"], st["vmin"], st["vmax"]], mm, atol=1e-6)
+    ref = osv.get()
+    u, v, phi = gs.fields_compact()
+    du, dv = float(np.max(np.abs(u - ref["u"]))), float(np.max(np.abs(v - ref["v"])))
+    assert du <= 1e-6 and dv <= 1e-6, (du, dv)
+    with pytest.raises(ValueError):
+        gs.set_fields_compact(u=np.zeros(og.N + 1))
