@@ -62,24 +62,60 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(n, re, dt, omega_v, omega_mg):
-    """The oracle (CPU restatement, 1 thread) running the SAME algorithm as the GPU path
-    (RB-SOR Helmholtz to rtol, multigrid Poisson to rtol 1e-8) for one full time step of
-    the same n^2 cavity (the first step from rest: a bounded sample, ~10-30 s)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from oracle import OGrid, OSolver  # CPU baseline leg only
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
-    g = OGrid.rectangle(n, n)
-    s = OSolver(g, dt, re, rtol=1e-8)
-    s.use_gpu_algorithm(omega_v, omega_mg)
-    t0 = time.perf_counter()
-    _, its = s.step()
-    t = time.perf_counter() - t0
+
+def _host_threads():
+    """The cores this process may use: the box's CPU share (OMP_NUM_THREADS is set to it on
+    the GPU pool; os.cpu_count() would name the whole machine), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(n, re, dt, omega_v, omega_mg, state):
+    """The oracle (CPU restatement, -O3, OpenMP) running the SAME algorithm as the GPU path
+    (RB-SOR Helmholtz to rtol, multigrid V(2,2) Poisson to rtol 1e-8) for one full time step
+    of the same n^2 cavity, from the GPU's own state after its warm-up + timed steps (u, v,
+    phi, the convective terms): a steady-state step, not the start-up one.
+    Timed at 1 thread (the serial reference) and at the host's cores (a bounded sample:
+    ~10-30 s in all).  value = the all-cores rate; value_1thread beside it."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # CPU baseline leg only
+
+    g = O.OGrid.rectangle(n, n)
+    gx, gy = g.grad_phi(state["phi"])
+    nt = _host_threads()
+    out = {}
+    for threads in (1, nt):
+        O.set_threads(threads)
+        s = O.OSolver(g, dt, re, rtol=1e-8)
+        s.use_gpu_algorithm(omega_v, omega_mg)
+        s.set(u=state["u"], v=state["v"], phi=state["phi"], cu=state["cu"], cv=state["cv"], gx=gx, gy=gy)
+        t0 = time.perf_counter()
+        _, its = s.step()
+        out[threads] = (time.perf_counter() - t0, [int(x) for x in its])
+        del s
+    O.set_threads(1)
+    t1, its1 = out[1]
+    tn, itsn = out[nt]
     return {
-        "value": g.N / t / 1e6, "unit": "MLUPS", "cores": 1, "kind": "port",
-        "sample": (f"one full time step (step 1 from rest) of the {n}^2 cavity in the oracle's C restatement "
-                   f"(oracle/ns_oracle.c), same algorithm as the GPU (MG Poisson: {its[2]} V-cycles, RB-SOR "
-                   f"Helmholtz: {its[0]} sweeps), 1 thread: {t:.1f} s"),
+        "value": g.N / tn / 1e6, "unit": "MLUPS", "cores": nt, "kind": "port",
+        "value_1thread": g.N / t1 / 1e6,
+        "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "threads_used": nt,
+        "sample": (f"one full time step of the {n}^2 cavity in the oracle's C restatement (oracle/ns_oracle.c, "
+                   f"-O3, OpenMP), started from the GPU's state after its timed steps; same algorithm as the GPU "
+                   f"(MG V(2,2) Poisson: {its1[2]} V-cycles from phi^(n-1) -- the GPU's extrapolated guess needs "
+                   f"fewer; RB-SOR Helmholtz: {its1[0]} sweeps per component), {t1:.1f} s on 1 thread, "
+                   f"{tn:.1f} s on {nt} threads"),
     }
 
 
@@ -150,6 +186,12 @@ def main():
              "helmholtz": (sum(s["t_helm_kernel_ms"] for s in stats), sum(s["n_helm_kernels"] for s in stats))}
     # finest-level sweeps: V(2,2) per cycle + the 2 pre-smoothing sweeps of the converged check
     fine_sweeps = 4 * cycles + 2 * K
+    # whole-step algorithmic bytes per cell: K1 64 + K3 24 + K5 40 + the phi
+    # extrapolation 32; Helmholtz 24 per pass, one pass = 2 sweeps of one component; multigrid
+    # per solve (cycles + 1) FUSE_R passes at 28 and `cycles` FUSE_P passes at 26 on the finest
+    # level, x 4/3 for the coarser levels (each a quarter of the one above)
+    step_bpc = (64 + 24 + 40 + 32 + 24 * hsweeps / K
+                + (28 * (cycles + K) + 26 * cycles) / K * 4.0 / 3.0)
     value = cells * K / elapsed / 1e6
 
     # the north star's roofline kernel: one Jacobi sweep of this rank's slab (random phi, b;
@@ -216,6 +258,11 @@ def main():
         "poisson_fine_sweeps_per_step": fine_sweeps / K,
         "helmholtz_sweeps_per_step": hsweeps / K,
         "roofline": kern.get(dominant),
+        "step_roofline": {"bound": "hbm", "bytes_per_cell": step_bpc, "bytes_per_step": step_bpc * cells,
+                          "achieved": step_bpc * cells / (elapsed / K) / 1e9, "peak": HBM_PEAK_GBS * world,
+                          "unit": "GB/s", "frac": step_bpc * cells / (elapsed / K) / 1e9 / (HBM_PEAK_GBS * world),
+                          "note": "every kernel's algorithmic bytes of a step / ms_per_step (host syncs, "
+                                  "kernel boundaries and latency-bound coarse levels included)"},
         "kernels": dict(kern),
     }
     if jacobi is not None:
@@ -225,7 +272,10 @@ def main():
                                                     jacobi32, 50)
     if world == 1 and not args.no_cpu:
         try:
-            line["cpu_baseline"] = cpu_baseline(n, re, dt, solver.omega_v, solver.mg_omega)
+            state = {k: solver.get(a).ravel() for k, a in (("u", nsa.NS_ARR_U), ("v", nsa.NS_ARR_V),
+                                                           ("phi", nsa.NS_ARR_PHI), ("cu", nsa.NS_ARR_CU),
+                                                           ("cv", nsa.NS_ARR_CV))}
+            line["cpu_baseline"] = cpu_baseline(n, re, dt, solver.omega_v, solver.mg_omega, state)
         except Exception as e:  # the baseline must never hide the GPU line
             line["cpu_baseline"] = {"error": repr(e)}
     print(json.dumps(line), flush=True)

@@ -1500,10 +1500,20 @@ int ns_abi_version(void) { return NSGPU_ABI_VERSION; }
 
 int ns_slab_range(int32_t nx, int32_t nranks, int32_t rank, int32_t* i0, int32_t* i1) {
     if (nx <= 0 || nranks <= 0 || rank < 0 || rank >= nranks) { set_err("bad slab arguments"); return NS_EINVAL; }
-    const int base = nx / nranks, rem = nx % nranks;
+    // balanced in units of U = 2^k rows (k <= 4, U | nx, at least one unit per rank): a slab edge
+    // then never splits a coarse cell of the first k multigrid coarsenings (16384^2 -> 1024^2,
+    // where the hierarchy is replicated), whatever the rank count (4096^2 on 3 ranks: 1376 /
+    // 1360 / 1360 rows instead of 1366 / 1365 / 1365, whose odd edges stopped the hierarchy at
+    // one level)
+    int k = 0;
+    while (k < 4 && nx % (2 << k) == 0) k++;
+    while (k > 0 && (nx >> k) < nranks) k--;
+    const int units = nx >> k;
+    if (units < nranks) { set_err("%d rows cannot be split over %d ranks", nx, nranks); return NS_EINVAL; }
+    const int base = units / nranks, rem = units % nranks;
     const int a = rank * base + std::min(rank, rem);
-    *i0 = a;
-    *i1 = a + base + (rank < rem ? 1 : 0);
+    *i0 = a << k;
+    *i1 = (a + base + (rank < rem ? 1 : 0)) << k;
     return 0;
 }
 
@@ -1815,7 +1825,15 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (p->mg_post > 0) s->mg_post = p->mg_post;
         if (int rc = build_levels(s, hx0, hy0)) return fail(rc);
         if (p->mg_coarse_iters > 0) s->mg_coarse_iters = p->mg_coarse_iters;
-        if (s->lv.size() < 2) s->poisson = NS_POISSON_RBSOR;  // nothing to coarsen: plain RB-SOR
+        if (s->lv.size() < 2) {
+            // nothing to coarsen: plain RB-SOR (O(n) sweeps per solve) -- say so when that is a
+            // real grid, not a toy
+            if ((long)g.nx * g.ny > 64L * 64L && s->rank == 0)
+                fprintf(stderr, "nsgpu: warning: the %d x %d grid cannot be coarsened (odd size%s): the multigrid "
+                        "Poisson solve falls back to red-black SOR sweeps\n", g.nx, g.ny,
+                        s->nranks > 1 ? " or slab edges" : "");
+            s->poisson = NS_POISSON_RBSOR;
+        }
         s->krylov_mg = true;
     }
     if (masked || g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3]) {

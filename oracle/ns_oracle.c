@@ -13,6 +13,13 @@
 
 static char og_err[512];
 const char* og_last_error(void) { return og_err; }
+
+/* OpenMP threads of the per-cell loops (1 unless og_set_threads: the checker stays serial;
+ * bench.py's cpu_baseline times 1 thread and the host's cores).  Loops write disjoint
+ * cells; a reduction's order depends only on the thread count. */
+static int og_nt = 1;
+void og_set_threads(int n) { og_nt = n > 0 ? n : 1; }
+int og_get_threads(void) { return og_nt; }
 static void set_err(const char* fmt, ...) {
     va_list ap; va_start(ap, fmt); vsnprintf(og_err, sizeof og_err, fmt, ap); va_end(ap);
 }
@@ -398,13 +405,15 @@ void og_rhs_velocity(const og_grid* g, double dt, double re, const double* u, co
                      const double* gx, const double* gy, double* cu, double* cv, double* ru, double* rv) {
     const double *hx = g->hx, *hy = g->hy;
     /* VecSet(0) ; VecAXPY(1, u) ; VecAXPY(0.5dt, conv0)  (:335-340) */
+#pragma omp parallel for schedule(static) num_threads(og_nt)
     for (int c = 0; c < g->N; c++) {
         ru[c] = 0.0 + 1.0 * u[c]; ru[c] += 0.5 * dt * cu[c];
         rv[c] = 0.0 + 1.0 * v[c]; rv[c] += 0.5 * dt * cv[c];
     }
-    double D[4], C[8], val;
+#pragma omp parallel for schedule(static) num_threads(og_nt)
     for (int i = 0; i < g->nx; i++)
         for (int j = 0; j < g->ny; j++) {
+            double D[4], C[8], val;
             int c = CID(g, i, j);
             if (c < 0) continue;
             diff_flux(g, re, u, i, j, 0, D);
@@ -455,6 +464,7 @@ static double div_v(const og_grid* g, const double* u, const double* v, int i, i
 }
 
 void og_divergence(const og_grid* g, double dt, const double* us, const double* vs, double* rhs) {
+#pragma omp parallel for schedule(static) num_threads(og_nt)
     for (int c = 0; c < g->N; c++) rhs[c] = div_v(g, us, vs, g->ci[c], g->cj[c]) / dt;
 }
 
@@ -470,8 +480,9 @@ static void grad_p(const og_grid* g, const double* p, int i, int j, double* gr) 
 }
 
 void og_grad_phi(const og_grid* g, const double* phi, double* gx, double* gy) {
-    double gr[2];
+#pragma omp parallel for schedule(static) num_threads(og_nt)
     for (int c = 0; c < g->N; c++) {
+        double gr[2];
         grad_p(g, phi, g->ci[c], g->cj[c], gr);
         gx[c] = gr[0]; gy[c] = gr[1];
     }
@@ -480,8 +491,9 @@ void og_grad_phi(const og_grid* g, const double* phi, double* gx, double* gy) {
 /* CorrectVelocities FluidSolver.cpp:512-534 */
 void og_correct(const og_grid* g, double dt, const double* us, const double* vs, const double* phi,
                 double* u, double* v, double* gx, double* gy) {
-    double gr[2];
+#pragma omp parallel for schedule(static) num_threads(og_nt)
     for (int c = 0; c < g->N; c++) {
+        double gr[2];
         grad_p(g, phi, g->ci[c], g->cj[c], gr);
         gx[c] = gr[0]; gy[c] = gr[1];
         u[c] = us[c] - dt * gr[0];
@@ -656,20 +668,58 @@ static inline double helm_rect(const og_grid* g, double a, const double* q, int 
     return s;
 }
 
+/* ||ru - (I - a L_V) u||^2 and the same for v (rectangle), in one pass */
+static void helm_resid2(const og_grid* g, double a, const double* u, const double* v, const double* ru,
+                        const double* rv, double* ru2, double* rv2) {
+    double su = 0.0, sv = 0.0;
+#pragma omp parallel for schedule(static) reduction(+ : su, sv) num_threads(og_nt)
+    for (int i = 0; i < g->nx; i++)
+        for (int j = 0; j < g->ny; j++) {
+            double d;
+            int c = i * g->ny + j;
+            double r1 = ru[c] - helm_rect(g, a, u, i, j, &d);
+            double r2v = rv[c] - helm_rect(g, a, v, i, j, &d);
+            su += r1 * r1;
+            sv += r2v * r2v;
+        }
+    *ru2 = su;
+    *rv2 = sv;
+}
+
+/* the two colour passes of one red-black SOR sweep of u and v */
+static void helm_rbsor_colours(const og_grid* g, double a, double* u, double* v, const double* ru,
+                               const double* rv, double omega) {
+    for (int color = 0; color < 2; color++)
+#pragma omp parallel for schedule(static) num_threads(og_nt)
+        for (int i = 0; i < g->nx; i++)
+            for (int j = (i + color) & 1; j < g->ny; j += 2) {
+                double d;
+                int c = i * g->ny + j;
+                double r1 = ru[c] - helm_rect(g, a, u, i, j, &d);
+                u[c] += omega * r1 / d;
+                double r2v = rv[c] - helm_rect(g, a, v, i, j, &d);
+                v[c] += omega * r2v / d;
+            }
+}
+
 double og_helmholtz_rbsor_sweep(const og_grid* g, double a, double* u, double* v, const double* ru,
                                 const double* rv, double omega) {
     if (!rect_dirichlet(g)) { set_err("sweeps need a rectangle with Dirichlet-type faces"); return -1; }
-    double r2 = 0.0, d;
+    double r2 = 0.0;
+#pragma omp parallel for schedule(static) reduction(+ : r2) num_threads(og_nt)
     for (int i = 0; i < g->nx; i++)
         for (int j = 0; j < g->ny; j++) {
+            double d;
             int c = i * g->ny + j;
             double r1 = ru[c] - helm_rect(g, a, u, i, j, &d);
             double r2v = rv[c] - helm_rect(g, a, v, i, j, &d);
             r2 += r1 * r1 + r2v * r2v;
         }
     for (int color = 0; color < 2; color++)
+#pragma omp parallel for schedule(static) num_threads(og_nt)
         for (int i = 0; i < g->nx; i++)
             for (int j = (i + color) & 1; j < g->ny; j += 2) {
+                double d;
                 int c = i * g->ny + j;
                 double r1 = ru[c] - helm_rect(g, a, u, i, j, &d);
                 u[c] += omega * r1 / d;
@@ -885,7 +935,9 @@ static double lap_at(const mg_level* L, const double* p, int i, int j) {
 
 /* one red-black sweep in place (red = (i+j) even first) */
 static void mg_rb(const mg_level* L, double* p, const double* b, double shift, double omega) {
+    const int nt = (size_t)L->nx * L->ny >= 65536 ? og_nt : 1;
     for (int color = 0; color < 2; color++)
+#pragma omp parallel for schedule(static) num_threads(nt)
         for (int i = 0; i < L->nx; i++)
             for (int j = (i + color) & 1; j < L->ny; j += 2) {
                 const double dg = -((L->cw[i] + L->ce[i]) + (L->cs[j] + L->cn[j]));
@@ -897,6 +949,8 @@ static void mg_rb(const mg_level* L, double* p, const double* b, double shift, d
 static double mg_restrict_lv(const mg_level* F, const double* phi, const double* b, double shift, const mg_level* C,
                              double* bc) {
     double r2 = 0.0;
+    const int nt = (size_t)F->nx * F->ny >= 65536 ? og_nt : 1;
+#pragma omp parallel for schedule(static) reduction(+ : r2) num_threads(nt)
     for (int I = 0; I < C->nx; I++)
         for (int J = 0; J < C->ny; J++) {
             double sum = 0.0;
@@ -914,6 +968,8 @@ static double mg_restrict_lv(const mg_level* F, const double* phi, const double*
 
 void og_mg_prolong(int nx, int ny, const double* ec, double* phi) {
     const int cnx = nx / 2, cny = ny / 2;
+    const int nt = (size_t)nx * ny >= 65536 ? og_nt : 1;
+#pragma omp parallel for schedule(static) num_threads(nt)
     for (int i = 0; i < nx; i++)
         for (int j = 0; j < ny; j++) {
             const int I = i >> 1, J = j >> 1;
@@ -1066,19 +1122,13 @@ int og_solver_step(og_solver* s, double* mm, int* its) {
         /* the GPU path's algorithm: RB-SOR Helmholtz from u^n, checked every sweep; MG Poisson */
         memcpy(s->us, s->u, sizeof(double) * n);
         memcpy(s->vs, s->v, sizeof(double) * n);
-        double bu = dot(n, s->ru, s->ru), bv = dot(n, s->rv, s->rv), r2;
+        double bu = dot(n, s->ru, s->ru), bv = dot(n, s->rv, s->rv);
         iu = 0;
         do {
-            double* tu = malloc(sizeof(double) * n);
-            double* tv = malloc(sizeof(double) * n);
-            og_apply_helmholtz(g, alpha, s->us, tu);
-            og_apply_helmholtz(g, alpha, s->vs, tv);
             double ru2 = 0, rv2 = 0;
-            for (int c = 0; c < n; c++) { ru2 += (s->ru[c] - tu[c]) * (s->ru[c] - tu[c]); rv2 += (s->rv[c] - tv[c]) * (s->rv[c] - tv[c]); }
-            free(tu); free(tv);
+            helm_resid2(g, alpha, s->us, s->vs, s->ru, s->rv, &ru2, &rv2);
             if ((ru2 <= s->rtol * s->rtol * bu || ru2 == 0) && (rv2 <= s->rtol * s->rtol * bv || rv2 == 0)) break;
-            r2 = og_helmholtz_rbsor_sweep(g, alpha, s->us, s->vs, s->ru, s->rv, s->omega_v);
-            (void)r2;
+            helm_rbsor_colours(g, alpha, s->us, s->vs, s->ru, s->rv, s->omega_v);
             iu++;
         } while (iu < maxit);
         iv = iu;

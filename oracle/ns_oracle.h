@@ -36,6 +36,11 @@ typedef struct og_solver og_solver;
 
 const char* og_last_error(void);
 
+/* OpenMP threads for the per-cell loops (default 1: the checker runs serially; bench.py's
+ * cpu_baseline times 1 thread and the host's cores). */
+void og_set_threads(int n);
+int  og_get_threads(void);
+
 /* Grid from a clockwise axis-parallel polygon (Grid.cpp:28-185).
  * xspec/yspec: nsx (nsy) rows of {start, end, ncells, ratio}; ratio -1 = uniform.
  * btype/binfo: one entry per polygon edge, in vertex order (FluidSolver.cpp:639-655). */

@@ -18,6 +18,8 @@ _I = ctypes.POINTER(ctypes.c_int)
 _P = ctypes.c_void_p
 _SIG = {
     "og_last_error": (ctypes.c_char_p, []),
+    "og_set_threads": (None, [ctypes.c_int]),
+    "og_get_threads": (ctypes.c_int, []),
     "og_grid_polygon": (_P, [ctypes.c_int, _D, _D, ctypes.c_int, _D, ctypes.c_int, _D, _I, _D]),
     "og_grid_free": (None, [_P]),
     "og_grid_N": (ctypes.c_int, [_P]),
@@ -62,6 +64,11 @@ def lib():
             f.restype, f.argtypes = r, a
         _lib = L
     return _lib
+
+
+def set_threads(n: int) -> None:
+    """OpenMP threads of the restatement's per-cell loops (default 1)."""
+    lib().og_set_threads(int(n))
 
 
 def _d(a):

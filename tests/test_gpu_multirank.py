@@ -42,6 +42,7 @@ def single(n, ny, steps, poisson, rtol, bc=None):
     (nsa.NS_POISSON_MG, 128, 96, True, "0", 2),
     (nsa.NS_POISSON_MG, 256, 128, False, "2048", 4),
     (nsa.NS_POISSON_MG, 264, 160, True, "4096", 3),
+    (nsa.NS_POISSON_MG, 256, 128, True, None, 3),   # 256 / 3: the old 86/85/85 rows stopped the hierarchy
 ])
 def test_slabs_host_transport_match_single_rank(tmp_path, monkeypatch, poisson, n, ny, pairs, agg, nproc):
     """pairs: every level smoothed by two-sweep passes with the fused restriction (5 ghost rows),
@@ -66,7 +67,8 @@ def test_slabs_host_transport_match_single_rank(tmp_path, monkeypatch, poisson, 
     # Helmholtz sweeps per step: the slabs' residual checks see the same residual as the
     # whole grid (a stale ghost row shows up as a solve that never reaches its tolerance)
     assert np.max(np.abs(r["mm"][:, 4] - mm[:, 4])) <= 2, (r["mm"][:, 4], mm[:, 4])
-    if poisson == nsa.NS_POISSON_MG and agg != "0" and n % nproc == 0 and (n // nproc) % 2 == 0:
+    edges = [nsa.slab_range(n, nproc, q)[0] for q in range(nproc)]
+    if poisson == nsa.NS_POISSON_MG and agg != "0" and all(e % 2 == 0 for e in edges) and n % 2 == 0:
         # agglomerated: the same hierarchy as one rank, so the same V-cycle count per step
         assert np.max(np.abs(r["mm"][:, 6] - mm[:, 6])) <= 1, (r["mm"][:, 6], mm[:, 6])
 
