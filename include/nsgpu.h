@@ -132,6 +132,8 @@ typedef struct ns_stats {
     double  t_helm_kernel_ms;        /* single rank: sum of the two-sweep Helmholtz pass durations (one velocity
                                         component each, K2; timing == 1) */
     int32_t n_helm_kernels;          /* number of those passes timed */
+    int32_t n_exchanges;             /* ghost-row exchange groups of the step (multi-rank / loopback) */
+    int32_t n_allreduces;            /* all-reduces of the step (multi-rank / loopback) */
 } ns_stats;
 
 /* device arrays addressable by ns_get_array / ns_set_array */

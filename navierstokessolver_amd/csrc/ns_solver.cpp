@@ -190,6 +190,17 @@ struct ns_solver {
     std::vector<int32_t> cid;
     int64_t cid0 = 0, ncid = 0;  // first compact id of the slab and its in-domain cell count
     std::vector<double> hbuf;    // host bounding-box staging for that gather / scatter
+    // NSGPU_RCCL_LOOPBACK=1 (test / measurement hook): a 1-rank RCCL communicator whose every
+    // peer is this process.  One rank: every exchange point of the step runs its RCCL group with
+    // peer == self (both ghost sides from this slab's own edge rows) and every reduction an
+    // ncclAllReduce -- the multi-rank call sites on one GPU; ghost rows beyond the walls carry
+    // zero weight, so the step is the plain single-rank step.  nranks > 1 with neither an
+    // ncclUniqueId nor a host transport: a VIRTUAL slab -- rank `rank`'s slab, hierarchy,
+    // launches and RCCL groups (exchanges, the agglomeration gather) with self as every peer,
+    // reductions over this slab only: the per-rank time of a multi-GPU step without the other
+    // GPUs (tools/slab_projection.py).
+    int loopback = 0;
+    int n_xchg = 0, n_allred = 0;   // exchange groups / all-reduces issued in the current step
 };
 
 namespace {
@@ -210,12 +221,18 @@ struct HaloReq {
     int w;
 };
 
+// the RCCL / host-transport call sites are live: several ranks, or the one-rank loopback
+inline bool comm_on(const ns_solver* s) { return s->nranks > 1 || s->loopback; }
+
 // ghost rows to / from the x-neighbours; every request of the list goes in ONE RCCL group
 // (one latency for all of them)
 int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs = nullptr) {
     if (!xs) xs = s->st;
-    if (s->nranks == 1) return 0;
-    const bool lo = s->rank > 0, hi = s->rank < s->nranks - 1;
+    if (!comm_on(s)) return 0;
+    s->n_xchg++;
+    const bool lo = s->rank > 0 || s->nranks == 1, hi = s->rank < s->nranks - 1 || s->nranks == 1;
+    // (loopback: the 1-rank communicator's only rank, 0, is every peer)
+    const int p_lo = s->loopback ? 0 : s->rank - 1, p_hi = s->loopback ? 0 : s->rank + 1;
     if (s->ht.exchange) {
         for (int k = 0; k < nreq; k++) {
             const HaloReq& q = reqs[k];
@@ -245,12 +262,12 @@ int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs = null
         const int ld = q.g->ld, nxl = q.g->nxl;
         double* f = q.f;
         if (lo) {
-            NCCLCHK(ncclSend(f, cnt, ncclDouble, s->rank - 1, s->comm, xs));
-            NCCLCHK(ncclRecv(f - (ptrdiff_t)q.w * ld, cnt, ncclDouble, s->rank - 1, s->comm, xs));
+            NCCLCHK(ncclSend(f, cnt, ncclDouble, p_lo, s->comm, xs));
+            NCCLCHK(ncclRecv(f - (ptrdiff_t)q.w * ld, cnt, ncclDouble, p_lo, s->comm, xs));
         }
         if (hi) {
-            NCCLCHK(ncclSend(f + (ptrdiff_t)(nxl - q.w) * ld, cnt, ncclDouble, s->rank + 1, s->comm, xs));
-            NCCLCHK(ncclRecv(f + (ptrdiff_t)nxl * ld, cnt, ncclDouble, s->rank + 1, s->comm, xs));
+            NCCLCHK(ncclSend(f + (ptrdiff_t)(nxl - q.w) * ld, cnt, ncclDouble, p_hi, s->comm, xs));
+            NCCLCHK(ncclRecv(f + (ptrdiff_t)nxl * ld, cnt, ncclDouble, p_hi, s->comm, xs));
         }
     }
     NCCLCHK(ncclGroupEnd());
@@ -266,7 +283,7 @@ int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs = null
 int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs);
 template <class F>
 int overlapped(ns_solver* s, const HaloReq* reqs, int nreq, F&& launch) {
-    if (s->nranks == 1 || !s->overlap || !s->cst) {
+    if (!comm_on(s) || !s->overlap || !s->cst) {
         CHK(halo_reqs(s, reqs, nreq, s->st));
         return launch();
     }
@@ -290,7 +307,7 @@ int halo_reqs(ns_solver* s, std::initializer_list<HaloReq> reqs) {
 }
 
 int halo_g(ns_solver* s, const nsg::Geo& g, std::initializer_list<double*> fields, int w) {
-    if (s->nranks == 1) return 0;
+    if (!comm_on(s)) return 0;
     HaloReq r[4];
     int n = 0;
     for (double* f : fields)
@@ -301,7 +318,8 @@ int halo_g(ns_solver* s, const nsg::Geo& g, std::initializer_list<double*> field
 int halo(ns_solver* s, std::initializer_list<double*> fields, int w) { return halo_g(s, s->g, fields, w); }
 
 int allreduce(ns_solver* s, double* d, int n, ncclRedOp_t op) {
-    if (s->nranks == 1) return 0;
+    if (!comm_on(s)) return 0;
+    s->n_allred++;
     if (s->ht.allreduce) {
         CHK(ensure_stage(s, 64));
         HIPCHK(hipMemcpyAsync(s->stage, d, n * 8, hipMemcpyDeviceToHost, s->st));
@@ -831,6 +849,12 @@ int gather_level(ns_solver* s, MgLevel& C) {
     NCCLCHK(ncclGroupStart());
     for (int q = 0; q < s->nranks; q++) {
         if (q == s->rank) continue;
+        if (s->loopback) {   // virtual slab: the same messages, every peer this process
+            const size_t cnt = (size_t)std::min(C.sn[q], C.gs.nxl) * ld;
+            NCCLCHK(ncclSend(C.b + (ptrdiff_t)C.gs.i0 * ld, cnt, ncclDouble, 0, s->comm, s->st));
+            NCCLCHK(ncclRecv(C.b + (ptrdiff_t)C.si0[q] * ld, cnt, ncclDouble, 0, s->comm, s->st));
+            continue;
+        }
         NCCLCHK(ncclSend(C.b + (ptrdiff_t)C.gs.i0 * ld, (size_t)C.gs.nxl * ld, ncclDouble, q, s->comm, s->st));
         NCCLCHK(ncclRecv(C.b + (ptrdiff_t)C.si0[q] * ld, (size_t)C.sn[q] * ld, ncclDouble, q, s->comm, s->st));
     }
@@ -1500,14 +1524,13 @@ int ns_abi_version(void) { return NSGPU_ABI_VERSION; }
 
 int ns_slab_range(int32_t nx, int32_t nranks, int32_t rank, int32_t* i0, int32_t* i1) {
     if (nx <= 0 || nranks <= 0 || rank < 0 || rank >= nranks) { set_err("bad slab arguments"); return NS_EINVAL; }
-    // balanced in units of U = 2^k rows (k <= 4, U | nx, at least one unit per rank): a slab edge
-    // then never splits a coarse cell of the first k multigrid coarsenings (16384^2 -> 1024^2,
-    // where the hierarchy is replicated), whatever the rank count (4096^2 on 3 ranks: 1376 /
-    // 1360 / 1360 rows instead of 1366 / 1365 / 1365, whose odd edges stopped the hierarchy at
-    // one level)
+    // balanced in units of U = 2^k rows (k <= 4, U | nx, at least 8 units per rank so the
+    // imbalance stays <= 1/8): a slab edge then never splits a coarse cell of the first k
+    // multigrid coarsenings (16384^2 -> 1024^2, where the hierarchy is replicated), whatever
+    // the rank count (4096^2 on 3 ranks: 1376 / 1360 / 1360 rows instead of 1366 / 1365 /
+    // 1365, whose odd edges stopped the hierarchy at one level)
     int k = 0;
-    while (k < 4 && nx % (2 << k) == 0) k++;
-    while (k > 0 && (nx >> k) < nranks) k--;
+    while (k < 4 && nx % (2 << k) == 0 && (nx >> (k + 1)) >= 8 * nranks) k++;
     const int units = nx >> k;
     if (units < nranks) { set_err("%d rows cannot be split over %d ranks", nx, nranks); return NS_EINVAL; }
     const int base = units / nranks, rem = units % nranks;
@@ -1541,7 +1564,10 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (!(p->dt > 0)) { set_err("Time step should be positive"); return NS_EINVAL; }
     if (!(p->re > 0)) { set_err("Reynolds number should be positive"); return NS_EINVAL; }
     if (p->nranks < 1 || p->rank < 0 || p->rank >= p->nranks) { set_err("bad rank/nranks"); return NS_EINVAL; }
-    if (p->nranks > 1 && !p->nccl_id && !(p->host_transport && p->host_transport->exchange && p->host_transport->allreduce)) {
+    const char* lbe = getenv("NSGPU_RCCL_LOOPBACK");
+    const bool has_ht = p->host_transport && p->host_transport->exchange && p->host_transport->allreduce;
+    const bool loopback = lbe && std::atoi(lbe) != 0 && (p->nranks == 1 || (!p->nccl_id && !has_ht));
+    if (p->nranks > 1 && !p->nccl_id && !has_ht && !loopback) {
         set_err("nranks > 1 needs an ncclUniqueId or a host transport");
         return NS_EINVAL;
     }
@@ -1759,7 +1785,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (hipSetDevice(dev) != hipSuccess) { set_err("hipSetDevice(%d) failed", dev); return fail(NS_EHIP); }
     if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); return fail(NS_EHIP); }
     if (hipEventCreateWithFlags(&s->fev, hipEventDisableTiming) != hipSuccess) { set_err("event create failed"); return fail(NS_EHIP); }
-    if (p->nranks > 1) {
+    s->loopback = loopback;
+    if (p->nranks > 1 || s->loopback) {
         const char* ov = getenv("NSGPU_OVERLAP");
         s->overlap = ov ? std::atoi(ov) != 0 : 1;
         if (hipStreamCreateWithFlags(&s->cst, hipStreamNonBlocking) != hipSuccess ||
@@ -1852,7 +1879,12 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (hipMemsetAsync(s->scal, 0, S_NUM * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     if (hipHostMalloc(&s->hs, S_NUM * sizeof(double), hipHostMallocDefault) != hipSuccess) { set_err("hipHostMalloc failed"); return fail(NS_ENOMEM); }
 
-    if (s->nranks > 1 && p->host_transport && p->host_transport->exchange) {
+    if (s->loopback) {
+        ncclUniqueId id;
+        ncclResult_t r = ncclGetUniqueId(&id);
+        if (r == ncclSuccess) r = ncclCommInitRank(&s->comm, 1, id, 0);
+        if (r != ncclSuccess) { set_err("loopback ncclCommInitRank: %s", ncclGetErrorString(r)); return fail(NS_ERCCL); }
+    } else if (s->nranks > 1 && p->host_transport && p->host_transport->exchange) {
         s->ht = *p->host_transport;
     } else if (s->nranks > 1) {
         ncclUniqueId id;
@@ -1905,7 +1937,16 @@ void ns_destroy(ns_solver* s) {
 }
 
 // the step up to CorrectVelocities (its min/max reduced into scal[S_MM], not yet fetched)
+static int step_body_(ns_solver* s, ns_stats& st);
 static int step_body(ns_solver* s, ns_stats& st) {
+    s->n_xchg = s->n_allred = 0;
+    const int rc = step_body_(s, st);
+    st.n_exchanges = s->n_xchg;
+    st.n_allreduces = s->n_allred;
+    return rc;
+}
+
+static int step_body_(ns_solver* s, ns_stats& st) {
     // single rank: the Poisson initial guess (phi extrapolation: reads PHI and the history
     // planes, writes TMP, which nothing reads before the Poisson solve) runs on st2 next to
     // K1, which only reads PHI; the compute stream joins it after the Helmholtz solve

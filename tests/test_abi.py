@@ -57,7 +57,7 @@ def test_ctypes_struct_layout_matches_c():
 @pytest.mark.parametrize("nx,p", [(4096, 1), (4096, 2), (4096, 3), (4096, 6), (4096, 8), (8192, 8), (1000, 7),
                                   (130, 3), (16384, 7), (8192, 5), (35, 3)])
 def test_slab_ranges_partition_the_grid(nx, p):
-    """Balanced in units of 2^k rows (k <= 4, 2^k | nx): every slab edge is a multiple of 2^k,
+    """Balanced in units of 2^k rows (k <= 4, 2^k | nx, >= 8 units per rank): every slab edge is a multiple of 2^k,
     so the multigrid can coarsen the slabs k times (a 3-rank 4096^2 split used to stop the
     hierarchy at one level: ADVICE r1)."""
     ranges = [nsa.slab_range(nx, p, r) for r in range(p)]
@@ -65,11 +65,13 @@ def test_slab_ranges_partition_the_grid(nx, p):
     for (a0, a1), (b0, b1) in zip(ranges, ranges[1:]):
         assert a1 == b0
     k = 0
-    while k < 4 and nx % (2 << k) == 0 and (nx >> (k + 1)) >= p:
+    while k < 4 and nx % (2 << k) == 0 and (nx >> (k + 1)) >= 8 * p:
         k += 1
     sizes = [b - a for a, b in ranges]
     assert all(a % (1 << k) == 0 for a, _ in ranges)
     assert max(sizes) - min(sizes) <= (1 << k)
+    if nx >= 16 * p:
+        assert max(sizes) <= 1.125 * nx / p + 1
 
 
 def test_bad_slab_arguments_rejected():

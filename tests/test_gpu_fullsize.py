@@ -1,5 +1,5 @@
-"""GPU parity at BASELINE.json's own sizes (configs[1] 2048^2, configs[2] 4096^2, configs[4]
-16384^2), where the small-grid tests of test_gpu_parity.py do not reach:
+"""GPU parity at BASELINE.json's own sizes (configs[1] 2048^2, configs[2] 4096^2, configs[3]
+8192^2, configs[4] 16384^2), where the small-grid tests of test_gpu_parity.py do not reach:
 
   * full time steps vs the oracle (oracle/ns_oracle.c running the same multigrid + RB-SOR
     algorithm, oracle/oracle.py OSolver.use_gpu_algorithm), both solves to rtol 1e-12 so the
@@ -9,7 +9,10 @@
     input: every value is a float32, and the difference is fp32 rounding only (<= 1e-5
     relative after 5 sweeps);
   * the x-slab path at 4096^2 (2 ranks, host transport, production hierarchy: levels 0-1
-    distributed, 2-6 replicated): the per-step monitor equals the single-rank run to 1e-12.
+    distributed, 2-6 replicated): the per-step monitor equals the single-rank run to 1e-12;
+  * configs[3]'s decomposition: 8192^2 on 8 slabs of 1024 rows (8 processes on the one GPU,
+    host transport; levels 0-2 distributed, 3-7 replicated): monitor to 1e-12 and the same
+    sweep / V-cycle counts as one rank.
 """
 import os
 import subprocess
@@ -24,8 +27,24 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.mark.parametrize("n,steps", [(2048, 3), (4096, 1)])
-def test_cavity_steps_vs_oracle_at_config_size(gpu, n, steps):
+def host_threads():
+    """The box's CPU share (OMP_NUM_THREADS on the GPU pool), else this host's cores."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    return int(env) if env.isdigit() and int(env) > 0 else len(os.sched_getaffinity(0))
+
+
+@pytest.fixture
+def oracle_threads():
+    """The oracle's OpenMP loops on the host's cores for the config-size checks (8192^2 from rest
+    at rtol 1e-12: ~20 s on 8 threads), serial again afterwards."""
+    import oracle as O
+    O.set_threads(min(16, host_threads()))
+    yield
+    O.set_threads(1)
+
+
+@pytest.mark.parametrize("n,steps", [(2048, 3), (4096, 1), (8192, 1)])
+def test_cavity_steps_vs_oracle_at_config_size(gpu, oracle_threads, n, steps):
     dt, re, rtol = 1.0 / (8 * n), 1000.0, 1e-12
     gs = gpu.GpuSolver(gpu.cavity(n), dt, re, rtol=rtol)
     og = OGrid.rectangle(n, n)
@@ -59,18 +78,20 @@ def test_fp32_sweeps_at_config_size(gpu, n):
     assert abs(r32 - r64) <= 1e-5 * r64
 
 
-def test_slabs_at_config_size(tmp_path, gpu):
-    n, steps = 4096, 2
+@pytest.mark.parametrize("n,nproc,steps", [(4096, 2, 2), (8192, 8, 2)])
+def test_slabs_at_config_size(tmp_path, gpu, n, nproc, steps):
     out = tmp_path / "r.npz"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", "--master-port=29671", os.path.join(HERE, "mr_worker.py"),
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={29671 + nproc}", os.path.join(HERE, "mr_worker.py"),
            "--output", str(out), "--xport", "host", "--size", str(n), "--nsteps", str(steps),
            "--solver", str(gpu.NS_POISSON_MG), "--tol", "1e-8", "--stats-only"]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ))
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     r = dict(np.load(out, allow_pickle=False))
     assert str(r["status"]) == "ok", r["status"]
     gs = gpu.GpuSolver(gpu.rectangle(n, n), 1.0 / (8 * n), 100.0, rtol=1e-8)
     mm = np.array([list(gs.step().values())[:7] for _ in range(steps)])
+    gs.close()
     assert np.max(np.abs(r["mm"][:, :4] - mm[:, :4])) <= 1e-12
     assert np.array_equal(r["mm"][:, 4:], mm[:, 4:])       # same sweep / V-cycle counts

@@ -22,7 +22,7 @@ def launch(tmp_path, *args, port=29561, nproc=2):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(HERE, "mr_worker.py"),
            "--output", str(out), *args]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ))
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=150, env=dict(os.environ))
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     return dict(np.load(out, allow_pickle=False))
 

@@ -7,8 +7,8 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 fault() { case $1 in 0|1) return 1;; *) return 0;; esac; }
-PYTEST_ARGS=${PYTEST_ARGS:-"tests -m gpu -q"}
-timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest $PYTEST_ARGS -p no:cacheprovider --timeout=400 > gpurun_out/pytest_gpu.log 2>&1
+PYTEST_ARGS=${PYTEST_ARGS:-"tests -m gpu -v"}
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest $PYTEST_ARGS -p no:cacheprovider --timeout=${TEST_TIMEOUT:-300} --timeout-method=thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -40 gpurun_out/pytest_gpu.log
 if fault $rc; then exit $rc; fi
 [ -n "$SKIP_BENCH" ] && exit 0
