@@ -91,8 +91,7 @@ int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, 
 // ns (3 or 4) Helmholtz sweeps of ONE component in one pass (q -> qo), a single slab only
 // (-1 otherwise); residual partials of the output if part (part_second: written after as many
 // slots, v's layout after u's); returns the partial count
-int launch_helm_sweepN(int ns, const Geo& g, const Coef& c, double alpha, double omega, const double* u, double* uo,
-                       const double* ru, double* part, hipStream_t st, bool part_second);
+
 // A/B reference: LDS-tiled fused sweeps (first version)
 int launch_pois_rbsor_tiled(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                             const double* rp, const double* shift, double* part, hipStream_t st);

@@ -1423,7 +1423,25 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
 // the written cone of the same 116-column layout).
 constexpr int SW2 = 120;
 constexpr int SW2X = 116;
-constexpr int SD2 = 3;
+// rows in flight per wave (prefetch depth) per pass type: each row costs 8 VGPRs (phi, b);
+// the Helmholtz pass (136 VGPRs at 3 rows) and FUSE_P (154) stay at 3 waves/SIMD up to 168
+// VGPRs, FUSE_R (164) does not
+#ifndef SD2_HELM
+#define SD2_HELM 3
+#endif
+#ifndef SD2_HELMR
+#define SD2_HELMR SD2_HELM
+#endif
+#ifndef SD2_PLAIN
+#define SD2_PLAIN 3
+#endif
+#ifndef SD2_FP
+#define SD2_FP 3
+#endif
+template <int OP, bool RES, int FUSE>
+constexpr int sd2_of() {
+    return FUSE == 1 ? 3 : FUSE == 2 ? SD2_FP : OP == 1 ? (RES ? SD2_HELMR : SD2_HELM) : SD2_PLAIN;
+}
 constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2;
 #ifndef XR_BUF
 #define XR_BUF 0   // FUSE_R's coarse stores through buffers too (1: 172 VGPRs, 2 waves/SIMD, slower)
@@ -1434,6 +1452,7 @@ constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2;
 // (two instantiations: runtime window selects would cost ~50 VGPRs)
 template <int OP, bool RES, int FUSE, int DIR>
 __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double (*rc)[4], int wid, int lane) {
+    constexpr int SD2 = sd2_of<OP, RES, FUSE>();
     constexpr bool XR = FUSE == FUSE_R, XP = FUSE == FUSE_P;
     constexpr bool R5 = RES || XR;
     constexpr int EXT = (R5 || XP) ? 1 : 0;
@@ -1679,143 +1698,6 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
         if (lane == 0 && w < nstr) a.part[wid] = res;
-    }
-}
-
-// ------------------------------------------------ K2: NS sweeps per HBM pass (one slab)
-// k_sweep2's temporal blocking generalised to NS red-black sweeps: 2 NS colour stages in the
-// row pipeline (stage s updates row r - s with colour (s - 1) % 2 from stage s - 1's 3-row
-// window) and, with RES, a last stage taking the residual of the finished row r - 2 NS - 1.
-// The dependency cone is 2 NS (+1) cells: strips read rows ib - 2NS - EXT .. ie + 2NS - 1 + EXT
-// and write 128 - 4 NS - 4 EXT columns.  For NS > 2 the cone exceeds the HALO ghost rows, so
-// only a single slab runs it (its out-of-domain rows are clamped like k_sweep2's).  Same
-// arithmetic as NS single sweeps (bit-identical; tests/test_gpu_parity.py).  The Helmholtz
-// solve needs 8 sweeps at 4096^2: two 4-sweep passes per component instead of four pairs.
-template <int OP, int NS, bool RES, int DIR>
-__device__ __forceinline__ double sweepN_strip(const StreamArgs& a, const double (*rc)[4], int wid, int lane) {
-    constexpr int EXT = RES ? 1 : 0;
-    constexpr int NST = 2 * NS;                    // colour stages
-    constexpr int RCO = NST + 1;                   // rc table row of strip row ib
-    constexpr int SWc = 128 - 4 * NS - 4 * EXT;    // written columns per strip
-    double res = 0.0;
-    const int si = wid / a.nsj, sj = wid - si * a.nsj;
-    const int jb = sj * SWc, ib = si * a.L;
-    const int ie = min(ib + a.L, a.nxl);
-    const int ny = a.ny, ld = a.ld;
-    const int c0 = jb - 2 * NS - 2 * EXT + 2 * lane, c1 = c0 + 1;
-    const int lc = min(max(c0, 0), ld - 2);
-    const bool v0 = c0 >= 0 && c0 < ny, v1 = c1 >= 0 && c1 < ny;
-    const bool wr = lane >= NS + EXT && lane <= 63 - NS - EXT && c0 < ny;
-    const bool o0 = wr && v0, o1 = wr && v1;
-    const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
-    const double cs0 = a.cs[k0], cn0 = a.cn[k0], cd0 = cs0 + cn0 + (OP == 1 ? a.by[k0] : 0.0);
-    const double cs1 = a.cs[k1], cn1 = a.cn[k1], cd1 = cs1 + cn1 + (OP == 1 ? a.by[k1] : 0.0);
-    const double shift = (OP == 0 && a.shift) ? a.shift[0] : 0.0;
-    const double alpha = a.alpha, omega = a.omega;
-    const int rlo = -HALO, rhi = a.nxl + HALO - 1;
-    const int r0 = ib - NST - EXT, r1 = ie + NST - 1 + EXT;
-    const int phi_lo = DIR > 0 ? rlo : max(r0, rlo), phi_hi = DIR > 0 ? min(r1, rhi) : rhi;
-    const int b_lo = DIR > 0 ? max(ib - NST + 1 - EXT, rlo) : rlo;
-    const int b_hi = DIR > 0 ? rhi : min(ie + NST - 2 + EXT, rhi);
-    auto load = [&](int slot_r, double2& p, double2& bb) {
-        const int lp = min(max(slot_r, phi_lo), phi_hi), lb = min(max(slot_r - DIR, b_lo), b_hi);
-        p = ld_stream(a.in + (ptrdiff_t)lp * ld + lc, a.ntl);
-        bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
-    };
-    double2 W[NST + 1][3];                          // stage s's last three output rows (s = 0: loaded)
-    double2 B[NST + 2];                             // B[s] = rhs of row r - s
-#pragma unroll
-    for (int s = 0; s <= NST; s++) W[s][0] = W[s][1] = W[s][2] = make_double2(0.0, 0.0);
-#pragma unroll
-    for (int s = 0; s < NST + 2; s++) B[s] = make_double2(0.0, 0.0);
-
-    auto half = [&](const double2& W0, const double2& W1, const double2& W2, const double2& Bv, int row,
-                    int par) -> double2 {
-        double2 o = W1;
-        const int gi = a.i0 + row;
-        if (gi < 0 || gi >= a.nx) return o;
-        const double* rw = rc[row - ib + RCO];
-        const double cw = rw[0], ce = rw[1];
-        double rr;
-        if ((gi & 1) == par) {
-            const double lf = __shfl_up(W1.y, 1, 64);
-            const double d = diag<OP>(rw[2], cd0, alpha), w = omega * rcp_nr(d);
-            if (v0) o.x = relax<OP>(W1.x, W0.x, W2.x, lf, W1.y, Bv.x, cw, ce, cs0, cn0, d, w, alpha, rr);
-        } else {
-            const double rt = __shfl_down(W1.x, 1, 64);
-            const double d = diag<OP>(rw[2], cd1, alpha), w = omega * rcp_nr(d);
-            if (v1) o.y = relax<OP>(W1.y, W0.y, W2.y, W1.x, rt, Bv.y, cw, ce, cs1, cn1, d, w, alpha, rr);
-        }
-        return o;
-    };
-
-    auto step = [&](double2 p, const double2 bb, int r) {
-        W[0][0] = W[0][1]; W[0][1] = W[0][2]; W[0][2] = p;
-#pragma unroll
-        for (int s = NST + 1; s > 1; s--) B[s] = B[s - 1];
-        B[1] = make_double2(bb.x - shift, bb.y - shift);
-#pragma unroll
-        for (int s = 1; s <= NST; s++) {
-            const int m = r - s * DIR;
-            double2 n = W[s - 1][1];
-            if (m >= ib - (NST - s) - EXT && m <= ie - 1 + (NST - s) + EXT)
-                n = DIR > 0 ? half(W[s - 1][0], W[s - 1][1], W[s - 1][2], B[s], m, (s - 1) & 1)
-                            : half(W[s - 1][2], W[s - 1][1], W[s - 1][0], B[s], m, (s - 1) & 1);
-            if (s == NST && m >= ib && m < ie && wr) st_stream(a.out + (ptrdiff_t)m * ld + c0, n, a.nt);
-            W[s][0] = W[s][1]; W[s][1] = W[s][2]; W[s][2] = n;
-        }
-        if (RES) {
-            // the residual of the finished row r - 2 NS - 1 (window W[NST]: rows m -+ 1 around it)
-            const int m = r - (NST + 1) * DIR;
-            if (m >= ib && m < ie) {
-                const double2 F1 = W[NST][1];
-                const double2 Fm = DIR > 0 ? W[NST][0] : W[NST][2], Fp = DIR > 0 ? W[NST][2] : W[NST][0];
-                const double lf = __shfl_up(F1.y, 1, 64), rt = __shfl_down(F1.x, 1, 64);
-                const double* rw = rc[m - ib + RCO];
-                const double cw = rw[0], ce = rw[1];
-                const double d0 = diag<OP>(rw[2], cd0, alpha), d1 = diag<OP>(rw[2], cd1, alpha);
-                double q0, q1;
-                relax<OP>(F1.x, Fm.x, Fp.x, lf, F1.y, B[NST + 1].x, cw, ce, cs0, cn0, d0, 0.0, alpha, q0);
-                relax<OP>(F1.y, Fm.y, Fp.y, F1.x, rt, B[NST + 1].y, cw, ce, cs1, cn1, d1, 0.0, alpha, q1);
-                res += (o0 ? q0 * q0 : 0.0) + (o1 ? q1 * q1 : 0.0);
-            }
-        }
-    };
-
-    double2 Q[SD2], QB[SD2];
-    const int rs = DIR > 0 ? r0 : r1, nr = r1 - r0 + 1;
-#pragma unroll
-    for (int q = 0; q < SD2; q++) load(rs + DIR * q, Q[q], QB[q]);
-    for (int t = 0; t < nr; t += SD2) {
-#pragma unroll
-        for (int q = 0; q < SD2; q++) {
-            if (t + q < nr) step(Q[q], QB[q], rs + DIR * (t + q));
-            load(rs + DIR * (t + q + SD2), Q[q], QB[q]);
-        }
-    }
-    return res;
-}
-
-template <int OP, int NS, bool RES>
-__global__ __launch_bounds__(256) void k_sweepN(StreamArgs a) {
-    constexpr int RCO = 2 * NS + 1;
-    __shared__ double rcs[4][64 + 2 * RCO][4];
-    const int lane = threadIdx.x & 63;
-    const int nstr = a.nsj * a.nsi;
-    const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-    double (*rc)[4] = rcs[threadIdx.x >> 6];
-    if (wid < nstr) stage_rows<OP, RCO>(a, rc, (wid / a.nsj) * a.L, lane);
-    __syncthreads();
-    double res = 0.0;
-    if (wid < nstr) {
-        const int si = wid / a.nsj;
-        if (a.alt && (si & 1)) res = sweepN_strip<OP, NS, RES, -1>(a, rc, wid, lane);
-        else res = sweepN_strip<OP, NS, RES, 1>(a, rc, wid, lane);
-    }
-    if (RES) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
-        if (lane == 0 && wid < nstr) a.part[wid] = res;
     }
 }
 
@@ -2776,8 +2658,7 @@ static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, dou
     a.part = part;
     const char* e = getenv("NSGPU_NT_STORES");
     a.nt = e ? std::atoi(e) != 0 : 1;
-    const char* e2 = getenv("NSGPU_ALT_DIR");   // NSGPU_ALT_DIR=0: every strip walks downwards (A/B)
-    a.alt = e2 ? std::atoi(e2) != 0 : 1;
+    a.alt = 1;
     const char* e3 = getenv("NSGPU_NT_LOADS");
     a.ntl = e3 ? std::atoi(e3) : -1;   // -1: per kernel (the prolongation pass only)
     return a;
@@ -2900,35 +2781,6 @@ int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, 
     return n;
 }
 
-// NS sweeps of one pass (k_sweepN; NS = 3, 4; a single slab only): residual partials of the
-// output if part, 1 per strip; returns the strip count
-template <int OP, int NS>
-static int launch_streamN(StreamArgs a, const Geo& g, hipStream_t st, bool count_only = false) {
-    if (count_only) a.part = reinterpret_cast<double*>(1);
-    const int swc = 128 - 4 * NS - (a.part ? 4 : 0);
-    a.nsj = (g.ny + swc - 1) / swc;
-    const long cap = resident_waves(a.part ? (const void*)k_sweepN<OP, NS, true> : (const void*)k_sweepN<OP, NS, false>);
-    a.L = std::min(64, strip_rows(a.nxl, a.nsj, cap, 16));
-    a.nsi = (g.nxl + a.L - 1) / a.L;
-    const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
-    if (count_only) return nstr;
-    if (a.part) NS_LAUNCH((k_sweepN<OP, NS, true>), dim3(nblk), dim3(256), 0, st, a);
-    else NS_LAUNCH((k_sweepN<OP, NS, false>), dim3(nblk), dim3(256), 0, st, a);
-    return nstr;
-}
-
-int launch_helm_sweepN(int ns, const Geo& g, const Coef& c, double alpha, double omega, const double* u, double* uo,
-                       const double* ru, double* part, hipStream_t st, bool part_second) {
-    if (g.i0 != 0 || g.nxl != g.nx) return -1;   // the cone exceeds the ghost rows: one slab only
-    StreamArgs a = stream_args(g, c, u, uo, ru, nullptr, alpha, omega, part, true);
-    auto go = [&](auto launch) {
-        if (part && part_second) a.part = part + launch(a, true);   // after the first component's partials
-        return launch(a, false);
-    };
-    if (ns == 3) return go([&](StreamArgs x, bool cnt) { return launch_streamN<1, 3>(x, g, st, cnt); });
-    if (ns == 4) return go([&](StreamArgs x, bool cnt) { return launch_streamN<1, 4>(x, g, st, cnt); });
-    return -1;
-}
 
 // -1 if the plane does not fit the kernel's 32-bit buffer offsets
 template <class T>

@@ -125,18 +125,7 @@ struct ns_solver {
     int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
     int tile_small = 1;          // NSGPU_TILE_SMALL=0: no LDS-tiled fused passes on small levels (A/B)
     int helm_split = 1;          // NSGPU_HELM_SPLIT=0: u and v pass by pass (A/B)
-    // NSGPU_HELM_CONC=1 (single rank, split): v's passes on a second stream, concurrent with
-    // u's, so each chain's dependent-kernel boundaries (launch + drain) overlap the other's work
     int ext_timing = 1;          // NSGPU_EXT_TIMING=0: marker events around timed launches (t_begin)
-    int helm_conc = 0;
-    hipStream_t st2 = nullptr;
-    hipEvent_t cev[2] = {nullptr, nullptr};
-    // NSGPU_EXTRAP_CONC (single rank): the phi extrapolation (HBM-bound) on st2 alongside K1
-    // (fp64-issue-bound) instead of under the Helmholtz check's host wait: K1 258 -> 317 us,
-    // the extrapolation 83 -> 247 us, +0.2 % on the step; off, so the kernel profile stays readable
-    int extrap_conc = 0;
-    hipEvent_t xev2[2] = {nullptr, nullptr};
-    int helm_ns = 2;             // Helmholtz sweeps per pass on one slab (NSGPU_HELM_NS: 2, 3, 4)
     int phi_extrap = 2;          // Poisson initial guess: NSGPU_PHI_EXTRAP=0 phi^{n-1}, 1 linear, 2 quadratic (default)
     int mg_predict = 1;          // NSGPU_MG_PREDICT=0: a residual check (host sync) after every V-cycle
     double mg_rate2 = 0.0;       // last measured per-cycle contraction of ||r||^2
@@ -200,6 +189,12 @@ struct ns_solver {
     // reductions over this slab only: the per-rank time of a multi-GPU step without the other
     // GPUs (tools/slab_projection.py).
     int loopback = 0;
+    // virtual slab only (NSGPU_VIRTUAL_ITERS="h:c,h:c,..."): the slab's own residuals are not the
+    // global solve's, so each step replays the global run's Helmholtz sweeps h and V-cycles c
+    // (cycled over the list), with one residual check (host sync) per solve like a predicted one
+    std::vector<std::pair<int, int>> replay;
+    size_t replay_k = 0;
+    int rp_h = 0, rp_c = -1;        // this step's replayed counts (0 / -1: converge normally)
     int n_xchg = 0, n_allred = 0;   // exchange groups / all-reduces issued in the current step
 };
 
@@ -378,15 +373,6 @@ int t_end(ns_solver* s, hipEvent_t a, hipEvent_t b) {
     HIPCHK(hipEventRecord(b, s->st));
     return 0;
 }
-// the second stream (NSGPU_HELM_CONC, NSGPU_EXTRAP_CONC) and its fork / join events
-int ensure_st2(ns_solver* s) {
-    if (s->st2) return 0;
-    HIPCHK(hipStreamCreateWithFlags(&s->st2, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&s->cev[0], &s->cev[1], &s->xev2[0], &s->xev2[1]})
-        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    return 0;
-}
-
 int ensure_events(ns_solver* s, size_t n) {
     while (s->ev.size() < n) {
         hipEvent_t e;
@@ -409,7 +395,7 @@ int helm_sweep(ns_solver* s, double alpha, double* part, int which = 3) {
 }
 
 // two Helmholtz sweeps in one pass (temporal blocking), then swap
-int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3, int ns = 2) {
+int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3) {
     // timing: one-component passes only (the bench's 24 B/cell roofline figure)
     const bool t = s->timing && which != 3;
     if (t) {
@@ -421,18 +407,9 @@ int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3, int ns 
         }
         if (t_begin(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]) != 0) return -1;
     }
-    int nb;
-    if (ns > 2) {   // ns sweeps of one component in one pass (single slab)
-        const bool u = which == 1;
-        nb = nsg::launch_helm_sweepN(ns, s->g, s->c, alpha, s->omega_v, s->arr[u ? NS_ARR_U : NS_ARR_V],
-                                     s->arr[u ? NS_ARR_TMPU : NS_ARR_TMPV], s->arr[u ? NS_ARR_RU : NS_ARR_RV], part,
-                                     s->st, !u);
-        if (nb < 0) { set_err("k_sweepN: %d sweeps per pass need a single slab", ns); return -1; }
-    } else {
-        nb = nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
-                                     s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
-                                     s->arr[NS_ARR_RV], part, s->st, which);
-    }
+    const int nb = nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
+                                           s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
+                                           s->arr[NS_ARR_RV], part, s->st, which);
     if (t) {
         if (t_end(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]) != 0) return -1;
         s->hn++;
@@ -454,26 +431,12 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                 int* first_at, int* last_at) {
     int nb = 0;
     const bool split = s->helm_split && s->nranks == 1;
-    const bool conc = split && s->helm_conc && !s->tiled;
-    hipStream_t main_st = s->st;
-    struct Restore {   // an error return inside v's chain leaves the main stream current
-        ns_solver* s; hipStream_t st;
-        ~Restore() { s->st = st; }
-    } restore{s, main_st};
-    if (conc) {
-        CHK(ensure_st2(s));
-        // fork: v's chain starts from the same point as u's
-        HIPCHK(hipEventRecord(s->cev[0], s->st));
-        HIPCHK(hipStreamWaitEvent(s->st2, s->cev[0], 0));
-    }
     for (int which : {split ? 1 : 3, split ? 2 : 0}) {
         if (!which) break;
-        if (conc && which == 2) s->st = s->st2;   // v's launches (and their timing events) on st2
         int k = 0, launch = 0;
         while (k < n) {
-            // sweeps per pass: up to helm_ns (NSGPU_HELM_NS) on one slab, pairs otherwise
-            const int wmax = s->tiled ? 1 : (split ? s->helm_ns : 2);
-            const int w = std::min(wmax, n - k);
+            // sweeps per pass: pairs (one sweep for an odd remainder, or with NSGPU_SWEEP=tiled)
+            const int w = std::min(s->tiled ? 1 : 2, n - k);
             const bool last = k + w >= n;
             double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
             const int hw = w == 2 ? (part ? 5 : 4) : 2;
@@ -499,7 +462,7 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                 }
                 if (which == 3) CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, hw));
                 else if (w <= 2) CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
-                nb = w >= 2 ? helm_sweep2(s, alpha, part, which, w) : helm_sweep(s, alpha, part, which);
+                nb = w >= 2 ? helm_sweep2(s, alpha, part, which) : helm_sweep(s, alpha, part, which);
                 if (nb < 0) return NS_EHIP;
             }
             const int at = w >= 2 ? k + w : k;   // a multi-sweep pass reports its output's residual
@@ -511,12 +474,6 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
             k += w;
             launch++;
         }
-    }
-    if (conc) {
-        // join: everything after the solve (the residual reductions) waits for v's chain
-        s->st = main_st;
-        HIPCHK(hipEventRecord(s->cev[1], s->st2));
-        HIPCHK(hipStreamWaitEvent(s->st, s->cev[1], 0));
     }
     return nb;
 }
@@ -624,7 +581,7 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
     const double tol2 = s->rtol * s->rtol;
     // first batch: what the previous step needed (consecutive steps converge alike), so a
     // step normally costs one residual check
-    int sweeps = 0, batch = s->helm_next, prev_at = -1;
+    int sweeps = 0, batch = s->rp_h > 0 ? s->rp_h : s->helm_next, prev_at = -1;
     const int n0 = batch;
     double prev_r2 = -1;
     double first_r2 = -1, last_r2 = -1;   // max over u, v of r^2 / ||b||^2
@@ -654,7 +611,7 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         CHK(fetch_end(s));
         const double r2u = s->hs[S_RES], r2v = s->hs[S_RES + 1];
         const double bu = s->hs[S_HBN], bv = s->hs[S_HBN + 1];
-        const bool ok = (r2u <= tol2 * bu || r2u == 0.0) && (r2v <= tol2 * bv || r2v == 0.0);
+        const bool ok = s->rp_h > 0 || ((r2u <= tol2 * bu || r2u == 0.0) && (r2v <= tol2 * bv || r2v == 0.0));
         *resu = bu > 0 ? std::sqrt(r2u / bu) : std::sqrt(r2u);
         *resv = bv > 0 ? std::sqrt(r2v / bv) : std::sqrt(r2v);
         if (!std::isfinite(r2u) || !std::isfinite(r2v)) { set_err("Helmholtz residual is not finite"); *its = sweeps; return NS_EDIVERGE; }
@@ -1017,6 +974,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
         if (m > 0) next_chk = m;
     }
     double prev_rr = -1.0;
+    if (s->rp_c >= 0) next_chk = s->rp_c;   // virtual slab: the replayed cycle count, one check
     auto check = [&](int nb) -> int {
         if (!(cycles >= next_chk || cycles >= maxc)) return 0;
         // fine residual after pre-smoothing: the convergence test (a host sync)
@@ -1041,7 +999,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
         *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
         if (s->verbose) fprintf(stderr, "nsgpu poisson: cycle %d rel. residual after pre-smoothing %.3e\n", cycles, *res);
         if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = cycles; return NS_EDIVERGE; }
-        if (r2 <= tol2 * b2 || r2 == 0.0 || cycles >= maxc) return 1;
+        if (r2 <= tol2 * b2 || r2 == 0.0 || cycles >= maxc || s->rp_c >= 0) return 1;
         if (s->mg_predict) {
             const double rr = r2 / b2;
             double rate = s->mg_rate2;   // per-cycle contraction of r^2
@@ -1740,10 +1698,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_HELM_SPLIT")) s->helm_split = std::atoi(e) != 0;
-    if (const char* e = getenv("NSGPU_HELM_CONC")) s->helm_conc = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_EXT_TIMING")) s->ext_timing = std::atoi(e) != 0;
-    if (const char* e = getenv("NSGPU_EXTRAP_CONC")) s->extrap_conc = std::atoi(e) != 0;
-    if (const char* e = getenv("NSGPU_HELM_NS")) s->helm_ns = std::max(2, std::min(4, std::atoi(e)));
     if (const char* e = getenv("NSGPU_HELM_EXTRAP")) s->helm_extrap = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = getenv("NSGPU_MG_PREDICT")) s->mg_predict = std::atoi(e) != 0;
@@ -1786,6 +1741,25 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); return fail(NS_EHIP); }
     if (hipEventCreateWithFlags(&s->fev, hipEventDisableTiming) != hipSuccess) { set_err("event create failed"); return fail(NS_EHIP); }
     s->loopback = loopback;
+    if (loopback && p->nranks > 1) {
+        if (const char* e = getenv("NSGPU_VIRTUAL_ITERS")) {
+            for (const char* q = e; *q;) {
+                int h = 0, c = 0, used = 0;
+                if (std::sscanf(q, "%d:%d%n", &h, &c, &used) != 2 || h < 2 || (h & 1) || c < 0) {
+                    set_err("NSGPU_VIRTUAL_ITERS: expected even sweeps:cycles pairs, got '%s'", q);
+                    return fail(NS_EINVAL);
+                }
+                s->replay.emplace_back(h, c);
+                q += used;
+                if (*q == ',') q++;
+            }
+        }
+        // (its own residuals would not converge the global problem: never solve to tolerance)
+        if (s->replay.empty()) {
+            set_err("a virtual slab (NSGPU_RCCL_LOOPBACK with nranks > 1) needs NSGPU_VIRTUAL_ITERS");
+            return fail(NS_EINVAL);
+        }
+    }
     if (p->nranks > 1 || s->loopback) {
         const char* ov = getenv("NSGPU_OVERLAP");
         s->overlap = ov ? std::atoi(ov) != 0 : 1;
@@ -1902,12 +1876,8 @@ void ns_destroy(ns_solver* s) {
     (void)hipSetDevice(s->device);
     if (s->st) (void)hipStreamSynchronize(s->st);
     if (s->comm) (void)ncclCommDestroy(s->comm);
-    if (s->st2) (void)hipStreamSynchronize(s->st2);
     if (s->mev) (void)hipEventDestroy(s->mev);
     if (s->mm_host) (void)hipHostFree(s->mm_host);
-    for (auto e : {s->cev[0], s->cev[1], s->xev2[0], s->xev2[1]})
-        if (e) (void)hipEventDestroy(e);
-    if (s->st2) (void)hipStreamDestroy(s->st2);
     for (auto e : s->ev) (void)hipEventDestroy(e);
     for (auto e : s->hev) (void)hipEventDestroy(e);
     for (size_t l = 1; l < s->lv.size(); l++) {
@@ -1940,6 +1910,11 @@ void ns_destroy(ns_solver* s) {
 static int step_body_(ns_solver* s, ns_stats& st);
 static int step_body(ns_solver* s, ns_stats& st) {
     s->n_xchg = s->n_allred = 0;
+    if (!s->replay.empty()) {
+        const auto& r = s->replay[s->replay_k++ % s->replay.size()];
+        s->rp_h = r.first;
+        s->rp_c = r.second;
+    }
     const int rc = step_body_(s, st);
     st.n_exchanges = s->n_xchg;
     st.n_allreduces = s->n_allred;
@@ -1947,24 +1922,7 @@ static int step_body(ns_solver* s, ns_stats& st) {
 }
 
 static int step_body_(ns_solver* s, ns_stats& st) {
-    // single rank: the Poisson initial guess (phi extrapolation: reads PHI and the history
-    // planes, writes TMP, which nothing reads before the Poisson solve) runs on st2 next to
-    // K1, which only reads PHI; the compute stream joins it after the Helmholtz solve
-    const bool xconc = s->extrap_conc && s->nranks == 1 && s->phim;
-    if (xconc) {
-        CHK(ensure_st2(s));
-        HIPCHK(hipEventRecord(s->xev2[0], s->st));
-    }
     CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
-    if (xconc) {   // (after K1's launch: it took the pre-rotation PHI pointer)
-        HIPCHK(hipStreamWaitEvent(s->st2, s->xev2[0], 0));
-        hipStream_t main_st = s->st;
-        s->st = s->st2;
-        const int rc = extrapolate_phi(s);
-        s->st = main_st;
-        CHK(rc);
-        HIPCHK(hipEventRecord(s->xev2[1], s->st2));
-    }
     // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
     CHK(helm_guess(s));
@@ -1973,10 +1931,10 @@ static int step_body_(ns_solver* s, ns_stats& st) {
     if (s->nranks > 1 && s->overlap && s->cst && !s->g.fc && !s->tiled) s->helm_b_pend = 1;
     else CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
     s->hn = 0;
-    s->extrap_pending = s->phim && !xconc ? 1 : 0;
+    // the Poisson initial guess (phi extrapolation) waits to hide the Helmholtz check's host sync
+    s->extrap_pending = s->phim ? 1 : 0;
     CHK(helm_solve(s, &st.it_u, &st.res_u, &st.res_v));            // KSPSolve(uSolver) x2 (:547-548)
     if (s->extrap_pending) { s->extrap_pending = 0; CHK(extrapolate_phi(s)); }
-    if (xconc) HIPCHK(hipStreamWaitEvent(s->st, s->xev2[1], 0));
     st.it_v = st.it_u;
     for (int k = 0; k < s->hn; k++) {   // (helm_solve's last residual check synchronised the stream)
         float ms = 0.f;

@@ -434,30 +434,6 @@ def test_two_sweep_pass_equals_two_sweeps(gpu, nx, ny, op):
         assert rel(gs.get(gpu.NS_ARR_V), vv) <= 1e-12
 
 
-@pytest.mark.parametrize("ns", [3, 4])
-@pytest.mark.parametrize("nx,ny", [(300, 200), (1030, 260), (64, 700)])
-def test_multi_sweep_helmholtz_pass_equals_pairs(gpu, monkeypatch, nx, ny, ns):
-    """k_sweepN (ns red-black sweeps of one velocity component per HBM pass, one slab) gives the
-    same iterate as two-sweep passes -- bit for bit -- and the same output residual.  Fixed work:
-    8 sweeps per component (check_every 8, max_iters 8, an unreachable rtol)."""
-    rng = np.random.default_rng(31)
-    dt, re = 1.0 / 64, 10.0
-    u, v, ru, rv = (rand(rng, nx * ny) for _ in range(4))
-    out = {}
-    for k in (2, ns):
-        monkeypatch.setenv("NSGPU_HELM_NS", str(k))
-        gs = gpu.GpuSolver(gpu.rectangle(nx, ny, bc=BC_FLOW), dt, re, omega_v=1.1, check_every=8, max_iters=8,
-                           rtol=1e-30)
-        for a, x in ((gpu.NS_ARR_U, u), (gpu.NS_ARR_V, v), (gpu.NS_ARR_RU, ru), (gpu.NS_ARR_RV, rv)):
-            gs.set(a, x)
-        its, res = gs.kernel(gpu.NS_K_HELM_SOLVE)[:2]
-        assert its == 8
-        out[k] = (gs.get(gpu.NS_ARR_U), gs.get(gpu.NS_ARR_V), res)
-        gs.close()
-    assert np.array_equal(out[2][0], out[ns][0]) and np.array_equal(out[2][1], out[ns][1])
-    assert out[2][2] == out[ns][2]
-
-
 @pytest.mark.parametrize("nx,ny", [(256, 192), (96, 160)])
 def test_fused_transfer_passes_match_separate_transfers(gpu, monkeypatch, nx, ny):
     """The last pre-smoothing pass with the restriction fused in (k_sweep2 FUSE_R) and the first
@@ -597,39 +573,6 @@ def test_known_answer_trace_128_async(gpu):
         got = gs.monitor() if it == 201 else (st["umin"], st["umax"], st["vmin"], st["vmax"])
         if it - 1 in KNOWN_TRACE_128:
             assert all(printed_equal(x, y) for x, y in zip(got, KNOWN_TRACE_128[it - 1])), (it - 1, got)
-
-
-def test_concurrent_helmholtz_streams_bit_identical(gpu, monkeypatch):
-    """NSGPU_HELM_CONC=1 (v's passes on a second stream, concurrent with u's) gives the same
-    steps bit for bit."""
-    n, dt, re = 160, 1.0 / 1280, 1000.0
-    out = {}
-    for conc in ("0", "1"):
-        monkeypatch.setenv("NSGPU_HELM_CONC", conc)
-        gs = gpu.GpuSolver(gpu.cavity(n), dt, re)
-        st = [gs.step() for _ in range(4)]
-        out[conc] = (st, gs.fields())
-        gs.close()
-    assert [s["umax"] for s in out["0"][0]] == [s["umax"] for s in out["1"][0]]
-    for x, y in zip(out["0"][1], out["1"][1]):
-        assert np.array_equal(x, y)
-
-
-@pytest.mark.parametrize("bc", [BC_CAVITY, BC_CHANNEL])
-def test_side_stream_extrapolation_bit_identical(gpu, monkeypatch, bc):
-    """NSGPU_EXTRAP_CONC=1 (the Poisson initial guess extrapolated on a second
-    stream next to K1) gives the same steps bit for bit as the in-order extrapolation."""
-    nx, ny, dt, re = 128, 96, 1.0 / 1024, 400.0
-    out = {}
-    for conc in ("0", "1"):
-        monkeypatch.setenv("NSGPU_EXTRAP_CONC", conc)
-        gs = gpu.GpuSolver(gpu.rectangle(nx, ny, bc=bc), dt, re)
-        st = [gs.step_async() for _ in range(6)] + [gs.step()]
-        out[conc] = (st, gs.fields())
-        gs.close()
-    assert [(s["it_u"], s["it_phi"]) for s in out["0"][0]] == [(s["it_u"], s["it_phi"]) for s in out["1"][0]]
-    for x, y in zip(out["0"][1], out["1"][1]):
-        assert np.array_equal(x, y)
 
 
 def test_dispatch_stamped_kernel_timing(gpu, monkeypatch):

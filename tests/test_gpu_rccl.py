@@ -55,3 +55,24 @@ def test_rccl_loopback_step_equals_single_rank(gpu, monkeypatch, case):
     mm_a = [[s[k] for k in ("umin", "umax", "vmin", "vmax")] for s in a[3]]
     mm_b = [[s[k] for k in ("umin", "umax", "vmin", "vmax")] for s in b[3]]
     assert mm_a == mm_b
+
+
+def test_virtual_slab_replays_counts(gpu, monkeypatch):
+    """A virtual slab (NSGPU_RCCL_LOOPBACK with nranks > 1, no ncclUniqueId): rank 2 of 4 builds
+    its slab and hierarchy and runs every RCCL group with itself as the peer; each step replays
+    the given (Helmholtz sweeps, V-cycles) -- tools/slab_projection.py's per-rank timing.  It
+    must run those counts exactly, issue exchanges and all-reduces (and the agglomeration
+    gather: the level hierarchy has replicated levels at 4 ranks), and stay finite."""
+    n = 512
+    monkeypatch.setenv("NSGPU_RCCL_LOOPBACK", "1")
+    monkeypatch.setenv("NSGPU_VIRTUAL_ITERS", "4:2,6:3")
+    gs = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0, device=0, rank=2, nranks=4)
+    st = [gs.step() for _ in range(4)]
+    u, v, _ = gs.fields()
+    gs.close()
+    assert [(s["it_u"], s["it_phi"]) for s in st] == [(4, 2), (6, 3), (4, 2), (6, 3)]
+    assert all(s["n_exchanges"] > 0 and s["n_allreduces"] > 0 for s in st)
+    assert np.all(np.isfinite(u)) and np.all(np.isfinite(v)) and u.shape == (n // 4, n)
+    monkeypatch.delenv("NSGPU_VIRTUAL_ITERS")
+    with pytest.raises(gpu.NsError):   # a virtual slab without replayed counts would never converge
+        gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0, device=0, rank=2, nranks=4)

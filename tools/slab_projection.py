@@ -24,25 +24,33 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(n, P, warmup, steps, re):
+def run(n, P, warmup, steps, re, replay=None):
+    """One configuration; P > 1 replays the single-rank run's per-step (Helmholtz sweeps,
+    V-cycles) sequence `replay` (NSGPU_VIRTUAL_ITERS): the same work per step as the global
+    solve, which the 8-slab tests show the P-rank run reproduces exactly."""
     import navierstokessolver_amd as nsa
     dt = 1.0 / (8 * n)
     kw = {}
     if P > 1:
         os.environ["NSGPU_RCCL_LOOPBACK"] = "1"
+        os.environ["NSGPU_VIRTUAL_ITERS"] = ",".join(f"{h}:{c}" for h, c in replay)
         kw = dict(rank=P // 2, nranks=P)
     gs = nsa.GpuSolver(nsa.cavity(n), dt, re, device=0, **kw)
     os.environ.pop("NSGPU_RCCL_LOOPBACK", None)
+    os.environ.pop("NSGPU_VIRTUAL_ITERS", None)
+    seq = []
     for _ in range(warmup):
-        gs.step_async()
+        s = gs.step_async()
+        seq.append((s["it_u"], s["it_phi"]))
     gs.monitor()
     t0 = time.perf_counter()
     st = [gs.step_async() for _ in range(steps)]
     gs.monitor()
     t = (time.perf_counter() - t0) / steps
+    seq += [(s["it_u"], s["it_phi"]) for s in st]
     i0, i1 = gs.i0, gs.i1
     gs.close()
-    return {"P": P, "rank": P // 2 if P > 1 else 0, "rows": i1 - i0, "ms_per_step": t * 1e3,
+    return seq, {"P": P, "rank": P // 2 if P > 1 else 0, "rows": i1 - i0, "ms_per_step": t * 1e3,
             "vcycles_per_step": sum(s["it_phi"] for s in st) / steps,
             "helm_sweeps_per_step": sum(s["it_u"] for s in st) / steps,
             "exchanges_per_step": sum(s["n_exchanges"] for s in st) / steps,
@@ -56,6 +64,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--re", type=float, default=1000.0)
+    ap.add_argument("--replay", default="", help="h:c,... per-step counts for P > 1 instead of a P = 1 run's")
     ap.add_argument("--allreduce-us", type=float, default=25.0,
                     help="assumed latency of one small (<= 4 doubles) RCCL all-reduce over P GPUs (xGMI)")
     ap.add_argument("--exchange-us", type=float, default=5.0,
@@ -64,8 +73,13 @@ def main():
                          "interior strips)")
     a = ap.parse_args()
     rows = []
+    replay = [tuple(int(x) for x in t.split(":")) for t in a.replay.split(",")] if a.replay else None
     for P in (int(x) for x in a.ranks.split(",")):
-        r = run(a.n, P, a.warmup, a.steps, a.re)
+        if P > 1 and replay is None:
+            replay, _ = run(a.n, 1, a.warmup, a.steps, a.re)
+        seq, r = run(a.n, P, a.warmup, a.steps, a.re, replay)
+        if P == 1:
+            replay = seq
         extra = 0.0 if P == 1 else (r["allreduces_per_step"] * a.allreduce_us + r["exchanges_per_step"] * a.exchange_us) * 1e-3
         r["projected_ms_per_step"] = r["ms_per_step"] + extra
         r["projected_mlups"] = a.n * a.n / (r["projected_ms_per_step"] * 1e-3) / 1e6
