@@ -257,6 +257,7 @@ def main():
         "poisson_fine_sweeps_per_s": fine_sweeps / elapsed,
         "poisson_fine_sweeps_per_step": fine_sweeps / K,
         "helmholtz_sweeps_per_step": hsweeps / K,
+        "poisson_checks_per_step": sum(s["n_checks"] for s in stats) / K,
         "roofline": kern.get(dominant),
         "step_roofline": {"bound": "hbm", "bytes_per_cell": step_bpc, "bytes_per_step": step_bpc * cells,
                           "achieved": step_bpc * cells / (elapsed / K) / 1e9, "peak": HBM_PEAK_GBS * world,

@@ -196,6 +196,12 @@ struct ns_solver {
     size_t replay_k = 0;
     int rp_h = 0, rp_c = -1;        // this step's replayed counts (0 / -1: converge normally)
     int n_xchg = 0, n_allred = 0;   // exchange groups / all-reduces issued in the current step
+    // speculative CorrectVelocities: inside a time step, the multigrid's residual check that
+    // the cycle history predicts to pass enqueues K5 (into the ping-pong partners, with its
+    // min/max) BEFORE the host waits for the residual, so the GPU works through the host round
+    // trip; k5_spec = 1 after a passing check (the step then only swaps), 0 otherwise (K5 runs
+    // again after the last cycle: u* is untouched, K5 writes TMPU / TMPV)
+    int in_step = 0, k5_spec = 0, n_spec = 0, n_spec_hit = 0;
 };
 
 namespace {
@@ -562,6 +568,7 @@ struct KrylovSolve {
 };
 
 int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res);
+int correct_launch(ns_solver* s, double* part2);
 
 // ---------------- Helmholtz (I - a L_V) u* = RHS_u, v* likewise (KSPSolve(uSolver), FluidSolver.cpp:547-548)
 // Initial guess u^n (in place): converged solution is the same; fewer sweeps than the reference's zero guess.
@@ -975,12 +982,22 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     }
     double prev_rr = -1.0;
     if (s->rp_c >= 0) next_chk = s->rp_c;   // virtual slab: the replayed cycle count, one check
+    // speculate at the first check when the last four solves all converged by then
+    const bool spec_ok = s->in_step && s->mg_predict && s->rp_c < 0 && next_chk > 0;
     auto check = [&](int nb) -> int {
         if (!(cycles >= next_chk || cycles >= maxc)) return 0;
         // fine residual after pre-smoothing: the convergence test (a host sync)
         nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
         CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
-        CHK(fetch(s));
+        const bool spec = spec_ok && nchk == 0;
+        if (spec) {
+            CHK(fetch_begin(s));   // (the residual's copy, then K5 behind it)
+            CHK(correct_launch(s, s->part + 4 * (size_t)nsg::max_partials(s->g)));
+            s->n_spec++;
+            CHK(fetch_end(s));
+        } else {
+            CHK(fetch(s));
+        }
         nchk++;
         if (s->timing) {
             for (int k = 0; k < tn; k++) {
@@ -999,7 +1016,10 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
         *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
         if (s->verbose) fprintf(stderr, "nsgpu poisson: cycle %d rel. residual after pre-smoothing %.3e\n", cycles, *res);
         if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = cycles; return NS_EDIVERGE; }
-        if (r2 <= tol2 * b2 || r2 == 0.0 || cycles >= maxc || s->rp_c >= 0) return 1;
+        if (r2 <= tol2 * b2 || r2 == 0.0 || cycles >= maxc || s->rp_c >= 0) {
+            if (spec) { s->k5_spec = 1; s->n_spec_hit++; }
+            return 1;
+        }
         if (s->mg_predict) {
             const double rr = r2 / b2;
             double rate = s->mg_rate2;   // per-cycle contraction of r^2
@@ -1453,17 +1473,26 @@ int rhs(ns_solver* s) {
 
 // u^{n+1} = u* - dt grad phi into the ping-pong partners (no in-place read/write hazard)
 // (K5 with phi's ghost rows, overlapped with the interior strips)
-int correct(ns_solver* s) {
+// K5 into the ping-pong partners (TMPU, TMPV) and its min/max into scal[S_MM]; `part2`: the
+// partial slots (the second half of s->part when speculating: the first half still holds
+// the residual partials the check is reducing)
+int correct_launch(ns_solver* s, double* part2) {
     const HaloReq r[1] = {{&s->g, s->arr[NS_ARR_PHI], 1}};
     const int nb = overlapped(s, r, 1, [&]() {
         return nsg::launch_correct(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
-                                   s->arr[NS_ARR_TMPV], s->arr[NS_ARR_PHI], s->part, s->st);
+                                   s->arr[NS_ARR_TMPV], s->arr[NS_ARR_PHI], part2, s->st);
     });
     if (nb < 0) return nb;
+    nsg::launch_reduce_min(part2, nb, 4, s->scal + S_MM, s->st);
+    CHK(allreduce(s, s->scal + S_MM, 4, ncclMin));
+    return 0;
+}
+
+int correct(ns_solver* s) {
+    if (!s->k5_spec) CHK(correct_launch(s, s->part));
+    s->k5_spec = 0;
     std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
     std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
-    nsg::launch_reduce_min(s->part, nb, 4, s->scal + S_MM, s->st);
-    CHK(allreduce(s, s->scal + S_MM, 4, ncclMin));
     return 0;
 }
 
@@ -1848,7 +1877,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (hipMemsetAsync(s->ksc, 0, nsg::KS_NUM * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     }
     const int np = nsg::max_partials(g);
-    if (hipMalloc(&s->part, (size_t)np * 4 * sizeof(double)) != hipSuccess) { set_err("hipMalloc partials failed"); return fail(NS_ENOMEM); }
+    // partials: [0, 4 np) for any kernel's, [4 np, 8 np) for a speculative K5's (correct_launch)
+    if (hipMalloc(&s->part, (size_t)np * 8 * sizeof(double)) != hipSuccess) { set_err("hipMalloc partials failed"); return fail(NS_ENOMEM); }
     if (hipMalloc(&s->scal, S_NUM * sizeof(double)) != hipSuccess) { set_err("hipMalloc scalars failed"); return fail(NS_ENOMEM); }
     if (hipMemsetAsync(s->scal, 0, S_NUM * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     if (hipHostMalloc(&s->hs, S_NUM * sizeof(double), hipHostMallocDefault) != hipSuccess) { set_err("hipHostMalloc failed"); return fail(NS_ENOMEM); }
@@ -1910,12 +1940,15 @@ void ns_destroy(ns_solver* s) {
 static int step_body_(ns_solver* s, ns_stats& st);
 static int step_body(ns_solver* s, ns_stats& st) {
     s->n_xchg = s->n_allred = 0;
+    s->k5_spec = 0;
     if (!s->replay.empty()) {
         const auto& r = s->replay[s->replay_k++ % s->replay.size()];
         s->rp_h = r.first;
         s->rp_c = r.second;
     }
+    s->in_step = 1;
     const int rc = step_body_(s, st);
+    s->in_step = 0;
     st.n_exchanges = s->n_xchg;
     st.n_allreduces = s->n_allred;
     return rc;

@@ -7,8 +7,8 @@ var=$1; shift
 mkdir -p gpurun_out
 for rep in 1 2; do
   for val in "$@"; do
-    env "$var=$val" timeout -k 10 200 python bench.py --steps ${STEPS:-10} --warmup ${WARMUP:-3} --no-cpu \
+    env "$var=$val" timeout -k 10 200 python bench.py --steps ${STEPS:-20} --warmup ${WARMUP:-10} --no-cpu \
       > gpurun_out/ab_${val}_$rep.log 2>&1
-    python3 -c "import json; d=json.loads(open('gpurun_out/ab_${val}_$rep.log').read().strip().splitlines()[-1]); print('$var=$val', round(d['value']), d['poisson_vcycles_per_step'], d['helmholtz_sweeps_per_step'], round(d['ms_per_step'], 3))"
+    python3 tools/bench_line.py "$var=$val" gpurun_out/ab_${val}_$rep.log
   done
 done
