@@ -28,6 +28,33 @@
 namespace nsg {
 
 // ---------------------------------------------------------------- helpers
+// The j-neighbour of a lane's column pair: the value of lane l - 1 (lane_up1) or l + 1
+// (lane_dn1), lane 0 / 63 keeping its own (__shfl_up / __shfl_down(x, 1, 64) semantics).  DPP
+// wave_shr:1 / wave_shl:1 row moves (two v_mov_b32_dpp per double, VALU) instead of the
+// ds_bpermute pair a shuffle compiles to: no LDS round trip on the sweeps' critical path
+// (LANE_DPP=0: the shuffles, A/B).
+#ifndef LANE_DPP
+#define LANE_DPP 1
+#endif
+__device__ __forceinline__ double lane_up1(double x) {
+#if LANE_DPP
+    const int lo = __double2loint(x), hi = __double2hiint(x);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, 0x138, 0xf, 0xf, false),
+                            __builtin_amdgcn_update_dpp(lo, lo, 0x138, 0xf, 0xf, false));
+#else
+    return __shfl_up(x, 1, 64);
+#endif
+}
+__device__ __forceinline__ double lane_dn1(double x) {
+#if LANE_DPP
+    const int lo = __double2loint(x), hi = __double2hiint(x);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, 0x130, 0xf, 0xf, false),
+                            __builtin_amdgcn_update_dpp(lo, lo, 0x130, 0xf, 0xf, false));
+#else
+    return __shfl_down(x, 1, 64);
+#endif
+}
+
 __device__ __forceinline__ double ldf(const double* f, int ld, int li, int j) {
     return f[(ptrdiff_t)li * ld + j];
 }
@@ -1002,7 +1029,7 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
             const int m = r - 1, gim = a.i0 + m;
             double2 Rn = P1;
             if (m >= ib - 1 && m <= ie) {
-                double lf = __shfl_up(P1.y, 1, 64), rt = __shfl_down(P1.x, 1, 64);
+                double lf = lane_up1(P1.y), rt = lane_dn1(P1.x);
                 const double* rw = rc[m - ib + RC_OFF];
                 const double cw = rw[0], ce = rw[1];
                 dm.at(rw[2], cd0, cd1, alpha, omega);
@@ -1031,7 +1058,7 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
                 R0 = R1; R1 = R2; R2 = Rn;
                 const int k = r - 2, gik = a.i0 + k;
                 if (k >= ib && k < ie) {
-                    const double lf = __shfl_up(R1.y, 1, 64), rt = __shfl_down(R1.x, 1, 64);
+                    const double lf = lane_up1(R1.y), rt = lane_dn1(R1.x);
                     const double* rw = rc[k - ib + RC_OFF];
                     const double cw = rw[0], ce = rw[1];
                     dk.at(rw[2], cd0, cd1, alpha, omega);
@@ -1199,7 +1226,7 @@ __global__ __launch_bounds__(256) void k_jacobi_s(JacobiArgs<T> a) {
                 xp[q] = Lane16<T>::get(P2, q);
                 bq[q] = Lane16<T>::get(bb, q);
             }
-            const double lf = __shfl_up(xq[V - 1], 1, 64), rt = __shfl_down(xq[0], 1, 64);
+            const double lf = lane_up1(xq[V - 1]), rt = lane_dn1(xq[0]);
             if (rd != rd_last) {   // the diagonal's row part repeats on a uniform grid
 #pragma unroll
                 for (int q = 0; q < V; q++) {
@@ -1324,7 +1351,7 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
             if (K == 3) {
                 // Div_V: u faces along x from the window, v faces along y from the lanes
                 const double2 vv = x;
-                const double vs0 = __shfl_up(vv.y, 1, 64), vn1 = __shfl_down(vv.x, 1, 64);
+                const double vs0 = lane_up1(vv.y), vn1 = lane_dn1(vv.x);
                 double val[2];
 #pragma unroll
                 for (int e = 0; e < 2; e++) {
@@ -1345,7 +1372,7 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
             } else {
                 // GradP (phi ghost = phi at wall / inlet faces: 0.5 (p + p); a NEUMANN side's
                 // extrapolated ghost goes through k_correct) and the correction
-                const double ps0 = __shfl_up(W1.y, 1, 64), pn1 = __shfl_down(W1.x, 1, 64);
+                const double ps0 = lane_up1(W1.y), pn1 = lane_dn1(W1.x);
                 double un[2], vn[2];
 #pragma unroll
                 for (int e = 0; e < 2; e++) {
@@ -1428,6 +1455,9 @@ constexpr int SW2X = 116;
 // VGPRs, FUSE_R (164) does not
 #ifndef SD2_HELM
 #define SD2_HELM 3
+#endif
+#ifndef SWEEP2_DIAG
+#define SWEEP2_DIAG 0
 #endif
 #ifndef SD2_HELMR
 #define SD2_HELMR SD2_HELM
@@ -1534,17 +1564,29 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
         double2 o = W1;
         const int gi = a.i0 + row;
         if (gi < 0 || gi >= a.nx) return o;
+#if SWEEP2_DIAG == 1   // diagnostic build (tools/sweep2_diag.py): the memory stream alone
+        o.x += B.x; o.y += B.y;
+        return o;
+#endif
         const double* rw = rc[row - ib + RC_OFF];
         const double cw = rw[0], ce = rw[1];
         double rr;
         // the row's colour is in one of the lane's two columns (wave-uniform): only that
         // column's diagonal, reciprocal and j-neighbour shuffle are formed
         if ((gi & 1) == par) {
-            const double lf = __shfl_up(W1.y, 1, 64);
+#if SWEEP2_DIAG == 2   // diagnostic: no cross-lane shuffles
+            const double lf = W1.y;
+#else
+            const double lf = lane_up1(W1.y);
+#endif
             const double d = diag<OP>(rw[2], cd0, alpha), w = omega * rcp_nr(d);
             if (v0) o.x = relax<OP>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr);
         } else {
-            const double rt = __shfl_down(W1.x, 1, 64);
+#if SWEEP2_DIAG == 2
+            const double rt = W1.x;
+#else
+            const double rt = lane_dn1(W1.x);
+#endif
             const double d = diag<OP>(rw[2], cd1, alpha), w = omega * rcp_nr(d);
             if (v1) o.y = relax<OP>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, d, w, alpha, rr);
         }
@@ -1554,8 +1596,8 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     auto step = [&](double2 p, const double2 bb, const double2 ee, int r) {
         if (XP) {
             // phi += P(e): e(I, J) = ee.x, e(In, J) = ee.y, column neighbours from lanes -+ 1
-            double m0 = __shfl_up(ee.x, 1, 64), m1 = __shfl_up(ee.y, 1, 64);
-            double q0 = __shfl_down(ee.x, 1, 64), q1 = __shfl_down(ee.y, 1, 64);
+            double m0 = lane_up1(ee.x), m1 = lane_up1(ee.y);
+            double q0 = lane_dn1(ee.x), q1 = lane_dn1(ee.y);
             if (!jm_ok) { m0 = ee.x; m1 = ee.y; }
             if (!jp_ok) { q0 = ee.x; q1 = ee.y; }
             p.x += (9.0 * ee.x + 3.0 * ee.y + 3.0 * m0 + m1) * 0.0625;
@@ -1603,7 +1645,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
             const int m5 = r - 5 * DIR;
             const double2 Fm = DIR > 0 ? F0 : F2, Fp = DIR > 0 ? F2 : F0;   // rows m5 - 1, m5 + 1
             if (m5 >= ib && m5 < ie) {
-                const double lf = __shfl_up(F1.y, 1, 64), rt = __shfl_down(F1.x, 1, 64);
+                const double lf = lane_up1(F1.y), rt = lane_dn1(F1.x);
                 const double* rw = rc[m5 - ib + RC_OFF];
                 const double cw = rw[0], ce = rw[1], hxr = rw[3];
                 const double d0 = diag<OP>(rw[2], cd0, alpha), d1 = diag<OP>(rw[2], cd1, alpha);
@@ -1673,7 +1715,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
 }
 
 template <int OP, bool RES, int FUSE>
-__global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
+__device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
     constexpr bool XR = FUSE == FUSE_R;
     constexpr bool R5 = RES || XR;                 // the fifth (output residual) stage
     __shared__ double rcs[4][RC_MAX][4];
@@ -1700,6 +1742,9 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) {
         if (lane == 0 && w < nstr) a.part[wid] = res;
     }
 }
+
+template <int OP, bool RES, int FUSE>
+__global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) { sweep2_body<OP, RES, FUSE>(a); }
 
 // ------------------------------------------------ K4 small levels: LDS-tiled fused passes
 // The multigrid levels below the streaming kernels' range (< 2048^2 cells: 1024^2 .. 128^2

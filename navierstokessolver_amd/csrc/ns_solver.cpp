@@ -202,6 +202,7 @@ struct ns_solver {
     // trip; k5_spec = 1 after a passing check (the step then only swaps), 0 otherwise (K5 runs
     // again after the last cycle: u* is untouched, K5 writes TMPU / TMPV)
     int in_step = 0, k5_spec = 0, n_spec = 0, n_spec_hit = 0;
+    int speculate = 1;           // NSGPU_SPECULATE=0: no speculative K5 (the equivalence test's reference)
 };
 
 namespace {
@@ -983,7 +984,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     double prev_rr = -1.0;
     if (s->rp_c >= 0) next_chk = s->rp_c;   // virtual slab: the replayed cycle count, one check
     // speculate at the first check when the last four solves all converged by then
-    const bool spec_ok = s->in_step && s->mg_predict && s->rp_c < 0 && next_chk > 0;
+    const bool spec_ok = s->speculate && s->in_step && s->mg_predict && s->rp_c < 0 && next_chk > 0;
     auto check = [&](int nb) -> int {
         if (!(cycles >= next_chk || cycles >= maxc)) return 0;
         // fine residual after pre-smoothing: the convergence test (a host sync)
@@ -1731,6 +1732,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_HELM_EXTRAP")) s->helm_extrap = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = getenv("NSGPU_MG_PREDICT")) s->mg_predict = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_SPECULATE")) s->speculate = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     {

@@ -600,20 +600,20 @@ def test_dispatch_stamped_kernel_timing(gpu, monkeypatch):
 def test_speculative_correction_is_bit_identical(gpu, monkeypatch, n):
     """The step's K5 (CorrectVelocities, FluidSolver.cpp:512-534) is enqueued behind the
     multigrid's predicted residual check, before the host reads the residual; a check that
-    fails discards it.  NSGPU_MG_PREDICT=0 checks after every V-cycle and never speculates:
-    the same cycles, so the fields must be bit-identical."""
+    fails discards it.  NSGPU_SPECULATE=0 runs K5 after the solve instead: the same cycles,
+    so the fields and monitors must be bit-identical."""
     dt, re = 1.0 / (8 * n), 1000.0
     out = []
-    for predict in ("1", "0"):
-        monkeypatch.setenv("NSGPU_MG_PREDICT", predict)
+    for spec in ("1", "0"):
+        monkeypatch.setenv("NSGPU_SPECULATE", spec)
         gs = gpu.GpuSolver(gpu.cavity(n), dt, re)
         st = [gs.step() for _ in range(12)]
+        st += [gs.step_async() for _ in range(3)]
         out.append((gs.fields(), [s["it_phi"] for s in st], [s["n_checks"] for s in st],
-                    [[s[k] for k in ("umin", "umax", "vmin", "vmax")] for s in st]))
+                    [[s[k] for k in ("umin", "umax", "vmin", "vmax")] for s in st[:12]], gs.monitor()))
         gs.close()
-    (fa, ca, na, ma), (fb, cb, nb, mb) = out
-    assert ca == cb
-    assert sum(na) < sum(nb)            # the predicted checks ran (and the speculation with them)
-    assert ma == mb
+    (fa, ca, na, ma, la), (fb, cb, nb, mb, lb) = out
+    assert ca == cb and na == nb
+    assert ma == mb and la == lb
     for x, y in zip(fa, fb):
         assert np.array_equal(x, y)
