@@ -899,7 +899,10 @@ struct StreamArgs {
     int ntl;                          // non-temporal iterate loads
     // strip subset of this launch (k_sweep2; exchange / compute overlap): launch strip-row k
     // is strip row k if k < slo, else shi0 + (k - slo); nrun strip rows in all
-    int slo, shi0, nrun;
+    // strip rows of this launch (plan_strips2; k_sweep2): launch strip row k covers rows
+    // [ib, min(ib + L, rend)) with ib = rb0 + k L for k < slo, else rb1 + (k - slo) L; its
+    // residual partials go to slot (pbase + k) nsj + j; nrun strip rows in all
+    int slo, nrun, rb0, rb1, rend, pbase;
 };
 
 // diagonal of the operator at a cell from its row / column coefficient sums
@@ -923,9 +926,9 @@ __device__ __forceinline__ double relax(double q, double xm, double xp, double y
 // Streamed field stores bypass the Infinity Cache (non-temporal): the 256 MiB die cache then
 // keeps what the NEXT pass re-reads -- the rhs b, read by every sweep of a solve -- instead
 // of filling with this pass's output (tools/membw2.hip, 4096^2 2-read + 1-write stream:
-// 5.3 TB/s with plain stores, 6.8-7.5 TB/s with nt stores).  NSGPU_NT_STORES=0: plain (A/B).
+// 5.3 TB/s with plain stores, 6.8-7.5 TB/s with nt stores).
 typedef double nsd2 __attribute__((ext_vector_type(2)));
-// the iterate's loads may be non-temporal too (NSGPU_NT_LOADS=1, A/B): it is read once per pass
+// the iterate's loads may be non-temporal too: it is read once per pass (the prolongation pass)
 __device__ __forceinline__ double2 ld_stream(const double* p, int nt) {
     if (nt > 0) {
         const nsd2 v = __builtin_nontemporal_load(reinterpret_cast<const nsd2*>(p));
@@ -1481,7 +1484,8 @@ constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2;
 // strip's residual partial (R5)
 // (two instantiations: runtime window selects would cost ~50 VGPRs)
 template <int OP, bool RES, int FUSE, int DIR>
-__device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double (*rc)[4], int wid, int lane) {
+__device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
+                                              int lane) {
     constexpr int SD2 = sd2_of<OP, RES, FUSE>();
     constexpr bool XR = FUSE == FUSE_R, XP = FUSE == FUSE_P;
     constexpr bool R5 = RES || XR;
@@ -1492,9 +1496,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     // (2 waves/SIMD, 112 -> 160 us), and at 3 waves it spilled and still lost 3 us
     constexpr bool BF = !XR;
     double res = 0.0;
-    const int si = wid / a.nsj, sj = wid - si * a.nsj;
-    const int jb = sj * SWc, ib = si * a.L;
-    const int ie = min(ib + a.L, a.nxl);
+    const int jb = sj * SWc;
     const int ny = a.ny, ld = a.ld;
     const int c0 = jb - 4 - 2 * EXT + 2 * lane, c1 = c0 + 1;
     const int lc = min(max(c0, 0), ld - 2);
@@ -1521,7 +1523,8 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     const __amdgpu_buffer_rsrc_t pco = __builtin_amdgcn_make_buffer_rsrc(
         XR ? a.pc + (ptrdiff_t)rbc * a.ldc : a.out, (short)0, XR ? (int)((unsigned)((a.L >> 1) + 2) * a.ldc * 8u) : 0,
         0x00020000);
-    double2 Q[SD2], QB[SD2], QE[SD2];
+    double2 Q[SD2], QB[SD2];
+    double QE[SD2];
     // phi rows ib-4-EXT .. ie+3+EXT and b rows ib-3-EXT .. ie+2+EXT (the first red
     // stage's) are read; the rest are clamped onto fetched rows (see k_sweep)
     const int r0 = ib - 4 - EXT, r1 = ie + 3 + EXT;
@@ -1534,17 +1537,20 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     const int Jc = c0 >> 1;
     const int Jl = XP ? min(max(Jc, 0), a.ncy - 1) : 0;
     const bool jm_ok = Jc - 1 >= 0, jp_ok = Jc + 1 < a.ncy;
-    auto load = [&](int slot_r, double2& p, double2& bb, double2& ee) {
+    // FUSE_P: fine row r needs coarse rows I = r >> 1 and its neighbour In (I + 1 for odd r, I - 1
+    // for even r, I at a wall).  Along the walk consecutive rows share one of them, so a row
+    // loads only In and takes I from the previous row's pair (`ep`): one coarse load per row
+    // instead of two, each coarse row fetched about once per strip
+    auto nbr = [&](int lp) {
+        const int I = lp >> 1;                      // floor, also for ghost rows
+        const int In = (lp & 1) ? I + 1 : I - 1;
+        return (a.ci0 + In < 0 || a.ci0 + In >= a.ncx) ? I : In;
+    };
+    auto load = [&](int slot_r, double2& p, double2& bb, double& ee) {
         const int lp = min(max(slot_r, phi_lo), phi_hi), lb = min(max(slot_r - DIR, b_lo), b_hi);
         p = ld_stream(a.in + (ptrdiff_t)lp * ld + lc, XP ? 1 : 0);   // compile-time policy: no branch
         bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
-        if (XP) {
-            const int I = lp >> 1;                      // floor, also for ghost rows
-            int In = (lp & 1) ? I + 1 : I - 1;
-            if (a.ci0 + In < 0 || a.ci0 + In >= a.ncx) In = I;
-            ee.x = a.ec[(ptrdiff_t)I * a.ldc + Jl];
-            ee.y = a.ec[(ptrdiff_t)In * a.ldc + Jl];
-        }
+        if (XP) ee = a.ec[(ptrdiff_t)nbr(lp) * a.ldc + Jl];
     };
     // windows (3 rows each) of the stages' inputs, rhs rows r-1 .. r-5
     double2 P0 = {0, 0}, P1 = {0, 0}, P2 = {0, 0};     // old:           rows r-2 .. r
@@ -1593,8 +1599,15 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
         return o;
     };
 
-    auto step = [&](double2 p, const double2 bb, const double2 ee, int r) {
+    double2 ep = {0, 0};   // FUSE_P: (e(I), e(In)) of the previous row of the walk
+    auto step = [&](double2 p, const double2 bb, const double ce, int r) {
         if (XP) {
+            // rows with a new neighbour row (odd r walking down, even r walking up) take it from
+            // the load; the others reuse the previous row's two coarse rows, swapped
+            // (at a wall the neighbour is I itself: k_prolong's reflection)
+            const bool fresh = ((r & 1) != 0) == (DIR > 0), wall = nbr(r) == (r >> 1);
+            const double2 ee = fresh ? make_double2(ep.x, ce) : make_double2(ep.y, wall ? ep.y : ep.x);
+            ep = ee;
             // phi += P(e): e(I, J) = ee.x, e(In, J) = ee.y, column neighbours from lanes -+ 1
             double m0 = lane_up1(ee.x), m1 = lane_up1(ee.y);
             double q0 = lane_dn1(ee.x), q1 = lane_dn1(ee.y);
@@ -1699,6 +1712,10 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     };
 
     const int rs = DIR > 0 ? r0 : r1, nr = r1 - r0 + 1;
+    if (XP) {   // the coarse pair of the row before the walk's first
+        const int lp = rs - DIR;
+        ep = make_double2(a.ec[(ptrdiff_t)(lp >> 1) * a.ldc + Jl], a.ec[(ptrdiff_t)nbr(lp) * a.ldc + Jl]);
+    }
 #pragma unroll
     for (int q = 0; q < SD2; q++) {
         load(rs + DIR * q, Q[q], QB[q], QE[q]);
@@ -1723,18 +1740,20 @@ __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
     const int nstr = a.nsj * a.nrun;
     const int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
     double (*rc)[4] = rcs[threadIdx.x >> 6];
-    // this wave's strip (row si of the slab's strips): the launch may cover a subset of them
-    const int run = w / a.nsj, si = run < a.slo ? run : a.shi0 + (run - a.slo);
-    const int wid = si * a.nsj + (w - run * a.nsj);
-    if (w < nstr) stage_rows<OP>(a, rc, si * a.L, lane);
+    // this wave's strip (plan_strips2: the launch may cover a subset of the pass's rows)
+    const int run = w / a.nsj, sj = w - run * a.nsj;
+    const int ib = run < a.slo ? a.rb0 + run * a.L : a.rb1 + (run - a.slo) * a.L;
+    const int ie = min(ib + a.L, a.rend);
+    const int si = a.pbase + run, wid = si * a.nsj + sj;
+    if (w < nstr) stage_rows<OP>(a, rc, ib, lane);
     __syncthreads();
     double res = 0.0;
     if (w < nstr) {
         // alternate strips walk in opposite directions (a.alt): the halo rows two strips
         // share are then read by both at about the same time -- an L2 hit for the second --
         // instead of at opposite ends of the kernel (each row band read twice from HBM)
-        if (a.alt && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1>(a, rc, wid, lane);
-        else res = sweep2_strip<OP, RES, FUSE, 1>(a, rc, wid, lane);
+        if (a.alt && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1>(a, rc, ib, ie, sj, lane);
+        else res = sweep2_strip<OP, RES, FUSE, 1>(a, rc, ib, ie, sj, lane);
     }
     if (R5) {
 #pragma unroll
@@ -2701,11 +2720,9 @@ static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, dou
     a.nx = g.nx; a.ny = g.ny; a.i0 = g.i0; a.nxl = g.nxl; a.ld = g.ld;
     a.nsj = (g.ny + SW - 1) / SW;
     a.part = part;
-    const char* e = getenv("NSGPU_NT_STORES");
-    a.nt = e ? std::atoi(e) != 0 : 1;
+    a.nt = 1;
     a.alt = 1;
-    const char* e3 = getenv("NSGPU_NT_LOADS");
-    a.ntl = e3 ? std::atoi(e3) : -1;   // -1: per kernel (the prolongation pass only)
+    a.ntl = -1;   // per kernel (non-temporal in the prolongation pass only)
     return a;
 }
 
@@ -2716,9 +2733,48 @@ void set_strip_phase(int phase) { g_phase = phase; }
 
 // the strip subset of the current phase (k_sweep2 launchers); returns the workgroup count
 // (0: nothing to launch)
-static int apply_phase(StreamArgs& a, int depth) {
-    a.nrun = phase_range(a.nxl, a.L, a.nsi, depth, &a.slo, &a.shi0);
-    return (a.nsj * a.nrun + 3) / 4;
+// The strip rows of a two-sweep pass for the current overlap phase (set_strip_phase), reading
+// `depth` rows beyond their own:
+//   phase 0: the slab's rows in strips of L (strip_rows: one resident round);
+//   phase 1: rows [d, nxl - d), whose read cone stays inside the slab (launched while the
+//            ghost rows travel), in strips of L over those rows;
+//   phase 2: the two edge bands [0, d) and [nxl - d, nxl) as two strips of d rows -- short
+//            strips, so the part after the exchange is a row pipeline of d + 8 steps rather than
+//            of L + 8;
+// d = depth rounded up to even (the fused restriction pairs rows).  Partial slots: phase 1's
+// strip rows, then phase 2's two.  Sets a.L and the launch's strip mapping; returns the
+// pass's strip count (the same for both phases) and the launch's workgroups in *nblk.
+static int plan_strips2(StreamArgs& a, long cap, int depth, int* nblk) {
+    const int d = (depth + 1) & ~1, R = a.nxl - 2 * d;
+    a.pbase = 0;
+    a.rb1 = 0;
+    if (g_phase == 0 || R < 2) {
+        a.L = strip_rows(a.nxl, a.nsj, cap, 16);
+        const int n = (a.nxl + a.L - 1) / a.L;
+        a.nrun = g_phase == 1 ? 0 : n;   // (a slab too thin to split: all of it after the exchange)
+        a.slo = n;
+        a.rb0 = 0;
+        a.rend = a.nxl;
+        *nblk = (a.nsj * a.nrun + 3) / 4;
+        return a.nsj * n;
+    }
+    a.L = strip_rows(R, a.nsj, cap, 16);
+    const int n1 = (R + a.L - 1) / a.L;
+    if (g_phase == 1) {
+        a.nrun = a.slo = n1;
+        a.rb0 = d;
+        a.rend = a.nxl - d;
+    } else {
+        a.L = d;
+        a.nrun = 2;
+        a.slo = 1;
+        a.rb0 = 0;
+        a.rb1 = a.nxl - d;
+        a.rend = a.nxl;
+        a.pbase = n1;
+    }
+    *nblk = (a.nsj * a.nrun + 3) / 4;
+    return a.nsj * (n1 + 2);
 }
 
 // count_only: return the strip (= partial) count a launch with residual would have, launch nothing
@@ -2748,9 +2804,8 @@ static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st, bool count
     a.nsj = a.part ? (g.ny + SW2X - 1) / SW2X : (g.ny + SW2 - 1) / SW2;
     const long cap = resident_waves(a.part ? (const void*)k_sweep2<OP, true, FUSE_NONE>
                                            : (const void*)k_sweep2<OP, false, FUSE_NONE>);
-    a.L = strip_rows(a.nxl, a.nsj, cap, 16);
-    a.nsi = (g.nxl + a.L - 1) / a.L;
-    const int nstr = a.nsj * a.nsi, nblk = apply_phase(a, a.part ? 5 : 4);
+    int nblk = 0;
+    const int nstr = plan_strips2(a, cap, a.part ? 5 : 4, &nblk);
     if (count_only || !nblk) return nstr;
     if (a.part) NS_LAUNCH((k_sweep2<OP, true, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
     else NS_LAUNCH((k_sweep2<OP, false, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
@@ -2763,9 +2818,8 @@ int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const
     StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
     a.hx = c.hx; a.hy = c.hy; a.bc = bc; a.pc = pc; a.ldc = gc.ld;
     a.nsj = (g.ny + SW2X - 1) / SW2X;
-    a.L = strip_rows(a.nxl, a.nsj, resident_waves((const void*)k_sweep2<0, false, FUSE_R>), 16);
-    a.nsi = (g.nxl + a.L - 1) / a.L;
-    const int nstr = a.nsj * a.nsi, nblk = apply_phase(a, 5);
+    int nblk = 0;
+    const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2<0, false, FUSE_R>), 5, &nblk);
     if (nblk) NS_LAUNCH((k_sweep2<0, false, FUSE_R>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
@@ -2779,9 +2833,8 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
     // correction keep the Infinity Cache); neutral-to-worse in the other passes
     if (a.ntl < 0) a.ntl = 1;
     a.nsj = (g.ny + SW2X - 1) / SW2X;
-    a.L = strip_rows(a.nxl, a.nsj, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 16);
-    a.nsi = (g.nxl + a.L - 1) / a.L;
-    const int nstr = a.nsj * a.nsi, nblk = apply_phase(a, 5);
+    int nblk = 0;
+    const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 5, &nblk);
     if (nblk) NS_LAUNCH((k_sweep2<0, false, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
@@ -2840,8 +2893,7 @@ static int launch_jacobi_s(const Geo& g, const Coef& c, double omega, const T* i
     constexpr int SWV = 62 * Lane16<T>::V;
     a.nsj = (g.ny + SWV - 1) / SWV;
     a.part = part;
-    const char* e = getenv("NSGPU_NT_STORES");
-    const bool nt = e ? std::atoi(e) != 0 : true;
+    const bool nt = true;
     const void* k = part ? (nt ? (const void*)k_jacobi_s<T, true, true> : (const void*)k_jacobi_s<T, true, false>)
                          : (nt ? (const void*)k_jacobi_s<T, false, true> : (const void*)k_jacobi_s<T, false, false>);
     a.L = strip_rows(a.nxl, a.nsj, resident_waves(k), 4);
@@ -2854,9 +2906,8 @@ static int launch_jacobi_s(const Geo& g, const Coef& c, double omega, const T* i
 
 int launch_pois_jacobi(const Geo& g, const Coef& c, double omega, const double* in, double* out, const double* rp,
                        const double* shift, double* part, hipStream_t st) {
-    // the branch-free streaming sweep; NSGPU_JACOBI_SWEEP=0, or a plane past 4 GiB: k_sweep<Jacobi>
-    static const int js = getenv("NSGPU_JACOBI_SWEEP") ? std::atoi(getenv("NSGPU_JACOBI_SWEEP")) : 1;
-    if (js) {
+    // the branch-free streaming sweep; a plane past 4 GiB: k_sweep<Jacobi>
+    {
         const int n = launch_jacobi_s<double>(g, c, omega, in, out, rp, shift, part, st);
         if (n >= 0) return n;
     }

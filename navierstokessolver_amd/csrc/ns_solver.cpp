@@ -124,7 +124,6 @@ struct ns_solver {
     int fuse_restrict = 1;       // NSGPU_FUSED_RESTRICT=0: separate k_restrict pass (A/B)
     int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
     int tile_small = 1;          // NSGPU_TILE_SMALL=0: no LDS-tiled fused passes on small levels (A/B)
-    int helm_split = 1;          // NSGPU_HELM_SPLIT=0: u and v pass by pass (A/B)
     int ext_timing = 1;          // NSGPU_EXT_TIMING=0: marker events around timed launches (t_begin)
     int phi_extrap = 2;          // Poisson initial guess: NSGPU_PHI_EXTRAP=0 phi^{n-1}, 1 linear, 2 quadratic (default)
     int mg_predict = 1;          // NSGPU_MG_PREDICT=0: a residual check (host sync) after every V-cycle
@@ -132,10 +131,6 @@ struct ns_solver {
     int mg_hist[4] = {-1, -1, -1, -1};   // V-cycles the last four solves converged at (first check)
     double* phim = nullptr;      // phi^{n-2} (the extrapolation's second point; rotates with PHI / TMP)
     double* phim2 = nullptr;     // phi^{n-3} (quadratic extrapolation only)
-    // NSGPU_HELM_EXTRAP=1 (A/B): Helmholtz initial guess 2 u*^n - u*^{n-1} instead of u^n
-    int helm_extrap = 0;
-    double *usm = nullptr, *vsm = nullptr, *usm_mem = nullptr;   // u*^{n-1}, v*^{n-1}
-    int us_valid = 0;            // 0: no u* kept; 1: TMPU/TMPV hold u*^n; 2: and usm/vsm u*^{n-1}
     double* phim_mem = nullptr;  // the extra planes' allocation
     float* f32_mem = nullptr;    // fp32-field sweep planes (configs[4]), allocated on first use
     float* f32[3] = {};          // phi, its ping-pong partner, rhs_phi (rows of g.ld floats)
@@ -437,7 +432,7 @@ int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3) {
 int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* part_last, int* nb_first,
                 int* first_at, int* last_at) {
     int nb = 0;
-    const bool split = s->helm_split && s->nranks == 1;
+    const bool split = s->nranks == 1;
     for (int which : {split ? 1 : 3, split ? 2 : 0}) {
         if (!which) break;
         int k = 0, launch = 0;
@@ -1280,9 +1275,8 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
     long agg_cells = 1024L * 1024L;
     if (const char* e = getenv("NSGPU_AGG_CELLS")) agg_cells = std::atol(e);
     const int agg_min_rows = 8;
-    // stop at the first whole level whose LDS V-cycle fits (<= ~64^2); NSGPU_LDS_CAP (bytes) for A/B
-    size_t lds_cap = 150 * 1024;
-    if (const char* e = getenv("NSGPU_LDS_CAP")) lds_cap = std::min<size_t>(std::atol(e), 150 * 1024);
+    // stop at the first whole level whose LDS V-cycle fits (<= ~64^2)
+    const size_t lds_cap = 150 * 1024;
     for (;;) {
         const MgLevel& F = s->lv.back();
         const nsg::Geo& gf = F.g;
@@ -1392,19 +1386,6 @@ int extrapolate_phi(ns_solver* s) {
     return 0;
 }
 
-// Helmholtz initial guess (NSGPU_HELM_EXTRAP=1): the linear extrapolation 2 u*^n - u*^{n-1} of the
-// previous steps' Helmholtz solutions into U (u^n is no longer needed once K1 has run).  u*^n
-// sits in TMPU / TMPV (correct() leaves it there); the planes rotate, no copies.
-int helm_guess(ns_solver* s) {
-    if (!s->helm_extrap || s->us_valid == 0) return 0;
-    if (s->us_valid >= 2) {
-        nsg::launch_axpby(s->g, 2.0, s->arr[NS_ARR_TMPU], -1.0, s->usm, s->arr[NS_ARR_U], s->st);
-        nsg::launch_axpby(s->g, 2.0, s->arr[NS_ARR_TMPV], -1.0, s->vsm, s->arr[NS_ARR_V], s->st);
-    }
-    std::swap(s->usm, s->arr[NS_ARR_TMPU]);
-    std::swap(s->vsm, s->arr[NS_ARR_TMPV]);
-    return 0;
-}
 
 // stretched grid without an outflow side: move rhs_phi onto the consistent system the oracle's
 // PCG solves (k_area_fix); a no-op elsewhere (uniform grids: sum A b = A sum b = 0 already).
@@ -1727,9 +1708,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_FUSED_RESTRICT")) s->fuse_restrict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
-    if (const char* e = getenv("NSGPU_HELM_SPLIT")) s->helm_split = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_EXT_TIMING")) s->ext_timing = std::atoi(e) != 0;
-    if (const char* e = getenv("NSGPU_HELM_EXTRAP")) s->helm_extrap = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = getenv("NSGPU_MG_PREDICT")) s->mg_predict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_SPECULATE")) s->speculate = std::atoi(e) != 0;
@@ -1749,7 +1728,6 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         for (int j = 1; j < gd->ny; j++) stretched |= std::fabs(gd->hy[j] - gd->hy[0]) > 1e-12 * gd->hy[0];
         for (int e = 0; e < gd->n_edges; e++) outflow |= gd->edges[e].type == NS_BC_NEUMANN;
         s->consist = stretched && !outflow;
-        if (const char* e = getenv("NSGPU_CONSISTENT_RHS")) s->consist = s->consist && std::atoi(e) != 0;
         double a = 0.0, ia = 0.0;
         for (int i = 0; i < gd->nx; i++)
             for (int j = 0; j < gd->ny; j++)
@@ -1817,12 +1795,6 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (np == 2) s->phim2 = s->phim + s->plane;
     }
 
-    if (s->helm_extrap) {
-        if (hipMalloc(&s->usm_mem, 2 * s->plane * sizeof(double)) != hipSuccess) { set_err("hipMalloc u* history failed"); return fail(NS_ENOMEM); }
-        if (hipMemsetAsync(s->usm_mem, 0, 2 * s->plane * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
-        s->usm = s->usm_mem + (size_t)nsg::HALO * g.ld;
-        s->vsm = s->usm + s->plane;
-    }
     if (masked) {
         if (hipMalloc(&s->fc_mem, fch.size() * sizeof(int32_t)) != hipSuccess ||
             hipMalloc(&s->et_mem, etab.size() * sizeof(nsg::EdgeDev)) != hipSuccess) { set_err("hipMalloc topology failed"); return fail(NS_ENOMEM); }
@@ -1847,10 +1819,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     // a masked domain's Poisson preconditioner: one V-cycle of the BOUNDING BOX's wall-closure
     // multigrid (a fictitious-domain preconditioner: the rhs is 0 outside the domain, the
     // outside values of the result are ignored by the masked operator), unless
-    // NSGPU_MASK_PC=jacobi
-    bool mask_mg = true;
-    if (const char* e = getenv("NSGPU_MASK_PC")) mask_mg = std::strcmp(e, "jacobi") != 0;
-    if (s->poisson == NS_POISSON_MG && (!masked || mask_mg)) {
+    if (s->poisson == NS_POISSON_MG) {
         if (p->mg_pre > 0) s->mg_pre = p->mg_pre;
         if (p->mg_omega > 0) s->mg_omega_s = p->mg_omega;
         if (const char* e = getenv("NSGPU_MG_OMEGA")) s->mg_omega_s = std::atof(e);   // smoother over-relaxation (A/B)
@@ -1919,7 +1888,6 @@ void ns_destroy(ns_solver* s) {
     if (s->base) (void)hipFree(s->base);
     if (s->phim_mem) (void)hipFree(s->phim_mem);
     if (s->kv_mem) (void)hipFree(s->kv_mem);
-    if (s->usm_mem) (void)hipFree(s->usm_mem);
     if (s->f32_mem) (void)hipFree(s->f32_mem);
     if (s->fc_mem) (void)hipFree(s->fc_mem);
     if (s->et_mem) (void)hipFree(s->et_mem);
@@ -1960,7 +1928,6 @@ static int step_body_(ns_solver* s, ns_stats& st) {
     CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
     // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
-    CHK(helm_guess(s));
     // rhs ghost rows (a checked pair pass reads ib-5): multi-rank pair passes take them with
     // their first overlapped exchange
     if (s->nranks > 1 && s->overlap && s->cst && !s->g.fc && !s->tiled) s->helm_b_pend = 1;
@@ -1978,7 +1945,6 @@ static int step_body_(ns_solver* s, ns_stats& st) {
         st.n_helm_kernels++;
     }
     s->hn = 0;
-    if (s->helm_extrap) s->us_valid = std::min(s->us_valid + 1, 2);  // correct() leaves u* in TMPU/TMPV
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
     CHK(consistent_rhs(s));                                        // stretched grids only
     // rhs_phi ghost rows: with the multigrid's first overlapped FUSE_R exchange when it has one
@@ -2082,7 +2048,6 @@ int ns_set_array(ns_solver* s, int which, const double* host) {
     if (which == NS_ARR_PHI || which == NS_ARR_TMP) s->phim_valid = 0;
     if (which == NS_ARR_PHI || which == NS_ARR_TMP || which == NS_ARR_RPHI)
         for (int& h : s->mg_hist) h = -1;   // an injected state: no cycle-count history
-    s->us_valid = 0;
     if (which == NS_ARR_RU || which == NS_ARR_RV) CHK(helm_bnorm(s));
     HIPCHK(hipStreamSynchronize(s->st));
     return 0;
@@ -2136,7 +2101,6 @@ int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* 
 
 int ns_kernel(ns_solver* s, int which, int iters, double* out) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
-    s->us_valid = 0;   // standalone kernels may overwrite the kept u*
     HIPCHK(hipSetDevice(s->device));
     const double alpha = s->dt / (2 * s->re);
     switch (which) {

@@ -1,3 +1,5 @@
+"""Per-step Helmholtz / Poisson counts and residuals of the 4096^2 cavity from rest; run with
+NSGPU_VERBOSE=1 for the solvers' residual histories on stderr.  python tools/verbose_steps.py"""
 import sys, os
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 import navierstokessolver_amd as nsa
