@@ -895,7 +895,6 @@ struct StreamArgs {
     const double* ec;
     int ncx, ncy, ci0;
     int nt;                           // non-temporal output stores
-    int alt;                          // alternate strips walk upwards
     int ntl;                          // non-temporal iterate loads
     // strip subset of this launch (k_sweep2; exchange / compute overlap): launch strip-row k
     // is strip row k if k < slo, else shi0 + (k - slo); nrun strip rows in all
@@ -1749,10 +1748,12 @@ __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
     __syncthreads();
     double res = 0.0;
     if (w < nstr) {
-        // alternate strips walk in opposite directions (a.alt): the halo rows two strips
-        // share are then read by both at about the same time -- an L2 hit for the second --
-        // instead of at opposite ends of the kernel (each row band read twice from HBM)
-        if (a.alt && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1>(a, rc, ib, ie, sj, lane);
+        // odd strips walk upwards: the halo rows two strips share are then read by both at about
+        // the same time -- an L2 hit for the second (Helmholtz pass 86.5 -> 84 us at 4096^2).
+        // The restriction pass walks downwards only: upwards, its fused restriction rounds some
+        // coarse sums differently, and its values would depend on how a pass is cut into strips
+        // (the overlapped exchange's split, the slab height)
+        if (FUSE != FUSE_R && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1>(a, rc, ib, ie, sj, lane);
         else res = sweep2_strip<OP, RES, FUSE, 1>(a, rc, ib, ie, sj, lane);
     }
     if (R5) {
@@ -2721,7 +2722,6 @@ static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, dou
     a.nsj = (g.ny + SW - 1) / SW;
     a.part = part;
     a.nt = 1;
-    a.alt = 1;
     a.ntl = -1;   // per kernel (non-temporal in the prolongation pass only)
     return a;
 }
