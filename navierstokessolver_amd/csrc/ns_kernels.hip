@@ -1488,8 +1488,10 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     constexpr int SD2 = sd2_of<OP, RES, FUSE>();
     constexpr bool XR = FUSE == FUSE_R, XP = FUSE == FUSE_P;
     constexpr bool R5 = RES || XR;
-    constexpr int EXT = (R5 || XP) ? 1 : 0;
-    constexpr int SWc = EXT ? SW2X : SW2;
+    // the residual stage needs one more finished row on each side (EXT: rows), the prolongation's
+    // coarse column neighbours one more column (EXTC: the written width)
+    constexpr int EXT = R5 ? 1 : 0, EXTC = (R5 || XP) ? 1 : 0;
+    constexpr int SWc = EXTC ? SW2X : SW2;
     // BF: the branch-free row loop (buffer stores, no tail guard; Helmholtz 95 -> 88 us, FUSE_P
     // 107 -> 104 us at 4096^2).  FUSE_R keeps plain stores: its deeper pipeline needed 172 VGPRs
     // (2 waves/SIMD, 112 -> 160 us), and at 3 waves it spilled and still lost 3 us
@@ -1497,10 +1499,10 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     double res = 0.0;
     const int jb = sj * SWc;
     const int ny = a.ny, ld = a.ld;
-    const int c0 = jb - 4 - 2 * EXT + 2 * lane, c1 = c0 + 1;
+    const int c0 = jb - 4 - 2 * EXTC + 2 * lane, c1 = c0 + 1;
     const int lc = min(max(c0, 0), ld - 2);
     const bool v0 = c0 >= 0 && c0 < ny, v1 = c1 >= 0 && c1 < ny;
-    const bool wr = lane >= 2 + EXT && lane <= 61 - EXT && c0 < ny;
+    const bool wr = lane >= 2 + EXTC && lane <= 61 - EXTC && c0 < ny;
     const bool o0 = wr && v0, o1 = wr && v1;
     const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
     const double cs0 = a.cs[k0], cn0 = a.cn[k0], cd0 = cs0 + cn0 + (OP == 1 ? a.by[k0] : 0.0);
@@ -2834,7 +2836,7 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
     if (a.ntl < 0) a.ntl = 1;
     a.nsj = (g.ny + SW2X - 1) / SW2X;
     int nblk = 0;
-    const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 5, &nblk);
+    const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 4, &nblk);
     if (nblk) NS_LAUNCH((k_sweep2<0, false, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
