@@ -37,6 +37,11 @@ struct Geo {
     int neu[4];
     double c0[4], c1[4];
     int enx[4], eny[4];  // outward normal of the edge on that side
+    // Poisson multigrid levels of the outflow preconditioner: x sides (bit 0: i = -1, bit 1:
+    // i = nx) closed by Dirichlet data on the face (weight 2/h^2 toward the ghost, which holds
+    // the face value) instead of a wall; prolongation extends the correction there oddly
+    // (0 on the face) rather than reflecting it
+    int dsx = 0;
 };
 
 // 1-D coefficient tables (global index) built once from hx, hy (ConstructLHS, FluidSolver.cpp:113-131)
@@ -171,7 +176,12 @@ int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const d
 // coarse levels as one LDS-resident V-cycle (single rank): level g and its 2x coarsenings
 size_t coarse_vcycle_bytes(const Geo& g);
 int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double* b, int cycles, int pre, int post,
-                         int citers, double comega, double somega, hipStream_t st);
+                         int citers, double comega, double somega, int dlo, int dhi, hipStream_t st);
+// the outflow side's 1-D line solve of the Poisson preconditioner into the row p (ny <= 4096;
+// -1 otherwise), and its constant extension along x over `rows` rows of the plane z (from its
+// first halo row) and the single row zg (if not null)
+int launch_line_solve(const double* r, const Coef& c, int ny, double* p, hipStream_t st);
+void launch_line_extend(const double* p, const Geo& g, double* z, int rows, double* zg, hipStream_t st);
 
 // NEUMANN outflow Poisson (BiCGStab on the true operator, right-preconditioned by one
 // wall-closure V-cycle; ns_solver.cpp pois_solve_krylov).  Device scalar slots:

@@ -894,6 +894,7 @@ struct StreamArgs {
     int ldc;
     const double* ec;
     int ncx, ncy, ci0;
+    int dsx;                          // FUSE_P: x sides closed by a value-0 ghost (Geo::dsx)
     int nt;                           // non-temporal output stores
     int ntl;                          // non-temporal iterate loads
     // strip subset of this launch (k_sweep2; exchange / compute overlap): launch strip-row k
@@ -1609,13 +1610,19 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
             const bool fresh = ((r & 1) != 0) == (DIR > 0), wall = nbr(r) == (r >> 1);
             const double2 ee = fresh ? make_double2(ep.x, ce) : make_double2(ep.y, wall ? ep.y : ep.x);
             ep = ee;
-            // phi += P(e): e(I, J) = ee.x, e(In, J) = ee.y, column neighbours from lanes -+ 1
-            double m0 = lane_up1(ee.x), m1 = lane_up1(ee.y);
-            double q0 = lane_dn1(ee.x), q1 = lane_dn1(ee.y);
-            if (!jm_ok) { m0 = ee.x; m1 = ee.y; }
-            if (!jp_ok) { q0 = ee.x; q1 = ee.y; }
-            p.x += (9.0 * ee.x + 3.0 * ee.y + 3.0 * m0 + m1) * 0.0625;
-            p.y += (9.0 * ee.x + 3.0 * ee.y + 3.0 * q0 + q1) * 0.0625;
+            // a side with face Dirichlet data (the outflow preconditioner) extends e oddly
+            // (0 on the face) instead of reflecting it; rows outside the domain keep their
+            // ghost data
+            const double ey = (wall && (a.dsx & ((r & 1) ? 2 : 1))) ? -ee.y : ee.y;
+            // phi += P(e): e(I, J) = ee.x, e(In, J) = ey, column neighbours from lanes -+ 1
+            double m0 = lane_up1(ee.x), m1 = lane_up1(ey);
+            double q0 = lane_dn1(ee.x), q1 = lane_dn1(ey);
+            if (!jm_ok) { m0 = ee.x; m1 = ey; }
+            if (!jp_ok) { q0 = ee.x; q1 = ey; }
+            if (a.i0 + r >= 0 && a.i0 + r < a.nx) {
+                p.x += (9.0 * ee.x + 3.0 * ey + 3.0 * m0 + m1) * 0.0625;
+                p.y += (9.0 * ee.x + 3.0 * ey + 3.0 * q0 + q1) * 0.0625;
+            }
         }
         P0 = P1; P1 = P2; P2 = (XP || !BF) ? p : vcopy(p);   // (XP: p is already a new value)
         B5 = B4; B4 = B3; B3 = B2; B2 = B1;
@@ -1867,11 +1874,16 @@ __global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
                 const int j = min(max(j0 - R + cc, 0), ny - 1);
                 const int I = li >> 1, Jc = j >> 1;
                 int In = (li & 1) ? I + 1 : I - 1;
-                if (a.ci0 + In < 0 || a.ci0 + In >= a.ncx) In = I;
+                double wn = 1.0;   // -1: a face-Dirichlet side (Geo::dsx), odd instead of even
+                if (a.ci0 + In < 0 || a.ci0 + In >= a.ncx) {
+                    if (a.dsx & ((li & 1) ? 2 : 1)) wn = -1.0;
+                    In = I;
+                }
                 int Jn = (j & 1) ? Jc + 1 : Jc - 1;
                 if (Jn < 0 || Jn >= a.ncy) Jn = Jc;
                 const int i1 = I - Ilo, i2 = In - Ilo, k1 = Jc - Jlo, k2 = Jn - Jlo;
-                p += (9.0 * se[i1][k1] + 3.0 * se[i2][k1] + 3.0 * se[i1][k2] + se[i2][k2]) * 0.0625;
+                if (a.i0 + li >= 0 && a.i0 + li < a.nx)
+                    p += (9.0 * se[i1][k1] + 3.0 * wn * se[i2][k1] + 3.0 * se[i1][k2] + wn * se[i2][k2]) * 0.0625;
             }
             sp[r][cc] = p;
             sb[r][cc] = bv[k] - shift;
@@ -1996,8 +2008,10 @@ __global__ __launch_bounds__(256) void k_prolong(Geo gf, double* __restrict__ ph
     const int gIn = gc.i0 + In;
     const int Iu = (gIn >= 0 && gIn < gc.nx) ? In : I;       // wall: reflect onto the parent
     const int Ju = (Jn >= 0 && Jn < gc.ny) ? Jn : Jc;
-    const double e = (9.0 * ldf(ec, gc.ld, I, Jc) + 3.0 * ldf(ec, gc.ld, Iu, Jc) + 3.0 * ldf(ec, gc.ld, I, Ju) +
-                      ldf(ec, gc.ld, Iu, Ju)) * 0.0625;
+    // a face-Dirichlet side (Geo::dsx): e extended oddly (0 on the face) instead
+    const double wn = (Iu == I && (gc.dsx & ((li & 1) ? 2 : 1))) ? -1.0 : 1.0;
+    const double e = (9.0 * ldf(ec, gc.ld, I, Jc) + 3.0 * wn * ldf(ec, gc.ld, Iu, Jc) + 3.0 * ldf(ec, gc.ld, I, Ju) +
+                      wn * ldf(ec, gc.ld, Iu, Ju)) * 0.0625;
     phi[(ptrdiff_t)li * gf.ld + j] += e;
     }
 }
@@ -2014,6 +2028,7 @@ constexpr int CV_THREADS = 1024;
 struct LdsLv {
     int nx, ny, phi, b, idg, cw, ce, cs, cn, hx, hy;  // offsets in doubles
     float rny;                                          // 1/ny for the index split
+    int dlo, dhi;   // a Dirichlet-centre closure (ghost value 0) on the x-low / x-high side
 };
 
 // k -> (k / ny, k % ny) without an integer division: float estimate + one correction
@@ -2027,7 +2042,10 @@ __device__ __forceinline__ void lv_split(const LdsLv& v, int k, int& i, int& j) 
 __device__ __forceinline__ double lv_lap(const double* L, const LdsLv& v, int i, int j) {
     const int ny = v.ny, k = i * ny + j;
     const double* p = L + v.phi;
-    const double s = L[v.cw + i] * p[k - (i > 0 ? ny : 0)] + L[v.ce + i] * p[k + (i < v.nx - 1 ? ny : 0)] +
+    // (a wall's weight is 0; a Dirichlet-centre side's ghost holds 0: the correction's data)
+    const double pw = i > 0 ? p[k - ny] : (v.dlo ? 0.0 : p[k]);
+    const double pe = i < v.nx - 1 ? p[k + ny] : (v.dhi ? 0.0 : p[k]);
+    const double s = L[v.cw + i] * pw + L[v.ce + i] * pe +
                      L[v.cs + j] * p[k - (j > 0 ? 1 : 0)] + L[v.cn + j] * p[k + (j < ny - 1 ? 1 : 0)];
     const double dg = -((L[v.cw + i] + L[v.ce + i]) + (L[v.cs + j] + L[v.cn + j]));
     return s + dg * p[k];
@@ -2111,11 +2129,15 @@ __host__ __device__ inline int lv_layout(int nx, int ny, LdsLv* lv, int* nlev) {
 
 __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, double* __restrict__ phi,
                                                               const double* __restrict__ b, int cycles, int pre,
-                                                              int post, int citers, double comega, double somega) {
+                                                              int post, int citers, double comega, double somega,
+                                                              int dlo, int dhi) {
     extern __shared__ __attribute__((aligned(16))) double L[];
     __shared__ LdsLv lv[LV_MAX];
     __shared__ int nlev;
-    if (threadIdx.x == 0) lv_layout(g.nx, g.ny, lv, &nlev);
+    if (threadIdx.x == 0) {
+        lv_layout(g.nx, g.ny, lv, &nlev);
+        for (int k = 0; k < nlev; k++) { lv[k].dlo = dlo; lv[k].dhi = dhi; }
+    }
     __syncthreads();
     const int nl = nlev;
     // level 0: the global coarsest level's phi, b and spacings
@@ -2142,8 +2164,8 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, dou
         }
         for (int t = threadIdx.x; t < v.nx; t += CV_THREADS) {
             const double h = L[v.hx + t];
-            L[v.cw + t] = t > 0 ? 2.0 / (h * (h + L[v.hx + t - 1])) : 0.0;
-            L[v.ce + t] = t < v.nx - 1 ? 2.0 / (h * (h + L[v.hx + t + 1])) : 0.0;
+            L[v.cw + t] = t > 0 ? 2.0 / (h * (h + L[v.hx + t - 1])) : (dlo ? 2.0 / (h * h) : 0.0);
+            L[v.ce + t] = t < v.nx - 1 ? 2.0 / (h * (h + L[v.hx + t + 1])) : (dhi ? 2.0 / (h * h) : 0.0);
         }
         for (int t = threadIdx.x; t < v.ny; t += CV_THREADS) {
             const double h = L[v.hy + t];
@@ -2187,11 +2209,15 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, dou
                 lv_split(f, t, i, j);
                 const int I = i >> 1, J = j >> 1;
                 int In = (i & 1) ? I + 1 : I - 1, Jn = (j & 1) ? J + 1 : J - 1;
-                if (In < 0 || In >= v.nx) In = I;
+                double wn = 1.0;   // a face-Dirichlet side (dlo / dhi): e extended oddly
+                if (In < 0 || In >= v.nx) {
+                    if (In < 0 ? dlo : dhi) wn = -1.0;
+                    In = I;
+                }
                 if (Jn < 0 || Jn >= v.ny) Jn = J;
                 const double* e = L + v.phi;
-                L[f.phi + t] += (9.0 * e[I * v.ny + J] + 3.0 * e[In * v.ny + J] + 3.0 * e[I * v.ny + Jn] +
-                                 e[In * v.ny + Jn]) * 0.0625;
+                L[f.phi + t] += (9.0 * e[I * v.ny + J] + 3.0 * wn * e[In * v.ny + J] + 3.0 * e[I * v.ny + Jn] +
+                                 wn * e[In * v.ny + Jn]) * 0.0625;
             }
             __syncthreads();
             lv_rb(L, f, somega, post);
@@ -2830,7 +2856,7 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
                                const double* rp, const double* shift, const Geo& gc, const double* ec,
                                hipStream_t st) {
     StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, nullptr, false);
-    a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0;
+    a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0; a.dsx = gc.dsx;
     // the iterate streamed non-temporally here: 113 -> 101 us at 4096^2 (b and the coarse
     // correction keep the Infinity Cache); neutral-to-worse in the other passes
     if (a.ntl < 0) a.ntl = 1;
@@ -2856,7 +2882,7 @@ int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const d
                               const double* rp, const double* shift, const Geo& gc, const double* ec,
                               hipStream_t st) {
     StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, nullptr, false);
-    a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0;
+    a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0; a.dsx = gc.dsx;
     const int tj = (g.ny + TT - 1) / TT, ntiles = tj * ((g.nxl + TT - 1) / TT);
     NS_LAUNCH(k_tile2<FUSE_P>, dim3(ntiles), dim3(256), 0, st, a, tj);
     return ntiles;
@@ -2998,7 +3024,7 @@ void launch_prolong(const Geo& gf, double* phi, const Geo& gc, const double* ec,
 size_t coarse_vcycle_bytes(const Geo& g) { return sizeof(double) * (size_t)lv_layout(g.nx, g.ny, nullptr, nullptr); }
 
 int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double* b, int cycles, int pre, int post,
-                         int citers, double comega, double somega, hipStream_t st) {
+                         int citers, double comega, double somega, int dlo, int dhi, hipStream_t st) {
     const size_t bytes = coarse_vcycle_bytes(g);
     if (bytes > 150 * 1024 || g.nxl != g.nx) return -1;
     static bool attr = false;
@@ -3007,8 +3033,125 @@ int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double*
         attr = true;
     }
     NS_LAUNCH(k_coarse_vcycle, dim3(1), dim3(CV_THREADS), bytes, st, g, c, phi, b, cycles, pre, post, citers,
-                       comega, somega);
+                       comega, somega, dlo, dhi);
     return 0;
+}
+
+// ---------------------------------------------- outflow line solve (NEUMANN side, preconditioner)
+// The 1-D problem of the Poisson preconditioner's outflow side: on the boundary
+// row (a W or E outflow side: one slab row, j contiguous) solve T p = r - <r>, T the operator's
+// y part (ConstructLHS's weights toward j -+ 1, walls closed), <r> the hy-weighted mean
+// (T's compatibility condition), p_0 pinned to 0, then the plain mean removed.  One
+// workgroup; parallel cyclic reduction in LDS (ny <= LINE_CAP).  p goes to the ghost row of
+// `z1` and `z2` (the V-cycle iterate's two planes), where the hierarchy's Dirichlet-centre
+// closure reads it as the side's data.
+constexpr int LINE_CAP = 4096;
+__global__ __launch_bounds__(1024) void k_line_solve(const double* __restrict__ r, const double* __restrict__ ps,
+                                                     const double* __restrict__ pn, const double* __restrict__ hy,
+                                                     int ny, double* __restrict__ p) {
+    extern __shared__ __attribute__((aligned(16))) double S[];
+    double *A = S, *B = S + ny, *C = S + 2 * ny, *D = S + 3 * ny;
+    __shared__ double red[2][16];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // hy-weighted mean of r (fixed order: per-thread strided partials, then waves)
+    double sr = 0.0, sh = 0.0;
+    for (int j = t; j < ny; j += 1024) { sr += hy[j] * r[j]; sh += hy[j]; }
+    for (int o = 32; o > 0; o >>= 1) { sr += __shfl_xor(sr, o, 64); sh += __shfl_xor(sh, o, 64); }
+    if (lane == 0) { red[0][w] = sr; red[1][w] = sh; }
+    __syncthreads();
+    if (t == 0) {
+        double a = 0.0, h = 0.0;
+        for (int k = 0; k < 16; k++) { a += red[0][k]; h += red[1][k]; }
+        red[0][0] = a / h;
+    }
+    __syncthreads();
+    const double mean = red[0][0];
+    for (int j = t; j < ny; j += 1024) {
+        const double cs = ps[j], cn = pn[j];
+        A[j] = j == 0 ? 0.0 : cs;
+        C[j] = j == 0 ? 0.0 : cn;
+        B[j] = j == 0 ? 1.0 : -(cs + cn);
+        D[j] = j == 0 ? 0.0 : r[j] - mean;
+    }
+    __syncthreads();
+    constexpr int PER = LINE_CAP / 1024;
+    for (int st = 1; st < ny; st <<= 1) {
+        double na[PER], nb[PER], nc[PER], nd[PER];
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const int j = t + q * 1024;
+            if (j >= ny) continue;
+            double a = A[j], b = B[j], c = C[j], d = D[j];
+            if (j - st >= 0) {
+                const double k1 = a / B[j - st];
+                b -= C[j - st] * k1;
+                d -= D[j - st] * k1;
+                a = -A[j - st] * k1;
+            } else {
+                a = 0.0;
+            }
+            if (j + st < ny) {
+                const double k2 = c / B[j + st];
+                b -= A[j + st] * k2;
+                d -= D[j + st] * k2;
+                c = -C[j + st] * k2;
+            } else {
+                c = 0.0;
+            }
+            na[q] = a; nb[q] = b; nc[q] = c; nd[q] = d;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const int j = t + q * 1024;
+            if (j >= ny) continue;
+            A[j] = na[q]; B[j] = nb[q]; C[j] = nc[q]; D[j] = nd[q];
+        }
+        __syncthreads();
+    }
+    // p = D / B, then its plain mean removed
+    double sp = 0.0;
+    for (int j = t; j < ny; j += 1024) { D[j] = D[j] / B[j]; sp += D[j]; }
+    for (int o = 32; o > 0; o >>= 1) sp += __shfl_xor(sp, o, 64);
+    __syncthreads();
+    if (lane == 0) red[0][w] = sp;
+    __syncthreads();
+    if (t == 0) {
+        double a = 0.0;
+        for (int k = 0; k < 16; k++) a += red[0][k];
+        red[1][0] = a / ny;
+    }
+    __syncthreads();
+    const double pm = red[1][0];
+    for (int j = t; j < ny; j += 1024) p[j] = D[j] - pm;
+}
+
+// the line solution p extended constantly along x: every row of the plane z (its halo rows
+// included; columns ny .. ld zero) and, if zg, the one row zg (the other plane's ghost)
+__global__ __launch_bounds__(256) void k_line_extend(const double* __restrict__ p, int ny, int ld, int rows,
+                                                     double* __restrict__ z, double* __restrict__ zg) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= ld) return;
+    const double v = j < ny ? p[j] : 0.0;
+    for (int r = blockIdx.y; r < rows; r += gridDim.y) z[(ptrdiff_t)r * ld + j] = v;
+    if (zg && blockIdx.y == 0) zg[j] = v;
+}
+
+int launch_line_solve(const double* r, const Coef& c, int ny, double* p, hipStream_t st) {
+    if (ny > LINE_CAP) return -1;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_line_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  4 * LINE_CAP * (int)sizeof(double));
+        attr = true;
+    }
+    NS_LAUNCH(k_line_solve, dim3(1), dim3(1024), (size_t)4 * ny * sizeof(double), st, r, c.ps, c.pn, c.hy, ny, p);
+    return 0;
+}
+
+void launch_line_extend(const double* p, const Geo& g, double* z, int rows, double* zg, hipStream_t st) {
+    NS_LAUNCH(k_line_extend, dim3((g.ld + 255) / 256, std::min(rows, 256)), dim3(256), 0, st, p, g.ny, g.ld, rows, z,
+              zg);
 }
 
 void launch_reduce_sum(const double* p, int n, int nv, double* out, hipStream_t st) {

@@ -158,9 +158,14 @@ struct ns_solver {
     // (null without an outflow side) and the recurrence scalars
     double* kv[9] = {};
     double* kv_mem = nullptr;
+    double* lrow = nullptr;      // outflow preconditioner: its line solution (one row, in kv_mem)
     double* ksc = nullptr;
     bool pc_active = false;      // inside mg_precond: level 0 has no mean shift, no timing
     bool krylov_mg = false;      // the Poisson BiCGStab is preconditioned by a V-cycle (else Jacobi)
+    // the outflow preconditioner: a rectangle whose only NEUMANN side is W (0) or
+    // E (1): the V-cycle's hierarchy closes that side with a Dirichlet-centre ghost whose data,
+    // on the finest level, is the side's 1-D line solve (launch_line_solve); -1 = walls
+    int out_side = -1;
     bool consist = false;        // stretched grid, no outflow: consistent_rhs() before every Poisson solve
     double area = 0.0;           // sum of the domain's cell areas
     double inv_area = 0.0;       // sum of their reciprocals
@@ -318,7 +323,7 @@ int allreduce(ns_solver* s, double* d, int n, ncclRedOp_t op) {
     if (!comm_on(s)) return 0;
     s->n_allred++;
     if (s->ht.allreduce) {
-        CHK(ensure_stage(s, 64));
+        CHK(ensure_stage(s, std::max(n, 64)));
         HIPCHK(hipMemcpyAsync(s->stage, d, n * 8, hipMemcpyDeviceToHost, s->st));
         HIPCHK(hipStreamSynchronize(s->st));
         if (s->ht.allreduce(s->ht.user, s->stage, n, op == ncclMin ? 1 : 0) != 0) {
@@ -847,7 +852,8 @@ int mg_coarse(ns_solver* s) {
     CHK(flush_b(s, l));
     if (s->mg_coarse_lds) {
         if (nsg::launch_coarse_vcycle(L.g, L.c, L.phi, L.b, 1, s->mg_pre, s->mg_post, s->mg_coarse_iters,
-                                      s->mg_omega_c, s->mg_omega_s, s->st) != 0) {
+                                      s->mg_omega_c, s->mg_omega_s, s->out_side == 0, s->out_side == 1,
+                                      s->st) != 0) {
             set_err("coarse LDS V-cycle does not fit");
             return NS_EINVAL;
         }
@@ -1072,12 +1078,33 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
 // mean-free, as MatNullSpaceRemove does to the reference's Krylov vectors.  All recurrence
 // scalars live on the device (k_bicg_scal); one host sync per iteration reads ||r||^2.
 
-// z = M^-1 q: one V-cycle of the wall-closure multigrid from z = 0 with level-0 rhs q (no
-// mean shift).  Level 0 is re-pointed at (z, scratch, q) and restored afterwards; the cycle's
+// z = M^-1 q: one V-cycle of the preconditioner's multigrid with level-0 rhs q (no mean
+// shift), from z = 0 (wall closure) or from the outflow line solve's extension (line closure).  Level 0 is re-pointed at (z, scratch, q) and restored afterwards; the cycle's
 // ping-pong may leave the result in either buffer, so z / scratch are swapped to match.
 int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch) {
     double* sv[3] = {s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP], s->arr[NS_ARR_RPHI]};
-    HIPCHK(hipMemsetAsync(z - (ptrdiff_t)nsg::HALO * s->g.ld, 0, s->plane * sizeof(double), s->st));
+    if (s->out_side >= 0) {
+        // the outflow side's data: its 1-D line solve (on the side's slab; summed over ranks so
+        // every slab has it), extended constantly along x as the cycle's initial iterate, and
+        // into the other ping-pong plane's ghost row beyond the side.  The cycle then works on
+        // the residual q - D z0, which is O(q), instead of on the O(ny^2 q) Dirichlet data
+        const bool mine = s->out_side == 0 ? s->g.i0 == 0 : s->g.i0 + s->g.nxl == s->g.nx;
+        const ptrdiff_t ld = s->g.ld;
+        const ptrdiff_t row = s->out_side == 0 ? 0 : s->g.nxl - 1, ghost = s->out_side == 0 ? -1 : s->g.nxl;
+        if (mine) {
+            if (nsg::launch_line_solve(q + row * ld, s->c, s->g.ny, s->lrow, s->st) != 0) {
+                set_err("outflow line solve: ny = %d exceeds its LDS capacity", s->g.ny);
+                return NS_EINVAL;
+            }
+        } else {
+            HIPCHK(hipMemsetAsync(s->lrow, 0, (size_t)s->g.ny * sizeof(double), s->st));
+        }
+        CHK(allreduce(s, s->lrow, s->g.ny, ncclSum));
+        nsg::launch_line_extend(s->lrow, s->g, z - (ptrdiff_t)nsg::HALO * ld, s->g.nxl + 2 * nsg::HALO,
+                                mine ? scratch + ghost * ld : nullptr, s->st);
+    } else {
+        HIPCHK(hipMemsetAsync(z - (ptrdiff_t)nsg::HALO * s->g.ld, 0, s->plane * sizeof(double), s->st));
+    }
     CHK(halo(s, {q}, 5));
     s->arr[NS_ARR_PHI] = z;
     s->arr[NS_ARR_TMP] = scratch;
@@ -1263,6 +1290,22 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
     L0.c = s->c;
     L0.hx = hx0;
     L0.hy = hy0;
+    // the outflow preconditioner's closure: the side's boundary weight 2/h^2 toward its ghost (face Dirichlet)
+    // (0 for a wall) in every level's tables; level 0 gets its own copy (the true operator's
+    // tables stay as they are)
+    auto close_side = [&](std::vector<double>& t, const std::vector<double>& hx) {
+        const size_t nx = hx.size();
+        if (s->out_side == 0) t[0] = 2.0 / (hx[0] * hx[0]);                        // pw[0]
+        if (s->out_side == 1) t[nx + nx - 1] = 2.0 / (hx[nx - 1] * hx[nx - 1]);   // pe[nx-1]
+    };
+    if (s->out_side >= 0) {
+        L0.g.dsx = s->out_side == 0 ? 1 : 2;   // inherited by every coarse level's Geo
+        std::vector<double> t = coef_tables(hx0, hy0, s->g.neu);
+        close_side(t, hx0);
+        HIPCHK(hipMalloc(&L0.coef, t.size() * sizeof(double)));
+        HIPCHK(hipMemcpy(L0.coef, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+        L0.c = coef_view(L0.coef, s->g.nx, s->g.ny);
+    }
     std::vector<int> ri0(s->nranks), rn(s->nranks);
     for (int q = 0; q < s->nranks; q++) {
         int32_t a, b;
@@ -1315,7 +1358,8 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
         C.hy.resize(gc.ny);
         for (int i = 0; i < gc.nx; i++) C.hx[i] = F.hx[2 * i] + F.hx[2 * i + 1];
         for (int j = 0; j < gc.ny; j++) C.hy[j] = F.hy[2 * j] + F.hy[2 * j + 1];
-        const std::vector<double> t = coef_tables(C.hx, C.hy);
+        std::vector<double> t = coef_tables(C.hx, C.hy);
+        if (s->out_side >= 0) close_side(t, C.hx);
         HIPCHK(hipMalloc(&C.coef, t.size() * sizeof(double)));
         HIPCHK(hipMemcpy(C.coef, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
         C.c = coef_view(C.coef, gc.nx, gc.ny);
@@ -1820,6 +1864,12 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     // multigrid (a fictitious-domain preconditioner: the rhs is 0 outside the domain, the
     // outside values of the result are ignored by the masked operator), unless
     if (s->poisson == NS_POISSON_MG) {
+        // one NEUMANN side, W or E (a grid row: one slab's, contiguous) of a rectangle: the
+        // line-solve preconditioner (NSGPU_OUTFLOW_PC=wall: the round-1 wall closure, A/B)
+        const int nneu = g.neu[0] + g.neu[1] + g.neu[2] + g.neu[3];
+        const char* ope = getenv("NSGPU_OUTFLOW_PC");
+        if (!masked && nneu == 1 && (g.neu[0] || g.neu[1]) && g.ny <= 4096 && !(ope && !std::strcmp(ope, "wall")))
+            s->out_side = g.neu[0] ? 0 : 1;
         if (p->mg_pre > 0) s->mg_pre = p->mg_pre;
         if (p->mg_omega > 0) s->mg_omega_s = p->mg_omega;
         if (const char* e = getenv("NSGPU_MG_OMEGA")) s->mg_omega_s = std::atof(e);   // smoother over-relaxation (A/B)
@@ -1841,9 +1891,11 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         // BiCGStab planes (outflow rectangle: the preconditioner is the hierarchy above -- with a
         // single level its coarse relaxation, 2n+10 SOR sweeps from zero; masked domain: Jacobi)
         const size_t nk = sizeof(s->kv) / sizeof(s->kv[0]);
-        if (hipMalloc(&s->kv_mem, nk * s->plane * sizeof(double)) != hipSuccess) { set_err("hipMalloc Krylov planes failed"); return fail(NS_ENOMEM); }
-        if (hipMemsetAsync(s->kv_mem, 0, nk * s->plane * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
+        const size_t kn = nk * s->plane + g.ld;
+        if (hipMalloc(&s->kv_mem, kn * sizeof(double)) != hipSuccess) { set_err("hipMalloc Krylov planes failed"); return fail(NS_ENOMEM); }
+        if (hipMemsetAsync(s->kv_mem, 0, kn * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
         for (size_t k = 0; k < nk; k++) s->kv[k] = s->kv_mem + k * s->plane + (size_t)nsg::HALO * g.ld;
+        s->lrow = s->kv_mem + nk * s->plane;
         if (hipMalloc(&s->ksc, nsg::KS_NUM * sizeof(double)) != hipSuccess) { set_err("hipMalloc failed"); return fail(NS_ENOMEM); }
         if (hipMemsetAsync(s->ksc, 0, nsg::KS_NUM * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     }
@@ -1881,8 +1933,8 @@ void ns_destroy(ns_solver* s) {
     if (s->mm_host) (void)hipHostFree(s->mm_host);
     for (auto e : s->ev) (void)hipEventDestroy(e);
     for (auto e : s->hev) (void)hipEventDestroy(e);
-    for (size_t l = 1; l < s->lv.size(); l++) {
-        if (s->lv[l].mem) (void)hipFree(s->lv[l].mem);
+    for (size_t l = 0; l < s->lv.size(); l++) {
+        if (l > 0 && s->lv[l].mem) (void)hipFree(s->lv[l].mem);
         if (s->lv[l].coef) (void)hipFree(s->lv[l].coef);
     }
     if (s->base) (void)hipFree(s->base);

@@ -617,3 +617,52 @@ def test_speculative_correction_is_bit_identical(gpu, monkeypatch, n):
     assert ma == mb and la == lb
     for x, y in zip(fa, fb):
         assert np.array_equal(x, y)
+
+
+BC_OUT_W = [(4, 0.0), (2, 0.0), (0, -1.0), (2, 0.0)]     # inflow from E, NEUMANN outflow W
+
+
+@pytest.mark.parametrize("nx,ny,bc,xr,yr", [(256, 64, BC_CHANNEL, -1, -1), (128, 96, BC_OUT_W, -1, -1),
+                                            (512, 128, BC_CHANNEL, -1, -1), (160, 48, BC_CHANNEL, 1.01, 0.98),
+                                            (96, 40, BC_OUT_W, 0.99, -1)])
+def test_outflow_line_preconditioner(gpu, monkeypatch, nx, ny, bc, xr, yr):
+    """A W or E NEUMANN outflow side (FluidSolver.cpp:98-101): the Poisson BiCGStab is
+    preconditioned by the outflow side's 1-D line solve (the linear-extrapolation closure's
+    decoupled column), extended along x as the initial iterate of a V-cycle whose hierarchy closes
+    that side by face-Dirichlet data.  From a random rhs on these anisotropic /
+    graded grids it reaches the oracle's direct solve of the same mean-projected system (1e-8
+    relative, phi modulo its mean) in fewer iterations than the round-1 wall-closure V-cycle
+    (NSGPU_OUTFLOW_PC=wall) and in at most 25 (square cells: test_outflow_channel_steps)."""
+    rng = np.random.default_rng(12)
+    its = {}
+    for pc in ("line", "wall"):
+        monkeypatch.setenv("NSGPU_OUTFLOW_PC", pc)
+        og, gs = pair(gpu, nx, ny, 1.0 / 256, 100.0, bc, xr, yr, rtol=1e-8)
+        b = rand(rng, nx * ny, 100.0)
+        gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny)); gs.set(gpu.NS_ARR_RPHI, b)
+        n, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+        its[pc] = n
+        assert res <= 1e-8, (pc, n, res)
+        if pc == "line":
+            xp, _ = og.solve_poisson(b)
+            g = gs.get(gpu.NS_ARR_PHI).ravel()
+            err = float(rel(g - g.mean(), xp - xp.mean()))
+            assert err <= 1e-6, (err, n)
+        gs.close()
+    assert its["line"] <= 25, its
+    assert its["line"] < its["wall"], its
+
+
+@pytest.mark.parametrize("nx,ny", [(1024, 256), (2048, 512)])
+def test_outflow_channel_steps(gpu, nx, ny):
+    """The channel of tools/bench_bcs.py (square cells, inlet W, NEUMANN outflow E, Re 1000) from
+    rest: the line-closure preconditioner holds the Poisson BiCGStab to <= 8 iterations per step
+    on average (VERDICT r1's target; the wall closure needs 30-60 here), every solve converged."""
+    h = 4.0 / nx
+    g = gpu.rectangle(nx, ny, lx=4.0, ly=ny * h, bc=BC_CHANNEL)
+    gs = gpu.GpuSolver(g, h / 8, 1000.0)
+    st = [gs.step() for _ in range(8)]
+    gs.close()
+    its = [x["it_phi"] for x in st]
+    assert np.mean(its) <= 8.0 and max(its) <= 10, its
+    assert max(x["res_phi"] for x in st) <= 1e-8
