@@ -2862,7 +2862,9 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
     if (a.ntl < 0) a.ntl = 1;
     a.nsj = (g.ny + SW2X - 1) / SW2X;
     int nblk = 0;
-    const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 4, &nblk);
+    // overlap depth 5, not the 4 of its fine-row cone: fine row 0 (even) reads coarse row -1,
+    // whose exchange runs concurrently with the interior strips
+    const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 5, &nblk);
     if (nblk) NS_LAUNCH((k_sweep2<0, false, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }

@@ -233,8 +233,11 @@ int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs = null
     if (!comm_on(s)) return 0;
     s->n_xchg++;
     const bool lo = s->rank > 0 || s->nranks == 1, hi = s->rank < s->nranks - 1 || s->nranks == 1;
-    // (loopback: the 1-rank communicator's only rank, 0, is every peer)
+    // (loopback: the 1-rank communicator's only rank, 0, is every peer; a one-rank loopback sends
+    // its physical ghost rows round trip unchanged -- they may hold boundary data, e.g. the
+    // outflow preconditioner's)
     const int p_lo = s->loopback ? 0 : s->rank - 1, p_hi = s->loopback ? 0 : s->rank + 1;
+    const bool self = s->nranks == 1;
     if (s->ht.exchange) {
         for (int k = 0; k < nreq; k++) {
             const HaloReq& q = reqs[k];
@@ -243,8 +246,9 @@ int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs = null
             double* f = q.f;
             CHK(ensure_stage(s, 4 * cnt));
             double *slo = s->stage, *shi = slo + cnt, *rlo = shi + cnt, *rhi = rlo + cnt;
-            if (lo) HIPCHK(hipMemcpyAsync(slo, f, cnt * 8, hipMemcpyDeviceToHost, xs));
-            if (hi) HIPCHK(hipMemcpyAsync(shi, f + (ptrdiff_t)(nxl - q.w) * ld, cnt * 8, hipMemcpyDeviceToHost, xs));
+            const double *flo = self ? f - (ptrdiff_t)q.w * ld : f, *fhi = f + (ptrdiff_t)(self ? nxl : nxl - q.w) * ld;
+            if (lo) HIPCHK(hipMemcpyAsync(slo, flo, cnt * 8, hipMemcpyDeviceToHost, xs));
+            if (hi) HIPCHK(hipMemcpyAsync(shi, fhi, cnt * 8, hipMemcpyDeviceToHost, xs));
             HIPCHK(hipStreamSynchronize(xs));
             if (s->ht.exchange(s->ht.user, lo ? slo : nullptr, hi ? shi : nullptr, lo ? rlo : nullptr,
                                hi ? rhi : nullptr, (int64_t)cnt) != 0) {
@@ -263,12 +267,13 @@ int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs = null
         const size_t cnt = (size_t)q.w * q.g->ld;
         const int ld = q.g->ld, nxl = q.g->nxl;
         double* f = q.f;
+        const double *flo = self ? f - (ptrdiff_t)q.w * ld : f, *fhi = f + (ptrdiff_t)(self ? nxl : nxl - q.w) * ld;
         if (lo) {
-            NCCLCHK(ncclSend(f, cnt, ncclDouble, p_lo, s->comm, xs));
+            NCCLCHK(ncclSend(flo, cnt, ncclDouble, p_lo, s->comm, xs));
             NCCLCHK(ncclRecv(f - (ptrdiff_t)q.w * ld, cnt, ncclDouble, p_lo, s->comm, xs));
         }
         if (hi) {
-            NCCLCHK(ncclSend(f + (ptrdiff_t)(nxl - q.w) * ld, cnt, ncclDouble, p_hi, s->comm, xs));
+            NCCLCHK(ncclSend(fhi, cnt, ncclDouble, p_hi, s->comm, xs));
             NCCLCHK(ncclRecv(f + (ptrdiff_t)nxl * ld, cnt, ncclDouble, p_hi, s->comm, xs));
         }
     }
