@@ -10,6 +10,12 @@ dt = 1/(8n)), inputs resident in HBM.  N > 1: x-slabs, one rank per GPU, RCCL ha
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--re 1000] [--no-cpu]
   (N > 1 under torch.distributed.run; RANK / WORLD_SIZE / LOCAL_RANK from the env)
+
+--case channel (not the headline line): the n x n/4
+channel (square cells h = 4/n, inlet W, walls S / N, the reference's NEUMANN outflow E,
+Re 1000, dt = h/8) -- Helmholtz RB-SOR as above, Poisson by BiCGStab on the true outflow
+operator preconditioned by the line-closure V-cycle; `roofline` from the same HIP-event
+timing (the preconditioner's level-0 FUSE_R / FUSE_P passes and the Helmholtz passes).
 """
 from __future__ import annotations
 
@@ -51,6 +57,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--case", choices=("cavity", "channel"), default="cavity")
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -140,9 +147,16 @@ def main():
         nccl_id = make_nccl_id(dist)
 
     n, re = args.n, args.re
-    dt = 1.0 / (8 * n)
+    channel = args.case == "channel"
+    if channel:
+        nyc, h = n // 4, 4.0 / n
+        dt = h / 8
+        grid = nsa.rectangle(n, nyc, lx=4.0, ly=nyc * h, bc=[(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0)])
+    else:
+        nyc, dt = n, 1.0 / (8 * n)
+        grid = nsa.cavity(n)
     torch.cuda.set_device(local)
-    solver = nsa.GpuSolver(nsa.cavity(n), dt, re, rtol=args.rtol, device=local, timing=True,
+    solver = nsa.GpuSolver(grid, dt, re, rtol=args.rtol, device=local, timing=True,
                            rank=rank, nranks=world, nccl_id=nccl_id)
 
     def barrier():
@@ -177,10 +191,10 @@ def main():
     K = args.steps
     timed_steps = K if args.time_every == 1 else (sum(1 for k in range(K) if k % args.time_every == 0)
                                                    if args.time_every > 0 else 0)
-    cells = n * n
+    cells = n * nyc
     cycles = sum(s["it_phi"] for s in stats)
     hsweeps = sum(s["it_u"] for s in stats)
-    local_cells = (solver.i1 - solver.i0) * n
+    local_cells = (solver.i1 - solver.i0) * nyc
     timed = {"prolong": (sum(s["t_poisson_kernel_ms"] for s in stats), sum(s["n_poisson_kernels"] for s in stats)),
              "restrict": (sum(s["t_restrict_kernel_ms"] for s in stats), sum(s["n_restrict_kernels"] for s in stats)),
              "helmholtz": (sum(s["t_helm_kernel_ms"] for s in stats), sum(s["n_helm_kernels"] for s in stats))}
@@ -192,12 +206,18 @@ def main():
     # level, x 4/3 for the coarser levels (each a quarter of the one above)
     step_bpc = (64 + 24 + 40 + 32 + 24 * hsweeps / K
                 + (28 * (cycles + K) + 26 * cycles) / K * 4.0 / 3.0)
+    if channel:
+        # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications
+        # of (line extension 8 + FUSE_R 28 + FUSE_P 26, x 4/3 for the coarser levels) = 80 each,
+        # two operator applications 24 + 16, KV_V 32, KV_T 24, KV_X 64 = 352; start-up (apply +
+        # KV_INIT) 64; no phi extrapolation
+        step_bpc = 64 + 24 + 40 + 64 + 24 * hsweeps / K + 352 * cycles / K
     value = cells * K / elapsed / 1e6
 
     # the north star's roofline kernel: one Jacobi sweep of this rank's slab (random phi, b;
     # 10 warm-up + 50 timed launches, HIP events), single rank only
     jacobi = jacobi32 = None
-    if world == 1:
+    if world == 1 and not channel:
         js = nsa.GpuSolver(nsa.cavity(n), dt, re, poisson=nsa.NS_POISSON_JACOBI, omega=1.0, device=local)
         js.fill_random(0x5EED)
         t = js.time_poisson(10, 50)
@@ -215,7 +235,7 @@ def main():
     if os.path.exists(prof):
         try:
             d = json.load(open(prof))
-            if d.get("n") == n:
+            if d.get("n") == n and not channel:
                 traffic = {k: v.get("kernel_bytes_per_launch") for k, v in d.get("kernels", {}).items()}
         except Exception:
             traffic = {}
@@ -247,13 +267,16 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (lid-driven cavity from rest, no input files)",
-        "config": {"workload": f"{n}x{n} lid-driven cavity, Re={re:g}, dt=1/{8 * n}, fp64, multigrid Poisson "
-                               f"(RB-GS smoother) + RB-SOR Helmholtz, both to rtol {args.rtol:g}",
-                   "nx": n, "ny": n, "re": re, "dt": dt, "parallelism": f"x-slab x{world}",
+        "config": {"workload": (f"{n}x{nyc} channel (inlet W, NEUMANN outflow E), Re={re:g}, dt=h/8, fp64, "
+                                f"BiCGStab Poisson with the line-closure V-cycle preconditioner + RB-SOR Helmholtz, "
+                                f"both to rtol {args.rtol:g}") if channel else
+                               (f"{n}x{n} lid-driven cavity, Re={re:g}, dt=1/{8 * n}, fp64, multigrid Poisson "
+                                f"(RB-GS smoother) + RB-SOR Helmholtz, both to rtol {args.rtol:g}"),
+                   "case": args.case, "nx": n, "ny": nyc, "re": re, "dt": dt, "parallelism": f"x-slab x{world}",
                    "step_api": "ns_step" if args.sync_monitor else "ns_step_async"},
         "monitor_last_step": {k: last_monitor[k] for k in ("umin", "umax", "vmin", "vmax")},
-        "poisson_vcycles_per_s": cycles / elapsed,
-        "poisson_vcycles_per_step": cycles / K,
+        ("poisson_bicgstab_its_per_s" if channel else "poisson_vcycles_per_s"): cycles / elapsed,
+        ("poisson_bicgstab_its_per_step" if channel else "poisson_vcycles_per_step"): cycles / K,
         "poisson_fine_sweeps_per_s": fine_sweeps / elapsed,
         "poisson_fine_sweeps_per_step": fine_sweeps / K,
         "helmholtz_sweeps_per_step": hsweeps / K,
@@ -271,7 +294,11 @@ def main():
     if jacobi32 is not None:
         line["kernels"]["jacobi_sweep_fp32"] = roof("jacobi_sweep_fp32", JACOBI32_LABEL, SWEEP32_BYTES_PER_CELL,
                                                     jacobi32, 50)
-    if world == 1 and not args.no_cpu:
+    if channel:
+        line["data"] = "synthetic (channel from rest, uniform inlet, no input files)"
+        for k in ("poisson_fine_sweeps_per_s", "poisson_fine_sweeps_per_step"):
+            line.pop(k)
+    if world == 1 and not args.no_cpu and not channel:
         try:
             state = {k: solver.get(a).ravel() for k, a in (("u", nsa.NS_ARR_U), ("v", nsa.NS_ARR_V),
                                                            ("phi", nsa.NS_ARR_PHI), ("cu", nsa.NS_ARR_CU),

@@ -160,7 +160,8 @@ struct ns_solver {
     double* kv_mem = nullptr;
     double* lrow = nullptr;      // outflow preconditioner: its line solution (one row, in kv_mem)
     double* ksc = nullptr;
-    bool pc_active = false;      // inside mg_precond: level 0 has no mean shift, no timing
+    bool pc_active = false;      // inside mg_precond: level 0 has no mean shift
+    bool pc_timing = false;      // ... and its level-0 passes are timed (the outflow Poisson solve)
     bool krylov_mg = false;      // the Poisson BiCGStab is preconditioned by a V-cycle (else Jacobi)
     // the outflow preconditioner: a rectangle whose only NEUMANN side is W (0) or
     // E (1): the V-cycle's hierarchy closes that side with a Dirichlet-centre ghost whose data,
@@ -571,6 +572,7 @@ struct KrylovSolve {
     const double* shift;
     double b2;
     const char* name;
+    ns_stats* stt = nullptr;   // the Poisson solve's: its preconditioner's level-0 passes are timed
 };
 
 int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res);
@@ -838,7 +840,7 @@ int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
     for (int k = 0; k < n;) {
         const int w = (n - k >= 2 && pair_level(s, l)) ? 2 : 1;   // two sweeps per HBM pass
         CHK(halo_l(s, l, {L.phi}, 2 * w));
-        const bool t = s->timing && l == 0 && !s->pc_active;
+        const bool t = s->timing && l == 0 && (!s->pc_active || s->pc_timing);
         if (t) { CHK(t_begin(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); s->evtag[ev0 + *tn] = 0; }
         const double* sh = l == 0 ? shift0(s) : nullptr;
         if (w == 2) nsg::launch_pois_rbsor2(L.g, L.c, s->mg_omega_s, L.phi, L.tmp, L.b, sh, nullptr, s->st);
@@ -889,7 +891,7 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
         if (fused_restrict(s, l)) {
             // last two pre-smoothing sweeps + residual + restriction in one HBM pass
             CHK(mg_smooth(s, l, s->mg_pre - 2, tn, ev0));
-            const bool t = s->timing && l == 0 && !s->pc_active;
+            const bool t = s->timing && l == 0 && (!s->pc_active || s->pc_timing);
             if (t) { CHK(t_begin(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); s->evtag[ev0 + *tn] = 1; }
             if (tile_level(s, l)) {
                 CHK(flush_b(s, l));
@@ -937,7 +939,7 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
         if (fused_prolong(s, l)) {
             // prolongation + the first two post-smoothing sweeps in one HBM pass; the coarse
             // and fine ghost rows travel in one group
-            const bool t = s->timing && l == 0 && !s->pc_active;
+            const bool t = s->timing && l == 0 && (!s->pc_active || s->pc_timing);
             const double* shp = l == 0 ? shift0(s) : nullptr;
             auto pass = [&]() {
                 return (tile_level(s, l) ? nsg::launch_pois_tile2_prolong : nsg::launch_pois_rbsor2_prolong)(
@@ -1086,7 +1088,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
 // z = M^-1 q: one V-cycle of the preconditioner's multigrid with level-0 rhs q (no mean
 // shift), from z = 0 (wall closure) or from the outflow line solve's extension (line closure).  Level 0 is re-pointed at (z, scratch, q) and restored afterwards; the cycle's
 // ping-pong may leave the result in either buffer, so z / scratch are swapped to match.
-int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch) {
+int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch, int* tn = nullptr) {
     double* sv[3] = {s->arr[NS_ARR_PHI], s->arr[NS_ARR_TMP], s->arr[NS_ARR_RPHI]};
     if (s->out_side >= 0) {
         // the outflow side's data: its 1-D line solve (on the side's slab; summed over ranks so
@@ -1115,10 +1117,13 @@ int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch) {
     s->arr[NS_ARR_TMP] = scratch;
     s->arr[NS_ARR_RPHI] = q;
     s->pc_active = true;
-    int tn = 0;
+    s->pc_timing = tn != nullptr;
+    int tn0 = 0;
+    if (tn) CHK(ensure_events(s, 2 * ((size_t)*tn + 2 * (s->mg_pre + s->mg_post) + 4)));
     bool done = false;
-    const int rc = mg_vcycle(s, &tn, 0, [](int) { return 0; }, &done);
+    const int rc = mg_vcycle(s, tn ? tn : &tn0, 0, [](int) { return 0; }, &done);
     s->pc_active = false;
+    s->pc_timing = false;
     // (level 0's own pointer: a single-level hierarchy relaxes it in mg_coarse, which does not
     // track the swaps in s->arr)
     if (s->lv[0].phi != z) std::swap(z, scratch);
@@ -1159,8 +1164,11 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
         const int nb = nsg::launch_apply(ks.op, s->g, s->c, ks.alpha, x, y, q, s->part, s->st);
         return reduce(nb, 2);
     };
+    // timed level-0 passes of the preconditioner (events 0 .. tn), read after each host sync
+    int tn = 0;
+    const bool timed = s->timing && ks.stt && ks.mg;
     auto precond = [&](double* q, int k) -> int {   // K[k] = M^-1 q
-        if (ks.mg) return mg_precond(s, q, s->kv[k], s->kv[8]);
+        if (ks.mg) return mg_precond(s, q, s->kv[k], s->kv[8], timed ? &tn : nullptr);
         nsg::launch_diag_pc(ks.op, s->g, s->c, ks.alpha, q, s->kv[k], s->st);
         return 0;
     };
@@ -1180,6 +1188,13 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
         HIPCHK(hipMemcpyAsync(s->scal + S_AUX + 1, s->ksc + nsg::KS_BRK, sizeof(double), hipMemcpyDeviceToDevice, s->st));
         if (s->verbose) HIPCHK(hipMemcpyAsync(s->scal + S_AUX + 2, s->ksc + nsg::KS_ALPHA, 2 * sizeof(double), hipMemcpyDeviceToDevice, s->st));
         CHK(fetch(s));
+        for (int k = 0; k < tn; k++) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
+            if (s->evtag[k]) { ks.stt->t_restrict_kernel_ms += ms; ks.stt->n_restrict_kernels++; }
+            else { ks.stt->t_poisson_kernel_ms += ms; ks.stt->n_poisson_kernels++; }
+        }
+        tn = 0;
         const double r2 = s->hs[S_AUX], b2 = ks.b2;
         *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
         if (s->verbose)
@@ -1220,7 +1235,7 @@ int pois_solve_any(ns_solver* s, int* its, double* res, ns_stats* stt) {
     if (s->kv[0]) {
         CHK(fetch(s));   // ||b - mean||^2 for the relative test
         const KrylovSolve ks{0, 0.0, s->krylov_mg, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI],
-                             s->scal + (s->consist ? S_KSHIFT : S_SHIFT), s->hs[S_SHIFT + 1], "poisson"};
+                             s->scal + (s->consist ? S_KSHIFT : S_SHIFT), s->hs[S_SHIFT + 1], "poisson", stt};
         const int rc = bicgstab(s, ks, its, res);
         if (stt) stt->n_checks += *its + 1;
         return rc;
