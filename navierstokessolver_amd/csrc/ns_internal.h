@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <vector>
 
 namespace nsg {
 
@@ -175,8 +176,12 @@ int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const d
 
 // coarse levels as one LDS-resident V-cycle (single rank): level g and its 2x coarsenings
 size_t coarse_vcycle_bytes(const Geo& g);
-int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double* b, int cycles, int pre, int post,
-                         int citers, double comega, double somega, int dlo, int dhi, hipStream_t st);
+// the host-built LDS image of the coarse V-cycle (every level's tables + the direct last-level
+// solve's matrix; dn = its size, 0 = RB-SOR sweeps); its size in doubles or < 0
+int cv_image(const double* hx, const double* hy, int nx, int ny, int dlo, int dhi, std::vector<double>& img, int* dn);
+int launch_coarse_vcycle(const Geo& g, const double* img, int img_n, int dn, double* phi, const double* b, int cycles,
+                         int pre, int post, int citers, double comega, double somega, int dlo, int dhi,
+                         hipStream_t st);
 // the outflow side's 1-D line solve of the Poisson preconditioner into the row p (ny <= 4096;
 // -1 otherwise), and its constant extension along x over `rows` rows of the plane z (from its
 // first halo row) and the single row zg (if not null)

@@ -17,6 +17,7 @@
 #include "ns_internal.h"
 #include <hip/hip_ext.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1788,9 +1789,10 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) { sweep2_body<OP, 
 //                    correction first -- k_sweep2<FUSE_P>'s pass.
 // Same arithmetic as k_sweep2 (relax<0>, the Newton reciprocal of the diagonal, the
 // restriction's summation order), so the two are interchangeable level by level.
-constexpr int TT = 32;
-
-template <int FUSE>
+// TT = 32, or 16 on the levels that would have fewer than 512 tiles of 32 (<= 512^2): four
+// times the workgroups and a quarter of the work per half-sweep -- these levels are latency-bound,
+// so the larger cone overhead costs nothing (8 -> ~? us per pass at 128^2 .. 512^2)
+template <int FUSE, int TT>
 __global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
     constexpr bool XR = FUSE == FUSE_R, XP = FUSE == FUSE_P;
     constexpr int R = XR ? 5 : 4;
@@ -1930,7 +1932,7 @@ __global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
         // one coarse cell per thread: k_restrict's area-weighted sum, same order
         const int Ic = threadIdx.x / (TT / 2), Jc = threadIdx.x - Ic * (TT / 2);
         const int li = li0 + 2 * Ic, j = j0 + 2 * Jc;
-        if (li < a.nxl && j < ny) {
+        if ((int)threadIdx.x < (TT / 2) * (TT / 2) && li < a.nxl && j < ny) {
             const int r = R + 2 * Ic, cc = R + 2 * Jc;
             double xs = (rw[r][3] * cl[cc][3]) * sb[r][cc];
             xs = xs + (rw[r][3] * cl[cc + 1][3]) * sb[r][cc + 1];
@@ -2024,6 +2026,18 @@ __global__ __launch_bounds__(256) void k_prolong(Geo gf, double* __restrict__ ph
 // that are pure launch latency at these sizes.  Single rank (the level is whole).
 constexpr int LV_MAX = 8;
 constexpr int CV_THREADS = 1024;
+
+// diagnostic build (CV_DIAG=1, tools/cv_diag.py): thread 0 stamps the 100 MHz wall clock at the
+// phase boundaries of the last launch into g_cv_t (vector stores), read back by nsg_cv_diag
+#ifndef CV_DIAG
+#define CV_DIAG 0
+#endif
+#if CV_DIAG
+__device__ unsigned long long g_cv_t[64];
+#define CV_STAMP(k) do { if (threadIdx.x == 0) g_cv_t[k] = wall_clock64(); } while (0)
+#else
+#define CV_STAMP(k) do { } while (0)
+#endif
 
 struct LdsLv {
     int nx, ny, phi, b, idg, cw, ce, cs, cn, hx, hy;  // offsets in doubles
@@ -2127,59 +2141,64 @@ __host__ __device__ inline int lv_layout(int nx, int ny, LdsLv* lv, int* nlev) {
     return off;
 }
 
-__global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, double* __restrict__ phi,
+// the last LDS level is solved directly when it has <= CV_DIRECT cells: x = M b with M the
+// inverse of its operator (a Dirichlet-closed side) or, pure Neumann, the n x n block of the
+// inverse of the bordered system [A 1; w^T 0] (w = cell areas, the left null vector): A x =
+// b - (w.b / w.1) and w.x = 0 -- what the 2n+10 RB-SOR sweeps of the old last-level solve
+// converged to up to a constant, in one LDS phase instead of 4n+20 (cv_image builds M)
+constexpr int CV_DIRECT = 64;
+
+// the LDS image's size in doubles (levels, then M if the last level is solved directly) and
+// the direct solve's size dn (0: RB-SOR sweeps)
+__host__ __device__ inline int cv_image_size(int nx, int ny, int* dn) {
+    LdsLv lv[LV_MAX];
+    int nl = 0;
+    const int off = lv_layout(nx, ny, lv, &nl);
+    const int n = lv[nl - 1].nx * lv[nl - 1].ny;
+    *dn = n <= CV_DIRECT ? n : 0;
+    return off + *dn * *dn;
+}
+
+// img: the host-built LDS image (cv_image) of every level's tables (idg, cw, ce, hx, cs, cn,
+// hy; phi and b zero) and M; one copy into LDS replaces ~3 barriers of table arithmetic per
+// level.  Level 0's phi and b come from the global coarsest level.
+__global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const double* __restrict__ img, int img_n,
+                                                              int dn, double* __restrict__ phi,
                                                               const double* __restrict__ b, int cycles, int pre,
                                                               int post, int citers, double comega, double somega,
                                                               int dlo, int dhi) {
     extern __shared__ __attribute__((aligned(16))) double L[];
     __shared__ LdsLv lv[LV_MAX];
     __shared__ int nlev;
+    CV_STAMP(0);
     if (threadIdx.x == 0) {
         lv_layout(g.nx, g.ny, lv, &nlev);
         for (int k = 0; k < nlev; k++) { lv[k].dlo = dlo; lv[k].dhi = dhi; }
     }
-    __syncthreads();
-    const int nl = nlev;
-    // level 0: the global coarsest level's phi, b and spacings
     {
-        const LdsLv v = lv[0];
-        for (int t = threadIdx.x; t < v.nx * v.ny; t += CV_THREADS) {
+        // the image from level 0's idg on (16 B per lane; the offsets are even), then level 0's
+        // phi and b from the global level
+        const int n0 = g.nx * g.ny, from = 2 * n0;
+        const double2* src = reinterpret_cast<const double2*>(img + from);
+        double2* dst = reinterpret_cast<double2*>(L + from);
+        const int n2 = (img_n - from) >> 1;
+#pragma unroll 8
+        for (int t = threadIdx.x; t < n2; t += CV_THREADS) dst[t] = src[t];
+        if (((img_n - from) & 1) && threadIdx.x == 0) L[img_n - 1] = img[img_n - 1];
+        LdsLv v;
+        v.ny = g.ny;
+        v.rny = 1.0f / (float)g.ny;
+        for (int t = threadIdx.x; t < n0; t += CV_THREADS) {
             int i, j;
             lv_split(v, t, i, j);
-            L[v.phi + t] = ldf(phi, g.ld, i, j);
-            L[v.b + t] = ldf(b, g.ld, i, j);
-        }
-        for (int t = threadIdx.x; t < v.nx; t += CV_THREADS) L[v.hx + t] = c.hx[t];
-        for (int t = threadIdx.x; t < v.ny; t += CV_THREADS) L[v.hy + t] = c.hy[t];
-    }
-    __syncthreads();
-    // coarser spacings (sums of children), every level's ConstructLHS weights and 1/diag
-    for (int k = 0; k < nl; k++) {
-        const LdsLv v = lv[k];
-        if (k > 0) {
-            const LdsLv f = lv[k - 1];
-            for (int t = threadIdx.x; t < v.nx; t += CV_THREADS) L[v.hx + t] = L[f.hx + 2 * t] + L[f.hx + 2 * t + 1];
-            for (int t = threadIdx.x; t < v.ny; t += CV_THREADS) L[v.hy + t] = L[f.hy + 2 * t] + L[f.hy + 2 * t + 1];
-            __syncthreads();
-        }
-        for (int t = threadIdx.x; t < v.nx; t += CV_THREADS) {
-            const double h = L[v.hx + t];
-            L[v.cw + t] = t > 0 ? 2.0 / (h * (h + L[v.hx + t - 1])) : (dlo ? 2.0 / (h * h) : 0.0);
-            L[v.ce + t] = t < v.nx - 1 ? 2.0 / (h * (h + L[v.hx + t + 1])) : (dhi ? 2.0 / (h * h) : 0.0);
-        }
-        for (int t = threadIdx.x; t < v.ny; t += CV_THREADS) {
-            const double h = L[v.hy + t];
-            L[v.cs + t] = t > 0 ? 2.0 / (h * (h + L[v.hy + t - 1])) : 0.0;
-            L[v.cn + t] = t < v.ny - 1 ? 2.0 / (h * (h + L[v.hy + t + 1])) : 0.0;
-        }
-        __syncthreads();
-        for (int t = threadIdx.x; t < v.nx * v.ny; t += CV_THREADS) {
-            int i, j;
-            lv_split(v, t, i, j);
-            L[v.idg + t] = -1.0 / ((L[v.cw + i] + L[v.ce + i]) + (L[v.cs + j] + L[v.cn + j]));
+            L[t] = ldf(phi, g.ld, i, j);
+            L[n0 + t] = ldf(b, g.ld, i, j);
         }
     }
     __syncthreads();
+    CV_STAMP(1);
+    const int nl = nlev;
+    CV_STAMP(2);
     for (int cyc = 0; cyc < cycles; cyc++) {
         for (int k = 0; k < nl - 1; k++) {
             const LdsLv f = lv[k], v = lv[k + 1];
@@ -2200,8 +2219,22 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, dou
                 L[v.phi + t] = 0.0;
             }
             __syncthreads();
+            if (cyc == 0) CV_STAMP(3 + k);
         }
-        lv_rb_last(L, lv[nl - 1], comega, citers);
+        if (dn > 0) {
+            // x = M b (M after the levels in the image)
+            const LdsLv v = lv[nl - 1];
+            if ((int)threadIdx.x < dn) {
+                const double* M = L + (img_n - dn * dn) + threadIdx.x * dn;
+                double x = 0.0;
+                for (int k = 0; k < dn; k++) x += M[k] * L[v.b + k];
+                L[v.phi + threadIdx.x] = x;
+            }
+            __syncthreads();
+        } else {
+            lv_rb_last(L, lv[nl - 1], comega, citers);
+        }
+        if (cyc == 0) CV_STAMP(12);
         for (int k = nl - 2; k >= 0; k--) {
             const LdsLv f = lv[k], v = lv[k + 1];
             for (int t = threadIdx.x; t < f.nx * f.ny; t += CV_THREADS) {
@@ -2221,6 +2254,7 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, dou
             }
             __syncthreads();
             lv_rb(L, f, somega, post);
+            if (cyc == 0) CV_STAMP(13 + k);
         }
     }
     {
@@ -2231,7 +2265,15 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, Coef c, dou
             phi[(ptrdiff_t)i * g.ld + j] = L[v.phi + t];
         }
     }
+    CV_STAMP(21);
 }
+
+#if CV_DIAG
+// the last k_coarse_vcycle launch's stamps (diagnostic builds only)
+extern "C" int nsg_cv_diag(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cv_t), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // ---------------------------------------------------------------- reductions
 __global__ __launch_bounds__(1024) void k_reduce_sum(const double* __restrict__ p, int n, int nv,
@@ -2870,14 +2912,24 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
 }
 
 // the LDS-tiled versions of the two launchers above (small levels); TT x TT tiles
+template <int FUSE>
+static int launch_tile2(const StreamArgs& a, const Geo& g, hipStream_t st) {
+    const int tj32 = (g.ny + 31) / 32, n32 = tj32 * ((g.nxl + 31) / 32);
+    if (n32 >= (getenv("NSGPU_TILE32_MIN") ? atoi(getenv("NSGPU_TILE32_MIN")) : 512)) {
+        NS_LAUNCH((k_tile2<FUSE, 32>), dim3(n32), dim3(256), 0, st, a, tj32);
+        return n32;
+    }
+    const int tj = (g.ny + 15) / 16, n = tj * ((g.nxl + 15) / 16);
+    NS_LAUNCH((k_tile2<FUSE, 16>), dim3(n), dim3(256), 0, st, a, tj);
+    return n;
+}
+
 int launch_pois_tile2_restrict(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                                const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
                                double* part, hipStream_t st) {
     StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
     a.hx = c.hx; a.hy = c.hy; a.bc = bc; a.pc = pc; a.ldc = gc.ld;
-    const int tj = (g.ny + TT - 1) / TT, ntiles = tj * ((g.nxl + TT - 1) / TT);
-    NS_LAUNCH(k_tile2<FUSE_R>, dim3(ntiles), dim3(256), 0, st, a, tj);
-    return ntiles;
+    return launch_tile2<FUSE_R>(a, g, st);
 }
 
 int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
@@ -2885,9 +2937,7 @@ int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const d
                               hipStream_t st) {
     StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, nullptr, false);
     a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0; a.dsx = gc.dsx;
-    const int tj = (g.ny + TT - 1) / TT, ntiles = tj * ((g.nxl + TT - 1) / TT);
-    NS_LAUNCH(k_tile2<FUSE_P>, dim3(ntiles), dim3(256), 0, st, a, tj);
-    return ntiles;
+    return launch_tile2<FUSE_P>(a, g, st);
 }
 
 int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
@@ -3023,19 +3073,111 @@ void launch_prolong(const Geo& gf, double* phi, const Geo& gc, const double* ec,
     NS_LAUNCH(k_prolong, cell_grid(gf, rows), dim3(64, 4), 0, st, gf, phi, gc, ec, rows);
 }
 
-size_t coarse_vcycle_bytes(const Geo& g) { return sizeof(double) * (size_t)lv_layout(g.nx, g.ny, nullptr, nullptr); }
+size_t coarse_vcycle_bytes(const Geo& g) {
+    int dn;
+    return sizeof(double) * (size_t)cv_image_size(g.nx, g.ny, &dn);
+}
 
-int launch_coarse_vcycle(const Geo& g, const Coef& c, double* phi, const double* b, int cycles, int pre, int post,
-                         int citers, double comega, double somega, int dlo, int dhi, hipStream_t st) {
+// Gauss-Jordan inverse with partial pivoting of the m x m row-major matrix a (in place)
+static bool invert_dense(std::vector<double>& a, int m) {
+    std::vector<double> inv((size_t)m * m, 0.0);
+    for (int k = 0; k < m; k++) inv[(size_t)k * m + k] = 1.0;
+    for (int c = 0; c < m; c++) {
+        int p = c;
+        for (int r = c + 1; r < m; r++)
+            if (std::fabs(a[(size_t)r * m + c]) > std::fabs(a[(size_t)p * m + c])) p = r;
+        if (a[(size_t)p * m + c] == 0.0) return false;
+        if (p != c)
+            for (int k = 0; k < m; k++) {
+                std::swap(a[(size_t)p * m + k], a[(size_t)c * m + k]);
+                std::swap(inv[(size_t)p * m + k], inv[(size_t)c * m + k]);
+            }
+        const double d = 1.0 / a[(size_t)c * m + c];
+        for (int k = 0; k < m; k++) { a[(size_t)c * m + k] *= d; inv[(size_t)c * m + k] *= d; }
+        for (int r = 0; r < m; r++) {
+            if (r == c) continue;
+            const double f = a[(size_t)r * m + c];
+            if (f == 0.0) continue;
+            for (int k = 0; k < m; k++) {
+                a[(size_t)r * m + k] -= f * a[(size_t)c * m + k];
+                inv[(size_t)r * m + k] -= f * inv[(size_t)c * m + k];
+            }
+        }
+    }
+    a.swap(inv);
+    return true;
+}
+
+// the LDS image of k_coarse_vcycle for a whole level with spacings hx (nx), hy (ny): every
+// level's spacings, ConstructLHS weights (a closed side: 2/h^2, face Dirichlet) and 1/diag,
+// exactly as the kernel computed them before, and M for the direct last-level solve
+int cv_image(const double* hx, const double* hy, int nx, int ny, int dlo, int dhi, std::vector<double>& img,
+             int* dn) {
+    const int n_img = cv_image_size(nx, ny, dn);
+    LdsLv lv[LV_MAX];
+    int nl = 0;
+    lv_layout(nx, ny, lv, &nl);
+    img.assign((size_t)n_img, 0.0);
+    double* L = img.data();
+    for (int k = 0; k < nl; k++) {
+        const LdsLv& v = lv[k];
+        for (int t = 0; t < v.nx; t++) L[v.hx + t] = k == 0 ? hx[t] : L[lv[k - 1].hx + 2 * t] + L[lv[k - 1].hx + 2 * t + 1];
+        for (int t = 0; t < v.ny; t++) L[v.hy + t] = k == 0 ? hy[t] : L[lv[k - 1].hy + 2 * t] + L[lv[k - 1].hy + 2 * t + 1];
+        for (int t = 0; t < v.nx; t++) {
+            const double h = L[v.hx + t];
+            L[v.cw + t] = t > 0 ? 2.0 / (h * (h + L[v.hx + t - 1])) : (dlo ? 2.0 / (h * h) : 0.0);
+            L[v.ce + t] = t < v.nx - 1 ? 2.0 / (h * (h + L[v.hx + t + 1])) : (dhi ? 2.0 / (h * h) : 0.0);
+        }
+        for (int t = 0; t < v.ny; t++) {
+            const double h = L[v.hy + t];
+            L[v.cs + t] = t > 0 ? 2.0 / (h * (h + L[v.hy + t - 1])) : 0.0;
+            L[v.cn + t] = t < v.ny - 1 ? 2.0 / (h * (h + L[v.hy + t + 1])) : 0.0;
+        }
+        for (int i = 0; i < v.nx; i++)
+            for (int j = 0; j < v.ny; j++)
+                L[v.idg + i * v.ny + j] = -1.0 / ((L[v.cw + i] + L[v.ce + i]) + (L[v.cs + j] + L[v.cn + j]));
+    }
+    if (*dn == 0) return n_img;
+    // the last level's operator (lv_lap), bordered when it is singular (no closed side)
+    const LdsLv& v = lv[nl - 1];
+    const int n = *dn;
+    const bool sing = !dlo && !dhi;
+    const int m = sing ? n + 1 : n;
+    std::vector<double> a((size_t)m * m, 0.0);
+    for (int i = 0; i < v.nx; i++)
+        for (int j = 0; j < v.ny; j++) {
+            const int r = i * v.ny + j;
+            const double cw = L[v.cw + i], ce = L[v.ce + i], cs = L[v.cs + j], cn = L[v.cn + j];
+            a[(size_t)r * m + r] = -((cw + ce) + (cs + cn));
+            if (i > 0) a[(size_t)r * m + r - v.ny] += cw;
+            if (i < v.nx - 1) a[(size_t)r * m + r + v.ny] += ce;
+            if (j > 0) a[(size_t)r * m + r - 1] += cs;
+            if (j < v.ny - 1) a[(size_t)r * m + r + 1] += cn;
+            if (sing) {
+                a[(size_t)r * m + n] = 1.0;
+                a[(size_t)n * m + r] = L[v.hx + i] * L[v.hy + j];
+            }
+        }
+    if (!invert_dense(a, m)) return -1;
+    double* M = L + (n_img - n * n);
+    for (int r = 0; r < n; r++)
+        for (int k = 0; k < n; k++) M[r * n + k] = a[(size_t)r * m + k];
+    return n_img;
+}
+
+int launch_coarse_vcycle(const Geo& g, const double* img, int img_n, int dn, double* phi, const double* b, int cycles,
+                         int pre, int post, int citers, double comega, double somega, int dlo, int dhi,
+                         hipStream_t st) {
     const size_t bytes = coarse_vcycle_bytes(g);
+    if (bytes != (size_t)img_n * sizeof(double)) return -1;
     if (bytes > 150 * 1024 || g.nxl != g.nx) return -1;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_coarse_vcycle, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         attr = true;
     }
-    NS_LAUNCH(k_coarse_vcycle, dim3(1), dim3(CV_THREADS), bytes, st, g, c, phi, b, cycles, pre, post, citers,
-                       comega, somega, dlo, dhi);
+    NS_LAUNCH(k_coarse_vcycle, dim3(1), dim3(CV_THREADS), bytes, st, g, img, img_n, dn, phi, b, cycles, pre, post,
+              citers, comega, somega, dlo, dhi);
     return 0;
 }
 

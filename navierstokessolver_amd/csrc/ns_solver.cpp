@@ -159,6 +159,8 @@ struct ns_solver {
     double* kv[9] = {};
     double* kv_mem = nullptr;
     double* lrow = nullptr;      // outflow preconditioner: its line solution (one row, in kv_mem)
+    double* cvimg = nullptr;     // the LDS coarse V-cycle's image (nsg::cv_image), cv_n doubles
+    int cv_n = 0, cv_dn = 0;
     double* ksc = nullptr;
     bool pc_active = false;      // inside mg_precond: level 0 has no mean shift
     bool pc_timing = false;      // ... and its level-0 passes are timed (the outflow Poisson solve)
@@ -858,9 +860,9 @@ int mg_coarse(ns_solver* s) {
     MgLevel& L = level(s, l);
     CHK(flush_b(s, l));
     if (s->mg_coarse_lds) {
-        if (nsg::launch_coarse_vcycle(L.g, L.c, L.phi, L.b, 1, s->mg_pre, s->mg_post, s->mg_coarse_iters,
-                                      s->mg_omega_c, s->mg_omega_s, s->out_side == 0, s->out_side == 1,
-                                      s->st) != 0) {
+        if (nsg::launch_coarse_vcycle(L.g, s->cvimg, s->cv_n, s->cv_dn, L.phi, L.b, 1, s->mg_pre, s->mg_post,
+                                      s->mg_coarse_iters, s->mg_omega_c, s->mg_omega_s, s->out_side == 0,
+                                      s->out_side == 1, s->st) != 0) {
             set_err("coarse LDS V-cycle does not fit");
             return NS_EINVAL;
         }
@@ -1410,6 +1412,14 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
     const double pi = 3.14159265358979323846;
     s->mg_omega_c = 2.0 / (1.0 + std::sin(pi / nc));
     s->mg_coarse_iters = 2 * nc + 10;
+    if (s->mg_coarse_lds) {
+        std::vector<double> img;
+        s->cv_n = nsg::cv_image(last.hx.data(), last.hy.data(), gc.nx, gc.ny, s->out_side == 0, s->out_side == 1, img,
+                                &s->cv_dn);
+        if (s->cv_n < 0) { set_err("coarse V-cycle: the last level's operator is singular"); return NS_EINVAL; }
+        HIPCHK(hipMalloc(&s->cvimg, img.size() * sizeof(double)));
+        HIPCHK(hipMemcpy(s->cvimg, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
     return 0;
 }
 
@@ -1960,6 +1970,7 @@ void ns_destroy(ns_solver* s) {
     if (s->base) (void)hipFree(s->base);
     if (s->phim_mem) (void)hipFree(s->phim_mem);
     if (s->kv_mem) (void)hipFree(s->kv_mem);
+    if (s->cvimg) (void)hipFree(s->cvimg);
     if (s->f32_mem) (void)hipFree(s->f32_mem);
     if (s->fc_mem) (void)hipFree(s->fc_mem);
     if (s->et_mem) (void)hipFree(s->et_mem);

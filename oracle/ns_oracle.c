@@ -933,6 +933,55 @@ static double lap_at(const mg_level* L, const double* p, int i, int j) {
     return s + dg * q;
 }
 
+/* The GPU path's last-level solve when that level has <= 64 cells (k_coarse_vcycle, CV_DIRECT):
+ * x = M b with M the n x n block of the inverse of the bordered system [A 1; w^T 0] (w = cell
+ * areas), i.e. A x = b - (w.b / w.1) 1 with w.x = 0.  Returns M (malloc'd) or NULL. */
+static double* mg_direct_matrix(const mg_level* L) {
+    const int n = L->nx * L->ny, m = n + 1;
+    double* a = calloc((size_t)m * m, sizeof(double));
+    double* inv = calloc((size_t)m * m, sizeof(double));
+    for (int i = 0; i < L->nx; i++)
+        for (int j = 0; j < L->ny; j++) {
+            const int r = i * L->ny + j;
+            a[(size_t)r * m + r] = -((L->cw[i] + L->ce[i]) + (L->cs[j] + L->cn[j]));
+            if (i > 0) a[(size_t)r * m + r - L->ny] += L->cw[i];
+            if (i < L->nx - 1) a[(size_t)r * m + r + L->ny] += L->ce[i];
+            if (j > 0) a[(size_t)r * m + r - 1] += L->cs[j];
+            if (j < L->ny - 1) a[(size_t)r * m + r + 1] += L->cn[j];
+            a[(size_t)r * m + n] = 1.0;
+            a[(size_t)n * m + r] = L->hx[i] * L->hy[j];
+        }
+    for (int k = 0; k < m; k++) inv[(size_t)k * m + k] = 1.0;
+    /* Gauss-Jordan, partial pivoting */
+    for (int c = 0; c < m; c++) {
+        int p = c;
+        for (int r = c + 1; r < m; r++)
+            if (fabs(a[(size_t)r * m + c]) > fabs(a[(size_t)p * m + c])) p = r;
+        if (a[(size_t)p * m + c] == 0.0) { free(a); free(inv); return NULL; }
+        if (p != c)
+            for (int k = 0; k < m; k++) {
+                double t = a[(size_t)p * m + k]; a[(size_t)p * m + k] = a[(size_t)c * m + k]; a[(size_t)c * m + k] = t;
+                t = inv[(size_t)p * m + k]; inv[(size_t)p * m + k] = inv[(size_t)c * m + k]; inv[(size_t)c * m + k] = t;
+            }
+        const double d = 1.0 / a[(size_t)c * m + c];
+        for (int k = 0; k < m; k++) { a[(size_t)c * m + k] *= d; inv[(size_t)c * m + k] *= d; }
+        for (int r = 0; r < m; r++) {
+            if (r == c) continue;
+            const double f = a[(size_t)r * m + c];
+            if (f == 0.0) continue;
+            for (int k = 0; k < m; k++) {
+                a[(size_t)r * m + k] -= f * a[(size_t)c * m + k];
+                inv[(size_t)r * m + k] -= f * inv[(size_t)c * m + k];
+            }
+        }
+    }
+    double* M = malloc(sizeof(double) * (size_t)n * n);
+    for (int r = 0; r < n; r++)
+        for (int k = 0; k < n; k++) M[(size_t)r * n + k] = inv[(size_t)r * m + k];
+    free(a); free(inv);
+    return M;
+}
+
 /* one red-black sweep in place (red = (i+j) even first) */
 static void mg_rb(const mg_level* L, double* p, const double* b, double shift, double omega) {
     const int nt = (size_t)L->nx * L->ny >= 65536 ? og_nt : 1;
@@ -1051,6 +1100,8 @@ int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre
     const int nc = Lc->nx > Lc->ny ? Lc->nx : Lc->ny;
     const double omc = 2.0 / (1.0 + sin(3.14159265358979323846 / nc));
     const int itc = 2 * nc + 10;
+    const int ncell = Lc->nx * Lc->ny;
+    double* Md = ncell <= 64 ? mg_direct_matrix(Lc) : NULL;
     int cycles = 0;
     for (;;) {
         /* down */
@@ -1066,7 +1117,15 @@ int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre
             bf = L[l + 1].b;
         }
         if (done) break;
-        for (int k = 0; k < itc; k++) mg_rb(Lc, L[nl - 1].x, L[nl - 1].b, 0.0, omc);
+        if (Md) {
+            for (int r = 0; r < ncell; r++) {
+                double x = 0.0;
+                for (int k = 0; k < ncell; k++) x += Md[(size_t)r * ncell + k] * L[nl - 1].b[k];
+                L[nl - 1].x[r] = x;
+            }
+        } else {
+            for (int k = 0; k < itc; k++) mg_rb(Lc, L[nl - 1].x, L[nl - 1].b, 0.0, omc);
+        }
         for (int l = nl - 2; l >= 0; l--) {
             double* xl = l == 0 ? x : L[l].x;
             const double* bl = l == 0 ? rhs : L[l].b;
@@ -1075,6 +1134,7 @@ int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre
         }
         cycles++;
     }
+    free(Md);
     mg_free(L, nl);
     return cycles;
 }
