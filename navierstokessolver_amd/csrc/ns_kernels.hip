@@ -1791,7 +1791,8 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) { sweep2_body<OP, 
 // restriction's summation order), so the two are interchangeable level by level.
 // TT = 32, or 16 on the levels that would have fewer than 512 tiles of 32 (<= 512^2): four
 // times the workgroups and a quarter of the work per half-sweep -- these levels are latency-bound,
-// so the larger cone overhead costs nothing (8 -> ~? us per pass at 128^2 .. 512^2)
+// so the larger cone overhead costs nothing (128^2 / 256^2: 8.2 -> 5.4 us per FUSE_R pass, 512^2:
+// 8.8 -> 7.6 us; at 1024^2 16 x 16 tiles measured 0.3 % slower overall, so 32 stays there)
 template <int FUSE, int TT>
 __global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
     constexpr bool XR = FUSE == FUSE_R, XP = FUSE == FUSE_P;
@@ -2915,7 +2916,7 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
 template <int FUSE>
 static int launch_tile2(const StreamArgs& a, const Geo& g, hipStream_t st) {
     const int tj32 = (g.ny + 31) / 32, n32 = tj32 * ((g.nxl + 31) / 32);
-    if (n32 >= (getenv("NSGPU_TILE32_MIN") ? atoi(getenv("NSGPU_TILE32_MIN")) : 512)) {
+    if (n32 >= 512) {
         NS_LAUNCH((k_tile2<FUSE, 32>), dim3(n32), dim3(256), 0, st, a, tj32);
         return n32;
     }
