@@ -2816,11 +2816,14 @@ void set_strip_phase(int phase) { g_phase = phase; }
 // strip rows, then phase 2's two.  Sets a.L and the launch's strip mapping; returns the
 // pass's strip count (the same for both phases) and the launch's workgroups in *nblk.
 static int plan_strips2(StreamArgs& a, long cap, int depth, int* nblk) {
+    // strips of >= 20 rows: at 2048^2 (the first coarse level) 16 -> 20 rows is 41.9 -> 38.8 us per
+    // FUSE_R pass (fewer halo rows per output row beats the extra waves); 24 / 28 measured slower
+    constexpr int lmin2 = 20;
     const int d = (depth + 1) & ~1, R = a.nxl - 2 * d;
     a.pbase = 0;
     a.rb1 = 0;
     if (g_phase == 0 || R < 2) {
-        a.L = strip_rows(a.nxl, a.nsj, cap, 16);
+        a.L = strip_rows(a.nxl, a.nsj, cap, lmin2);
         const int n = (a.nxl + a.L - 1) / a.L;
         a.nrun = g_phase == 1 ? 0 : n;   // (a slab too thin to split: all of it after the exchange)
         a.slo = n;
@@ -2829,7 +2832,7 @@ static int plan_strips2(StreamArgs& a, long cap, int depth, int* nblk) {
         *nblk = (a.nsj * a.nrun + 3) / 4;
         return a.nsj * n;
     }
-    a.L = strip_rows(R, a.nsj, cap, 16);
+    a.L = strip_rows(R, a.nsj, cap, lmin2);
     const int n1 = (R + a.L - 1) / a.L;
     if (g_phase == 1) {
         a.nrun = a.slo = n1;
