@@ -1898,8 +1898,28 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         // line-solve preconditioner (NSGPU_OUTFLOW_PC=wall: the round-1 wall closure, A/B)
         const int nneu = g.neu[0] + g.neu[1] + g.neu[2] + g.neu[3];
         const char* ope = getenv("NSGPU_OUTFLOW_PC");
-        if (!masked && nneu == 1 && (g.neu[0] || g.neu[1]) && g.ny <= 4096 && !(ope && !std::strcmp(ope, "wall")))
-            s->out_side = g.neu[0] ? 0 : 1;
+        const bool line_pc = g.ny <= 4096 && !(ope && !std::strcmp(ope, "wall"));
+        if (!masked && nneu == 1 && (g.neu[0] || g.neu[1]) && line_pc) s->out_side = g.neu[0] ? 0 : 1;
+        if (masked && line_pc) {
+            // a polygon whose only NEUMANN edge is exactly the bounding box's W or E column (every
+            // cell of it in the domain -- e.g. the backward-facing step's outflow): the box
+            // hierarchy takes the same line closure on that side
+            int en = -1, nne = 0;
+            for (int e = 0; e < gd->n_edges; e++)
+                if (gd->edges[e].type == NS_BC_NEUMANN) { en = e; nne++; }
+            for (int k = 0; k < 2 && nne == 1 && s->out_side < 0; k++) {
+                const int i = k == 0 ? 0 : g.nx - 1;
+                bool whole = true;
+                for (int j = 0; j < g.ny && whole; j++) {
+                    const size_t c = (size_t)i * g.ny + j;
+                    whole = gd->cell_id[c] >= 0 && gd->face_edge[4 * c + k] == en;
+                }
+                long faces = 0;   // the edge must not reach any other cell face
+                for (size_t c = 0; c < (size_t)g.nx * g.ny && whole; c++)
+                    for (int f = 0; f < 4; f++) faces += gd->face_edge[4 * c + f] == en;
+                if (whole && faces == g.ny) s->out_side = k;
+            }
+        }
         if (p->mg_pre > 0) s->mg_pre = p->mg_pre;
         if (p->mg_omega > 0) s->mg_omega_s = p->mg_omega;
         if (const char* e = getenv("NSGPU_MG_OMEGA")) s->mg_omega_s = std::atof(e);   // smoother over-relaxation (A/B)

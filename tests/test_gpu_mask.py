@@ -158,3 +158,27 @@ def test_mask_compact_fields_through_the_c_abi(gpu, name):
     assert du <= 1e-6 and dv <= 1e-6, (du, dv)
     with pytest.raises(ValueError):
         gs.set_fields_compact(u=np.zeros(og.N + 1))
+
+
+def test_mask_step_outflow_line_preconditioner(gpu, monkeypatch):
+    """The backward-facing step of tools/bench_bcs.py (512 x 256, inlet W upper half, NEUMANN
+    outflow on the whole E column, Re 1000) from rest: its only NEUMANN edge is the bounding
+    box's E column, so the box hierarchy takes the outflow line closure -- Poisson
+    BiCGStab <= 15 iterations per step where the wall closure (NSGPU_OUTFLOW_PC=wall) needs
+    ~35 -- and both runs take the same steps (monitor to 1e-6, the solves' rtol 1e-8)."""
+    n = 512
+    hs = 2.0 / n
+    verts = [(0, 0.5), (0, 1), (2, 1), (2, 0), (0.5, 0), (0.5, 0.5)]
+    bc = [(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0), (2, 0.0), (2, 0.0)]
+    out = {}
+    for pc in ("line", "wall"):
+        monkeypatch.setenv("NSGPU_OUTFLOW_PC", pc)
+        gs = gpu.GpuSolver(gpu.polygon(verts, np.full(n, hs), np.full(n // 2, hs), bc), hs / 8, 1000.0)
+        st = [gs.step() for _ in range(6)]
+        gs.close()
+        out[pc] = st
+    its = {k: [x["it_phi"] for x in v] for k, v in out.items()}
+    assert np.mean(its["line"]) <= 15 and np.mean(its["line"]) < 0.6 * np.mean(its["wall"]), its
+    for a, b in zip(out["line"], out["wall"]):
+        np.testing.assert_allclose([a[k] for k in ("umin", "umax", "vmin", "vmax")],
+                                   [b[k] for k in ("umin", "umax", "vmin", "vmax")], atol=1e-6)
