@@ -26,6 +26,10 @@
 
 #include <algorithm>
 
+#ifndef K1_DIAG
+#define K1_DIAG 0
+#endif
+
 namespace nsg {
 
 // ---------------------------------------------------------------- helpers
@@ -565,8 +569,16 @@ __global__ __launch_bounds__(256) void k_rhs_lds(Geo g, Coef c, double dt, doubl
             auto X = [&](int t, int d) { return tx[t][R - 1 + d]; };
             auto Y = [&](int t, int d) { return ty[t][C - 1 + d]; };
             double cun, cvn, ru_, rv_;
+#if K1_DIAG   // diagnostic build: the tile's memory stream alone (trivial per-cell arithmetic)
+            cun = U(0, 0) + U(-2, 0) + U(2, 0) + U(0, -2) + U(0, 2) + X(0, 0);
+            cvn = V(0, 0) + V(-2, 0) + V(2, 0) + V(0, -2) + V(0, 2) + Y(0, 0);
+            ru_ = cun + scu[R - 2][C - 2];
+            rv_ = cvn + scv[R - 2][C - 2];
+            (void)sizeof(T);
+#else
             rhs_cell<false, T>(g, c, dt, re, U, V, X, Y, phi, li, j, scu[R - 2][C - 2], scv[R - 2][C - 2], cun, cvn,
                                ru_, rv_);
+#endif
             cu[o] = cun;
             cv[o] = cvn;
             ru[o] = ru_;
