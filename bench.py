@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--sync-monitor", action="store_true",
                     help="ns_step (host sync at every step's end) instead of ns_step_async")
-    ap.add_argument("--time-every", type=int, default=3,
+    ap.add_argument("--time-every", type=int, default=10,
                     help="HIP-event kernel timing on every k-th timed step (each event pair costs a few us of "
                          "GPU idle; 0 = none)")
     return ap.parse_args()
