@@ -916,6 +916,12 @@ struct StreamArgs {
     // [ib, min(ib + L, rend)) with ib = rb0 + k L for k < slo, else rb1 + (k - slo) L; its
     // residual partials go to slot (pbase + k) nsj + j; nrun strip rows in all
     int slo, nrun, rb0, rb1, rend, pbase;
+    // k_sweep2<..., FUSE_UV>: two fields in one launch (the multi-rank Helmholtz pair pass, u and
+    // v): waves [nstr, 2 nstr) take in2 / out2 / b2 and write their partials to part2
+    const double* in2;
+    double* out2;
+    const double* b2;
+    double* part2;
 };
 
 // diagonal of the operator at a cell from its row / column coefficient sums
@@ -1488,7 +1494,8 @@ template <int OP, bool RES, int FUSE>
 constexpr int sd2_of() {
     return FUSE == 1 ? 3 : FUSE == 2 ? SD2_FP : OP == 1 ? (RES ? SD2_HELMR : SD2_HELM) : SD2_PLAIN;
 }
-constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2;
+// FUSE_UV: no transfer fused; two fields (the multi-rank Helmholtz pair pass, u and v) in one launch
+constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2, FUSE_UV = 3;
 #ifndef XR_BUF
 #define XR_BUF 0   // FUSE_R's coarse stores through buffers too (1: 172 VGPRs, 2 waves/SIMD, slower)
 #endif
@@ -1759,14 +1766,20 @@ __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
     __shared__ double rcs[4][RC_MAX][4];
     const int lane = threadIdx.x & 63;
     const int nstr = a.nsj * a.nrun;
-    const int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
     double (*rc)[4] = rcs[threadIdx.x >> 6];
+    // the second field's waves (nf = 2; wave-uniform, same coefficient tables)
+    StreamArgs af = a;
+    if (FUSE == FUSE_UV && w >= nstr) {
+        w -= nstr;
+        af.in = a.in2; af.out = a.out2; af.b = a.b2; af.part = a.part2;
+    }
     // this wave's strip (plan_strips2: the launch may cover a subset of the pass's rows)
     const int run = w / a.nsj, sj = w - run * a.nsj;
     const int ib = run < a.slo ? a.rb0 + run * a.L : a.rb1 + (run - a.slo) * a.L;
     const int ie = min(ib + a.L, a.rend);
     const int si = a.pbase + run, wid = si * a.nsj + sj;
-    if (w < nstr) stage_rows<OP>(a, rc, ib, lane);
+    if (w < nstr) stage_rows<OP>(af, rc, ib, lane);
     __syncthreads();
     double res = 0.0;
     if (w < nstr) {
@@ -1775,13 +1788,13 @@ __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
         // The restriction pass walks downwards only: upwards, its fused restriction rounds some
         // coarse sums differently, and its values would depend on how a pass is cut into strips
         // (the overlapped exchange's split, the slab height)
-        if (FUSE != FUSE_R && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1>(a, rc, ib, ie, sj, lane);
-        else res = sweep2_strip<OP, RES, FUSE, 1>(a, rc, ib, ie, sj, lane);
+        if (FUSE != FUSE_R && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1>(af, rc, ib, ie, sj, lane);
+        else res = sweep2_strip<OP, RES, FUSE, 1>(af, rc, ib, ie, sj, lane);
     }
     if (R5) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
-        if (lane == 0 && w < nstr) a.part[wid] = res;
+        if (lane == 0 && w < nstr) af.part[wid] = res;
     }
 }
 
@@ -2893,6 +2906,14 @@ static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st, bool count
     int nblk = 0;
     const int nstr = plan_strips2(a, cap, a.part ? 5 : 4, &nblk);
     if (count_only || !nblk) return nstr;
+    if constexpr (OP == 1) {
+        if (a.in2) {   // two fields: the multi-rank Helmholtz pair pass
+            nblk = (2 * a.nsj * a.nrun + 3) / 4;
+            if (a.part) NS_LAUNCH((k_sweep2<OP, true, FUSE_UV>), dim3(nblk), dim3(256), 0, st, a);
+            else NS_LAUNCH((k_sweep2<OP, false, FUSE_UV>), dim3(nblk), dim3(256), 0, st, a);
+            return nstr;
+        }
+    }
     if (a.part) NS_LAUNCH((k_sweep2<OP, true, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
     else NS_LAUNCH((k_sweep2<OP, false, FUSE_NONE>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
@@ -2965,6 +2986,14 @@ int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, 
                        double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st,
                        int which) {
     int n = 0;
+    if (which == 3) {
+        // both components in one launch (the multi-rank pair pass: one launch boundary, and one
+        // edge-strip launch after the exchange, instead of two); partials: u at [0, n), v at [n, 2n)
+        StreamArgs a = stream_args(g, c, u, uo, ru, nullptr, alpha, omega, part, true);
+        n = launch_stream2<1>(a, g, st, true);   // strip count only
+        a.in2 = v; a.out2 = vo; a.b2 = rv; a.part2 = part ? part + n : nullptr;
+        return launch_stream2<1>(a, g, st);
+    }
     if (which & 1) n = launch_stream2<1>(stream_args(g, c, u, uo, ru, nullptr, alpha, omega, part, true), g, st);
     if (which & 2) {
         StreamArgs a = stream_args(g, c, v, vo, rv, nullptr, alpha, omega, nullptr, true);
