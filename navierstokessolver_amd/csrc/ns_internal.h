@@ -91,6 +91,9 @@ void launch_to_f64(const Geo& g, const float* src, double* dst, hipStream_t st);
 // (4 without)
 int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st);
+// K2: three RB-SOR sweeps per pass (k_sweep3; no residual partials); which as above
+int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                       double* uo, double* vo, const double* ru, const double* rv, hipStream_t st, int which);
 int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
                        double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st,
                        int which = 3);

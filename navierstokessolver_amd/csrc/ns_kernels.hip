@@ -988,6 +988,8 @@ struct DiagCache {
 // critical path (hipcc cannot prove the tables read-only against the `out` stores)
 constexpr int RC_OFF = 5;            // table row of strip row ib
 constexpr int RC_MAX = 64 + 2 * RC_OFF;  // L <= 64
+constexpr int RC_OFF3 = 5;           // k_sweep3: its first stage reads rows ib-5 .. ie+4 too
+constexpr int RC_MAX3 = 64 + 2 * RC_OFF3;
 template <int OP, int RCO = RC_OFF>
 __device__ __forceinline__ void stage_rows(const StreamArgs& a, double (*rc)[4], int ib, int lane) {
     for (int t = lane; t < a.L + 2 * RCO && t < 64 + 2 * RCO; t += 64) {
@@ -1757,6 +1759,135 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
         }
     }
     return res;
+}
+
+// ------------------------------------------------ K2: three Helmholtz sweeps per HBM pass
+// The Helmholtz solve needs 7 RB-SOR sweeps per component at 4096^2 (rtol 1e-8; the pairs of
+// k_sweep2 made that 8).  k_sweep3 carries six stages (red / black of sweeps 1-3) in the same
+// register pipeline: 7 sweeps = 3 + 2 + 2, three HBM passes instead of four.  Helmholtz
+// operator only, no residual stage (the pass is never a batch's last: helm_sweeps), strips of
+// 116 written columns (a 6-column cone on each side), rows ib-6 .. ie+5 read; every value is
+// the same arithmetic as three single sweeps (bit-identical).  FUSE_UV: u and v in one launch.
+template <int DIR>
+__device__ __forceinline__ void sweep3_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
+                                             int lane) {
+    constexpr int SD3 = 2;
+    const int jb = sj * SW2X;
+    const int ny = a.ny, ld = a.ld;
+    const int c0 = jb - 6 + 2 * lane, c1 = c0 + 1;
+    const int lc = min(max(c0, 0), ld - 2);
+    const bool v0 = c0 >= 0 && c0 < ny, v1 = c1 >= 0 && c1 < ny;
+    const bool wr = lane >= 3 && lane <= 60 && c0 < ny;
+    const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
+    const double cs0 = a.cs[k0], cn0 = a.cn[k0], cd0 = cs0 + cn0 + a.by[k0];
+    const double cs1 = a.cs[k1], cn1 = a.cn[k1], cd1 = cs1 + cn1 + a.by[k1];
+    const double alpha = a.alpha, omega = a.omega;
+    const int rlo = -HALO, rhi = a.nxl + HALO - 1;
+    const int rb = __builtin_amdgcn_readfirstlane(ib - 1);
+    const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + (ptrdiff_t)rb * ld, (short)0, (int)((unsigned)(a.L + 2) * ld * 8u), 0x00020000);
+    double2 Q[SD3], QB[SD3];
+    // q rows ib-6 .. ie+5 and b rows ib-5 .. ie+4 (the first red stage's) are read
+    const int r0 = ib - 6, r1 = ie + 5;
+    const int phi_lo = DIR > 0 ? rlo : max(r0, rlo), phi_hi = DIR > 0 ? min(r1, rhi) : rhi;
+    const int b_lo = DIR > 0 ? max(ib - 5, rlo) : rlo, b_hi = DIR > 0 ? rhi : min(ie + 4, rhi);
+    auto load = [&](int slot_r, double2& p, double2& bb) {
+        const int lp = min(max(slot_r, phi_lo), phi_hi), lb = min(max(slot_r - DIR, b_lo), b_hi);
+        p = ld_stream(a.in + (ptrdiff_t)lp * ld + lc, 0);
+        bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
+    };
+    // windows (3 rows each) of the six stages' inputs; rhs rows r-1 .. r-6
+    double2 P0 = {0, 0}, P1 = {0, 0}, P2 = {0, 0};
+    double2 A0 = {0, 0}, A1 = {0, 0}, A2 = {0, 0};
+    double2 C0 = {0, 0}, C1 = {0, 0}, C2 = {0, 0};
+    double2 E0 = {0, 0}, E1 = {0, 0}, E2 = {0, 0};
+    double2 G0 = {0, 0}, G1 = {0, 0}, G2 = {0, 0};
+    double2 H0 = {0, 0}, H1 = {0, 0}, H2 = {0, 0};
+    double2 B1 = {0, 0}, B2 = {0, 0}, B3 = {0, 0}, B4 = {0, 0}, B5 = {0, 0}, B6 = {0, 0};
+    auto half = [&](const double2& W0, const double2& W1, const double2& W2, const double2& B, int row,
+                    int par) -> double2 {
+        double2 o = W1;
+        const int gi = a.i0 + row;
+        if (gi < 0 || gi >= a.nx) return o;
+        const double* rw = rc[row - ib + RC_OFF3];
+        const double cw = rw[0], ce = rw[1];
+        double rr;
+        if ((gi & 1) == par) {
+            const double lf = lane_up1(W1.y);
+            const double d = diag<1>(rw[2], cd0, alpha), w = omega * rcp_nr(d);
+            if (v0) o.x = relax<1>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr);
+        } else {
+            const double rt = lane_dn1(W1.x);
+            const double d = diag<1>(rw[2], cd1, alpha), w = omega * rcp_nr(d);
+            if (v1) o.y = relax<1>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, d, w, alpha, rr);
+        }
+        return o;
+    };
+    // one pipeline stage: colour `par` at row m if m lies in [lo, hi] (else the value passes on)
+    auto stage = [&](const double2& W0, const double2& W1, const double2& W2, const double2& B, int m, int lo,
+                     int hi, int par) -> double2 {
+        if (m < lo || m > hi) return W1;
+        return DIR > 0 ? half(W0, W1, W2, B, m, par) : half(W2, W1, W0, B, m, par);
+    };
+    auto step = [&](double2 p, const double2 bb, int r) {
+        P0 = P1; P1 = P2; P2 = vcopy(p);
+        B6 = B5; B5 = B4; B4 = B3; B3 = B2; B2 = B1;
+        B1 = bb;
+        const double2 n1 = stage(P0, P1, P2, B1, r - DIR, ib - 5, ie + 4, 0);       // red 1
+        A0 = A1; A1 = A2; A2 = n1;
+        const double2 n2 = stage(A0, A1, A2, B2, r - 2 * DIR, ib - 4, ie + 3, 1);   // black 1
+        C0 = C1; C1 = C2; C2 = n2;
+        const double2 n3 = stage(C0, C1, C2, B3, r - 3 * DIR, ib - 3, ie + 2, 0);   // red 2
+        E0 = E1; E1 = E2; E2 = n3;
+        const double2 n4 = stage(E0, E1, E2, B4, r - 4 * DIR, ib - 2, ie + 1, 1);   // black 2
+        G0 = G1; G1 = G2; G2 = n4;
+        const double2 n5 = stage(G0, G1, G2, B5, r - 5 * DIR, ib - 1, ie, 0);       // red 3
+        H0 = H1; H1 = H2; H2 = n5;
+        // black 3 at r-6, stored on the strip's rows (out-of-range offset: dropped)
+        const int k = r - 6 * DIR;
+        const double2 n6 = stage(H0, H1, H2, B6, k, ib, ie - 1, 1);
+        const unsigned off = (k >= ib && k < ie && wr) ? ((unsigned)(k - rb) * (unsigned)ld + (unsigned)c0) * 8u : OOB;
+        const nsu4 d = {(unsigned)__double2loint(n6.x), (unsigned)__double2hiint(n6.x),
+                        (unsigned)__double2loint(n6.y), (unsigned)__double2hiint(n6.y)};
+        __builtin_amdgcn_raw_buffer_store_b128(d, out, (int)off, 0, 2);
+    };
+    const int rs = DIR > 0 ? r0 : r1, nr = r1 - r0 + 1;
+#pragma unroll
+    for (int q = 0; q < SD3; q++) {
+        load(rs + DIR * q, Q[q], QB[q]);
+        asm volatile("" ::: "memory");
+    }
+    for (int t = 0; t < nr; t += SD3) {
+#pragma unroll
+        for (int q = 0; q < SD3; q++) {
+            step(Q[q], QB[q], rs + DIR * (t + q));
+            load(rs + DIR * (t + q + SD3), Q[q], QB[q]);
+        }
+    }
+}
+
+template <int FUSE>
+__global__ __launch_bounds__(256) void k_sweep3(StreamArgs a) {
+    __shared__ double rcs[4][RC_MAX3][4];
+    const int nstr = a.nsj * a.nrun;
+    int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    double (*rc)[4] = rcs[threadIdx.x >> 6];
+    StreamArgs af = a;
+    if (FUSE == FUSE_UV && w >= nstr) {
+        w -= nstr;
+        af.in = a.in2; af.out = a.out2; af.b = a.b2;
+    }
+    const int lane = threadIdx.x & 63;
+    const int run = w / a.nsj, sj = w - run * a.nsj;
+    const int ib = run < a.slo ? a.rb0 + run * a.L : a.rb1 + (run - a.slo) * a.L;
+    const int ie = min(ib + a.L, a.rend);
+    const int si = a.pbase + run;
+    if (w < nstr) stage_rows<1, RC_OFF3>(af, rc, ib, lane);
+    __syncthreads();
+    if (w < nstr) {
+        if (si & 1) sweep3_strip<-1>(af, rc, ib, ie, sj, lane);
+        else sweep3_strip<1>(af, rc, ib, ie, sj, lane);
+    }
 }
 
 template <int OP, bool RES, int FUSE>
@@ -2980,6 +3111,26 @@ int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const d
 int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st) {
     return launch_stream2<0>(stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false), g, st);
+}
+
+// three Helmholtz sweeps in one pass (k_sweep3; no residual): which = 1 u, 2 v, 3 both in one launch
+int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                       double* uo, double* vo, const double* ru, const double* rv, hipStream_t st, int which) {
+    StreamArgs a = stream_args(g, c, which == 2 ? v : u, which == 2 ? vo : uo, which == 2 ? rv : ru, nullptr, alpha,
+                               omega, nullptr, true);
+    a.nsj = (g.ny + SW2X - 1) / SW2X;
+    const void* k = which == 3 ? (const void*)k_sweep3<FUSE_UV> : (const void*)k_sweep3<FUSE_NONE>;
+    int nblk = 0;
+    const int nstr = plan_strips2(a, resident_waves(k), 6, &nblk);
+    if (!nblk) return nstr;
+    if (which == 3) {
+        a.in2 = v; a.out2 = vo; a.b2 = rv;
+        nblk = (2 * a.nsj * a.nrun + 3) / 4;
+        NS_LAUNCH(k_sweep3<FUSE_UV>, dim3(nblk), dim3(256), 0, st, a);
+    } else {
+        NS_LAUNCH(k_sweep3<FUSE_NONE>, dim3(nblk), dim3(256), 0, st, a);
+    }
+    return nstr;
 }
 
 int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,

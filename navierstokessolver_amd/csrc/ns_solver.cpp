@@ -119,6 +119,7 @@ struct ns_solver {
     int helm_batch0 = 4, pois_batch0 = 8;
     int helm_next = 4;           // first Helmholtz batch of the next step (adaptive unless check_every)
     int helm_adapt = 1;
+    bool sweep3 = true;          // single rank: odd Helmholtz batches start with a 3-sweep pass (k_sweep3)
     int helm_probe = 0;          // steps since the Helmholtz first-pass residual was last sampled
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
     int fuse_restrict = 1;       // NSGPU_FUSED_RESTRICT=0: separate k_restrict pass (A/B)
@@ -409,6 +410,16 @@ int helm_sweep(ns_solver* s, double alpha, double* part, int which = 3) {
     return nb;
 }
 
+// three Helmholtz sweeps in one pass (k_sweep3; no residual), then swap (single rank)
+int helm_sweep3(ns_solver* s, double alpha, int which) {
+    const int nb = nsg::launch_helm_sweep3(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
+                                           s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
+                                           s->arr[NS_ARR_RV], s->st, which);
+    if (which & 1) std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
+    if (which & 2) std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
+    return nb;
+}
+
 // two Helmholtz sweeps in one pass (temporal blocking), then swap
 int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3) {
     // timing: one-component passes only (the bench's 24 B/cell roofline figure)
@@ -450,8 +461,14 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
         if (!which) break;
         int k = 0, launch = 0;
         while (k < n) {
-            // sweeps per pass: pairs (one sweep for an odd remainder, or with NSGPU_SWEEP=tiled)
-            const int w = std::min(s->tiled ? 1 : 2, n - k);
+            // sweeps per pass: pairs (single sweeps with NSGPU_SWEEP=tiled).  An odd remainder is
+            // taken first, so that the batch ends on a pair, whose residual is its output's: by
+            // one 3-sweep pass on one rank when >= 5 remain (7 = 3 + 2 + 2: three HBM passes
+            // instead of four), else by one single sweep (7 = 1 + 2 + 2 + 2) -- the same sweeps,
+            // bit-identical values; a probing first pass stays a pair (2 + 3 + 2, 2 + 1 + 2 + 2)
+            int w = std::min(s->tiled ? 1 : 2, n - k);
+            if (!s->tiled && ((n - k) & 1) && n - k >= 3 && !(launch == 0 && part_first))
+                w = (s->sweep3 && split && n - k >= 5) ? 3 : 1;
             const bool last = k + w >= n;
             double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
             const int hw = w == 2 ? (part ? 5 : 4) : 2;
@@ -477,7 +494,8 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                 }
                 if (which == 3) CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, hw));
                 else if (w <= 2) CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
-                nb = w >= 2 ? helm_sweep2(s, alpha, part, which) : helm_sweep(s, alpha, part, which);
+                nb = w == 3 ? helm_sweep3(s, alpha, which)
+                            : (w >= 2 ? helm_sweep2(s, alpha, part, which) : helm_sweep(s, alpha, part, which));
                 if (nb < 0) return NS_EHIP;
             }
             const int at = w >= 2 ? k + w : k;   // a multi-sweep pass reports its output's residual
@@ -653,7 +671,9 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         const int nbatch = next_batch(batch, prev_r2, prev_at, r2, at, tol2, s->max_iters) - (sweeps - at);
         prev_r2 = r2;
         prev_at = at;
-        batch = std::max(nbatch + (nbatch & 1), 2);  // even batches: whole 2-sweep passes
+        // even batches (whole 2-sweep passes), or any with the 3-sweep pass (3 + 2 + ... ; a
+        // multi-rank odd batch ends with a single sweep: the same count, bit-identical values)
+        batch = std::max(s->sweep3 ? nbatch : nbatch + (nbatch & 1), 2);
     }
     *its = sweeps;
     // next step's first batch: the sweeps this step's measured contraction says suffice
@@ -664,7 +684,7 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         const double more = std::log(tol2 / first_r2) / rate;
         if (std::isfinite(more)) need = std::min(sweeps, first_at + std::max(0, (int)std::ceil(more)));
     }
-    s->helm_next = s->helm_adapt ? std::max(2, need + (need & 1)) : s->helm_batch0;
+    s->helm_next = s->helm_adapt ? std::max(2, s->sweep3 ? need : need + (need & 1)) : s->helm_batch0;
     // probe again in 8 steps, or on the next step if this one needed more than one batch
     s->helm_probe = (sweeps > n0) ? 0 : (s->helm_probe + 1) % 8;
     return 0;
@@ -1779,6 +1799,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     s->helm_adapt = p->check_every <= 0;
     s->timing = p->timing;
     if (const char* e = getenv("NSGPU_SWEEP")) s->tiled = std::strcmp(e, "tiled") == 0;
+    if (const char* e = getenv("NSGPU_SWEEP3")) s->sweep3 = std::atoi(e) != 0;   // A/B: pairs only
     if (const char* e = getenv("NSGPU_FUSED_RESTRICT")) s->fuse_restrict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
@@ -2214,15 +2235,18 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         return 0;
     case NS_K_HELMHOLTZ: {
         if (s->g.fc) { set_err("NS_K_HELMHOLTZ sweeps are rectangle-only; use NS_K_HELM_SOLVE on a masked domain"); return NS_EINVAL; }
-        // (iters-1)/2 two-sweep passes, then single sweeps; the residual is of the last sweep's input
+        // single rank with the 3-sweep pass and iters >= 4: one k_sweep3 pass first; then
+        // (rest-1)/2 two-sweep passes, then single sweeps; the residual is of the last sweep's input
         int nb = 0;
         CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
-        const int pairs = iters > 0 ? (iters - 1) / 2 : 0;
+        const int three = (s->sweep3 && s->nranks == 1 && !s->tiled && iters >= 4) ? 3 : 0;
+        if (three) helm_sweep3(s, alpha, 1), helm_sweep3(s, alpha, 2);
+        const int pairs = iters - three > 0 ? (iters - three - 1) / 2 : 0;
         for (int k = 0; k < pairs; k++) {
             CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 4));
             helm_sweep2(s, alpha, nullptr);
         }
-        for (int k = 2 * pairs; k < iters; k++) {
+        for (int k = three + 2 * pairs; k < iters; k++) {
             CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, 2));
             nb = helm_sweep(s, alpha, k == iters - 1 ? s->part : nullptr);
         }

@@ -407,9 +407,10 @@ def test_mg_step_algorithm_matches_oracle_mg(gpu):
 
 
 @pytest.mark.parametrize("nx,ny,op", [(64, 64, "poisson"), (130, 250, "poisson"), (37, 129, "helmholtz"),
-                                      (1024, 512, "poisson")])
+                                      (1024, 512, "poisson"), (700, 300, "helmholtz")])
 def test_two_sweep_pass_equals_two_sweeps(gpu, nx, ny, op):
-    """The temporally-blocked kernel (two red-black sweeps per HBM pass) = the oracle's two sweeps."""
+    """The temporally-blocked kernels (two red-black sweeps per HBM pass, k_sweep2; Helmholtz on
+    one rank: a three-sweep pass first, k_sweep3) = the oracle's single sweeps, to 1e-12."""
     rng = np.random.default_rng(17)
     if op == "poisson":
         og, gs = pair(gpu, nx, ny, 1e-3, 100.0, omega=1.6)
