@@ -1771,7 +1771,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
 template <int DIR>
 __device__ __forceinline__ void sweep3_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
                                              int lane) {
-    constexpr int SD3 = 2;
+    constexpr int SD3 = 2;   // rows in flight: 3 would need 174 VGPRs (2 waves/SIMD), or spill at 168 (measured equal)
     const int jb = sj * SW2X;
     const int ny = a.ny, ld = a.ld;
     const int c0 = jb - 6 + 2 * lane, c1 = c0 + 1;

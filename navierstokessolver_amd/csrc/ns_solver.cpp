@@ -461,14 +461,16 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
         if (!which) break;
         int k = 0, launch = 0;
         while (k < n) {
-            // sweeps per pass: pairs (single sweeps with NSGPU_SWEEP=tiled).  An odd remainder is
-            // taken first, so that the batch ends on a pair, whose residual is its output's: by
-            // one 3-sweep pass on one rank when >= 5 remain (7 = 3 + 2 + 2: three HBM passes
-            // instead of four), else by one single sweep (7 = 1 + 2 + 2 + 2) -- the same sweeps,
-            // bit-identical values; a probing first pass stays a pair (2 + 3 + 2, 2 + 1 + 2 + 2)
+            // sweeps per pass: pairs (single sweeps with NSGPU_SWEEP=tiled), and the batch ends on
+            // a pair, whose residual is its output's.  One rank: 3-sweep passes while >= 5 remain
+            // (7 = 3+2+2, 8 = 3+3+2, 11 = 3+3+3+2: a third fewer HBM passes); an odd remainder of
+            // >= 3 otherwise starts with a single sweep (multi-rank 7 = 1+2+2+2) -- the same sweeps,
+            // bit-identical values.  A probing first pass stays a pair (2+3+2, 2+1+2+2)
             int w = std::min(s->tiled ? 1 : 2, n - k);
-            if (!s->tiled && ((n - k) & 1) && n - k >= 3 && !(launch == 0 && part_first))
-                w = (s->sweep3 && split && n - k >= 5) ? 3 : 1;
+            if (!s->tiled && !(launch == 0 && part_first)) {
+                if (s->sweep3 && split && n - k >= 5) w = 3;
+                else if (((n - k) & 1) && n - k >= 3) w = 1;
+            }
             const bool last = k + w >= n;
             double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
             const int hw = w == 2 ? (part ? 5 : 4) : 2;
