@@ -88,6 +88,23 @@ def _host_threads():
     return len(os.sched_getaffinity(0))
 
 
+def helm_passes(n, world):
+    """HBM passes of one component's n Helmholtz sweeps (ns_solver.cpp helm_sweeps): one rank
+    takes 3-sweep passes while >= 5 remain and ends on a pair (7 = 3+2+2); slabs take an odd
+    remainder as a single sweep first, then pairs (7 = 1+2+2+2)."""
+    p, r = 0, n
+    while r > 0:
+        if world == 1 and r >= 5:
+            w = 3
+        elif r % 2 and r >= 3:
+            w = 1
+        else:
+            w = min(2, r)
+        r -= w
+        p += 1
+    return p
+
+
 def cpu_baseline(n, re, dt, omega_v, omega_mg, state):
     """The oracle (CPU restatement, -O3, OpenMP) running the SAME algorithm as the GPU path
     (RB-SOR Helmholtz to rtol, multigrid V(2,2) Poisson to rtol 1e-8) for one full time step
@@ -201,17 +218,18 @@ def main():
     # finest-level sweeps: V(2,2) per cycle + the 2 pre-smoothing sweeps of the converged check
     fine_sweeps = 4 * cycles + 2 * K
     # whole-step algorithmic bytes per cell: K1 64 + K3 24 + K5 40 + the phi
-    # extrapolation 32; Helmholtz 24 per pass, one pass = 2 sweeps of one component; multigrid
-    # per solve (cycles + 1) FUSE_R passes at 28 and `cycles` FUSE_P passes at 26 on the finest
-    # level, x 4/3 for the coarser levels (each a quarter of the one above)
-    step_bpc = (64 + 24 + 40 + 32 + 24 * hsweeps / K
+    # extrapolation 32; Helmholtz 24 per pass of one component (a pass = 2 or 3 sweeps: see
+    # helm_passes); multigrid per solve (cycles + 1) FUSE_R passes at 28 and `cycles` FUSE_P
+    # passes at 26 on the finest level, x 4/3 for the coarser levels (each a quarter of the one above)
+    hpasses = sum(helm_passes(int(s["it_u"]), world) for s in stats)
+    step_bpc = (64 + 24 + 40 + 32 + 2 * 24 * hpasses / K
                 + (28 * (cycles + K) + 26 * cycles) / K * 4.0 / 3.0)
     if channel:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications
         # of (line extension 8 + FUSE_R 28 + FUSE_P 26, x 4/3 for the coarser levels) = 80 each,
         # two operator applications 24 + 16, KV_V 32, KV_T 24, KV_X 64 = 352; start-up (apply +
         # KV_INIT) 64; no phi extrapolation
-        step_bpc = 64 + 24 + 40 + 64 + 24 * hsweeps / K + 352 * cycles / K
+        step_bpc = 64 + 24 + 40 + 64 + 2 * 24 * hpasses / K + 352 * cycles / K
     value = cells * K / elapsed / 1e6
 
     # the north star's roofline kernel: one Jacobi sweep of this rank's slab (random phi, b;
@@ -280,6 +298,7 @@ def main():
         "poisson_fine_sweeps_per_s": fine_sweeps / elapsed,
         "poisson_fine_sweeps_per_step": fine_sweeps / K,
         "helmholtz_sweeps_per_step": hsweeps / K,
+        "helmholtz_passes_per_step": 2 * hpasses / K,
         "poisson_checks_per_step": sum(s["n_checks"] for s in stats) / K,
         "roofline": kern.get(dominant),
         "step_roofline": {"bound": "hbm", "bytes_per_cell": step_bpc, "bytes_per_step": step_bpc * cells,
