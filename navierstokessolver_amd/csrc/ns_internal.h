@@ -7,8 +7,8 @@
 
 namespace nsg {
 
-constexpr int HALO = 5;  // ghost rows per side: K1's MUSCL stencil (2), the 2-sweep pass's cone (4),
-                         // the 2-sweep pass with fused restriction (5)
+constexpr int HALO = 6;  // ghost rows per side: K1's MUSCL stencil (2), the 2-sweep pass's cone (4),
+                         // the 2-sweep pass with fused restriction (5), the 3-sweep pass (6)
 
 // Non-rectangular domains (polygons with holes / steps, Grid.cpp:131-185): one int32 code per
 // cell of the bounding box, in a plane laid out like the fields (halo rows included):

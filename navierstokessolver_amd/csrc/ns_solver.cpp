@@ -119,6 +119,7 @@ struct ns_solver {
     int helm_batch0 = 4, pois_batch0 = 8;
     int helm_next = 4;           // first Helmholtz batch of the next step (adaptive unless check_every)
     int helm_adapt = 1;
+    bool triple = true;          // 3-sweep passes allowed on this decomposition (slabs >= 2*HALO rows)
     bool sweep3 = true;          // single rank: odd Helmholtz batches start with a 3-sweep pass (k_sweep3)
     int helm_probe = 0;          // steps since the Helmholtz first-pass residual was last sampled
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
@@ -462,26 +463,33 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
         int k = 0, launch = 0;
         while (k < n) {
             // sweeps per pass: pairs (single sweeps with NSGPU_SWEEP=tiled), and the batch ends on
-            // a pair, whose residual is its output's.  One rank: 3-sweep passes while >= 5 remain
-            // (7 = 3+2+2, 8 = 3+3+2, 11 = 3+3+3+2: a third fewer HBM passes); an odd remainder of
-            // >= 3 otherwise starts with a single sweep (multi-rank 7 = 1+2+2+2) -- the same sweeps,
-            // bit-identical values.  A probing first pass stays a pair (2+3+2, 2+1+2+2)
+            // a pair, whose residual is its output's: 3-sweep passes while >= 5 remain (7 = 3+2+2,
+            // 8 = 3+3+2, 11 = 3+3+3+2: a third fewer HBM passes); an odd remainder of >= 3 otherwise
+            // starts with a single sweep.  Every pass equals its single sweeps bit for bit, so one
+            // rank and slabs agree.  A probing first pass stays a pair (2+3+2)
             int w = std::min(s->tiled ? 1 : 2, n - k);
             if (!s->tiled && !(launch == 0 && part_first)) {
-                if (s->sweep3 && split && n - k >= 5) w = 3;
+                if (s->sweep3 && s->triple && n - k >= 5) w = 3;
                 else if (((n - k) & 1) && n - k >= 3) w = 1;
             }
             const bool last = k + w >= n;
             double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
-            const int hw = w == 2 ? (part ? 5 : 4) : 2;
-            if (which == 3 && w == 2 && !s->tiled) {
-                // multi-rank pair pass: u and v ghost rows in one exchange, overlapped (the rhs
-                // ghost rows ride along on the solve's first pass)
+            // iterate ghost rows each pass reads: its cone (3-sweep 6, 2-sweep 4, + 1 with the
+            // residual stage; single sweep 2 -- k_sweep reads one, K1 needs two anyway)
+            const int hw = w == 3 ? 6 : (w == 2 ? (part ? 5 : 4) : 2);
+            if (which == 3 && w >= 2 && !s->tiled) {
+                // multi-rank pair / triple pass: u and v ghost rows in one exchange, overlapped
+                // (the rhs ghost rows -- 5: the 3-sweep pass's first stage -- ride along on the
+                // solve's first pass)
                 const HaloReq r[4] = {{&s->g, s->arr[NS_ARR_U], hw}, {&s->g, s->arr[NS_ARR_V], hw},
-                                      {&s->g, s->arr[NS_ARR_RU], 4}, {&s->g, s->arr[NS_ARR_RV], 4}};
+                                      {&s->g, s->arr[NS_ARR_RU], 5}, {&s->g, s->arr[NS_ARR_RV], 5}};
                 const int nr = s->helm_b_pend ? 4 : 2;
                 s->helm_b_pend = 0;
                 nb = overlapped(s, r, nr, [&]() {
+                    if (w == 3)
+                        return nsg::launch_helm_sweep3(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
+                                                       s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
+                                                       s->arr[NS_ARR_RV], s->st, 3);
                     return nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
                                                    s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
                                                    s->arr[NS_ARR_RV], part, s->st, 3);
@@ -492,7 +500,7 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
             } else {
                 if (s->helm_b_pend) {
                     s->helm_b_pend = 0;
-                    CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
+                    CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 5));
                 }
                 if (which == 3) CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, hw));
                 else if (w <= 2) CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
@@ -1649,8 +1657,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (ns_slab_range(gd->nx, p->nranks, p->rank, &i0, &i1)) return NS_EINVAL;
     g.i0 = i0;
     g.nxl = i1 - i0;
-    if (p->nranks > 1 && g.nxl < 2 * nsg::HALO) {
-        set_err("slab of %d rows is thinner than the %d-row halo exchange", g.nxl, 2 * nsg::HALO);
+    if (p->nranks > 1 && g.nxl < 2 * (nsg::HALO - 1)) {
+        set_err("slab of %d rows is thinner than the %d-row halo exchange", g.nxl, 2 * (nsg::HALO - 1));
         return NS_EINVAL;
     }
     // ConstructGhostStencils (FluidSolver.cpp:84-103) of one edge
@@ -1802,6 +1810,14 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     s->timing = p->timing;
     if (const char* e = getenv("NSGPU_SWEEP")) s->tiled = std::strcmp(e, "tiled") == 0;
     if (const char* e = getenv("NSGPU_SWEEP3")) s->sweep3 = std::atoi(e) != 0;   // A/B: pairs only
+    // the 3-sweep pass reads HALO ghost rows, which one neighbour feeds only from slabs of
+    // >= 2*HALO rows; thinner slabs (the thinnest of all ranks: a global decision) take the
+    // same sweeps as a single sweep + pairs
+    for (int q = 0; q < s->nranks && s->nranks > 1; q++) {
+        int32_t a0, a1;
+        ns_slab_range(s->g.nx, s->nranks, q, &a0, &a1);
+        if (a1 - a0 < 2 * nsg::HALO) s->triple = false;
+    }
     if (const char* e = getenv("NSGPU_FUSED_RESTRICT")) s->fuse_restrict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
@@ -2054,10 +2070,10 @@ static int step_body_(ns_solver* s, ns_stats& st) {
     CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
     // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
-    // rhs ghost rows (a checked pair pass reads ib-5): multi-rank pair passes take them with
+    // rhs ghost rows (a checked pair pass and the 3-sweep pass read ib-5): multi-rank passes take them with
     // their first overlapped exchange
     if (s->nranks > 1 && s->overlap && s->cst && !s->g.fc && !s->tiled) s->helm_b_pend = 1;
-    else CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
+    else CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 5));
     s->hn = 0;
     // the Poisson initial guess (phi extrapolation) waits to hide the Helmholtz check's host sync
     s->extrap_pending = s->phim ? 1 : 0;
@@ -2240,7 +2256,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         // single rank with the 3-sweep pass and iters >= 4: one k_sweep3 pass first; then
         // (rest-1)/2 two-sweep passes, then single sweeps; the residual is of the last sweep's input
         int nb = 0;
-        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 5));
         const int three = (s->sweep3 && s->nranks == 1 && !s->tiled && iters >= 4) ? 3 : 0;
         if (three) helm_sweep3(s, alpha, 1), helm_sweep3(s, alpha, 2);
         const int pairs = iters - three > 0 ? (iters - three - 1) / 2 : 0;
@@ -2302,7 +2318,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         int its = 0;
         double ru = 0, rv = 0;
         CHK(helm_bnorm(s));
-        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 4));
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 5));
         CHK(helm_solve(s, &its, &ru, &rv));
         if (out) { out[0] = its; out[1] = std::max(ru, rv); }
         return 0;

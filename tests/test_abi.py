@@ -83,8 +83,8 @@ def test_bad_slab_arguments_rejected():
 
 def test_device_bytes():
     # NS_NUM_ARR planes of (rows + 8 ghost rows) x ld doubles
-    assert L.lib().ns_device_bytes(4096, 4096) == 11 * (4096 + 2 * 5) * 4096 * 8
-    assert L.lib().ns_device_bytes(10, 33) == 11 * (10 + 2 * 5) * 128 * 8
+    assert L.lib().ns_device_bytes(4096, 4096) == 11 * (4096 + 2 * 6) * 4096 * 8
+    assert L.lib().ns_device_bytes(10, 33) == 11 * (10 + 2 * 6) * 128 * 8
 
 
 def test_nccl_unique_id_size():
