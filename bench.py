@@ -41,7 +41,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level 
 # The one with the largest total time per step is `roofline` (the dominant kernel).
 KERNELS = {
     "restrict": ("k_sweep2<Poisson, FUSE_R> (finest pre-smoothing pass: 2 RB sweeps + residual + restriction)", 28),
-    "prolong": ("k_sweep2<Poisson, FUSE_P> (finest post-smoothing pass: prolongation + 2 RB sweeps)", 26),
+    "prolong": ("k_sweep2<Poisson, FUSE_P> (finest post-smoothing pass: prolongation + 2 RB sweeps + output residual)", 26),
     "helmholtz": ("k_sweep2<Helmholtz> (2 RB-SOR sweeps of one velocity component of (I - a L_V) u* = RHS)", 24),
 }
 JACOBI_LABEL = "k_jacobi_s<double> (one weighted-Jacobi sweep of the Poisson operator, the north star's roofline kernel)"
@@ -215,15 +215,15 @@ def main():
     timed = {"prolong": (sum(s["t_poisson_kernel_ms"] for s in stats), sum(s["n_poisson_kernels"] for s in stats)),
              "restrict": (sum(s["t_restrict_kernel_ms"] for s in stats), sum(s["n_restrict_kernels"] for s in stats)),
              "helmholtz": (sum(s["t_helm_kernel_ms"] for s in stats), sum(s["n_helm_kernels"] for s in stats))}
-    # finest-level sweeps: V(2,2) per cycle + the 2 pre-smoothing sweeps of the converged check
-    fine_sweeps = 4 * cycles + 2 * K
+    # finest-level sweeps: V(2,2) per cycle (the convergence check rides on each cycle's last pass)
+    fine_sweeps = 4 * cycles
     # whole-step algorithmic bytes per cell: K1 64 + K3 24 + K5 40 + the phi
     # extrapolation 32; Helmholtz 24 per pass of one component (a pass = 2 or 3 sweeps: see
-    # helm_passes); multigrid per solve (cycles + 1) FUSE_R passes at 28 and `cycles` FUSE_P
-    # passes at 26 on the finest level, x 4/3 for the coarser levels (each a quarter of the one above)
+    # helm_passes); multigrid per solve `cycles` FUSE_R passes at 28 and `cycles` FUSE_P passes
+    # at 26 on the finest level, x 4/3 for the coarser levels (each a quarter of the one above)
     hpasses = sum(helm_passes(int(s["it_u"]), world) for s in stats)
     step_bpc = (64 + 24 + 40 + 32 + 2 * 24 * hpasses / K
-                + (28 * (cycles + K) + 26 * cycles) / K * 4.0 / 3.0)
+                + (28 * cycles + 26 * cycles) / K * 4.0 / 3.0)
     if channel:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications
         # of (line extension 8 + FUSE_R 28 + FUSE_P 26, x 4/3 for the coarser levels) = 80 each,

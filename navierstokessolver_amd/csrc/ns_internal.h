@@ -163,10 +163,11 @@ int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const
                                 double* part, hipStream_t st);
 
 // the first post-smoothing pass with the prolongation fused in: phi + P(ec) enters two RB
-// sweeps -> out (phi itself is not modified); needs 5 ghost rows of phi, 3 of ec
+// sweeps -> out (phi itself is not modified); needs 5 ghost rows of phi, 3 of ec.  part != null:
+// partials of r^2 of `out` too (the V-cycle's convergence check after its last pass)
 int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                                const double* rp, const double* shift, const Geo& gc, const double* ec,
-                               hipStream_t st);
+                               double* part, hipStream_t st);
 
 // the same two passes as LDS-tiled kernels for the latency-bound small levels (one load
 // round per pass instead of a row pipeline); same results
@@ -175,7 +176,7 @@ int launch_pois_tile2_restrict(const Geo& g, const Coef& c, double omega, const 
                                double* part, hipStream_t st);
 int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                               const double* rp, const double* shift, const Geo& gc, const double* ec,
-                              hipStream_t st);
+                              double* part, hipStream_t st);
 
 // coarse levels as one LDS-resident V-cycle (single rank): level g and its 2x coarsenings
 size_t coarse_vcycle_bytes(const Geo& g);

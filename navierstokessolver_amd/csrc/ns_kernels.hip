@@ -1492,9 +1492,14 @@ constexpr int SW2X = 116;
 #ifndef SD2_FP
 #define SD2_FP 3
 #endif
+#ifndef SD2_FPR
+#define SD2_FPR 2
+#endif
 template <int OP, bool RES, int FUSE>
 constexpr int sd2_of() {
-    return FUSE == 1 ? 3 : FUSE == 2 ? SD2_FP : OP == 1 ? (RES ? SD2_HELMR : SD2_HELM) : SD2_PLAIN;
+    // (FUSE_P with the output residual: 172 VGPRs at 3 rows in flight = 2 waves/SIMD, 147 us per
+    // pass at 4096^2 against 98 without it; 2 rows keep 3 waves)
+    return FUSE == 1 ? 3 : FUSE == 2 ? (RES ? SD2_FPR : SD2_FP) : OP == 1 ? (RES ? SD2_HELMR : SD2_HELM) : SD2_PLAIN;
 }
 // FUSE_UV: no transfer fused; two fields (the multi-rank Helmholtz pair pass, u and v) in one launch
 constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2, FUSE_UV = 3;
@@ -1949,10 +1954,11 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) { sweep2_body<OP, 
 // times the workgroups and a quarter of the work per half-sweep -- these levels are latency-bound,
 // so the larger cone overhead costs nothing (128^2 / 256^2: 8.2 -> 5.4 us per FUSE_R pass, 512^2:
 // 8.8 -> 7.6 us; at 1024^2 16 x 16 tiles measured 0.3 % slower overall, so 32 stays there)
-template <int FUSE, int TT>
+template <int FUSE, int TT, bool RES = false>
 __global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
     constexpr bool XR = FUSE == FUSE_R, XP = FUSE == FUSE_P;
-    constexpr int R = XR ? 5 : 4;
+    constexpr bool R5 = XR || RES;   // the output residual (RES: FUSE_P's, partials only)
+    constexpr int R = R5 ? 5 : 4;
     constexpr int E = TT + 2 * R;
     constexpr int NQ = (E * E + 255) / 256;     // staged cells per thread
     constexpr int CE = E / 2 + 3;                // XP: staged coarse rows / columns
@@ -2075,14 +2081,18 @@ __global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
         const int li = li0 + r - R, j = j0 + cc - R;
         if (li >= a.nxl || j >= ny) continue;
         a.out[(ptrdiff_t)li * ld + j] = sp[r][cc];
-        if (XR) {
+        if (R5) {
             const double dg = diag<0>(rw[r][2], cl[cc][2], 0.0);
             double rr;
             relax<0>(sp[r][cc], sp[r - 1][cc], sp[r + 1][cc], sp[r][cc - 1], sp[r][cc + 1], sb[r][cc], rw[r][0],
                      rw[r][1], cl[cc][0], cl[cc][1], dg, 0.0, 0.0, rr);
             res += rr * rr;
-            sb[r][cc] = rr;   // this cell's own b is no longer needed
+            if (XR) sb[r][cc] = rr;   // this cell's own b is no longer needed
         }
+    }
+    if (RES && !XR && a.part) {
+        double x[1] = {res};
+        block_reduce_sum<1>(x, a.part + blockIdx.x);
     }
     if (XR) {
         __syncthreads();
@@ -3064,8 +3074,8 @@ int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const
 
 int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                                const double* rp, const double* shift, const Geo& gc, const double* ec,
-                               hipStream_t st) {
-    StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, nullptr, false);
+                               double* part, hipStream_t st) {
+    StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
     a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0; a.dsx = gc.dsx;
     // the iterate streamed non-temporally here: 113 -> 101 us at 4096^2 (b and the coarse
     // correction keep the Infinity Cache); neutral-to-worse in the other passes
@@ -3074,21 +3084,27 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
     int nblk = 0;
     // overlap depth 5, not the 4 of its fine-row cone: fine row 0 (even) reads coarse row -1,
     // whose exchange runs concurrently with the interior strips
+    // (with the output residual the fine cone is 5 rows too; the coarse one stays at 3)
+    if (part) {
+        const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2<0, true, FUSE_P>), 5, &nblk);
+        if (nblk) NS_LAUNCH((k_sweep2<0, true, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
+        return nstr;
+    }
     const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 5, &nblk);
     if (nblk) NS_LAUNCH((k_sweep2<0, false, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 
 // the LDS-tiled versions of the two launchers above (small levels); TT x TT tiles
-template <int FUSE>
+template <int FUSE, bool RES = false>
 static int launch_tile2(const StreamArgs& a, const Geo& g, hipStream_t st) {
     const int tj32 = (g.ny + 31) / 32, n32 = tj32 * ((g.nxl + 31) / 32);
     if (n32 >= 512) {
-        NS_LAUNCH((k_tile2<FUSE, 32>), dim3(n32), dim3(256), 0, st, a, tj32);
+        NS_LAUNCH((k_tile2<FUSE, 32, RES>), dim3(n32), dim3(256), 0, st, a, tj32);
         return n32;
     }
     const int tj = (g.ny + 15) / 16, n = tj * ((g.nxl + 15) / 16);
-    NS_LAUNCH((k_tile2<FUSE, 16>), dim3(n), dim3(256), 0, st, a, tj);
+    NS_LAUNCH((k_tile2<FUSE, 16, RES>), dim3(n), dim3(256), 0, st, a, tj);
     return n;
 }
 
@@ -3102,10 +3118,10 @@ int launch_pois_tile2_restrict(const Geo& g, const Coef& c, double omega, const 
 
 int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                               const double* rp, const double* shift, const Geo& gc, const double* ec,
-                              hipStream_t st) {
-    StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, nullptr, false);
+                              double* part, hipStream_t st) {
+    StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
     a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0; a.dsx = gc.dsx;
-    return launch_tile2<FUSE_P>(a, g, st);
+    return part ? launch_tile2<FUSE_P, true>(a, g, st) : launch_tile2<FUSE_P>(a, g, st);
 }
 
 int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,

@@ -907,11 +907,15 @@ int mg_coarse(ns_solver* s) {
 }
 
 // one V-cycle (pre-smoothing + restriction down to the coarsest level, the coarse solve,
-// prolongation + post-smoothing back up).  `check(nb)` runs after the finest level's
-// restriction pass (r^2 partials of the finest residual in s->part, nb of them) and returns
-// 1 to end the solve there, 0 to go on, < 0 on error; the preconditioner passes none.
+// prolongation + post-smoothing back up).  With `want_check`, `check(nb)` runs after the
+// finest level's last post-smoothing pass (r^2 partials of the cycle's output residual in
+// s->part, nb of them: the fused prolongation pass computes them in the same HBM pass) and
+// returns 1 to end the solve there, 0 to go on, < 0 on error; the preconditioner asks for none.
+// (Round 1-2 checked after the NEXT cycle's fused restriction pass, so a converged solve paid
+// one restriction pass it then discarded; two more RB sweeps shrink a cycle's output residual
+// only ~1.2x -- the post-smoothed residual is smooth -- so the counts stay the same.)
 template <class Check>
-int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
+int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool want_check, bool* done) {
     const int nl = (int)s->lv.size();
     *done = false;
     for (int l = 0; l < nl - 1; l++) {
@@ -953,17 +957,14 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
             CHK(halo_l(s, l, {F.phi}, 1));
             nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, sh, cv.g, C.c, cv.b, cv.phi, s->part, s->st);
         }
-        if (l == 0) {
-            const int rc = check(nb);
-            if (rc < 0) return rc;
-            if (rc > 0) { *done = true; return 0; }
-        }
+        (void)nb;   // (the restriction's partials: the pre-smoothed residual, unused)
         if (cv.gather) CHK(gather_level(s, C));
         else if (s->nranks > 1 && s->overlap && s->cst && !C.repl && fused_restrict(s, l + 1) && !tile_level(s, l + 1))
             C.b_pend = true;   // sent with level l+1's FUSE_R exchange
         else CHK(halo_l(s, l + 1, {C.b}, 4));
     }
     CHK(mg_coarse(s));
+    int nb_out = -1;   // partials of the finest level's output residual (-1: none yet)
     for (int l = nl - 2; l >= 0; l--) {
         MgLevel& F = level(s, l);
         MgLevel& C = level(s, l + 1);
@@ -973,23 +974,27 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
             // and fine ghost rows travel in one group
             const bool t = s->timing && l == 0 && (!s->pc_active || s->pc_timing);
             const double* shp = l == 0 ? shift0(s) : nullptr;
+            // the finest level's last pass also sums its output residual (the convergence check)
+            double* pp = (l == 0 && want_check && s->mg_post == 2) ? s->part : nullptr;
             auto pass = [&]() {
                 return (tile_level(s, l) ? nsg::launch_pois_tile2_prolong : nsg::launch_pois_rbsor2_prolong)(
-                    F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, shp, cv.g, cv.phi, s->st);
+                    F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, shp, cv.g, cv.phi, pp, s->st);
             };
             if (t) { CHK(t_begin(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); s->evtag[ev0 + *tn] = 0; }
+            int n;
             if (F.repl) {
-                pass();
+                n = pass();
             } else if (tile_level(s, l)) {
                 if (cv.gather || C.repl) CHK(halo_l(s, l, {F.phi}, 5));
                 else CHK(halo_reqs(s, {HaloReq{&C.g, C.phi, 3}, HaloReq{&F.g, F.phi, 5}}));
-                pass();
+                n = pass();
             } else {
                 // (the coarse ghost rows are read by the edge strips only)
                 const HaloReq r[2] = {{&F.g, F.phi, 5}, {&C.g, C.phi, 3}};
-                const int n = overlapped(s, r, (cv.gather || C.repl) ? 1 : 2, pass);
+                n = overlapped(s, r, (cv.gather || C.repl) ? 1 : 2, pass);
                 if (n < 0) return n;
             }
+            if (pp) nb_out = n;
             if (t) { CHK(t_end(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); (*tn)++; }
             std::swap(F.phi, F.tmp);
             if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
@@ -1000,13 +1005,27 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool* done) {
             CHK(mg_smooth(s, l, s->mg_post, tn, ev0));
         }
     }
+    if (want_check && nl > 1) {
+        if (nb_out < 0) {
+            // (unfused or longer post-smoothing: the residual by a restriction pass of its own,
+            // whose coarse output the next cycle's restriction overwrites)
+            MgLevel& F = level(s, 0);
+            const CoarseView cv = coarse_view(s, 0);
+            CHK(halo_l(s, 0, {F.phi}, 1));
+            nb_out = nsg::launch_restrict(F.g, F.c, F.phi, F.b, shift0(s), cv.g, level(s, 1).c, cv.b, cv.phi,
+                                          s->part, s->st);
+        }
+        const int rc = check(nb_out);
+        if (rc < 0) return rc;
+        if (rc > 0) *done = true;
+    }
     return 0;
 }
 
 int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     const double tol2 = s->rtol * s->rtol;
     const int maxc = std::min(s->max_iters, 1000);
-    int cycles = 0, tn = 0, nchk = 0;
+    int cyc = 0, tn = 0, nchk = 0;   // cyc: V-cycles done before the current one
     double tms = 0.0;
     const int per_cycle = s->mg_pre + s->mg_post;
     // residual checks (host syncs): after cycle 0, then where the contraction rate (measured
@@ -1026,8 +1045,9 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     // speculate at the first check when the last four solves all converged by then
     const bool spec_ok = s->speculate && s->in_step && s->mg_predict && s->rp_c < 0 && next_chk > 0;
     auto check = [&](int nb) -> int {
+        const int cycles = cyc + 1;   // complete cycles (this check ends one)
         if (!(cycles >= next_chk || cycles >= maxc)) return 0;
-        // fine residual after pre-smoothing: the convergence test (a host sync)
+        // the cycle's output residual: the convergence test (a host sync)
         nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
         CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
         const bool spec = spec_ok && nchk == 0;
@@ -1055,7 +1075,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
         }
         const double r2 = s->hs[S_RES], b2 = s->hs[S_SHIFT + 1];
         *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
-        if (s->verbose) fprintf(stderr, "nsgpu poisson: cycle %d rel. residual after pre-smoothing %.3e\n", cycles, *res);
+        if (s->verbose) fprintf(stderr, "nsgpu poisson: after %d V-cycles rel. residual %.3e\n", cycles, *res);
         if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); *its = cycles; return NS_EDIVERGE; }
         if (r2 <= tol2 * b2 || r2 == 0.0 || cycles >= maxc || s->rp_c >= 0) {
             if (spec) { s->k5_spec = 1; s->n_spec_hit++; }
@@ -1085,10 +1105,11 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     for (;;) {
         if (s->timing) CHK(ensure_events(s, 2 * (size_t)(tn + per_cycle + 2)));
         bool done = false;
-        CHK(mg_vcycle(s, &tn, 0, check, &done));
+        CHK(mg_vcycle(s, &tn, 0, check, true, &done));
+        cyc++;
         if (done) break;
-        cycles++;
     }
+    const int cycles = cyc;
     *its = cycles;
     // history: the cycle count this solve needed -- one fewer when its only check came with a
     // full cycle's contraction to spare (the earlier check point would have passed too)
@@ -1153,7 +1174,7 @@ int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch, int* tn = 
     int tn0 = 0;
     if (tn) CHK(ensure_events(s, 2 * ((size_t)*tn + 2 * (s->mg_pre + s->mg_post) + 4)));
     bool done = false;
-    const int rc = mg_vcycle(s, tn ? tn : &tn0, 0, [](int) { return 0; }, &done);
+    const int rc = mg_vcycle(s, tn ? tn : &tn0, 0, [](int) { return 0; }, false, &done);
     s->pc_active = false;
     s->pc_timing = false;
     // (level 0's own pointer: a single-level hierarchy relaxes it in mg_coarse, which does not

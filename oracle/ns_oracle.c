@@ -1110,13 +1110,11 @@ int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre
         int done = 0;
         for (int l = 0; l < nl - 1; l++) {
             for (int k = 0; k < pre; k++) mg_rb(&L[l], xf, bf, 0.0, omega);
-            const double r2 = mg_restrict_lv(&L[l], xf, bf, 0.0, &L[l + 1], L[l + 1].b);
+            mg_restrict_lv(&L[l], xf, bf, 0.0, &L[l + 1], L[l + 1].b);
             memset(L[l + 1].x, 0, sizeof(double) * (size_t)L[l + 1].nx * L[l + 1].ny);
-            if (l == 0 && (r2 <= rtol * rtol * b2 || r2 == 0.0 || cycles >= maxcycles)) { done = 1; break; }
             xf = L[l + 1].x;
             bf = L[l + 1].b;
         }
-        if (done) break;
         if (Md) {
             for (int r = 0; r < ncell; r++) {
                 double x = 0.0;
@@ -1133,6 +1131,11 @@ int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre
             for (int k = 0; k < post; k++) mg_rb(&L[l], xl, bl, 0.0, omega);
         }
         cycles++;
+        /* the convergence test on the cycle's output residual (the GPU's fused prolongation
+         * pass sums it; the restriction written here is overwritten by the next cycle's) */
+        const double r2 = mg_restrict_lv(&L[0], x, rhs, 0.0, &L[1], L[1].b);
+        if (r2 <= rtol * rtol * b2 || r2 == 0.0 || cycles >= maxcycles) done = 1;
+        if (done) break;
     }
     free(Md);
     mg_free(L, nl);
