@@ -89,12 +89,12 @@ def _host_threads():
 
 
 def helm_passes(n, world):
-    """HBM passes of one component's n Helmholtz sweeps (ns_solver.cpp helm_sweeps): one rank
-    takes 3-sweep passes while >= 5 remain and ends on a pair (7 = 3+2+2); slabs take an odd
-    remainder as a single sweep first, then pairs (7 = 1+2+2+2)."""
+    """HBM passes of one component's n Helmholtz sweeps (ns_solver.cpp helm_sweeps): 3-sweep
+    passes while >= 5 remain, ending on a pair (5 = 3+2, 7 = 3+2+2; slabs too, unless thinner
+    than 12 rows); an odd remainder otherwise starts with a single sweep."""
     p, r = 0, n
     while r > 0:
-        if world == 1 and r >= 5:
+        if r >= 5:
             w = 3
         elif r % 2 and r >= 3:
             w = 1
@@ -222,7 +222,10 @@ def main():
     # helm_passes); multigrid per solve `cycles` FUSE_R passes at 28 and `cycles` FUSE_P passes
     # at 26 on the finest level, x 4/3 for the coarser levels (each a quarter of the one above)
     hpasses = sum(helm_passes(int(s["it_u"]), world) for s in stats)
-    step_bpc = (64 + 24 + 40 + 32 + 2 * 24 * hpasses / K
+    # the Helmholtz wall bands (k_helm_band + its copy-back) on the cells within 32 of a wall:
+    # u, v read 16 + rhs 16 + write 16, copy 32 -> 80 B per band cell
+    band_frac = 1.0 - max(n - 64, 0) * max(nyc - 64, 0) / float(n * nyc)
+    step_bpc = (64 + 24 + 40 + 32 + 2 * 24 * hpasses / K + 80 * band_frac
                 + (28 * cycles + 26 * cycles) / K * 4.0 / 3.0)
     if channel:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications

@@ -161,6 +161,8 @@ typedef struct ns_stats {
 #define NS_K_RESIDUAL   8  /* Poisson residual ||rhs - mean - L phi||^2 -> out[0] (no update) */
 #define NS_K_POISSON32  9  /* K4 Jacobi x iters on fp32 copies of phi, rhs_phi (fp64 arithmetic and residual,
                               SURVEY.md 8(d) C5); phi <- the fp32 result widened */
+#define NS_K_HELM_BAND 10  /* the Helmholtz solve's wall-band relaxation of u, v (k_helm_band: 3 RB-SOR sweeps
+                              on the cells within 32 of a wall, the rest held); no output */
 
 /* ---- lifecycle: FluidSolver(char*, Grid*) = SolverInitialize + SolverSetup (FluidSolver.cpp:8-58) ---- */
 int  ns_create(const ns_grid_desc* grid, const ns_params* params, ns_solver** out);

@@ -22,7 +22,7 @@ NS_POISSON_RBSOR, NS_POISSON_JACOBI, NS_POISSON_MG = 0, 1, 2
  NS_ARR_TMP, NS_ARR_TMPU, NS_ARR_TMPV) = range(11)
 NS_NUM_ARR = 11
 (NS_K_RHS, NS_K_HELMHOLTZ, NS_K_DIV, NS_K_POISSON, NS_K_CORRECT, NS_K_HELM_SOLVE,
- NS_K_POIS_SOLVE, NS_K_RESIDUAL, NS_K_POISSON32) = range(1, 10)
+ NS_K_POIS_SOLVE, NS_K_RESIDUAL, NS_K_POISSON32, NS_K_HELM_BAND) = range(1, 11)
 
 
 class NsEdge(ctypes.Structure):

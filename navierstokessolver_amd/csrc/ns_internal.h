@@ -92,6 +92,10 @@ void launch_to_f64(const Geo& g, const float* src, double* dst, hipStream_t st);
 int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st);
 // K2: three RB-SOR sweeps per pass (k_sweep3; no residual partials); which as above
+// the Helmholtz wall-band relaxation (k_helm_band): 3 RB-SOR sweeps of u and v restricted to the
+// cells within 32 of a wall, every other cell held; uo / vo are scratch; returns the tile count
+int launch_helm_band(const Geo& g, const Coef& c, double alpha, double omega, double* u, double* v, double* uo,
+                     double* vo, const double* ru, const double* rv, hipStream_t st);
 int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
                        double* uo, double* vo, const double* ru, const double* rv, hipStream_t st, int which);
 int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,

@@ -1473,6 +1473,7 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
 // come from the adjacent lanes (the outermost lanes' missing neighbours fall outside
 // the written cone of the same 116-column layout).
 constexpr int SW2 = 120;
+constexpr int BAND_W = 32, BAND_SWEEPS = 3, BT = 32;   // Helmholtz wall bands (k_helm_band)
 constexpr int SW2X = 116;
 // rows in flight per wave (prefetch depth) per pass type: each row costs 8 VGPRs (phi, b);
 // the Helmholtz pass (136 VGPRs at 3 rows) and FUSE_P (154) stay at 3 waves/SIMD up to 168
@@ -2113,6 +2114,121 @@ __global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
             double x[1] = {res};
             block_reduce_sum<1>(x, a.part + blockIdx.x);
         }
+    }
+}
+
+// ------------------------------------------------ K2 wall bands (before the global Helmholtz passes)
+// The Helmholtz residual of the guess u^n lives in thin layers along the walls -- the lid's and
+// the side walls' boundary layers: at 4096^2 > 99.9 % of ||r||^2 lies within 16 cells of a wall
+// -- where the global RB-SOR sweeps converge at their asymptotic rate.  BAND_SWEEPS RB-SOR
+// sweeps restricted to the cells within BAND_W of a wall (every other cell held) first cut the
+// global sweeps rtol 1e-8 needs from 7 to 4 (u) / 5 (v) at 4096^2 (tools/helm_band_study.py):
+// two HBM passes per component (3 + 2) instead of three (3 + 2 + 2), for two launches over
+// ~3 % of the cells.  One workgroup per BT x BT tile that touches the band stages the tile and
+// its dependency cone (one cell per half-sweep: 2 BAND_SWEEPS) in LDS -- k_tile2's temporal
+// blocking -- so its band cells come out exactly as from the global masked sweeps, whatever the
+// tiling (one rank and slabs agree).  They go to `out`; k_band_copy moves them back into the
+// iterate (in place, a tile would race with its neighbours' cones).  Same arithmetic as the
+// streaming passes (relax<1>, diag<1>, the Newton reciprocal).  blockIdx.y: 0 u, 1 v.
+struct BandTiles {
+    int nti, ntj;   // tiles of the slab: rows, columns
+    int fa, fb;     // tile rows [0, fa) and [fb, nti) touch the W / E bands: every column
+    int ncl, ncr;   // other tile rows: columns [0, ncl) and [ncr, ntj) only
+};
+__device__ __forceinline__ void band_tile(int b, const BandTiles& t, int& ti, int& tj) {
+    const int nf = t.fa * t.ntj, nl = (t.nti - t.fb) * t.ntj;
+    if (b < nf) { ti = b / t.ntj; tj = b - ti * t.ntj; return; }
+    b -= nf;
+    if (b < nl) { ti = t.fb + b / t.ntj; tj = b - (b / t.ntj) * t.ntj; return; }
+    b -= nl;
+    const int k = t.ncl + t.ntj - t.ncr, c = b % k;
+    ti = t.fa + b / k;
+    tj = c < t.ncl ? c : t.ncr + (c - t.ncl);
+}
+__device__ __forceinline__ bool in_band(int gi, int j, int nx, int ny) {
+    return gi < BAND_W || gi >= nx - BAND_W || j < BAND_W || j >= ny - BAND_W;
+}
+
+__global__ __launch_bounds__(256) void k_helm_band(StreamArgs a, BandTiles bt) {
+    constexpr int R = 2 * BAND_SWEEPS, E = BT + 2 * R;
+    constexpr int NQ = (E * E + 255) / 256;
+    __shared__ double sp[E][E];
+    __shared__ double sb[E][E];
+    __shared__ double rw[E][3];   // per staged row: cw, ce, cw + ce + bx
+    __shared__ double cl[E][3];   // per staged column: cs, cn, cs + cn + by
+    int ti, tj;
+    band_tile(blockIdx.x, bt, ti, tj);
+    const double* in = blockIdx.y ? a.in2 : a.in;
+    const double* b = blockIdx.y ? a.b2 : a.b;
+    double* out = blockIdx.y ? a.out2 : a.out;
+    const int li0 = ti * BT, j0 = tj * BT, ld = a.ld, ny = a.ny, nx = a.nx;
+    const int rlo = -HALO, rhi = a.nxl + HALO - 1;
+    double pv[NQ], bv[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const int q = threadIdx.x + 256 * k;
+        if (q < E * E) {
+            const int r = q / E, cc = q - r * E;
+            const int li = min(max(li0 - R + r, rlo), rhi);
+            const int j = min(max(j0 - R + cc, 0), ny - 1);
+            pv[k] = in[(ptrdiff_t)li * ld + j];
+            bv[k] = b[(ptrdiff_t)li * ld + j];
+        }
+    }
+    if (threadIdx.x < E) {
+        const int gi = min(max(a.i0 + li0 - R + (int)threadIdx.x, 0), nx - 1);
+        const double cw = a.cw[gi], ce = a.ce[gi];
+        rw[threadIdx.x][0] = cw; rw[threadIdx.x][1] = ce; rw[threadIdx.x][2] = cw + ce + a.bx[gi];
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + E) {
+        const int q = threadIdx.x - 64;
+        const int j = min(max(j0 - R + q, 0), ny - 1);
+        const double cs = a.cs[j], cn = a.cn[j];
+        cl[q][0] = cs; cl[q][1] = cn; cl[q][2] = cs + cn + a.by[j];
+    }
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const int q = threadIdx.x + 256 * k;
+        if (q < E * E) {
+            sp[q / E][q % E] = pv[k];
+            sb[q / E][q % E] = bv[k];
+        }
+    }
+    __syncthreads();
+    const double alpha = a.alpha, omega = a.omega;
+    const int gib = a.i0 + li0 - R, jb = j0 - R;   // global row / column of staged (0, 0)
+    for (int h = 0; h < R; h++) {
+        const int par = h & 1;                      // red ((gi + j) even), black, ...
+        const int W = E - 2 - 2 * h;                // the half-sweep's region: [h+1, E-2-h]^2
+        for (int q = threadIdx.x; q < W * W; q += 256) {
+            const int r = h + 1 + q / W, cc = h + 1 + q % W;
+            const int gi = gib + r, j = jb + cc;
+            if (((gi + j) & 1) != par || gi < 0 || gi >= nx || j < 0 || j >= ny || !in_band(gi, j, nx, ny)) continue;
+            const double d = diag<1>(rw[r][2], cl[cc][2], alpha), w = omega * rcp_nr(d);
+            double rr;
+            sp[r][cc] = relax<1>(sp[r][cc], sp[r - 1][cc], sp[r + 1][cc], sp[r][cc - 1], sp[r][cc + 1], sb[r][cc],
+                                 rw[r][0], rw[r][1], cl[cc][0], cl[cc][1], d, w, alpha, rr);
+        }
+        __syncthreads();
+    }
+    for (int q = threadIdx.x; q < BT * BT; q += 256) {
+        const int r = R + q / BT, cc = R + q % BT;
+        const int li = li0 + r - R, j = j0 + cc - R;
+        if (li >= a.nxl || j >= ny || !in_band(a.i0 + li, j, nx, ny)) continue;
+        out[(ptrdiff_t)li * ld + j] = sp[r][cc];
+    }
+}
+
+// the band cells of each tile: out -> in (u: blockIdx.y 0, v: 1)
+__global__ __launch_bounds__(256) void k_band_copy(StreamArgs a, BandTiles bt) {
+    int ti, tj;
+    band_tile(blockIdx.x, bt, ti, tj);
+    double* dst = const_cast<double*>(blockIdx.y ? a.in2 : a.in);
+    const double* src = blockIdx.y ? a.out2 : a.out;
+    for (int q = threadIdx.x; q < BT * BT; q += 256) {
+        const int li = ti * BT + q / BT, j = tj * BT + q % BT;
+        if (li >= a.nxl || j >= a.ny || !in_band(a.i0 + li, j, a.nx, a.ny)) continue;
+        const ptrdiff_t o = (ptrdiff_t)li * a.ld + j;
+        dst[o] = src[o];
     }
 }
 
@@ -3127,6 +3243,32 @@ int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const d
 int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st) {
     return launch_stream2<0>(stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false), g, st);
+}
+
+// the Helmholtz wall-band relaxation of u and v (k_helm_band + k_band_copy); uo / vo: scratch
+// planes (their band cells are overwritten); needs 6 ghost rows of u, v and 5 of ru, rv
+int launch_helm_band(const Geo& g, const Coef& c, double alpha, double omega, double* u, double* v, double* uo,
+                     double* vo, const double* ru, const double* rv, hipStream_t st) {
+    StreamArgs a = stream_args(g, c, u, uo, ru, nullptr, alpha, omega, nullptr, true);
+    a.in2 = v; a.out2 = vo; a.b2 = rv;
+    BandTiles t{};
+    t.nti = (g.nxl + BT - 1) / BT;
+    t.ntj = (g.ny + BT - 1) / BT;
+    auto full = [&](int ti) {   // the tile row touches the W or E band
+        const int lo = g.i0 + ti * BT, hi = std::min(g.i0 + (ti + 1) * BT, g.i0 + g.nxl);
+        return lo < BAND_W || hi > g.nx - BAND_W;
+    };
+    t.fa = 0;
+    while (t.fa < t.nti && full(t.fa)) t.fa++;
+    t.fb = t.nti;
+    while (t.fb > t.fa && full(t.fb - 1)) t.fb--;
+    t.ncl = std::min((BAND_W + BT - 1) / BT, t.ntj);
+    t.ncr = std::max((g.ny - BAND_W) / BT, t.ncl);
+    const int n = (t.fa + t.nti - t.fb) * t.ntj + (t.fb - t.fa) * (t.ncl + t.ntj - t.ncr);
+    if (n <= 0) return 0;
+    NS_LAUNCH(k_helm_band, dim3(n, 2), dim3(256), 0, st, a, t);
+    NS_LAUNCH(k_band_copy, dim3(n, 2), dim3(256), 0, st, a, t);
+    return n;
 }
 
 // three Helmholtz sweeps in one pass (k_sweep3; no residual): which = 1 u, 2 v, 3 both in one launch

@@ -121,6 +121,7 @@ struct ns_solver {
     int helm_adapt = 1;
     bool triple = true;          // 3-sweep passes allowed on this decomposition (slabs >= 2*HALO rows)
     bool sweep3 = true;          // single rank: odd Helmholtz batches start with a 3-sweep pass (k_sweep3)
+    bool helm_band = true;       // Helmholtz: wall-band relaxation before the global passes (k_helm_band)
     int helm_probe = 0;          // steps since the Helmholtz first-pass residual was last sampled
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
     int fuse_restrict = 1;       // NSGPU_FUSED_RESTRICT=0: separate k_restrict pass (A/B)
@@ -608,8 +609,25 @@ struct KrylovSolve {
 int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res);
 int correct_launch(ns_solver* s, double* part2);
 
+// the wall bands' relaxation before the global Helmholtz passes (k_helm_band: 3 RB-SOR sweeps of
+// u and v on the cells within 32 of a wall, the rest held; the residual of the guess u^n lives
+// there).  Slabs: the iterates' ghost rows (6: the kernel's cone) and the right-hand sides' (5)
+// first; the first global pass exchanges the relaxed iterates' rows again.
+int helm_band(ns_solver* s, double alpha) {
+    if (s->nranks > 1) {
+        const HaloReq r[4] = {{&s->g, s->arr[NS_ARR_U], 6}, {&s->g, s->arr[NS_ARR_V], 6},
+                              {&s->g, s->arr[NS_ARR_RU], 5}, {&s->g, s->arr[NS_ARR_RV], 5}};
+        CHK(halo_reqs(s, r, s->helm_b_pend ? 4 : 2));
+        s->helm_b_pend = 0;
+    }
+    nsg::launch_helm_band(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
+                          s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU], s->arr[NS_ARR_RV], s->st);
+    return 0;
+}
+
 // ---------------- Helmholtz (I - a L_V) u* = RHS_u, v* likewise (KSPSolve(uSolver), FluidSolver.cpp:547-548)
-// Initial guess u^n (in place): converged solution is the same; fewer sweeps than the reference's zero guess.
+// Initial guess u^n (in place), its wall bands relaxed first: converged solution is the same;
+// fewer sweeps than the reference's zero guess.
 int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
     const double alpha = s->dt / (2 * s->re);
     if (s->g.fc) {
@@ -624,6 +642,7 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         return 0;
     }
     const double tol2 = s->rtol * s->rtol;
+    if (s->helm_band && !s->tiled) CHK(helm_band(s, alpha));
     // first batch: what the previous step needed (consecutive steps converge alike), so a
     // step normally costs one residual check
     int sweeps = 0, batch = s->rp_h > 0 ? s->rp_h : s->helm_next, prev_at = -1;
@@ -1831,6 +1850,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     s->timing = p->timing;
     if (const char* e = getenv("NSGPU_SWEEP")) s->tiled = std::strcmp(e, "tiled") == 0;
     if (const char* e = getenv("NSGPU_SWEEP3")) s->sweep3 = std::atoi(e) != 0;   // A/B: pairs only
+    if (const char* e = getenv("NSGPU_HELM_BAND")) s->helm_band = std::atoi(e) != 0;   // A/B: no wall bands
     // the 3-sweep pass reads HALO ghost rows, which one neighbour feeds only from slabs of
     // >= 2*HALO rows; thinner slabs (the thinnest of all ranks: a global decision) take the
     // same sweeps as a single sweep + pairs
@@ -2295,6 +2315,13 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         }
         CHK(fetch(s));
         if (out) { out[0] = s->hs[S_RES]; out[1] = s->hs[S_RES + 1]; }
+        return 0;
+    }
+    case NS_K_HELM_BAND: {
+        if (s->g.fc || s->tiled) { set_err("NS_K_HELM_BAND needs a rectangle and the streaming sweeps"); return NS_EINVAL; }
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 5));
+        CHK(helm_band(s, alpha));
+        CHK(fetch(s));
         return 0;
     }
     case NS_K_DIV:

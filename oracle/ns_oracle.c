@@ -668,6 +668,36 @@ static inline double helm_rect(const og_grid* g, double a, const double* q, int 
     return s;
 }
 
+/* the GPU path's wall-band relaxation (k_helm_band, ns_kernels.hip): `sweeps` red-black SOR
+ * sweeps of u and v restricted to the cells within `w` of a wall, every other cell held (the
+ * residual of the guess u^n lies in the walls' boundary layers) */
+static void helm_band_sweeps(const og_grid* g, double a, double* u, double* v, const double* ru, const double* rv,
+                             double omega, int w, int sweeps) {
+    const int nx = g->nx, ny = g->ny;
+    for (int k = 0; k < sweeps; k++)
+        for (int color = 0; color < 2; color++)
+#pragma omp parallel for schedule(static) num_threads(og_nt)
+            for (int i = 0; i < nx; i++) {
+                const int side = i < w || i >= nx - w;
+                for (int j = (i + color) & 1; j < ny; j += 2) {
+                    if (!side && j >= w && j < ny - w) continue;
+                    double d;
+                    int c = i * ny + j;
+                    double r1 = ru[c] - helm_rect(g, a, u, i, j, &d);
+                    u[c] += omega * r1 / d;
+                    double r2v = rv[c] - helm_rect(g, a, v, i, j, &d);
+                    v[c] += omega * r2v / d;
+                }
+            }
+}
+
+int og_helm_band(const og_grid* g, double a, double* u, double* v, const double* ru, const double* rv, double omega,
+                 int w, int sweeps) {
+    if (!rect_dirichlet(g)) { set_err("band sweeps need a rectangle with Dirichlet-type faces"); return -1; }
+    helm_band_sweeps(g, a, u, v, ru, rv, omega, w, sweeps);
+    return 0;
+}
+
 /* ||ru - (I - a L_V) u||^2 and the same for v (rectangle), in one pass */
 static void helm_resid2(const og_grid* g, double a, const double* u, const double* v, const double* ru,
                         const double* rv, double* ru2, double* rv2) {
@@ -1150,6 +1180,7 @@ struct og_solver {
     double dt, re, rtol;
     int gpu_alg;
     double omega_v, omega_mg;
+    int band_w, band_sweeps;   /* GPU algorithm: the Helmholtz wall-band relaxation (0: none) */
     double *u, *v, *phi, *cu, *cv, *gx, *gy, *ru, *rv, *us, *vs, *rp;
 };
 
@@ -1166,6 +1197,11 @@ void og_solver_set_algorithm(og_solver* s, int gpu_algorithm, double omega_v, do
     s->gpu_alg = gpu_algorithm;
     s->omega_v = omega_v;
     s->omega_mg = omega_mg;
+}
+
+void og_solver_set_band(og_solver* s, int width, int sweeps) {
+    s->band_w = width;
+    s->band_sweeps = sweeps;
 }
 
 void og_solver_free(og_solver* s) {
@@ -1185,6 +1221,8 @@ int og_solver_step(og_solver* s, double* mm, int* its) {
         /* the GPU path's algorithm: RB-SOR Helmholtz from u^n, checked every sweep; MG Poisson */
         memcpy(s->us, s->u, sizeof(double) * n);
         memcpy(s->vs, s->v, sizeof(double) * n);
+        if (s->band_w > 0)
+            helm_band_sweeps(g, alpha, s->us, s->vs, s->ru, s->rv, s->omega_v, s->band_w, s->band_sweeps);
         double bu = dot(n, s->ru, s->ru), bv = dot(n, s->rv, s->rv);
         iu = 0;
         do {

@@ -126,6 +126,11 @@ void og_solver_free(og_solver* s);
  * algorithm (red-black SOR Helmholtz with omega_v, multigrid Poisson V(2,2) with the
  * red-black smoother over-relaxed by omega_mg) */
 void og_solver_set_algorithm(og_solver* s, int gpu_algorithm, double omega_v, double omega_mg);
+/* k_helm_band restated: `sweeps` RB-SOR sweeps of u and v on the cells within w of a wall */
+int og_helm_band(const og_grid* g, double a, double* u, double* v, const double* ru, const double* rv, double omega,
+                 int w, int sweeps);
+/* the GPU algorithm's Helmholtz wall-band relaxation: `sweeps` RB-SOR sweeps within `width` of a wall */
+void og_solver_set_band(og_solver* s, int width, int sweeps);
 /* one time step; mm = {umin, umax, vmin, vmax}; its = {it_u, it_v, it_phi} */
 int  og_solver_step(og_solver* s, double* mm, int* its);
 /* get / set state: u, v, phi, cu0, cv0, gx, gy (divPhi) -- any pointer may be NULL */

@@ -44,6 +44,8 @@ _SIG = {
     "og_mg_solve_w": (ctypes.c_int, [_P, _D, _D, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_double]),
     "og_solver_set_algorithm": (None, [_P, ctypes.c_int, ctypes.c_double, ctypes.c_double]),
+    "og_solver_set_band": (None, [_P, ctypes.c_int, ctypes.c_int]),
+    "og_helm_band": (ctypes.c_int, [_P, ctypes.c_double, _D, _D, _D, _D, ctypes.c_double, ctypes.c_int, ctypes.c_int]),
     "og_solver_new": (_P, [_P, ctypes.c_double, ctypes.c_double, ctypes.c_double]),
     "og_solver_free": (None, [_P]),
     "og_solver_step": (ctypes.c_int, [_P, _D, _I]),
@@ -170,6 +172,13 @@ class OGrid:
         r2 = lib().og_helmholtz_rbsor_sweep(self.h, alpha, _d(u), _d(v), _d(_f(ru)), _d(_f(rv)), omega)
         return u, v, r2
 
+    def helm_band(self, alpha, u, v, ru, rv, omega=1.0, width=32, sweeps=3):
+        """k_helm_band restated: RB-SOR sweeps of u, v on the cells within `width` of a wall."""
+        u, v = _f(u).copy(), _f(v).copy()
+        if lib().og_helm_band(self.h, alpha, _d(u), _d(v), _d(_f(ru)), _d(_f(rv)), omega, width, sweeps) != 0:
+            raise ValueError(lib().og_last_error().decode())
+        return u, v
+
     def solve_helmholtz(self, alpha, rhs, x0=None, rtol=1e-13, maxit=100000):
         x = self.z() if x0 is None else _f(x0).copy()
         it = lib().og_solve_helmholtz(self.h, alpha, _d(_f(rhs)), _d(x), rtol, maxit)
@@ -214,9 +223,13 @@ class OSolver:
         except Exception:
             pass
 
-    def use_gpu_algorithm(self, omega_v, omega_mg=1.1):
-        """RB-SOR Helmholtz + multigrid Poisson (the GPU path's algorithm; CPU baseline)."""
+    def use_gpu_algorithm(self, omega_v, omega_mg=1.1, band=(32, 3)):
+        """RB-SOR Helmholtz (after `band` = (width, sweeps) RB-SOR sweeps on the cells within
+        `width` of a wall: k_helm_band; None = no band step) + multigrid Poisson (the GPU path's
+        algorithm; CPU baseline)."""
         lib().og_solver_set_algorithm(self.h, 1, omega_v, omega_mg)
+        w, k = band if band else (0, 0)
+        lib().og_solver_set_band(self.h, w, k)
 
     def step(self):
         mm = np.zeros(4)

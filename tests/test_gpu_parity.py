@@ -435,6 +435,45 @@ def test_two_sweep_pass_equals_two_sweeps(gpu, nx, ny, op):
         assert rel(gs.get(gpu.NS_ARR_V), vv) <= 1e-12
 
 
+@pytest.mark.parametrize("nx,ny,xr,yr,bc", [(64, 64, -1, -1, BC_CAVITY), (200, 150, -1, -1, BC_CAVITY),
+                                         (300, 517, 1.003, 0.998, BC_FLOW), (97, 45, -1, -1, BC_FLOW)])
+def test_helm_band_matches_oracle(gpu, nx, ny, xr, yr, bc):
+    """The Helmholtz wall-band relaxation (k_helm_band: 3 RB-SOR sweeps of u and v on the cells
+    within 32 of a wall, 32 x 32 tiles with their 6-cell cone in LDS) = the oracle's masked
+    sweeps (og_helm_band) to 1e-12; cells off the band keep their values bit for bit."""
+    rng = np.random.default_rng(31)
+    dt, re = 1.0 / 64, 10.0
+    og, gs = pair(gpu, nx, ny, dt, re, bc, xr, yr, omega_v=1.1)
+    u, v, ru, rv = (rand(rng, nx * ny) for _ in range(4))
+    for a, x in ((gpu.NS_ARR_U, u), (gpu.NS_ARR_V, v), (gpu.NS_ARR_RU, ru), (gpu.NS_ARR_RV, rv)):
+        gs.set(a, x)
+    gs.kernel(gpu.NS_K_HELM_BAND)
+    uu, vv = og.helm_band(dt / (2 * re), u, v, ru, rv, 1.1)
+    gu, gv = gs.get(gpu.NS_ARR_U).ravel(), gs.get(gpu.NS_ARR_V).ravel()
+    assert rel(gu, uu) <= 1e-12
+    assert rel(gv, vv) <= 1e-12
+    I, J = np.meshgrid(np.arange(nx), np.arange(ny), indexing="ij")
+    far = ((I >= 32) & (I < nx - 32) & (J >= 32) & (J < ny - 32)).ravel()
+    assert np.array_equal(gu[far], u[far]) and np.array_equal(gv[far], v[far])
+
+
+def test_helm_band_cuts_sweeps(gpu, monkeypatch):
+    """The wall bands first: the same converged steps (rtol 1e-10) in fewer global Helmholtz
+    sweeps than from the plain guess u^n (NSGPU_HELM_BAND=0) at the bench's 4096^2 (at 512^2 the
+    counts are equal: a smaller a/h^2 converges in fewer sweeps either way)."""
+    n, steps = 4096, 3
+    out = {}
+    for band in ("1", "0"):
+        monkeypatch.setenv("NSGPU_HELM_BAND", band)
+        gs = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0, rtol=1e-10)
+        st = [gs.step() for _ in range(steps)]
+        out[band] = (sum(s["it_u"] for s in st), gs.fields())
+        gs.close()
+    assert out["1"][0] < out["0"][0], (out["1"][0], out["0"][0])
+    for a, b in zip(out["1"][1][:2], out["0"][1][:2]):
+        assert np.max(np.abs(a - b)) <= 1e-8
+
+
 @pytest.mark.parametrize("nx,ny", [(256, 192), (96, 160)])
 def test_fused_transfer_passes_match_separate_transfers(gpu, monkeypatch, nx, ny):
     """The last pre-smoothing pass with the restriction fused in (k_sweep2 FUSE_R) and the first
