@@ -92,12 +92,17 @@ void launch_to_f64(const Geo& g, const float* src, double* dst, hipStream_t st);
 int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                        const double* rp, const double* shift, double* part, hipStream_t st);
 // K2: three RB-SOR sweeps per pass (k_sweep3; no residual partials); which as above
-// the Helmholtz wall-band relaxation (k_helm_band): 3 RB-SOR sweeps of u and v restricted to the
-// cells within 32 of a wall, every other cell held; uo / vo are scratch; returns the tile count
-int launch_helm_band(const Geo& g, const Coef& c, double alpha, double omega, double* u, double* v, double* uo,
-                     double* vo, const double* ru, const double* rv, hipStream_t st);
+// one launch of the Helmholtz wall-band relaxation (k_helm_band): 3 RB-SOR sweeps of u and v
+// restricted to the cells within bw of a wall, every other cell held; the band cells are read from
+// qu / qv and written to ou / ov, the others read from u / v; copy != 0: the band cells qu / qv ->
+// ou / ov instead.  Needs 6 ghost rows of u, v, qu, qv and 5 of ru, rv; returns the tile count
+int launch_helm_band(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                     const double* qu, const double* qv, double* ou, double* ov, const double* ru, const double* rv,
+                     int bw, int copy, hipStream_t st);
+// part != null: the pass also sums its output's residual (one field, one rank; < 0 otherwise)
 int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
-                       double* uo, double* vo, const double* ru, const double* rv, hipStream_t st, int which);
+                       double* uo, double* vo, const double* ru, const double* rv, hipStream_t st, int which,
+                       double* part = nullptr);
 int launch_helm_sweep2(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
                        double* uo, double* vo, const double* ru, const double* rv, double* part, hipStream_t st,
                        int which = 3);

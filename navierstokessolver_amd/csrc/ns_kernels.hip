@@ -988,7 +988,7 @@ struct DiagCache {
 // critical path (hipcc cannot prove the tables read-only against the `out` stores)
 constexpr int RC_OFF = 5;            // table row of strip row ib
 constexpr int RC_MAX = 64 + 2 * RC_OFF;  // L <= 64
-constexpr int RC_OFF3 = 5;           // k_sweep3: its first stage reads rows ib-5 .. ie+4 too
+constexpr int RC_OFF3 = 6;           // k_sweep3: its first stage reads rows ib-5 .. ie+4 (ib-6 .. ie+5 with RES)
 constexpr int RC_MAX3 = 64 + 2 * RC_OFF3;
 template <int OP, int RCO = RC_OFF>
 __device__ __forceinline__ void stage_rows(const StreamArgs& a, double (*rc)[4], int ib, int lane) {
@@ -1473,7 +1473,7 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
 // come from the adjacent lanes (the outermost lanes' missing neighbours fall outside
 // the written cone of the same 116-column layout).
 constexpr int SW2 = 120;
-constexpr int BAND_W = 32, BAND_SWEEPS = 3, BT = 32;   // Helmholtz wall bands (k_helm_band)
+constexpr int BT = 32;   // Helmholtz wall bands (k_helm_band): tile size
 constexpr int SW2X = 116;
 // rows in flight per wave (prefetch depth) per pass type: each row costs 8 VGPRs (phi, b);
 // the Helmholtz pass (136 VGPRs at 3 rows) and FUSE_P (154) stay at 3 waves/SIMD up to 168
@@ -1774,29 +1774,36 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
 // operator only, no residual stage (the pass is never a batch's last: helm_sweeps), strips of
 // 116 written columns (a 6-column cone on each side), rows ib-6 .. ie+5 read; every value is
 // the same arithmetic as three single sweeps (bit-identical).  FUSE_UV: u and v in one launch.
-template <int DIR>
-__device__ __forceinline__ void sweep3_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
-                                             int lane) {
+// RES: a seventh stage at row r-7 takes the residual of the finished values (the batch's last
+// pass: its partials of r^2 per strip are the convergence check's); the cone grows by one cell:
+// rows ib-7 .. ie+6, 112 written columns (SW3R), 7 ghost rows -- one rank only (HALO = 6)
+constexpr int SW3R = SW2X - 4;
+template <int DIR, bool RES>
+__device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
+                                               int lane) {
     constexpr int SD3 = 2;   // rows in flight: 3 would need 174 VGPRs (2 waves/SIMD), or spill at 168 (measured equal)
-    const int jb = sj * SW2X;
+    constexpr int EXT = RES ? 1 : 0;
+    const int jb = sj * (RES ? SW3R : SW2X);
     const int ny = a.ny, ld = a.ld;
-    const int c0 = jb - 6 + 2 * lane, c1 = c0 + 1;
+    const int c0 = jb - 6 - 2 * EXT + 2 * lane, c1 = c0 + 1;
     const int lc = min(max(c0, 0), ld - 2);
     const bool v0 = c0 >= 0 && c0 < ny, v1 = c1 >= 0 && c1 < ny;
-    const bool wr = lane >= 3 && lane <= 60 && c0 < ny;
+    const bool wr = lane >= 3 + EXT && lane <= 60 - EXT && c0 < ny;
+    const bool o0 = wr && v0, o1 = wr && v1;
+    double res = 0.0;
     const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
     const double cs0 = a.cs[k0], cn0 = a.cn[k0], cd0 = cs0 + cn0 + a.by[k0];
     const double cs1 = a.cs[k1], cn1 = a.cn[k1], cd1 = cs1 + cn1 + a.by[k1];
     const double alpha = a.alpha, omega = a.omega;
     const int rlo = -HALO, rhi = a.nxl + HALO - 1;
-    const int rb = __builtin_amdgcn_readfirstlane(ib - 1);
+    const int rb = __builtin_amdgcn_readfirstlane(ib - 1 - EXT);
     const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
-        a.out + (ptrdiff_t)rb * ld, (short)0, (int)((unsigned)(a.L + 2) * ld * 8u), 0x00020000);
+        a.out + (ptrdiff_t)rb * ld, (short)0, (int)((unsigned)(a.L + 2 + 2 * EXT) * ld * 8u), 0x00020000);
     double2 Q[SD3], QB[SD3];
-    // q rows ib-6 .. ie+5 and b rows ib-5 .. ie+4 (the first red stage's) are read
-    const int r0 = ib - 6, r1 = ie + 5;
+    // q rows ib-6-EXT .. ie+5+EXT and b rows ib-5-EXT .. ie+4+EXT (the first red stage's) are read
+    const int r0 = ib - 6 - EXT, r1 = ie + 5 + EXT;
     const int phi_lo = DIR > 0 ? rlo : max(r0, rlo), phi_hi = DIR > 0 ? min(r1, rhi) : rhi;
-    const int b_lo = DIR > 0 ? max(ib - 5, rlo) : rlo, b_hi = DIR > 0 ? rhi : min(ie + 4, rhi);
+    const int b_lo = DIR > 0 ? max(ib - 5 - EXT, rlo) : rlo, b_hi = DIR > 0 ? rhi : min(ie + 4 + EXT, rhi);
     auto load = [&](int slot_r, double2& p, double2& bb) {
         const int lp = min(max(slot_r, phi_lo), phi_hi), lb = min(max(slot_r - DIR, b_lo), b_hi);
         p = ld_stream(a.in + (ptrdiff_t)lp * ld + lc, 0);
@@ -1809,7 +1816,8 @@ __device__ __forceinline__ void sweep3_strip(const StreamArgs& a, const double (
     double2 E0 = {0, 0}, E1 = {0, 0}, E2 = {0, 0};
     double2 G0 = {0, 0}, G1 = {0, 0}, G2 = {0, 0};
     double2 H0 = {0, 0}, H1 = {0, 0}, H2 = {0, 0};
-    double2 B1 = {0, 0}, B2 = {0, 0}, B3 = {0, 0}, B4 = {0, 0}, B5 = {0, 0}, B6 = {0, 0};
+    double2 F0 = {0, 0}, F1 = {0, 0}, F2 = {0, 0};   // RES: after black 3, rows r-8 .. r-6
+    double2 B1 = {0, 0}, B2 = {0, 0}, B3 = {0, 0}, B4 = {0, 0}, B5 = {0, 0}, B6 = {0, 0}, B7 = {0, 0};
     auto half = [&](const double2& W0, const double2& W1, const double2& W2, const double2& B, int row,
                     int par) -> double2 {
         double2 o = W1;
@@ -1837,25 +1845,42 @@ __device__ __forceinline__ void sweep3_strip(const StreamArgs& a, const double (
     };
     auto step = [&](double2 p, const double2 bb, int r) {
         P0 = P1; P1 = P2; P2 = vcopy(p);
+        if (RES) B7 = B6;
         B6 = B5; B5 = B4; B4 = B3; B3 = B2; B2 = B1;
         B1 = bb;
-        const double2 n1 = stage(P0, P1, P2, B1, r - DIR, ib - 5, ie + 4, 0);       // red 1
+        const double2 n1 = stage(P0, P1, P2, B1, r - DIR, ib - 5 - EXT, ie + 4 + EXT, 0);       // red 1
         A0 = A1; A1 = A2; A2 = n1;
-        const double2 n2 = stage(A0, A1, A2, B2, r - 2 * DIR, ib - 4, ie + 3, 1);   // black 1
+        const double2 n2 = stage(A0, A1, A2, B2, r - 2 * DIR, ib - 4 - EXT, ie + 3 + EXT, 1);   // black 1
         C0 = C1; C1 = C2; C2 = n2;
-        const double2 n3 = stage(C0, C1, C2, B3, r - 3 * DIR, ib - 3, ie + 2, 0);   // red 2
+        const double2 n3 = stage(C0, C1, C2, B3, r - 3 * DIR, ib - 3 - EXT, ie + 2 + EXT, 0);   // red 2
         E0 = E1; E1 = E2; E2 = n3;
-        const double2 n4 = stage(E0, E1, E2, B4, r - 4 * DIR, ib - 2, ie + 1, 1);   // black 2
+        const double2 n4 = stage(E0, E1, E2, B4, r - 4 * DIR, ib - 2 - EXT, ie + 1 + EXT, 1);   // black 2
         G0 = G1; G1 = G2; G2 = n4;
-        const double2 n5 = stage(G0, G1, G2, B5, r - 5 * DIR, ib - 1, ie, 0);       // red 3
+        const double2 n5 = stage(G0, G1, G2, B5, r - 5 * DIR, ib - 1 - EXT, ie + EXT, 0);       // red 3
         H0 = H1; H1 = H2; H2 = n5;
         // black 3 at r-6, stored on the strip's rows (out-of-range offset: dropped)
         const int k = r - 6 * DIR;
-        const double2 n6 = stage(H0, H1, H2, B6, k, ib, ie - 1, 1);
+        const double2 n6 = stage(H0, H1, H2, B6, k, ib - EXT, ie - 1 + EXT, 1);
         const unsigned off = (k >= ib && k < ie && wr) ? ((unsigned)(k - rb) * (unsigned)ld + (unsigned)c0) * 8u : OOB;
         const nsu4 d = {(unsigned)__double2loint(n6.x), (unsigned)__double2hiint(n6.x),
                         (unsigned)__double2loint(n6.y), (unsigned)__double2hiint(n6.y)};
         __builtin_amdgcn_raw_buffer_store_b128(d, out, (int)off, 0, 2);
+        if (RES) {
+            // stage 7: residual of the finished row r-7 (k_sweep2's fifth stage)
+            F0 = F1; F1 = F2; F2 = n6;
+            const int m7 = r - 7 * DIR;
+            const double2 Fm = DIR > 0 ? F0 : F2, Fp = DIR > 0 ? F2 : F0;   // rows m7 - 1, m7 + 1
+            if (m7 >= ib && m7 < ie) {
+                const double lf = lane_up1(F1.y), rt = lane_dn1(F1.x);
+                const double* rw = rc[m7 - ib + RC_OFF3];
+                const double cw = rw[0], ce = rw[1];
+                const double d0 = diag<1>(rw[2], cd0, alpha), d1 = diag<1>(rw[2], cd1, alpha);
+                double q0, q1;
+                relax<1>(F1.x, Fm.x, Fp.x, lf, F1.y, B7.x, cw, ce, cs0, cn0, d0, 0.0, alpha, q0);
+                relax<1>(F1.y, Fm.y, Fp.y, F1.x, rt, B7.y, cw, ce, cs1, cn1, d1, 0.0, alpha, q1);
+                res += (o0 ? q0 * q0 : 0.0) + (o1 ? q1 * q1 : 0.0);
+            }
+        }
     };
     const int rs = DIR > 0 ? r0 : r1, nr = r1 - r0 + 1;
 #pragma unroll
@@ -1870,9 +1895,10 @@ __device__ __forceinline__ void sweep3_strip(const StreamArgs& a, const double (
             load(rs + DIR * (t + q + SD3), Q[q], QB[q]);
         }
     }
+    return res;
 }
 
-template <int FUSE>
+template <int FUSE, bool RES = false>
 __global__ __launch_bounds__(256) void k_sweep3(StreamArgs a) {
     __shared__ double rcs[4][RC_MAX3][4];
     const int nstr = a.nsj * a.nrun;
@@ -1890,9 +1916,15 @@ __global__ __launch_bounds__(256) void k_sweep3(StreamArgs a) {
     const int si = a.pbase + run;
     if (w < nstr) stage_rows<1, RC_OFF3>(af, rc, ib, lane);
     __syncthreads();
+    double res = 0.0;
     if (w < nstr) {
-        if (si & 1) sweep3_strip<-1>(af, rc, ib, ie, sj, lane);
-        else sweep3_strip<1>(af, rc, ib, ie, sj, lane);
+        if (si & 1) res = sweep3_strip<-1, RES>(af, rc, ib, ie, sj, lane);
+        else res = sweep3_strip<1, RES>(af, rc, ib, ie, sj, lane);
+    }
+    if (RES) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
+        if (lane == 0 && w < nstr) af.part[si * a.nsj + sj] = res;
     }
 }
 
@@ -2120,22 +2152,33 @@ __global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
 // ------------------------------------------------ K2 wall bands (before the global Helmholtz passes)
 // The Helmholtz residual of the guess u^n lives in thin layers along the walls -- the lid's and
 // the side walls' boundary layers: at 4096^2 > 99.9 % of ||r||^2 lies within 16 cells of a wall
-// -- where the global RB-SOR sweeps converge at their asymptotic rate.  BAND_SWEEPS RB-SOR
-// sweeps restricted to the cells within BAND_W of a wall (every other cell held) first cut the
-// global sweeps rtol 1e-8 needs from 7 to 4 (u) / 5 (v) at 4096^2 (tools/helm_band_study.py):
-// two HBM passes per component (3 + 2) instead of three (3 + 2 + 2), for two launches over
-// ~3 % of the cells.  One workgroup per BT x BT tile that touches the band stages the tile and
-// its dependency cone (one cell per half-sweep: 2 BAND_SWEEPS) in LDS -- k_tile2's temporal
-// blocking -- so its band cells come out exactly as from the global masked sweeps, whatever the
-// tiling (one rank and slabs agree).  They go to `out`; k_band_copy moves them back into the
-// iterate (in place, a tile would race with its neighbours' cones).  Same arithmetic as the
-// streaming passes (relax<1>, diag<1>, the Newton reciprocal).  blockIdx.y: 0 u, 1 v.
-struct BandTiles {
-    int nti, ntj;   // tiles of the slab: rows, columns
-    int fa, fb;     // tile rows [0, fa) and [fb, nti) touch the W / E bands: every column
-    int ncl, ncr;   // other tile rows: columns [0, ncl) and [ncr, ntj) only
+// -- where the global RB-SOR sweeps converge at their asymptotic rate.  6 RB-SOR sweeps
+// restricted to the cells within 128 of a wall (every other cell held; the solver's band_w /
+// band_sweeps) first cut the global sweeps rtol 1e-8 needs from 7 to 3 at 4096^2
+// (tools/helm_band_study.py): ONE HBM pass per component (k_sweep3 with its residual stage)
+// instead of three (3 + 2 + 2).  A launch does 3 of the sweeps: one workgroup per BT x BT tile
+// that touches the band stages the tile and its 6-cell dependency cone (one cell per half-sweep)
+// in LDS -- k_tile2's temporal blocking -- so its band cells come out exactly as from the global
+// masked sweeps, whatever the tiling (one rank and slabs agree).  The band cells are read from
+// `qb` and written to `out`, the other cells read from `q` (never written): launch 1 reads the
+// iterate and writes the scratch plane, launch 2 reads the scratch plane's band and writes the
+// iterate -- no tile ever writes what another reads, and no copy-back.  Same arithmetic as the
+// streaming passes (relax<1>, diag<1>, the Newton reciprocal: w = omega / d is formed once per
+// cell, 0 off the band).  blockIdx.y: 0 u, 1 v.
+struct BandArgs {
+    const double* q[2];    // the iterates u, v (cells off the band; never written)
+    const double* qb[2];   // the band cells' current values
+    double* out[2];        // the band cells' new values
+    const double* b[2];    // RHS_u, RHS_v
+    const double *cw, *ce, *bx, *cs, *cn, *by;
+    double alpha, omega;
+    int nx, ny, i0, nxl, ld;
+    int bw;                // band width (cells from a wall)
+    int nti, ntj;          // tiles of the slab: rows, columns
+    int fa, fb;            // tile rows [0, fa) and [fb, nti) touch the W / E bands: every column
+    int ncl, ncr;          // other tile rows: columns [0, ncl) and [ncr, ntj) only
 };
-__device__ __forceinline__ void band_tile(int b, const BandTiles& t, int& ti, int& tj) {
+__device__ __forceinline__ void band_tile(int b, const BandArgs& t, int& ti, int& tj) {
     const int nf = t.fa * t.ntj, nl = (t.nti - t.fb) * t.ntj;
     if (b < nf) { ti = b / t.ntj; tj = b - ti * t.ntj; return; }
     b -= nf;
@@ -2145,90 +2188,105 @@ __device__ __forceinline__ void band_tile(int b, const BandTiles& t, int& ti, in
     ti = t.fa + b / k;
     tj = c < t.ncl ? c : t.ncr + (c - t.ncl);
 }
-__device__ __forceinline__ bool in_band(int gi, int j, int nx, int ny) {
-    return gi < BAND_W || gi >= nx - BAND_W || j < BAND_W || j >= ny - BAND_W;
+// a band cell of the domain (global row gi, column j)
+__device__ __forceinline__ bool in_band(int gi, int j, int nx, int ny, int bw) {
+    return gi >= 0 && gi < nx && (gi < bw || gi >= nx - bw || j < bw || j >= ny - bw);
 }
 
-__global__ __launch_bounds__(256) void k_helm_band(StreamArgs a, BandTiles bt) {
-    constexpr int R = 2 * BAND_SWEEPS, E = BT + 2 * R;
+constexpr int BAND_NSW = 3;   // sweeps per launch: a 6-cell cone, within the slabs' 6 ghost rows
+__global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
+    constexpr int R = 2 * BAND_NSW, E = BT + 2 * R, EH = E / 2;
     constexpr int NQ = (E * E + 255) / 256;
     __shared__ double sp[E][E];
     __shared__ double sb[E][E];
+    __shared__ double sw[E][E];   // omega / diag, 0 where the cell is held
     __shared__ double rw[E][3];   // per staged row: cw, ce, cw + ce + bx
     __shared__ double cl[E][3];   // per staged column: cs, cn, cs + cn + by
     int ti, tj;
-    band_tile(blockIdx.x, bt, ti, tj);
-    const double* in = blockIdx.y ? a.in2 : a.in;
-    const double* b = blockIdx.y ? a.b2 : a.b;
-    double* out = blockIdx.y ? a.out2 : a.out;
+    band_tile(blockIdx.x, a, ti, tj);
+    const int f = blockIdx.y;
+    const double* q = a.q[f];
+    const double* qb = a.qb[f];
+    const double* b = a.b[f];
     const int li0 = ti * BT, j0 = tj * BT, ld = a.ld, ny = a.ny, nx = a.nx;
     const int rlo = -HALO, rhi = a.nxl + HALO - 1;
+    const int gib = a.i0 + li0 - R, jb = j0 - R;   // global row / column of staged (0, 0)
     double pv[NQ], bv[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; k++) {
-        const int q = threadIdx.x + 256 * k;
-        if (q < E * E) {
-            const int r = q / E, cc = q - r * E;
+        const int t = threadIdx.x + 256 * k;
+        if (t < E * E) {
+            const int r = t / E, cc = t - r * E;
             const int li = min(max(li0 - R + r, rlo), rhi);
             const int j = min(max(j0 - R + cc, 0), ny - 1);
-            pv[k] = in[(ptrdiff_t)li * ld + j];
-            bv[k] = b[(ptrdiff_t)li * ld + j];
+            const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+            pv[k] = in_band(a.i0 + li, j, nx, ny, a.bw) ? qb[o] : q[o];
+            bv[k] = b[o];
         }
     }
     if (threadIdx.x < E) {
-        const int gi = min(max(a.i0 + li0 - R + (int)threadIdx.x, 0), nx - 1);
+        const int gi = min(max(gib + (int)threadIdx.x, 0), nx - 1);
         const double cw = a.cw[gi], ce = a.ce[gi];
         rw[threadIdx.x][0] = cw; rw[threadIdx.x][1] = ce; rw[threadIdx.x][2] = cw + ce + a.bx[gi];
     } else if (threadIdx.x >= 64 && threadIdx.x < 64 + E) {
-        const int q = threadIdx.x - 64;
-        const int j = min(max(j0 - R + q, 0), ny - 1);
+        const int t = threadIdx.x - 64;
+        const int j = min(max(jb + t, 0), ny - 1);
         const double cs = a.cs[j], cn = a.cn[j];
-        cl[q][0] = cs; cl[q][1] = cn; cl[q][2] = cs + cn + a.by[j];
+        cl[t][0] = cs; cl[t][1] = cn; cl[t][2] = cs + cn + a.by[j];
     }
 #pragma unroll
     for (int k = 0; k < NQ; k++) {
-        const int q = threadIdx.x + 256 * k;
-        if (q < E * E) {
-            sp[q / E][q % E] = pv[k];
-            sb[q / E][q % E] = bv[k];
+        const int t = threadIdx.x + 256 * k;
+        if (t < E * E) {
+            sp[t / E][t % E] = pv[k];
+            sb[t / E][t % E] = bv[k];
         }
     }
     __syncthreads();
     const double alpha = a.alpha, omega = a.omega;
-    const int gib = a.i0 + li0 - R, jb = j0 - R;   // global row / column of staged (0, 0)
-    for (int h = 0; h < R; h++) {
-        const int par = h & 1;                      // red ((gi + j) even), black, ...
-        const int W = E - 2 - 2 * h;                // the half-sweep's region: [h+1, E-2-h]^2
-        for (int q = threadIdx.x; q < W * W; q += 256) {
-            const int r = h + 1 + q / W, cc = h + 1 + q % W;
-            const int gi = gib + r, j = jb + cc;
-            if (((gi + j) & 1) != par || gi < 0 || gi >= nx || j < 0 || j >= ny || !in_band(gi, j, nx, ny)) continue;
-            const double d = diag<1>(rw[r][2], cl[cc][2], alpha), w = omega * rcp_nr(d);
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const int t = threadIdx.x + 256 * k;
+        if (t < E * E) {
+            const int r = t / E, cc = t - r * E;
+            sw[r][cc] = in_band(gib + r, jb + cc, nx, ny, a.bw) && jb + cc >= 0 && jb + cc < ny
+                            ? omega * rcp_nr(diag<1>(rw[r][2], cl[cc][2], alpha)) : 0.0;
+        }
+    }
+    __syncthreads();
+    for (int h = 0; h < 2 * BAND_NSW; h++) {
+        const int par = h & 1;                   // red ((gi + j) even), black, ...
+        const int lo = h + 1, hi = E - 2 - h;    // the half-sweep's region: [lo, hi]^2
+        for (int t = threadIdx.x; t < E * EH; t += 256) {
+            const int r = t / EH;
+            const int cc = 2 * (t - r * EH) + ((par + gib + r + jb) & 1);
+            if (r < lo || r > hi || cc < lo || cc > hi) continue;
+            const double d = diag<1>(rw[r][2], cl[cc][2], alpha);
             double rr;
             sp[r][cc] = relax<1>(sp[r][cc], sp[r - 1][cc], sp[r + 1][cc], sp[r][cc - 1], sp[r][cc + 1], sb[r][cc],
-                                 rw[r][0], rw[r][1], cl[cc][0], cl[cc][1], d, w, alpha, rr);
+                                 rw[r][0], rw[r][1], cl[cc][0], cl[cc][1], d, sw[r][cc], alpha, rr);
         }
         __syncthreads();
     }
-    for (int q = threadIdx.x; q < BT * BT; q += 256) {
-        const int r = R + q / BT, cc = R + q % BT;
+    double* out = a.out[f];
+    for (int t = threadIdx.x; t < BT * BT; t += 256) {
+        const int r = R + t / BT, cc = R + t % BT;
         const int li = li0 + r - R, j = j0 + cc - R;
-        if (li >= a.nxl || j >= ny || !in_band(a.i0 + li, j, nx, ny)) continue;
+        if (li >= a.nxl || j >= ny || !in_band(a.i0 + li, j, nx, ny, a.bw)) continue;
         out[(ptrdiff_t)li * ld + j] = sp[r][cc];
     }
 }
 
-// the band cells of each tile: out -> in (u: blockIdx.y 0, v: 1)
-__global__ __launch_bounds__(256) void k_band_copy(StreamArgs a, BandTiles bt) {
+// the band cells of each tile: qb -> out (an odd number of band launches ends in the scratch plane)
+__global__ __launch_bounds__(256) void k_band_copy(BandArgs a) {
     int ti, tj;
-    band_tile(blockIdx.x, bt, ti, tj);
-    double* dst = const_cast<double*>(blockIdx.y ? a.in2 : a.in);
-    const double* src = blockIdx.y ? a.out2 : a.out;
-    for (int q = threadIdx.x; q < BT * BT; q += 256) {
-        const int li = ti * BT + q / BT, j = tj * BT + q % BT;
-        if (li >= a.nxl || j >= a.ny || !in_band(a.i0 + li, j, a.nx, a.ny)) continue;
+    band_tile(blockIdx.x, a, ti, tj);
+    const int f = blockIdx.y;
+    for (int t = threadIdx.x; t < BT * BT; t += 256) {
+        const int li = ti * BT + t / BT, j = tj * BT + t % BT;
+        if (li >= a.nxl || j >= a.ny || !in_band(a.i0 + li, j, a.nx, a.ny, a.bw)) continue;
         const ptrdiff_t o = (ptrdiff_t)li * a.ld + j;
-        dst[o] = src[o];
+        a.out[f][o] = a.qb[f][o];
     }
 }
 
@@ -3245,37 +3303,52 @@ int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* 
     return launch_stream2<0>(stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false), g, st);
 }
 
-// the Helmholtz wall-band relaxation of u and v (k_helm_band + k_band_copy); uo / vo: scratch
-// planes (their band cells are overwritten); needs 6 ghost rows of u, v and 5 of ru, rv
-int launch_helm_band(const Geo& g, const Coef& c, double alpha, double omega, double* u, double* v, double* uo,
-                     double* vo, const double* ru, const double* rv, hipStream_t st) {
-    StreamArgs a = stream_args(g, c, u, uo, ru, nullptr, alpha, omega, nullptr, true);
-    a.in2 = v; a.out2 = vo; a.b2 = rv;
-    BandTiles t{};
-    t.nti = (g.nxl + BT - 1) / BT;
-    t.ntj = (g.ny + BT - 1) / BT;
+// one launch of the Helmholtz wall-band relaxation (k_helm_band: 3 RB-SOR sweeps of u and v on
+// the cells within bw of a wall), band cells read from qu / qv (the rest from u / v), written to
+// ou / ov; copy != 0: the band cells qu / qv -> ou / ov instead (k_band_copy).  Returns the tiles.
+int launch_helm_band(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                     const double* qu, const double* qv, double* ou, double* ov, const double* ru, const double* rv,
+                     int bw, int copy, hipStream_t st) {
+    BandArgs a{};
+    a.q[0] = u; a.q[1] = v; a.qb[0] = qu; a.qb[1] = qv; a.out[0] = ou; a.out[1] = ov; a.b[0] = ru; a.b[1] = rv;
+    a.cw = c.pw; a.ce = c.pe; a.bx = c.bx; a.cs = c.ps; a.cn = c.pn; a.by = c.by;
+    a.alpha = alpha; a.omega = omega;
+    a.nx = g.nx; a.ny = g.ny; a.i0 = g.i0; a.nxl = g.nxl; a.ld = g.ld;
+    a.bw = bw;
+    a.nti = (g.nxl + BT - 1) / BT;
+    a.ntj = (g.ny + BT - 1) / BT;
     auto full = [&](int ti) {   // the tile row touches the W or E band
         const int lo = g.i0 + ti * BT, hi = std::min(g.i0 + (ti + 1) * BT, g.i0 + g.nxl);
-        return lo < BAND_W || hi > g.nx - BAND_W;
+        return lo < bw || hi > g.nx - bw;
     };
-    t.fa = 0;
-    while (t.fa < t.nti && full(t.fa)) t.fa++;
-    t.fb = t.nti;
-    while (t.fb > t.fa && full(t.fb - 1)) t.fb--;
-    t.ncl = std::min((BAND_W + BT - 1) / BT, t.ntj);
-    t.ncr = std::max((g.ny - BAND_W) / BT, t.ncl);
-    const int n = (t.fa + t.nti - t.fb) * t.ntj + (t.fb - t.fa) * (t.ncl + t.ntj - t.ncr);
+    a.fa = 0;
+    while (a.fa < a.nti && full(a.fa)) a.fa++;
+    a.fb = a.nti;
+    while (a.fb > a.fa && full(a.fb - 1)) a.fb--;
+    a.ncl = std::min((bw + BT - 1) / BT, a.ntj);
+    a.ncr = std::max((g.ny - bw) / BT, a.ncl);
+    const int n = (a.fa + a.nti - a.fb) * a.ntj + (a.fb - a.fa) * (a.ncl + a.ntj - a.ncr);
     if (n <= 0) return 0;
-    NS_LAUNCH(k_helm_band, dim3(n, 2), dim3(256), 0, st, a, t);
-    NS_LAUNCH(k_band_copy, dim3(n, 2), dim3(256), 0, st, a, t);
+    if (copy) NS_LAUNCH(k_band_copy, dim3(n, 2), dim3(256), 0, st, a);
+    else NS_LAUNCH(k_helm_band, dim3(n, 2), dim3(256), 0, st, a);
     return n;
 }
 
 // three Helmholtz sweeps in one pass (k_sweep3; no residual): which = 1 u, 2 v, 3 both in one launch
 int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
-                       double* uo, double* vo, const double* ru, const double* rv, hipStream_t st, int which) {
+                       double* uo, double* vo, const double* ru, const double* rv, hipStream_t st, int which,
+                       double* part) {
     StreamArgs a = stream_args(g, c, which == 2 ? v : u, which == 2 ? vo : uo, which == 2 ? rv : ru, nullptr, alpha,
-                               omega, nullptr, true);
+                               omega, part, true);
+    if (part) {   // the batch's last pass with its output residual (one field, one rank: 7-row cone)
+        if (which == 3 || g.i0 != 0 || g.nxl != g.nx) return -1;
+        a.nsj = (g.ny + SW3R - 1) / SW3R;
+        int nblk = 0;
+        const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep3<FUSE_NONE, true>), 7, &nblk);
+        if (which == 2) a.part = part + nstr;   // partials: u at [0, n), v at [n, 2n) (launch_helm_sweep2)
+        if (nblk) NS_LAUNCH((k_sweep3<FUSE_NONE, true>), dim3(nblk), dim3(256), 0, st, a);
+        return nstr;
+    }
     a.nsj = (g.ny + SW2X - 1) / SW2X;
     const void* k = which == 3 ? (const void*)k_sweep3<FUSE_UV> : (const void*)k_sweep3<FUSE_NONE>;
     int nblk = 0;

@@ -122,6 +122,8 @@ struct ns_solver {
     bool triple = true;          // 3-sweep passes allowed on this decomposition (slabs >= 2*HALO rows)
     bool sweep3 = true;          // single rank: odd Helmholtz batches start with a 3-sweep pass (k_sweep3)
     bool helm_band = true;       // Helmholtz: wall-band relaxation before the global passes (k_helm_band)
+    int band_w = 128, band_sweeps = 6;   // its width (cells from a wall) and RB-SOR sweeps (a multiple of 3)
+    bool sweep3_res = true;      // one rank: a Helmholtz batch may end on a 3-sweep pass with its residual
     int helm_probe = 0;          // steps since the Helmholtz first-pass residual was last sampled
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
     int fuse_restrict = 1;       // NSGPU_FUSED_RESTRICT=0: separate k_restrict pass (A/B)
@@ -412,11 +414,12 @@ int helm_sweep(ns_solver* s, double alpha, double* part, int which = 3) {
     return nb;
 }
 
-// three Helmholtz sweeps in one pass (k_sweep3; no residual), then swap (single rank)
-int helm_sweep3(ns_solver* s, double alpha, int which) {
+// three Helmholtz sweeps in one pass (k_sweep3; with `part`: + the output residual, one rank), then swap
+int helm_sweep3(ns_solver* s, double alpha, int which, double* part = nullptr) {
     const int nb = nsg::launch_helm_sweep3(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
                                            s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
-                                           s->arr[NS_ARR_RV], s->st, which);
+                                           s->arr[NS_ARR_RV], s->st, which, part);
+    if (nb < 0) return nb;
     if (which & 1) std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
     if (which & 2) std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
     return nb;
@@ -470,7 +473,10 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
             // rank and slabs agree.  A probing first pass stays a pair (2+3+2)
             int w = std::min(s->tiled ? 1 : 2, n - k);
             if (!s->tiled && !(launch == 0 && part_first)) {
-                if (s->sweep3 && s->triple && n - k >= 5) w = 3;
+                // (one rank: a batch may also end on a 3-sweep pass with the residual stage, 7-row
+                // cone: 5 = 3+2, 3 = 3, 6 = 3+3)
+                const bool end3 = s->nranks == 1 && s->sweep3_res;
+                if (s->sweep3 && s->triple && (n - k >= 5 || (end3 && (n - k == 3 || n - k == 6)))) w = 3;
                 else if (((n - k) & 1) && n - k >= 3) w = 1;
             }
             const bool last = k + w >= n;
@@ -505,7 +511,7 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                 }
                 if (which == 3) CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, hw));
                 else if (w <= 2) CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
-                nb = w == 3 ? helm_sweep3(s, alpha, which)
+                nb = w == 3 ? helm_sweep3(s, alpha, which, part)
                             : (w >= 2 ? helm_sweep2(s, alpha, part, which) : helm_sweep(s, alpha, part, which));
                 if (nb < 0) return NS_EHIP;
             }
@@ -614,14 +620,25 @@ int correct_launch(ns_solver* s, double* part2);
 // there).  Slabs: the iterates' ghost rows (6: the kernel's cone) and the right-hand sides' (5)
 // first; the first global pass exchanges the relaxed iterates' rows again.
 int helm_band(ns_solver* s, double alpha) {
-    if (s->nranks > 1) {
-        const HaloReq r[4] = {{&s->g, s->arr[NS_ARR_U], 6}, {&s->g, s->arr[NS_ARR_V], 6},
-                              {&s->g, s->arr[NS_ARR_RU], 5}, {&s->g, s->arr[NS_ARR_RV], 5}};
-        CHK(halo_reqs(s, r, s->helm_b_pend ? 4 : 2));
-        s->helm_b_pend = 0;
+    // launches of 3 sweeps: even ones read the band from the iterates and write it to the
+    // scratch planes, odd ones back (no tile writes what another reads); an odd count ends with
+    // a copy-back.  Slabs: each launch after a 6-row exchange of the planes it reads the band from
+    double *U = s->arr[NS_ARR_U], *V = s->arr[NS_ARR_V], *TU = s->arr[NS_ARR_TMPU], *TV = s->arr[NS_ARR_TMPV];
+    const int rounds = std::max(1, s->band_sweeps / 3);
+    for (int k = 0; k < rounds; k++) {
+        const bool odd = k & 1;
+        if (s->nranks > 1) {
+            const HaloReq r[4] = {{&s->g, odd ? TU : U, 6}, {&s->g, odd ? TV : V, 6},
+                                  {&s->g, s->arr[NS_ARR_RU], 5}, {&s->g, s->arr[NS_ARR_RV], 5}};
+            CHK(halo_reqs(s, r, s->helm_b_pend ? 4 : 2));
+            s->helm_b_pend = 0;
+        }
+        nsg::launch_helm_band(s->g, s->c, alpha, s->omega_v, U, V, odd ? TU : U, odd ? TV : V, odd ? U : TU,
+                              odd ? V : TV, s->arr[NS_ARR_RU], s->arr[NS_ARR_RV], s->band_w, 0, s->st);
     }
-    nsg::launch_helm_band(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
-                          s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU], s->arr[NS_ARR_RV], s->st);
+    if (rounds & 1)
+        nsg::launch_helm_band(s->g, s->c, alpha, s->omega_v, U, V, TU, TV, U, V, s->arr[NS_ARR_RU],
+                              s->arr[NS_ARR_RV], s->band_w, 1, s->st);
     return 0;
 }
 
@@ -656,7 +673,9 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         // the first pass's residual (a fifth pipeline stage: +20 % on that pass) feeds the next
         // step's batch prediction; consecutive steps converge alike, so it is sampled on every
         // 8th step only (and whenever the predicted batch fell short: see below)
-        const bool first = sweeps == 0 && n > 2 && (s->helm_probe == 0 || !s->helm_adapt);
+        // (not on a batch of <= 3 sweeps: one pass, or 1 + 2 on slabs -- a probing pair would leave
+        // a lone last sweep, whose residual is its input's)
+        const bool first = sweeps == 0 && n > 3 && (s->helm_probe == 0 || !s->helm_adapt);
         int nb0 = 0, at0 = 0, at = 0;
         const int nb = helm_sweeps(s, alpha, n, first ? p0 : nullptr, s->part, &nb0, &at0, &at);
         at += sweeps;
@@ -1851,6 +1870,9 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_SWEEP")) s->tiled = std::strcmp(e, "tiled") == 0;
     if (const char* e = getenv("NSGPU_SWEEP3")) s->sweep3 = std::atoi(e) != 0;   // A/B: pairs only
     if (const char* e = getenv("NSGPU_HELM_BAND")) s->helm_band = std::atoi(e) != 0;   // A/B: no wall bands
+    if (const char* e = getenv("NSGPU_BAND_W")) s->band_w = std::max(1, std::atoi(e));   // A/B: band width
+    if (const char* e = getenv("NSGPU_BAND_SWEEPS")) s->band_sweeps = std::max(3, std::atoi(e) / 3 * 3);
+    if (const char* e = getenv("NSGPU_SWEEP3_RES")) s->sweep3_res = std::atoi(e) != 0;   // A/B: batches end on pairs
     // the 3-sweep pass reads HALO ghost rows, which one neighbour feeds only from slabs of
     // >= 2*HALO rows; thinner slabs (the thinnest of all ranks: a global decision) take the
     // same sweeps as a single sweep + pairs

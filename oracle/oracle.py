@@ -172,7 +172,7 @@ class OGrid:
         r2 = lib().og_helmholtz_rbsor_sweep(self.h, alpha, _d(u), _d(v), _d(_f(ru)), _d(_f(rv)), omega)
         return u, v, r2
 
-    def helm_band(self, alpha, u, v, ru, rv, omega=1.0, width=32, sweeps=3):
+    def helm_band(self, alpha, u, v, ru, rv, omega=1.0, width=128, sweeps=6):
         """k_helm_band restated: RB-SOR sweeps of u, v on the cells within `width` of a wall."""
         u, v = _f(u).copy(), _f(v).copy()
         if lib().og_helm_band(self.h, alpha, _d(u), _d(v), _d(_f(ru)), _d(_f(rv)), omega, width, sweeps) != 0:
@@ -223,7 +223,7 @@ class OSolver:
         except Exception:
             pass
 
-    def use_gpu_algorithm(self, omega_v, omega_mg=1.1, band=(32, 3)):
+    def use_gpu_algorithm(self, omega_v, omega_mg=1.1, band=(128, 6)):
         """RB-SOR Helmholtz (after `band` = (width, sweeps) RB-SOR sweeps on the cells within
         `width` of a wall: k_helm_band; None = no band step) + multigrid Poisson (the GPU path's
         algorithm; CPU baseline)."""
