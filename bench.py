@@ -37,12 +37,13 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level 
 #   prolongation pass (k_sweep2 FUSE_P): prolongation + two RB sweeps:
 #       read phi 8 + read b 8 + write phi 8 + read the coarse correction 8 / 4         = 26
 # and the Helmholtz solve's passes (K2, single rank: one velocity component per pass):
-#   Helmholtz pass (k_sweep2<Helmholtz>): two RB-SOR sweeps: read q 8 + read b 8 + write q 8 = 24
+#   Helmholtz pass (k_sweep3 / k_sweep2<Helmholtz>): 3 or 2 RB-SOR sweeps: read q 8 + read b 8 + write q 8 = 24
 # The one with the largest total time per step is `roofline` (the dominant kernel).
 KERNELS = {
     "restrict": ("k_sweep2<Poisson, FUSE_R> (finest pre-smoothing pass: 2 RB sweeps + residual + restriction)", 28),
     "prolong": ("k_sweep2<Poisson, FUSE_P> (finest post-smoothing pass: prolongation + 2 RB sweeps + output residual)", 26),
-    "helmholtz": ("k_sweep2<Helmholtz> (2 RB-SOR sweeps of one velocity component of (I - a L_V) u* = RHS)", 24),
+    "helmholtz": ("Helmholtz pass of one velocity component of (I - a L_V) u* = RHS (k_sweep3 + residual stage: "
+                  "3 RB-SOR sweeps, after the wall bands; or k_sweep2: 2 sweeps)", 24),
 }
 JACOBI_LABEL = "k_jacobi_s<double> (one weighted-Jacobi sweep of the Poisson operator, the north star's roofline kernel)"
 SWEEP_BYTES_PER_CELL = 24
@@ -90,11 +91,12 @@ def _host_threads():
 
 def helm_passes(n, world):
     """HBM passes of one component's n Helmholtz sweeps (ns_solver.cpp helm_sweeps): 3-sweep
-    passes while >= 5 remain, ending on a pair (5 = 3+2, 7 = 3+2+2; slabs too, unless thinner
-    than 12 rows); an odd remainder otherwise starts with a single sweep."""
+    passes while >= 5 remain (slabs too, unless thinner than 12 rows); one rank may also end on
+    a 3-sweep pass with its residual (3 = 3, 6 = 3+3), otherwise a batch ends on a pair (5 = 3+2);
+    an odd remainder otherwise starts with a single sweep (slabs: 3 = 1+2)."""
     p, r = 0, n
     while r > 0:
-        if r >= 5:
+        if r >= 5 or (world == 1 and r in (3, 6)):
             w = 3
         elif r % 2 and r >= 3:
             w = 1
@@ -222,10 +224,10 @@ def main():
     # helm_passes); multigrid per solve `cycles` FUSE_R passes at 28 and `cycles` FUSE_P passes
     # at 26 on the finest level, x 4/3 for the coarser levels (each a quarter of the one above)
     hpasses = sum(helm_passes(int(s["it_u"]), world) for s in stats)
-    # the Helmholtz wall bands (k_helm_band + its copy-back) on the cells within 32 of a wall:
-    # u, v read 16 + rhs 16 + write 16, copy 32 -> 80 B per band cell
-    band_frac = 1.0 - max(n - 64, 0) * max(nyc - 64, 0) / float(n * nyc)
-    step_bpc = (64 + 24 + 40 + 32 + 2 * 24 * hpasses / K + 80 * band_frac
+    # the Helmholtz wall bands (two k_helm_band launches) on the cells within 128 of a wall:
+    # per launch u, v read 16 + rhs 16 + write 16 -> 96 B per band cell
+    band_frac = 1.0 - max(n - 256, 0) * max(nyc - 256, 0) / float(n * nyc)
+    step_bpc = (64 + 24 + 40 + 32 + 2 * 24 * hpasses / K + 96 * band_frac
                 + (28 * cycles + 26 * cycles) / K * 4.0 / 3.0)
     if channel:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications

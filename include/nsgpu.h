@@ -129,8 +129,9 @@ typedef struct ns_stats {
     int32_t n_checks;                /* residual checks (host syncs) in the step */
     double  t_restrict_kernel_ms;    /* multigrid: sum of the finest level's restriction-pass durations (timing == 1) */
     int32_t n_restrict_kernels;      /* number of those passes timed */
-    double  t_helm_kernel_ms;        /* single rank: sum of the two-sweep Helmholtz pass durations (one velocity
-                                        component each, K2; timing == 1) */
+    double  t_helm_kernel_ms;        /* single rank: sum of the timed Helmholtz pass durations (one velocity
+                                        component each, K2: the two-sweep passes and the 3-sweep passes
+                                        with the residual stage -- 24 B/cell either; timing == 1) */
     int32_t n_helm_kernels;          /* number of those passes timed */
     int32_t n_exchanges;             /* ghost-row exchange groups of the step (multi-rank / loopback) */
     int32_t n_allreduces;            /* all-reduces of the step (multi-rank / loopback) */

@@ -14,5 +14,5 @@ python3 tools/trace_summary.py $(find $out/trace -name "*kernel_trace.csv" | hea
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu > $out/fetch.log 2>&1
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu > $out/write.log 2>&1
 python3 tools/pmc_summarize.py 4096 $out/fetch $out/write $out/pmc_traffic.json \
-  'restrict=k_sweep2<0, false, 1>=28' 'prolong=k_sweep2<0, false, 2>=26' 'jacobi_sweep=k_jacobi_s<double=24' 'jacobi_sweep_fp32=k_jacobi_s<float=12' \
-  'helmholtz=k_sweep2<1, =24'
+  'restrict=k_sweep2<0, false, 1>=28' 'prolong=k_sweep2<0, true, 2>=26' 'jacobi_sweep=k_jacobi_s<double=24' 'jacobi_sweep_fp32=k_jacobi_s<float=12' \
+  'helmholtz=k_sweep3<0, true>=24'

@@ -18,4 +18,6 @@ bash tools/profile_round.sh $out/prof || exit $?
 timeout -k 10 200 python -u bench.py --case channel > $out/bench_channel.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/channel_trace -o run -- python3 bench.py --case channel > $out/channel_trace.log 2>&1 || exit $?
 python3 tools/trace_summary.py $(find $out/channel_trace -name "*kernel_trace.csv" | head -1) 30 > $out/channel_per_step_summary.txt
+timeout -k 10 600 python -u tools/slab_projection.py > $out/projection.log 2>&1 || exit $?
+cat $out/projection.log | tail -5
 echo done
