@@ -2194,12 +2194,17 @@ __device__ __forceinline__ bool in_band(int gi, int j, int nx, int ny, int bw) {
 }
 
 constexpr int BAND_NSW = 3;   // sweeps per launch: a 6-cell cone, within the slabs' 6 ghost rows
+// Thread layout: the staged E x E region (E = BT + 12 = 44) is cut into 22 column pairs x 11
+// segments of 4 rows; a thread keeps its 8 cells (value, rhs, weight) in registers and meets
+// its neighbours in LDS only across the segment / pair edges: per update ~1.5 LDS reads instead
+// of ~12.  A row of a pair holds one cell of each colour, and the colour's column in row s is
+// (par + gi + j0) parity: uniform over the workgroup (every pair starts on an even column,
+// every segment on an even row), so there is no divergence.  One barrier per half-sweep: a
+// half-sweep reads only the other colour (stable) and publishes its own cells.
 __global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
-    constexpr int R = 2 * BAND_NSW, E = BT + 2 * R, EH = E / 2;
-    constexpr int NQ = (E * E + 255) / 256;
+    constexpr int R = 2 * BAND_NSW, E = BT + 2 * R, NP = E / 2, SEG = 4, NSEG = E / SEG;
+    static_assert(E % SEG == 0 && NP * NSEG <= 256, "band tile layout");
     __shared__ double sp[E][E];
-    __shared__ double sb[E][E];
-    __shared__ double sw[E][E];   // omega / diag, 0 where the cell is held
     __shared__ double rw[E][3];   // per staged row: cw, ce, cw + ce + bx
     __shared__ double cl[E][3];   // per staged column: cs, cn, cs + cn + by
     int ti, tj;
@@ -2211,69 +2216,101 @@ __global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
     const int li0 = ti * BT, j0 = tj * BT, ld = a.ld, ny = a.ny, nx = a.nx;
     const int rlo = -HALO, rhi = a.nxl + HALO - 1;
     const int gib = a.i0 + li0 - R, jb = j0 - R;   // global row / column of staged (0, 0)
-    double pv[NQ], bv[NQ];
+    const int t = threadIdx.x;
+    const bool act = t < NP * NSEG;
+    const int kp = act ? t % NP : 0, sg = act ? t / NP : 0;
+    const int c0 = 2 * kp, r0 = SEG * sg;          // columns c0, c0 + 1; rows r0 .. r0 + SEG - 1
+    double2 v[SEG], bq[SEG];
+    int jj[2];
+    bool jin[2];
 #pragma unroll
-    for (int k = 0; k < NQ; k++) {
-        const int t = threadIdx.x + 256 * k;
-        if (t < E * E) {
-            const int r = t / E, cc = t - r * E;
-            const int li = min(max(li0 - R + r, rlo), rhi);
-            const int j = min(max(j0 - R + cc, 0), ny - 1);
-            const ptrdiff_t o = (ptrdiff_t)li * ld + j;
-            pv[k] = in_band(a.i0 + li, j, nx, ny, a.bw) ? qb[o] : q[o];
-            bv[k] = b[o];
-        }
+    for (int e = 0; e < 2; e++) {
+        const int j = jb + c0 + e;
+        jin[e] = j >= 0 && j < ny;
+        jj[e] = min(max(j, 0), ny - 1);
     }
-    if (threadIdx.x < E) {
-        const int gi = min(max(gib + (int)threadIdx.x, 0), nx - 1);
+#pragma unroll
+    for (int s = 0; s < SEG; s++) {
+        const int li = min(max(li0 - R + r0 + s, rlo), rhi);
+        const ptrdiff_t o = (ptrdiff_t)li * ld;
+        const bool b0 = in_band(a.i0 + li, jj[0], nx, ny, a.bw), b1 = in_band(a.i0 + li, jj[1], nx, ny, a.bw);
+        v[s].x = (b0 ? qb : q)[o + jj[0]];
+        v[s].y = (b1 ? qb : q)[o + jj[1]];
+        bq[s].x = b[o + jj[0]];
+        bq[s].y = b[o + jj[1]];
+    }
+    if (t < E) {
+        const int gi = min(max(gib + t, 0), nx - 1);
         const double cw = a.cw[gi], ce = a.ce[gi];
-        rw[threadIdx.x][0] = cw; rw[threadIdx.x][1] = ce; rw[threadIdx.x][2] = cw + ce + a.bx[gi];
-    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + E) {
-        const int t = threadIdx.x - 64;
-        const int j = min(max(jb + t, 0), ny - 1);
+        rw[t][0] = cw; rw[t][1] = ce; rw[t][2] = cw + ce + a.bx[gi];
+    } else if (t >= 64 && t < 64 + E) {
+        const int k = t - 64;
+        const int j = min(max(jb + k, 0), ny - 1);
         const double cs = a.cs[j], cn = a.cn[j];
-        cl[t][0] = cs; cl[t][1] = cn; cl[t][2] = cs + cn + a.by[j];
+        cl[k][0] = cs; cl[k][1] = cn; cl[k][2] = cs + cn + a.by[j];
     }
+    if (act) {
 #pragma unroll
-    for (int k = 0; k < NQ; k++) {
-        const int t = threadIdx.x + 256 * k;
-        if (t < E * E) {
-            sp[t / E][t % E] = pv[k];
-            sb[t / E][t % E] = bv[k];
-        }
+        for (int s = 0; s < SEG; s++) { sp[r0 + s][c0] = v[s].x; sp[r0 + s][c0 + 1] = v[s].y; }
     }
     __syncthreads();
     const double alpha = a.alpha, omega = a.omega;
+    // this thread's coefficients and relaxation weights (0 on held cells)
+    double2 w[SEG];
+    double rcw[SEG], rce[SEG], rd[SEG];
+    const double ccs0 = cl[c0][0], ccn0 = cl[c0][1], ccd0 = cl[c0][2];
+    const double ccs1 = cl[c0 + 1][0], ccn1 = cl[c0 + 1][1], ccd1 = cl[c0 + 1][2];
 #pragma unroll
-    for (int k = 0; k < NQ; k++) {
-        const int t = threadIdx.x + 256 * k;
-        if (t < E * E) {
-            const int r = t / E, cc = t - r * E;
-            sw[r][cc] = in_band(gib + r, jb + cc, nx, ny, a.bw) && jb + cc >= 0 && jb + cc < ny
-                            ? omega * rcp_nr(diag<1>(rw[r][2], cl[cc][2], alpha)) : 0.0;
-        }
+    for (int s = 0; s < SEG; s++) {
+        const int r = r0 + s, gi = gib + r;
+        rcw[s] = rw[r][0]; rce[s] = rw[r][1]; rd[s] = rw[r][2];
+        w[s].x = (jin[0] && in_band(gi, jj[0], nx, ny, a.bw)) ? omega * rcp_nr(diag<1>(rd[s], ccd0, alpha)) : 0.0;
+        w[s].y = (jin[1] && in_band(gi, jj[1], nx, ny, a.bw)) ? omega * rcp_nr(diag<1>(rd[s], ccd1, alpha)) : 0.0;
     }
-    __syncthreads();
+    const int cpar = (gib + jb) & 1;   // colour parity of staged (0, 0)
     for (int h = 0; h < 2 * BAND_NSW; h++) {
         const int par = h & 1;                   // red ((gi + j) even), black, ...
         const int lo = h + 1, hi = E - 2 - h;    // the half-sweep's region: [lo, hi]^2
-        for (int t = threadIdx.x; t < E * EH; t += 256) {
-            const int r = t / EH;
-            const int cc = 2 * (t - r * EH) + ((par + gib + r + jb) & 1);
-            if (r < lo || r > hi || cc < lo || cc > hi) continue;
-            const double d = diag<1>(rw[r][2], cl[cc][2], alpha);
-            double rr;
-            sp[r][cc] = relax<1>(sp[r][cc], sp[r - 1][cc], sp[r + 1][cc], sp[r][cc - 1], sp[r][cc + 1], sb[r][cc],
-                                 rw[r][0], rw[r][1], cl[cc][0], cl[cc][1], d, sw[r][cc], alpha, rr);
+        if (act) {
+#pragma unroll
+            for (int s = 0; s < SEG; s++) {
+                const int r = r0 + s;
+                if (r < lo || r > hi) continue;
+                // the colour's column in this row: c0 + e, e = (par + gi + j) parity, uniform
+                const int e = (par + cpar + r) & 1;
+                const int cc = c0 + e;
+                if (cc < lo || cc > hi) continue;
+                const double xm = s > 0 ? (e ? v[s - 1].y : v[s - 1].x) : sp[r - 1][cc];
+                const double xp = s < SEG - 1 ? (e ? v[s + 1].y : v[s + 1].x) : sp[r + 1][cc];
+                double rr;
+                if (e == 0) {
+                    const double ym = sp[r][cc - 1], yp = v[s].y;
+                    v[s].x = relax<1>(v[s].x, xm, xp, ym, yp, bq[s].x, rcw[s], rce[s], ccs0, ccn0,
+                                      diag<1>(rd[s], ccd0, alpha), w[s].x, alpha, rr);
+                    sp[r][cc] = v[s].x;
+                } else {
+                    const double ym = v[s].x, yp = sp[r][cc + 1];
+                    v[s].y = relax<1>(v[s].y, xm, xp, ym, yp, bq[s].y, rcw[s], rce[s], ccs1, ccn1,
+                                      diag<1>(rd[s], ccd1, alpha), w[s].y, alpha, rr);
+                    sp[r][cc] = v[s].y;
+                }
+            }
         }
         __syncthreads();
     }
-    double* out = a.out[f];
-    for (int t = threadIdx.x; t < BT * BT; t += 256) {
-        const int r = R + t / BT, cc = R + t % BT;
-        const int li = li0 + r - R, j = j0 + cc - R;
-        if (li >= a.nxl || j >= ny || !in_band(a.i0 + li, j, nx, ny, a.bw)) continue;
-        out[(ptrdiff_t)li * ld + j] = sp[r][cc];
+    if (act) {
+        double* out = a.out[f];
+#pragma unroll
+        for (int s = 0; s < SEG; s++) {
+            const int r = r0 + s, li = li0 + r - R;
+            if (r < R || r >= R + BT || li >= a.nxl) continue;
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const int cc = c0 + e, j = jb + cc;
+                if (cc < R || cc >= R + BT || j >= ny || !in_band(a.i0 + li, j, nx, ny, a.bw)) continue;
+                out[(ptrdiff_t)li * ld + j] = e ? v[s].y : v[s].x;
+            }
+        }
     }
 }
 
