@@ -95,6 +95,6 @@ def test_constants_match_header():
     txt = open(L.HEADER).read()
     import re
     for name in ["NS_OK", "NS_EINVAL", "NS_BC_WALL", "NS_BC_NEUMANN", "NS_POISSON_JACOBI", "NS_ARR_RPHI",
-                 "NS_NUM_ARR", "NS_K_RESIDUAL", "NS_K_POIS_SOLVE"]:
+                 "NS_NUM_ARR", "NS_K_RESIDUAL", "NS_K_POIS_SOLVE", "NS_K_POISSON32", "NS_K_HELM_BAND"]:
         m = re.search(rf"#define {name}\s+(-?\d+)", txt)
         assert m and int(m.group(1)) == getattr(L, name), name
