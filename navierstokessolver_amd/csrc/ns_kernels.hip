@@ -2177,6 +2177,8 @@ struct BandArgs {
     int nti, ntj;          // tiles of the slab: rows, columns
     int fa, fb;            // tile rows [0, fa) and [fb, nti) touch the W / E bands: every column
     int ncl, ncr;          // other tile rows: columns [0, ncl) and [ncr, ntj) only
+    int phase;             // exchange overlap (set_strip_phase): 1 the tiles that read no neighbour's
+                           // ghost rows, 2 the others, 0 all
 };
 __device__ __forceinline__ void band_tile(int b, const BandArgs& t, int& ti, int& tj) {
     const int nf = t.fa * t.ntj, nl = (t.nti - t.fb) * t.ntj;
@@ -2214,6 +2216,10 @@ __global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
     const double* qb = a.qb[f];
     const double* b = a.b[f];
     const int li0 = ti * BT, j0 = tj * BT, ld = a.ld, ny = a.ny, nx = a.nx;
+    if (a.phase) {   // (workgroup-uniform) does the staged region reach a neighbour rank's rows?
+        const bool touch = (a.i0 > 0 && li0 - R < 0) || (a.i0 + a.nxl < nx && li0 + BT + R > a.nxl);
+        if (touch != (a.phase == 2)) return;
+    }
     const int rlo = -HALO, rhi = a.nxl + HALO - 1;
     const int gib = a.i0 + li0 - R, jb = j0 - R;   // global row / column of staged (0, 0)
     const int t = threadIdx.x;
@@ -3352,6 +3358,8 @@ int launch_helm_band(const Geo& g, const Coef& c, double alpha, double omega, co
     a.alpha = alpha; a.omega = omega;
     a.nx = g.nx; a.ny = g.ny; a.i0 = g.i0; a.nxl = g.nxl; a.ld = g.ld;
     a.bw = bw;
+    a.phase = copy ? 0 : g_phase;
+    if (copy && g_phase == 1) return 0;   // (the copy-back runs whole, after the exchange)
     a.nti = (g.nxl + BT - 1) / BT;
     a.ntj = (g.ny + BT - 1) / BT;
     auto full = [&](int ti) {   // the tile row touches the W or E band

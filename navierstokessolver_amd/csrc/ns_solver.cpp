@@ -643,14 +643,22 @@ int helm_band(ns_solver* s, double alpha) {
     const int rounds = std::max(1, s->band_sweeps / 3);
     for (int k = 0; k < rounds; k++) {
         const bool odd = k & 1;
+        auto launch = [&]() {
+            return nsg::launch_helm_band(s->g, s->c, alpha, s->omega_v, U, V, odd ? TU : U, odd ? TV : V,
+                                         odd ? U : TU, odd ? V : TV, s->arr[NS_ARR_RU], s->arr[NS_ARR_RV],
+                                         s->band_w, 0, s->st);
+        };
         if (s->nranks > 1) {
+            // the exchange overlapped with the tiles that read no neighbour's rows
             const HaloReq r[4] = {{&s->g, odd ? TU : U, 6}, {&s->g, odd ? TV : V, 6},
                                   {&s->g, s->arr[NS_ARR_RU], 5}, {&s->g, s->arr[NS_ARR_RV], 5}};
-            CHK(halo_reqs(s, r, s->helm_b_pend ? 4 : 2));
+            const int nr = s->helm_b_pend ? 4 : 2;
             s->helm_b_pend = 0;
+            const int n = overlapped(s, r, nr, launch);
+            if (n < 0) return n;
+        } else {
+            launch();
         }
-        nsg::launch_helm_band(s->g, s->c, alpha, s->omega_v, U, V, odd ? TU : U, odd ? TV : V, odd ? U : TU,
-                              odd ? V : TV, s->arr[NS_ARR_RU], s->arr[NS_ARR_RV], s->band_w, 0, s->st);
     }
     if (rounds & 1)
         nsg::launch_helm_band(s->g, s->c, alpha, s->omega_v, U, V, TU, TV, U, V, s->arr[NS_ARR_RU],
