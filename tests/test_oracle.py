@@ -115,3 +115,55 @@ def test_golden_fixtures_reproduced():
         st = s.get()
         np.testing.assert_allclose(st["u"], d["u"], rtol=0, atol=1e-11)
         np.testing.assert_allclose(st["v"], d["v"], rtol=0, atol=1e-11)
+
+
+def test_helm_band_restatement_is_masked_rbsor():
+    """og_helm_band (the GPU's k_helm_band restated) = red-black SOR sweeps of the Helmholtz
+    operator applied only on the cells within `width` of a wall, every other cell held: checked
+    against an independent numpy restatement (uniform cavity; Dirichlet faces add 2/h^2 to the
+    diagonal, FluidSolver.cpp:105-145 + :140-141)."""
+    nx, ny, w, sweeps = 64, 48, 10, 3
+    dt, re, om = 1.0 / 64, 10.0, 1.1
+    alpha = dt / (2 * re)
+    g = OGrid.rectangle(nx, ny)
+    rng = np.random.default_rng(41)
+    u, v, ru, rv = (rng.uniform(-1, 1, nx * ny) for _ in range(4))
+    uu, vv = g.helm_band(alpha, u, v, ru, rv, om, width=w, sweeps=sweeps)
+    cx, cy = alpha * nx * nx, alpha * ny * ny
+    D = np.full((nx, ny), 1 + 2 * cx + 2 * cy)
+    D[0, :] += cx; D[-1, :] += cx; D[:, 0] += cy; D[:, -1] += cy
+
+    def apply(U):
+        o = D * U
+        o[1:, :] -= cx * U[:-1, :]; o[:-1, :] -= cx * U[1:, :]
+        o[:, 1:] -= cy * U[:, :-1]; o[:, :-1] -= cy * U[:, 1:]
+        return o
+
+    I, J = np.meshgrid(np.arange(nx), np.arange(ny), indexing="ij")
+    band = (I < w) | (I >= nx - w) | (J < w) | (J >= ny - w)
+    red = (I + J) % 2 == 0
+    for q, b, ref in ((u, ru, uu), (v, rv, vv)):
+        Q, Bq = q.reshape(nx, ny).copy(), b.reshape(nx, ny)
+        for _ in range(sweeps):
+            for col in (red, ~red):
+                m = col & band
+                # one colour at a time: every cell of the colour sees only the other colour's values
+                Q[m] += om * (Bq - apply(Q))[m] / D[m]
+        assert np.max(np.abs(Q.ravel() - ref)) <= 1e-13 * max(1.0, np.max(np.abs(ref)))
+        assert np.array_equal(ref.reshape(nx, ny)[~band], q.reshape(nx, ny)[~band])
+
+
+def test_multigrid_checks_the_cycle_output():
+    """og_mg_solve stops on the residual of a V-cycle's OUTPUT (the GPU's FUSE_P + RES pass): the
+    returned cycle count is the first whose output meets rtol."""
+    n = 64
+    g = OGrid.rectangle(n, n)
+    rng = np.random.default_rng(43)
+    b = rng.uniform(-1, 1, n * n)
+    b -= b.mean()
+    rtol = 1e-9
+    x, cyc = g.mg_solve(b, rtol=rtol)
+    rel = lambda y: np.linalg.norm(b - g.apply_poisson(y)) / np.linalg.norm(b)   # noqa: E731
+    assert cyc >= 1 and rel(x) <= rtol
+    xm, cm = g.mg_solve(b, rtol=1e-30, maxcycles=cyc - 1)
+    assert cm == cyc - 1 and (cyc == 1 or rel(xm) > rtol)
