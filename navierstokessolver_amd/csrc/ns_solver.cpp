@@ -122,7 +122,7 @@ struct ns_solver {
     bool triple = true;          // 3-sweep passes allowed on this decomposition (slabs >= 2*HALO rows)
     bool sweep3 = true;          // single rank: odd Helmholtz batches start with a 3-sweep pass (k_sweep3)
     bool helm_band = true;       // Helmholtz: wall-band relaxation before the global passes (k_helm_band)
-    int band_w = 128, band_sweeps = 6;   // its width (cells from a wall) and RB-SOR sweeps (a multiple of 3)
+    int band_w = 128, band_sweeps = 6;   // its width (cells from a wall: min(nx, ny) / 32) and RB-SOR sweeps (a multiple of 3)
     bool sweep3_res = true;      // one rank: a Helmholtz batch may end on a 3-sweep pass with its residual
     int helm_probe = 0;          // steps since the Helmholtz first-pass residual was last sampled
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
@@ -1896,6 +1896,10 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_SWEEP")) s->tiled = std::strcmp(e, "tiled") == 0;
     if (const char* e = getenv("NSGPU_SWEEP3")) s->sweep3 = std::atoi(e) != 0;   // A/B: pairs only
     if (const char* e = getenv("NSGPU_HELM_BAND")) s->helm_band = std::atoi(e) != 0;   // A/B: no wall bands
+    // the walls' boundary layers span a fixed fraction of the grid: 1/32 of the shorter side (128
+    // at 4096^2; 8192^2 with 128 needed 8.5 global sweeps per step, with 256: 4.5 -- 7173 -> 8057
+    // MLUPS), at least 32
+    s->band_w = std::max(32, std::min(s->g.nx, s->g.ny) / 32);
     if (const char* e = getenv("NSGPU_BAND_W")) s->band_w = std::max(1, std::atoi(e));   // A/B: band width
     if (const char* e = getenv("NSGPU_BAND_SWEEPS")) s->band_sweeps = std::max(3, std::atoi(e) / 3 * 3);
     if (const char* e = getenv("NSGPU_SWEEP3_RES")) s->sweep3_res = std::atoi(e) != 0;   // A/B: batches end on pairs

@@ -172,8 +172,14 @@ class OGrid:
         r2 = lib().og_helmholtz_rbsor_sweep(self.h, alpha, _d(u), _d(v), _d(_f(ru)), _d(_f(rv)), omega)
         return u, v, r2
 
-    def helm_band(self, alpha, u, v, ru, rv, omega=1.0, width=128, sweeps=6):
-        """k_helm_band restated: RB-SOR sweeps of u, v on the cells within `width` of a wall."""
+    def band_width(self):
+        """The GPU's default wall-band width: 1/32 of the shorter side, at least 32 cells."""
+        return max(32, min(self.nx, self.ny) // 32)
+
+    def helm_band(self, alpha, u, v, ru, rv, omega=1.0, width=None, sweeps=6):
+        """k_helm_band restated: RB-SOR sweeps of u, v on the cells within `width` of a wall
+        (None: the GPU's default, band_width())."""
+        width = self.band_width() if width is None else width
         u, v = _f(u).copy(), _f(v).copy()
         if lib().og_helm_band(self.h, alpha, _d(u), _d(v), _d(_f(ru)), _d(_f(rv)), omega, width, sweeps) != 0:
             raise ValueError(lib().og_last_error().decode())
@@ -223,12 +229,14 @@ class OSolver:
         except Exception:
             pass
 
-    def use_gpu_algorithm(self, omega_v, omega_mg=1.1, band=(128, 6)):
+    def use_gpu_algorithm(self, omega_v, omega_mg=1.1, band=(None, 6)):
         """RB-SOR Helmholtz (after `band` = (width, sweeps) RB-SOR sweeps on the cells within
-        `width` of a wall: k_helm_band; None = no band step) + multigrid Poisson (the GPU path's
-        algorithm; CPU baseline)."""
+        `width` of a wall: k_helm_band; width None = the GPU's default, band=None = no band step)
+        + multigrid Poisson (the GPU path's algorithm; CPU baseline)."""
         lib().og_solver_set_algorithm(self.h, 1, omega_v, omega_mg)
         w, k = band if band else (0, 0)
+        if band and w is None:
+            w = self.g.band_width()
         lib().og_solver_set_band(self.h, w, k)
 
     def step(self):

@@ -436,11 +436,13 @@ def test_two_sweep_pass_equals_two_sweeps(gpu, nx, ny, op):
 
 
 @pytest.mark.parametrize("nx,ny,xr,yr,bc", [(64, 64, -1, -1, BC_CAVITY), (300, 517, 1.003, 0.998, BC_FLOW),
-                                         (97, 45, -1, -1, BC_FLOW), (520, 390, -1, -1, BC_CAVITY)])
+                                         (97, 45, -1, -1, BC_FLOW), (520, 390, -1, -1, BC_CAVITY),
+                                         (1300, 1100, -1, -1, BC_CAVITY)])
 def test_helm_band_matches_oracle(gpu, nx, ny, xr, yr, bc):
     """The Helmholtz wall-band relaxation (k_helm_band: 6 RB-SOR sweeps of u and v on the cells
-    within 128 of a wall, 32 x 32 tiles with their 12-cell cone in LDS) = the oracle's masked
-    sweeps (og_helm_band) to 1e-12; cells off the band keep their values bit for bit."""
+    within min(nx, ny)/32 >= 32 of a wall, two launches of 32 x 32 tiles with their 6-cell cone in
+    LDS) = the oracle's masked sweeps (og_helm_band) to 1e-12; cells off the band keep their
+    values bit for bit."""
     rng = np.random.default_rng(31)
     dt, re = 1.0 / 64, 10.0
     og, gs = pair(gpu, nx, ny, dt, re, bc, xr, yr, omega_v=1.1)
@@ -453,7 +455,8 @@ def test_helm_band_matches_oracle(gpu, nx, ny, xr, yr, bc):
     assert rel(gu, uu) <= 1e-12
     assert rel(gv, vv) <= 1e-12
     I, J = np.meshgrid(np.arange(nx), np.arange(ny), indexing="ij")
-    far = ((I >= 128) & (I < nx - 128) & (J >= 128) & (J < ny - 128)).ravel()
+    w = og.band_width()
+    far = ((I >= w) & (I < nx - w) & (J >= w) & (J < ny - w)).ravel()
     assert np.array_equal(gu[far], u[far]) and np.array_equal(gv[far], v[far])
 
 
