@@ -91,12 +91,12 @@ def _host_threads():
 
 def helm_passes(n, world):
     """HBM passes of one component's n Helmholtz sweeps (ns_solver.cpp helm_sweeps): 3-sweep
-    passes while >= 5 remain (slabs too, unless thinner than 12 rows); one rank may also end on
-    a 3-sweep pass with its residual (3 = 3, 6 = 3+3), otherwise a batch ends on a pair (5 = 3+2);
-    an odd remainder otherwise starts with a single sweep (slabs: 3 = 1+2)."""
+    passes while >= 5 remain (slabs too, unless thinner than 14 rows); a batch may end on a
+    3-sweep pass with its residual (3 = 3, 6 = 3+3; slabs too since HALO = 7), otherwise on a pair
+    (5 = 3+2); an odd remainder otherwise starts with a single sweep."""
     p, r = 0, n
     while r > 0:
-        if r >= 5 or (world == 1 and r in (3, 6)):
+        if r >= 5 or r in (3, 6):
             w = 3
         elif r % 2 and r >= 3:
             w = 1
@@ -107,13 +107,17 @@ def helm_passes(n, world):
     return p
 
 
-def cpu_baseline(n, re, dt, omega_v, omega_mg, state):
+def cpu_baseline(n, re, dt, omega_v, omega_mg, state, gpu_next=None):
     """The oracle (CPU restatement, -O3, OpenMP) running the SAME algorithm as the GPU path
     (RB-SOR Helmholtz to rtol, multigrid V(2,2) Poisson to rtol 1e-8) for one full time step
     of the same n^2 cavity, from the GPU's own state after its warm-up + timed steps (u, v,
     phi, the convective terms): a steady-state step, not the start-up one.
     Timed at 1 thread (the serial reference) and at the host's cores (a bounded sample:
-    ~10-30 s in all).  value = the all-cores rate; value_1thread beside it."""
+    ~10-30 s in all).  value = the all-cores rate; value_1thread beside it.
+    gpu_next = the GPU's own next step from that state (u, v): the oracle's step must agree with
+    it to SURVEY 8(c)'s 1e-6 (both solves to rtol 1e-8) -- parity at the bench's own
+    configuration, reported as `parity`."""
+    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # CPU baseline leg only
 
@@ -121,14 +125,22 @@ def cpu_baseline(n, re, dt, omega_v, omega_mg, state):
     gx, gy = g.grad_phi(state["phi"])
     nt = _host_threads()
     out = {}
+    parity = None
     for threads in (1, nt):
         O.set_threads(threads)
         s = O.OSolver(g, dt, re, rtol=1e-8)
         s.use_gpu_algorithm(omega_v, omega_mg)
         s.set(u=state["u"], v=state["v"], phi=state["phi"], cu=state["cu"], cv=state["cv"], gx=gx, gy=gy)
         t0 = time.perf_counter()
-        _, its = s.step()
+        mm, its = s.step()
         out[threads] = (time.perf_counter() - t0, [int(x) for x in its])
+        if threads == nt and gpu_next is not None:
+            ref = s.get()
+            parity = {"max_abs_du": float(np.max(np.abs(gpu_next["u"] - ref["u"]))),
+                      "max_abs_dv": float(np.max(np.abs(gpu_next["v"] - ref["v"]))),
+                      "oracle_monitor": [float(x) for x in mm], "gpu_monitor": gpu_next["monitor"],
+                      "tol": 1e-6}
+            parity["ok"] = parity["max_abs_du"] <= 1e-6 and parity["max_abs_dv"] <= 1e-6
         del s
     O.set_threads(1)
     t1, its1 = out[1]
@@ -142,16 +154,40 @@ def cpu_baseline(n, re, dt, omega_v, omega_mg, state):
                    f"(MG V(2,2) Poisson: {its1[2]} V-cycles from phi^(n-1) -- the GPU's extrapolated guess needs "
                    f"fewer; RB-SOR Helmholtz: {its1[0]} sweeps per component), {t1:.1f} s on 1 thread, "
                    f"{tn:.1f} s on {nt} threads"),
+        "parity": parity,
     }
+
+
+def self_launch(args) -> int:
+    """--gpus N > 1 without a launcher (no WORLD_SIZE in the env): start N ranks, one per GPU,
+    under torch.distributed.run on 127.0.0.1 as a CHILD process -- before anything here touches
+    the GPU -- and return its exit code.  Rank 0 of the child prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this pool (RCCL)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         world = max(world, 1)
+    if os.environ.get("NSBENCH_LAUNCH_PROBE"):
+        # (tests/test_bench_launch.py: the self-launch reached every rank; nothing touches a GPU)
+        print(json.dumps({"probe_rank": rank, "world": world, "local_rank": local}), flush=True)
+        return
     import torch
     import torch.distributed as dist
 
@@ -327,7 +363,12 @@ def main():
             state = {k: solver.get(a).ravel() for k, a in (("u", nsa.NS_ARR_U), ("v", nsa.NS_ARR_V),
                                                            ("phi", nsa.NS_ARR_PHI), ("cu", nsa.NS_ARR_CU),
                                                            ("cv", nsa.NS_ARR_CV))}
-            line["cpu_baseline"] = cpu_baseline(n, re, dt, solver.omega_v, solver.mg_omega, state)
+            # the GPU's own next step from that state (after the timed region), for the oracle to match
+            st_next = solver.step()
+            gpu_next = {"u": solver.get(nsa.NS_ARR_U).ravel(), "v": solver.get(nsa.NS_ARR_V).ravel(),
+                        "monitor": [st_next[k] for k in ("umin", "umax", "vmin", "vmax")]}
+            line["cpu_baseline"] = cpu_baseline(n, re, dt, solver.omega_v, solver.mg_omega, state, gpu_next)
+            line["parity_vs_oracle"] = line["cpu_baseline"].get("parity")
         except Exception as e:  # the baseline must never hide the GPU line
             line["cpu_baseline"] = {"error": repr(e)}
     print(json.dumps(line), flush=True)

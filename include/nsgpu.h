@@ -33,8 +33,10 @@
 extern "C" {
 #endif
 
-#define NSGPU_ABI_VERSION 3   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
-                                 3: ns_get/set_fields in compact-id order on polygons, ns_local_cells */
+#define NSGPU_ABI_VERSION 4   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
+                                 3: ns_get/set_fields in compact-id order on polygons, ns_local_cells;
+                                 4: NS_POISSON_MG is 0, so a zero-initialised ns_params selects the
+                                    multigrid (RB-SOR moved to 3; the value 2 is rejected) */
 
 typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm */
 
@@ -56,9 +58,9 @@ typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm
                                     preconditions a BiCGStab solve of the true Poisson matrix */
 
 /* Poisson solvers */
-#define NS_POISSON_RBSOR  0  /* fused red-black SOR, one HBM pass per sweep (default) */
-#define NS_POISSON_JACOBI 1  /* weighted Jacobi (ping-pong) */
-#define NS_POISSON_MG     2  /* geometric multigrid V-cycles, RB Gauss-Seidel smoother (default) */
+#define NS_POISSON_MG     0  /* geometric multigrid V-cycles, RB Gauss-Seidel smoother (the default: 0) */
+#define NS_POISSON_JACOBI 1  /* weighted Jacobi sweeps (ping-pong) to rtol: O(n^2) sweeps per solve */
+#define NS_POISSON_RBSOR  3  /* fused red-black SOR sweeps to rtol: O(n) sweeps per solve */
 
 /* One boundary edge of the polygon (Edge, Grid.h:20-26). */
 typedef struct ns_edge {
@@ -72,7 +74,8 @@ typedef struct ns_edge {
  * exactly one edge (found by its normal) -- the streaming / multigrid fast path.
  * Any other polygon (steps, holes, split sides; Grid.cpp:131-185): cell_id and
  * face_edge describe it cell by cell over the nx*ny bounding box; the time step then
- * runs the masked kernels and Jacobi-preconditioned BiCGStab solves. */
+ * runs the masked kernels, a Jacobi-preconditioned BiCGStab Helmholtz solve and a BiCGStab
+ * Poisson solve preconditioned by one V-cycle of the bounding box's multigrid. */
 typedef struct ns_grid_desc {
     int32_t nx, ny;           /* cells in x and y (Grid::hx.size(), hy.size()) */
     const double* hx;         /* nx spacings (Grid::hx) */
@@ -162,8 +165,9 @@ typedef struct ns_stats {
 #define NS_K_RESIDUAL   8  /* Poisson residual ||rhs - mean - L phi||^2 -> out[0] (no update) */
 #define NS_K_POISSON32  9  /* K4 Jacobi x iters on fp32 copies of phi, rhs_phi (fp64 arithmetic and residual,
                               SURVEY.md 8(d) C5); phi <- the fp32 result widened */
-#define NS_K_HELM_BAND 10  /* the Helmholtz solve's wall-band relaxation of u, v (k_helm_band: 3 RB-SOR sweeps
-                              on the cells within 32 of a wall, the rest held); no output */
+#define NS_K_HELM_BAND 10  /* the Helmholtz solve's wall-band relaxation of u, v (k_helm_band: 6 RB-SOR sweeps,
+                              two launches of 3, on the cells within max(32, min(nx, ny) / 32) of a wall,
+                              the rest held); no output */
 
 /* ---- lifecycle: FluidSolver(char*, Grid*) = SolverInitialize + SolverSetup (FluidSolver.cpp:8-58) ---- */
 int  ns_create(const ns_grid_desc* grid, const ns_params* params, ns_solver** out);

@@ -17,7 +17,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "nsgpu.h")
 # ---- constants mirrored from include/nsgpu.h (checked by tests/test_abi.py) ----
 NS_OK, NS_EINVAL, NS_EHIP, NS_ERCCL, NS_ENOMEM, NS_EDIVERGE = 0, -1, -2, -3, -4, -5
 NS_BC_INLET_UNI, NS_BC_INLET_PARABOLIC, NS_BC_WALL, NS_BC_PRESSURE, NS_BC_NEUMANN = 0, 1, 2, 3, 4
-NS_POISSON_RBSOR, NS_POISSON_JACOBI, NS_POISSON_MG = 0, 1, 2
+NS_POISSON_MG, NS_POISSON_JACOBI, NS_POISSON_RBSOR = 0, 1, 3   # ABI 4: zeroed params select MG
 (NS_ARR_U, NS_ARR_V, NS_ARR_PHI, NS_ARR_CU, NS_ARR_CV, NS_ARR_RU, NS_ARR_RV, NS_ARR_RPHI,
  NS_ARR_TMP, NS_ARR_TMPU, NS_ARR_TMPV) = range(11)
 NS_NUM_ARR = 11

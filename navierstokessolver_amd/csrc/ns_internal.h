@@ -7,8 +7,10 @@
 
 namespace nsg {
 
-constexpr int HALO = 6;  // ghost rows per side: K1's MUSCL stencil (2), the 2-sweep pass's cone (4),
-                         // the 2-sweep pass with fused restriction (5), the 3-sweep pass (6)
+constexpr int HALO = 7;  // ghost rows per side: K1's MUSCL stencil (2), the 2-sweep pass's cone (4),
+                         // the 2-sweep pass with fused restriction (5), the 3-sweep pass (6), the
+                         // 3-sweep pass with its output residual (7: slabs end a Helmholtz batch
+                         // on it like one rank does)
 
 // Non-rectangular domains (polygons with holes / steps, Grid.cpp:131-185): one int32 code per
 // cell of the bounding box, in a plane laid out like the fields (halo rows included):
@@ -165,11 +167,13 @@ int launch_restrict(const Geo& gf, const Coef& cf, const double* phi, const doub
 void launch_prolong(const Geo& gf, double* phi, const Geo& gc, const double* ec, hipStream_t st);
 
 // the last pre-smoothing pass with the restriction fused in: two RB sweeps of phi -> out,
-// then the residual of `out` restricted to the coarse rhs bc (+ coarse phi pc := 0) and
-// partials of r^2 over the fine cells (the MG convergence check); needs 5 ghost rows
+// then the residual of `out` restricted to the coarse rhs bc (+ coarse phi pc := 0 unless pc
+// is null: the coarse level's first pass then takes its iterate as zero without reading it)
+// and partials of r^2 over the fine cells (the MG convergence check); needs 5 ghost rows
+// (none of phi with zin: the input iterate is identically zero and is not read)
 int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                                 const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
-                                double* part, hipStream_t st);
+                                double* part, hipStream_t st, bool zin = false);
 
 // the first post-smoothing pass with the prolongation fused in: phi + P(ec) enters two RB
 // sweeps -> out (phi itself is not modified); needs 5 ghost rows of phi, 3 of ec.  part != null:
@@ -182,7 +186,7 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
 // round per pass instead of a row pipeline); same results
 int launch_pois_tile2_restrict(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                                const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
-                               double* part, hipStream_t st);
+                               double* part, hipStream_t st, bool zin = false);
 int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                               const double* rp, const double* shift, const Geo& gc, const double* ec,
                               double* part, hipStream_t st);
@@ -192,9 +196,10 @@ size_t coarse_vcycle_bytes(const Geo& g);
 // the host-built LDS image of the coarse V-cycle (every level's tables + the direct last-level
 // solve's matrix; dn = its size, 0 = RB-SOR sweeps); its size in doubles or < 0
 int cv_image(const double* hx, const double* hy, int nx, int ny, int dlo, int dhi, std::vector<double>& img, int* dn);
+// zin: the level's phi is implicitly zero (not read)
 int launch_coarse_vcycle(const Geo& g, const double* img, int img_n, int dn, double* phi, const double* b, int cycles,
                          int pre, int post, int citers, double comega, double somega, int dlo, int dhi,
-                         hipStream_t st);
+                         hipStream_t st, int zin = 0);
 // the outflow side's 1-D line solve of the Poisson preconditioner into the row p (ny <= 4096;
 // -1 otherwise), and its constant extension along x over `rows` rows of the plane z (from its
 // first halo row) and the single row zg (if not null)

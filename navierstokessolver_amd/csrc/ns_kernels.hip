@@ -26,10 +26,6 @@
 
 #include <algorithm>
 
-#ifndef K1_DIAG
-#define K1_DIAG 0
-#endif
-
 namespace nsg {
 
 // ---------------------------------------------------------------- helpers
@@ -569,16 +565,8 @@ __global__ __launch_bounds__(256) void k_rhs_lds(Geo g, Coef c, double dt, doubl
             auto X = [&](int t, int d) { return tx[t][R - 1 + d]; };
             auto Y = [&](int t, int d) { return ty[t][C - 1 + d]; };
             double cun, cvn, ru_, rv_;
-#if K1_DIAG   // diagnostic build: the tile's memory stream alone (trivial per-cell arithmetic)
-            cun = U(0, 0) + U(-2, 0) + U(2, 0) + U(0, -2) + U(0, 2) + X(0, 0);
-            cvn = V(0, 0) + V(-2, 0) + V(2, 0) + V(0, -2) + V(0, 2) + Y(0, 0);
-            ru_ = cun + scu[R - 2][C - 2];
-            rv_ = cvn + scv[R - 2][C - 2];
-            (void)sizeof(T);
-#else
             rhs_cell<false, T>(g, c, dt, re, U, V, X, Y, phi, li, j, scu[R - 2][C - 2], scv[R - 2][C - 2], cun, cvn,
                                ru_, rv_);
-#endif
             cu[o] = cun;
             cv[o] = cvn;
             ru[o] = ru_;
@@ -617,6 +605,258 @@ __global__ __launch_bounds__(256) void k_rhs_bc(Geo g, Coef c, double dt, double
         const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
         double ru_ = ru[o], rv_ = rv[o];
         rhs_bc(g, c, dt, re, phi, li, j, ru_, rv_);
+        ru[o] = ru_;
+        rv[o] = rv_;
+        acc[0] = ru_ * ru_;
+        acc[1] = rv_ * rv_;
+    }
+    block_reduce_sum<2>(acc, part + 2 * blockIdx.x);
+}
+
+// ---------------------------------------------------------------- K1 as streaming strips
+// k_rhs_s: ConstructRHS_V on the cells at least two from every wall -- the MUSCL stencil's
+// reach, so every neighbour exists and no ghost is evaluated (TopoInner) -- with every MUSCL
+// slope and every face flux computed ONCE.  (rhs_cell, per cell, evaluates 12 slopes and 8 face
+// fluxes -- each face twice, once from each side: ~500 fp64 wave-instructions per cell, K1's
+// bound.)  The strip walk of the sweeps: a wave owns 128 columns (2 per lane, 124 written) and
+// walks L rows; when row r arrives, row r-1's x-slopes are formed (rows r-2 .. r in the
+// window), then the x-face between rows r-2 and r-1 (its two states from those rows' slopes),
+// and row r-2 is complete: its W face is the previous step's, its E face this one's, its y-faces
+// come from row r-2's y-slopes across the lanes (face (c0-1 | c0) per lane, (c0 | c1) inside the
+// lane, the third from lane + 1 by DPP).  Face states / fluxes / the RHS assembly are rhs_cell's
+// expressions, so every value equals the tile kernel's up to FMA contraction.  The ring of cells
+// within two of a wall (and an odd ny's last column) is k_rhs_ring's: rhs_cell<BC> per cell, the
+// ApplyBoundaryConditions terms included.  u, v rows ib-2 .. ie+1 are read (2 ghost rows), cu0 /
+// cv0 at the output rows (updated in place: each lane reads its cells' old values before it
+// stores them), stores through buffer resources (dropped offsets for unwritten lanes / rows).
+struct RhsStreamArgs {
+    Geo g;
+    Coef c;
+    double dt, re;
+    const double *u, *v;
+    double *cu, *cv, *ru, *rv;
+    double* part;                 // 2 per strip: sum ru^2, sum rv^2 of its written cells
+    int nsj, nsi, L;
+    int slo, shi0, nrun;          // strip-row subset of this launch (phase_range)
+    int ilo, ihi, jhi;            // written cells: local rows [ilo, ihi), columns [2, jhi)
+};
+constexpr int RC_K1 = 3;          // k_rhs_s: row tables from row ib-3
+template <bool NT>
+__global__ __launch_bounds__(256) void k_rhs_s(RhsStreamArgs A) {
+    const Geo& g = A.g;
+    const Coef& c = A.c;
+    __shared__ double rcs[4][64 + 2 * RC_K1 + 2][4];   // per row: hx, 1/hx, 2/(h_{i-1}+h_i), 2/(h_i+h_{i+1})
+    const int lane = threadIdx.x & 63;
+    const int nstr = A.nsj * A.nrun;
+    const int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    double (*rc)[4] = rcs[threadIdx.x >> 6];
+    const int run = w / A.nsj;
+    const int wid = phase_block(run, A.slo, A.shi0) * A.nsj + (w - run * A.nsj);
+    const int si = wid / A.nsj, sj = wid - si * A.nsj;
+    const int ib = si * A.L, ie = min(ib + A.L, g.nxl);
+    if (w < nstr) {
+        for (int t = lane; t < ie - ib + 2 * RC_K1 + 2; t += 64) {
+            const int gi = min(max(g.i0 + ib - RC_K1 + t, 0), g.nx - 1);
+            rc[t][0] = c.hx[gi];
+            rc[t][1] = c.rhx[gi];
+            rc[t][2] = c.rsx[gi];
+            rc[t][3] = c.rsx[gi + 1];
+        }
+    }
+    __syncthreads();
+    double acc0 = 0.0, acc1 = 0.0;
+    if (w < nstr) {
+        const int ny = g.ny, ld = g.ld;
+        const int jb = sj * SW;
+        const int c0 = jb - 2 + 2 * lane;
+        const int lc = min(max(c0, 0), ld - 2);
+        const bool wr = lane >= 1 && lane <= 62 && c0 >= 2 && c0 < A.jhi;
+        // column tables (clamped; a clamped column only feeds unwritten lanes)
+        const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c0 + 1, 0), ny - 1), km = min(max(c0 - 1, 0), ny - 1);
+        const double hy0 = c.hy[k0], hy1 = c.hy[k1], hym = c.hy[km];
+        const double ry0 = c.rhy[k0], ry1 = c.rhy[k1];
+        const double rs0 = c.rsy[k0], rs1 = c.rsy[k1], rs2 = c.rsy[min(k1 + 1, ny)];
+        const double dt = A.dt, hre = 0.5 / A.re;
+        const int rlo = -HALO, rhi = g.nxl + HALO - 1;
+        const __amdgpu_buffer_rsrc_t bcu = __builtin_amdgcn_make_buffer_rsrc(A.cu, (short)0, 0x7FFFFFF0, 0x00020000);
+        const __amdgpu_buffer_rsrc_t bcv = __builtin_amdgcn_make_buffer_rsrc(A.cv, (short)0, 0x7FFFFFF0, 0x00020000);
+        const __amdgpu_buffer_rsrc_t bru = __builtin_amdgcn_make_buffer_rsrc(A.ru, (short)0, 0x7FFFFFF0, 0x00020000);
+        const __amdgpu_buffer_rsrc_t brv = __builtin_amdgcn_make_buffer_rsrc(A.rv, (short)0, 0x7FFFFFF0, 0x00020000);
+        // one row of u, v (row r) and of cu0, cv0 (row r-2, the output row of that step)
+        double2 QU[SD], QV[SD], QC[SD], QD[SD];
+        auto load = [&](int r, double2& qu, double2& qv, double2& qc, double2& qd) {
+            const int lr = min(max(r, rlo), rhi), lo = min(max(r - 2, 0), g.nxl - 1);
+            qu = *reinterpret_cast<const double2*>(A.u + (ptrdiff_t)lr * ld + lc);
+            qv = *reinterpret_cast<const double2*>(A.v + (ptrdiff_t)lr * ld + lc);
+            qc = *reinterpret_cast<const double2*>(A.cu + (ptrdiff_t)lo * ld + lc);
+            qd = *reinterpret_cast<const double2*>(A.cv + (ptrdiff_t)lo * ld + lc);
+        };
+        // window rows r-3 .. r; x-slopes of rows r-2 (SP*) and r-1 (SC*); the x-face (r-3 | r-2)'s fluxes
+        double2 U0 = {0, 0}, U1 = {0, 0}, U2 = {0, 0}, U3 = {0, 0};
+        double2 V0 = {0, 0}, V1 = {0, 0}, V2 = {0, 0}, V3 = {0, 0};
+        double2 SPu = {0, 0}, SPv = {0, 0};
+        double2 FWnn = {0, 0}, FWuv = {0, 0};
+        auto xslope = [&](double qm, double qc, double qp, const double* rw) {
+            return minmode_nd((qp - qc) * rw[3], (qc - qm) * rw[2]);
+        };
+        auto step = [&](const double2 qu, const double2 qv, const double2 cu0, const double2 cv0, int r) {
+            U0 = U1; U1 = U2; U2 = U3; U3 = vcopy(qu);
+            V0 = V1; V1 = V2; V2 = V3; V3 = vcopy(qv);
+            const double* rm = rc[r - 2 - ib + RC_K1];   // output row m = r-2
+            const double* rn = rc[r - 1 - ib + RC_K1];   // row r-1
+            // x-slopes of row r-1
+            const double2 SCu = make_double2(xslope(U1.x, U2.x, U3.x, rn), xslope(U1.y, U2.y, U3.y, rn));
+            const double2 SCv = make_double2(xslope(V1.x, V2.x, V3.x, rn), xslope(V1.y, V2.y, V3.y, rn));
+            // x-face (r-2 | r-1): left states from row r-2, right from row r-1 (rhs_cell's C[2] / C[0])
+            const double hxm = rm[0], hxn = rn[0];
+            double2 FEnn, FEuv;
+            {
+                const double ul0 = U1.x + hxm / 2 * SPu.x, vl0 = V1.x + hxm / 2 * SPv.x;
+                const double ur0 = U2.x - hxn / 2 * SCu.x, vr0 = V2.x - hxn / 2 * SCv.x;
+                const double ul1 = U1.y + hxm / 2 * SPu.y, vl1 = V1.y + hxm / 2 * SPv.y;
+                const double ur1 = U2.y - hxn / 2 * SCu.y, vr1 = V2.y - hxn / 2 * SCv.y;
+                FEnn = make_double2(fnn(ul0, ur0), fnn(ul1, ur1));
+                FEuv = make_double2(fuv(ul0, vl0, ur0, vr0), fuv(ul1, vl1, ur1, vr1));
+            }
+            // row m = r-2: y-slopes across the lanes (columns c0 - 1 .. c1 + 1)
+            const double um = lane_up1(U1.y), up = lane_dn1(U1.x), vm = lane_up1(V1.y), vp = lane_dn1(V1.x);
+            const double su0 = minmode_nd((U1.y - U1.x) * rs1, (U1.x - um) * rs0);
+            const double su1 = minmode_nd((up - U1.y) * rs2, (U1.y - U1.x) * rs1);
+            const double sv0 = minmode_nd((V1.y - V1.x) * rs1, (V1.x - vm) * rs0);
+            const double sv1 = minmode_nd((vp - V1.y) * rs2, (V1.y - V1.x) * rs1);
+            const double sum_ = lane_up1(su1), svm = lane_up1(sv1);   // column c0 - 1's slopes
+            // y-faces (c0-1 | c0) and (c0 | c1): lower / upper states (rhs_cell's C[4..7])
+            double fa_nn, fa_uv, fb_nn, fb_uv;
+            {
+                const double u1 = um + hym / 2 * sum_, v1 = vm + hym / 2 * svm;
+                const double u2 = U1.x - hy0 / 2 * su0, v2 = V1.x - hy0 / 2 * sv0;
+                fa_nn = fnn(v1, v2);
+                fa_uv = fuv(u1, v1, u2, v2);
+            }
+            {
+                const double u1 = U1.x + hy0 / 2 * su0, v1 = V1.x + hy0 / 2 * sv0;
+                const double u2 = U1.y - hy1 / 2 * su1, v2 = V1.y - hy1 / 2 * sv1;
+                fb_nn = fnn(v1, v2);
+                fb_uv = fuv(u1, v1, u2, v2);
+            }
+            const double fc_nn = lane_dn1(fa_nn), fc_uv = lane_dn1(fa_uv);   // (c1 | c1+1)
+            // the cells of row m
+            const double rx = rm[1], sxW = rm[2], sxE = rm[3];
+            double out[4][2];
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const double uc = e ? U1.y : U1.x, vc = e ? V1.y : V1.x;
+                const double uW = e ? U0.y : U0.x, vW = e ? V0.y : V0.x, uE = e ? U2.y : U2.x, vE = e ? V2.y : V2.x;
+                const double uS = e ? U1.x : um, vS = e ? V1.x : vm, uN = e ? up : U1.y, vN = e ? vp : V1.y;
+                const double ry = e ? ry1 : ry0, syS = e ? rs1 : rs0, syN = e ? rs2 : rs1;
+                double ru_ = 0.0 + 1.0 * uc, rv_ = 0.0 + 1.0 * vc;
+                ru_ += 0.5 * dt * (e ? cu0.y : cu0.x);
+                rv_ += 0.5 * dt * (e ? cv0.y : cv0.x);
+                double D0 = hre * (uc - uW) * sxW, D1 = hre * (uE - uc) * sxE;
+                double D2 = hre * (uc - uS) * syS, D3 = hre * (uN - uc) * syN;
+                ru_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
+                D0 = hre * (vc - vW) * sxW; D1 = hre * (vE - vc) * sxE;
+                D2 = hre * (vc - vS) * syS; D3 = hre * (vN - vc) * syN;
+                rv_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
+                // C[0..3] from the x-faces (W: previous step, E: this one), C[4..7] from the y-faces
+                const double C0 = e ? FWnn.y : FWnn.x, C1 = e ? FWuv.y : FWuv.x;
+                const double C2 = e ? FEnn.y : FEnn.x, C3 = e ? FEuv.y : FEuv.x;
+                const double C4 = e ? fb_uv : fa_uv, C5 = e ? fb_nn : fa_nn;
+                const double C6 = e ? fc_uv : fb_uv, C7 = e ? fc_nn : fb_nn;
+                double val = (C2 - C0) * rx + (C6 - C4) * ry;
+                out[0][e] = val;
+                ru_ += val * (-1.5 * dt);
+                val = (C3 - C1) * rx + (C7 - C5) * ry;
+                out[1][e] = val;
+                rv_ += val * (-1.5 * dt);
+                out[2][e] = ru_;
+                out[3][e] = rv_;
+            }
+            const int m = r - 2;
+            const bool live = m >= ib && m < ie && m >= A.ilo && m < A.ihi;
+            if (live && wr) {
+                acc0 += out[2][0] * out[2][0] + out[2][1] * out[2][1];
+                acc1 += out[3][0] * out[3][0] + out[3][1] * out[3][1];
+            }
+            const unsigned off = (live && wr) ? ((unsigned)m * (unsigned)ld + (unsigned)c0) * 8u : OOB;
+            auto st2 = [&](__amdgpu_buffer_rsrc_t rs, int k) {
+                const nsu4 d = {(unsigned)__double2loint(out[k][0]), (unsigned)__double2hiint(out[k][0]),
+                                (unsigned)__double2loint(out[k][1]), (unsigned)__double2hiint(out[k][1])};
+                __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)off, 0, NT ? 2 : 0);
+            };
+            st2(bcu, 0);
+            st2(bcv, 1);
+            st2(bru, 2);
+            st2(brv, 3);
+            FWnn = FEnn; FWuv = FEuv;
+            SPu = SCu; SPv = SCv;
+        };
+        // rows ib-2 .. ie+1 (the first two steps only fill the window; row ib-1's slope needs ib)
+        const int r0 = ib - 2, r1 = ie + 1;
+#pragma unroll
+        for (int q = 0; q < SD; q++) {
+            load(r0 + q, QU[q], QV[q], QC[q], QD[q]);
+            asm volatile("" ::: "memory");
+        }
+        for (int r = r0; r <= r1; r += SD) {
+#pragma unroll
+            for (int q = 0; q < SD; q++) {
+                step(QU[q], QV[q], QC[q], QD[q], r + q);   // (rows past r1: computed, not stored)
+                load(r + q + SD, QU[q], QV[q], QC[q], QD[q]);
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        acc0 += __shfl_xor(acc0, off, 64);
+        acc1 += __shfl_xor(acc1, off, 64);
+    }
+    if (lane == 0 && w < nstr) {
+        A.part[2 * wid] = acc0;
+        A.part[2 * wid + 1] = acc1;
+    }
+}
+
+// the ring of k_rhs_s: the slab's cells within two rows of the W / E walls (whole rows), and on
+// the other rows the columns 0, 1 and [jhi, ny) -- rhs_cell<BC> per cell (ghosts, the MUSCL
+// stencil's wall cases and the ApplyBoundaryConditions terms), global loads; partials (ru^2, rv^2)
+// per block.  Thread k: the whole wall rows first (nfull of them, from local row fr[q]), then
+// (ncol columns) x the other rows.
+struct RhsRingArgs {
+    int nfull, fr[4];             // whole rows (local indices)
+    int ncol, jhi;                // ring columns per other row: 0, 1, jhi .. ny-1
+    int rlo, rhi;                 // the other rows: local [rlo, rhi)
+    int n;                        // ring cells
+};
+__global__ __launch_bounds__(256) void k_rhs_ring(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
+                                                  const double* __restrict__ v, const double* __restrict__ phi,
+                                                  double* __restrict__ cu, double* __restrict__ cv,
+                                                  double* __restrict__ ru, double* __restrict__ rv,
+                                                  double* __restrict__ part, RhsRingArgs R) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    double acc[2] = {0.0, 0.0};
+    if (k < R.n) {
+        int li, j;
+        const int nf = R.nfull * g.ny;
+        if (k < nf) {
+            const int q = k / g.ny;
+            li = R.fr[q];
+            j = k - q * g.ny;
+        } else {
+            const int q = (k - nf) / R.ncol, e = (k - nf) - q * R.ncol;
+            li = R.rlo + q;
+            j = e < 2 ? e : R.jhi + (e - 2);
+        }
+        const int ld = g.ld, gi = g.i0 + li;
+        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+        auto U = [&](int di, int dj) { return ldf(u, ld, li + di, j + dj); };
+        auto V = [&](int di, int dj) { return ldf(v, ld, li + di, j + dj); };
+        auto X = [&](int t, int d) { return (t == 0 ? c.hx : t == 1 ? c.rhx : c.rsx)[gi + d]; };
+        auto Y = [&](int t, int d) { return (t == 0 ? c.hy : t == 1 ? c.rhy : c.rsy)[j + d]; };
+        double cun, cvn, ru_, rv_;
+        rhs_cell<true, TopoRect>(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
+        cu[o] = cun;
+        cv[o] = cvn;
         ru[o] = ru_;
         rv[o] = rv_;
         acc[0] = ru_ * ru_;
@@ -1007,7 +1247,7 @@ __global__ __launch_bounds__(256) void k_sweep(StreamArgs a) {
     __shared__ double rcs[4][RC_MAX][4];
     const int lane = threadIdx.x & 63;
     const int nstr = a.nsj * a.nsi;
-    const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double (*rc)[4] = rcs[threadIdx.x >> 6];
     if (wid < nstr) stage_rows<OP>(a, rc, (wid / a.nsj) * a.L, lane);
     __syncthreads();
@@ -1189,7 +1429,7 @@ __global__ __launch_bounds__(256) void k_jacobi_s(JacobiArgs<T> a) {
     __shared__ double rcs[4][RC_MAX][3];
     const int lane = threadIdx.x & 63;
     const int nstr = a.nsj * a.nsi;
-    const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    const int wid = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double (*rc)[3] = rcs[threadIdx.x >> 6];
     if (wid < nstr) {
         const int ib = (wid / a.nsj) * a.L;
@@ -1481,9 +1721,6 @@ constexpr int SW2X = 116;
 #ifndef SD2_HELM
 #define SD2_HELM 3
 #endif
-#ifndef SWEEP2_DIAG
-#define SWEEP2_DIAG 0
-#endif
 #ifndef SD2_HELMR
 #define SD2_HELMR SD2_HELM
 #endif
@@ -1511,7 +1748,10 @@ constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2, FUSE_UV = 3;
 // one strip of k_sweep2, walked downwards (DIR = 1) or upwards (DIR = -1); returns the
 // strip's residual partial (R5)
 // (two instantiations: runtime window selects would cost ~50 VGPRs)
-template <int OP, bool RES, int FUSE, int DIR>
+// ZIN (FUSE_R only): the input iterate is identically zero -- a coarse level's first pass of a
+// V-cycle, whose phi the restriction above no longer stores as zeros: no phi read at all (the
+// same values as reading the zeros)
+template <int OP, bool RES, int FUSE, int DIR, bool ZIN = false>
 __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
                                               int lane) {
     constexpr int SD2 = sd2_of<OP, RES, FUSE>();
@@ -1578,7 +1818,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     };
     auto load = [&](int slot_r, double2& p, double2& bb, double& ee) {
         const int lp = min(max(slot_r, phi_lo), phi_hi), lb = min(max(slot_r - DIR, b_lo), b_hi);
-        p = ld_stream(a.in + (ptrdiff_t)lp * ld + lc, XP ? 1 : 0);   // compile-time policy: no branch
+        p = ZIN ? make_double2(0.0, 0.0) : ld_stream(a.in + (ptrdiff_t)lp * ld + lc, XP ? 1 : 0);   // (no branch)
         bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
         if (XP) ee = a.ec[(ptrdiff_t)nbr(lp) * a.ldc + Jl];
     };
@@ -1600,29 +1840,17 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
         double2 o = W1;
         const int gi = a.i0 + row;
         if (gi < 0 || gi >= a.nx) return o;
-#if SWEEP2_DIAG == 1   // diagnostic build (tools/sweep2_diag.py): the memory stream alone
-        o.x += B.x; o.y += B.y;
-        return o;
-#endif
         const double* rw = rc[row - ib + RC_OFF];
         const double cw = rw[0], ce = rw[1];
         double rr;
         // the row's colour is in one of the lane's two columns (wave-uniform): only that
         // column's diagonal, reciprocal and j-neighbour shuffle are formed
         if ((gi & 1) == par) {
-#if SWEEP2_DIAG == 2   // diagnostic: no cross-lane shuffles
-            const double lf = W1.y;
-#else
             const double lf = lane_up1(W1.y);
-#endif
             const double d = diag<OP>(rw[2], cd0, alpha), w = omega * rcp_nr(d);
             if (v0) o.x = relax<OP>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr);
         } else {
-#if SWEEP2_DIAG == 2
-            const double rt = W1.x;
-#else
             const double rt = lane_dn1(W1.x);
-#endif
             const double d = diag<OP>(rw[2], cd1, alpha), w = omega * rcp_nr(d);
             if (v1) o.y = relax<OP>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, d, w, alpha, rr);
         }
@@ -1719,7 +1947,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
                         } else if (wr) {
                             const ptrdiff_t o = (ptrdiff_t)(m5 >> 1) * a.ldc + (c0 >> 1);
                             a.bc[o] = xs / ((hxr + hxo) * (hy0 + hy1));
-                            a.pc[o] = 0.0;
+                            if (a.pc) a.pc[o] = 0.0;   // (null: the coarse pass reads zeros implicitly)
                         }
                     }
                 } else if (((a.i0 + m5) & 1) == 0) {
@@ -1735,7 +1963,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
                     } else if (wr) {
                         const ptrdiff_t o = (ptrdiff_t)(m5 >> 1) * a.ldc + (c0 >> 1);
                         a.bc[o] = xs / ((hxe + hxr) * (hy0 + hy1));
-                        a.pc[o] = 0.0;
+                        if (a.pc) a.pc[o] = 0.0;
                     }
                 }
             }
@@ -1776,7 +2004,8 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
 // the same arithmetic as three single sweeps (bit-identical).  FUSE_UV: u and v in one launch.
 // RES: a seventh stage at row r-7 takes the residual of the finished values (the batch's last
 // pass: its partials of r^2 per strip are the convergence check's); the cone grows by one cell:
-// rows ib-7 .. ie+6, 112 written columns (SW3R), 7 ghost rows -- one rank only (HALO = 6)
+// rows ib-7 .. ie+6, 112 written columns (SW3R), 7 ghost rows (HALO = 7: slabs too; FUSE_UV + RES is
+// the multi-rank batch end, u and v in one launch, v's partials at part2)
 constexpr int SW3R = SW2X - 4;
 template <int DIR, bool RES>
 __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
@@ -1902,12 +2131,12 @@ template <int FUSE, bool RES = false>
 __global__ __launch_bounds__(256) void k_sweep3(StreamArgs a) {
     __shared__ double rcs[4][RC_MAX3][4];
     const int nstr = a.nsj * a.nrun;
-    int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double (*rc)[4] = rcs[threadIdx.x >> 6];
     StreamArgs af = a;
     if (FUSE == FUSE_UV && w >= nstr) {
         w -= nstr;
-        af.in = a.in2; af.out = a.out2; af.b = a.b2;
+        af.in = a.in2; af.out = a.out2; af.b = a.b2; af.part = a.part2;
     }
     const int lane = threadIdx.x & 63;
     const int run = w / a.nsj, sj = w - run * a.nsj;
@@ -1928,14 +2157,14 @@ __global__ __launch_bounds__(256) void k_sweep3(StreamArgs a) {
     }
 }
 
-template <int OP, bool RES, int FUSE>
+template <int OP, bool RES, int FUSE, bool ZIN = false>
 __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
     constexpr bool XR = FUSE == FUSE_R;
     constexpr bool R5 = RES || XR;                 // the fifth (output residual) stage
     __shared__ double rcs[4][RC_MAX][4];
     const int lane = threadIdx.x & 63;
     const int nstr = a.nsj * a.nrun;
-    int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double (*rc)[4] = rcs[threadIdx.x >> 6];
     // the second field's waves (nf = 2; wave-uniform, same coefficient tables)
     StreamArgs af = a;
@@ -1958,7 +2187,7 @@ __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
         // coarse sums differently, and its values would depend on how a pass is cut into strips
         // (the overlapped exchange's split, the slab height)
         if (FUSE != FUSE_R && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1>(af, rc, ib, ie, sj, lane);
-        else res = sweep2_strip<OP, RES, FUSE, 1>(af, rc, ib, ie, sj, lane);
+        else res = sweep2_strip<OP, RES, FUSE, 1, ZIN>(af, rc, ib, ie, sj, lane);
     }
     if (R5) {
 #pragma unroll
@@ -1967,8 +2196,8 @@ __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
     }
 }
 
-template <int OP, bool RES, int FUSE>
-__global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) { sweep2_body<OP, RES, FUSE>(a); }
+template <int OP, bool RES, int FUSE, bool ZIN = false>
+__global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) { sweep2_body<OP, RES, FUSE, ZIN>(a); }
 
 // ------------------------------------------------ K4 small levels: LDS-tiled fused passes
 // The multigrid levels below the streaming kernels' range (< 2048^2 cells: 1024^2 .. 128^2
@@ -1987,7 +2216,8 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) { sweep2_body<OP, 
 // times the workgroups and a quarter of the work per half-sweep -- these levels are latency-bound,
 // so the larger cone overhead costs nothing (128^2 / 256^2: 8.2 -> 5.4 us per FUSE_R pass, 512^2:
 // 8.8 -> 7.6 us; at 1024^2 16 x 16 tiles measured 0.3 % slower overall, so 32 stays there)
-template <int FUSE, int TT, bool RES = false>
+// ZIN (FUSE_R): the input iterate is identically zero (see sweep2_strip): no phi load
+template <int FUSE, int TT, bool RES = false, bool ZIN = false>
 __global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
     constexpr bool XR = FUSE == FUSE_R, XP = FUSE == FUSE_P;
     constexpr bool R5 = XR || RES;   // the output residual (RES: FUSE_P's, partials only)
@@ -2018,7 +2248,7 @@ __global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
             const int r = q / E, cc = q - r * E;
             const int li = min(max(li0 - R + r, rlo), rhi);
             const int j = min(max(j0 - R + cc, 0), ny - 1);
-            pv[k] = a.in[(ptrdiff_t)li * ld + j];
+            pv[k] = ZIN ? 0.0 : a.in[(ptrdiff_t)li * ld + j];
             bv[k] = a.b[(ptrdiff_t)li * ld + j];
         }
     }
@@ -2140,7 +2370,7 @@ __global__ __launch_bounds__(256) void k_tile2(StreamArgs a, int tiles_j) {
             xs = xs + (rw[r + 1][3] * cl[cc + 1][3]) * sb[r + 1][cc + 1];
             const ptrdiff_t o = (ptrdiff_t)(li >> 1) * a.ldc + (j >> 1);
             a.bc[o] = xs / ((rw[r][3] + rw[r + 1][3]) * (cl[cc][3] + cl[cc + 1][3]));
-            a.pc[o] = 0.0;
+            if (a.pc) a.pc[o] = 0.0;
         }
         if (a.part) {
             double x[1] = {res};
@@ -2411,17 +2641,6 @@ __global__ __launch_bounds__(256) void k_prolong(Geo gf, double* __restrict__ ph
 constexpr int LV_MAX = 8;
 constexpr int CV_THREADS = 1024;
 
-// diagnostic build (CV_DIAG=1, tools/cv_diag.py): thread 0 stamps the 100 MHz wall clock at the
-// phase boundaries of the last launch into g_cv_t (vector stores), read back by nsg_cv_diag
-#ifndef CV_DIAG
-#define CV_DIAG 0
-#endif
-#if CV_DIAG
-__device__ unsigned long long g_cv_t[64];
-#define CV_STAMP(k) do { if (threadIdx.x == 0) g_cv_t[k] = wall_clock64(); } while (0)
-#else
-#define CV_STAMP(k) do { } while (0)
-#endif
 
 struct LdsLv {
     int nx, ny, phi, b, idg, cw, ce, cs, cn, hx, hy;  // offsets in doubles
@@ -2550,11 +2769,10 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
                                                               int dn, double* __restrict__ phi,
                                                               const double* __restrict__ b, int cycles, int pre,
                                                               int post, int citers, double comega, double somega,
-                                                              int dlo, int dhi) {
+                                                              int dlo, int dhi, int zin) {
     extern __shared__ __attribute__((aligned(16))) double L[];
     __shared__ LdsLv lv[LV_MAX];
     __shared__ int nlev;
-    CV_STAMP(0);
     if (threadIdx.x == 0) {
         lv_layout(g.nx, g.ny, lv, &nlev);
         for (int k = 0; k < nlev; k++) { lv[k].dlo = dlo; lv[k].dhi = dhi; }
@@ -2575,14 +2793,12 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
         for (int t = threadIdx.x; t < n0; t += CV_THREADS) {
             int i, j;
             lv_split(v, t, i, j);
-            L[t] = ldf(phi, g.ld, i, j);
+            L[t] = zin ? 0.0 : ldf(phi, g.ld, i, j);   // (zin: the level's phi is implicitly zero)
             L[n0 + t] = ldf(b, g.ld, i, j);
         }
     }
     __syncthreads();
-    CV_STAMP(1);
     const int nl = nlev;
-    CV_STAMP(2);
     for (int cyc = 0; cyc < cycles; cyc++) {
         for (int k = 0; k < nl - 1; k++) {
             const LdsLv f = lv[k], v = lv[k + 1];
@@ -2603,7 +2819,6 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
                 L[v.phi + t] = 0.0;
             }
             __syncthreads();
-            if (cyc == 0) CV_STAMP(3 + k);
         }
         if (dn > 0) {
             // x = M b (M after the levels in the image)
@@ -2618,7 +2833,6 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
         } else {
             lv_rb_last(L, lv[nl - 1], comega, citers);
         }
-        if (cyc == 0) CV_STAMP(12);
         for (int k = nl - 2; k >= 0; k--) {
             const LdsLv f = lv[k], v = lv[k + 1];
             for (int t = threadIdx.x; t < f.nx * f.ny; t += CV_THREADS) {
@@ -2638,7 +2852,6 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
             }
             __syncthreads();
             lv_rb(L, f, somega, post);
-            if (cyc == 0) CV_STAMP(13 + k);
         }
     }
     {
@@ -2649,15 +2862,8 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
             phi[(ptrdiff_t)i * g.ld + j] = L[v.phi + t];
         }
     }
-    CV_STAMP(21);
 }
 
-#if CV_DIAG
-// the last k_coarse_vcycle launch's stamps (diagnostic builds only)
-extern "C" int nsg_cv_diag(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cv_t), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : -1;
-}
-#endif
 
 // ---------------------------------------------------------------- reductions
 __global__ __launch_bounds__(1024) void k_reduce_sum(const double* __restrict__ p, int n, int nv,
@@ -3014,7 +3220,42 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
             NS_LAUNCH(k_rhs<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
         return (int)(cg.x * cg.y);
     }
-    if (!(e && std::strcmp(e, "global") == 0)) {
+    if (!e) {
+        // the streaming inner kernel (k_rhs_s) and its wall ring (k_rhs_ring)
+        RhsStreamArgs A{};
+        A.g = g; A.c = c; A.dt = dt; A.re = re; A.u = u; A.v = v; A.cu = cu; A.cv = cv; A.ru = ru; A.rv = rv;
+        A.part = part;
+        A.jhi = std::max(2, (g.ny - 2) & ~1);
+        A.ilo = std::max(0, std::min(2 - g.i0, g.nxl));
+        A.ihi = std::max(A.ilo, std::min(g.nx - 2 - g.i0, g.nxl));
+        A.nsj = (g.ny + SW - 1) / SW;
+        const void* kk = (const void*)k_rhs_s<true>;
+        A.L = strip_rows(g.nxl, A.nsj, resident_waves(kk), 8);
+        A.nsi = (g.nxl + A.L - 1) / A.L;
+        const int nstr = A.nsj * A.nsi;
+        A.nrun = phase_range(g.nxl, A.L, A.nsi, 2, &A.slo, &A.shi0);   // u, v rows ib-2 .. ie+1
+        if (A.nrun > 0 && A.jhi > 2 && A.ihi > A.ilo)
+            NS_LAUNCH(k_rhs_s<true>, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), 0, st, A);
+        else if (g_phase != 1)
+            (void)hipMemsetAsync(part, 0, 2 * sizeof(double) * nstr, st);   // (no inner cells: zero partials)
+        RhsRingArgs R{};
+        R.jhi = A.jhi;
+        for (int li = 0; li < g.nxl; li++)
+            if ((li < A.ilo || li >= A.ihi) && R.nfull < 4) R.fr[R.nfull++] = li;
+        R.rlo = A.ilo;
+        R.rhi = A.ihi;
+        R.ncol = 2 + (g.ny - A.jhi);
+        if (A.jhi <= 2) R.ncol = g.ny;   // (tiny grids: whole rows, columns 0, 1 and from jhi = 2 on)
+        R.n = R.nfull * g.ny + (R.rhi - R.rlo) * R.ncol;
+        const int nring = (R.n + 255) / 256;
+        if (R.nfull == 4 && A.ilo + (g.nxl - A.ihi) > 4) return -1;   // (cannot happen: ilo <= 2, nxl - ihi <= 2)
+        // the ring reads phi's and u, v's ghost rows (wall terms, MUSCL): with the edge phase
+        if (g_phase != 1 && nring > 0)
+            NS_LAUNCH(k_rhs_ring, dim3(nring), dim3(256), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv,
+                      part + 2 * nstr, R);
+        return nstr + nring;
+    }
+    if (std::strcmp(e, "global") != 0) {   // NSGPU_RHS=lds: the LDS-tiled K1 (A/B)
         const int nti = (g.nxl + RT - 1) / RT;
         int tlo, thi0;
         const int nrun = phase_range(g.nxl, RT, nti, 2, &tlo, &thi0);   // MUSCL: rows li0-2 .. li0+RT+1
@@ -3279,13 +3520,16 @@ static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st, bool count
 
 int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                                 const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
-                                double* part, hipStream_t st) {
+                                double* part, hipStream_t st, bool zin) {
     StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
     a.hx = c.hx; a.hy = c.hy; a.bc = bc; a.pc = pc; a.ldc = gc.ld;
     a.nsj = (g.ny + SW2X - 1) / SW2X;
     int nblk = 0;
-    const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2<0, false, FUSE_R>), 5, &nblk);
-    if (nblk) NS_LAUNCH((k_sweep2<0, false, FUSE_R>), dim3(nblk), dim3(256), 0, st, a);
+    const void* k = zin ? (const void*)k_sweep2<0, false, FUSE_R, true> : (const void*)k_sweep2<0, false, FUSE_R>;
+    const int nstr = plan_strips2(a, resident_waves(k), 5, &nblk);
+    if (!nblk) return nstr;
+    if (zin) NS_LAUNCH((k_sweep2<0, false, FUSE_R, true>), dim3(nblk), dim3(256), 0, st, a);
+    else NS_LAUNCH((k_sweep2<0, false, FUSE_R>), dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 
@@ -3313,24 +3557,24 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
 }
 
 // the LDS-tiled versions of the two launchers above (small levels); TT x TT tiles
-template <int FUSE, bool RES = false>
+template <int FUSE, bool RES = false, bool ZIN = false>
 static int launch_tile2(const StreamArgs& a, const Geo& g, hipStream_t st) {
     const int tj32 = (g.ny + 31) / 32, n32 = tj32 * ((g.nxl + 31) / 32);
     if (n32 >= 512) {
-        NS_LAUNCH((k_tile2<FUSE, 32, RES>), dim3(n32), dim3(256), 0, st, a, tj32);
+        NS_LAUNCH((k_tile2<FUSE, 32, RES, ZIN>), dim3(n32), dim3(256), 0, st, a, tj32);
         return n32;
     }
     const int tj = (g.ny + 15) / 16, n = tj * ((g.nxl + 15) / 16);
-    NS_LAUNCH((k_tile2<FUSE, 16, RES>), dim3(n), dim3(256), 0, st, a, tj);
+    NS_LAUNCH((k_tile2<FUSE, 16, RES, ZIN>), dim3(n), dim3(256), 0, st, a, tj);
     return n;
 }
 
 int launch_pois_tile2_restrict(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
                                const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
-                               double* part, hipStream_t st) {
+                               double* part, hipStream_t st, bool zin) {
     StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
     a.hx = c.hx; a.hy = c.hy; a.bc = bc; a.pc = pc; a.ldc = gc.ld;
-    return launch_tile2<FUSE_R>(a, g, st);
+    return zin ? launch_tile2<FUSE_R, false, true>(a, g, st) : launch_tile2<FUSE_R>(a, g, st);
 }
 
 int launch_pois_tile2_prolong(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
@@ -3385,13 +3629,20 @@ int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, 
                        double* part) {
     StreamArgs a = stream_args(g, c, which == 2 ? v : u, which == 2 ? vo : uo, which == 2 ? rv : ru, nullptr, alpha,
                                omega, part, true);
-    if (part) {   // the batch's last pass with its output residual (one field, one rank: 7-row cone)
-        if (which == 3 || g.i0 != 0 || g.nxl != g.nx) return -1;
+    if (part) {   // the batch's last pass with its output residual (7-row cone: 7 ghost rows on slabs)
         a.nsj = (g.ny + SW3R - 1) / SW3R;
         int nblk = 0;
-        const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep3<FUSE_NONE, true>), 7, &nblk);
+        const void* kr = which == 3 ? (const void*)k_sweep3<FUSE_UV, true> : (const void*)k_sweep3<FUSE_NONE, true>;
+        const int nstr = plan_strips2(a, resident_waves(kr), 7, &nblk);
         if (which == 2) a.part = part + nstr;   // partials: u at [0, n), v at [n, 2n) (launch_helm_sweep2)
-        if (nblk) NS_LAUNCH((k_sweep3<FUSE_NONE, true>), dim3(nblk), dim3(256), 0, st, a);
+        if (!nblk) return nstr;
+        if (which == 3) {
+            a.in2 = v; a.out2 = vo; a.b2 = rv; a.part2 = part + nstr;
+            nblk = (2 * a.nsj * a.nrun + 3) / 4;
+            NS_LAUNCH((k_sweep3<FUSE_UV, true>), dim3(nblk), dim3(256), 0, st, a);
+        } else {
+            NS_LAUNCH((k_sweep3<FUSE_NONE, true>), dim3(nblk), dim3(256), 0, st, a);
+        }
         return nstr;
     }
     a.nsj = (g.ny + SW2X - 1) / SW2X;
@@ -3639,7 +3890,7 @@ int cv_image(const double* hx, const double* hy, int nx, int ny, int dlo, int dh
 
 int launch_coarse_vcycle(const Geo& g, const double* img, int img_n, int dn, double* phi, const double* b, int cycles,
                          int pre, int post, int citers, double comega, double somega, int dlo, int dhi,
-                         hipStream_t st) {
+                         hipStream_t st, int zin) {
     const size_t bytes = coarse_vcycle_bytes(g);
     if (bytes != (size_t)img_n * sizeof(double)) return -1;
     if (bytes > 150 * 1024 || g.nxl != g.nx) return -1;
@@ -3649,7 +3900,7 @@ int launch_coarse_vcycle(const Geo& g, const double* img, int img_n, int dn, dou
         attr = true;
     }
     NS_LAUNCH(k_coarse_vcycle, dim3(1), dim3(CV_THREADS), bytes, st, g, img, img_n, dn, phi, b, cycles, pre, post,
-              citers, comega, somega, dlo, dhi);
+              citers, comega, somega, dlo, dhi, zin);
     return 0;
 }
 

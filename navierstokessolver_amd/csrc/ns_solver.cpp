@@ -91,6 +91,11 @@ struct MgLevel {
     // multi-rank: the rhs ghost rows are owed -- they travel with the level's next overlapped
     // FUSE_R exchange instead of in an exchange round of their own (flush_b otherwise)
     bool b_pend = false;
+    // the level's iterate is identically zero but not stored (the restriction from the level
+    // above skipped its phi := 0 writes): its first pass -- the fused restriction pass or the LDS
+    // coarse V-cycle -- takes it as zero without reading it or its ghost rows; any other consumer
+    // materialises the zeros first (zero_phi)
+    bool zero = false;
     nsg::Geo gs{};
     std::vector<int> si0, sn;
 };
@@ -101,7 +106,7 @@ struct ns_solver {
     int device = 0;
     hipStream_t st = nullptr;
     double dt = 0, re = 0, rtol = 1e-8, omega = 0, omega_v = 1.0;
-    int poisson = NS_POISSON_RBSOR, max_iters = 200000, check_every = 0, timing = 0;
+    int poisson = NS_POISSON_MG, max_iters = 200000, check_every = 0, timing = 0;
     double* base = nullptr;      // all fields
     size_t plane = 0;            // doubles per field plane
     double* arr[NS_NUM_ARR] = {};  // pointer to local row 0 of each field
@@ -489,9 +494,9 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
             // rank and slabs agree.  A probing first pass stays a pair (2+3+2)
             int w = std::min(s->tiled ? 1 : 2, n - k);
             if (!s->tiled && !(launch == 0 && part_first)) {
-                // (one rank: a batch may also end on a 3-sweep pass with the residual stage, 7-row
-                // cone: 5 = 3+2, 3 = 3, 6 = 3+3)
-                const bool end3 = s->nranks == 1 && s->sweep3_res;
+                // (a batch may also end on a 3-sweep pass with the residual stage, 7-row cone:
+                // 5 = 3+2, 3 = 3, 6 = 3+3 -- slabs too, with 7 ghost rows)
+                const bool end3 = s->sweep3_res;
                 if (s->sweep3 && s->triple && (n - k >= 5 || (end3 && (n - k == 3 || n - k == 6)))) w = 3;
                 else if (((n - k) & 1) && n - k >= 3) w = 1;
             }
@@ -499,20 +504,20 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
             double* part = last ? part_last : (launch == 0 ? part_first : nullptr);
             // iterate ghost rows each pass reads: its cone (3-sweep 6, 2-sweep 4, + 1 with the
             // residual stage; single sweep 2 -- k_sweep reads one, K1 needs two anyway)
-            const int hw = w == 3 ? 6 : (w == 2 ? (part ? 5 : 4) : 2);
+            const int hw = w == 3 ? (part ? 7 : 6) : (w == 2 ? (part ? 5 : 4) : 2);
             if (which == 3 && w >= 2 && !s->tiled) {
                 // multi-rank pair / triple pass: u and v ghost rows in one exchange, overlapped
-                // (the rhs ghost rows -- 5: the 3-sweep pass's first stage -- ride along on the
-                // solve's first pass)
+                // (the rhs ghost rows -- 6: the residual 3-sweep pass's first stage -- ride along on
+                // the solve's first pass)
                 const HaloReq r[4] = {{&s->g, s->arr[NS_ARR_U], hw}, {&s->g, s->arr[NS_ARR_V], hw},
-                                      {&s->g, s->arr[NS_ARR_RU], 5}, {&s->g, s->arr[NS_ARR_RV], 5}};
+                                      {&s->g, s->arr[NS_ARR_RU], 6}, {&s->g, s->arr[NS_ARR_RV], 6}};
                 const int nr = s->helm_b_pend ? 4 : 2;
                 s->helm_b_pend = 0;
                 nb = overlapped(s, r, nr, [&]() {
                     if (w == 3)
                         return nsg::launch_helm_sweep3(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
                                                        s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
-                                                       s->arr[NS_ARR_RV], s->st, 3);
+                                                       s->arr[NS_ARR_RV], s->st, 3, part);
                     return nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
                                                    s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
                                                    s->arr[NS_ARR_RV], part, s->st, 3);
@@ -523,7 +528,7 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
             } else {
                 if (s->helm_b_pend) {
                     s->helm_b_pend = 0;
-                    CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 5));
+                    CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 6));
                 }
                 if (which == 3) CHK(halo(s, {s->arr[NS_ARR_U], s->arr[NS_ARR_V]}, hw));
                 else if (w <= 2) CHK(halo(s, {s->arr[which == 1 ? NS_ARR_U : NS_ARR_V]}, hw));
@@ -631,10 +636,11 @@ struct KrylovSolve {
 int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res);
 int correct_launch(ns_solver* s, double* part2);
 
-// the wall bands' relaxation before the global Helmholtz passes (k_helm_band: 3 RB-SOR sweeps of
-// u and v on the cells within 32 of a wall, the rest held; the residual of the guess u^n lives
-// there).  Slabs: the iterates' ghost rows (6: the kernel's cone) and the right-hand sides' (5)
-// first; the first global pass exchanges the relaxed iterates' rows again.
+// the wall bands' relaxation before the global Helmholtz passes (k_helm_band: band_sweeps RB-SOR
+// sweeps, 6 by default in launches of 3, of u and v on the cells within band_w = max(32, min(nx,
+// ny) / 32) of a wall, the rest held; the residual of the guess u^n lives there).  Slabs: the
+// iterates' ghost rows (6: the kernel's cone) and the right-hand sides' (5) before each launch;
+// the first global pass exchanges the relaxed iterates' rows again.
 int helm_band(ns_solver* s, double alpha) {
     // launches of 3 sweeps: even ones read the band from the iterates and write it to the
     // scratch planes, odd ones back (no tile writes what another reads); an odd count ends with
@@ -651,7 +657,7 @@ int helm_band(ns_solver* s, double alpha) {
         if (s->nranks > 1) {
             // the exchange overlapped with the tiles that read no neighbour's rows
             const HaloReq r[4] = {{&s->g, odd ? TU : U, 6}, {&s->g, odd ? TV : V, 6},
-                                  {&s->g, s->arr[NS_ARR_RU], 5}, {&s->g, s->arr[NS_ARR_RV], 5}};
+                                  {&s->g, s->arr[NS_ARR_RU], 6}, {&s->g, s->arr[NS_ARR_RV], 6}};
             const int nr = s->helm_b_pend ? 4 : 2;
             s->helm_b_pend = 0;
             const int n = overlapped(s, r, nr, launch);
@@ -871,6 +877,12 @@ bool fused_prolong(const ns_solver* s, int l) {
     return s->fuse_prolong && (pair_level(s, l) || tile_level(s, l)) && s->mg_post >= 2;
 }
 
+bool zero_ok(const ns_solver* s, int l) {
+    if (l <= 0 || l >= (int)s->lv.size()) return false;
+    if (l == (int)s->lv.size() - 1) return s->mg_coarse_lds;
+    return fused_restrict(s, l) && s->mg_pre == 2;
+}
+
 // level l+1 as level l's restriction target / prolongation source: the first replicated
 // level is seen through this rank's slab of it (rows gs.i0 .. of the whole level)
 struct CoarseView {
@@ -894,8 +906,10 @@ CoarseView coarse_view(ns_solver* s, int l) {
 // host transport: an exact sum-allreduce of the level with every foreign row zeroed.
 int gather_level(ns_solver* s, MgLevel& C) {
     const size_t ld = C.g.ld;
-    HIPCHK(hipMemsetAsync(C.phi - (ptrdiff_t)nsg::HALO * ld, 0,
-                          (size_t)(C.g.nx + 2 * nsg::HALO) * ld * sizeof(double), s->st));
+    // (with C.zero the level's first pass takes its iterate as zero: nothing to clear)
+    if (!C.zero)
+        HIPCHK(hipMemsetAsync(C.phi - (ptrdiff_t)nsg::HALO * ld, 0,
+                              (size_t)(C.g.nx + 2 * nsg::HALO) * ld * sizeof(double), s->st));
     if (s->ht.allreduce) {
         const size_t n = (size_t)C.g.nx * ld;
         if (n > (size_t)INT32_MAX) { set_err("agglomerated level too large for the host transport"); return NS_EINVAL; }
@@ -928,9 +942,25 @@ int gather_level(ns_solver* s, MgLevel& C) {
     return 0;
 }
 
+// level l's implicit zero iterate as stored zeros (a consumer that reads phi)
+int zero_phi(ns_solver* s, int l) {
+    MgLevel& L = level(s, l);
+    if (!L.zero) return 0;
+    L.zero = false;
+    const size_t ld = L.g.ld;
+    HIPCHK(hipMemsetAsync(L.phi - (ptrdiff_t)nsg::HALO * ld, 0, (size_t)(L.g.nxl + 2 * nsg::HALO) * ld * sizeof(double),
+                          s->st));
+    return 0;
+}
+
+// the first consumer of level l's phi in a V-cycle takes an implicit zero (MgLevel::zero): the
+// fused restriction pass when it is the level's first pre-smoothing pass, or the LDS coarse solve
+bool zero_ok(const ns_solver* s, int l);
+
 int mg_smooth(ns_solver* s, int l, int n, int* tn, int ev0) {
     MgLevel& L = level(s, l);
     if (n > 0) CHK(flush_b(s, l));
+    if (n > 0) CHK(zero_phi(s, l));
     for (int k = 0; k < n;) {
         const int w = (n - k >= 2 && pair_level(s, l)) ? 2 : 1;   // two sweeps per HBM pass
         CHK(halo_l(s, l, {L.phi}, 2 * w));
@@ -952,14 +982,17 @@ int mg_coarse(ns_solver* s) {
     MgLevel& L = level(s, l);
     CHK(flush_b(s, l));
     if (s->mg_coarse_lds) {
+        const int zin = L.zero ? 1 : 0;
+        L.zero = false;
         if (nsg::launch_coarse_vcycle(L.g, s->cvimg, s->cv_n, s->cv_dn, L.phi, L.b, 1, s->mg_pre, s->mg_post,
                                       s->mg_coarse_iters, s->mg_omega_c, s->mg_omega_s, s->out_side == 0,
-                                      s->out_side == 1, s->st) != 0) {
+                                      s->out_side == 1, s->st, zin) != 0) {
             set_err("coarse LDS V-cycle does not fit");
             return NS_EINVAL;
         }
         return 0;
     }
+    CHK(zero_phi(s, l));
     for (int k = 0; k < s->mg_coarse_iters; k++) {
         CHK(halo_l(s, l, {L.phi}, 2));
         nsg::launch_pois_rbsor(L.g, L.c, s->mg_omega_c, L.phi, L.tmp, L.b, nullptr, nullptr, s->st);
@@ -986,40 +1019,51 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool want_check, bo
         const CoarseView cv = coarse_view(s, l);
         const double* sh = l == 0 ? shift0(s) : nullptr;
         int nb;
+        // the coarse level's first pass takes its iterate as zero: the restriction stores no zeros
+        const bool czero = zero_ok(s, l + 1);
+        double* pcz = czero ? nullptr : cv.phi;
         if (fused_restrict(s, l)) {
             // last two pre-smoothing sweeps + residual + restriction in one HBM pass
             CHK(mg_smooth(s, l, s->mg_pre - 2, tn, ev0));
+            const bool zin = F.zero;   // (then the pass reads neither phi nor its ghost rows)
+            F.zero = false;
             const bool t = s->timing && l == 0 && (!s->pc_active || s->pc_timing);
             if (t) { CHK(t_begin(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); s->evtag[ev0 + *tn] = 1; }
             if (tile_level(s, l)) {
                 CHK(flush_b(s, l));
-                CHK(halo_l(s, l, {F.phi}, 5));
-                nb = nsg::launch_pois_tile2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b, cv.phi,
-                                                     s->part, s->st);
+                if (!zin) CHK(halo_l(s, l, {F.phi}, 5));
+                nb = nsg::launch_pois_tile2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b, pcz,
+                                                     s->part, s->st, zin);
             } else if (F.repl) {
                 nb = nsg::launch_pois_rbsor2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.b,
-                                                      cv.phi, s->part, s->st);
+                                                      pcz, s->part, s->st, zin);
             } else {
-                // (the level's rhs ghost rows ride along when owed)
+                // (the level's rhs ghost rows ride along when owed; a zero iterate has none to send)
                 const HaloReq r[2] = {{&F.g, F.phi, 5}, {&F.g, F.b, 4}};
-                const int nr = F.b_pend ? 2 : 1;
+                const HaloReq* rq = zin ? r + 1 : r;
+                const int nr = zin ? (F.b_pend ? 1 : 0) : (F.b_pend ? 2 : 1);
                 F.b_pend = false;
-                nb = overlapped(s, r, nr, [&]() {
+                auto pass = [&]() {
                     return nsg::launch_pois_rbsor2_restrict(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g,
-                                                            cv.b, cv.phi, s->part, s->st);
-                });
+                                                            cv.b, pcz, s->part, s->st, zin);
+                };
+                nb = nr ? overlapped(s, rq, nr, pass) : pass();
                 if (nb < 0) return nb;
             }
             if (t) { CHK(t_end(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); (*tn)++; }
             std::swap(F.phi, F.tmp);
             if (l == 0) { s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp; }
         } else {
+            CHK(zero_phi(s, l));
             CHK(mg_smooth(s, l, s->mg_pre, tn, ev0));
             CHK(flush_b(s, l));
             CHK(halo_l(s, l, {F.phi}, 1));
             nb = nsg::launch_restrict(F.g, F.c, F.phi, F.b, sh, cv.g, C.c, cv.b, cv.phi, s->part, s->st);
         }
         (void)nb;   // (the restriction's partials: the pre-smoothed residual, unused)
+        // (k_restrict always stores the zeros; the fused passes skip them when the coarse level takes
+        // them implicitly)
+        C.zero = czero && fused_restrict(s, l);
         if (cv.gather) CHK(gather_level(s, C));
         else if (s->nranks > 1 && s->overlap && s->cst && !C.repl && fused_restrict(s, l + 1) && !tile_level(s, l + 1))
             C.b_pend = true;   // sent with level l+1's FUSE_R exchange
@@ -1730,7 +1774,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         return NS_EINVAL;
     }
     if (p->poisson != NS_POISSON_RBSOR && p->poisson != NS_POISSON_JACOBI && p->poisson != NS_POISSON_MG) {
-        set_err("unknown Poisson solver %d", p->poisson);
+        set_err("unknown Poisson solver %d (NS_POISSON_MG 0, NS_POISSON_JACOBI 1, NS_POISSON_RBSOR 3; ABI %d)",
+                p->poisson, NSGPU_ABI_VERSION);
         return NS_EINVAL;
     }
 
@@ -1742,8 +1787,11 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (ns_slab_range(gd->nx, p->nranks, p->rank, &i0, &i1)) return NS_EINVAL;
     g.i0 = i0;
     g.nxl = i1 - i0;
-    if (p->nranks > 1 && g.nxl < 2 * (nsg::HALO - 1)) {
-        set_err("slab of %d rows is thinner than the %d-row halo exchange", g.nxl, 2 * (nsg::HALO - 1));
+    // (the widest exchange outside the 3-sweep passes -- which need slabs of 2*HALO rows, `triple`
+    // -- is 6 rows, fed from one neighbour; the overlapped passes want an interior beyond it)
+    constexpr int min_slab_rows = 10;
+    if (p->nranks > 1 && g.nxl < min_slab_rows) {
+        set_err("slab of %d rows is thinner than the %d-row halo exchange", g.nxl, min_slab_rows);
         return NS_EINVAL;
     }
     // ConstructGhostStencils (FluidSolver.cpp:84-103) of one edge
@@ -2166,7 +2214,7 @@ static int step_body_(ns_solver* s, ns_stats& st) {
     // rhs ghost rows (a checked pair pass and the 3-sweep pass read ib-5): multi-rank passes take them with
     // their first overlapped exchange
     if (s->nranks > 1 && s->overlap && s->cst && !s->g.fc && !s->tiled) s->helm_b_pend = 1;
-    else CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 5));
+    else CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 6));
     s->hn = 0;
     // the Poisson initial guess (phi extrapolation) waits to hide the Helmholtz check's host sync
     s->extrap_pending = s->phim ? 1 : 0;
@@ -2349,7 +2397,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         // single rank with the 3-sweep pass and iters >= 4: one k_sweep3 pass first; then
         // (rest-1)/2 two-sweep passes, then single sweeps; the residual is of the last sweep's input
         int nb = 0;
-        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 5));
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 6));
         const int three = (s->sweep3 && s->nranks == 1 && !s->tiled && iters >= 4) ? 3 : 0;
         if (three) helm_sweep3(s, alpha, 1), helm_sweep3(s, alpha, 2);
         const int pairs = iters - three > 0 ? (iters - three - 1) / 2 : 0;
@@ -2371,7 +2419,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
     }
     case NS_K_HELM_BAND: {
         if (s->g.fc || s->tiled) { set_err("NS_K_HELM_BAND needs a rectangle and the streaming sweeps"); return NS_EINVAL; }
-        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 5));
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 6));
         CHK(helm_band(s, alpha));
         CHK(fetch(s));
         return 0;
@@ -2418,7 +2466,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
         int its = 0;
         double ru = 0, rv = 0;
         CHK(helm_bnorm(s));
-        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 5));
+        CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 6));
         CHK(helm_solve(s, &its, &ru, &rv));
         if (out) { out[0] = its; out[1] = std::max(ru, rv); }
         return 0;

@@ -19,7 +19,7 @@ def test_library_exports_every_header_symbol():
     for n in names:
         assert hasattr(lib, n), f"libnsgpu.so does not export {n}"
     assert set(names) == set(L.SIGNATURES), "ctypes signatures out of sync with include/nsgpu.h"
-    assert lib.ns_abi_version() == 3
+    assert lib.ns_abi_version() == 4
 
 
 def test_lib_is_gfx950_code_object():
@@ -83,8 +83,8 @@ def test_bad_slab_arguments_rejected():
 
 def test_device_bytes():
     # NS_NUM_ARR planes of (rows + 8 ghost rows) x ld doubles
-    assert L.lib().ns_device_bytes(4096, 4096) == 11 * (4096 + 2 * 6) * 4096 * 8
-    assert L.lib().ns_device_bytes(10, 33) == 11 * (10 + 2 * 6) * 128 * 8
+    assert L.lib().ns_device_bytes(4096, 4096) == 11 * (4096 + 2 * 7) * 4096 * 8   # HALO = 7 ghost rows per side
+    assert L.lib().ns_device_bytes(10, 33) == 11 * (10 + 2 * 7) * 128 * 8
 
 
 def test_nccl_unique_id_size():

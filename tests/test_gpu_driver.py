@@ -67,6 +67,19 @@ def test_driver_matches_oracle(tmp_path, exe, oracle_run):
         np.testing.assert_allclose(pc, p - p.mean(), rtol=0, atol=1e-5 * np.abs(p).max())
         top = d[np.isclose(d[:, 1], 1.0)]
         np.testing.assert_allclose(top[:, 3], 1.0, atol=1e-6)   # lid face value u = b (ghost -u + 2b)
+        # every boundary-face row (FluidSolver.cpp:596-603): the face point x + nx h/2, the face
+        # velocities 0.5 (q + ghost) = c/2 (walls: -q + c, :89-96 -- u = 1 on the lid, 0 elsewhere;
+        # v = 0 on every wall) and 0.5 (phi + ghost_phi) - dt/(2 Re) L phi, which for a wall
+        # (ghost_phi = phi) is the cell's own Pr
+        faces, owner, exp = _face_rows(og)
+        fr = d[faces]
+        np.testing.assert_allclose(fr[:, 0], exp[:, 0], atol=1e-6)
+        np.testing.assert_allclose(fr[:, 1], exp[:, 1], atol=1e-6)
+        np.testing.assert_allclose(fr[:, 3], exp[:, 2], atol=1e-12)
+        np.testing.assert_allclose(fr[:, 4], exp[:, 3], atol=1e-12)
+        np.testing.assert_allclose(fr[:, 5], d[owner, 5], rtol=1e-5, atol=1e-12)
+        np.testing.assert_allclose(fr[:, 5] - cells[:, 5].mean(), p[owner_cells(owner)] - p.mean(), rtol=0,
+                                   atol=1e-5 * np.abs(p).max())
     assert (tmp_path / "CellCenters.csv").exists()
 
 
@@ -78,6 +91,33 @@ def _cell_rows():
             rows.append(r)
             r += 1 + (i == 0) + (i == N - 1) + (j == 0) + (j == N - 1)
     return rows
+
+
+def _face_rows(og):
+    """Row indices of the boundary-face rows, the row of the cell each belongs to, and the
+    expected (x, y, u, v) of each: faces follow their cell in Cell::edges order W, E, S, N
+    (Grid.h:33); the cavity's lid (N side) has u = 1, every other wall 0."""
+    h = 1.0 / N
+    faces, owner, exp, r = [], [], [], 0
+    for i in range(N):
+        for j in range(N):
+            cell = r
+            r += 1
+            xc, yc = (i + 0.5) * h, (j + 0.5) * h
+            for on, (nx, ny) in zip((i == 0, i == N - 1, j == 0, j == N - 1), ((-1, 0), (1, 0), (0, -1), (0, 1))):
+                if not on:
+                    continue
+                faces.append(r)
+                owner.append(cell)
+                exp.append((xc + nx * h / 2, yc + ny * h / 2, 1.0 if ny == 1 else 0.0, 0.0))
+                r += 1
+    return np.array(faces), np.array(owner), np.array(exp)
+
+
+def owner_cells(owner_rows):
+    """Cell index (compact id order) of each owner row."""
+    idx = {row: k for k, row in enumerate(_cell_rows())}
+    return np.array([idx[r] for r in owner_rows])
 
 
 # ---- a backward-facing step with an inlet and a NEUMANN outflow (tests/polygons.py STEP):

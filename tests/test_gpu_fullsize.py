@@ -43,7 +43,10 @@ def oracle_threads():
     O.set_threads(1)
 
 
-@pytest.mark.parametrize("n,steps", [(2048, 3), (4096, 1), (8192, 1)])
+# (8192^2 x 4 steps: from step 2 on the wall tangential-correction terms (FluidSolver.cpp:458-510,
+# grad phi^{n-1} != 0), the AB2 history (:335-340), the phi extrapolation (quadratic from step 3),
+# the batch predictors and the speculative K5 all run at configs[3]'s size)
+@pytest.mark.parametrize("n,steps", [(2048, 3), (4096, 1), (8192, 4)])
 def test_cavity_steps_vs_oracle_at_config_size(gpu, oracle_threads, n, steps):
     dt, re, rtol = 1.0 / (8 * n), 1000.0, 1e-12
     gs = gpu.GpuSolver(gpu.cavity(n), dt, re, rtol=rtol)
@@ -60,6 +63,33 @@ def test_cavity_steps_vs_oracle_at_config_size(gpu, oracle_threads, n, steps):
     assert np.max(np.abs(u.ravel() - ref["u"])) <= 1e-9
     assert np.max(np.abs(v.ravel() - ref["v"])) <= 1e-9
     assert abs(np.max(u) - 1.0) <= 1.0     # the lid drives the flow; nothing blew up
+
+
+def test_bench_workload_vs_oracle(gpu, oracle_threads):
+    """The driver's exact timed workload (bench.py defaults as the driver runs them: 4096^2 cavity,
+    Re 1000, dt = 1/32768, both solves to rtol 1e-8, ns_step_async, 5 warm-up + 20 steps, default
+    knobs: wall bands, 3-sweep passes, extrapolated phi, predicted checks, speculative K5) against
+    the oracle running the same algorithm (OSolver.use_gpu_algorithm) at the same rtol 1e-8.
+    Tolerance: SURVEY 8(c)'s 1e-6 on u, v (two rtol-1e-8 solves per step, 25 steps) and on every
+    step's monitor (which ns_step_async returns one call late)."""
+    n, re, rtol, steps = 4096, 1000.0, 1e-8, 25
+    dt = 1.0 / (8 * n)
+    gs = gpu.GpuSolver(gpu.cavity(n), dt, re, rtol=rtol)
+    osv = OSolver(OGrid.rectangle(n, n), dt, re, rtol=rtol)
+    osv.use_gpu_algorithm(gs.omega_v, gs.mg_omega)
+    gmm, omm = [], []
+    for k in range(steps):
+        st = gs.step_async()
+        if k > 0:
+            gmm.append([st["umin"], st["umax"], st["vmin"], st["vmax"]])
+        omm.append(list(osv.step()[0]))
+    gmm.append(list(gs.monitor()))
+    ref = osv.get()
+    u, v, _ = gs.fields()
+    gs.close()
+    assert np.max(np.abs(np.array(gmm) - np.array(omm))) <= 1e-6
+    assert np.max(np.abs(u.ravel() - ref["u"])) <= 1e-6
+    assert np.max(np.abs(v.ravel() - ref["v"])) <= 1e-6
 
 
 @pytest.mark.parametrize("n", [4096, 16384])
