@@ -613,258 +613,6 @@ __global__ __launch_bounds__(256) void k_rhs_bc(Geo g, Coef c, double dt, double
     block_reduce_sum<2>(acc, part + 2 * blockIdx.x);
 }
 
-// ---------------------------------------------------------------- K1 as streaming strips
-// k_rhs_s: ConstructRHS_V on the cells at least two from every wall -- the MUSCL stencil's
-// reach, so every neighbour exists and no ghost is evaluated (TopoInner) -- with every MUSCL
-// slope and every face flux computed ONCE.  (rhs_cell, per cell, evaluates 12 slopes and 8 face
-// fluxes -- each face twice, once from each side: ~500 fp64 wave-instructions per cell, K1's
-// bound.)  The strip walk of the sweeps: a wave owns 128 columns (2 per lane, 124 written) and
-// walks L rows; when row r arrives, row r-1's x-slopes are formed (rows r-2 .. r in the
-// window), then the x-face between rows r-2 and r-1 (its two states from those rows' slopes),
-// and row r-2 is complete: its W face is the previous step's, its E face this one's, its y-faces
-// come from row r-2's y-slopes across the lanes (face (c0-1 | c0) per lane, (c0 | c1) inside the
-// lane, the third from lane + 1 by DPP).  Face states / fluxes / the RHS assembly are rhs_cell's
-// expressions, so every value equals the tile kernel's up to FMA contraction.  The ring of cells
-// within two of a wall (and an odd ny's last column) is k_rhs_ring's: rhs_cell<BC> per cell, the
-// ApplyBoundaryConditions terms included.  u, v rows ib-2 .. ie+1 are read (2 ghost rows), cu0 /
-// cv0 at the output rows (updated in place: each lane reads its cells' old values before it
-// stores them), stores through buffer resources (dropped offsets for unwritten lanes / rows).
-struct RhsStreamArgs {
-    Geo g;
-    Coef c;
-    double dt, re;
-    const double *u, *v;
-    double *cu, *cv, *ru, *rv;
-    double* part;                 // 2 per strip: sum ru^2, sum rv^2 of its written cells
-    int nsj, nsi, L;
-    int slo, shi0, nrun;          // strip-row subset of this launch (phase_range)
-    int ilo, ihi, jhi;            // written cells: local rows [ilo, ihi), columns [2, jhi)
-};
-constexpr int RC_K1 = 3;          // k_rhs_s: row tables from row ib-3
-template <bool NT>
-__global__ __launch_bounds__(256) void k_rhs_s(RhsStreamArgs A) {
-    const Geo& g = A.g;
-    const Coef& c = A.c;
-    __shared__ double rcs[4][64 + 2 * RC_K1 + 2][4];   // per row: hx, 1/hx, 2/(h_{i-1}+h_i), 2/(h_i+h_{i+1})
-    const int lane = threadIdx.x & 63;
-    const int nstr = A.nsj * A.nrun;
-    const int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    double (*rc)[4] = rcs[threadIdx.x >> 6];
-    const int run = w / A.nsj;
-    const int wid = phase_block(run, A.slo, A.shi0) * A.nsj + (w - run * A.nsj);
-    const int si = wid / A.nsj, sj = wid - si * A.nsj;
-    const int ib = si * A.L, ie = min(ib + A.L, g.nxl);
-    if (w < nstr) {
-        for (int t = lane; t < ie - ib + 2 * RC_K1 + 2; t += 64) {
-            const int gi = min(max(g.i0 + ib - RC_K1 + t, 0), g.nx - 1);
-            rc[t][0] = c.hx[gi];
-            rc[t][1] = c.rhx[gi];
-            rc[t][2] = c.rsx[gi];
-            rc[t][3] = c.rsx[gi + 1];
-        }
-    }
-    __syncthreads();
-    double acc0 = 0.0, acc1 = 0.0;
-    if (w < nstr) {
-        const int ny = g.ny, ld = g.ld;
-        const int jb = sj * SW;
-        const int c0 = jb - 2 + 2 * lane;
-        const int lc = min(max(c0, 0), ld - 2);
-        const bool wr = lane >= 1 && lane <= 62 && c0 >= 2 && c0 < A.jhi;
-        // column tables (clamped; a clamped column only feeds unwritten lanes)
-        const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c0 + 1, 0), ny - 1), km = min(max(c0 - 1, 0), ny - 1);
-        const double hy0 = c.hy[k0], hy1 = c.hy[k1], hym = c.hy[km];
-        const double ry0 = c.rhy[k0], ry1 = c.rhy[k1];
-        const double rs0 = c.rsy[k0], rs1 = c.rsy[k1], rs2 = c.rsy[min(k1 + 1, ny)];
-        const double dt = A.dt, hre = 0.5 / A.re;
-        const int rlo = -HALO, rhi = g.nxl + HALO - 1;
-        const __amdgpu_buffer_rsrc_t bcu = __builtin_amdgcn_make_buffer_rsrc(A.cu, (short)0, 0x7FFFFFF0, 0x00020000);
-        const __amdgpu_buffer_rsrc_t bcv = __builtin_amdgcn_make_buffer_rsrc(A.cv, (short)0, 0x7FFFFFF0, 0x00020000);
-        const __amdgpu_buffer_rsrc_t bru = __builtin_amdgcn_make_buffer_rsrc(A.ru, (short)0, 0x7FFFFFF0, 0x00020000);
-        const __amdgpu_buffer_rsrc_t brv = __builtin_amdgcn_make_buffer_rsrc(A.rv, (short)0, 0x7FFFFFF0, 0x00020000);
-        // one row of u, v (row r) and of cu0, cv0 (row r-2, the output row of that step)
-        double2 QU[SD], QV[SD], QC[SD], QD[SD];
-        auto load = [&](int r, double2& qu, double2& qv, double2& qc, double2& qd) {
-            const int lr = min(max(r, rlo), rhi), lo = min(max(r - 2, 0), g.nxl - 1);
-            qu = *reinterpret_cast<const double2*>(A.u + (ptrdiff_t)lr * ld + lc);
-            qv = *reinterpret_cast<const double2*>(A.v + (ptrdiff_t)lr * ld + lc);
-            qc = *reinterpret_cast<const double2*>(A.cu + (ptrdiff_t)lo * ld + lc);
-            qd = *reinterpret_cast<const double2*>(A.cv + (ptrdiff_t)lo * ld + lc);
-        };
-        // window rows r-3 .. r; x-slopes of rows r-2 (SP*) and r-1 (SC*); the x-face (r-3 | r-2)'s fluxes
-        double2 U0 = {0, 0}, U1 = {0, 0}, U2 = {0, 0}, U3 = {0, 0};
-        double2 V0 = {0, 0}, V1 = {0, 0}, V2 = {0, 0}, V3 = {0, 0};
-        double2 SPu = {0, 0}, SPv = {0, 0};
-        double2 FWnn = {0, 0}, FWuv = {0, 0};
-        auto xslope = [&](double qm, double qc, double qp, const double* rw) {
-            return minmode_nd((qp - qc) * rw[3], (qc - qm) * rw[2]);
-        };
-        auto step = [&](const double2 qu, const double2 qv, const double2 cu0, const double2 cv0, int r) {
-            U0 = U1; U1 = U2; U2 = U3; U3 = vcopy(qu);
-            V0 = V1; V1 = V2; V2 = V3; V3 = vcopy(qv);
-            const double* rm = rc[r - 2 - ib + RC_K1];   // output row m = r-2
-            const double* rn = rc[r - 1 - ib + RC_K1];   // row r-1
-            // x-slopes of row r-1
-            const double2 SCu = make_double2(xslope(U1.x, U2.x, U3.x, rn), xslope(U1.y, U2.y, U3.y, rn));
-            const double2 SCv = make_double2(xslope(V1.x, V2.x, V3.x, rn), xslope(V1.y, V2.y, V3.y, rn));
-            // x-face (r-2 | r-1): left states from row r-2, right from row r-1 (rhs_cell's C[2] / C[0])
-            const double hxm = rm[0], hxn = rn[0];
-            double2 FEnn, FEuv;
-            {
-                const double ul0 = U1.x + hxm / 2 * SPu.x, vl0 = V1.x + hxm / 2 * SPv.x;
-                const double ur0 = U2.x - hxn / 2 * SCu.x, vr0 = V2.x - hxn / 2 * SCv.x;
-                const double ul1 = U1.y + hxm / 2 * SPu.y, vl1 = V1.y + hxm / 2 * SPv.y;
-                const double ur1 = U2.y - hxn / 2 * SCu.y, vr1 = V2.y - hxn / 2 * SCv.y;
-                FEnn = make_double2(fnn(ul0, ur0), fnn(ul1, ur1));
-                FEuv = make_double2(fuv(ul0, vl0, ur0, vr0), fuv(ul1, vl1, ur1, vr1));
-            }
-            // row m = r-2: y-slopes across the lanes (columns c0 - 1 .. c1 + 1)
-            const double um = lane_up1(U1.y), up = lane_dn1(U1.x), vm = lane_up1(V1.y), vp = lane_dn1(V1.x);
-            const double su0 = minmode_nd((U1.y - U1.x) * rs1, (U1.x - um) * rs0);
-            const double su1 = minmode_nd((up - U1.y) * rs2, (U1.y - U1.x) * rs1);
-            const double sv0 = minmode_nd((V1.y - V1.x) * rs1, (V1.x - vm) * rs0);
-            const double sv1 = minmode_nd((vp - V1.y) * rs2, (V1.y - V1.x) * rs1);
-            const double sum_ = lane_up1(su1), svm = lane_up1(sv1);   // column c0 - 1's slopes
-            // y-faces (c0-1 | c0) and (c0 | c1): lower / upper states (rhs_cell's C[4..7])
-            double fa_nn, fa_uv, fb_nn, fb_uv;
-            {
-                const double u1 = um + hym / 2 * sum_, v1 = vm + hym / 2 * svm;
-                const double u2 = U1.x - hy0 / 2 * su0, v2 = V1.x - hy0 / 2 * sv0;
-                fa_nn = fnn(v1, v2);
-                fa_uv = fuv(u1, v1, u2, v2);
-            }
-            {
-                const double u1 = U1.x + hy0 / 2 * su0, v1 = V1.x + hy0 / 2 * sv0;
-                const double u2 = U1.y - hy1 / 2 * su1, v2 = V1.y - hy1 / 2 * sv1;
-                fb_nn = fnn(v1, v2);
-                fb_uv = fuv(u1, v1, u2, v2);
-            }
-            const double fc_nn = lane_dn1(fa_nn), fc_uv = lane_dn1(fa_uv);   // (c1 | c1+1)
-            // the cells of row m
-            const double rx = rm[1], sxW = rm[2], sxE = rm[3];
-            double out[4][2];
-#pragma unroll
-            for (int e = 0; e < 2; e++) {
-                const double uc = e ? U1.y : U1.x, vc = e ? V1.y : V1.x;
-                const double uW = e ? U0.y : U0.x, vW = e ? V0.y : V0.x, uE = e ? U2.y : U2.x, vE = e ? V2.y : V2.x;
-                const double uS = e ? U1.x : um, vS = e ? V1.x : vm, uN = e ? up : U1.y, vN = e ? vp : V1.y;
-                const double ry = e ? ry1 : ry0, syS = e ? rs1 : rs0, syN = e ? rs2 : rs1;
-                double ru_ = 0.0 + 1.0 * uc, rv_ = 0.0 + 1.0 * vc;
-                ru_ += 0.5 * dt * (e ? cu0.y : cu0.x);
-                rv_ += 0.5 * dt * (e ? cv0.y : cv0.x);
-                double D0 = hre * (uc - uW) * sxW, D1 = hre * (uE - uc) * sxE;
-                double D2 = hre * (uc - uS) * syS, D3 = hre * (uN - uc) * syN;
-                ru_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
-                D0 = hre * (vc - vW) * sxW; D1 = hre * (vE - vc) * sxE;
-                D2 = hre * (vc - vS) * syS; D3 = hre * (vN - vc) * syN;
-                rv_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
-                // C[0..3] from the x-faces (W: previous step, E: this one), C[4..7] from the y-faces
-                const double C0 = e ? FWnn.y : FWnn.x, C1 = e ? FWuv.y : FWuv.x;
-                const double C2 = e ? FEnn.y : FEnn.x, C3 = e ? FEuv.y : FEuv.x;
-                const double C4 = e ? fb_uv : fa_uv, C5 = e ? fb_nn : fa_nn;
-                const double C6 = e ? fc_uv : fb_uv, C7 = e ? fc_nn : fb_nn;
-                double val = (C2 - C0) * rx + (C6 - C4) * ry;
-                out[0][e] = val;
-                ru_ += val * (-1.5 * dt);
-                val = (C3 - C1) * rx + (C7 - C5) * ry;
-                out[1][e] = val;
-                rv_ += val * (-1.5 * dt);
-                out[2][e] = ru_;
-                out[3][e] = rv_;
-            }
-            const int m = r - 2;
-            const bool live = m >= ib && m < ie && m >= A.ilo && m < A.ihi;
-            if (live && wr) {
-                acc0 += out[2][0] * out[2][0] + out[2][1] * out[2][1];
-                acc1 += out[3][0] * out[3][0] + out[3][1] * out[3][1];
-            }
-            const unsigned off = (live && wr) ? ((unsigned)m * (unsigned)ld + (unsigned)c0) * 8u : OOB;
-            auto st2 = [&](__amdgpu_buffer_rsrc_t rs, int k) {
-                const nsu4 d = {(unsigned)__double2loint(out[k][0]), (unsigned)__double2hiint(out[k][0]),
-                                (unsigned)__double2loint(out[k][1]), (unsigned)__double2hiint(out[k][1])};
-                __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)off, 0, NT ? 2 : 0);
-            };
-            st2(bcu, 0);
-            st2(bcv, 1);
-            st2(bru, 2);
-            st2(brv, 3);
-            FWnn = FEnn; FWuv = FEuv;
-            SPu = SCu; SPv = SCv;
-        };
-        // rows ib-2 .. ie+1 (the first two steps only fill the window; row ib-1's slope needs ib)
-        const int r0 = ib - 2, r1 = ie + 1;
-#pragma unroll
-        for (int q = 0; q < SD; q++) {
-            load(r0 + q, QU[q], QV[q], QC[q], QD[q]);
-            asm volatile("" ::: "memory");
-        }
-        for (int r = r0; r <= r1; r += SD) {
-#pragma unroll
-            for (int q = 0; q < SD; q++) {
-                step(QU[q], QV[q], QC[q], QD[q], r + q);   // (rows past r1: computed, not stored)
-                load(r + q + SD, QU[q], QV[q], QC[q], QD[q]);
-            }
-        }
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        acc0 += __shfl_xor(acc0, off, 64);
-        acc1 += __shfl_xor(acc1, off, 64);
-    }
-    if (lane == 0 && w < nstr) {
-        A.part[2 * wid] = acc0;
-        A.part[2 * wid + 1] = acc1;
-    }
-}
-
-// the ring of k_rhs_s: the slab's cells within two rows of the W / E walls (whole rows), and on
-// the other rows the columns 0, 1 and [jhi, ny) -- rhs_cell<BC> per cell (ghosts, the MUSCL
-// stencil's wall cases and the ApplyBoundaryConditions terms), global loads; partials (ru^2, rv^2)
-// per block.  Thread k: the whole wall rows first (nfull of them, from local row fr[q]), then
-// (ncol columns) x the other rows.
-struct RhsRingArgs {
-    int nfull, fr[4];             // whole rows (local indices)
-    int ncol, jhi;                // ring columns per other row: 0, 1, jhi .. ny-1
-    int rlo, rhi;                 // the other rows: local [rlo, rhi)
-    int n;                        // ring cells
-};
-__global__ __launch_bounds__(256) void k_rhs_ring(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
-                                                  const double* __restrict__ v, const double* __restrict__ phi,
-                                                  double* __restrict__ cu, double* __restrict__ cv,
-                                                  double* __restrict__ ru, double* __restrict__ rv,
-                                                  double* __restrict__ part, RhsRingArgs R) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    double acc[2] = {0.0, 0.0};
-    if (k < R.n) {
-        int li, j;
-        const int nf = R.nfull * g.ny;
-        if (k < nf) {
-            const int q = k / g.ny;
-            li = R.fr[q];
-            j = k - q * g.ny;
-        } else {
-            const int q = (k - nf) / R.ncol, e = (k - nf) - q * R.ncol;
-            li = R.rlo + q;
-            j = e < 2 ? e : R.jhi + (e - 2);
-        }
-        const int ld = g.ld, gi = g.i0 + li;
-        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
-        auto U = [&](int di, int dj) { return ldf(u, ld, li + di, j + dj); };
-        auto V = [&](int di, int dj) { return ldf(v, ld, li + di, j + dj); };
-        auto X = [&](int t, int d) { return (t == 0 ? c.hx : t == 1 ? c.rhx : c.rsx)[gi + d]; };
-        auto Y = [&](int t, int d) { return (t == 0 ? c.hy : t == 1 ? c.rhy : c.rsy)[j + d]; };
-        double cun, cvn, ru_, rv_;
-        rhs_cell<true, TopoRect>(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
-        cu[o] = cun;
-        cv[o] = cvn;
-        ru[o] = ru_;
-        rv[o] = rv_;
-        acc[0] = ru_ * ru_;
-        acc[1] = rv_ * rv_;
-    }
-    block_reduce_sum<2>(acc, part + 2 * blockIdx.x);
-}
-
 // ---------------------------------------------------------------- K3
 // ConstructRHS_phi / Div_V (FluidSolver.cpp:365-418): rhs = div(u*)/dt, plus
 // block partials of (sum rhs, sum rhs^2) for the null-space mean (:550) and ||b||.
@@ -1540,6 +1288,266 @@ __global__ __launch_bounds__(256) void k_to_f32(const double* __restrict__ src, 
 }
 __global__ __launch_bounds__(256) void k_to_f64(const float* __restrict__ src, double* __restrict__ dst, long n) {
     for (long k = (long)blockIdx.x * 256 + threadIdx.x; k < n; k += (long)gridDim.x * 256) dst[k] = (double)src[k];
+}
+
+// ---------------------------------------------------------------- K1 as streaming strips
+// k_rhs_s: ConstructRHS_V on the cells at least two from every wall -- the MUSCL stencil's
+// reach, so every neighbour exists and no ghost is evaluated (TopoInner) -- with every MUSCL
+// slope and every face flux computed ONCE.  (rhs_cell, per cell, evaluates 12 slopes and 8 face
+// fluxes -- each face twice, once from each side: ~500 fp64 wave-instructions per cell, K1's
+// bound.)  The strip walk of the sweeps: a wave owns 128 columns (2 per lane, 124 written) and
+// walks L rows; when row r arrives, row r-1's x-slopes are formed (rows r-2 .. r in the
+// window), then the x-face between rows r-2 and r-1 (its two states from those rows' slopes),
+// and row r-2 is complete: its W face is the previous step's, its E face this one's, its y-faces
+// come from row r-2's y-slopes across the lanes (face (c0-1 | c0) per lane, (c0 | c1) inside the
+// lane, the third from lane + 1 by DPP).  Face states / fluxes / the RHS assembly are rhs_cell's
+// expressions, so every value equals the tile kernel's up to FMA contraction.  The ring of cells
+// within two of a wall (and an odd ny's last column) is k_rhs_ring's: rhs_cell<BC> per cell, the
+// ApplyBoundaryConditions terms included.  u, v rows ib-2 .. ie+1 are read (2 ghost rows), cu0 /
+// cv0 at the output rows (updated in place: each lane reads its cells' old values before it
+// stores them), stores through buffer resources (dropped offsets for unwritten lanes / rows).
+struct RhsStreamArgs {
+    Geo g;
+    Coef c;
+    double dt, re;
+    const double *u, *v;
+    double *cu, *cv, *ru, *rv;
+    double* part;                 // 2 per strip: sum ru^2, sum rv^2 of its written cells
+    int nsj, nsi, L;
+    int slo, shi0, nrun;          // strip-row subset of this launch (phase_range)
+    int ilo, ihi, jhi;            // written cells: local rows [ilo, ihi), columns [2, jhi)
+};
+constexpr int RC_K1 = 4;          // k_rhs_s: row tables from row ib-4 (the window-fill steps read ib-4 .. )
+template <bool NT>
+__device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
+    const Geo& g = A.g;
+    const Coef& c = A.c;
+    __shared__ double rcs[4][64 + 2 * RC_K1 + 2][4];   // per row: hx, 1/hx, 2/(h_{i-1}+h_i), 2/(h_i+h_{i+1})
+    const int lane = threadIdx.x & 63;
+    const int nstr = A.nsj * A.nrun;
+    const int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    double (*rc)[4] = rcs[threadIdx.x >> 6];
+    const int run = w / A.nsj;
+    const int wid = phase_block(run, A.slo, A.shi0) * A.nsj + (w - run * A.nsj);
+    const int si = wid / A.nsj, sj = wid - si * A.nsj;
+    const int ib = si * A.L, ie = min(ib + A.L, g.nxl);
+    if (w < nstr) {
+        for (int t = lane; t < ie - ib + 2 * RC_K1 + 2; t += 64) {
+            const int gi = min(max(g.i0 + ib - RC_K1 + t, 0), g.nx - 1);
+            rc[t][0] = c.hx[gi];
+            rc[t][1] = c.rhx[gi];
+            rc[t][2] = c.rsx[gi];
+            rc[t][3] = c.rsx[gi + 1];
+        }
+    }
+    __syncthreads();
+    double acc0 = 0.0, acc1 = 0.0;
+    if (w < nstr) {
+        const int ny = g.ny, ld = g.ld;
+        const int jb = sj * SW;
+        const int c0 = jb - 2 + 2 * lane;
+        const int lc = min(max(c0, 0), ld - 2);
+        const bool wr = lane >= 1 && lane <= 62 && c0 >= 2 && c0 < A.jhi;
+        // column tables (clamped; a clamped column only feeds unwritten lanes)
+        const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c0 + 1, 0), ny - 1), km = min(max(c0 - 1, 0), ny - 1);
+        const double hy0 = c.hy[k0], hy1 = c.hy[k1], hym = c.hy[km];
+        const double ry0 = c.rhy[k0], ry1 = c.rhy[k1];
+        const double rs0 = c.rsy[k0], rs1 = c.rsy[k1], rs2 = c.rsy[min(k1 + 1, ny)];
+        const double dt = A.dt, hre = 0.5 / A.re;
+        const int rlo = -HALO, rhi = g.nxl + HALO - 1;
+        const __amdgpu_buffer_rsrc_t bcu = __builtin_amdgcn_make_buffer_rsrc(A.cu, (short)0, 0x7FFFFFF0, 0x00020000);
+        const __amdgpu_buffer_rsrc_t bcv = __builtin_amdgcn_make_buffer_rsrc(A.cv, (short)0, 0x7FFFFFF0, 0x00020000);
+        const __amdgpu_buffer_rsrc_t bru = __builtin_amdgcn_make_buffer_rsrc(A.ru, (short)0, 0x7FFFFFF0, 0x00020000);
+        const __amdgpu_buffer_rsrc_t brv = __builtin_amdgcn_make_buffer_rsrc(A.rv, (short)0, 0x7FFFFFF0, 0x00020000);
+        // one row of u, v (row r) and of cu0, cv0 (row r-2, the output row of that step)
+        constexpr int SK = 2;   // rows in flight (4 double2 per row: 3 at 208 VGPRs were 2 waves / SIMD)
+        double2 QU[SK], QV[SK], QC[SK], QD[SK];
+        auto load = [&](int r, double2& qu, double2& qv, double2& qc, double2& qd) {
+            const int lr = min(max(r, rlo), rhi), lo = min(max(r - 2, 0), g.nxl - 1);
+            qu = *reinterpret_cast<const double2*>(A.u + (ptrdiff_t)lr * ld + lc);
+            qv = *reinterpret_cast<const double2*>(A.v + (ptrdiff_t)lr * ld + lc);
+            qc = *reinterpret_cast<const double2*>(A.cu + (ptrdiff_t)lo * ld + lc);
+            qd = *reinterpret_cast<const double2*>(A.cv + (ptrdiff_t)lo * ld + lc);
+        };
+        // window rows r-3 .. r; x-slopes of rows r-2 (SP*) and r-1 (SC*); the x-face (r-3 | r-2)'s fluxes
+        double2 U0 = {0, 0}, U1 = {0, 0}, U2 = {0, 0}, U3 = {0, 0};
+        double2 V0 = {0, 0}, V1 = {0, 0}, V2 = {0, 0}, V3 = {0, 0};
+        double2 SPu = {0, 0}, SPv = {0, 0};
+        double2 FWnn = {0, 0}, FWuv = {0, 0};
+        auto xslope = [&](double qm, double qc, double qp, const double* rw) {
+            return minmode_nd((qp - qc) * rw[3], (qc - qm) * rw[2]);
+        };
+        auto step = [&](const double2 qu, const double2 qv, const double2 cu0, const double2 cv0, int r) {
+            U0 = U1; U1 = U2; U2 = U3; U3 = vcopy(qu);
+            V0 = V1; V1 = V2; V2 = V3; V3 = vcopy(qv);
+            const double* rm = rc[r - 2 - ib + RC_K1];   // output row m = r-2
+            const double* rn = rc[r - 1 - ib + RC_K1];   // row r-1
+            // x-slopes of row r-1
+            const double2 SCu = make_double2(xslope(U1.x, U2.x, U3.x, rn), xslope(U1.y, U2.y, U3.y, rn));
+            const double2 SCv = make_double2(xslope(V1.x, V2.x, V3.x, rn), xslope(V1.y, V2.y, V3.y, rn));
+            // x-face (r-2 | r-1): left states from row r-2, right from row r-1 (rhs_cell's C[2] / C[0])
+            const double hxm = rm[0], hxn = rn[0];
+            double2 FEnn, FEuv;
+            {
+                const double ul0 = U1.x + hxm / 2 * SPu.x, vl0 = V1.x + hxm / 2 * SPv.x;
+                const double ur0 = U2.x - hxn / 2 * SCu.x, vr0 = V2.x - hxn / 2 * SCv.x;
+                const double ul1 = U1.y + hxm / 2 * SPu.y, vl1 = V1.y + hxm / 2 * SPv.y;
+                const double ur1 = U2.y - hxn / 2 * SCu.y, vr1 = V2.y - hxn / 2 * SCv.y;
+                FEnn = make_double2(fnn(ul0, ur0), fnn(ul1, ur1));
+                FEuv = make_double2(fuv(ul0, vl0, ur0, vr0), fuv(ul1, vl1, ur1, vr1));
+            }
+            // row m = r-2: y-slopes across the lanes (columns c0 - 1 .. c1 + 1)
+            const double um = lane_up1(U1.y), up = lane_dn1(U1.x), vm = lane_up1(V1.y), vp = lane_dn1(V1.x);
+            const double su0 = minmode_nd((U1.y - U1.x) * rs1, (U1.x - um) * rs0);
+            const double su1 = minmode_nd((up - U1.y) * rs2, (U1.y - U1.x) * rs1);
+            const double sv0 = minmode_nd((V1.y - V1.x) * rs1, (V1.x - vm) * rs0);
+            const double sv1 = minmode_nd((vp - V1.y) * rs2, (V1.y - V1.x) * rs1);
+            const double sum_ = lane_up1(su1), svm = lane_up1(sv1);   // column c0 - 1's slopes
+            // y-faces (c0-1 | c0) and (c0 | c1): lower / upper states (rhs_cell's C[4..7])
+            double fa_nn, fa_uv, fb_nn, fb_uv;
+            {
+                const double u1 = um + hym / 2 * sum_, v1 = vm + hym / 2 * svm;
+                const double u2 = U1.x - hy0 / 2 * su0, v2 = V1.x - hy0 / 2 * sv0;
+                fa_nn = fnn(v1, v2);
+                fa_uv = fuv(u1, v1, u2, v2);
+            }
+            {
+                const double u1 = U1.x + hy0 / 2 * su0, v1 = V1.x + hy0 / 2 * sv0;
+                const double u2 = U1.y - hy1 / 2 * su1, v2 = V1.y - hy1 / 2 * sv1;
+                fb_nn = fnn(v1, v2);
+                fb_uv = fuv(u1, v1, u2, v2);
+            }
+            const double fc_nn = lane_dn1(fa_nn), fc_uv = lane_dn1(fa_uv);   // (c1 | c1+1)
+            // the cells of row m
+            const double rx = rm[1], sxW = rm[2], sxE = rm[3];
+            double out[4][2];
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const double uc = e ? U1.y : U1.x, vc = e ? V1.y : V1.x;
+                const double uW = e ? U0.y : U0.x, vW = e ? V0.y : V0.x, uE = e ? U2.y : U2.x, vE = e ? V2.y : V2.x;
+                const double uS = e ? U1.x : um, vS = e ? V1.x : vm, uN = e ? up : U1.y, vN = e ? vp : V1.y;
+                const double ry = e ? ry1 : ry0, syS = e ? rs1 : rs0, syN = e ? rs2 : rs1;
+                double ru_ = 0.0 + 1.0 * uc, rv_ = 0.0 + 1.0 * vc;
+                ru_ += 0.5 * dt * (e ? cu0.y : cu0.x);
+                rv_ += 0.5 * dt * (e ? cv0.y : cv0.x);
+                double D0 = hre * (uc - uW) * sxW, D1 = hre * (uE - uc) * sxE;
+                double D2 = hre * (uc - uS) * syS, D3 = hre * (uN - uc) * syN;
+                ru_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
+                D0 = hre * (vc - vW) * sxW; D1 = hre * (vE - vc) * sxE;
+                D2 = hre * (vc - vS) * syS; D3 = hre * (vN - vc) * syN;
+                rv_ += dt * ((D1 - D0) * rx + (D3 - D2) * ry);
+                // C[0..3] from the x-faces (W: previous step, E: this one), C[4..7] from the y-faces
+                const double C0 = e ? FWnn.y : FWnn.x, C1 = e ? FWuv.y : FWuv.x;
+                const double C2 = e ? FEnn.y : FEnn.x, C3 = e ? FEuv.y : FEuv.x;
+                const double C4 = e ? fb_uv : fa_uv, C5 = e ? fb_nn : fa_nn;
+                const double C6 = e ? fc_uv : fb_uv, C7 = e ? fc_nn : fb_nn;
+                double val = (C2 - C0) * rx + (C6 - C4) * ry;
+                out[0][e] = val;
+                ru_ += val * (-1.5 * dt);
+                val = (C3 - C1) * rx + (C7 - C5) * ry;
+                out[1][e] = val;
+                rv_ += val * (-1.5 * dt);
+                out[2][e] = ru_;
+                out[3][e] = rv_;
+            }
+            const int m = r - 2;
+            const bool live = m >= ib && m < ie && m >= A.ilo && m < A.ihi;
+            if (live && wr) {
+                acc0 += out[2][0] * out[2][0] + out[2][1] * out[2][1];
+                acc1 += out[3][0] * out[3][0] + out[3][1] * out[3][1];
+            }
+            const unsigned off = (live && wr) ? ((unsigned)m * (unsigned)ld + (unsigned)c0) * 8u : OOB;
+            auto st2 = [&](__amdgpu_buffer_rsrc_t rs, int k) {
+                const nsu4 d = {(unsigned)__double2loint(out[k][0]), (unsigned)__double2hiint(out[k][0]),
+                                (unsigned)__double2loint(out[k][1]), (unsigned)__double2hiint(out[k][1])};
+                __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)off, 0, NT ? 2 : 0);
+            };
+            st2(bcu, 0);
+            st2(bcv, 1);
+            st2(bru, 2);
+            st2(brv, 3);
+            FWnn = FEnn; FWuv = FEuv;
+            SPu = SCu; SPv = SCv;
+        };
+        // rows ib-2 .. ie+1 (the first two steps only fill the window; row ib-1's slope needs ib)
+        const int r0 = ib - 2, r1 = ie + 1;
+#pragma unroll
+        for (int q = 0; q < SK; q++) {
+            load(r0 + q, QU[q], QV[q], QC[q], QD[q]);
+            asm volatile("" ::: "memory");
+        }
+        for (int r = r0; r <= r1; r += SK) {
+#pragma unroll
+            for (int q = 0; q < SK; q++) {
+                step(QU[q], QV[q], QC[q], QD[q], r + q);   // (rows past r1: computed, not stored)
+                load(r + q + SK, QU[q], QV[q], QC[q], QD[q]);
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        acc0 += __shfl_xor(acc0, off, 64);
+        acc1 += __shfl_xor(acc1, off, 64);
+    }
+    if (lane == 0 && w < nstr) {
+        A.part[2 * wid] = acc0;
+        A.part[2 * wid + 1] = acc1;
+    }
+}
+// 176 VGPRs: 2 waves / SIMD; held to 168 (3 waves) it spills 36 B per lane (NSGPU_K1S=3 picks it: A/B)
+template <bool NT>
+__global__ __launch_bounds__(256) void k_rhs_s(RhsStreamArgs A) { rhs_s_body<NT>(A); }
+template <bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_rhs_s3(RhsStreamArgs A) {
+    rhs_s_body<NT>(A);
+}
+
+// the ring of k_rhs_s: the slab's cells within two rows of the W / E walls (whole rows), and on
+// the other rows the columns 0, 1 and [jhi, ny) -- rhs_cell<BC> per cell (ghosts, the MUSCL
+// stencil's wall cases and the ApplyBoundaryConditions terms), global loads; partials (ru^2, rv^2)
+// per block.  Thread k: the whole wall rows first (nfull of them, from local row fr[q]), then
+// (ncol columns) x the other rows.
+struct RhsRingArgs {
+    int nfull, fr[4];             // whole rows (local indices)
+    int ncol, jhi;                // ring columns per other row: 0, 1, jhi .. ny-1
+    int rlo, rhi;                 // the other rows: local [rlo, rhi)
+    int n;                        // ring cells
+};
+__global__ __launch_bounds__(256) void k_rhs_ring(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
+                                                  const double* __restrict__ v, const double* __restrict__ phi,
+                                                  double* __restrict__ cu, double* __restrict__ cv,
+                                                  double* __restrict__ ru, double* __restrict__ rv,
+                                                  double* __restrict__ part, RhsRingArgs R) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    double acc[2] = {0.0, 0.0};
+    if (k < R.n) {
+        int li, j;
+        const int nf = R.nfull * g.ny;
+        if (k < nf) {
+            const int q = k / g.ny;
+            li = R.fr[q];
+            j = k - q * g.ny;
+        } else {
+            const int q = (k - nf) / R.ncol, e = (k - nf) - q * R.ncol;
+            li = R.rlo + q;
+            j = e < 2 ? e : R.jhi + (e - 2);
+        }
+        const int ld = g.ld, gi = g.i0 + li;
+        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+        auto U = [&](int di, int dj) { return ldf(u, ld, li + di, j + dj); };
+        auto V = [&](int di, int dj) { return ldf(v, ld, li + di, j + dj); };
+        auto X = [&](int t, int d) { return (t == 0 ? c.hx : t == 1 ? c.rhx : c.rsx)[gi + d]; };
+        auto Y = [&](int t, int d) { return (t == 0 ? c.hy : t == 1 ? c.rhy : c.rsy)[j + d]; };
+        double cun, cvn, ru_, rv_;
+        rhs_cell<true, TopoRect>(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
+        cu[o] = cun;
+        cv[o] = cvn;
+        ru[o] = ru_;
+        rv[o] = rv_;
+        acc[0] = ru_ * ru_;
+        acc[1] = rv_ * rv_;
+    }
+    block_reduce_sum<2>(acc, part + 2 * blockIdx.x);
 }
 
 // ------------------------------------------------ K3 / K5 as streaming strips
@@ -3208,6 +3216,9 @@ static hipError_t launch_raw(const void* k, dim3 grid, dim3 block, void** args, 
     return hipLaunchKernel(k, grid, block, args, shmem, st);
 }
 
+static long resident_waves(const void* k);
+static int strip_rows(int nxl, long nsj, long cap, int lmin);
+
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
                const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st) {
     const char* e = getenv("NSGPU_RHS");   // NSGPU_RHS=global: the global-load K1 (A/B)
@@ -3229,13 +3240,17 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         A.ilo = std::max(0, std::min(2 - g.i0, g.nxl));
         A.ihi = std::max(A.ilo, std::min(g.nx - 2 - g.i0, g.nxl));
         A.nsj = (g.ny + SW - 1) / SW;
-        const void* kk = (const void*)k_rhs_s<true>;
+        const char* w3 = getenv("NSGPU_K1S");
+        const bool three = w3 && std::atoi(w3) == 3;
+        const void* kk = three ? (const void*)k_rhs_s3<true> : (const void*)k_rhs_s<true>;
         A.L = strip_rows(g.nxl, A.nsj, resident_waves(kk), 8);
         A.nsi = (g.nxl + A.L - 1) / A.L;
         const int nstr = A.nsj * A.nsi;
         A.nrun = phase_range(g.nxl, A.L, A.nsi, 2, &A.slo, &A.shi0);   // u, v rows ib-2 .. ie+1
-        if (A.nrun > 0 && A.jhi > 2 && A.ihi > A.ilo)
-            NS_LAUNCH(k_rhs_s<true>, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), 0, st, A);
+        if (A.nrun > 0 && A.jhi > 2 && A.ihi > A.ilo) {
+            if (three) NS_LAUNCH(k_rhs_s3<true>, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), 0, st, A);
+            else NS_LAUNCH(k_rhs_s<true>, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), 0, st, A);
+        }
         else if (g_phase != 1)
             (void)hipMemsetAsync(part, 0, 2 * sizeof(double) * nstr, st);   // (no inner cells: zero partials)
         RhsRingArgs R{};
@@ -3275,9 +3290,6 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         NS_LAUNCH(k_rhs<TopoRect>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
     return (int)(cg.x * cg.y);
 }
-
-static long resident_waves(const void* k);
-static int strip_rows(int nxl, long nsj, long cap, int lmin);
 
 template <int K>
 static int launch_cell_s(CellStreamArgs A, hipStream_t st) {

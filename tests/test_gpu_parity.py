@@ -533,19 +533,28 @@ def test_tiled_small_level_passes_match_streaming(gpu, monkeypatch, nx, ny):
     assert rel(g - g.mean(), xp - xp.mean()) <= 1e-8
 
 
-@pytest.mark.parametrize("nx,ny,xr,yr,bc", [(300, 200, 1.002, 0.998, BC_FLOW), (37, 70, -1, -1, BC_CAVITY)])
-def test_k1_lds_equals_global_kernel(gpu, monkeypatch, nx, ny, xr, yr, bc):
-    """K1 staged in LDS (k_rhs_lds + the wall-cell kernel k_rhs_bc) = the global-load K1
-    (NSGPU_RHS=global): same per-cell source (rhs_cell / rhs_bc); the compiler's FMA
-    contraction differs between the two kernels, so equal to 1e-14 relative, not bit for bit."""
+@pytest.mark.parametrize("nx,ny,xr,yr,bc", [(300, 200, 1.002, 0.998, BC_FLOW), (37, 70, -1, -1, BC_CAVITY),
+                                            (261, 131, 1.003, -1, BC_CAVITY), (5, 5, -1, -1, BC_CAVITY)])
+@pytest.mark.parametrize("mode", ["stream", "stream3", "lds"])
+def test_k1_equals_global_kernel(gpu, monkeypatch, mode, nx, ny, xr, yr, bc):
+    """K1 as streaming strips (k_rhs_s: each MUSCL slope and face flux once, + the wall ring
+    k_rhs_ring; NSGPU_K1S=3 its 3-waves build), or staged in LDS (NSGPU_RHS=lds: k_rhs_lds + the
+    wall-cell kernel k_rhs_bc) = the global-load K1 (NSGPU_RHS=global, rhs_cell per cell): the same
+    face states and fluxes; the compiler's FMA contraction differs between the kernels, so equal
+    to 1e-14 relative (of the field's max), not bit for bit.  Odd ny (the ring's third column),
+    a stretched grid, and a grid with no inner cell (5 x 5: all ring) included."""
     rng = np.random.default_rng(31)
     dt, re = 1e-3, 250.0
     N = nx * ny
     ins = [rand(rng, N) for _ in range(5)]
     outs = []
-    for mode in ("lds", "global"):
-        if mode == "global":
-            monkeypatch.setenv("NSGPU_RHS", "global")
+    for mode in (mode, "global"):
+        monkeypatch.delenv("NSGPU_RHS", raising=False)
+        monkeypatch.delenv("NSGPU_K1S", raising=False)
+        if mode == "stream3":
+            monkeypatch.setenv("NSGPU_K1S", "3")
+        if mode in ("lds", "global"):
+            monkeypatch.setenv("NSGPU_RHS", mode)
         _, gs = pair(gpu, nx, ny, dt, re, bc, xr, yr)
         for a, x in zip((gpu.NS_ARR_U, gpu.NS_ARR_V, gpu.NS_ARR_PHI, gpu.NS_ARR_CU, gpu.NS_ARR_CV), ins):
             gs.set(a, x)
