@@ -1318,7 +1318,7 @@ struct RhsStreamArgs {
     int ilo, ihi, jhi;            // written cells: local rows [ilo, ihi), columns [2, jhi)
 };
 constexpr int RC_K1 = 4;          // k_rhs_s: row tables from row ib-4 (the window-fill steps read ib-4 .. )
-template <bool NT>
+template <bool NT, int SK>
 __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
     const Geo& g = A.g;
     const Coef& c = A.c;
@@ -1360,7 +1360,7 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
         const __amdgpu_buffer_rsrc_t bru = __builtin_amdgcn_make_buffer_rsrc(A.ru, (short)0, 0x7FFFFFF0, 0x00020000);
         const __amdgpu_buffer_rsrc_t brv = __builtin_amdgcn_make_buffer_rsrc(A.rv, (short)0, 0x7FFFFFF0, 0x00020000);
         // one row of u, v (row r) and of cu0, cv0 (row r-2, the output row of that step)
-        constexpr int SK = 2;   // rows in flight (4 double2 per row: 3 at 208 VGPRs were 2 waves / SIMD)
+        // SK rows in flight, 4 double2 each (u, v, cu0, cv0)
         double2 QU[SK], QV[SK], QC[SK], QD[SK];
         auto load = [&](int r, double2& qu, double2& qv, double2& qc, double2& qd) {
             const int lr = min(max(r, rlo), rhi), lo = min(max(r - 2, 0), g.nxl - 1);
@@ -1494,12 +1494,13 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
         A.part[2 * wid + 1] = acc1;
     }
 }
-// 176 VGPRs: 2 waves / SIMD; held to 168 (3 waves) it spills 36 B per lane (NSGPU_K1S=3 picks it: A/B)
-template <bool NT>
-__global__ __launch_bounds__(256) void k_rhs_s(RhsStreamArgs A) { rhs_s_body<NT>(A); }
+// SK = 2 rows in flight: 176 VGPRs, 2 waves / SIMD; held to 168 (3 waves: k_rhs_s3) it spills 36 B per
+// lane.  NSGPU_K1S picks the variant (A/B): 3 = k_rhs_s3, 23 / 24 = 2 waves with 3 / 4 rows in flight
+template <bool NT, int SK>
+__global__ __launch_bounds__(256) void k_rhs_s(RhsStreamArgs A) { rhs_s_body<NT, SK>(A); }
 template <bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_rhs_s3(RhsStreamArgs A) {
-    rhs_s_body<NT>(A);
+    rhs_s_body<NT, 2>(A);
 }
 
 // the ring of k_rhs_s: the slab's cells within two rows of the W / E walls (whole rows), and on
@@ -1560,7 +1561,7 @@ __global__ __launch_bounds__(256) void k_rhs_ring(Geo g, Coef c, double dt, doub
 struct CellStreamArgs {
     Geo g;
     Coef c;
-    double dt;
+    double dt, rdt;               // dt and 1/dt
     const double *a0, *a1, *a2;   // K3: u, v, -;  K5: phi, u*, v*
     double *o0, *o1;              // K3: rhs_phi, -;  K5: u, v
     double* part;
@@ -1594,7 +1595,6 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
         const bool wr = lane >= 1 && lane <= 62 && c0 < ny;
         const bool o0 = wr && v0, o1 = wr && v1;
         const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
-        const double hy0 = c.hy[k0], hy1 = c.hy[k1];
         const double fs0 = c.fsy[k0], fn0 = c.fny[k0], fs1 = c.fsy[k1], fn1 = c.fny[k1];
         const bool s0 = c0 > 0, n0 = c0 < ny - 1, s1 = c1 > 0, n1 = c1 < ny - 1;
         const int rlo = -HALO, rhi = g.nxl + HALO - 1;
@@ -1613,13 +1613,27 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                 y = *reinterpret_cast<const double2*>(A.a2 + (ptrdiff_t)lr * ld + lc);
             }
         };
+        // outputs through buffer resources: a lane / row that must not write gets a dropped
+        // offset (no store inside a branch; k_jacobi_s), an odd ny's padding column included
+        const __amdgpu_buffer_rsrc_t bo0 = __builtin_amdgcn_make_buffer_rsrc(A.o0, (short)0, 0x7FFFFFF0, 0x00020000);
+        const __amdgpu_buffer_rsrc_t bo1 =
+            __builtin_amdgcn_make_buffer_rsrc(K == 5 ? A.o1 : A.o0, (short)0, 0x7FFFFFF0, 0x00020000);
+        const double ry0 = c.rhy[k0], ry1 = c.rhy[k1], rdt = A.rdt;
         auto step = [&](const double2 q, const double2 x, const double2 y, int r) {
-            W0 = W1; W1 = W2; W2 = q;
+            W0 = W1; W1 = W2; W2 = vcopy(q);
             const int m = r - 1;
-            if (m < ib || m >= ie) return;
-            const int gi = g.i0 + m;
+            const bool live = m >= ib && m < ie;
+            const int gi = min(max(g.i0 + m, 0), g.nx - 1);
             const bool hW = gi > 0, hE = gi < g.nx - 1;
-            const double hx = c.hx[gi], fw = c.fwx[gi], fe = c.fex[gi];
+            const double fw = c.fwx[gi], fe = c.fex[gi], rx = c.rhx[gi];
+            const unsigned base = ((unsigned)max(m, 0) * (unsigned)ld + (unsigned)c0) * 8u;
+            const unsigned off0 = (live && o0) ? base : OOB, off1 = (live && o1) ? base + 8u : OOB;
+            auto st2 = [&](__amdgpu_buffer_rsrc_t rs, double a0, double a1) {
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    (nsu2){(unsigned)__double2loint(a0), (unsigned)__double2hiint(a0)}, rs, (int)off0, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    (nsu2){(unsigned)__double2loint(a1), (unsigned)__double2hiint(a1)}, rs, (int)off1, 0, 0);
+            };
             if (K == 3) {
                 // Div_V: u faces along x from the window, v faces along y from the lanes
                 const double2 vv = x;
@@ -1633,14 +1647,12 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                     const double V1 = face_val(uc, ue, hE, fe, ghost_v(g, uc, 1, 0));
                     const double V2 = face_val(vc, vs, e ? s1 : s0, e ? fs1 : fs0, ghost_v(g, vc, 2, 1));
                     const double V3 = face_val(vc, vn, e ? n1 : n0, e ? fn1 : fn0, ghost_v(g, vc, 3, 1));
-                    val[e] = ((V1 - V0) / hx + (V3 - V2) / (e ? hy1 : hy0)) / A.dt;
+                    // (reciprocals: 1/h from the tables, 1/dt -- within an ulp of Div_V's divisions)
+                    val[e] = ((V1 - V0) * rx + (V3 - V2) * (e ? ry1 : ry0)) * rdt;
                 }
-                if (wr) {   // (an odd ny's last pair: column ny is row padding, left untouched)
-                    if (v1) st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(val[0], val[1]), false);
-                    else A.o0[(ptrdiff_t)m * ld + c0] = val[0];
-                }
-                if (o0) { acc[0] += val[0]; acc[1] += val[0] * val[0]; }
-                if (o1) { acc[0] += val[1]; acc[1] += val[1] * val[1]; }
+                st2(bo0, val[0], val[1]);   // (an odd ny's padding column: dropped, left untouched)
+                if (live && o0) { acc[0] += val[0]; acc[1] += val[0] * val[0]; }
+                if (live && o1) { acc[0] += val[1]; acc[1] += val[1] * val[1]; }
             } else {
                 // GradP (phi ghost = phi at wall / inlet faces: 0.5 (p + p); a NEUMANN side's
                 // extrapolated ghost goes through k_correct) and the correction
@@ -1654,20 +1666,15 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                     const double V1 = face_val(pc, pe, hE, fe, pc);
                     const double V2 = face_val(pc, ps, e ? s1 : s0, e ? fs1 : fs0, pc);
                     const double V3 = face_val(pc, pn, e ? n1 : n0, e ? fn1 : fn0, pc);
-                    const double gx = (V1 - V0) / hx, gy = (V3 - V2) / (e ? hy1 : hy0);
+                    const double gx = (V1 - V0) * rx, gy = (V3 - V2) * (e ? ry1 : ry0);
                     un[e] = (e ? x.y : x.x) - A.dt * gx;
                     vn[e] = (e ? y.y : y.x) - A.dt * gy;
                 }
-                if (wr && v1) {
-                    st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(un[0], un[1]), false);
-                    st_stream(A.o1 + (ptrdiff_t)m * ld + c0, make_double2(vn[0], vn[1]), false);
-                } else if (wr) {
-                    A.o0[(ptrdiff_t)m * ld + c0] = un[0];
-                    A.o1[(ptrdiff_t)m * ld + c0] = vn[0];
-                }
+                st2(bo0, un[0], un[1]);
+                st2(bo1, vn[0], vn[1]);
 #pragma unroll
                 for (int e = 0; e < 2; e++) {
-                    if (!(e ? o1 : o0)) continue;
+                    if (!live || !(e ? o1 : o0)) continue;
                     // NaN-propagating min so a blown-up step is visible in the stats
                     acc[0] = fmin(acc[0], un[e] != un[e] ? -INFINITY : un[e]);
                     acc[1] = fmin(acc[1], un[e] != un[e] ? -INFINITY : -un[e]);
@@ -1678,11 +1685,14 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
         };
         const int r0 = ib - 1, r1 = ie;
 #pragma unroll
-        for (int q = 0; q < SD; q++) load(r0 + q, Q[q], X[q], Y[q]);
+        for (int q = 0; q < SD; q++) {
+            load(r0 + q, Q[q], X[q], Y[q]);
+            asm volatile("" ::: "memory");   // (keep the slots' issue order: the loop's vmcnt bookkeeping)
+        }
         for (int r = r0; r <= r1; r += SD) {
 #pragma unroll
             for (int q = 0; q < SD; q++) {
-                if (r + q <= r1) step(Q[q], X[q], Y[q], r + q);
+                step(Q[q], X[q], Y[q], r + q);   // (rows past r1: computed, not stored)
                 load(r + q + SD, Q[q], X[q], Y[q]);
             }
         }
@@ -2015,10 +2025,11 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
 // rows ib-7 .. ie+6, 112 written columns (SW3R), 7 ghost rows (HALO = 7: slabs too; FUSE_UV + RES is
 // the multi-rank batch end, u and v in one launch, v's partials at part2)
 constexpr int SW3R = SW2X - 4;
-template <int DIR, bool RES>
+template <int DIR, bool RES, int SD3>
 __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
                                                int lane) {
-    constexpr int SD3 = 2;   // rows in flight: 3 would need 174 VGPRs (2 waves/SIMD), or spill at 168 (measured equal)
+    // SD3: rows in flight (round 2: 3 needed 174 VGPRs then; with the wave-uniform strip index the
+    // pass takes 140-152 at 2, so 3 fits 3 waves / SIMD too: NSGPU_SD3=3, A/B)
     constexpr int EXT = RES ? 1 : 0;
     const int jb = sj * (RES ? SW3R : SW2X);
     const int ny = a.ny, ld = a.ld;
@@ -2135,8 +2146,8 @@ __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double
     return res;
 }
 
-template <int FUSE, bool RES = false>
-__global__ __launch_bounds__(256) void k_sweep3(StreamArgs a) {
+template <int FUSE, bool RES = false, int SD3 = 2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SD3 == 3 ? 3 : 1))) void k_sweep3(StreamArgs a) {
     __shared__ double rcs[4][RC_MAX3][4];
     const int nstr = a.nsj * a.nrun;
     int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2155,8 +2166,8 @@ __global__ __launch_bounds__(256) void k_sweep3(StreamArgs a) {
     __syncthreads();
     double res = 0.0;
     if (w < nstr) {
-        if (si & 1) res = sweep3_strip<-1, RES>(af, rc, ib, ie, sj, lane);
-        else res = sweep3_strip<1, RES>(af, rc, ib, ie, sj, lane);
+        if (si & 1) res = sweep3_strip<-1, RES, SD3>(af, rc, ib, ie, sj, lane);
+        else res = sweep3_strip<1, RES, SD3>(af, rc, ib, ie, sj, lane);
     }
     if (RES) {
 #pragma unroll
@@ -3241,15 +3252,17 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         A.ihi = std::max(A.ilo, std::min(g.nx - 2 - g.i0, g.nxl));
         A.nsj = (g.ny + SW - 1) / SW;
         const char* w3 = getenv("NSGPU_K1S");
-        const bool three = w3 && std::atoi(w3) == 3;
-        const void* kk = three ? (const void*)k_rhs_s3<true> : (const void*)k_rhs_s<true>;
+        const int kv = w3 ? std::atoi(w3) : 0;
+        const void* kk = kv == 3 ? (const void*)k_rhs_s3<true>
+                       : kv == 23 ? (const void*)k_rhs_s<true, 3>
+                       : kv == 24 ? (const void*)k_rhs_s<true, 4> : (const void*)k_rhs_s<true, 2>;
         A.L = strip_rows(g.nxl, A.nsj, resident_waves(kk), 8);
         A.nsi = (g.nxl + A.L - 1) / A.L;
         const int nstr = A.nsj * A.nsi;
         A.nrun = phase_range(g.nxl, A.L, A.nsi, 2, &A.slo, &A.shi0);   // u, v rows ib-2 .. ie+1
         if (A.nrun > 0 && A.jhi > 2 && A.ihi > A.ilo) {
-            if (three) NS_LAUNCH(k_rhs_s3<true>, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), 0, st, A);
-            else NS_LAUNCH(k_rhs_s<true>, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), 0, st, A);
+            void* args[] = {&A};
+            if (launch_raw(kk, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), args, 0, st) != hipSuccess) return -1;
         }
         else if (g_phase != 1)
             (void)hipMemsetAsync(part, 0, 2 * sizeof(double) * nstr, st);   // (no inner cells: zero partials)
@@ -3311,7 +3324,7 @@ int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const do
                hipStream_t st) {
     if (cell_streaming() && !g.fc) {
         CellStreamArgs A{};
-        A.g = g; A.c = c; A.dt = dt; A.a0 = u; A.a1 = v; A.o0 = rp; A.part = part;
+        A.g = g; A.c = c; A.dt = dt; A.rdt = 1.0 / dt; A.a0 = u; A.a1 = v; A.o0 = rp; A.part = part;
         return launch_cell_s<3>(A, st);
     }
     const int rows = cell_rows(g);
@@ -3363,7 +3376,8 @@ int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, con
     // (a NEUMANN side's phi ghost reaches two cells inward: the grid kernel's grad_phi)
     if (cell_streaming() && !g.fc && !(g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3])) {
         CellStreamArgs A{};
-        A.g = g; A.c = c; A.dt = dt; A.a0 = phi; A.a1 = us; A.a2 = vs; A.o0 = u; A.o1 = v; A.part = part;
+        A.g = g; A.c = c; A.dt = dt; A.rdt = 1.0 / dt; A.a0 = phi; A.a1 = us; A.a2 = vs; A.o0 = u; A.o1 = v;
+        A.part = part;
         return launch_cell_s<5>(A, st);
     }
     const int rows = cell_rows(g);
@@ -3641,6 +3655,15 @@ int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, 
                        double* part) {
     StreamArgs a = stream_args(g, c, which == 2 ? v : u, which == 2 ? vo : uo, which == 2 ? rv : ru, nullptr, alpha,
                                omega, part, true);
+    static const int sd3 = getenv("NSGPU_SD3") ? std::atoi(getenv("NSGPU_SD3")) : 2;
+    if (part && which != 3 && sd3 == 3) {   // (A/B: 3 rows in flight)
+        a.nsj = (g.ny + SW3R - 1) / SW3R;
+        int nblk = 0;
+        const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep3<FUSE_NONE, true, 3>), 7, &nblk);
+        if (which == 2) a.part = part + nstr;
+        if (nblk) NS_LAUNCH((k_sweep3<FUSE_NONE, true, 3>), dim3(nblk), dim3(256), 0, st, a);
+        return nstr;
+    }
     if (part) {   // the batch's last pass with its output residual (7-row cone: 7 ghost rows on slabs)
         a.nsj = (g.ny + SW3R - 1) / SW3R;
         int nblk = 0;

@@ -28,6 +28,8 @@ ap.add_argument("--poly", default="", help="a tests/polygons.py geometry instead
 ap.add_argument("--sweep32", type=int, default=0,
                 help="instead of time steps: K fp32-field Jacobi sweeps (NS_K_POISSON32) of the random input")
 ap.add_argument("--stats-only", action="store_true", help="gather only the per-step stats (large grids)")
+ap.add_argument("--hash", action="store_true",
+                help="gather each slab's sha256 of u, v, phi (bytes, row-major) instead of the fields (large grids)")
 ap.add_argument("--async-steps", action="store_true",
                 help="ns_step_async (monitor one call late, realigned here) instead of ns_step")
 a = ap.parse_args()
@@ -65,7 +67,13 @@ try:
             mm[k][:4] = mm[k + 1][:4] if k + 1 < a.nsteps else last
     else:
         mm = [list(gs.step().values())[:7] for _ in range(a.nsteps)]
-    u, v, phi = (np.zeros((1, ny)),) * 3 if a.stats_only else gs.fields()
+    if a.hash:
+        import hashlib
+        f = gs.fields()
+        u, v, phi = (np.frombuffer(hashlib.sha256(np.ascontiguousarray(x).tobytes()).digest(), dtype=np.uint8)[None]
+                     for x in f)
+    else:
+        u, v, phi = (np.zeros((1, ny)),) * 3 if a.stats_only else gs.fields()
 except Exception as e:  # report, don't hang the other rank
     status = f"error: {e}"
     u = v = phi = np.zeros((1, ny))

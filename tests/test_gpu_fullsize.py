@@ -12,7 +12,11 @@
     distributed, 2-6 replicated): the per-step monitor equals the single-rank run to 1e-12;
   * configs[3]'s decomposition: 8192^2 on 8 slabs of 1024 rows (8 processes on the one GPU,
     host transport; levels 0-2 distributed, 3-7 replicated): monitor to 1e-12 and the same
-    sweep / V-cycle counts as one rank.
+    sweep / V-cycle counts as one rank;
+  * configs[3]'s weak-scaling point: 2048 x 8192 per rank on 8 ranks (16384 x 8192 global,
+    host transport): monitor to 1e-12 and the same counts as one rank;
+  * configs[4]'s decomposition: the 16384^2 fp32-field Jacobi sweep on 2 and 8 slabs (host
+    transport), bit-identical to one rank (sha256 of every slab's phi, u, v).
 """
 import os
 import subprocess
@@ -108,20 +112,45 @@ def test_fp32_sweeps_at_config_size(gpu, n):
     assert abs(r32 - r64) <= 1e-5 * r64
 
 
-@pytest.mark.parametrize("n,nproc,steps", [(4096, 2, 2), (8192, 8, 2)])
-def test_slabs_at_config_size(tmp_path, gpu, n, nproc, steps):
-    out = tmp_path / "r.npz"
+def _mr(tmp_path, nproc, port, *args, timeout=240):
+    out = tmp_path / f"r{port}.npz"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr=127.0.0.1", f"--master-port={29671 + nproc}", os.path.join(HERE, "mr_worker.py"),
-           "--output", str(out), "--xport", "host", "--size", str(n), "--nsteps", str(steps),
-           "--solver", str(gpu.NS_POISSON_MG), "--tol", "1e-8", "--stats-only"]
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(HERE, "mr_worker.py"),
+           "--output", str(out), "--xport", "host", *args]
     env = dict(os.environ, OMP_NUM_THREADS="2")
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     r = dict(np.load(out, allow_pickle=False))
     assert str(r["status"]) == "ok", r["status"]
-    gs = gpu.GpuSolver(gpu.rectangle(n, n), 1.0 / (8 * n), 100.0, rtol=1e-8)
+    return r
+
+
+# (n, ny) global; 16384 x 8192 on 8 ranks = configs[3]'s weak-scaling point, 2048 x 8192 per rank
+@pytest.mark.parametrize("n,ny,nproc,steps", [(4096, 4096, 2, 2), (8192, 8192, 8, 2), (16384, 8192, 8, 2)])
+def test_slabs_at_config_size(tmp_path, gpu, n, ny, nproc, steps):
+    r = _mr(tmp_path, nproc, 29671 + nproc + (ny != n), "--size", str(n), "--size-y", str(ny), "--nsteps",
+            str(steps), "--solver", str(gpu.NS_POISSON_MG), "--tol", "1e-8", "--stats-only", timeout=280)
+    gs = gpu.GpuSolver(gpu.rectangle(n, ny), 1.0 / (8 * n), 100.0, rtol=1e-8)
     mm = np.array([list(gs.step().values())[:7] for _ in range(steps)])
     gs.close()
     assert np.max(np.abs(r["mm"][:, :4] - mm[:, :4])) <= 1e-12
     assert np.array_equal(r["mm"][:, 4:], mm[:, 4:])       # same sweep / V-cycle counts
+
+
+@pytest.mark.parametrize("nproc", [2, 8])
+def test_fp32_sweep_slabs_at_config_size(tmp_path, gpu, nproc):
+    """configs[4]: 16384^2 fp32 fields + fp64 residual on `nproc` slabs (host transport): every
+    slab's phi bit-identical to the single rank's rows (sha256), the residual to 1e-12."""
+    import hashlib
+    n, k = 16384, 5
+    r = _mr(tmp_path, nproc, 29691 + nproc, "--size", str(n), "--sweep32", str(k), "--hash", timeout=280)
+    gs = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 100.0, poisson=gpu.NS_POISSON_JACOBI, omega=0.8)
+    gs.fill_random(0x5EED)
+    res = gs.kernel(gpu.NS_K_POISSON32, k)[0]
+    phi = gs.get(gpu.NS_ARR_PHI)
+    gs.close()
+    for q in range(nproc):
+        i0, i1 = gpu.slab_range(n, nproc, q)
+        h = np.frombuffer(hashlib.sha256(np.ascontiguousarray(phi[i0:i1]).tobytes()).digest(), dtype=np.uint8)
+        assert np.array_equal(r["phi"][q], h), q
+    assert abs(r["mm"][0, 0] - res) <= 1e-12 * res

@@ -13,6 +13,12 @@ n_allreduces / n_exchanges.  Reductions cover the slab only, so the slab's itera
 can differ from the global solve's by a cycle; both are printed.
 
   python tools/slab_projection.py [--n 8192] [--ranks 1,2,4,8] [--warmup 5] [--steps 10]
+  python tools/slab_projection.py --weak-rows 2048 --ny 8192      # configs[3]'s weak scaling
+
+--weak-rows W: weak scaling, W rows per rank on a (W P) x ny grid (configs[3]: 2048 x 8192 per GPU).
+For each P the single-rank run of the global (W P) x ny grid gives the replayed counts (its own
+problem: the grid grows with P); the row reports the virtual slab's ms/step, the projected one, and
+the weak-scaling efficiency t(P = 1) / t(P).
 """
 import argparse
 import json
@@ -24,18 +30,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(n, P, warmup, steps, re, replay=None):
+def run(n, P, warmup, steps, re, replay=None, ny=None):
     """One configuration; P > 1 replays the single-rank run's per-step (Helmholtz sweeps,
     V-cycles) sequence `replay` (NSGPU_VIRTUAL_ITERS): the same work per step as the global
     solve, which the 8-slab tests show the P-rank run reproduces exactly."""
     import navierstokessolver_amd as nsa
-    dt = 1.0 / (8 * n)
+    ny = ny or n
+    dt = 1.0 / (8 * max(n, ny))
     kw = {}
     if P > 1:
         os.environ["NSGPU_RCCL_LOOPBACK"] = "1"
         os.environ["NSGPU_VIRTUAL_ITERS"] = ",".join(f"{h}:{c}" for h, c in replay)
         kw = dict(rank=P // 2, nranks=P)
-    gs = nsa.GpuSolver(nsa.cavity(n), dt, re, device=0, **kw)
+    grid = nsa.cavity(n) if ny == n else nsa.rectangle(n, ny, lx=1.0, ly=ny / n)
+    gs = nsa.GpuSolver(grid, dt, re, device=0, **kw)
     os.environ.pop("NSGPU_RCCL_LOOPBACK", None)
     os.environ.pop("NSGPU_VIRTUAL_ITERS", None)
     seq = []
@@ -50,7 +58,7 @@ def run(n, P, warmup, steps, re, replay=None):
     seq += [(s["it_u"], s["it_phi"]) for s in st]
     i0, i1 = gs.i0, gs.i1
     gs.close()
-    return seq, {"P": P, "rank": P // 2 if P > 1 else 0, "rows": i1 - i0, "ms_per_step": t * 1e3,
+    return seq, {"P": P, "nx": n, "ny": ny, "rank": P // 2 if P > 1 else 0, "rows": i1 - i0, "ms_per_step": t * 1e3,
             "vcycles_per_step": sum(s["it_phi"] for s in st) / steps,
             "helm_sweeps_per_step": sum(s["it_u"] for s in st) / steps,
             "exchanges_per_step": sum(s["n_exchanges"] for s in st) / steps,
@@ -71,8 +79,32 @@ def main():
                     help="assumed exposed cost of one ghost-row exchange group beyond the self-copy measured "
                          "here (64 KB per row per side over one 153 GB/s-class xGMI link, overlapped with the "
                          "interior strips)")
+    ap.add_argument("--weak-rows", type=int, default=0, help="weak scaling: rows per rank (grid (W P) x ny)")
+    ap.add_argument("--ny", type=int, default=0, help="columns of the weak-scaling grid (default --n)")
     a = ap.parse_args()
     rows = []
+    if a.weak_rows:
+        ny = a.ny or a.n
+        t1 = None
+        for P in (int(x) for x in a.ranks.split(",")):
+            n = a.weak_rows * P
+            seq, r1 = run(n, 1, a.warmup, a.steps, a.re, ny=ny)   # the global problem's counts
+            if P == 1:
+                r = r1
+            else:
+                _, r = run(n, P, a.warmup, a.steps, a.re, seq, ny=ny)
+            extra = 0.0 if P == 1 else (r["allreduces_per_step"] * a.allreduce_us + r["exchanges_per_step"] * a.exchange_us) * 1e-3
+            r["projected_ms_per_step"] = r["ms_per_step"] + extra
+            r["projected_mlups"] = n * ny / (r["projected_ms_per_step"] * 1e-3) / 1e6
+            r["single_gpu_ms_per_step_of_this_grid"] = r1["ms_per_step"]
+            t1 = t1 or r["projected_ms_per_step"]
+            r["weak_efficiency"] = t1 / r["projected_ms_per_step"]
+            rows.append(r)
+            print(json.dumps(r), flush=True)
+        print(json.dumps({"weak_rows": a.weak_rows, "ny": ny, "assumptions": {"allreduce_us": a.allreduce_us,
+                          "exchange_us": a.exchange_us},
+                          "weak_efficiency": {r["P"]: round(r["weak_efficiency"], 3) for r in rows}}), flush=True)
+        return
     replay = [tuple(int(x) for x in t.split(":")) for t in a.replay.split(",")] if a.replay else None
     for P in (int(x) for x in a.ranks.split(",")):
         if P > 1 and replay is None:
