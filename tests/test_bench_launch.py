@@ -3,6 +3,7 @@ driver's `python3 bench.py --gpus N` form must reach every rank).  CPU only: the
 (NSBENCH_LAUNCH_PROBE) makes each rank report its rank / world and exit before any GPU call."""
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -16,7 +17,8 @@ def test_bench_self_launches_n_ranks():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--steps", "1"],
                        capture_output=True, text=True, env=env, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
-    probes = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    # (the ranks share the child's stdout: their lines may interleave)
+    probes = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", r.stdout)]
     assert sorted(p["probe_rank"] for p in probes) == [0, 1, 2]
     assert all(p["world"] == 3 for p in probes)
     assert sorted(p["local_rank"] for p in probes) == [0, 1, 2]
