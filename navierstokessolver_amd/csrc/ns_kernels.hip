@@ -1317,12 +1317,13 @@ struct RhsStreamArgs {
     int slo, shi0, nrun;          // strip-row subset of this launch (phase_range)
     int ilo, ihi, jhi;            // written cells: local rows [ilo, ihi), columns [2, jhi)
 };
+constexpr int K1_LMAX = 128;      // k_rhs_s: rows per strip at most (one resident round of strips)
 constexpr int RC_K1 = 4;          // k_rhs_s: row tables from row ib-4 (the window-fill steps read ib-4 .. )
 template <bool NT, int SK>
 __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
     const Geo& g = A.g;
     const Coef& c = A.c;
-    __shared__ double rcs[4][64 + 2 * RC_K1 + 2][4];   // per row: hx, 1/hx, 2/(h_{i-1}+h_i), 2/(h_i+h_{i+1})
+    __shared__ double rcs[4][K1_LMAX + 2 * RC_K1 + 2][4];   // per row: hx, 1/hx, 2/(h_{i-1}+h_i), 2/(h_i+h_{i+1})
     const int lane = threadIdx.x & 63;
     const int nstr = A.nsj * A.nrun;
     const int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1561,7 +1562,7 @@ __global__ __launch_bounds__(256) void k_rhs_ring(Geo g, Coef c, double dt, doub
 struct CellStreamArgs {
     Geo g;
     Coef c;
-    double dt, rdt;               // dt and 1/dt
+    double dt;
     const double *a0, *a1, *a2;   // K3: u, v, -;  K5: phi, u*, v*
     double *o0, *o1;              // K3: rhs_phi, -;  K5: u, v
     double* part;
@@ -1595,6 +1596,7 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
         const bool wr = lane >= 1 && lane <= 62 && c0 < ny;
         const bool o0 = wr && v0, o1 = wr && v1;
         const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
+        const double hy0 = c.hy[k0], hy1 = c.hy[k1];
         const double fs0 = c.fsy[k0], fn0 = c.fny[k0], fs1 = c.fsy[k1], fn1 = c.fny[k1];
         const bool s0 = c0 > 0, n0 = c0 < ny - 1, s1 = c1 > 0, n1 = c1 < ny - 1;
         const int rlo = -HALO, rhi = g.nxl + HALO - 1;
@@ -1613,27 +1615,13 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                 y = *reinterpret_cast<const double2*>(A.a2 + (ptrdiff_t)lr * ld + lc);
             }
         };
-        // outputs through buffer resources: a lane / row that must not write gets a dropped
-        // offset (no store inside a branch; k_jacobi_s), an odd ny's padding column included
-        const __amdgpu_buffer_rsrc_t bo0 = __builtin_amdgcn_make_buffer_rsrc(A.o0, (short)0, 0x7FFFFFF0, 0x00020000);
-        const __amdgpu_buffer_rsrc_t bo1 =
-            __builtin_amdgcn_make_buffer_rsrc(K == 5 ? A.o1 : A.o0, (short)0, 0x7FFFFFF0, 0x00020000);
-        const double ry0 = c.rhy[k0], ry1 = c.rhy[k1], rdt = A.rdt;
         auto step = [&](const double2 q, const double2 x, const double2 y, int r) {
-            W0 = W1; W1 = W2; W2 = vcopy(q);
+            W0 = W1; W1 = W2; W2 = q;
             const int m = r - 1;
-            const bool live = m >= ib && m < ie;
-            const int gi = min(max(g.i0 + m, 0), g.nx - 1);
+            if (m < ib || m >= ie) return;
+            const int gi = g.i0 + m;
             const bool hW = gi > 0, hE = gi < g.nx - 1;
-            const double fw = c.fwx[gi], fe = c.fex[gi], rx = c.rhx[gi];
-            const unsigned base = ((unsigned)max(m, 0) * (unsigned)ld + (unsigned)c0) * 8u;
-            const unsigned off0 = (live && o0) ? base : OOB, off1 = (live && o1) ? base + 8u : OOB;
-            auto st2 = [&](__amdgpu_buffer_rsrc_t rs, double a0, double a1) {
-                __builtin_amdgcn_raw_buffer_store_b64(
-                    (nsu2){(unsigned)__double2loint(a0), (unsigned)__double2hiint(a0)}, rs, (int)off0, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b64(
-                    (nsu2){(unsigned)__double2loint(a1), (unsigned)__double2hiint(a1)}, rs, (int)off1, 0, 0);
-            };
+            const double hx = c.hx[gi], fw = c.fwx[gi], fe = c.fex[gi];
             if (K == 3) {
                 // Div_V: u faces along x from the window, v faces along y from the lanes
                 const double2 vv = x;
@@ -1647,12 +1635,14 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                     const double V1 = face_val(uc, ue, hE, fe, ghost_v(g, uc, 1, 0));
                     const double V2 = face_val(vc, vs, e ? s1 : s0, e ? fs1 : fs0, ghost_v(g, vc, 2, 1));
                     const double V3 = face_val(vc, vn, e ? n1 : n0, e ? fn1 : fn0, ghost_v(g, vc, 3, 1));
-                    // (reciprocals: 1/h from the tables, 1/dt -- within an ulp of Div_V's divisions)
-                    val[e] = ((V1 - V0) * rx + (V3 - V2) * (e ? ry1 : ry0)) * rdt;
+                    val[e] = ((V1 - V0) / hx + (V3 - V2) / (e ? hy1 : hy0)) / A.dt;
                 }
-                st2(bo0, val[0], val[1]);   // (an odd ny's padding column: dropped, left untouched)
-                if (live && o0) { acc[0] += val[0]; acc[1] += val[0] * val[0]; }
-                if (live && o1) { acc[0] += val[1]; acc[1] += val[1] * val[1]; }
+                if (wr) {   // (an odd ny's last pair: column ny is row padding, left untouched)
+                    if (v1) st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(val[0], val[1]), false);
+                    else A.o0[(ptrdiff_t)m * ld + c0] = val[0];
+                }
+                if (o0) { acc[0] += val[0]; acc[1] += val[0] * val[0]; }
+                if (o1) { acc[0] += val[1]; acc[1] += val[1] * val[1]; }
             } else {
                 // GradP (phi ghost = phi at wall / inlet faces: 0.5 (p + p); a NEUMANN side's
                 // extrapolated ghost goes through k_correct) and the correction
@@ -1666,15 +1656,20 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                     const double V1 = face_val(pc, pe, hE, fe, pc);
                     const double V2 = face_val(pc, ps, e ? s1 : s0, e ? fs1 : fs0, pc);
                     const double V3 = face_val(pc, pn, e ? n1 : n0, e ? fn1 : fn0, pc);
-                    const double gx = (V1 - V0) * rx, gy = (V3 - V2) * (e ? ry1 : ry0);
+                    const double gx = (V1 - V0) / hx, gy = (V3 - V2) / (e ? hy1 : hy0);
                     un[e] = (e ? x.y : x.x) - A.dt * gx;
                     vn[e] = (e ? y.y : y.x) - A.dt * gy;
                 }
-                st2(bo0, un[0], un[1]);
-                st2(bo1, vn[0], vn[1]);
+                if (wr && v1) {
+                    st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(un[0], un[1]), false);
+                    st_stream(A.o1 + (ptrdiff_t)m * ld + c0, make_double2(vn[0], vn[1]), false);
+                } else if (wr) {
+                    A.o0[(ptrdiff_t)m * ld + c0] = un[0];
+                    A.o1[(ptrdiff_t)m * ld + c0] = vn[0];
+                }
 #pragma unroll
                 for (int e = 0; e < 2; e++) {
-                    if (!live || !(e ? o1 : o0)) continue;
+                    if (!(e ? o1 : o0)) continue;
                     // NaN-propagating min so a blown-up step is visible in the stats
                     acc[0] = fmin(acc[0], un[e] != un[e] ? -INFINITY : un[e]);
                     acc[1] = fmin(acc[1], un[e] != un[e] ? -INFINITY : -un[e]);
@@ -1685,14 +1680,11 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
         };
         const int r0 = ib - 1, r1 = ie;
 #pragma unroll
-        for (int q = 0; q < SD; q++) {
-            load(r0 + q, Q[q], X[q], Y[q]);
-            asm volatile("" ::: "memory");   // (keep the slots' issue order: the loop's vmcnt bookkeeping)
-        }
+        for (int q = 0; q < SD; q++) load(r0 + q, Q[q], X[q], Y[q]);
         for (int r = r0; r <= r1; r += SD) {
 #pragma unroll
             for (int q = 0; q < SD; q++) {
-                step(Q[q], X[q], Y[q], r + q);   // (rows past r1: computed, not stored)
+                if (r + q <= r1) step(Q[q], X[q], Y[q], r + q);
                 load(r + q + SD, Q[q], X[q], Y[q]);
             }
         }
@@ -3256,7 +3248,12 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         const void* kk = kv == 3 ? (const void*)k_rhs_s3<true>
                        : kv == 23 ? (const void*)k_rhs_s<true, 3>
                        : kv == 24 ? (const void*)k_rhs_s<true, 4> : (const void*)k_rhs_s<true, 2>;
-        A.L = strip_rows(g.nxl, A.nsj, resident_waves(kk), 8);
+        {
+            // the fewest rows that keep every strip in ONE resident round (strip_rows caps at 64:
+            // 4096^2 at 2 waves / SIMD then left 128 of 2176 strips to a second round)
+            const long nsi = std::max(1L, resident_waves(kk) / A.nsj);
+            A.L = std::min(std::max((int)((g.nxl + nsi - 1) / nsi + 1) & ~1, 8), K1_LMAX);
+        }
         A.nsi = (g.nxl + A.L - 1) / A.L;
         const int nstr = A.nsj * A.nsi;
         A.nrun = phase_range(g.nxl, A.L, A.nsi, 2, &A.slo, &A.shi0);   // u, v rows ib-2 .. ie+1
@@ -3324,7 +3321,7 @@ int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const do
                hipStream_t st) {
     if (cell_streaming() && !g.fc) {
         CellStreamArgs A{};
-        A.g = g; A.c = c; A.dt = dt; A.rdt = 1.0 / dt; A.a0 = u; A.a1 = v; A.o0 = rp; A.part = part;
+        A.g = g; A.c = c; A.dt = dt; A.a0 = u; A.a1 = v; A.o0 = rp; A.part = part;
         return launch_cell_s<3>(A, st);
     }
     const int rows = cell_rows(g);
@@ -3376,8 +3373,7 @@ int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, con
     // (a NEUMANN side's phi ghost reaches two cells inward: the grid kernel's grad_phi)
     if (cell_streaming() && !g.fc && !(g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3])) {
         CellStreamArgs A{};
-        A.g = g; A.c = c; A.dt = dt; A.rdt = 1.0 / dt; A.a0 = phi; A.a1 = us; A.a2 = vs; A.o0 = u; A.o1 = v;
-        A.part = part;
+        A.g = g; A.c = c; A.dt = dt; A.a0 = phi; A.a1 = us; A.a2 = vs; A.o0 = u; A.o1 = v; A.part = part;
         return launch_cell_s<5>(A, st);
     }
     const int rows = cell_rows(g);
@@ -3655,7 +3651,7 @@ int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, 
                        double* part) {
     StreamArgs a = stream_args(g, c, which == 2 ? v : u, which == 2 ? vo : uo, which == 2 ? rv : ru, nullptr, alpha,
                                omega, part, true);
-    static const int sd3 = getenv("NSGPU_SD3") ? std::atoi(getenv("NSGPU_SD3")) : 2;
+    static const int sd3 = getenv("NSGPU_SD3") ? std::atoi(getenv("NSGPU_SD3")) : 3;   // (3: 114 vs 118 us at 4096^2)
     if (part && which != 3 && sd3 == 3) {   // (A/B: 3 rows in flight)
         a.nsj = (g.ny + SW3R - 1) / SW3R;
         int nblk = 0;
