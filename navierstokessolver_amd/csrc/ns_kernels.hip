@@ -1306,27 +1306,82 @@ __global__ __launch_bounds__(256) void k_to_f64(const float* __restrict__ src, d
 // ApplyBoundaryConditions terms included.  u, v rows ib-2 .. ie+1 are read (2 ghost rows), cu0 /
 // cv0 at the output rows (updated in place: each lane reads its cells' old values before it
 // stores them), stores through buffer resources (dropped offsets for unwritten lanes / rows).
+// the ring of k_rhs_s (below): the slab's cells within two rows of the W / E walls (whole rows),
+// and on the other rows the columns 0, 1 and [jhi, ny).  Thread k: the whole wall rows first
+// (nfull of them, from local row fr[q]), then (ncol columns) x the other rows.
+struct RhsRingArgs {
+    int nfull, fr[4];             // whole rows (local indices)
+    int ncol, jhi;                // ring columns per other row: 0, 1, jhi .. ny-1
+    int rlo, rhi;                 // the other rows: local [rlo, rhi)
+    int n;                        // ring cells
+};
 struct RhsStreamArgs {
     Geo g;
     Coef c;
     double dt, re;
-    const double *u, *v;
+    const double *u, *v, *phi;
     double *cu, *cv, *ru, *rv;
-    double* part;                 // 2 per strip: sum ru^2, sum rv^2 of its written cells
+    double* part;                 // 2 per strip: sum ru^2, sum rv^2 of its written cells; then 2 per ring block
     int nsj, nsi, L;
     int slo, shi0, nrun;          // strip-row subset of this launch (phase_range)
     int ilo, ihi, jhi;            // written cells: local rows [ilo, ihi), columns [2, jhi)
+    int nsblk;                    // workgroups of strips; those past it take the ring (nring of them)
+    int nring, nstr;              // ring workgroups of this launch, the pass's strip count (partial offset)
+    RhsRingArgs R;
 };
+__device__ __forceinline__ void rhs_ring_body(const Geo& g, const Coef& c, double dt, double re,
+                                              const double* __restrict__ u, const double* __restrict__ v,
+                                              const double* __restrict__ phi, double* __restrict__ cu,
+                                              double* __restrict__ cv, double* __restrict__ ru,
+                                              double* __restrict__ rv, double* __restrict__ part, const RhsRingArgs& R,
+                                              int blk) {
+    const int k = blk * 256 + threadIdx.x;
+    double acc[2] = {0.0, 0.0};
+    if (k < R.n) {
+        int li, j;
+        const int nf = R.nfull * g.ny;
+        if (k < nf) {
+            const int q = k / g.ny;
+            li = R.fr[q];
+            j = k - q * g.ny;
+        } else {
+            const int q = (k - nf) / R.ncol, e = (k - nf) - q * R.ncol;
+            li = R.rlo + q;
+            j = e < 2 ? e : R.jhi + (e - 2);
+        }
+        const int ld = g.ld, gi = g.i0 + li;
+        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+        auto U = [&](int di, int dj) { return ldf(u, ld, li + di, j + dj); };
+        auto V = [&](int di, int dj) { return ldf(v, ld, li + di, j + dj); };
+        auto X = [&](int t, int d) { return (t == 0 ? c.hx : t == 1 ? c.rhx : c.rsx)[gi + d]; };
+        auto Y = [&](int t, int d) { return (t == 0 ? c.hy : t == 1 ? c.rhy : c.rsy)[j + d]; };
+        double cun, cvn, ru_, rv_;
+        rhs_cell<true, TopoRect>(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
+        cu[o] = cun;
+        cv[o] = cvn;
+        ru[o] = ru_;
+        rv[o] = rv_;
+        acc[0] = ru_ * ru_;
+        acc[1] = rv_ * rv_;
+    }
+    block_reduce_sum<2>(acc, part + 2 * blk);
+}
+
 constexpr int K1_LMAX = 128;      // k_rhs_s: rows per strip at most (one resident round of strips)
 constexpr int RC_K1 = 4;          // k_rhs_s: row tables from row ib-4 (the window-fill steps read ib-4 .. )
 template <bool NT, int SK>
 __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
     const Geo& g = A.g;
     const Coef& c = A.c;
+    if ((int)blockIdx.x >= A.nsblk) {   // the wall ring's workgroups, beside the strips (block-uniform)
+        rhs_ring_body(g, c, A.dt, A.re, A.u, A.v, A.phi, A.cu, A.cv, A.ru, A.rv, A.part + 2 * A.nstr, A.R,
+                      (int)blockIdx.x - A.nsblk);
+        return;
+    }
     __shared__ double rcs[4][K1_LMAX + 2 * RC_K1 + 2][4];   // per row: hx, 1/hx, 2/(h_{i-1}+h_i), 2/(h_i+h_{i+1})
     const int lane = threadIdx.x & 63;
     const int nstr = A.nsj * A.nrun;
-    const int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = xcd_swizzle(blockIdx.x, A.nsblk) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double (*rc)[4] = rcs[threadIdx.x >> 6];
     const int run = w / A.nsj;
     const int wid = phase_block(run, A.slo, A.shi0) * A.nsj + (w - run * A.nsj);
@@ -1509,48 +1564,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 // stencil's wall cases and the ApplyBoundaryConditions terms), global loads; partials (ru^2, rv^2)
 // per block.  Thread k: the whole wall rows first (nfull of them, from local row fr[q]), then
 // (ncol columns) x the other rows.
-struct RhsRingArgs {
-    int nfull, fr[4];             // whole rows (local indices)
-    int ncol, jhi;                // ring columns per other row: 0, 1, jhi .. ny-1
-    int rlo, rhi;                 // the other rows: local [rlo, rhi)
-    int n;                        // ring cells
-};
-__global__ __launch_bounds__(256) void k_rhs_ring(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
-                                                  const double* __restrict__ v, const double* __restrict__ phi,
-                                                  double* __restrict__ cu, double* __restrict__ cv,
-                                                  double* __restrict__ ru, double* __restrict__ rv,
-                                                  double* __restrict__ part, RhsRingArgs R) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    double acc[2] = {0.0, 0.0};
-    if (k < R.n) {
-        int li, j;
-        const int nf = R.nfull * g.ny;
-        if (k < nf) {
-            const int q = k / g.ny;
-            li = R.fr[q];
-            j = k - q * g.ny;
-        } else {
-            const int q = (k - nf) / R.ncol, e = (k - nf) - q * R.ncol;
-            li = R.rlo + q;
-            j = e < 2 ? e : R.jhi + (e - 2);
-        }
-        const int ld = g.ld, gi = g.i0 + li;
-        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
-        auto U = [&](int di, int dj) { return ldf(u, ld, li + di, j + dj); };
-        auto V = [&](int di, int dj) { return ldf(v, ld, li + di, j + dj); };
-        auto X = [&](int t, int d) { return (t == 0 ? c.hx : t == 1 ? c.rhx : c.rsx)[gi + d]; };
-        auto Y = [&](int t, int d) { return (t == 0 ? c.hy : t == 1 ? c.rhy : c.rsy)[j + d]; };
-        double cun, cvn, ru_, rv_;
-        rhs_cell<true, TopoRect>(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
-        cu[o] = cun;
-        cv[o] = cvn;
-        ru[o] = ru_;
-        rv[o] = rv_;
-        acc[0] = ru_ * ru_;
-        acc[1] = rv_ * rv_;
-    }
-    block_reduce_sum<2>(acc, part + 2 * blockIdx.x);
-}
 
 // ------------------------------------------------ K3 / K5 as streaming strips
 // The same strip walk as k_sweep (128 loaded columns, 124 written, 2 per lane, x-neighbours
@@ -3235,10 +3248,10 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         return (int)(cg.x * cg.y);
     }
     if (!e) {
-        // the streaming inner kernel (k_rhs_s) and its wall ring (k_rhs_ring)
+        // the streaming inner kernel (k_rhs_s) with its wall ring (extra workgroups of the same launch)
         RhsStreamArgs A{};
-        A.g = g; A.c = c; A.dt = dt; A.re = re; A.u = u; A.v = v; A.cu = cu; A.cv = cv; A.ru = ru; A.rv = rv;
-        A.part = part;
+        A.g = g; A.c = c; A.dt = dt; A.re = re; A.u = u; A.v = v; A.phi = phi; A.cu = cu; A.cv = cv; A.ru = ru;
+        A.rv = rv; A.part = part;
         A.jhi = std::max(2, (g.ny - 2) & ~1);
         A.ilo = std::max(0, std::min(2 - g.i0, g.nxl));
         A.ihi = std::max(A.ilo, std::min(g.nx - 2 - g.i0, g.nxl));
@@ -3246,7 +3259,6 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         const char* w3 = getenv("NSGPU_K1S");
         const int kv = w3 ? std::atoi(w3) : 0;
         const void* kk = kv == 3 ? (const void*)k_rhs_s3<true>
-                       : kv == 23 ? (const void*)k_rhs_s<true, 3>
                        : kv == 24 ? (const void*)k_rhs_s<true, 4> : (const void*)k_rhs_s<true, 2>;
         {
             // the fewest rows that keep every strip in ONE resident round (strip_rows caps at 64:
@@ -3255,30 +3267,29 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
             A.L = std::min(std::max((int)((g.nxl + nsi - 1) / nsi + 1) & ~1, 8), K1_LMAX);
         }
         A.nsi = (g.nxl + A.L - 1) / A.L;
-        const int nstr = A.nsj * A.nsi;
+        A.nstr = A.nsj * A.nsi;
         A.nrun = phase_range(g.nxl, A.L, A.nsi, 2, &A.slo, &A.shi0);   // u, v rows ib-2 .. ie+1
-        if (A.nrun > 0 && A.jhi > 2 && A.ihi > A.ilo) {
-            void* args[] = {&A};
-            if (launch_raw(kk, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), args, 0, st) != hipSuccess) return -1;
-        }
-        else if (g_phase != 1)
-            (void)hipMemsetAsync(part, 0, 2 * sizeof(double) * nstr, st);   // (no inner cells: zero partials)
-        RhsRingArgs R{};
+        const bool inner = A.jhi > 2 && A.ihi > A.ilo;
+        if (!inner) A.nrun = 0;
+        RhsRingArgs& R = A.R;
         R.jhi = A.jhi;
         for (int li = 0; li < g.nxl; li++)
             if ((li < A.ilo || li >= A.ihi) && R.nfull < 4) R.fr[R.nfull++] = li;
         R.rlo = A.ilo;
         R.rhi = A.ihi;
-        R.ncol = 2 + (g.ny - A.jhi);
-        if (A.jhi <= 2) R.ncol = g.ny;   // (tiny grids: whole rows, columns 0, 1 and from jhi = 2 on)
+        R.ncol = A.jhi <= 2 ? g.ny : 2 + (g.ny - A.jhi);   // (tiny grids: whole rows)
         R.n = R.nfull * g.ny + (R.rhi - R.rlo) * R.ncol;
         const int nring = (R.n + 255) / 256;
-        if (R.nfull == 4 && A.ilo + (g.nxl - A.ihi) > 4) return -1;   // (cannot happen: ilo <= 2, nxl - ihi <= 2)
         // the ring reads phi's and u, v's ghost rows (wall terms, MUSCL): with the edge phase
-        if (g_phase != 1 && nring > 0)
-            NS_LAUNCH(k_rhs_ring, dim3(nring), dim3(256), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv,
-                      part + 2 * nstr, R);
-        return nstr + nring;
+        A.nring = g_phase != 1 ? nring : 0;
+        A.nsblk = (A.nsj * A.nrun + 3) / 4;
+        if (!inner && g_phase != 1)
+            (void)hipMemsetAsync(part, 0, 2 * sizeof(double) * A.nstr, st);   // (no inner cells: zero partials)
+        if (A.nsblk + A.nring > 0) {
+            void* args[] = {&A};
+            if (launch_raw(kk, dim3(A.nsblk + A.nring), dim3(256), args, 0, st) != hipSuccess) return -1;
+        }
+        return A.nstr + nring;
     }
     if (std::strcmp(e, "global") != 0) {   // NSGPU_RHS=lds: the LDS-tiled K1 (A/B)
         const int nti = (g.nxl + RT - 1) / RT;
