@@ -96,6 +96,10 @@ struct MgLevel {
     // coarse V-cycle -- takes it as zero without reading it or its ghost rows; any other consumer
     // materialises the zeros first (zero_phi)
     bool zero = false;
+    // multi-rank: the iterate's 5 ghost rows were sent right after this level's fused restriction
+    // pass (riding on the next exchange group down the V-cycle): the prolongation pass needs no
+    // exchange of its own for them -- phi is not written in between
+    bool phi_ghost = false;
     nsg::Geo gs{};
     std::vector<int> si0, sn;
 };
@@ -151,6 +155,11 @@ struct ns_solver {
     // pass's interior strips run (NSGPU_OVERLAP=0: exchange, then the whole pass)
     int overlap = 1;
     int helm_b_pend = 0;          // RHS_u / RHS_v ghost rows owed to the first Helmholtz pair pass
+    // ghost-row requests riding on the NEXT exchange group (halo_reqs / gather_level), e.g. a
+    // multigrid level's post-restriction iterate (MgLevel::phi_ghost)
+    struct Piggy { const nsg::Geo* g; double* f; int w; };
+    Piggy piggy[4];
+    int npiggy = 0;
     hipStream_t cst = nullptr;
     hipEvent_t xev[2] = {nullptr, nullptr};
     hipEvent_t fev = nullptr;     // fetch_begin / fetch_end: the scalars' copy to the host is done
@@ -239,17 +248,45 @@ struct HaloReq {
 // the RCCL / host-transport call sites are live: several ranks, or the one-rank loopback
 inline bool comm_on(const ns_solver* s) { return s->nranks > 1 || s->loopback; }
 
+// the RCCL send / recv pairs of ghost-row requests (inside the caller's ncclGroupStart / End)
+int halo_rccl(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs) {
+    const bool lo = s->rank > 0 || s->nranks == 1, hi = s->rank < s->nranks - 1 || s->nranks == 1;
+    const int p_lo = s->loopback ? 0 : s->rank - 1, p_hi = s->loopback ? 0 : s->rank + 1;
+    const bool self = s->nranks == 1;
+    for (int k = 0; k < nreq; k++) {
+        const HaloReq& q = reqs[k];
+        const size_t cnt = (size_t)q.w * q.g->ld;
+        const int ld = q.g->ld, nxl = q.g->nxl;
+        double* f = q.f;
+        const double *flo = self ? f - (ptrdiff_t)q.w * ld : f, *fhi = f + (ptrdiff_t)(self ? nxl : nxl - q.w) * ld;
+        if (lo) {
+            NCCLCHK(ncclSend(flo, cnt, ncclDouble, p_lo, s->comm, xs));
+            NCCLCHK(ncclRecv(f - (ptrdiff_t)q.w * ld, cnt, ncclDouble, p_lo, s->comm, xs));
+        }
+        if (hi) {
+            NCCLCHK(ncclSend(fhi, cnt, ncclDouble, p_hi, s->comm, xs));
+            NCCLCHK(ncclRecv(f + (ptrdiff_t)nxl * ld, cnt, ncclDouble, p_hi, s->comm, xs));
+        }
+    }
+    return 0;
+}
+
 // ghost rows to / from the x-neighbours; every request of the list goes in ONE RCCL group
 // (one latency for all of them)
-int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs = nullptr) {
+int halo_reqs(ns_solver* s, const HaloReq* reqs_in, int nreq_in, hipStream_t xs = nullptr) {
     if (!xs) xs = s->st;
     if (!comm_on(s)) return 0;
     s->n_xchg++;
+    // the requests riding along (ns_solver::piggy) join this group
+    HaloReq reqs[12];
+    int nreq = 0;
+    for (int k = 0; k < nreq_in && nreq < 12; k++) reqs[nreq++] = reqs_in[k];
+    for (int k = 0; k < s->npiggy && nreq < 12; k++) reqs[nreq++] = HaloReq{s->piggy[k].g, s->piggy[k].f, s->piggy[k].w};
+    s->npiggy = 0;
     const bool lo = s->rank > 0 || s->nranks == 1, hi = s->rank < s->nranks - 1 || s->nranks == 1;
     // (loopback: the 1-rank communicator's only rank, 0, is every peer; a one-rank loopback sends
     // its physical ghost rows round trip unchanged -- they may hold boundary data, e.g. the
     // outflow preconditioner's)
-    const int p_lo = s->loopback ? 0 : s->rank - 1, p_hi = s->loopback ? 0 : s->rank + 1;
     const bool self = s->nranks == 1;
     if (s->ht.exchange) {
         for (int k = 0; k < nreq; k++) {
@@ -275,21 +312,7 @@ int halo_reqs(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs = null
         return 0;
     }
     NCCLCHK(ncclGroupStart());
-    for (int k = 0; k < nreq; k++) {
-        const HaloReq& q = reqs[k];
-        const size_t cnt = (size_t)q.w * q.g->ld;
-        const int ld = q.g->ld, nxl = q.g->nxl;
-        double* f = q.f;
-        const double *flo = self ? f - (ptrdiff_t)q.w * ld : f, *fhi = f + (ptrdiff_t)(self ? nxl : nxl - q.w) * ld;
-        if (lo) {
-            NCCLCHK(ncclSend(flo, cnt, ncclDouble, p_lo, s->comm, xs));
-            NCCLCHK(ncclRecv(f - (ptrdiff_t)q.w * ld, cnt, ncclDouble, p_lo, s->comm, xs));
-        }
-        if (hi) {
-            NCCLCHK(ncclSend(fhi, cnt, ncclDouble, p_hi, s->comm, xs));
-            NCCLCHK(ncclRecv(f + (ptrdiff_t)nxl * ld, cnt, ncclDouble, p_hi, s->comm, xs));
-        }
-    }
+    CHK(halo_rccl(s, reqs, nreq, xs));
     NCCLCHK(ncclGroupEnd());
     return 0;
 }
@@ -911,6 +934,7 @@ int gather_level(ns_solver* s, MgLevel& C) {
         HIPCHK(hipMemsetAsync(C.phi - (ptrdiff_t)nsg::HALO * ld, 0,
                               (size_t)(C.g.nx + 2 * nsg::HALO) * ld * sizeof(double), s->st));
     if (s->ht.allreduce) {
+        if (s->npiggy) CHK(halo_reqs(s, nullptr, 0));   // (the rows riding along: an exchange of their own)
         const size_t n = (size_t)C.g.nx * ld;
         if (n > (size_t)INT32_MAX) { set_err("agglomerated level too large for the host transport"); return NS_EINVAL; }
         CHK(ensure_stage(s, n));
@@ -927,6 +951,13 @@ int gather_level(ns_solver* s, MgLevel& C) {
         return 0;
     }
     NCCLCHK(ncclGroupStart());
+    if (s->npiggy) {   // the ghost rows riding along (ns_solver::piggy) join the gather's group
+        HaloReq r[4];
+        for (int k = 0; k < s->npiggy; k++) r[k] = HaloReq{s->piggy[k].g, s->piggy[k].f, s->piggy[k].w};
+        const int n = s->npiggy;
+        s->npiggy = 0;
+        CHK(halo_rccl(s, r, n, s->st));
+    }
     for (int q = 0; q < s->nranks; q++) {
         if (q == s->rank) continue;
         if (s->loopback) {   // virtual slab: the same messages, every peer this process
@@ -1049,6 +1080,13 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool want_check, bo
                 };
                 nb = nr ? overlapped(s, rq, nr, pass) : pass();
                 if (nb < 0) return nb;
+                // the pass's output is this level's iterate until its prolongation pass: its ghost
+                // rows ride on the next exchange group down the V-cycle (piggy), so that pass needs
+                // no exchange of its own for them
+                if (comm_on(s) && fused_prolong(s, l) && s->npiggy < 4) {
+                    s->piggy[s->npiggy++] = ns_solver::Piggy{&F.g, F.tmp, 5};   // (F.tmp: the output, swapped below)
+                    F.phi_ghost = true;
+                }
             }
             if (t) { CHK(t_end(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); (*tn)++; }
             std::swap(F.phi, F.tmp);
@@ -1095,9 +1133,15 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool want_check, bo
                 else CHK(halo_reqs(s, {HaloReq{&C.g, C.phi, 3}, HaloReq{&F.g, F.phi, 5}}));
                 n = pass();
             } else {
-                // (the coarse ghost rows are read by the edge strips only)
+                // (the coarse ghost rows are read by the edge strips only; the fine ones were sent
+                // after the restriction pass when phi_ghost -- or still ride on this group)
+                const bool cx = !(cv.gather || C.repl);
                 const HaloReq r[2] = {{&F.g, F.phi, 5}, {&C.g, C.phi, 3}};
-                n = overlapped(s, r, (cv.gather || C.repl) ? 1 : 2, pass);
+                const HaloReq* rq = F.phi_ghost ? r + 1 : r;
+                const int nr = F.phi_ghost ? (cx ? 1 : 0) : (cx ? 2 : 1);
+                F.phi_ghost = false;
+                if (nr == 0 && s->npiggy) CHK(halo_reqs(s, nullptr, 0));   // (rows still riding: send them now)
+                n = nr ? overlapped(s, rq, nr, pass) : pass();
                 if (n < 0) return n;
             }
             if (pp) nb_out = n;

@@ -6,7 +6,7 @@ import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 phase, agg = 0, collections.defaultdict(lambda: [0, 0.0])
-names = {1: "allreduce x10", 2: "send+recv self x10", 3: "7 send/recv pairs x10", 4: "end"}
+names = {0: "RCCL init (before the first marker)", 1: "allreduce x10", 2: "send+recv self x10", 3: "7 send/recv pairs x10", 4: "end"}
 for r in rows:
     n = r["Kernel_Name"].split("(")[0].replace("void ", "")
     if n.startswith("marker"):
@@ -16,4 +16,4 @@ for r in rows:
     a[0] += 1
     a[1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
 for (p, n), (c, t) in sorted(agg.items()):
-    print(f"phase {p} ({names.get((p - 1) % 4 + 1, '?')}): {n:60s} x{c:3d} avg {t / c:8.1f} us")
+    print(f"phase {p} ({names.get(0 if p == 0 else (p - 1) % 4 + 1, "?")}): {n:60s} x{c:3d} avg {t / c:8.1f} us")
