@@ -16,4 +16,5 @@ for r in rows:
     a[0] += 1
     a[1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
 for (p, n), (c, t) in sorted(agg.items()):
-    print(f"phase {p} ({names.get(0 if p == 0 else (p - 1) % 4 + 1, "?")}): {n:60s} x{c:3d} avg {t / c:8.1f} us")
+    label = names.get(0 if p == 0 else (p - 1) % 4 + 1, "?")
+    print(f"phase {p} ({label}): {n:60s} x{c:3d} avg {t / c:8.1f} us")
