@@ -119,6 +119,8 @@ int launch_pois_jacobi_tiled(const Geo& g, const Coef& c, double omega, const do
                              const double* rp, const double* shift, double* part, hipStream_t st);
 // rows per streaming strip (tuning knob)
 void set_strip_rows(int L);
+// CUs the following launches' streams may use (0 = all): sizes "one resident round" of strips
+void set_compute_cus(int n);
 // the next kernel launch records a, b at its begin / end (hipExtLaunchKernel); pending() clears
 // the request and says whether no launch took it
 void time_next_launch(hipEvent_t a, hipEvent_t b);

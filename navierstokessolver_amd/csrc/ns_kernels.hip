@@ -467,6 +467,56 @@ static int g_phase = 0;
 // the row-block subset of phase g_phase for blocks of `rows` rows (n of them) reading `depth`
 // rows beyond their own: launch block k is block k if k < *lo, else *hi0 + (k - *lo); returns
 // how many blocks the launch covers
+// The strip rows of a streaming launch for the exchange / compute overlap phase (set_strip_phase),
+// for a kernel reading `depth` rows beyond its own (plan_rows below):
+//   phase 0: the slab's rows in strips of L;
+//   phase 1: rows [d, nxl - d) (their read cone inside the slab: launched while the ghost rows
+//            travel), in strips of L;
+//   phase 2: the two edge bands [0, d) and [nxl - d, nxl), one strip of d rows each -- a short
+//            row pipeline after the exchange instead of a whole strip of L rows;
+// d = depth rounded up to even.  Launch strip row k covers rows [ib, min(ib + L, rend)) with
+// ib = rb0 + k L for k < slo, else rb1 + (k - slo) L; its partial slot is (pbase + k) nsj + sj.
+struct RowPlan {
+    int L, slo, nrun, rb0, rb1, rend, pbase;
+    __device__ __forceinline__ void rows(int run, int& ib, int& ie) const {
+        ib = run < slo ? rb0 + run * L : rb1 + (run - slo) * L;
+        ie = min(ib + L, rend);
+    }
+};
+
+// host side of RowPlan: the strip rows of the current phase (g_phase) for `nxl` rows in strips of
+// `L` (one resident round), reading `depth` rows beyond their own; returns the pass's strip-row
+// count (partial slots / nsj, the same in every phase) and sets the plan's launch subset
+static int plan_rows(int nxl, int L, int depth, RowPlan* p) {
+    const int d = (depth + 1) & ~1, R = nxl - 2 * d;
+    p->pbase = 0;
+    p->rb1 = 0;
+    p->L = L;
+    if (g_phase == 0 || R < 2) {
+        const int n = (nxl + L - 1) / L;
+        p->nrun = g_phase == 1 ? 0 : n;   // (a slab too thin to split: all of it after the exchange)
+        p->slo = n;
+        p->rb0 = 0;
+        p->rend = nxl;
+        return n;
+    }
+    const int n1 = (R + L - 1) / L;
+    if (g_phase == 1) {
+        p->nrun = p->slo = n1;
+        p->rb0 = d;
+        p->rend = nxl - d;
+    } else {
+        p->L = d;
+        p->nrun = 2;
+        p->slo = 1;
+        p->rb0 = 0;
+        p->rb1 = nxl - d;
+        p->rend = nxl;
+        p->pbase = n1;
+    }
+    return n1 + 2;
+}
+
 static int phase_range(int nxl, int rows, int n, int depth, int* lo, int* hi0) {
     *lo = n; *hi0 = 0;
     if (!g_phase) return n;
@@ -477,6 +527,7 @@ static int phase_range(int nxl, int rows, int n, int depth, int* lo, int* hi0) {
     return sa + (n - sb);
 }
 __device__ __forceinline__ int phase_block(int k, int lo, int hi0) { return k < lo ? k : hi0 + (k - lo); }
+
 
 constexpr int RT = 16;
 __global__ __launch_bounds__(256) void k_rhs_lds(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
@@ -1322,8 +1373,8 @@ struct RhsStreamArgs {
     const double *u, *v, *phi;
     double *cu, *cv, *ru, *rv;
     double* part;                 // 2 per strip: sum ru^2, sum rv^2 of its written cells; then 2 per ring block
-    int nsj, nsi, L;
-    int slo, shi0, nrun;          // strip-row subset of this launch (phase_range)
+    int nsj;
+    RowPlan P;                    // strip rows of this launch (plan_rows)
     int ilo, ihi, jhi;            // written cells: local rows [ilo, ihi), columns [2, jhi)
     int nsblk;                    // workgroups of strips; those past it take the ring (nring of them)
     int nring, nstr;              // ring workgroups of this launch, the pass's strip count (partial offset)
@@ -1380,13 +1431,13 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
     }
     __shared__ double rcs[4][K1_LMAX + 2 * RC_K1 + 2][4];   // per row: hx, 1/hx, 2/(h_{i-1}+h_i), 2/(h_i+h_{i+1})
     const int lane = threadIdx.x & 63;
-    const int nstr = A.nsj * A.nrun;
+    const int nstr = A.nsj * A.P.nrun;
     const int w = xcd_swizzle(blockIdx.x, A.nsblk) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double (*rc)[4] = rcs[threadIdx.x >> 6];
-    const int run = w / A.nsj;
-    const int wid = phase_block(run, A.slo, A.shi0) * A.nsj + (w - run * A.nsj);
-    const int si = wid / A.nsj, sj = wid - si * A.nsj;
-    const int ib = si * A.L, ie = min(ib + A.L, g.nxl);
+    const int run = w / A.nsj, sj = w - run * A.nsj;
+    const int wid = (A.P.pbase + run) * A.nsj + sj;
+    int ib, ie;
+    A.P.rows(run, ib, ie);
     if (w < nstr) {
         for (int t = lane; t < ie - ib + 2 * RC_K1 + 2; t += 64) {
             const int gi = min(max(g.i0 + ib - RC_K1 + t, 0), g.nx - 1);
@@ -1579,8 +1630,8 @@ struct CellStreamArgs {
     const double *a0, *a1, *a2;   // K3: u, v, -;  K5: phi, u*, v*
     double *o0, *o1;              // K3: rhs_phi, -;  K5: u, v
     double* part;
-    int nsj, nsi, L;
-    int slo, shi0, nrun;          // strip-row subset of this launch (phase_range)
+    int nsj;
+    RowPlan P;                    // strip rows of this launch (plan_rows)
 };
 
 // one face value along a line: interior r-weighted interpolation, or the wall's (q + ghost)/2
@@ -1593,15 +1644,17 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
     const Geo& g = A.g;
     const Coef& c = A.c;
     const int lane = threadIdx.x & 63;
-    const int nstr = A.nsj * A.nrun;
+    const int nstr = A.nsj * A.P.nrun;
     const int w = __builtin_amdgcn_readfirstlane(xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (int)(threadIdx.x >> 6));
     const int run = w / A.nsj;
-    const int wid = phase_block(run, A.slo, A.shi0) * A.nsj + (w - run * A.nsj);   // the strip (partial slot)
+    const int wid = (A.P.pbase + run) * A.nsj + (w - run * A.nsj);   // the strip (partial slot)
     double acc[4] = {0.0, 0.0, INFINITY, INFINITY};   // K3: sum, sum^2; K5: (umin, -umax, vmin, -vmax)
     if (K == 5) acc[0] = acc[1] = INFINITY;
     if (w < nstr) {
-        const int si = wid / A.nsj, sj = wid - si * A.nsj;
-        const int jb = sj * SW, ib = si * A.L, ie = min(ib + A.L, g.nxl);
+        const int sj = w - run * A.nsj;
+        int ib, ie;
+        A.P.rows(run, ib, ie);
+        const int jb = sj * SW;
         const int ny = g.ny, ld = g.ld;
         const int c0 = jb - 2 + 2 * lane, c1 = c0 + 1;
         const int lc = min(max(c0, 0), ld - 2);
@@ -3264,13 +3317,11 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
             // the fewest rows that keep every strip in ONE resident round (strip_rows caps at 64:
             // 4096^2 at 2 waves / SIMD then left 128 of 2176 strips to a second round)
             const long nsi = std::max(1L, resident_waves(kk) / A.nsj);
-            A.L = std::min(std::max((int)((g.nxl + nsi - 1) / nsi + 1) & ~1, 8), K1_LMAX);
+            const int L = std::min(std::max((int)((g.nxl + nsi - 1) / nsi + 1) & ~1, 8), K1_LMAX);
+            A.nstr = A.nsj * plan_rows(g.nxl, L, 2, &A.P);   // u, v rows ib-2 .. ie+1
         }
-        A.nsi = (g.nxl + A.L - 1) / A.L;
-        A.nstr = A.nsj * A.nsi;
-        A.nrun = phase_range(g.nxl, A.L, A.nsi, 2, &A.slo, &A.shi0);   // u, v rows ib-2 .. ie+1
         const bool inner = A.jhi > 2 && A.ihi > A.ilo;
-        if (!inner) A.nrun = 0;
+        if (!inner) A.P.nrun = 0;
         RhsRingArgs& R = A.R;
         R.jhi = A.jhi;
         for (int li = 0; li < g.nxl; li++)
@@ -3282,7 +3333,7 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         const int nring = (R.n + 255) / 256;
         // the ring reads phi's and u, v's ghost rows (wall terms, MUSCL): with the edge phase
         A.nring = g_phase != 1 ? nring : 0;
-        A.nsblk = (A.nsj * A.nrun + 3) / 4;
+        A.nsblk = (A.nsj * A.P.nrun + 3) / 4;
         if (!inner && g_phase != 1)
             (void)hipMemsetAsync(part, 0, 2 * sizeof(double) * A.nstr, st);   // (no inner cells: zero partials)
         if (A.nsblk + A.nring > 0) {
@@ -3315,11 +3366,9 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
 template <int K>
 static int launch_cell_s(CellStreamArgs A, hipStream_t st) {
     A.nsj = (A.g.ny + SW - 1) / SW;
-    A.L = strip_rows(A.g.nxl, A.nsj, resident_waves((const void*)k_cell_s<K>), 4);
-    A.nsi = (A.g.nxl + A.L - 1) / A.L;
-    const int nstr = A.nsj * A.nsi;
-    A.nrun = phase_range(A.g.nxl, A.L, A.nsi, 1, &A.slo, &A.shi0);   // window rows ib-1 .. ie
-    if (A.nrun > 0) NS_LAUNCH(k_cell_s<K>, dim3((A.nsj * A.nrun + 3) / 4), dim3(256), 0, st, A);
+    const int L = strip_rows(A.g.nxl, A.nsj, resident_waves((const void*)k_cell_s<K>), 4);
+    const int nstr = A.nsj * plan_rows(A.g.nxl, L, 1, &A.P);   // window rows ib-1 .. ie
+    if (A.P.nrun > 0) NS_LAUNCH(k_cell_s<K>, dim3((A.nsj * A.P.nrun + 3) / 4), dim3(256), 0, st, A);
     return nstr;
 }
 
@@ -3411,20 +3460,32 @@ static int g_strip_rows = 0;  // 0 = adaptive
 void set_strip_rows(int L) { g_strip_rows = L >= 4 ? (std::min(L, 64) & ~1) : 0; }
 
 // waves of kernel `k` (256-thread workgroups) the whole chip holds at once
+// CUs the compute stream may use (0: all): a multi-rank solver's compute stream leaves a few CUs
+// to its comm stream (ns_solver.cpp, NSGPU_COMM_CUS), and "one resident round" is sized for the rest
+static thread_local int g_compute_cus = 0;
+void set_compute_cus(int n) { g_compute_cus = n; }
+
 static long resident_waves(const void* k) {
     static std::mutex mu;
-    static std::map<const void*, long> cache;
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = cache.find(k);
-    if (it != cache.end()) return it->second;
-    int nb = 0, dev = 0, cus = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0);
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const long cap = std::max(1L, (long)nb * 4 * cus);
-    cache[k] = cap;
-    if (getenv("NSGPU_VERBOSE")) fprintf(stderr, "nsgpu: %p holds %d blocks/CU x %d CUs\n", k, nb, cus);
-    return cap;
+    static std::map<const void*, int> cache;   // blocks per CU
+    static int cus = 0;
+    int nb = 0;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = cache.find(k);
+        if (it != cache.end()) {
+            nb = it->second;
+        } else {
+            int dev = 0;
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0);
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            cache[k] = nb;
+            if (getenv("NSGPU_VERBOSE")) fprintf(stderr, "nsgpu: %p holds %d blocks/CU x %d CUs\n", k, nb, cus);
+        }
+    }
+    const int n = g_compute_cus > 0 ? std::min(g_compute_cus, cus) : cus;
+    return std::max(1L, (long)nb * 4 * n);
 }
 
 // rows per strip: the fewest rows (re-read halo rows cost (rows + halo) / rows of the
@@ -3662,29 +3723,23 @@ int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, 
                        double* part) {
     StreamArgs a = stream_args(g, c, which == 2 ? v : u, which == 2 ? vo : uo, which == 2 ? rv : ru, nullptr, alpha,
                                omega, part, true);
-    static const int sd3 = getenv("NSGPU_SD3") ? std::atoi(getenv("NSGPU_SD3")) : 3;   // (3: 114 vs 118 us at 4096^2)
-    if (part && which != 3 && sd3 == 3) {   // (A/B: 3 rows in flight)
+    // the batch's last pass with its output residual (7-row cone: 7 ghost rows on slabs); rows in
+    // flight: 3 (114 vs 118 us at 4096^2 with 2; NSGPU_SD3=2: A/B)
+    static const int sd3 = getenv("NSGPU_SD3") ? std::atoi(getenv("NSGPU_SD3")) : 3;
+    if (part) {
         a.nsj = (g.ny + SW3R - 1) / SW3R;
         int nblk = 0;
-        const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep3<FUSE_NONE, true, 3>), 7, &nblk);
-        if (which == 2) a.part = part + nstr;
-        if (nblk) NS_LAUNCH((k_sweep3<FUSE_NONE, true, 3>), dim3(nblk), dim3(256), 0, st, a);
-        return nstr;
-    }
-    if (part) {   // the batch's last pass with its output residual (7-row cone: 7 ghost rows on slabs)
-        a.nsj = (g.ny + SW3R - 1) / SW3R;
-        int nblk = 0;
-        const void* kr = which == 3 ? (const void*)k_sweep3<FUSE_UV, true> : (const void*)k_sweep3<FUSE_NONE, true>;
+        const void* kr = which == 3 ? (sd3 == 3 ? (const void*)k_sweep3<FUSE_UV, true, 3> : (const void*)k_sweep3<FUSE_UV, true, 2>)
+                                    : (sd3 == 3 ? (const void*)k_sweep3<FUSE_NONE, true, 3> : (const void*)k_sweep3<FUSE_NONE, true, 2>);
         const int nstr = plan_strips2(a, resident_waves(kr), 7, &nblk);
         if (which == 2) a.part = part + nstr;   // partials: u at [0, n), v at [n, 2n) (launch_helm_sweep2)
         if (!nblk) return nstr;
         if (which == 3) {
             a.in2 = v; a.out2 = vo; a.b2 = rv; a.part2 = part + nstr;
             nblk = (2 * a.nsj * a.nrun + 3) / 4;
-            NS_LAUNCH((k_sweep3<FUSE_UV, true>), dim3(nblk), dim3(256), 0, st, a);
-        } else {
-            NS_LAUNCH((k_sweep3<FUSE_NONE, true>), dim3(nblk), dim3(256), 0, st, a);
         }
+        void* args[] = {&a};
+        if (launch_raw(kr, dim3(nblk), dim3(256), args, 0, st) != hipSuccess) return -1;
         return nstr;
     }
     a.nsj = (g.ny + SW2X - 1) / SW2X;

@@ -161,6 +161,9 @@ struct ns_solver {
     Piggy piggy[4];
     int npiggy = 0;
     hipStream_t cst = nullptr;
+    // multi-rank: CUs reserved for the comm stream (its RCCL kernels run beside the compute
+    // stream's strips instead of queueing behind them; NSGPU_COMM_CUS, 0 = no masks)
+    int comm_cus = 0, compute_cus = 0;
     hipEvent_t xev[2] = {nullptr, nullptr};
     hipEvent_t fev = nullptr;     // fetch_begin / fetch_end: the scalars' copy to the host is done
     // ns_step_async: the step's min/max travel to mm_host behind the step's last kernel (mev);
@@ -2045,7 +2048,29 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     }
     s->device = dev;
     if (hipSetDevice(dev) != hipSuccess) { set_err("hipSetDevice(%d) failed", dev); return fail(NS_EHIP); }
-    if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); return fail(NS_EHIP); }
+    {
+        // multi-rank: the compute stream leaves `comm_cus` CUs (the highest ids) to the comm stream,
+        // whose RCCL kernels then run beside the interior strips of an overlapped pass instead of
+        // queueing until the strips' resident round drains
+        int cus = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const bool comm = p->nranks > 1 || loopback;
+        s->comm_cus = comm ? 8 : 0;
+        if (const char* e = getenv("NSGPU_COMM_CUS")) s->comm_cus = std::max(0, std::atoi(e));
+        if (s->comm_cus > 0 && s->comm_cus < cus && cus <= 1024) {
+            std::vector<uint32_t> mc((cus + 31) / 32, 0u), mx((cus + 31) / 32, 0u);
+            for (int k = 0; k < cus; k++) (k < cus - s->comm_cus ? mc : mx)[k / 32] |= 1u << (k % 32);
+            if (hipExtStreamCreateWithCUMask(&s->st, (uint32_t)mc.size(), mc.data()) != hipSuccess ||
+                hipExtStreamCreateWithCUMask(&s->cst, (uint32_t)mx.size(), mx.data()) != hipSuccess) {
+                set_err("CU-masked stream create failed");
+                return fail(NS_EHIP);
+            }
+            s->compute_cus = cus - s->comm_cus;
+        } else {
+            s->comm_cus = 0;
+        }
+    }
+    if (!s->st && hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); return fail(NS_EHIP); }
     if (hipEventCreateWithFlags(&s->fev, hipEventDisableTiming) != hipSuccess) { set_err("event create failed"); return fail(NS_EHIP); }
     s->loopback = loopback;
     if (loopback && p->nranks > 1) {
@@ -2070,7 +2095,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (p->nranks > 1 || s->loopback) {
         const char* ov = getenv("NSGPU_OVERLAP");
         s->overlap = ov ? std::atoi(ov) != 0 : 1;
-        if (hipStreamCreateWithFlags(&s->cst, hipStreamNonBlocking) != hipSuccess ||
+        if ((!s->cst && hipStreamCreateWithFlags(&s->cst, hipStreamNonBlocking) != hipSuccess) ||
             hipEventCreateWithFlags(&s->xev[0], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s->xev[1], hipEventDisableTiming) != hipSuccess) {
             set_err("comm stream / event create failed");
@@ -2296,6 +2321,7 @@ int ns_step(ns_solver* s, ns_stats* out) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     ns_stats st{};
     HIPCHK(hipSetDevice(s->device));
+    nsg::set_compute_cus(s->compute_cus);
     if (s->mm_pending) HIPCHK(hipEventSynchronize(s->mev));   // (an ns_step_async before: its copy lands first)
     s->mm_pending = 0;
     CHK(step_body(s, st));
@@ -2316,6 +2342,7 @@ int ns_step_async(ns_solver* s, ns_stats* out) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     ns_stats st{};
     HIPCHK(hipSetDevice(s->device));
+    nsg::set_compute_cus(s->compute_cus);
     if (!s->mm_host) {
         HIPCHK(hipHostMalloc(&s->mm_host, 4 * sizeof(double), hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&s->mev, hipEventDisableTiming));
@@ -2340,6 +2367,7 @@ int ns_monitor(ns_solver* s, double* mm) {
     if (!s || !mm) { set_err("null argument"); return NS_EINVAL; }
     if (!s->mm_pending) { set_err("ns_monitor: no ns_step_async since the last ns_step / ns_monitor"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
+    nsg::set_compute_cus(s->compute_cus);
     HIPCHK(hipEventSynchronize(s->mev));
     s->mm_pending = 0;
     ns_stats st{};
@@ -2359,6 +2387,7 @@ int ns_set_timing(ns_solver* s, int on) {
 int ns_get_array(ns_solver* s, int which, double* host) {
     CHK(check_arr(s, which));
     HIPCHK(hipSetDevice(s->device));
+    nsg::set_compute_cus(s->compute_cus);
     HIPCHK(hipMemcpy2DAsync(host, (size_t)s->g.ny * 8, s->arr[which], (size_t)s->g.ld * 8, (size_t)s->g.ny * 8,
                             s->g.nxl, hipMemcpyDeviceToHost, s->st));
     HIPCHK(hipStreamSynchronize(s->st));
@@ -2368,6 +2397,7 @@ int ns_get_array(ns_solver* s, int which, double* host) {
 int ns_set_array(ns_solver* s, int which, const double* host) {
     CHK(check_arr(s, which));
     HIPCHK(hipSetDevice(s->device));
+    nsg::set_compute_cus(s->compute_cus);
     HIPCHK(hipMemcpy2DAsync(s->arr[which], (size_t)s->g.ld * 8, host, (size_t)s->g.ny * 8, (size_t)s->g.ny * 8,
                             s->g.nxl, hipMemcpyHostToDevice, s->st));
     // keep the derived scalars consistent with an injected right-hand side
@@ -2429,6 +2459,7 @@ int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* 
 int ns_kernel(ns_solver* s, int which, int iters, double* out) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
+    nsg::set_compute_cus(s->compute_cus);
     const double alpha = s->dt / (2 * s->re);
     switch (which) {
     case NS_K_RHS:
@@ -2565,6 +2596,7 @@ int ns_mg_transfer(ns_solver* s, int op, double* coarse) {
         return NS_EINVAL;
     }
     HIPCHK(hipSetDevice(s->device));
+    nsg::set_compute_cus(s->compute_cus);
     MgLevel& F = level(s, 0);
     MgLevel& C = level(s, 1);
     const CoarseView cv = coarse_view(s, 0);   // this rank's coarse rows (a slab of a replicated level)
@@ -2594,6 +2626,7 @@ int ns_fill_random(ns_solver* s, uint64_t seed) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     if (s->g.fc) { set_err("ns_fill_random (the sweep benchmark input) is rectangle-only"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
+    nsg::set_compute_cus(s->compute_cus);
     nsg::launch_fill_random(s->g, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], seed, s->st);
     CHK(rhs_mean(s));  // the random rhs's mean becomes the Poisson shift (null-space removal)
     CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
@@ -2605,6 +2638,7 @@ int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
     if (!s || iters <= 0) { set_err("bad arguments"); return NS_EINVAL; }
     if (s->kv[0]) { set_err("ns_time_poisson times the rectangle's sweeps (no NEUMANN side, no mask)"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
+    nsg::set_compute_cus(s->compute_cus);
     CHK(ensure_events(s, 2 * (size_t)iters));
     // NSGPU_TIME_PAIRS=1: time the two-sweep (temporally blocked) pass instead of a single sweep
     const bool pairs = getenv("NSGPU_TIME_PAIRS") && s->poisson != NS_POISSON_JACOBI;
@@ -2643,6 +2677,7 @@ int ns_time_poisson_fp32(ns_solver* s, int warmup, int iters, double* out) {
     if (!s || iters <= 0) { set_err("bad arguments"); return NS_EINVAL; }
     if (s->kv[0]) { set_err("ns_time_poisson_fp32 times the rectangle's sweeps (no NEUMANN side, no mask)"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
+    nsg::set_compute_cus(s->compute_cus);
     CHK(ensure_events(s, 2 * (size_t)iters));
     CHK(to_f32(s));
     int nb = 0;
