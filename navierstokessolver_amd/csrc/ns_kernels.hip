@@ -1647,7 +1647,9 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
     const int nstr = A.nsj * A.P.nrun;
     const int w = __builtin_amdgcn_readfirstlane(xcd_swizzle(blockIdx.x, gridDim.x) * 4 + (int)(threadIdx.x >> 6));
     const int run = w / A.nsj;
-    const int wid = (A.P.pbase + run) * A.nsj + (w - run * A.nsj);   // the strip (partial slot)
+    // the strip's partial slot: pbase + run, or (pbase < 0: K3's fixed strips) the strip-row index
+    const int srow = A.P.pbase >= 0 ? A.P.pbase + run : (run < A.P.slo ? run : A.P.rb1 / A.P.L + (run - A.P.slo));
+    const int wid = srow * A.nsj + (w - run * A.nsj);
     double acc[4] = {0.0, 0.0, INFINITY, INFINITY};   // K3: sum, sum^2; K5: (umin, -umax, vmin, -vmax)
     if (K == 5) acc[0] = acc[1] = INFINITY;
     if (w < nstr) {
@@ -3367,7 +3369,22 @@ template <int K>
 static int launch_cell_s(CellStreamArgs A, hipStream_t st) {
     A.nsj = (A.g.ny + SW - 1) / SW;
     const int L = strip_rows(A.g.nxl, A.nsj, resident_waves((const void*)k_cell_s<K>), 4);
-    const int nstr = A.nsj * plan_rows(A.g.nxl, L, 1, &A.P);   // window rows ib-1 .. ie
+    int nstr;
+    if (K == 3) {
+        // K3's (sum, sum^2) partials set the null-space mean (values, not just a norm): the same
+        // strips in both overlap phases (phase_range), so the overlapped exchange stays bit-identical
+        const int nsi = (A.g.nxl + L - 1) / L;
+        int lo = 0, hi0 = 0;
+        const int nrun = phase_range(A.g.nxl, L, nsi, 1, &lo, &hi0);
+        A.P.L = L; A.P.rb0 = 0; A.P.rend = A.g.nxl;
+        A.P.nrun = nrun;
+        A.P.slo = lo;
+        A.P.rb1 = hi0 * L;   // launch strip row k >= lo is strip row hi0 + (k - lo)
+        A.P.pbase = -1;      // (partial slots: that strip-row numbering)
+        nstr = A.nsj * nsi;
+    } else {
+        nstr = A.nsj * plan_rows(A.g.nxl, L, 1, &A.P);   // window rows ib-1 .. ie
+    }
     if (A.P.nrun > 0) NS_LAUNCH(k_cell_s<K>, dim3((A.nsj * A.P.nrun + 3) / 4), dim3(256), 0, st, A);
     return nstr;
 }

@@ -2057,9 +2057,18 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         const bool comm = p->nranks > 1 || loopback;
         s->comm_cus = comm ? 8 : 0;
         if (const char* e = getenv("NSGPU_COMM_CUS")) s->comm_cus = std::max(0, std::atoi(e));
-        if (s->comm_cus > 0 && s->comm_cus < cus && cus <= 1024) {
+        if (s->comm_cus > 0 && s->comm_cus < cus && cus <= 1024 && cus % 8 == 0) {
+            // the reserved CUs spread evenly over the 8 XCDs: workgroups are dispatched round-robin
+            // over the XCDs, so an XCD short of CUs would be every launch's straggler (all 8 on one
+            // XCD made the strips ~40 % slower).  Bit 32 x + ((x + 8 j) % 32), j < comm_cus / 8: one
+            // CU of XCD x per j whether mask bits number the CUs XCD-major or XCD-interleaved
+            const int per = cus / 8;
+            s->comm_cus = std::max(8, s->comm_cus / 8 * 8);
             std::vector<uint32_t> mc((cus + 31) / 32, 0u), mx((cus + 31) / 32, 0u);
-            for (int k = 0; k < cus; k++) (k < cus - s->comm_cus ? mc : mx)[k / 32] |= 1u << (k % 32);
+            std::vector<char> comm_cu(cus, 0);
+            for (int x = 0; x < 8; x++)
+                for (int j = 0; j < s->comm_cus / 8; j++) comm_cu[per * x + (x + 8 * j) % per] = 1;
+            for (int k = 0; k < cus; k++) (comm_cu[k] ? mx : mc)[k / 32] |= 1u << (k % 32);
             if (hipExtStreamCreateWithCUMask(&s->st, (uint32_t)mc.size(), mc.data()) != hipSuccess ||
                 hipExtStreamCreateWithCUMask(&s->cst, (uint32_t)mx.size(), mx.data()) != hipSuccess) {
                 set_err("CU-masked stream create failed");
