@@ -1822,6 +1822,9 @@ constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2, FUSE_UV = 3;
 #ifndef XR_BUF
 #define XR_BUF 0   // FUSE_R's coarse stores through buffers too (1: 172 VGPRs, 2 waves/SIMD, slower)
 #endif
+#ifndef XR_BF
+#define XR_BF 0    // FUSE_R with the branch-free row loop (A/B builds)
+#endif
 
 // one strip of k_sweep2, walked downwards (DIR = 1) or upwards (DIR = -1); returns the
 // strip's residual partial (R5)
@@ -1842,7 +1845,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     // BF: the branch-free row loop (buffer stores, no tail guard; Helmholtz 95 -> 88 us, FUSE_P
     // 107 -> 104 us at 4096^2).  FUSE_R keeps plain stores: its deeper pipeline needed 172 VGPRs
     // (2 waves/SIMD, 112 -> 160 us), and at 3 waves it spilled and still lost 3 us
-    constexpr bool BF = !XR;
+    constexpr bool BF = !XR || XR_BF;
     double res = 0.0;
     const int jb = sj * SWc;
     const int ny = a.ny, ld = a.ld;
