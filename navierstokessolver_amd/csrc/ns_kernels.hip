@@ -1623,12 +1623,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 // r = h / (h_nb + h) come from tables (the same values Div_V / GradP compute).
 //   K3 (k_div_s):     rhs_phi = div(u*) / dt, + per-strip (sum, sum^2)     (FluidSolver.cpp:365-418)
 //   K5 (k_correct_s): u = u* - dt dphi/dx, v = v* - dt dphi/dy, + per-strip min/max (:420-456, 512-534)
+//   K7 (Poisson apply of the rectangle's BiCGStab): y = A x (LHS_phi with the NEUMANN outflow
+//       ghosts, :105-163), + per-strip (sum y, sum q y)
 struct CellStreamArgs {
     Geo g;
     Coef c;
     double dt;
-    const double *a0, *a1, *a2;   // K3: u, v, -;  K5: phi, u*, v*
-    double *o0, *o1;              // K3: rhs_phi, -;  K5: u, v
+    const double *a0, *a1, *a2;   // K3: u, v, -;  K5: phi, u*, v*;  K7: x, q (or null), -
+    double *o0, *o1;              // K3: rhs_phi, -;  K5: u, v;  K7: y, -
     double* part;
     int nsj;
     RowPlan P;                    // strip rows of this launch (plan_rows)
@@ -1639,7 +1641,7 @@ __device__ __forceinline__ double face_val(double q, double qn, bool has, double
     return has ? qn * r + q * (1 - r) : 0.5 * (q + ghost);
 }
 
-template <int K>   // 3: divergence, 5: correction
+template <int K>   // 3: divergence, 5: correction, 7: Poisson apply
 __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
     const Geo& g = A.g;
     const Coef& c = A.c;
@@ -1667,6 +1669,9 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
         const double hy0 = c.hy[k0], hy1 = c.hy[k1];
         const double fs0 = c.fsy[k0], fn0 = c.fny[k0], fs1 = c.fsy[k1], fn1 = c.fny[k1];
         const bool s0 = c0 > 0, n0 = c0 < ny - 1, s1 = c1 > 0, n1 = c1 < ny - 1;
+        // (K7: the operator's y weights toward S / N)
+        const double ps0 = K == 7 ? c.ps[k0] : 0.0, pn0c = K == 7 ? c.pn[k0] : 0.0;
+        const double ps1 = K == 7 ? c.ps[k1] : 0.0, pn1c = K == 7 ? c.pn[k1] : 0.0;
         const int rlo = -HALO, rhi = g.nxl + HALO - 1;
         // window field (K3: u; K5: phi) at rows ib-1 .. ie, row fields (K3: v; K5: u*, v*) at
         // row r-1 when row r arrives (prefetch overruns clamped onto fetched rows)
@@ -1676,9 +1681,9 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
             const int lw = min(max(r, max(ib - 1, rlo)), min(ie, rhi));
             const int lr = min(max(r - 1, ib), ie - 1);
             q = *reinterpret_cast<const double2*>(A.a0 + (ptrdiff_t)lw * ld + lc);
-            if (K == 3) {
+            if (K == 3 || (K == 7 && A.a1)) {
                 x = *reinterpret_cast<const double2*>(A.a1 + (ptrdiff_t)lr * ld + lc);
-            } else {
+            } else if (K == 5) {
                 x = *reinterpret_cast<const double2*>(A.a1 + (ptrdiff_t)lr * ld + lc);
                 y = *reinterpret_cast<const double2*>(A.a2 + (ptrdiff_t)lr * ld + lc);
             }
@@ -1711,6 +1716,38 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                 }
                 if (o0) { acc[0] += val[0]; acc[1] += val[0] * val[0]; }
                 if (o1) { acc[0] += val[1]; acc[1] += val[1] * val[1]; }
+            } else if (K == 7) {
+                // k_apply<0, TopoRect>'s sum in its order (W, E, S, N): pn (x_nb - x_c), 0 across a
+                // wall / inlet face, (ghost - x_c) / h^2 across a NEUMANN one, ghost = 2.5 x_c -
+                // 2 x_1 + 0.5 x_2 (x_1, x_2 inward: the window row, one extra row load on the side's row)
+                const double xs0 = lane_up1(W1.y), xn1 = lane_dn1(W1.x);
+                const double xs1 = lane_up1(W1.x), xn2 = lane_dn1(W1.y);   // columns c0 - 2, c1 + 2
+                const double pw = c.pw[gi], pe = c.pe[gi], wx = 1.0 / (hx * hx);
+                double2 X2 = {0.0, 0.0};   // row m + 2 (W side) or m - 2 (E side) of a NEUMANN x side
+                const bool nW = !hW && g.neu[0], nE = !hE && g.neu[1];
+                if (nW || nE) X2 = *reinterpret_cast<const double2*>(A.a0 + (ptrdiff_t)(nW ? m + 2 : m - 2) * ld + lc);
+                double val[2];
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    const double xc = e ? W1.y : W1.x, xw = e ? W0.y : W0.x, xe = e ? W2.y : W2.x;
+                    const double x2 = e ? X2.y : X2.x;
+                    const double xs = e ? W1.x : xs0, xn = e ? xn1 : W1.y;
+                    const double xss = e ? xs0 : xs1, xnn = e ? xn2 : xn1;
+                    const double hyc = e ? hy1 : hy0, wy = 1.0 / (hyc * hyc);
+                    double sm = 0.0;
+                    sm += hW ? pw * (xw - xc) : (g.neu[0] ? (2.5 * xc - 2.0 * xe + 0.5 * x2 - xc) * wx : 0.0);
+                    sm += hE ? pe * (xe - xc) : (g.neu[1] ? (2.5 * xc - 2.0 * xw + 0.5 * x2 - xc) * wx : 0.0);
+                    sm += (e ? s1 : s0) ? (e ? ps1 : ps0) * (xs - xc) : (g.neu[2] ? (2.5 * xc - 2.0 * xn + 0.5 * xnn - xc) * wy : 0.0);
+                    sm += (e ? n1 : n0) ? (e ? pn1c : pn0c) * (xn - xc) : (g.neu[3] ? (2.5 * xc - 2.0 * xs + 0.5 * xss - xc) * wy : 0.0);
+                    val[e] = sm;
+                }
+                if (wr) {
+                    if (v1) st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(val[0], val[1]), false);
+                    else A.o0[(ptrdiff_t)m * ld + c0] = val[0];
+                }
+                const double q0 = A.a1 ? x.x : 0.0, q1 = A.a1 ? x.y : 0.0;
+                if (o0) { acc[0] += val[0]; acc[1] += q0 * val[0]; }
+                if (o1) { acc[0] += val[1]; acc[1] += q1 * val[1]; }
             } else {
                 // GradP (phi ghost = phi at wall / inlet faces: 0.5 (p + p); a NEUMANN side's
                 // extrapolated ghost goes through k_correct) and the correction
@@ -1757,13 +1794,13 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
             }
         }
     }
-    constexpr int NV = K == 3 ? 2 : 4;
+    constexpr int NV = K == 5 ? 4 : 2;
 #pragma unroll
     for (int k = 0; k < NV; k++)
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             const double o = __shfl_xor(acc[k], off, 64);
-            acc[k] = K == 3 ? acc[k] + o : fmin(acc[k], o);
+            acc[k] = K == 5 ? fmin(acc[k], o) : acc[k] + o;
         }
     if (lane == 0 && w < nstr)
 #pragma unroll
@@ -1806,7 +1843,7 @@ constexpr int SW2X = 116;
 #define SD2_PLAIN 3
 #endif
 #ifndef SD2_FP
-#define SD2_FP 3
+#define SD2_FP 4   // (3: 97.4-98.4 us per 4096^2 FUSE_P pass, 4: 95.2-95.8, interleaved A/B)
 #endif
 #ifndef SD2_FPR
 #define SD2_FPR 2
@@ -3414,6 +3451,12 @@ int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const do
 
 int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double* x, double* y, const double* q,
                  double* part, hipStream_t st) {
+    const char* ae = getenv("NSGPU_APPLY");   // NSGPU_APPLY=grid: k_apply only (A/B)
+    if (op == 0 && !g.fc && cell_streaming() && !(ae && std::strcmp(ae, "grid") == 0)) {
+        CellStreamArgs A{};
+        A.g = g; A.c = c; A.a0 = x; A.a1 = q; A.o0 = y; A.part = part;
+        return launch_cell_s<7>(A, st);
+    }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
     if (op == 0 && g.fc) NS_LAUNCH((k_apply<0, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);

@@ -2049,13 +2049,14 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     s->device = dev;
     if (hipSetDevice(dev) != hipSuccess) { set_err("hipSetDevice(%d) failed", dev); return fail(NS_EHIP); }
     {
-        // multi-rank: the compute stream leaves `comm_cus` CUs (the highest ids) to the comm stream,
+        // multi-rank, opt-in (NSGPU_COMM_CUS=n): the compute stream leaves n CUs to the comm stream,
         // whose RCCL kernels then run beside the interior strips of an overlapped pass instead of
-        // queueing until the strips' resident round drains
+        // queueing until the strips' resident round drains.  Off by default: the masked compute
+        // kernels lost what the exchanges gained (virtual-slab projections, profiles/r03)
         int cus = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const bool comm = p->nranks > 1 || loopback;
-        s->comm_cus = comm ? 8 : 0;
+        s->comm_cus = 0;
         if (const char* e = getenv("NSGPU_COMM_CUS")) s->comm_cus = std::max(0, std::atoi(e));
         if (s->comm_cus > 0 && s->comm_cus < cus && cus <= 1024 && cus % 8 == 0) {
             // the reserved CUs spread evenly over the 8 XCDs: workgroups are dispatched round-robin

@@ -718,3 +718,32 @@ def test_outflow_channel_steps(gpu, nx, ny):
     its = [x["it_phi"] for x in st]
     assert np.mean(its) <= 8.0 and max(its) <= 10, its
     assert max(x["res_phi"] for x in st) <= 1e-8
+
+
+@pytest.mark.parametrize("nx,ny,bc", [(40, 24, BC_CHANNEL), (24, 48, BC_OUT_N), (30, 26, BC_OUT_WS),
+                                      (33, 20, BC_CHANNEL), (200, 134, BC_OUT_WS), (512, 130, BC_OUT_W)])
+def test_streaming_poisson_apply_matches_grid_kernel(gpu, monkeypatch, nx, ny, bc):
+    """The rectangle's BiCGStab applies LHS_phi (FluidSolver.cpp:105-163, the NEUMANN ghost
+    2.5 / -2 / 0.5 of :98-101 on every outflow side) with the streaming strip kernel
+    (k_cell_s<7>); NSGPU_CELL=grid is the thread-per-cell k_apply it replaced.  Same solve from
+    the same rhs: iteration counts within one and phi within 1e-8 relative at rtol 1e-10 (the strips'
+    partial sums group the dot products differently), at the oracle's direct solve (1e-8)."""
+    rng = np.random.default_rng(21)
+    b = rand(rng, nx * ny, 100.0)
+    out = {}
+    for mode in ("grid", "stream"):
+        if mode == "grid":
+            monkeypatch.setenv("NSGPU_CELL", "grid")
+        else:
+            monkeypatch.delenv("NSGPU_CELL", raising=False)
+        og, gs = pair(gpu, nx, ny, 1.0 / 256, 100.0, bc, rtol=1e-10)
+        gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny)); gs.set(gpu.NS_ARR_RPHI, b)
+        its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+        assert res <= 1e-10, (mode, its, res)
+        g = gs.get(gpu.NS_ARR_PHI).ravel()
+        out[mode] = (int(its), g - g.mean())
+        gs.close()
+    assert abs(out["grid"][0] - out["stream"][0]) <= 1, (out["grid"][0], out["stream"][0])
+    assert float(rel(out["stream"][1], out["grid"][1])) <= 1e-8
+    xp, _ = og.solve_poisson(b)
+    assert float(rel(out["stream"][1], xp - xp.mean())) <= 1e-8
