@@ -2881,6 +2881,16 @@ __host__ __device__ inline int cv_image_size(int nx, int ny, int* dn) {
     return off + *dn * *dn;
 }
 
+#ifndef CV_PROF
+#define CV_PROF 0   // (A/B builds: thread 0 prints the phase times of a few launches)
+#endif
+#if CV_PROF
+__device__ int cv_prof_count = 0;
+#define CV_T(k) do { if (threadIdx.x == 0 && (k) < 48) tp[(k)] = wall_clock64(); } while (0)
+#else
+#define CV_T(k) do {} while (0)
+#endif
+
 // img: the host-built LDS image (cv_image) of every level's tables (idg, cw, ce, hx, cs, cn,
 // hy; phi and b zero) and M; one copy into LDS replaces ~3 barriers of table arithmetic per
 // level.  Level 0's phi and b come from the global coarsest level.
@@ -2892,6 +2902,11 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
     extern __shared__ __attribute__((aligned(16))) double L[];
     __shared__ LdsLv lv[LV_MAX];
     __shared__ int nlev;
+#if CV_PROF
+    unsigned long long tp[48];
+    int np = 0;
+    CV_T(np); np++;
+#endif
     if (threadIdx.x == 0) {
         lv_layout(g.nx, g.ny, lv, &nlev);
         for (int k = 0; k < nlev; k++) { lv[k].dlo = dlo; lv[k].dhi = dhi; }
@@ -2909,6 +2924,10 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
         LdsLv v;
         v.ny = g.ny;
         v.rny = 1.0f / (float)g.ny;
+#if CV_PROF
+        __syncthreads();
+        CV_T(np); np++;
+#endif
         for (int t = threadIdx.x; t < n0; t += CV_THREADS) {
             int i, j;
             lv_split(v, t, i, j);
@@ -2917,11 +2936,17 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
         }
     }
     __syncthreads();
+#if CV_PROF
+    CV_T(np); np++;
+#endif
     const int nl = nlev;
     for (int cyc = 0; cyc < cycles; cyc++) {
         for (int k = 0; k < nl - 1; k++) {
             const LdsLv f = lv[k], v = lv[k + 1];
             lv_rb(L, f, somega, pre);
+#if CV_PROF
+            CV_T(np); np++;
+#endif
             for (int t = threadIdx.x; t < v.nx * v.ny; t += CV_THREADS) {
                 int I, J;
                 lv_split(v, t, I, J);
@@ -2938,6 +2963,9 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
                 L[v.phi + t] = 0.0;
             }
             __syncthreads();
+#if CV_PROF
+            CV_T(np); np++;
+#endif
         }
         if (dn > 0) {
             // x = M b (M after the levels in the image)
@@ -2952,6 +2980,9 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
         } else {
             lv_rb_last(L, lv[nl - 1], comega, citers);
         }
+#if CV_PROF
+        CV_T(np); np++;
+#endif
         for (int k = nl - 2; k >= 0; k--) {
             const LdsLv f = lv[k], v = lv[k + 1];
             for (int t = threadIdx.x; t < f.nx * f.ny; t += CV_THREADS) {
@@ -2970,7 +3001,13 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
                                  wn * e[In * v.ny + Jn]) * 0.0625;
             }
             __syncthreads();
+#if CV_PROF
+            CV_T(np); np++;
+#endif
             lv_rb(L, f, somega, post);
+#if CV_PROF
+            CV_T(np); np++;
+#endif
         }
     }
     {
@@ -2981,6 +3018,17 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
             phi[(ptrdiff_t)i * g.ld + j] = L[v.phi + t];
         }
     }
+#if CV_PROF
+    CV_T(np); np++;
+    if (threadIdx.x == 0) {
+        const int c = atomicAdd(&cv_prof_count, 1);
+        if (c >= 200 && c < 203) {
+            printf("cvprof nl=%d n0=%dx%d img=%d dn=%d :", nl, g.nx, g.ny, img_n, dn);
+            for (int k = 1; k < np && k < 48; k++) printf(" %.2f", (tp[k] - tp[k - 1]) * 0.01);
+            printf(" total %.2f us\n", (tp[np - 1] - tp[0]) * 0.01);
+        }
+    }
+#endif
 }
 
 
