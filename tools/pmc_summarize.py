@@ -7,6 +7,33 @@ gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half the bytes 
 coalesced stream -> x2; WRITE_SIZE is exact for 16-B/lane stores; both in KiB."""
 import csv, glob, json, re, sys
 
+if sys.argv[1] == "--valu":
+    # python tools/pmc_summarize.py --valu <n> <valu_dir> <out.json> key=regex ...: SQ_INSTS_VALU
+    # (wave-instructions, summed over the dispatch) per finest-level cell, median over dispatches
+    import statistics
+    n, d, out = int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    res = {"n": n, "kernels": {}, "note": "SQ_INSTS_VALU wave-instructions per dispatch / n^2 cells (finest-level dispatches, median)"}
+    for spec in sys.argv[5:]:
+        key, rx = spec.split("=", 1)
+        pat = re.compile(rx)
+        vals = {}
+        for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+            for r in csv.DictReader(open(f)):
+                if pat.search(r.get("Kernel_Name", "")) and r.get("Counter_Name") in ("SQ_INSTS_VALU", "SQ_WAVES"):
+                    g = int(r.get("Grid_Size", r.get("Grid_Size_X", "0")) or 0)
+                    vals.setdefault((r.get("Dispatch_Id"), g), {})[r["Counter_Name"]] = float(r["Counter_Value"])
+        if not vals:
+            continue
+        gmax = max(g for _, g in vals)
+        v = [x["SQ_INSTS_VALU"] for (_, g), x in vals.items() if g == gmax and "SQ_INSTS_VALU" in x]
+        w = [x["SQ_WAVES"] for (_, g), x in vals.items() if g == gmax and "SQ_WAVES" in x]
+        med = statistics.median(v)
+        res["kernels"][key] = {"regex": rx, "dispatches": len(v), "valu_wave_insts": med, "waves": statistics.median(w) if w else None,
+                               "valu_per_cell": med / (n * n), "lane_ops_per_cell": 64 * med / (n * n)}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+    sys.exit(0)
+
 n = int(sys.argv[1]); fetch_dir, write_dir, out = sys.argv[2], sys.argv[3], sys.argv[4]
 
 
