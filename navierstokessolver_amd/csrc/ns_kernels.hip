@@ -2767,6 +2767,20 @@ struct LdsLv {
     int dlo, dhi;   // a Dirichlet-centre closure (ghost value 0) on the x-low / x-high side
 };
 
+// a level's descriptor read from LDS, made wave-uniform (SGPRs instead of ~14 VGPRs per copy)
+__device__ __forceinline__ LdsLv lv_uni(const LdsLv& s) {
+    LdsLv v;
+    v.nx = __builtin_amdgcn_readfirstlane(s.nx); v.ny = __builtin_amdgcn_readfirstlane(s.ny);
+    v.phi = __builtin_amdgcn_readfirstlane(s.phi); v.b = __builtin_amdgcn_readfirstlane(s.b);
+    v.idg = __builtin_amdgcn_readfirstlane(s.idg); v.cw = __builtin_amdgcn_readfirstlane(s.cw);
+    v.ce = __builtin_amdgcn_readfirstlane(s.ce); v.cs = __builtin_amdgcn_readfirstlane(s.cs);
+    v.cn = __builtin_amdgcn_readfirstlane(s.cn); v.hx = __builtin_amdgcn_readfirstlane(s.hx);
+    v.hy = __builtin_amdgcn_readfirstlane(s.hy);
+    v.rny = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s.rny)));
+    v.dlo = __builtin_amdgcn_readfirstlane(s.dlo); v.dhi = __builtin_amdgcn_readfirstlane(s.dhi);
+    return v;
+}
+
 // k -> (k / ny, k % ny) without an integer division: float estimate + one correction
 __device__ __forceinline__ void lv_split(const LdsLv& v, int k, int& i, int& j) {
     i = __float2int_rz(__int2float_rn(k) * v.rny);
@@ -2874,10 +2888,10 @@ __device__ __forceinline__ double blk_lap(const double* L, const LdsLv& v, const
     const double* p = L + v.phi;
     const double pc = B.p[Q];
     double pw, pe, ps, pn;
-    if (di == 1) pw = B.p[Q - 2]; else pw = i > 0 ? p[k - ny] : (v.dlo ? 0.0 : pc);
-    if (di == 0) pe = B.p[Q + 2]; else pe = i < v.nx - 1 ? p[k + ny] : (v.dhi ? 0.0 : pc);
-    if (dj == 1) ps = B.p[Q - 1]; else ps = j > 0 ? p[k - 1] : pc;
-    if (dj == 0) pn = B.p[Q + 1]; else pn = j < ny - 1 ? p[k + 1] : pc;
+    if constexpr (di == 1) pw = B.p[Q - 2]; else pw = i > 0 ? p[k - ny] : (v.dlo ? 0.0 : pc);
+    if constexpr (di == 0) pe = B.p[Q + 2]; else pe = i < v.nx - 1 ? p[k + ny] : (v.dhi ? 0.0 : pc);
+    if constexpr (dj == 1) ps = B.p[Q - 1]; else ps = j > 0 ? p[k - 1] : pc;
+    if constexpr (dj == 0) pn = B.p[Q + 1]; else pn = j < ny - 1 ? p[k + 1] : pc;
     const double cw = L[v.cw + i], ce = L[v.ce + i], cs = L[v.cs + j], cn = L[v.cn + j];
     const double s = cw * pw + ce * pe + cs * ps + cn * pn;
     const double dg = -((cw + ce) + (cs + cn));
@@ -2913,6 +2927,30 @@ __device__ __forceinline__ void blk_rb(double* L, const LdsLv& v, CvBlk& B, doub
         if (B.act) { blk_upd<1>(L, v, B, omega); blk_upd<2>(L, v, B, omega); }
         __syncthreads();
     }
+}
+// the area-weighted residual sum of the block = coarse cell (I, J)'s rhs (k_restrict's order),
+// the coarse iterate zeroed
+__device__ __forceinline__ void blk_restrict(double* L, const LdsLv& f, const LdsLv& v, const CvBlk& B) {
+    if (!B.act) return;
+    double sum = 0.0;
+    double r = B.b[0] - blk_lap<0>(L, f, B);
+    sum += (L[f.hx + B.i0] * L[f.hy + B.j0]) * r;
+    r = B.b[1] - blk_lap<1>(L, f, B);
+    sum += (L[f.hx + B.i0] * L[f.hy + B.j0 + 1]) * r;
+    r = B.b[2] - blk_lap<2>(L, f, B);
+    sum += (L[f.hx + B.i0 + 1] * L[f.hy + B.j0]) * r;
+    r = B.b[3] - blk_lap<3>(L, f, B);
+    sum += (L[f.hx + B.i0 + 1] * L[f.hy + B.j0 + 1]) * r;
+    const int I = B.i0 >> 1, J = B.j0 >> 1, t = I * v.ny + J;
+    L[v.b + t] = sum / (L[v.hx + I] * L[v.hy + J]);
+    L[v.phi + t] = 0.0;
+}
+__device__ __forceinline__ void blk_prolong_all(double* L, const LdsLv& f, const LdsLv& v, CvBlk& B) {
+    if (!B.act) return;
+    blk_prolong<0>(L, f, v, B);
+    blk_prolong<1>(L, f, v, B);
+    blk_prolong<2>(L, f, v, B);
+    blk_prolong<3>(L, f, v, B);
 }
 
 // LDS footprint (doubles) of the levels from (nx, ny) down; fills lv when non-null
@@ -3016,7 +3054,7 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
     const int nl = nlev;
     for (int cyc = 0; cyc < cycles; cyc++) {
         for (int k = 0; k < nl - 1; k++) {
-            const LdsLv f = lv[k], v = lv[k + 1];
+            const LdsLv f = lv_uni(lv[k]), v = lv_uni(lv[k + 1]);
             if (BLK) {
                 CvBlk B;
                 blk_load(L, f, B);
@@ -3024,20 +3062,7 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
 #if CV_PROF
                 CV_T(np); np++;
 #endif
-                if (B.act) {
-                    double sum = 0.0;
-                    double r = B.b[0] - blk_lap<0>(L, f, B);
-                    sum += (L[f.hx + B.i0] * L[f.hy + B.j0]) * r;
-                    r = B.b[1] - blk_lap<1>(L, f, B);
-                    sum += (L[f.hx + B.i0] * L[f.hy + B.j0 + 1]) * r;
-                    r = B.b[2] - blk_lap<2>(L, f, B);
-                    sum += (L[f.hx + B.i0 + 1] * L[f.hy + B.j0]) * r;
-                    r = B.b[3] - blk_lap<3>(L, f, B);
-                    sum += (L[f.hx + B.i0 + 1] * L[f.hy + B.j0 + 1]) * r;
-                    const int I = B.i0 >> 1, J = B.j0 >> 1, t = I * v.ny + J;
-                    L[v.b + t] = sum / (L[v.hx + I] * L[v.hy + J]);
-                    L[v.phi + t] = 0.0;
-                }
+                blk_restrict(L, f, v, B);
                 __syncthreads();
 #if CV_PROF
                 CV_T(np); np++;
@@ -3070,7 +3095,7 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
         }
         if (dn > 0) {
             // x = M b (M after the levels in the image)
-            const LdsLv v = lv[nl - 1];
+            const LdsLv v = lv_uni(lv[nl - 1]);
             if ((int)threadIdx.x < dn) {
                 const double* M = L + (img_n - dn * dn) + threadIdx.x * dn;
                 double x = 0.0;
@@ -3085,16 +3110,11 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
         CV_T(np); np++;
 #endif
         for (int k = nl - 2; k >= 0; k--) {
-            const LdsLv f = lv[k], v = lv[k + 1];
+            const LdsLv f = lv_uni(lv[k]), v = lv_uni(lv[k + 1]);
             if (BLK) {
                 CvBlk B;
                 blk_load(L, f, B);
-                if (B.act) {
-                    blk_prolong<0>(L, f, v, B);
-                    blk_prolong<1>(L, f, v, B);
-                    blk_prolong<2>(L, f, v, B);
-                    blk_prolong<3>(L, f, v, B);
-                }
+                blk_prolong_all(L, f, v, B);
                 __syncthreads();
 #if CV_PROF
                 CV_T(np); np++;
@@ -3131,7 +3151,7 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
         }
     }
     {
-        const LdsLv v = lv[0];
+        const LdsLv v = lv_uni(lv[0]);
         for (int t = threadIdx.x; t < v.nx * v.ny; t += CV_THREADS) {
             int i, j;
             lv_split(v, t, i, j);
