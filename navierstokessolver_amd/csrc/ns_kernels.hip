@@ -975,10 +975,12 @@ template <int OP>
 __device__ __forceinline__ double relax(double q, double xm, double xp, double ym, double yp, double b, double cw,
                                         double ce, double cs, double cn, double dg, double w, double alpha,
                                         double& res) {
-    const double s = cw * xm + ce * xp + cs * ym + cn * yp;
-    const double aq = OP == 0 ? s + dg * q : dg * q - alpha * s;
+    // explicit fmas: every instantiation (walk direction, branch-free or not, strip or tile) rounds
+    // alike, so a cell's value does not depend on which strip or pass shape computed it
+    const double s = fma(cn, yp, fma(cs, ym, fma(cw, xm, ce * xp)));
+    const double aq = OP == 0 ? fma(dg, q, s) : fma(dg, q, -(alpha * s));
     res = b - aq;
-    return q + w * res;
+    return fma(w, res, q);
 }
 
 // Streamed field stores bypass the Infinity Cache (non-temporal): the 256 MiB die cache then
@@ -1856,12 +1858,68 @@ constexpr int sd2_of() {
 }
 // FUSE_UV: no transfer fused; two fields (the multi-rank Helmholtz pair pass, u and v) in one launch
 constexpr int FUSE_NONE = 0, FUSE_R = 1, FUSE_P = 2, FUSE_UV = 3;
+
+// Strips of a workgroup (k_sweep2 / k_sweep3).  WG2X2 = 0: the four waves take four strips side
+// by side (w = 4 t + wave).  WG2X2 = 1: a 2 x 2 block -- strip rows 2k, 2k+1 and strip columns
+// 2m, 2m+1.  Strip row 2k walks down and 2k+1 up (sweep2_body), so the 5-6 halo rows the two
+// share are read by both at the END of their walks; in different workgroups their progress drifts
+// apart over the pass and the second read misses L2, in one workgroup (one CU) they read them
+// together.  The start-of-walk halos (2k+1 / 2k+2) are read at the kernel's start by workgroups
+// launched together.  Returns whether the wave has a strip; FUSE_UV: the second field's
+// workgroups (or waves) switch `af` to in2 / out2 / b2 / part2.
+#ifndef WG2X2
+#define WG2X2 1
+#endif
+template <bool UV>
+__device__ __forceinline__ bool strip_of(const StreamArgs& a, StreamArgs& af, int& run, int& sj) {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int t = xcd_swizzle(blockIdx.x, gridDim.x);
+    if (WG2X2) {
+        const int h = (a.nsj + 1) >> 1, nt = h * ((a.nrun + 1) >> 1);
+        if (UV && t >= nt) {
+            t -= nt;
+            af.in = a.in2; af.out = a.out2; af.b = a.b2; af.part = a.part2;
+        }
+        const int tr = t / h, tj = t - tr * h;
+        run = 2 * tr + (wv >> 1);
+        sj = 2 * tj + (wv & 1);
+        return run < a.nrun && sj < a.nsj;
+    }
+    const int nstr = a.nsj * a.nrun;
+    int w = t * 4 + wv;
+    if (UV && w >= nstr) {
+        w -= nstr;
+        af.in = a.in2; af.out = a.out2; af.b = a.b2; af.part = a.part2;
+    }
+    run = w / a.nsj;
+    sj = w - run * a.nsj;
+    return w < nstr;
+}
 #ifndef XR_BUF
 #define XR_BUF 0   // FUSE_R's coarse stores through buffers too (1: 172 VGPRs, 2 waves/SIMD, slower)
+#endif
+#ifndef XR_UP
+#define XR_UP 0    // FUSE_R's odd strips walk upwards too (A/B builds)
 #endif
 #ifndef XR_BF
 #define XR_BF 0    // FUSE_R with the branch-free row loop (A/B builds)
 #endif
+
+// BF_STAGE: the pipeline stages of k_sweep2 / k_sweep3 relax every row they see -- a row outside a
+// stage's range [lo, hi] is read by no row inside the next stage's range (each range is the
+// previous one shrunk by a row; the stores and the residual stage take only the strip's rows) --
+// and keep ghost rows / columns outside the domain by selects: no branch in a stage but the
+// row colour's (wave-uniform).  Bit-identical to the guarded stages (relax rounds alike in every
+// instantiation: explicit fmas)
+#ifndef BF_STAGE
+#define BF_STAGE 1
+#endif
+// a value the compiler must materialise here: a select on it stays a v_cndmask instead of
+// becoming a branch around the value's computation
+__device__ __forceinline__ double keep(double x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
 
 // one strip of k_sweep2, walked downwards (DIR = 1) or upwards (DIR = -1); returns the
 // strip's residual partial (R5)
@@ -1957,20 +2015,28 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
                     int par) -> double2 {
         double2 o = W1;
         const int gi = a.i0 + row;
-        if (gi < 0 || gi >= a.nx) return o;
-        const double* rw = rc[row - ib + RC_OFF];
+        if (!BF_STAGE && (gi < 0 || gi >= a.nx)) return o;
+        const double* rw = rc[BF_STAGE ? min(max(row - ib + RC_OFF, 0), RC_MAX - 1) : row - ib + RC_OFF];
         const double cw = rw[0], ce = rw[1];
         double rr;
+        // BF_STAGE: a ghost row or a column outside the domain keeps its value through a select
+        const bool in = !BF_STAGE || (gi >= 0 && gi < a.nx);
         // the row's colour is in one of the lane's two columns (wave-uniform): only that
         // column's diagonal, reciprocal and j-neighbour shuffle are formed
         if ((gi & 1) == par) {
             const double lf = lane_up1(W1.y);
             const double d = diag<OP>(rw[2], cd0, alpha), w = omega * rcp_nr(d);
-            if (v0) o.x = relax<OP>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr);
+            if (BF_STAGE) {
+                const double n = keep(relax<OP>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr));
+                o.x = (in && v0) ? n : W1.x;
+            } else if (v0) o.x = relax<OP>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr);
         } else {
             const double rt = lane_dn1(W1.x);
             const double d = diag<OP>(rw[2], cd1, alpha), w = omega * rcp_nr(d);
-            if (v1) o.y = relax<OP>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, d, w, alpha, rr);
+            if (BF_STAGE) {
+                const double n = keep(relax<OP>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, d, w, alpha, rr));
+                o.y = (in && v1) ? n : W1.y;
+            } else if (v1) o.y = relax<OP>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, d, w, alpha, rr);
         }
         return o;
     };
@@ -2005,17 +2071,17 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
         // (windows run oldest -> newest; half() wants rows i-1, i, i+1: swapped when DIR < 0)
         const int m = r - DIR;
         double2 n1 = P1;
-        if (m >= ib - 3 - EXT && m <= ie + 2 + EXT) n1 = DIR > 0 ? half(P0, P1, P2, B1, m, 0) : half(P2, P1, P0, B1, m, 0);
+        if (BF_STAGE || (m >= ib - 3 - EXT && m <= ie + 2 + EXT)) n1 = DIR > 0 ? half(P0, P1, P2, B1, m, 0) : half(P2, P1, P0, B1, m, 0);
         A0 = A1; A1 = A2; A2 = n1;
         // stage 2: black of sweep 1 at r-2
         double2 n2 = A1;
         const int m2 = r - 2 * DIR;
-        if (m2 >= ib - 2 - EXT && m2 <= ie + 1 + EXT) n2 = DIR > 0 ? half(A0, A1, A2, B2, m2, 1) : half(A2, A1, A0, B2, m2, 1);
+        if (BF_STAGE || (m2 >= ib - 2 - EXT && m2 <= ie + 1 + EXT)) n2 = DIR > 0 ? half(A0, A1, A2, B2, m2, 1) : half(A2, A1, A0, B2, m2, 1);
         C0 = C1; C1 = C2; C2 = n2;
         // stage 3: red of sweep 2 at r-3
         double2 n3 = C1;
         const int m3 = r - 3 * DIR;
-        if (m3 >= ib - 1 - EXT && m3 <= ie + EXT) n3 = DIR > 0 ? half(C0, C1, C2, B3, m3, 0) : half(C2, C1, C0, B3, m3, 0);
+        if (BF_STAGE || (m3 >= ib - 1 - EXT && m3 <= ie + EXT)) n3 = DIR > 0 ? half(C0, C1, C2, B3, m3, 0) : half(C2, C1, C0, B3, m3, 0);
         E0 = E1; E1 = E2; E2 = n3;
         // stage 4: black of sweep 2 at r-4, stored on the strip's rows
         const int k = r - 4 * DIR;
@@ -2026,7 +2092,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
                 if (k >= ib && k < ie && wr) st_stream(a.out + (ptrdiff_t)k * ld + c0, n4, a.nt);
             }
         } else {
-            if (k >= ib - EXT && k < ie + EXT) n4 = DIR > 0 ? half(E0, E1, E2, B4, k, 1) : half(E2, E1, E0, B4, k, 1);
+            if (BF_STAGE || (k >= ib - EXT && k < ie + EXT)) n4 = DIR > 0 ? half(E0, E1, E2, B4, k, 1) : half(E2, E1, E0, B4, k, 1);
             const unsigned off = (k >= ib && k < ie && wr) ? ((unsigned)(k - rb) * (unsigned)ld + (unsigned)c0) * 8u : OOB;
             const nsu4 d = {(unsigned)__double2loint(n4.x), (unsigned)__double2hiint(n4.x),
                             (unsigned)__double2loint(n4.y), (unsigned)__double2hiint(n4.y)};
@@ -2125,6 +2191,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
 // rows ib-7 .. ie+6, 112 written columns (SW3R), 7 ghost rows (HALO = 7: slabs too; FUSE_UV + RES is
 // the multi-rank batch end, u and v in one launch, v's partials at part2)
 constexpr int SW3R = SW2X - 4;
+
 template <int DIR, bool RES, int SD3>
 __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
                                                int lane) {
@@ -2170,25 +2237,37 @@ __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double
                     int par) -> double2 {
         double2 o = W1;
         const int gi = a.i0 + row;
-        if (gi < 0 || gi >= a.nx) return o;
-        const double* rw = rc[row - ib + RC_OFF3];
+        if (!BF_STAGE && (gi < 0 || gi >= a.nx)) return o;
+        const double* rw = rc[BF_STAGE ? min(max(row - ib + RC_OFF3, 0), RC_MAX3 - 1) : row - ib + RC_OFF3];
         const double cw = rw[0], ce = rw[1];
         double rr;
+        // BF_STAGE: no branch but the colour's: a ghost row or a column outside the domain keeps
+        // its value through a select (the relaxation is computed anyway)
+        const bool in = !BF_STAGE || (gi >= 0 && gi < a.nx);
         if ((gi & 1) == par) {
             const double lf = lane_up1(W1.y);
             const double d = diag<1>(rw[2], cd0, alpha), w = omega * rcp_nr(d);
-            if (v0) o.x = relax<1>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr);
+            if (BF_STAGE) {
+                const double n = keep(relax<1>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr));
+                o.x = (in && v0) ? n : W1.x;
+            } else if (v0) o.x = relax<1>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr);
         } else {
             const double rt = lane_dn1(W1.x);
             const double d = diag<1>(rw[2], cd1, alpha), w = omega * rcp_nr(d);
-            if (v1) o.y = relax<1>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, d, w, alpha, rr);
+            if (BF_STAGE) {
+                const double n = keep(relax<1>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, d, w, alpha, rr));
+                o.y = (in && v1) ? n : W1.y;
+            } else if (v1) o.y = relax<1>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, d, w, alpha, rr);
         }
         return o;
     };
-    // one pipeline stage: colour `par` at row m if m lies in [lo, hi] (else the value passes on)
+    // one pipeline stage: colour `par` at row m if m lies in [lo, hi] (else the value passes on).
+    // BF_STAGE: every row is relaxed -- a row outside [lo, hi] is read by no row inside the next
+    // stage's range (each stage's range is the previous one's shrunk by a row), and the stores
+    // and the residual stage take only the strip's rows
     auto stage = [&](const double2& W0, const double2& W1, const double2& W2, const double2& B, int m, int lo,
                      int hi, int par) -> double2 {
-        if (m < lo || m > hi) return W1;
+        if (!BF_STAGE && (m < lo || m > hi)) return W1;
         return DIR > 0 ? half(W0, W1, W2, B, m, par) : half(W2, W1, W0, B, m, par);
     };
     auto step = [&](double2 p, const double2 bb, int r) {
@@ -2249,30 +2328,25 @@ __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double
 template <int FUSE, bool RES = false, int SD3 = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SD3 == 3 ? 3 : 1))) void k_sweep3(StreamArgs a) {
     __shared__ double rcs[4][RC_MAX3][4];
-    const int nstr = a.nsj * a.nrun;
-    int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double (*rc)[4] = rcs[threadIdx.x >> 6];
     StreamArgs af = a;
-    if (FUSE == FUSE_UV && w >= nstr) {
-        w -= nstr;
-        af.in = a.in2; af.out = a.out2; af.b = a.b2; af.part = a.part2;
-    }
+    int run, sj;
+    const bool live = strip_of<FUSE == FUSE_UV>(a, af, run, sj);
     const int lane = threadIdx.x & 63;
-    const int run = w / a.nsj, sj = w - run * a.nsj;
     const int ib = run < a.slo ? a.rb0 + run * a.L : a.rb1 + (run - a.slo) * a.L;
     const int ie = min(ib + a.L, a.rend);
     const int si = a.pbase + run;
-    if (w < nstr) stage_rows<1, RC_OFF3>(af, rc, ib, lane);
+    if (live) stage_rows<1, RC_OFF3>(af, rc, ib, lane);
     __syncthreads();
     double res = 0.0;
-    if (w < nstr) {
+    if (live) {
         if (si & 1) res = sweep3_strip<-1, RES, SD3>(af, rc, ib, ie, sj, lane);
         else res = sweep3_strip<1, RES, SD3>(af, rc, ib, ie, sj, lane);
     }
     if (RES) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
-        if (lane == 0 && w < nstr) af.part[si * a.nsj + sj] = res;
+        if (lane == 0 && live) af.part[si * a.nsj + sj] = res;
     }
 }
 
@@ -2282,36 +2356,31 @@ __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
     constexpr bool R5 = RES || XR;                 // the fifth (output residual) stage
     __shared__ double rcs[4][RC_MAX][4];
     const int lane = threadIdx.x & 63;
-    const int nstr = a.nsj * a.nrun;
-    int w = xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double (*rc)[4] = rcs[threadIdx.x >> 6];
-    // the second field's waves (nf = 2; wave-uniform, same coefficient tables)
+    // this wave's strip (plan_strips2: the launch may cover a subset of the pass's rows) and
+    // field (FUSE_UV: the second field's workgroups take in2 / out2 / b2 / part2)
     StreamArgs af = a;
-    if (FUSE == FUSE_UV && w >= nstr) {
-        w -= nstr;
-        af.in = a.in2; af.out = a.out2; af.b = a.b2; af.part = a.part2;
-    }
-    // this wave's strip (plan_strips2: the launch may cover a subset of the pass's rows)
-    const int run = w / a.nsj, sj = w - run * a.nsj;
+    int run, sj;
+    const bool live = strip_of<FUSE == FUSE_UV>(a, af, run, sj);
     const int ib = run < a.slo ? a.rb0 + run * a.L : a.rb1 + (run - a.slo) * a.L;
     const int ie = min(ib + a.L, a.rend);
     const int si = a.pbase + run, wid = si * a.nsj + sj;
-    if (w < nstr) stage_rows<OP>(af, rc, ib, lane);
+    if (live) stage_rows<OP>(af, rc, ib, lane);
     __syncthreads();
     double res = 0.0;
-    if (w < nstr) {
+    if (live) {
         // odd strips walk upwards: the halo rows two strips share are then read by both at about
         // the same time -- an L2 hit for the second (Helmholtz pass 86.5 -> 84 us at 4096^2).
         // The restriction pass walks downwards only: upwards, its fused restriction rounds some
         // coarse sums differently, and its values would depend on how a pass is cut into strips
         // (the overlapped exchange's split, the slab height)
-        if (FUSE != FUSE_R && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1>(af, rc, ib, ie, sj, lane);
+        if ((FUSE != FUSE_R || XR_UP) && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1, ZIN>(af, rc, ib, ie, sj, lane);
         else res = sweep2_strip<OP, RES, FUSE, 1, ZIN>(af, rc, ib, ie, sj, lane);
     }
     if (R5) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
-        if (lane == 0 && w < nstr) af.part[wid] = res;
+        if (lane == 0 && live) af.part[wid] = res;
     }
 }
 
@@ -3784,6 +3853,12 @@ void set_strip_phase(int phase) { g_phase = phase; }
 // d = depth rounded up to even (the fused restriction pairs rows).  Partial slots: phase 1's
 // strip rows, then phase 2's two.  Sets a.L and the launch's strip mapping; returns the
 // pass's strip count (the same for both phases) and the launch's workgroups in *nblk.
+// workgroups of a k_sweep2 / k_sweep3 launch over nf fields (strip_of's mapping)
+static int strip_blocks(const StreamArgs& a, int nf) {
+    if (WG2X2) return nf * ((a.nsj + 1) / 2) * ((a.nrun + 1) / 2);
+    return (nf * a.nsj * a.nrun + 3) / 4;
+}
+
 static int plan_strips2(StreamArgs& a, long cap, int depth, int* nblk) {
     // strips of >= 20 rows: at 2048^2 (the first coarse level) 16 -> 20 rows is 41.9 -> 38.8 us per
     // FUSE_R pass (fewer halo rows per output row beats the extra waves); 24 / 28 measured slower
@@ -3791,17 +3866,20 @@ static int plan_strips2(StreamArgs& a, long cap, int depth, int* nblk) {
     const int d = (depth + 1) & ~1, R = a.nxl - 2 * d;
     a.pbase = 0;
     a.rb1 = 0;
+    // WG2X2: the 2 x 2 workgroups pad nsj and the strip rows to even counts; size the round for that
+    const long nsj_e = WG2X2 ? (a.nsj + 1) & ~1 : a.nsj;
+    if (WG2X2) cap = std::max(2L, (cap / nsj_e) & ~1L) * nsj_e;
     if (g_phase == 0 || R < 2) {
-        a.L = strip_rows(a.nxl, a.nsj, cap, lmin2);
+        a.L = strip_rows(a.nxl, nsj_e, cap, lmin2);
         const int n = (a.nxl + a.L - 1) / a.L;
         a.nrun = g_phase == 1 ? 0 : n;   // (a slab too thin to split: all of it after the exchange)
         a.slo = n;
         a.rb0 = 0;
         a.rend = a.nxl;
-        *nblk = (a.nsj * a.nrun + 3) / 4;
+        *nblk = strip_blocks(a, 1);
         return a.nsj * n;
     }
-    a.L = strip_rows(R, a.nsj, cap, lmin2);
+    a.L = strip_rows(R, nsj_e, cap, lmin2);
     const int n1 = (R + a.L - 1) / a.L;
     if (g_phase == 1) {
         a.nrun = a.slo = n1;
@@ -3816,7 +3894,7 @@ static int plan_strips2(StreamArgs& a, long cap, int depth, int* nblk) {
         a.rend = a.nxl;
         a.pbase = n1;
     }
-    *nblk = (a.nsj * a.nrun + 3) / 4;
+    *nblk = strip_blocks(a, 1);
     return a.nsj * (n1 + 2);
 }
 
@@ -3852,7 +3930,7 @@ static int launch_stream2(StreamArgs a, const Geo& g, hipStream_t st, bool count
     if (count_only || !nblk) return nstr;
     if constexpr (OP == 1) {
         if (a.in2) {   // two fields: the multi-rank Helmholtz pair pass
-            nblk = (2 * a.nsj * a.nrun + 3) / 4;
+            nblk = strip_blocks(a, 2);
             if (a.part) NS_LAUNCH((k_sweep2<OP, true, FUSE_UV>), dim3(nblk), dim3(256), 0, st, a);
             else NS_LAUNCH((k_sweep2<OP, false, FUSE_UV>), dim3(nblk), dim3(256), 0, st, a);
             return nstr;
@@ -3885,7 +3963,10 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
     a.ec = ec; a.ldc = gc.ld; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0; a.dsx = gc.dsx;
     // the iterate streamed non-temporally here: 113 -> 101 us at 4096^2 (b and the coarse
     // correction keep the Infinity Cache); neutral-to-worse in the other passes
-    if (a.ntl < 0) a.ntl = 1;
+#ifndef FP_NTL
+#define FP_NTL 1
+#endif
+    if (a.ntl < 0) a.ntl = FP_NTL;
     a.nsj = (g.ny + SW2X - 1) / SW2X;
     int nblk = 0;
     // overlap depth 5, not the 4 of its fine-row cone: fine row 0 (even) reads coarse row -1,
@@ -3987,7 +4068,7 @@ int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, 
         if (!nblk) return nstr;
         if (which == 3) {
             a.in2 = v; a.out2 = vo; a.b2 = rv; a.part2 = part + nstr;
-            nblk = (2 * a.nsj * a.nrun + 3) / 4;
+            nblk = strip_blocks(a, 2);
         }
         void* args[] = {&a};
         if (launch_raw(kr, dim3(nblk), dim3(256), args, 0, st) != hipSuccess) return -1;
@@ -4000,7 +4081,7 @@ int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, 
     if (!nblk) return nstr;
     if (which == 3) {
         a.in2 = v; a.out2 = vo; a.b2 = rv;
-        nblk = (2 * a.nsj * a.nrun + 3) / 4;
+        nblk = strip_blocks(a, 2);
         NS_LAUNCH(k_sweep3<FUSE_UV>, dim3(nblk), dim3(256), 0, st, a);
     } else {
         NS_LAUNCH(k_sweep3<FUSE_NONE>, dim3(nblk), dim3(256), 0, st, a);
