@@ -1921,13 +1921,53 @@ __device__ __forceinline__ double keep(double x) {
     return x;
 }
 
+// UNI: a strip whose staged rows (its own and its read cone) all share one row sum -- every strip
+// of a uniform grid but those within a cone of the top / bottom wall -- takes each lane's diagonal
+// and omega / diagonal of its two columns from registers formed once per strip, instead of per
+// stage (1 add, 1 fma, rcp + 4 fma, 1 mul).  Same expressions, so bit-identical results.
+#ifndef DIAGC
+#define DIAGC 1
+#endif
+struct DiagC {
+    double d0, d1, w0, w1;
+};
+template <int OP>
+__device__ __forceinline__ DiagC diag_cache(double rdc, double cd0, double cd1, double alpha, double omega) {
+    DiagC c;
+    c.d0 = diag<OP>(rdc, cd0, alpha);
+    c.d1 = diag<OP>(rdc, cd1, alpha);
+    c.w0 = omega * rcp_nr(c.d0);
+    c.w1 = omega * rcp_nr(c.d1);
+    return c;
+}
+// the diagonal and omega / diagonal of one column of a row (row sum rd, column sum cd)
+template <int OP, bool UNI>
+__device__ __forceinline__ void diag_w(const DiagC& c, int col, double rd, double cd, double alpha, double omega,
+                                       double& d, double& w) {
+    if (UNI) {
+        d = col ? c.d1 : c.d0;
+        w = col ? c.w1 : c.w0;
+    } else {
+        d = diag<OP>(rd, cd, alpha);
+        w = omega * rcp_nr(d);
+    }
+}
+// whether every staged row of this wave's table (n rows) has the row sum of row `mid` (UNI)
+__device__ __forceinline__ bool rows_uniform(const double (*rc)[4], int n, int mid, int lane) {
+    if (!DIAGC) return false;
+    const double r = rc[mid][2];
+    bool ok = true;
+    for (int t = lane; t < n; t += 64) ok = ok && rc[t][2] == r;
+    return __builtin_amdgcn_ballot_w64(!ok) == 0;
+}
+
 // one strip of k_sweep2, walked downwards (DIR = 1) or upwards (DIR = -1); returns the
 // strip's residual partial (R5)
 // (two instantiations: runtime window selects would cost ~50 VGPRs)
 // ZIN (FUSE_R only): the input iterate is identically zero -- a coarse level's first pass of a
 // V-cycle, whose phi the restriction above no longer stores as zeros: no phi read at all (the
 // same values as reading the zeros)
-template <int OP, bool RES, int FUSE, int DIR, bool ZIN = false>
+template <int OP, bool RES, int FUSE, int DIR, bool ZIN = false, bool UNI = false>
 __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
                                               int lane) {
     constexpr int SD2 = sd2_of<OP, RES, FUSE>();
@@ -2008,6 +2048,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     // XR: this lane's column spacings, the even row's partial sum and spacing
     const double hy0 = XR ? a.hy[k0] : 0.0, hy1 = XR ? a.hy[k1] : 0.0;
     double xs = 0.0, hxe = 0.0, ro0 = 0.0, ro1 = 0.0, hxo = 0.0;
+    const DiagC dcc = UNI ? diag_cache<OP>(rc[RC_OFF + ((ie - ib) >> 1)][2], cd0, cd1, alpha, omega) : DiagC{};
 
     // one colour update of row `row` (window W0 above, W1 the row, W2 below); colour
     // parity: update c0 when (gi + c0) % 2 == par
@@ -2025,14 +2066,16 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
         // column's diagonal, reciprocal and j-neighbour shuffle are formed
         if ((gi & 1) == par) {
             const double lf = lane_up1(W1.y);
-            const double d = diag<OP>(rw[2], cd0, alpha), w = omega * rcp_nr(d);
+            double d, w;
+            diag_w<OP, UNI>(dcc, 0, rw[2], cd0, alpha, omega, d, w);
             if (BF_STAGE) {
                 const double n = keep(relax<OP>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr));
                 o.x = (in && v0) ? n : W1.x;
             } else if (v0) o.x = relax<OP>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr);
         } else {
             const double rt = lane_dn1(W1.x);
-            const double d = diag<OP>(rw[2], cd1, alpha), w = omega * rcp_nr(d);
+            double d, w;
+            diag_w<OP, UNI>(dcc, 1, rw[2], cd1, alpha, omega, d, w);
             if (BF_STAGE) {
                 const double n = keep(relax<OP>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, d, w, alpha, rr));
                 o.y = (in && v1) ? n : W1.y;
@@ -2109,7 +2152,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
                 const double lf = lane_up1(F1.y), rt = lane_dn1(F1.x);
                 const double* rw = rc[m5 - ib + RC_OFF];
                 const double cw = rw[0], ce = rw[1], hxr = rw[3];
-                const double d0 = diag<OP>(rw[2], cd0, alpha), d1 = diag<OP>(rw[2], cd1, alpha);
+                const double d0 = UNI ? dcc.d0 : diag<OP>(rw[2], cd0, alpha), d1 = UNI ? dcc.d1 : diag<OP>(rw[2], cd1, alpha);
                 double r0, r1;
                 relax<OP>(F1.x, Fm.x, Fp.x, lf, F1.y, B5.x, cw, ce, cs0, cn0, d0, 0.0, alpha, r0);
                 relax<OP>(F1.y, Fm.y, Fp.y, F1.x, rt, B5.y, cw, ce, cs1, cn1, d1, 0.0, alpha, r1);
@@ -2192,7 +2235,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
 // the multi-rank batch end, u and v in one launch, v's partials at part2)
 constexpr int SW3R = SW2X - 4;
 
-template <int DIR, bool RES, int SD3>
+template <int DIR, bool RES, int SD3, bool UNI = false>
 __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
                                                int lane) {
     // SD3: rows in flight (round 2: 3 needed 174 VGPRs then; with the wave-uniform strip index the
@@ -2214,6 +2257,7 @@ __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double
     const int rb = __builtin_amdgcn_readfirstlane(ib - 1 - EXT);
     const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
         a.out + (ptrdiff_t)rb * ld, (short)0, (int)((unsigned)(a.L + 2 + 2 * EXT) * ld * 8u), 0x00020000);
+    const DiagC dcc = UNI ? diag_cache<1>(rc[RC_OFF3 + ((ie - ib) >> 1)][2], cd0, cd1, alpha, omega) : DiagC{};
     double2 Q[SD3], QB[SD3];
     // q rows ib-6-EXT .. ie+5+EXT and b rows ib-5-EXT .. ie+4+EXT (the first red stage's) are read
     const int r0 = ib - 6 - EXT, r1 = ie + 5 + EXT;
@@ -2246,14 +2290,16 @@ __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double
         const bool in = !BF_STAGE || (gi >= 0 && gi < a.nx);
         if ((gi & 1) == par) {
             const double lf = lane_up1(W1.y);
-            const double d = diag<1>(rw[2], cd0, alpha), w = omega * rcp_nr(d);
+            double d, w;
+            diag_w<1, UNI>(dcc, 0, rw[2], cd0, alpha, omega, d, w);
             if (BF_STAGE) {
                 const double n = keep(relax<1>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr));
                 o.x = (in && v0) ? n : W1.x;
             } else if (v0) o.x = relax<1>(W1.x, W0.x, W2.x, lf, W1.y, B.x, cw, ce, cs0, cn0, d, w, alpha, rr);
         } else {
             const double rt = lane_dn1(W1.x);
-            const double d = diag<1>(rw[2], cd1, alpha), w = omega * rcp_nr(d);
+            double d, w;
+            diag_w<1, UNI>(dcc, 1, rw[2], cd1, alpha, omega, d, w);
             if (BF_STAGE) {
                 const double n = keep(relax<1>(W1.y, W0.y, W2.y, W1.x, rt, B.y, cw, ce, cs1, cn1, d, w, alpha, rr));
                 o.y = (in && v1) ? n : W1.y;
@@ -2301,7 +2347,7 @@ __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double
                 const double lf = lane_up1(F1.y), rt = lane_dn1(F1.x);
                 const double* rw = rc[m7 - ib + RC_OFF3];
                 const double cw = rw[0], ce = rw[1];
-                const double d0 = diag<1>(rw[2], cd0, alpha), d1 = diag<1>(rw[2], cd1, alpha);
+                const double d0 = UNI ? dcc.d0 : diag<1>(rw[2], cd0, alpha), d1 = UNI ? dcc.d1 : diag<1>(rw[2], cd1, alpha);
                 double q0, q1;
                 relax<1>(F1.x, Fm.x, Fp.x, lf, F1.y, B7.x, cw, ce, cs0, cn0, d0, 0.0, alpha, q0);
                 relax<1>(F1.y, Fm.y, Fp.y, F1.x, rt, B7.y, cw, ce, cs1, cn1, d1, 0.0, alpha, q1);
@@ -2340,8 +2386,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SD3 == 3 ? 
     __syncthreads();
     double res = 0.0;
     if (live) {
-        if (si & 1) res = sweep3_strip<-1, RES, SD3>(af, rc, ib, ie, sj, lane);
-        else res = sweep3_strip<1, RES, SD3>(af, rc, ib, ie, sj, lane);
+        const bool uni = rows_uniform(rc, min(ie - ib + 2 * RC_OFF3, RC_MAX3), RC_OFF3 + ((ie - ib) >> 1), lane);
+        if (si & 1) res = uni ? sweep3_strip<-1, RES, SD3, true>(af, rc, ib, ie, sj, lane)
+                              : sweep3_strip<-1, RES, SD3>(af, rc, ib, ie, sj, lane);
+        else res = uni ? sweep3_strip<1, RES, SD3, true>(af, rc, ib, ie, sj, lane)
+                       : sweep3_strip<1, RES, SD3>(af, rc, ib, ie, sj, lane);
     }
     if (RES) {
 #pragma unroll
@@ -2374,8 +2423,13 @@ __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
         // The restriction pass walks downwards only: upwards, its fused restriction rounds some
         // coarse sums differently, and its values would depend on how a pass is cut into strips
         // (the overlapped exchange's split, the slab height)
-        if ((FUSE != FUSE_R || XR_UP) && (si & 1)) res = sweep2_strip<OP, RES, FUSE, -1, ZIN>(af, rc, ib, ie, sj, lane);
-        else res = sweep2_strip<OP, RES, FUSE, 1, ZIN>(af, rc, ib, ie, sj, lane);
+        const bool uni = rows_uniform(rc, min(ie - ib + 2 * RC_OFF, RC_MAX), RC_OFF + ((ie - ib) >> 1), lane);
+        if ((FUSE != FUSE_R || XR_UP) && (si & 1))
+            res = uni ? sweep2_strip<OP, RES, FUSE, -1, ZIN, true>(af, rc, ib, ie, sj, lane)
+                      : sweep2_strip<OP, RES, FUSE, -1, ZIN>(af, rc, ib, ie, sj, lane);
+        else
+            res = uni ? sweep2_strip<OP, RES, FUSE, 1, ZIN, true>(af, rc, ib, ie, sj, lane)
+                      : sweep2_strip<OP, RES, FUSE, 1, ZIN>(af, rc, ib, ie, sj, lane);
     }
     if (R5) {
 #pragma unroll
@@ -3337,13 +3391,14 @@ __global__ void k_fill_random(Geo g, double* phi, double* rp, uint64_t seed) {
 // out = a x + b y (+ c z) over the slab's own cells (the Poisson initial-guess extrapolation)
 __global__ __launch_bounds__(256) void k_axpby(Geo g, double a, const double* __restrict__ x, double b,
                                                const double* __restrict__ y, double c, const double* __restrict__ z,
-                                               double* __restrict__ out) {
+                                               double d, const double* __restrict__ w, double* __restrict__ out) {
     const int j = blockIdx.x * 64 + threadIdx.x;
     const int li = blockIdx.y * 4 + threadIdx.y;
     if (j >= g.ny || li >= g.nxl) return;
     const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
     double r = a * x[o] + b * y[o];
     if (z) r += c * z[o];
+    if (w) r += d * w[o];
     out[o] = r;
 }
 
@@ -4478,8 +4533,8 @@ int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st) {
     return (int)(cg.x * cg.y);
 }
 void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st,
-                  double c, const double* z) {
-    NS_LAUNCH(k_axpby, cell_grid(g), dim3(64, 4), 0, st, g, a, x, b, y, c, z, out);
+                  double c, const double* z, double d, const double* w) {
+    NS_LAUNCH(k_axpby, cell_grid(g), dim3(64, 4), 0, st, g, a, x, b, y, c, z, d, w, out);
 }
 int launch_area_sum(const Geo& g, const Coef& c, const double* b, double* part, hipStream_t st) {
     const int rows = cell_rows(g);

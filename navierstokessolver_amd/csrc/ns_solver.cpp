@@ -139,12 +139,14 @@ struct ns_solver {
     int fuse_prolong = 1;        // NSGPU_FUSED_PROLONG=0: separate k_prolong pass (A/B)
     int tile_small = 1;          // NSGPU_TILE_SMALL=0: no LDS-tiled fused passes on small levels (A/B)
     int ext_timing = 1;          // NSGPU_EXT_TIMING=0: marker events around timed launches (t_begin)
-    int phi_extrap = 2;          // Poisson initial guess: NSGPU_PHI_EXTRAP=0 phi^{n-1}, 1 linear, 2 quadratic (default)
+    int phi_extrap = 3;          // Poisson initial guess: NSGPU_PHI_EXTRAP=0 phi^{n-1}, 1 linear, 2 quadratic,
+                                 // 3 (default) cubic while the last solve took > 1 V-cycle, else quadratic
     int mg_predict = 1;          // NSGPU_MG_PREDICT=0: a residual check (host sync) after every V-cycle
     double mg_rate2 = 0.0;       // last measured per-cycle contraction of ||r||^2
     int mg_hist[4] = {-1, -1, -1, -1};   // V-cycles the last four solves converged at (first check)
     double* phim = nullptr;      // phi^{n-2} (the extrapolation's second point; rotates with PHI / TMP)
-    double* phim2 = nullptr;     // phi^{n-3} (quadratic extrapolation only)
+    double* phim2 = nullptr;     // phi^{n-3} (quadratic / cubic extrapolation)
+    double* phim3 = nullptr;     // phi^{n-4} (cubic extrapolation only)
     double* phim_mem = nullptr;  // the extra planes' allocation
     float* f32_mem = nullptr;    // fp32-field sweep planes (configs[4]), allocated on first use
     float* f32[3] = {};          // phi, its ping-pong partner, rhs_phi (rows of g.ld floats)
@@ -1643,11 +1645,34 @@ int extrapolate_phi(ns_solver* s) {
         return 0;
     }
     double* prev = s->arr[NS_ARR_PHI];
+    if (s->phi_extrap >= 3 && s->phim_valid >= 3) {
+        // cubic: 4 phi^{n-1} - 6 phi^{n-2} + 4 phi^{n-3} - phi^{n-4}, while the last multigrid solve
+        // needed more than one V-cycle (the start-up transient: 3.2 -> 2.9 V-cycles per step over
+        // steps 6-25 of the 4096^2 cavity); once one cycle suffices (developed flow) the quadratic
+        // guess does as well and reads a plane less (both keep the four-plane history)
+        if (s->mg_hist[0] >= 2)
+            nsg::launch_axpby(s->g, 4.0, prev, -6.0, s->phim, s->arr[NS_ARR_TMP], s->st, 4.0, s->phim2, -1.0, s->phim3);
+        else
+            nsg::launch_axpby(s->g, 3.0, prev, -3.0, s->phim, s->arr[NS_ARR_TMP], s->st, 1.0, s->phim2);
+        s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
+        s->arr[NS_ARR_TMP] = s->phim3;
+        s->phim3 = s->phim2;
+        s->phim2 = s->phim;
+        s->phim = prev;
+        return 0;
+    }
     if (s->phi_extrap >= 2 && s->phim_valid >= 2) {
         // 3 phi^{n-1} - 3 phi^{n-2} + phi^{n-3}
         nsg::launch_axpby(s->g, 3.0, prev, -3.0, s->phim, s->arr[NS_ARR_TMP], s->st, 1.0, s->phim2);
         s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
-        s->arr[NS_ARR_TMP] = s->phim2;
+        if (s->phi_extrap >= 3) {
+            // keep phi^{n-3} as the cubic's fourth point; the spare plane becomes scratch
+            s->arr[NS_ARR_TMP] = s->phim3;
+            s->phim3 = s->phim2;
+            s->phim_valid = 3;
+        } else {
+            s->arr[NS_ARR_TMP] = s->phim2;
+        }
         s->phim2 = s->phim;
         s->phim = prev;
         return 0;
@@ -2010,7 +2035,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_EXT_TIMING")) s->ext_timing = std::atoi(e) != 0;
-    if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(2, std::atoi(e)));
+    if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(3, std::atoi(e)));
     if (const char* e = getenv("NSGPU_MG_PREDICT")) s->mg_predict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_SPECULATE")) s->speculate = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
@@ -2121,11 +2146,12 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (hipMemsetAsync(s->base, 0, s->plane * NS_NUM_ARR * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     for (int k = 0; k < NS_NUM_ARR; k++) s->arr[k] = s->base + k * s->plane + (size_t)nsg::HALO * g.ld;
     if (s->phi_extrap) {
-        const size_t np = s->phi_extrap >= 2 ? 2 : 1;
+        const size_t np = (size_t)std::min(s->phi_extrap, 3);
         if (hipMalloc(&s->phim_mem, np * s->plane * sizeof(double)) != hipSuccess) { set_err("hipMalloc phim failed"); return fail(NS_ENOMEM); }
         if (hipMemsetAsync(s->phim_mem, 0, np * s->plane * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
         s->phim = s->phim_mem + (size_t)nsg::HALO * g.ld;
-        if (np == 2) s->phim2 = s->phim + s->plane;
+        if (np >= 2) s->phim2 = s->phim + s->plane;
+        if (np >= 3) s->phim3 = s->phim2 + s->plane;
     }
 
     if (masked) {
