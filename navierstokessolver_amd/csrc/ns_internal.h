@@ -144,9 +144,10 @@ void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t 
 void launch_finish_mean(const double* sums, double ncells, double* shift_and_bn2, hipStream_t st);
 // (sum f, sum f^2) partials over own cells
 int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st);
-// out = a x + b y (+ c z if z) (+ d w if w) over the slab's own cells
+// out = a x + b y (+ c z if z) (+ d w if w) (+ e v if v) over the slab's own cells
 void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st,
-                  double c = 0.0, const double* z = nullptr, double d = 0.0, const double* w = nullptr);
+                  double c = 0.0, const double* z = nullptr, double d = 0.0, const double* w = nullptr,
+                  double e = 0.0, const double* v = nullptr);
 // stretched grids: partials of sum_c A_c b_c, then b_c -= m / A_c with m = (sab - shift * area) / n
 // and kshift = the shift that leaves b - kshift mean-free (the Krylov solves)
 int launch_area_sum(const Geo& g, const Coef& c, const double* b, double* part, hipStream_t st);

@@ -3391,7 +3391,8 @@ __global__ void k_fill_random(Geo g, double* phi, double* rp, uint64_t seed) {
 // out = a x + b y (+ c z) over the slab's own cells (the Poisson initial-guess extrapolation)
 __global__ __launch_bounds__(256) void k_axpby(Geo g, double a, const double* __restrict__ x, double b,
                                                const double* __restrict__ y, double c, const double* __restrict__ z,
-                                               double d, const double* __restrict__ w, double* __restrict__ out) {
+                                               double d, const double* __restrict__ w, double e,
+                                               const double* __restrict__ v, double* __restrict__ out) {
     const int j = blockIdx.x * 64 + threadIdx.x;
     const int li = blockIdx.y * 4 + threadIdx.y;
     if (j >= g.ny || li >= g.nxl) return;
@@ -3399,6 +3400,7 @@ __global__ __launch_bounds__(256) void k_axpby(Geo g, double a, const double* __
     double r = a * x[o] + b * y[o];
     if (z) r += c * z[o];
     if (w) r += d * w[o];
+    if (v) r += e * v[o];
     out[o] = r;
 }
 
@@ -4533,8 +4535,8 @@ int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st) {
     return (int)(cg.x * cg.y);
 }
 void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st,
-                  double c, const double* z, double d, const double* w) {
-    NS_LAUNCH(k_axpby, cell_grid(g), dim3(64, 4), 0, st, g, a, x, b, y, c, z, d, w, out);
+                  double c, const double* z, double d, const double* w, double e, const double* v) {
+    NS_LAUNCH(k_axpby, cell_grid(g), dim3(64, 4), 0, st, g, a, x, b, y, c, z, d, w, e, v, out);
 }
 int launch_area_sum(const Geo& g, const Coef& c, const double* b, double* part, hipStream_t st) {
     const int rows = cell_rows(g);

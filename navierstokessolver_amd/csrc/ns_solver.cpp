@@ -146,7 +146,8 @@ struct ns_solver {
     int mg_hist[4] = {-1, -1, -1, -1};   // V-cycles the last four solves converged at (first check)
     double* phim = nullptr;      // phi^{n-2} (the extrapolation's second point; rotates with PHI / TMP)
     double* phim2 = nullptr;     // phi^{n-3} (quadratic / cubic extrapolation)
-    double* phim3 = nullptr;     // phi^{n-4} (cubic extrapolation only)
+    double* phim3 = nullptr;     // phi^{n-4} (cubic extrapolation)
+    double* phim4 = nullptr;     // phi^{n-5} (quartic, NSGPU_PHI_EXTRAP=4: A/B only)
     double* phim_mem = nullptr;  // the extra planes' allocation
     float* f32_mem = nullptr;    // fp32-field sweep planes (configs[4]), allocated on first use
     float* f32[3] = {};          // phi, its ping-pong partner, rhs_phi (rows of g.ld floats)
@@ -1645,6 +1646,18 @@ int extrapolate_phi(ns_solver* s) {
         return 0;
     }
     double* prev = s->arr[NS_ARR_PHI];
+    if (s->phi_extrap >= 4 && s->phim_valid >= 4) {
+        // quartic (A/B: NSGPU_PHI_EXTRAP=4): 5 phi^{n-1} - 10 phi^{n-2} + 10 phi^{n-3} - 5 phi^{n-4} + phi^{n-5}
+        nsg::launch_axpby(s->g, 5.0, prev, -10.0, s->phim, s->arr[NS_ARR_TMP], s->st, 10.0, s->phim2, -5.0, s->phim3,
+                          1.0, s->phim4);
+        s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
+        s->arr[NS_ARR_TMP] = s->phim4;
+        s->phim4 = s->phim3;
+        s->phim3 = s->phim2;
+        s->phim2 = s->phim;
+        s->phim = prev;
+        return 0;
+    }
     if (s->phi_extrap >= 3 && s->phim_valid >= 3) {
         // cubic: 4 phi^{n-1} - 6 phi^{n-2} + 4 phi^{n-3} - phi^{n-4}, while the last multigrid solve
         // needed more than one V-cycle (the start-up transient: 3.2 -> 2.9 V-cycles per step over
@@ -1655,7 +1668,13 @@ int extrapolate_phi(ns_solver* s) {
         else
             nsg::launch_axpby(s->g, 3.0, prev, -3.0, s->phim, s->arr[NS_ARR_TMP], s->st, 1.0, s->phim2);
         s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
-        s->arr[NS_ARR_TMP] = s->phim3;
+        if (s->phi_extrap >= 4) {
+            s->arr[NS_ARR_TMP] = s->phim4;
+            s->phim4 = s->phim3;
+            s->phim_valid = 4;
+        } else {
+            s->arr[NS_ARR_TMP] = s->phim3;
+        }
         s->phim3 = s->phim2;
         s->phim2 = s->phim;
         s->phim = prev;
@@ -2035,7 +2054,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_FUSED_PROLONG")) s->fuse_prolong = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_TILE_SMALL")) s->tile_small = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_EXT_TIMING")) s->ext_timing = std::atoi(e) != 0;
-    if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(3, std::atoi(e)));
+    if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(4, std::atoi(e)));
     if (const char* e = getenv("NSGPU_MG_PREDICT")) s->mg_predict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_SPECULATE")) s->speculate = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
@@ -2146,12 +2165,13 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (hipMemsetAsync(s->base, 0, s->plane * NS_NUM_ARR * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     for (int k = 0; k < NS_NUM_ARR; k++) s->arr[k] = s->base + k * s->plane + (size_t)nsg::HALO * g.ld;
     if (s->phi_extrap) {
-        const size_t np = (size_t)std::min(s->phi_extrap, 3);
+        const size_t np = (size_t)std::min(s->phi_extrap, 4);
         if (hipMalloc(&s->phim_mem, np * s->plane * sizeof(double)) != hipSuccess) { set_err("hipMalloc phim failed"); return fail(NS_ENOMEM); }
         if (hipMemsetAsync(s->phim_mem, 0, np * s->plane * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
         s->phim = s->phim_mem + (size_t)nsg::HALO * g.ld;
         if (np >= 2) s->phim2 = s->phim + s->plane;
         if (np >= 3) s->phim3 = s->phim2 + s->plane;
+        if (np >= 4) s->phim4 = s->phim3 + s->plane;
     }
 
     if (masked) {
