@@ -1930,10 +1930,15 @@ __device__ __forceinline__ double keep(double x) {
 #endif
 struct DiagC {
     double d0, d1, w0, w1;
+    double cw, ce, hx;   // the shared row coefficients (no LDS read per stage either)
 };
 template <int OP>
-__device__ __forceinline__ DiagC diag_cache(double rdc, double cd0, double cd1, double alpha, double omega) {
+__device__ __forceinline__ DiagC diag_cache(const double* rm, double cd0, double cd1, double alpha, double omega) {
     DiagC c;
+    const double rdc = rm[2];
+    c.cw = rm[0];
+    c.ce = rm[1];
+    c.hx = rm[3];
     c.d0 = diag<OP>(rdc, cd0, alpha);
     c.d1 = diag<OP>(rdc, cd1, alpha);
     c.w0 = omega * rcp_nr(c.d0);
@@ -1952,12 +1957,13 @@ __device__ __forceinline__ void diag_w(const DiagC& c, int col, double rd, doubl
         w = omega * rcp_nr(d);
     }
 }
-// whether every staged row of this wave's table (n rows) has the row sum of row `mid` (UNI)
+// whether every staged row of this wave's table (n rows) has the coefficients (weights, row sum,
+// spacing) of row `mid` (UNI)
 __device__ __forceinline__ bool rows_uniform(const double (*rc)[4], int n, int mid, int lane) {
     if (!DIAGC) return false;
-    const double r = rc[mid][2];
     bool ok = true;
-    for (int t = lane; t < n; t += 64) ok = ok && rc[t][2] == r;
+    for (int t = lane; t < n; t += 64)
+        ok = ok && rc[t][0] == rc[mid][0] && rc[t][1] == rc[mid][1] && rc[t][2] == rc[mid][2] && rc[t][3] == rc[mid][3];
     return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
@@ -2048,7 +2054,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     // XR: this lane's column spacings, the even row's partial sum and spacing
     const double hy0 = XR ? a.hy[k0] : 0.0, hy1 = XR ? a.hy[k1] : 0.0;
     double xs = 0.0, hxe = 0.0, ro0 = 0.0, ro1 = 0.0, hxo = 0.0;
-    const DiagC dcc = UNI ? diag_cache<OP>(rc[RC_OFF + ((ie - ib) >> 1)][2], cd0, cd1, alpha, omega) : DiagC{};
+    const DiagC dcc = UNI ? diag_cache<OP>(rc[RC_OFF + ((ie - ib) >> 1)], cd0, cd1, alpha, omega) : DiagC{};
 
     // one colour update of row `row` (window W0 above, W1 the row, W2 below); colour
     // parity: update c0 when (gi + c0) % 2 == par
@@ -2058,7 +2064,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
         const int gi = a.i0 + row;
         if (!BF_STAGE && (gi < 0 || gi >= a.nx)) return o;
         const double* rw = rc[BF_STAGE ? min(max(row - ib + RC_OFF, 0), RC_MAX - 1) : row - ib + RC_OFF];
-        const double cw = rw[0], ce = rw[1];
+        const double cw = UNI ? dcc.cw : rw[0], ce = UNI ? dcc.ce : rw[1];
         double rr;
         // BF_STAGE: a ghost row or a column outside the domain keeps its value through a select
         const bool in = !BF_STAGE || (gi >= 0 && gi < a.nx);
@@ -2151,7 +2157,7 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
             if (m5 >= ib && m5 < ie) {
                 const double lf = lane_up1(F1.y), rt = lane_dn1(F1.x);
                 const double* rw = rc[m5 - ib + RC_OFF];
-                const double cw = rw[0], ce = rw[1], hxr = rw[3];
+                const double cw = UNI ? dcc.cw : rw[0], ce = UNI ? dcc.ce : rw[1], hxr = UNI ? dcc.hx : rw[3];
                 const double d0 = UNI ? dcc.d0 : diag<OP>(rw[2], cd0, alpha), d1 = UNI ? dcc.d1 : diag<OP>(rw[2], cd1, alpha);
                 double r0, r1;
                 relax<OP>(F1.x, Fm.x, Fp.x, lf, F1.y, B5.x, cw, ce, cs0, cn0, d0, 0.0, alpha, r0);
@@ -2257,7 +2263,7 @@ __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double
     const int rb = __builtin_amdgcn_readfirstlane(ib - 1 - EXT);
     const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
         a.out + (ptrdiff_t)rb * ld, (short)0, (int)((unsigned)(a.L + 2 + 2 * EXT) * ld * 8u), 0x00020000);
-    const DiagC dcc = UNI ? diag_cache<1>(rc[RC_OFF3 + ((ie - ib) >> 1)][2], cd0, cd1, alpha, omega) : DiagC{};
+    const DiagC dcc = UNI ? diag_cache<1>(rc[RC_OFF3 + ((ie - ib) >> 1)], cd0, cd1, alpha, omega) : DiagC{};
     double2 Q[SD3], QB[SD3];
     // q rows ib-6-EXT .. ie+5+EXT and b rows ib-5-EXT .. ie+4+EXT (the first red stage's) are read
     const int r0 = ib - 6 - EXT, r1 = ie + 5 + EXT;
@@ -2283,7 +2289,7 @@ __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double
         const int gi = a.i0 + row;
         if (!BF_STAGE && (gi < 0 || gi >= a.nx)) return o;
         const double* rw = rc[BF_STAGE ? min(max(row - ib + RC_OFF3, 0), RC_MAX3 - 1) : row - ib + RC_OFF3];
-        const double cw = rw[0], ce = rw[1];
+        const double cw = UNI ? dcc.cw : rw[0], ce = UNI ? dcc.ce : rw[1];
         double rr;
         // BF_STAGE: no branch but the colour's: a ghost row or a column outside the domain keeps
         // its value through a select (the relaxation is computed anyway)
@@ -2346,7 +2352,7 @@ __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double
             if (m7 >= ib && m7 < ie) {
                 const double lf = lane_up1(F1.y), rt = lane_dn1(F1.x);
                 const double* rw = rc[m7 - ib + RC_OFF3];
-                const double cw = rw[0], ce = rw[1];
+                const double cw = UNI ? dcc.cw : rw[0], ce = UNI ? dcc.ce : rw[1];
                 const double d0 = UNI ? dcc.d0 : diag<1>(rw[2], cd0, alpha), d1 = UNI ? dcc.d1 : diag<1>(rw[2], cd1, alpha);
                 double q0, q1;
                 relax<1>(F1.x, Fm.x, Fp.x, lf, F1.y, B7.x, cw, ce, cs0, cn0, d0, 0.0, alpha, q0);
