@@ -33,10 +33,11 @@
 extern "C" {
 #endif
 
-#define NSGPU_ABI_VERSION 4   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
+#define NSGPU_ABI_VERSION 5   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
                                  3: ns_get/set_fields in compact-id order on polygons, ns_local_cells;
                                  4: NS_POISSON_MG is 0, so a zero-initialised ns_params selects the
-                                    multigrid (RB-SOR moved to 3; the value 2 is rejected) */
+                                    multigrid (RB-SOR moved to 3; the value 2 is rejected);
+                                 5: ns_stats.x_link_bytes appended */
 
 typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm */
 
@@ -138,6 +139,9 @@ typedef struct ns_stats {
     int32_t n_helm_kernels;          /* number of those passes timed */
     int32_t n_exchanges;             /* ghost-row exchange groups of the step (multi-rank / loopback) */
     int32_t n_allreduces;            /* all-reduces of the step (multi-rank / loopback) */
+    double  x_link_bytes;            /* bytes this rank sends over its busiest peer link in the step
+                                      * (one side's ghost rows of every exchange + its slab of every
+                                      * agglomeration gather; multi-rank / loopback) */
 } ns_stats;
 
 /* device arrays addressable by ns_get_array / ns_set_array */

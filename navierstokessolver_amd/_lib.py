@@ -66,7 +66,8 @@ class NsStats(ctypes.Structure):
                 ("n_poisson_kernels", ctypes.c_int32), ("n_checks", ctypes.c_int32),
                 ("t_restrict_kernel_ms", ctypes.c_double), ("n_restrict_kernels", ctypes.c_int32),
                 ("t_helm_kernel_ms", ctypes.c_double), ("n_helm_kernels", ctypes.c_int32),
-                ("n_exchanges", ctypes.c_int32), ("n_allreduces", ctypes.c_int32)]
+                ("n_exchanges", ctypes.c_int32), ("n_allreduces", ctypes.c_int32),
+                ("x_link_bytes", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

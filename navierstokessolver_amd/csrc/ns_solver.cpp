@@ -225,6 +225,7 @@ struct ns_solver {
     size_t replay_k = 0;
     int rp_h = 0, rp_c = -1;        // this step's replayed counts (0 / -1: converge normally)
     int n_xchg = 0, n_allred = 0;   // exchange groups / all-reduces issued in the current step
+    double x_link = 0.0;            // bytes over this rank's busiest peer link in the current step
     // speculative CorrectVelocities: inside a time step, the multigrid's residual check that
     // the cycle history predicts to pass enqueues K5 (into the ping-pong partners, with its
     // min/max) BEFORE the host waits for the residual, so the GPU works through the host round
@@ -266,6 +267,7 @@ int halo_rccl(ns_solver* s, const HaloReq* reqs, int nreq, hipStream_t xs) {
         const int ld = q.g->ld, nxl = q.g->nxl;
         double* f = q.f;
         const double *flo = self ? f - (ptrdiff_t)q.w * ld : f, *fhi = f + (ptrdiff_t)(self ? nxl : nxl - q.w) * ld;
+        s->x_link += 8.0 * (double)cnt;   // (each side is its own link)
         if (lo) {
             NCCLCHK(ncclSend(flo, cnt, ncclDouble, p_lo, s->comm, xs));
             NCCLCHK(ncclRecv(f - (ptrdiff_t)q.w * ld, cnt, ncclDouble, p_lo, s->comm, xs));
@@ -970,10 +972,12 @@ int gather_level(ns_solver* s, MgLevel& C) {
         if (s->loopback) {   // virtual slab: the same messages, every peer this process
             const size_t cnt = (size_t)std::min(C.sn[q], C.gs.nxl) * ld;
             NCCLCHK(ncclSend(C.b + (ptrdiff_t)C.gs.i0 * ld, cnt, ncclDouble, 0, s->comm, s->st));
+            if (q == (s->rank == 0 ? 1 : 0)) s->x_link += 8.0 * (double)C.gs.nxl * ld;
             NCCLCHK(ncclRecv(C.b + (ptrdiff_t)C.si0[q] * ld, cnt, ncclDouble, 0, s->comm, s->st));
             continue;
         }
         NCCLCHK(ncclSend(C.b + (ptrdiff_t)C.gs.i0 * ld, (size_t)C.gs.nxl * ld, ncclDouble, q, s->comm, s->st));
+        if (q == (s->rank == 0 ? 1 : 0)) s->x_link += 8.0 * (double)C.gs.nxl * ld;   // (one link per peer)
         NCCLCHK(ncclRecv(C.b + (ptrdiff_t)C.si0[q] * ld, (size_t)C.sn[q] * ld, ncclDouble, q, s->comm, s->st));
     }
     NCCLCHK(ncclGroupEnd());
@@ -2322,6 +2326,7 @@ void ns_destroy(ns_solver* s) {
 static int step_body_(ns_solver* s, ns_stats& st);
 static int step_body(ns_solver* s, ns_stats& st) {
     s->n_xchg = s->n_allred = 0;
+    s->x_link = 0.0;
     s->k5_spec = 0;
     if (!s->replay.empty()) {
         const auto& r = s->replay[s->replay_k++ % s->replay.size()];
@@ -2333,6 +2338,7 @@ static int step_body(ns_solver* s, ns_stats& st) {
     s->in_step = 0;
     st.n_exchanges = s->n_xchg;
     st.n_allreduces = s->n_allred;
+    st.x_link_bytes = s->x_link;
     return rc;
 }
 

@@ -62,7 +62,8 @@ def run(n, P, warmup, steps, re, replay=None, ny=None):
             "vcycles_per_step": sum(s["it_phi"] for s in st) / steps,
             "helm_sweeps_per_step": sum(s["it_u"] for s in st) / steps,
             "exchanges_per_step": sum(s["n_exchanges"] for s in st) / steps,
-            "allreduces_per_step": sum(s["n_allreduces"] for s in st) / steps}
+            "allreduces_per_step": sum(s["n_allreduces"] for s in st) / steps,
+            "link_mb_per_step": sum(s.get("x_link_bytes", 0.0) for s in st) / steps / 1e6}
 
 
 def main():
@@ -79,6 +80,10 @@ def main():
                     help="assumed exposed cost of one ghost-row exchange group beyond the self-copy measured "
                          "here (64 KB per row per side over one 153 GB/s-class xGMI link, overlapped with the "
                          "interior strips)")
+    ap.add_argument("--link-gbs", type=float, default=50.0,
+                    help="assumed sustained one-direction bandwidth of one GPU-to-GPU xGMI link (GB/s): the "
+                         "upper projection adds every byte the rank sends over its busiest link (ghost rows "
+                         "and agglomeration gathers, ns_stats.x_link_bytes) as exposed transfer time")
     ap.add_argument("--weak-rows", type=int, default=0, help="weak scaling: rows per rank (grid (W P) x ny)")
     ap.add_argument("--ny", type=int, default=0, help="columns of the weak-scaling grid (default --n)")
     a = ap.parse_args()
@@ -115,14 +120,20 @@ def main():
         extra = 0.0 if P == 1 else (r["allreduces_per_step"] * a.allreduce_us + r["exchanges_per_step"] * a.exchange_us) * 1e-3
         r["projected_ms_per_step"] = r["ms_per_step"] + extra
         r["projected_mlups"] = a.n * a.n / (r["projected_ms_per_step"] * 1e-3) / 1e6
+        # upper bound: every link byte exposed at --link-gbs (no overlap with the interior strips)
+        r["projected_ms_per_step_link"] = r["projected_ms_per_step"] + (0.0 if P == 1 else r["link_mb_per_step"] / a.link_gbs)
         rows.append(r)
         print(json.dumps(r), flush=True)
     base = rows[0]["projected_ms_per_step"] if rows and rows[0]["P"] == 1 else None
     if base:
         for r in rows:
             r["projected_speedup"] = base / r["projected_ms_per_step"]
-        print(json.dumps({"n": a.n, "assumptions": {"allreduce_us": a.allreduce_us, "exchange_us": a.exchange_us},
-                          "speedup": {r["P"]: round(r["projected_speedup"], 2) for r in rows}}), flush=True)
+            r["projected_speedup_link"] = base / r["projected_ms_per_step_link"]
+        print(json.dumps({"n": a.n, "assumptions": {"allreduce_us": a.allreduce_us, "exchange_us": a.exchange_us,
+                                                    "link_gbs": a.link_gbs},
+                          "speedup": {r["P"]: round(r["projected_speedup"], 2) for r in rows},
+                          "speedup_link_bytes_exposed": {r["P"]: round(r["projected_speedup_link"], 2) for r in rows}}),
+              flush=True)
 
 
 if __name__ == "__main__":
