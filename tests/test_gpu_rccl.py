@@ -46,7 +46,8 @@ def test_rccl_loopback_step_equals_single_rank(gpu, monkeypatch, case):
     overlap = case != "cavity_mg_no_overlap"
     a = run(gpu, monkeypatch, grid, dt, re, 4, False)
     b = run(gpu, monkeypatch, grid, dt, re, 4, True, overlap=overlap)
-    assert all(s["n_exchanges"] == 0 and s["n_allreduces"] == 0 for s in a[3])
+    assert all(s["n_exchanges"] == 0 and s["n_allreduces"] == 0 and s["x_link_bytes"] == 0 for s in a[3])
+    assert all(s["x_link_bytes"] > 0 for s in b[3])
     assert all(s["n_exchanges"] > 0 and s["n_allreduces"] > 0 for s in b[3]), [
         (s["n_exchanges"], s["n_allreduces"]) for s in b[3]]
     assert counts(a[3]) == counts(b[3])
@@ -72,6 +73,9 @@ def test_virtual_slab_replays_counts(gpu, monkeypatch):
     gs.close()
     assert [(s["it_u"], s["it_phi"]) for s in st] == [(4, 2), (6, 3), (4, 2), (6, 3)]
     assert all(s["n_exchanges"] > 0 and s["n_allreduces"] > 0 for s in st)
+    # ns_stats.x_link_bytes (ABI 5): at least this rank's slab of the replicated 256^2 level per
+    # V-cycle (the agglomeration gather: 64 of its rows) plus ghost rows
+    assert all(s["x_link_bytes"] >= s["it_phi"] * (n // 8) * (n // 2) * 8 for s in st), [s["x_link_bytes"] for s in st]
     assert np.all(np.isfinite(u)) and np.all(np.isfinite(v)) and u.shape == (n // 4, n)
     monkeypatch.delenv("NSGPU_VIRTUAL_ITERS")
     with pytest.raises(gpu.NsError):   # a virtual slab without replayed counts would never converge
