@@ -3395,6 +3395,9 @@ __global__ void k_fill_random(Geo g, double* phi, double* rp, uint64_t seed) {
 }
 
 // out = a x + b y (+ c z) over the slab's own cells (the Poisson initial-guess extrapolation)
+#ifndef AXPBY_NT
+#define AXPBY_NT 1
+#endif
 // (rows are ld = a multiple of 128 doubles long: each thread takes an aligned pair of columns,
 // 16-B loads, non-temporal 16-B stores -- the extrapolated guess is read once, by the next solve's
 // first pass)
@@ -3412,7 +3415,7 @@ __global__ __launch_bounds__(256) void k_axpby(Geo g, double a, const double* __
     if (z) { const double2 t = ld2(z); r.x += c * t.x; r.y += c * t.y; }
     if (w) { const double2 t = ld2(w); r.x += d * t.x; r.y += d * t.y; }
     if (v) { const double2 t = ld2(v); r.x += e * t.x; r.y += e * t.y; }
-    if (j + 1 < g.ny) st_stream(out + o, r, true);
+    if (j + 1 < g.ny) st_stream(out + o, r, AXPBY_NT);
     else out[o] = r.x;   // (an odd ny's last column: column ny is row padding, left untouched)
 }
 
