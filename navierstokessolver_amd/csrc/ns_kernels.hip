@@ -3395,28 +3395,21 @@ __global__ void k_fill_random(Geo g, double* phi, double* rp, uint64_t seed) {
 }
 
 // out = a x + b y (+ c z) over the slab's own cells (the Poisson initial-guess extrapolation)
-#ifndef AXPBY_NT
-#define AXPBY_NT 1
-#endif
-// (rows are ld = a multiple of 128 doubles long: each thread takes an aligned pair of columns,
-// 16-B loads, non-temporal 16-B stores -- the extrapolated guess is read once, by the next solve's
-// first pass)
 __global__ __launch_bounds__(256) void k_axpby(Geo g, double a, const double* __restrict__ x, double b,
                                                const double* __restrict__ y, double c, const double* __restrict__ z,
                                                double d, const double* __restrict__ w, double e,
                                                const double* __restrict__ v, double* __restrict__ out) {
-    const int j = 2 * (blockIdx.x * 64 + threadIdx.x);
+    // (one column per thread: 103.8 us per cubic guess at 4096^2 against 105.3 with 16-B loads and
+    // stores and 110.5 with non-temporal 16-B stores, kernel traces gpurun_out/ab_trace)
+    const int j = blockIdx.x * 64 + threadIdx.x;
     const int li = blockIdx.y * 4 + threadIdx.y;
     if (j >= g.ny || li >= g.nxl) return;
     const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
-    auto ld2 = [&](const double* p) { return *reinterpret_cast<const double2*>(p + o); };
-    const double2 xx = ld2(x), yy = ld2(y);
-    double2 r = make_double2(a * xx.x + b * yy.x, a * xx.y + b * yy.y);
-    if (z) { const double2 t = ld2(z); r.x += c * t.x; r.y += c * t.y; }
-    if (w) { const double2 t = ld2(w); r.x += d * t.x; r.y += d * t.y; }
-    if (v) { const double2 t = ld2(v); r.x += e * t.x; r.y += e * t.y; }
-    if (j + 1 < g.ny) st_stream(out + o, r, AXPBY_NT);
-    else out[o] = r.x;   // (an odd ny's last column: column ny is row padding, left untouched)
+    double r = a * x[o] + b * y[o];
+    if (z) r += c * z[o];
+    if (w) r += d * w[o];
+    if (v) r += e * v[o];
+    out[o] = r;
 }
 
 // ------------------------------------------------ NEUMANN outflow: BiCGStab pieces
@@ -4551,7 +4544,7 @@ int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st) {
 }
 void launch_axpby(const Geo& g, double a, const double* x, double b, const double* y, double* out, hipStream_t st,
                   double c, const double* z, double d, const double* w, double e, const double* v) {
-    NS_LAUNCH(k_axpby, dim3((g.ny + 127) / 128, (g.nxl + 3) / 4), dim3(64, 4), 0, st, g, a, x, b, y, c, z, d, w, e, v, out);
+    NS_LAUNCH(k_axpby, cell_grid(g), dim3(64, 4), 0, st, g, a, x, b, y, c, z, d, w, e, v, out);
 }
 int launch_area_sum(const Geo& g, const Coef& c, const double* b, double* part, hipStream_t st) {
     const int rows = cell_rows(g);
