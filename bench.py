@@ -43,7 +43,8 @@ KERNELS = {
     "restrict": ("k_sweep2<Poisson, FUSE_R> (finest pre-smoothing pass: 2 RB sweeps + residual + restriction)", 28),
     "prolong": ("k_sweep2<Poisson, FUSE_P> (finest post-smoothing pass: prolongation + 2 RB sweeps + output residual)", 26),
     "helmholtz": ("Helmholtz pass of one velocity component of (I - a L_V) u* = RHS (k_sweep3 + residual stage: "
-                  "3 RB-SOR sweeps, after the wall bands; or k_sweep2: 2 sweeps)", 24),
+                  "3 RB-SOR sweeps, after the wall bands; or k_sweep2: 2 sweeps; the one-rank two-field "
+                  "k_sweep3<FUSE_UV> launch counts as two component passes)", 24),
 }
 JACOBI_LABEL = "k_jacobi_s<double> (one weighted-Jacobi sweep of the Poisson operator, the north star's roofline kernel)"
 SWEEP_BYTES_PER_CELL = 24

@@ -1030,10 +1030,11 @@ struct DiagCache {
 constexpr int RC_OFF = 5;            // table row of strip row ib
 constexpr int RC_MAX = 64 + 2 * RC_OFF;  // L <= 64
 constexpr int RC_OFF3 = 6;           // k_sweep3: its first stage reads rows ib-5 .. ie+4 (ib-6 .. ie+5 with RES)
-constexpr int RC_MAX3 = 64 + 2 * RC_OFF3;
-template <int OP, int RCO = RC_OFF>
+constexpr int L3_MAX = 128;          // k_sweep3's longest strip (the two-field pass: one resident round)
+constexpr int RC_MAX3 = L3_MAX + 2 * RC_OFF3;
+template <int OP, int RCO = RC_OFF, int LMAX = 64>
 __device__ __forceinline__ void stage_rows(const StreamArgs& a, double (*rc)[4], int ib, int lane) {
-    for (int t = lane; t < a.L + 2 * RCO && t < 64 + 2 * RCO; t += 64) {
+    for (int t = lane; t < a.L + 2 * RCO && t < LMAX + 2 * RCO; t += 64) {
         const int gi = min(max(a.i0 + ib - RCO + t, 0), a.nx - 1);
         const double cw = a.cw[gi], ce = a.ce[gi];
         rc[t][0] = cw;
@@ -2388,7 +2389,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SD3 == 3 ? 
     const int ib = run < a.slo ? a.rb0 + run * a.L : a.rb1 + (run - a.slo) * a.L;
     const int ie = min(ib + a.L, a.rend);
     const int si = a.pbase + run;
-    if (live) stage_rows<1, RC_OFF3>(af, rc, ib, lane);
+    if (live) stage_rows<1, RC_OFF3, L3_MAX>(af, rc, ib, lane);
     __syncthreads();
     double res = 0.0;
     if (live) {
@@ -3650,7 +3651,7 @@ static hipError_t launch_raw(const void* k, dim3 grid, dim3 block, void** args, 
 }
 
 static long resident_waves(const void* k);
-static int strip_rows(int nxl, long nsj, long cap, int lmin);
+static int strip_rows(int nxl, long nsj, long cap, int lmin, int lmax = 64);
 
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
                const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st) {
@@ -3877,12 +3878,12 @@ static long resident_waves(const void* k) {
 // traffic) such that every strip is resident in ONE round -- a second, partial round of
 // the same length runs with the chip mostly idle.  lmin: below it the halo re-reads
 // dominate (coarse multigrid levels are latency-bound and want short strips).
-static int strip_rows(int nxl, long nsj, long cap, int lmin) {
+static int strip_rows(int nxl, long nsj, long cap, int lmin, int lmax) {
     if (g_strip_rows) return g_strip_rows;
     const long nsi = std::max(1L, cap / nsj);
     int L = (int)((nxl + nsi - 1) / nsi);
     L = (L + 1) & ~1;
-    return std::min(std::max(L, lmin), 64);
+    return std::min(std::max(L, lmin), lmax);
 }
 
 static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, double* out, const double* b,
@@ -3924,7 +3925,7 @@ static int strip_blocks(const StreamArgs& a, int nf) {
     return (nf * a.nsj * a.nrun + 3) / 4;
 }
 
-static int plan_strips2(StreamArgs& a, long cap, int depth, int* nblk) {
+static int plan_strips2(StreamArgs& a, long cap, int depth, int* nblk, int lmax = 64) {
     // strips of >= 20 rows: at 2048^2 (the first coarse level) 16 -> 20 rows is 41.9 -> 38.8 us per
     // FUSE_R pass (fewer halo rows per output row beats the extra waves); 24 / 28 measured slower
     constexpr int lmin2 = 20;
@@ -3935,7 +3936,7 @@ static int plan_strips2(StreamArgs& a, long cap, int depth, int* nblk) {
     const long nsj_e = WG2X2 ? (a.nsj + 1) & ~1 : a.nsj;
     if (WG2X2) cap = std::max(2L, (cap / nsj_e) & ~1L) * nsj_e;
     if (g_phase == 0 || R < 2) {
-        a.L = strip_rows(a.nxl, nsj_e, cap, lmin2);
+        a.L = strip_rows(a.nxl, nsj_e, cap, lmin2, lmax);
         const int n = (a.nxl + a.L - 1) / a.L;
         a.nrun = g_phase == 1 ? 0 : n;   // (a slab too thin to split: all of it after the exchange)
         a.slo = n;
@@ -3944,7 +3945,7 @@ static int plan_strips2(StreamArgs& a, long cap, int depth, int* nblk) {
         *nblk = strip_blocks(a, 1);
         return a.nsj * n;
     }
-    a.L = strip_rows(R, nsj_e, cap, lmin2);
+    a.L = strip_rows(R, nsj_e, cap, lmin2, lmax);
     const int n1 = (R + a.L - 1) / a.L;
     if (g_phase == 1) {
         a.nrun = a.slo = n1;
@@ -4128,7 +4129,8 @@ int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, 
         int nblk = 0;
         const void* kr = which == 3 ? (sd3 == 3 ? (const void*)k_sweep3<FUSE_UV, true, 3> : (const void*)k_sweep3<FUSE_UV, true, 2>)
                                     : (sd3 == 3 ? (const void*)k_sweep3<FUSE_NONE, true, 3> : (const void*)k_sweep3<FUSE_NONE, true, 2>);
-        const int nstr = plan_strips2(a, resident_waves(kr), 7, &nblk);
+        // (two fields: half the resident round per field, strips up to L3_MAX rows)
+        const int nstr = plan_strips2(a, resident_waves(kr) / (which == 3 ? 2 : 1), 7, &nblk, L3_MAX);
         if (which == 2) a.part = part + nstr;   // partials: u at [0, n), v at [n, 2n) (launch_helm_sweep2)
         if (!nblk) return nstr;
         if (which == 3) {
@@ -4142,7 +4144,7 @@ int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, 
     a.nsj = (g.ny + SW2X - 1) / SW2X;
     const void* k = which == 3 ? (const void*)k_sweep3<FUSE_UV> : (const void*)k_sweep3<FUSE_NONE>;
     int nblk = 0;
-    const int nstr = plan_strips2(a, resident_waves(k), 6, &nblk);
+    const int nstr = plan_strips2(a, resident_waves(k) / (which == 3 ? 2 : 1), 6, &nblk, L3_MAX);
     if (!nblk) return nstr;
     if (which == 3) {
         a.in2 = v; a.out2 = vo; a.b2 = rv;

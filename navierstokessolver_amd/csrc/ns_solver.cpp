@@ -125,6 +125,7 @@ struct ns_solver {
     std::vector<char> evtag;     // per pair: 0 = sweep / prolongation pass, 1 = restriction pass
     std::vector<hipEvent_t> hev; // Helmholtz pass timing events (pairs; timing == 1, single rank)
     int hn = 0;                  // Helmholtz pairs recorded this step
+    std::vector<int> hcomp;      // components per recorded Helmholtz launch (2: the one-rank two-field pass)
     int helm_batch0 = 4, pois_batch0 = 8;
     int helm_next = 4;           // first Helmholtz batch of the next step (adaptive unless check_every)
     int helm_adapt = 1;
@@ -133,6 +134,7 @@ struct ns_solver {
     bool helm_band = true;       // Helmholtz: wall-band relaxation before the global passes (k_helm_band)
     int band_w = 128, band_sweeps = 6;   // its width (cells from a wall: min(nx, ny) / 32) and RB-SOR sweeps (a multiple of 3)
     bool sweep3_res = true;      // one rank: a Helmholtz batch may end on a 3-sweep pass with its residual
+    int helm_uv = 1;             // NSGPU_HELM_UV=0: one rank's 3-sweep batch as two one-field launches (A/B)
     int helm_probe = 0;          // steps since the Helmholtz first-pass residual was last sampled
     int tiled = 0;               // NSGPU_SWEEP=tiled: A/B against the first (LDS-tiled) sweep kernels
     int fuse_restrict = 1;       // NSGPU_FUSED_RESTRICT=0: separate k_restrict pass (A/B)
@@ -471,7 +473,8 @@ int helm_sweep3(ns_solver* s, double alpha, int which, double* part = nullptr) {
     if (nb < 0) return nb;
     if (t) {
         if (t_end(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]) != 0) return -1;
-        s->hn++;
+        if (s->hcomp.size() <= (size_t)s->hn) s->hcomp.resize(s->hn + 8, 1);
+        s->hcomp[s->hn++] = 1;
     }
     if (which & 1) std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
     if (which & 2) std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
@@ -496,7 +499,8 @@ int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3) {
                                            s->arr[NS_ARR_RV], part, s->st, which);
     if (t) {
         if (t_end(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]) != 0) return -1;
-        s->hn++;
+        if (s->hcomp.size() <= (size_t)s->hn) s->hcomp.resize(s->hn + 8, 1);
+        s->hcomp[s->hn++] = 1;
     }
     if (which & 1) std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
     if (which & 2) std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
@@ -514,7 +518,10 @@ int helm_sweep2(ns_solver* s, double alpha, double* part, int which = 3) {
 int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* part_last, int* nb_first,
                 int* first_at, int* last_at) {
     int nb = 0;
-    const bool split = s->nranks == 1;
+    // one rank: u's passes, then v's -- or, with helm_uv, a batch of a single 3-sweep residual pass
+    // per component as ONE two-field launch (each field's strips twice as long: one resident round)
+    const bool split = s->nranks == 1 && !(s->helm_uv && n == 3 && s->sweep3 && s->triple && s->sweep3_res &&
+                                          !part_first && !s->tiled);
     for (int which : {split ? 1 : 3, split ? 2 : 0}) {
         if (!which) break;
         int k = 0, launch = 0;
@@ -545,6 +552,17 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                                       {&s->g, s->arr[NS_ARR_RU], 6}, {&s->g, s->arr[NS_ARR_RV], 6}};
                 const int nr = s->helm_b_pend ? 4 : 2;
                 s->helm_b_pend = 0;
+                // (one rank: the two-field residual pass is HIP-event timed as two component passes)
+                const bool t2 = s->nranks == 1 && s->timing && part && w == 3;
+                if (t2) {
+                    if (s->hev.size() < 2 * (size_t)(s->hn + 1)) {
+                        const size_t old = s->hev.size();
+                        s->hev.resize(2 * (size_t)(s->hn + 8));
+                        for (size_t q = old; q < s->hev.size(); q++)
+                            if (hipEventCreate(&s->hev[q]) != hipSuccess) { set_err("hipEventCreate failed"); return -1; }
+                    }
+                    CHK(t_begin(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]));
+                }
                 nb = overlapped(s, r, nr, [&]() {
                     if (w == 3)
                         return nsg::launch_helm_sweep3(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
@@ -555,6 +573,11 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                                                    s->arr[NS_ARR_RV], part, s->st, 3);
                 });
                 if (nb < 0) return nb;
+                if (t2) {
+                    CHK(t_end(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]));
+                    if (s->hcomp.size() <= (size_t)s->hn) s->hcomp.resize(s->hn + 8, 1);
+                    s->hcomp[s->hn++] = 2;
+                }
                 std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
                 std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
             } else {
@@ -2050,6 +2073,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_BAND_W")) s->band_w = std::max(1, std::atoi(e));   // A/B: band width
     if (const char* e = getenv("NSGPU_BAND_SWEEPS")) s->band_sweeps = std::max(3, std::atoi(e) / 3 * 3);
     if (const char* e = getenv("NSGPU_SWEEP3_RES")) s->sweep3_res = std::atoi(e) != 0;   // A/B: batches end on pairs
+    if (const char* e = getenv("NSGPU_HELM_UV")) s->helm_uv = std::atoi(e);
     // the 3-sweep pass reads HALO ghost rows, which one neighbour feeds only from slabs of
     // >= 2*HALO rows; thinner slabs (the thinnest of all ranks: a global decision) take the
     // same sweeps as a single sweep + pairs
@@ -2360,7 +2384,7 @@ static int step_body_(ns_solver* s, ns_stats& st) {
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, s->hev[2 * k], s->hev[2 * k + 1]));
         st.t_helm_kernel_ms += ms;
-        st.n_helm_kernels++;
+        st.n_helm_kernels += (size_t)k < s->hcomp.size() ? s->hcomp[k] : 1;   // (per component: 24 B/cell)
     }
     s->hn = 0;
     CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
