@@ -477,6 +477,28 @@ def test_helm_band_cuts_sweeps(gpu, monkeypatch):
         assert np.max(np.abs(a - b)) <= 1e-8
 
 
+@pytest.mark.parametrize("n", [2048, 4096])
+def test_two_field_helmholtz_pass_is_bit_identical(gpu, monkeypatch, n):
+    """One rank runs a Helmholtz batch of one 3-sweep residual pass per component as ONE
+    two-field launch (k_sweep3<FUSE_UV, RES>, strips up to 128 rows); NSGPU_HELM_UV=0 launches u
+    and v separately (64-row strips).  Different strips, same arithmetic: the fields, monitors
+    and counts of 6 steps are bit-identical, and the two-field batch did run (3-sweep batches)."""
+    out = {}
+    for uv in ("1", "0"):
+        monkeypatch.setenv("NSGPU_HELM_UV", uv)
+        gs = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0)
+        st = [gs.step() for _ in range(6)]
+        out[uv] = (st, gs.fields())
+        gs.close()
+    (sa, fa), (sb, fb) = out["1"], out["0"]
+    assert any(s["it_u"] == 3 for s in sa), [s["it_u"] for s in sa]
+    for a, b in zip(sa, sb):
+        for k in ("umin", "umax", "vmin", "vmax", "it_u", "it_phi"):
+            assert a[k] == b[k], (k, a[k], b[k])
+    for x, y in zip(fa, fb):
+        assert np.array_equal(x, y), float(np.max(np.abs(x - y)))
+
+
 @pytest.mark.parametrize("nx,ny", [(256, 192), (96, 160)])
 def test_fused_transfer_passes_match_separate_transfers(gpu, monkeypatch, nx, ny):
     """The last pre-smoothing pass with the restriction fused in (k_sweep2 FUSE_R) and the first
