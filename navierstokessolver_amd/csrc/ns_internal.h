@@ -141,6 +141,8 @@ void launch_reduce_sum_segs(const double* p, int n, int nseg, double* out, hipSt
 // min/max: partials are (umin, -umax, vmin, -vmax) per block -> out[4] = mins of each
 void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t st);
 // Poisson prep: from sums (S, S2) and N -> shift = S/N, out[1] = S2 - S^2/N (= ||b||^2)
+// one rank: launch_reduce_sum (nv = 2) + launch_finish_mean in one launch
+void launch_reduce_sum_mean(const double* p, int n, double* sums, double ncells, double* out, hipStream_t st);
 void launch_finish_mean(const double* sums, double ncells, double* shift_and_bn2, hipStream_t st);
 // (sum f, sum f^2) partials over own cells
 int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st);

@@ -3357,6 +3357,32 @@ __global__ __launch_bounds__(1024) void k_reduce_min(const double* __restrict__ 
     }
 }
 
+// one rank: k_reduce_sum of the (sum, sum^2) partials and k_finish_mean in one launch (no
+// all-reduce between them; the same arithmetic in the same order)
+__global__ __launch_bounds__(1024) void k_reduce_sum_mean(const double* __restrict__ p, int n,
+                                                          double* __restrict__ sums, double nc,
+                                                          double* __restrict__ out) {
+    __shared__ double sh[1024];
+    double r[2];
+    for (int v = 0; v < 2; v++) {
+        double s = 0.0;
+        for (int k = threadIdx.x; k < n; k += 1024) s += p[(size_t)k * 2 + v];
+        sh[threadIdx.x] = s;
+        __syncthreads();
+        for (int w = 512; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+            __syncthreads();
+        }
+        r[v] = sh[0];
+        if (threadIdx.x == 0) sums[v] = sh[0];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double s = r[0], s2 = r[1];
+        out[0] = s / nc;
+        out[1] = fmax(s2 - s * s / nc, 0.0);
+    }
+}
 __global__ void k_finish_mean(const double* __restrict__ sums, double n, double* __restrict__ out) {
     const double s = sums[0], s2 = sums[1];
     out[0] = s / n;                 // MatNullSpaceRemove: subtract the plain mean (FluidSolver.cpp:550)
@@ -4534,6 +4560,9 @@ void launch_reduce_sum_segs(const double* p, int n, int nseg, double* out, hipSt
 }
 void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t st) {
     NS_LAUNCH(k_reduce_min, dim3(1), dim3(1024), 0, st, p, n, nv, out);
+}
+void launch_reduce_sum_mean(const double* p, int n, double* sums, double ncells, double* out, hipStream_t st) {
+    NS_LAUNCH(k_reduce_sum_mean, dim3(1), dim3(1024), 0, st, p, n, sums, ncells, out);
 }
 void launch_finish_mean(const double* sums, double ncells, double* out, hipStream_t st) {
     NS_LAUNCH(k_finish_mean, dim3(1), dim3(1), 0, st, sums, ncells, out);

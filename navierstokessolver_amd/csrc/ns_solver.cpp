@@ -1766,6 +1766,10 @@ int divergence(ns_solver* s) {
                                s->st);
     });
     if (nb < 0) return nb;
+    if (!comm_on(s)) {
+        nsg::launch_reduce_sum_mean(s->part, nb, s->scal + S_DIVSUM, s->ncells, s->scal + S_SHIFT, s->st);
+        return 0;
+    }
     nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_DIVSUM, s->st);
     CHK(allreduce(s, s->scal + S_DIVSUM, 2, ncclSum));
     nsg::launch_finish_mean(s->scal + S_DIVSUM, s->ncells, s->scal + S_SHIFT, s->st);
