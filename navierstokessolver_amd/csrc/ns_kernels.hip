@@ -3954,7 +3954,10 @@ static int strip_blocks(const StreamArgs& a, int nf) {
 static int plan_strips2(StreamArgs& a, long cap, int depth, int* nblk, int lmax = 64) {
     // strips of >= 20 rows: at 2048^2 (the first coarse level) 16 -> 20 rows is 41.9 -> 38.8 us per
     // FUSE_R pass (fewer halo rows per output row beats the extra waves); 24 / 28 measured slower
-    constexpr int lmin2 = 20;
+#ifndef LMIN2
+#define LMIN2 20
+#endif
+    constexpr int lmin2 = LMIN2;
     const int d = (depth + 1) & ~1, R = a.nxl - 2 * d;
     a.pbase = 0;
     a.rb1 = 0;
