@@ -2447,6 +2447,14 @@ __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
 
 template <int OP, bool RES, int FUSE, bool ZIN = false>
 __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) { sweep2_body<OP, RES, FUSE, ZIN>(a); }
+// FP_W4 (A/B): the finest prolongation pass held to 4 waves / SIMD (128 VGPRs; with SD2_FP = 2)
+#ifndef FP_W4
+#define FP_W4 0
+#endif
+template <bool RES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_sweep2_fp4(StreamArgs a) {
+    sweep2_body<0, RES, FUSE_P>(a);
+}
 
 // ------------------------------------------------ K4 small levels: LDS-tiled fused passes
 // The multigrid levels below the streaming kernels' range (< 2048^2 cells: 1024^2 .. 128^2
@@ -4067,6 +4075,13 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
     // overlap depth 5, not the 4 of its fine-row cone: fine row 0 (even) reads coarse row -1,
     // whose exchange runs concurrently with the interior strips
     // (with the output residual the fine cone is 5 rows too; the coarse one stays at 3)
+    if (FP_W4) {
+        const void* k = part ? (const void*)k_sweep2_fp4<true> : (const void*)k_sweep2_fp4<false>;
+        const int nstr = plan_strips2(a, resident_waves(k), 5, &nblk);
+        if (nblk && part) NS_LAUNCH((k_sweep2_fp4<true>), dim3(nblk), dim3(256), 0, st, a);
+        else if (nblk) NS_LAUNCH((k_sweep2_fp4<false>), dim3(nblk), dim3(256), 0, st, a);
+        return nstr;
+    }
     if (part) {
         const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2<0, true, FUSE_P>), 5, &nblk);
         if (nblk) NS_LAUNCH((k_sweep2<0, true, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
