@@ -3350,18 +3350,27 @@ __global__ __launch_bounds__(1024) void k_reduce_sum_segs(const double* __restri
 
 __global__ __launch_bounds__(1024) void k_reduce_min(const double* __restrict__ p, int n, int nv,
                                                      double* __restrict__ out) {
-    __shared__ double sh[1024];
-    for (int v = 0; v < nv; v++) {
-        double s = INFINITY;
-        for (int k = threadIdx.x; k < n; k += 1024) s = fmin(s, p[(size_t)k * nv + v]);
-        sh[threadIdx.x] = s;
-        __syncthreads();
-        for (int w = 512; w > 0; w >>= 1) {
-            if ((int)threadIdx.x < w) sh[threadIdx.x] = fmin(sh[threadIdx.x], sh[threadIdx.x + w]);
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) out[v] = sh[0];
-        __syncthreads();
+    // all nv (<= 4) minima in one pass: per-thread registers, a wave's shuffles, the 16 waves'
+    // results through LDS (2 barriers instead of 11 per value; fmin is order-independent)
+    __shared__ double sh[16][4];
+    double m[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+    for (int k = threadIdx.x; k < n; k += 1024)
+#pragma unroll
+        for (int v = 0; v < 4; v++)
+            if (v < nv) m[v] = fmin(m[v], p[(size_t)k * nv + v]);
+#pragma unroll
+    for (int v = 0; v < 4; v++)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) m[v] = fmin(m[v], __shfl_xor(m[v], off, 64));
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0)
+#pragma unroll
+        for (int v = 0; v < 4; v++) sh[wv][v] = m[v];
+    __syncthreads();
+    if (threadIdx.x < 4 && (int)threadIdx.x < nv) {
+        double r = sh[0][threadIdx.x];
+        for (int w = 1; w < 16; w++) r = fmin(r, sh[w][threadIdx.x]);
+        out[threadIdx.x] = r;
     }
 }
 
