@@ -33,14 +33,16 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level 
 # stream around every launch in the timed region (ns_params.timing).  Algorithmic bytes per
 # cell (24 B/cell for one unfused sweep: read phi, read b, write phi):
 #   restriction pass (k_sweep2 FUSE_R): two RB sweeps + residual + restriction:
-#       read phi 8 + read b 8 + write phi 8 + write the coarse rhs and phi 2 x 8 / 4  = 28
+#       read phi 8 + read b 8 + write phi 8 + write the coarse rhs 8 / 4                = 26
+#       (the coarse level's first pass takes its iterate as zero -- ZIN, r3 -- so no coarse phi
+#       store; PMC write bytes: phi 134.2 MB + coarse b 33.6 MB at 4096^2)
 #   prolongation pass (k_sweep2 FUSE_P): prolongation + two RB sweeps:
 #       read phi 8 + read b 8 + write phi 8 + read the coarse correction 8 / 4         = 26
 # and the Helmholtz solve's passes (K2, single rank: one velocity component per pass):
 #   Helmholtz pass (k_sweep3 / k_sweep2<Helmholtz>): 3 or 2 RB-SOR sweeps: read q 8 + read b 8 + write q 8 = 24
 # The one with the largest total time per step is `roofline` (the dominant kernel).
 KERNELS = {
-    "restrict": ("k_sweep2<Poisson, FUSE_R> (finest pre-smoothing pass: 2 RB sweeps + residual + restriction)", 28),
+    "restrict": ("k_sweep2<Poisson, FUSE_R> (finest pre-smoothing pass: 2 RB sweeps + residual + restriction)", 26),
     "prolong": ("k_sweep2<Poisson, FUSE_P> (finest post-smoothing pass: prolongation + 2 RB sweeps + output residual)", 26),
     "helmholtz": ("Helmholtz pass of one velocity component of (I - a L_V) u* = RHS (k_sweep3 + residual stage: "
                   "3 RB-SOR sweeps, after the wall bands; or k_sweep2: 2 sweeps; the one-rank two-field "
@@ -71,6 +73,14 @@ def parse():
     return ap.parse_args()
 
 
+def _sha16(path):
+    import hashlib
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -90,14 +100,19 @@ def _host_threads():
     return len(os.sched_getaffinity(0))
 
 
-def helm_passes(n, world):
+HALO = 7   # ghost rows per side (ns_internal.h nsg::HALO)
+
+
+def helm_passes(n, min_rows):
     """HBM passes of one component's n Helmholtz sweeps (ns_solver.cpp helm_sweeps): 3-sweep
-    passes while >= 5 remain (slabs too, unless thinner than 14 rows); a batch may end on a
-    3-sweep pass with its residual (3 = 3, 6 = 3+3; slabs too since HALO = 7), otherwise on a pair
-    (5 = 3+2); an odd remainder otherwise starts with a single sweep."""
+    passes while >= 5 remain; a batch may end on a 3-sweep pass with its residual (3 = 3,
+    6 = 3+3; slabs too since HALO = 7), otherwise on a pair (5 = 3+2); an odd remainder otherwise
+    starts with a single sweep.  `min_rows` = the thinnest slab's rows: below 2 HALO rows the
+    solver allows no 3-sweep pass on any rank (ns_solver::triple), so pairs and single sweeps."""
+    triple = min_rows >= 2 * HALO
     p, r = 0, n
     while r > 0:
-        if r >= 5 or r in (3, 6):
+        if triple and (r >= 5 or r in (3, 6)):
             w = 3
         elif r % 2 and r >= 3:
             w = 1
@@ -257,15 +272,21 @@ def main():
     # finest-level sweeps: V(2,2) per cycle (the convergence check rides on each cycle's last pass)
     fine_sweeps = 4 * cycles
     # whole-step algorithmic bytes per cell: K1 64 + K3 24 + K5 40 + the phi
-    # extrapolation 32; Helmholtz 24 per pass of one component (a pass = 2 or 3 sweeps: see
-    # helm_passes); multigrid per solve `cycles` FUSE_R passes at 28 and `cycles` FUSE_P passes
-    # at 26 on the finest level, x 4/3 for the coarser levels (each a quarter of the one above)
-    hpasses = sum(helm_passes(int(s["it_u"]), world) for s in stats)
+    # extrapolation 32 or 40; Helmholtz 24 per pass of one component (a pass = 2 or 3 sweeps: see
+    # helm_passes); multigrid per solve `cycles` FUSE_R and `cycles` FUSE_P passes at 26 each on
+    # the finest level, x 4/3 for the coarser levels (each a quarter of the one above)
+    min_rows = min(b - a for a, b in (nsa._lib.slab_range(n, world, r) for r in range(world)))
+    hpasses = sum(helm_passes(int(s["it_u"]), min_rows) for s in stats)
+    # the phi extrapolation: cubic (4 planes read + 1 written = 40 B/cell) after a solve that
+    # needed >= 2 V-cycles, else quadratic (32); the solver's `need` may be one less than the
+    # cycles a solve ran, so this counts the cubic at most one step too often
+    prev_c = [None] + [int(s["it_phi"]) for s in stats[:-1]]
+    extrap_bpc = sum(40 if (c is None or c >= 2) else 32 for c in prev_c) / K
     # the Helmholtz wall bands (two k_helm_band launches) on the cells within 128 of a wall:
     # per launch u, v read 16 + rhs 16 + write 16 -> 96 B per band cell
     band_frac = 1.0 - max(n - 256, 0) * max(nyc - 256, 0) / float(n * nyc)
-    step_bpc = (64 + 24 + 40 + 32 + 2 * 24 * hpasses / K + 96 * band_frac
-                + (28 * cycles + 26 * cycles) / K * 4.0 / 3.0)
+    step_bpc = (64 + 24 + 40 + extrap_bpc + 2 * 24 * hpasses / K + 96 * band_frac
+                + (26 * cycles + 26 * cycles) / K * 4.0 / 3.0)
     if channel:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications
         # of (line extension 8 + FUSE_R 28 + FUSE_P 26, x 4/3 for the coarser levels) = 80 each,
@@ -290,21 +311,33 @@ def main():
         js.close()
     if rank != 0:
         return
-    traffic = {}
+    # roofline.traffic: HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE
+    # cannot be read inside this run); profiles/pmc_traffic.json names the run that measured them
+    # and the sha256 of the libnsgpu.so it ran, and `traffic_source` says whether that is this
+    # run's library
+    traffic, tsrc = {}, None
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(prof):
+    if os.path.exists(prof) and world == 1:
         try:
             d = json.load(open(prof))
             if d.get("n") == n and not channel:
                 traffic = {k: v.get("kernel_bytes_per_launch") for k, v in d.get("kernels", {}).items()}
+                src = dict(d.get("source") or {})
+                src["file"] = "profiles/pmc_traffic.json"
+                src["same_library_as_this_run"] = (src.get("libnsgpu_sha16") is not None and
+                                                   src.get("libnsgpu_sha16") == _sha16(nsa._lib.LIB_PATH))
+                tsrc = src
         except Exception:
             traffic = {}
 
     def roof(key, label, bpc, avg_s, launches):
         achieved = bpc * local_cells / avg_s / 1e9
-        return {"bound": "hbm", "kernel": label, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get(key), "avg_kernel_us": avg_s * 1e6,
-                "launches_timed": launches, "bytes_per_launch": bpc * local_cells, "bytes_per_cell": bpc}
+        r = {"bound": "hbm", "kernel": label, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get(key), "avg_kernel_us": avg_s * 1e6,
+             "launches_timed": launches, "bytes_per_launch": bpc * local_cells, "bytes_per_cell": bpc}
+        if r["traffic"] is not None:
+            r["traffic_source"] = tsrc
+        return r
 
     kern = {}
     for key, (label, bpc) in KERNELS.items():

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("NSGPU_LIB", os.path.join(HERE, "libnsgpu.so"))
 HEADER = os.path.join(os.path.dirname(HERE), "include", "nsgpu.h")
 
 # ---- constants mirrored from include/nsgpu.h (checked by tests/test_abi.py) ----
+NSGPU_ABI_VERSION = 5   # the struct layouts / enum values below; lib() refuses a library of another ABI
 NS_OK, NS_EINVAL, NS_EHIP, NS_ERCCL, NS_ENOMEM, NS_EDIVERGE = 0, -1, -2, -3, -4, -5
 NS_BC_INLET_UNI, NS_BC_INLET_PARABOLIC, NS_BC_WALL, NS_BC_PRESSURE, NS_BC_NEUMANN = 0, 1, 2, 3, 4
 NS_POISSON_MG, NS_POISSON_JACOBI, NS_POISSON_RBSOR = 0, 1, 3   # ABI 4: zeroed params select MG
@@ -124,6 +125,12 @@ def lib():
                 continue
             fn.restype = res
             fn.argtypes = args
+        # these bindings mirror one ABI's ns_params / ns_stats layouts and enum values: a library of
+        # another ABI would read them wrongly (or write past a shorter ns_stats) -- refuse it
+        abi = L.ns_abi_version()
+        if abi != NSGPU_ABI_VERSION:
+            raise ImportError(f"{LIB_PATH} has ABI {abi}; these bindings expect ABI {NSGPU_ABI_VERSION} "
+                              "(rebuild with __graft_entry__.build())")
         _lib = L
     return _lib
 

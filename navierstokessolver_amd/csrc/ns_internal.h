@@ -205,6 +205,13 @@ int cv_image(const double* hx, const double* hy, int nx, int ny, int dlo, int dh
 int launch_coarse_vcycle(const Geo& g, const double* img, int img_n, int dn, double* phi, const double* b, int cycles,
                          int pre, int post, int citers, double comega, double somega, int dlo, int dhi,
                          hipStream_t st, int zin = 0);
+// the coarsest level's exact separable solve (k_direct), one stage G = [E o] (P M Q): P n1p x n1p,
+// Q n2p x n2p, E n1p x n2p (null: none), row-major and zero-padded to n1p / n2p = n1 / n2 rounded up
+// to 16 (<= 128); M, G: n1 x n2 with row strides ldm, ldg.  < 0 if the sizes do not fit
+// (direct_fits: padded sides <= 128, so that M and the workgroup's rows of P fit 160 KiB of LDS)
+bool direct_fits(int n1, int n2);
+int launch_direct(const double* P, const double* M, const double* Q, const double* E, double* G, int n1, int n2,
+                  int ldm, int ldg, hipStream_t st);
 // the outflow side's 1-D line solve of the Poisson preconditioner into the row p (ny <= 4096;
 // -1 otherwise), and its constant extension along x over `rows` rows of the plane z (from its
 // first halo row) and the single row zg (if not null)

@@ -4462,6 +4462,137 @@ int launch_coarse_vcycle(const Geo& g, const double* img, int img_n, int dn, dou
     return 0;
 }
 
+// ---------------------------------------------- K4 coarsest level: exact separable solve (r4)
+// The last multigrid level (<= 128^2 cells at 4096^2) is a box whose operator is separable:
+// L = Lx (x) I + I (x) Ly, Lx / Ly the level's tridiagonal 1-D operators (pw / pe, ps / pn;
+// symmetric after a diagonal scaling by sqrt(h)).  With their eigen-decompositions Lx = Vx Lx' Vx^-1
+// (host, once: ns_solver.cpp direct_setup) the solve L X = B is
+//     Y = E o (Vx^-1 B Vy^-T),  E_km = 1 / (lx_k + ly_m)  (0 on the null mode),   X = Vx Y Vy^T
+// -- the same answer as the bordered system [A 1; w^T 0] the LDS V-cycle's last level solves
+// (w.x = 0 with w the cell areas).  One launch per stage G = [E o] (P M Q): a workgroup owns a
+// 16 x 16 block of G.  Every global load is issued up front, in one round (a chunked loop that
+// waited for each chunk's loads took 26 us per launch): M whole and P's 16 rows go to LDS, the
+// block's columns of Q to registers.  The four waves then form T = P[I, :] M (16 x n2p) by fp64
+// MFMA (16x16x4, K over n1p), T goes back through LDS, and the waves split T Q[:, J] over K,
+// summed in a fixed order.  n1p, n2p = the sides rounded up to 16 (<= 128); P, Q, E are
+// zero-padded there, M / G are guarded.  Replaces the 128^2 LDS-tiled passes and the
+// one-workgroup coarse V-cycle (38 us per V-cycle at 4096^2, profiles/r03).
+typedef double nsd4 __attribute__((ext_vector_type(4)));
+constexpr int DIRECT_MAX = 128;                    // largest padded side
+constexpr int DIRECT_LDS = 20480;                  // doubles (160 KiB)
+__host__ __device__ inline int direct_r1(int n1p, int n2p) {   // region 1: M, then the 4 partial tiles
+    return n1p * n2p > 1024 ? n1p * n2p : 1024;
+}
+__host__ __device__ inline int direct_r2(int n1p, int n2p) {   // region 2: P rows, then T, in doubles
+    const int a = 16 * (n1p + 2), b = 16 * (n2p + 1);
+    return a > b ? a : b;
+}
+__global__ __launch_bounds__(256) void k_direct(const double* __restrict__ P, const double* __restrict__ M,
+                                                const double* __restrict__ Q, const double* __restrict__ E,
+                                                double* __restrict__ G, int n1, int n2, int n1p, int n2p, int ldm,
+                                                int ldg) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* Ms = sm;                        // n1p x n2p, row k's columns XOR-swizzled by 16 on odd k
+    double* R2 = sm + direct_r1(n1p, n2p);  // P[I, :] (stride n1p + 2), later T (stride n2p + 1)
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int bi = blockIdx.x, bj = blockIdx.y;
+    const int r16 = lane & 15, k4 = lane >> 4;
+    const int sw = (n2p & 31) ? 0 : 16;     // (half-waves read rows k, k+1: their banks stay disjoint)
+    const int ps = n1p + 2, ts = n2p + 1;
+    // ---- one round of loads: Q's block columns (this wave's K-quarter) to registers, P's rows and
+    // M to LDS
+    constexpr int QV = DIRECT_MAX / 16;
+    const int kq = n2p / 4, colq = 16 * bj + r16;
+    double qv[QV];
+#pragma unroll
+    for (int q = 0; q < QV; q++) qv[q] = 4 * q < kq ? Q[(size_t)(w * kq + 4 * q + k4) * n2p + colq] : 0.0;
+    {
+        constexpr int NM = DIRECT_MAX * DIRECT_MAX / 256, NP = 16 * DIRECT_MAX / 256;
+        double mv[NM], pv[NP];
+        const int nm = n1p * n2p, np = 16 * n1p;
+#pragma unroll
+        for (int q = 0; q < NM; q++) {
+            const int e = threadIdx.x + 256 * q, k = e / n2p, c = e - k * n2p;
+            mv[q] = (e < nm && k < n1 && c < n2) ? M[(size_t)k * ldm + c] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            const int e = threadIdx.x + 256 * q;
+            pv[q] = e < np ? P[(size_t)16 * bi * n1p + e] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < NM; q++) {
+            const int e = threadIdx.x + 256 * q, k = e / n2p, c = e - k * n2p;
+            if (e < nm) Ms[k * n2p + (c ^ ((k & 1) ? sw : 0))] = mv[q];
+        }
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            const int e = threadIdx.x + 256 * q, r = e / n1p, k = e - r * n1p;
+            if (e < np) R2[r * ps + k] = pv[q];
+        }
+    }
+    __syncthreads();
+    // ---- step 1: T = P[I, :] M, the wave's column tiles ct = w, w + 4 (at most DIRECT_MAX / 64)
+    constexpr int NT = DIRECT_MAX / 64;
+    const int ntile = n2p / 16;
+    nsd4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) acc[t] = nsd4{0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < n1p; k0 += 4) {
+        const int k = k0 + k4;
+        const double av = R2[r16 * ps + k];
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+            if (w + 4 * t < ntile) {
+                const int col = 16 * (w + 4 * t) + r16;
+                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Ms[k * n2p + (col ^ ((k & 1) ? sw : 0))], acc[t],
+                                                             0, 0, 0);
+            }
+    }
+    __syncthreads();   // (every wave is done with P's rows: T takes their place)
+#pragma unroll
+    for (int t = 0; t < NT; t++)
+        if (w + 4 * t < ntile) {
+            const int col = 16 * (w + 4 * t) + r16;
+#pragma unroll
+            for (int r = 0; r < 4; r++) R2[(k4 + 4 * r) * ts + col] = acc[t][r];   // (f64 C/D: row = k4 + 4 r)
+        }
+    __syncthreads();
+    // ---- step 2: G[I, J] = T Q[:, J], K = n2p split over the four waves
+    nsd4 g4 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < QV; q++)
+        if (4 * q < kq) g4 = __builtin_amdgcn_mfma_f64_16x16x4f64(R2[r16 * ts + w * kq + 4 * q + k4], qv[q], g4, 0, 0, 0);
+    // (M's region is free: the four partial tiles, summed in a fixed order)
+#pragma unroll
+    for (int r = 0; r < 4; r++) Ms[w * 256 + (k4 + 4 * r) * 16 + r16] = g4[r];
+    __syncthreads();
+    const int t = threadIdx.x, gi = 16 * bi + (t >> 4), gj = 16 * bj + (t & 15);
+    double g = ((Ms[t] + Ms[256 + t]) + Ms[512 + t]) + Ms[768 + t];
+    if (E) g *= E[(size_t)gi * n2p + gj];
+    if (gi < n1 && gj < n2) G[(size_t)gi * ldg + gj] = g;
+}
+
+bool direct_fits(int n1, int n2) {
+    const int n1p = (n1 + 15) / 16 * 16, n2p = (n2 + 15) / 16 * 16;
+    return n1 >= 1 && n2 >= 1 && n1p <= DIRECT_MAX && n2p <= DIRECT_MAX &&
+           direct_r1(n1p, n2p) + direct_r2(n1p, n2p) <= DIRECT_LDS;
+}
+
+int launch_direct(const double* P, const double* M, const double* Q, const double* E, double* G, int n1, int n2,
+                  int ldm, int ldg, hipStream_t st) {
+    const int n1p = (n1 + 15) / 16 * 16, n2p = (n2 + 15) / 16 * 16;
+    if (!direct_fits(n1, n2) || ldm < n2 || ldg < n2) return -1;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_direct, hipFuncAttributeMaxDynamicSharedMemorySize, DIRECT_LDS * 8);
+        attr = true;
+    }
+    const size_t bytes = (size_t)(direct_r1(n1p, n2p) + direct_r2(n1p, n2p)) * sizeof(double);
+    NS_LAUNCH(k_direct, dim3(n1p / 16, n2p / 16), dim3(256), bytes, st, P, M, Q, E, G, n1, n2, n1p, n2p, ldm, ldg);
+    return 0;
+}
+
 // ---------------------------------------------- outflow line solve (NEUMANN side, preconditioner)
 // The 1-D problem of the Poisson preconditioner's outflow side: on the boundary
 // row (a W or E outflow side: one slab row, j contiguous) solve T p = r - <r>, T the operator's

@@ -182,6 +182,14 @@ struct ns_solver {
     int mg_pre = 2, mg_post = 2, mg_coarse_iters = 0;
     double mg_omega_c = 1.0, mg_omega_s = 1.1;
     bool mg_coarse_lds = false;
+    // r4: the coarsest level solved exactly by its separable eigen-decomposition (k_direct, two
+    // launches): the first whole coarse level of <= direct_cells cells (NSGPU_DIRECT_CELLS, default
+    // 128^2; 0 = the LDS V-cycle below it as in round 3).  dmat: P1 = Vx^-1, Q1 = Vy^-T, E, P2 = Vx,
+    // Q2 = Vy^T (direct_setup), padded to multiples of 16
+    bool mg_direct = false;
+    long direct_cells = 128L * 128L;
+    double* dmat = nullptr;
+    const double *dP1 = nullptr, *dQ1 = nullptr, *dE = nullptr, *dP2 = nullptr, *dQ2 = nullptr;
     // NEUMANN outflow (pois_solve_krylov): BiCGStab planes r, r0, p, v, s, t, ph, sh, scratch
     // (null without an outflow side) and the recurrence scalars
     double* kv[9] = {};
@@ -288,11 +296,17 @@ int halo_reqs(ns_solver* s, const HaloReq* reqs_in, int nreq_in, hipStream_t xs 
     if (!xs) xs = s->st;
     if (!comm_on(s)) return 0;
     s->n_xchg++;
-    // the requests riding along (ns_solver::piggy) join this group
-    HaloReq reqs[12];
+    // the requests riding along (ns_solver::piggy) join this group; a list that does not fit is
+    // an error, never a silently dropped request (its level would read stale ghost rows)
+    constexpr int MAXREQ = 8 + 4;
+    if (nreq_in < 0 || nreq_in + s->npiggy > MAXREQ) {
+        set_err("halo exchange: %d requests + %d riding along exceed %d", nreq_in, s->npiggy, MAXREQ);
+        return NS_EINVAL;
+    }
+    HaloReq reqs[MAXREQ];
     int nreq = 0;
-    for (int k = 0; k < nreq_in && nreq < 12; k++) reqs[nreq++] = reqs_in[k];
-    for (int k = 0; k < s->npiggy && nreq < 12; k++) reqs[nreq++] = HaloReq{s->piggy[k].g, s->piggy[k].f, s->piggy[k].w};
+    for (int k = 0; k < nreq_in; k++) reqs[nreq++] = reqs_in[k];
+    for (int k = 0; k < s->npiggy; k++) reqs[nreq++] = HaloReq{s->piggy[k].g, s->piggy[k].f, s->piggy[k].w};
     s->npiggy = 0;
     const bool lo = s->rank > 0 || s->nranks == 1, hi = s->rank < s->nranks - 1 || s->nranks == 1;
     // (loopback: the 1-rank communicator's only rank, 0, is every peer; a one-rank loopback sends
@@ -308,6 +322,7 @@ int halo_reqs(ns_solver* s, const HaloReq* reqs_in, int nreq_in, hipStream_t xs 
             CHK(ensure_stage(s, 4 * cnt));
             double *slo = s->stage, *shi = slo + cnt, *rlo = shi + cnt, *rhi = rlo + cnt;
             const double *flo = self ? f - (ptrdiff_t)q.w * ld : f, *fhi = f + (ptrdiff_t)(self ? nxl : nxl - q.w) * ld;
+            s->x_link += 8.0 * (double)cnt;   // (as halo_rccl: each side is its own link)
             if (lo) HIPCHK(hipMemcpyAsync(slo, flo, cnt * 8, hipMemcpyDeviceToHost, xs));
             if (hi) HIPCHK(hipMemcpyAsync(shi, fhi, cnt * 8, hipMemcpyDeviceToHost, xs));
             HIPCHK(hipStreamSynchronize(xs));
@@ -934,7 +949,7 @@ bool fused_prolong(const ns_solver* s, int l) {
 
 bool zero_ok(const ns_solver* s, int l) {
     if (l <= 0 || l >= (int)s->lv.size()) return false;
-    if (l == (int)s->lv.size() - 1) return s->mg_coarse_lds;
+    if (l == (int)s->lv.size() - 1) return s->mg_coarse_lds || s->mg_direct;
     return fused_restrict(s, l) && s->mg_pre == 2;
 }
 
@@ -975,6 +990,7 @@ int gather_level(ns_solver* s, MgLevel& C) {
         const size_t r0 = (size_t)C.gs.i0 * ld, r1 = r0 + (size_t)C.gs.nxl * ld;
         std::fill(s->stage, s->stage + r0, 0.0);
         std::fill(s->stage + r1, s->stage + n, 0.0);
+        s->x_link += 8.0 * (double)C.gs.nxl * ld;   // (as the RCCL gather: this rank's slab, one link per peer)
         if (s->ht.allreduce(s->ht.user, s->stage, (int32_t)n, 0) != 0) {
             set_err("host transport allreduce failed");
             return NS_ERCCL;
@@ -1046,6 +1062,18 @@ int mg_coarse(ns_solver* s) {
     const int l = (int)s->lv.size() - 1;
     MgLevel& L = level(s, l);
     CHK(flush_b(s, l));
+    if (s->mg_direct) {
+        // Y = E o (Vx^-1 b Vy^-T) into the level's spare plane, phi = Vx Y Vy^T (phi is not read:
+        // the implicit zero iterate needs nothing)
+        L.zero = false;
+        const int nx = L.g.nx, ny = L.g.ny, ld = L.g.ld;
+        if (nsg::launch_direct(s->dP1, L.b, s->dQ1, s->dE, L.tmp, nx, ny, ld, ld, s->st) != 0 ||
+            nsg::launch_direct(s->dP2, L.tmp, s->dQ2, nullptr, L.phi, nx, ny, ld, ld, s->st) != 0) {
+            set_err("coarse direct solve does not fit");
+            return NS_EINVAL;
+        }
+        return 0;
+    }
     if (s->mg_coarse_lds) {
         const int zin = L.zero ? 1 : 0;
         L.zero = false;
@@ -1539,6 +1567,118 @@ nsg::Coef coef_view(double* d, int nx, int ny) {
     return c;
 }
 
+// symmetric eigen-decomposition by cyclic Jacobi rotations: a (n x n, row-major, destroyed) ->
+// eigenvalues lam, orthonormal eigenvectors in the columns of v (row-major)
+void jacobi_eigen(int n, std::vector<double>& a, std::vector<double>& lam, std::vector<double>& v) {
+    v.assign((size_t)n * n, 0.0);
+    for (int i = 0; i < n; i++) v[(size_t)i * n + i] = 1.0;
+    for (int sweep = 0; sweep < 100; sweep++) {
+        double off = 0.0, dg = 0.0;
+        for (int p = 0; p < n; p++) {
+            dg += a[(size_t)p * n + p] * a[(size_t)p * n + p];
+            for (int q = p + 1; q < n; q++) off += a[(size_t)p * n + q] * a[(size_t)p * n + q];
+        }
+        if (off <= 1e-34 * dg) break;
+        for (int p = 0; p < n; p++)
+            for (int q = p + 1; q < n; q++) {
+                const double apq = a[(size_t)p * n + q];
+                if (apq == 0.0) continue;
+                // the rotation in (p, q) that zeroes a_pq: t = tan(theta), the smaller root of
+                // t^2 + 2 tau t - 1 = 0, tau = (a_qq - a_pp) / (2 a_pq)
+                const double tau = (a[(size_t)q * n + q] - a[(size_t)p * n + p]) / (2.0 * apq);
+                const double t = (tau >= 0.0 ? 1.0 : -1.0) / (std::fabs(tau) + std::sqrt(1.0 + tau * tau));
+                const double c = 1.0 / std::sqrt(1.0 + t * t), sn = t * c;
+                for (int k = 0; k < n; k++) {   // A J
+                    const double akp = a[(size_t)k * n + p], akq = a[(size_t)k * n + q];
+                    a[(size_t)k * n + p] = c * akp - sn * akq;
+                    a[(size_t)k * n + q] = sn * akp + c * akq;
+                }
+                for (int k = 0; k < n; k++) {   // J^T (A J)
+                    const double apk = a[(size_t)p * n + k], aqk = a[(size_t)q * n + k];
+                    a[(size_t)p * n + k] = c * apk - sn * aqk;
+                    a[(size_t)q * n + k] = sn * apk + c * aqk;
+                }
+                for (int k = 0; k < n; k++) {   // V J
+                    const double vkp = v[(size_t)k * n + p], vkq = v[(size_t)k * n + q];
+                    v[(size_t)k * n + p] = c * vkp - sn * vkq;
+                    v[(size_t)k * n + q] = sn * vkp + c * vkq;
+                }
+            }
+    }
+    lam.resize(n);
+    for (int i = 0; i < n; i++) lam[i] = a[(size_t)i * n + i];
+}
+
+// The exact solve of the coarsest level (k_direct): its 1-D operators from the level's own
+// tables (w = pw, e = pe: the outflow closure's pw[0] / pe[n-1] toward a zero ghost included),
+// L1 = tridiag(w_i, -(w_i + e_i), e_i); H L1 is symmetric (h_i w_i = 2 / (h_i + h_{i-1}) =
+// h_{i-1} e_{i-1}), so S = H^1/2 L1 H^-1/2 = U diag(lam) U^T and L1 = V diag(lam) V^-1 with
+// V = H^-1/2 U, V^-1 = U^T H^1/2.  A side without a closure is singular (its null vector
+// sqrt(h)); when both are, E's null-mode entry is 0, i.e. the solution with w.x = 0 (w the cell
+// areas) of the system projected onto the range -- the LDS V-cycle's bordered last-level solve.
+int direct_setup(ns_solver* s, const MgLevel& L) {
+    const int nx = L.g.nx, ny = L.g.ny;
+    const int n1p = (nx + 15) / 16 * 16, n2p = (ny + 15) / 16 * 16;
+    std::vector<double> t(8 * (size_t)nx + 8 * (size_t)ny + 2);
+    HIPCHK(hipMemcpy(t.data(), L.coef, t.size() * sizeof(double), hipMemcpyDeviceToHost));
+    const nsg::Coef hc = coef_view(t.data(), nx, ny);
+    auto decompose = [](int n, const double* w, const double* e, const std::vector<double>& h, std::vector<double>& lam,
+                        std::vector<double>& U, bool& singular) {
+        std::vector<double> S((size_t)n * n, 0.0);
+        for (int i = 0; i < n; i++) {
+            S[(size_t)i * n + i] = -(w[i] + e[i]);
+            if (i > 0) S[(size_t)i * n + i - 1] = std::sqrt(h[i] / h[i - 1]) * w[i];
+            if (i < n - 1) S[(size_t)i * n + i + 1] = std::sqrt(h[i] / h[i + 1]) * e[i];
+        }
+        for (int i = 0; i + 1 < n; i++) {   // (exactly symmetric: the mean of the two equal products)
+            const double m = 0.5 * (S[(size_t)i * n + i + 1] + S[(size_t)(i + 1) * n + i]);
+            S[(size_t)i * n + i + 1] = S[(size_t)(i + 1) * n + i] = m;
+        }
+        jacobi_eigen(n, S, lam, U);
+        singular = w[0] == 0.0 && e[n - 1] == 0.0;   // walls on both ends: L1 1 = 0
+        if (singular) {
+            int k0 = 0;
+            for (int k = 1; k < n; k++)
+                if (std::fabs(lam[k]) < std::fabs(lam[k0])) k0 = k;
+            lam[k0] = 0.0;
+            return k0;
+        }
+        return -1;
+    };
+    std::vector<double> lx, ly, Ux, Uy;
+    bool sx = false, sy = false;
+    const int kx0 = decompose(nx, hc.pw, hc.pe, L.hx, lx, Ux, sx);
+    const int ky0 = decompose(ny, hc.ps, hc.pn, L.hy, ly, Uy, sy);
+    const size_t nP = (size_t)n1p * n1p, nQ = (size_t)n2p * n2p, nE = (size_t)n1p * n2p;
+    std::vector<double> img(2 * nP + 2 * nQ + nE, 0.0);
+    double *P1 = img.data(), *Q1 = P1 + nP, *E = Q1 + nQ, *P2 = E + nE, *Q2 = P2 + nP;
+    for (int i = 0; i < nx; i++)
+        for (int k = 0; k < nx; k++) {
+            const double u = Ux[(size_t)i * nx + k], r = std::sqrt(L.hx[i]);
+            P1[(size_t)k * n1p + i] = u * r;   // V^-1 = U^T H^1/2
+            P2[(size_t)i * n1p + k] = u / r;   // V = H^-1/2 U
+        }
+    for (int j = 0; j < ny; j++)
+        for (int m = 0; m < ny; m++) {
+            const double u = Uy[(size_t)j * ny + m], r = std::sqrt(L.hy[j]);
+            Q1[(size_t)j * n2p + m] = u * r;   // Vy^-T = H^1/2 U
+            Q2[(size_t)m * n2p + j] = u / r;   // Vy^T = U^T H^-1/2
+        }
+    for (int k = 0; k < nx; k++)
+        for (int m = 0; m < ny; m++) {
+            const double d = lx[k] + ly[m];
+            E[(size_t)k * n2p + m] = (sx && sy && k == kx0 && m == ky0) || d == 0.0 ? 0.0 : 1.0 / d;
+        }
+    HIPCHK(hipMalloc(&s->dmat, img.size() * sizeof(double)));
+    HIPCHK(hipMemcpy(s->dmat, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice));
+    s->dP1 = s->dmat;
+    s->dQ1 = s->dP1 + nP;
+    s->dE = s->dQ1 + nQ;
+    s->dP2 = s->dE + nE;
+    s->dQ2 = s->dP2 + nP;
+    return 0;
+}
+
 // multigrid hierarchy: halve while every level stays even; stop at the first level small
 // enough for the single-workgroup LDS coarse solve.  With nranks > 1 the first coarse level
 // of <= agg_cells cells (NSGPU_AGG_CELLS, default 1024^2; 0 = never), or whose slabs would
@@ -1580,12 +1720,17 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
     long agg_cells = 1024L * 1024L;
     if (const char* e = getenv("NSGPU_AGG_CELLS")) agg_cells = std::atol(e);
     const int agg_min_rows = 8;
-    // stop at the first whole level whose LDS V-cycle fits (<= ~64^2)
+    // stop at the first whole coarse level the exact separable solve takes (<= direct_cells, sides
+    // <= 128: nsg::direct_fits), else (NSGPU_DIRECT_CELLS=0) at the first whose LDS V-cycle fits (<= ~64^2)
     const size_t lds_cap = 150 * 1024;
+    auto direct_fits = [&](const nsg::Geo& g) {
+        return s->direct_cells > 0 && (long)g.nx * g.ny <= s->direct_cells && nsg::direct_fits(g.nx, g.ny);
+    };
     for (;;) {
         const MgLevel& F = s->lv.back();
         const nsg::Geo& gf = F.g;
         const bool whole = s->nranks == 1 || F.repl;
+        if (whole && s->lv.size() > 1 && direct_fits(gf)) break;
         if (whole && s->lv.size() > 1 && nsg::coarse_vcycle_bytes(gf) <= lds_cap) break;
         if (!nsg::mg_can_coarsen(gf.nx, gf.ny)) break;
         nsg::Geo gc = gf;
@@ -1635,13 +1780,17 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
     }
     const MgLevel& last = s->lv.back();
     const nsg::Geo& gc = last.g;
-    s->mg_coarse_lds = (s->nranks == 1 || last.repl) && s->lv.size() > 1 && nsg::coarse_vcycle_bytes(gc) <= lds_cap;
+    s->mg_direct = (s->nranks == 1 || last.repl) && s->lv.size() > 1 && direct_fits(gc);
+    s->mg_coarse_lds = !s->mg_direct && (s->nranks == 1 || last.repl) && s->lv.size() > 1 &&
+                       nsg::coarse_vcycle_bytes(gc) <= lds_cap;
+    if (s->mg_direct) CHK(direct_setup(s, last));
     if (s->verbose && s->rank == 0) {
         for (size_t l = 0; l < s->lv.size(); l++)
             fprintf(stderr, "nsgpu mg level %zu: %d x %d%s, rows/rank >= %d, %s\n", l, s->lv[l].g.nx, s->lv[l].g.ny,
                     s->lv[l].repl ? " (replicated)" : "", s->lv[l].minrows,
                     pair_level(s, (int)l) ? "2-sweep passes" : (tile_level(s, (int)l) ? "LDS-tiled passes" : "single sweeps"));
-        fprintf(stderr, "nsgpu mg coarse solve: %s\n", s->mg_coarse_lds ? "LDS V-cycle" : "sweeps");
+        fprintf(stderr, "nsgpu mg coarse solve: %s\n",
+                s->mg_direct ? "exact (separable eigen-decomposition)" : (s->mg_coarse_lds ? "LDS V-cycle" : "sweeps"));
     }
     // coarsest relaxation: on the last LDS level (<= 4x4 after the in-LDS coarsening) when the
     // LDS V-cycle is used, else on gc itself by (distributed) sweeps
@@ -2095,6 +2244,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_SPECULATE")) s->speculate = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
+    if (const char* e = getenv("NSGPU_DIRECT_CELLS")) s->direct_cells = std::max(0L, std::atol(e));
     {
         const char* e = getenv("NSGPU_STRIP_ROWS");  // tuning override; unset = adaptive
         nsg::set_strip_rows(e ? atoi(e) : 0);
@@ -2138,7 +2288,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         const bool comm = p->nranks > 1 || loopback;
         s->comm_cus = 0;
         if (const char* e = getenv("NSGPU_COMM_CUS")) s->comm_cus = std::max(0, std::atoi(e));
-        if (s->comm_cus > 0 && s->comm_cus < cus && cus <= 1024 && cus % 8 == 0) {
+        // (a single rank without the loopback has no comm traffic: no masks, every CU computes)
+        if (comm && s->comm_cus > 0 && s->comm_cus < cus && cus <= 1024 && cus % 8 == 0) {
             // the reserved CUs spread evenly over the 8 XCDs: workgroups are dispatched round-robin
             // over the XCDs, so an XCD short of CUs would be every launch's straggler (all 8 on one
             // XCD made the strips ~40 % slower).  Bit 32 x + ((x + 8 j) % 32), j < comm_cus / 8: one
@@ -2332,6 +2483,7 @@ void ns_destroy(ns_solver* s) {
     if (s->phim_mem) (void)hipFree(s->phim_mem);
     if (s->kv_mem) (void)hipFree(s->kv_mem);
     if (s->cvimg) (void)hipFree(s->cvimg);
+    if (s->dmat) (void)hipFree(s->dmat);
     if (s->f32_mem) (void)hipFree(s->f32_mem);
     if (s->fc_mem) (void)hipFree(s->fc_mem);
     if (s->et_mem) (void)hipFree(s->et_mem);

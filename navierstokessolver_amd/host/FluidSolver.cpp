@@ -169,6 +169,13 @@ FluidSolver::FluidSolver(char* fname, Grid* g) : grid(g) {
     pr.device = g_opt.device;
     pr.rank = 0;
     pr.nranks = 1;
+    // a libnsgpu.so of another ABI would read this build's ns_params / ns_stats with other
+    // layouts or enum values: refuse it (the reference's error style: message, setup = false)
+    if (ns_abi_version() != NSGPU_ABI_VERSION) {
+        cout << "GPU solver setup failed: libnsgpu.so has ABI " << ns_abi_version() << ", this build expects "
+             << NSGPU_ABI_VERSION << "\n";
+        return;
+    }
     if (ns_create(&gd, &pr, &m.gpu) != 0) {
         cout << "GPU solver setup failed: " << ns_last_error() << "\n";
         return;

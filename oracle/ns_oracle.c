@@ -1012,6 +1012,140 @@ static double* mg_direct_matrix(const mg_level* L) {
     return M;
 }
 
+/* The GPU path's exact solve of its coarsest level (r4, ns_solver.cpp direct_setup / k_direct):
+ * the level's first coarse level of <= og_direct_cells cells (sides <= 128; 0 = off) is the
+ * last one, and L x = b is solved through the eigen-decompositions of the separable 1-D
+ * operators: L1 = tridiag(w_i, -(w_i + e_i), e_i) with H L1 symmetric, S = H^1/2 L1 H^-1/2 =
+ * U diag(lam) U^T (cyclic Jacobi rotations), C = Vx^-1 b Vy^-T, Y = C / (lx_k + ly_m) with the
+ * null mode (both sides singular) set to 0, x = Vx Y Vy^T -- i.e. w.x = 0 (w the cell areas), as
+ * mg_direct_matrix's bordered system. */
+static long og_direct_cells = 128L * 128L;
+void og_mg_set_direct(long cells) { og_direct_cells = cells < 0 ? 0 : cells; }
+static int mg_direct_fits(int nx, int ny) {
+    return og_direct_cells > 0 && (long)nx * ny <= og_direct_cells && nx <= 128 && ny <= 128;
+}
+
+static void eig_jacobi(int n, double* a, double* lam, double* v) {
+    for (int i = 0; i < n * n; i++) v[i] = 0.0;
+    for (int i = 0; i < n; i++) v[i * n + i] = 1.0;
+    for (int sweep = 0; sweep < 100; sweep++) {
+        double off = 0.0, dg = 0.0;
+        for (int p = 0; p < n; p++) {
+            dg += a[p * n + p] * a[p * n + p];
+            for (int q = p + 1; q < n; q++) off += a[p * n + q] * a[p * n + q];
+        }
+        if (off <= 1e-34 * dg) break;
+        for (int p = 0; p < n; p++)
+            for (int q = p + 1; q < n; q++) {
+                const double apq = a[p * n + q];
+                if (apq == 0.0) continue;
+                const double tau = (a[q * n + q] - a[p * n + p]) / (2.0 * apq);
+                const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+                const double c = 1.0 / sqrt(1.0 + t * t), sn = t * c;
+                for (int k = 0; k < n; k++) {
+                    const double x = a[k * n + p], y = a[k * n + q];
+                    a[k * n + p] = c * x - sn * y; a[k * n + q] = sn * x + c * y;
+                }
+                for (int k = 0; k < n; k++) {
+                    const double x = a[p * n + k], y = a[q * n + k];
+                    a[p * n + k] = c * x - sn * y; a[q * n + k] = sn * x + c * y;
+                }
+                for (int k = 0; k < n; k++) {
+                    const double x = v[k * n + p], y = v[k * n + q];
+                    v[k * n + p] = c * x - sn * y; v[k * n + q] = sn * x + c * y;
+                }
+            }
+    }
+    for (int i = 0; i < n; i++) lam[i] = a[i * n + i];
+}
+
+/* one side: V (n x n, column k = eigenvector k scaled by H^-1/2), Vi = V^-1, lam; returns the
+ * index of the null mode (walls at both ends) or -1 */
+static int mg_direct_side(int n, const double* h, const double* w, const double* e, double* V, double* Vi,
+                          double* lam) {
+    double* S = calloc((size_t)n * n, sizeof(double));
+    double* U = malloc(sizeof(double) * (size_t)n * n);
+    for (int i = 0; i < n; i++) {
+        S[i * n + i] = -(w[i] + e[i]);
+        if (i + 1 < n) S[i * n + i + 1] = S[(i + 1) * n + i] = 2.0 / (sqrt(h[i] * h[i + 1]) * (h[i] + h[i + 1]));
+    }
+    eig_jacobi(n, S, lam, U);
+    for (int i = 0; i < n; i++)
+        for (int k = 0; k < n; k++) {
+            V[i * n + k] = U[i * n + k] / sqrt(h[i]);
+            Vi[k * n + i] = U[i * n + k] * sqrt(h[i]);
+        }
+    free(S); free(U);
+    if (w[0] != 0.0 || e[n - 1] != 0.0) return -1;
+    int k0 = 0;
+    for (int k = 1; k < n; k++)
+        if (fabs(lam[k]) < fabs(lam[k0])) k0 = k;
+    lam[k0] = 0.0;
+    return k0;
+}
+
+typedef struct {
+    int nx, ny;
+    double *Vx, *Vxi, *Vy, *Vyi, *D, *T;
+} mg_direct;
+
+static mg_direct* mg_direct_new(int nx, int ny, const double* hx, const double* hy, const double* cw,
+                                const double* ce, const double* cs, const double* cn) {
+    mg_direct* d = calloc(1, sizeof *d);
+    d->nx = nx; d->ny = ny;
+    d->Vx = malloc(sizeof(double) * nx * nx); d->Vxi = malloc(sizeof(double) * nx * nx);
+    d->Vy = malloc(sizeof(double) * ny * ny); d->Vyi = malloc(sizeof(double) * ny * ny);
+    d->D = malloc(sizeof(double) * nx * ny); d->T = malloc(sizeof(double) * nx * ny);
+    double* lx = malloc(sizeof(double) * nx);
+    double* ly = malloc(sizeof(double) * ny);
+    const int kx0 = mg_direct_side(nx, hx, cw, ce, d->Vx, d->Vxi, lx);
+    const int ky0 = mg_direct_side(ny, hy, cs, cn, d->Vy, d->Vyi, ly);
+    for (int k = 0; k < nx; k++)
+        for (int m = 0; m < ny; m++) {
+            const double s = lx[k] + ly[m];
+            d->D[k * ny + m] = (k == kx0 && m == ky0) || s == 0.0 ? 0.0 : 1.0 / s;
+        }
+    free(lx); free(ly);
+    return d;
+}
+
+static void mg_direct_free(mg_direct* d) {
+    if (!d) return;
+    free(d->Vx); free(d->Vxi); free(d->Vy); free(d->Vyi); free(d->D); free(d->T); free(d);
+}
+
+/* x = L^-1 b (w.x = 0 when L is singular) */
+static void mg_direct_solve(const mg_direct* d, const double* b, double* x) {
+    const int nx = d->nx, ny = d->ny;
+    double* T = d->T;
+    /* T = Vx^-1 b, then Y = D o (T Vy^-T) into x */
+    for (int k = 0; k < nx; k++)
+        for (int j = 0; j < ny; j++) {
+            double acc = 0.0;
+            for (int i = 0; i < nx; i++) acc += d->Vxi[k * nx + i] * b[i * ny + j];
+            T[k * ny + j] = acc;
+        }
+    for (int k = 0; k < nx; k++)
+        for (int m = 0; m < ny; m++) {
+            double acc = 0.0;
+            for (int j = 0; j < ny; j++) acc += T[k * ny + j] * d->Vyi[m * ny + j];   /* Vy^-T[j][m] = Vyi[m][j] */
+            x[k * ny + m] = acc * d->D[k * ny + m];
+        }
+    /* x = Vx Y Vy^T */
+    for (int i = 0; i < nx; i++)
+        for (int m = 0; m < ny; m++) {
+            double acc = 0.0;
+            for (int k = 0; k < nx; k++) acc += d->Vx[i * nx + k] * x[k * ny + m];
+            T[i * ny + m] = acc;
+        }
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < ny; j++) {
+            double acc = 0.0;
+            for (int m = 0; m < ny; m++) acc += T[i * ny + m] * d->Vy[j * ny + m];   /* Vy^T[m][j] = Vy[j][m] */
+            x[i * ny + j] = acc;
+        }
+}
+
 /* one red-black sweep in place (red = (i+j) even first) */
 static void mg_rb(const mg_level* L, double* p, const double* b, double shift, double omega) {
     const int nt = (size_t)L->nx * L->ny >= 65536 ? og_nt : 1;
@@ -1080,8 +1214,10 @@ static mg_level* mg_build(int nx, int ny, const double* hx, const double* hy, in
         l->b = calloc((size_t)nx * ny, sizeof(double));
         n++;
         /* same rule as the GPU hierarchy (global levels + the LDS V-cycle, mg_can_coarsen in
-         * ns_internal.h): halve while both sizes are even, >= 4, and the level has > 16 cells */
+         * ns_internal.h): halve while both sizes are even, >= 4, and the level has > 16 cells;
+         * (r4) stop at the first coarse level the exact direct solve takes */
         if (nx % 2 || ny % 2 || nx < 4 || ny < 4 || nx * ny <= 16 || n == cap) break;
+        if (n >= 2 && mg_direct_fits(nx, ny)) break;
         nx /= 2; ny /= 2;
     }
     *nlev = n;
@@ -1131,7 +1267,9 @@ int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre
     const double omc = 2.0 / (1.0 + sin(3.14159265358979323846 / nc));
     const int itc = 2 * nc + 10;
     const int ncell = Lc->nx * Lc->ny;
-    double* Md = ncell <= 64 ? mg_direct_matrix(Lc) : NULL;
+    mg_direct* Dd = mg_direct_fits(Lc->nx, Lc->ny)
+                        ? mg_direct_new(Lc->nx, Lc->ny, Lc->hx, Lc->hy, Lc->cw, Lc->ce, Lc->cs, Lc->cn) : NULL;
+    double* Md = !Dd && ncell <= 64 ? mg_direct_matrix(Lc) : NULL;
     int cycles = 0;
     for (;;) {
         /* down */
@@ -1145,7 +1283,9 @@ int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre
             xf = L[l + 1].x;
             bf = L[l + 1].b;
         }
-        if (Md) {
+        if (Dd) {
+            mg_direct_solve(Dd, L[nl - 1].b, L[nl - 1].x);
+        } else if (Md) {
             for (int r = 0; r < ncell; r++) {
                 double x = 0.0;
                 for (int k = 0; k < ncell; k++) x += Md[(size_t)r * ncell + k] * L[nl - 1].b[k];
@@ -1168,6 +1308,7 @@ int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre
         if (done) break;
     }
     free(Md);
+    mg_direct_free(Dd);
     mg_free(L, nl);
     return cycles;
 }

@@ -110,6 +110,10 @@ void og_mg_restrict(int nx, int ny, const double* hx, const double* hy, const do
                     double shift, double* bc);
 /* phi (nx x ny) += bilinear prolongation of the coarse correction ec (nx/2 x ny/2) */
 void og_mg_prolong(int nx, int ny, const double* ec, double* phi);
+/* the multigrid's exact coarsest-level solve: the first coarse level of <= cells cells (sides
+ * <= 128) ends the hierarchy and is solved by its separable eigen-decomposition (the GPU's
+ * NSGPU_DIRECT_CELLS; default 128^2, 0 = the round-3 hierarchy down to <= 16 cells) */
+void og_mg_set_direct(long cells);
 /* V-cycle solve of L x = rhs - mean(rhs) (rhs is mean-removed in place): RB Gauss-Seidel
  * smoothing (pre/post sweeps), coarsening while both sizes are even, >= 4 and > 16 cells,
  * coarsest level by red-black SOR (2n+10 iterations at the optimal omega); stops when the residual after pre-smoothing is

@@ -40,6 +40,7 @@ _SIG = {
     "og_solve_poisson": (ctypes.c_int, [_P, _D, _D, ctypes.c_double, ctypes.c_int]),
     "og_mg_restrict": (None, [ctypes.c_int, ctypes.c_int, _D, _D, _D, _D, ctypes.c_double, _D]),
     "og_mg_prolong": (None, [ctypes.c_int, ctypes.c_int, _D, _D]),
+    "og_mg_set_direct": (None, [ctypes.c_long]),
     "og_mg_solve": (ctypes.c_int, [_P, _D, _D, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "og_mg_solve_w": (ctypes.c_int, [_P, _D, _D, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_double]),
@@ -66,6 +67,12 @@ def lib():
             f.restype, f.argtypes = r, a
         _lib = L
     return _lib
+
+
+def set_direct_cells(n: int) -> None:
+    """The multigrid's exact coarsest-level solve threshold (the GPU's NSGPU_DIRECT_CELLS; default
+    128^2, 0 = off) -- set both sides alike when a test changes it."""
+    lib().og_mg_set_direct(int(n))
 
 
 def set_threads(n: int) -> None:

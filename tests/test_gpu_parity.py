@@ -362,6 +362,32 @@ def test_mg_poisson_solve_matches_oracle(gpu, nx, ny):
     assert rel(g - g.mean(), xp - xp.mean()) <= 1e-8
 
 
+@pytest.mark.parametrize("direct", [None, "0"])
+@pytest.mark.parametrize("nx,ny", [(64, 64), (256, 256), (512, 128), (96, 48), (100, 60)])
+def test_mg_vcycles_match_oracle_mg(gpu, monkeypatch, direct, nx, ny):
+    """The multigrid solve = the oracle's restatement of the same V(2,2) cycle (og_mg_solve_w, the
+    same hierarchy rule) from zero at rtol 1e-10: the same V-cycle count and the same iterate to
+    1e-9.  Default (r4): the coarsest level is the first coarse one of <= 128^2 cells, solved exactly
+    by its separable eigen-decomposition (k_direct: fp64 MFMA, sides padded to 16 -- 48 x 24 and
+    50 x 30 here); NSGPU_DIRECT_CELLS=0: round 3's LDS V-cycle down to <= 16 cells."""
+    import oracle as O
+    if direct is not None:
+        monkeypatch.setenv("NSGPU_DIRECT_CELLS", direct)
+    O.set_direct_cells(128 * 128 if direct is None else int(direct))
+    try:
+        rng = np.random.default_rng(23)
+        og, gs = pair(gpu, nx, ny, 1e-3, 100.0, poisson=gpu.NS_POISSON_MG, rtol=1e-10)
+        b = rand(rng, nx * ny, 100.0)
+        gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny)); gs.set(gpu.NS_ARR_RPHI, b)
+        its = gs.kernel(gpu.NS_K_POIS_SOLVE)[0]
+        x, cyc = og.mg_solve(b, rtol=1e-10, omega=gs.mg_omega)
+        assert its == cyc, (its, cyc)
+        g = gs.get(gpu.NS_ARR_PHI).ravel()
+        assert rel(g - g.mean(), x - x.mean()) <= 1e-9
+    finally:
+        O.set_direct_cells(128 * 128)
+
+
 @pytest.mark.parametrize("solver", ["rbsor", "jacobi_small"])
 def test_full_steps_other_poisson_solvers(gpu, solver):
     n, steps, re = 16 if solver == "jacobi_small" else 32, 8, 100.0
@@ -704,26 +730,34 @@ def test_outflow_line_preconditioner(gpu, monkeypatch, nx, ny, bc, xr, yr):
     preconditioned by the outflow side's 1-D line solve (the linear-extrapolation closure's
     decoupled column), extended along x as the initial iterate of a V-cycle whose hierarchy closes
     that side by face-Dirichlet data.  From a random rhs on these anisotropic /
-    graded grids it reaches the oracle's direct solve of the same mean-projected system (1e-8
-    relative, phi modulo its mean) in fewer iterations than the round-1 wall-closure V-cycle
-    (NSGPU_OUTFLOW_PC=wall) and in at most 25 (square cells: test_outflow_channel_steps)."""
+    graded grids it converges (rtol 1e-8) in fewer iterations than the round-1 wall-closure V-cycle
+    (NSGPU_OUTFLOW_PC=wall) and in at most 25 (square cells: test_outflow_channel_steps); at rtol
+    1e-11 it reaches the oracle's direct solve of the same mean-projected system to 1e-8 relative
+    (phi modulo its mean)."""
     rng = np.random.default_rng(12)
     its = {}
+    b = rand(rng, nx * ny, 100.0)
     for pc in ("line", "wall"):
         monkeypatch.setenv("NSGPU_OUTFLOW_PC", pc)
         og, gs = pair(gpu, nx, ny, 1.0 / 256, 100.0, bc, xr, yr, rtol=1e-8)
-        b = rand(rng, nx * ny, 100.0)
         gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny)); gs.set(gpu.NS_ARR_RPHI, b)
         n, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
         its[pc] = n
         assert res <= 1e-8, (pc, n, res)
-        if pc == "line":
-            xp, _ = og.solve_poisson(b)
-            g = gs.get(gpu.NS_ARR_PHI).ravel()
-            err = float(rel(g - g.mean(), xp - xp.mean()))
-            assert err <= 1e-6, (err, n)
         gs.close()
     assert its["line"] <= 25, its
+    # the solution: the line-closure solve at rtol 1e-11 against the oracle's direct solve (the
+    # error of a residual-converged iterate grows with the condition number of these anisotropic
+    # grids: rtol 1e-8 left 1.1e-6 at 512 x 128)
+    monkeypatch.setenv("NSGPU_OUTFLOW_PC", "line")
+    og, gs = pair(gpu, nx, ny, 1.0 / 256, 100.0, bc, xr, yr, rtol=1e-11)
+    gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny)); gs.set(gpu.NS_ARR_RPHI, b)
+    n, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+    xp, _ = og.solve_poisson(b)
+    g = gs.get(gpu.NS_ARR_PHI).ravel()
+    err = float(rel(g - g.mean(), xp - xp.mean()))
+    assert err <= 1e-8, (err, n)
+    gs.close()
     assert its["line"] < its["wall"], its
 
 

@@ -50,8 +50,23 @@ def per_dispatch(d, counter, pat):
     return [v for g, v in rows if g == gmax]
 
 
+def _sha16(path):
+    import hashlib
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+import os
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 res = {"n": n, "kernels": {},
-       "note": "median over the finest-level dispatches; FETCH_SIZE x2 (gfx950 wide-stream correction), KiB -> bytes"}
+       "note": "median over the finest-level dispatches; FETCH_SIZE x2 (gfx950 wide-stream correction), KiB -> bytes",
+       # the stamp bench.py copies into each roofline.traffic: which run and which library measured it
+       "source": {"fetch_dir": fetch_dir, "write_dir": write_dir,
+                  "command": os.environ.get("PMC_COMMAND", "rocprofv3 --pmc FETCH_SIZE (then WRITE_SIZE) -- "
+                                            "python3 bench.py --steps 3 --warmup 1 --no-cpu"),
+                  "libnsgpu_sha16": _sha16(os.path.join(ROOT, "navierstokessolver_amd", "libnsgpu.so"))}}
 for spec in sys.argv[5:]:
     key, rx, bpc = spec.split("=")
     pat = re.compile(rx)
