@@ -9,7 +9,15 @@ dt = 1/(8n)), inputs resident in HBM.  N > 1: x-slabs, one rank per GPU, RCCL ha
 (strong scaling: the global grid is fixed).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--re 1000] [--no-cpu]
-  (N > 1 under torch.distributed.run; RANK / WORLD_SIZE / LOCAL_RANK from the env)
+                  [--transport rccl|host]
+  (N > 1 under torch.distributed.run; RANK / WORLD_SIZE / LOCAL_RANK from the env; without a
+  launcher, --gpus N starts its own N ranks and relays rank 0's JSON line)
+
+--transport host (or NSBENCH_TRANSPORT=host): the N > 1 branch as a rehearsal on ONE GPU -- every
+rank on device 0, the ghost rows / gathers / reductions through the host (gloo) instead of RCCL
+(libnsgpu.so's ns_host_transport call sites).  The line is then functional evidence for the
+multi-rank path (self-launch, slab step, per-rank timing max, local-cell rooflines, rank-0 JSON),
+not a scaling number: `config.transport` says so.
 
 --case channel (not the headline line): the n x n/4
 channel (square cells h = 4/n, inlet W, walls S / N, the reference's NEUMANN outflow E,
@@ -44,6 +52,11 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level 
 KERNELS = {
     "restrict": ("k_sweep2<Poisson, FUSE_R> (finest pre-smoothing pass: 2 RB sweeps + residual + restriction)", 26),
     "prolong": ("k_sweep2<Poisson, FUSE_P> (finest post-smoothing pass: prolongation + 2 RB sweeps + output residual)", 26),
+    # (r4) a V-cycle boundary in one pass, when the cycle's output is not checked: the prolongation
+    # + 4 RB sweeps + residual + restriction (k_sweep4): read phi 8 + b 8 + the coarse correction
+    # 8 / 4, write phi 8 + the coarse rhs 8 / 4 = 28
+    "cycle": ("k_sweep4 (finest V-cycle boundary: prolongation + 4 RB sweeps + residual + restriction, "
+              "cycle c's FUSE_P and cycle c+1's FUSE_R in one pass)", 28),
     "helmholtz": ("Helmholtz pass of one velocity component of (I - a L_V) u* = RHS (k_sweep3 + residual stage: "
                   "3 RB-SOR sweeps, after the wall bands; or k_sweep2: 2 sweeps; the one-rank two-field "
                   "k_sweep3<FUSE_UV> launch counts as two component passes)", 24),
@@ -55,7 +68,7 @@ JACOBI32_LABEL = "k_jacobi_s<float> (one Jacobi sweep on fp32 phi, b; fp64 arith
 SWEEP32_BYTES_PER_CELL = 12
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -67,10 +80,13 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--sync-monitor", action="store_true",
                     help="ns_step (host sync at every step's end) instead of ns_step_async")
+    ap.add_argument("--transport", choices=("rccl", "host"), default=os.environ.get("NSBENCH_TRANSPORT", "rccl"),
+                    help="N > 1: RCCL over xGMI (one GPU per rank), or the host transport (every rank on GPU 0: "
+                         "a one-GPU rehearsal of the multi-rank path)")
     ap.add_argument("--time-every", type=int, default=10,
                     help="HIP-event kernel timing on every k-th timed step (each event pair costs a few us of "
                          "GPU idle; 0 = none)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def _sha16(path):
@@ -184,15 +200,33 @@ def self_launch(args) -> int:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)]
     env = dict(os.environ)
+    # this run's arguments travel in the environment: torch.distributed.run's own parser takes an
+    # abbreviation of its options after the script name as its own (--n: ambiguous, --re: --redirects)
+    env["NSBENCH_ARGV"] = json.dumps(sys.argv[1:])
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this pool (RCCL)
     env.setdefault("OMP_NUM_THREADS", "1")
-    return subprocess.call(cmd, env=env)
+    # relay: only whole JSON lines (rank 0's bench line; the launch probe's) reach stdout;
+    # everything else the ranks or RCCL print goes to stderr, so no banner can precede or split
+    # the line
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    for ln in p.stdout:
+        t = ln.strip()
+        if t.startswith("{"):
+            try:
+                json.loads(t)
+                print(t, flush=True)
+                continue
+            except ValueError:
+                pass
+        sys.stderr.write(ln)
+    return p.wait()
 
 
 def main():
-    args = parse()
+    argv = json.loads(os.environ["NSBENCH_ARGV"]) if "NSBENCH_ARGV" in os.environ and "WORLD_SIZE" in os.environ else None
+    args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args))
     rank = int(os.environ.get("RANK", "0"))
@@ -202,20 +236,26 @@ def main():
         world = max(world, 1)
     if os.environ.get("NSBENCH_LAUNCH_PROBE"):
         # (tests/test_bench_launch.py: the self-launch reached every rank; nothing touches a GPU)
-        print(json.dumps({"probe_rank": rank, "world": world, "local_rank": local}), flush=True)
+        print(json.dumps({"probe_rank": rank, "world": world, "local_rank": local, "n": args.n, "re": args.re}),
+              flush=True)
         return
     import torch
     import torch.distributed as dist
 
     import navierstokessolver_amd as nsa
 
-    nccl_id = None
+    nccl_id = xport = None
+    host = world > 1 and args.transport == "host"
     if world > 1:
         # gloo carries only the bootstrap (RCCL unique id), the barrier and the timing max;
         # the data path (ghost rows, residual / mean / min-max reductions) is RCCL in libnsgpu.so
-        from navierstokessolver_amd.dist import nccl_id as make_nccl_id
+        # -- or, --transport host, the same call sites through gloo on the host
+        from navierstokessolver_amd.dist import TorchHostTransport, nccl_id as make_nccl_id
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        nccl_id = make_nccl_id(dist)
+        if host:
+            xport = TorchHostTransport(dist)
+        else:
+            nccl_id = make_nccl_id(dist)
 
     n, re = args.n, args.re
     channel = args.case == "channel"
@@ -226,9 +266,10 @@ def main():
     else:
         nyc, dt = n, 1.0 / (8 * n)
         grid = nsa.cavity(n)
-    torch.cuda.set_device(local)
-    solver = nsa.GpuSolver(grid, dt, re, rtol=args.rtol, device=local, timing=True,
-                           rank=rank, nranks=world, nccl_id=nccl_id)
+    device = 0 if host else local   # (the host transport's rehearsal: every rank on the one GPU)
+    torch.cuda.set_device(device)
+    solver = nsa.GpuSolver(grid, dt, re, rtol=args.rtol, device=device, timing=True,
+                           rank=rank, nranks=world, nccl_id=nccl_id, host_transport=xport)
 
     def barrier():
         if world > 1:
@@ -268,13 +309,15 @@ def main():
     local_cells = (solver.i1 - solver.i0) * nyc
     timed = {"prolong": (sum(s["t_poisson_kernel_ms"] for s in stats), sum(s["n_poisson_kernels"] for s in stats)),
              "restrict": (sum(s["t_restrict_kernel_ms"] for s in stats), sum(s["n_restrict_kernels"] for s in stats)),
-             "helmholtz": (sum(s["t_helm_kernel_ms"] for s in stats), sum(s["n_helm_kernels"] for s in stats))}
+             "helmholtz": (sum(s["t_helm_kernel_ms"] for s in stats), sum(s["n_helm_kernels"] for s in stats)),
+             "cycle": (sum(s["t_cycle_kernel_ms"] for s in stats), sum(s["n_cycle_kernels"] for s in stats))}
     # finest-level sweeps: V(2,2) per cycle (the convergence check rides on each cycle's last pass)
     fine_sweeps = 4 * cycles
     # whole-step algorithmic bytes per cell: K1 64 + K3 24 + K5 40 + the phi
     # extrapolation 32 or 40; Helmholtz 24 per pass of one component (a pass = 2 or 3 sweeps: see
     # helm_passes); multigrid per solve `cycles` FUSE_R and `cycles` FUSE_P passes at 26 each on
-    # the finest level, x 4/3 for the coarser levels (each a quarter of the one above)
+    # the finest level (less the fused boundaries below), + 1/3 of that for the coarser levels
+    # (each a quarter of the one above)
     min_rows = min(b - a for a, b in (nsa._lib.slab_range(n, world, r) for r in range(world)))
     hpasses = sum(helm_passes(int(s["it_u"]), min_rows) for s in stats)
     # the phi extrapolation: cubic (4 planes read + 1 written = 40 B/cell) after a solve that
@@ -285,8 +328,14 @@ def main():
     # the Helmholtz wall bands (two k_helm_band launches) on the cells within 128 of a wall:
     # per launch u, v read 16 + rhs 16 + write 16 -> 96 B per band cell
     band_frac = 1.0 - max(n - 256, 0) * max(nyc - 256, 0) / float(n * nyc)
+    # the finest level: a V-cycle whose output is not checked hands its prolongation pass to the next
+    # cycle's restriction pass (one k_sweep4 pass of 28 B/cell instead of 26 + 26): cycles - checks
+    # such boundaries per solve (one rank, multigrid)
+    fused = sum(max(0, int(s["it_phi"]) - int(s["n_checks"])) for s in stats) if (world == 1 and not channel) else 0
+    if not any(s["n_cycle_kernels"] for s in stats) and args.time_every:
+        fused = 0   # (NSGPU_FUSE4=0: no boundary pass was timed, none ran)
     step_bpc = (64 + 24 + 40 + extrap_bpc + 2 * 24 * hpasses / K + 96 * band_frac
-                + (26 * cycles + 26 * cycles) / K * 4.0 / 3.0)
+                + (52 * (cycles - fused) + 28 * fused) / K + 52 * cycles / K / 3.0)
     if channel:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications
         # of (line extension 8 + FUSE_R 28 + FUSE_P 26, x 4/3 for the coarser levels) = 80 each,
@@ -299,7 +348,7 @@ def main():
     # 10 warm-up + 50 timed launches, HIP events), single rank only
     jacobi = jacobi32 = None
     if world == 1 and not channel:
-        js = nsa.GpuSolver(nsa.cavity(n), dt, re, poisson=nsa.NS_POISSON_JACOBI, omega=1.0, device=local)
+        js = nsa.GpuSolver(nsa.cavity(n), dt, re, poisson=nsa.NS_POISSON_JACOBI, omega=1.0, device=device)
         js.fill_random(0x5EED)
         t = js.time_poisson(10, 50)
         jacobi = t["avg_ms"] * 1e-3
@@ -366,7 +415,12 @@ def main():
                                (f"{n}x{n} lid-driven cavity, Re={re:g}, dt=1/{8 * n}, fp64, multigrid Poisson "
                                 f"(RB-GS smoother) + RB-SOR Helmholtz, both to rtol {args.rtol:g}"),
                    "case": args.case, "nx": n, "ny": nyc, "re": re, "dt": dt, "parallelism": f"x-slab x{world}",
-                   "step_api": "ns_step" if args.sync_monitor else "ns_step_async"},
+                   "step_api": "ns_step" if args.sync_monitor else "ns_step_async",
+                   "transport": ("none (one rank)" if world == 1 else
+                                 "RCCL over xGMI, one GPU per rank" if not host else
+                                 f"host (gloo): a rehearsal of the multi-rank path with all {world} ranks on one GPU "
+                                 "-- functional evidence, not a scaling number"),
+                   "local_rows_rank0": solver.i1 - solver.i0},
         "monitor_last_step": {k: last_monitor[k] for k in ("umin", "umax", "vmin", "vmax")},
         ("poisson_bicgstab_its_per_s" if channel else "poisson_vcycles_per_s"): cycles / elapsed,
         ("poisson_bicgstab_its_per_step" if channel else "poisson_vcycles_per_step"): cycles / K,
@@ -405,7 +459,9 @@ def main():
             line["parity_vs_oracle"] = line["cpu_baseline"].get("parity")
         except Exception as e:  # the baseline must never hide the GPU line
             line["cpu_baseline"] = {"error": repr(e)}
-    print(json.dumps(line), flush=True)
+    # one write: the line cannot be split by other output of this process
+    sys.stdout.write("\n" + json.dumps(line) + "\n")
+    sys.stdout.flush()
 
 
 if __name__ == "__main__":

@@ -33,11 +33,13 @@
 extern "C" {
 #endif
 
-#define NSGPU_ABI_VERSION 5   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
+#define NSGPU_ABI_VERSION 6   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
                                  3: ns_get/set_fields in compact-id order on polygons, ns_local_cells;
                                  4: NS_POISSON_MG is 0, so a zero-initialised ns_params selects the
                                     multigrid (RB-SOR moved to 3; the value 2 is rejected);
-                                 5: ns_stats.x_link_bytes appended */
+                                 5: ns_stats.x_link_bytes appended;
+                                 6: ns_stats.t_cycle_kernel_ms / n_cycle_kernels appended (the
+                                    finest level's V-cycle-boundary passes) */
 
 typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm */
 
@@ -142,6 +144,10 @@ typedef struct ns_stats {
     double  x_link_bytes;            /* bytes this rank sends over its busiest peer link in the step
                                       * (one side's ghost rows of every exchange + its slab of every
                                       * agglomeration gather; multi-rank / loopback) */
+    double  t_cycle_kernel_ms;       /* multigrid, one rank: sum of the finest level's V-cycle-boundary
+                                      * pass durations (k_sweep4: cycle c's prolongation + 2 sweeps and
+                                      * cycle c+1's 2 sweeps + restriction in one pass; timing == 1) */
+    int32_t n_cycle_kernels;         /* number of those passes timed */
 } ns_stats;
 
 /* device arrays addressable by ns_get_array / ns_set_array */

@@ -134,6 +134,13 @@ int launch_pois_residual(const Geo& g, const Coef& c, const double* phi, const d
 // K5: u = u* - dt grad phi ; min/max partials (4 per block)
 int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, const double* vs, double* u, double* v,
                    const double* phi, double* part, hipStream_t st);
+// K5 takes the streaming strips here (a rectangle without a NEUMANN side)
+bool correct_streams(const Geo& g);
+// K5 + the next step's Poisson guess in the same pass (k_cell_s<6>): gout = gc[0] phi + gc[1] h1
+// + gc[2] h2 + gc[3] h3 (h2 / h3 may be null) -- k_axpby's combination; -1 where K5 does not stream
+int launch_correct_guess(const Geo& g, const Coef& c, double dt, const double* us, const double* vs, double* u,
+                         double* v, const double* phi, double* part, const double* h1, const double* h2,
+                         const double* h3, const double* gc, double* gout, hipStream_t st);
 // reductions: sum `nv` interleaved values over n partials (p[k*nv + v]) -> out[v]
 void launch_reduce_sum(const double* p, int n, int nv, double* out, hipStream_t st);
 // nseg contiguous segments of n partials -> out[0..nseg) (k_reduce_sum's order per segment)
@@ -187,6 +194,12 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
                                const double* rp, const double* shift, const Geo& gc, const double* ec,
                                double* part, hipStream_t st);
 
+// a V-cycle boundary in one pass (k_sweep4, r4): FUSE_P of cycle c and FUSE_R of cycle c + 1 --
+// phi + P(ec) enters four RB sweeps -> out, whose residual is restricted into bc (+ pc := 0 unless
+// null) with r^2 partials; the same values as the two passes.  A whole level (one rank), -1 otherwise
+int launch_pois_sweep4(const Geo& g, const Coef& c, double omega, const double* phi, double* out, const double* rp,
+                       const double* shift, const Geo& gc, const double* ec, double* bc, double* pc, double* part,
+                       hipStream_t st);
 // the same two passes as LDS-tiled kernels for the latency-bound small levels (one load
 // round per pass instead of a row pipeline); same results
 int launch_pois_tile2_restrict(const Geo& g, const Coef& c, double omega, const double* phi, double* out,

@@ -1637,6 +1637,11 @@ struct CellStreamArgs {
     double* part;
     int nsj;
     RowPlan P;                    // strip rows of this launch (plan_rows)
+    // K6 = K5 + the next step's Poisson guess (r4): gout = gc0 phi + gc1 h1 + gc2 h2 + gc3 h3 (the
+    // phi extrapolation, k_axpby's arithmetic), h2 / h3 null when unused
+    const double *h1, *h2, *h3;
+    double* gout;
+    double gc0, gc1, gc2, gc3;
 };
 
 // one face value along a line: interior r-weighted interpolation, or the wall's (q + ghost)/2
@@ -1644,7 +1649,20 @@ __device__ __forceinline__ double face_val(double q, double qn, bool has, double
     return has ? qn * r + q * (1 - r) : 0.5 * (q + ghost);
 }
 
-template <int K>   // 3: divergence, 5: correction, 7: Poisson apply
+// the phi extrapolation's combination, in one order for k_axpby and K6 (bit-identical guesses)
+__device__ __forceinline__ double extrap_comb(double a, double x, double b, double y, double c, const double* z,
+                                              double zv, double d, const double* w, double wv) {
+    double r = fma(b, y, a * x);
+    if (z) r = fma(c, zv, r);
+    if (w) r = fma(d, wv, r);
+    return r;
+}
+
+// K6's rows in flight (A/B: make variant DEFS=-DK6_SD=n)
+#ifndef K6_SD
+#define K6_SD 2
+#endif
+template <int K>   // 3: divergence, 5: correction, 6: correction + the next Poisson guess, 7: Poisson apply
 __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
     const Geo& g = A.g;
     const Coef& c = A.c;
@@ -1655,8 +1673,10 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
     // the strip's partial slot: pbase + run, or (pbase < 0: K3's fixed strips) the strip-row index
     const int srow = A.P.pbase >= 0 ? A.P.pbase + run : (run < A.P.slo ? run : A.P.rb1 / A.P.L + (run - A.P.slo));
     const int wid = srow * A.nsj + (w - run * A.nsj);
+    constexpr bool K5 = K == 5 || K == 6;
+    constexpr int SDK = K == 6 ? K6_SD : SD;   // rows in flight (K6 streams six planes)
     double acc[4] = {0.0, 0.0, INFINITY, INFINITY};   // K3: sum, sum^2; K5: (umin, -umax, vmin, -vmax)
-    if (K == 5) acc[0] = acc[1] = INFINITY;
+    if (K5) acc[0] = acc[1] = INFINITY;
     if (w < nstr) {
         const int sj = w - run * A.nsj;
         int ib, ie;
@@ -1679,19 +1699,27 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
         // window field (K3: u; K5: phi) at rows ib-1 .. ie, row fields (K3: v; K5: u*, v*) at
         // row r-1 when row r arrives (prefetch overruns clamped onto fetched rows)
         double2 W0 = {0, 0}, W1 = {0, 0}, W2 = {0, 0};
-        double2 Q[SD], X[SD], Y[SD];
-        auto load = [&](int r, double2& q, double2& x, double2& y) {
+        double2 Q[SDK], X[SDK], Y[SDK];
+        constexpr int SH = K == 6 ? SDK : 1;   // K6: the history planes' rows, prefetched alike
+        double2 H1[SH], H2[SH], H3[SH];
+        auto load = [&](int r, double2& q, double2& x, double2& y, double2& h1, double2& h2, double2& h3) {
             const int lw = min(max(r, max(ib - 1, rlo)), min(ie, rhi));
             const int lr = min(max(r - 1, ib), ie - 1);
             q = *reinterpret_cast<const double2*>(A.a0 + (ptrdiff_t)lw * ld + lc);
             if (K == 3 || (K == 7 && A.a1)) {
                 x = *reinterpret_cast<const double2*>(A.a1 + (ptrdiff_t)lr * ld + lc);
-            } else if (K == 5) {
+            } else if (K5) {
                 x = *reinterpret_cast<const double2*>(A.a1 + (ptrdiff_t)lr * ld + lc);
                 y = *reinterpret_cast<const double2*>(A.a2 + (ptrdiff_t)lr * ld + lc);
             }
+            if (K == 6) {
+                h1 = *reinterpret_cast<const double2*>(A.h1 + (ptrdiff_t)lr * ld + lc);
+                if (A.h2) h2 = *reinterpret_cast<const double2*>(A.h2 + (ptrdiff_t)lr * ld + lc);
+                if (A.h3) h3 = *reinterpret_cast<const double2*>(A.h3 + (ptrdiff_t)lr * ld + lc);
+            }
         };
-        auto step = [&](const double2 q, const double2 x, const double2 y, int r) {
+        auto step = [&](const double2 q, const double2 x, const double2 y, const double2 h1, const double2 h2,
+                        const double2 h3, int r) {
             W0 = W1; W1 = W2; W2 = q;
             const int m = r - 1;
             if (m < ib || m >= ie) return;
@@ -1775,6 +1803,14 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                     A.o0[(ptrdiff_t)m * ld + c0] = un[0];
                     A.o1[(ptrdiff_t)m * ld + c0] = vn[0];
                 }
+                if (K == 6) {
+                    // the next step's Poisson guess from this step's phi (the window's row m) and the
+                    // history rows -- extrapolate_phi's combination, which then only rotates planes
+                    const double g0 = extrap_comb(A.gc0, W1.x, A.gc1, h1.x, A.gc2, A.h2, h2.x, A.gc3, A.h3, h3.x);
+                    const double g1 = extrap_comb(A.gc0, W1.y, A.gc1, h1.y, A.gc2, A.h2, h2.y, A.gc3, A.h3, h3.y);
+                    if (wr && v1) st_stream(A.gout + (ptrdiff_t)m * ld + c0, make_double2(g0, g1), false);
+                    else if (wr) A.gout[(ptrdiff_t)m * ld + c0] = g0;
+                }
 #pragma unroll
                 for (int e = 0; e < 2; e++) {
                     if (!(e ? o1 : o0)) continue;
@@ -1788,22 +1824,22 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
         };
         const int r0 = ib - 1, r1 = ie;
 #pragma unroll
-        for (int q = 0; q < SD; q++) load(r0 + q, Q[q], X[q], Y[q]);
-        for (int r = r0; r <= r1; r += SD) {
+        for (int q = 0; q < SDK; q++) load(r0 + q, Q[q], X[q], Y[q], H1[q % SH], H2[q % SH], H3[q % SH]);
+        for (int r = r0; r <= r1; r += SDK) {
 #pragma unroll
-            for (int q = 0; q < SD; q++) {
-                if (r + q <= r1) step(Q[q], X[q], Y[q], r + q);
-                load(r + q + SD, Q[q], X[q], Y[q]);
+            for (int q = 0; q < SDK; q++) {
+                if (r + q <= r1) step(Q[q], X[q], Y[q], H1[q % SH], H2[q % SH], H3[q % SH], r + q);
+                load(r + q + SDK, Q[q], X[q], Y[q], H1[q % SH], H2[q % SH], H3[q % SH]);
             }
         }
     }
-    constexpr int NV = K == 5 ? 4 : 2;
+    constexpr int NV = K5 ? 4 : 2;
 #pragma unroll
     for (int k = 0; k < NV; k++)
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             const double o = __shfl_xor(acc[k], off, 64);
-            acc[k] = K == 5 ? fmin(acc[k], o) : acc[k] + o;
+            acc[k] = K5 ? fmin(acc[k], o) : acc[k] + o;
         }
     if (lane == 0 && w < nstr)
 #pragma unroll
@@ -2454,6 +2490,201 @@ __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) { sweep2_body<OP, 
 template <bool RES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_sweep2_fp4(StreamArgs a) {
     sweep2_body<0, RES, FUSE_P>(a);
+}
+
+// ------------------------------------------------ K4: a V-cycle boundary in one HBM pass (r4)
+// Between two V-cycles the finest level runs FUSE_P of cycle c (prolongation + 2 RB sweeps) and
+// then FUSE_R of cycle c + 1 (2 RB sweeps + residual + restriction): two passes over phi and b
+// (~90 us each at 4096^2), latency-bound rather than bandwidth-bound.  When cycle c's output is not
+// checked (the solver predicts the check point), k_sweep4 does both in ONE pass: the prolongation
+// on each row entering the pipeline, eight stages (red / black of four sweeps), the output stored
+// after the eighth and the residual of the finished rows restricted in row pairs into the coarse
+// rhs -- k_sweep2<FUSE_P>'s input stage and k_sweep2<FUSE_R>'s output stages around k_sweep2's
+// stages, the same arithmetic in the same order, so bit-identical to the two passes.  Walks
+// downwards (FUSE_R's restriction sums must not depend on the walk); one rank / replicated levels
+// only (the cone reads 9 rows beyond the strip: more than HALO; walls clamp onto ghost rows).
+// Strips: 108 written columns of 128 (prolongation 1 + 8 stages + residual 1 on each side).
+constexpr int SW4 = 108;
+constexpr int RC_OFF4 = 9;               // table row of strip row ib: stage 1 reads rows ib-8 .. ie+7
+constexpr int L4_MAX = 128;
+constexpr int RC_MAX4 = L4_MAX + 2 * RC_OFF4;
+#ifndef SD4
+#define SD4 2                            // rows in flight
+#endif
+template <bool UNI>
+__device__ __forceinline__ double sweep4_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
+                                               int lane) {
+    double res = 0.0;
+    const int jb = sj * SW4;
+    const int ny = a.ny, ld = a.ld;
+    const int c0 = jb - 10 + 2 * lane, c1 = c0 + 1;
+    const int lc = min(max(c0, 0), ld - 2);
+    const bool v0 = c0 >= 0 && c0 < ny, v1 = c1 >= 0 && c1 < ny;
+    const bool wr = lane >= 5 && lane <= 58 && c0 < ny;
+    const bool o0 = wr && v0, o1 = wr && v1;
+    const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c1, 0), ny - 1);
+    const double cs0 = a.cs[k0], cn0 = a.cn[k0], cd0 = cs0 + cn0;
+    const double cs1 = a.cs[k1], cn1 = a.cn[k1], cd1 = cs1 + cn1;
+    const double shift = a.shift ? a.shift[0] : 0.0;
+    const double omega = a.omega;
+    const int rlo = -HALO, rhi = a.nxl + HALO - 1;
+    const int rb = __builtin_amdgcn_readfirstlane(ib);
+    const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + (ptrdiff_t)rb * ld, (short)0, (int)((unsigned)a.L * ld * 8u), 0x00020000);
+    double2 Q[SD4], QB[SD4];
+    double QE[SD4];
+    // phi rows ib-9 .. ie+8 and b rows ib-8 .. ie+7 are read (the rest clamp onto fetched rows)
+    const int r0 = ib - 9, r1 = ie + 8;
+    const int phi_lo = rlo, phi_hi = min(r1, rhi);
+    const int b_lo = max(ib - 8, rlo), b_hi = rhi;
+    const int Jc = c0 >> 1;
+    const int Jl = min(max(Jc, 0), a.ncy - 1);
+    const bool jm_ok = Jc - 1 >= 0, jp_ok = Jc + 1 < a.ncy;
+    auto nbr = [&](int lp) {
+        const int I = lp >> 1;
+        const int In = (lp & 1) ? I + 1 : I - 1;
+        return (a.ci0 + In < 0 || a.ci0 + In >= a.ncx) ? I : In;
+    };
+    auto load = [&](int slot_r, double2& p, double2& bb, double& ee) {
+        const int lp = min(max(slot_r, phi_lo), phi_hi), lb = min(max(slot_r - 1, b_lo), b_hi);
+        p = ld_stream(a.in + (ptrdiff_t)lp * ld + lc, 1);
+        bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
+        ee = a.ec[(ptrdiff_t)nbr(lp) * a.ldc + Jl];
+    };
+    // windows of the nine stages' inputs (3 rows each), rhs rows r-1 .. r-9
+    double2 W[9][3];
+#pragma unroll
+    for (int s = 0; s < 9; s++) W[s][0] = W[s][1] = W[s][2] = make_double2(0.0, 0.0);
+    double2 B[9];
+#pragma unroll
+    for (int s = 0; s < 9; s++) B[s] = make_double2(0.0, 0.0);
+    const double hy0 = a.hy[k0], hy1 = a.hy[k1];
+    double xs = 0.0, hxe = 0.0;
+    const DiagC dcc = UNI ? diag_cache<0>(rc[RC_OFF4 + ((ie - ib) >> 1)], cd0, cd1, 0.0, omega) : DiagC{};
+    auto half = [&](const double2& W0, const double2& W1, const double2& W2, const double2& Bv, int row,
+                    int par) -> double2 {
+        double2 o = W1;
+        const int gi = a.i0 + row;
+        const double* rw = rc[min(max(row - ib + RC_OFF4, 0), RC_MAX4 - 1)];
+        const double cw = UNI ? dcc.cw : rw[0], ce = UNI ? dcc.ce : rw[1];
+        double rr;
+        const bool in = gi >= 0 && gi < a.nx;
+        if ((gi & 1) == par) {
+            const double lf = lane_up1(W1.y);
+            double d, w;
+            diag_w<0, UNI>(dcc, 0, rw[2], cd0, 0.0, omega, d, w);
+            const double n = keep(relax<0>(W1.x, W0.x, W2.x, lf, W1.y, Bv.x, cw, ce, cs0, cn0, d, w, 0.0, rr));
+            o.x = (in && v0) ? n : W1.x;
+        } else {
+            const double rt = lane_dn1(W1.x);
+            double d, w;
+            diag_w<0, UNI>(dcc, 1, rw[2], cd1, 0.0, omega, d, w);
+            const double n = keep(relax<0>(W1.y, W0.y, W2.y, W1.x, rt, Bv.y, cw, ce, cs1, cn1, d, w, 0.0, rr));
+            o.y = (in && v1) ? n : W1.y;
+        }
+        return o;
+    };
+    double2 ep = {0, 0};   // (e(I), e(In)) of the previous row of the walk (k_sweep2<FUSE_P>)
+    auto step = [&](double2 p, const double2 bb, const double ce, int r) {
+        {
+            // phi += P(e) on the entering row (k_sweep2<FUSE_P>'s input stage, walking down)
+            const bool fresh = (r & 1) != 0, wall = nbr(r) == (r >> 1);
+            const double2 ee = fresh ? make_double2(ep.x, ce) : make_double2(ep.y, wall ? ep.y : ep.x);
+            ep = ee;
+            const double ey = (wall && (a.dsx & ((r & 1) ? 2 : 1))) ? -ee.y : ee.y;
+            double m0 = lane_up1(ee.x), m1 = lane_up1(ey);
+            double q0 = lane_dn1(ee.x), q1 = lane_dn1(ey);
+            if (!jm_ok) { m0 = ee.x; m1 = ey; }
+            if (!jp_ok) { q0 = ee.x; q1 = ey; }
+            if (a.i0 + r >= 0 && a.i0 + r < a.nx) {
+                p.x += (9.0 * ee.x + 3.0 * ey + 3.0 * m0 + m1) * 0.0625;
+                p.y += (9.0 * ee.x + 3.0 * ey + 3.0 * q0 + q1) * 0.0625;
+            }
+        }
+#pragma unroll
+        for (int s = 8; s > 0; s--) B[s] = B[s - 1];
+        B[0] = make_double2(bb.x - shift, bb.y - shift);
+        W[0][0] = W[0][1]; W[0][1] = W[0][2]; W[0][2] = p;
+        // stages 1 .. 8 at rows r-1 .. r-8 (red, black, ...): stage s reads window s-1, writes window s
+#pragma unroll
+        for (int s = 1; s <= 8; s++) {
+            const double2 n = half(W[s - 1][0], W[s - 1][1], W[s - 1][2], B[s - 1], r - s, (s + 1) & 1);
+            W[s][0] = W[s][1]; W[s][1] = W[s][2]; W[s][2] = n;
+        }
+        // the eighth stage's row r-8 is the pass's output (strip rows only; else the offset drops it)
+        const int k = r - 8;
+        const double2 n8 = W[8][2];
+        const unsigned off = (k >= ib && k < ie && wr) ? ((unsigned)(k - rb) * (unsigned)ld + (unsigned)c0) * 8u : OOB;
+        const nsu4 d = {(unsigned)__double2loint(n8.x), (unsigned)__double2hiint(n8.x),
+                        (unsigned)__double2loint(n8.y), (unsigned)__double2hiint(n8.y)};
+        __builtin_amdgcn_raw_buffer_store_b128(d, out, (int)off, 0, 2);
+        // residual of the finished row r-9, restricted in row pairs (k_sweep2<FUSE_R>'s fifth stage)
+        const int m9 = r - 9;
+        if (m9 >= ib && m9 < ie) {
+            const double2 F1 = W[8][1], Fm = W[8][0], Fp = W[8][2];
+            const double lf = lane_up1(F1.y), rt = lane_dn1(F1.x);
+            const double* rw = rc[m9 - ib + RC_OFF4];
+            const double cw = UNI ? dcc.cw : rw[0], ce = UNI ? dcc.ce : rw[1], hxr = UNI ? dcc.hx : rw[3];
+            const double d0 = UNI ? dcc.d0 : diag<0>(rw[2], cd0, 0.0), d1 = UNI ? dcc.d1 : diag<0>(rw[2], cd1, 0.0);
+            double q0, q1;
+            relax<0>(F1.x, Fm.x, Fp.x, lf, F1.y, B[8].x, cw, ce, cs0, cn0, d0, 0.0, 0.0, q0);
+            relax<0>(F1.y, Fm.y, Fp.y, F1.x, rt, B[8].y, cw, ce, cs1, cn1, d1, 0.0, 0.0, q1);
+            res += (o0 ? q0 * q0 : 0.0) + (o1 ? q1 * q1 : 0.0);
+            if (((a.i0 + m9) & 1) == 0) {
+                xs = (hxr * hy0) * q0;
+                xs = xs + (hxr * hy1) * q1;
+                hxe = hxr;
+            } else {
+                xs = xs + (hxr * hy0) * q0;
+                xs = xs + (hxr * hy1) * q1;
+                if (wr) {
+                    const ptrdiff_t o = (ptrdiff_t)(m9 >> 1) * a.ldc + (c0 >> 1);
+                    a.bc[o] = xs / ((hxe + hxr) * (hy0 + hy1));
+                    if (a.pc) a.pc[o] = 0.0;
+                }
+            }
+        }
+    };
+    {   // the coarse pair of the row before the walk's first
+        const int lp = r0 - 1;
+        ep = make_double2(a.ec[(ptrdiff_t)(lp >> 1) * a.ldc + Jl], a.ec[(ptrdiff_t)nbr(lp) * a.ldc + Jl]);
+    }
+    const int nr = r1 - r0 + 1;
+#pragma unroll
+    for (int q = 0; q < SD4; q++) {
+        load(r0 + q, Q[q], QB[q], QE[q]);
+        asm volatile("" ::: "memory");
+    }
+    for (int t = 0; t < nr; t += SD4) {
+#pragma unroll
+        for (int q = 0; q < SD4; q++) {
+            step(Q[q], QB[q], QE[q], r0 + t + q);   // (steps past the strip store nothing)
+            load(r0 + t + q + SD4, Q[q], QB[q], QE[q]);
+        }
+    }
+    return res;
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_sweep4(StreamArgs a) {
+    __shared__ double rcs[4][RC_MAX4][4];
+    double (*rc)[4] = rcs[threadIdx.x >> 6];
+    StreamArgs af = a;
+    int run, sj;
+    const bool live = strip_of<false>(a, af, run, sj);
+    const int lane = threadIdx.x & 63;
+    const int ib = run < a.slo ? a.rb0 + run * a.L : a.rb1 + (run - a.slo) * a.L;
+    const int ie = min(ib + a.L, a.rend);
+    const int si = a.pbase + run, wid = si * a.nsj + sj;
+    if (live) stage_rows<0, RC_OFF4, L4_MAX>(af, rc, ib, lane);
+    __syncthreads();
+    double res = 0.0;
+    if (live) {
+        const bool uni = rows_uniform(rc, min(ie - ib + 2 * RC_OFF4, RC_MAX4), RC_OFF4 + ((ie - ib) >> 1), lane);
+        res = uni ? sweep4_strip<true>(af, rc, ib, ie, sj, lane) : sweep4_strip<false>(af, rc, ib, ie, sj, lane);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) res += __shfl_xor(res, off, 64);
+    if (lane == 0 && live && af.part) af.part[wid] = res;
 }
 
 // ------------------------------------------------ K4 small levels: LDS-tiled fused passes
@@ -3449,10 +3680,8 @@ __global__ __launch_bounds__(256) void k_axpby(Geo g, double a, const double* __
     const int li = blockIdx.y * 4 + threadIdx.y;
     if (j >= g.ny || li >= g.nxl) return;
     const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
-    double r = a * x[o] + b * y[o];
-    if (z) r += c * z[o];
-    if (w) r += d * w[o];
-    if (v) r += e * v[o];
+    double r = extrap_comb(a, x[o], b, y[o], c, z, z ? z[o] : 0.0, d, w, w ? w[o] : 0.0);
+    if (v) r = fma(e, v[o], r);
     out[o] = r;
 }
 
@@ -3857,10 +4086,25 @@ void launch_bicg_scal(int stage, const double* d, double n, double* sc, hipStrea
     NS_LAUNCH(k_bicg_scal, dim3(1), dim3(1), 0, st, stage, d, n, sc);
 }
 
+bool correct_streams(const Geo& g) {
+    // (a NEUMANN side's phi ghost reaches two cells inward: the grid kernel's grad_phi)
+    return cell_streaming() && !g.fc && !(g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3]);
+}
+
+int launch_correct_guess(const Geo& g, const Coef& c, double dt, const double* us, const double* vs, double* u,
+                         double* v, const double* phi, double* part, const double* h1, const double* h2,
+                         const double* h3, const double* gc, double* gout, hipStream_t st) {
+    if (!correct_streams(g) || !h1 || (h3 && !h2)) return -1;
+    CellStreamArgs A{};
+    A.g = g; A.c = c; A.dt = dt; A.a0 = phi; A.a1 = us; A.a2 = vs; A.o0 = u; A.o1 = v; A.part = part;
+    A.h1 = h1; A.h2 = h2; A.h3 = h3; A.gout = gout;
+    A.gc0 = gc[0]; A.gc1 = gc[1]; A.gc2 = gc[2]; A.gc3 = gc[3];
+    return launch_cell_s<6>(A, st);
+}
+
 int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, const double* vs, double* u, double* v,
                    const double* phi, double* part, hipStream_t st) {
-    // (a NEUMANN side's phi ghost reaches two cells inward: the grid kernel's grad_phi)
-    if (cell_streaming() && !g.fc && !(g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3])) {
+    if (correct_streams(g)) {
         CellStreamArgs A{};
         A.g = g; A.c = c; A.dt = dt; A.a0 = phi; A.a1 = us; A.a2 = vs; A.o0 = u; A.o1 = v; A.part = part;
         return launch_cell_s<5>(A, st);
@@ -4098,6 +4342,22 @@ int launch_pois_rbsor2_prolong(const Geo& g, const Coef& c, double omega, const 
     }
     const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2<0, false, FUSE_P>), 5, &nblk);
     if (nblk) NS_LAUNCH((k_sweep2<0, false, FUSE_P>), dim3(nblk), dim3(256), 0, st, a);
+    return nstr;
+}
+
+// a V-cycle boundary of a whole level (k_sweep4): phi + P(ec) -> four RB sweeps -> out, the
+// residual of `out` restricted into bc (pc := 0 unless null), r^2 partials; one rank only
+int launch_pois_sweep4(const Geo& g, const Coef& c, double omega, const double* phi, double* out, const double* rp,
+                       const double* shift, const Geo& gc, const double* ec, double* bc, double* pc, double* part,
+                       hipStream_t st) {
+    if (g.nxl != g.nx || g_phase != 0) return -1;
+    StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
+    a.hx = c.hx; a.hy = c.hy; a.bc = bc; a.pc = pc; a.ldc = gc.ld;
+    a.ec = ec; a.ncx = gc.nx; a.ncy = gc.ny; a.ci0 = gc.i0; a.dsx = gc.dsx;
+    a.nsj = (g.ny + SW4 - 1) / SW4;
+    int nblk = 0;
+    const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep4), 9, &nblk, L4_MAX);
+    if (nblk) NS_LAUNCH(k_sweep4, dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 
@@ -4472,25 +4732,26 @@ int launch_coarse_vcycle(const Geo& g, const double* img, int img_n, int dn, dou
 // (w.x = 0 with w the cell areas).  One launch per stage G = [E o] (P M Q): a workgroup owns a
 // 16 x 16 block of G.  Every global load is issued up front, in one round (a chunked loop that
 // waited for each chunk's loads took 26 us per launch): M whole and P's 16 rows go to LDS, the
-// block's columns of Q to registers.  The four waves then form T = P[I, :] M (16 x n2p) by fp64
-// MFMA (16x16x4, K over n1p), T goes back through LDS, and the waves split T Q[:, J] over K,
-// summed in a fixed order.  n1p, n2p = the sides rounded up to 16 (<= 128); P, Q, E are
+// block's columns of Q to registers.  Eight waves then form T = P[I, :] M (16 x n2p, a column
+// tile each) by fp64 MFMA (16x16x4, K over n1p, four independent accumulators per wave), T goes
+// back through LDS, and the waves split T Q[:, J] over K, summed in a fixed order.  n1p, n2p = the sides rounded up to 16 (<= 128); P, Q, E are
 // zero-padded there, M / G are guarded.  Replaces the 128^2 LDS-tiled passes and the
 // one-workgroup coarse V-cycle (38 us per V-cycle at 4096^2, profiles/r03).
 typedef double nsd4 __attribute__((ext_vector_type(4)));
 constexpr int DIRECT_MAX = 128;                    // largest padded side
 constexpr int DIRECT_LDS = 20480;                  // doubles (160 KiB)
-__host__ __device__ inline int direct_r1(int n1p, int n2p) {   // region 1: M, then the 4 partial tiles
-    return n1p * n2p > 1024 ? n1p * n2p : 1024;
+constexpr int DIRECT_THREADS = 512;                // 8 waves: 2 per SIMD
+__host__ __device__ inline int direct_r1(int n1p, int n2p) {   // region 1: M, then the 8 partial tiles
+    return n1p * n2p > 2048 ? n1p * n2p : 2048;
 }
 __host__ __device__ inline int direct_r2(int n1p, int n2p) {   // region 2: P rows, then T, in doubles
     const int a = 16 * (n1p + 2), b = 16 * (n2p + 1);
     return a > b ? a : b;
 }
-__global__ __launch_bounds__(256) void k_direct(const double* __restrict__ P, const double* __restrict__ M,
-                                                const double* __restrict__ Q, const double* __restrict__ E,
-                                                double* __restrict__ G, int n1, int n2, int n1p, int n2p, int ldm,
-                                                int ldg) {
+__global__ __launch_bounds__(DIRECT_THREADS) void k_direct(const double* __restrict__ P, const double* __restrict__ M,
+                                                           const double* __restrict__ Q, const double* __restrict__ E,
+                                                           double* __restrict__ G, int n1, int n2, int n1p, int n2p,
+                                                           int ldm, int ldg) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* Ms = sm;                        // n1p x n2p, row k's columns XOR-swizzled by 16 on odd k
     double* R2 = sm + direct_r1(n1p, n2p);  // P[I, :] (stride n1p + 2), later T (stride n2p + 1)
@@ -4499,78 +4760,93 @@ __global__ __launch_bounds__(256) void k_direct(const double* __restrict__ P, co
     const int r16 = lane & 15, k4 = lane >> 4;
     const int sw = (n2p & 31) ? 0 : 16;     // (half-waves read rows k, k+1: their banks stay disjoint)
     const int ps = n1p + 2, ts = n2p + 1;
-    // ---- one round of loads: Q's block columns (this wave's K-quarter) to registers, P's rows and
-    // M to LDS
-    constexpr int QV = DIRECT_MAX / 16;
-    const int kq = n2p / 4, colq = 16 * bj + r16;
+    // ---- one round of loads: Q's block columns (this wave's k-steps) to registers, P's rows and M
+    // to LDS (16-B loads)
+    constexpr int QV = DIRECT_MAX / 4 / 8;  // k-steps of 4 per wave in step 2
+    const int nks = n2p / 4, colq = 16 * bj + r16;
     double qv[QV];
 #pragma unroll
-    for (int q = 0; q < QV; q++) qv[q] = 4 * q < kq ? Q[(size_t)(w * kq + 4 * q + k4) * n2p + colq] : 0.0;
+    for (int q = 0; q < QV; q++) {
+        const int ks = w + 8 * q;
+        qv[q] = ks < nks ? Q[(size_t)(4 * ks + k4) * n2p + colq] : 0.0;
+    }
     {
-        constexpr int NM = DIRECT_MAX * DIRECT_MAX / 256, NP = 16 * DIRECT_MAX / 256;
-        double mv[NM], pv[NP];
-        const int nm = n1p * n2p, np = 16 * n1p;
+        constexpr int NM = DIRECT_MAX * DIRECT_MAX / 2 / DIRECT_THREADS, NP = 16 * DIRECT_MAX / 2 / DIRECT_THREADS;
+        double2 mv[NM], pv[NP];
+        const int hm = n2p / 2, nm = n1p * hm, np = 8 * n1p;
 #pragma unroll
         for (int q = 0; q < NM; q++) {
-            const int e = threadIdx.x + 256 * q, k = e / n2p, c = e - k * n2p;
-            mv[q] = (e < nm && k < n1 && c < n2) ? M[(size_t)k * ldm + c] : 0.0;
+            const int e = threadIdx.x + DIRECT_THREADS * q, k = e / hm, c = 2 * (e - k * hm);
+            double2 v = {0.0, 0.0};
+            if (e < nm && k < n1) {
+                const double* src = M + (size_t)k * ldm + c;
+                if (c + 1 < n2) v = *reinterpret_cast<const double2*>(src);
+                else if (c < n2) v.x = src[0];
+            }
+            mv[q] = v;
         }
 #pragma unroll
         for (int q = 0; q < NP; q++) {
-            const int e = threadIdx.x + 256 * q;
-            pv[q] = e < np ? P[(size_t)16 * bi * n1p + e] : 0.0;
+            const int e = threadIdx.x + DIRECT_THREADS * q;
+            pv[q] = e < np ? reinterpret_cast<const double2*>(P + (size_t)16 * bi * n1p)[e] : double2{0.0, 0.0};
         }
 #pragma unroll
         for (int q = 0; q < NM; q++) {
-            const int e = threadIdx.x + 256 * q, k = e / n2p, c = e - k * n2p;
-            if (e < nm) Ms[k * n2p + (c ^ ((k & 1) ? sw : 0))] = mv[q];
+            const int e = threadIdx.x + DIRECT_THREADS * q, k = e / hm, c = 2 * (e - k * hm);
+            if (e < nm) *reinterpret_cast<double2*>(Ms + k * n2p + (c ^ ((k & 1) ? sw : 0))) = mv[q];
         }
 #pragma unroll
         for (int q = 0; q < NP; q++) {
-            const int e = threadIdx.x + 256 * q, r = e / n1p, k = e - r * n1p;
-            if (e < np) R2[r * ps + k] = pv[q];
+            const int e = threadIdx.x + DIRECT_THREADS * q, r = (2 * e) / n1p, k = 2 * e - r * n1p;
+            if (e < np) { R2[r * ps + k] = pv[q].x; R2[r * ps + k + 1] = pv[q].y; }
         }
     }
     __syncthreads();
-    // ---- step 1: T = P[I, :] M, the wave's column tiles ct = w, w + 4 (at most DIRECT_MAX / 64)
-    constexpr int NT = DIRECT_MAX / 64;
+    // ---- step 1: T = P[I, :] M, one column tile per wave (ct = w; n2p <= 128), four independent
+    // accumulators (k-steps mod 4) so the MFMA chains overlap, summed in a fixed order
     const int ntile = n2p / 16;
-    nsd4 acc[NT];
+    nsd4 t4 = {0.0, 0.0, 0.0, 0.0};
+    if (w < ntile) {
+        nsd4 acc[4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+        const int col = 16 * w + r16;
+        for (int k0 = 0; k0 < n1p; k0 += 16) {
+            double av[4], bv[4];
 #pragma unroll
-    for (int t = 0; t < NT; t++) acc[t] = nsd4{0.0, 0.0, 0.0, 0.0};
-    for (int k0 = 0; k0 < n1p; k0 += 4) {
-        const int k = k0 + k4;
-        const double av = R2[r16 * ps + k];
-#pragma unroll
-        for (int t = 0; t < NT; t++)
-            if (w + 4 * t < ntile) {
-                const int col = 16 * (w + 4 * t) + r16;
-                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Ms[k * n2p + (col ^ ((k & 1) ? sw : 0))], acc[t],
-                                                             0, 0, 0);
+            for (int j = 0; j < 4; j++) {
+                const int k = k0 + 4 * j + k4;
+                av[j] = R2[r16 * ps + k];
+                bv[j] = Ms[k * n2p + (col ^ ((k & 1) ? sw : 0))];
             }
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[j], bv[j], acc[j], 0, 0, 0);
+        }
+        t4 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     }
     __syncthreads();   // (every wave is done with P's rows: T takes their place)
+    if (w < ntile) {
 #pragma unroll
-    for (int t = 0; t < NT; t++)
-        if (w + 4 * t < ntile) {
-            const int col = 16 * (w + 4 * t) + r16;
-#pragma unroll
-            for (int r = 0; r < 4; r++) R2[(k4 + 4 * r) * ts + col] = acc[t][r];   // (f64 C/D: row = k4 + 4 r)
-        }
+        for (int r = 0; r < 4; r++) R2[(k4 + 4 * r) * ts + 16 * w + r16] = t4[r];   // (f64 C/D: row = k4 + 4 r)
+    }
     __syncthreads();
-    // ---- step 2: G[I, J] = T Q[:, J], K = n2p split over the four waves
+    // ---- step 2: G[I, J] = T Q[:, J], the k-steps of K = n2p dealt over the 8 waves
     nsd4 g4 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int q = 0; q < QV; q++)
-        if (4 * q < kq) g4 = __builtin_amdgcn_mfma_f64_16x16x4f64(R2[r16 * ts + w * kq + 4 * q + k4], qv[q], g4, 0, 0, 0);
-    // (M's region is free: the four partial tiles, summed in a fixed order)
+    for (int q = 0; q < QV; q++) {
+        const int ks = w + 8 * q;
+        if (ks < nks) g4 = __builtin_amdgcn_mfma_f64_16x16x4f64(R2[r16 * ts + 4 * ks + k4], qv[q], g4, 0, 0, 0);
+    }
+    // (M's region is free: the eight partial tiles, summed in a fixed order)
 #pragma unroll
     for (int r = 0; r < 4; r++) Ms[w * 256 + (k4 + 4 * r) * 16 + r16] = g4[r];
     __syncthreads();
-    const int t = threadIdx.x, gi = 16 * bi + (t >> 4), gj = 16 * bj + (t & 15);
-    double g = ((Ms[t] + Ms[256 + t]) + Ms[512 + t]) + Ms[768 + t];
-    if (E) g *= E[(size_t)gi * n2p + gj];
-    if (gi < n1 && gj < n2) G[(size_t)gi * ldg + gj] = g;
+    const int t = threadIdx.x;
+    if (t < 256) {
+        const int gi = 16 * bi + (t >> 4), gj = 16 * bj + (t & 15);
+        double g = ((Ms[t] + Ms[256 + t]) + (Ms[512 + t] + Ms[768 + t])) +
+                   ((Ms[1024 + t] + Ms[1280 + t]) + (Ms[1536 + t] + Ms[1792 + t]));
+        if (E) g *= E[(size_t)gi * n2p + gj];
+        if (gi < n1 && gj < n2) G[(size_t)gi * ldg + gj] = g;
+    }
 }
 
 bool direct_fits(int n1, int n2) {
@@ -4589,7 +4865,8 @@ int launch_direct(const double* P, const double* M, const double* Q, const doubl
         attr = true;
     }
     const size_t bytes = (size_t)(direct_r1(n1p, n2p) + direct_r2(n1p, n2p)) * sizeof(double);
-    NS_LAUNCH(k_direct, dim3(n1p / 16, n2p / 16), dim3(256), bytes, st, P, M, Q, E, G, n1, n2, n1p, n2p, ldm, ldg);
+    NS_LAUNCH(k_direct, dim3(n1p / 16, n2p / 16), dim3(DIRECT_THREADS), bytes, st, P, M, Q, E, G, n1, n2, n1p, n2p,
+              ldm, ldg);
     return 0;
 }
 

@@ -146,7 +146,6 @@ struct ns_solver {
     int mg_predict = 1;          // NSGPU_MG_PREDICT=0: a residual check (host sync) after every V-cycle
     double mg_rate2 = 0.0;       // last measured per-cycle contraction of ||r||^2
     int mg_hist[4] = {-1, -1, -1, -1};   // V-cycles the last four solves converged at (first check)
-    int last_solve = -1;         // V-cycles of the last multigrid Poisson solve (-1: none / Krylov)
     double* phim = nullptr;      // phi^{n-2} (the extrapolation's second point; rotates with PHI / TMP)
     double* phim2 = nullptr;     // phi^{n-3} (quadratic / cubic extrapolation)
     double* phim3 = nullptr;     // phi^{n-4} (cubic extrapolation)
@@ -186,6 +185,11 @@ struct ns_solver {
     // launches): the first whole coarse level of <= direct_cells cells (NSGPU_DIRECT_CELLS, default
     // 128^2; 0 = the LDS V-cycle below it as in round 3).  dmat: P1 = Vx^-1, Q1 = Vy^-T, E, P2 = Vx,
     // Q2 = Vy^T (direct_setup), padded to multiples of 16
+    // r4: a V-cycle boundary on the finest level in one pass (k_sweep4): cycle c's prolongation pass
+    // is deferred when c's output is not checked (p_pending) and runs fused with cycle c+1's
+    // restriction pass.  NSGPU_FUSE4=0: the two passes (A/B, the equivalence test's reference)
+    int fuse4 = 1;
+    bool p_pending = false;
     bool mg_direct = false;
     long direct_cells = 128L * 128L;
     double* dmat = nullptr;
@@ -242,7 +246,14 @@ struct ns_solver {
     // trip; k5_spec = 1 after a passing check (the step then only swaps), 0 otherwise (K5 runs
     // again after the last cycle: u* is untouched, K5 writes TMPU / TMPV)
     int in_step = 0, k5_spec = 0, n_spec = 0, n_spec_hit = 0;
-    int speculate = 1;           // NSGPU_SPECULATE=0: no speculative K5 (the equivalence test's reference)
+    int speculate = 1;           // NSGPU_SPECULATE=0: no speculative K5 / K3 (the equivalence test's reference)
+    // r4: K5 forms the next step's Poisson guess (k_cell_s<6>, NSGPU_K5_GUESS=0: k_axpby at the next
+    // step as in round 3); guess_ready: TMP holds it (branch guess_branch of extrap_plan) -- any entry
+    // point that may write TMP or the phi planes clears it.  K3 then runs speculatively behind the
+    // Helmholtz residual check (k3_spec: rhs_phi is this step's), which the extrapolation used to fill
+    int k5_guess = 1, guess_ready = 0, guess_branch = 0, k3_spec = 0;
+    int cur_cycles = -1;         // V-cycles of the Poisson solve in progress (at its K5)
+    int last_cycles = -1;        // V-cycles of the last multigrid solve (-1: none / Krylov)
 };
 
 namespace {
@@ -705,6 +716,7 @@ struct KrylovSolve {
 
 int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res);
 int correct_launch(ns_solver* s, double* part2);
+int divergence(ns_solver* s);
 
 // the wall bands' relaxation before the global Helmholtz passes (k_helm_band: band_sweeps RB-SOR
 // sweeps, 6 by default in launches of 3, of u and v on the cells within band_w = max(32, min(nx,
@@ -785,11 +797,16 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
         if (first) CHK(allreduce(s, s->scal + S_AUX, 2, ncclSum));
         CHK(fetch_begin(s));
-        if (s->extrap_pending) {
+        if (s->extrap_pending && !s->guess_ready) {
             // the Poisson initial guess does not depend on u*: it runs on the GPU while the
             // host waits for this check
             s->extrap_pending = 0;
             CHK(extrapolate_phi(s));
+        } else if (s->speculate && s->in_step) {
+            // (r4: K5 formed the guess) K3 instead: the divergence of this batch's u*, v* --
+            // the step's rhs_phi if the check passes, formed again after the next batch if not
+            CHK(divergence(s));
+            s->k3_spec = 1;
         }
         CHK(fetch_end(s));
         const double r2u = s->hs[S_RES], r2v = s->hs[S_RES + 1];
@@ -945,6 +962,16 @@ bool fused_restrict(const ns_solver* s, int l) {
 // NSGPU_FUSED_PROLONG=0 keeps the separate k_prolong pass
 bool fused_prolong(const ns_solver* s, int l) {
     return s->fuse_prolong && (pair_level(s, l) || tile_level(s, l)) && s->mg_post >= 2;
+}
+
+// the finest level's V-cycle boundary may run as one k_sweep4 pass: one rank (the pass reads 9 rows
+// past a strip), V(2,2) with both transfers fused on a level of two-sweep passes, and the level
+// below taking its iterate as zero (the pass reads that level's phi as the correction; it must not
+// also store zeros into it)
+bool zero_ok(const ns_solver* s, int l);
+bool fuse4_level0(const ns_solver* s) {
+    return s->fuse4 && !comm_on(s) && !s->pc_active && s->lv.size() > 1 && !s->lv[0].repl && pair_level(s, 0) &&
+           fused_restrict(s, 0) && fused_prolong(s, 0) && s->mg_pre == 2 && s->mg_post == 2 && zero_ok(s, 1);
 }
 
 bool zero_ok(const ns_solver* s, int l) {
@@ -1115,7 +1142,19 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool want_check, bo
         // the coarse level's first pass takes its iterate as zero: the restriction stores no zeros
         const bool czero = zero_ok(s, l + 1);
         double* pcz = czero ? nullptr : cv.phi;
-        if (fused_restrict(s, l)) {
+        if (l == 0 && s->p_pending) {
+            // the previous cycle's prolongation pass (deferred: its output was not checked) and this
+            // cycle's restriction pass in one (k_sweep4); level 1's phi still holds that correction
+            s->p_pending = false;
+            const bool t = s->timing && (!s->pc_active || s->pc_timing);
+            if (t) { CHK(t_begin(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); s->evtag[ev0 + *tn] = 2; }
+            nb = nsg::launch_pois_sweep4(F.g, F.c, s->mg_omega_s, F.phi, F.tmp, F.b, sh, cv.g, cv.phi, cv.b, nullptr,
+                                         s->part, s->st);
+            if (nb < 0) { set_err("V-cycle boundary pass does not fit"); return NS_EINVAL; }
+            if (t) { CHK(t_end(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); (*tn)++; }
+            std::swap(F.phi, F.tmp);
+            s->arr[NS_ARR_PHI] = F.phi; s->arr[NS_ARR_TMP] = F.tmp;
+        } else if (fused_restrict(s, l)) {
             // last two pre-smoothing sweeps + residual + restriction in one HBM pass
             CHK(mg_smooth(s, l, s->mg_pre - 2, tn, ev0));
             const bool zin = F.zero;   // (then the pass reads neither phi nor its ghost rows)
@@ -1175,7 +1214,11 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool want_check, bo
         MgLevel& F = level(s, l);
         MgLevel& C = level(s, l + 1);
         const CoarseView cv = coarse_view(s, l);
-        if (fused_prolong(s, l)) {
+        if (l == 0 && !want_check && fuse4_level0(s)) {
+            // (this cycle's output is not checked, so another cycle follows: the prolongation pass
+            // runs fused with its restriction pass, k_sweep4)
+            s->p_pending = true;
+        } else if (fused_prolong(s, l)) {
             // prolongation + the first two post-smoothing sweeps in one HBM pass; the coarse
             // and fine ghost rows travel in one group
             const bool t = s->timing && l == 0 && (!s->pc_active || s->pc_timing);
@@ -1235,6 +1278,7 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool want_check, bo
 }
 
 int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
+    s->p_pending = false;
     const double tol2 = s->rtol * s->rtol;
     const int maxc = std::min(s->max_iters, 1000);
     int cyc = 0, tn = 0, nchk = 0;   // cyc: V-cycles done before the current one
@@ -1264,6 +1308,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
         CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
         const bool spec = spec_ok && nchk == 0;
         if (spec) {
+            s->cur_cycles = cycles;   // (the guess K5 forms: this solve's count if the check passes)
             CHK(fetch_begin(s));   // (the residual's copy, then K5 behind it)
             CHK(correct_launch(s, s->part + 4 * (size_t)nsg::max_partials(s->g)));
             s->n_spec++;
@@ -1276,7 +1321,9 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
             for (int k = 0; k < tn; k++) {
                 float ms = 0.f;
                 HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
-                if (s->evtag[k]) {
+                if (s->evtag[k] == 2) {
+                    if (stt) { stt->t_cycle_kernel_ms += ms; stt->n_cycle_kernels++; }
+                } else if (s->evtag[k]) {
                     if (stt) { stt->t_restrict_kernel_ms += ms; stt->n_restrict_kernels++; }
                 } else {
                     tms += ms;
@@ -1334,7 +1381,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     }
     for (int k = 3; k > 0; k--) s->mg_hist[k] = s->mg_hist[k - 1];
     s->mg_hist[0] = need;
-    s->last_solve = need;
+    s->last_cycles = s->cur_cycles = cycles;
     if (stt) {
         stt->t_poisson_kernel_ms += tms;
         stt->n_checks += nchk;
@@ -1506,11 +1553,13 @@ int pois_solve_any(ns_solver* s, int* its, double* res, ns_stats* stt) {
                              s->scal + (s->consist ? S_KSHIFT : S_SHIFT), s->hs[S_SHIFT + 1], "poisson", stt};
         const int rc = bicgstab(s, ks, its, res);
         if (stt) stt->n_checks += *its + 1;
-        // (last_solve stays -1: the channel's BiCGStab took 5.1 iterations per step with the cubic
-        // guess against 4.75 with the quadratic, gpurun_out/r03_chan_ex)
+        // (last_cycles / cur_cycles -1: the quadratic guess -- the channel's BiCGStab took 5.1
+        // iterations per step with the cubic against 4.75 with the quadratic, r3)
+        s->last_cycles = s->cur_cycles = -1;
         return rc;
     }
     if (s->poisson == NS_POISSON_MG) return pois_solve_mg(s, its, res, stt);
+    s->last_cycles = s->cur_cycles = -1;
     return pois_solve(s, its, res, stt);
 }
 
@@ -1813,9 +1862,52 @@ int build_levels(ns_solver* s, const std::vector<double>& hx0, const std::vector
 }
 
 // Poisson initial guess: the reference warm-starts from phi^{n-1} (KSPSetInitialGuessNonzero,
-// FluidSolver.cpp:54); here from the linear extrapolation 2 phi^{n-1} - phi^{n-2}, which is
-// O(dt^2) closer to phi^n (the converged answer is the same: both solve to rtol).  The
-// three planes PHI (phi^{n-1}), phim (phi^{n-2}) and TMP rotate: no copies.
+// FluidSolver.cpp:54); here from an extrapolation of the last solutions, which is O(dt^k) closer
+// to phi^n (the converged answer is the same: both solve to rtol).  PHI (phi^{n-1}), the history
+// planes phim, phim2, phim3 and TMP rotate: no copies.
+//   linear 2 phi^{n-1} - phi^{n-2};  quadratic 3 phi^{n-1} - 3 phi^{n-2} + phi^{n-3};
+//   cubic 4 phi^{n-1} - 6 phi^{n-2} + 4 phi^{n-3} - phi^{n-4}, while the last multigrid solve
+//   needed more than one V-cycle (the start-up transient: 3.2 -> 2.9 V-cycles per step over steps
+//   6-25 of the 4096^2 cavity); once one cycle suffices (developed flow) the quadratic guess does
+//   as well and reads a plane less (both keep the four-plane history).
+// The guess is formed by K5 in the same pass (r4, k_cell_s<6>: K5 reads phi^{n-1} anyway) into
+// TMP; extrapolate_phi then only rotates the planes.  Elsewhere (masked / NEUMANN grids, the
+// quartic A/B, NSGPU_K5_GUESS=0) extrapolate_phi runs k_axpby with the same arithmetic.
+struct ExtrapPlan {
+    int branch = 0;            // 0: none (phi^{n-1} is the guess: the first step copies it to phim),
+                               // 1 linear, 2 quadratic, 3 cubic history, 4 quartic (A/B)
+    double c[5] = {0, 0, 0, 0, 0};
+    const double* h[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+ExtrapPlan extrap_plan(const ns_solver* s, int cycles) {
+    ExtrapPlan p;
+    if (!s->phim || s->phim_valid == 0) return p;
+    if (s->phi_extrap >= 4 && s->phim_valid >= 4) {
+        p.branch = 4;
+        const double c[5] = {5.0, -10.0, 10.0, -5.0, 1.0};
+        std::copy(c, c + 5, p.c);
+        p.h[0] = s->phim; p.h[1] = s->phim2; p.h[2] = s->phim3; p.h[3] = s->phim4;
+    } else if (s->phi_extrap >= 3 && s->phim_valid >= 3) {
+        p.branch = 3;
+        p.h[0] = s->phim; p.h[1] = s->phim2;
+        if (cycles >= 2) {
+            p.c[0] = 4.0; p.c[1] = -6.0; p.c[2] = 4.0; p.c[3] = -1.0;
+            p.h[2] = s->phim3;
+        } else {
+            p.c[0] = 3.0; p.c[1] = -3.0; p.c[2] = 1.0;
+        }
+    } else if (s->phi_extrap >= 2 && s->phim_valid >= 2) {
+        p.branch = 2;
+        p.c[0] = 3.0; p.c[1] = -3.0; p.c[2] = 1.0;
+        p.h[0] = s->phim; p.h[1] = s->phim2;
+    } else {
+        p.branch = 1;
+        p.c[0] = 2.0; p.c[1] = -1.0;
+        p.h[0] = s->phim;
+    }
+    return p;
+}
+
 int extrapolate_phi(ns_solver* s) {
     if (!s->phim) return 0;
     const size_t back = (size_t)nsg::HALO * s->g.ld;
@@ -1823,31 +1915,24 @@ int extrapolate_phi(ns_solver* s) {
         HIPCHK(hipMemcpyAsync(s->phim - back, s->arr[NS_ARR_PHI] - back, s->plane * sizeof(double),
                               hipMemcpyDeviceToDevice, s->st));
         s->phim_valid = 1;
+        s->guess_ready = 0;
         return 0;
     }
+    const ExtrapPlan p = extrap_plan(s, s->last_cycles);
     double* prev = s->arr[NS_ARR_PHI];
-    if (s->phi_extrap >= 4 && s->phim_valid >= 4) {
-        // quartic (A/B: NSGPU_PHI_EXTRAP=4): 5 phi^{n-1} - 10 phi^{n-2} + 10 phi^{n-3} - 5 phi^{n-4} + phi^{n-5}
-        nsg::launch_axpby(s->g, 5.0, prev, -10.0, s->phim, s->arr[NS_ARR_TMP], s->st, 10.0, s->phim2, -5.0, s->phim3,
-                          1.0, s->phim4);
-        s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
+    if (!(s->guess_ready && s->guess_branch == p.branch))
+        nsg::launch_axpby(s->g, p.c[0], prev, p.c[1], p.h[0], s->arr[NS_ARR_TMP], s->st, p.c[2], p.h[1], p.c[3], p.h[2],
+                          p.c[4], p.h[3]);
+    s->guess_ready = 0;
+    s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
+    switch (p.branch) {
+    case 4:
         s->arr[NS_ARR_TMP] = s->phim4;
         s->phim4 = s->phim3;
         s->phim3 = s->phim2;
         s->phim2 = s->phim;
-        s->phim = prev;
-        return 0;
-    }
-    if (s->phi_extrap >= 3 && s->phim_valid >= 3) {
-        // cubic: 4 phi^{n-1} - 6 phi^{n-2} + 4 phi^{n-3} - phi^{n-4}, while the last multigrid
-        // solve needed more than one V-cycle (the start-up transient: 3.2 -> 2.9 V-cycles per step over
-        // steps 6-25 of the 4096^2 cavity); once one cycle suffices (developed flow) the quadratic
-        // guess does as well and reads a plane less (both keep the four-plane history)
-        if (s->last_solve >= 2)
-            nsg::launch_axpby(s->g, 4.0, prev, -6.0, s->phim, s->arr[NS_ARR_TMP], s->st, 4.0, s->phim2, -1.0, s->phim3);
-        else
-            nsg::launch_axpby(s->g, 3.0, prev, -3.0, s->phim, s->arr[NS_ARR_TMP], s->st, 1.0, s->phim2);
-        s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
+        break;
+    case 3:
         if (s->phi_extrap >= 4) {
             s->arr[NS_ARR_TMP] = s->phim4;
             s->phim4 = s->phim3;
@@ -1857,15 +1942,9 @@ int extrapolate_phi(ns_solver* s) {
         }
         s->phim3 = s->phim2;
         s->phim2 = s->phim;
-        s->phim = prev;
-        return 0;
-    }
-    if (s->phi_extrap >= 2 && s->phim_valid >= 2) {
-        // 3 phi^{n-1} - 3 phi^{n-2} + phi^{n-3}
-        nsg::launch_axpby(s->g, 3.0, prev, -3.0, s->phim, s->arr[NS_ARR_TMP], s->st, 1.0, s->phim2);
-        s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
-        if (s->phi_extrap >= 3) {
-            // keep phi^{n-3} as the cubic's fourth point; the spare plane becomes scratch
+        break;
+    case 2:
+        if (s->phi_extrap >= 3) {   // keep phi^{n-3} as the cubic's fourth point; the spare plane becomes scratch
             s->arr[NS_ARR_TMP] = s->phim3;
             s->phim3 = s->phim2;
             s->phim_valid = 3;
@@ -1873,18 +1952,16 @@ int extrapolate_phi(ns_solver* s) {
             s->arr[NS_ARR_TMP] = s->phim2;
         }
         s->phim2 = s->phim;
-        s->phim = prev;
-        return 0;
-    }
-    nsg::launch_axpby(s->g, 2.0, prev, -1.0, s->phim, s->arr[NS_ARR_TMP], s->st);
-    s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
-    if (s->phi_extrap >= 2) {
-        // keep phi^{n-2} as the quadratic's third point; the spare plane becomes scratch
-        s->arr[NS_ARR_TMP] = s->phim2;
-        s->phim2 = s->phim;
-        s->phim_valid = 2;
-    } else {
-        s->arr[NS_ARR_TMP] = s->phim;
+        break;
+    default:
+        if (s->phi_extrap >= 2) {   // keep phi^{n-2} as the quadratic's third point
+            s->arr[NS_ARR_TMP] = s->phim2;
+            s->phim2 = s->phim;
+            s->phim_valid = 2;
+        } else {
+            s->arr[NS_ARR_TMP] = s->phim;
+        }
+        break;
     }
     s->phim = prev;
     return 0;
@@ -1968,10 +2045,24 @@ int rhs(ns_solver* s) {
 // the residual partials the check is reducing)
 int correct_launch(ns_solver* s, double* part2) {
     const HaloReq r[1] = {{&s->g, s->arr[NS_ARR_PHI], 1}};
+    // inside a step: the next step's Poisson guess in the same pass (k_cell_s<6>) into TMP, which the
+    // finished solve leaves free (a speculative K5 whose check fails is re-run after the last cycle,
+    // with that solve's cycle count: the guess is formed again)
+    const ExtrapPlan p = extrap_plan(s, s->cur_cycles);
+    const bool guess = s->in_step && s->k5_guess && p.branch >= 1 && p.branch <= 3 && nsg::correct_streams(s->g);
+    s->guess_ready = 0;
     const int nb = overlapped(s, r, 1, [&]() {
+        if (guess)
+            return nsg::launch_correct_guess(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
+                                             s->arr[NS_ARR_TMPV], s->arr[NS_ARR_PHI], part2, p.h[0], p.h[1], p.h[2], p.c,
+                                             s->arr[NS_ARR_TMP], s->st);
         return nsg::launch_correct(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
                                    s->arr[NS_ARR_TMPV], s->arr[NS_ARR_PHI], part2, s->st);
     });
+    if (guess && nb >= 0) {
+        s->guess_ready = 1;
+        s->guess_branch = p.branch;
+    }
     if (nb < 0) return nb;
     nsg::launch_reduce_min(part2, nb, 4, s->scal + S_MM, s->st);
     CHK(allreduce(s, s->scal + S_MM, 4, ncclMin));
@@ -2242,6 +2333,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_PHI_EXTRAP")) s->phi_extrap = std::max(0, std::min(4, std::atoi(e)));
     if (const char* e = getenv("NSGPU_MG_PREDICT")) s->mg_predict = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_SPECULATE")) s->speculate = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_K5_GUESS")) s->k5_guess = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_FUSE4")) s->fuse4 = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     if (const char* e = getenv("NSGPU_DIRECT_CELLS")) s->direct_cells = std::max(0L, std::atol(e));
@@ -2543,7 +2636,8 @@ static int step_body_(ns_solver* s, ns_stats& st) {
         st.n_helm_kernels += (size_t)k < s->hcomp.size() ? s->hcomp[k] : 1;   // (per component: 24 B/cell)
     }
     s->hn = 0;
-    CHK(divergence(s));                                            // ConstructRHS_phi + mean (:549-550)
+    if (!s->k3_spec) CHK(divergence(s));                           // ConstructRHS_phi + mean (:549-550)
+    s->k3_spec = 0;
     CHK(consistent_rhs(s));                                        // stretched grids only
     // rhs_phi ghost rows: with the multigrid's first overlapped FUSE_R exchange when it has one
     if (s->nranks > 1 && s->overlap && s->cst && s->poisson == NS_POISSON_MG && !s->kv[0] && !s->lv.empty() &&
@@ -2642,6 +2736,7 @@ int ns_get_array(ns_solver* s, int which, double* host) {
 
 int ns_set_array(ns_solver* s, int which, const double* host) {
     CHK(check_arr(s, which));
+    s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);
     HIPCHK(hipMemcpy2DAsync(s->arr[which], (size_t)s->g.ld * 8, host, (size_t)s->g.ny * 8, (size_t)s->g.ny * 8,
@@ -2694,6 +2789,7 @@ int ns_get_fields(ns_solver* s, double* u, double* v, double* phi) {
 int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* phi, const double* cu0,
                   const double* cv0) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
+    s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     if (u) CHK(set_compact(s, NS_ARR_U, u));
     if (v) CHK(set_compact(s, NS_ARR_V, v));
     if (phi) CHK(set_compact(s, NS_ARR_PHI, phi));
@@ -2704,6 +2800,7 @@ int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* 
 
 int ns_kernel(ns_solver* s, int which, int iters, double* out) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
+    s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);
     const double alpha = s->dt / (2 * s->re);
@@ -2841,6 +2938,7 @@ int ns_mg_transfer(ns_solver* s, int op, double* coarse) {
         set_err("ns_mg_transfer needs a multigrid solver with at least two levels");
         return NS_EINVAL;
     }
+    s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);
     MgLevel& F = level(s, 0);
@@ -2870,6 +2968,7 @@ int ns_mg_transfer(ns_solver* s, int op, double* coarse) {
 
 int ns_fill_random(ns_solver* s, uint64_t seed) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
+    s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     if (s->g.fc) { set_err("ns_fill_random (the sweep benchmark input) is rectangle-only"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);
@@ -2882,6 +2981,7 @@ int ns_fill_random(ns_solver* s, uint64_t seed) {
 
 int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
     if (!s || iters <= 0) { set_err("bad arguments"); return NS_EINVAL; }
+    s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     if (s->kv[0]) { set_err("ns_time_poisson times the rectangle's sweeps (no NEUMANN side, no mask)"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);
@@ -2921,6 +3021,7 @@ int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
 
 int ns_time_poisson_fp32(ns_solver* s, int warmup, int iters, double* out) {
     if (!s || iters <= 0) { set_err("bad arguments"); return NS_EINVAL; }
+    s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     if (s->kv[0]) { set_err("ns_time_poisson_fp32 times the rectangle's sweeps (no NEUMANN side, no mask)"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);

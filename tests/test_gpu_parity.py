@@ -719,6 +719,60 @@ def test_speculative_correction_is_bit_identical(gpu, monkeypatch, n):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("n", [256, 1024])
+def test_k5_poisson_guess_is_bit_identical(gpu, monkeypatch, n):
+    """r4: K5 forms the next step's Poisson guess (the phi extrapolation) in its own pass
+    (k_cell_s<6>), and K3 runs speculatively behind the Helmholtz residual check.  NSGPU_K5_GUESS=0
+    is round 3's order (k_axpby at the next step, K3 after the check): the same arithmetic, so the
+    fields, the V-cycle counts and the monitors must be bit-identical -- through the start-up
+    (linear, quadratic, cubic guesses), an injected phi (ns_set_array: the history restarts) and
+    a standalone solve between steps (ns_kernel: TMP is overwritten, the guess is formed again)."""
+    dt, re = 1.0 / (8 * n), 1000.0
+    out = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("NSGPU_K5_GUESS", fuse)
+        gs = gpu.GpuSolver(gpu.cavity(n), dt, re)
+        st = [gs.step() for _ in range(10)]
+        phi = gs.get(gpu.NS_ARR_PHI)
+        gs.set(gpu.NS_ARR_PHI, phi)
+        st += [gs.step() for _ in range(4)]
+        rp = gs.get(gpu.NS_ARR_RPHI)
+        gs.kernel(gpu.NS_K_RESIDUAL)
+        gs.set(gpu.NS_ARR_RPHI, rp)
+        st += [gs.step_async() for _ in range(4)]
+        out.append((gs.fields(), [s["it_phi"] for s in st], [s["it_u"] for s in st],
+                    [[s[k] for k in ("umin", "umax", "vmin", "vmax")] for s in st[:14]], gs.monitor()))
+        gs.close()
+    (fa, ca, ha, ma, la), (fb, cb, hb, mb, lb) = out
+    assert ca == cb and ha == hb
+    assert ma == mb and la == lb
+    for x, y in zip(fa, fb):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("n,xr", [(256, -1), (1024, -1), (512, 1.002)])
+def test_fused_cycle_boundary_is_bit_identical(gpu, monkeypatch, n, xr):
+    """r4: a V-cycle whose output is not checked hands its finest prolongation pass to the next
+    cycle's restriction pass, one k_sweep4 pass (prolongation + four RB sweeps + residual +
+    restriction).  NSGPU_FUSE4=0 runs the two k_sweep2 passes: the same arithmetic in the same
+    order, so fields, V-cycle counts and monitors must be bit-identical (uniform and stretched
+    rows: the pass's UNI and general instantiations), and the timed boundary passes show it ran."""
+    dt, re = 1.0 / (8 * n), 1000.0
+    out = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("NSGPU_FUSE4", fuse)
+        gs = gpu.GpuSolver(gpu.rectangle(n, n, bc=BC_CAVITY, xratio=xr, yratio=xr), dt, re, timing=True)
+        st = [gs.step() for _ in range(12)]
+        out.append((gs.fields(), [s["it_phi"] for s in st], [s["n_checks"] for s in st],
+                    [[s[k] for k in ("umin", "umax", "vmin", "vmax")] for s in st], sum(s["n_cycle_kernels"] for s in st)))
+        gs.close()
+    (fa, ca, na, ma, ka), (fb, cb, nb, mb, kb) = out
+    assert ca == cb and na == nb and ma == mb
+    assert ka > 0 and kb == 0, (ka, kb)   # (the fused run had cycles whose output went unchecked)
+    for x, y in zip(fa, fb):
+        assert np.array_equal(x, y)
+
+
 BC_OUT_W = [(4, 0.0), (2, 0.0), (0, -1.0), (2, 0.0)]     # inflow from E, NEUMANN outflow W
 
 
