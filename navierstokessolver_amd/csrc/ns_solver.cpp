@@ -247,11 +247,13 @@ struct ns_solver {
     // again after the last cycle: u* is untouched, K5 writes TMPU / TMPV)
     int in_step = 0, k5_spec = 0, n_spec = 0, n_spec_hit = 0;
     int speculate = 1;           // NSGPU_SPECULATE=0: no speculative K5 / K3 (the equivalence test's reference)
-    // r4: K5 forms the next step's Poisson guess (k_cell_s<6>, NSGPU_K5_GUESS=0: k_axpby at the next
-    // step as in round 3); guess_ready: TMP holds it (branch guess_branch of extrap_plan) -- any entry
+    // r4: K5 may form the next step's Poisson guess (k_cell_s<6>, NSGPU_K5_GUESS=1; default: k_axpby
+    // at the next step as in round 3); guess_ready: TMP holds it (branch guess_branch of extrap_plan) -- any entry
     // point that may write TMP or the phi planes clears it.  K3 then runs speculatively behind the
     // Helmholtz residual check (k3_spec: rhs_phi is this step's), which the extrapolation used to fill
-    int k5_guess = 1, guess_ready = 0, guess_branch = 0, k3_spec = 0;
+    // Measured (r4, 4096^2 driver form): k_cell_s<6> 242 us against K5 128 + k_axpby 104 us -- no gain
+    // (9,819-9,822 vs 9,821-9,863 MLUPS), so it is opt-in (NSGPU_K5_GUESS=1)
+    int k5_guess = 0, guess_ready = 0, guess_branch = 0, k3_spec = 0;
     int cur_cycles = -1;         // V-cycles of the Poisson solve in progress (at its K5)
     int last_cycles = -1;        // V-cycles of the last multigrid solve (-1: none / Krylov)
 };
