@@ -57,6 +57,10 @@ KERNELS = {
     # 8 / 4, write phi 8 + the coarse rhs 8 / 4 = 28
     "cycle": ("k_sweep4 (finest V-cycle boundary: prolongation + 4 RB sweeps + residual + restriction, "
               "cycle c's FUSE_P and cycle c+1's FUSE_R in one pass)", 28),
+    # (r4) a solve's first FUSE_R pass forming the phi extrapolation on the fly (k_sweep2_gin): FUSE_R's
+    # 26 B/cell with 4 history planes read instead of phi (cubic guess; 3 quadratic): 26 + 24 = 50
+    "guess": ("k_sweep2_gin (a Poisson solve's first finest restriction pass; its input, the cubic phi "
+              "extrapolation, formed from 4 history planes as rows enter)", 50),
     "helmholtz": ("Helmholtz pass of one velocity component of (I - a L_V) u* = RHS (k_sweep3 + residual stage: "
                   "3 RB-SOR sweeps, after the wall bands; or k_sweep2: 2 sweeps; the one-rank two-field "
                   "k_sweep3<FUSE_UV> launch counts as two component passes)", 24),
@@ -310,7 +314,8 @@ def main():
     timed = {"prolong": (sum(s["t_poisson_kernel_ms"] for s in stats), sum(s["n_poisson_kernels"] for s in stats)),
              "restrict": (sum(s["t_restrict_kernel_ms"] for s in stats), sum(s["n_restrict_kernels"] for s in stats)),
              "helmholtz": (sum(s["t_helm_kernel_ms"] for s in stats), sum(s["n_helm_kernels"] for s in stats)),
-             "cycle": (sum(s["t_cycle_kernel_ms"] for s in stats), sum(s["n_cycle_kernels"] for s in stats))}
+             "cycle": (sum(s["t_cycle_kernel_ms"] for s in stats), sum(s["n_cycle_kernels"] for s in stats)),
+             "guess": (sum(s["t_guess_kernel_ms"] for s in stats), sum(s["n_guess_kernels"] for s in stats))}
     # finest-level sweeps: V(2,2) per cycle (the convergence check rides on each cycle's last pass)
     fine_sweeps = 4 * cycles
     # whole-step algorithmic bytes per cell: K1 64 + K3 24 + K5 40 + the phi
@@ -325,6 +330,10 @@ def main():
     # cycles a solve ran, so this counts the cubic at most one step too often
     prev_c = [None] + [int(s["it_phi"]) for s in stats[:-1]]
     extrap_bpc = sum(40 if (c is None or c >= 2) else 32 for c in prev_c) / K
+    if any(s["n_guess_kernels"] for s in stats) or (args.time_every == 0 and world == 1 and not channel):
+        # (r4, GIN: no k_axpby; the solve's first FUSE_R reads 4 / 3 history planes instead of phi:
+        # + 24 / 16 B/cell on that pass, counted here in place of the extrapolation's 40 / 32)
+        extrap_bpc -= 16
     # the Helmholtz wall bands (two k_helm_band launches) on the cells within 128 of a wall:
     # per launch u, v read 16 + rhs 16 + write 16 -> 96 B per band cell
     band_frac = 1.0 - max(n - 256, 0) * max(nyc - 256, 0) / float(n * nyc)

@@ -38,8 +38,9 @@ extern "C" {
                                  4: NS_POISSON_MG is 0, so a zero-initialised ns_params selects the
                                     multigrid (RB-SOR moved to 3; the value 2 is rejected);
                                  5: ns_stats.x_link_bytes appended;
-                                 6: ns_stats.t_cycle_kernel_ms / n_cycle_kernels appended (the
-                                    finest level's V-cycle-boundary passes) */
+                                 6: ns_stats.t_cycle_kernel_ms / n_cycle_kernels and
+                                    t_guess_kernel_ms / n_guess_kernels appended (the finest
+                                    level's V-cycle-boundary and guess-forming passes) */
 
 typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm */
 
@@ -148,6 +149,10 @@ typedef struct ns_stats {
                                       * pass durations (k_sweep4: cycle c's prolongation + 2 sweeps and
                                       * cycle c+1's 2 sweeps + restriction in one pass; timing == 1) */
     int32_t n_cycle_kernels;         /* number of those passes timed */
+    double  t_guess_kernel_ms;       /* multigrid, one rank: sum of the durations of the solves' first
+                                      * finest restriction passes that form the phi extrapolation on the
+                                      * fly (k_sweep2_gin; timing == 1) */
+    int32_t n_guess_kernels;         /* number of those passes timed */
 } ns_stats;
 
 /* device arrays addressable by ns_get_array / ns_set_array */

@@ -69,7 +69,8 @@ class NsStats(ctypes.Structure):
                 ("t_helm_kernel_ms", ctypes.c_double), ("n_helm_kernels", ctypes.c_int32),
                 ("n_exchanges", ctypes.c_int32), ("n_allreduces", ctypes.c_int32),
                 ("x_link_bytes", ctypes.c_double), ("t_cycle_kernel_ms", ctypes.c_double),
-                ("n_cycle_kernels", ctypes.c_int32)]
+                ("n_cycle_kernels", ctypes.c_int32), ("t_guess_kernel_ms", ctypes.c_double),
+                ("n_guess_kernels", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

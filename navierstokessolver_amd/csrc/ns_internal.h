@@ -187,6 +187,14 @@ int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const
                                 const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
                                 double* part, hipStream_t st, bool zin = false);
 
+// the same with the input iterate formed on the fly (r4): gcoef[0] phi + gcoef[1] h1 + gcoef[2] h2 +
+// gcoef[3] h3 (h2 / h3 may be null) -- the phi extrapolation, k_axpby's arithmetic; a whole level
+// only (-1 otherwise)
+int launch_pois_rbsor2_restrict_guess(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                                      const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
+                                      double* part, const double* h1, const double* h2, const double* h3,
+                                      const double* gcoef, hipStream_t st);
+
 // the first post-smoothing pass with the prolongation fused in: phi + P(ec) enters two RB
 // sweeps -> out (phi itself is not modified); needs 5 ghost rows of phi, 3 of ec.  part != null:
 // partials of r^2 of `out` too (the V-cycle's convergence check after its last pass)

@@ -961,6 +961,10 @@ struct StreamArgs {
     double* out2;
     const double* b2;
     double* part2;
+    // GIN (k_sweep2<FUSE_R>, r4): the input iterate is the Poisson guess gc0 in + gc1 gh1 + gc2 gh2
+    // + gc3 gh3 (the phi extrapolation, extrap_comb), formed per row as it enters the pipeline
+    const double *gh1, *gh2, *gh3;
+    double gc0, gc1, gc2, gc3;
 };
 
 // diagonal of the operator at a cell from its row / column coefficient sums
@@ -1887,6 +1891,9 @@ constexpr int SW2X = 116;
 #ifndef SD2_FPR
 #define SD2_FPR 2
 #endif
+#ifndef SD2_GIN
+#define SD2_GIN 2   // FUSE_R with the guess input (GIN): rows in flight
+#endif
 template <int OP, bool RES, int FUSE>
 constexpr int sd2_of() {
     // (FUSE_P with the output residual: 172 VGPRs at 3 rows in flight = 2 waves/SIMD, 147 us per
@@ -2010,10 +2017,10 @@ __device__ __forceinline__ bool rows_uniform(const double (*rc)[4], int n, int m
 // ZIN (FUSE_R only): the input iterate is identically zero -- a coarse level's first pass of a
 // V-cycle, whose phi the restriction above no longer stores as zeros: no phi read at all (the
 // same values as reading the zeros)
-template <int OP, bool RES, int FUSE, int DIR, bool ZIN = false, bool UNI = false>
+template <int OP, bool RES, int FUSE, int DIR, bool ZIN = false, bool UNI = false, bool GIN = false>
 __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
                                               int lane) {
-    constexpr int SD2 = sd2_of<OP, RES, FUSE>();
+    constexpr int SD2 = GIN ? SD2_GIN : sd2_of<OP, RES, FUSE>();
     constexpr bool XR = FUSE == FUSE_R, XP = FUSE == FUSE_P;
     constexpr bool R5 = RES || XR;
     // the residual stage needs one more finished row on each side (EXT: rows), the prolongation's
@@ -2054,6 +2061,8 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
         0x00020000);
     double2 Q[SD2], QB[SD2];
     double QE[SD2];
+    constexpr int SG = GIN ? SD2 : 1;   // GIN: the history planes' rows, prefetched alike
+    double2 G1[SG], G2[SG], G3[SG];
     // phi rows ib-4-EXT .. ie+3+EXT and b rows ib-3-EXT .. ie+2+EXT (the first red
     // stage's) are read; the rest are clamped onto fetched rows (see k_sweep)
     const int r0 = ib - 4 - EXT, r1 = ie + 3 + EXT;
@@ -2075,11 +2084,16 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
         const int In = (lp & 1) ? I + 1 : I - 1;
         return (a.ci0 + In < 0 || a.ci0 + In >= a.ncx) ? I : In;
     };
-    auto load = [&](int slot_r, double2& p, double2& bb, double& ee) {
+    auto load = [&](int slot_r, double2& p, double2& bb, double& ee, double2& g1, double2& g2, double2& g3) {
         const int lp = min(max(slot_r, phi_lo), phi_hi), lb = min(max(slot_r - DIR, b_lo), b_hi);
         p = ZIN ? make_double2(0.0, 0.0) : ld_stream(a.in + (ptrdiff_t)lp * ld + lc, XP ? 1 : 0);   // (no branch)
         bb = *reinterpret_cast<const double2*>(a.b + (ptrdiff_t)lb * ld + lc);
         if (XP) ee = a.ec[(ptrdiff_t)nbr(lp) * a.ldc + Jl];
+        if (GIN) {
+            g1 = *reinterpret_cast<const double2*>(a.gh1 + (ptrdiff_t)lp * ld + lc);
+            if (a.gh2) g2 = *reinterpret_cast<const double2*>(a.gh2 + (ptrdiff_t)lp * ld + lc);
+            if (a.gh3) g3 = *reinterpret_cast<const double2*>(a.gh3 + (ptrdiff_t)lp * ld + lc);
+        }
     };
     // windows (3 rows each) of the stages' inputs, rhs rows r-1 .. r-5
     double2 P0 = {0, 0}, P1 = {0, 0}, P2 = {0, 0};     // old:           rows r-2 .. r
@@ -2128,7 +2142,13 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     };
 
     double2 ep = {0, 0};   // FUSE_P: (e(I), e(In)) of the previous row of the walk
-    auto step = [&](double2 p, const double2 bb, const double ce, int r) {
+    auto step = [&](double2 p, const double2 bb, const double ce, const double2 g1, const double2 g2,
+                    const double2 g3, int r) {
+        if (GIN) {
+            // the Poisson guess of this row: extrapolate_phi's combination (k_axpby, bit-identical)
+            p.x = extrap_comb(a.gc0, p.x, a.gc1, g1.x, a.gc2, a.gh2, g2.x, a.gc3, a.gh3, g3.x);
+            p.y = extrap_comb(a.gc0, p.y, a.gc1, g1.y, a.gc2, a.gh2, g2.y, a.gc3, a.gh3, g3.y);
+        }
         if (XP) {
             // rows with a new neighbour row (odd r walking down, even r walking up) take it from
             // the load; the others reuse the previous row's two coarse rows, swapped
@@ -2252,14 +2272,15 @@ __device__ __forceinline__ double sweep2_strip(const StreamArgs& a, const double
     }
 #pragma unroll
     for (int q = 0; q < SD2; q++) {
-        load(rs + DIR * q, Q[q], QB[q], QE[q]);
+        load(rs + DIR * q, Q[q], QB[q], QE[q], G1[q % SG], G2[q % SG], G3[q % SG]);
         if (BF) asm volatile("" ::: "memory");   // keep the slots' issue order (the loop's vmcnt bookkeeping)
     }
     for (int t = 0; t < nr; t += SD2) {
 #pragma unroll
         for (int q = 0; q < SD2; q++) {
-            if (BF || t + q < nr) step(Q[q], QB[q], QE[q], rs + DIR * (t + q));   // (BF: steps past the strip store nothing)
-            load(rs + DIR * (t + q + SD2), Q[q], QB[q], QE[q]);
+            if (BF || t + q < nr)   // (BF: steps past the strip store nothing)
+                step(Q[q], QB[q], QE[q], G1[q % SG], G2[q % SG], G3[q % SG], rs + DIR * (t + q));
+            load(rs + DIR * (t + q + SD2), Q[q], QB[q], QE[q], G1[q % SG], G2[q % SG], G3[q % SG]);
         }
     }
     return res;
@@ -2442,7 +2463,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SD3 == 3 ? 
     }
 }
 
-template <int OP, bool RES, int FUSE, bool ZIN = false>
+template <int OP, bool RES, int FUSE, bool ZIN = false, bool GIN = false>
 __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
     constexpr bool XR = FUSE == FUSE_R;
     constexpr bool R5 = RES || XR;                 // the fifth (output residual) stage
@@ -2468,11 +2489,11 @@ __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
         // (the overlapped exchange's split, the slab height)
         const bool uni = rows_uniform(rc, min(ie - ib + 2 * RC_OFF, RC_MAX), RC_OFF + ((ie - ib) >> 1), lane);
         if ((FUSE != FUSE_R || XR_UP) && (si & 1))
-            res = uni ? sweep2_strip<OP, RES, FUSE, -1, ZIN, true>(af, rc, ib, ie, sj, lane)
-                      : sweep2_strip<OP, RES, FUSE, -1, ZIN>(af, rc, ib, ie, sj, lane);
+            res = uni ? sweep2_strip<OP, RES, FUSE, -1, ZIN, true, GIN>(af, rc, ib, ie, sj, lane)
+                      : sweep2_strip<OP, RES, FUSE, -1, ZIN, false, GIN>(af, rc, ib, ie, sj, lane);
         else
-            res = uni ? sweep2_strip<OP, RES, FUSE, 1, ZIN, true>(af, rc, ib, ie, sj, lane)
-                      : sweep2_strip<OP, RES, FUSE, 1, ZIN>(af, rc, ib, ie, sj, lane);
+            res = uni ? sweep2_strip<OP, RES, FUSE, 1, ZIN, true, GIN>(af, rc, ib, ie, sj, lane)
+                      : sweep2_strip<OP, RES, FUSE, 1, ZIN, false, GIN>(af, rc, ib, ie, sj, lane);
     }
     if (R5) {
 #pragma unroll
@@ -2483,6 +2504,8 @@ __device__ __forceinline__ void sweep2_body(const StreamArgs& a) {
 
 template <int OP, bool RES, int FUSE, bool ZIN = false>
 __global__ __launch_bounds__(256) void k_sweep2(StreamArgs a) { sweep2_body<OP, RES, FUSE, ZIN>(a); }
+// the first restriction pass of a Poisson solve with the phi extrapolation formed on the fly (GIN)
+__global__ __launch_bounds__(256) void k_sweep2_gin(StreamArgs a) { sweep2_body<0, false, FUSE_R, false, true>(a); }
 // FP_W4 (A/B): the finest prolongation pass held to 4 waves / SIMD (128 VGPRs; with SD2_FP = 2)
 #ifndef FP_W4
 #define FP_W4 0
@@ -4309,6 +4332,22 @@ int launch_pois_rbsor2_restrict(const Geo& g, const Coef& c, double omega, const
     if (!nblk) return nstr;
     if (zin) NS_LAUNCH((k_sweep2<0, false, FUSE_R, true>), dim3(nblk), dim3(256), 0, st, a);
     else NS_LAUNCH((k_sweep2<0, false, FUSE_R>), dim3(nblk), dim3(256), 0, st, a);
+    return nstr;
+}
+
+int launch_pois_rbsor2_restrict_guess(const Geo& g, const Coef& c, double omega, const double* phi, double* out,
+                                      const double* rp, const double* shift, const Geo& gc, double* bc, double* pc,
+                                      double* part, const double* h1, const double* h2, const double* h3,
+                                      const double* gcoef, hipStream_t st) {
+    if (g.nxl != g.nx || g_phase != 0 || !h1 || (h3 && !h2)) return -1;
+    StreamArgs a = stream_args(g, c, phi, out, rp, shift, 0.0, omega, part, false);
+    a.hx = c.hx; a.hy = c.hy; a.bc = bc; a.pc = pc; a.ldc = gc.ld;
+    a.gh1 = h1; a.gh2 = h2; a.gh3 = h3;
+    a.gc0 = gcoef[0]; a.gc1 = gcoef[1]; a.gc2 = gcoef[2]; a.gc3 = gcoef[3];
+    a.nsj = (g.ny + SW2X - 1) / SW2X;
+    int nblk = 0;
+    const int nstr = plan_strips2(a, resident_waves((const void*)k_sweep2_gin), 5, &nblk);
+    if (nblk) NS_LAUNCH(k_sweep2_gin, dim3(nblk), dim3(256), 0, st, a);
     return nstr;
 }
 

@@ -190,6 +190,13 @@ struct ns_solver {
     // restriction pass.  NSGPU_FUSE4=0: the two passes (A/B, the equivalence test's reference)
     int fuse4 = 1;
     bool p_pending = false;
+    // r4: the phi extrapolation formed inside the solve's first restriction pass (k_sweep2_gin) instead
+    // of by k_axpby: extrapolate_phi only rotates the planes and leaves the guess's sources here;
+    // K3 then runs speculatively behind the Helmholtz check.  NSGPU_GIN=0: k_axpby (round 3)
+    int gin = 1;
+    bool gin_pending = false;
+    const double* gin_src[4] = {nullptr, nullptr, nullptr, nullptr};
+    double gin_c[4] = {0, 0, 0, 0};
     bool mg_direct = false;
     long direct_cells = 128L * 128L;
     double* dmat = nullptr;
@@ -719,6 +726,7 @@ struct KrylovSolve {
 int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res);
 int correct_launch(ns_solver* s, double* part2);
 int divergence(ns_solver* s);
+bool gin_ok(const ns_solver* s);
 
 // the wall bands' relaxation before the global Helmholtz passes (k_helm_band: band_sweeps RB-SOR
 // sweeps, 6 by default in launches of 3, of u and v on the cells within band_w = max(32, min(nx,
@@ -799,7 +807,7 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
         if (first) CHK(allreduce(s, s->scal + S_AUX, 2, ncclSum));
         CHK(fetch_begin(s));
-        if (s->extrap_pending && !s->guess_ready) {
+        if (s->extrap_pending && !s->guess_ready && !(s->gin && gin_ok(s) && s->phim_valid > 0)) {
             // the Poisson initial guess does not depend on u*: it runs on the GPU while the
             // host waits for this check
             s->extrap_pending = 0;
@@ -976,6 +984,13 @@ bool fuse4_level0(const ns_solver* s) {
            fused_restrict(s, 0) && fused_prolong(s, 0) && s->mg_pre == 2 && s->mg_post == 2 && zero_ok(s, 1);
 }
 
+// the Poisson guess may be formed inside the solve's first level-0 restriction pass (GIN): one rank,
+// the multigrid solve (no Krylov outflow / masked path), its first pass a streaming FUSE_R
+bool gin_ok(const ns_solver* s) {
+    return s->gin && s->in_step && !comm_on(s) && s->poisson == NS_POISSON_MG && !s->kv[0] && !s->g.fc &&
+           s->lv.size() > 1 && !s->lv[0].repl && pair_level(s, 0) && fused_restrict(s, 0) && s->mg_pre == 2;
+}
+
 bool zero_ok(const ns_solver* s, int l) {
     if (l <= 0 || l >= (int)s->lv.size()) return false;
     if (l == (int)s->lv.size() - 1) return s->mg_coarse_lds || s->mg_direct;
@@ -1144,7 +1159,19 @@ int mg_vcycle(ns_solver* s, int* tn, int ev0, Check&& check, bool want_check, bo
         // the coarse level's first pass takes its iterate as zero: the restriction stores no zeros
         const bool czero = zero_ok(s, l + 1);
         double* pcz = czero ? nullptr : cv.phi;
-        if (l == 0 && s->p_pending) {
+        if (l == 0 && s->gin_pending) {
+            // the solve's first restriction pass with its input, the phi extrapolation, formed per
+            // row from the history planes (k_sweep2_gin); it writes PHI (extrapolate_phi left the
+            // output plane there and TMP free), so no swap
+            s->gin_pending = false;
+            const bool t = s->timing && (!s->pc_active || s->pc_timing);
+            if (t) { CHK(t_begin(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); s->evtag[ev0 + *tn] = 3; }
+            nb = nsg::launch_pois_rbsor2_restrict_guess(F.g, F.c, s->mg_omega_s, s->gin_src[0], F.phi, F.b, sh, cv.g,
+                                                        cv.b, pcz, s->part, s->gin_src[1], s->gin_src[2],
+                                                        s->gin_src[3], s->gin_c, s->st);
+            if (nb < 0) { set_err("guess restriction pass does not fit"); return NS_EINVAL; }
+            if (t) { CHK(t_end(s, s->ev[2 * (ev0 + *tn)], s->ev[2 * (ev0 + *tn) + 1])); (*tn)++; }
+        } else if (l == 0 && s->p_pending) {
             // the previous cycle's prolongation pass (deferred: its output was not checked) and this
             // cycle's restriction pass in one (k_sweep4); level 1's phi still holds that correction
             s->p_pending = false;
@@ -1325,6 +1352,8 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
                 HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
                 if (s->evtag[k] == 2) {
                     if (stt) { stt->t_cycle_kernel_ms += ms; stt->n_cycle_kernels++; }
+                } else if (s->evtag[k] == 3) {
+                    if (stt) { stt->t_guess_kernel_ms += ms; stt->n_guess_kernels++; }
                 } else if (s->evtag[k]) {
                     if (stt) { stt->t_restrict_kernel_ms += ms; stt->n_restrict_kernels++; }
                 } else {
@@ -1384,6 +1413,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     for (int k = 3; k > 0; k--) s->mg_hist[k] = s->mg_hist[k - 1];
     s->mg_hist[0] = need;
     s->last_cycles = s->cur_cycles = cycles;
+    s->gin_pending = false;
     if (stt) {
         stt->t_poisson_kernel_ms += tms;
         stt->n_checks += nchk;
@@ -1922,9 +1952,20 @@ int extrapolate_phi(ns_solver* s) {
     }
     const ExtrapPlan p = extrap_plan(s, s->last_cycles);
     double* prev = s->arr[NS_ARR_PHI];
-    if (!(s->guess_ready && s->guess_branch == p.branch))
+    s->gin_pending = false;
+    if (s->guess_ready && s->guess_branch == p.branch) {
+        // (K5 formed it: nothing to launch)
+    } else if (p.branch >= 1 && p.branch <= 3 && gin_ok(s)) {
+        // the solve's first restriction pass forms it from these planes (the rotation below does
+        // not move their contents) and writes its output into TMP, which becomes PHI below
+        s->gin_pending = true;
+        s->gin_src[0] = prev;
+        for (int k = 0; k < 3; k++) s->gin_src[k + 1] = p.h[k];
+        for (int k = 0; k < 4; k++) s->gin_c[k] = p.c[k];
+    } else {
         nsg::launch_axpby(s->g, p.c[0], prev, p.c[1], p.h[0], s->arr[NS_ARR_TMP], s->st, p.c[2], p.h[1], p.c[3], p.h[2],
                           p.c[4], p.h[3]);
+    }
     s->guess_ready = 0;
     s->arr[NS_ARR_PHI] = s->arr[NS_ARR_TMP];
     switch (p.branch) {
@@ -2337,6 +2378,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_SPECULATE")) s->speculate = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_K5_GUESS")) s->k5_guess = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_FUSE4")) s->fuse4 = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_GIN")) s->gin = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     if (const char* e = getenv("NSGPU_DIRECT_CELLS")) s->direct_cells = std::max(0L, std::atol(e));

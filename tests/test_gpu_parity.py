@@ -751,24 +751,27 @@ def test_k5_poisson_guess_is_bit_identical(gpu, monkeypatch, n):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("knob,ran", [("NSGPU_FUSE4", "n_cycle_kernels"), ("NSGPU_GIN", "n_guess_kernels")])
 @pytest.mark.parametrize("n,xr", [(256, -1), (2048, -1), (512, 1.002)])
-def test_fused_cycle_boundary_is_bit_identical(gpu, monkeypatch, n, xr):
-    """r4: a V-cycle whose output is not checked hands its finest prolongation pass to the next
-    cycle's restriction pass, one k_sweep4 pass (prolongation + four RB sweeps + residual +
-    restriction).  NSGPU_FUSE4=0 runs the two k_sweep2 passes: the same arithmetic in the same
-    order, so fields, V-cycle counts and monitors must be bit-identical (uniform and stretched
-    rows: the pass's UNI and general instantiations), and the timed boundary passes show it ran.
+def test_fused_cycle_boundary_is_bit_identical(gpu, monkeypatch, n, xr, knob, ran):
+    """r4, NSGPU_FUSE4: a V-cycle whose output is not checked hands its finest prolongation pass to
+    the next cycle's restriction pass, one k_sweep4 pass (prolongation + four RB sweeps + residual +
+    restriction).  NSGPU_GIN: the solve's first restriction pass forms the phi extrapolation from
+    the history planes as rows enter it (k_sweep2_gin) instead of reading k_axpby's guess, and K3
+    runs speculatively behind the Helmholtz check.  =0 runs round 3's passes: the same arithmetic
+    in the same order, so fields, V-cycle counts and monitors must be bit-identical (uniform and
+    stretched rows: the UNI and general instantiations), and the timed passes show each ran.
     (Below 2048^2 the finest level is LDS-tiled; NSGPU_PAIR_MIN_CELLS=0 streams it.)"""
     dt, re = 1.0 / (8 * n), 1000.0
     if n < 2048:
         monkeypatch.setenv("NSGPU_PAIR_MIN_CELLS", "0")
     out = []
     for fuse in ("1", "0"):
-        monkeypatch.setenv("NSGPU_FUSE4", fuse)
+        monkeypatch.setenv(knob, fuse)
         gs = gpu.GpuSolver(gpu.rectangle(n, n, bc=BC_CAVITY, xratio=xr, yratio=xr), dt, re, timing=True)
         st = [gs.step() for _ in range(12)]
         out.append((gs.fields(), [s["it_phi"] for s in st], [s["n_checks"] for s in st],
-                    [[s[k] for k in ("umin", "umax", "vmin", "vmax")] for s in st], sum(s["n_cycle_kernels"] for s in st)))
+                    [[s[k] for k in ("umin", "umax", "vmin", "vmax")] for s in st], sum(s[ran] for s in st)))
         gs.close()
     (fa, ca, na, ma, ka), (fb, cb, nb, mb, kb) = out
     assert ca == cb and na == nb and ma == mb
