@@ -192,8 +192,10 @@ struct ns_solver {
     bool p_pending = false;
     // r4: the phi extrapolation formed inside the solve's first restriction pass (k_sweep2_gin) instead
     // of by k_axpby: extrapolate_phi only rotates the planes and leaves the guess's sources here;
-    // K3 then runs speculatively behind the Helmholtz check.  NSGPU_GIN=0: k_axpby (round 3)
-    int gin = 1;
+    // K3 then runs speculatively behind the Helmholtz check.  Measured (r4, 4096^2 driver form): the
+    // pass takes 241 us (184 VGPRs, 2 waves / SIMD, five streams) against FUSE_R 87 + k_axpby 104 us,
+    // 9,924-9,961 vs 9,957-10,143 MLUPS -- so opt-in (NSGPU_GIN=1); default k_axpby (round 3)
+    int gin = 0;
     bool gin_pending = false;
     const double* gin_src[4] = {nullptr, nullptr, nullptr, nullptr};
     double gin_c[4] = {0, 0, 0, 0};

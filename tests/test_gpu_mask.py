@@ -98,26 +98,34 @@ def test_mask_converged_solves(gpu, name):
     assert err <= 1e-8, (err, its)
 
 
+@pytest.mark.parametrize("rtol", [1e-8, 1e-11])
 @pytest.mark.parametrize("name,steps,re", [("step", 15, 100.0), ("lshape", 12, 400.0), ("split", 10, 100.0),
                                            ("uchannel", 10, 100.0), ("lshape_s", 10, 200.0)])
-def test_mask_full_steps_vs_oracle(gpu, name, steps, re):
+def test_mask_full_steps_vs_oracle(gpu, name, steps, re, rtol):
+    """Full steps on the polygons against the oracle (rtol 1e-13).  At the reference's rtol 1e-8:
+    u, v <= 1e-6 (the parity bar) and phi (modulo its mean, relative L2) <= 1e-4 -- phi is the
+    projection's multiplier, whose error at a converged residual scales with the masked operator's
+    condition number (the backward-facing step: 1.9e-6 with round 3's LDS coarse V-cycle in the
+    box preconditioner, 2.2e-5 with r4's exact coarse solve, both solves converged to 1e-8; u 2e-9
+    / 2e-8).  At rtol 1e-11 both must reach the oracle's solution: u, v <= 1e-9, phi <= 1e-7."""
     P = ALL[name]
     n = max(P["xspec"][-1][2], P["yspec"][-1][2])
     dt = 1.0 / (16 * n)
-    og, gs, m = pair(gpu, name, dt, re)
+    og, gs, m = pair(gpu, name, dt, re, rtol=rtol)
     osv = OSolver(og, dt, re, rtol=1e-13)
+    tu, tp = (1e-6, 1e-4) if rtol >= 1e-8 else (1e-9, 1e-7)
     for _ in range(steps):
         st = gs.step()
         mm, _ = osv.step()
-        np.testing.assert_allclose([st["umin"], st["umax"], st["vmin"], st["vmax"]], mm, atol=1e-6)
+        np.testing.assert_allclose([st["umin"], st["umax"], st["vmin"], st["vmax"]], mm, atol=tu)
     ref = osv.get()
     u, v, phi = (a.ravel() for a in gs.fields())
     du, dv = float(np.max(np.abs(u[m] - ref["u"]))), float(np.max(np.abs(v[m] - ref["v"])))
-    assert du <= 1e-6 and dv <= 1e-6, (du, dv)
+    assert du <= tu and dv <= tu, (du, dv)
     assert not np.any(u[~m]) and not np.any(v[~m])
     p, q = phi[m] - phi[m].mean(), ref["phi"] - ref["phi"].mean()
     ep = float(np.linalg.norm(p - q) / np.linalg.norm(q))
-    assert ep <= 1e-5, ep
+    assert ep <= tp, ep
 
 
 def test_mask_rectangle_only_entry_points_fail_loudly(gpu):
