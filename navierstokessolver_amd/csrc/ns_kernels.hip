@@ -2532,7 +2532,7 @@ constexpr int RC_OFF4 = 9;               // table row of strip row ib: stage 1 r
 constexpr int L4_MAX = 128;
 constexpr int RC_MAX4 = L4_MAX + 2 * RC_OFF4;
 #ifndef SD4
-#define SD4 2                            // rows in flight
+#define SD4 3                            // rows in flight (1 / 2 / 3: 179 / 140 / 129 us per pass at 4096^2)
 #endif
 template <bool UNI>
 __device__ __forceinline__ double sweep4_strip(const StreamArgs& a, const double (*rc)[4], int ib, int ie, int sj,
@@ -4547,7 +4547,10 @@ static int launch_jacobi_s(const Geo& g, const Coef& c, double omega, const T* i
     const bool nt = true;
     const void* k = part ? (nt ? (const void*)k_jacobi_s<T, true, true> : (const void*)k_jacobi_s<T, true, false>)
                          : (nt ? (const void*)k_jacobi_s<T, false, true> : (const void*)k_jacobi_s<T, false, false>);
-    a.L = strip_rows(a.nxl, a.nsj, resident_waves(k), 4);
+    // strips of at most 24 rows (r4, tools/sweep_c5.py over NSGPU_STRIP_ROWS): past the Infinity Cache
+    // one resident round of 64-row strips ran at 0.62 of the HBM peak (8192^2, 16384^2), several
+    // rounds of 20-24-row strips at 0.66-0.67; at 4096^2 the one-round height is below 24 anyway
+    a.L = strip_rows(a.nxl, a.nsj, resident_waves(k), 4, 24);
     a.nsi = (a.nxl + a.L - 1) / a.L;
     const int nstr = a.nsj * a.nsi, nblk = (nstr + 3) / 4;
     void* args[] = {&a};
