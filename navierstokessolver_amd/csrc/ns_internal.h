@@ -267,4 +267,33 @@ void launch_bicg_scal(int stage, const double* d, double n, double* sc, hipStrea
 // max partials any launcher writes for this geometry
 int max_partials(const Geo& g);
 
+// ---- the direct Poisson solve of rectangles with uniform hy (ns_fps.hip, r4) ----
+constexpr int FPS_M = 16;          // rows per chunk of the tridiagonal recurrences
+constexpr int FPS_G = 8;           // chunks per group (one workgroup)
+constexpr int FPS_LOGN_MIN = 4;    // ny = 2^4 .. 2^13 (the row pair's FFT fits 128 KiB of LDS)
+constexpr int FPS_LOGN_MAX = 13;
+struct FpsArgs {
+    int nx, i0, nxl, ny, ld;       // global rows, slab start, local rows, modes (= ny), row stride
+    int nch, ngrp;                 // local chunks (nxl / FPS_M rounded up), groups (nch / FPS_G rounded up)
+    int pin;                       // both x sides zero-flux: mode 0 is singular, its last row pinned
+    const double *pw, *pe;         // x coefficients (global index; Coef::pw / pe)
+    const double* mu;              // mode eigenvalues of Ly (ny)
+    const double* rp0;             // nch x ld: 1 / pivot of the row before each chunk
+    double *ga, *gc;               // forward: group aggregates (E, Pi: 2 x ngrp x ld), group carry-ins
+    double *gb, *gx;               // backward: group aggregates (X, R), group carry-ins
+    double* cb;                    // backward chunk aggregates (2 x nch x ld)
+};
+// log2(ny) if ny is a supported power of two, else -1
+int fps_log2(int ny);
+// DCT-II of nrows rows of (in - *shift) (shift may be null) -> out, or (inverse) DCT-III of in -> out;
+// tw: ny complex e^{-2 pi i m / ny}, wk: ny complex e^{-i pi k / 2 ny} (interleaved doubles)
+int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
+                   const double* tw, const double* wk, hipStream_t st);
+void launch_fps_t1(const FpsArgs& a, const double* f, hipStream_t st);
+void launch_fps_t2(const FpsArgs& a, double* f, hipStream_t st);
+void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st);
+// group scan (forward: ga -> gc ascending; backward: gb -> gx descending) from the carry-in rin (null:
+// 0; multi-rank: the fold of the other ranks' aggregates); rout (if not null) <- this rank's aggregate
+void launch_fps_scan(const FpsArgs& a, bool backward, const double* rin, double* rout, hipStream_t st);
+
 }  // namespace nsg

@@ -265,6 +265,18 @@ struct ns_solver {
     int k5_guess = 0, guess_ready = 0, guess_branch = 0, k3_spec = 0;
     int cur_cycles = -1;         // V-cycles of the Poisson solve in progress (at its K5)
     int last_cycles = -1;        // V-cycles of the last multigrid solve (-1: none / Krylov)
+    // r4: the direct Poisson solve (ns_fps.hip) of a rectangle with zero-flux phi sides and uniform hy
+    // (ny a power of two): DCT along y, tridiagonal recurrences along x, inverse DCT -- no iteration,
+    // so no initial guess (no phi history planes).  Its output residual is checked every fps_check-th
+    // solve (NSGPU_FPS_CHECK, default 1: every solve; the check's host sync hides behind a speculative
+    // K5); a residual above rtol continues with multigrid V-cycles from it.  NSGPU_FPS=0: multigrid
+    bool fps = false;
+    nsg::FpsArgs fa{};
+    double* fps_mem = nullptr;
+    const double *fps_tw = nullptr, *fps_wk = nullptr;
+    int fps_check = 1;
+    long fps_solves = 0;
+    double fps_res = -1.0;       // the last checked solve's relative residual
 };
 
 namespace {
@@ -1580,6 +1592,78 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
     return 0;
 }
 
+// the direct solve (ns_fps.hip): RPHI - shift -> PHI through the transformed plane in TMP; one
+// "iteration".  A checked solve computes its residual; speculating, K5 is enqueued before the host
+// reads it (as after a predicted multigrid check).  A residual above rtol (never seen: ~1e-14)
+// continues with multigrid V-cycles from this phi.
+int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
+    const nsg::Geo& g = s->g;
+    double* F = s->arr[NS_ARR_TMP];
+    const bool t = s->timing && s->in_step;
+    if (t) {
+        CHK(ensure_events(s, 2));
+        HIPCHK(hipEventRecord(s->ev[0], s->st));
+    }
+    if (nsg::launch_fps_dct(false, s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, F, g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk,
+                            s->st) < 0) {
+        set_err("direct Poisson solve: ny = %d is not a supported power of two", g.ny);
+        return NS_EINVAL;
+    }
+    nsg::launch_fps_t1(s->fa, F, s->st);
+    nsg::launch_fps_scan(s->fa, false, nullptr, nullptr, s->st);
+    nsg::launch_fps_t2(s->fa, F, s->st);
+    nsg::launch_fps_scan(s->fa, true, nullptr, nullptr, s->st);
+    nsg::launch_fps_t3(s->fa, F, s->st);
+    nsg::launch_fps_dct(true, F, nullptr, s->arr[NS_ARR_PHI], g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st);
+    if (t) HIPCHK(hipEventRecord(s->ev[1], s->st));
+    *its = 1;
+    s->last_cycles = s->cur_cycles = -1;
+    const bool check = s->fps_check > 0 && s->fps_solves % s->fps_check == 0;
+    s->fps_solves++;
+    if (!check) {
+        *res = s->fps_res;
+        if (t) {
+            HIPCHK(hipEventSynchronize(s->ev[1]));
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, s->ev[0], s->ev[1]));
+            if (stt) { stt->t_poisson_kernel_ms += ms; stt->n_poisson_kernels++; }
+        }
+        return 0;
+    }
+    const int nb = nsg::launch_pois_residual(g, s->c, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,
+                                             s->part, s->st);
+    nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
+    CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
+    const bool spec = s->speculate && s->in_step;
+    if (spec) {
+        CHK(fetch_begin(s));
+        CHK(correct_launch(s, s->part + 4 * (size_t)nsg::max_partials(s->g)));
+        s->n_spec++;
+        CHK(fetch_end(s));
+    } else {
+        CHK(fetch(s));
+    }
+    if (stt) stt->n_checks++;
+    if (t) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, s->ev[0], s->ev[1]));
+        if (stt) { stt->t_poisson_kernel_ms += ms; stt->n_poisson_kernels++; }
+    }
+    const double r2 = s->hs[S_RES], b2 = s->hs[S_SHIFT + 1];
+    *res = s->fps_res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
+    if (s->verbose) fprintf(stderr, "nsgpu poisson: direct solve, rel. residual %.3e\n", *res);
+    if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); return NS_EDIVERGE; }
+    if (r2 <= s->rtol * s->rtol * b2 || r2 == 0.0) {
+        if (spec) { s->k5_spec = 1; s->n_spec_hit++; }
+        return 0;
+    }
+    // (the speculative K5 wrote only the ping-pong partners: correct() runs it again)
+    int c = 0;
+    CHK(s->poisson == NS_POISSON_MG ? pois_solve_mg(s, &c, res, stt) : pois_solve(s, &c, res, stt));
+    *its = 1 + c;
+    return 0;
+}
+
 int pois_solve_any(ns_solver* s, int* its, double* res, ns_stats* stt) {
     if (s->kv[0]) {
         CHK(fetch(s));   // ||b - mean||^2 for the relative test
@@ -1592,9 +1676,70 @@ int pois_solve_any(ns_solver* s, int* its, double* res, ns_stats* stt) {
         s->last_cycles = s->cur_cycles = -1;
         return rc;
     }
+    if (s->fps) return pois_solve_fps(s, its, res, stt);
     if (s->poisson == NS_POISSON_MG) return pois_solve_mg(s, its, res, stt);
     s->last_cycles = s->cur_cycles = -1;
     return pois_solve(s, its, res, stt);
+}
+
+// host tables of the direct solve (ns_create): twiddles, the modes' eigenvalues and every chunk's
+// entry pivot.  The pivots p_i(k) of Thomas' recurrence (ns_fps.hip) depend on the operator only:
+// the host runs the recurrence over the global rows up to the slab's end and keeps 1 / p of the row
+// before each chunk of this slab (0 before global row 0, whose pw is 0)
+int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, const double* pe) {
+    const nsg::Geo& g = s->g;
+    const int N = g.ny, ld = g.ld;
+    nsg::FpsArgs& a = s->fa;
+    a.nx = g.nx; a.i0 = g.i0; a.nxl = g.nxl; a.ny = N; a.ld = ld;
+    a.nch = (g.nxl + nsg::FPS_M - 1) / nsg::FPS_M;
+    a.ngrp = (a.nch + nsg::FPS_G - 1) / nsg::FPS_G;
+    a.pin = 1;   // (every side of the rectangle is zero-flux for phi: Lx 1 = 0)
+    const int nchp = a.ngrp * nsg::FPS_G;   // (t1 / t2 / t3 address whole groups' chunks)
+    const size_t n_tab = 4 * (size_t)N + (size_t)N, n_rp0 = (size_t)nchp * ld, n_g = (size_t)a.ngrp * ld;
+    const size_t total = n_tab + n_rp0 + 6 * n_g + 2 * (size_t)nchp * ld;
+    std::vector<double> h(n_tab + n_rp0, 0.0);
+    const double pi = 3.14159265358979323846;
+    for (int m = 0; m < N; m++) {
+        const double t = 2.0 * pi * ((double)m / N);
+        h[2 * m] = std::cos(t);
+        h[2 * m + 1] = -std::sin(t);
+        const double u = pi * ((double)m / (2.0 * N));
+        h[2 * N + 2 * m] = std::cos(u);
+        h[2 * N + 2 * m + 1] = -std::sin(u);
+        const double sn = std::sin(u);
+        h[4 * N + m] = -4.0 / (hy[0] * hy[0]) * sn * sn;   // -(2/hy^2)(1 - cos(pi m / N))
+    }
+    double* rp0 = h.data() + n_tab;
+    std::vector<double> r(N, 0.0);   // 1 / p of the previous row, per mode
+    const int iend = g.i0 + g.nxl;
+    for (int gi = 0; gi < iend; gi++) {
+        const int li = gi - g.i0;
+        if (li >= 0 && li % nsg::FPS_M == 0)
+            for (int k = 0; k < N; k++) rp0[(size_t)(li / nsg::FPS_M) * ld + k] = r[k];
+        const double pem = gi > 0 ? pe[gi - 1] : 0.0;
+        for (int k = 0; k < N; k++) {
+            const double gg = pw[gi] * r[k];
+            const double p = -(pw[gi] + pe[gi]) + h[4 * N + k] - gg * pem;
+            r[k] = (k == 0 && gi == g.nx - 1) ? 0.0 : 1.0 / p;
+        }
+    }
+    HIPCHK(hipMalloc(&s->fps_mem, total * sizeof(double)));
+    HIPCHK(hipMemset(s->fps_mem, 0, total * sizeof(double)));
+    HIPCHK(hipMemcpy(s->fps_mem, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    double* d = s->fps_mem;
+    s->fps_tw = d;
+    s->fps_wk = d + 2 * (size_t)N;
+    a.mu = d + 4 * (size_t)N;
+    a.rp0 = d + n_tab;
+    double* q = d + n_tab + n_rp0;
+    a.ga = q; q += 2 * n_g;
+    a.gc = q; q += n_g;
+    a.gb = q; q += 2 * n_g;
+    a.gx = q; q += n_g;
+    a.cb = q;
+    a.pw = s->c.pw;
+    a.pe = s->c.pe;
+    return 0;
 }
 
 // coefficient tables of one level: [pw pe bx | ps pn by | hx hy]  (ConstructLHS, FluidSolver.cpp:113-131)
@@ -2407,6 +2552,17 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
                 }
         s->area = a;
         s->inv_area = ia;
+        // the direct Poisson solve: a rectangle without an outflow side, uniform spacings (the DCT
+        // needs hy uniform; hx uniform keeps b - plain mean consistent, as the oracle's og_fps_ok
+        // assumes), ny a power of two
+        bool yuni = true;
+        for (int j = 1; j < gd->ny; j++) yuni &= gd->hy[j] == gd->hy[0];
+        for (int i = 1; i < gd->nx; i++) yuni &= gd->hx[i] == gd->hx[0];
+        const char* fe = getenv("NSGPU_FPS");
+        s->fps = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !masked && !outflow && yuni &&
+                 nsg::fps_log2(gd->ny) >= 0 && p->nranks == 1;
+        if (const char* e = getenv("NSGPU_FPS_CHECK")) s->fps_check = std::max(0, std::atoi(e));
+        if (s->fps) s->phi_extrap = 0;   // (no initial guess: no history planes)
     }
 
     auto fail = [&](int rc) { ns_destroy(s); return rc; };
@@ -2520,6 +2676,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (hipMalloc(&s->coef, h.size() * sizeof(double)) != hipSuccess) { set_err("hipMalloc coef failed"); return fail(NS_ENOMEM); }
         if (hipMemcpy(s->coef, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) { set_err("coef upload failed"); return fail(NS_EHIP); }
         s->c = coef_view(s->coef, g.nx, g.ny);
+        if (s->fps)
+            if (int rc = fps_setup(s, hy0, h.data(), h.data() + g.nx)) return fail(rc);
     }
     // a masked domain's Poisson preconditioner: one V-cycle of the BOUNDING BOX's wall-closure
     // multigrid (a fictitious-domain preconditioner: the rhs is 0 outside the domain, the
@@ -2623,6 +2781,7 @@ void ns_destroy(ns_solver* s) {
     if (s->kv_mem) (void)hipFree(s->kv_mem);
     if (s->cvimg) (void)hipFree(s->cvimg);
     if (s->dmat) (void)hipFree(s->dmat);
+    if (s->fps_mem) (void)hipFree(s->fps_mem);
     if (s->f32_mem) (void)hipFree(s->f32_mem);
     if (s->fc_mem) (void)hipFree(s->fc_mem);
     if (s->et_mem) (void)hipFree(s->et_mem);

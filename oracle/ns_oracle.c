@@ -1314,6 +1314,119 @@ int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre
 }
 
 /* ---------------------------------------------------------------------- */
+/* the GPU's direct Poisson solve restated (ns_fps.hip, r4).  On a rectangle with Dirichlet-type
+ * (zero-flux phi) faces and uniform spacings, L = Lx (x) I + I (x) Ly; the DCT-II along y
+ * (j, contiguous) diagonalises Ly (mu_k = -(4/hy^2) sin^2(pi k / 2ny)), leaving one tridiagonal
+ * system (Lx + mu_k) x_k = f_k along x per mode, solved by Thomas' recurrences; mode 0 is
+ * singular (Lx 1 = 0) and its last unknown is pinned to 0; then the DCT-III.  This restatement
+ * runs the plain sequential recurrences and a textbook radix-2 FFT: it checks the GPU's chunked
+ * scans and Stockham transforms, not their arithmetic order (agreement ~1e-13, not bitwise). */
+
+int og_fps_ok(const og_grid* g) {
+    if (!rect_dirichlet(g)) return 0;
+    for (int i = 1; i < g->nx; i++) if (g->hx[i] != g->hx[0]) return 0;
+    for (int j = 1; j < g->ny; j++) if (g->hy[j] != g->hy[0]) return 0;
+    return g->ny >= 16 && g->ny <= 8192 && (g->ny & (g->ny - 1)) == 0 && g->nx >= 2;
+}
+
+/* in-place forward DFT of n = 2^p complex points (iterative radix-2, bit-reversed input order) */
+static void fft_inplace(int n, double* re, double* im, const double* cw, const double* sw) {
+    for (int i = 1, j = 0; i < n; i++) {
+        int bit = n >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) {
+            double t = re[i]; re[i] = re[j]; re[j] = t;
+            t = im[i]; im[i] = im[j]; im[j] = t;
+        }
+    }
+    for (int len = 2; len <= n; len <<= 1) {
+        const int st = n / len;
+        for (int i = 0; i < n; i += len)
+            for (int k = 0; k < len / 2; k++) {
+                const double c = cw[k * st], s = -sw[k * st];   /* e^{-2 pi i k / len} */
+                const int a = i + k, b = a + len / 2;
+                const double xr = re[b] * c - im[b] * s, xi = re[b] * s + im[b] * c;
+                re[b] = re[a] - xr; im[b] = im[a] - xi;
+                re[a] += xr; im[a] += xi;
+            }
+    }
+}
+
+int og_fps_solve(const og_grid* g, double* rhs, double* x) {
+    if (!og_fps_ok(g)) { set_err("the direct solve needs a uniform rectangle with zero-flux faces, ny = 2^p in [16, 8192]"); return -1; }
+    const int nx = g->nx, N = g->ny;
+    const size_t n = (size_t)nx * N;
+    double m = 0.0;
+    for (size_t c = 0; c < n; c++) m += rhs[c];
+    m /= (double)n;
+    for (size_t c = 0; c < n; c++) rhs[c] -= m;
+    const double PI = 3.14159265358979323846;
+    double* cw = malloc(sizeof(double) * N); double* sw = malloc(sizeof(double) * N);
+    double* ck = malloc(sizeof(double) * N); double* sk = malloc(sizeof(double) * N);
+    double* mu = malloc(sizeof(double) * N);
+    double* re = malloc(sizeof(double) * N); double* im = malloc(sizeof(double) * N);
+    double* F = malloc(sizeof(double) * n);
+    for (int k = 0; k < N; k++) {
+        cw[k] = cos(2.0 * PI * ((double)k / N)); sw[k] = sin(2.0 * PI * ((double)k / N));
+        const double u = PI * ((double)k / (2.0 * N));
+        ck[k] = cos(u); sk[k] = sin(u);
+        mu[k] = -4.0 / (g->hy[0] * g->hy[0]) * sk[k] * sk[k];
+    }
+    /* DCT-II of each row (Makhoul: v_n = x_2n, v_{N-1-n} = x_{2n+1}; X_k = Re(e^{-i pi k/2N} V_k)) */
+    for (int i = 0; i < nx; i++) {
+        const double* r = rhs + (size_t)i * N;
+        for (int j = 0; j < N; j++) {
+            const int q = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
+            re[q] = r[j]; im[q] = 0.0;
+        }
+        fft_inplace(N, re, im, cw, sw);
+        for (int k = 0; k < N; k++) F[(size_t)i * N + k] = ck[k] * re[k] + sk[k] * im[k];
+    }
+    /* Thomas per mode along x: a_i = cw_i, c_i = ce_i, d_i = -(cw_i + ce_i) + mu_k */
+    double* p = malloc(sizeof(double) * nx);
+    double* y = malloc(sizeof(double) * nx);
+    for (int k = 0; k < N; k++) {
+        for (int i = 0; i < nx; i++) {
+            double a, c, cs, cn;
+            pcoef(g, i, 0, &a, &c, &cs, &cn);
+            const double d = -(a + c) + mu[k];
+            if (i == 0) { p[0] = d; y[0] = F[k]; continue; }
+            double ap, cp, csp, cnp;
+            pcoef(g, i - 1, 0, &ap, &cp, &csp, &cnp);
+            const double gg = a / p[i - 1];
+            p[i] = d - gg * cp;
+            y[i] = F[(size_t)i * N + k] - gg * y[i - 1];
+        }
+        double xn = (k == 0) ? 0.0 : y[nx - 1] / p[nx - 1];
+        F[(size_t)(nx - 1) * N + k] = xn;
+        for (int i = nx - 2; i >= 0; i--) {
+            double a, c, cs, cn;
+            pcoef(g, i, 0, &a, &c, &cs, &cn);
+            xn = (y[i] - c * xn) / p[i];
+            F[(size_t)i * N + k] = xn;
+        }
+    }
+    /* DCT-III: V_k = e^{i pi k/2N}(X_k - i X_{N-k}), v = IFFT(V) = conj(FFT(conj V)) / N */
+    for (int i = 0; i < nx; i++) {
+        const double* X = F + (size_t)i * N;
+        for (int k = 0; k < N; k++) {
+            const double a = X[k], b = k ? X[N - k] : 0.0;
+            re[k] = ck[k] * a + sk[k] * b;
+            im[k] = -(sk[k] * a - ck[k] * b);
+        }
+        fft_inplace(N, re, im, cw, sw);
+        double* o = x + (size_t)i * N;
+        for (int j = 0; j < N; j++) {
+            const int q = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
+            o[j] = re[q] / N;
+        }
+    }
+    free(cw); free(sw); free(ck); free(sk); free(mu); free(re); free(im); free(F); free(p); free(y);
+    return 1;
+}
+
+/* ---------------------------------------------------------------------- */
 /* time stepper, FluidSolver::Solve FluidSolver.cpp:536-567                */
 
 struct og_solver {
@@ -1375,7 +1488,8 @@ int og_solver_step(og_solver* s, double* mm, int* its) {
         } while (iu < maxit);
         iv = iu;
         og_divergence(g, s->dt, s->us, s->vs, s->rp);
-        ip = og_mg_solve_w(g, s->rp, s->phi, s->rtol, 2, 2, 1000, s->omega_mg);
+        ip = s->gpu_alg == 2 && og_fps_ok(g) ? og_fps_solve(g, s->rp, s->phi)
+                                             : og_mg_solve_w(g, s->rp, s->phi, s->rtol, 2, 2, 1000, s->omega_mg);
     } else {
         /* KSPSolve(uSolver, ...) x2 with zero initial guess (:547-548) */
         memset(s->us, 0, sizeof(double) * n);

@@ -123,12 +123,20 @@ int og_mg_solve(const og_grid* g, double* rhs, double* x, double rtol, int pre, 
 int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre, int post, int maxcycles,
                   double omega);
 
+/* ---- the GPU's direct Poisson solve (ns_fps.hip, r4), restated: a uniform rectangle with
+ *      zero-flux faces, ny = 2^p in [16, 8192] (og_fps_ok); DCT-II along y, one Thomas solve per
+ *      mode along x (mode 0's last unknown pinned to 0), DCT-III.  rhs is mean-removed in place;
+ *      returns 1 (one "iteration") or -1 ---- */
+int og_fps_ok(const og_grid* g);
+int og_fps_solve(const og_grid* g, double* rhs, double* x);
+
 /* ---- full time stepper (FluidSolver::Solve, FluidSolver.cpp:536-567) ---- */
 og_solver* og_solver_new(og_grid* g, double dt, double re, double rtol);
 void og_solver_free(og_solver* s);
 /* algorithm: 0 = Krylov solves (the reference's kind, default); 1 = the GPU path's
  * algorithm (red-black SOR Helmholtz with omega_v, multigrid Poisson V(2,2) with the
- * red-black smoother over-relaxed by omega_mg) */
+ * red-black smoother over-relaxed by omega_mg); 2 = the same with the direct Poisson solve
+ * where og_fps_ok (the GPU's default there, r4), multigrid elsewhere */
 void og_solver_set_algorithm(og_solver* s, int gpu_algorithm, double omega_v, double omega_mg);
 /* k_helm_band restated: `sweeps` RB-SOR sweeps of u and v on the cells within w of a wall */
 int og_helm_band(const og_grid* g, double a, double* u, double* v, const double* ru, const double* rv, double omega,

@@ -44,6 +44,8 @@ _SIG = {
     "og_mg_solve": (ctypes.c_int, [_P, _D, _D, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "og_mg_solve_w": (ctypes.c_int, [_P, _D, _D, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_double]),
+    "og_fps_ok": (ctypes.c_int, [_P]),
+    "og_fps_solve": (ctypes.c_int, [_P, _D, _D]),
     "og_solver_set_algorithm": (None, [_P, ctypes.c_int, ctypes.c_double, ctypes.c_double]),
     "og_solver_set_band": (None, [_P, ctypes.c_int, ctypes.c_int]),
     "og_helm_band": (ctypes.c_int, [_P, ctypes.c_double, _D, _D, _D, _D, ctypes.c_double, ctypes.c_int, ctypes.c_int]),
@@ -215,6 +217,19 @@ class OGrid:
             raise ValueError(lib().og_last_error().decode())
         return x, cyc
 
+    def fps_ok(self):
+        """The GPU's direct Poisson solve applies (a uniform rectangle with zero-flux phi faces,
+        ny = 2^p in [16, 8192]): the GPU's default Poisson solve there (NSGPU_FPS)."""
+        return bool(lib().og_fps_ok(self.h))
+
+    def fps_solve(self, rhs):
+        """The direct solve (DCT along y, Thomas along x, mode 0 pinned) of L x = rhs - mean."""
+        b = _f(rhs).copy()
+        x = self.z()
+        if lib().og_fps_solve(self.h, _d(b), _d(x)) < 0:
+            raise ValueError(lib().og_last_error().decode())
+        return x
+
     def solve_poisson(self, rhs, x0=None, rtol=1e-13, maxit=100000):
         b = _f(rhs).copy()
         x = self.z() if x0 is None else _f(x0).copy()
@@ -236,11 +251,12 @@ class OSolver:
         except Exception:
             pass
 
-    def use_gpu_algorithm(self, omega_v, omega_mg=1.1, band=(None, 6)):
+    def use_gpu_algorithm(self, omega_v, omega_mg=1.1, band=(None, 6), fps=True):
         """RB-SOR Helmholtz (after `band` = (width, sweeps) RB-SOR sweeps on the cells within
         `width` of a wall: k_helm_band; width None = the GPU's default, band=None = no band step)
-        + multigrid Poisson (the GPU path's algorithm; CPU baseline)."""
-        lib().og_solver_set_algorithm(self.h, 1, omega_v, omega_mg)
+        + the Poisson solve of the GPU path: the direct solve where it applies (fps, the GPU's
+        NSGPU_FPS default), multigrid otherwise (CPU baseline)."""
+        lib().og_solver_set_algorithm(self.h, 2 if fps else 1, omega_v, omega_mg)
         w, k = band if band else (0, 0)
         if band and w is None:
             w = self.g.band_width()

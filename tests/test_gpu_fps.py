@@ -1,0 +1,121 @@
+"""The direct Poisson solve (ns_fps.hip, r4): DCT along y, chunked Thomas recurrences along x, inverse
+DCT -- the GPU's default Poisson solve on uniform rectangles with zero-flux phi faces and ny = 2^p
+(16 ... 8192).  Replaces KSPSolve(phiSolver) (/root/reference/SRC/FluidSolver.cpp:551) there.
+
+Tolerances (written per test):
+  * against the oracle's restatement (og_fps_solve: sequential Thomas, textbook radix-2 FFT; the same
+    discrete solution, another arithmetic order): <= 1e-10 of max|phi|, phi modulo its mean;
+  * against the oracle's Krylov solve of the reference's matrix at rtol 1e-13: <= 1e-8;
+  * the solve's own relative residual ||b - mean - L phi|| / ||b - mean||: <= 1e-11 (one solve, no
+    iteration: its = 1);
+  * repeat runs: bit-identical (a fixed arithmetic sequence)."""
+import numpy as np
+import pytest
+
+from oracle import OGrid, OSolver
+
+pytestmark = pytest.mark.gpu
+
+BC_CAVITY = [(2, 0.0), (2, 1.0), (2, 0.0), (2, 0.0)]
+BC_FLOW = [(0, 1.0), (2, 0.0), (0, 1.0), (2, 0.5)]   # inlets and moving walls: phi faces are zero-flux too
+
+
+def rel(a, b):
+    return float(np.max(np.abs(np.asarray(a).ravel() - np.asarray(b).ravel())) / max(np.max(np.abs(b)), 1e-300))
+
+
+def demean(x):
+    x = np.asarray(x).ravel()
+    return x - x.mean()
+
+
+# (nx, ny): square / wide / tall, odd nx (a half row pair, a partial chunk and group), the smallest
+# and one large transform, and a slab of one chunk group
+SIZES = [(64, 64), (96, 128), (40, 256), (37, 64), (1001, 512), (16, 16), (130, 32), (300, 4096), (128, 8192)]
+
+
+@pytest.mark.parametrize("nx,ny", SIZES)
+def test_direct_solve_matches_oracle(gpu, nx, ny):
+    rng = np.random.default_rng(nx * 7 + ny)
+    og = OGrid.rectangle(nx, ny, lx=nx / ny)
+    assert og.fps_ok()
+    gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny), 1e-3, 100.0, rtol=1e-11)
+    b = rng.uniform(-100, 100, nx * ny)
+    gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny))
+    gs.set(gpu.NS_ARR_RPHI, b)
+    its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+    assert its == 1 and res <= 1e-11, (its, res)
+    g = demean(gs.get(gpu.NS_ARR_PHI))
+    x = demean(og.fps_solve(b))
+    assert rel(g, x) <= 1e-10, rel(g, x)
+    r = og.apply_poisson(g) - (b - b.mean())
+    assert np.linalg.norm(r) <= 1e-11 * np.linalg.norm(b - b.mean())
+    if nx * ny <= 64 * 64:
+        xk, _ = og.solve_poisson(b)
+        assert rel(g, demean(xk)) <= 1e-8
+
+
+def test_direct_solve_is_deterministic(gpu):
+    n = 512
+    out = []
+    for _ in range(2):
+        gs = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0)
+        gs.fill_random(11)
+        gs.kernel(gpu.NS_K_POIS_SOLVE)
+        out.append(gs.get(gpu.NS_ARR_PHI))
+        gs.close()
+    assert np.array_equal(out[0], out[1])
+
+
+def test_direct_solve_inlet_sides(gpu):
+    """Inlet / moving-wall sides give the same zero-flux phi faces: the direct solve applies."""
+    nx, ny = 48, 64
+    rng = np.random.default_rng(5)
+    og = OGrid.rectangle(nx, ny, bc=BC_FLOW)
+    gs = gpu.GpuSolver(gpu.rectangle(nx, ny, bc=BC_FLOW), 1e-3, 100.0, rtol=1e-12)
+    b = rng.uniform(-1, 1, nx * ny)
+    gs.set(gpu.NS_ARR_RPHI, b)
+    its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+    assert its == 1 and res <= 1e-12
+    assert rel(demean(gs.get(gpu.NS_ARR_PHI)), demean(og.fps_solve(b))) <= 1e-10
+
+
+@pytest.mark.parametrize("n,steps", [(64, 20), (256, 10)])
+def test_steps_match_oracle_direct_algorithm(gpu, n, steps):
+    """Full steps, GPU (direct solve) against the oracle running the same algorithm (RB-SOR Helmholtz +
+    og_fps_solve) at rtol 1e-10: max|du|, max|dv| <= 1e-8; and against the multigrid on the GPU
+    (NSGPU_FPS=0 would be the same step solved to rtol): the monitor to 1e-6."""
+    re = 1000.0
+    dt = 1.0 / (8 * n)
+    og = OGrid.rectangle(n, n)
+    gs = gpu.GpuSolver(gpu.cavity(n), dt, re, rtol=1e-10)
+    osv = OSolver(og, dt, re, rtol=1e-10)
+    osv.use_gpu_algorithm(gs.omega_v, band=(None, 6))
+    for _ in range(steps):
+        st = gs.step()
+        mm, its = osv.step()
+        assert st["it_phi"] == 1 and its[2] == 1
+        np.testing.assert_allclose([st["umin"], st["umax"], st["vmin"], st["vmax"]], mm, atol=1e-8)
+    ref = osv.get()
+    u, v, phi = gs.fields()
+    assert np.max(np.abs(u.ravel() - ref["u"])) <= 1e-8
+    assert np.max(np.abs(v.ravel() - ref["v"])) <= 1e-8
+    assert rel(demean(phi), demean(ref["phi"])) <= 1e-8
+
+
+def test_multigrid_still_selectable(gpu, monkeypatch):
+    """NSGPU_FPS=0: the same grid solved by V-cycles (its > 1 cycles from zero), same solution."""
+    n = 128
+    rng = np.random.default_rng(3)
+    b = rng.uniform(-1, 1, n * n)
+    sol = {}
+    for fps in ("1", "0"):
+        monkeypatch.setenv("NSGPU_FPS", fps)
+        gs = gpu.GpuSolver(gpu.cavity(n), 1e-3, 100.0, rtol=1e-11)
+        gs.set(gpu.NS_ARR_PHI, np.zeros(n * n)); gs.set(gpu.NS_ARR_RPHI, b)
+        its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+        assert res <= 1e-11
+        assert (its == 1) == (fps == "1"), its
+        sol[fps] = demean(gs.get(gpu.NS_ARR_PHI))
+        gs.close()
+    assert rel(sol["0"], sol["1"]) <= 1e-9

@@ -17,6 +17,14 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+@pytest.fixture(autouse=True)
+def _multigrid(monkeypatch):
+    """These tests check the multigrid slab protocol (hierarchy, agglomeration, overlapped
+    exchanges): the single-rank reference runs the multigrid too (NSGPU_FPS=0; the direct solve's
+    slabs: test_gpu_fps.py)."""
+    monkeypatch.setenv("NSGPU_FPS", "0")
+
+
 def launch(tmp_path, *args, port=29561, nproc=2):
     out = tmp_path / "r.npz"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",

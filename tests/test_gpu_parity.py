@@ -347,8 +347,10 @@ def test_sweeps_deterministic_and_exact_with_many_tiles(gpu):
 
 
 @pytest.mark.parametrize("nx,ny", [(64, 64), (96, 160), (100, 60), (33, 47), (256, 512)])
-def test_mg_poisson_solve_matches_oracle(gpu, nx, ny):
-    """Multigrid V-cycles converge to the oracle's Krylov solution (odd sizes: RB-SOR fallback)."""
+def test_mg_poisson_solve_matches_oracle(gpu, monkeypatch, nx, ny):
+    """Multigrid V-cycles converge to the oracle's Krylov solution (odd sizes: RB-SOR fallback).
+    (NSGPU_FPS=0: the multigrid also where the direct solve applies, test_gpu_fps.py.)"""
+    monkeypatch.setenv("NSGPU_FPS", "0")
     rng = np.random.default_rng(11)
     og, gs = pair(gpu, nx, ny, 1e-3, 100.0, poisson=gpu.NS_POISSON_MG, rtol=1e-11)
     b = rand(rng, nx * ny, 100.0)
@@ -371,6 +373,7 @@ def test_mg_vcycles_match_oracle_mg(gpu, monkeypatch, direct, nx, ny):
     by its separable eigen-decomposition (k_direct: fp64 MFMA, sides padded to 16 -- 48 x 24 and
     50 x 30 here); NSGPU_DIRECT_CELLS=0: round 3's LDS V-cycle down to <= 16 cells."""
     import oracle as O
+    monkeypatch.setenv("NSGPU_FPS", "0")
     if direct is not None:
         monkeypatch.setenv("NSGPU_DIRECT_CELLS", direct)
     O.set_direct_cells(128 * 128 if direct is None else int(direct))
@@ -418,13 +421,16 @@ def test_mg_restrict_and_prolong_match_oracle(gpu, nx, ny, xr, yr):
     assert rel(gs.get(gpu.NS_ARR_PHI), og.mg_prolong(phi, ec)) <= 1e-13
 
 
-def test_mg_step_algorithm_matches_oracle_mg(gpu):
-    """Same algorithm on both sides (MG Poisson + RB-SOR Helmholtz): the CPU baseline leg."""
+@pytest.mark.parametrize("fps", ["1", "0"])
+def test_mg_step_algorithm_matches_oracle_mg(gpu, monkeypatch, fps):
+    """Same algorithm on both sides (RB-SOR Helmholtz + the direct Poisson solve, or with
+    NSGPU_FPS=0 the multigrid): the CPU baseline leg."""
+    monkeypatch.setenv("NSGPU_FPS", fps)
     n, re, steps = 64, 100.0, 8
     dt = 1.0 / (8 * n)
     og, gs = pair(gpu, n, n, dt, re, rtol=1e-10)
     osv = OSolver(og, dt, re, rtol=1e-10)
-    osv.use_gpu_algorithm(1.0)
+    osv.use_gpu_algorithm(1.0, fps=fps == "1")
     for _ in range(steps):
         gs.step(); osv.step()
     u, v, _ = gs.fields()
@@ -534,6 +540,7 @@ def test_fused_transfer_passes_match_separate_transfers(gpu, monkeypatch, nx, ny
     rng = np.random.default_rng(23)
     b = rand(rng, nx * ny, 100.0)
     out = {}
+    monkeypatch.setenv("NSGPU_FPS", "0")
     monkeypatch.setenv("NSGPU_PAIR_MIN_CELLS", "0")
     for fr, fp in (("1", "1"), ("0", "0"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("NSGPU_FUSED_RESTRICT", fr)
@@ -562,6 +569,7 @@ def test_tiled_small_level_passes_match_streaming(gpu, monkeypatch, nx, ny):
     rng = np.random.default_rng(29)
     b = rand(rng, nx * ny, 100.0)
     out = {}
+    monkeypatch.setenv("NSGPU_FPS", "0")
     for mode, env in (("tile", {}), ("stream", {"NSGPU_PAIR_MIN_CELLS": "0"}), ("single", {"NSGPU_TILE_SMALL": "0"})):
         for k in ("NSGPU_PAIR_MIN_CELLS", "NSGPU_TILE_SMALL"):
             monkeypatch.delenv(k, raising=False)
@@ -682,6 +690,7 @@ def test_dispatch_stamped_kernel_timing(gpu, monkeypatch):
     step timings stay positive and per-pass."""
     n = 1024
     avg = {}
+    monkeypatch.setenv("NSGPU_FPS", "0")   # (the multigrid's timed passes)
     for ext in ("1", "0"):
         monkeypatch.setenv("NSGPU_EXT_TIMING", ext)
         js = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0, poisson=gpu.NS_POISSON_JACOBI, omega=1.0)
@@ -730,6 +739,7 @@ def test_k5_poisson_guess_is_bit_identical(gpu, monkeypatch, n):
     a standalone solve between steps (ns_kernel: TMP is overwritten, the guess is formed again)."""
     dt, re = 1.0 / (8 * n), 1000.0
     out = []
+    monkeypatch.setenv("NSGPU_FPS", "0")   # (the multigrid's guess: the direct solve takes none)
     for fuse in ("1", "0"):
         monkeypatch.setenv("NSGPU_K5_GUESS", fuse)
         gs = gpu.GpuSolver(gpu.cavity(n), dt, re)
@@ -763,6 +773,7 @@ def test_fused_cycle_boundary_is_bit_identical(gpu, monkeypatch, n, xr, knob, ra
     stretched rows: the UNI and general instantiations), and the timed passes show each ran.
     (Below 2048^2 the finest level is LDS-tiled; NSGPU_PAIR_MIN_CELLS=0 streams it.)"""
     dt, re = 1.0 / (8 * n), 1000.0
+    monkeypatch.setenv("NSGPU_FPS", "0")
     if n < 2048:
         monkeypatch.setenv("NSGPU_PAIR_MIN_CELLS", "0")
     out = []

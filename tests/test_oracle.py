@@ -167,3 +167,34 @@ def test_multigrid_checks_the_cycle_output():
     assert cyc >= 1 and rel(x) <= rtol
     xm, cm = g.mg_solve(b, rtol=1e-30, maxcycles=cyc - 1)
     assert cm == cyc - 1 and (cyc == 1 or rel(xm) > rtol)
+
+
+@pytest.mark.parametrize("nx,ny", [(40, 64), (33, 16), (24, 32)])
+def test_direct_poisson_restatement(nx, ny):
+    """og_fps_solve (the GPU's direct Poisson solve restated: DCT-II along y, Thomas along x with mode
+    0 pinned, DCT-III) against an independent sparse LU of the reference's matrix (ConstructLHS,
+    FluidSolver.cpp:113-131; one unknown pinned to fix the constant): phi modulo its mean to 1e-11
+    of max|phi|, relative residual <= 1e-12."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spl
+    og = OGrid.rectangle(nx, ny, lx=nx / ny)
+    assert og.fps_ok()
+    rng = np.random.default_rng(nx + ny)
+    b = rng.uniform(-1, 1, og.N)
+    x = og.fps_solve(b)
+    bb = b - b.mean()
+    r = og.apply_poisson(x) - bb
+    assert np.linalg.norm(r) <= 1e-12 * np.linalg.norm(bb)
+    cols = [og.apply_poisson(e) for e in np.eye(og.N)]   # the operator column by column
+    A = sp.csc_matrix(np.array(cols).T)
+    A = A[1:, 1:]   # x_0 = 0: drop its row and column (the system is consistent)
+    xs = np.concatenate([[0.0], spl.spsolve(A.tocsc(), bb[1:])])
+    d = (x - x.mean()) - (xs - xs.mean())
+    assert np.max(np.abs(d)) <= 1e-11 * np.max(np.abs(xs))
+
+
+def test_direct_poisson_applies_only_to_uniform_walled_rectangles():
+    assert not OGrid.rectangle(64, 48).fps_ok()                     # ny not a power of two
+    assert not OGrid.rectangle(64, 64, xratio=1.01).fps_ok()        # stretched
+    assert not OGrid.rectangle(64, 64, bc=[(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0)]).fps_ok()   # outflow
+    assert OGrid.rectangle(64, 64, bc=[(0, 1.0), (2, 0.0), (0, 1.0), (2, 0.5)]).fps_ok()       # inlets
