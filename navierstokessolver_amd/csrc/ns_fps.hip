@@ -23,6 +23,8 @@
 // (N <= 8192 complex = 128 KiB), one workgroup of N/16 threads, one butterfly per thread and stage.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "ns_internal.h"
 
 namespace nsg {
@@ -71,14 +73,37 @@ __device__ inline void dft(cplx* v) {
     }
 }
 
+// radix 2^FPS_LR stages (A/B: 3 = radix 8, N/8 threads per row pair, more waves per CU)
+#ifndef FPS_LR
+#define FPS_LR 4
+#endif
+#ifndef FPS_PREF
+#define FPS_PREF 0   // 1: the persistent transforms load the next row pair during this one (A/B, r4: 365 vs 343 us per solve -- its registers cost more than the overlap gains)
+#endif
+// (radix 8: two workgroups of N/8 threads per CU need <= 128 VGPRs)
+#if FPS_LR == 3
+#define FPS_WAVES __attribute__((amdgpu_waves_per_eu(4)))
+#else
+#define FPS_WAVES
+#endif
 template <int LOGN>
 struct Fft {
     static constexpr int N = 1 << LOGN;
-    static constexpr int T = N / 16 < 64 ? 64 : (N / 16 > 512 ? 512 : N / 16);   // threads
+    static constexpr int R = 1 << FPS_LR;
+    static constexpr int T = (N >> FPS_LR) < 64 ? 64 : ((N >> FPS_LR) > 1024 ? 1024 : (N >> FPS_LR));   // threads
+};
+
+// LDS slot of element i: one pad slot every 16 and every 256 elements, so that the Stockham
+// writes of stride 16 and 256 elements (272 / 4368 B apart after padding) fall on distinct banks
+__device__ inline int pz(int i) { return i + (i >> 4) + (i >> 8); }
+template <int LOGN>
+struct FftLds {
+    static constexpr int n = (1 << LOGN) - 1 + (((1 << LOGN) - 1) >> 4) + (((1 << LOGN) - 1) >> 8) + 1;
 };
 
 // one Stockham stage of radix R over z[N] in LDS (sub-transform length Ns so far); every thread
-// reads its butterflies' inputs, the block synchronises, then writes (in place)
+// reads its butterflies' inputs, the block synchronises, then writes (in place).  Twiddles
+// w^r = e^{-2 pi i r k / (Ns R)}: w from the table, its powers by repeated products (r <= 15 roundings)
 template <int LOGN, int R>
 __device__ inline void fft_stage(cplx* z, const cplx* __restrict__ tw, int tid, int Ns) {
     constexpr int N = Fft<LOGN>::N, T = Fft<LOGN>::T;
@@ -90,7 +115,7 @@ __device__ inline void fft_stage(cplx* z, const cplx* __restrict__ tw, int tid, 
         const int jb = tid + b * T;
         if (jb < NB) {
 #pragma unroll
-            for (int r = 0; r < R; r++) v[b][r] = z[jb + r * NB];
+            for (int r = 0; r < R; r++) v[b][r] = z[pz(jb + r * NB)];
         }
     }
     __syncthreads();
@@ -100,14 +125,18 @@ __device__ inline void fft_stage(cplx* z, const cplx* __restrict__ tw, int tid, 
         if (jb < NB) {
             const int k = jb & (Ns - 1);
             if (Ns > 1) {
-                const int step = k * (N / (Ns * R));
+                const cplx w = tw[k * (N / (Ns * R))];
+                cplx wr = w;
 #pragma unroll
-                for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[(r * step) & (N - 1)]);
+                for (int r = 1; r < R; r++) {
+                    v[b][r] = cmul(v[b][r], wr);
+                    if (r + 1 < R) wr = cmul(wr, w);
+                }
             }
             dft<R>(v[b]);
             const int d = (jb - k) * R + k;
 #pragma unroll
-            for (int r = 0; r < R; r++) z[d + r * Ns] = v[b][r];
+            for (int r = 0; r < R; r++) z[pz(d + r * Ns)] = v[b][r];
         }
     }
     __syncthreads();
@@ -117,99 +146,164 @@ template <int LOGN>
 __device__ inline void fft_lds(cplx* z, const cplx* __restrict__ tw, int tid) {
     int Ns = 1;
 #pragma unroll
-    for (int s = 0; s < LOGN / 4; s++) {
-        fft_stage<LOGN, 16>(z, tw, tid, Ns);
-        Ns *= 16;
+    for (int s = 0; s < LOGN / FPS_LR; s++) {
+        fft_stage<LOGN, (1 << FPS_LR)>(z, tw, tid, Ns);
+        Ns *= 1 << FPS_LR;
     }
-    if constexpr (LOGN % 4 != 0) fft_stage<LOGN, (1 << (LOGN % 4))>(z, tw, tid, Ns);
+    if constexpr (LOGN % FPS_LR != 0) fft_stage<LOGN, (1 << (LOGN % FPS_LR))>(z, tw, tid, Ns);
 }
 
-// (1) rows r0 = 2 blockIdx.x and r0 + 1 (the latter absent when nrows is odd) of in - shift ->
-// their DCT-II coefficients in out.  tw[m] = e^{-2 pi i m / N}, wk[k] = e^{-i pi k / 2N}
+// (1) DCT-II of row pairs (r0 = 2 p, r0 + 1; the latter absent when nrows is odd) of in - shift
+// -> their coefficients in out.  tw[m] = e^{-2 pi i m / N}, wk[k] = e^{-i pi k / 2N}.  Persistent:
+// a workgroup walks pairs p = blockIdx.x, + gridDim.x, ...; the next pair's rows are loaded into
+// registers while this pair's coefficients are formed and stored (the LDS allows two workgroups
+// per CU, so without that overlap the CU idles through every load)
 template <int LOGN>
-__global__ void __launch_bounds__(Fft<LOGN>::T) k_fps_dct(const double* __restrict__ in, const double* shiftp,
+__global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double* __restrict__ in, const double* shiftp,
                                                            double* __restrict__ out, int nrows, int ld,
                                                            const cplx* __restrict__ tw, const cplx* __restrict__ wk) {
     constexpr int N = Fft<LOGN>::N, T = Fft<LOGN>::T;
+    constexpr int PT = (N + T - 1) / T;
     extern __shared__ cplx z[];
     const int tid = threadIdx.x;
-    const int r0 = 2 * blockIdx.x;
-    const bool two = r0 + 1 < nrows;
+    const int npairs = (nrows + 1) / 2;
     const double sh = shiftp ? *shiftp : 0.0;
-    const double* a = in + (size_t)r0 * ld;
-    const double* b = a + ld;
-    for (int j = tid; j < N; j += T) {
-        const int n = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
-        z[n] = cplx{a[j] - sh, two ? b[j] - sh : 0.0};
-    }
-    __syncthreads();
-    fft_lds<LOGN>(z, tw, tid);
-    double* oa = out + (size_t)r0 * ld;
-    double* ob = oa + ld;
-    for (int k = tid; k < N; k += T) {
-        const cplx Zk = z[k], Zn = z[(N - k) & (N - 1)];
-        const cplx Va{0.5 * (Zk.x + Zn.x), 0.5 * (Zk.y - Zn.y)};
-        const cplx Vb{0.5 * (Zk.y + Zn.y), 0.5 * (Zn.x - Zk.x)};
-        const cplx w = wk[k];
-        oa[k] = fma(w.x, Va.x, -w.y * Va.y);
-        if (two) ob[k] = fma(w.x, Vb.x, -w.y * Vb.y);
+    double ra[PT], rb[PT];
+    auto load = [&](int p) {
+        const int r0 = 2 * p;
+        const bool two = r0 + 1 < nrows;
+        const double* a = in + (size_t)r0 * ld;
+#pragma unroll
+        for (int q = 0; q < PT; q++) {
+            const int j = tid + q * T;
+            if (j < N) {
+                ra[q] = a[j];
+                rb[q] = two ? a[ld + j] : sh;
+            }
+        }
+    };
+    // (N = 8192: the prefetch registers would spill -- load each pair when it starts)
+    constexpr bool PREF = FPS_PREF && LOGN <= 12;
+    int p = blockIdx.x;
+    if (PREF && p < npairs) load(p);
+    for (; p < npairs; p += gridDim.x) {
+        const int r0 = 2 * p;
+        const bool two = r0 + 1 < nrows;
+        if (!PREF) load(p);
+#pragma unroll
+        for (int q = 0; q < PT; q++) {
+            const int j = tid + q * T;
+            if (j < N) {
+                const int n = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
+                z[pz(n)] = cplx{ra[q] - sh, rb[q] - sh};
+            }
+        }
+        __syncthreads();
+        fft_lds<LOGN>(z, tw, tid);
+        if (PREF && p + (int)gridDim.x < npairs) load(p + gridDim.x);
+        double* oa = out + (size_t)r0 * ld;
+        double* ob = oa + ld;
+#pragma unroll
+        for (int q = 0; q < PT; q++) {
+            const int k = tid + q * T;
+            if (k < N) {
+                const cplx Zk = z[pz(k)], Zn = z[pz((N - k) & (N - 1))];
+                const cplx Va{0.5 * (Zk.x + Zn.x), 0.5 * (Zk.y - Zn.y)};
+                const cplx Vb{0.5 * (Zk.y + Zn.y), 0.5 * (Zn.x - Zk.x)};
+                const cplx w = wk[k];
+                oa[k] = fma(w.x, Va.x, -w.y * Va.y);
+                if (two) ob[k] = fma(w.x, Vb.x, -w.y * Vb.y);
+            }
+        }
+        __syncthreads();   // (z is rewritten by the next pair)
     }
 }
 
 // (3) the inverse: DCT-III with x_j = X_0 / N + (2 / N) sum_k>0 X_k cos(pi k (2j+1) / 2N), through
-// V_k = e^{i pi k / 2N} (X_k - i X_{N-k}) (X_N = 0), v = IFFT(V) = conj(FFT(conj(V))) / N
+// V_k = e^{i pi k / 2N} (X_k - i X_{N-k}) (X_N = 0), v = IFFT(V) = conj(FFT(conj(V))) / N.
+// Persistent like k_fps_dct
 template <int LOGN>
-__global__ void __launch_bounds__(Fft<LOGN>::T) k_fps_idct(const double* __restrict__ in, double* __restrict__ out,
+__global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const double* __restrict__ in, double* __restrict__ out,
                                                             int nrows, int ld, const cplx* __restrict__ tw,
                                                             const cplx* __restrict__ wk) {
     constexpr int N = Fft<LOGN>::N, T = Fft<LOGN>::T;
     constexpr int PT = (N + T - 1) / T;
     extern __shared__ cplx z[];
     const int tid = threadIdx.x;
-    const int r0 = 2 * blockIdx.x;
-    const bool two = r0 + 1 < nrows;
-    const double* a = in + (size_t)r0 * ld;
-    const double* b = a + ld;
-    for (int k = tid; k < N; k += T) z[k] = cplx{a[k], two ? b[k] : 0.0};
-    __syncthreads();
-    cplx v[PT];
-#pragma unroll
-    for (int p = 0; p < PT; p++) {
-        const int k = tid + p * T;
-        if (k < N) {
-            const cplx Xk = z[k];
-            const cplx Xn = k ? z[N - k] : cplx{0.0, 0.0};
-            const cplx w = wk[k];   // e^{-i theta}: e^{i theta} = (w.x, -w.y)
-            const double c = w.x, s = -w.y;
-            // Va = e^{i theta} (A_k - i A_{N-k}), Vb likewise; V = Va + i Vb; store conj(V)
-            const cplx Va{fma(c, Xk.x, s * Xn.x), fma(s, Xk.x, -c * Xn.x)};
-            const cplx Vb{fma(c, Xk.y, s * Xn.y), fma(s, Xk.y, -c * Xn.y)};
-            v[p] = cplx{Va.x - Vb.y, -(Va.y + Vb.x)};
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int p = 0; p < PT; p++) {
-        const int k = tid + p * T;
-        if (k < N) z[k] = v[p];
-    }
-    __syncthreads();
-    fft_lds<LOGN>(z, tw, tid);
+    const int npairs = (nrows + 1) / 2;
     const double rn = 1.0 / N;
-    double* oa = out + (size_t)r0 * ld;
-    double* ob = oa + ld;
-    for (int j = tid; j < N; j += T) {
-        const int n = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
-        const cplx y = z[n];
-        oa[j] = y.x * rn;
-        if (two) ob[j] = -y.y * rn;
+    double ra[PT], rb[PT];
+    auto load = [&](int p) {
+        const int r0 = 2 * p;
+        const bool two = r0 + 1 < nrows;
+        const double* a = in + (size_t)r0 * ld;
+#pragma unroll
+        for (int q = 0; q < PT; q++) {
+            const int k = tid + q * T;
+            if (k < N) {
+                ra[q] = a[k];
+                rb[q] = two ? a[ld + k] : 0.0;
+            }
+        }
+    };
+    constexpr bool PREF = FPS_PREF && LOGN <= 12;
+    int p = blockIdx.x;
+    if (PREF && p < npairs) load(p);
+    for (; p < npairs; p += gridDim.x) {
+        const int r0 = 2 * p;
+        const bool two = r0 + 1 < nrows;
+        if (!PREF) load(p);
+#pragma unroll
+        for (int q = 0; q < PT; q++) {
+            const int k = tid + q * T;
+            if (k < N) z[pz(k)] = cplx{ra[q], rb[q]};
+        }
+        __syncthreads();
+        cplx v[PT];
+#pragma unroll
+        for (int q = 0; q < PT; q++) {
+            const int k = tid + q * T;
+            if (k < N) {
+                const cplx Xk = z[pz(k)];
+                const cplx Xn = k ? z[pz(N - k)] : cplx{0.0, 0.0};
+                const cplx w = wk[k];   // e^{-i theta}: e^{i theta} = (w.x, -w.y)
+                const double c = w.x, s = -w.y;
+                // Va = e^{i theta} (A_k - i A_{N-k}), Vb likewise; V = Va + i Vb; store conj(V)
+                const cplx Va{fma(c, Xk.x, s * Xn.x), fma(s, Xk.x, -c * Xn.x)};
+                const cplx Vb{fma(c, Xk.y, s * Xn.y), fma(s, Xk.y, -c * Xn.y)};
+                v[q] = cplx{Va.x - Vb.y, -(Va.y + Vb.x)};
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PT; q++) {
+            const int k = tid + q * T;
+            if (k < N) z[pz(k)] = v[q];
+        }
+        __syncthreads();
+        fft_lds<LOGN>(z, tw, tid);
+        if (PREF && p + (int)gridDim.x < npairs) load(p + gridDim.x);
+        double* oa = out + (size_t)r0 * ld;
+        double* ob = oa + ld;
+#pragma unroll
+        for (int q = 0; q < PT; q++) {
+            const int j = tid + q * T;
+            if (j < N) {
+                const int n = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
+                const cplx y = z[pz(n)];
+                oa[j] = y.x * rn;
+                if (two) ob[j] = -y.y * rn;
+            }
+        }
+        __syncthreads();
     }
 }
 
 // ---- (2) the tridiagonal systems along x, one per mode (column k of the transformed plane) ----
 // Thomas on rows i (global gi): d_i = -(pw_i + pe_i) + mu_k, g_i = pw_i / p_{i-1},
 // p_i = d_i - g_i pe_{i-1}, y_i = f_i - g_i y_{i-1}; back: x_i = y_i / p_i - (pe_i / p_i) x_{i+1}.
-// Workgroup = FPS_G chunks (one wave each) x 64 modes.  rp0[c][k] = 1 / p of the row before chunk c.
+// Workgroup = FPS_G chunks (one wave each) x 128 modes (two per lane: 16-B loads, 1 KiB per wave
+// and row).  rp0[c][k] = 1 / p of the row before chunk c.
 
 // one row of the pivot recurrence: g = pw_i / p_{i-1} (from rprev = 1 / p_{i-1}); returns 1 / p_i
 // (mode 0's pinned last global row: 0)
@@ -220,40 +314,55 @@ __device__ inline double piv_next(const FpsArgs& a, int gi, int k, double mu, do
     return (a.pin && k == 0 && gi == a.nx - 1) ? 0.0 : 1.0 / p;
 }
 
-// T1: per chunk the forward recurrence from zero -> (E, Pi); the workgroup folds its chunks into
-// the group's aggregate (y_out = E + Pi y_in)
+__device__ inline double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+__device__ inline void st2(double* p, double x, double y) { *reinterpret_cast<double2*>(p) = double2{x, y}; }
+
+// T1: per chunk the forward recurrence from zero -> (E, Pi) into ca; the workgroup folds its chunks
+// into the group's aggregate ga (y_out = E + Pi y_in)
 __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1(FpsArgs a, const double* __restrict__ f) {
-    __shared__ double sE[FPS_G][64], sP[FPS_G][64];
+    __shared__ double2 sE[FPS_G][64], sP[FPS_G][64];
     const int lane = threadIdx.x, w = threadIdx.y;
-    const int k = blockIdx.x * 64 + lane;
+    const int k0 = 2 * (blockIdx.x * 64 + lane);
     const int grp = blockIdx.y, c = grp * FPS_G + w;
     const int li0 = c * FPS_M;
-    const int rows = k < a.ny ? min(FPS_M, a.nxl - li0) : 0;
-    double E = 0.0, Pi = 1.0;
+    const int rows = k0 < a.ny ? min(FPS_M, a.nxl - li0) : 0;
+    double E[2] = {0.0, 0.0}, P[2] = {1.0, 1.0};
     if (rows > 0) {
-        const double mu = a.mu[k];
-        double r = a.rp0[(size_t)c * a.ld + k];
+        const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
+        const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
+        double r[2] = {r0.x, r0.y};
 #pragma unroll
         for (int t = 0; t < FPS_M; t++) {
             if (t < rows) {
-                double g;
-                r = piv_next(a, a.i0 + li0 + t, k, mu, r, g);
-                E = fma(-g, E, f[(size_t)(li0 + t) * a.ld + k]);
-                Pi = -g * Pi;
+                const int gi = a.i0 + li0 + t;
+                const double2 fv = ld2(f + (size_t)(li0 + t) * a.ld + k0);
+                const double fm[2] = {fv.x, fv.y};
+#pragma unroll
+                for (int m = 0; m < 2; m++) {
+                    double g;
+                    r[m] = piv_next(a, gi, k0 + m, mu[m], r[m], g);
+                    E[m] = fma(-g, E[m], fm[m]);
+                    P[m] = -g * P[m];
+                }
             }
         }
+        st2(a.ca + (size_t)c * a.ld + k0, E[0], E[1]);
+        st2(a.ca + (size_t)(a.nch + c) * a.ld + k0, P[0], P[1]);
     }
-    sE[w][lane] = E;
-    sP[w][lane] = Pi;
+    sE[w][lane] = double2{E[0], E[1]};
+    sP[w][lane] = double2{P[0], P[1]};
     __syncthreads();
-    if (w == 0 && k < a.ny) {
-        double GE = 0.0, GP = 1.0;
+    if (w == 0 && k0 < a.ny) {
+        double GE[2] = {0.0, 0.0}, GP[2] = {1.0, 1.0};
         for (int q = 0; q < FPS_G; q++) {
-            GE = fma(sP[q][lane], GE, sE[q][lane]);
-            GP = sP[q][lane] * GP;
+            const double2 e = sE[q][lane], pp = sP[q][lane];
+            GE[0] = fma(pp.x, GE[0], e.x);
+            GE[1] = fma(pp.y, GE[1], e.y);
+            GP[0] = pp.x * GP[0];
+            GP[1] = pp.y * GP[1];
         }
-        a.ga[(size_t)grp * a.ld + k] = GE;
-        a.ga[(size_t)(a.ngrp + grp) * a.ld + k] = GP;
+        st2(a.ga + (size_t)grp * a.ld + k0, GE[0], GE[1]);
+        st2(a.ga + (size_t)(a.ngrp + grp) * a.ld + k0, GP[0], GP[1]);
     }
 }
 
@@ -265,13 +374,27 @@ __global__ void k_fps_scan(int ngrp, int ld, int ny, const double* __restrict__ 
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ny) return;
     double Y = rin ? rin[k] : 0.0, AE = 0.0, AP = 1.0;
-    for (int q = 0; q < ngrp; q++) {
-        const int grp = backward ? ngrp - 1 - q : q;
-        const double E = agg[(size_t)grp * ld + k], P = agg[(size_t)(ngrp + grp) * ld + k];
-        carry[(size_t)grp * ld + k] = Y;
-        Y = fma(P, Y, E);
-        AE = fma(P, AE, E);
-        AP = P * AP;
+    constexpr int B = 8;   // (the loads of B groups in flight together: the fold is a dependent chain)
+    for (int q0 = 0; q0 < ngrp; q0 += B) {
+        double E[B], P[B];
+#pragma unroll
+        for (int t = 0; t < B; t++) {
+            const int q = q0 + t;
+            const int grp = backward ? ngrp - 1 - q : q;
+            E[t] = q < ngrp ? agg[(size_t)grp * ld + k] : 0.0;
+            P[t] = q < ngrp ? agg[(size_t)(ngrp + grp) * ld + k] : 1.0;
+        }
+#pragma unroll
+        for (int t = 0; t < B; t++) {
+            const int q = q0 + t;
+            if (q < ngrp) {
+                const int grp = backward ? ngrp - 1 - q : q;
+                carry[(size_t)grp * ld + k] = Y;
+                Y = fma(P[t], Y, E[t]);
+                AE = fma(P[t], AE, E[t]);
+                AP = P[t] * AP;
+            }
+        }
     }
     if (rout) {
         rout[k] = AE;
@@ -279,112 +402,134 @@ __global__ void k_fps_scan(int ngrp, int ld, int ny, const double* __restrict__ 
     }
 }
 
-// T2: the chunk's exact forward values (its carry-in: the group's, through the group's earlier
-// chunks), then the back substitution from zero -> xl (in place over f) and the chunk's backward
-// aggregate (x_s = BX + BR x_e) into cb; the workgroup folds its chunks into gb
+// T2: the chunk's carry-in (the group's, through the group's earlier chunks: T1's aggregates), the
+// exact forward values from it, then the back substitution from zero -> xl (in place over f) and the
+// chunk's backward aggregate (x_s = BX + BR x_e) into cb; the workgroup folds its chunks into gb
 __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2(FpsArgs a, double* __restrict__ f) {
-    __shared__ double sE[FPS_G][64], sP[FPS_G][64];
+    __shared__ double2 sX[FPS_G][64], sR[FPS_G][64];
     const int lane = threadIdx.x, w = threadIdx.y;
-    const int k = blockIdx.x * 64 + lane;
+    const int k0 = 2 * (blockIdx.x * 64 + lane);
     const int grp = blockIdx.y, c = grp * FPS_G + w;
     const int li0 = c * FPS_M;
-    const int rows = k < a.ny ? min(FPS_M, a.nxl - li0) : 0;
-    double y[FPS_M], pi[FPS_M], rp[FPS_M];
-    double E = 0.0, Pi = 1.0;
+    const int rows = k0 < a.ny ? min(FPS_M, a.nxl - li0) : 0;
+    double BX[2] = {0.0, 0.0}, BR[2] = {1.0, 1.0};
     if (rows > 0) {
-        const double mu = a.mu[k];
-        double r = a.rp0[(size_t)c * a.ld + k];
+        const double2 y0 = ld2(a.gc + (size_t)grp * a.ld + k0);
+        double y[2] = {y0.x, y0.y};
+        for (int q = grp * FPS_G; q < c; q++) {
+            const double2 e = ld2(a.ca + (size_t)q * a.ld + k0), pp = ld2(a.ca + (size_t)(a.nch + q) * a.ld + k0);
+            y[0] = fma(pp.x, y[0], e.x);
+            y[1] = fma(pp.y, y[1], e.y);
+        }
+        const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
+        const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
+        double r[2] = {r0.x, r0.y};
+        double yv[FPS_M][2], rv[FPS_M][2];
 #pragma unroll
         for (int t = 0; t < FPS_M; t++) {
             if (t < rows) {
-                double g;
-                r = piv_next(a, a.i0 + li0 + t, k, mu, r, g);
-                E = fma(-g, E, f[(size_t)(li0 + t) * a.ld + k]);
-                Pi = -g * Pi;
-                y[t] = E;
-                pi[t] = Pi;
-                rp[t] = r;
+                const int gi = a.i0 + li0 + t;
+                const double2 fv = ld2(f + (size_t)(li0 + t) * a.ld + k0);
+                const double fm[2] = {fv.x, fv.y};
+#pragma unroll
+                for (int m = 0; m < 2; m++) {
+                    double g;
+                    r[m] = piv_next(a, gi, k0 + m, mu[m], r[m], g);
+                    y[m] = fma(-g, y[m], fm[m]);
+                    yv[t][m] = y[m];
+                    rv[t][m] = r[m];
+                }
             }
         }
-    }
-    sE[w][lane] = E;
-    sP[w][lane] = Pi;
-    __syncthreads();
-    double Y = k < a.ny ? a.gc[(size_t)grp * a.ld + k] : 0.0;
-    for (int q = 0; q < w; q++) Y = fma(sP[q][lane], Y, sE[q][lane]);
-    double BX = 0.0, BR = 1.0;
-    if (rows > 0) {
-        double xl = 0.0, rho = 1.0;
+        double xl[2] = {0.0, 0.0};
 #pragma unroll
         for (int t = FPS_M - 1; t >= 0; t--) {
             if (t < rows) {
                 const int gi = a.i0 + li0 + t;
-                const double yt = fma(pi[t], Y, y[t]);
-                const double q = -a.pe[gi] * rp[t];
-                xl = fma(yt, rp[t], q * xl);
-                rho = q * rho;
-                f[(size_t)(li0 + t) * a.ld + k] = xl;
+                const double pe = a.pe[gi];
+#pragma unroll
+                for (int m = 0; m < 2; m++) {
+                    const double q = -pe * rv[t][m];
+                    xl[m] = fma(yv[t][m], rv[t][m], q * xl[m]);
+                    BR[m] = q * BR[m];
+                }
+                st2(f + (size_t)(li0 + t) * a.ld + k0, xl[0], xl[1]);
             }
         }
-        BX = xl;
-        BR = rho;
-        a.cb[(size_t)c * a.ld + k] = BX;
-        a.cb[(size_t)(a.nch + c) * a.ld + k] = BR;
+        BX[0] = xl[0];
+        BX[1] = xl[1];
+        st2(a.cb + (size_t)c * a.ld + k0, BX[0], BX[1]);
+        st2(a.cb + (size_t)(a.nch + c) * a.ld + k0, BR[0], BR[1]);
     }
-    __syncthreads();   // (sE / sP reused)
-    sE[w][lane] = BX;
-    sP[w][lane] = BR;
+    sX[w][lane] = double2{BX[0], BX[1]};
+    sR[w][lane] = double2{BR[0], BR[1]};
     __syncthreads();
-    if (w == 0 && k < a.ny) {
-        double GX = 0.0, GR = 1.0;
+    if (w == 0 && k0 < a.ny) {
+        double GX[2] = {0.0, 0.0}, GR[2] = {1.0, 1.0};
         for (int q = FPS_G - 1; q >= 0; q--) {
-            GX = fma(sP[q][lane], GX, sE[q][lane]);
-            GR = sP[q][lane] * GR;
+            const double2 x = sX[q][lane], rr = sR[q][lane];
+            GX[0] = fma(rr.x, GX[0], x.x);
+            GX[1] = fma(rr.y, GX[1], x.y);
+            GR[0] = rr.x * GR[0];
+            GR[1] = rr.y * GR[1];
         }
-        a.gb[(size_t)grp * a.ld + k] = GX;
-        a.gb[(size_t)(a.ngrp + grp) * a.ld + k] = GR;
+        st2(a.gb + (size_t)grp * a.ld + k0, GX[0], GX[1]);
+        st2(a.gb + (size_t)(a.ngrp + grp) * a.ld + k0, GR[0], GR[1]);
     }
 }
 
 // T3: the chunk's carry-in from the next chunk (the group's carry through its later chunks), then
 // x_i = xl_i + rho_i x_e (in place)
 __global__ void __launch_bounds__(64 * FPS_G) k_fps_t3(FpsArgs a, double* __restrict__ f) {
-    __shared__ double sX[FPS_G][64], sR[FPS_G][64];
+    __shared__ double2 sX[FPS_G][64], sR[FPS_G][64];
     const int lane = threadIdx.x, w = threadIdx.y;
-    const int k = blockIdx.x * 64 + lane;
+    const int k0 = 2 * (blockIdx.x * 64 + lane);
     const int grp = blockIdx.y, c = grp * FPS_G + w;
     const int li0 = c * FPS_M;
-    const int rows = k < a.ny ? min(FPS_M, a.nxl - li0) : 0;
-    double BX = 0.0, BR = 1.0;
+    const int rows = k0 < a.ny ? min(FPS_M, a.nxl - li0) : 0;
+    double2 bx{0.0, 0.0}, br{1.0, 1.0};
     if (rows > 0) {
-        BX = a.cb[(size_t)c * a.ld + k];
-        BR = a.cb[(size_t)(a.nch + c) * a.ld + k];
+        bx = ld2(a.cb + (size_t)c * a.ld + k0);
+        br = ld2(a.cb + (size_t)(a.nch + c) * a.ld + k0);
     }
-    sX[w][lane] = BX;
-    sR[w][lane] = BR;
+    sX[w][lane] = bx;
+    sR[w][lane] = br;
     __syncthreads();
     if (rows <= 0) return;
-    double X = a.gx[(size_t)grp * a.ld + k];
-    for (int q = FPS_G - 1; q > w; q--) X = fma(sR[q][lane], X, sX[q][lane]);
-    const double mu = a.mu[k];
-    double rp[FPS_M];
-    double r = a.rp0[(size_t)c * a.ld + k];
+    const double2 x0 = ld2(a.gx + (size_t)grp * a.ld + k0);
+    double X[2] = {x0.x, x0.y};
+    for (int q = FPS_G - 1; q > w; q--) {
+        const double2 x = sX[q][lane], rr = sR[q][lane];
+        X[0] = fma(rr.x, X[0], x.x);
+        X[1] = fma(rr.y, X[1], x.y);
+    }
+    const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
+    const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
+    double r[2] = {r0.x, r0.y};
+    double rv[FPS_M][2];
 #pragma unroll
     for (int t = 0; t < FPS_M; t++) {
         if (t < rows) {
-            double g;
-            r = piv_next(a, a.i0 + li0 + t, k, mu, r, g);
-            rp[t] = r;
+            const int gi = a.i0 + li0 + t;
+#pragma unroll
+            for (int m = 0; m < 2; m++) {
+                double g;
+                r[m] = piv_next(a, gi, k0 + m, mu[m], r[m], g);
+                rv[t][m] = r[m];
+            }
         }
     }
-    double rho = 1.0;
+    double rho[2] = {1.0, 1.0};
 #pragma unroll
     for (int t = FPS_M - 1; t >= 0; t--) {
         if (t < rows) {
             const int gi = a.i0 + li0 + t;
-            rho = -a.pe[gi] * rp[t] * rho;
-            double* p = f + (size_t)(li0 + t) * a.ld + k;
-            *p = fma(rho, X, *p);
+            const double pe = a.pe[gi];
+            double* p = f + (size_t)(li0 + t) * a.ld + k0;
+            const double2 xl = ld2(p);
+            rho[0] = -pe * rv[t][0] * rho[0];
+            rho[1] = -pe * rv[t][1] * rho[1];
+            st2(p, fma(rho[0], X[0], xl.x), fma(rho[1], X[1], xl.y));
         }
     }
 }
@@ -393,8 +538,15 @@ template <int LOGN>
 void dct_pair(bool inverse, const double* in, const double* shift, double* out, int nrows, int ld, const void* tw,
               const void* wk, hipStream_t st) {
     constexpr int T = Fft<LOGN>::T;
-    const size_t lds = sizeof(cplx) * (size_t)Fft<LOGN>::N;
-    const dim3 grid((nrows + 1) / 2);
+    const size_t lds = sizeof(cplx) * (size_t)FftLds<LOGN>::n;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    }
+    // (two workgroups per CU fit the LDS: one persistent round)
+    const dim3 grid(std::min((nrows + 1) / 2, 2 * cus));
     if (inverse) {
         static bool attr = false;
         if (!attr) {
@@ -441,16 +593,16 @@ int launch_fps_dct(bool inverse, const double* in, const double* shift, double* 
 }
 
 void launch_fps_t1(const FpsArgs& a, const double* f, hipStream_t st) {
-    hipLaunchKernelGGL(k_fps_t1, dim3((a.ny + 63) / 64, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
+    hipLaunchKernelGGL(k_fps_t1, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
 }
 void launch_fps_t2(const FpsArgs& a, double* f, hipStream_t st) {
-    hipLaunchKernelGGL(k_fps_t2, dim3((a.ny + 63) / 64, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
+    hipLaunchKernelGGL(k_fps_t2, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
 }
 void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st) {
-    hipLaunchKernelGGL(k_fps_t3, dim3((a.ny + 63) / 64, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
+    hipLaunchKernelGGL(k_fps_t3, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
 }
 void launch_fps_scan(const FpsArgs& a, bool backward, const double* rin, double* rout, hipStream_t st) {
-    hipLaunchKernelGGL(k_fps_scan, dim3((a.ny + 255) / 256), dim3(256), 0, st, a.ngrp, a.ld, a.ny,
+    hipLaunchKernelGGL(k_fps_scan, dim3((a.ny + 63) / 64), dim3(64), 0, st, a.ngrp, a.ld, a.ny,
                        backward ? a.gb : a.ga, backward ? a.gx : a.gc, rin, rout, backward ? 1 : 0);
 }
 

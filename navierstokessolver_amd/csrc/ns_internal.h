@@ -279,6 +279,7 @@ struct FpsArgs {
     const double *pw, *pe;         // x coefficients (global index; Coef::pw / pe)
     const double* mu;              // mode eigenvalues of Ly (ny)
     const double* rp0;             // nch x ld: 1 / pivot of the row before each chunk
+    double* ca;                    // forward chunk aggregates (E, Pi: 2 x nch x ld)
     double *ga, *gc;               // forward: group aggregates (E, Pi: 2 x ngrp x ld), group carry-ins
     double *gb, *gx;               // backward: group aggregates (X, R), group carry-ins
     double* cb;                    // backward chunk aggregates (2 x nch x ld)
