@@ -534,6 +534,21 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t3(FpsArgs a, double* __rest
     }
 }
 
+// multi-rank: this rank's carry-in from every rank's aggregate (g: P slots of 2 x ld, slot q = rank
+// q's (E, Pi) or (X, R)): forward, the fold of ranks 0 .. r-1 in order; backward, of P-1 .. r+1
+__global__ void k_fps_rank_carry(const double* __restrict__ g, int P, int r, int ld, int ny, int backward,
+                                 double* __restrict__ rin) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ny) return;
+    double Y = 0.0;
+    if (!backward) {
+        for (int q = 0; q < r; q++) Y = fma(g[(size_t)(2 * q + 1) * ld + k], Y, g[(size_t)(2 * q) * ld + k]);
+    } else {
+        for (int q = P - 1; q > r; q--) Y = fma(g[(size_t)(2 * q + 1) * ld + k], Y, g[(size_t)(2 * q) * ld + k]);
+    }
+    rin[k] = Y;
+}
+
 template <int LOGN>
 void dct_pair(bool inverse, const double* in, const double* shift, double* out, int nrows, int ld, const void* tw,
               const void* wk, hipStream_t st) {
@@ -600,6 +615,11 @@ void launch_fps_t2(const FpsArgs& a, double* f, hipStream_t st) {
 }
 void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_t3, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
+}
+void launch_fps_rank_carry(const FpsArgs& a, const double* gathered, int P, int r, bool backward, double* rin,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(k_fps_rank_carry, dim3((a.ny + 255) / 256), dim3(256), 0, st, gathered, P, r, a.ld, a.ny,
+                       backward ? 1 : 0, rin);
 }
 void launch_fps_scan(const FpsArgs& a, bool backward, const double* rin, double* rout, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_scan, dim3((a.ny + 63) / 64), dim3(64), 0, st, a.ngrp, a.ld, a.ny,

@@ -296,5 +296,9 @@ void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st);
 // group scan (forward: ga -> gc ascending; backward: gb -> gx descending) from the carry-in rin (null:
 // 0; multi-rank: the fold of the other ranks' aggregates); rout (if not null) <- this rank's aggregate
 void launch_fps_scan(const FpsArgs& a, bool backward, const double* rin, double* rout, hipStream_t st);
+// multi-rank: rin <- the fold of the other ranks' aggregates before (forward) / after (backward) rank r
+// (gathered: P slots of 2 x ld doubles, rank q's in slot q)
+void launch_fps_rank_carry(const FpsArgs& a, const double* gathered, int P, int r, bool backward, double* rin,
+                           hipStream_t st);
 
 }  // namespace nsg

@@ -279,6 +279,9 @@ struct ns_solver {
     const double *fps_tw = nullptr, *fps_wk = nullptr;
     int fps_check = 16;
     long fps_solves = 0;
+    // multi-rank: this rank's aggregate of a recurrence (2 x ld), every rank's (nranks x 2 x ld, one
+    // allgather per direction and solve) and the carry-in folded from them (ld)
+    double *fps_ragg = nullptr, *fps_gath = nullptr, *fps_rin = nullptr;
     double fps_res = -1.0;       // the last checked solve's relative residual
 };
 
@@ -1595,6 +1598,57 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
     return 0;
 }
 
+// every rank's aggregate of one recurrence direction (fps_ragg, 2 x ld) into fps_gath (slot q = rank q).
+// RCCL: ncclAllGather; host transport: an exact sum-allreduce with the foreign slots zeroed; a virtual
+// slab (loopback, nranks > 1): the same messages with itself as every peer
+int fps_allgather(ns_solver* s) {
+    const size_t n = 2 * (size_t)s->g.ld, P = (size_t)s->nranks, r = (size_t)s->rank;
+    s->n_allred++;
+    s->x_link += 8.0 * (double)n;   // (this rank's slot, one link per peer)
+    if (s->ht.allreduce) {
+        CHK(ensure_stage(s, P * n));
+        // (the stream first: an earlier allreduce's copy back from the stage may still be queued --
+        // the stage is written on the host only after the sync)
+        HIPCHK(hipMemcpyAsync(s->stage + r * n, s->fps_ragg, n * 8, hipMemcpyDeviceToHost, s->st));
+        HIPCHK(hipStreamSynchronize(s->st));
+        std::fill(s->stage, s->stage + r * n, 0.0);
+        std::fill(s->stage + (r + 1) * n, s->stage + P * n, 0.0);
+        if (s->ht.allreduce(s->ht.user, s->stage, (int32_t)(P * n), 0) != 0) {
+            set_err("host transport allreduce failed");
+            return NS_ERCCL;
+        }
+        HIPCHK(hipMemcpyAsync(s->fps_gath, s->stage, P * n * 8, hipMemcpyHostToDevice, s->st));
+        return 0;
+    }
+    if (s->loopback) {
+        HIPCHK(hipMemcpyAsync(s->fps_gath + r * n, s->fps_ragg, n * 8, hipMemcpyDeviceToDevice, s->st));
+        NCCLCHK(ncclGroupStart());
+        for (size_t q = 0; q < P; q++) {
+            if (q == r) continue;
+            NCCLCHK(ncclSend(s->fps_ragg, n, ncclDouble, 0, s->comm, s->st));
+            NCCLCHK(ncclRecv(s->fps_gath + q * n, n, ncclDouble, 0, s->comm, s->st));
+        }
+        NCCLCHK(ncclGroupEnd());
+        return 0;
+    }
+    NCCLCHK(ncclAllGather(s->fps_ragg, s->fps_gath, n, ncclDouble, s->comm, s->st));
+    return 0;
+}
+
+// the group scan of one direction; multi-rank: this rank's aggregate first (its carries from zero,
+// rewritten below), the allgather, the carry-in from the ranks before / after, then the scan from it
+int fps_scan(ns_solver* s, bool backward) {
+    if (s->nranks == 1) {
+        nsg::launch_fps_scan(s->fa, backward, nullptr, nullptr, s->st);
+        return 0;
+    }
+    nsg::launch_fps_scan(s->fa, backward, nullptr, s->fps_ragg, s->st);
+    CHK(fps_allgather(s));
+    nsg::launch_fps_rank_carry(s->fa, s->fps_gath, s->nranks, s->rank, backward, s->fps_rin, s->st);
+    nsg::launch_fps_scan(s->fa, backward, s->fps_rin, nullptr, s->st);
+    return 0;
+}
+
 // the direct solve (ns_fps.hip): RPHI - shift -> PHI through the transformed plane in TMP; one
 // "iteration".  A checked solve computes its residual; speculating, K5 is enqueued before the host
 // reads it (as after a predicted multigrid check).  A residual above rtol (never seen: ~1e-14)
@@ -1613,9 +1667,9 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         return NS_EINVAL;
     }
     nsg::launch_fps_t1(s->fa, F, s->st);
-    nsg::launch_fps_scan(s->fa, false, nullptr, nullptr, s->st);
+    CHK(fps_scan(s, false));
     nsg::launch_fps_t2(s->fa, F, s->st);
-    nsg::launch_fps_scan(s->fa, true, nullptr, nullptr, s->st);
+    CHK(fps_scan(s, true));
     nsg::launch_fps_t3(s->fa, F, s->st);
     nsg::launch_fps_dct(true, F, nullptr, s->arr[NS_ARR_PHI], g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st);
     if (t) HIPCHK(hipEventRecord(s->ev[1], s->st));
@@ -1634,6 +1688,7 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         }
         return 0;
     }
+    CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));   // (slabs: the residual's neighbour rows)
     const int nb = nsg::launch_pois_residual(g, s->c, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,
                                              s->part, s->st);
     nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
@@ -1657,11 +1712,13 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     *res = s->fps_res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
     if (s->verbose) fprintf(stderr, "nsgpu poisson: direct solve, rel. residual %.3e\n", *res);
     if (!std::isfinite(r2)) { set_err("Poisson residual is not finite"); return NS_EDIVERGE; }
-    if (r2 <= s->rtol * s->rtol * b2 || r2 == 0.0) {
+    // (a virtual slab's own residual is not the global solve's: it replays, never falls back)
+    if (r2 <= s->rtol * s->rtol * b2 || r2 == 0.0 || s->rp_c >= 0) {
         if (spec) { s->k5_spec = 1; s->n_spec_hit++; }
         return 0;
     }
     // (the speculative K5 wrote only the ping-pong partners: correct() runs it again)
+    CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));   // (the direct solve read no rhs ghost rows)
     int c = 0;
     CHK(s->poisson == NS_POISSON_MG ? pois_solve_mg(s, &c, res, stt) : pois_solve(s, &c, res, stt));
     *its = 1 + c;
@@ -1700,7 +1757,8 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     a.pin = 1;   // (every side of the rectangle is zero-flux for phi: Lx 1 = 0)
     const int nchp = a.ngrp * nsg::FPS_G;   // (t1 / t2 / t3 address whole groups' chunks)
     const size_t n_tab = 4 * (size_t)N + (size_t)N, n_rp0 = (size_t)nchp * ld, n_g = (size_t)a.ngrp * ld;
-    const size_t total = n_tab + n_rp0 + 6 * n_g + 4 * (size_t)nchp * ld;
+    const size_t n_mr = s->nranks > 1 ? (size_t)(2 + 2 * s->nranks + 1) * ld : 0;
+    const size_t total = n_tab + n_rp0 + 6 * n_g + 4 * (size_t)nchp * ld + n_mr;
     std::vector<double> h(n_tab + n_rp0, 0.0);
     const double pi = 3.14159265358979323846;
     for (int m = 0; m < N; m++) {
@@ -1741,7 +1799,12 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     a.gb = q; q += 2 * n_g;
     a.gx = q; q += n_g;
     a.cb = q; q += 2 * (size_t)nchp * ld;
-    a.ca = q;
+    a.ca = q; q += 2 * (size_t)nchp * ld;
+    if (n_mr) {
+        s->fps_ragg = q; q += 2 * (size_t)ld;
+        s->fps_gath = q; q += 2 * (size_t)s->nranks * ld;
+        s->fps_rin = q;
+    }
     a.pw = s->c.pw;
     a.pe = s->c.pe;
     return 0;
@@ -2565,7 +2628,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         for (int i = 1; i < gd->nx; i++) yuni &= gd->hx[i] == gd->hx[0];
         const char* fe = getenv("NSGPU_FPS");
         s->fps = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !masked && !outflow && yuni &&
-                 nsg::fps_log2(gd->ny) >= 0 && p->nranks == 1;
+                 nsg::fps_log2(gd->ny) >= 0;
         if (const char* e = getenv("NSGPU_FPS_CHECK")) s->fps_check = std::max(0, std::atoi(e));
         if (s->fps) s->phi_extrap = 0;   // (no initial guess: no history planes)
     }
@@ -2850,10 +2913,14 @@ static int step_body_(ns_solver* s, ns_stats& st) {
     s->k3_spec = 0;
     CHK(consistent_rhs(s));                                        // stretched grids only
     // rhs_phi ghost rows: with the multigrid's first overlapped FUSE_R exchange when it has one
-    if (s->nranks > 1 && s->overlap && s->cst && s->poisson == NS_POISSON_MG && !s->kv[0] && !s->lv.empty() &&
-        !s->lv[0].repl && fused_restrict(s, 0) && !tile_level(s, 0))
+    // (the direct solve reads only the slab's own rows)
+    if (s->fps) {
+    } else if (s->nranks > 1 && s->overlap && s->cst && s->poisson == NS_POISSON_MG && !s->kv[0] &&
+               !s->lv.empty() && !s->lv[0].repl && fused_restrict(s, 0) && !tile_level(s, 0)) {
         level(s, 0).b_pend = true;
-    else CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
+    } else {
+        CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
+    }
     CHK(pois_solve_any(s, &st.it_phi, &st.res_phi, &st));         // KSPSolve(phiSolver)  (:551)
     CHK(correct(s));                                               // CorrectVelocities    (:552)
     return 0;

@@ -9,10 +9,16 @@ Tolerances (written per test):
   * the solve's own relative residual ||b - mean - L phi|| / ||b - mean||: <= 1e-11 (one solve, no
     iteration: its = 1);
   * repeat runs: bit-identical (a fixed arithmetic sequence)."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
 from oracle import OGrid, OSolver
+
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 pytestmark = pytest.mark.gpu
 
@@ -119,3 +125,35 @@ def test_multigrid_still_selectable(gpu, monkeypatch):
         sol[fps] = demean(gs.get(gpu.NS_ARR_PHI))
         gs.close()
     assert rel(sol["0"], sol["1"]) <= 1e-9
+
+
+def _slabs(tmp_path, nproc, *args, port):
+    out = tmp_path / "r.npz"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(HERE, "mr_worker.py"),
+           "--output", str(out), *args]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=150, env=dict(os.environ))
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    r = dict(np.load(out, allow_pickle=False))
+    assert str(r["status"]) == "ok", r["status"]
+    return r
+
+
+@pytest.mark.parametrize("n,ny,nproc", [(128, 128, 2), (200, 64, 3), (256, 256, 4)])
+def test_direct_solve_on_slabs_matches_one_rank(tmp_path, gpu, n, ny, nproc):
+    """x-slabs (host transport, every rank on the one GPU): each rank runs its chunks' recurrences,
+    the ranks' aggregates travel in one allgather per direction and solve, and the gathered steps
+    equal one rank's -- the chunk boundaries move with the slab edges, so to rounding: u, v and the
+    monitor to 1e-10, phi (modulo its mean) to 1e-10 of its max; one solve per step on every rank."""
+    steps = 6
+    r = _slabs(tmp_path, nproc, "--xport", "host", "--size", str(n), "--size-y", str(ny), "--nsteps", str(steps),
+               "--solver", str(gpu.NS_POISSON_MG), "--tol", "1e-10", port=29761 + nproc)
+    gs = gpu.GpuSolver(gpu.rectangle(n, ny), 1.0 / (8 * n), 100.0, rtol=1e-10, device=0)
+    mm = np.array([list(gs.step().values())[:7] for _ in range(steps)])
+    u, v, phi = gs.fields()
+    gs.close()
+    assert np.max(np.abs(r["u"] - u)) <= 1e-10
+    assert np.max(np.abs(r["v"] - v)) <= 1e-10
+    assert rel(demean(r["phi"]), demean(phi)) <= 1e-10
+    np.testing.assert_allclose(r["mm"][:, :4], mm[:, :4], atol=1e-10)
+    assert np.all(r["mm"][:, 6] == 1) and np.all(mm[:, 6] == 1), (r["mm"][:, 6], mm[:, 6])

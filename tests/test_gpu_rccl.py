@@ -65,6 +65,7 @@ def test_virtual_slab_replays_counts(gpu, monkeypatch):
     must run those counts exactly, issue exchanges and all-reduces (and the agglomeration
     gather: the level hierarchy has replicated levels at 4 ranks), and stay finite."""
     n = 512
+    monkeypatch.setenv("NSGPU_FPS", "0")   # (the multigrid's replayed cycles; the direct solve's: below)
     monkeypatch.setenv("NSGPU_RCCL_LOOPBACK", "1")
     monkeypatch.setenv("NSGPU_VIRTUAL_ITERS", "4:2,6:3")
     gs = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0, device=0, rank=2, nranks=4)
@@ -80,3 +81,19 @@ def test_virtual_slab_replays_counts(gpu, monkeypatch):
     monkeypatch.delenv("NSGPU_VIRTUAL_ITERS")
     with pytest.raises(gpu.NsError):   # a virtual slab without replayed counts would never converge
         gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0, device=0, rank=2, nranks=4)
+
+
+def test_virtual_slab_direct_solve(gpu, monkeypatch):
+    """The direct Poisson solve on a virtual slab (rank 2 of 4): one solve per step (it_phi 1), the
+    two per-direction allgathers of the ranks' recurrence aggregates counted as collectives and their
+    bytes on the link, finite fields."""
+    n = 512
+    monkeypatch.setenv("NSGPU_RCCL_LOOPBACK", "1")
+    monkeypatch.setenv("NSGPU_VIRTUAL_ITERS", "4:1")
+    gs = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0, device=0, rank=2, nranks=4)
+    st = [gs.step() for _ in range(3)]
+    u, v, _ = gs.fields()
+    gs.close()
+    assert [(s["it_u"], s["it_phi"]) for s in st] == [(4, 1)] * 3
+    assert all(s["n_allreduces"] >= 2 and s["x_link_bytes"] >= 2 * 2 * n * 8 for s in st)
+    assert np.all(np.isfinite(u)) and np.all(np.isfinite(v))
