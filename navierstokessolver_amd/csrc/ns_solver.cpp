@@ -283,6 +283,7 @@ struct ns_solver {
     // allgather per direction and solve) and the carry-in folded from them (ld)
     double *fps_ragg = nullptr, *fps_gath = nullptr, *fps_rin = nullptr;
     double fps_res = -1.0;       // the last checked solve's relative residual
+    bool fps_strict = false;     // a check failed (rtol below the solve's round-off): check every solve
 };
 
 namespace {
@@ -1676,7 +1677,7 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     *its = 1;
     s->last_cycles = s->cur_cycles = -1;
     // (a standalone solve -- ns_kernel -- is always checked; inside steps every fps_check-th)
-    const bool check = !s->in_step || (s->fps_check > 0 && s->fps_solves % s->fps_check == 0);
+    const bool check = !s->in_step || s->fps_strict || (s->fps_check > 0 && s->fps_solves % s->fps_check == 0);
     if (s->in_step) s->fps_solves++;
     if (!check) {
         *res = s->fps_res;
@@ -1717,10 +1718,14 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         if (spec) { s->k5_spec = 1; s->n_spec_hit++; }
         return 0;
     }
-    // (the speculative K5 wrote only the ping-pong partners: correct() runs it again)
+    // (the speculative K5 wrote only the ping-pong partners: correct() runs it again).  An rtol below
+    // the direct solve's round-off (e.g. 1e-12 at 2048^2: 1.25e-12) -- every later solve is checked
+    // and refined the same way
+    if (s->in_step) s->fps_strict = true;
     CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));   // (the direct solve read no rhs ghost rows)
     int c = 0;
     CHK(s->poisson == NS_POISSON_MG ? pois_solve_mg(s, &c, res, stt) : pois_solve(s, &c, res, stt));
+    s->fps_res = *res;
     *its = 1 + c;
     return 0;
 }
