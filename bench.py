@@ -64,7 +64,20 @@ KERNELS = {
     "helmholtz": ("Helmholtz pass of one velocity component of (I - a L_V) u* = RHS (k_sweep3 + residual stage: "
                   "3 RB-SOR sweeps, after the wall bands; or k_sweep2: 2 sweeps; the one-rank two-field "
                   "k_sweep3<FUSE_UV> launch counts as two component passes)", 24),
+    # K1 (ConstructRHS_V): read u, v, phi^{n-1}, cu, cv 40 + write cu, cv, ru, rv 32 -- minus the
+    # in-place cu / cv reads counted once: 64
+    "rhs": ("k_rhs_s (K1, ConstructRHS_V: AB2 MUSCL/Rusanov convection + CN-explicit diffusion + wall terms)", 64),
+    # (r4) the direct Poisson solve (ns_fps.hip): the rows' DCT-II read b 8 + write 8; the
+    # recurrences along x: t1 read 8, t2 read 8 + write 8, t3 read 8 + write 8 (chunk / group
+    # aggregates ~1 B/cell more, not counted) -- one interval over five launches; the inverse DCT
+    # read 8 + write 8
+    "fps_dct": ("k_fps_dct (direct Poisson solve: DCT-II of every row pair of b - mean, Stockham FFT in LDS)", 16),
+    "fps_tri": ("k_fps_t1 + scan + k_fps_t2 + scan + k_fps_t3 (direct Poisson solve: the tridiagonal "
+                "recurrences along x, one per mode, chunked; five launches timed as one interval)", 40),
+    "fps_idct": ("k_fps_idct (direct Poisson solve: DCT-III of every row pair -> phi)", 16),
 }
+# one-launch kernels (the `roofline` candidates; fps_tri is five launches)
+SINGLE_LAUNCH = ("restrict", "prolong", "cycle", "guess", "helmholtz", "rhs", "fps_dct", "fps_idct")
 JACOBI_LABEL = "k_jacobi_s<double> (one weighted-Jacobi sweep of the Poisson operator, the north star's roofline kernel)"
 SWEEP_BYTES_PER_CELL = 24
 # configs[4]'s fp32-field Jacobi sweep: read phi 4 + read b 4 + write phi 4 (fp64 arithmetic / residual)
@@ -187,8 +200,10 @@ def cpu_baseline(n, re, dt, omega_v, omega_mg, state, gpu_next=None):
         "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "threads_used": nt,
         "sample": (f"one full time step of the {n}^2 cavity in the oracle's C restatement (oracle/ns_oracle.c, "
                    f"-O3, OpenMP), started from the GPU's state after its timed steps; same algorithm as the GPU "
-                   f"(MG V(2,2) Poisson: {its1[2]} V-cycles from phi^(n-1) -- the GPU's extrapolated guess needs "
-                   f"fewer; RB-SOR Helmholtz: {its1[0]} sweeps per component), {t1:.1f} s on 1 thread, "
+                   + ("(the direct Poisson solve: DCT along y, Thomas along x; " if its1[2] == 1 else
+                      f"(MG V(2,2) Poisson: {its1[2]} V-cycles from phi^(n-1) -- the GPU's extrapolated guess needs "
+                      f"fewer; ")
+                   + f"RB-SOR Helmholtz: {its1[0]} sweeps per component), {t1:.1f} s on 1 thread, "
                    f"{tn:.1f} s on {nt} threads"),
         "parity": parity,
     }
@@ -315,7 +330,13 @@ def main():
              "restrict": (sum(s["t_restrict_kernel_ms"] for s in stats), sum(s["n_restrict_kernels"] for s in stats)),
              "helmholtz": (sum(s["t_helm_kernel_ms"] for s in stats), sum(s["n_helm_kernels"] for s in stats)),
              "cycle": (sum(s["t_cycle_kernel_ms"] for s in stats), sum(s["n_cycle_kernels"] for s in stats)),
-             "guess": (sum(s["t_guess_kernel_ms"] for s in stats), sum(s["n_guess_kernels"] for s in stats))}
+             "guess": (sum(s["t_guess_kernel_ms"] for s in stats), sum(s["n_guess_kernels"] for s in stats)),
+             "rhs": (sum(s["t_rhs_kernel_ms"] for s in stats), sum(s["n_rhs_kernels"] for s in stats))}
+    for k in ("dct", "tri", "idct"):
+        timed["fps_" + k] = (sum(s[f"t_fps_{k}_ms"] for s in stats), sum(s["n_fps_solves"] for s in stats))
+    # the direct Poisson solve ran (one solve per step, no V-cycles) -- or, untimed, no restriction pass
+    direct = (any(s["n_fps_solves"] for s in stats) or
+              (args.time_every == 0 and all(int(s["it_phi"]) == 1 for s in stats) and not channel))
     # finest-level sweeps: V(2,2) per cycle (the convergence check rides on each cycle's last pass)
     fine_sweeps = 4 * cycles
     # whole-step algorithmic bytes per cell: K1 64 + K3 24 + K5 40 + the phi
@@ -345,6 +366,11 @@ def main():
         fused = 0   # (NSGPU_FUSE4=0: no boundary pass was timed, none ran)
     step_bpc = (64 + 24 + 40 + extrap_bpc + 2 * 24 * hpasses / K + 96 * band_frac
                 + (52 * (cycles - fused) + 28 * fused) / K + 52 * cycles / K / 3.0)
+    if direct:
+        # the direct solve: 72 B/cell (fps_* above) per solve, plus its residual check (phi 8 + b 8)
+        # on the checked solves; no phi extrapolation (no initial guess)
+        checks = sum(int(s["n_checks"]) for s in stats)
+        step_bpc = 64 + 24 + 40 + 2 * 24 * hpasses / K + 96 * band_frac + 72 * cycles / K + 16 * checks / K
     if channel:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications
         # of (line extension 8 + FUSE_R 28 + FUSE_P 26, x 4/3 for the coarser levels) = 80 each,
@@ -380,6 +406,9 @@ def main():
             d = json.load(open(prof))
             if d.get("n") == n and not channel:
                 traffic = {k: v.get("kernel_bytes_per_launch") for k, v in d.get("kernels", {}).items()}
+                tri = [traffic.get(k) for k in ("fps_t1", "fps_t2", "fps_t3")]
+                if all(x is not None for x in tri):
+                    traffic["fps_tri"] = sum(tri)
                 src = dict(d.get("source") or {})
                 src["file"] = "profiles/pmc_traffic.json"
                 src["same_library_as_this_run"] = (src.get("libnsgpu_sha16") is not None and
@@ -404,7 +433,8 @@ def main():
             kern[key] = roof(key, label, bpc, ms / cnt / 1e3, cnt)
             # (launches are timed on every --time-every'th step: scale to all K steps)
             kern[key]["ms_per_step"] = ms / max(1, timed_steps)
-    dominant = max(kern, key=lambda k: kern[k]["ms_per_step"]) if kern else None
+    single = [k for k in kern if k in SINGLE_LAUNCH]
+    dominant = max(single, key=lambda k: kern[k]["ms_per_step"]) if single else None
     line = {
         "metric": "cell-updates/sec (MLUPS) + Poisson iters/sec, 4096^2 grid at 1/2/4/8 GPUs",
         "value": value,
@@ -421,8 +451,11 @@ def main():
         "config": {"workload": (f"{n}x{nyc} channel (inlet W, NEUMANN outflow E), Re={re:g}, dt=h/8, fp64, "
                                 f"BiCGStab Poisson with the line-closure V-cycle preconditioner + RB-SOR Helmholtz, "
                                 f"both to rtol {args.rtol:g}") if channel else
-                               (f"{n}x{n} lid-driven cavity, Re={re:g}, dt=1/{8 * n}, fp64, multigrid Poisson "
-                                f"(RB-GS smoother) + RB-SOR Helmholtz, both to rtol {args.rtol:g}"),
+                               (f"{n}x{n} lid-driven cavity, Re={re:g}, dt=1/{8 * n}, fp64, "
+                                + ("direct Poisson solve (DCT along y + tridiagonal recurrences along x; residual "
+                                   "checked on every 16th solve)" if direct else
+                                   "multigrid Poisson (RB-GS smoother)")
+                                + f" + RB-SOR Helmholtz, both to rtol {args.rtol:g}"),
                    "case": args.case, "nx": n, "ny": nyc, "re": re, "dt": dt, "parallelism": f"x-slab x{world}",
                    "step_api": "ns_step" if args.sync_monitor else "ns_step_async",
                    "transport": ("none (one rank)" if world == 1 else
@@ -431,8 +464,10 @@ def main():
                                  "-- functional evidence, not a scaling number"),
                    "local_rows_rank0": solver.i1 - solver.i0},
         "monitor_last_step": {k: last_monitor[k] for k in ("umin", "umax", "vmin", "vmax")},
-        ("poisson_bicgstab_its_per_s" if channel else "poisson_vcycles_per_s"): cycles / elapsed,
-        ("poisson_bicgstab_its_per_step" if channel else "poisson_vcycles_per_step"): cycles / K,
+        ("poisson_bicgstab_its_per_s" if channel else "poisson_direct_solves_per_s" if direct else
+         "poisson_vcycles_per_s"): cycles / elapsed,
+        ("poisson_bicgstab_its_per_step" if channel else "poisson_direct_solves_per_step" if direct else
+         "poisson_vcycles_per_step"): cycles / K,
         "poisson_fine_sweeps_per_s": fine_sweeps / elapsed,
         "poisson_fine_sweeps_per_step": fine_sweeps / K,
         "helmholtz_sweeps_per_step": hsweeps / K,
@@ -451,10 +486,11 @@ def main():
     if jacobi32 is not None:
         line["kernels"]["jacobi_sweep_fp32"] = roof("jacobi_sweep_fp32", JACOBI32_LABEL, SWEEP32_BYTES_PER_CELL,
                                                     jacobi32, 50)
-    if channel:
-        line["data"] = "synthetic (channel from rest, uniform inlet, no input files)"
+    if channel or direct:
         for k in ("poisson_fine_sweeps_per_s", "poisson_fine_sweeps_per_step"):
             line.pop(k)
+    if channel:
+        line["data"] = "synthetic (channel from rest, uniform inlet, no input files)"
     if world == 1 and not args.no_cpu and not channel:
         try:
             state = {k: solver.get(a).ravel() for k, a in (("u", nsa.NS_ARR_U), ("v", nsa.NS_ARR_V),

@@ -33,14 +33,17 @@
 extern "C" {
 #endif
 
-#define NSGPU_ABI_VERSION 6   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
+#define NSGPU_ABI_VERSION 7   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
                                  3: ns_get/set_fields in compact-id order on polygons, ns_local_cells;
                                  4: NS_POISSON_MG is 0, so a zero-initialised ns_params selects the
                                     multigrid (RB-SOR moved to 3; the value 2 is rejected);
                                  5: ns_stats.x_link_bytes appended;
                                  6: ns_stats.t_cycle_kernel_ms / n_cycle_kernels and
                                     t_guess_kernel_ms / n_guess_kernels appended (the finest
-                                    level's V-cycle-boundary and guess-forming passes) */
+                                    level's V-cycle-boundary and guess-forming passes);
+                                 7: ns_stats.t_rhs_kernel_ms / n_rhs_kernels (K1) and the direct
+                                    Poisson solve's kernel times t_fps_dct_ms / t_fps_tri_ms /
+                                    t_fps_idct_ms / n_fps_solves appended */
 
 typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm */
 
@@ -62,7 +65,12 @@ typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm
                                     preconditions a BiCGStab solve of the true Poisson matrix */
 
 /* Poisson solvers */
-#define NS_POISSON_MG     0  /* geometric multigrid V-cycles, RB Gauss-Seidel smoother (the default: 0) */
+#define NS_POISSON_MG     0  /* the default (0): on a rectangle without outflow sides, uniform spacings and
+                                ny = 2^p (16 .. 8192) the direct solve -- DCT along y, tridiagonal
+                                recurrences along x, inverse DCT: one "iteration", residual ~1e-13,
+                                checked periodically and refined by V-cycles if above rtol; elsewhere
+                                (NSGPU_FPS=0 everywhere) geometric multigrid V-cycles, RB Gauss-Seidel
+                                smoother */
 #define NS_POISSON_JACOBI 1  /* weighted Jacobi sweeps (ping-pong) to rtol: O(n^2) sweeps per solve */
 #define NS_POISSON_RBSOR  3  /* fused red-black SOR sweeps to rtol: O(n) sweeps per solve */
 
@@ -153,6 +161,14 @@ typedef struct ns_stats {
                                       * finest restriction passes that form the phi extrapolation on the
                                       * fly (k_sweep2_gin; timing == 1) */
     int32_t n_guess_kernels;         /* number of those passes timed */
+    double  t_rhs_kernel_ms;         /* sum of K1's durations (ConstructRHS_V, k_rhs_s; timing == 1; multi-rank:
+                                      * the split launch between marker events) */
+    int32_t n_rhs_kernels;           /* number of K1 launches timed */
+    double  t_fps_dct_ms;            /* direct Poisson solve (timing == 1): the rows' DCT (k_fps_dct) */
+    double  t_fps_tri_ms;            /*   the tridiagonal recurrences along x (k_fps_t1, scan, t2, scan, t3;
+                                      *   one interval, allgathers included on slabs) */
+    double  t_fps_idct_ms;           /*   the inverse DCT (k_fps_idct) */
+    int32_t n_fps_solves;            /* number of direct solves timed */
 } ns_stats;
 
 /* device arrays addressable by ns_get_array / ns_set_array */

@@ -21,6 +21,7 @@
 // v_{N-1-n} = x_{2n+1}; X_k = Re(e^{-i pi k / 2N} V_k)), two real rows packed as the real and
 // imaginary parts of one complex sequence.  The FFT is a Stockham radix-16 transform in LDS
 // (N <= 8192 complex = 128 KiB), one workgroup of N/16 threads, one butterfly per thread and stage.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -568,16 +569,26 @@ void dct_pair(bool inverse, const double* in, const double* shift, double* out, 
             (void)hipFuncSetAttribute((const void*)k_fps_idct<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             attr = true;
         }
-        hipLaunchKernelGGL(k_fps_idct<LOGN>, grid, dim3(T), lds, st, in, out, nrows, ld, (const cplx*)tw,
-                           (const cplx*)wk);
+        hipEvent_t a, b;
+        if (take_launch_timing(a, b))
+            hipExtLaunchKernelGGL(k_fps_idct<LOGN>, grid, dim3(T), lds, st, a, b, 0, in, out, nrows, ld,
+                                  (const cplx*)tw, (const cplx*)wk);
+        else
+            hipLaunchKernelGGL(k_fps_idct<LOGN>, grid, dim3(T), lds, st, in, out, nrows, ld, (const cplx*)tw,
+                               (const cplx*)wk);
     } else {
         static bool attr = false;
         if (!attr) {
             (void)hipFuncSetAttribute((const void*)k_fps_dct<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             attr = true;
         }
-        hipLaunchKernelGGL(k_fps_dct<LOGN>, grid, dim3(T), lds, st, in, shift, out, nrows, ld, (const cplx*)tw,
-                           (const cplx*)wk);
+        hipEvent_t a, b;
+        if (take_launch_timing(a, b))
+            hipExtLaunchKernelGGL(k_fps_dct<LOGN>, grid, dim3(T), lds, st, a, b, 0, in, shift, out, nrows, ld,
+                                  (const cplx*)tw, (const cplx*)wk);
+        else
+            hipLaunchKernelGGL(k_fps_dct<LOGN>, grid, dim3(T), lds, st, in, shift, out, nrows, ld, (const cplx*)tw,
+                               (const cplx*)wk);
     }
 }
 

@@ -125,6 +125,8 @@ void set_compute_cus(int n);
 // the request and says whether no launch took it
 void time_next_launch(hipEvent_t a, hipEvent_t b);
 bool time_next_launch_pending();
+// a launcher outside ns_kernels.hip takes the pending request (and stamps its launch with a, b)
+bool take_launch_timing(hipEvent_t& a, hipEvent_t& b);
 // strip subset of the following two-sweep pass launches (k_sweep2): 0 all, 1 the strips
 // whose read cone lies inside the slab, 2 the others (exchange / compute overlap)
 void set_strip_phase(int phase);

@@ -3927,6 +3927,13 @@ bool time_next_launch_pending() {
     g_tev[0] = g_tev[1] = nullptr;
     return p;
 }
+bool take_launch_timing(hipEvent_t& a, hipEvent_t& b) {
+    if (!g_tev[0]) return false;
+    a = g_tev[0];
+    b = g_tev[1];
+    g_tev[0] = g_tev[1] = nullptr;
+    return true;
+}
 #define NS_LAUNCH(kern, grid, block, shmem, st, ...)                                                     \
     do {                                                                                              \
         if (::nsg::g_tev[0]) {                                                                        \

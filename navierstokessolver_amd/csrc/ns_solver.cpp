@@ -284,6 +284,8 @@ struct ns_solver {
     double *fps_ragg = nullptr, *fps_gath = nullptr, *fps_rin = nullptr;
     double fps_res = -1.0;       // the last checked solve's relative residual
     bool fps_strict = false;     // a check failed (rtol below the solve's round-off): check every solve
+    // timed steps: K1 (kev[0..1]) and the direct solve's transforms / recurrences (kev[2..7])
+    hipEvent_t kev[8] = {};
 };
 
 namespace {
@@ -487,6 +489,15 @@ int t_end(ns_solver* s, hipEvent_t a, hipEvent_t b) {
     }
     HIPCHK(hipEventRecord(b, s->st));
     return 0;
+}
+int ensure_kev(ns_solver* s) {
+    for (auto& e : s->kev)
+        if (!e) HIPCHK(hipEventCreate(&e));
+    return 0;
+}
+float kev_ms(ns_solver* s, int k) {
+    float ms = 0.f;
+    return hipEventElapsedTime(&ms, s->kev[k], s->kev[k + 1]) == hipSuccess ? ms : 0.f;
 }
 int ensure_events(ns_solver* s, size_t n) {
     while (s->ev.size() < n) {
@@ -1657,23 +1668,42 @@ int fps_scan(ns_solver* s, bool backward) {
 int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     const nsg::Geo& g = s->g;
     double* F = s->arr[NS_ARR_TMP];
+    // timed steps: the transforms by their dispatch stamps (one rank), the recurrences (five launches,
+    // the allgathers on slabs) between marker events
     const bool t = s->timing && s->in_step;
     if (t) {
-        CHK(ensure_events(s, 2));
-        HIPCHK(hipEventRecord(s->ev[0], s->st));
+        CHK(ensure_kev(s));
+        CHK(t_begin(s, s->kev[2], s->kev[3]));
     }
     if (nsg::launch_fps_dct(false, s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, F, g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk,
                             s->st) < 0) {
         set_err("direct Poisson solve: ny = %d is not a supported power of two", g.ny);
         return NS_EINVAL;
     }
+    if (t) {
+        CHK(t_end(s, s->kev[2], s->kev[3]));
+        HIPCHK(hipEventRecord(s->kev[4], s->st));
+    }
     nsg::launch_fps_t1(s->fa, F, s->st);
     CHK(fps_scan(s, false));
     nsg::launch_fps_t2(s->fa, F, s->st);
     CHK(fps_scan(s, true));
     nsg::launch_fps_t3(s->fa, F, s->st);
+    if (t) {
+        HIPCHK(hipEventRecord(s->kev[5], s->st));
+        CHK(t_begin(s, s->kev[6], s->kev[7]));
+    }
     nsg::launch_fps_dct(true, F, nullptr, s->arr[NS_ARR_PHI], g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st);
-    if (t) HIPCHK(hipEventRecord(s->ev[1], s->st));
+    if (t) CHK(t_end(s, s->kev[6], s->kev[7]));
+    auto take_times = [&]() -> int {
+        if (!t || !stt) return 0;
+        HIPCHK(hipEventSynchronize(s->kev[7]));
+        stt->t_fps_dct_ms += kev_ms(s, 2);
+        stt->t_fps_tri_ms += kev_ms(s, 4);
+        stt->t_fps_idct_ms += kev_ms(s, 6);
+        stt->n_fps_solves++;
+        return 0;
+    };
     *its = 1;
     s->last_cycles = s->cur_cycles = -1;
     // (a standalone solve -- ns_kernel -- is always checked; inside steps every fps_check-th)
@@ -1681,13 +1711,7 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     if (s->in_step) s->fps_solves++;
     if (!check) {
         *res = s->fps_res;
-        if (t) {
-            HIPCHK(hipEventSynchronize(s->ev[1]));
-            float ms = 0.f;
-            HIPCHK(hipEventElapsedTime(&ms, s->ev[0], s->ev[1]));
-            if (stt) { stt->t_poisson_kernel_ms += ms; stt->n_poisson_kernels++; }
-        }
-        return 0;
+        return take_times();
     }
     CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));   // (slabs: the residual's neighbour rows)
     const int nb = nsg::launch_pois_residual(g, s->c, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,
@@ -1704,11 +1728,7 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         CHK(fetch(s));
     }
     if (stt) stt->n_checks++;
-    if (t) {
-        float ms = 0.f;
-        HIPCHK(hipEventElapsedTime(&ms, s->ev[0], s->ev[1]));
-        if (stt) { stt->t_poisson_kernel_ms += ms; stt->n_poisson_kernels++; }
-    }
+    CHK(take_times());
     const double r2 = s->hs[S_RES], b2 = s->hs[S_SHIFT + 1];
     *res = s->fps_res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
     if (s->verbose) fprintf(stderr, "nsgpu poisson: direct solve, rel. residual %.3e\n", *res);
@@ -2290,12 +2310,18 @@ int helm_bnorm(ns_solver* s) {
 // exchange group, overlapped with the interior tiles
 int rhs(ns_solver* s) {
     const HaloReq r[3] = {{&s->g, s->arr[NS_ARR_U], 2}, {&s->g, s->arr[NS_ARR_V], 2}, {&s->g, s->arr[NS_ARR_PHI], 1}};
+    const bool t = s->timing && s->in_step;
+    if (t) {
+        CHK(ensure_kev(s));
+        CHK(t_begin(s, s->kev[0], s->kev[1]));
+    }
     const int nb = overlapped(s, r, 3, [&]() {
         return nsg::launch_rhs(s->g, s->c, s->dt, s->re, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_PHI],
                                s->arr[NS_ARR_CU], s->arr[NS_ARR_CV], s->arr[NS_ARR_RU], s->arr[NS_ARR_RV], s->part,
                                s->st);
     });
     if (nb < 0) return nb;
+    if (t) CHK(t_end(s, s->kev[0], s->kev[1]));
     nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_HBN, s->st);
     CHK(allreduce(s, s->scal + S_HBN, 2, ncclSum));
     return 0;
@@ -2855,6 +2881,8 @@ void ns_destroy(ns_solver* s) {
     if (s->cvimg) (void)hipFree(s->cvimg);
     if (s->dmat) (void)hipFree(s->dmat);
     if (s->fps_mem) (void)hipFree(s->fps_mem);
+    for (auto e : s->kev)
+        if (e) (void)hipEventDestroy(e);
     if (s->f32_mem) (void)hipFree(s->f32_mem);
     if (s->fc_mem) (void)hipFree(s->fc_mem);
     if (s->et_mem) (void)hipFree(s->et_mem);
@@ -2914,6 +2942,10 @@ static int step_body_(ns_solver* s, ns_stats& st) {
         st.n_helm_kernels += (size_t)k < s->hcomp.size() ? s->hcomp[k] : 1;   // (per component: 24 B/cell)
     }
     s->hn = 0;
+    if (s->timing && s->kev[0]) {   // (K1 ended before the Helmholtz checks' host syncs)
+        st.t_rhs_kernel_ms += kev_ms(s, 0);
+        st.n_rhs_kernels++;
+    }
     if (!s->k3_spec) CHK(divergence(s));                           // ConstructRHS_phi + mean (:549-550)
     s->k3_spec = 0;
     CHK(consistent_rhs(s));                                        // stretched grids only
