@@ -307,9 +307,9 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
 // and row).  rp0[c][k] = 1 / p of the row before chunk c.
 
 // one row of the pivot recurrence: g = pw_i / p_{i-1} (from rprev = 1 / p_{i-1}); returns 1 / p_i
-// (mode 0's pinned last global row: 0)
-__device__ inline double piv_next(const FpsArgs& a, int gi, int k, double mu, double rprev, double& g) {
-    const double pw = a.pw[gi], pe = a.pe[gi], pem = gi > 0 ? a.pe[gi - 1] : 0.0;
+// (mode 0's pinned last global row: 0).  pw, pe, pem: the row's coefficients pw_i, pe_i, pe_{i-1}
+__device__ inline double piv_next(const FpsArgs& a, int gi, int k, double mu, double rprev, double pw, double pe,
+                                  double pem, double& g) {
     g = pw * rprev;
     const double p = -(pw + pe) + mu - g * pem;
     return (a.pin && k == 0 && gi == a.nx - 1) ? 0.0 : 1.0 / p;
@@ -318,11 +318,28 @@ __device__ inline double piv_next(const FpsArgs& a, int gi, int k, double mu, do
 __device__ inline double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
 __device__ inline void st2(double* p, double x, double y) { *reinterpret_cast<double2*>(p) = double2{x, y}; }
 
+// a chunk's rows: every load issued before the recurrence consumes the first (the recurrence is a
+// dependent chain of divisions; one row in flight at a time left the passes at 3 TB/s)
+struct ChunkRows {
+    double pw[FPS_M], pe[FPS_M], pem[FPS_M];
+    __device__ inline void load(const FpsArgs& a, int li0, int rows) {
+#pragma unroll
+        for (int t = 0; t < FPS_M; t++) {
+            if (t < rows) {
+                const int gi = a.i0 + li0 + t;
+                pw[t] = a.pw[gi];
+                pe[t] = a.pe[gi];
+                pem[t] = gi > 0 ? a.pe[gi - 1] : 0.0;
+            }
+        }
+    }
+};
+
 // T1: per chunk the forward recurrence from zero -> (E, Pi) into ca; the workgroup folds its chunks
 // into the group's aggregate ga (y_out = E + Pi y_in)
 __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1(FpsArgs a, const double* __restrict__ f) {
     __shared__ double2 sE[FPS_G][64], sP[FPS_G][64];
-    const int lane = threadIdx.x, w = threadIdx.y;
+    const int lane = threadIdx.x, w = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int k0 = 2 * (blockIdx.x * 64 + lane);
     const int grp = blockIdx.y, c = grp * FPS_G + w;
     const int li0 = c * FPS_M;
@@ -331,17 +348,22 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1(FpsArgs a, const double* 
     if (rows > 0) {
         const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
         const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
+        ChunkRows cr;
+        cr.load(a, li0, rows);
+        double2 fv[FPS_M];
+#pragma unroll
+        for (int t = 0; t < FPS_M; t++)
+            if (t < rows) fv[t] = ld2(f + (size_t)(li0 + t) * a.ld + k0);
         double r[2] = {r0.x, r0.y};
 #pragma unroll
         for (int t = 0; t < FPS_M; t++) {
             if (t < rows) {
                 const int gi = a.i0 + li0 + t;
-                const double2 fv = ld2(f + (size_t)(li0 + t) * a.ld + k0);
-                const double fm[2] = {fv.x, fv.y};
+                const double fm[2] = {fv[t].x, fv[t].y};
 #pragma unroll
                 for (int m = 0; m < 2; m++) {
                     double g;
-                    r[m] = piv_next(a, gi, k0 + m, mu[m], r[m], g);
+                    r[m] = piv_next(a, gi, k0 + m, mu[m], r[m], cr.pw[t], cr.pe[t], cr.pem[t], g);
                     E[m] = fma(-g, E[m], fm[m]);
                     P[m] = -g * P[m];
                 }
@@ -408,13 +430,19 @@ __global__ void k_fps_scan(int ngrp, int ld, int ny, const double* __restrict__ 
 // chunk's backward aggregate (x_s = BX + BR x_e) into cb; the workgroup folds its chunks into gb
 __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2(FpsArgs a, double* __restrict__ f) {
     __shared__ double2 sX[FPS_G][64], sR[FPS_G][64];
-    const int lane = threadIdx.x, w = threadIdx.y;
+    const int lane = threadIdx.x, w = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int k0 = 2 * (blockIdx.x * 64 + lane);
     const int grp = blockIdx.y, c = grp * FPS_G + w;
     const int li0 = c * FPS_M;
     const int rows = k0 < a.ny ? min(FPS_M, a.nxl - li0) : 0;
     double BX[2] = {0.0, 0.0}, BR[2] = {1.0, 1.0};
     if (rows > 0) {
+        ChunkRows cr;
+        cr.load(a, li0, rows);
+        double2 yv[FPS_M];   // f, then the exact forward values in place
+#pragma unroll
+        for (int t = 0; t < FPS_M; t++)
+            if (t < rows) yv[t] = ld2(f + (size_t)(li0 + t) * a.ld + k0);
         const double2 y0 = ld2(a.gc + (size_t)grp * a.ld + k0);
         double y[2] = {y0.x, y0.y};
         for (int q = grp * FPS_G; q < c; q++) {
@@ -425,35 +453,29 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2(FpsArgs a, double* __rest
         const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
         const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
         double r[2] = {r0.x, r0.y};
-        double yv[FPS_M][2], rv[FPS_M][2];
+        double2 rv[FPS_M];
 #pragma unroll
         for (int t = 0; t < FPS_M; t++) {
             if (t < rows) {
                 const int gi = a.i0 + li0 + t;
-                const double2 fv = ld2(f + (size_t)(li0 + t) * a.ld + k0);
-                const double fm[2] = {fv.x, fv.y};
-#pragma unroll
-                for (int m = 0; m < 2; m++) {
-                    double g;
-                    r[m] = piv_next(a, gi, k0 + m, mu[m], r[m], g);
-                    y[m] = fma(-g, y[m], fm[m]);
-                    yv[t][m] = y[m];
-                    rv[t][m] = r[m];
-                }
+                double g0, g1;
+                r[0] = piv_next(a, gi, k0, mu[0], r[0], cr.pw[t], cr.pe[t], cr.pem[t], g0);
+                r[1] = piv_next(a, gi, k0 + 1, mu[1], r[1], cr.pw[t], cr.pe[t], cr.pem[t], g1);
+                y[0] = fma(-g0, y[0], yv[t].x);
+                y[1] = fma(-g1, y[1], yv[t].y);
+                yv[t] = double2{y[0], y[1]};
+                rv[t] = double2{r[0], r[1]};
             }
         }
         double xl[2] = {0.0, 0.0};
 #pragma unroll
         for (int t = FPS_M - 1; t >= 0; t--) {
             if (t < rows) {
-                const int gi = a.i0 + li0 + t;
-                const double pe = a.pe[gi];
-#pragma unroll
-                for (int m = 0; m < 2; m++) {
-                    const double q = -pe * rv[t][m];
-                    xl[m] = fma(yv[t][m], rv[t][m], q * xl[m]);
-                    BR[m] = q * BR[m];
-                }
+                const double q0 = -cr.pe[t] * rv[t].x, q1 = -cr.pe[t] * rv[t].y;
+                xl[0] = fma(yv[t].x, rv[t].x, q0 * xl[0]);
+                xl[1] = fma(yv[t].y, rv[t].y, q1 * xl[1]);
+                BR[0] = q0 * BR[0];
+                BR[1] = q1 * BR[1];
                 st2(f + (size_t)(li0 + t) * a.ld + k0, xl[0], xl[1]);
             }
         }
@@ -483,7 +505,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2(FpsArgs a, double* __rest
 // x_i = xl_i + rho_i x_e (in place)
 __global__ void __launch_bounds__(64 * FPS_G) k_fps_t3(FpsArgs a, double* __restrict__ f) {
     __shared__ double2 sX[FPS_G][64], sR[FPS_G][64];
-    const int lane = threadIdx.x, w = threadIdx.y;
+    const int lane = threadIdx.x, w = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int k0 = 2 * (blockIdx.x * 64 + lane);
     const int grp = blockIdx.y, c = grp * FPS_G + w;
     const int li0 = c * FPS_M;
@@ -497,6 +519,12 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t3(FpsArgs a, double* __rest
     sR[w][lane] = br;
     __syncthreads();
     if (rows <= 0) return;
+    ChunkRows cr;
+    cr.load(a, li0, rows);
+    double2 xv[FPS_M];
+#pragma unroll
+    for (int t = 0; t < FPS_M; t++)
+        if (t < rows) xv[t] = ld2(f + (size_t)(li0 + t) * a.ld + k0);
     const double2 x0 = ld2(a.gx + (size_t)grp * a.ld + k0);
     double X[2] = {x0.x, x0.y};
     for (int q = FPS_G - 1; q > w; q--) {
@@ -507,30 +535,24 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t3(FpsArgs a, double* __rest
     const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
     const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
     double r[2] = {r0.x, r0.y};
-    double rv[FPS_M][2];
+    double2 rv[FPS_M];
 #pragma unroll
     for (int t = 0; t < FPS_M; t++) {
         if (t < rows) {
             const int gi = a.i0 + li0 + t;
-#pragma unroll
-            for (int m = 0; m < 2; m++) {
-                double g;
-                r[m] = piv_next(a, gi, k0 + m, mu[m], r[m], g);
-                rv[t][m] = r[m];
-            }
+            double g;
+            r[0] = piv_next(a, gi, k0, mu[0], r[0], cr.pw[t], cr.pe[t], cr.pem[t], g);
+            r[1] = piv_next(a, gi, k0 + 1, mu[1], r[1], cr.pw[t], cr.pe[t], cr.pem[t], g);
+            rv[t] = double2{r[0], r[1]};
         }
     }
     double rho[2] = {1.0, 1.0};
 #pragma unroll
     for (int t = FPS_M - 1; t >= 0; t--) {
         if (t < rows) {
-            const int gi = a.i0 + li0 + t;
-            const double pe = a.pe[gi];
-            double* p = f + (size_t)(li0 + t) * a.ld + k0;
-            const double2 xl = ld2(p);
-            rho[0] = -pe * rv[t][0] * rho[0];
-            rho[1] = -pe * rv[t][1] * rho[1];
-            st2(p, fma(rho[0], X[0], xl.x), fma(rho[1], X[1], xl.y));
+            rho[0] = -cr.pe[t] * rv[t].x * rho[0];
+            rho[1] = -cr.pe[t] * rv[t].y * rho[1];
+            st2(f + (size_t)(li0 + t) * a.ld + k0, fma(rho[0], X[0], xv[t].x), fma(rho[1], X[1], xv[t].y));
         }
     }
 }
