@@ -233,7 +233,12 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
     const int tid = threadIdx.x;
     const int npairs = (nrows + 1) / 2;
     const double rn = 1.0 / N;
-    double ra[PT], rb[PT];
+    // (each thread loads its coefficients X_k and their mirrors X_{N-k} itself -- the mirrors are
+    // the same cache lines, read in reverse -- so conj(V) goes to LDS in one pass.  N = 8192: the
+    // mirrors' registers would spill; they come through LDS, one pass more)
+    constexpr bool MIRROR = LOGN <= 12;
+    constexpr int PM = MIRROR ? PT : 1;
+    double ra[PT], rb[PT], na[PM], nb[PM];
     auto load = [&](int p) {
         const int r0 = 2 * p;
         const bool two = r0 + 1 < nrows;
@@ -244,6 +249,10 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
             if (k < N) {
                 ra[q] = a[k];
                 rb[q] = two ? a[ld + k] : 0.0;
+                if constexpr (MIRROR) {
+                    na[q] = k ? a[N - k] : 0.0;
+                    nb[q] = two && k ? a[ld + N - k] : 0.0;
+                }
             }
         }
     };
@@ -254,32 +263,43 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
         const int r0 = 2 * p;
         const bool two = r0 + 1 < nrows;
         if (!PREF) load(p);
+        // Va = e^{i theta} (A_k - i A_{N-k}), Vb likewise; V = Va + i Vb; z <- conj(V)
+        auto conjv = [&](int k, double xa, double xb, double ya, double yb) {
+            const cplx w = wk[k];   // e^{-i theta}: e^{i theta} = (w.x, -w.y)
+            const double c = w.x, s = -w.y;
+            const cplx Va{fma(c, xa, s * ya), fma(s, xa, -c * ya)};
+            const cplx Vb{fma(c, xb, s * yb), fma(s, xb, -c * yb)};
+            return cplx{Va.x - Vb.y, -(Va.y + Vb.x)};
+        };
+        if constexpr (MIRROR) {
 #pragma unroll
-        for (int q = 0; q < PT; q++) {
-            const int k = tid + q * T;
-            if (k < N) z[pz(k)] = cplx{ra[q], rb[q]};
-        }
-        __syncthreads();
-        cplx v[PT];
-#pragma unroll
-        for (int q = 0; q < PT; q++) {
-            const int k = tid + q * T;
-            if (k < N) {
-                const cplx Xk = z[pz(k)];
-                const cplx Xn = k ? z[pz(N - k)] : cplx{0.0, 0.0};
-                const cplx w = wk[k];   // e^{-i theta}: e^{i theta} = (w.x, -w.y)
-                const double c = w.x, s = -w.y;
-                // Va = e^{i theta} (A_k - i A_{N-k}), Vb likewise; V = Va + i Vb; store conj(V)
-                const cplx Va{fma(c, Xk.x, s * Xn.x), fma(s, Xk.x, -c * Xn.x)};
-                const cplx Vb{fma(c, Xk.y, s * Xn.y), fma(s, Xk.y, -c * Xn.y)};
-                v[q] = cplx{Va.x - Vb.y, -(Va.y + Vb.x)};
+            for (int q = 0; q < PT; q++) {
+                const int k = tid + q * T;
+                if (k < N) z[pz(k)] = conjv(k, ra[q], rb[q], na[q], nb[q]);
             }
-        }
-        __syncthreads();
+        } else {
 #pragma unroll
-        for (int q = 0; q < PT; q++) {
-            const int k = tid + q * T;
-            if (k < N) z[pz(k)] = v[q];
+            for (int q = 0; q < PT; q++) {
+                const int k = tid + q * T;
+                if (k < N) z[pz(k)] = cplx{ra[q], rb[q]};
+            }
+            __syncthreads();
+            cplx v[PT];
+#pragma unroll
+            for (int q = 0; q < PT; q++) {
+                const int k = tid + q * T;
+                if (k < N) {
+                    const cplx Xk = z[pz(k)];
+                    const cplx Xn = k ? z[pz(N - k)] : cplx{0.0, 0.0};
+                    v[q] = conjv(k, Xk.x, Xk.y, Xn.x, Xn.y);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < PT; q++) {
+                const int k = tid + q * T;
+                if (k < N) z[pz(k)] = v[q];
+            }
         }
         __syncthreads();
         fft_lds<LOGN>(z, tw, tid);
