@@ -15,7 +15,7 @@ def g(r, k):
         if key in r: return r[key]
     return "?"
 for r in rows:
-    name = r["Kernel_Name"].split("(")[0].replace("void ", "")[:40]
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")[:40]
     grid = g(r, "Grid_Size_X") if "Grid_Size_X" in r else g(r, "Grid_Size")
     gy = r.get("Grid_Size_Y", "")
     dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
