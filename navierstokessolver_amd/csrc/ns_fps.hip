@@ -577,6 +577,170 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t3(FpsArgs a, double* __rest
     }
 }
 
+// ---- the same recurrences in two full passes (r4, default; NSGPU_FPS_PASSES=3: t1 / t2 / t3 above) ----
+// A chunk's back substitution from zero over its exact forward values y' = y_loc + pi Y_in is linear in
+// the carry-in: its start value is BXl + beta Y_in, where BXl runs the back substitution over y_loc
+// and beta = the same recurrence over pi -- with BR (the product of the back multipliers) a property
+// of the operator alone, tabulated by the host (bt).  So T1b forms (E, Pi) and BXl from f, the
+// forward scan gives the carries, k_fps_mid forms every chunk's carry-in and final (BX, BR) and the
+// groups' backward aggregates, the backward scan gives their carries, and T2b writes the exact values:
+// f is read twice and written once (24 B/cell) instead of read three times and written twice (40).
+
+// T1b: t1 + the chunk's back substitution from zero over its local forward values -> BXl into cb
+__global__ void __launch_bounds__(64 * FPS_G) k_fps_t1b(FpsArgs a, const double* __restrict__ f) {
+    __shared__ double2 sE[FPS_G][64], sP[FPS_G][64];
+    const int lane = threadIdx.x, w = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int k0 = 2 * (blockIdx.x * 64 + lane);
+    const int grp = blockIdx.y, c = grp * FPS_G + w;
+    const int li0 = c * FPS_M;
+    const int rows = k0 < a.ny ? min(FPS_M, a.nxl - li0) : 0;
+    double E[2] = {0.0, 0.0}, P[2] = {1.0, 1.0};
+    if (rows > 0) {
+        const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
+        const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
+        ChunkRows cr;
+        cr.load(a, li0, rows);
+        double2 yv[FPS_M], rv[FPS_M];
+#pragma unroll
+        for (int t = 0; t < FPS_M; t++)
+            if (t < rows) yv[t] = ld2(f + (size_t)(li0 + t) * a.ld + k0);
+        double r[2] = {r0.x, r0.y};
+#pragma unroll
+        for (int t = 0; t < FPS_M; t++) {
+            if (t < rows) {
+                const int gi = a.i0 + li0 + t;
+                double g0, g1;
+                r[0] = piv_next(a, gi, k0, mu[0], r[0], cr.pw[t], cr.pe[t], cr.pem[t], g0);
+                r[1] = piv_next(a, gi, k0 + 1, mu[1], r[1], cr.pw[t], cr.pe[t], cr.pem[t], g1);
+                E[0] = fma(-g0, E[0], yv[t].x);
+                E[1] = fma(-g1, E[1], yv[t].y);
+                P[0] = -g0 * P[0];
+                P[1] = -g1 * P[1];
+                yv[t] = double2{E[0], E[1]};
+                rv[t] = double2{r[0], r[1]};
+            }
+        }
+        double xl[2] = {0.0, 0.0};
+#pragma unroll
+        for (int t = FPS_M - 1; t >= 0; t--) {
+            if (t < rows) {
+                xl[0] = fma(yv[t].x, rv[t].x, -cr.pe[t] * rv[t].x * xl[0]);
+                xl[1] = fma(yv[t].y, rv[t].y, -cr.pe[t] * rv[t].y * xl[1]);
+            }
+        }
+        st2(a.ca + (size_t)c * a.ld + k0, E[0], E[1]);
+        st2(a.ca + (size_t)(a.nch + c) * a.ld + k0, P[0], P[1]);
+        st2(a.cb + (size_t)c * a.ld + k0, xl[0], xl[1]);
+    }
+    sE[w][lane] = double2{E[0], E[1]};
+    sP[w][lane] = double2{P[0], P[1]};
+    __syncthreads();
+    if (w == 0 && k0 < a.ny) {
+        double GE[2] = {0.0, 0.0}, GP[2] = {1.0, 1.0};
+        for (int q = 0; q < FPS_G; q++) {
+            const double2 e = sE[q][lane], pp = sP[q][lane];
+            GE[0] = fma(pp.x, GE[0], e.x);
+            GE[1] = fma(pp.y, GE[1], e.y);
+            GP[0] = pp.x * GP[0];
+            GP[1] = pp.y * GP[1];
+        }
+        st2(a.ga + (size_t)grp * a.ld + k0, GE[0], GE[1]);
+        st2(a.ga + (size_t)(a.ngrp + grp) * a.ld + k0, GP[0], GP[1]);
+    }
+}
+
+// every chunk's forward carry-in (ya) and final backward aggregate (cb <- BXl + beta Y_in; BR from bt),
+// and the group's backward aggregate gb; one thread per group and mode pair
+__global__ void __launch_bounds__(64) k_fps_mid(FpsArgs a) {
+    const int k0 = 2 * (blockIdx.x * 64 + threadIdx.x);
+    const int grp = blockIdx.y;
+    if (k0 >= a.ny) return;
+    const double2 y0 = ld2(a.gc + (size_t)grp * a.ld + k0);
+    double Y[2] = {y0.x, y0.y};
+    double BX[FPS_G][2], BR[FPS_G][2];
+#pragma unroll
+    for (int w = 0; w < FPS_G; w++) {
+        const int c = grp * FPS_G + w;
+        BX[w][0] = BX[w][1] = 0.0;
+        BR[w][0] = BR[w][1] = 1.0;
+        if (c < a.nch) {
+            const double2 e = ld2(a.ca + (size_t)c * a.ld + k0), pp = ld2(a.ca + (size_t)(a.nch + c) * a.ld + k0);
+            const double2 bl = ld2(a.cb + (size_t)c * a.ld + k0);
+            const double2 be = ld2(a.bt + (size_t)c * a.ld + k0), br = ld2(a.bt + (size_t)(a.nch + c) * a.ld + k0);
+            st2(a.ya + (size_t)c * a.ld + k0, Y[0], Y[1]);
+            BX[w][0] = fma(be.x, Y[0], bl.x);
+            BX[w][1] = fma(be.y, Y[1], bl.y);
+            BR[w][0] = br.x;
+            BR[w][1] = br.y;
+            st2(a.cb + (size_t)c * a.ld + k0, BX[w][0], BX[w][1]);
+            Y[0] = fma(pp.x, Y[0], e.x);
+            Y[1] = fma(pp.y, Y[1], e.y);
+        }
+    }
+    double GX[2] = {0.0, 0.0}, GR[2] = {1.0, 1.0};
+#pragma unroll
+    for (int w = FPS_G - 1; w >= 0; w--) {
+        GX[0] = fma(BR[w][0], GX[0], BX[w][0]);
+        GX[1] = fma(BR[w][1], GX[1], BX[w][1]);
+        GR[0] = BR[w][0] * GR[0];
+        GR[1] = BR[w][1] * GR[1];
+    }
+    st2(a.gb + (size_t)grp * a.ld + k0, GX[0], GX[1]);
+    st2(a.gb + (size_t)(a.ngrp + grp) * a.ld + k0, GR[0], GR[1]);
+}
+
+// T2b: the chunk's exact values -- the forward recurrence from its carry-in Y_in (ya), the back
+// substitution from its carry-in X_in (the group's, through the later chunks' (BX, BR)) -- in place
+__global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __restrict__ f) {
+    const int lane = threadIdx.x, w = __builtin_amdgcn_readfirstlane(threadIdx.y);
+    const int k0 = 2 * (blockIdx.x * 64 + lane);
+    const int grp = blockIdx.y, c = grp * FPS_G + w;
+    const int li0 = c * FPS_M;
+    const int rows = k0 < a.ny ? min(FPS_M, a.nxl - li0) : 0;
+    if (rows <= 0) return;
+    ChunkRows cr;
+    cr.load(a, li0, rows);
+    double2 yv[FPS_M];
+#pragma unroll
+    for (int t = 0; t < FPS_M; t++)
+        if (t < rows) yv[t] = ld2(f + (size_t)(li0 + t) * a.ld + k0);
+    const double2 yin = ld2(a.ya + (size_t)c * a.ld + k0);
+    const double2 x0 = ld2(a.gx + (size_t)grp * a.ld + k0);
+    double X[2] = {x0.x, x0.y};
+    for (int q = FPS_G - 1; q > w; q--) {
+        const int cq = grp * FPS_G + q;
+        if (cq >= a.nch) continue;
+        const double2 bx = ld2(a.cb + (size_t)cq * a.ld + k0), br = ld2(a.bt + (size_t)(a.nch + cq) * a.ld + k0);
+        X[0] = fma(br.x, X[0], bx.x);
+        X[1] = fma(br.y, X[1], bx.y);
+    }
+    const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
+    const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
+    double r[2] = {r0.x, r0.y}, y[2] = {yin.x, yin.y};
+    double2 rv[FPS_M];
+#pragma unroll
+    for (int t = 0; t < FPS_M; t++) {
+        if (t < rows) {
+            const int gi = a.i0 + li0 + t;
+            double g0, g1;
+            r[0] = piv_next(a, gi, k0, mu[0], r[0], cr.pw[t], cr.pe[t], cr.pem[t], g0);
+            r[1] = piv_next(a, gi, k0 + 1, mu[1], r[1], cr.pw[t], cr.pe[t], cr.pem[t], g1);
+            y[0] = fma(-g0, y[0], yv[t].x);
+            y[1] = fma(-g1, y[1], yv[t].y);
+            yv[t] = double2{y[0], y[1]};
+            rv[t] = double2{r[0], r[1]};
+        }
+    }
+#pragma unroll
+    for (int t = FPS_M - 1; t >= 0; t--) {
+        if (t < rows) {
+            X[0] = fma(yv[t].x, rv[t].x, -cr.pe[t] * rv[t].x * X[0]);
+            X[1] = fma(yv[t].y, rv[t].y, -cr.pe[t] * rv[t].y * X[1]);
+            st2(f + (size_t)(li0 + t) * a.ld + k0, X[0], X[1]);
+        }
+    }
+}
+
 // multi-rank: this rank's carry-in from every rank's aggregate (g: P slots of 2 x ld, slot q = rank
 // q's (E, Pi) or (X, R)): forward, the fold of ranks 0 .. r-1 in order; backward, of P-1 .. r+1
 __global__ void k_fps_rank_carry(const double* __restrict__ g, int P, int r, int ld, int ny, int backward,
@@ -665,6 +829,15 @@ void launch_fps_t1(const FpsArgs& a, const double* f, hipStream_t st) {
 }
 void launch_fps_t2(const FpsArgs& a, double* f, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_t2, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
+}
+void launch_fps_t1b(const FpsArgs& a, const double* f, hipStream_t st) {
+    hipLaunchKernelGGL(k_fps_t1b, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
+}
+void launch_fps_mid(const FpsArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_fps_mid, dim3((a.ny + 127) / 128, a.ngrp), dim3(64), 0, st, a);
+}
+void launch_fps_t2b(const FpsArgs& a, double* f, hipStream_t st) {
+    hipLaunchKernelGGL(k_fps_t2b, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
 }
 void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_t3, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);

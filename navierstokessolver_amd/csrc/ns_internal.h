@@ -285,6 +285,8 @@ struct FpsArgs {
     double *ga, *gc;               // forward: group aggregates (E, Pi: 2 x ngrp x ld), group carry-ins
     double *gb, *gx;               // backward: group aggregates (X, R), group carry-ins
     double* cb;                    // backward chunk aggregates (2 x nch x ld)
+    const double* bt;              // two-pass recurrences: per chunk beta (d BX / d Y_in) and BR (2 x nch x ld, host)
+    double* ya;                    // two-pass recurrences: every chunk's forward carry-in (nch x ld)
 };
 // log2(ny) if ny is a supported power of two, else -1
 int fps_log2(int ny);
@@ -295,6 +297,11 @@ int launch_fps_dct(bool inverse, const double* in, const double* shift, double* 
 void launch_fps_t1(const FpsArgs& a, const double* f, hipStream_t st);
 void launch_fps_t2(const FpsArgs& a, double* f, hipStream_t st);
 void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st);
+// the two-pass form (ns_fps.hip): t1b (t1 + the local back substitution), mid (carries and final
+// backward aggregates per chunk), t2b (the exact values)
+void launch_fps_t1b(const FpsArgs& a, const double* f, hipStream_t st);
+void launch_fps_mid(const FpsArgs& a, hipStream_t st);
+void launch_fps_t2b(const FpsArgs& a, double* f, hipStream_t st);
 // group scan (forward: ga -> gc ascending; backward: gb -> gx descending) from the carry-in rin (null:
 // 0; multi-rank: the fold of the other ranks' aggregates); rout (if not null) <- this rank's aggregate
 void launch_fps_scan(const FpsArgs& a, bool backward, const double* rin, double* rout, hipStream_t st);

@@ -278,6 +278,7 @@ struct ns_solver {
     double* fps_mem = nullptr;
     const double *fps_tw = nullptr, *fps_wk = nullptr;
     int fps_check = 16;
+    int fps_passes = 2;          // full passes of the tridiagonal recurrences (NSGPU_FPS_PASSES=3: t1 / t2 / t3)
     long fps_solves = 0;
     // multi-rank: this rank's aggregate of a recurrence (2 x ld), every rank's (nranks x 2 x ld, one
     // allgather per direction and solve) and the carry-in folded from them (ld)
@@ -1684,11 +1685,19 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         CHK(t_end(s, s->kev[2], s->kev[3]));
         HIPCHK(hipEventRecord(s->kev[4], s->st));
     }
-    nsg::launch_fps_t1(s->fa, F, s->st);
-    CHK(fps_scan(s, false));
-    nsg::launch_fps_t2(s->fa, F, s->st);
-    CHK(fps_scan(s, true));
-    nsg::launch_fps_t3(s->fa, F, s->st);
+    if (s->fps_passes == 3) {   // (A/B: round 4's first form)
+        nsg::launch_fps_t1(s->fa, F, s->st);
+        CHK(fps_scan(s, false));
+        nsg::launch_fps_t2(s->fa, F, s->st);
+        CHK(fps_scan(s, true));
+        nsg::launch_fps_t3(s->fa, F, s->st);
+    } else {
+        nsg::launch_fps_t1b(s->fa, F, s->st);
+        CHK(fps_scan(s, false));
+        nsg::launch_fps_mid(s->fa, s->st);
+        CHK(fps_scan(s, true));
+        nsg::launch_fps_t2b(s->fa, F, s->st);
+    }
     if (t) {
         HIPCHK(hipEventRecord(s->kev[5], s->st));
         CHK(t_begin(s, s->kev[6], s->kev[7]));
@@ -1783,8 +1792,9 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     const int nchp = a.ngrp * nsg::FPS_G;   // (t1 / t2 / t3 address whole groups' chunks)
     const size_t n_tab = 4 * (size_t)N + (size_t)N, n_rp0 = (size_t)nchp * ld, n_g = (size_t)a.ngrp * ld;
     const size_t n_mr = s->nranks > 1 ? (size_t)(2 + 2 * s->nranks + 1) * ld : 0;
-    const size_t total = n_tab + n_rp0 + 6 * n_g + 4 * (size_t)nchp * ld + n_mr;
-    std::vector<double> h(n_tab + n_rp0, 0.0);
+    const size_t n_bt = 2 * (size_t)nchp * ld;
+    const size_t total = n_tab + n_rp0 + n_bt + 6 * n_g + 5 * (size_t)nchp * ld + n_mr;
+    std::vector<double> h(n_tab + n_rp0 + n_bt, 0.0);
     const double pi = 3.14159265358979323846;
     for (int m = 0; m < N; m++) {
         const double t = 2.0 * pi * ((double)m / N);
@@ -1797,17 +1807,37 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
         h[4 * N + m] = -4.0 / (hy[0] * hy[0]) * sn * sn;   // -(2/hy^2)(1 - cos(pi m / N))
     }
     double* rp0 = h.data() + n_tab;
+    double* bt = rp0 + n_rp0;   // per chunk: beta (the local back substitution over pi) and BR
     std::vector<double> r(N, 0.0);   // 1 / p of the previous row, per mode
+    std::vector<double> crp((size_t)nsg::FPS_M * N), cpi((size_t)nsg::FPS_M * N);   // this chunk's 1/p, pi
     const int iend = g.i0 + g.nxl;
     for (int gi = 0; gi < iend; gi++) {
         const int li = gi - g.i0;
         if (li >= 0 && li % nsg::FPS_M == 0)
             for (int k = 0; k < N; k++) rp0[(size_t)(li / nsg::FPS_M) * ld + k] = r[k];
         const double pem = gi > 0 ? pe[gi - 1] : 0.0;
+        const int t = li >= 0 ? li % nsg::FPS_M : 0;
         for (int k = 0; k < N; k++) {
             const double gg = pw[gi] * r[k];
             const double p = -(pw[gi] + pe[gi]) + h[4 * N + k] - gg * pem;
             r[k] = (k == 0 && gi == g.nx - 1) ? 0.0 : 1.0 / p;
+            if (li >= 0) {
+                crp[(size_t)t * N + k] = r[k];
+                cpi[(size_t)t * N + k] = -gg * (t ? cpi[(size_t)(t - 1) * N + k] : 1.0);
+            }
+        }
+        if (li >= 0 && (t == nsg::FPS_M - 1 || gi == iend - 1)) {   // the chunk's (beta, BR)
+            const int c = li / nsg::FPS_M;
+            for (int k = 0; k < N; k++) {
+                double b = 0.0, R = 1.0;
+                for (int u = t; u >= 0; u--) {
+                    const double rr = crp[(size_t)u * N + k], q = -pe[gi - t + u] * rr;
+                    b = cpi[(size_t)u * N + k] * rr + q * b;
+                    R = q * R;
+                }
+                bt[(size_t)c * ld + k] = b;
+                bt[(size_t)(a.nch + c) * ld + k] = R;
+            }
         }
     }
     HIPCHK(hipMalloc(&s->fps_mem, total * sizeof(double)));
@@ -1818,13 +1848,15 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     s->fps_wk = d + 2 * (size_t)N;
     a.mu = d + 4 * (size_t)N;
     a.rp0 = d + n_tab;
-    double* q = d + n_tab + n_rp0;
+    a.bt = d + n_tab + n_rp0;
+    double* q = d + n_tab + n_rp0 + n_bt;
     a.ga = q; q += 2 * n_g;
     a.gc = q; q += n_g;
     a.gb = q; q += 2 * n_g;
     a.gx = q; q += n_g;
     a.cb = q; q += 2 * (size_t)nchp * ld;
     a.ca = q; q += 2 * (size_t)nchp * ld;
+    a.ya = q; q += (size_t)nchp * ld;
     if (n_mr) {
         s->fps_ragg = q; q += 2 * (size_t)ld;
         s->fps_gath = q; q += 2 * (size_t)s->nranks * ld;
@@ -2661,6 +2693,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         s->fps = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !masked && !outflow && yuni &&
                  nsg::fps_log2(gd->ny) >= 0;
         if (const char* e = getenv("NSGPU_FPS_CHECK")) s->fps_check = std::max(0, std::atoi(e));
+        if (const char* e = getenv("NSGPU_FPS_PASSES")) s->fps_passes = std::atoi(e) == 3 ? 3 : 2;
         if (s->fps) s->phi_extrap = 0;   // (no initial guess: no history planes)
     }
 
