@@ -68,12 +68,14 @@ KERNELS = {
     # in-place cu / cv reads counted once: 64
     "rhs": ("k_rhs_s (K1, ConstructRHS_V: AB2 MUSCL/Rusanov convection + CN-explicit diffusion + wall terms)", 64),
     # (r4) the direct Poisson solve (ns_fps.hip): the rows' DCT-II read b 8 + write 8; the
-    # recurrences along x: t1 read 8, t2 read 8 + write 8, t3 read 8 + write 8 (chunk / group
-    # aggregates ~1 B/cell more, not counted) -- one interval over five launches; the inverse DCT
+    # recurrences along x, two full passes: t1b read 8, t2b read 8 + write 8 (the three-pass form,
+    # NSGPU_FPS_PASSES=3: t1 read 8, t2 read 8 + write 8, t3 read 8 + write 8 = 40; chunk / group
+    # aggregates ~1-2 B/cell more, not counted) -- one interval over five launches; the inverse DCT
     # read 8 + write 8
     "fps_dct": ("k_fps_dct (direct Poisson solve: DCT-II of every row pair of b - mean, Stockham FFT in LDS)", 16),
-    "fps_tri": ("k_fps_t1 + scan + k_fps_t2 + scan + k_fps_t3 (direct Poisson solve: the tridiagonal "
-                "recurrences along x, one per mode, chunked; five launches timed as one interval)", 40),
+    "fps_tri": ("k_fps_t1b + scan + k_fps_mid + scan + k_fps_t2b (direct Poisson solve: the tridiagonal "
+                "recurrences along x, one per mode, chunked; five launches timed as one interval)",
+                40 if os.environ.get("NSGPU_FPS_PASSES") == "3" else 24),
     "fps_idct": ("k_fps_idct (direct Poisson solve: DCT-III of every row pair -> phi)", 16),
 }
 # one-launch kernels (the `roofline` candidates; fps_tri is five launches)
@@ -367,10 +369,11 @@ def main():
     step_bpc = (64 + 24 + 40 + extrap_bpc + 2 * 24 * hpasses / K + 96 * band_frac
                 + (52 * (cycles - fused) + 28 * fused) / K + 52 * cycles / K / 3.0)
     if direct:
-        # the direct solve: 72 B/cell (fps_* above) per solve, plus its residual check (phi 8 + b 8)
+        # the direct solve: 56 B/cell (fps_* above; 72 in the three-pass form) per solve, plus its residual check (phi 8 + b 8)
         # on the checked solves; no phi extrapolation (no initial guess)
         checks = sum(int(s["n_checks"]) for s in stats)
-        step_bpc = 64 + 24 + 40 + 2 * 24 * hpasses / K + 96 * band_frac + 72 * cycles / K + 16 * checks / K
+        fps_bpc = 16 + KERNELS["fps_tri"][1] + 16
+        step_bpc = 64 + 24 + 40 + 2 * 24 * hpasses / K + 96 * band_frac + fps_bpc * cycles / K + 16 * checks / K
     if channel:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications
         # of (line extension 8 + FUSE_R 28 + FUSE_P 26, x 4/3 for the coarser levels) = 80 each,
@@ -406,7 +409,8 @@ def main():
             d = json.load(open(prof))
             if d.get("n") == n and not channel:
                 traffic = {k: v.get("kernel_bytes_per_launch") for k, v in d.get("kernels", {}).items()}
-                tri = [traffic.get(k) for k in ("fps_t1", "fps_t2", "fps_t3")]
+                tri = [traffic.get(k) for k in (("fps_t1", "fps_t2", "fps_t3")
+                                                if os.environ.get("NSGPU_FPS_PASSES") == "3" else ("fps_t1b", "fps_t2b"))]
                 if all(x is not None for x in tri):
                     traffic["fps_tri"] = sum(tri)
                 src = dict(d.get("source") or {})

@@ -154,6 +154,43 @@ __device__ inline void fft_lds(cplx* z, const cplx* __restrict__ tw, int tid) {
     if constexpr (LOGN % FPS_LR != 0) fft_stage<LOGN, (1 << (LOGN % FPS_LR))>(z, tw, tid, Ns);
 }
 
+// The same transform with its first stage fed from registers and its last stage left in registers
+// (N = 4096: three radix-16 stages, N/16 threads): thread t holds the points t + (N/16) r, r < 16, on
+// entry -- exactly the first Stockham stage's inputs -- and Z[t + (N/16) r] on exit, the last stage's
+// outputs.  Two LDS write passes and two read passes instead of four and four.
+#ifndef FPS_REGIO
+#define FPS_REGIO 1
+#endif
+#ifndef FPS_NT
+#define FPS_NT 0   // A/B: non-temporal stores of the inverse transform's phi
+#endif
+template <int LOGN>
+__device__ inline void fft_regs(cplx* z, const cplx* __restrict__ tw, int tid, cplx* v) {
+    constexpr int N = 1 << LOGN, NB = N / 16, S = LOGN / 4;
+    static_assert(LOGN % 4 == 0 && S >= 2 && Fft<LOGN>::T == NB, "fft_regs: radix-16 stages, N / 16 threads");
+    dft<16>(v);   // stage 1 (Ns = 1: no twiddles), outputs to 16 tid + r
+#pragma unroll
+    for (int r = 0; r < 16; r++) z[pz(16 * tid + r)] = v[r];
+    __syncthreads();
+    int Ns = 16;
+#pragma unroll
+    for (int st = 1; st < S - 1; st++) {
+        fft_stage<LOGN, 16>(z, tw, tid, Ns);
+        Ns *= 16;
+    }
+    // last stage (Ns = N / 16 > tid): k = tid, outputs at tid + Ns r
+#pragma unroll
+    for (int r = 0; r < 16; r++) v[r] = z[pz(tid + r * NB)];
+    const cplx w = tw[tid * (N / (Ns * 16))];
+    cplx wr = w;
+#pragma unroll
+    for (int r = 1; r < 16; r++) {
+        v[r] = cmul(v[r], wr);
+        if (r + 1 < 16) wr = cmul(wr, w);
+    }
+    dft<16>(v);
+}
+
 // (1) DCT-II of row pairs (r0 = 2 p, r0 + 1; the latter absent when nrows is odd) of in - shift
 // -> their coefficients in out.  tw[m] = e^{-2 pi i m / N}, wk[k] = e^{-i pi k / 2N}.  Persistent:
 // a workgroup walks pairs p = blockIdx.x, + gridDim.x, ...; the next pair's rows are loaded into
@@ -186,6 +223,41 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
     // (N = 8192: the prefetch registers would spill -- load each pair when it starts)
     constexpr bool PREF = FPS_PREF && LOGN <= 12;
     int p = blockIdx.x;
+    constexpr bool REGIO = FPS_REGIO && LOGN == 12;
+    if constexpr (REGIO) {
+        // thread t holds v_n, n = t + 256 r: v_n = x_2n (n < N/2), x_{2(N-1-n)+1} (n >= N/2)
+        for (; p < npairs; p += gridDim.x) {
+            const int r0 = 2 * p;
+            const bool two = r0 + 1 < nrows;
+            const double* a = in + (size_t)r0 * ld;
+            cplx v[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int n = tid + r * T;
+                const int j = n < N / 2 ? 2 * n : 2 * (N - 1 - n) + 1;
+                v[r] = cplx{a[j] - sh, two ? a[ld + j] - sh : 0.0};
+            }
+            fft_regs<LOGN>(z, tw, tid, v);
+            __syncthreads();   // (every thread has read its last stage's inputs)
+#pragma unroll
+            for (int r = 0; r < 16; r++) z[pz(tid + r * T)] = v[r];
+            __syncthreads();
+            double* oa = out + (size_t)r0 * ld;
+            double* ob = oa + ld;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int k = tid + r * T;
+                const cplx Zk = v[r], Zn = z[pz((N - k) & (N - 1))];
+                const cplx Va{0.5 * (Zk.x + Zn.x), 0.5 * (Zk.y - Zn.y)};
+                const cplx Vb{0.5 * (Zk.y + Zn.y), 0.5 * (Zn.x - Zk.x)};
+                const cplx w = wk[k];
+                oa[k] = fma(w.x, Va.x, -w.y * Va.y);
+                if (two) ob[k] = fma(w.x, Vb.x, -w.y * Vb.y);
+            }
+            __syncthreads();   // (z is rewritten by the next pair)
+        }
+        return;
+    }
     if (PREF && p < npairs) load(p);
     for (; p < npairs; p += gridDim.x) {
         const int r0 = 2 * p;
@@ -258,6 +330,45 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
     };
     constexpr bool PREF = FPS_PREF && LOGN <= 12;
     int p = blockIdx.x;
+    constexpr bool REGIO = FPS_REGIO && LOGN == 12;
+    if constexpr (REGIO) {
+        // thread t forms conj(V_n), n = t + 256 r, from X_n and X_{N-n} of both rows, and writes
+        // x_2n = Re z_n (n < N/2), x_{2(N-1-n)+1} (n >= N/2) straight from its last stage
+        for (; p < npairs; p += gridDim.x) {
+            const int r0 = 2 * p;
+            const bool two = r0 + 1 < nrows;
+            const double* a = in + (size_t)r0 * ld;
+            cplx v[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int k = tid + r * T;
+                const double xa = a[k], xb = two ? a[ld + k] : 0.0;
+                const double ya = k ? a[N - k] : 0.0, yb = two && k ? a[ld + N - k] : 0.0;
+                const cplx w = wk[k];   // e^{-i theta}: e^{i theta} = (w.x, -w.y)
+                const double c = w.x, s = -w.y;
+                const cplx Va{fma(c, xa, s * ya), fma(s, xa, -c * ya)};
+                const cplx Vb{fma(c, xb, s * yb), fma(s, xb, -c * yb)};
+                v[r] = cplx{Va.x - Vb.y, -(Va.y + Vb.x)};
+            }
+            fft_regs<LOGN>(z, tw, tid, v);
+            double* oa = out + (size_t)r0 * ld;
+            double* ob = oa + ld;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int n = tid + r * T;
+                const int j = n < N / 2 ? 2 * n : 2 * (N - 1 - n) + 1;
+                if constexpr (FPS_NT) {   // (phi goes to HBM, not into the Infinity Cache as dirty lines)
+                    __builtin_nontemporal_store(v[r].x * rn, oa + j);
+                    if (two) __builtin_nontemporal_store(-v[r].y * rn, ob + j);
+                } else {
+                    oa[j] = v[r].x * rn;
+                    if (two) ob[j] = -v[r].y * rn;
+                }
+            }
+            __syncthreads();   // (z is rewritten by the next pair)
+        }
+        return;
+    }
     if (PREF && p < npairs) load(p);
     for (; p < npairs; p += gridDim.x) {
         const int r0 = 2 * p;

@@ -285,6 +285,7 @@ struct ns_solver {
     double *fps_ragg = nullptr, *fps_gath = nullptr, *fps_rin = nullptr;
     double fps_res = -1.0;       // the last checked solve's relative residual
     bool fps_strict = false;     // a check failed (rtol below the solve's round-off): check every solve
+    bool hbn_pend = false;       // slabs: K1's ||RHS||^2 partial sums await the Helmholtz check's all-reduce
     // timed steps: K1 (kev[0..1]) and the direct solve's transforms / recurrences (kev[2..7])
     hipEvent_t kev[8] = {};
 };
@@ -837,7 +838,10 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         sweeps += n;
         nsg::launch_reduce_sum_segs(s->part, nb, 2, s->scal + S_RES, s->st);          // u, v
         if (first) nsg::launch_reduce_sum_segs(p0, nb0, 2, s->scal + S_AUX, s->st);
-        CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
+        static_assert(S_RES == S_HBN + 2, "the deferred RHS norms and the residuals in one all-reduce");
+        if (s->hbn_pend) CHK(allreduce(s, s->scal + S_HBN, 4, ncclSum));
+        else CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
+        s->hbn_pend = false;
         if (first) CHK(allreduce(s, s->scal + S_AUX, 2, ncclSum));
         CHK(fetch_begin(s));
         if (s->extrap_pending && !s->guess_ready && !(s->gin && gin_ok(s) && s->phim_valid > 0)) {
@@ -2340,7 +2344,7 @@ int helm_bnorm(ns_solver* s) {
 
 // K1 with its ghost rows (u, v width 2: MUSCL; phi width 1: grad phi^{n-1} on walls) in one
 // exchange group, overlapped with the interior tiles
-int rhs(ns_solver* s) {
+int rhs(ns_solver* s, bool defer_norm = false) {
     const HaloReq r[3] = {{&s->g, s->arr[NS_ARR_U], 2}, {&s->g, s->arr[NS_ARR_V], 2}, {&s->g, s->arr[NS_ARR_PHI], 1}};
     const bool t = s->timing && s->in_step;
     if (t) {
@@ -2355,7 +2359,10 @@ int rhs(ns_solver* s) {
     if (nb < 0) return nb;
     if (t) CHK(t_end(s, s->kev[0], s->kev[1]));
     nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_HBN, s->st);
-    CHK(allreduce(s, s->scal + S_HBN, 2, ncclSum));
+    // (slabs, rectangle: the norms ride on the Helmholtz solve's first residual all-reduce --
+    // S_HBN and S_RES are adjacent -- one collective less per step)
+    if (defer_norm && comm_on(s) && !s->g.fc) s->hbn_pend = true;
+    else CHK(allreduce(s, s->scal + S_HBN, 2, ncclSum));
     return 0;
 }
 
@@ -2955,7 +2962,7 @@ static int step_body(ns_solver* s, ns_stats& st) {
 }
 
 static int step_body_(ns_solver* s, ns_stats& st) {
-    CHK(rhs(s));                                                   // ConstructRHS_V       (:546)
+    CHK(rhs(s, true));                                             // ConstructRHS_V       (:546)
     // Helmholtz initial guess: u^n.  (The previous step's u* -- kept by correct() in TMPU/TMPV --
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
     // rhs ghost rows (a checked pair pass and the 3-sweep pass read ib-5): multi-rank passes take them with

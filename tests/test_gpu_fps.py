@@ -157,3 +157,26 @@ def test_direct_solve_on_slabs_matches_one_rank(tmp_path, gpu, n, ny, nproc):
     assert rel(demean(r["phi"]), demean(phi)) <= 1e-10
     np.testing.assert_allclose(r["mm"][:, :4], mm[:, :4], atol=1e-10)
     assert np.all(r["mm"][:, 6] == 1) and np.all(mm[:, 6] == 1), (r["mm"][:, 6], mm[:, 6])
+
+
+@pytest.mark.parametrize("nx,ny", [(4096, 4096), (1001, 512), (96, 128)])
+def test_two_pass_recurrences_equal_three_pass(gpu, monkeypatch, nx, ny):
+    """The recurrences in two full passes (t1b, mid, t2b: the local back substitution's dependence on
+    the forward carry-in through host-tabulated coefficients) = the three-pass form
+    (NSGPU_FPS_PASSES=3: t1, t2, t3) to 1e-12 of max|phi| (another rounding order), both against the
+    oracle's restatement; N = 4096 takes the register-fed first / last FFT stage."""
+    rng = np.random.default_rng(nx + 3 * ny)
+    b = rng.uniform(-1, 1, nx * ny)
+    out = {}
+    for passes in ("2", "3"):
+        monkeypatch.setenv("NSGPU_FPS_PASSES", passes)
+        gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny), 1e-3, 100.0, rtol=1e-11)
+        gs.set(gpu.NS_ARR_RPHI, b)
+        its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+        assert its == 1 and res <= 1e-11, (passes, its, res)
+        out[passes] = demean(gs.get(gpu.NS_ARR_PHI))
+        gs.close()
+    assert rel(out["2"], out["3"]) <= 1e-12, rel(out["2"], out["3"])
+    if nx * ny <= 1001 * 512:
+        og = OGrid.rectangle(nx, ny, lx=nx / ny)
+        assert rel(out["2"], demean(og.fps_solve(b))) <= 1e-10
