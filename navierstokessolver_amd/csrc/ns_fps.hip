@@ -155,9 +155,10 @@ __device__ inline void fft_lds(cplx* z, const cplx* __restrict__ tw, int tid) {
 }
 
 // The same transform with its first stage fed from registers and its last stage left in registers
-// (N = 4096: three radix-16 stages, N/16 threads): thread t holds the points t + (N/16) r, r < 16, on
-// entry -- exactly the first Stockham stage's inputs -- and Z[t + (N/16) r] on exit, the last stage's
-// outputs.  Two LDS write passes and two read passes instead of four and four.
+// (N = 1024 ... 8192, N/16 threads): thread t holds the points t + (N/16) r, r < 16, on entry --
+// exactly the first Stockham stage's inputs -- and Z[t + (N/16) r] on exit, the last stage's outputs
+// (a radix-2/4/8 last stage: 16/R butterflies per thread).  At N = 4096 two LDS write passes and two
+// read passes instead of four and four.
 #ifndef FPS_REGIO
 #define FPS_REGIO 1
 #endif
@@ -166,29 +167,39 @@ __device__ inline void fft_lds(cplx* z, const cplx* __restrict__ tw, int tid) {
 #endif
 template <int LOGN>
 __device__ inline void fft_regs(cplx* z, const cplx* __restrict__ tw, int tid, cplx* v) {
-    constexpr int N = 1 << LOGN, NB = N / 16, S = LOGN / 4;
-    static_assert(LOGN % 4 == 0 && S >= 2 && Fft<LOGN>::T == NB, "fft_regs: radix-16 stages, N / 16 threads");
+    constexpr int N = 1 << LOGN, T = N / 16, S16 = LOGN / 4, RL = 1 << (LOGN % 4);
+    static_assert(Fft<LOGN>::T == T && S16 >= 2, "fft_regs: N / 16 threads, at least two radix-16 stages");
     dft<16>(v);   // stage 1 (Ns = 1: no twiddles), outputs to 16 tid + r
 #pragma unroll
     for (int r = 0; r < 16; r++) z[pz(16 * tid + r)] = v[r];
     __syncthreads();
     int Ns = 16;
+    constexpr int MID = RL == 1 ? S16 - 2 : S16 - 1;   // LDS-to-LDS radix-16 stages
 #pragma unroll
-    for (int st = 1; st < S - 1; st++) {
+    for (int st = 0; st < MID; st++) {
         fft_stage<LOGN, 16>(z, tw, tid, Ns);
         Ns *= 16;
     }
-    // last stage (Ns = N / 16 > tid): k = tid, outputs at tid + Ns r
+    // last stage: radix R (16, or the remainder 2 / 4 / 8), Ns = N / R; butterfly jb = tid + b T has
+    // k = jb and outputs Z[jb + Ns r] = Z[tid + T (b + (16 / R) r)]: slot b + (16 / R) r of v
+    constexpr int R = RL == 1 ? 16 : RL, BPT = 16 / R, NB = N / R;
 #pragma unroll
-    for (int r = 0; r < 16; r++) v[r] = z[pz(tid + r * NB)];
-    const cplx w = tw[tid * (N / (Ns * 16))];
-    cplx wr = w;
+    for (int bb = 0; bb < BPT; bb++) {
+        const int jb = tid + bb * T;
+        cplx u[R];
 #pragma unroll
-    for (int r = 1; r < 16; r++) {
-        v[r] = cmul(v[r], wr);
-        if (r + 1 < 16) wr = cmul(wr, w);
+        for (int r = 0; r < R; r++) u[r] = z[pz(jb + r * NB)];
+        const cplx w = tw[jb];   // e^{-2 pi i jb / N}: k (N / (Ns R)) with Ns R = N
+        cplx wr = w;
+#pragma unroll
+        for (int r = 1; r < R; r++) {
+            u[r] = cmul(u[r], wr);
+            if (r + 1 < R) wr = cmul(wr, w);
+        }
+        dft<R>(u);
+#pragma unroll
+        for (int r = 0; r < R; r++) v[bb + BPT * r] = u[r];
     }
-    dft<16>(v);
 }
 
 // (1) DCT-II of row pairs (r0 = 2 p, r0 + 1; the latter absent when nrows is odd) of in - shift
@@ -223,7 +234,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
     // (N = 8192: the prefetch registers would spill -- load each pair when it starts)
     constexpr bool PREF = FPS_PREF && LOGN <= 12;
     int p = blockIdx.x;
-    constexpr bool REGIO = FPS_REGIO && LOGN == 12;
+    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 12;   // (N = 8192: 420 B of spills)
     if constexpr (REGIO) {
         // thread t holds v_n, n = t + 256 r: v_n = x_2n (n < N/2), x_{2(N-1-n)+1} (n >= N/2)
         for (; p < npairs; p += gridDim.x) {
@@ -330,7 +341,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
     };
     constexpr bool PREF = FPS_PREF && LOGN <= 12;
     int p = blockIdx.x;
-    constexpr bool REGIO = FPS_REGIO && LOGN == 12;
+    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 12;   // (N = 8192: 420 B of spills)
     if constexpr (REGIO) {
         // thread t forms conj(V_n), n = t + 256 r, from X_n and X_{N-n} of both rows, and writes
         // x_2n = Re z_n (n < N/2), x_{2(N-1-n)+1} (n >= N/2) straight from its last stage
