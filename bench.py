@@ -78,6 +78,12 @@ KERNELS = {
                 40 if os.environ.get("NSGPU_FPS_PASSES") == "3" else 24),
     "fps_idct": ("k_fps_idct (direct Poisson solve: DCT-III of every row pair -> phi)", 16),
 }
+# (r4) K3 fused into the DCT (NSGPU_FPS_FUSE, default on): the divergence of u*, v* formed in the
+# transform's LDS -- read u*, v* 16 + write the coefficients 8; rhs_phi (8 more) only for a checked solve
+FPS_FUSED = os.environ.get("NSGPU_FPS_FUSE", "1") != "0"
+if FPS_FUSED:
+    KERNELS["fps_dct"] = ("k_fps_dct_div (direct Poisson solve: K3's divergence of u*, v* fused into the DCT-II of "
+                          "every row pair, Stockham FFT in LDS)", 24)
 # one-launch kernels (the `roofline` candidates; fps_tri is five launches)
 SINGLE_LAUNCH = ("restrict", "prolong", "cycle", "guess", "helmholtz", "rhs", "fps_dct", "fps_idct")
 JACOBI_LABEL = "k_jacobi_s<double> (one weighted-Jacobi sweep of the Poisson operator, the north star's roofline kernel)"
@@ -369,11 +375,15 @@ def main():
     step_bpc = (64 + 24 + 40 + extrap_bpc + 2 * 24 * hpasses / K + 96 * band_frac
                 + (52 * (cycles - fused) + 28 * fused) / K + 52 * cycles / K / 3.0)
     if direct:
-        # the direct solve: 56 B/cell (fps_* above; 72 in the three-pass form) per solve, plus its residual check (phi 8 + b 8)
+        # the direct solve: 56 B/cell (fps_* above; 72 in the three-pass form; 64 with K3 fused) per solve, plus its
+        # residual check (phi 8 + b 8)
         # on the checked solves; no phi extrapolation (no initial guess)
+        # (fused K3: no K3 pass (24), the DCT reads u*, v* (24 instead of 16) and stores rhs_phi for the
+        # checked solves, 8 more there)
         checks = sum(int(s["n_checks"]) for s in stats)
-        fps_bpc = 16 + KERNELS["fps_tri"][1] + 16
-        step_bpc = 64 + 24 + 40 + 2 * 24 * hpasses / K + 96 * band_frac + fps_bpc * cycles / K + 16 * checks / K
+        fps_bpc = KERNELS["fps_dct"][1] + KERNELS["fps_tri"][1] + 16
+        step_bpc = (64 + (0 if FPS_FUSED else 24) + 40 + 2 * 24 * hpasses / K + 96 * band_frac + fps_bpc * cycles / K
+                    + (24 if FPS_FUSED else 16) * checks / K)
     if channel:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications
         # of (line extension 8 + FUSE_R 28 + FUSE_P 26, x 4/3 for the coarser levels) = 80 each,
@@ -413,6 +423,7 @@ def main():
                                                 if os.environ.get("NSGPU_FPS_PASSES") == "3" else ("fps_t1b", "fps_t2b"))]
                 if all(x is not None for x in tri):
                     traffic["fps_tri"] = sum(tri)
+                traffic["fps_dct"] = traffic.get("fps_dct_div") if FPS_FUSED else traffic.get("fps_dct")
                 src = dict(d.get("source") or {})
                 src["file"] = "profiles/pmc_traffic.json"
                 src["same_library_as_this_run"] = (src.get("libnsgpu_sha16") is not None and

@@ -39,6 +39,9 @@ __device__ inline cplx cadd(cplx a, cplx b) { return {a.x + b.x, a.y + b.y}; }
 __device__ inline cplx csub(cplx a, cplx b) { return {a.x - b.x, a.y - b.y}; }
 __device__ inline cplx cmul(cplx a, cplx b) { return {fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x)}; }
 
+__device__ inline double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+__device__ inline void st2(double* p, double x, double y) { *reinterpret_cast<double2*>(p) = double2{x, y}; }
+
 // cos / sin (2 pi k / 16), k < 8
 __device__ constexpr double C16[8] = {1.0, 0.92387953251128675613, 0.70710678118654752440, 0.38268343236508977173,
                                       0.0, -0.38268343236508977173, -0.70710678118654752440, -0.92387953251128675613};
@@ -82,6 +85,9 @@ __device__ inline void dft(cplx* v) {
 #define FPS_PREF 0   // 1: the persistent transforms load the next row pair during this one (A/B, r4: 365 vs 343 us per solve -- its registers cost more than the overlap gains)
 #endif
 // (radix 8: two workgroups of N/8 threads per CU need <= 128 VGPRs)
+// (radix 16: the register-fed stages of N = 1024 ... 4096 (FPS_REGIO) take 256 VGPRs + up to 123 AGPRs
+// in k_fps_dct / k_fps_idct -- one workgroup per CU; held to two waves per SIMD they spill 190-510 B
+// per lane to scratch.  k_fps_dct_div, which stages its input through LDS, needs 205-236)
 #if FPS_LR == 3
 #define FPS_WAVES __attribute__((amdgpu_waves_per_eu(4)))
 #else
@@ -202,6 +208,18 @@ __device__ inline void fft_regs(cplx* z, const cplx* __restrict__ tw, int tid, c
     }
 }
 
+// the persistent transforms: tid made opaque at every row pair, so that the LDS slot and twiddle indices
+// of every stage are formed per pair instead of hoisted out of the loop into ~100 live registers (they
+// pushed the kernels past 256 VGPRs, one workgroup per CU).  FPS_REMAT=0: hoisted (A/B)
+#ifndef FPS_REMAT
+#define FPS_REMAT 1
+#endif
+__device__ inline void fps_remat(int& t) {
+#if FPS_REMAT
+    asm volatile("" : "+v"(t));
+#endif
+}
+
 // (1) DCT-II of row pairs (r0 = 2 p, r0 + 1; the latter absent when nrows is odd) of in - shift
 // -> their coefficients in out.  tw[m] = e^{-2 pi i m / N}, wk[k] = e^{-i pi k / 2N}.  Persistent:
 // a workgroup walks pairs p = blockIdx.x, + gridDim.x, ...; the next pair's rows are loaded into
@@ -214,7 +232,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
     constexpr int N = Fft<LOGN>::N, T = Fft<LOGN>::T;
     constexpr int PT = (N + T - 1) / T;
     extern __shared__ cplx z[];
-    const int tid = threadIdx.x;
+    int tid = threadIdx.x;
     const int npairs = (nrows + 1) / 2;
     const double sh = shiftp ? *shiftp : 0.0;
     double ra[PT], rb[PT];
@@ -238,6 +256,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
     if constexpr (REGIO) {
         // thread t holds v_n, n = t + 256 r: v_n = x_2n (n < N/2), x_{2(N-1-n)+1} (n >= N/2)
         for (; p < npairs; p += gridDim.x) {
+            fps_remat(tid);
             const int r0 = 2 * p;
             const bool two = r0 + 1 < nrows;
             const double* a = in + (size_t)r0 * ld;
@@ -271,6 +290,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
     }
     if (PREF && p < npairs) load(p);
     for (; p < npairs; p += gridDim.x) {
+        fps_remat(tid);
         const int r0 = 2 * p;
         const bool two = r0 + 1 < nrows;
         if (!PREF) load(p);
@@ -303,6 +323,180 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
     }
 }
 
+// (1') K3 fused into the transform (r4): the row pair's b = Div_V(u*, v*) / dt (FluidSolver.cpp:380-418,
+// k_cell_s<3>'s arithmetic) formed in the transform's LDS, its sums (sum, sum^2: the mean and
+// ||b - mean|| of MatNullSpaceRemove, :550) as workgroup partials, b itself stored only when asked
+// (the checked solves' residual).  The mean is not known yet: the coefficients are those of b, and the
+// recurrences take N mean off mode 0 (FpsArgs::sh0) -- the DCT of a constant.  One HBM pass less per
+// step (K3's b written and read back).  Pairs p = plo + q pstep, q < cnt (slabs: the interior pairs,
+// then the two edge pairs after the u*, v* ghost-row exchange); consecutive pairs on one XCD (their
+// shared u* rows in its L2).
+__device__ inline double fv_face(double q, double qn, bool has, double r, double ghost) {
+    return has ? qn * r + q * (1 - r) : 0.5 * (q + ghost);
+}
+__device__ inline double fv_ghost(const Geo& g, double q, int side, int d) {
+    return g.neu[side] ? q : (-q + (d == 0 ? g.c0[side] : g.c1[side]));
+}
+__device__ inline double dpp_up1(double x) {   // lane l <- lane l - 1
+    const int lo = __double2loint(x), hi = __double2hiint(x);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, 0x138, 0xf, 0xf, false),
+                            __builtin_amdgcn_update_dpp(lo, lo, 0x138, 0xf, 0xf, false));
+}
+__device__ inline double dpp_dn1(double x) {   // lane l <- lane l + 1
+    const int lo = __double2loint(x), hi = __double2hiint(x);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, 0x130, 0xf, 0xf, false),
+                            __builtin_amdgcn_update_dpp(lo, lo, 0x130, 0xf, 0xf, false));
+}
+
+struct FpsDivArgs {
+    Geo g;
+    Coef c;
+    double dt;
+    const double *u, *v;   // u*, v* (local row 0; one ghost row each side read)
+    double* b;             // null, or rhs_phi is stored too
+    double* out;           // coefficients
+    double* part;          // (sum, sum^2) per workgroup at part + 2 (pbase + blockIdx.x)
+    int nrows, ld, plo, cnt, pstep, pbase;
+    const cplx *tw, *wk;
+};
+
+template <int LOGN>
+__global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivArgs A) {
+    constexpr int N = Fft<LOGN>::N, T = Fft<LOGN>::T, NC = N / 2;   // column pairs per row
+    extern __shared__ cplx z[];
+    const Geo& g = A.g;
+    int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int ld = A.ld;
+    double acc[2] = {0.0, 0.0};
+    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 12;
+    const int G = gridDim.x;
+    const int q0 = G % 8 == 0 ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+    for (int q = q0; q < A.cnt; q += G) {
+        fps_remat(tid);
+        const int p = A.plo + q * A.pstep;
+        const int r0 = 2 * p;
+        const bool two = r0 + 1 < A.nrows;
+        const int gi = g.i0 + r0;
+        const bool hWa = gi > 0, hEa = gi < g.nx - 1, hWb = gi + 1 > 0, hEb = gi + 1 < g.nx - 1;
+        const double hxa = A.c.hx[gi], fwa = A.c.fwx[gi], fea = A.c.fex[gi];
+        const double hxb = two ? A.c.hx[gi + 1] : 1.0, fwb = two ? A.c.fwx[gi + 1] : 0.0, feb = two ? A.c.fex[gi + 1] : 0.0;
+        const double* u0 = A.u + (ptrdiff_t)(r0 - 1) * ld;
+        const double* va = A.v + (ptrdiff_t)r0 * ld;
+        for (int cb = tid; cb < NC; cb += T) {   // (uniform trip count when NC is a multiple of T)
+            const int j = 2 * cb;
+            const double2 uw = ld2(u0 + j), ua = ld2(u0 + ld + j), ub = ld2(u0 + 2 * ld + j), ue = ld2(u0 + 3 * ld + j);
+            const double2 vA = ld2(va + j), vB = ld2(va + ld + j);
+            // v at columns j - 1 / j + 2 from the neighbouring lanes (the wave's edge lanes load them)
+            double vsA = dpp_up1(vA.y), vsB = dpp_up1(vB.y), vnA = dpp_dn1(vA.x), vnB = dpp_dn1(vB.x);
+            if (lane == 0) {
+                const int js = max(j - 1, 0);
+                vsA = va[js];
+                vsB = va[ld + js];
+            }
+            if (lane == 63 || cb + 1 >= NC) {
+                const int jn = min(j + 2, g.ny - 1);
+                vnA = va[jn];
+                vnB = va[ld + jn];
+            }
+            double d[2][2];
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const int jj = j + e;
+                const bool s = jj > 0, n = jj < g.ny - 1;
+                const double hy = A.c.hy[jj], fs = A.c.fsy[jj], fn = A.c.fny[jj];
+#pragma unroll
+                for (int rr = 0; rr < 2; rr++) {
+                    const double2 uc2 = rr ? ub : ua, uw2 = rr ? ua : uw, ue2 = rr ? ue : ub, vv = rr ? vB : vA;
+                    const double uc = e ? uc2.y : uc2.x, uwv = e ? uw2.y : uw2.x, uev = e ? ue2.y : ue2.x;
+                    const double vc = e ? vv.y : vv.x;
+                    const double vs = e ? vv.x : (rr ? vsB : vsA), vn = e ? (rr ? vnB : vnA) : vv.y;
+                    const bool hW = rr ? hWb : hWa, hE = rr ? hEb : hEa;
+                    const double V0 = fv_face(uc, uwv, hW, rr ? fwb : fwa, fv_ghost(g, uc, 0, 0));
+                    const double V1 = fv_face(uc, uev, hE, rr ? feb : fea, fv_ghost(g, uc, 1, 0));
+                    const double V2 = fv_face(vc, vs, s, fs, fv_ghost(g, vc, 2, 1));
+                    const double V3 = fv_face(vc, vn, n, fn, fv_ghost(g, vc, 3, 1));
+                    d[rr][e] = ((V1 - V0) / (rr ? hxb : hxa) + (V3 - V2) / hy) / A.dt;
+                }
+            }
+            if (!two) d[1][0] = d[1][1] = 0.0;
+            acc[0] += d[0][0] + d[0][1];
+            acc[1] += d[0][0] * d[0][0] + d[0][1] * d[0][1];
+            if (two) {
+                acc[0] += d[1][0] + d[1][1];
+                acc[1] += d[1][0] * d[1][0] + d[1][1] * d[1][1];
+            }
+            if (A.b) {
+                st2(A.b + (ptrdiff_t)r0 * ld + j, d[0][0], d[0][1]);
+                if (two) st2(A.b + (ptrdiff_t)(r0 + 1) * ld + j, d[1][0], d[1][1]);
+            }
+            // v_n = x_2n, v_{N-1-n} = x_{2n+1}
+            z[pz(cb)] = cplx{d[0][0], d[1][0]};
+            z[pz(N - 1 - cb)] = cplx{d[0][1], d[1][1]};
+        }
+        __syncthreads();
+        double* oa = A.out + (size_t)r0 * ld;
+        double* ob = oa + ld;
+        if constexpr (REGIO) {
+            cplx v[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) v[r] = z[pz(tid + r * T)];
+            __syncthreads();
+            fft_regs<LOGN>(z, A.tw, tid, v);
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 16; r++) z[pz(tid + r * T)] = v[r];
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int k = tid + r * T;
+                const cplx Zk = v[r], Zn = z[pz((N - k) & (N - 1))];
+                const cplx Va{0.5 * (Zk.x + Zn.x), 0.5 * (Zk.y - Zn.y)};
+                const cplx Vb{0.5 * (Zk.y + Zn.y), 0.5 * (Zn.x - Zk.x)};
+                const cplx w = A.wk[k];
+                oa[k] = fma(w.x, Va.x, -w.y * Va.y);
+                if (two) ob[k] = fma(w.x, Vb.x, -w.y * Vb.y);
+            }
+        } else {
+            constexpr int PT = (N + T - 1) / T;
+            fft_lds<LOGN>(z, A.tw, tid);
+#pragma unroll
+            for (int qq = 0; qq < PT; qq++) {
+                const int k = tid + qq * T;
+                if (k < N) {
+                    const cplx Zk = z[pz(k)], Zn = z[pz((N - k) & (N - 1))];
+                    const cplx Va{0.5 * (Zk.x + Zn.x), 0.5 * (Zk.y - Zn.y)};
+                    const cplx Vb{0.5 * (Zk.y + Zn.y), 0.5 * (Zn.x - Zk.x)};
+                    const cplx w = A.wk[k];
+                    oa[k] = fma(w.x, Va.x, -w.y * Va.y);
+                    if (two) ob[k] = fma(w.x, Vb.x, -w.y * Vb.y);
+                }
+            }
+        }
+        __syncthreads();   // (z is rewritten by the next pair)
+    }
+    // the workgroup's (sum, sum^2): waves by shuffles, then LDS (z is free now)
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc[k] += __shfl_xor(acc[k], off, 64);
+    double* sh = reinterpret_cast<double*>(z);
+    if (lane == 0) {
+        sh[2 * (tid >> 6)] = acc[0];
+        sh[2 * (tid >> 6) + 1] = acc[1];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int w = 0; w < T / 64; w++) {
+            s0 += sh[2 * w];
+            s1 += sh[2 * w + 1];
+        }
+        A.part[2 * (A.pbase + blockIdx.x)] = s0;
+        A.part[2 * (A.pbase + blockIdx.x) + 1] = s1;
+    }
+}
+
 // (3) the inverse: DCT-III with x_j = X_0 / N + (2 / N) sum_k>0 X_k cos(pi k (2j+1) / 2N), through
 // V_k = e^{i pi k / 2N} (X_k - i X_{N-k}) (X_N = 0), v = IFFT(V) = conj(FFT(conj(V))) / N.
 // Persistent like k_fps_dct
@@ -313,7 +507,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
     constexpr int N = Fft<LOGN>::N, T = Fft<LOGN>::T;
     constexpr int PT = (N + T - 1) / T;
     extern __shared__ cplx z[];
-    const int tid = threadIdx.x;
+    int tid = threadIdx.x;
     const int npairs = (nrows + 1) / 2;
     const double rn = 1.0 / N;
     // (each thread loads its coefficients X_k and their mirrors X_{N-k} itself -- the mirrors are
@@ -346,6 +540,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
         // thread t forms conj(V_n), n = t + 256 r, from X_n and X_{N-n} of both rows, and writes
         // x_2n = Re z_n (n < N/2), x_{2(N-1-n)+1} (n >= N/2) straight from its last stage
         for (; p < npairs; p += gridDim.x) {
+            if constexpr (LOGN <= 12) fps_remat(tid);   // (N = 8192: more spills with it)
             const int r0 = 2 * p;
             const bool two = r0 + 1 < nrows;
             const double* a = in + (size_t)r0 * ld;
@@ -382,6 +577,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
     }
     if (PREF && p < npairs) load(p);
     for (; p < npairs; p += gridDim.x) {
+        if constexpr (LOGN <= 12) fps_remat(tid);   // (N = 8192: more spills with it)
         const int r0 = 2 * p;
         const bool two = r0 + 1 < nrows;
         if (!PREF) load(p);
@@ -457,8 +653,14 @@ __device__ inline double piv_next(const FpsArgs& a, int gi, int k, double mu, do
     return (a.pin && k == 0 && gi == a.nx - 1) ? 0.0 : 1.0 / p;
 }
 
-__device__ inline double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
-__device__ inline void st2(double* p, double x, double y) { *reinterpret_cast<double2*>(p) = double2{x, y}; }
+
+// a raw coefficient pair of row li, modes k0, k0 + 1; with the transform fused into K3 (sh0) mode 0
+// takes N mean off here (the DCT of the constant; x - 0.0 is exact for every other mode)
+__device__ inline double2 ldf0(const FpsArgs& a, const double* f, int li, int k0) {
+    double2 x = ld2(f + (size_t)li * a.ld + k0);
+    if (a.sh0 && k0 == 0) x.x -= a.ny * *a.sh0;
+    return x;
+}
 
 // a chunk's rows: every load issued before the recurrence consumes the first (the recurrence is a
 // dependent chain of divisions; one row in flight at a time left the passes at 3 TB/s)
@@ -495,7 +697,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1(FpsArgs a, const double* 
         double2 fv[FPS_M];
 #pragma unroll
         for (int t = 0; t < FPS_M; t++)
-            if (t < rows) fv[t] = ld2(f + (size_t)(li0 + t) * a.ld + k0);
+            if (t < rows) fv[t] = ldf0(a, f, li0 + t, k0);
         double r[2] = {r0.x, r0.y};
 #pragma unroll
         for (int t = 0; t < FPS_M; t++) {
@@ -584,7 +786,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2(FpsArgs a, double* __rest
         double2 yv[FPS_M];   // f, then the exact forward values in place
 #pragma unroll
         for (int t = 0; t < FPS_M; t++)
-            if (t < rows) yv[t] = ld2(f + (size_t)(li0 + t) * a.ld + k0);
+            if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0);
         const double2 y0 = ld2(a.gc + (size_t)grp * a.ld + k0);
         double y[2] = {y0.x, y0.y};
         for (int q = grp * FPS_G; q < c; q++) {
@@ -725,7 +927,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1b(FpsArgs a, const double*
         double2 yv[FPS_M], rv[FPS_M];
 #pragma unroll
         for (int t = 0; t < FPS_M; t++)
-            if (t < rows) yv[t] = ld2(f + (size_t)(li0 + t) * a.ld + k0);
+            if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0);
         double r[2] = {r0.x, r0.y};
 #pragma unroll
         for (int t = 0; t < FPS_M; t++) {
@@ -825,7 +1027,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
     double2 yv[FPS_M];
 #pragma unroll
     for (int t = 0; t < FPS_M; t++)
-        if (t < rows) yv[t] = ld2(f + (size_t)(li0 + t) * a.ld + k0);
+        if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0);
     const double2 yin = ld2(a.ya + (size_t)c * a.ld + k0);
     const double2 x0 = ld2(a.gx + (size_t)grp * a.ld + k0);
     double X[2] = {x0.x, x0.y};
@@ -920,6 +1122,28 @@ void dct_pair(bool inverse, const double* in, const double* shift, double* out, 
     }
 }
 
+template <int LOGN>
+int div_pair(const FpsDivArgs& a0, hipStream_t st) {
+    constexpr int T = Fft<LOGN>::T;
+    const size_t lds = sizeof(cplx) * (size_t)FftLds<LOGN>::n;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    }
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_fps_dct_div<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    const dim3 grid(std::min(a0.cnt, 2 * cus));
+    hipEvent_t a, b;
+    if (take_launch_timing(a, b)) hipExtLaunchKernelGGL(k_fps_dct_div<LOGN>, grid, dim3(T), lds, st, a, b, 0, a0);
+    else hipLaunchKernelGGL(k_fps_dct_div<LOGN>, grid, dim3(T), lds, st, a0);
+    return (int)grid.x;
+}
+
 }  // namespace
 
 int fps_log2(int ny) {
@@ -944,6 +1168,35 @@ int launch_fps_dct(bool inverse, const double* in, const double* shift, double* 
     default: return -1;
     }
     return 0;
+}
+
+int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* b, double* out,
+                   double* part, int phase, int pbase, const double* tw, const double* wk, hipStream_t st) {
+    const int np = (g.nxl + 1) / 2;
+    FpsDivArgs a{g, c, dt, u, v, b, out, part, g.nxl, g.ld, 0, np, 1, pbase, (const cplx*)tw, (const cplx*)wk};
+    if (phase == 1) {
+        a.plo = 1;
+        a.cnt = std::max(np - 2, 0);
+    } else if (phase == 2) {
+        a.cnt = std::min(np, 2);
+        a.pstep = std::max(np - 1, 1);
+    }
+    if (a.cnt <= 0) return pbase;
+    int n = -1;
+    switch (fps_log2(g.ny)) {
+    case 4: n = div_pair<4>(a, st); break;
+    case 5: n = div_pair<5>(a, st); break;
+    case 6: n = div_pair<6>(a, st); break;
+    case 7: n = div_pair<7>(a, st); break;
+    case 8: n = div_pair<8>(a, st); break;
+    case 9: n = div_pair<9>(a, st); break;
+    case 10: n = div_pair<10>(a, st); break;
+    case 11: n = div_pair<11>(a, st); break;
+    case 12: n = div_pair<12>(a, st); break;
+    case 13: n = div_pair<13>(a, st); break;
+    default: return -1;
+    }
+    return pbase + n;
 }
 
 void launch_fps_t1(const FpsArgs& a, const double* f, hipStream_t st) {

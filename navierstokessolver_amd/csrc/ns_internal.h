@@ -287,6 +287,7 @@ struct FpsArgs {
     double* cb;                    // backward chunk aggregates (2 x nch x ld)
     const double* bt;              // two-pass recurrences: per chunk beta (d BX / d Y_in) and BR (2 x nch x ld, host)
     double* ya;                    // two-pass recurrences: every chunk's forward carry-in (nch x ld)
+    const double* sh0 = nullptr;   // fused K3 (launch_fps_div): the mean, taken off mode 0 as ny * mean
 };
 // log2(ny) if ny is a supported power of two, else -1
 int fps_log2(int ny);
@@ -294,6 +295,13 @@ int fps_log2(int ny);
 // tw: ny complex e^{-2 pi i m / ny}, wk: ny complex e^{-i pi k / 2 ny} (interleaved doubles)
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
                    const double* tw, const double* wk, hipStream_t st);
+// K3 fused into the DCT (k_fps_dct_div): b = Div_V(u*, v*) / dt of the slab's rows -> their DCT-II
+// coefficients in out (of b itself: FpsArgs::sh0 takes the mean off later), b stored too if not null,
+// (sum b, sum b^2) per workgroup from part + 2 pbase.  phase 0: every row pair; 1: those whose rows
+// need no ghost row of u*; 2: the others (the first and last pair).  Returns pbase + the partials
+// written, or -1 (ny unsupported)
+int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* b, double* out,
+                   double* part, int phase, int pbase, const double* tw, const double* wk, hipStream_t st);
 void launch_fps_t1(const FpsArgs& a, const double* f, hipStream_t st);
 void launch_fps_t2(const FpsArgs& a, double* f, hipStream_t st);
 void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st);

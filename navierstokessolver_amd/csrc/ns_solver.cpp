@@ -286,6 +286,10 @@ struct ns_solver {
     double fps_res = -1.0;       // the last checked solve's relative residual
     bool fps_strict = false;     // a check failed (rtol below the solve's round-off): check every solve
     bool hbn_pend = false;       // slabs: K1's ||RHS||^2 partial sums await the Helmholtz check's all-reduce
+    // K3 fused into the direct solve's DCT (r4, launch_fps_div; NSGPU_FPS_FUSE=0: K3 + the DCT): inside
+    // steps the divergence goes straight into the transformed plane, rhs_phi is stored only for a checked
+    // solve; fps_pre: the plane holds this step's coefficients (pois_solve_fps skips its DCT)
+    bool fps_fuse = true, fps_pre = false, fps_pre_b = false;
     // timed steps: K1 (kev[0..1]) and the direct solve's transforms / recurrences (kev[2..7])
     hipEvent_t kev[8] = {};
 };
@@ -760,6 +764,7 @@ struct KrylovSolve {
 int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res);
 int correct_launch(ns_solver* s, double* part2);
 int divergence(ns_solver* s);
+bool fps_checks_next(const ns_solver* s);
 bool gin_ok(const ns_solver* s);
 
 // the wall bands' relaxation before the global Helmholtz passes (k_helm_band: band_sweeps RB-SOR
@@ -1676,31 +1681,37 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     // timed steps: the transforms by their dispatch stamps (one rank), the recurrences (five launches,
     // the allgathers on slabs) between marker events
     const bool t = s->timing && s->in_step;
+    // (fps_pre: K3's fused launch left this step's coefficients of b in F -- the recurrences take the
+    // mean off mode 0 -- and timed itself into kev[2..3])
+    const bool pre = s->fps_pre && s->in_step;
+    s->fps_pre = false;
+    nsg::FpsArgs fa = s->fa;
+    if (pre) fa.sh0 = s->scal + S_SHIFT;
     if (t) {
         CHK(ensure_kev(s));
-        CHK(t_begin(s, s->kev[2], s->kev[3]));
+        if (!pre) CHK(t_begin(s, s->kev[2], s->kev[3]));
     }
-    if (nsg::launch_fps_dct(false, s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, F, g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk,
-                            s->st) < 0) {
+    if (!pre && nsg::launch_fps_dct(false, s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, F, g.nxl, g.ny, g.ld, s->fps_tw,
+                                    s->fps_wk, s->st) < 0) {
         set_err("direct Poisson solve: ny = %d is not a supported power of two", g.ny);
         return NS_EINVAL;
     }
     if (t) {
-        CHK(t_end(s, s->kev[2], s->kev[3]));
+        if (!pre) CHK(t_end(s, s->kev[2], s->kev[3]));
         HIPCHK(hipEventRecord(s->kev[4], s->st));
     }
     if (s->fps_passes == 3) {   // (A/B: round 4's first form)
-        nsg::launch_fps_t1(s->fa, F, s->st);
+        nsg::launch_fps_t1(fa, F, s->st);
         CHK(fps_scan(s, false));
-        nsg::launch_fps_t2(s->fa, F, s->st);
+        nsg::launch_fps_t2(fa, F, s->st);
         CHK(fps_scan(s, true));
-        nsg::launch_fps_t3(s->fa, F, s->st);
+        nsg::launch_fps_t3(fa, F, s->st);
     } else {
-        nsg::launch_fps_t1b(s->fa, F, s->st);
+        nsg::launch_fps_t1b(fa, F, s->st);
         CHK(fps_scan(s, false));
-        nsg::launch_fps_mid(s->fa, s->st);
+        nsg::launch_fps_mid(fa, s->st);
         CHK(fps_scan(s, true));
-        nsg::launch_fps_t2b(s->fa, F, s->st);
+        nsg::launch_fps_t2b(fa, F, s->st);
     }
     if (t) {
         HIPCHK(hipEventRecord(s->kev[5], s->st));
@@ -1720,7 +1731,8 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     *its = 1;
     s->last_cycles = s->cur_cycles = -1;
     // (a standalone solve -- ns_kernel -- is always checked; inside steps every fps_check-th)
-    const bool check = !s->in_step || s->fps_strict || (s->fps_check > 0 && s->fps_solves % s->fps_check == 0);
+    // (fused: the check the launch stored rhs_phi for -- the same prediction, fps_checks_next)
+    const bool check = pre ? s->fps_pre_b : !s->in_step || fps_checks_next(s);
     if (s->in_step) s->fps_solves++;
     if (!check) {
         *res = s->fps_res;
@@ -2302,15 +2314,13 @@ int consistent_rhs(ns_solver* s) {
     return 0;
 }
 
-// K3 + null-space mean
-// K3 with the u*, v* ghost rows, overlapped with the interior strips
-int divergence(ns_solver* s) {
-    const HaloReq r[2] = {{&s->g, s->arr[NS_ARR_U], 1}, {&s->g, s->arr[NS_ARR_V], 1}};
-    const int nb = overlapped(s, r, 2, [&]() {
-        return nsg::launch_div(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_RPHI], s->part,
-                               s->st);
-    });
-    if (nb < 0) return nb;
+// whether the direct solve about to run (inside a step) checks its residual (pois_solve_fps)
+bool fps_checks_next(const ns_solver* s) {
+    return s->fps_strict || (s->fps_check > 0 && s->fps_solves % s->fps_check == 0);
+}
+
+// the (sum, sum^2) partials of rhs_phi -> the sums and the null-space shift (one rank: one launch)
+int div_mean(ns_solver* s, int nb) {
     if (!comm_on(s)) {
         nsg::launch_reduce_sum_mean(s->part, nb, s->scal + S_DIVSUM, s->ncells, s->scal + S_SHIFT, s->st);
         return 0;
@@ -2319,6 +2329,59 @@ int divergence(ns_solver* s) {
     CHK(allreduce(s, s->scal + S_DIVSUM, 2, ncclSum));
     nsg::launch_finish_mean(s->scal + S_DIVSUM, s->ncells, s->scal + S_SHIFT, s->st);
     return 0;
+}
+
+// K3 fused into the direct solve's DCT (launch_fps_div): the transformed plane (TMP) and the sums;
+// rhs_phi itself only for a checked solve.  Slabs: the interior row pairs while the u*, v* ghost rows
+// travel, then the two edge pairs (as overlapped() does for the strip kernels)
+int divergence_fps(ns_solver* s) {
+    const bool t = s->timing;
+    if (t) {
+        CHK(ensure_kev(s));
+        CHK(t_begin(s, s->kev[2], s->kev[3]));
+    }
+    double* b = fps_checks_next(s) ? s->arr[NS_ARR_RPHI] : nullptr;
+    auto launch = [&](int phase, int pbase) {
+        return nsg::launch_fps_div(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], b, s->arr[NS_ARR_TMP],
+                                   s->part, phase, pbase, s->fps_tw, s->fps_wk, s->st);
+    };
+    const HaloReq r[2] = {{&s->g, s->arr[NS_ARR_U], 1}, {&s->g, s->arr[NS_ARR_V], 1}};
+    int nb;
+    if (!comm_on(s) || !s->overlap || !s->cst) {
+        CHK(halo_reqs(s, r, 2, s->st));
+        nb = launch(0, 0);
+    } else {
+        HIPCHK(hipEventRecord(s->xev[0], s->st));
+        const int n1 = launch(1, 0);
+        if (n1 < 0) return NS_EINVAL;
+        HIPCHK(hipStreamWaitEvent(s->cst, s->xev[0], 0));
+        CHK(halo_reqs(s, r, 2, s->cst));
+        HIPCHK(hipEventRecord(s->xev[1], s->cst));
+        HIPCHK(hipStreamWaitEvent(s->st, s->xev[1], 0));
+        nb = launch(2, n1);
+    }
+    if (nb < 0) {
+        set_err("direct Poisson solve: ny = %d is not a supported power of two", s->g.ny);
+        return NS_EINVAL;
+    }
+    if (t) CHK(t_end(s, s->kev[2], s->kev[3]));
+    s->fps_pre = true;
+    s->fps_pre_b = b != nullptr;
+    return div_mean(s, nb);
+}
+
+// K3 + null-space mean
+// K3 with the u*, v* ghost rows, overlapped with the interior strips
+int divergence(ns_solver* s) {
+    if (s->fps && s->fps_fuse && s->in_step) return divergence_fps(s);
+    s->fps_pre = false;
+    const HaloReq r[2] = {{&s->g, s->arr[NS_ARR_U], 1}, {&s->g, s->arr[NS_ARR_V], 1}};
+    const int nb = overlapped(s, r, 2, [&]() {
+        return nsg::launch_div(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_RPHI], s->part,
+                               s->st);
+    });
+    if (nb < 0) return nb;
+    return div_mean(s, nb);
 }
 
 // sums of an arbitrary RHS_phi -> null-space shift (standalone solves / sweep benchmark)
@@ -2701,6 +2764,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
                  nsg::fps_log2(gd->ny) >= 0;
         if (const char* e = getenv("NSGPU_FPS_CHECK")) s->fps_check = std::max(0, std::atoi(e));
         if (const char* e = getenv("NSGPU_FPS_PASSES")) s->fps_passes = std::atoi(e) == 3 ? 3 : 2;
+        if (const char* e = getenv("NSGPU_FPS_FUSE")) s->fps_fuse = std::atoi(e) != 0;
         if (s->fps) s->phi_extrap = 0;   // (no initial guess: no history planes)
     }
 

@@ -180,3 +180,34 @@ def test_two_pass_recurrences_equal_three_pass(gpu, monkeypatch, nx, ny):
     if nx * ny <= 1001 * 512:
         og = OGrid.rectangle(nx, ny, lx=nx / ny)
         assert rel(out["2"], demean(og.fps_solve(b))) <= 1e-10
+
+
+@pytest.mark.parametrize("nx,ny", [(64, 64), (37, 64), (1024, 1024), (130, 256)])
+def test_fused_divergence_equals_k3(gpu, monkeypatch, nx, ny):
+    """K3 fused into the DCT (k_fps_dct_div, default inside steps) against K3 + the DCT of b - mean
+    (NSGPU_FPS_FUSE=0): the same steps -- the mean comes off mode 0 instead of every cell, so to
+    rounding: u, v and the monitor to 1e-12, phi (modulo its mean) to 1e-11 of its max; with every
+    solve checked (NSGPU_FPS_CHECK=1) the fused launch stores rhs_phi, K3's values to 1e-13 of their
+    max.  Sizes: the LDS-fed transform (N = 64, 256; odd nx: a one-row last pair) and the register-fed
+    one (N = 1024)."""
+    steps = 6
+    out = {}
+    for fuse, check in (("0", "1"), ("1", "1"), ("1", "16")):
+        monkeypatch.setenv("NSGPU_FPS_FUSE", fuse)
+        monkeypatch.setenv("NSGPU_FPS_CHECK", check)
+        gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny), 1.0 / (8 * max(nx, ny)), 1000.0, rtol=1e-10)
+        mm = np.array([[st[k] for k in ("umin", "umax", "vmin", "vmax", "it_phi")] for st in
+                       (gs.step() for _ in range(steps))])
+        u, v, phi = gs.fields()
+        out[fuse + check] = (mm, u.ravel(), v.ravel(), demean(phi), gs.get(gpu.NS_ARR_RPHI).ravel())
+        gs.close()
+    ref = out["01"]
+    assert np.all(ref[0][:, 4] == 1)
+    for key in ("11", "116"):
+        mm, u, v, phi, _ = out[key]
+        assert np.all(mm[:, 4] == 1), (key, mm[:, 4])
+        np.testing.assert_allclose(mm[:, :4], ref[0][:, :4], atol=1e-12)
+        assert np.max(np.abs(u - ref[1])) <= 1e-12, key
+        assert np.max(np.abs(v - ref[2])) <= 1e-12, key
+        assert rel(phi, ref[3]) <= 1e-11, (key, rel(phi, ref[3]))
+    assert rel(out["11"][4], ref[4]) <= 1e-13, rel(out["11"][4], ref[4])
