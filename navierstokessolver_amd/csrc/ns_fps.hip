@@ -211,6 +211,10 @@ __device__ inline void fft_regs(cplx* z, const cplx* __restrict__ tw, int tid, c
 // the persistent transforms: tid made opaque at every row pair, so that the LDS slot and twiddle indices
 // of every stage are formed per pair instead of hoisted out of the loop into ~100 live registers (they
 // pushed the kernels past 256 VGPRs, one workgroup per CU).  FPS_REMAT=0: hoisted (A/B)
+// pass orders alternating up / down the slab between the direct solve's passes (A/B: 0)
+#ifndef FPS_SNAKE
+#define FPS_SNAKE 1
+#endif
 #ifndef FPS_REMAT
 #define FPS_REMAT 1
 #endif
@@ -330,7 +334,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
 // recurrences take N mean off mode 0 (FpsArgs::sh0) -- the DCT of a constant.  One HBM pass less per
 // step (K3's b written and read back).  Pairs p = plo + q pstep, q < cnt (slabs: the interior pairs,
 // then the two edge pairs after the u*, v* ghost-row exchange); consecutive pairs on one XCD (their
-// shared u* rows in its L2).
+// shared u* rows in its L2).  The sums go out per row pair (deterministic under any split).
 __device__ inline double fv_face(double q, double qn, bool has, double r, double ghost) {
     return has ? qn * r + q * (1 - r) : 0.5 * (q + ghost);
 }
@@ -351,12 +355,12 @@ __device__ inline double dpp_dn1(double x) {   // lane l <- lane l + 1
 struct FpsDivArgs {
     Geo g;
     Coef c;
-    double dt;
+    double rdt;            // 1 / dt
     const double *u, *v;   // u*, v* (local row 0; one ghost row each side read)
     double* b;             // null, or rhs_phi is stored too
     double* out;           // coefficients
-    double* part;          // (sum, sum^2) per workgroup at part + 2 (pbase + blockIdx.x)
-    int nrows, ld, plo, cnt, pstep, pbase;
+    double* part;          // (sum, sum^2) per row pair p at part + 2 p
+    int nrows, ld, plo, cnt, pstep;
     const cplx *tw, *wk;
 };
 
@@ -364,6 +368,7 @@ template <int LOGN>
 __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivArgs A) {
     constexpr int N = Fft<LOGN>::N, T = Fft<LOGN>::T, NC = N / 2;   // column pairs per row
     extern __shared__ cplx z[];
+    __shared__ double red[T / 64][2];
     const Geo& g = A.g;
     int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -379,44 +384,61 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
         const bool two = r0 + 1 < A.nrows;
         const int gi = g.i0 + r0;
         const bool hWa = gi > 0, hEa = gi < g.nx - 1, hWb = gi + 1 > 0, hEb = gi + 1 < g.nx - 1;
-        const double hxa = A.c.hx[gi], fwa = A.c.fwx[gi], fea = A.c.fex[gi];
-        const double hxb = two ? A.c.hx[gi + 1] : 1.0, fwb = two ? A.c.fwx[gi + 1] : 0.0, feb = two ? A.c.fex[gi + 1] : 0.0;
+        const double fwa = A.c.fwx[gi], fea = A.c.fex[gi];
+        const double fwb = two ? A.c.fwx[gi + 1] : 0.0, feb = two ? A.c.fex[gi + 1] : 0.0;
         const double* u0 = A.u + (ptrdiff_t)(r0 - 1) * ld;
         const double* va = A.v + (ptrdiff_t)r0 * ld;
-        for (int cb = tid; cb < NC; cb += T) {   // (uniform trip count when NC is a multiple of T)
+        // (hy uniform -- the transform's premise: one interior column's 1 / hy and face weights; 1 / h and
+        // 1 / dt as products instead of K3's divisions, ~1 ulp apart)
+        const double rhy = A.c.rhy[1], fsy = A.c.fsy[1], fny = A.c.fny[1];
+        const double rhxa = A.c.rhx[gi], rhxb = two ? A.c.rhx[gi + 1] : 0.0;
+        // column pair cb (columns j = 2 cb, j + 1): u* rows r0 - 1 .. r0 + 2, v* rows r0, r0 + 1; v* at
+        // columns j - 1 / j + 2 from the neighbouring lanes, loaded by the wave's edge lanes (E)
+        auto load = [&](int cb, double2(&U)[4], double2(&Vv)[2], double(&E)[4]) {
             const int j = 2 * cb;
-            const double2 uw = ld2(u0 + j), ua = ld2(u0 + ld + j), ub = ld2(u0 + 2 * ld + j), ue = ld2(u0 + 3 * ld + j);
-            const double2 vA = ld2(va + j), vB = ld2(va + ld + j);
-            // v at columns j - 1 / j + 2 from the neighbouring lanes (the wave's edge lanes load them)
-            double vsA = dpp_up1(vA.y), vsB = dpp_up1(vB.y), vnA = dpp_dn1(vA.x), vnB = dpp_dn1(vB.x);
+#pragma unroll
+            for (int k = 0; k < 4; k++) U[k] = ld2(u0 + k * ld + j);
+            Vv[0] = ld2(va + j);
+            Vv[1] = ld2(va + ld + j);
             if (lane == 0) {
                 const int js = max(j - 1, 0);
-                vsA = va[js];
-                vsB = va[ld + js];
+                E[0] = va[js];
+                E[1] = va[ld + js];
             }
             if (lane == 63 || cb + 1 >= NC) {
                 const int jn = min(j + 2, g.ny - 1);
-                vnA = va[jn];
-                vnB = va[ld + jn];
+                E[2] = va[jn];
+                E[3] = va[ld + jn];
+            }
+        };
+        auto cell = [&](int cb, const double2(&U)[4], const double2(&Vv)[2], const double(&E)[4]) {
+            const int j = 2 * cb;
+            double vsA = dpp_up1(Vv[0].y), vsB = dpp_up1(Vv[1].y), vnA = dpp_dn1(Vv[0].x), vnB = dpp_dn1(Vv[1].x);
+            if (lane == 0) {
+                vsA = E[0];
+                vsB = E[1];
+            }
+            if (lane == 63 || cb + 1 >= NC) {
+                vnA = E[2];
+                vnB = E[3];
             }
             double d[2][2];
 #pragma unroll
             for (int e = 0; e < 2; e++) {
                 const int jj = j + e;
                 const bool s = jj > 0, n = jj < g.ny - 1;
-                const double hy = A.c.hy[jj], fs = A.c.fsy[jj], fn = A.c.fny[jj];
 #pragma unroll
                 for (int rr = 0; rr < 2; rr++) {
-                    const double2 uc2 = rr ? ub : ua, uw2 = rr ? ua : uw, ue2 = rr ? ue : ub, vv = rr ? vB : vA;
+                    const double2 uc2 = U[rr + 1], uw2 = U[rr], ue2 = U[rr + 2], vv = Vv[rr];
                     const double uc = e ? uc2.y : uc2.x, uwv = e ? uw2.y : uw2.x, uev = e ? ue2.y : ue2.x;
                     const double vc = e ? vv.y : vv.x;
                     const double vs = e ? vv.x : (rr ? vsB : vsA), vn = e ? (rr ? vnB : vnA) : vv.y;
                     const bool hW = rr ? hWb : hWa, hE = rr ? hEb : hEa;
                     const double V0 = fv_face(uc, uwv, hW, rr ? fwb : fwa, fv_ghost(g, uc, 0, 0));
                     const double V1 = fv_face(uc, uev, hE, rr ? feb : fea, fv_ghost(g, uc, 1, 0));
-                    const double V2 = fv_face(vc, vs, s, fs, fv_ghost(g, vc, 2, 1));
-                    const double V3 = fv_face(vc, vn, n, fn, fv_ghost(g, vc, 3, 1));
-                    d[rr][e] = ((V1 - V0) / (rr ? hxb : hxa) + (V3 - V2) / hy) / A.dt;
+                    const double V2 = fv_face(vc, vs, s, fsy, fv_ghost(g, vc, 2, 1));
+                    const double V3 = fv_face(vc, vn, n, fny, fv_ghost(g, vc, 3, 1));
+                    d[rr][e] = ((V1 - V0) * (rr ? rhxb : rhxa) + (V3 - V2) * rhy) * A.rdt;
                 }
             }
             if (!two) d[1][0] = d[1][1] = 0.0;
@@ -433,8 +455,48 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
             // v_n = x_2n, v_{N-1-n} = x_{2n+1}
             z[pz(cb)] = cplx{d[0][0], d[1][0]};
             z[pz(N - 1 - cb)] = cplx{d[0][1], d[1][1]};
+        };
+        if constexpr (NC % T == 0) {
+            // (N >= 128: every lane has NC / T column pairs; their loads issued in batches of 4 before the
+            // arithmetic -- one HBM latency per batch instead of two per column pair)
+            constexpr int NCT = NC / T, B = NCT < 4 ? NCT : 4;
+#pragma unroll
+            for (int c0 = 0; c0 < NCT; c0 += B) {
+                double2 U[B][4], Vv[B][2];
+                double E[B][4];
+#pragma unroll
+                for (int q = 0; q < B; q++) load(tid + (c0 + q) * T, U[q], Vv[q], E[q]);
+#pragma unroll
+                for (int q = 0; q < B; q++) cell(tid + (c0 + q) * T, U[q], Vv[q], E[q]);
+            }
+        } else {
+            for (int cb = tid; cb < NC; cb += T) {
+                double2 U[4], Vv[2];
+                double E[4];
+                load(cb, U, Vv, E);
+                cell(cb, U, Vv, E);
+            }
         }
+        // the pair's (sum, sum^2) -> part[2 p]: one fixed order per pair, whatever the launches' split
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) acc[k] += __shfl_xor(acc[k], off, 64);
+        if (lane == 0) {
+            red[tid >> 6][0] = acc[0];
+            red[tid >> 6][1] = acc[1];
+        }
+        acc[0] = acc[1] = 0.0;
         __syncthreads();
+        if (tid == 0) {
+            double s0 = 0.0, s1 = 0.0;
+            for (int w = 0; w < T / 64; w++) {
+                s0 += red[w][0];
+                s1 += red[w][1];
+            }
+            A.part[2 * p] = s0;
+            A.part[2 * p + 1] = s1;
+        }
         double* oa = A.out + (size_t)r0 * ld;
         double* ob = oa + ld;
         if constexpr (REGIO) {
@@ -474,26 +536,6 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
             }
         }
         __syncthreads();   // (z is rewritten by the next pair)
-    }
-    // the workgroup's (sum, sum^2): waves by shuffles, then LDS (z is free now)
-#pragma unroll
-    for (int k = 0; k < 2; k++)
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) acc[k] += __shfl_xor(acc[k], off, 64);
-    double* sh = reinterpret_cast<double*>(z);
-    if (lane == 0) {
-        sh[2 * (tid >> 6)] = acc[0];
-        sh[2 * (tid >> 6) + 1] = acc[1];
-    }
-    __syncthreads();
-    if (tid == 0) {
-        double s0 = 0.0, s1 = 0.0;
-        for (int w = 0; w < T / 64; w++) {
-            s0 += sh[2 * w];
-            s1 += sh[2 * w + 1];
-        }
-        A.part[2 * (A.pbase + blockIdx.x)] = s0;
-        A.part[2 * (A.pbase + blockIdx.x) + 1] = s1;
     }
 }
 
@@ -541,7 +583,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
         // x_2n = Re z_n (n < N/2), x_{2(N-1-n)+1} (n >= N/2) straight from its last stage
         for (; p < npairs; p += gridDim.x) {
             if constexpr (LOGN <= 12) fps_remat(tid);   // (N = 8192: more spills with it)
-            const int r0 = 2 * p;
+            const int r0 = 2 * (FPS_SNAKE ? npairs - 1 - p : p);
             const bool two = r0 + 1 < nrows;
             const double* a = in + (size_t)r0 * ld;
             cplx v[16];
@@ -656,9 +698,11 @@ __device__ inline double piv_next(const FpsArgs& a, int gi, int k, double mu, do
 
 // a raw coefficient pair of row li, modes k0, k0 + 1; with the transform fused into K3 (sh0) mode 0
 // takes N mean off here (the DCT of the constant; x - 0.0 is exact for every other mode)
-__device__ inline double2 ldf0(const FpsArgs& a, const double* f, int li, int k0) {
+// (branch-free: a branch per row would keep the chunk's row loads from being issued together)
+__device__ inline double mode0_shift(const FpsArgs& a, int k0) { return a.sh0 && k0 == 0 ? a.ny * *a.sh0 : 0.0; }
+__device__ inline double2 ldf0(const FpsArgs& a, const double* f, int li, int k0, double s0) {
     double2 x = ld2(f + (size_t)li * a.ld + k0);
-    if (a.sh0 && k0 == 0) x.x -= a.ny * *a.sh0;
+    x.x -= s0;
     return x;
 }
 
@@ -692,12 +736,13 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1(FpsArgs a, const double* 
     if (rows > 0) {
         const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
         const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
+        const double s0 = mode0_shift(a, k0);
         ChunkRows cr;
         cr.load(a, li0, rows);
         double2 fv[FPS_M];
 #pragma unroll
         for (int t = 0; t < FPS_M; t++)
-            if (t < rows) fv[t] = ldf0(a, f, li0 + t, k0);
+            if (t < rows) fv[t] = ldf0(a, f, li0 + t, k0, s0);
         double r[2] = {r0.x, r0.y};
 #pragma unroll
         for (int t = 0; t < FPS_M; t++) {
@@ -781,12 +826,13 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2(FpsArgs a, double* __rest
     const int rows = k0 < a.ny ? min(FPS_M, a.nxl - li0) : 0;
     double BX[2] = {0.0, 0.0}, BR[2] = {1.0, 1.0};
     if (rows > 0) {
+        const double s0 = mode0_shift(a, k0);
         ChunkRows cr;
         cr.load(a, li0, rows);
         double2 yv[FPS_M];   // f, then the exact forward values in place
 #pragma unroll
         for (int t = 0; t < FPS_M; t++)
-            if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0);
+            if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0, s0);
         const double2 y0 = ld2(a.gc + (size_t)grp * a.ld + k0);
         double y[2] = {y0.x, y0.y};
         for (int q = grp * FPS_G; q < c; q++) {
@@ -910,24 +956,27 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t3(FpsArgs a, double* __rest
 // groups' backward aggregates, the backward scan gives their carries, and T2b writes the exact values:
 // f is read twice and written once (24 B/cell) instead of read three times and written twice (40).
 
-// T1b: t1 + the chunk's back substitution from zero over its local forward values -> BXl into cb
+// T1b: t1 + the chunk's back substitution from zero over its local forward values -> BXl into cb.
+// (FPS_SNAKE: the groups walk down the slab -- the transform's last rows first, while the Infinity Cache
+// still holds them; t2b then walks up, and the inverse transform down again)
 __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1b(FpsArgs a, const double* __restrict__ f) {
     __shared__ double2 sE[FPS_G][64], sP[FPS_G][64];
     const int lane = threadIdx.x, w = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int k0 = 2 * (blockIdx.x * 64 + lane);
-    const int grp = blockIdx.y, c = grp * FPS_G + w;
+    const int grp = FPS_SNAKE ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y, c = grp * FPS_G + w;
     const int li0 = c * FPS_M;
     const int rows = k0 < a.ny ? min(FPS_M, a.nxl - li0) : 0;
     double E[2] = {0.0, 0.0}, P[2] = {1.0, 1.0};
     if (rows > 0) {
         const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
         const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
+        const double s0 = mode0_shift(a, k0);
         ChunkRows cr;
         cr.load(a, li0, rows);
         double2 yv[FPS_M], rv[FPS_M];
 #pragma unroll
         for (int t = 0; t < FPS_M; t++)
-            if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0);
+            if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0, s0);
         double r[2] = {r0.x, r0.y};
 #pragma unroll
         for (int t = 0; t < FPS_M; t++) {
@@ -1022,12 +1071,13 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
     const int li0 = c * FPS_M;
     const int rows = k0 < a.ny ? min(FPS_M, a.nxl - li0) : 0;
     if (rows <= 0) return;
+    const double s0 = mode0_shift(a, k0);
     ChunkRows cr;
     cr.load(a, li0, rows);
     double2 yv[FPS_M];
 #pragma unroll
     for (int t = 0; t < FPS_M; t++)
-        if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0);
+        if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0, s0);
     const double2 yin = ld2(a.ya + (size_t)c * a.ld + k0);
     const double2 x0 = ld2(a.gx + (size_t)grp * a.ld + k0);
     double X[2] = {x0.x, x0.y};
@@ -1171,9 +1221,9 @@ int launch_fps_dct(bool inverse, const double* in, const double* shift, double* 
 }
 
 int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* b, double* out,
-                   double* part, int phase, int pbase, const double* tw, const double* wk, hipStream_t st) {
+                   double* part, int phase, const double* tw, const double* wk, hipStream_t st) {
     const int np = (g.nxl + 1) / 2;
-    FpsDivArgs a{g, c, dt, u, v, b, out, part, g.nxl, g.ld, 0, np, 1, pbase, (const cplx*)tw, (const cplx*)wk};
+    FpsDivArgs a{g, c, 1.0 / dt, u, v, b, out, part, g.nxl, g.ld, 0, np, 1, (const cplx*)tw, (const cplx*)wk};
     if (phase == 1) {
         a.plo = 1;
         a.cnt = std::max(np - 2, 0);
@@ -1181,7 +1231,7 @@ int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, cons
         a.cnt = std::min(np, 2);
         a.pstep = std::max(np - 1, 1);
     }
-    if (a.cnt <= 0) return pbase;
+    if (a.cnt <= 0) return np;
     int n = -1;
     switch (fps_log2(g.ny)) {
     case 4: n = div_pair<4>(a, st); break;
@@ -1196,7 +1246,7 @@ int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, cons
     case 13: n = div_pair<13>(a, st); break;
     default: return -1;
     }
-    return pbase + n;
+    return n < 0 ? -1 : np;
 }
 
 void launch_fps_t1(const FpsArgs& a, const double* f, hipStream_t st) {

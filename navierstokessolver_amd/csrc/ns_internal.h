@@ -297,11 +297,11 @@ int launch_fps_dct(bool inverse, const double* in, const double* shift, double* 
                    const double* tw, const double* wk, hipStream_t st);
 // K3 fused into the DCT (k_fps_dct_div): b = Div_V(u*, v*) / dt of the slab's rows -> their DCT-II
 // coefficients in out (of b itself: FpsArgs::sh0 takes the mean off later), b stored too if not null,
-// (sum b, sum b^2) per workgroup from part + 2 pbase.  phase 0: every row pair; 1: those whose rows
-// need no ghost row of u*; 2: the others (the first and last pair).  Returns pbase + the partials
-// written, or -1 (ny unsupported)
+// (sum b, sum b^2) per row pair p at part + 2 p.  phase 0: every row pair; 1: those whose rows need no
+// ghost row of u*; 2: the others (the first and last pair).  Returns the partial count (the pairs), or
+// -1 (ny unsupported)
 int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* b, double* out,
-                   double* part, int phase, int pbase, const double* tw, const double* wk, hipStream_t st);
+                   double* part, int phase, const double* tw, const double* wk, hipStream_t st);
 void launch_fps_t1(const FpsArgs& a, const double* f, hipStream_t st);
 void launch_fps_t2(const FpsArgs& a, double* f, hipStream_t st);
 void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st);

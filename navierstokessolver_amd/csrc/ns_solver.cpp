@@ -2341,24 +2341,23 @@ int divergence_fps(ns_solver* s) {
         CHK(t_begin(s, s->kev[2], s->kev[3]));
     }
     double* b = fps_checks_next(s) ? s->arr[NS_ARR_RPHI] : nullptr;
-    auto launch = [&](int phase, int pbase) {
+    auto launch = [&](int phase) {
         return nsg::launch_fps_div(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], b, s->arr[NS_ARR_TMP],
-                                   s->part, phase, pbase, s->fps_tw, s->fps_wk, s->st);
+                                   s->part, phase, s->fps_tw, s->fps_wk, s->st);
     };
     const HaloReq r[2] = {{&s->g, s->arr[NS_ARR_U], 1}, {&s->g, s->arr[NS_ARR_V], 1}};
     int nb;
     if (!comm_on(s) || !s->overlap || !s->cst) {
         CHK(halo_reqs(s, r, 2, s->st));
-        nb = launch(0, 0);
+        nb = launch(0);
     } else {
         HIPCHK(hipEventRecord(s->xev[0], s->st));
-        const int n1 = launch(1, 0);
-        if (n1 < 0) return NS_EINVAL;
+        if (launch(1) < 0) return NS_EINVAL;
         HIPCHK(hipStreamWaitEvent(s->cst, s->xev[0], 0));
         CHK(halo_reqs(s, r, 2, s->cst));
         HIPCHK(hipEventRecord(s->xev[1], s->cst));
         HIPCHK(hipStreamWaitEvent(s->st, s->xev[1], 0));
-        nb = launch(2, n1);
+        nb = launch(2);   // (the partials are per row pair: the same sums as one launch)
     }
     if (nb < 0) {
         set_err("direct Poisson solve: ny = %d is not a supported power of two", s->g.ny);
