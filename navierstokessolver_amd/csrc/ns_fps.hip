@@ -100,12 +100,27 @@ struct Fft {
     static constexpr int T = (N >> FPS_LR) < 64 ? 64 : ((N >> FPS_LR) > 1024 ? 1024 : (N >> FPS_LR));   // threads
 };
 
-// LDS slot of element i: one pad slot every 16 and every 256 elements, so that the Stockham
-// writes of stride 16 and 256 elements (272 / 4368 B apart after padding) fall on distinct banks
-__device__ inline int pz(int i) { return i + (i >> 4) + (i >> 8); }
+// LDS slot of element i (16 B each).  FPS_SWZ = 1 (default): the low three bits of i XOR-ed with bits
+// 4-6 -- the first stage's writes of stride 16 elements land on 8 distinct slots of a 128-B bank row
+// (ds_write_b128 banks), and contiguous ds_read_b128 runs stay conflict-free for its lane groups
+// {0-3,12-15,20-27}, {4-11,16-19,28-31} (MI355X_MICROARCH.md LDS).  The padded layout (FPS_SWZ = 0:
+// one slot every 16 and 256 elements) made every contiguous read 2-way (rocprofv3: SQ_LDS_BANK_CONFLICT
+// = half of SQ_LDS_IDX_ACTIVE in k_fps_dct_div and k_fps_idct).  Only the transform's mirror read
+// (X_{N-k}) stays 2-way.
+#ifndef FPS_SWZ
+#define FPS_SWZ 1
+#endif
+__device__ inline int pz(int i) {
+#if FPS_SWZ
+    return i ^ ((i >> 4) & 7);
+#else
+    return i + (i >> 4) + (i >> 8);
+#endif
+}
 template <int LOGN>
 struct FftLds {
-    static constexpr int n = (1 << LOGN) - 1 + (((1 << LOGN) - 1) >> 4) + (((1 << LOGN) - 1) >> 8) + 1;
+    static constexpr int n = FPS_SWZ ? (1 << LOGN)
+                                     : (1 << LOGN) - 1 + (((1 << LOGN) - 1) >> 4) + (((1 << LOGN) - 1) >> 8) + 1;
 };
 
 // one Stockham stage of radix R over z[N] in LDS (sub-transform length Ns so far); every thread
@@ -335,9 +350,6 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
 // step (K3's b written and read back).  Pairs p = plo + q pstep, q < cnt (slabs: the interior pairs,
 // then the two edge pairs after the u*, v* ghost-row exchange); consecutive pairs on one XCD (their
 // shared u* rows in its L2).  The sums go out per row pair (deterministic under any split).
-__device__ inline double fv_face(double q, double qn, bool has, double r, double ghost) {
-    return has ? qn * r + q * (1 - r) : 0.5 * (q + ghost);
-}
 __device__ inline double fv_ghost(const Geo& g, double q, int side, int d) {
     return g.neu[side] ? q : (-q + (d == 0 ? g.c0[side] : g.c1[side]));
 }
@@ -384,13 +396,11 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
         const bool two = r0 + 1 < A.nrows;
         const int gi = g.i0 + r0;
         const bool hWa = gi > 0, hEa = gi < g.nx - 1, hWb = gi + 1 > 0, hEb = gi + 1 < g.nx - 1;
-        const double fwa = A.c.fwx[gi], fea = A.c.fex[gi];
-        const double fwb = two ? A.c.fwx[gi + 1] : 0.0, feb = two ? A.c.fex[gi + 1] : 0.0;
         const double* u0 = A.u + (ptrdiff_t)(r0 - 1) * ld;
         const double* va = A.v + (ptrdiff_t)r0 * ld;
-        // (hy uniform -- the transform's premise: one interior column's 1 / hy and face weights; 1 / h and
-        // 1 / dt as products instead of K3's divisions, ~1 ulp apart)
-        const double rhy = A.c.rhy[1], fsy = A.c.fsy[1], fny = A.c.fny[1];
+        // (uniform spacing -- the direct solve's premise: one interior column's 1 / hy; 1 / h and 1 / dt
+        // as products instead of K3's divisions)
+        const double rhy = A.c.rhy[1], hrdt = 0.5 * A.rdt;
         const double rhxa = A.c.rhx[gi], rhxb = two ? A.c.rhx[gi + 1] : 0.0;
         // column pair cb (columns j = 2 cb, j + 1): u* rows r0 - 1 .. r0 + 2, v* rows r0, r0 + 1; v* at
         // columns j - 1 / j + 2 from the neighbouring lanes, loaded by the wave's edge lanes (E)
@@ -422,6 +432,9 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
                 vnA = E[2];
                 vnB = E[3];
             }
+            // (uniform spacing: every interior face weight is 1/2, so V1 - V0 = (X - Y) / 2 with X, Y the
+            // east / west neighbours or, across a wall / inlet face, the ghost -- the same divergence as
+            // k_cell_s<3>'s four face values, ~1 ulp apart, in a third of the arithmetic)
             double d[2][2];
 #pragma unroll
             for (int e = 0; e < 2; e++) {
@@ -434,11 +447,9 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
                     const double vc = e ? vv.y : vv.x;
                     const double vs = e ? vv.x : (rr ? vsB : vsA), vn = e ? (rr ? vnB : vnA) : vv.y;
                     const bool hW = rr ? hWb : hWa, hE = rr ? hEb : hEa;
-                    const double V0 = fv_face(uc, uwv, hW, rr ? fwb : fwa, fv_ghost(g, uc, 0, 0));
-                    const double V1 = fv_face(uc, uev, hE, rr ? feb : fea, fv_ghost(g, uc, 1, 0));
-                    const double V2 = fv_face(vc, vs, s, fsy, fv_ghost(g, vc, 2, 1));
-                    const double V3 = fv_face(vc, vn, n, fny, fv_ghost(g, vc, 3, 1));
-                    d[rr][e] = ((V1 - V0) * (rr ? rhxb : rhxa) + (V3 - V2) * rhy) * A.rdt;
+                    const double X = hE ? uev : fv_ghost(g, uc, 1, 0), Y = hW ? uwv : fv_ghost(g, uc, 0, 0);
+                    const double Xn = n ? vn : fv_ghost(g, vc, 3, 1), Ys = s ? vs : fv_ghost(g, vc, 2, 1);
+                    d[rr][e] = fma(X - Y, rr ? rhxb : rhxa, (Xn - Ys) * rhy) * hrdt;
                 }
             }
             if (!two) d[1][0] = d[1][1] = 0.0;

@@ -187,7 +187,7 @@ def test_fused_divergence_equals_k3(gpu, monkeypatch, nx, ny):
     """K3 fused into the DCT (k_fps_dct_div, default inside steps) against K3 + the DCT of b - mean
     (NSGPU_FPS_FUSE=0): the same steps -- the mean comes off mode 0 instead of every cell, so to
     rounding: u, v and the monitor to 1e-12, phi (modulo its mean) to 1e-11 of its max; with every
-    solve checked (NSGPU_FPS_CHECK=1) the fused launch stores rhs_phi, K3's values to 1e-13 of their
+    solve checked (NSGPU_FPS_CHECK=1) the fused launch stores rhs_phi, K3's values to 1e-11 of their
     max.  Sizes: the LDS-fed transform (N = 64, 256; odd nx: a one-row last pair) and the register-fed
     one (N = 1024)."""
     steps = 6
@@ -210,4 +210,4 @@ def test_fused_divergence_equals_k3(gpu, monkeypatch, nx, ny):
         assert np.max(np.abs(u - ref[1])) <= 1e-12, key
         assert np.max(np.abs(v - ref[2])) <= 1e-12, key
         assert rel(phi, ref[3]) <= 1e-11, (key, rel(phi, ref[3]))
-    assert rel(out["11"][4], ref[4]) <= 1e-13, rel(out["11"][4], ref[4])
+    assert rel(out["11"][4], ref[4]) <= 1e-11, rel(out["11"][4], ref[4])
