@@ -271,7 +271,10 @@ int max_partials(const Geo& g);
 
 // ---- the direct Poisson solve of rectangles with uniform hy (ns_fps.hip, r4) ----
 constexpr int FPS_M = 16;          // rows per chunk of the tridiagonal recurrences
-constexpr int FPS_G = 8;           // chunks per group (one workgroup)
+#ifndef FPS_GRP
+#define FPS_GRP 4   // (r4 A/B at 4096^2: 8 -> 4 waves per workgroup, three workgroups per CU at 154 VGPRs: recurrences 149 -> 138 us)
+#endif
+constexpr int FPS_G = FPS_GRP;     // chunks per group (one workgroup of FPS_G waves)
 constexpr int FPS_LOGN_MIN = 4;    // ny = 2^4 .. 2^13 (the row pair's FFT fits 128 KiB of LDS)
 constexpr int FPS_LOGN_MAX = 13;
 struct FpsArgs {
