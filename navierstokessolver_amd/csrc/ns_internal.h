@@ -270,7 +270,10 @@ void launch_bicg_scal(int stage, const double* d, double n, double* sc, hipStrea
 int max_partials(const Geo& g);
 
 // ---- the direct Poisson solve of rectangles with uniform hy (ns_fps.hip, r4) ----
-constexpr int FPS_M = 16;          // rows per chunk of the tridiagonal recurrences
+#ifndef FPS_ROWS
+#define FPS_ROWS 16
+#endif
+constexpr int FPS_M = FPS_ROWS;    // rows per chunk of the tridiagonal recurrences
 #ifndef FPS_GRP
 #define FPS_GRP 4   // (r4 A/B at 4096^2: 8 -> 4 waves per workgroup, three workgroups per CU at 154 VGPRs: recurrences 149 -> 138 us)
 #endif
