@@ -825,6 +825,81 @@ __global__ void k_fps_scan(int ngrp, int ld, int ny, const double* __restrict__ 
     }
 }
 
+// The same scan with the groups cut into FPS_SSEG segments per mode (one wave each, modes across the
+// lanes): every wave folds its segment from zero, the first wave folds the segments' aggregates in
+// order into their carry-ins (and the rank's aggregate), then every wave walks its segment again from
+// its carry-in -- a chain of ngrp / S + S dependent steps instead of ngrp (the single-thread-per-mode
+// scan's 64 groups at 4096^2 took 9 us a direction).  The same affine maps composed in another
+// grouping (~1 ulp apart).  FPS_SSEG = 1: k_fps_scan (A/B)
+#ifndef FPS_SSEG
+#define FPS_SSEG 8
+#endif
+template <int S>
+__global__ void __launch_bounds__(64 * S) k_fps_scan_seg(int ngrp, int ld, int ny, const double* __restrict__ agg,
+                                                         double* __restrict__ carry, const double* __restrict__ rin,
+                                                         double* __restrict__ rout, int backward) {
+    __shared__ double sE[S][64], sP[S][64], sY[S][64];
+    const int lane = threadIdx.x, s = threadIdx.y;
+    const int k = blockIdx.x * 64 + lane;
+    const int per = (ngrp + S - 1) / S, q0 = s * per, q1 = min(ngrp, q0 + per);
+    constexpr int B = 8;
+    auto gq = [&](int q) { return backward ? ngrp - 1 - q : q; };
+    double AE = 0.0, AP = 1.0;
+    if (k < ny) {
+        for (int qb = q0; qb < q1; qb += B) {
+            double E[B], P[B];
+#pragma unroll
+            for (int t = 0; t < B; t++) {
+                const int q = qb + t;
+                E[t] = q < q1 ? agg[(size_t)gq(q) * ld + k] : 0.0;
+                P[t] = q < q1 ? agg[(size_t)(ngrp + gq(q)) * ld + k] : 1.0;
+            }
+#pragma unroll
+            for (int t = 0; t < B; t++) {
+                AE = fma(P[t], AE, E[t]);
+                AP = P[t] * AP;
+            }
+        }
+    }
+    sE[s][lane] = AE;
+    sP[s][lane] = AP;
+    __syncthreads();
+    if (s == 0 && k < ny) {
+        double Y = rin ? rin[k] : 0.0, TE = 0.0, TP = 1.0;
+        for (int t = 0; t < S; t++) {
+            sY[t][lane] = Y;
+            Y = fma(sP[t][lane], Y, sE[t][lane]);
+            TE = fma(sP[t][lane], TE, sE[t][lane]);
+            TP = sP[t][lane] * TP;
+        }
+        if (rout) {
+            rout[k] = TE;
+            rout[ld + k] = TP;
+        }
+    }
+    __syncthreads();
+    if (k < ny) {
+        double Y = sY[s][lane];
+        for (int qb = q0; qb < q1; qb += B) {
+            double E[B], P[B];
+#pragma unroll
+            for (int t = 0; t < B; t++) {
+                const int q = qb + t;
+                E[t] = q < q1 ? agg[(size_t)gq(q) * ld + k] : 0.0;
+                P[t] = q < q1 ? agg[(size_t)(ngrp + gq(q)) * ld + k] : 1.0;
+            }
+#pragma unroll
+            for (int t = 0; t < B; t++) {
+                const int q = qb + t;
+                if (q < q1) {
+                    carry[(size_t)gq(q) * ld + k] = Y;
+                    Y = fma(P[t], Y, E[t]);
+                }
+            }
+        }
+    }
+}
+
 // T2: the chunk's carry-in (the group's, through the group's earlier chunks: T1's aggregates), the
 // exact forward values from it, then the back substitution from zero -> xl (in place over f) and the
 // chunk's backward aggregate (x_s = BX + BR x_e) into cb; the workgroup folds its chunks into gb
@@ -1284,8 +1359,12 @@ void launch_fps_rank_carry(const FpsArgs& a, const double* gathered, int P, int 
                        backward ? 1 : 0, rin);
 }
 void launch_fps_scan(const FpsArgs& a, bool backward, const double* rin, double* rout, hipStream_t st) {
-    hipLaunchKernelGGL(k_fps_scan, dim3((a.ny + 63) / 64), dim3(64), 0, st, a.ngrp, a.ld, a.ny,
-                       backward ? a.gb : a.ga, backward ? a.gx : a.gc, rin, rout, backward ? 1 : 0);
+    if (FPS_SSEG > 1 && a.ngrp >= 2 * FPS_SSEG)
+        hipLaunchKernelGGL(k_fps_scan_seg<FPS_SSEG>, dim3((a.ny + 63) / 64), dim3(64, FPS_SSEG), 0, st, a.ngrp, a.ld,
+                           a.ny, backward ? a.gb : a.ga, backward ? a.gx : a.gc, rin, rout, backward ? 1 : 0);
+    else
+        hipLaunchKernelGGL(k_fps_scan, dim3((a.ny + 63) / 64), dim3(64), 0, st, a.ngrp, a.ld, a.ny,
+                           backward ? a.gb : a.ga, backward ? a.gx : a.gc, rin, rout, backward ? 1 : 0);
 }
 
 }  // namespace nsg
