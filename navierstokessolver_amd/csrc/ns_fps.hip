@@ -183,6 +183,9 @@ __device__ inline void fft_lds(cplx* z, const cplx* __restrict__ tw, int tid) {
 #ifndef FPS_REGIO
 #define FPS_REGIO 1
 #endif
+#ifndef FPS_ISTAGE
+#define FPS_ISTAGE 1   // the register-fed inverse transform's output staged through LDS (A/B: 0)
+#endif
 #ifndef FPS_NT
 #define FPS_NT 0   // A/B: non-temporal stores of the inverse transform's phi
 #endif
@@ -612,16 +615,33 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
             fft_regs<LOGN>(z, tw, tid, v);
             double* oa = out + (size_t)r0 * ld;
             double* ob = oa + ld;
+            if constexpr (FPS_ISTAGE) {
+                // (staged through LDS: each lane then stores columns 2m, 2m + 1 of both rows as 16 B --
+                // the direct stores of x_2n / x_{2n+1} from the registers left every line half-written
+                // at a time: rocprofv3 WRITE_SIZE 1.34x of phi's bytes)
+                __syncthreads();   // (every thread has read its last stage's inputs)
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int n = tid + r * T;
-                const int j = n < N / 2 ? 2 * n : 2 * (N - 1 - n) + 1;
-                if constexpr (FPS_NT) {   // (phi goes to HBM, not into the Infinity Cache as dirty lines)
-                    __builtin_nontemporal_store(v[r].x * rn, oa + j);
-                    if (two) __builtin_nontemporal_store(-v[r].y * rn, ob + j);
-                } else {
-                    oa[j] = v[r].x * rn;
-                    if (two) ob[j] = -v[r].y * rn;
+                for (int r = 0; r < 16; r++) z[pz(tid + r * T)] = v[r];
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const int m = tid + q * T;   // columns 2m (v_m) and 2m + 1 (v_{N-1-m})
+                    const cplx e = z[pz(m)], o = z[pz(N - 1 - m)];
+                    st2(oa + 2 * m, e.x * rn, o.x * rn);
+                    if (two) st2(ob + 2 * m, -e.y * rn, -o.y * rn);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int n = tid + r * T;
+                    const int j = n < N / 2 ? 2 * n : 2 * (N - 1 - n) + 1;
+                    if constexpr (FPS_NT) {   // (phi goes to HBM, not into the Infinity Cache as dirty lines)
+                        __builtin_nontemporal_store(v[r].x * rn, oa + j);
+                        if (two) __builtin_nontemporal_store(-v[r].y * rn, ob + j);
+                    } else {
+                        oa[j] = v[r].x * rn;
+                        if (two) ob[j] = -v[r].y * rn;
+                    }
                 }
             }
             __syncthreads();   // (z is rewritten by the next pair)
