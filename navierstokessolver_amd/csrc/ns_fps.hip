@@ -85,9 +85,8 @@ __device__ inline void dft(cplx* v) {
 #define FPS_PREF 0   // 1: the persistent transforms load the next row pair during this one (A/B, r4: 365 vs 343 us per solve -- its registers cost more than the overlap gains)
 #endif
 // (radix 8: two workgroups of N/8 threads per CU need <= 128 VGPRs)
-// (radix 16: the register-fed stages of N = 1024 ... 4096 (FPS_REGIO) take 256 VGPRs + up to 123 AGPRs
-// in k_fps_dct / k_fps_idct -- one workgroup per CU; held to two waves per SIMD they spill 190-510 B
-// per lane to scratch.  k_fps_dct_div, which stages its input through LDS, needs 205-236)
+// (radix 16: the register-fed stages (FPS_REGIO, N = 1024 ... 8192) need 134-210 VGPRs with the LDS indices
+// formed per row pair (fps_remat); hoisted, they took 256 VGPRs + up to 123 AGPRs -- one workgroup per CU)
 #if FPS_LR == 3
 #define FPS_WAVES __attribute__((amdgpu_waves_per_eu(4)))
 #else
@@ -274,7 +273,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
     // (N = 8192: the prefetch registers would spill -- load each pair when it starts)
     constexpr bool PREF = FPS_PREF && LOGN <= 12;
     int p = blockIdx.x;
-    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 12;   // (N = 8192: 420 B of spills)
+    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 13;
     if constexpr (REGIO) {
         // thread t holds v_n, n = t + 256 r: v_n = x_2n (n < N/2), x_{2(N-1-n)+1} (n >= N/2)
         for (; p < npairs; p += gridDim.x) {
@@ -389,7 +388,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
     const int lane = tid & 63;
     const int ld = A.ld;
     double acc[2] = {0.0, 0.0};
-    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 12;
+    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 13;
     const int G = gridDim.x;
     const int q0 = G % 8 == 0 ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
     for (int q = q0; q < A.cnt; q += G) {
@@ -591,12 +590,12 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
     };
     constexpr bool PREF = FPS_PREF && LOGN <= 12;
     int p = blockIdx.x;
-    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 12;   // (N = 8192: 420 B of spills)
+    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 13;
     if constexpr (REGIO) {
         // thread t forms conj(V_n), n = t + 256 r, from X_n and X_{N-n} of both rows, and writes
         // x_2n = Re z_n (n < N/2), x_{2(N-1-n)+1} (n >= N/2) straight from its last stage
         for (; p < npairs; p += gridDim.x) {
-            if constexpr (LOGN <= 12) fps_remat(tid);   // (N = 8192: more spills with it)
+            fps_remat(tid);
             const int r0 = 2 * (FPS_SNAKE ? npairs - 1 - p : p);
             const bool two = r0 + 1 < nrows;
             const double* a = in + (size_t)r0 * ld;
@@ -650,7 +649,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
     }
     if (PREF && p < npairs) load(p);
     for (; p < npairs; p += gridDim.x) {
-        if constexpr (LOGN <= 12) fps_remat(tid);   // (N = 8192: more spills with it)
+        fps_remat(tid);
         const int r0 = 2 * p;
         const bool two = r0 + 1 < nrows;
         if (!PREF) load(p);
