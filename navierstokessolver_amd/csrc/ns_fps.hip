@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
     // (N = 8192: the prefetch registers would spill -- load each pair when it starts)
     constexpr bool PREF = FPS_PREF && LOGN <= 12;
     int p = blockIdx.x;
-    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 13;
+    constexpr bool REGIO = FPS_REGIO && FPS_LR == 4 && LOGN >= 10 && LOGN <= 13;
     if constexpr (REGIO) {
         // thread t holds v_n, n = t + 256 r: v_n = x_2n (n < N/2), x_{2(N-1-n)+1} (n >= N/2)
         for (; p < npairs; p += gridDim.x) {
@@ -388,7 +388,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
     const int lane = tid & 63;
     const int ld = A.ld;
     double acc[2] = {0.0, 0.0};
-    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 13;
+    constexpr bool REGIO = FPS_REGIO && FPS_LR == 4 && LOGN >= 10 && LOGN <= 13;
     const int G = gridDim.x;
     const int q0 = G % 8 == 0 ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
     for (int q = q0; q < A.cnt; q += G) {
@@ -590,7 +590,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
     };
     constexpr bool PREF = FPS_PREF && LOGN <= 12;
     int p = blockIdx.x;
-    constexpr bool REGIO = FPS_REGIO && LOGN >= 10 && LOGN <= 13;
+    constexpr bool REGIO = FPS_REGIO && FPS_LR == 4 && LOGN >= 10 && LOGN <= 13;
     if constexpr (REGIO) {
         // thread t forms conj(V_n), n = t + 256 r, from X_n and X_{N-n} of both rows, and writes
         // x_2n = Re z_n (n < N/2), x_{2(N-1-n)+1} (n >= N/2) straight from its last stage

@@ -1662,6 +1662,10 @@ __device__ __forceinline__ double extrap_comb(double a, double x, double b, doub
     return r;
 }
 
+// K5's rows in flight (A/B: make variant DEFS=-DK5_SD=n)
+#ifndef K5_SD
+#define K5_SD 4
+#endif
 // K6's rows in flight (A/B: make variant DEFS=-DK6_SD=n)
 #ifndef K6_SD
 #define K6_SD 2
@@ -1678,7 +1682,7 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
     const int srow = A.P.pbase >= 0 ? A.P.pbase + run : (run < A.P.slo ? run : A.P.rb1 / A.P.L + (run - A.P.slo));
     const int wid = srow * A.nsj + (w - run * A.nsj);
     constexpr bool K5 = K == 5 || K == 6;
-    constexpr int SDK = K == 6 ? K6_SD : SD;   // rows in flight (K6 streams six planes)
+    constexpr int SDK = K == 6 ? K6_SD : K == 5 ? K5_SD : SD;   // rows in flight (K6 streams six planes)
     double acc[4] = {0.0, 0.0, INFINITY, INFINITY};   // K3: sum, sum^2; K5: (umin, -umax, vmin, -vmax)
     if (K5) acc[0] = acc[1] = INFINITY;
     if (w < nstr) {
