@@ -211,3 +211,28 @@ def test_fused_divergence_equals_k3(gpu, monkeypatch, nx, ny):
         assert np.max(np.abs(v - ref[2])) <= 1e-12, key
         assert rel(phi, ref[3]) <= 1e-11, (key, rel(phi, ref[3]))
     assert rel(out["11"][4], ref[4]) <= 1e-11, rel(out["11"][4], ref[4])
+
+
+def test_direct_solve_steps_vs_reference_krylov_256(gpu):
+    """The GPU's default step (direct Poisson solve, RB-SOR Helmholtz) against the oracle's
+    reference-faithful algorithm (OSolver's default: the Krylov solves of the reference's assembled
+    matrices, KSPSolve at FluidSolver.cpp:547-551), both at rtol 1e-12 on a 256^2 Re-1000 cavity for
+    4 steps: both converge onto the same discrete solution -- u, v and the monitor to 1e-9, phi
+    (modulo its mean) to 1e-7 of its norm.  Extends the reference-path comparison past 128^2."""
+    n, steps, re = 256, 4, 1000.0
+    dt = 1.0 / (8 * n)
+    og = OGrid.rectangle(n, n)
+    gs = gpu.GpuSolver(gpu.cavity(n), dt, re, rtol=1e-12)
+    osv = OSolver(og, dt, re, rtol=1e-12)
+    for _ in range(steps):
+        st = gs.step()
+        mm, _ = osv.step()
+        assert st["it_phi"] == 1
+        np.testing.assert_allclose([st["umin"], st["umax"], st["vmin"], st["vmax"]], mm, atol=1e-9)
+    ref = osv.get()
+    u, v, phi = gs.fields()
+    gs.close()
+    assert np.max(np.abs(u.ravel() - ref["u"])) <= 1e-9
+    assert np.max(np.abs(v.ravel() - ref["v"])) <= 1e-9
+    p, q = demean(phi), demean(ref["phi"])
+    assert np.linalg.norm(p - q) <= 1e-7 * np.linalg.norm(q)
