@@ -274,6 +274,7 @@ struct ns_solver {
     // phi.  The solve is a fixed arithmetic sequence: its residual does not drift between checks
     // (1e-13 .. 1e-12 of ||b|| at 4096^2).  NSGPU_FPS=0: multigrid
     bool fps = false;
+    bool fps_pc = false;         // masked domain: the bounding box's direct solve preconditions BiCGStab (NSGPU_FPS_PC=0: V-cycle)
     nsg::FpsArgs fa{};
     double* fps_mem = nullptr;
     const double *fps_tw = nullptr, *fps_wk = nullptr;
@@ -1522,6 +1523,26 @@ int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch, int* tn = 
     return rc;
 }
 
+// (r4) z = M^-1 q for a masked domain on one rank whose bounding box admits the direct solve: the
+// box's exact Poisson solve (ns_fps.hip: DCT, recurrences, inverse DCT; F in `scratch`) in place of
+// one V-cycle of its multigrid -- the same fictitious-domain preconditioner, solved exactly.  q is
+// mean-free over the domain and 0 outside it, so the box's mode 0 is consistent
+int fps_scan(ns_solver* s, bool backward);
+int fps_precond(ns_solver* s, const double* q, double* z, double* scratch) {
+    const nsg::Geo& g = s->g;
+    if (nsg::launch_fps_dct(false, q, nullptr, scratch, g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st) < 0) {
+        set_err("direct Poisson preconditioner: ny = %d is not a supported power of two", g.ny);
+        return NS_EINVAL;
+    }
+    nsg::launch_fps_t1b(s->fa, scratch, s->st);
+    CHK(fps_scan(s, false));
+    nsg::launch_fps_mid(s->fa, s->st);
+    CHK(fps_scan(s, true));
+    nsg::launch_fps_t2b(s->fa, scratch, s->st);
+    nsg::launch_fps_dct(true, scratch, nullptr, z, g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st);
+    return 0;
+}
+
 // One BiCGStab solve A x = b - shift on this solver's planes (x updated in place).
 //   op 0: the Poisson matrix (NEUMANN outflow rows / a masked domain), solved as
 //         P A x = P (b - shift) with P the mean projection over the domain's cells;
@@ -1557,6 +1578,7 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
     int tn = 0;
     const bool timed = s->timing && ks.stt && ks.mg;
     auto precond = [&](double* q, int k) -> int {   // K[k] = M^-1 q
+        if (ks.mg && ks.op == 0 && s->fps_pc) return fps_precond(s, q, s->kv[k], s->kv[8]);
         if (ks.mg) return mg_precond(s, q, s->kv[k], s->kv[8], timed ? &tn : nullptr);
         nsg::launch_diag_pc(ks.op, s->g, s->c, ks.alpha, q, s->kv[k], s->st);
         return 0;
@@ -2765,6 +2787,9 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (const char* e = getenv("NSGPU_FPS_PASSES")) s->fps_passes = std::atoi(e) == 3 ? 3 : 2;
         if (const char* e = getenv("NSGPU_FPS_FUSE")) s->fps_fuse = std::atoi(e) != 0;
         if (s->fps) s->phi_extrap = 0;   // (no initial guess: no history planes)
+        const char* fpc = getenv("NSGPU_FPS_PC");
+        s->fps_pc = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !(fpc && std::atoi(fpc) == 0) &&
+                    masked && !outflow && yuni && p->nranks == 1 && nsg::fps_log2(gd->ny) >= 0;
     }
 
     auto fail = [&](int rc) { ns_destroy(s); return rc; };
@@ -2878,7 +2903,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (hipMalloc(&s->coef, h.size() * sizeof(double)) != hipSuccess) { set_err("hipMalloc coef failed"); return fail(NS_ENOMEM); }
         if (hipMemcpy(s->coef, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) { set_err("coef upload failed"); return fail(NS_EHIP); }
         s->c = coef_view(s->coef, g.nx, g.ny);
-        if (s->fps)
+        if (s->fps || s->fps_pc)
             if (int rc = fps_setup(s, hy0, h.data(), h.data() + g.nx)) return fail(rc);
     }
     // a masked domain's Poisson preconditioner: one V-cycle of the BOUNDING BOX's wall-closure
