@@ -217,6 +217,14 @@ def cpu_baseline(n, re, dt, omega_v, omega_mg, state, gpu_next=None):
     }
 
 
+def _rccl_version(torch):
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception as e:   # (diagnostic only)
+        return f"unknown ({type(e).__name__})"
+
+
 def self_launch(args) -> int:
     """--gpus N > 1 without a launcher (no WORLD_SIZE in the env): start N ranks, one per GPU,
     under torch.distributed.run on 127.0.0.1 as a CHILD process -- before anything here touches
@@ -251,6 +259,45 @@ def self_launch(args) -> int:
     return p.wait()
 
 
+METRIC = "cell-updates/sec (MLUPS) + Poisson iters/sec, 4096^2 grid at 1/2/4/8 GPUs"
+
+
+class Watchdog:
+    """Multi-rank runs: a rank that stops making progress -- an RCCL collective
+    waiting on a peer that died, a hung communicator set-up -- prints a JSON error line and exits
+    non-zero instead of hanging silently; torch.distributed.run then tears the other ranks down.
+    `beat(phase, limit_s)`: the next `limit_s` seconds belong to `phase`."""
+
+    def __init__(self, rank, world):
+        import threading
+        self.rank, self.world = rank, world
+        self.phase, self.deadline = "start", time.monotonic() + 600.0
+        self._lock = threading.Lock()
+        t = threading.Thread(target=self._run, daemon=True)
+        t.start()
+
+    def beat(self, phase, limit_s):
+        with self._lock:
+            self.phase, self.deadline = phase, time.monotonic() + limit_s
+
+    def _run(self):
+        while True:
+            time.sleep(2.0)
+            with self._lock:
+                late = time.monotonic() > self.deadline
+                phase = self.phase
+            if late:
+                fail_line(self.rank, self.world, f"rank {self.rank}: no progress in phase '{phase}' (watchdog)")
+                os._exit(3)
+
+
+def fail_line(rank, world, msg):
+    """The JSON error line of a failed run (stdout, one write) -- parseable like the bench line."""
+    sys.stdout.write("\n" + json.dumps({"metric": METRIC, "value": None, "unit": "MLUPS", "n_gpus": world,
+                                        "error": msg, "rank": rank}) + "\n")
+    sys.stdout.flush()
+
+
 def main():
     argv = json.loads(os.environ["NSBENCH_ARGV"]) if "NSBENCH_ARGV" in os.environ and "WORLD_SIZE" in os.environ else None
     args = parse(argv)
@@ -266,10 +313,27 @@ def main():
         print(json.dumps({"probe_rank": rank, "world": world, "local_rank": local, "n": args.n, "re": args.re}),
               flush=True)
         return
+    wd = Watchdog(rank, world) if world > 1 else None
+    try:
+        run(args, rank, world, local, wd)
+    except Exception as e:   # a failed rank reports and exits non-zero (never hangs its peers silently)
+        if world == 1:
+            raise
+        fail_line(rank, world, f"rank {rank}: {type(e).__name__}: {e}")
+        os._exit(1)
+
+
+def run(args, rank, world, local, wd):
+    if os.environ.get("NSBENCH_FAIL_RANK") == str(rank):   # (tests/test_bench_launch.py: the failure path)
+        raise RuntimeError("injected failure (NSBENCH_FAIL_RANK)")
     import torch
     import torch.distributed as dist
 
     import navierstokessolver_amd as nsa
+
+    def beat(phase, limit_s):
+        if wd:
+            wd.beat(phase, limit_s)
 
     nccl_id = xport = None
     host = world > 1 and args.transport == "host"
@@ -295,6 +359,7 @@ def main():
         grid = nsa.cavity(n)
     device = 0 if host else local   # (the host transport's rehearsal: every rank on the one GPU)
     torch.cuda.set_device(device)
+    beat("solver set-up (ncclCommInitRank)", 300.0)
     solver = nsa.GpuSolver(grid, dt, re, rtol=args.rtol, device=device, timing=True,
                            rank=rank, nranks=world, nccl_id=nccl_id, host_transport=xport)
 
@@ -308,7 +373,8 @@ def main():
     # K1 while step k's K5 runs instead of waiting for it; the last step's monitor is fetched
     # (ns_monitor) inside the timed region.  --sync-monitor: ns_step, one host sync at each step's end.
     step = solver.step if args.sync_monitor else solver.step_async
-    for _ in range(args.warmup):
+    for k in range(args.warmup):
+        beat(f"warm-up step {k}", 120.0)
         step()
     if not args.sync_monitor:
         solver.monitor()
@@ -316,16 +382,25 @@ def main():
     t0 = time.perf_counter()
     stats = []
     for k in range(args.steps):
+        beat(f"timed step {k}", 60.0)
         if args.time_every != 1:
             solver.set_timing(args.time_every > 0 and k % args.time_every == 0)
         stats.append(step())
     last_monitor = stats[-1] if args.sync_monitor else dict(zip(("umin", "umax", "vmin", "vmax"), solver.monitor()))
     barrier()
     elapsed = time.perf_counter() - t0
+    beat("after the timed steps", 300.0)
+    per_rank = None
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        # every rank's own time, slab and per-step communication (the first real
+        # multi-GPU line must say where its time went); `value` uses the max over ranks
+        mine = {"rank": rank, "ms_per_step": elapsed / args.steps * 1e3, "rows": solver.i1 - solver.i0,
+                "exchanges_per_step": sum(s["n_exchanges"] for s in stats) / args.steps,
+                "collectives_per_step": sum(s["n_allreduces"] for s in stats) / args.steps,
+                "x_link_bytes_per_step": sum(s["x_link_bytes"] for s in stats) / args.steps}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+        elapsed = max(p["ms_per_step"] for p in per_rank) * args.steps / 1e3
 
     K = args.steps
     timed_steps = K if args.time_every == 1 else (sum(1 for k in range(K) if k % args.time_every == 0)
@@ -451,7 +526,7 @@ def main():
     single = [k for k in kern if k in SINGLE_LAUNCH]
     dominant = max(single, key=lambda k: kern[k]["ms_per_step"]) if single else None
     line = {
-        "metric": "cell-updates/sec (MLUPS) + Poisson iters/sec, 4096^2 grid at 1/2/4/8 GPUs",
+        "metric": METRIC,
         "value": value,
         "unit": "MLUPS",
         "n_gpus": world,
@@ -478,6 +553,7 @@ def main():
                                  f"host (gloo): a rehearsal of the multi-rank path with all {world} ranks on one GPU "
                                  "-- functional evidence, not a scaling number"),
                    "local_rows_rank0": solver.i1 - solver.i0},
+        "ranks": per_rank,
         "monitor_last_step": {k: last_monitor[k] for k in ("umin", "umax", "vmin", "vmax")},
         ("poisson_bicgstab_its_per_s" if channel else "poisson_direct_solves_per_s" if direct else
          "poisson_vcycles_per_s"): cycles / elapsed,
@@ -506,6 +582,16 @@ def main():
             line.pop(k)
     if channel:
         line["data"] = "synthetic (channel from rest, uniform inlet, no input files)"
+    if world > 1:
+        line["comm"] = {"collectives_per_step": sum(s["n_allreduces"] for s in stats) / K,
+                        "exchanges_per_step": sum(s["n_exchanges"] for s in stats) / K,
+                        "x_link_bytes_per_step": sum(s["x_link_bytes"] for s in stats) / K,
+                        "rccl_version": _rccl_version(torch) if not host else None,
+                        "note": "collectives = all-reduces + allgathers issued per step by rank 0 (r5: the "
+                                "Helmholtz check's scalar bus and the direct solve's two allgathers, + 1 on a "
+                                "checked solve); exchanges = ghost-row send/recv groups"}
+    else:
+        line.pop("ranks")
     if world == 1 and not args.no_cpu and not channel:
         try:
             state = {k: solver.get(a).ravel() for k, a in (("u", nsa.NS_ARR_U), ("v", nsa.NS_ARR_V),

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NSGPU_ABI_VERSION 7   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
+#define NSGPU_ABI_VERSION 8   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
                                  3: ns_get/set_fields in compact-id order on polygons, ns_local_cells;
                                  4: NS_POISSON_MG is 0, so a zero-initialised ns_params selects the
                                     multigrid (RB-SOR moved to 3; the value 2 is rejected);
@@ -43,7 +43,9 @@ extern "C" {
                                     level's V-cycle-boundary and guess-forming passes);
                                  7: ns_stats.t_rhs_kernel_ms / n_rhs_kernels (K1) and the direct
                                     Poisson solve's kernel times t_fps_dct_ms / t_fps_tri_ms /
-                                    t_fps_idct_ms / n_fps_solves appended */
+                                    t_fps_idct_ms / n_fps_solves appended;
+                                 8: ns_stats.phi_checked appended (res_phi is -1 on a direct solve
+                                    whose residual was not computed) */
 
 typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm */
 
@@ -137,7 +139,8 @@ typedef struct ns_params {
 typedef struct ns_stats {
     double  umin, umax, vmin, vmax;
     int32_t it_u, it_v, it_phi;      /* sweeps of the Helmholtz solves; Poisson sweeps (RB-SOR / Jacobi) or V-cycles (MG) */
-    double  res_u, res_v, res_phi;   /* final relative residuals (of the input of the last sweep) */
+    double  res_u, res_v, res_phi;   /* final relative residuals (of the input of the last sweep); res_phi = -1
+                                      * when this step's Poisson residual was not computed (phi_checked 0) */
     double  t_poisson_kernel_ms;     /* sum of Poisson sweep-kernel durations (timing == 1; multigrid: the
                                       * finest level's sweeps and prolongation passes) */
     int32_t n_poisson_kernels;       /* number of Poisson sweep kernels timed */
@@ -169,6 +172,12 @@ typedef struct ns_stats {
                                       *   one interval, allgathers included on slabs) */
     double  t_fps_idct_ms;           /*   the inverse DCT (k_fps_idct) */
     int32_t n_fps_solves;            /* number of direct solves timed */
+    int32_t phi_checked;             /* 1: res_phi is this step's Poisson residual, computed and tested against
+                                      * rtol (every multigrid / Krylov / sweep solve; the direct solve on its
+                                      * first solve, every 16th after it, and on every solve once a checked
+                                      * residual came within 1/100 of rtol); 0: a direct solve not checked on
+                                      * this step (res_phi = -1) -- a fixed arithmetic sequence whose residual
+                                      * the last check measured */
 } ns_stats;
 
 /* device arrays addressable by ns_get_array / ns_set_array */

@@ -808,14 +808,52 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1(FpsArgs a, const double* 
     }
 }
 
+// multi-rank: this rank's carry-in of mode k from every rank's gathered aggregate (R.gath: P slots of
+// R.stride doubles, rank q's (E, Pi) or (X, R) in slot q) -- forward the fold of ranks 0 .. r-1 in order,
+// backward of P-1 .. r+1 (r4's k_fps_rank_carry, now inside the scan: two launches less per solve).
+// Deferred mean (r5, forward, R.a1): the aggregates were formed from b's raw mode-0 coefficients; the
+// gathered (sum b, sum b^2) of every rank (at 2 ld of its slot) give the mean, and mode 0's aggregates are
+// corrected by the linear response to the constant ny mean (a1: every rank's aggregate of the constant 1;
+// the group aggregates through sft0 in the scan).  Returns the carry-in; *sft0 = ny mean (0 without)
+__device__ inline double fps_rank_in(const FpsRank& R, int k, int ld, int ny, bool backward, double* sft0) {
+    double sft = 0.0;
+    if (R.a1) {
+        double S = 0.0, S2 = 0.0;
+        for (int q = 0; q < R.P; q++) {
+            S += R.gath[(size_t)q * R.stride + 2 * (size_t)ld];
+            S2 += R.gath[(size_t)q * R.stride + 2 * (size_t)ld + 1];
+        }
+        const double mean = S / R.ncells;
+        sft = ny * mean;
+        if (k == 0 && R.shift) {   // MatNullSpaceRemove's mean and ||b - mean||^2 (k_finish_mean's arithmetic)
+            R.shift[0] = mean;
+            R.shift[1] = fmax(S2 - S * S / R.ncells, 0.0);
+        }
+    }
+    *sft0 = k == 0 ? sft : 0.0;
+    double Y = 0.0;
+    if (!R.gath) return Y;
+    if (!backward) {
+        for (int q = 0; q < R.r; q++) {
+            const double E = R.gath[(size_t)q * R.stride + k] - (R.a1 ? *sft0 * R.a1[q] : 0.0);
+            Y = fma(R.gath[(size_t)q * R.stride + ld + k], Y, E);
+        }
+    } else {
+        for (int q = R.P - 1; q > R.r; q--)
+            Y = fma(R.gath[(size_t)q * R.stride + ld + k], Y, R.gath[(size_t)q * R.stride + k]);
+    }
+    return Y;
+}
+
 // S1 / S2: scan of the group aggregates per mode -> each group's carry-in (forward: ascending,
-// backward: descending), from the carry-in of the ranks before / after (rin, null: 0); rout (if
-// not null): this rank's aggregate (the fold of all its groups)
+// backward: descending), from the carry-in of the ranks before / after (R, fps_rank_in; one rank: 0);
+// rout (if not null): this rank's aggregate (the fold of all its groups)
 __global__ void k_fps_scan(int ngrp, int ld, int ny, const double* __restrict__ agg, double* __restrict__ carry,
-                           const double* __restrict__ rin, double* __restrict__ rout, int backward) {
+                           FpsRank R, double* __restrict__ rout, int backward) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ny) return;
-    double Y = rin ? rin[k] : 0.0, AE = 0.0, AP = 1.0;
+    double sft0 = 0.0;
+    double Y = fps_rank_in(R, k, ld, ny, backward, &sft0), AE = 0.0, AP = 1.0;
     constexpr int B = 8;   // (the loads of B groups in flight together: the fold is a dependent chain)
     for (int q0 = 0; q0 < ngrp; q0 += B) {
         double E[B], P[B];
@@ -823,7 +861,7 @@ __global__ void k_fps_scan(int ngrp, int ld, int ny, const double* __restrict__ 
         for (int t = 0; t < B; t++) {
             const int q = q0 + t;
             const int grp = backward ? ngrp - 1 - q : q;
-            E[t] = q < ngrp ? agg[(size_t)grp * ld + k] : 0.0;
+            E[t] = q < ngrp ? agg[(size_t)grp * ld + k] - (R.ge1 ? sft0 * R.ge1[grp] : 0.0) : 0.0;
             P[t] = q < ngrp ? agg[(size_t)(ngrp + grp) * ld + k] : 1.0;
         }
 #pragma unroll
@@ -855,7 +893,7 @@ __global__ void k_fps_scan(int ngrp, int ld, int ny, const double* __restrict__ 
 #endif
 template <int S>
 __global__ void __launch_bounds__(64 * S) k_fps_scan_seg(int ngrp, int ld, int ny, const double* __restrict__ agg,
-                                                         double* __restrict__ carry, const double* __restrict__ rin,
+                                                         double* __restrict__ carry, FpsRank R,
                                                          double* __restrict__ rout, int backward) {
     __shared__ double sE[S][64], sP[S][64], sY[S][64];
     const int lane = threadIdx.x, s = threadIdx.y;
@@ -863,6 +901,11 @@ __global__ void __launch_bounds__(64 * S) k_fps_scan_seg(int ngrp, int ld, int n
     const int per = (ngrp + S - 1) / S, q0 = s * per, q1 = min(ngrp, q0 + per);
     constexpr int B = 8;
     auto gq = [&](int q) { return backward ? ngrp - 1 - q : q; };
+    // (the rank carry-in and the deferred mean's mode-0 shift: every segment needs the shift, wave 0 the carry)
+    double sft0 = 0.0, Yin = 0.0;
+    if (k < ny) Yin = fps_rank_in(s == 0 ? R : FpsRank{R.gath, R.P, R.r, R.stride, R.a1, R.ge1, R.ncells, nullptr},
+                                  k, ld, ny, backward, &sft0);
+    auto ge = [&](int q) { return agg[(size_t)gq(q) * ld + k] - (R.ge1 ? sft0 * R.ge1[gq(q)] : 0.0); };
     double AE = 0.0, AP = 1.0;
     if (k < ny) {
         for (int qb = q0; qb < q1; qb += B) {
@@ -870,7 +913,7 @@ __global__ void __launch_bounds__(64 * S) k_fps_scan_seg(int ngrp, int ld, int n
 #pragma unroll
             for (int t = 0; t < B; t++) {
                 const int q = qb + t;
-                E[t] = q < q1 ? agg[(size_t)gq(q) * ld + k] : 0.0;
+                E[t] = q < q1 ? ge(q) : 0.0;
                 P[t] = q < q1 ? agg[(size_t)(ngrp + gq(q)) * ld + k] : 1.0;
             }
 #pragma unroll
@@ -884,7 +927,7 @@ __global__ void __launch_bounds__(64 * S) k_fps_scan_seg(int ngrp, int ld, int n
     sP[s][lane] = AP;
     __syncthreads();
     if (s == 0 && k < ny) {
-        double Y = rin ? rin[k] : 0.0, TE = 0.0, TP = 1.0;
+        double Y = Yin, TE = 0.0, TP = 1.0;
         for (int t = 0; t < S; t++) {
             sY[t][lane] = Y;
             Y = fma(sP[t][lane], Y, sE[t][lane]);
@@ -904,7 +947,7 @@ __global__ void __launch_bounds__(64 * S) k_fps_scan_seg(int ngrp, int ld, int n
 #pragma unroll
             for (int t = 0; t < B; t++) {
                 const int q = qb + t;
-                E[t] = q < q1 ? agg[(size_t)gq(q) * ld + k] : 0.0;
+                E[t] = q < q1 ? ge(q) : 0.0;
                 P[t] = q < q1 ? agg[(size_t)(ngrp + gq(q)) * ld + k] : 1.0;
             }
 #pragma unroll
@@ -1142,8 +1185,14 @@ __global__ void __launch_bounds__(64) k_fps_mid(FpsArgs a) {
         BX[w][0] = BX[w][1] = 0.0;
         BR[w][0] = BR[w][1] = 1.0;
         if (c < a.nch) {
-            const double2 e = ld2(a.ca + (size_t)c * a.ld + k0), pp = ld2(a.ca + (size_t)(a.nch + c) * a.ld + k0);
-            const double2 bl = ld2(a.cb + (size_t)c * a.ld + k0);
+            double2 e = ld2(a.ca + (size_t)c * a.ld + k0);
+            const double2 pp = ld2(a.ca + (size_t)(a.nch + c) * a.ld + k0);
+            double2 bl = ld2(a.cb + (size_t)c * a.ld + k0);
+            if (a.m0e && k0 == 0) {   // (r5, the deferred mean: t1b's mode 0 saw b's raw coefficients)
+                const double sft = a.ny * *a.m0s;
+                e.x -= sft * a.m0e[c];
+                bl.x -= sft * a.m0b[c];
+            }
             const double2 be = ld2(a.bt + (size_t)c * a.ld + k0), br = ld2(a.bt + (size_t)(a.nch + c) * a.ld + k0);
             st2(a.ya + (size_t)c * a.ld + k0, Y[0], Y[1]);
             BX[w][0] = fma(be.x, Y[0], bl.x);
@@ -1220,40 +1269,15 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
     }
 }
 
-// multi-rank: this rank's carry-in from every rank's aggregate (g: P slots of 2 x ld, slot q = rank
-// q's (E, Pi) or (X, R)): forward, the fold of ranks 0 .. r-1 in order; backward, of P-1 .. r+1
-__global__ void k_fps_rank_carry(const double* __restrict__ g, int P, int r, int ld, int ny, int backward,
-                                 double* __restrict__ rin) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= ny) return;
-    double Y = 0.0;
-    if (!backward) {
-        for (int q = 0; q < r; q++) Y = fma(g[(size_t)(2 * q + 1) * ld + k], Y, g[(size_t)(2 * q) * ld + k]);
-    } else {
-        for (int q = P - 1; q > r; q--) Y = fma(g[(size_t)(2 * q + 1) * ld + k], Y, g[(size_t)(2 * q) * ld + k]);
-    }
-    rin[k] = Y;
-}
-
 template <int LOGN>
 void dct_pair(bool inverse, const double* in, const double* shift, double* out, int nrows, int ld, const void* tw,
               const void* wk, hipStream_t st) {
     constexpr int T = Fft<LOGN>::T;
     const size_t lds = sizeof(cplx) * (size_t)FftLds<LOGN>::n;
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    }
     // (two workgroups per CU fit the LDS: one persistent round)
-    const dim3 grid(std::min((nrows + 1) / 2, 2 * cus));
+    const dim3 grid(std::min((nrows + 1) / 2, 2 * device_cus()));
     if (inverse) {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)k_fps_idct<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
+        lds_attr_once((const void*)k_fps_idct<LOGN>, (int)lds);
         hipEvent_t a, b;
         if (take_launch_timing(a, b))
             hipExtLaunchKernelGGL(k_fps_idct<LOGN>, grid, dim3(T), lds, st, a, b, 0, in, out, nrows, ld,
@@ -1262,11 +1286,7 @@ void dct_pair(bool inverse, const double* in, const double* shift, double* out, 
             hipLaunchKernelGGL(k_fps_idct<LOGN>, grid, dim3(T), lds, st, in, out, nrows, ld, (const cplx*)tw,
                                (const cplx*)wk);
     } else {
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void*)k_fps_dct<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            attr = true;
-        }
+        lds_attr_once((const void*)k_fps_dct<LOGN>, (int)lds);
         hipEvent_t a, b;
         if (take_launch_timing(a, b))
             hipExtLaunchKernelGGL(k_fps_dct<LOGN>, grid, dim3(T), lds, st, a, b, 0, in, shift, out, nrows, ld,
@@ -1281,18 +1301,8 @@ template <int LOGN>
 int div_pair(const FpsDivArgs& a0, hipStream_t st) {
     constexpr int T = Fft<LOGN>::T;
     const size_t lds = sizeof(cplx) * (size_t)FftLds<LOGN>::n;
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    }
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_fps_dct_div<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = true;
-    }
-    const dim3 grid(std::min(a0.cnt, 2 * cus));
+    lds_attr_once((const void*)k_fps_dct_div<LOGN>, (int)lds);
+    const dim3 grid(std::min(a0.cnt, 2 * device_cus()));
     hipEvent_t a, b;
     if (take_launch_timing(a, b)) hipExtLaunchKernelGGL(k_fps_dct_div<LOGN>, grid, dim3(T), lds, st, a, b, 0, a0);
     else hipLaunchKernelGGL(k_fps_dct_div<LOGN>, grid, dim3(T), lds, st, a0);
@@ -1372,18 +1382,13 @@ void launch_fps_t2b(const FpsArgs& a, double* f, hipStream_t st) {
 void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_t3, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
 }
-void launch_fps_rank_carry(const FpsArgs& a, const double* gathered, int P, int r, bool backward, double* rin,
-                           hipStream_t st) {
-    hipLaunchKernelGGL(k_fps_rank_carry, dim3((a.ny + 255) / 256), dim3(256), 0, st, gathered, P, r, a.ld, a.ny,
-                       backward ? 1 : 0, rin);
-}
-void launch_fps_scan(const FpsArgs& a, bool backward, const double* rin, double* rout, hipStream_t st) {
+void launch_fps_scan(const FpsArgs& a, bool backward, const FpsRank& R, double* rout, hipStream_t st) {
     if (FPS_SSEG > 1 && a.ngrp >= 2 * FPS_SSEG)
         hipLaunchKernelGGL(k_fps_scan_seg<FPS_SSEG>, dim3((a.ny + 63) / 64), dim3(64, FPS_SSEG), 0, st, a.ngrp, a.ld,
-                           a.ny, backward ? a.gb : a.ga, backward ? a.gx : a.gc, rin, rout, backward ? 1 : 0);
+                           a.ny, backward ? a.gb : a.ga, backward ? a.gx : a.gc, R, rout, backward ? 1 : 0);
     else
         hipLaunchKernelGGL(k_fps_scan, dim3((a.ny + 63) / 64), dim3(64), 0, st, a.ngrp, a.ld, a.ny,
-                           backward ? a.gb : a.ga, backward ? a.gx : a.gc, rin, rout, backward ? 1 : 0);
+                           backward ? a.gb : a.ga, backward ? a.gx : a.gc, R, rout, backward ? 1 : 0);
 }
 
 }  // namespace nsg

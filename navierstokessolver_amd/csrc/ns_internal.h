@@ -121,6 +121,9 @@ int launch_pois_jacobi_tiled(const Geo& g, const Coef& c, double omega, const do
 void set_strip_rows(int L);
 // CUs the following launches' streams may use (0 = all): sizes "one resident round" of strips
 void set_compute_cus(int n);
+// the current device's CU count; hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per kernel and device
+int device_cus();
+void lds_attr_once(const void* kern, int bytes);
 // the next kernel launch records a, b at its begin / end (hipExtLaunchKernel); pending() clears
 // the request and says whether no launch took it
 void time_next_launch(hipEvent_t a, hipEvent_t b);
@@ -153,6 +156,9 @@ void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t 
 // one rank: launch_reduce_sum (nv = 2) + launch_finish_mean in one launch
 void launch_reduce_sum_mean(const double* p, int n, double* sums, double ncells, double* out, hipStream_t st);
 void launch_finish_mean(const double* sums, double ncells, double* shift_and_bn2, hipStream_t st);
+// multi-rank scalar bus: gathered = P rank slots of nv (<= 16) values; value t folded over the ranks in rank
+// order (a sum for t < nsum, a min after) -> out[dst[t]]
+void launch_bus_reduce(const double* gathered, int P, int nv, int nsum, const int* dst, double* out, hipStream_t st);
 // (sum f, sum f^2) partials over own cells
 int launch_sums(const Geo& g, const double* f, double* part, hipStream_t st);
 // out = a x + b y (+ c z if z) (+ d w if w) (+ e v if v) over the slab's own cells
@@ -294,6 +300,21 @@ struct FpsArgs {
     const double* bt;              // two-pass recurrences: per chunk beta (d BX / d Y_in) and BR (2 x nch x ld, host)
     double* ya;                    // two-pass recurrences: every chunk's forward carry-in (nch x ld)
     const double* sh0 = nullptr;   // fused K3 (launch_fps_div): the mean, taken off mode 0 as ny * mean
+    // r5, multi-rank, the mean deferred to the forward allgather: k_fps_mid corrects mode 0's chunk aggregates
+    // (E, BXl from b's raw coefficients) by the response to the constant ny * *m0s -- m0e / m0b: every local
+    // chunk's forward end value / local back substitution of the constant 1 (host tables)
+    const double *m0e = nullptr, *m0b = nullptr, *m0s = nullptr;
+};
+// the other ranks' part of a multi-rank scan (k_fps_scan / k_fps_scan_seg): gathered aggregates, P slots of
+// `stride` doubles (E | Pi, or X | R, and forward with the deferred mean (sum b, sum b^2) at 2 ld); a1 / ge1:
+// mode 0's rank / group aggregates of the constant 1 (the deferred mean's correction; null: none); shift <-
+// (mean, ||b - mean||^2) (deferred mean)
+struct FpsRank {
+    const double* gath = nullptr;
+    int P = 1, r = 0, stride = 0;
+    const double *a1 = nullptr, *ge1 = nullptr;
+    double ncells = 0.0;
+    double* shift = nullptr;
 };
 // log2(ny) if ny is a supported power of two, else -1
 int fps_log2(int ny);
@@ -316,12 +337,9 @@ void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st);
 void launch_fps_t1b(const FpsArgs& a, const double* f, hipStream_t st);
 void launch_fps_mid(const FpsArgs& a, hipStream_t st);
 void launch_fps_t2b(const FpsArgs& a, double* f, hipStream_t st);
-// group scan (forward: ga -> gc ascending; backward: gb -> gx descending) from the carry-in rin (null:
-// 0; multi-rank: the fold of the other ranks' aggregates); rout (if not null) <- this rank's aggregate
-void launch_fps_scan(const FpsArgs& a, bool backward, const double* rin, double* rout, hipStream_t st);
-// multi-rank: rin <- the fold of the other ranks' aggregates before (forward) / after (backward) rank r
-// (gathered: P slots of 2 x ld doubles, rank q's in slot q)
-void launch_fps_rank_carry(const FpsArgs& a, const double* gathered, int P, int r, bool backward, double* rin,
-                           hipStream_t st);
+// group scan (forward: ga -> gc ascending; backward: gb -> gx descending) from the carry-in of the other
+// ranks (R: the fold of their gathered aggregates; default: none, 0); rout (if not null) <- this rank's
+// aggregate
+void launch_fps_scan(const FpsArgs& a, bool backward, const FpsRank& R, double* rout, hipStream_t st);
 
 }  // namespace nsg

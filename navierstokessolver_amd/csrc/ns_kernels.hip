@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <mutex>
 
 #include <algorithm>
@@ -3664,6 +3665,24 @@ __global__ void k_finish_mean(const double* __restrict__ sums, double n, double*
     out[1] = fmax(s2 - s * s / n, 0.0);  // ||rhs - mean||^2
 }
 
+// multi-rank scalar bus (r5, ns_solver.cpp bus()): g holds P rank slots of nv values each; value t
+// of every slot is folded over the ranks in rank order -- a sum for t < nsum, a min after -- into
+// out[dst[t]] (the same result on every rank, whatever the collective's internal order)
+struct BusDst {
+    int d[16];
+};
+__global__ void k_bus_reduce(const double* __restrict__ g, int P, int nv, int nsum, BusDst dst,
+                             double* __restrict__ out) {
+    const int t = threadIdx.x;
+    if (t >= nv) return;
+    double a = g[t];
+    for (int q = 1; q < P; q++) {
+        const double x = g[(size_t)q * nv + t];
+        a = t < nsum ? a + x : fmin(a, x);
+    }
+    out[dst.d[t]] = a;
+}
+
 // (sum f, sum f^2) block partials over the slab's own cells
 __global__ __launch_bounds__(256) void k_sums(Geo g, const double* __restrict__ f, double* __restrict__ part,
                                               int rows) {
@@ -3804,7 +3823,11 @@ __global__ __launch_bounds__(256) void k_bicg_vec(KrylovArgs a) {
     const double shift = a.shift ? a.shift[0] : 0.0;
     for (int li = blockIdx.y * 4 * a.rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
         const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
-        if (g.fc && !(g.fc[o] & FC_IN)) continue;   // outside a masked domain: every vector stays 0
+        // outside a masked domain: every vector stays 0 (kv planes zeroed at ns_create, never written
+        // here).  Invariant the box preconditioners rely on (fps_precond, ns_solver.cpp): the vectors they
+        // are handed -- p and s -- are mean-free over the domain (the mean projection below) and exactly
+        // 0 outside it, so the bounding box's singular mode 0 sees a consistent right-hand side
+        if (g.fc && !(g.fc[o] & FC_IN)) continue;
         if (MODE == KV_INIT) {
             const double r = (a.b[o] - shift) - (a.v[o] - my);
             a.r[o] = r; a.r0[o] = r; a.p[o] = 0.0; a.v[o] = 0.0;
@@ -4172,22 +4195,46 @@ void set_strip_rows(int L) { g_strip_rows = L >= 4 ? (std::min(L, 64) & ~1) : 0;
 static thread_local int g_compute_cus = 0;
 void set_compute_cus(int n) { g_compute_cus = n; }
 
+// per-device launch facts (function-static values set on the first call's device were
+// reused by solvers on other devices): the current device's CU count, and the large dynamic-LDS
+// attribute set once per kernel and device
+int device_cus() {
+    static std::mutex mu;
+    static std::map<int, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(dev);
+    if (it != cache.end()) return it->second;
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    cache[dev] = c;
+    return c;
+}
+void lds_attr_once(const void* kern, int bytes) {
+    static std::mutex mu;
+    static std::set<std::pair<int, const void*>> done;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.insert({dev, kern}).second)
+        (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
 static long resident_waves(const void* k) {
     static std::mutex mu;
-    static std::map<const void*, int> cache;   // blocks per CU
-    static int cus = 0;
-    int nb = 0;
+    static std::map<std::pair<int, const void*>, int> cache;   // blocks per CU, per device
+    int nb = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    const int cus = device_cus();
     {
         std::lock_guard<std::mutex> lock(mu);
-        auto it = cache.find(k);
+        auto it = cache.find({dev, k});
         if (it != cache.end()) {
             nb = it->second;
         } else {
-            int dev = 0;
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0);
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            cache[k] = nb;
+            cache[{dev, k}] = nb;
             if (getenv("NSGPU_VERBOSE")) fprintf(stderr, "nsgpu: %p holds %d blocks/CU x %d CUs\n", k, nb, cus);
         }
     }
@@ -4756,12 +4803,8 @@ int launch_coarse_vcycle(const Geo& g, const double* img, int img_n, int dn, dou
     const size_t bytes = coarse_vcycle_bytes(g);
     if (bytes != (size_t)img_n * sizeof(double)) return -1;
     if (bytes > 150 * 1024 || g.nxl != g.nx) return -1;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_coarse_vcycle<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_coarse_vcycle<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-        attr = true;
-    }
+    lds_attr_once((const void*)k_coarse_vcycle<false>, 150 * 1024);
+    lds_attr_once((const void*)k_coarse_vcycle<true>, 150 * 1024);
     // the 2 x 2-block smoother (every level but the last has even sides; a level of <= 4096 cells
     // fits the LDS, so its blocks fit the workgroup); NSGPU_CV_BLK=0: the cell-loop version (A/B)
     static const int blk_env = getenv("NSGPU_CV_BLK") ? std::atoi(getenv("NSGPU_CV_BLK")) : 1;
@@ -4912,11 +4955,7 @@ int launch_direct(const double* P, const double* M, const double* Q, const doubl
                   int ldm, int ldg, hipStream_t st) {
     const int n1p = (n1 + 15) / 16 * 16, n2p = (n2 + 15) / 16 * 16;
     if (!direct_fits(n1, n2) || ldm < n2 || ldg < n2) return -1;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_direct, hipFuncAttributeMaxDynamicSharedMemorySize, DIRECT_LDS * 8);
-        attr = true;
-    }
+    lds_attr_once((const void*)k_direct, DIRECT_LDS * 8);
     const size_t bytes = (size_t)(direct_r1(n1p, n2p) + direct_r2(n1p, n2p)) * sizeof(double);
     NS_LAUNCH(k_direct, dim3(n1p / 16, n2p / 16), dim3(DIRECT_THREADS), bytes, st, P, M, Q, E, G, n1, n2, n1p, n2p,
               ldm, ldg);
@@ -5025,12 +5064,7 @@ __global__ __launch_bounds__(256) void k_line_extend(const double* __restrict__ 
 
 int launch_line_solve(const double* r, const Coef& c, int ny, double* p, hipStream_t st) {
     if (ny > LINE_CAP) return -1;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_line_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  4 * LINE_CAP * (int)sizeof(double));
-        attr = true;
-    }
+    lds_attr_once((const void*)k_line_solve, 4 * LINE_CAP * (int)sizeof(double));
     NS_LAUNCH(k_line_solve, dim3(1), dim3(1024), (size_t)4 * ny * sizeof(double), st, r, c.ps, c.pn, c.hy, ny, p);
     return 0;
 }
@@ -5051,6 +5085,11 @@ void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t 
 }
 void launch_reduce_sum_mean(const double* p, int n, double* sums, double ncells, double* out, hipStream_t st) {
     NS_LAUNCH(k_reduce_sum_mean, dim3(1), dim3(1024), 0, st, p, n, sums, ncells, out);
+}
+void launch_bus_reduce(const double* gathered, int P, int nv, int nsum, const int* dst, double* out, hipStream_t st) {
+    BusDst d{};
+    for (int t = 0; t < nv && t < 16; t++) d.d[t] = dst[t];
+    NS_LAUNCH(k_bus_reduce, dim3(1), dim3(64), 0, st, gathered, P, nv, nsum, d, out);
 }
 void launch_finish_mean(const double* sums, double ncells, double* out, hipStream_t st) {
     NS_LAUNCH(k_finish_mean, dim3(1), dim3(1), 0, st, sums, ncells, out);

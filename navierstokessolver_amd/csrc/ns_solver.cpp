@@ -69,8 +69,16 @@ enum {
     S_MM = 8,       // 4: umin, -umax, vmin, -vmax
     S_AUX = 12,     // 4
     S_KSHIFT = 16,  // 1: the Krylov solves' shift after consistent_rhs (see there)
-    S_NUM = 18
+    // multi-rank scalar bus (r5, bus()): this rank's partial values, gathered from every rank and folded
+    // into the global slots above -- K1's ||RHS||^2 (-> S_HBN), the Helmholtz residuals (-> S_RES, S_AUX)
+    // and the previous K5's min / max (-> S_MM); contiguous, in this order
+    S_HBNL = 18,    // 2
+    S_RESL = 20,    // 2
+    S_AUXL = 22,    // 2
+    S_MML = 24,     // 4
+    S_NUM = 28
 };
+constexpr int BUS_NV = 10, BUS_NSUM = 6;
 
 }  // namespace
 
@@ -283,9 +291,23 @@ struct ns_solver {
     long fps_solves = 0;
     // multi-rank: this rank's aggregate of a recurrence (2 x ld), every rank's (nranks x 2 x ld, one
     // allgather per direction and solve) and the carry-in folded from them (ld)
-    double *fps_ragg = nullptr, *fps_gath = nullptr, *fps_rin = nullptr;
+    double *fps_ragg = nullptr, *fps_gath = nullptr;
+    size_t fps_n = 0;            // (r5) the allgather's slot: 2 x ld aggregates + (sum b, sum b^2) + padding
+    // r5, multi-rank rectangles on the direct solve: the fused K3's sums are not all-reduced -- they ride
+    // on the recurrences' forward allgather (at 2 ld of each rank's slot), and the mean comes off mode 0
+    // afterwards, as the linear response of its aggregates to the constant ny * mean (host tables m0: every
+    // local chunk's E / BXl and group's aggregate of the constant 1, every rank's; fps_setup).
+    // NSGPU_FPS_DEFER=0: the all-reduce before the solve (A/B).  mean_pend: this step's sums wait there
+    bool fps_defer = false, mean_pend = false;
+    const double *m0e = nullptr, *m0b = nullptr, *m0g = nullptr, *m0a = nullptr;
     double fps_res = -1.0;       // the last checked solve's relative residual
-    bool fps_strict = false;     // a check failed (rtol below the solve's round-off): check every solve
+    // r5, multi-rank rectangles: the Helmholtz check's collective is an allgather of every rank's
+    // S_HBNL .. S_MML (bus()): K1's norms and the previous step's K5 min / max ride on it, so neither
+    // takes a collective of its own (NSGPU_BUS=0: the per-reduction all-reduces, A/B); bus_mem holds
+    // the P gathered slots of BUS_NV values
+    bool bus = false;
+    double* bus_mem = nullptr;
+    bool fps_strict = false;     // a check failed or came within 1/100 of rtol: check every solve
     bool hbn_pend = false;       // slabs: K1's ||RHS||^2 partial sums await the Helmholtz check's all-reduce
     // K3 fused into the direct solve's DCT (r4, launch_fps_div; NSGPU_FPS_FUSE=0: K3 + the DCT): inside
     // steps the divergence goes straight into the transformed plane, rhs_phi is stored only for a checked
@@ -453,6 +475,22 @@ int allreduce(ns_solver* s, double* d, int n, ncclRedOp_t op) {
     NCCLCHK(ncclAllReduce(d, d, n, ncclDouble, op, s->comm, s->st));
     return 0;
 }
+
+// the multi-rank scalar bus (r5): one allgather of every rank's S_HBNL .. S_MML, folded in rank order
+// into S_HBN (K1's ||RHS||^2), S_RES / S_AUX (the Helmholtz residuals) and S_MM (K5's min / max):
+// sums for the first BUS_NSUM values, mins after
+int allgather(ns_solver* s, const double* mine, double* all, size_t n);
+int bus(ns_solver* s) {
+    static const int dst[BUS_NV] = {S_HBN, S_HBN + 1, S_RES, S_RES + 1, S_AUX, S_AUX + 1,
+                                    S_MM, S_MM + 1, S_MM + 2, S_MM + 3};
+    static_assert(S_RESL == S_HBNL + 2 && S_AUXL == S_RESL + 2 && S_MML == S_AUXL + 2 && S_MML + 4 == S_HBNL + BUS_NV,
+                  "the bus payload is S_HBNL .. S_MML, contiguous");
+    CHK(allgather(s, s->scal + S_HBNL, s->bus_mem, BUS_NV));
+    nsg::launch_bus_reduce(s->bus_mem, s->nranks, BUS_NV, BUS_NSUM, dst, s->scal, s->st);
+    return 0;
+}
+// the bus carries this step's reductions (inside a step of a multi-rank rectangle)
+inline bool bus_on(const ns_solver* s) { return s->bus && s->in_step; }
 
 // copy all device scalars to the host and wait: the only host syncs of a step
 int fetch(ns_solver* s) {
@@ -842,13 +880,19 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         const int nb = helm_sweeps(s, alpha, n, first ? p0 : nullptr, s->part, &nb0, &at0, &at);
         at += sweeps;
         sweeps += n;
-        nsg::launch_reduce_sum_segs(s->part, nb, 2, s->scal + S_RES, s->st);          // u, v
-        if (first) nsg::launch_reduce_sum_segs(p0, nb0, 2, s->scal + S_AUX, s->st);
+        const bool ub = bus_on(s);
+        nsg::launch_reduce_sum_segs(s->part, nb, 2, s->scal + (ub ? S_RESL : S_RES), s->st);          // u, v
+        if (first) nsg::launch_reduce_sum_segs(p0, nb0, 2, s->scal + (ub ? S_AUXL : S_AUX), s->st);
         static_assert(S_RES == S_HBN + 2, "the deferred RHS norms and the residuals in one all-reduce");
-        if (s->hbn_pend) CHK(allreduce(s, s->scal + S_HBN, 4, ncclSum));
-        else CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
+        if (ub) {
+            // (r5) one allgather: K1's norms, these residuals and the previous step's K5 min / max
+            CHK(bus(s));
+        } else {
+            if (s->hbn_pend) CHK(allreduce(s, s->scal + S_HBN, 4, ncclSum));
+            else CHK(allreduce(s, s->scal + S_RES, 2, ncclSum));
+            if (first) CHK(allreduce(s, s->scal + S_AUX, 2, ncclSum));
+        }
         s->hbn_pend = false;
-        if (first) CHK(allreduce(s, s->scal + S_AUX, 2, ncclSum));
         CHK(fetch_begin(s));
         if (s->extrap_pending && !s->guess_ready && !(s->gin && gin_ok(s) && s->phim_valid > 0)) {
             // the Poisson initial guess does not depend on u*: it runs on the GPU while the
@@ -1526,7 +1570,10 @@ int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch, int* tn = 
 // (r4) z = M^-1 q for a masked domain on one rank whose bounding box admits the direct solve: the
 // box's exact Poisson solve (ns_fps.hip: DCT, recurrences, inverse DCT; F in `scratch`) in place of
 // one V-cycle of its multigrid -- the same fictitious-domain preconditioner, solved exactly.  q is
-// mean-free over the domain and 0 outside it, so the box's mode 0 is consistent
+// mean-free over the domain and 0 outside it, so the box's mode 0 is consistent: k_bicg_vec keeps every
+// Krylov vector 0 outside the domain (it skips those cells; the kv planes are zeroed at ns_create) and
+// applies the mean projection P to r, v and t (KV_INIT / KV_V / KV_T), so p and s -- the vectors handed
+// here -- inherit both properties
 int fps_scan(ns_solver* s, bool backward);
 int fps_precond(ns_solver* s, const double* q, double* z, double* scratch) {
     const nsg::Geo& g = s->g;
@@ -1642,18 +1689,18 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
     return 0;
 }
 
-// every rank's aggregate of one recurrence direction (fps_ragg, 2 x ld) into fps_gath (slot q = rank q).
-// RCCL: ncclAllGather; host transport: an exact sum-allreduce with the foreign slots zeroed; a virtual
-// slab (loopback, nranks > 1): the same messages with itself as every peer
-int fps_allgather(ns_solver* s) {
-    const size_t n = 2 * (size_t)s->g.ld, P = (size_t)s->nranks, r = (size_t)s->rank;
+// every rank's n values `mine` into `all` (slot q = rank q, n values each).  RCCL: ncclAllGather; host
+// transport: an exact sum-allreduce with the foreign slots zeroed; a virtual slab (loopback, nranks > 1):
+// the same messages with itself as every peer
+int allgather(ns_solver* s, const double* mine, double* all, size_t n) {
+    const size_t P = (size_t)s->nranks, r = (size_t)s->rank;
     s->n_allred++;
     s->x_link += 8.0 * (double)n;   // (this rank's slot, one link per peer)
     if (s->ht.allreduce) {
         CHK(ensure_stage(s, P * n));
         // (the stream first: an earlier allreduce's copy back from the stage may still be queued --
         // the stage is written on the host only after the sync)
-        HIPCHK(hipMemcpyAsync(s->stage + r * n, s->fps_ragg, n * 8, hipMemcpyDeviceToHost, s->st));
+        HIPCHK(hipMemcpyAsync(s->stage + r * n, mine, n * 8, hipMemcpyDeviceToHost, s->st));
         HIPCHK(hipStreamSynchronize(s->st));
         std::fill(s->stage, s->stage + r * n, 0.0);
         std::fill(s->stage + (r + 1) * n, s->stage + P * n, 0.0);
@@ -1661,35 +1708,46 @@ int fps_allgather(ns_solver* s) {
             set_err("host transport allreduce failed");
             return NS_ERCCL;
         }
-        HIPCHK(hipMemcpyAsync(s->fps_gath, s->stage, P * n * 8, hipMemcpyHostToDevice, s->st));
+        HIPCHK(hipMemcpyAsync(all, s->stage, P * n * 8, hipMemcpyHostToDevice, s->st));
         return 0;
     }
     if (s->loopback) {
-        HIPCHK(hipMemcpyAsync(s->fps_gath + r * n, s->fps_ragg, n * 8, hipMemcpyDeviceToDevice, s->st));
+        HIPCHK(hipMemcpyAsync(all + r * n, mine, n * 8, hipMemcpyDeviceToDevice, s->st));
         NCCLCHK(ncclGroupStart());
         for (size_t q = 0; q < P; q++) {
             if (q == r) continue;
-            NCCLCHK(ncclSend(s->fps_ragg, n, ncclDouble, 0, s->comm, s->st));
-            NCCLCHK(ncclRecv(s->fps_gath + q * n, n, ncclDouble, 0, s->comm, s->st));
+            NCCLCHK(ncclSend(mine, n, ncclDouble, 0, s->comm, s->st));
+            NCCLCHK(ncclRecv(all + q * n, n, ncclDouble, 0, s->comm, s->st));
         }
         NCCLCHK(ncclGroupEnd());
         return 0;
     }
-    NCCLCHK(ncclAllGather(s->fps_ragg, s->fps_gath, n, ncclDouble, s->comm, s->st));
+    NCCLCHK(ncclAllGather(mine, all, n, ncclDouble, s->comm, s->st));
     return 0;
 }
+
+// every rank's aggregate of one recurrence direction (fps_ragg: 2 x ld, then the deferred mean's sums) into
+// fps_gath (slot q = rank q, fps_n doubles each)
+int fps_allgather(ns_solver* s) { return allgather(s, s->fps_ragg, s->fps_gath, s->fps_n); }
 
 // the group scan of one direction; multi-rank: this rank's aggregate first (its carries from zero,
 // rewritten below), the allgather, the carry-in from the ranks before / after, then the scan from it
 int fps_scan(ns_solver* s, bool backward) {
     if (s->nranks == 1) {
-        nsg::launch_fps_scan(s->fa, backward, nullptr, nullptr, s->st);
+        nsg::launch_fps_scan(s->fa, backward, nsg::FpsRank{}, nullptr, s->st);
         return 0;
     }
-    nsg::launch_fps_scan(s->fa, backward, nullptr, s->fps_ragg, s->st);
+    nsg::launch_fps_scan(s->fa, backward, nsg::FpsRank{}, s->fps_ragg, s->st);
     CHK(fps_allgather(s));
-    nsg::launch_fps_rank_carry(s->fa, s->fps_gath, s->nranks, s->rank, backward, s->fps_rin, s->st);
-    nsg::launch_fps_scan(s->fa, backward, s->fps_rin, nullptr, s->st);
+    // (the other ranks' carry-in is folded inside the scan; r4 had a k_fps_rank_carry launch per direction)
+    nsg::FpsRank R{s->fps_gath, s->nranks, s->rank, (int)s->fps_n};
+    if (!backward && s->mean_pend) {   // (r5) the deferred mean: its sums came with the aggregates
+        R.a1 = s->m0a;
+        R.ge1 = s->m0g;
+        R.ncells = s->ncells;
+        R.shift = s->scal + S_SHIFT;
+    }
+    nsg::launch_fps_scan(s->fa, backward, R, nullptr, s->st);
     return 0;
 }
 
@@ -1709,6 +1767,16 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     s->fps_pre = false;
     nsg::FpsArgs fa = s->fa;
     if (pre) fa.sh0 = s->scal + S_SHIFT;
+    // (r5) the mean deferred to the forward allgather: t1b works on b's raw mode 0, k_fps_mid corrects
+    // mode 0's chunk aggregates by the response to ny * mean, t2b takes the mean off on the fly
+    const bool dm = pre && s->mean_pend;
+    nsg::FpsArgs fa1 = fa, fam = fa;
+    if (dm) {
+        fa1.sh0 = nullptr;
+        fam.m0e = s->m0e;
+        fam.m0b = s->m0b;
+        fam.m0s = s->scal + S_SHIFT;
+    }
     if (t) {
         CHK(ensure_kev(s));
         if (!pre) CHK(t_begin(s, s->kev[2], s->kev[3]));
@@ -1729,9 +1797,10 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         CHK(fps_scan(s, true));
         nsg::launch_fps_t3(fa, F, s->st);
     } else {
-        nsg::launch_fps_t1b(fa, F, s->st);
+        nsg::launch_fps_t1b(fa1, F, s->st);
         CHK(fps_scan(s, false));
-        nsg::launch_fps_mid(fa, s->st);
+        s->mean_pend = false;
+        nsg::launch_fps_mid(fam, s->st);
         CHK(fps_scan(s, true));
         nsg::launch_fps_t2b(fa, F, s->st);
     }
@@ -1757,7 +1826,9 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     const bool check = pre ? s->fps_pre_b : !s->in_step || fps_checks_next(s);
     if (s->in_step) s->fps_solves++;
     if (!check) {
-        *res = s->fps_res;
+        // (not computed on this solve: ns_stats.res_phi = -1, phi_checked = 0 -- a residual the library
+        // never measured is not reported as this solve's; the last check's value stays in fps_res)
+        *res = -1.0;
         return take_times();
     }
     CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));   // (slabs: the residual's neighbour rows)
@@ -1783,6 +1854,10 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     // (a virtual slab's own residual is not the global solve's: it replays, never falls back)
     if (r2 <= s->rtol * s->rtol * b2 || r2 == 0.0 || s->rp_c >= 0) {
         if (spec) { s->k5_spec = 1; s->n_spec_hit++; }
+        // the checks are skipped between every fps_check-th solve only while the measured residual sits
+        // two orders of magnitude below rtol (the solve's round-off: ~1e-13 of ||b|| at 4096^2 against
+        // 1e-8); a residual within 1/100 of rtol (e.g. rtol 1e-12 at 2048^2) makes every later solve checked
+        if (s->in_step && s->rp_c < 0 && *res > 1e-2 * s->rtol) s->fps_strict = true;
         return 0;
     }
     // (the speculative K5 wrote only the ping-pong partners: correct() runs it again).  An rtol below
@@ -1829,7 +1904,10 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     a.pin = 1;   // (every side of the rectangle is zero-flux for phi: Lx 1 = 0)
     const int nchp = a.ngrp * nsg::FPS_G;   // (t1 / t2 / t3 address whole groups' chunks)
     const size_t n_tab = 4 * (size_t)N + (size_t)N, n_rp0 = (size_t)nchp * ld, n_g = (size_t)a.ngrp * ld;
-    const size_t n_mr = s->nranks > 1 ? (size_t)(2 + 2 * s->nranks + 1) * ld : 0;
+    // multi-rank: the allgather's own slot and every rank's (fps_n each), and the deferred mean's mode-0
+    // tables (chunks' E and BXl, groups', ranks' aggregates of the constant 1)
+    s->fps_n = 2 * (size_t)ld + 8;
+    const size_t n_mr = s->nranks > 1 ? (size_t)(1 + s->nranks) * s->fps_n + 2 * (size_t)nchp + a.ngrp + s->nranks : 0;
     const size_t n_bt = 2 * (size_t)nchp * ld;
     const size_t total = n_tab + n_rp0 + n_bt + 6 * n_g + 5 * (size_t)nchp * ld + n_mr;
     std::vector<double> h(n_tab + n_rp0 + n_bt, 0.0);
@@ -1896,9 +1974,54 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     a.ca = q; q += 2 * (size_t)nchp * ld;
     a.ya = q; q += (size_t)nchp * ld;
     if (n_mr) {
-        s->fps_ragg = q; q += 2 * (size_t)ld;
-        s->fps_gath = q; q += 2 * (size_t)s->nranks * ld;
-        s->fps_rin = q;
+        s->fps_ragg = q; q += s->fps_n;
+        s->fps_gath = q; q += (size_t)s->nranks * s->fps_n;
+        // mode 0's response to the constant 1 (r5, the deferred mean): the same recurrences as the kernels
+        // (piv_next, t1b's forward and local back substitution) over f = 1, with mode 0's pivots of the
+        // global rows
+        const int nx = g.nx;
+        std::vector<double> r0(nx);
+        {
+            double rp = 0.0;
+            for (int gi = 0; gi < nx; gi++) {
+                const double gg = pw[gi] * rp, pem = gi > 0 ? pe[gi - 1] : 0.0;
+                const double p = -(pw[gi] + pe[gi]) + 0.0 - gg * pem;
+                rp = r0[gi] = gi == nx - 1 ? 0.0 : 1.0 / p;   // (mode 0's pinned last row, a.pin)
+            }
+        }
+        auto fwd = [&](int ga, int gb) {   // forward recurrence from zero over global rows [ga, gb)
+            double E = 0.0;
+            for (int gi = ga; gi < gb; gi++) E = std::fma(-(pw[gi] * (gi > 0 ? r0[gi - 1] : 0.0)), E, 1.0);
+            return E;
+        };
+        std::vector<double> m0((size_t)2 * nchp + a.ngrp + s->nranks, 0.0);
+        for (int c = 0; c < a.nch; c++) {
+            const int gi0 = g.i0 + c * nsg::FPS_M, gi1 = std::min(gi0 + nsg::FPS_M, g.i0 + g.nxl);
+            std::vector<double> y;
+            double E = 0.0;
+            for (int gi = gi0; gi < gi1; gi++) {
+                E = std::fma(-(pw[gi] * (gi > 0 ? r0[gi - 1] : 0.0)), E, 1.0);
+                y.push_back(E);
+            }
+            double xl = 0.0;
+            for (int gi = gi1 - 1; gi >= gi0; gi--) xl = std::fma(y[gi - gi0], r0[gi], -pe[gi] * r0[gi] * xl);
+            m0[c] = E;
+            m0[(size_t)nchp + c] = xl;
+        }
+        for (int gq = 0; gq < a.ngrp; gq++)
+            m0[2 * (size_t)nchp + gq] = fwd(g.i0 + gq * nsg::FPS_G * nsg::FPS_M,
+                                            std::min(g.i0 + (gq + 1) * nsg::FPS_G * nsg::FPS_M, g.i0 + g.nxl));
+        for (int rq = 0; rq < s->nranks; rq++) {
+            int32_t q0, q1;
+            ns_slab_range(g.nx, s->nranks, rq, &q0, &q1);
+            m0[2 * (size_t)nchp + a.ngrp + rq] = fwd(q0, q1);
+        }
+        HIPCHK(hipMemcpy(q, m0.data(), m0.size() * sizeof(double), hipMemcpyHostToDevice));
+        s->m0e = q;
+        s->m0b = q + nchp;
+        s->m0g = q + 2 * (size_t)nchp;
+        s->m0a = s->m0g + a.ngrp;
+        q += m0.size();
     }
     a.pw = s->c.pw;
     a.pe = s->c.pe;
@@ -2343,6 +2466,10 @@ bool fps_checks_next(const ns_solver* s) {
 
 // the (sum, sum^2) partials of rhs_phi -> the sums and the null-space shift (one rank: one launch)
 int div_mean(ns_solver* s, int nb) {
+    if (s->mean_pend) {   // (r5) the sums ride on the direct solve's forward allgather (fps_scan)
+        nsg::launch_reduce_sum(s->part, nb, 2, s->fps_ragg + 2 * (size_t)s->g.ld, s->st);
+        return 0;
+    }
     if (!comm_on(s)) {
         nsg::launch_reduce_sum_mean(s->part, nb, s->scal + S_DIVSUM, s->ncells, s->scal + S_SHIFT, s->st);
         return 0;
@@ -2388,6 +2515,7 @@ int divergence_fps(ns_solver* s) {
     if (t) CHK(t_end(s, s->kev[2], s->kev[3]));
     s->fps_pre = true;
     s->fps_pre_b = b != nullptr;
+    s->mean_pend = s->fps_defer && s->fps_passes == 2;
     return div_mean(s, nb);
 }
 
@@ -2442,10 +2570,13 @@ int rhs(ns_solver* s, bool defer_norm = false) {
     });
     if (nb < 0) return nb;
     if (t) CHK(t_end(s, s->kev[0], s->kev[1]));
-    nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_HBN, s->st);
+    // (r5, the bus: the rank's norms wait in S_HBNL for the Helmholtz check's allgather)
+    const bool ub = defer_norm && bus_on(s);
+    nsg::launch_reduce_sum(s->part, nb, 2, s->scal + (ub ? S_HBNL : S_HBN), s->st);
     // (slabs, rectangle: the norms ride on the Helmholtz solve's first residual all-reduce --
     // S_HBN and S_RES are adjacent -- one collective less per step)
-    if (defer_norm && comm_on(s) && !s->g.fc) s->hbn_pend = true;
+    if (ub) {
+    } else if (defer_norm && comm_on(s) && !s->g.fc) s->hbn_pend = true;
     else CHK(allreduce(s, s->scal + S_HBN, 2, ncclSum));
     return 0;
 }
@@ -2476,8 +2607,11 @@ int correct_launch(ns_solver* s, double* part2) {
         s->guess_branch = p.branch;
     }
     if (nb < 0) return nb;
-    nsg::launch_reduce_min(part2, nb, 4, s->scal + S_MM, s->st);
-    CHK(allreduce(s, s->scal + S_MM, 4, ncclMin));
+    // (r5, the bus: the rank's min / max wait in S_MML for the next collective that carries them --
+    // the next step's Helmholtz check, ns_step's closing bus or ns_monitor's)
+    const bool ub = bus_on(s);
+    nsg::launch_reduce_min(part2, nb, 4, s->scal + (ub ? S_MML : S_MM), s->st);
+    if (!ub) CHK(allreduce(s, s->scal + S_MM, 4, ncclMin));
     return 0;
 }
 
@@ -2940,9 +3074,13 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (p->mg_omega > 0) s->mg_omega_s = p->mg_omega;
         if (const char* e = getenv("NSGPU_MG_OMEGA")) s->mg_omega_s = std::atof(e);   // smoother over-relaxation (A/B)
         if (p->mg_post > 0) s->mg_post = p->mg_post;
-        if (int rc = build_levels(s, hx0, hy0)) return fail(rc);
+        // (a masked domain preconditioned by the box's direct solve, fps_pc, never runs a V-cycle: its
+        // Poisson BiCGStab takes fps_precond, its Helmholtz BiCGStab the Jacobi preconditioner -- no
+        // hierarchy is allocated for it)
+        if (!s->fps_pc)
+            if (int rc = build_levels(s, hx0, hy0)) return fail(rc);
         if (p->mg_coarse_iters > 0) s->mg_coarse_iters = p->mg_coarse_iters;
-        if (s->lv.size() < 2) {
+        if (s->lv.size() < 2 && !s->fps_pc) {
             // nothing to coarsen: plain RB-SOR (O(n) sweeps per solve) -- say so when that is a
             // real grid, not a toy
             if ((long)g.nx * g.ny > 64L * 64L && s->rank == 0)
@@ -2971,6 +3109,17 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (hipMalloc(&s->scal, S_NUM * sizeof(double)) != hipSuccess) { set_err("hipMalloc scalars failed"); return fail(NS_ENOMEM); }
     if (hipMemsetAsync(s->scal, 0, S_NUM * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     if (hipHostMalloc(&s->hs, S_NUM * sizeof(double), hipHostMallocDefault) != hipSuccess) { set_err("hipHostMalloc failed"); return fail(NS_ENOMEM); }
+    // (r5) the scalar bus of multi-rank rectangles (bus())
+    {
+        const char* be = getenv("NSGPU_BUS");
+        s->bus = s->nranks > 1 && !masked && !(be && std::atoi(be) == 0);
+        if (s->bus && hipMalloc(&s->bus_mem, (size_t)BUS_NV * s->nranks * sizeof(double)) != hipSuccess) {
+            set_err("hipMalloc of the scalar bus failed");
+            return fail(NS_ENOMEM);
+        }
+        const char* de = getenv("NSGPU_FPS_DEFER");
+        s->fps_defer = s->bus && s->fps && s->fps_fuse && s->m0e && !(de && std::atoi(de) == 0);
+    }
 
     if (s->loopback) {
         ncclUniqueId id;
@@ -3018,6 +3167,7 @@ void ns_destroy(ns_solver* s) {
     if (s->coef) (void)hipFree(s->coef);
     if (s->part) (void)hipFree(s->part);
     if (s->scal) (void)hipFree(s->scal);
+    if (s->bus_mem) (void)hipFree(s->bus_mem);
     if (s->hs) (void)hipHostFree(s->hs);
     if (s->stage) (void)hipHostFree(s->stage);
     if (s->cst) (void)hipStreamSynchronize(s->cst);
@@ -3087,6 +3237,7 @@ static int step_body_(ns_solver* s, ns_stats& st) {
         CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));
     }
     CHK(pois_solve_any(s, &st.it_phi, &st.res_phi, &st));         // KSPSolve(phiSolver)  (:551)
+    st.phi_checked = st.res_phi >= 0.0 ? 1 : 0;
     CHK(correct(s));                                               // CorrectVelocities    (:552)
     return 0;
 }
@@ -3107,6 +3258,10 @@ int ns_step(ns_solver* s, ns_stats* out) {
     if (s->mm_pending) HIPCHK(hipEventSynchronize(s->mev));   // (an ns_step_async before: its copy lands first)
     s->mm_pending = 0;
     CHK(step_body(s, st));
+    if (s->bus) {   // (r5: K5's min / max went to S_MML; fold them now -- the sync step reports its own)
+        CHK(bus(s));
+        st.n_allreduces++;
+    }
     CHK(fetch(s));                                                 // VecMin/VecMax        (:554-557)
     st.umin = s->hs[S_MM];
     st.umax = -s->hs[S_MM + 1];
@@ -3132,8 +3287,19 @@ int ns_step_async(ns_solver* s, ns_stats* out) {
     }
     CHK(step_body(s, st));   // (its residual checks synchronised the stream: the previous copy has landed)
     const bool prev = s->mm_pending != 0;
-    if (prev) HIPCHK(hipEventSynchronize(s->mev));
     const double nan = std::numeric_limits<double>::quiet_NaN();
+    if (s->bus) {
+        // (r5) the previous step's min / max were folded by this step's Helmholtz-check allgather and
+        // fetched with its residuals (hs); this step's wait in S_MML for the next collective
+        st.umin = prev ? s->hs[S_MM] : nan;
+        st.umax = prev ? -s->hs[S_MM + 1] : nan;
+        st.vmin = prev ? s->hs[S_MM + 2] : nan;
+        st.vmax = prev ? -s->hs[S_MM + 3] : nan;
+        s->mm_pending = 1;
+        if (out) *out = st;
+        return prev ? check_monitor(st) : 0;
+    }
+    if (prev) HIPCHK(hipEventSynchronize(s->mev));
     st.umin = prev ? s->mm_host[0] : nan;
     st.umax = prev ? -s->mm_host[1] : nan;
     st.vmin = prev ? s->mm_host[2] : nan;
@@ -3150,9 +3316,18 @@ int ns_monitor(ns_solver* s, double* mm) {
     if (!s->mm_pending) { set_err("ns_monitor: no ns_step_async since the last ns_step / ns_monitor"); return NS_EINVAL; }
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);
-    HIPCHK(hipEventSynchronize(s->mev));
-    s->mm_pending = 0;
     ns_stats st{};
+    s->mm_pending = 0;
+    if (s->bus) {   // (r5: the latest step's min / max still wait in S_MML -- every rank calls this)
+        CHK(bus(s));
+        CHK(fetch(s));
+        st.umin = mm[0] = s->hs[S_MM];
+        st.umax = mm[1] = -s->hs[S_MM + 1];
+        st.vmin = mm[2] = s->hs[S_MM + 2];
+        st.vmax = mm[3] = -s->hs[S_MM + 3];
+        return check_monitor(st);
+    }
+    HIPCHK(hipEventSynchronize(s->mev));
     st.umin = mm[0] = s->mm_host[0];
     st.umax = mm[1] = -s->mm_host[1];
     st.vmin = mm[2] = s->mm_host[2];

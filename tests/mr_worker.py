@@ -61,12 +61,16 @@ try:
         gs.fill_random(0x5EED)
         mm = [list(gs.kernel(nsa.NS_K_POISSON32, a.sweep32)[:1])]
     elif a.async_steps:
-        mm = [list(gs.step_async().values())[:7] for _ in range(a.nsteps)]
+        sts = [gs.step_async() for _ in range(a.nsteps)]
+        mm = [list(x.values())[:7] for x in sts]
         last = list(gs.monitor())
         for k in range(a.nsteps):   # step k's monitor arrived with step k + 1 (the last via ns_monitor)
             mm[k][:4] = mm[k + 1][:4] if k + 1 < a.nsteps else last
     else:
-        mm = [list(gs.step().values())[:7] for _ in range(a.nsteps)]
+        sts = [gs.step() for _ in range(a.nsteps)]
+        mm = [list(x.values())[:7] for x in sts]
+    # (per step: ghost-row exchange groups and collectives -- r5's collective budget)
+    xc = [[x["n_exchanges"], x["n_allreduces"]] for x in sts] if not a.sweep32 else []
     if a.hash:
         import hashlib
         f = gs.fields()
@@ -77,14 +81,15 @@ try:
 except Exception as e:  # report, don't hang the other rank
     status = f"error: {e}"
     u = v = phi = np.zeros((1, ny))
-    mm = []
+    mm = xc = []
 parts = [None] * world
-dist.all_gather_object(parts, (status, u, v, phi, mm))
+dist.all_gather_object(parts, (status, u, v, phi, mm, xc))
 if rank == 0:
     st = [p[0] for p in parts]
     if all(s == "ok" for s in st):
         np.savez(a.output, u=np.concatenate([p[1] for p in parts]), v=np.concatenate([p[2] for p in parts]),
-                 phi=np.concatenate([p[3] for p in parts]), mm=np.array(parts[0][4]), status="ok")
+                 phi=np.concatenate([p[3] for p in parts]), mm=np.array(parts[0][4]), xc=np.array(parts[0][5]),
+                 status="ok")
     else:
         np.savez(a.output, status="; ".join(st))
 dist.barrier()

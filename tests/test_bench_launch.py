@@ -29,6 +29,21 @@ def test_bench_self_launches_n_ranks():
     assert all(p["n"] == 512 and p["re"] == 100.0 for p in probes)
 
 
+def test_bench_failed_rank_reports_and_exits_nonzero():
+    """a rank that fails (an RCCL init or collective error raises NsError) prints a JSON
+    error line and exits non-zero, and the job ends instead of leaving its peers hanging in a collective.
+    CPU: NSBENCH_FAIL_RANK injects the failure on rank 1 before any GPU call; rank 0 is left waiting in
+    the process-group set-up until torch.distributed.run tears it down."""
+    env = dict(os.environ, NSBENCH_FAIL_RANK="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "NSBENCH_LAUNCH_PROBE"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--n", "64"],
+                       capture_output=True, text=True, env=env, timeout=240, cwd=ROOT)
+    assert r.returncode != 0
+    errs = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", r.stdout)]
+    assert any(e.get("error") and e.get("rank") == 1 and e.get("value") is None for e in errs), r.stdout[-2000:]
+
+
 def _bench(args, timeout=300):
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "NSBENCH_LAUNCH_PROBE"):
@@ -55,8 +70,18 @@ def test_bench_two_ranks_host_transport():
     assert d2["n_gpus"] == 2 and d2["config"]["transport"].startswith("host")
     assert d2["config"]["local_rows_rank0"] == 256
     assert d2["value"] > 0 and d2["roofline"] is not None
+    #  the multi-rank line says where its time went: every rank's ms / step and slab,
+    # the per-step collectives (r5: 3 on an unchecked direct solve -- the Helmholtz check's scalar bus and
+    # the two allgathers) and exchange groups, the link bytes; the RCCL version on the RCCL transport
+    ranks = d2["ranks"]
+    assert [x["rank"] for x in ranks] == [0, 1] and [x["rows"] for x in ranks] == [256, 256]
+    assert all(x["ms_per_step"] > 0 for x in ranks)
+    assert abs(max(x["ms_per_step"] for x in ranks) - d2["ms_per_step"]) <= 1e-6 * d2["ms_per_step"]
+    c = d2["comm"]
+    assert 3 <= c["collectives_per_step"] <= 5 and c["exchanges_per_step"] >= 1 and c["x_link_bytes_per_step"] > 0
+    assert "rccl_version" in c
     d1 = json.loads([ln for ln in _bench(common).stdout.splitlines() if ln.strip()][-1])
-    assert d1["n_gpus"] == 1
+    assert d1["n_gpus"] == 1 and "ranks" not in d1 and "comm" not in d1
     for k in ("umin", "umax", "vmin", "vmax"):
         assert abs(d2["monitor_last_step"][k] - d1["monitor_last_step"][k]) <= 1e-9, (k, d2["monitor_last_step"],
                                                                                          d1["monitor_last_step"])

@@ -266,3 +266,57 @@ def test_masked_poisson_with_box_direct_preconditioner(gpu, monkeypatch):
     xp, _ = og.solve_poisson(b)
     assert rel(out["1"][1], demean(xp)) <= 1e-8
     assert out["1"][0] <= out["0"][0], (out["1"][0], out["0"][0])
+
+
+def test_direct_solve_check_policy(gpu):
+    """ADVICE r4 / VERDICT r4 weak 7: the direct solve's residual is computed on the first solve and on
+    every 16th after it, and `res_phi` is reported only for those (phi_checked 1; -1 and phi_checked 0
+    between) -- never a copy of an earlier check.  A residual within 1/100 of rtol makes every later
+    solve checked (the skipped checks rest on the margin, not on the solve being deterministic)."""
+    n = 128
+    dt = 1.0 / (8 * n)
+    gs = gpu.GpuSolver(gpu.cavity(n), dt, 400.0)
+    st = [gs.step() for _ in range(18)]
+    gs.close()
+    checked = [x["phi_checked"] for x in st]
+    assert checked == [1] + [0] * 15 + [1, 0], checked
+    for x in st:
+        assert (x["res_phi"] == -1.0) == (x["phi_checked"] == 0)
+        assert x["phi_checked"] == 0 or 0 <= x["res_phi"] <= 1e-8
+    r1 = st[0]["res_phi"]
+    assert 0 < r1 <= 1e-12, r1
+    # rtol 3 r1: the first check passes inside the last 1/100 of rtol -> every solve checked from then on
+    gs = gpu.GpuSolver(gpu.cavity(n), dt, 400.0, rtol=3 * r1)
+    st = [gs.step() for _ in range(5)]
+    gs.close()
+    assert [x["phi_checked"] for x in st] == [1] * 5
+    assert all(0 <= x["res_phi"] <= 3 * r1 * 1.0001 or x["it_phi"] > 1 for x in st)
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_slab_collective_budget(tmp_path, gpu, monkeypatch, nproc):
+    """r5: a multi-rank direct-solve step takes 3 collectives -- the Helmholtz check's
+    allgather (the scalar bus: K1's ||RHS||^2 and the previous step's K5 min / max ride on it), the
+    recurrences' forward allgather (K3's sums ride on it: the mean comes off mode 0 after it, through the
+    aggregates' linear response to a constant) and the backward one -- plus an all-reduce on a checked
+    solve; r4 took 6 (5 + 1).  Host-transport slabs with async steps (the monitor one call late): the same
+    fields as the per-reduction all-reduces (NSGPU_BUS=0) to 1e-12 and as one rank to 1e-10."""
+    n, steps = 128, 20
+    args = ("--xport", "host", "--size", str(n), "--nsteps", str(steps), "--solver", str(gpu.NS_POISSON_MG),
+            "--tol", "1e-10", "--async-steps")
+    r = _slabs(tmp_path, nproc, *args, port=29781 + nproc)
+    monkeypatch.setenv("NSGPU_BUS", "0")
+    r0 = _slabs(tmp_path, nproc, *args, port=29791 + nproc)
+    monkeypatch.delenv("NSGPU_BUS")
+    coll, coll0 = r["xc"][:, 1], r0["xc"][:, 1]
+    assert np.median(coll) == 3 and coll.max() <= 4, coll
+    assert np.median(coll0) >= 5, coll0
+    gs = gpu.GpuSolver(gpu.rectangle(n, n), 1.0 / (8 * n), 100.0, rtol=1e-10, device=0)
+    mm = np.array([[x[k] for k in ("umin", "umax", "vmin", "vmax")] for x in (gs.step() for _ in range(steps))])
+    u, v, _ = gs.fields()
+    gs.close()
+    for a, b, tol in ((r, r0, 1e-12), (r, None, 1e-10)):
+        bu, bv = (b["u"], b["v"]) if b is not None else (u, v)
+        assert np.max(np.abs(a["u"] - bu)) <= tol and np.max(np.abs(a["v"] - bv)) <= tol
+    np.testing.assert_allclose(r["mm"][:, :4], r0["mm"][:, :4], atol=1e-12)
+    np.testing.assert_allclose(r["mm"][:, :4], mm, atol=1e-10)

@@ -126,6 +126,18 @@ def test_mask_full_steps_vs_oracle(gpu, name, steps, re, rtol):
     p, q = phi[m] - phi[m].mean(), ref["phi"] - ref["phi"].mean()
     ep = float(np.linalg.norm(p - q) / np.linalg.norm(q))
     assert ep <= tp, ep
+    #  phi's own bar above is loose because the oracle's phi differs by the masked operator's
+    # conditioning; the solve itself is pinned here: the last step's Poisson solve, P A phi = P (b - mean b)
+    # (P the mean projection over the domain), re-evaluated by the oracle's operator -- relative residual
+    # <= rtol (+ 1 % for the host's other rounding).  Uniform grids (a stretched one solves the area-
+    # consistent rhs instead: DESIGN 5)
+    if np.ptp(og.hx) == 0 and np.ptp(og.hy) == 0:
+        b = gs.get(gpu.NS_ARR_RPHI).ravel()[m]
+        bm = b - b.mean()
+        r = bm - og.apply_poisson(phi[m])
+        r -= r.mean()
+        rr = float(np.linalg.norm(r) / np.linalg.norm(bm))
+        assert rr <= 1.01 * rtol + 1e-14, rr
 
 
 def test_mask_rectangle_only_entry_points_fail_loudly(gpu):
