@@ -21,9 +21,9 @@ not a scaling number: `config.transport` says so.
 
 --case channel (not the headline line): the n x n/4
 channel (square cells h = 4/n, inlet W, walls S / N, the reference's NEUMANN outflow E,
-Re 1000, dt = h/8) -- Helmholtz RB-SOR as above, Poisson by BiCGStab on the true outflow
-operator preconditioned by the line-closure V-cycle; `roofline` from the same HIP-event
-timing (the preconditioner's level-0 FUSE_R / FUSE_P passes and the Helmholtz passes).
+Re 1000, dt = h/8) -- Helmholtz RB-SOR as above; Poisson (r5) by the direct solve with the outflow
+row eliminated (one rank, nx even; NSGPU_FPS_OUTFLOW=0 or slabs: BiCGStab on the true outflow operator
+preconditioned by the line-closure V-cycle); `roofline` from the same HIP-event timing.
 """
 from __future__ import annotations
 
@@ -418,8 +418,9 @@ def run(args, rank, world, local, wd):
     for k in ("dct", "tri", "idct"):
         timed["fps_" + k] = (sum(s[f"t_fps_{k}_ms"] for s in stats), sum(s["n_fps_solves"] for s in stats))
     # the direct Poisson solve ran (one solve per step, no V-cycles) -- or, untimed, no restriction pass
+    # (r5: the E-outflow channel takes the direct solve too, with its eliminated outflow row)
     direct = (any(s["n_fps_solves"] for s in stats) or
-              (args.time_every == 0 and all(int(s["it_phi"]) == 1 for s in stats) and not channel))
+              (args.time_every == 0 and all(int(s["it_phi"]) == 1 for s in stats)))
     # finest-level sweeps: V(2,2) per cycle (the convergence check rides on each cycle's last pass)
     fine_sweeps = 4 * cycles
     # whole-step algorithmic bytes per cell: K1 64 + K3 24 + K5 40 + the phi
@@ -457,9 +458,10 @@ def run(args, rank, world, local, wd):
         # checked solves, 8 more there)
         checks = sum(int(s["n_checks"]) for s in stats)
         fps_bpc = KERNELS["fps_dct"][1] + KERNELS["fps_tri"][1] + 16
+        # (the channel's checked residual is the outflow operator's: apply 16 + b - y 24 + sums 8 = 48, vs 16)
         step_bpc = (64 + (0 if FPS_FUSED else 24) + 40 + 2 * 24 * hpasses / K + 96 * band_frac + fps_bpc * cycles / K
-                    + (24 if FPS_FUSED else 16) * checks / K)
-    if channel:
+                    + ((48 if channel else 16) + (8 if FPS_FUSED else 0)) * checks / K)
+    if channel and not direct:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications
         # of (line extension 8 + FUSE_R 28 + FUSE_P 26, x 4/3 for the coarser levels) = 80 each,
         # two operator applications 24 + 16, KV_V 32, KV_T 24, KV_X 64 = 352; start-up (apply +
@@ -539,8 +541,11 @@ def run(args, rank, world, local, wd):
         "dtype": "f64",
         "data": "synthetic (lid-driven cavity from rest, no input files)",
         "config": {"workload": (f"{n}x{nyc} channel (inlet W, NEUMANN outflow E), Re={re:g}, dt=h/8, fp64, "
-                                f"BiCGStab Poisson with the line-closure V-cycle preconditioner + RB-SOR Helmholtz, "
-                                f"both to rtol {args.rtol:g}") if channel else
+                                + ("direct Poisson solve (DCT along y; the outflow row eliminated into tridiagonal "
+                                   "recurrences along x, mode 0 in the projected sense; residual checked on every "
+                                   "16th solve)" if direct else
+                                   "BiCGStab Poisson with the line-closure V-cycle preconditioner")
+                                + f" + RB-SOR Helmholtz, both to rtol {args.rtol:g}") if channel else
                                (f"{n}x{n} lid-driven cavity, Re={re:g}, dt=1/{8 * n}, fp64, "
                                 + ("direct Poisson solve (DCT along y + tridiagonal recurrences along x; residual "
                                    "checked on every 16th solve)" if direct else
@@ -555,9 +560,9 @@ def run(args, rank, world, local, wd):
                    "local_rows_rank0": solver.i1 - solver.i0},
         "ranks": per_rank,
         "monitor_last_step": {k: last_monitor[k] for k in ("umin", "umax", "vmin", "vmax")},
-        ("poisson_bicgstab_its_per_s" if channel else "poisson_direct_solves_per_s" if direct else
+        ("poisson_direct_solves_per_s" if direct else "poisson_bicgstab_its_per_s" if channel else
          "poisson_vcycles_per_s"): cycles / elapsed,
-        ("poisson_bicgstab_its_per_step" if channel else "poisson_direct_solves_per_step" if direct else
+        ("poisson_direct_solves_per_step" if direct else "poisson_bicgstab_its_per_step" if channel else
          "poisson_vcycles_per_step"): cycles / K,
         "poisson_fine_sweeps_per_s": fine_sweeps / elapsed,
         "poisson_fine_sweeps_per_step": fine_sweeps / K,

@@ -246,10 +246,13 @@ __device__ inline void fps_remat(int& t) {
 // a workgroup walks pairs p = blockIdx.x, + gridDim.x, ...; the next pair's rows are loaded into
 // registers while this pair's coefficients are formed and stored (the LDS allows two workgroups
 // per CU, so without that overlap the CU idles through every load)
+// (r5) oe_pair: the row pair whose second row is the NEUMANN outflow row -- it transforms b_{n-1} - b_{n-2} / 2
+// (the elimination of piv_next); -1: none
 template <int LOGN>
 __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double* __restrict__ in, const double* shiftp,
                                                            double* __restrict__ out, int nrows, int ld,
-                                                           const cplx* __restrict__ tw, const cplx* __restrict__ wk) {
+                                                           const cplx* __restrict__ tw, const cplx* __restrict__ wk,
+                                                           int oe_pair) {
     constexpr int N = Fft<LOGN>::N, T = Fft<LOGN>::T;
     constexpr int PT = (N + T - 1) / T;
     extern __shared__ cplx z[];
@@ -282,11 +285,13 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
             const bool two = r0 + 1 < nrows;
             const double* a = in + (size_t)r0 * ld;
             cplx v[16];
+            const double lam = p == oe_pair ? 0.5 : 0.0;
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const int n = tid + r * T;
                 const int j = n < N / 2 ? 2 * n : 2 * (N - 1 - n) + 1;
-                v[r] = cplx{a[j] - sh, two ? a[ld + j] - sh : 0.0};
+                const double xa = a[j] - sh;
+                v[r] = cplx{xa, two ? a[ld + j] - sh - lam * xa : 0.0};
             }
             fft_regs<LOGN>(z, tw, tid, v);
             __syncthreads();   // (every thread has read its last stage's inputs)
@@ -315,12 +320,13 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct(const double
         const int r0 = 2 * p;
         const bool two = r0 + 1 < nrows;
         if (!PREF) load(p);
+        const double lam = p == oe_pair ? 0.5 : 0.0;
 #pragma unroll
         for (int q = 0; q < PT; q++) {
             const int j = tid + q * T;
             if (j < N) {
                 const int n = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
-                z[pz(n)] = cplx{ra[q] - sh, rb[q] - sh};
+                z[pz(n)] = cplx{ra[q] - sh, rb[q] - sh - lam * (ra[q] - sh)};
             }
         }
         __syncthreads();
@@ -376,6 +382,7 @@ struct FpsDivArgs {
     double* part;          // (sum, sum^2) per row pair p at part + 2 p
     int nrows, ld, plo, cnt, pstep;
     const cplx *tw, *wk;
+    int outE;              // (r5) NEUMANN outflow E side: the last row pair's second row transforms b_{n-1} - b_{n-2} / 2
 };
 
 template <int LOGN>
@@ -464,6 +471,10 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
             if (A.b) {
                 st2(A.b + (ptrdiff_t)r0 * ld + j, d[0][0], d[0][1]);
                 if (two) st2(A.b + (ptrdiff_t)(r0 + 1) * ld + j, d[1][0], d[1][1]);
+            }
+            if (A.outE && two && gi + 1 == g.nx - 1) {   // (the outflow row's elimination, piv_next)
+                d[1][0] -= 0.5 * d[0][0];
+                d[1][1] -= 0.5 * d[0][1];
             }
             // v_n = x_2n, v_{N-1-n} = x_{2n+1}
             z[pz(cb)] = cplx{d[0][0], d[1][0]};
@@ -718,10 +729,15 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
 
 // one row of the pivot recurrence: g = pw_i / p_{i-1} (from rprev = 1 / p_{i-1}); returns 1 / p_i
 // (mode 0's pinned last global row: 0).  pw, pe, pem: the row's coefficients pw_i, pe_i, pe_{i-1}
+// (r5) a NEUMANN outflow E side (a.outE, uniform hx): the last row 0.5 x_{n-3} - x_{n-2} + (0.5 + mu h^2) x_{n-1}
+// (AddGhostStencils' 2.5 / -2 / 0.5 ghost, FluidSolver.cpp:98-101, 147-163) minus half the row above it is
+// tridiagonal again: (-mu / 2) x_{n-2} + mu x_{n-1} = f_{n-1} - f_{n-2} / 2 (the transform of that rhs row is
+// formed by k_fps_dct / k_fps_dct_div)
 __device__ inline double piv_next(const FpsArgs& a, int gi, int k, double mu, double rprev, double pw, double pe,
                                   double pem, double& g) {
-    g = pw * rprev;
-    const double p = -(pw + pe) + mu - g * pem;
+    const bool oe = a.outE && gi == a.nx - 1;
+    g = (oe ? -0.5 * mu : pw) * rprev;
+    const double p = (oe ? mu : -(pw + pe) + mu) - g * pem;
     return (a.pin && k == 0 && gi == a.nx - 1) ? 0.0 : 1.0 / p;
 }
 
@@ -729,7 +745,16 @@ __device__ inline double piv_next(const FpsArgs& a, int gi, int k, double mu, do
 // a raw coefficient pair of row li, modes k0, k0 + 1; with the transform fused into K3 (sh0) mode 0
 // takes N mean off here (the DCT of the constant; x - 0.0 is exact for every other mode)
 // (branch-free: a branch per row would keep the chunk's row loads from being issued together)
-__device__ inline double mode0_shift(const FpsArgs& a, int k0) { return a.sh0 && k0 == 0 ? a.ny * *a.sh0 : 0.0; }
+// (r5) with an outflow side mode 0 is solved in the projected sense of the BiCGStab path (P A x = P b: A x =
+// b + C 1 for the C that makes it consistent).  Its eliminated last row is 0 = f'_{n-1} + C / 2, so
+// C = -2 f'_{n-1}, known from the transform alone: every row's mode 0 takes it as this shift (the pinned
+// last row ignores its own).  t1b reads it from the plane f (not yet overwritten), k_fps_mid stores it in
+// *a.s0 for t2b (which overwrites the plane)
+__device__ inline double mode0_shift(const FpsArgs& a, int k0, const double* f = nullptr) {
+    if (k0 != 0) return 0.0;
+    if (a.outE) return f ? 2.0 * f[(size_t)(a.nxl - 1) * a.ld] : *a.s0;
+    return a.sh0 ? a.ny * *a.sh0 : 0.0;
+}
 __device__ inline double2 ldf0(const FpsArgs& a, const double* f, int li, int k0, double s0) {
     double2 x = ld2(f + (size_t)li * a.ld + k0);
     x.x -= s0;
@@ -1118,7 +1143,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1b(FpsArgs a, const double*
     if (rows > 0) {
         const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
         const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
-        const double s0 = mode0_shift(a, k0);
+        const double s0 = mode0_shift(a, k0, f);
         ChunkRows cr;
         cr.load(a, li0, rows);
         double2 yv[FPS_M], rv[FPS_M];
@@ -1172,10 +1197,11 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1b(FpsArgs a, const double*
 
 // every chunk's forward carry-in (ya) and final backward aggregate (cb <- BXl + beta Y_in; BR from bt),
 // and the group's backward aggregate gb; one thread per group and mode pair
-__global__ void __launch_bounds__(64) k_fps_mid(FpsArgs a) {
+__global__ void __launch_bounds__(64) k_fps_mid(FpsArgs a, const double* __restrict__ f) {
     const int k0 = 2 * (blockIdx.x * 64 + threadIdx.x);
     const int grp = blockIdx.y;
     if (k0 >= a.ny) return;
+    if (a.outE && k0 == 0 && grp == 0) *a.s0 = mode0_shift(a, 0, f);   // (t2b overwrites the plane)
     const double2 y0 = ld2(a.gc + (size_t)grp * a.ld + k0);
     double Y[2] = {y0.x, y0.y};
     double BX[FPS_G][2], BR[FPS_G][2];
@@ -1271,7 +1297,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
 
 template <int LOGN>
 void dct_pair(bool inverse, const double* in, const double* shift, double* out, int nrows, int ld, const void* tw,
-              const void* wk, hipStream_t st) {
+              const void* wk, hipStream_t st, int oe_pair) {
     constexpr int T = Fft<LOGN>::T;
     const size_t lds = sizeof(cplx) * (size_t)FftLds<LOGN>::n;
     // (two workgroups per CU fit the LDS: one persistent round)
@@ -1290,10 +1316,10 @@ void dct_pair(bool inverse, const double* in, const double* shift, double* out, 
         hipEvent_t a, b;
         if (take_launch_timing(a, b))
             hipExtLaunchKernelGGL(k_fps_dct<LOGN>, grid, dim3(T), lds, st, a, b, 0, in, shift, out, nrows, ld,
-                                  (const cplx*)tw, (const cplx*)wk);
+                                  (const cplx*)tw, (const cplx*)wk, oe_pair);
         else
             hipLaunchKernelGGL(k_fps_dct<LOGN>, grid, dim3(T), lds, st, in, shift, out, nrows, ld, (const cplx*)tw,
-                               (const cplx*)wk);
+                               (const cplx*)wk, oe_pair);
     }
 }
 
@@ -1318,27 +1344,27 @@ int fps_log2(int ny) {
 }
 
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
-                   const double* tw, const double* wk, hipStream_t st) {
+                   const double* tw, const double* wk, hipStream_t st, int oe_pair) {
     switch (fps_log2(ny)) {
-    case 4: dct_pair<4>(inverse, in, shift, out, nrows, ld, tw, wk, st); break;
-    case 5: dct_pair<5>(inverse, in, shift, out, nrows, ld, tw, wk, st); break;
-    case 6: dct_pair<6>(inverse, in, shift, out, nrows, ld, tw, wk, st); break;
-    case 7: dct_pair<7>(inverse, in, shift, out, nrows, ld, tw, wk, st); break;
-    case 8: dct_pair<8>(inverse, in, shift, out, nrows, ld, tw, wk, st); break;
-    case 9: dct_pair<9>(inverse, in, shift, out, nrows, ld, tw, wk, st); break;
-    case 10: dct_pair<10>(inverse, in, shift, out, nrows, ld, tw, wk, st); break;
-    case 11: dct_pair<11>(inverse, in, shift, out, nrows, ld, tw, wk, st); break;
-    case 12: dct_pair<12>(inverse, in, shift, out, nrows, ld, tw, wk, st); break;
-    case 13: dct_pair<13>(inverse, in, shift, out, nrows, ld, tw, wk, st); break;
+    case 4: dct_pair<4>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;
+    case 5: dct_pair<5>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;
+    case 6: dct_pair<6>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;
+    case 7: dct_pair<7>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;
+    case 8: dct_pair<8>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;
+    case 9: dct_pair<9>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;
+    case 10: dct_pair<10>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;
+    case 11: dct_pair<11>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;
+    case 12: dct_pair<12>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;
+    case 13: dct_pair<13>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;
     default: return -1;
     }
     return 0;
 }
 
 int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* b, double* out,
-                   double* part, int phase, const double* tw, const double* wk, hipStream_t st) {
+                   double* part, int phase, const double* tw, const double* wk, hipStream_t st, int outE) {
     const int np = (g.nxl + 1) / 2;
-    FpsDivArgs a{g, c, 1.0 / dt, u, v, b, out, part, g.nxl, g.ld, 0, np, 1, (const cplx*)tw, (const cplx*)wk};
+    FpsDivArgs a{g, c, 1.0 / dt, u, v, b, out, part, g.nxl, g.ld, 0, np, 1, (const cplx*)tw, (const cplx*)wk, outE};
     if (phase == 1) {
         a.plo = 1;
         a.cnt = std::max(np - 2, 0);
@@ -1373,8 +1399,8 @@ void launch_fps_t2(const FpsArgs& a, double* f, hipStream_t st) {
 void launch_fps_t1b(const FpsArgs& a, const double* f, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_t1b, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
 }
-void launch_fps_mid(const FpsArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_fps_mid, dim3((a.ny + 127) / 128, a.ngrp), dim3(64), 0, st, a);
+void launch_fps_mid(const FpsArgs& a, const double* f, hipStream_t st) {
+    hipLaunchKernelGGL(k_fps_mid, dim3((a.ny + 127) / 128, a.ngrp), dim3(64), 0, st, a, f);
 }
 void launch_fps_t2b(const FpsArgs& a, double* f, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_t2b, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);

@@ -304,6 +304,10 @@ struct FpsArgs {
     // (E, BXl from b's raw coefficients) by the response to the constant ny * *m0s -- m0e / m0b: every local
     // chunk's forward end value / local back substitution of the constant 1 (host tables)
     const double *m0e = nullptr, *m0b = nullptr, *m0s = nullptr;
+    // r5: a NEUMANN outflow E side (one rank, uniform hx, nx even): the last row eliminated into tridiagonal
+    // form (piv_next), mode 0 solved in the projected sense with the shift k_fps_mid keeps in *s0
+    int outE = 0;
+    double* s0 = nullptr;
 };
 // the other ranks' part of a multi-rank scan (k_fps_scan / k_fps_scan_seg): gathered aggregates, P slots of
 // `stride` doubles (E | Pi, or X | R, and forward with the deferred mean (sum b, sum b^2) at 2 ld); a1 / ge1:
@@ -320,22 +324,24 @@ struct FpsRank {
 int fps_log2(int ny);
 // DCT-II of nrows rows of (in - *shift) (shift may be null) -> out, or (inverse) DCT-III of in -> out;
 // tw: ny complex e^{-2 pi i m / ny}, wk: ny complex e^{-i pi k / 2 ny} (interleaved doubles)
+// oe_pair (forward only): the row pair whose second row is a NEUMANN outflow row (transformed as b_{n-1} -
+// b_{n-2} / 2, FpsArgs::outE); -1: none
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
-                   const double* tw, const double* wk, hipStream_t st);
+                   const double* tw, const double* wk, hipStream_t st, int oe_pair = -1);
 // K3 fused into the DCT (k_fps_dct_div): b = Div_V(u*, v*) / dt of the slab's rows -> their DCT-II
 // coefficients in out (of b itself: FpsArgs::sh0 takes the mean off later), b stored too if not null,
 // (sum b, sum b^2) per row pair p at part + 2 p.  phase 0: every row pair; 1: those whose rows need no
 // ghost row of u*; 2: the others (the first and last pair).  Returns the partial count (the pairs), or
 // -1 (ny unsupported)
 int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* b, double* out,
-                   double* part, int phase, const double* tw, const double* wk, hipStream_t st);
+                   double* part, int phase, const double* tw, const double* wk, hipStream_t st, int outE = 0);
 void launch_fps_t1(const FpsArgs& a, const double* f, hipStream_t st);
 void launch_fps_t2(const FpsArgs& a, double* f, hipStream_t st);
 void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st);
 // the two-pass form (ns_fps.hip): t1b (t1 + the local back substitution), mid (carries and final
 // backward aggregates per chunk), t2b (the exact values)
 void launch_fps_t1b(const FpsArgs& a, const double* f, hipStream_t st);
-void launch_fps_mid(const FpsArgs& a, hipStream_t st);
+void launch_fps_mid(const FpsArgs& a, const double* f, hipStream_t st);
 void launch_fps_t2b(const FpsArgs& a, double* f, hipStream_t st);
 // group scan (forward: ga -> gc ascending; backward: gb -> gx descending) from the carry-in of the other
 // ranks (R: the fold of their gathered aggregates; default: none, 0); rout (if not null) <- this rank's

@@ -1583,7 +1583,7 @@ int fps_precond(ns_solver* s, const double* q, double* z, double* scratch) {
     }
     nsg::launch_fps_t1b(s->fa, scratch, s->st);
     CHK(fps_scan(s, false));
-    nsg::launch_fps_mid(s->fa, s->st);
+    nsg::launch_fps_mid(s->fa, scratch, s->st);
     CHK(fps_scan(s, true));
     nsg::launch_fps_t2b(s->fa, scratch, s->st);
     nsg::launch_fps_dct(true, scratch, nullptr, z, g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st);
@@ -1712,14 +1712,10 @@ int allgather(ns_solver* s, const double* mine, double* all, size_t n) {
         return 0;
     }
     if (s->loopback) {
-        HIPCHK(hipMemcpyAsync(all + r * n, mine, n * 8, hipMemcpyDeviceToDevice, s->st));
-        NCCLCHK(ncclGroupStart());
-        for (size_t q = 0; q < P; q++) {
-            if (q == r) continue;
-            NCCLCHK(ncclSend(mine, n, ncclDouble, 0, s->comm, s->st));
-            NCCLCHK(ncclRecv(all + q * n, n, ncclDouble, 0, s->comm, s->st));
-        }
-        NCCLCHK(ncclGroupEnd());
+        // (a virtual slab: the same ONE ncclAllGather launch as the real call, on the 1-rank communicator --
+        // it fills this rank's slot; the others keep their zeros (r4 issued P - 1 self send / recv pairs,
+        // which cost the slab's stream far more than one collective launch does)
+        NCCLCHK(ncclAllGather(mine, all + r * n, n, ncclDouble, s->comm, s->st));
         return 0;
     }
     NCCLCHK(ncclAllGather(mine, all, n, ncclDouble, s->comm, s->st));
@@ -1732,6 +1728,7 @@ int fps_allgather(ns_solver* s) { return allgather(s, s->fps_ragg, s->fps_gath, 
 
 // the group scan of one direction; multi-rank: this rank's aggregate first (its carries from zero,
 // rewritten below), the allgather, the carry-in from the ranks before / after, then the scan from it
+int pois_solve_krylov(ns_solver* s, int* its, double* res, ns_stats* stt);
 int fps_scan(ns_solver* s, bool backward) {
     if (s->nranks == 1) {
         nsg::launch_fps_scan(s->fa, backward, nsg::FpsRank{}, nullptr, s->st);
@@ -1766,7 +1763,10 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     const bool pre = s->fps_pre && s->in_step;
     s->fps_pre = false;
     nsg::FpsArgs fa = s->fa;
-    if (pre) fa.sh0 = s->scal + S_SHIFT;
+    // (r5: with an outflow side the mean never enters -- mode 0 takes the projected shift instead, ns_fps.hip
+    // mode0_shift -- and the outflow row pair is transformed eliminated)
+    const bool oe = s->fa.outE != 0;
+    if (pre && !oe) fa.sh0 = s->scal + S_SHIFT;
     // (r5) the mean deferred to the forward allgather: t1b works on b's raw mode 0, k_fps_mid corrects
     // mode 0's chunk aggregates by the response to ny * mean, t2b takes the mean off on the fly
     const bool dm = pre && s->mean_pend;
@@ -1781,8 +1781,8 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         CHK(ensure_kev(s));
         if (!pre) CHK(t_begin(s, s->kev[2], s->kev[3]));
     }
-    if (!pre && nsg::launch_fps_dct(false, s->arr[NS_ARR_RPHI], s->scal + S_SHIFT, F, g.nxl, g.ny, g.ld, s->fps_tw,
-                                    s->fps_wk, s->st) < 0) {
+    if (!pre && nsg::launch_fps_dct(false, s->arr[NS_ARR_RPHI], oe ? nullptr : s->scal + S_SHIFT, F, g.nxl, g.ny,
+                                    g.ld, s->fps_tw, s->fps_wk, s->st, oe ? g.nxl / 2 - 1 : -1) < 0) {
         set_err("direct Poisson solve: ny = %d is not a supported power of two", g.ny);
         return NS_EINVAL;
     }
@@ -1800,7 +1800,7 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         nsg::launch_fps_t1b(fa1, F, s->st);
         CHK(fps_scan(s, false));
         s->mean_pend = false;
-        nsg::launch_fps_mid(fam, s->st);
+        nsg::launch_fps_mid(fam, F, s->st);
         CHK(fps_scan(s, true));
         nsg::launch_fps_t2b(fa, F, s->st);
     }
@@ -1832,10 +1832,23 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         return take_times();
     }
     CHK(halo(s, {s->arr[NS_ARR_PHI]}, 1));   // (slabs: the residual's neighbour rows)
-    const int nb = nsg::launch_pois_residual(g, s->c, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,
-                                             s->part, s->st);
-    nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
-    CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
+    if (oe) {
+        // (r5) the outflow system's residual in the projected sense of the BiCGStab path: ||P (b - A phi)||
+        // with A the reference's matrix (k_apply: the outflow rows' 2.5 / -2 / 0.5 ghost) and P the mean
+        // projection; into S_RES through (sum r, sum r^2) and k_finish_mean's ||r - mean r||^2 (one rank)
+        double* y = s->kv[0];
+        nsg::launch_apply(0, g, s->c, 0.0, s->arr[NS_ARR_PHI], y, nullptr, s->part, s->st);
+        nsg::launch_axpby(g, 1.0, s->arr[NS_ARR_RPHI], -1.0, y, y, s->st);
+        const int nb = nsg::launch_sums(g, y, s->part, s->st);
+        nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_AUX + 2, s->st);
+        nsg::launch_finish_mean(s->scal + S_AUX + 2, s->ncells, s->scal + S_AUX, s->st);
+        HIPCHK(hipMemcpyAsync(s->scal + S_RES, s->scal + S_AUX + 1, sizeof(double), hipMemcpyDeviceToDevice, s->st));
+    } else {
+        const int nb = nsg::launch_pois_residual(g, s->c, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,
+                                                 s->part, s->st);
+        nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
+        CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
+    }
     const bool spec = s->speculate && s->in_step;
     if (spec) {
         CHK(fetch_begin(s));
@@ -1866,25 +1879,30 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     if (s->in_step) s->fps_strict = true;
     CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));   // (the direct solve read no rhs ghost rows)
     int c = 0;
-    CHK(s->poisson == NS_POISSON_MG ? pois_solve_mg(s, &c, res, stt) : pois_solve(s, &c, res, stt));
+    // (an outflow side: the BiCGStab solve of the true matrix, from this phi)
+    CHK(oe ? pois_solve_krylov(s, &c, res, stt)
+           : s->poisson == NS_POISSON_MG ? pois_solve_mg(s, &c, res, stt) : pois_solve(s, &c, res, stt));
     s->fps_res = *res;
     *its = 1 + c;
     return 0;
 }
 
+int pois_solve_krylov(ns_solver* s, int* its, double* res, ns_stats* stt) {
+    CHK(fetch(s));   // ||b - mean||^2 for the relative test
+    const KrylovSolve ks{0, 0.0, s->krylov_mg, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI],
+                         s->scal + (s->consist ? S_KSHIFT : S_SHIFT), s->hs[S_SHIFT + 1], "poisson", stt};
+    const int rc = bicgstab(s, ks, its, res);
+    if (stt) stt->n_checks += *its + 1;
+    // (last_cycles / cur_cycles -1: the quadratic guess -- the channel's BiCGStab took 5.1
+    // iterations per step with the cubic against 4.75 with the quadratic, r3)
+    s->last_cycles = s->cur_cycles = -1;
+    return rc;
+}
+
 int pois_solve_any(ns_solver* s, int* its, double* res, ns_stats* stt) {
-    if (s->kv[0]) {
-        CHK(fetch(s));   // ||b - mean||^2 for the relative test
-        const KrylovSolve ks{0, 0.0, s->krylov_mg, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI],
-                             s->scal + (s->consist ? S_KSHIFT : S_SHIFT), s->hs[S_SHIFT + 1], "poisson", stt};
-        const int rc = bicgstab(s, ks, its, res);
-        if (stt) stt->n_checks += *its + 1;
-        // (last_cycles / cur_cycles -1: the quadratic guess -- the channel's BiCGStab took 5.1
-        // iterations per step with the cubic against 4.75 with the quadratic, r3)
-        s->last_cycles = s->cur_cycles = -1;
-        return rc;
-    }
+    // (r5: the direct solve first -- it now covers the E-outflow channel, whose Krylov planes exist too)
     if (s->fps) return pois_solve_fps(s, its, res, stt);
+    if (s->kv[0]) return pois_solve_krylov(s, its, res, stt);
     if (s->poisson == NS_POISSON_MG) return pois_solve_mg(s, its, res, stt);
     s->last_cycles = s->cur_cycles = -1;
     return pois_solve(s, its, res, stt);
@@ -1909,7 +1927,7 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     s->fps_n = 2 * (size_t)ld + 8;
     const size_t n_mr = s->nranks > 1 ? (size_t)(1 + s->nranks) * s->fps_n + 2 * (size_t)nchp + a.ngrp + s->nranks : 0;
     const size_t n_bt = 2 * (size_t)nchp * ld;
-    const size_t total = n_tab + n_rp0 + n_bt + 6 * n_g + 5 * (size_t)nchp * ld + n_mr;
+    const size_t total = n_tab + n_rp0 + n_bt + 6 * n_g + 5 * (size_t)nchp * ld + n_mr + 8;
     std::vector<double> h(n_tab + n_rp0 + n_bt, 0.0);
     const double pi = 3.14159265358979323846;
     for (int m = 0; m < N; m++) {
@@ -1933,9 +1951,11 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
             for (int k = 0; k < N; k++) rp0[(size_t)(li / nsg::FPS_M) * ld + k] = r[k];
         const double pem = gi > 0 ? pe[gi - 1] : 0.0;
         const int t = li >= 0 ? li % nsg::FPS_M : 0;
+        // (r5: the NEUMANN outflow row eliminated to (-mu / 2, mu): ns_fps.hip piv_next)
+        const bool oe = a.outE && gi == g.nx - 1;
         for (int k = 0; k < N; k++) {
-            const double gg = pw[gi] * r[k];
-            const double p = -(pw[gi] + pe[gi]) + h[4 * N + k] - gg * pem;
+            const double gg = (oe ? -0.5 * h[4 * N + k] : pw[gi]) * r[k];
+            const double p = (oe ? h[4 * N + k] : -(pw[gi] + pe[gi]) + h[4 * N + k]) - gg * pem;
             r[k] = (k == 0 && gi == g.nx - 1) ? 0.0 : 1.0 / p;
             if (li >= 0) {
                 crp[(size_t)t * N + k] = r[k];
@@ -1973,6 +1993,7 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     a.cb = q; q += 2 * (size_t)nchp * ld;
     a.ca = q; q += 2 * (size_t)nchp * ld;
     a.ya = q; q += (size_t)nchp * ld;
+    a.s0 = d + total - 8;   // (r5: the outflow's mode-0 shift, k_fps_mid -> t2b)
     if (n_mr) {
         s->fps_ragg = q; q += s->fps_n;
         s->fps_gath = q; q += (size_t)s->nranks * s->fps_n;
@@ -2492,7 +2513,7 @@ int divergence_fps(ns_solver* s) {
     double* b = fps_checks_next(s) ? s->arr[NS_ARR_RPHI] : nullptr;
     auto launch = [&](int phase) {
         return nsg::launch_fps_div(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], b, s->arr[NS_ARR_TMP],
-                                   s->part, phase, s->fps_tw, s->fps_wk, s->st);
+                                   s->part, phase, s->fps_tw, s->fps_wk, s->st, s->fa.outE);
     };
     const HaloReq r[2] = {{&s->g, s->arr[NS_ARR_U], 1}, {&s->g, s->arr[NS_ARR_V], 1}};
     int nb;
@@ -2860,6 +2881,16 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     // at 4096^2; 8192^2 with 128 needed 8.5 global sweeps per step, with 256: 4.5 -- 7173 -> 8057
     // MLUPS), at least 32
     s->band_w = std::max(32, std::min(s->g.nx, s->g.ny) / 32);
+    // (r5) the Helmholtz operator loses diagonal dominance as the grid grows (alpha / h^2 = n / (16 Re) at
+    // dt = h / 8: Jacobi radius 0.51 at 4096^2, 0.67 at 8192^2), so the band needs more sweeps there:
+    // 8192^2 with 6 sweeps in 256-wide bands took 4.5 global sweeps per step (4.55 ms), with 9 in 384-wide
+    // bands 3.0 (4.47 ms; 9 in 256: 5.8, 6 in 384 / 512: 4.5; profiles/r05/bands_8192.log)
+    // (16384^2: 12 sweeps in 768-wide bands 3.0 global sweeps, 31.9 ms per step; 9 in 768: 5.0, 34.1 ms;
+    // profiles/r05/bands_16384.log)
+    if (std::min(s->g.nx, s->g.ny) > 4096) {
+        s->band_sweeps = std::min(s->g.nx, s->g.ny) > 8192 ? 12 : 9;
+        s->band_w = 3 * std::min(s->g.nx, s->g.ny) / 64;
+    }
     if (const char* e = getenv("NSGPU_BAND_W")) s->band_w = std::max(1, std::atoi(e));   // A/B: band width
     if (const char* e = getenv("NSGPU_BAND_SWEEPS")) s->band_sweeps = std::max(3, std::atoi(e) / 3 * 3);
     if (const char* e = getenv("NSGPU_SWEEP3_RES")) s->sweep3_res = std::atoi(e) != 0;   // A/B: batches end on pairs
@@ -2915,10 +2946,17 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         for (int j = 1; j < gd->ny; j++) yuni &= gd->hy[j] == gd->hy[0];
         for (int i = 1; i < gd->nx; i++) yuni &= gd->hx[i] == gd->hx[0];
         const char* fe = getenv("NSGPU_FPS");
-        s->fps = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !masked && !outflow && yuni &&
-                 nsg::fps_log2(gd->ny) >= 0;
+        // (r5) or a rectangle whose only NEUMANN side is E, on one rank with nx even (the outflow row is
+        // the second row of the last row pair, the elimination of ns_fps.hip's piv_next): the channel
+        const int nneu_r = masked ? 0 : g.neu[0] + g.neu[1] + g.neu[2] + g.neu[3];
+        const char* foe = getenv("NSGPU_FPS_OUTFLOW");
+        const bool out_ok = nneu_r == 1 && g.neu[1] && p->nranks == 1 && gd->nx % 2 == 0 && gd->nx >= 4 &&
+                            !(foe && std::atoi(foe) == 0);
+        s->fps = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !masked && (!outflow || out_ok) &&
+                 yuni && nsg::fps_log2(gd->ny) >= 0;
+        s->fa.outE = s->fps && outflow ? 1 : 0;
         if (const char* e = getenv("NSGPU_FPS_CHECK")) s->fps_check = std::max(0, std::atoi(e));
-        if (const char* e = getenv("NSGPU_FPS_PASSES")) s->fps_passes = std::atoi(e) == 3 ? 3 : 2;
+        if (const char* e = getenv("NSGPU_FPS_PASSES")) s->fps_passes = std::atoi(e) == 3 && !s->fa.outE ? 3 : 2;
         if (const char* e = getenv("NSGPU_FPS_FUSE")) s->fps_fuse = std::atoi(e) != 0;
         if (s->fps) s->phi_extrap = 0;   // (no initial guess: no history planes)
         const char* fpc = getenv("NSGPU_FPS_PC");
@@ -3113,7 +3151,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     {
         const char* be = getenv("NSGPU_BUS");
         s->bus = s->nranks > 1 && !masked && !(be && std::atoi(be) == 0);
-        if (s->bus && hipMalloc(&s->bus_mem, (size_t)BUS_NV * s->nranks * sizeof(double)) != hipSuccess) {
+        if (s->bus && (hipMalloc(&s->bus_mem, (size_t)BUS_NV * s->nranks * sizeof(double)) != hipSuccess ||
+                       hipMemsetAsync(s->bus_mem, 0, (size_t)BUS_NV * s->nranks * sizeof(double), s->st) != hipSuccess)) {
             set_err("hipMalloc of the scalar bus failed");
             return fail(NS_ENOMEM);
         }

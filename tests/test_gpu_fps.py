@@ -320,3 +320,74 @@ def test_slab_collective_budget(tmp_path, gpu, monkeypatch, nproc):
         assert np.max(np.abs(a["u"] - bu)) <= tol and np.max(np.abs(a["v"] - bv)) <= tol
     np.testing.assert_allclose(r["mm"][:, :4], r0["mm"][:, :4], atol=1e-12)
     np.testing.assert_allclose(r["mm"][:, :4], mm, atol=1e-10)
+
+
+BC_CHANNEL = [(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0)]   # inlet W, walls N / S, NEUMANN outflow E
+
+
+def _channel(gpu, nx, ny, **kw):
+    h = 4.0 / nx
+    return gpu.GpuSolver(gpu.rectangle(nx, ny, lx=4.0, ly=ny * h, bc=BC_CHANNEL), h / 8, 1000.0, **kw)
+
+
+@pytest.mark.parametrize("nx,ny", [(64, 32), (130, 64), (256, 128), (512, 64), (32, 256)])
+def test_outflow_direct_solve_matches_oracle(gpu, nx, ny):
+    """r5: the E-outflow channel's Poisson solve by the direct method -- the outflow row
+    (2.5 / -2 / 0.5 ghost, FluidSolver.cpp:98-101) eliminated into tridiagonal form per mode, mode 0 in
+    the BiCGStab path's projected sense (A x = b + C 1) -- against the oracle's banded-LU solve of the same
+    mean-projected system (phi modulo its mean, <= 1e-10 of max|phi|) and its own projected residual
+    ||P (b - A phi)|| <= 1e-11 ||b - mean b|| (the library's check); re-evaluated by the oracle's operator
+    on the host <= 1e-10 (that evaluation's own round-off, ~||A|| ||phi|| eps, reaches 2e-11 at 512 x 64);
+    one 'iteration'."""
+    rng = np.random.default_rng(nx * 5 + ny)
+    h = 4.0 / nx
+    og = OGrid.rectangle(nx, ny, lx=4.0, ly=ny * h, bc=BC_CHANNEL)
+    gs = _channel(gpu, nx, ny, rtol=1e-11)
+    b = rng.uniform(-100, 100, nx * ny)
+    gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny))
+    gs.set(gpu.NS_ARR_RPHI, b)
+    its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+    assert its == 1 and res <= 1e-11, (its, res)
+    g = demean(gs.get(gpu.NS_ARR_PHI))
+    gs.close()
+    xk, _ = og.solve_poisson(b)
+    assert rel(g, demean(xk)) <= 1e-10, rel(g, demean(xk))
+    r = (b - b.mean()) - og.apply_poisson(g)
+    r -= r.mean()
+    assert np.linalg.norm(r) <= 1e-10 * np.linalg.norm(b - b.mean())
+
+
+def test_outflow_direct_solve_equals_krylov_at_size(gpu, monkeypatch):
+    """The bench's channel grid (4096 x 1024): the direct solve against the GPU's BiCGStab path
+    (NSGPU_FPS_OUTFLOW=0, line-closure V-cycle preconditioner) run to rtol 1e-12 on the same rhs:
+    phi modulo its mean <= 1e-9 of its max."""
+    nx, ny = 4096, 1024
+    b = np.random.default_rng(3).uniform(-1, 1, nx * ny)
+    sol = {}
+    for fo in ("1", "0"):
+        monkeypatch.setenv("NSGPU_FPS_OUTFLOW", fo)
+        gs = _channel(gpu, nx, ny, rtol=1e-12)
+        gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny))
+        gs.set(gpu.NS_ARR_RPHI, b)
+        its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+        assert res <= 1e-12 and ((its == 1) == (fo == "1")), (fo, its, res)
+        sol[fo] = demean(gs.get(gpu.NS_ARR_PHI))
+        gs.close()
+    assert rel(sol["1"], sol["0"]) <= 1e-9, rel(sol["1"], sol["0"])
+
+
+def test_outflow_channel_steps_direct_vs_krylov(gpu, monkeypatch):
+    """Full channel steps (1024 x 256 from rest, 12 steps): the direct solve against the BiCGStab path, both
+    at rtol 1e-10: u, v <= 1e-8 and one Poisson 'iteration' per step."""
+    nx, ny, steps = 1024, 256, 12
+    out = {}
+    for fo in ("1", "0"):
+        monkeypatch.setenv("NSGPU_FPS_OUTFLOW", fo)
+        gs = _channel(gpu, nx, ny, rtol=1e-10)
+        st = [gs.step() for _ in range(steps)]
+        out[fo] = (gs.fields(), st)
+        gs.close()
+    (u1, v1, _), st1 = out["1"]
+    (u0, v0, _), st0 = out["0"]
+    assert all(x["it_phi"] == 1 for x in st1) and all(x["it_phi"] > 1 for x in st0)
+    assert np.max(np.abs(u1 - u0)) <= 1e-8 and np.max(np.abs(v1 - v0)) <= 1e-8
