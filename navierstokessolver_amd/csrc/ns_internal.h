@@ -57,6 +57,9 @@ struct Coef {
     // face interpolation weights of Div_V / GradP (FluidSolver.cpp:389-414, 429-452):
     // r = h_i / (h_nb + h_i) toward the lower (fw, fs) and upper (fe, fn) neighbour, 0 at a wall
     const double *fwx, *fex, *fsy, *fny;
+    // (r5) hy uniform (every hy[j] equal): K1's column tables are then one wave-uniform value each
+    // (k_rhs_s's UY variant keeps them in SGPRs; set by the solver for its finest level only)
+    int yuni = 0;
 };
 
 struct Partials {

@@ -1428,7 +1428,7 @@ __device__ __forceinline__ void rhs_ring_body(const Geo& g, const Coef& c, doubl
 
 constexpr int K1_LMAX = 128;      // k_rhs_s: rows per strip at most (one resident round of strips)
 constexpr int RC_K1 = 4;          // k_rhs_s: row tables from row ib-4 (the window-fill steps read ib-4 .. )
-template <bool NT, int SK>
+template <bool NT, int SK, bool UY = false>
 __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
     const Geo& g = A.g;
     const Coef& c = A.c;
@@ -1463,11 +1463,15 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
         const int c0 = jb - 2 + 2 * lane;
         const int lc = min(max(c0, 0), ld - 2);
         const bool wr = lane >= 1 && lane <= 62 && c0 >= 2 && c0 < A.jhi;
-        // column tables (clamped; a clamped column only feeds unwritten lanes)
+        // column tables (clamped; a clamped column only feeds unwritten lanes).  (r5) UY: hy uniform -- every
+        // column's hy, 1 / hy and 2 / (hy + hy) are one value (the same doubles: written cells never reach
+        // rsy[0] or rsy[ny], the only different entries), kept wave-uniform (SGPRs): 16 VGPRs less, three
+        // waves per SIMD
         const int k0 = min(max(c0, 0), ny - 1), k1 = min(max(c0 + 1, 0), ny - 1), km = min(max(c0 - 1, 0), ny - 1);
-        const double hy0 = c.hy[k0], hy1 = c.hy[k1], hym = c.hy[km];
-        const double ry0 = c.rhy[k0], ry1 = c.rhy[k1];
-        const double rs0 = c.rsy[k0], rs1 = c.rsy[k1], rs2 = c.rsy[min(k1 + 1, ny)];
+        const double hy0 = UY ? c.hy[0] : c.hy[k0], hy1 = UY ? c.hy[0] : c.hy[k1], hym = UY ? c.hy[0] : c.hy[km];
+        const double ry0 = UY ? c.rhy[0] : c.rhy[k0], ry1 = UY ? c.rhy[0] : c.rhy[k1];
+        const double rs0 = UY ? c.rsy[1] : c.rsy[k0], rs1 = UY ? c.rsy[1] : c.rsy[k1],
+                     rs2 = UY ? c.rsy[1] : c.rsy[min(k1 + 1, ny)];
         const double dt = A.dt, hre = 0.5 / A.re;
         const int rlo = -HALO, rhi = g.nxl + HALO - 1;
         const __amdgpu_buffer_rsrc_t bcu = __builtin_amdgcn_make_buffer_rsrc(A.cu, (short)0, 0x7FFFFFF0, 0x00020000);
@@ -1616,6 +1620,11 @@ __global__ __launch_bounds__(256) void k_rhs_s(RhsStreamArgs A) { rhs_s_body<NT,
 template <bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_rhs_s3(RhsStreamArgs A) {
     rhs_s_body<NT, 2>(A);
+}
+// (r5) uniform hy: the column tables in SGPRs -- three waves per SIMD, SK rows in flight
+template <bool NT, int SK>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_rhs_su(RhsStreamArgs A) {
+    rhs_s_body<NT, SK, true>(A);
 }
 
 // the ring of k_rhs_s: the slab's cells within two rows of the W / E walls (whole rows), and on
@@ -4005,7 +4014,13 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         A.nsj = (g.ny + SW - 1) / SW;
         const char* w3 = getenv("NSGPU_K1S");
         const int kv = w3 ? std::atoi(w3) : 0;
-        const void* kk = kv == 3 ? (const void*)k_rhs_s3<true>
+        // (r5) uniform hy: k_rhs_su, the column tables in SGPRs -- 164 VGPRs, three waves per SIMD, no spill
+        // (NSGPU_K1S=32; 33: three rows in flight, spills).  Measured slower (driver form, interleaved:
+        // 243-246 us vs k_rhs_s's 230 us; profiles/r05/k1_waves.log): K1 moves its bytes at ~0.8 of the
+        // measured HBM copy rate already (4 streams read, 4 written), more waves only shorten the strips
+        const bool uy = c.yuni && (kv == 32 || kv == 33);
+        const void* kk = uy ? (kv == 33 ? (const void*)k_rhs_su<true, 3> : (const void*)k_rhs_su<true, 2>)
+                       : kv == 3 ? (const void*)k_rhs_s3<true>
                        : kv == 24 ? (const void*)k_rhs_s<true, 4> : (const void*)k_rhs_s<true, 2>;
         {
             // the fewest rows that keep every strip in ONE resident round (strip_rows caps at 64:

@@ -3075,6 +3075,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (hipMalloc(&s->coef, h.size() * sizeof(double)) != hipSuccess) { set_err("hipMalloc coef failed"); return fail(NS_ENOMEM); }
         if (hipMemcpy(s->coef, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) { set_err("coef upload failed"); return fail(NS_EHIP); }
         s->c = coef_view(s->coef, g.nx, g.ny);
+        s->c.yuni = 1;
+        for (int j = 1; j < g.ny; j++) s->c.yuni &= hy0[j] == hy0[0];
         if (s->fps || s->fps_pc)
             if (int rc = fps_setup(s, hy0, h.data(), h.data() + g.nx)) return fail(rc);
     }
