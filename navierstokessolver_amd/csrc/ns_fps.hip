@@ -745,6 +745,23 @@ __device__ inline double piv_next(const FpsArgs& a, int gi, int k, double mu, do
 // a raw coefficient pair of row li, modes k0, k0 + 1; with the transform fused into K3 (sh0) mode 0
 // takes N mean off here (the DCT of the constant; x - 0.0 is exact for every other mode)
 // (branch-free: a branch per row would keep the chunk's row loads from being issued together)
+// (r5) the pivots of a mode pair's row without the fp64 division chain where they are tabled (FpsArgs::ptab):
+// a wave whose modes all converge (k >= kfast) reads 1 / p of rows < prow from the table and the converged
+// 1 / p after (pinf); the last global row (no east neighbour) and the slow modes keep piv_next
+__device__ inline void piv_pair(const FpsArgs& a, bool fast, double2 pinf, int gi, int k0, const double (&mu)[2],
+                                double (&r)[2], double pw, double pe, double pem, double& g0, double& g1) {
+    if (fast && gi != a.nx - 1) {
+        g0 = pw * r[0];
+        g1 = pw * r[1];
+        const double2 t = gi < a.prow ? ld2(a.ptab + (size_t)gi * a.ld + k0) : pinf;
+        r[0] = t.x;
+        r[1] = t.y;
+    } else {
+        r[0] = piv_next(a, gi, k0, mu[0], r[0], pw, pe, pem, g0);
+        r[1] = piv_next(a, gi, k0 + 1, mu[1], r[1], pw, pe, pem, g1);
+    }
+}
+
 // (r5) with an outflow side mode 0 is solved in the projected sense of the BiCGStab path (P A x = P b: A x =
 // b + C 1 for the C that makes it consistent).  Its eliminated last row is 0 = f'_{n-1} + C / 2, so
 // C = -2 f'_{n-1}, known from the transform alone: every row's mode 0 takes it as this shift (the pinned
@@ -1151,13 +1168,14 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1b(FpsArgs a, const double*
         for (int t = 0; t < FPS_M; t++)
             if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0, s0);
         double r[2] = {r0.x, r0.y};
+        const bool fast = a.ptab && (int)(blockIdx.x * 128) >= a.kfast;
+        const double2 pinf = fast ? ld2(a.pinf + k0) : double2{0.0, 0.0};
 #pragma unroll
         for (int t = 0; t < FPS_M; t++) {
             if (t < rows) {
                 const int gi = a.i0 + li0 + t;
                 double g0, g1;
-                r[0] = piv_next(a, gi, k0, mu[0], r[0], cr.pw[t], cr.pe[t], cr.pem[t], g0);
-                r[1] = piv_next(a, gi, k0 + 1, mu[1], r[1], cr.pw[t], cr.pe[t], cr.pem[t], g1);
+                piv_pair(a, fast, pinf, gi, k0, mu, r, cr.pw[t], cr.pe[t], cr.pem[t], g0, g1);
                 E[0] = fma(-g0, E[0], yv[t].x);
                 E[1] = fma(-g1, E[1], yv[t].y);
                 P[0] = -g0 * P[0];
@@ -1272,13 +1290,14 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
     const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
     double r[2] = {r0.x, r0.y}, y[2] = {yin.x, yin.y};
     double2 rv[FPS_M];
+    const bool fast = a.ptab && (int)(blockIdx.x * 128) >= a.kfast;
+    const double2 pinf = fast ? ld2(a.pinf + k0) : double2{0.0, 0.0};
 #pragma unroll
     for (int t = 0; t < FPS_M; t++) {
         if (t < rows) {
             const int gi = a.i0 + li0 + t;
             double g0, g1;
-            r[0] = piv_next(a, gi, k0, mu[0], r[0], cr.pw[t], cr.pe[t], cr.pem[t], g0);
-            r[1] = piv_next(a, gi, k0 + 1, mu[1], r[1], cr.pw[t], cr.pe[t], cr.pem[t], g1);
+            piv_pair(a, fast, pinf, gi, k0, mu, r, cr.pw[t], cr.pe[t], cr.pem[t], g0, g1);
             y[0] = fma(-g0, y[0], yv[t].x);
             y[1] = fma(-g1, y[1], yv[t].y);
             yv[t] = double2{y[0], y[1]};
@@ -1335,6 +1354,166 @@ int div_pair(const FpsDivArgs& a0, hipStream_t st) {
     return (int)grid.x;
 }
 
+// ---- (r5) N = 16384 (configs[4]'s grid): the row pair's 16384-point FFT does not fit the LDS (256 KiB), so it runs
+// as two 8192-point halves through HBM -- radix-2 decimation in time, Z_k = E_k + W^k O_k and Z_{k+N/2} = E_k -
+// W^k O_k with E = FFT(z_{2m}), O = FFT(z_{2m+1}) -- in two launches per direction: (a) a persistent workgroup
+// per row pair forms both halves' inputs, transforms each in LDS (fft_regs<13>: first / last stage in registers)
+// and writes E and O to a scratch plane (rows 2p, 2p + 1 of the pair's own rows); (b) an elementwise pass combines
+// them and applies the DCT's post- (forward) or output (inverse) step.  8 B/cell more each way than the one-pass
+// transforms of N <= 8192 (NSGPU's ny <= 8192 path, unchanged).
+constexpr int N14 = 1 << 14, NH14 = N14 / 2, TH14 = NH14 / 16;
+
+// forward (a): z_n = (x_a[j(n)], x_b[j(n)]) - shift (Makhoul's reordering j(n) = 2n, n < N/2; 2(N-1-n)+1 after),
+// n = 2m + h -> E (h = 0) / O (h = 1) = FFT_{N/2} -> scratch rows 2p + h (8192 complex = one row of ld doubles);
+// oe_pair as k_fps_dct
+__global__ void __launch_bounds__(TH14) k_fps_dct14a(const double* __restrict__ in, const double* shiftp,
+                                                    double* __restrict__ scr, int nrows, int ld,
+                                                    const cplx* __restrict__ tw8, int oe_pair) {
+    extern __shared__ cplx z[];
+    int tid = threadIdx.x;
+    const int npairs = (nrows + 1) / 2;
+    const double sh = shiftp ? *shiftp : 0.0;
+    for (int p = blockIdx.x; p < npairs; p += gridDim.x) {
+        const int r0 = 2 * p;
+        const bool two = r0 + 1 < nrows;
+        const double* a = in + (size_t)r0 * ld;
+        const double lam = p == oe_pair ? 0.5 : 0.0;
+        for (int h = 0; h < 2; h++) {
+            fps_remat(tid);
+            cplx v[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int n = 2 * (tid + r * TH14) + h;
+                const int j = n < N14 / 2 ? 2 * n : 2 * (N14 - 1 - n) + 1;
+                const double xa = a[j] - sh;
+                v[r] = cplx{xa, two ? a[ld + j] - sh - lam * xa : 0.0};
+            }
+            fft_regs<13>(z, tw8, tid, v);
+            cplx* o = reinterpret_cast<cplx*>(scr + (size_t)(r0 + h) * ld);
+#pragma unroll
+            for (int r = 0; r < 16; r++) o[tid + r * TH14] = v[r];
+            __syncthreads();   // (z is rewritten by the next half)
+        }
+    }
+}
+
+// forward (b): per row pair and q in [0, N/4]: E, O at q and N/2 - q give Z at q, q + N/2, N/2 - q, N - q, and
+// from them the DCT-II coefficients X at the same four indices of both rows (k_fps_dct's post-processing:
+// X_k = Re(e^{-i pi k / 2N} V_k), V_a / V_b from Z_k and Z_{N-k})
+__global__ void __launch_bounds__(256) k_fps_dct14b(const double* __restrict__ scr, double* __restrict__ out, int nrows,
+                                                    int ld, const cplx* __restrict__ tw, const cplx* __restrict__ wk) {
+    const int npairs = (nrows + 1) / 2, nq = NH14 / 2 + 1;
+    for (long t = blockIdx.x * 256L + threadIdx.x; t < (long)npairs * nq; t += (long)gridDim.x * 256) {
+        const int p = (int)(t / nq), q = (int)(t - (long)p * nq);
+        const int r0 = 2 * p;
+        const bool two = r0 + 1 < nrows;
+        const cplx* E = reinterpret_cast<const cplx*>(scr + (size_t)r0 * ld);
+        const cplx* O = reinterpret_cast<const cplx*>(scr + (size_t)(r0 + 1) * ld);
+        const int k2 = NH14 - q;   // (q = 0: E, O are N/2-periodic; W^{N/2} = -1)
+        const cplx e1 = E[q], o1 = cmul(O[q], tw[q]), e2 = E[k2 & (NH14 - 1)], o2 = cmul(O[k2 & (NH14 - 1)], tw[k2]);
+        const cplx Zq = cadd(e1, o1), Zq2 = csub(e1, o1), Zk2 = cadd(e2, o2), Zk22 = csub(e2, o2);
+        // (index: Zq = Z_q, Zq2 = Z_{q + N/2}, Zk2 = Z_{N/2 - q}, Zk22 = Z_{N - q})
+        double* oa = out + (size_t)r0 * ld;
+        double* ob = oa + ld;
+        auto post = [&](int k, cplx Zk, cplx Zn) {
+            const cplx Va{0.5 * (Zk.x + Zn.x), 0.5 * (Zk.y - Zn.y)};
+            const cplx Vb{0.5 * (Zk.y + Zn.y), 0.5 * (Zn.x - Zk.x)};
+            const cplx w = wk[k];
+            oa[k] = fma(w.x, Va.x, -w.y * Va.y);
+            if (two) ob[k] = fma(w.x, Vb.x, -w.y * Vb.y);
+        };
+        post(q, Zq, q ? Zk22 : Zq);
+        if (q) post(N14 - q, Zk22, Zq);
+        post(NH14 + q, Zq2, Zk2);
+        if (q && q != NH14 / 2) post(NH14 - q, Zk2, Zq2);
+        else if (!q) post(NH14, Zk2, Zq2);   // (q = 0: N/2 - q = N/2 itself)
+    }
+}
+
+// inverse (a): y_n = conj(V_n), V_k = e^{i pi k / 2N} (X_k - i X_{N-k}) packed over the two rows (k_fps_idct's
+// input step), n = 2m + h -> FFT_{N/2} -> scratch rows 2p + h
+__global__ void __launch_bounds__(TH14) k_fps_idct14a(const double* __restrict__ in, double* __restrict__ scr,
+                                                     int nrows, int ld, const cplx* __restrict__ tw8,
+                                                     const cplx* __restrict__ wk) {
+    extern __shared__ cplx z[];
+    int tid = threadIdx.x;
+    const int npairs = (nrows + 1) / 2;
+    for (int p = blockIdx.x; p < npairs; p += gridDim.x) {
+        const int r0 = 2 * (FPS_SNAKE ? npairs - 1 - p : p);
+        const bool two = r0 + 1 < nrows;
+        const double* a = in + (size_t)r0 * ld;
+        for (int h = 0; h < 2; h++) {
+            fps_remat(tid);
+            cplx v[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int k = 2 * (tid + r * TH14) + h;
+                const double xa = a[k], xb = two ? a[ld + k] : 0.0;
+                const double ya = k ? a[N14 - k] : 0.0, yb = two && k ? a[ld + N14 - k] : 0.0;
+                const cplx w = wk[k];
+                const double c = w.x, s = -w.y;
+                const cplx Va{fma(c, xa, s * ya), fma(s, xa, -c * ya)};
+                const cplx Vb{fma(c, xb, s * yb), fma(s, xb, -c * yb)};
+                v[r] = cplx{Va.x - Vb.y, -(Va.y + Vb.x)};
+            }
+            fft_regs<13>(z, tw8, tid, v);
+            cplx* o = reinterpret_cast<cplx*>(scr + (size_t)(r0 + h) * ld);
+#pragma unroll
+            for (int r = 0; r < 16; r++) o[tid + r * TH14] = v[r];
+            __syncthreads();
+        }
+    }
+}
+
+// inverse (b): per row pair and n < N/2: Y_n = E_n + W^n O_n and Y_{N-1-n} = E_{N/2-1-n} - W^{N/2-1-n} O_{N/2-1-n}
+// are the values of columns 2n and 2n + 1 (Makhoul's order); x = conj(Y) / N -> both rows, 16-B stores
+__global__ void __launch_bounds__(256) k_fps_idct14b(const double* __restrict__ scr, double* __restrict__ out, int nrows,
+                                                     int ld, const cplx* __restrict__ tw) {
+    const int npairs = (nrows + 1) / 2;
+    const double rn = 1.0 / N14;
+    for (long t = blockIdx.x * 256L + threadIdx.x; t < (long)npairs * NH14; t += (long)gridDim.x * 256) {
+        const int p = (int)(t / NH14), n = (int)(t - (long)p * NH14);
+        const int r0 = 2 * p;
+        const bool two = r0 + 1 < nrows;
+        const cplx* E = reinterpret_cast<const cplx*>(scr + (size_t)r0 * ld);
+        const cplx* O = reinterpret_cast<const cplx*>(scr + (size_t)(r0 + 1) * ld);
+        const int m = NH14 - 1 - n;
+        const cplx Y0 = cadd(E[n], cmul(O[n], tw[n])), Y1 = csub(E[m], cmul(O[m], tw[m]));
+        double* oa = out + (size_t)r0 * ld;
+        st2(oa + 2 * n, Y0.x * rn, Y1.x * rn);
+        if (two) st2(oa + ld + 2 * n, -Y0.y * rn, -Y1.y * rn);
+    }
+}
+
+void dct14(bool inverse, const double* in, const double* shift, double* out, double* scr, int nrows, int ld,
+           const double* tw, const double* tw8, const double* wk, hipStream_t st, int oe_pair) {
+    const size_t lds = sizeof(cplx) * (size_t)FftLds<13>::n;
+    const int cus = device_cus(), npairs = (nrows + 1) / 2;
+    const dim3 ga(std::min(npairs, cus)), gb(std::min((long)npairs * NH14 / 256 + 1, 8L * cus));
+    hipEvent_t a, b;
+    const bool tm = take_launch_timing(a, b);   // (timed: the first launch's begin to the second's end)
+    if (!inverse) {
+        lds_attr_once((const void*)k_fps_dct14a, (int)lds);
+        if (tm) hipExtLaunchKernelGGL(k_fps_dct14a, ga, dim3(TH14), lds, st, a, nullptr, 0, in, shift, scr, nrows, ld,
+                                      (const cplx*)tw8, oe_pair);
+        else hipLaunchKernelGGL(k_fps_dct14a, ga, dim3(TH14), lds, st, in, shift, scr, nrows, ld, (const cplx*)tw8,
+                                oe_pair);
+        if (tm) hipExtLaunchKernelGGL(k_fps_dct14b, gb, dim3(256), 0, st, nullptr, b, 0, scr, out, nrows, ld,
+                                      (const cplx*)tw, (const cplx*)wk);
+        else hipLaunchKernelGGL(k_fps_dct14b, gb, dim3(256), 0, st, scr, out, nrows, ld, (const cplx*)tw,
+                                (const cplx*)wk);
+    } else {
+        lds_attr_once((const void*)k_fps_idct14a, (int)lds);
+        if (tm) hipExtLaunchKernelGGL(k_fps_idct14a, ga, dim3(TH14), lds, st, a, nullptr, 0, in, scr, nrows, ld,
+                                      (const cplx*)tw8, (const cplx*)wk);
+        else hipLaunchKernelGGL(k_fps_idct14a, ga, dim3(TH14), lds, st, in, scr, nrows, ld, (const cplx*)tw8,
+                                (const cplx*)wk);
+        if (tm) hipExtLaunchKernelGGL(k_fps_idct14b, gb, dim3(256), 0, st, nullptr, b, 0, scr, out, nrows, ld,
+                                      (const cplx*)tw);
+        else hipLaunchKernelGGL(k_fps_idct14b, gb, dim3(256), 0, st, scr, out, nrows, ld, (const cplx*)tw);
+    }
+}
+
 }  // namespace
 
 int fps_log2(int ny) {
@@ -1342,9 +1521,15 @@ int fps_log2(int ny) {
     while ((1 << l) < ny) l++;
     return (1 << l) == ny && l >= FPS_LOGN_MIN && l <= FPS_LOGN_MAX ? l : -1;
 }
+int fps_log2x(int ny) { return ny == N14 ? 14 : fps_log2(ny); }
 
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
-                   const double* tw, const double* wk, hipStream_t st, int oe_pair) {
+                   const double* tw, const double* wk, hipStream_t st, int oe_pair, double* scratch, const double* tw8) {
+    if (ny == N14) {   // (r5: two launches through the scratch plane)
+        if (!scratch || !tw8 || ld != N14) return -1;
+        dct14(inverse, in, shift, out, scratch, nrows, ld, tw, tw8, wk, st, oe_pair);
+        return 0;
+    }
     switch (fps_log2(ny)) {
     case 4: dct_pair<4>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;
     case 5: dct_pair<5>(inverse, in, shift, out, nrows, ld, tw, wk, st, oe_pair); break;

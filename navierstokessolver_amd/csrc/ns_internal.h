@@ -40,6 +40,10 @@ struct Geo {
     int neu[4];
     double c0[4], c1[4];
     int enx[4], eny[4];  // outward normal of the edge on that side
+    // (r5) the rows whose values enter a launch's reductions (residual / norm / min-max partials), in
+    // this geometry's local rows: a launch that also computes rows of the neighbours' slabs -- the deep
+    // ghost rows of multi-rank steps (ns_solver.cpp deep_geo) -- sums only its own slab's rows
+    int sr0 = 0, sr1 = 1 << 30;
     // Poisson multigrid levels of the outflow preconditioner: x sides (bit 0: i = -1, bit 1:
     // i = nx) closed by Dirichlet data on the face (weight 2/h^2 toward the ghost, which holds
     // the face value) instead of a wall; prolongation extends the correction there oddly
@@ -69,8 +73,11 @@ struct Partials {
 
 // ---- launchers (all asynchronous on `st`) ----
 // K1: rhs_velocity (ConstructRHS_V); partials (sum ru^2, sum rv^2) per block
+// depth: the rows beyond a strip it reads (2: MUSCL), which the exchange / compute overlap's phases split by
+// (a deep-ghost launch passes its extension + 2: its extension rows wait for the exchange too)
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
-               const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st);
+               const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st,
+               int depth = 2);
 // K2: fused red-black SOR sweep of (I - a L_V) on u and v, (u,v) -> (uo,vo);
 //     residual^2 partials of the input if part != null: u at part[0..n), v at part[n..2n), n returned
 int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
@@ -311,6 +318,11 @@ struct FpsArgs {
     // form (piv_next), mode 0 solved in the projected sense with the shift k_fps_mid keeps in *s0
     int outE = 0;
     double* s0 = nullptr;
+    // r5: the pivots tabled (t1b / t2b without the fp64 division chain): for the modes k >= kfast (a multiple
+    // of 128: whole waves) 1 / p of global rows < prow (ptab, prow x ld) and the converged value (pinf, ld);
+    // ptab null: none
+    const double *ptab = nullptr, *pinf = nullptr;
+    int prow = 0, kfast = 1 << 30;
 };
 // the other ranks' part of a multi-rank scan (k_fps_scan / k_fps_scan_seg): gathered aggregates, P slots of
 // `stride` doubles (E | Pi, or X | R, and forward with the deferred mean (sum b, sum b^2) at 2 ld); a1 / ge1:
@@ -329,8 +341,13 @@ int fps_log2(int ny);
 // tw: ny complex e^{-2 pi i m / ny}, wk: ny complex e^{-i pi k / 2 ny} (interleaved doubles)
 // oe_pair (forward only): the row pair whose second row is a NEUMANN outflow row (transformed as b_{n-1} -
 // b_{n-2} / 2, FpsArgs::outE); -1: none
+// (r5) ny = 16384 (fps_log2x): two launches per direction through `scratch` (a plane of the slab's rows;
+// tw8: the 8192-point twiddles); ny <= 8192: scratch / tw8 unused
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
-                   const double* tw, const double* wk, hipStream_t st, int oe_pair = -1);
+                   const double* tw, const double* wk, hipStream_t st, int oe_pair = -1, double* scratch = nullptr,
+                   const double* tw8 = nullptr);
+// (r5) log2(ny) also for ny = 16384 (the two-half transforms of launch_fps_dct), else as fps_log2
+int fps_log2x(int ny);
 // K3 fused into the DCT (k_fps_dct_div): b = Div_V(u*, v*) / dt of the slab's rows -> their DCT-II
 // coefficients in out (of b itself: FpsArgs::sh0 takes the mean off later), b stored too if not null,
 // (sum b, sum b^2) per row pair p at part + 2 p.  phase 0: every row pair; 1: those whose rows need no

@@ -1420,8 +1420,10 @@ __device__ __forceinline__ void rhs_ring_body(const Geo& g, const Coef& c, doubl
         cv[o] = cvn;
         ru[o] = ru_;
         rv[o] = rv_;
-        acc[0] = ru_ * ru_;
-        acc[1] = rv_ * rv_;
+        if (li >= g.sr0 && li < g.sr1) {   // (r5: own rows only)
+            acc[0] = ru_ * ru_;
+            acc[1] = rv_ * rv_;
+        }
     }
     block_reduce_sum<2>(acc, part + 2 * blk);
 }
@@ -1571,7 +1573,7 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
             }
             const int m = r - 2;
             const bool live = m >= ib && m < ie && m >= A.ilo && m < A.ihi;
-            if (live && wr) {
+            if (live && wr && m >= g.sr0 && m < g.sr1) {   // (r5: a deep-ghost launch sums its own rows only)
                 acc0 += out[2][0] * out[2][0] + out[2][1] * out[2][1];
                 acc1 += out[3][0] * out[3][0] + out[3][1] * out[3][1];
             }
@@ -3992,7 +3994,8 @@ static long resident_waves(const void* k);
 static int strip_rows(int nxl, long nsj, long cap, int lmin, int lmax = 64);
 
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
-               const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st) {
+               const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st,
+               int depth) {
     const char* e = getenv("NSGPU_RHS");   // NSGPU_RHS=global: the global-load K1 (A/B)
     // (the grid kernels cannot split: the interior phase launches nothing, the edge phase all;
     // K1 updates cu / cv in place, so no cell may run twice)
@@ -4027,7 +4030,7 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
             // 4096^2 at 2 waves / SIMD then left 128 of 2176 strips to a second round)
             const long nsi = std::max(1L, resident_waves(kk) / A.nsj);
             const int L = std::min(std::max((int)((g.nxl + nsi - 1) / nsi + 1) & ~1, 8), K1_LMAX);
-            A.nstr = A.nsj * plan_rows(g.nxl, L, 2, &A.P);   // u, v rows ib-2 .. ie+1
+            A.nstr = A.nsj * plan_rows(g.nxl, L, depth, &A.P);   // u, v rows ib-2 .. ie+1
         }
         const bool inner = A.jhi > 2 && A.ihi > A.ilo;
         if (!inner) A.P.nrun = 0;

@@ -286,6 +286,7 @@ struct ns_solver {
     nsg::FpsArgs fa{};
     double* fps_mem = nullptr;
     const double *fps_tw = nullptr, *fps_wk = nullptr;
+    const double* fps_tw8 = nullptr;   // (r5) ny = 16384: the 8192-point halves' twiddles
     int fps_check = 16;
     int fps_passes = 2;          // full passes of the tridiagonal recurrences (NSGPU_FPS_PASSES=3: t1 / t2 / t3)
     long fps_solves = 0;
@@ -307,6 +308,16 @@ struct ns_solver {
     // the P gathered slots of BUS_NV values
     bool bus = false;
     double* bus_mem = nullptr;
+    // r5, multi-rank rectangles on the direct solve: DEEP ghost rows.  K1 computes its rows and deep_e =
+    // 7 + 6 R rows of each neighbour's slab (R: the wall bands' 3-sweep launches), its exchange carrying u,
+    // v, phi that deep; the band launches then compute 6 rows fewer each and need no exchange, and the
+    // residual 3-sweep pass finds its 7-row cone valid -- one exchange group where r4 had 1 + R + 1
+    // (deep_geo; NSGPU_DEEP=0: the r4 exchanges, A/B).  hp: the finest planes' ghost rows per side
+    // (HALO, or deep_e + HALO + 2); cu_ext / u_ext: ghost rows of cu, cv / of u, v (the Helmholtz
+    // iterates) known valid now
+    int hp = nsg::HALO;
+    bool deep = false;
+    int deep_e = 0, cu_ext = 0, u_ext = 0;
     bool fps_strict = false;     // a check failed or came within 1/100 of rtol: check every solve
     bool hbn_pend = false;       // slabs: K1's ||RHS||^2 partial sums await the Helmholtz check's all-reduce
     // K3 fused into the direct solve's DCT (r4, launch_fps_div; NSGPU_FPS_FUSE=0: K3 + the DCT): inside
@@ -457,6 +468,21 @@ int halo_g(ns_solver* s, const nsg::Geo& g, std::initializer_list<double*> field
 }
 
 int halo(ns_solver* s, std::initializer_list<double*> fields, int w) { return halo_g(s, s->g, fields, w); }
+
+// (r5) the geometry of a launch that also computes e rows of each neighbour's slab (none beyond the domain);
+// *elo = the rows added below (pointers into the planes move down by as many rows: shp); reductions keep to
+// the slab's own rows (Geo::sr0 / sr1)
+nsg::Geo deep_geo(const ns_solver* s, int e, int* elo) {
+    nsg::Geo g = s->g;
+    const int lo = std::min(e, g.i0), hi = std::min(e, g.nx - g.i0 - g.nxl);
+    g.i0 -= lo;
+    g.nxl += lo + hi;
+    g.sr0 = lo;
+    g.sr1 = lo + s->g.nxl;
+    *elo = lo;
+    return g;
+}
+inline double* shp(double* p, int elo, int ld) { return p - (ptrdiff_t)elo * ld; }
 
 int allreduce(ns_solver* s, double* d, int n, ncclRedOp_t op) {
     if (!comm_on(s)) return 0;
@@ -675,7 +701,10 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                     }
                     CHK(t_begin(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]));
                 }
-                nb = overlapped(s, r, nr, [&]() {
+                // (r5, deep ghost rows: the wall bands left u, v valid deep enough -- no exchange)
+                const bool valid = s->deep && s->u_ext >= hw;
+                nb = valid ? -1 : 0;
+                auto pass = [&]() {
                     if (w == 3)
                         return nsg::launch_helm_sweep3(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
                                                        s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
@@ -683,7 +712,9 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                     return nsg::launch_helm_sweep2(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
                                                    s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
                                                    s->arr[NS_ARR_RV], part, s->st, 3);
-                });
+                };
+                nb = valid ? pass() : overlapped(s, r, nr, pass);
+                s->u_ext = 0;
                 if (nb < 0) return nb;
                 if (t2) {
                     CHK(t_end(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]));
@@ -744,7 +775,7 @@ int ensure_f32(ns_solver* s) {
         return NS_ENOMEM;
     }
     HIPCHK(hipMemsetAsync(s->f32_mem, 0, 3 * s->plane * sizeof(float), s->st));
-    for (int k = 0; k < 3; k++) s->f32[k] = s->f32_mem + k * s->plane + (size_t)nsg::HALO * s->g.ld;
+    for (int k = 0; k < 3; k++) s->f32[k] = s->f32_mem + k * s->plane + (size_t)s->hp * s->g.ld;
     return 0;
 }
 
@@ -817,6 +848,33 @@ int helm_band(ns_solver* s, double alpha) {
     // a copy-back.  Slabs: each launch after a 6-row exchange of the planes it reads the band from
     double *U = s->arr[NS_ARR_U], *V = s->arr[NS_ARR_V], *TU = s->arr[NS_ARR_TMPU], *TV = s->arr[NS_ARR_TMPV];
     const int rounds = std::max(1, s->band_sweeps / 3);
+    if (s->deep && s->u_ext >= s->deep_e && s->in_step) {
+        // (r5) deep ghost rows: round k computes deep_e - 6 (k + 1) rows of each neighbour's slab from the
+        // rows K1's exchange brought (u, v) and K1 computed (rhs) -- no exchange; the last round leaves
+        // deep_e - 6 R = 7 valid rows for the residual 3-sweep pass
+        const int ld = s->g.ld;
+        double *RU = s->arr[NS_ARR_RU], *RV = s->arr[NS_ARR_RV];
+        int e = s->deep_e;
+        for (int k = 0; k < rounds; k++) {
+            const bool odd = k & 1;
+            e -= 6;
+            int lo = 0;
+            const nsg::Geo gk = deep_geo(s, e, &lo);
+            nsg::launch_helm_band(gk, s->c, alpha, s->omega_v, shp(U, lo, ld), shp(V, lo, ld), shp(odd ? TU : U, lo, ld),
+                                  shp(odd ? TV : V, lo, ld), shp(odd ? U : TU, lo, ld), shp(odd ? V : TV, lo, ld),
+                                  shp(RU, lo, ld), shp(RV, lo, ld), s->band_w, 0, s->st);
+        }
+        if (rounds & 1) {
+            int lo = 0;
+            const nsg::Geo gk = deep_geo(s, e, &lo);
+            nsg::launch_helm_band(gk, s->c, alpha, s->omega_v, shp(U, lo, ld), shp(V, lo, ld), shp(TU, lo, ld),
+                                  shp(TV, lo, ld), shp(U, lo, ld), shp(V, lo, ld), shp(RU, lo, ld), shp(RV, lo, ld),
+                                  s->band_w, 1, s->st);
+        }
+        s->u_ext = e;
+        s->helm_b_pend = 0;
+        return 0;
+    }
     for (int k = 0; k < rounds; k++) {
         const bool odd = k & 1;
         auto launch = [&]() {
@@ -1544,7 +1602,7 @@ int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch, int* tn = 
         nsg::launch_line_extend(s->lrow, s->g, z - (ptrdiff_t)nsg::HALO * ld, s->g.nxl + 2 * nsg::HALO,
                                 mine ? scratch + ghost * ld : nullptr, s->st);
     } else {
-        HIPCHK(hipMemsetAsync(z - (ptrdiff_t)nsg::HALO * s->g.ld, 0, s->plane * sizeof(double), s->st));
+        HIPCHK(hipMemsetAsync(z - (ptrdiff_t)s->hp * s->g.ld, 0, s->plane * sizeof(double), s->st));
     }
     CHK(halo(s, {q}, 5));
     s->arr[NS_ARR_PHI] = z;
@@ -1781,8 +1839,12 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         CHK(ensure_kev(s));
         if (!pre) CHK(t_begin(s, s->kev[2], s->kev[3]));
     }
+    // (r5) ny = 16384: the transforms run as two 8192-point halves through a scratch plane -- TMPU, the
+    // Helmholtz sweeps' ping-pong partner, free between the Helmholtz solves and K5 (which writes it whole)
+    double* scr = s->arr[NS_ARR_TMPU];
     if (!pre && nsg::launch_fps_dct(false, s->arr[NS_ARR_RPHI], oe ? nullptr : s->scal + S_SHIFT, F, g.nxl, g.ny,
-                                    g.ld, s->fps_tw, s->fps_wk, s->st, oe ? g.nxl / 2 - 1 : -1) < 0) {
+                                    g.ld, s->fps_tw, s->fps_wk, s->st, oe ? g.nxl / 2 - 1 : -1, scr,
+                                    s->fps_tw8) < 0) {
         set_err("direct Poisson solve: ny = %d is not a supported power of two", g.ny);
         return NS_EINVAL;
     }
@@ -1808,7 +1870,8 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         HIPCHK(hipEventRecord(s->kev[5], s->st));
         CHK(t_begin(s, s->kev[6], s->kev[7]));
     }
-    nsg::launch_fps_dct(true, F, nullptr, s->arr[NS_ARR_PHI], g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st);
+    nsg::launch_fps_dct(true, F, nullptr, s->arr[NS_ARR_PHI], g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st, -1,
+                        scr, s->fps_tw8);
     if (t) CHK(t_end(s, s->kev[6], s->kev[7]));
     auto take_times = [&]() -> int {
         if (!t || !stt) return 0;
@@ -1976,9 +2039,79 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
             }
         }
     }
-    HIPCHK(hipMalloc(&s->fps_mem, total * sizeof(double)));
-    HIPCHK(hipMemset(s->fps_mem, 0, total * sizeof(double)));
+    // (r5) the pivots tabled for t1b / t2b (ns_fps.hip piv_pair): the recurrence of every mode from global row
+    // 0 over uniform interior rows reaches its fixed point (to 4 ulp) after c_k rows -- many for the low modes,
+    // few for the high ones; whole waves of modes k >= kfast whose c_k are all below prow read 1 / p from
+    // the table there and the converged value after it, instead of one fp64 division per row and mode
+    // (NSGPU_FPS_PTAB=0: divisions everywhere, A/B)
+    std::vector<double> ptab, pinf;
+    int prow = 0, kfast = 1 << 30;
+    {
+        const char* pe_env = getenv("NSGPU_FPS_PTAB");
+        const int PRMAX = std::min(g.nx - 1, 1024);
+        if (!(pe_env && std::atoi(pe_env) == 0) && N > 128 && PRMAX > 64) {
+            std::vector<double> rr(N, 0.0);
+            std::vector<int> conv(N, -1);
+            ptab.assign((size_t)PRMAX * ld, 0.0);
+            for (int gi = 0; gi < PRMAX; gi++) {
+                const double pem = gi > 0 ? pe[gi - 1] : 0.0;
+                for (int k = 0; k < N; k++) {
+                    const double gg = pw[gi] * rr[k];
+                    const double pv = -(pw[gi] + pe[gi]) + h[4 * N + k] - gg * pem;
+                    const double rn = 1.0 / pv;
+                    if (conv[k] < 0 && gi > 1 && std::fabs(rn - rr[k]) <= 4 * 2.220446049250313e-16 * std::fabs(rn))
+                        conv[k] = gi;
+                    rr[k] = rn;
+                    ptab[(size_t)gi * ld + k] = rn;
+                }
+            }
+            for (int kf = 128; kf < N; kf += 128) {
+                int mx = 0;
+                bool ok = true;
+                for (int k = kf; k < N && ok; k++) {
+                    ok = conv[k] >= 0;
+                    mx = std::max(mx, conv[k]);
+                }
+                if (ok) {
+                    kfast = kf;
+                    prow = std::min(PRMAX, (mx + 1 + 15) / 16 * 16);
+                    break;
+                }
+            }
+            if (kfast < N) {
+                pinf.assign(ld, 0.0);
+                for (int k = 0; k < N; k++) pinf[k] = rr[k];
+                ptab.resize((size_t)prow * ld);
+            } else {
+                ptab.clear();
+                kfast = 1 << 30;
+            }
+        }
+    }
+    const size_t n_pt = ptab.empty() ? 0 : ptab.size() + (size_t)ld;
+    // (r5) ny = 16384: e^{-2 pi i m / 8192}, m < 8192, after the pivot table (the two-half transforms)
+    const size_t n_t8 = nsg::fps_log2(N) < 0 ? (size_t)N : 0;
+    HIPCHK(hipMalloc(&s->fps_mem, (total + n_pt + n_t8) * sizeof(double)));
+    HIPCHK(hipMemset(s->fps_mem, 0, (total + n_pt + n_t8) * sizeof(double)));
     HIPCHK(hipMemcpy(s->fps_mem, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (n_t8) {
+        std::vector<double> t8(n_t8);
+        for (int m = 0; m < N / 2; m++) {
+            t8[2 * m] = h[4 * m];   // (the 16384-point table's even entries)
+            t8[2 * m + 1] = h[4 * m + 1];
+        }
+        s->fps_tw8 = s->fps_mem + total + n_pt;
+        HIPCHK(hipMemcpy(s->fps_mem + total + n_pt, t8.data(), n_t8 * sizeof(double), hipMemcpyHostToDevice));
+    }
+    if (n_pt) {
+        double* pt = s->fps_mem + total;
+        HIPCHK(hipMemcpy(pt, ptab.data(), ptab.size() * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(pt + ptab.size(), pinf.data(), (size_t)ld * sizeof(double), hipMemcpyHostToDevice));
+        a.ptab = pt;
+        a.pinf = pt + ptab.size();
+        a.prow = prow;
+        a.kfast = kfast;
+    }
     double* d = s->fps_mem;
     s->fps_tw = d;
     s->fps_wk = d + 2 * (size_t)N;
@@ -2396,7 +2529,7 @@ ExtrapPlan extrap_plan(const ns_solver* s, int cycles) {
 
 int extrapolate_phi(ns_solver* s) {
     if (!s->phim) return 0;
-    const size_t back = (size_t)nsg::HALO * s->g.ld;
+    const size_t back = (size_t)s->hp * s->g.ld;
     if (s->phim_valid == 0) {
         HIPCHK(hipMemcpyAsync(s->phim - back, s->arr[NS_ARR_PHI] - back, s->plane * sizeof(double),
                               hipMemcpyDeviceToDevice, s->st));
@@ -2578,17 +2711,40 @@ int helm_bnorm(ns_solver* s) {
 // K1 with its ghost rows (u, v width 2: MUSCL; phi width 1: grad phi^{n-1} on walls) in one
 // exchange group, overlapped with the interior tiles
 int rhs(ns_solver* s, bool defer_norm = false) {
-    const HaloReq r[3] = {{&s->g, s->arr[NS_ARR_U], 2}, {&s->g, s->arr[NS_ARR_V], 2}, {&s->g, s->arr[NS_ARR_PHI], 1}};
     const bool t = s->timing && s->in_step;
     if (t) {
         CHK(ensure_kev(s));
         CHK(t_begin(s, s->kev[0], s->kev[1]));
     }
-    const int nb = overlapped(s, r, 3, [&]() {
-        return nsg::launch_rhs(s->g, s->c, s->dt, s->re, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_PHI],
-                               s->arr[NS_ARR_CU], s->arr[NS_ARR_CV], s->arr[NS_ARR_RU], s->arr[NS_ARR_RV], s->part,
-                               s->st);
-    });
+    int nb;
+    if (s->deep && s->in_step) {
+        // (r5) deep ghost rows: u, v (e + 2 rows: MUSCL), phi (e + 1: the wall terms' grad phi^{n-1}) and, when
+        // not known valid, cu^{n-1}, cv^{n-1} (e) in ONE exchange, overlapped with the strips of the slab's own
+        // interior; K1 then computes its rows and e of each neighbour's (their rhs and convective terms), its
+        // ||RHS||^2 over its own rows
+        const int e = s->deep_e, ld = s->g.ld;
+        const HaloReq r[5] = {{&s->g, s->arr[NS_ARR_U], e + 2}, {&s->g, s->arr[NS_ARR_V], e + 2},
+                              {&s->g, s->arr[NS_ARR_PHI], e + 1}, {&s->g, s->arr[NS_ARR_CU], e},
+                              {&s->g, s->arr[NS_ARR_CV], e}};
+        int lo = 0;
+        const nsg::Geo gk = deep_geo(s, e, &lo);
+        nb = overlapped(s, r, s->cu_ext >= e ? 3 : 5, [&]() {
+            return nsg::launch_rhs(gk, s->c, s->dt, s->re, shp(s->arr[NS_ARR_U], lo, ld), shp(s->arr[NS_ARR_V], lo, ld),
+                                   shp(s->arr[NS_ARR_PHI], lo, ld), shp(s->arr[NS_ARR_CU], lo, ld),
+                                   shp(s->arr[NS_ARR_CV], lo, ld), shp(s->arr[NS_ARR_RU], lo, ld),
+                                   shp(s->arr[NS_ARR_RV], lo, ld), s->part, s->st, e + 2);
+        });
+        s->cu_ext = e;
+        s->u_ext = e + 2;
+    } else {
+        const HaloReq r[3] = {{&s->g, s->arr[NS_ARR_U], 2}, {&s->g, s->arr[NS_ARR_V], 2}, {&s->g, s->arr[NS_ARR_PHI], 1}};
+        nb = overlapped(s, r, 3, [&]() {
+            return nsg::launch_rhs(s->g, s->c, s->dt, s->re, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_PHI],
+                                   s->arr[NS_ARR_CU], s->arr[NS_ARR_CV], s->arr[NS_ARR_RU], s->arr[NS_ARR_RV], s->part,
+                                   s->st);
+        });
+        s->cu_ext = 0;
+    }
     if (nb < 0) return nb;
     if (t) CHK(t_end(s, s->kev[0], s->kev[1]));
     // (r5, the bus: the rank's norms wait in S_HBNL for the Helmholtz check's allgather)
@@ -2953,11 +3109,13 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         const bool out_ok = nneu_r == 1 && g.neu[1] && p->nranks == 1 && gd->nx % 2 == 0 && gd->nx >= 4 &&
                             !(foe && std::atoi(foe) == 0);
         s->fps = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !masked && (!outflow || out_ok) &&
-                 yuni && nsg::fps_log2(gd->ny) >= 0;
+                 yuni && nsg::fps_log2x(gd->ny) >= 0;
         s->fa.outE = s->fps && outflow ? 1 : 0;
         if (const char* e = getenv("NSGPU_FPS_CHECK")) s->fps_check = std::max(0, std::atoi(e));
         if (const char* e = getenv("NSGPU_FPS_PASSES")) s->fps_passes = std::atoi(e) == 3 && !s->fa.outE ? 3 : 2;
         if (const char* e = getenv("NSGPU_FPS_FUSE")) s->fps_fuse = std::atoi(e) != 0;
+        // (r5) ny = 16384 (configs[4]): the two-half transforms have no fused K3 form -- K3, then the DCT
+        if (nsg::fps_log2(gd->ny) < 0) s->fps_fuse = false;
         if (s->fps) s->phi_extrap = 0;   // (no initial guess: no history planes)
         const char* fpc = getenv("NSGPU_FPS_PC");
         s->fps_pc = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !(fpc && std::atoi(fpc) == 0) &&
@@ -3038,18 +3196,42 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         }
     }
 
-    s->plane = (size_t)(g.nxl + 2 * nsg::HALO) * g.ld;
+    {
+        // (r5) deep ghost rows (ns_solver::deep): multi-rank rectangles on the direct solve with the wall bands and
+        // the residual 3-sweep pass, every rank's slab at least deep_e + 3 rows (one neighbour feeds the exchange)
+        const char* de = getenv("NSGPU_DEEP");
+        const int R = std::max(1, s->band_sweeps / 3), E1 = 7 + 6 * R;
+        bool ok = p->nranks > 1 && !masked && s->fps && s->helm_band && s->sweep3 && s->sweep3_res && s->triple &&
+                  !(de && std::atoi(de) == 0);
+        for (int q = 0; q < p->nranks && ok; q++) {
+            int32_t a0, a1;
+            ns_slab_range(g.nx, p->nranks, q, &a0, &a1);
+            ok = a1 - a0 >= E1 + 3;
+        }
+        if (ok) {
+            s->deep = true;
+            s->deep_e = E1;
+            s->hp = E1 + nsg::HALO + 2;
+        }
+        if (s->verbose)
+            fprintf(stderr, "nsgpu rank %d/%d: %d x %d, rows %d; direct solve %d (outflow %d, fused K3 %d), wall bands %d "
+                    "(%d sweeps, %d wide), 3-sweep passes %d (residual %d, triple %d), deep ghost rows %d (%d)\n",
+                    s->rank, s->nranks, g.nx, g.ny, g.nxl, (int)s->fps, s->fa.outE, (int)s->fps_fuse, (int)s->helm_band,
+                    s->band_sweeps, s->band_w, (int)s->sweep3, (int)s->sweep3_res, (int)s->triple, (int)s->deep,
+                    s->deep_e);
+    }
+    s->plane = (size_t)(g.nxl + 2 * s->hp) * g.ld;
     if (hipMalloc(&s->base, s->plane * NS_NUM_ARR * sizeof(double)) != hipSuccess) {
         set_err("hipMalloc of %zu bytes failed", s->plane * NS_NUM_ARR * sizeof(double));
         return fail(NS_ENOMEM);
     }
     if (hipMemsetAsync(s->base, 0, s->plane * NS_NUM_ARR * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
-    for (int k = 0; k < NS_NUM_ARR; k++) s->arr[k] = s->base + k * s->plane + (size_t)nsg::HALO * g.ld;
+    for (int k = 0; k < NS_NUM_ARR; k++) s->arr[k] = s->base + k * s->plane + (size_t)s->hp * g.ld;
     if (s->phi_extrap) {
         const size_t np = (size_t)std::min(s->phi_extrap, 4);
         if (hipMalloc(&s->phim_mem, np * s->plane * sizeof(double)) != hipSuccess) { set_err("hipMalloc phim failed"); return fail(NS_ENOMEM); }
         if (hipMemsetAsync(s->phim_mem, 0, np * s->plane * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
-        s->phim = s->phim_mem + (size_t)nsg::HALO * g.ld;
+        s->phim = s->phim_mem + (size_t)s->hp * g.ld;
         if (np >= 2) s->phim2 = s->phim + s->plane;
         if (np >= 3) s->phim3 = s->phim2 + s->plane;
         if (np >= 4) s->phim4 = s->phim3 + s->plane;
@@ -3138,7 +3320,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         const size_t kn = nk * s->plane + g.ld;
         if (hipMalloc(&s->kv_mem, kn * sizeof(double)) != hipSuccess) { set_err("hipMalloc Krylov planes failed"); return fail(NS_ENOMEM); }
         if (hipMemsetAsync(s->kv_mem, 0, kn * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
-        for (size_t k = 0; k < nk; k++) s->kv[k] = s->kv_mem + k * s->plane + (size_t)nsg::HALO * g.ld;
+        for (size_t k = 0; k < nk; k++) s->kv[k] = s->kv_mem + k * s->plane + (size_t)s->hp * g.ld;
         s->lrow = s->kv_mem + nk * s->plane;
         if (hipMalloc(&s->ksc, nsg::KS_NUM * sizeof(double)) != hipSuccess) { set_err("hipMalloc failed"); return fail(NS_ENOMEM); }
         if (hipMemsetAsync(s->ksc, 0, nsg::KS_NUM * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
@@ -3246,7 +3428,8 @@ static int step_body_(ns_solver* s, ns_stats& st) {
     // was measured worse during the cavity's start-up transient: 14.7 vs 11 sweeps/step at 4096^2.)
     // rhs ghost rows (a checked pair pass and the 3-sweep pass read ib-5): multi-rank passes take them with
     // their first overlapped exchange
-    if (s->nranks > 1 && s->overlap && s->cst && !s->g.fc && !s->tiled) s->helm_b_pend = 1;
+    if (s->deep) {   // (r5: K1 computed the rhs deep into the neighbours' rows)
+    } else if (s->nranks > 1 && s->overlap && s->cst && !s->g.fc && !s->tiled) s->helm_b_pend = 1;
     else CHK(halo(s, {s->arr[NS_ARR_RU], s->arr[NS_ARR_RV]}, 6));
     s->hn = 0;
     // the Poisson initial guess (phi extrapolation) waits to hide the Helmholtz check's host sync
@@ -3395,6 +3578,7 @@ int ns_get_array(ns_solver* s, int which, double* host) {
 int ns_set_array(ns_solver* s, int which, const double* host) {
     CHK(check_arr(s, which));
     s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
+    s->cu_ext = s->u_ext = 0;   // (r5: the deep ghost rows are stale now)
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);
     HIPCHK(hipMemcpy2DAsync(s->arr[which], (size_t)s->g.ld * 8, host, (size_t)s->g.ny * 8, (size_t)s->g.ny * 8,
@@ -3448,6 +3632,7 @@ int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* 
                   const double* cv0) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
+    s->cu_ext = s->u_ext = 0;   // (r5: the deep ghost rows are stale now)
     if (u) CHK(set_compact(s, NS_ARR_U, u));
     if (v) CHK(set_compact(s, NS_ARR_V, v));
     if (phi) CHK(set_compact(s, NS_ARR_PHI, phi));
@@ -3459,6 +3644,7 @@ int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* 
 int ns_kernel(ns_solver* s, int which, int iters, double* out) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
+    s->cu_ext = s->u_ext = 0;   // (r5: a kernel alone writes the slab's own rows: the deep ghost rows are stale)
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);
     const double alpha = s->dt / (2 * s->re);

@@ -1326,7 +1326,7 @@ int og_fps_ok(const og_grid* g) {
     if (!rect_dirichlet(g)) return 0;
     for (int i = 1; i < g->nx; i++) if (g->hx[i] != g->hx[0]) return 0;
     for (int j = 1; j < g->ny; j++) if (g->hy[j] != g->hy[0]) return 0;
-    return g->ny >= 16 && g->ny <= 8192 && (g->ny & (g->ny - 1)) == 0 && g->nx >= 2;
+    return g->ny >= 16 && g->ny <= 16384 && (g->ny & (g->ny - 1)) == 0 && g->nx >= 2;
 }
 
 /* in-place forward DFT of n = 2^p complex points (iterative radix-2, bit-reversed input order) */
@@ -1354,7 +1354,7 @@ static void fft_inplace(int n, double* re, double* im, const double* cw, const d
 }
 
 int og_fps_solve(const og_grid* g, double* rhs, double* x) {
-    if (!og_fps_ok(g)) { set_err("the direct solve needs a uniform rectangle with zero-flux faces, ny = 2^p in [16, 8192]"); return -1; }
+    if (!og_fps_ok(g)) { set_err("the direct solve needs a uniform rectangle with zero-flux faces, ny = 2^p in [16, 16384]"); return -1; }
     const int nx = g->nx, N = g->ny;
     const size_t n = (size_t)nx * N;
     double m = 0.0;

@@ -219,7 +219,7 @@ class OGrid:
 
     def fps_ok(self):
         """The GPU's direct Poisson solve applies (a uniform rectangle with zero-flux phi faces,
-        ny = 2^p in [16, 8192]): the GPU's default Poisson solve there (NSGPU_FPS)."""
+        ny = 2^p in [16, 16384]): the GPU's default Poisson solve there (NSGPU_FPS)."""
         return bool(lib().og_fps_ok(self.h))
 
     def fps_solve(self, rhs):

@@ -1,6 +1,6 @@
 """The direct Poisson solve (ns_fps.hip, r4): DCT along y, chunked Thomas recurrences along x, inverse
 DCT -- the GPU's default Poisson solve on uniform rectangles with zero-flux phi faces and ny = 2^p
-(16 ... 8192).  Replaces KSPSolve(phiSolver) (/root/reference/SRC/FluidSolver.cpp:551) there.
+(16 ... 16384; r5: 16384 through two 8192-point halves).  Replaces KSPSolve(phiSolver) (/root/reference/SRC/FluidSolver.cpp:551) there.
 
 Tolerances (written per test):
   * against the oracle's restatement (og_fps_solve: sequential Thomas, textbook radix-2 FFT; the same
@@ -37,7 +37,9 @@ def demean(x):
 
 # (nx, ny): square / wide / tall, odd nx (a half row pair, a partial chunk and group), the smallest
 # and one large transform, and a slab of one chunk group
-SIZES = [(64, 64), (96, 128), (40, 256), (37, 64), (1001, 512), (16, 16), (130, 32), (300, 4096), (128, 8192)]
+# (r5) ny = 16384 (configs[4]'s grid): the two-half transforms through the scratch plane, an odd nx among them
+SIZES = [(64, 64), (96, 128), (40, 256), (37, 64), (1001, 512), (16, 16), (130, 32), (300, 4096), (128, 8192),
+         (64, 16384), (37, 16384)]
 
 
 @pytest.mark.parametrize("nx,ny", SIZES)
@@ -45,17 +47,22 @@ def test_direct_solve_matches_oracle(gpu, nx, ny):
     rng = np.random.default_rng(nx * 7 + ny)
     og = OGrid.rectangle(nx, ny, lx=nx / ny)
     assert og.fps_ok()
-    gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny), 1e-3, 100.0, rtol=1e-11)
+    # (ny = 16384: the solve agrees with the oracle to 3e-15 of max|phi|, but its residual is the operator's
+    # evaluation round-off, ~||L|| ||phi|| eps with 1/hy^2 = 2.7e8 here: 4.7e-11 measured (1.0e-11 at
+    # 8192; profiles/r05/diag16k.log) -- 1e-10 written)
+    tol = 1e-11 if ny <= 8192 else 1e-10
+    gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny), 1e-3, 100.0, rtol=tol)
     b = rng.uniform(-100, 100, nx * ny)
     gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny))
     gs.set(gpu.NS_ARR_RPHI, b)
     its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
-    assert its == 1 and res <= 1e-11, (its, res)
+    print(f"{nx}x{ny}: direct solve residual {res:.3e}")
+    assert its == 1 and res <= tol, (its, res)
     g = demean(gs.get(gpu.NS_ARR_PHI))
     x = demean(og.fps_solve(b))
     assert rel(g, x) <= 1e-10, rel(g, x)
     r = og.apply_poisson(g) - (b - b.mean())
-    assert np.linalg.norm(r) <= 1e-11 * np.linalg.norm(b - b.mean())
+    assert np.linalg.norm(r) <= tol * np.linalg.norm(b - b.mean())
     if nx * ny <= 64 * 64:
         xk, _ = og.solve_poisson(b)
         assert rel(g, demean(xk)) <= 1e-8
@@ -139,16 +146,19 @@ def _slabs(tmp_path, nproc, *args, port):
     return r
 
 
-@pytest.mark.parametrize("n,ny,nproc", [(128, 128, 2), (200, 64, 3), (256, 256, 4)])
-def test_direct_solve_on_slabs_matches_one_rank(tmp_path, gpu, n, ny, nproc):
+# (66 x 16384: the two-half transforms on slabs; rtol 1e-9 -- the solve's round-off residual at hy = 1/16384,
+# hx = 1/66 lies near 1e-10, and a check above rtol would iterate on round-off)
+@pytest.mark.parametrize("n,ny,nproc,tol", [(128, 128, 2, 1e-10), (200, 64, 3, 1e-10), (256, 256, 4, 1e-10),
+                                            (66, 16384, 2, 1e-9)])
+def test_direct_solve_on_slabs_matches_one_rank(tmp_path, gpu, n, ny, nproc, tol):
     """x-slabs (host transport, every rank on the one GPU): each rank runs its chunks' recurrences,
     the ranks' aggregates travel in one allgather per direction and solve, and the gathered steps
     equal one rank's -- the chunk boundaries move with the slab edges, so to rounding: u, v and the
     monitor to 1e-10, phi (modulo its mean) to 1e-10 of its max; one solve per step on every rank."""
     steps = 6
     r = _slabs(tmp_path, nproc, "--xport", "host", "--size", str(n), "--size-y", str(ny), "--nsteps", str(steps),
-               "--solver", str(gpu.NS_POISSON_MG), "--tol", "1e-10", port=29761 + nproc)
-    gs = gpu.GpuSolver(gpu.rectangle(n, ny), 1.0 / (8 * n), 100.0, rtol=1e-10, device=0)
+               "--solver", str(gpu.NS_POISSON_MG), "--tol", str(tol), port=29761 + nproc + 20 * (ny > 8192))
+    gs = gpu.GpuSolver(gpu.rectangle(n, ny), 1.0 / (8 * n), 100.0, rtol=tol, device=0)
     mm = np.array([list(gs.step().values())[:7] for _ in range(steps)])
     u, v, phi = gs.fields()
     gs.close()
@@ -391,3 +401,53 @@ def test_outflow_channel_steps_direct_vs_krylov(gpu, monkeypatch):
     (u0, v0, _), st0 = out["0"]
     assert all(x["it_phi"] == 1 for x in st1) and all(x["it_phi"] > 1 for x in st0)
     assert np.max(np.abs(u1 - u0)) <= 1e-8 and np.max(np.abs(v1 - v0)) <= 1e-8
+
+
+# (the direct solve needs ny = 2^p: 256 on 3 ranks -- slabs of 88 / 84 / 84 rows)
+@pytest.mark.parametrize("n,nproc", [(128, 2), (256, 3)])
+def test_slab_deep_ghost_rows(tmp_path, gpu, monkeypatch, n, nproc):
+    """r5: deep ghost rows -- K1 computes 7 + 6 R rows of each neighbour's slab (R = 2
+    band launches) from ONE exchange of u, v, phi (and cu, cv on the first step), the wall-band launches
+    compute 6 rows fewer each without an exchange, the residual 3-sweep pass finds its 7-row cone valid:
+    3 exchange groups per step (K1's, K3's u*, v* row, K5's phi row) where r4 had 6.  Host-transport slabs
+    against the r4 exchanges (NSGPU_DEEP=0): the same fields to 1e-13 (the redundant rows are the
+    neighbours' own values, recomputed by the same arithmetic) and the same step counts."""
+    steps = 12
+    args = ("--xport", "host", "--size", str(n), "--nsteps", str(steps), "--solver", str(gpu.NS_POISSON_MG),
+            "--tol", "1e-10")
+    r = _slabs(tmp_path, nproc, *args, port=29801 + nproc)
+    monkeypatch.setenv("NSGPU_DEEP", "0")
+    r0 = _slabs(tmp_path, nproc, *args, port=29811 + nproc)
+    monkeypatch.delenv("NSGPU_DEEP")
+    ex, ex0 = r["xc"][:, 0], r0["xc"][:, 0]
+    # (the two band launches' and the first Helmholtz pass's exchanges are gone every step; a batch of more
+    # passes, at rtol 1e-10 here, exchanges for its later passes either way)
+    assert np.all(ex0 - ex == 3), (ex, ex0)
+    assert np.array_equal(r["mm"][:, 4:7], r0["mm"][:, 4:7])
+    for k in ("u", "v"):
+        assert np.max(np.abs(r[k] - r0[k])) <= 1e-13, k
+    np.testing.assert_allclose(r["mm"][:, :4], r0["mm"][:, :4], atol=1e-13)
+
+
+def test_direct_solve_16384_steps_vs_multigrid(gpu, monkeypatch):
+    """r5: configs[4]'s grid (16384^2 cavity, Re 1000, from rest, 2 steps) with the direct solve's two-half
+    transforms against the GPU's multigrid Poisson solve (NSGPU_FPS=0), both at rtol 1e-10: u, v <= 1e-9 and
+    the monitor <= 1e-9; one 'iteration' per direct solve."""
+    n, steps = 16384, 2
+    out = {}
+    for fe in ("1", "0"):
+        monkeypatch.setenv("NSGPU_FPS", fe)
+        gs = gpu.GpuSolver(gpu.cavity(n), 1.0 / (8 * n), 1000.0, rtol=1e-10)
+        st = [gs.step() for _ in range(steps)]
+        u, v, _ = gs.fields()
+        out[fe] = (u, v, st)
+        gs.close()
+        del u, v
+    u1, v1, st1 = out["1"]
+    u0, v0, st0 = out["0"]
+    assert all(x["it_phi"] == 1 and (x["phi_checked"] == 0 or 0 <= x["res_phi"] <= 1e-10) for x in st1), st1
+    assert all(x["it_phi"] > 1 for x in st0)
+    for a, b in zip(st1, st0):
+        for k in ("umin", "umax", "vmin", "vmax"):
+            assert abs(a[k] - b[k]) <= 1e-9, (k, a[k], b[k])
+    assert np.max(np.abs(u1 - u0)) <= 1e-9 and np.max(np.abs(v1 - v0)) <= 1e-9

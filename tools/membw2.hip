@@ -50,7 +50,63 @@ __global__ __launch_bounds__(256) void k_copy(const double2* __restrict__ a, dou
     }
 }
 
+// (r5) K1's stream mix: read u, v, cu0, cv0 and write cu, cv (in place), ru, rv -- 4 reads + 4 writes of 16 B
+// per lane (64 B/cell), non-temporal stores like k_rhs_s: the ceiling of K1's own access pattern
+template <int U>
+__global__ __launch_bounds__(256) void k_4r4w(const double2* __restrict__ u, const double2* __restrict__ v,
+                                              double2* cu, double2* cv, double2* __restrict__ ru,
+                                              double2* __restrict__ rv, size_t n2) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i0 = blockIdx.x * 256 + threadIdx.x; i0 < n2; i0 += stride * U) {
+        double2 a[U], b[U], c[U], d[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const size_t i = i0 + k * stride;
+            if (i < n2) { a[k] = u[i]; b[k] = v[i]; c[k] = cu[i]; d[k] = cv[i]; }
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const size_t i = i0 + k * stride;
+            if (i < n2) {
+                auto st = [](double2* p, double x, double y) {
+                    __builtin_nontemporal_store(x, &p->x); __builtin_nontemporal_store(y, &p->y);
+                };
+                st(&cu[i], a[k].x + c[k].x, a[k].y + c[k].y);
+                st(&cv[i], b[k].x + d[k].x, b[k].y + d[k].y);
+                st(&ru[i], a[k].x - d[k].x, a[k].y - d[k].y);
+                st(&rv[i], b[k].x - c[k].x, b[k].y - c[k].y);
+            }
+        }
+    }
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "k1") {   // K1's 4-read / 4-write mix at 4096^2 and 8192^2
+        for (int n : {4096, 8192}) {
+            const size_t N = (size_t)n * n;
+            double* f[6];
+            for (auto& x : f) { hipMalloc(&x, N * 8); hipMemset(x, 0, N * 8); }
+            hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+            for (int g : {2048, 4096, 8192}) {
+                for (int w = 0; w < 5; w++)
+                    hipLaunchKernelGGL((k_4r4w<2>), dim3(g), dim3(256), 0, 0, (const double2*)f[0], (const double2*)f[1],
+                                       (double2*)f[2], (double2*)f[3], (double2*)f[4], (double2*)f[5], N / 2);
+                std::vector<float> ts;
+                for (int it = 0; it < 20; it++) {
+                    hipEventRecord(e0);
+                    hipLaunchKernelGGL((k_4r4w<2>), dim3(g), dim3(256), 0, 0, (const double2*)f[0], (const double2*)f[1],
+                                       (double2*)f[2], (double2*)f[3], (double2*)f[4], (double2*)f[5], N / 2);
+                    hipEventRecord(e1); hipEventSynchronize(e1);
+                    float ms; hipEventElapsedTime(&ms, e0, e1); ts.push_back(ms);
+                }
+                std::sort(ts.begin(), ts.end());
+                printf("n=%d 4R4W (K1 mix, nt stores) grid=%d median %8.1f us  %7.1f GB/s (64 B/cell)\n", n, g,
+                       ts[10] * 1e3, 64.0 * N / (ts[10] * 1e-3) / 1e9);
+            }
+            for (auto x : f) hipFree(x);
+        }
+        return 0;
+    }
     for (int n : {4096, 8192}) {
         const size_t N = (size_t)n * n;
         double *a, *b, *c;
