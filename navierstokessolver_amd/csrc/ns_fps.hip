@@ -1354,21 +1354,24 @@ int div_pair(const FpsDivArgs& a0, hipStream_t st) {
     return (int)grid.x;
 }
 
-// ---- (r5) N = 16384 (configs[4]'s grid): the row pair's 16384-point FFT does not fit the LDS (256 KiB), so it runs
-// as two 8192-point halves through HBM -- radix-2 decimation in time, Z_k = E_k + W^k O_k and Z_{k+N/2} = E_k -
-// W^k O_k with E = FFT(z_{2m}), O = FFT(z_{2m+1}) -- in two launches per direction: (a) a persistent workgroup
-// per row pair forms both halves' inputs, transforms each in LDS (fft_regs<13>: first / last stage in registers)
-// and writes E and O to a scratch plane (rows 2p, 2p + 1 of the pair's own rows); (b) an elementwise pass combines
-// them and applies the DCT's post- (forward) or output (inverse) step.  8 B/cell more each way than the one-pass
-// transforms of N <= 8192 (NSGPU's ny <= 8192 path, unchanged).
+// ---- (r5) N = 16384 (configs[4]'s grid): the row pair's 16384-point FFT does not fit the LDS (256 KiB), so each
+// row pair runs as two 8192-point transforms (fft_regs<13>, 128 KiB) in ONE persistent launch, one workgroup per CU:
+//   forward, decimation in frequency: a_n = z_n + z_{n+N/2}, b_n = (z_n - z_{n+N/2}) W^n (n < N/2, W = e^{-2 pi i/N})
+//     give Z_{2k} = FFT_{N/2}(a)_k and Z_{2k+1} = FFT_{N/2}(b)_k; the DCT's post-step pairs Z_k with Z_{N-k}, of the
+//     same parity, so each half finishes on its own (its mirror through the LDS) and thread t stores
+//     (X_{2k}, X_{2k+1}) of both rows as 16 B;
+//   inverse, decimation in time: E = FFT_{N/2}(y_{2m}), O = FFT_{N/2}(y_{2m+1}), Y_n = E_n + W^n O_n,
+//     Y_{n+N/2} = E_n - W^n O_n -- thread t holds E_n, O_n for the same n; the second half goes through the LDS
+//     so that columns 2n, 2n + 1 leave as 16 B.
+// HBM: the row pair read once and written once (16 B/cell), as the one-pass transforms of N <= 8192.
 constexpr int N14 = 1 << 14, NH14 = N14 / 2, TH14 = NH14 / 16;
 
-// forward (a): z_n = (x_a[j(n)], x_b[j(n)]) - shift (Makhoul's reordering j(n) = 2n, n < N/2; 2(N-1-n)+1 after),
-// n = 2m + h -> E (h = 0) / O (h = 1) = FFT_{N/2} -> scratch rows 2p + h (8192 complex = one row of ld doubles);
-// oe_pair as k_fps_dct
-__global__ void __launch_bounds__(TH14) k_fps_dct14a(const double* __restrict__ in, const double* shiftp,
-                                                    double* __restrict__ scr, int nrows, int ld,
-                                                    const cplx* __restrict__ tw8, int oe_pair) {
+// forward: z_n = (x_a[j(n)], x_b[j(n)]) - shift, j(n) = 2n (n < N/2), 2(N-1-n)+1 after (Makhoul's order);
+// oe_pair as k_fps_dct.  tw: e^{-2 pi i m/N} (m < N), tw8: e^{-2 pi i m/(N/2)}, wk[k] = e^{-i pi k/2N}
+__global__ void __launch_bounds__(TH14) k_fps_dct14(const double* __restrict__ in, const double* shiftp,
+                                                   double* __restrict__ out, int nrows, int ld,
+                                                   const cplx* __restrict__ tw, const cplx* __restrict__ tw8,
+                                                   const cplx* __restrict__ wk, int oe_pair) {
     extern __shared__ cplx z[];
     int tid = threadIdx.x;
     const int npairs = (nrows + 1) / 2;
@@ -1377,71 +1380,65 @@ __global__ void __launch_bounds__(TH14) k_fps_dct14a(const double* __restrict__ 
         const int r0 = 2 * p;
         const bool two = r0 + 1 < nrows;
         const double* a = in + (size_t)r0 * ld;
+        double* oa = out + (size_t)r0 * ld;
         const double lam = p == oe_pair ? 0.5 : 0.0;
+        double xe[2][16];   // X_{2k} of both rows, stored with X_{2k+1}
+        // (one loop body for both halves: the two transforms' index arithmetic is not kept live together)
+#pragma unroll 1
         for (int h = 0; h < 2; h++) {
             fps_remat(tid);
+            // z_n (n < N/2) = x_{2n}, z_{n+N/2} = x_{N-1-2n}; h = 0: a_n = z_n + z_{n+N/2}, 1: b_n = (z_n - z_{n+N/2}) W^n
             cplx v[16];
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                const int n = 2 * (tid + r * TH14) + h;
-                const int j = n < N14 / 2 ? 2 * n : 2 * (N14 - 1 - n) + 1;
-                const double xa = a[j] - sh;
-                v[r] = cplx{xa, two ? a[ld + j] - sh - lam * xa : 0.0};
+                const int n = tid + r * TH14;
+                const int j0 = 2 * n, j1 = N14 - 1 - 2 * n;
+                const double x0 = a[j0] - sh, x1 = a[j1] - sh;
+                const cplx z0{x0, two ? a[ld + j0] - sh - lam * x0 : 0.0}, z1{x1, two ? a[ld + j1] - sh - lam * x1 : 0.0};
+                v[r] = h ? cmul(csub(z0, z1), tw[n]) : cadd(z0, z1);
             }
-            fft_regs<13>(z, tw8, tid, v);
-            cplx* o = reinterpret_cast<cplx*>(scr + (size_t)(r0 + h) * ld);
+            fft_regs<13>(z, tw8, tid, v);   // Z_{2k + h}, k = tid + r TH14
+            __syncthreads();
 #pragma unroll
-            for (int r = 0; r < 16; r++) o[tid + r * TH14] = v[r];
-            __syncthreads();   // (z is rewritten by the next half)
+            for (int r = 0; r < 16; r++) z[pz(tid + r * TH14)] = v[r];
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int k = tid + r * TH14;
+                // the mirror Z_{N-2k-h}: Z_{2(N/2-k)} (h = 0), Z_{2(N/2-1-k)+1} (h = 1)
+                const cplx Zk = v[r], Zn = z[pz((NH14 - k - h) & (NH14 - 1))];
+                const cplx Va{0.5 * (Zk.x + Zn.x), 0.5 * (Zk.y - Zn.y)};
+                const cplx Vb{0.5 * (Zk.y + Zn.y), 0.5 * (Zn.x - Zk.x)};
+                const cplx w = wk[2 * k + h];
+                const double ya = fma(w.x, Va.x, -w.y * Va.y), yb = fma(w.x, Vb.x, -w.y * Vb.y);
+                if (!h) {
+                    xe[0][r] = ya;
+                    xe[1][r] = yb;
+                } else {
+                    st2(oa + 2 * k, xe[0][r], ya);
+                    if (two) st2(oa + ld + 2 * k, xe[1][r], yb);
+                }
+            }
+            __syncthreads();   // (z is rewritten by the next transform)
         }
     }
 }
 
-// forward (b): per row pair and q in [0, N/4]: E, O at q and N/2 - q give Z at q, q + N/2, N/2 - q, N - q, and
-// from them the DCT-II coefficients X at the same four indices of both rows (k_fps_dct's post-processing:
-// X_k = Re(e^{-i pi k / 2N} V_k), V_a / V_b from Z_k and Z_{N-k})
-__global__ void __launch_bounds__(256) k_fps_dct14b(const double* __restrict__ scr, double* __restrict__ out, int nrows,
-                                                    int ld, const cplx* __restrict__ tw, const cplx* __restrict__ wk) {
-    const int npairs = (nrows + 1) / 2, nq = NH14 / 2 + 1;
-    for (long t = blockIdx.x * 256L + threadIdx.x; t < (long)npairs * nq; t += (long)gridDim.x * 256) {
-        const int p = (int)(t / nq), q = (int)(t - (long)p * nq);
-        const int r0 = 2 * p;
-        const bool two = r0 + 1 < nrows;
-        const cplx* E = reinterpret_cast<const cplx*>(scr + (size_t)r0 * ld);
-        const cplx* O = reinterpret_cast<const cplx*>(scr + (size_t)(r0 + 1) * ld);
-        const int k2 = NH14 - q;   // (q = 0: E, O are N/2-periodic; W^{N/2} = -1)
-        const cplx e1 = E[q], o1 = cmul(O[q], tw[q]), e2 = E[k2 & (NH14 - 1)], o2 = cmul(O[k2 & (NH14 - 1)], tw[k2]);
-        const cplx Zq = cadd(e1, o1), Zq2 = csub(e1, o1), Zk2 = cadd(e2, o2), Zk22 = csub(e2, o2);
-        // (index: Zq = Z_q, Zq2 = Z_{q + N/2}, Zk2 = Z_{N/2 - q}, Zk22 = Z_{N - q})
-        double* oa = out + (size_t)r0 * ld;
-        double* ob = oa + ld;
-        auto post = [&](int k, cplx Zk, cplx Zn) {
-            const cplx Va{0.5 * (Zk.x + Zn.x), 0.5 * (Zk.y - Zn.y)};
-            const cplx Vb{0.5 * (Zk.y + Zn.y), 0.5 * (Zn.x - Zk.x)};
-            const cplx w = wk[k];
-            oa[k] = fma(w.x, Va.x, -w.y * Va.y);
-            if (two) ob[k] = fma(w.x, Vb.x, -w.y * Vb.y);
-        };
-        post(q, Zq, q ? Zk22 : Zq);
-        if (q) post(N14 - q, Zk22, Zq);
-        post(NH14 + q, Zq2, Zk2);
-        if (q && q != NH14 / 2) post(NH14 - q, Zk2, Zq2);
-        else if (!q) post(NH14, Zk2, Zq2);   // (q = 0: N/2 - q = N/2 itself)
-    }
-}
-
-// inverse (a): y_n = conj(V_n), V_k = e^{i pi k / 2N} (X_k - i X_{N-k}) packed over the two rows (k_fps_idct's
-// input step), n = 2m + h -> FFT_{N/2} -> scratch rows 2p + h
-__global__ void __launch_bounds__(TH14) k_fps_idct14a(const double* __restrict__ in, double* __restrict__ scr,
-                                                     int nrows, int ld, const cplx* __restrict__ tw8,
-                                                     const cplx* __restrict__ wk) {
+// inverse: y_k = conj(V_k), V_k = e^{i pi k/2N} (X_k - i X_{N-k}) packed over the two rows (k_fps_idct's input
+// step); E from the even k, O from the odd; x_{2n} = Re Y_n / N, x_{2n+1} = Re Y_{N-1-n} / N (row b: -Im)
+__global__ void __launch_bounds__(TH14) k_fps_idct14(const double* __restrict__ in, double* __restrict__ out,
+                                                    int nrows, int ld, const cplx* __restrict__ tw,
+                                                    const cplx* __restrict__ tw8, const cplx* __restrict__ wk) {
     extern __shared__ cplx z[];
     int tid = threadIdx.x;
     const int npairs = (nrows + 1) / 2;
+    const double rn = 1.0 / N14;
     for (int p = blockIdx.x; p < npairs; p += gridDim.x) {
         const int r0 = 2 * (FPS_SNAKE ? npairs - 1 - p : p);
         const bool two = r0 + 1 < nrows;
         const double* a = in + (size_t)r0 * ld;
+        cplx e[16];   // E_n, then Y_n
+#pragma unroll 1
         for (int h = 0; h < 2; h++) {
             fps_remat(tid);
             cplx v[16];
@@ -1450,67 +1447,57 @@ __global__ void __launch_bounds__(TH14) k_fps_idct14a(const double* __restrict__
                 const int k = 2 * (tid + r * TH14) + h;
                 const double xa = a[k], xb = two ? a[ld + k] : 0.0;
                 const double ya = k ? a[N14 - k] : 0.0, yb = two && k ? a[ld + N14 - k] : 0.0;
-                const cplx w = wk[k];
+                const cplx w = wk[k];   // e^{-i theta}: e^{i theta} = (w.x, -w.y)
                 const double c = w.x, s = -w.y;
                 const cplx Va{fma(c, xa, s * ya), fma(s, xa, -c * ya)};
                 const cplx Vb{fma(c, xb, s * yb), fma(s, xb, -c * yb)};
                 v[r] = cplx{Va.x - Vb.y, -(Va.y + Vb.x)};
             }
-            fft_regs<13>(z, tw8, tid, v);
-            cplx* o = reinterpret_cast<cplx*>(scr + (size_t)(r0 + h) * ld);
+            fft_regs<13>(z, tw8, tid, v);   // E_n (h = 0), O_n (h = 1), n = tid + r TH14
+            __syncthreads();   // (every thread has read its last stage's inputs)
+            if (!h) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) o[tid + r * TH14] = v[r];
+                for (int r = 0; r < 16; r++) e[r] = v[r];
+                continue;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const cplx t = cmul(v[r], tw[tid + r * TH14]);
+                z[pz(tid + r * TH14)] = csub(e[r], t);   // Y_{n+N/2}
+                e[r] = cadd(e[r], t);                    // Y_n
+            }
             __syncthreads();
+            double* oa = out + (size_t)r0 * ld;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int n = tid + r * TH14;
+                const cplx o = z[pz(NH14 - 1 - n)];   // Y_{N-1-n} = Y_{(N/2-1-n)+N/2}
+                st2(oa + 2 * n, e[r].x * rn, o.x * rn);
+                if (two) st2(oa + ld + 2 * n, -e[r].y * rn, -o.y * rn);
+            }
+            __syncthreads();   // (z is rewritten by the next pair)
         }
     }
 }
 
-// inverse (b): per row pair and n < N/2: Y_n = E_n + W^n O_n and Y_{N-1-n} = E_{N/2-1-n} - W^{N/2-1-n} O_{N/2-1-n}
-// are the values of columns 2n and 2n + 1 (Makhoul's order); x = conj(Y) / N -> both rows, 16-B stores
-__global__ void __launch_bounds__(256) k_fps_idct14b(const double* __restrict__ scr, double* __restrict__ out, int nrows,
-                                                     int ld, const cplx* __restrict__ tw) {
-    const int npairs = (nrows + 1) / 2;
-    const double rn = 1.0 / N14;
-    for (long t = blockIdx.x * 256L + threadIdx.x; t < (long)npairs * NH14; t += (long)gridDim.x * 256) {
-        const int p = (int)(t / NH14), n = (int)(t - (long)p * NH14);
-        const int r0 = 2 * p;
-        const bool two = r0 + 1 < nrows;
-        const cplx* E = reinterpret_cast<const cplx*>(scr + (size_t)r0 * ld);
-        const cplx* O = reinterpret_cast<const cplx*>(scr + (size_t)(r0 + 1) * ld);
-        const int m = NH14 - 1 - n;
-        const cplx Y0 = cadd(E[n], cmul(O[n], tw[n])), Y1 = csub(E[m], cmul(O[m], tw[m]));
-        double* oa = out + (size_t)r0 * ld;
-        st2(oa + 2 * n, Y0.x * rn, Y1.x * rn);
-        if (two) st2(oa + ld + 2 * n, -Y0.y * rn, -Y1.y * rn);
-    }
-}
-
-void dct14(bool inverse, const double* in, const double* shift, double* out, double* scr, int nrows, int ld,
-           const double* tw, const double* tw8, const double* wk, hipStream_t st, int oe_pair) {
+void dct14(bool inverse, const double* in, const double* shift, double* out, int nrows, int ld, const double* tw,
+           const double* tw8, const double* wk, hipStream_t st, int oe_pair) {
     const size_t lds = sizeof(cplx) * (size_t)FftLds<13>::n;
-    const int cus = device_cus(), npairs = (nrows + 1) / 2;
-    const dim3 ga(std::min(npairs, cus)), gb(std::min((long)npairs * NH14 / 256 + 1, 8L * cus));
+    const dim3 grid(std::min((nrows + 1) / 2, device_cus()));   // (128 KiB of LDS: one workgroup per CU)
     hipEvent_t a, b;
-    const bool tm = take_launch_timing(a, b);   // (timed: the first launch's begin to the second's end)
+    const bool tm = take_launch_timing(a, b);
     if (!inverse) {
-        lds_attr_once((const void*)k_fps_dct14a, (int)lds);
-        if (tm) hipExtLaunchKernelGGL(k_fps_dct14a, ga, dim3(TH14), lds, st, a, nullptr, 0, in, shift, scr, nrows, ld,
-                                      (const cplx*)tw8, oe_pair);
-        else hipLaunchKernelGGL(k_fps_dct14a, ga, dim3(TH14), lds, st, in, shift, scr, nrows, ld, (const cplx*)tw8,
-                                oe_pair);
-        if (tm) hipExtLaunchKernelGGL(k_fps_dct14b, gb, dim3(256), 0, st, nullptr, b, 0, scr, out, nrows, ld,
-                                      (const cplx*)tw, (const cplx*)wk);
-        else hipLaunchKernelGGL(k_fps_dct14b, gb, dim3(256), 0, st, scr, out, nrows, ld, (const cplx*)tw,
-                                (const cplx*)wk);
+        lds_attr_once((const void*)k_fps_dct14, (int)lds);
+        if (tm) hipExtLaunchKernelGGL(k_fps_dct14, grid, dim3(TH14), lds, st, a, b, 0, in, shift, out, nrows, ld,
+                                      (const cplx*)tw, (const cplx*)tw8, (const cplx*)wk, oe_pair);
+        else hipLaunchKernelGGL(k_fps_dct14, grid, dim3(TH14), lds, st, in, shift, out, nrows, ld, (const cplx*)tw,
+                                (const cplx*)tw8, (const cplx*)wk, oe_pair);
     } else {
-        lds_attr_once((const void*)k_fps_idct14a, (int)lds);
-        if (tm) hipExtLaunchKernelGGL(k_fps_idct14a, ga, dim3(TH14), lds, st, a, nullptr, 0, in, scr, nrows, ld,
-                                      (const cplx*)tw8, (const cplx*)wk);
-        else hipLaunchKernelGGL(k_fps_idct14a, ga, dim3(TH14), lds, st, in, scr, nrows, ld, (const cplx*)tw8,
-                                (const cplx*)wk);
-        if (tm) hipExtLaunchKernelGGL(k_fps_idct14b, gb, dim3(256), 0, st, nullptr, b, 0, scr, out, nrows, ld,
-                                      (const cplx*)tw);
-        else hipLaunchKernelGGL(k_fps_idct14b, gb, dim3(256), 0, st, scr, out, nrows, ld, (const cplx*)tw);
+        lds_attr_once((const void*)k_fps_idct14, (int)lds);
+        if (tm) hipExtLaunchKernelGGL(k_fps_idct14, grid, dim3(TH14), lds, st, a, b, 0, in, out, nrows, ld,
+                                      (const cplx*)tw, (const cplx*)tw8, (const cplx*)wk);
+        else hipLaunchKernelGGL(k_fps_idct14, grid, dim3(TH14), lds, st, in, out, nrows, ld, (const cplx*)tw,
+                                (const cplx*)tw8, (const cplx*)wk);
     }
 }
 
@@ -1525,9 +1512,10 @@ int fps_log2x(int ny) { return ny == N14 ? 14 : fps_log2(ny); }
 
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
                    const double* tw, const double* wk, hipStream_t st, int oe_pair, double* scratch, const double* tw8) {
-    if (ny == N14) {   // (r5: two launches through the scratch plane)
-        if (!scratch || !tw8 || ld != N14) return -1;
-        dct14(inverse, in, shift, out, scratch, nrows, ld, tw, tw8, wk, st, oe_pair);
+    (void)scratch;
+    if (ny == N14) {   // (r5: two 8192-point transforms per row pair)
+        if (!tw8) return -1;
+        dct14(inverse, in, shift, out, nrows, ld, tw, tw8, wk, st, oe_pair);
         return 0;
     }
     switch (fps_log2(ny)) {

@@ -259,9 +259,13 @@ void launch_line_extend(const double* p, const Geo& g, double* z, int rows, doub
 
 // NEUMANN outflow Poisson (BiCGStab on the true operator, right-preconditioned by one
 // wall-closure V-cycle; ns_solver.cpp pois_solve_krylov).  Device scalar slots:
-enum { KS_RHO = 0, KS_ALPHA, KS_OMEGA, KS_BETA, KS_MEAN, KS_SUMR0, KS_BRK, KS_D = 8, KS_NUM = 16 };
+// (r5) the convergence test on the device: KS_STOP freezes every scalar stage and vector update (and the gated
+// apply / diagonal launches) once r.r <= KS_THR, r.r = 0, a breakdown, divergence or KS_MAXIT iterations;
+// KS_R2 keeps that r.r, KS_IT counts the completed iterations -- the host reads them once per batch of iterations
+enum { KS_RHO = 0, KS_ALPHA, KS_OMEGA, KS_BETA, KS_MEAN, KS_SUMR0, KS_BRK, KS_STOP, KS_D = 8, KS_THR = 11, KS_IT,
+       KS_MAXIT, KS_R2, KS_B2, KS_NUM = 16 };
 // scalar stages (k_bicg_scal) and vector modes (k_bicg_vec)
-enum { KSC_INIT = 0, KSC_RHO, KSC_ALPHA, KSC_MEAN, KSC_OMEGA };
+enum { KSC_INIT = 0, KSC_RHO, KSC_ALPHA, KSC_MEAN, KSC_OMEGA, KSC_CHECK, KSC_RESET };
 enum { KV_INIT = 0, KV_P, KV_V, KV_T, KV_X };
 struct KrylovArgs {
     Geo g;
@@ -273,14 +277,18 @@ struct KrylovArgs {
 // y = A x with A the reference's Poisson matrix (op 0, NEUMANN outflow rows included) or its
 // Helmholtz matrix I - alpha L_V (op 1), on a rectangle or a masked domain; partials
 // (sum y, sum q*y) per block (q may be null); returns the partial count
+// (stop: a KS_STOP slot -- the grid kernels then do nothing once it is set; null: always run)
 int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double* x, double* y, const double* q,
-                 double* part, hipStream_t st);
+                 double* part, hipStream_t st, const double* stop = nullptr);
 // z = q / diag(A) (Jacobi preconditioner of the masked-domain solves)
-void launch_diag_pc(int op, const Geo& g, const Coef& c, double alpha, const double* q, double* z, hipStream_t st);
+void launch_diag_pc(int op, const Geo& g, const Coef& c, double alpha, const double* q, double* z, hipStream_t st,
+                    const double* stop = nullptr);
 // one fused BiCGStab vector update (KV_*); 3 partials per block for KV_INIT / KV_T / KV_X
 int launch_bicg_vec(int mode, KrylovArgs a, hipStream_t st);
 // the scalar recurrences (KSC_*) from reduced sums d
 void launch_bicg_scal(int stage, const double* d, double n, double* sc, hipStream_t st);
+// (r5) a solve's start: KS_IT = 0, KS_STOP = 0, the test's threshold tol^2 b2, b2 and the iteration cap
+void launch_bicg_start(double* sc, double thr, double b2, int maxit, hipStream_t st);
 
 // max partials any launcher writes for this geometry
 int max_partials(const Geo& g);

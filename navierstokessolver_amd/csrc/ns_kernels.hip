@@ -3757,7 +3757,8 @@ __global__ __launch_bounds__(256) void k_axpby(Geo g, double a, const double* __
 template <int OP, class T>
 __global__ __launch_bounds__(256) void k_apply(Geo g, Coef c, double alpha, const double* __restrict__ x,
                                                double* __restrict__ y, const double* __restrict__ q,
-                                               double* __restrict__ part, int rows) {
+                                               double* __restrict__ part, int rows, const double* stop) {
+    if (stop && *stop != 0.0) return;   // (r5: a converged Krylov batch's remaining launches)
     const int j = blockIdx.x * 64 + threadIdx.x;
     const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
     double acc[2] = {0.0, 0.0};
@@ -3793,7 +3794,8 @@ __global__ __launch_bounds__(256) void k_apply(Geo g, Coef c, double alpha, cons
 // outflow rows' diagonal -(sum p) + 1.5 w, oracle diag_poisson / diag_helmholtz)
 template <int OP, class T>
 __global__ __launch_bounds__(256) void k_diag_pc(Geo g, Coef c, double alpha, const double* __restrict__ qv,
-                                                 double* __restrict__ z) {
+                                                 double* __restrict__ z, const double* stop) {
+    if (stop && *stop != 0.0) return;
     const int j = blockIdx.x * 64 + threadIdx.x;
     const int li = blockIdx.y * 4 + threadIdx.y;
     if (j >= g.ny || li >= g.nxl) return;
@@ -3826,6 +3828,7 @@ __global__ __launch_bounds__(256) void k_diag_pc(Geo g, Coef c, double alpha, co
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_bicg_vec(KrylovArgs a) {
+    if (a.sc[KS_STOP] != 0.0) return;   // (r5: frozen -- the partials stay unread, every scalar stage is frozen too)
     const Geo& g = a.g;
     const int j = blockIdx.x * 64 + threadIdx.x;
     const int lend = min((int)(blockIdx.y + 1) * 4 * a.rows, g.nxl);
@@ -3869,13 +3872,36 @@ __global__ __launch_bounds__(256) void k_bicg_vec(KrylovArgs a) {
 //   KSC_ALPHA (d = sum y, r0.y):       mean_y, alpha = rho / (r0.y - mean_y sum r0)
 //   KSC_MEAN  (d = sum y):             mean_y
 //   KSC_OMEGA (d = t.s, t.t):          omega = t.s / t.t
-__global__ void k_bicg_scal(int stage, const double* __restrict__ d, double n, double* __restrict__ sc) {
+//   KSC_CHECK (d = r.r, ...):          the convergence test of the host loop's head (r5), in its order: divergence
+//                                      (non-finite, or 1e16 b2), convergence (<= tol^2 b2, = 0), the cap, a breakdown
+//   KSC_RESET:                         a restart after a breakdown (KS_STOP, KS_BRK cleared)
+__global__ void k_bicg_scal(int stage, const double* __restrict__ d, double n, double* __restrict__ sc, double thr,
+                            double b2, int maxit) {
     // a breakdown (a zero or non-finite denominator) zeroes the coefficient -- the vector
     // updates then leave x untouched -- and raises KS_BRK; the host restarts from x
     auto guard = [&](double v) {
         if (!isfinite(v)) { sc[KS_BRK] = 1.0; return 0.0; }
         return v;
     };
+    if (stage == KSC_RESET) {
+        sc[KS_STOP] = 0.0;
+        sc[KS_BRK] = 0.0;
+        if (maxit >= 0) {   // (a solve's start)
+            sc[KS_IT] = 0.0; sc[KS_THR] = thr; sc[KS_B2] = b2; sc[KS_MAXIT] = maxit;
+        }
+        return;
+    }
+    if (sc[KS_STOP] != 0.0) return;
+    if (stage == KSC_CHECK) {
+        const double r2 = d[0], bb = sc[KS_B2];
+        const bool stop = !isfinite(r2) || (bb > 0 && r2 > 1e16 * bb) || r2 <= sc[KS_THR] || r2 == 0.0 ||
+                          sc[KS_IT] >= sc[KS_MAXIT] || sc[KS_BRK] != 0.0;
+        if (stop) {
+            sc[KS_STOP] = 1.0;
+            sc[KS_R2] = r2;
+        }
+        return;
+    }
     if (stage == KSC_INIT) {
         sc[KS_RHO] = 1.0; sc[KS_ALPHA] = 1.0; sc[KS_OMEGA] = 1.0; sc[KS_SUMR0] = d[2]; sc[KS_BRK] = 0.0;
     } else if (stage == KSC_RHO) {
@@ -3893,6 +3919,7 @@ __global__ void k_bicg_scal(int stage, const double* __restrict__ d, double n, d
         const double om = d[1] > 0.0 ? d[0] / d[1] : 0.0;
         sc[KS_OMEGA] = guard(om);
         if (om == 0.0) sc[KS_BRK] = 1.0;
+        sc[KS_IT] += 1.0;   // (the iteration's last scalar stage)
     }
 }
 
@@ -4120,7 +4147,7 @@ int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const do
 }
 
 int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double* x, double* y, const double* q,
-                 double* part, hipStream_t st) {
+                 double* part, hipStream_t st, const double* stop) {
     const char* ae = getenv("NSGPU_APPLY");   // NSGPU_APPLY=grid: k_apply only (A/B)
     if (op == 0 && !g.fc && cell_streaming() && !(ae && std::strcmp(ae, "grid") == 0)) {
         CellStreamArgs A{};
@@ -4129,19 +4156,20 @@ int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double
     }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
-    if (op == 0 && g.fc) NS_LAUNCH((k_apply<0, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
-    else if (op == 0) NS_LAUNCH((k_apply<0, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
-    else if (g.fc) NS_LAUNCH((k_apply<1, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
-    else NS_LAUNCH((k_apply<1, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows);
+    if (op == 0 && g.fc) NS_LAUNCH((k_apply<0, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows, stop);
+    else if (op == 0) NS_LAUNCH((k_apply<0, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows, stop);
+    else if (g.fc) NS_LAUNCH((k_apply<1, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows, stop);
+    else NS_LAUNCH((k_apply<1, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, x, y, q, part, rows, stop);
     return (int)(cg.x * cg.y);
 }
 
-void launch_diag_pc(int op, const Geo& g, const Coef& c, double alpha, const double* q, double* z, hipStream_t st) {
+void launch_diag_pc(int op, const Geo& g, const Coef& c, double alpha, const double* q, double* z, hipStream_t st,
+                    const double* stop) {
     const dim3 cg = cell_grid(g);
-    if (op == 0 && g.fc) NS_LAUNCH((k_diag_pc<0, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
-    else if (op == 0) NS_LAUNCH((k_diag_pc<0, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
-    else if (g.fc) NS_LAUNCH((k_diag_pc<1, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
-    else NS_LAUNCH((k_diag_pc<1, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z);
+    if (op == 0 && g.fc) NS_LAUNCH((k_diag_pc<0, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z, stop);
+    else if (op == 0) NS_LAUNCH((k_diag_pc<0, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z, stop);
+    else if (g.fc) NS_LAUNCH((k_diag_pc<1, TopoMask>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z, stop);
+    else NS_LAUNCH((k_diag_pc<1, TopoRect>), cg, dim3(64, 4), 0, st, g, c, alpha, q, z, stop);
 }
 
 int launch_bicg_vec(int mode, KrylovArgs a, hipStream_t st) {
@@ -4158,7 +4186,11 @@ int launch_bicg_vec(int mode, KrylovArgs a, hipStream_t st) {
 }
 
 void launch_bicg_scal(int stage, const double* d, double n, double* sc, hipStream_t st) {
-    NS_LAUNCH(k_bicg_scal, dim3(1), dim3(1), 0, st, stage, d, n, sc);
+    NS_LAUNCH(k_bicg_scal, dim3(1), dim3(1), 0, st, stage, d, n, sc, 0.0, 0.0, stage == KSC_RESET ? -1 : 0);
+}
+void launch_bicg_start(double* sc, double thr, double b2, int maxit, hipStream_t st) {
+    NS_LAUNCH(k_bicg_scal, dim3(1), dim3(1), 0, st, (int)KSC_RESET, (const double*)nullptr, 0.0, sc, thr, b2,
+              std::max(maxit, 0));
 }
 
 bool correct_streams(const Geo& g) {

@@ -76,7 +76,8 @@ enum {
     S_RESL = 20,    // 2
     S_AUXL = 22,    // 2
     S_MML = 24,     // 4
-    S_NUM = 28
+    S_KRY = 28,     // 7: (r5) a BiCGStab batch's verdict for the host (KS_STOP, KS_BRK, KS_IT, KS_R2, r.r, alpha, omega)
+    S_NUM = 35
 };
 constexpr int BUS_NV = 10, BUS_NSUM = 6;
 
@@ -302,6 +303,7 @@ struct ns_solver {
     bool fps_defer = false, mean_pend = false;
     const double *m0e = nullptr, *m0b = nullptr, *m0g = nullptr, *m0a = nullptr;
     double fps_res = -1.0;       // the last checked solve's relative residual
+    int kpred[3] = {1, 1, 1};    // (r5) the last BiCGStab solve's iterations: Poisson, Helmholtz u, v (bicgstab's batch)
     // r5, multi-rank rectangles: the Helmholtz check's collective is an allgather of every rank's
     // S_HBNL .. S_MML (bus()): K1's norms and the previous step's K5 min / max ride on it, so neither
     // takes a collective of its own (NSGPU_BUS=0: the per-reduction all-reduces, A/B); bus_mem holds
@@ -1668,15 +1670,18 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
     a.sc = s->ksc;
     a.part = s->part;
     double* d = s->ksc + nsg::KS_D;
+    const double* stop = s->ksc + nsg::KS_STOP;
     // the projection's cell count (k_bicg_scal: mean = sum / n); infinite = no projection
     const double n = ks.op == 0 ? s->ncells : INFINITY;
     auto reduce = [&](int nb, int nv) -> int {
         nsg::launch_reduce_sum(s->part, nb, nv, d, s->st);
         return allreduce(s, d, nv, ncclSum);
     };
-    auto apply = [&](double* x, double* y, const double* q) -> int {
+    // (r5) the grid apply / Jacobi launches of a converged batch do nothing (KS_STOP); the initial residual's
+    // apply always runs
+    auto apply = [&](double* x, double* y, const double* q, bool gate = true) -> int {
         CHK(halo(s, {x}, 1));
-        const int nb = nsg::launch_apply(ks.op, s->g, s->c, ks.alpha, x, y, q, s->part, s->st);
+        const int nb = nsg::launch_apply(ks.op, s->g, s->c, ks.alpha, x, y, q, s->part, s->st, gate ? stop : nullptr);
         return reduce(nb, 2);
     };
     // timed level-0 passes of the preconditioner (events 0 .. tn), read after each host sync
@@ -1685,48 +1690,19 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
     auto precond = [&](double* q, int k) -> int {   // K[k] = M^-1 q
         if (ks.mg && ks.op == 0 && s->fps_pc) return fps_precond(s, q, s->kv[k], s->kv[8]);
         if (ks.mg) return mg_precond(s, q, s->kv[k], s->kv[8], timed ? &tn : nullptr);
-        nsg::launch_diag_pc(ks.op, s->g, s->c, ks.alpha, q, s->kv[k], s->st);
+        nsg::launch_diag_pc(ks.op, s->g, s->c, ks.alpha, q, s->kv[k], s->st, stop);
         return 0;
     };
     // r = P(b - shift - A x), r0 = r, p = v = 0 (also the restart after a breakdown)
     auto init = [&]() -> int {
-        CHK(apply(a.x, a.v, nullptr));
+        CHK(apply(a.x, a.v, nullptr, false));
         nsg::launch_bicg_scal(nsg::KSC_MEAN, d, n, s->ksc, s->st);
         CHK(reduce(nsg::launch_bicg_vec(nsg::KV_INIT, a, s->st), 3));
         nsg::launch_bicg_scal(nsg::KSC_INIT, d, n, s->ksc, s->st);
         return 0;
     };
-    CHK(init());
-    int it = 0, restarts = 0;
-    for (;;) {
-        // ||r||^2 and the breakdown flag to the host: the convergence test (KSPSolve's rtol)
-        HIPCHK(hipMemcpyAsync(s->scal + S_AUX, d, sizeof(double), hipMemcpyDeviceToDevice, s->st));
-        HIPCHK(hipMemcpyAsync(s->scal + S_AUX + 1, s->ksc + nsg::KS_BRK, sizeof(double), hipMemcpyDeviceToDevice, s->st));
-        if (s->verbose) HIPCHK(hipMemcpyAsync(s->scal + S_AUX + 2, s->ksc + nsg::KS_ALPHA, 2 * sizeof(double), hipMemcpyDeviceToDevice, s->st));
-        CHK(fetch(s));
-        for (int k = 0; k < tn; k++) {
-            float ms = 0.f;
-            HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
-            if (s->evtag[k]) { ks.stt->t_restrict_kernel_ms += ms; ks.stt->n_restrict_kernels++; }
-            else { ks.stt->t_poisson_kernel_ms += ms; ks.stt->n_poisson_kernels++; }
-        }
-        tn = 0;
-        const double r2 = s->hs[S_AUX], b2 = ks.b2;
-        *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
-        if (s->verbose)
-            fprintf(stderr, "nsgpu %s (bicgstab): it %d rel. residual %.3e (alpha %.3e omega %.3e%s)\n", ks.name, it,
-                    *res, s->hs[S_AUX + 2], s->hs[S_AUX + 3], s->hs[S_AUX + 1] != 0.0 ? ", breakdown: restart" : "");
-        if (!std::isfinite(r2) || (b2 > 0 && r2 > 1e16 * b2)) {
-            set_err("%s (BiCGStab) diverged: relative residual %g after %d iterations", ks.name, *res, it);
-            *its = it;
-            return NS_EDIVERGE;
-        }
-        if (r2 <= tol2 * b2 || r2 == 0.0 || it >= maxit) break;
-        if (s->hs[S_AUX + 1] != 0.0) {
-            if (++restarts > 50) { set_err("BiCGStab (%s) broke down 50 times", ks.name); *its = it; return NS_EDIVERGE; }
-            CHK(init());
-            continue;
-        }
+    auto iteration = [&]() -> int {
+        nsg::launch_bicg_scal(nsg::KSC_CHECK, d, n, s->ksc, s->st);      // (the loop head's test, on the device)
         nsg::launch_bicg_scal(nsg::KSC_RHO, d, n, s->ksc, s->st);        // beta, rho
         nsg::launch_bicg_vec(nsg::KV_P, a, s->st);                        // p = r + beta (p - omega v)
         CHK(precond(a.p, 6));                                             // ph = M^-1 p
@@ -1739,11 +1715,65 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
         CHK(apply(a.sh, a.t, nullptr));                                   // y = A sh
         nsg::launch_bicg_scal(nsg::KSC_MEAN, d, n, s->ksc, s->st);
         CHK(reduce(nsg::launch_bicg_vec(nsg::KV_T, a, s->st), 3));       // t = P y; t.s, t.t (3-wide partials)
-        nsg::launch_bicg_scal(nsg::KSC_OMEGA, d, n, s->ksc, s->st);
+        nsg::launch_bicg_scal(nsg::KSC_OMEGA, d, n, s->ksc, s->st);      // omega; KS_IT + 1
         CHK(reduce(nsg::launch_bicg_vec(nsg::KV_X, a, s->st), 3));       // x, r; r.r, r0.r, sum r
-        it++;
+        return 0;
+    };
+    // (r5) the convergence test runs on the device at every iteration's head (KSC_CHECK) and freezes the rest of a
+    // batch once it stops; the host reads the verdict once per batch -- the first sized from the previous solve of
+    // this kind (Poisson, Helmholtz u, v), whose preconditioner launches cost a full iteration when frozen only for
+    // the Poisson solve (its multigrid / box-direct preconditioners are not gated): one short there, one over for
+    // the gated Helmholtz solves; then 1 (Poisson) or 2 (Helmholtz) at a time.  NSGPU_VERBOSE: every iteration
+    const int kind = ks.op == 0 ? 0 : (ks.x == s->arr[NS_ARR_U] ? 1 : 2);
+    const bool gated = !ks.mg;
+    int batch = s->verbose ? 1 : std::max(1, gated ? s->kpred[kind] + 1 : s->kpred[kind] - 1);
+    nsg::launch_bicg_start(s->ksc, tol2 * ks.b2, ks.b2, maxit, s->st);
+    CHK(init());
+    int restarts = 0;
+    for (;;) {
+        for (int q = 0; q < batch; q++) CHK(iteration());
+        nsg::launch_bicg_scal(nsg::KSC_CHECK, d, n, s->ksc, s->st);
+        // KS_STOP, KS_R2 / d[0], KS_IT, KS_BRK to the host (one sync per batch)
+        HIPCHK(hipMemcpyAsync(s->scal + S_KRY, s->ksc + nsg::KS_STOP, sizeof(double), hipMemcpyDeviceToDevice, s->st));
+        HIPCHK(hipMemcpyAsync(s->scal + S_KRY + 1, s->ksc + nsg::KS_BRK, sizeof(double), hipMemcpyDeviceToDevice, s->st));
+        HIPCHK(hipMemcpyAsync(s->scal + S_KRY + 2, s->ksc + nsg::KS_IT, sizeof(double), hipMemcpyDeviceToDevice, s->st));
+        HIPCHK(hipMemcpyAsync(s->scal + S_KRY + 3, s->ksc + nsg::KS_R2, sizeof(double), hipMemcpyDeviceToDevice, s->st));
+        if (s->verbose) {
+            HIPCHK(hipMemcpyAsync(s->scal + S_KRY + 4, d, sizeof(double), hipMemcpyDeviceToDevice, s->st));
+            HIPCHK(hipMemcpyAsync(s->scal + S_KRY + 5, s->ksc + nsg::KS_ALPHA, 2 * sizeof(double), hipMemcpyDeviceToDevice, s->st));
+        }
+        CHK(fetch(s));
+        for (int k = 0; k < tn; k++) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, s->ev[2 * k], s->ev[2 * k + 1]));
+            if (s->evtag[k]) { ks.stt->t_restrict_kernel_ms += ms; ks.stt->n_restrict_kernels++; }
+            else { ks.stt->t_poisson_kernel_ms += ms; ks.stt->n_poisson_kernels++; }
+        }
+        tn = 0;
+        const bool stopped = s->hs[S_KRY] != 0.0, brk = s->hs[S_KRY + 1] != 0.0;
+        const int it = (int)s->hs[S_KRY + 2];
+        const double r2 = stopped ? s->hs[S_KRY + 3] : s->hs[S_KRY + 4], b2 = ks.b2;
+        *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
+        if (s->verbose)
+            fprintf(stderr, "nsgpu %s (bicgstab): it %d rel. residual %.3e (alpha %.3e omega %.3e%s)\n", ks.name, it,
+                    *res, s->hs[S_KRY + 5], s->hs[S_KRY + 6], brk ? ", breakdown: restart" : "");
+        *its = it;
+        if (!stopped) {
+            batch = s->verbose ? 1 : (gated ? 2 : 1);
+            continue;
+        }
+        if (!std::isfinite(r2) || (b2 > 0 && r2 > 1e16 * b2)) {
+            set_err("%s (BiCGStab) diverged: relative residual %g after %d iterations", ks.name, *res, it);
+            return NS_EDIVERGE;
+        }
+        if (r2 <= tol2 * b2 || r2 == 0.0 || it >= maxit) break;
+        // (stopped on a breakdown)
+        if (++restarts > 50) { set_err("BiCGStab (%s) broke down 50 times", ks.name); return NS_EDIVERGE; }
+        nsg::launch_bicg_scal(nsg::KSC_RESET, d, n, s->ksc, s->st);
+        CHK(init());
+        batch = 1;
     }
-    *its = it;
+    s->kpred[kind] = *its;
     return 0;
 }
 
