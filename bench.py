@@ -103,6 +103,8 @@ def parse(argv=None):
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-jacobi", action="store_true",
+                    help="skip the Jacobi-sweep roofline leg (kernel traces of the step alone)")
     ap.add_argument("--sync-monitor", action="store_true",
                     help="ns_step (host sync at every step's end) instead of ns_step_async")
     ap.add_argument("--transport", choices=("rccl", "host"), default=os.environ.get("NSBENCH_TRANSPORT", "rccl"),
@@ -472,7 +474,7 @@ def run(args, rank, world, local, wd):
     # the north star's roofline kernel: one Jacobi sweep of this rank's slab (random phi, b;
     # 10 warm-up + 50 timed launches, HIP events), single rank only
     jacobi = jacobi32 = None
-    if world == 1 and not channel:
+    if world == 1 and not channel and not args.no_jacobi:
         js = nsa.GpuSolver(nsa.cavity(n), dt, re, poisson=nsa.NS_POISSON_JACOBI, omega=1.0, device=device)
         js.fill_random(0x5EED)
         t = js.time_poisson(10, 50)

@@ -748,12 +748,17 @@ __device__ inline double piv_next(const FpsArgs& a, int gi, int k, double mu, do
 // (r5) the pivots of a mode pair's row without the fp64 division chain where they are tabled (FpsArgs::ptab):
 // a wave whose modes all converge (k >= kfast) reads 1 / p of rows < prow from the table and the converged
 // 1 / p after (pinf); the last global row (no east neighbour) and the slow modes keep piv_next
+// (pb: the first global row of this mode block's fixed point -- 0 with the table, prowb's entry without)
+__device__ inline int fps_prow_block(const FpsArgs& a) {
+    if (a.prowb) return a.prowb[blockIdx.x];
+    return a.ptab && (int)(blockIdx.x * 128) >= a.kfast ? 0 : (1 << 30);
+}
 __device__ inline void piv_pair(const FpsArgs& a, bool fast, double2 pinf, int gi, int k0, const double (&mu)[2],
-                                double (&r)[2], double pw, double pe, double pem, double& g0, double& g1) {
-    if (fast && gi != a.nx - 1) {
+                                double (&r)[2], double pw, double pe, double pem, double& g0, double& g1, int pb) {
+    if (fast && gi >= pb && gi != a.nx - 1) {
         g0 = pw * r[0];
         g1 = pw * r[1];
-        const double2 t = gi < a.prow ? ld2(a.ptab + (size_t)gi * a.ld + k0) : pinf;
+        const double2 t = a.ptab && gi < a.prow ? ld2(a.ptab + (size_t)gi * a.ld + k0) : pinf;
         r[0] = t.x;
         r[1] = t.y;
     } else {
@@ -1168,14 +1173,15 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1b(FpsArgs a, const double*
         for (int t = 0; t < FPS_M; t++)
             if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0, s0);
         double r[2] = {r0.x, r0.y};
-        const bool fast = a.ptab && (int)(blockIdx.x * 128) >= a.kfast;
+        const int pb = fps_prow_block(a);
+        const bool fast = pb < a.nx;
         const double2 pinf = fast ? ld2(a.pinf + k0) : double2{0.0, 0.0};
 #pragma unroll
         for (int t = 0; t < FPS_M; t++) {
             if (t < rows) {
                 const int gi = a.i0 + li0 + t;
                 double g0, g1;
-                piv_pair(a, fast, pinf, gi, k0, mu, r, cr.pw[t], cr.pe[t], cr.pem[t], g0, g1);
+                piv_pair(a, fast, pinf, gi, k0, mu, r, cr.pw[t], cr.pe[t], cr.pem[t], g0, g1, pb);
                 E[0] = fma(-g0, E[0], yv[t].x);
                 E[1] = fma(-g1, E[1], yv[t].y);
                 P[0] = -g0 * P[0];
@@ -1290,14 +1296,15 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
     const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
     double r[2] = {r0.x, r0.y}, y[2] = {yin.x, yin.y};
     double2 rv[FPS_M];
-    const bool fast = a.ptab && (int)(blockIdx.x * 128) >= a.kfast;
+    const int pb = fps_prow_block(a);
+    const bool fast = pb < a.nx;
     const double2 pinf = fast ? ld2(a.pinf + k0) : double2{0.0, 0.0};
 #pragma unroll
     for (int t = 0; t < FPS_M; t++) {
         if (t < rows) {
             const int gi = a.i0 + li0 + t;
             double g0, g1;
-            piv_pair(a, fast, pinf, gi, k0, mu, r, cr.pw[t], cr.pe[t], cr.pem[t], g0, g1);
+            piv_pair(a, fast, pinf, gi, k0, mu, r, cr.pw[t], cr.pe[t], cr.pem[t], g0, g1, pb);
             y[0] = fma(-g0, y[0], yv[t].x);
             y[1] = fma(-g1, y[1], yv[t].y);
             yv[t] = double2{y[0], y[1]};

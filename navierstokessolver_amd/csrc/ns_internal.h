@@ -331,6 +331,10 @@ struct FpsArgs {
     // ptab null: none
     const double *ptab = nullptr, *pinf = nullptr;
     int prow = 0, kfast = 1 << 30;
+    // (r5, default: NSGPU_FPS_PTAB=2) no table: per 128-mode block the global row from which all its modes' pivots
+    // sit at their fixed point (prowb, ld / 128 ints; 1 << 30: never) -- rows before it keep the division, rows
+    // after it take pinf.  The table's reads (up to 1024 rows x ld) cost t1b more than the divisions they saved
+    const int* prowb = nullptr;
 };
 // the other ranks' part of a multi-rank scan (k_fps_scan / k_fps_scan_seg): gathered aggregates, P slots of
 // `stride` doubles (E | Pi, or X | R, and forward with the deferred mean (sum b, sum b^2) at 2 ld); a1 / ge1:

@@ -2075,14 +2075,17 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     // the table there and the converged value after it, instead of one fp64 division per row and mode
     // (NSGPU_FPS_PTAB=0: divisions everywhere, A/B)
     std::vector<double> ptab, pinf;
+    std::vector<int> prowb;
     int prow = 0, kfast = 1 << 30;
     {
+        // NSGPU_FPS_PTAB: 0 divisions everywhere, 1 the table (A/B), 2 (default) per 128-mode block its fixed-point row
         const char* pe_env = getenv("NSGPU_FPS_PTAB");
-        const int PRMAX = std::min(g.nx - 1, 1024);
-        if (!(pe_env && std::atoi(pe_env) == 0) && N > 128 && PRMAX > 64) {
+        const int mode = pe_env ? std::atoi(pe_env) : 2;
+        const int PRMAX = std::min(g.nx - 1, mode == 1 ? 1024 : 4096);
+        if (mode != 0 && N > 128 && PRMAX > 64) {
             std::vector<double> rr(N, 0.0);
             std::vector<int> conv(N, -1);
-            ptab.assign((size_t)PRMAX * ld, 0.0);
+            if (mode == 1) ptab.assign((size_t)PRMAX * ld, 0.0);
             for (int gi = 0; gi < PRMAX; gi++) {
                 const double pem = gi > 0 ? pe[gi - 1] : 0.0;
                 for (int k = 0; k < N; k++) {
@@ -2092,9 +2095,31 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
                     if (conv[k] < 0 && gi > 1 && std::fabs(rn - rr[k]) <= 4 * 2.220446049250313e-16 * std::fabs(rn))
                         conv[k] = gi;
                     rr[k] = rn;
-                    ptab[(size_t)gi * ld + k] = rn;
+                    if (mode == 1) ptab[(size_t)gi * ld + k] = rn;
                 }
             }
+            if (mode == 2) {
+                // (each block's row: the last of its modes to converge, + 1; a block with a mode that did not
+                // converge within PRMAX rows never takes the fixed point)
+                const int nb = (ld + 127) / 128;
+                prowb.assign(nb, 1 << 30);
+                bool any = false;
+                for (int b = 0; b < nb; b++) {
+                    int mx = 0;
+                    bool ok = b * 128 < N;
+                    for (int k = b * 128; k < std::min(N, (b + 1) * 128) && ok; k++) {
+                        ok = conv[k] >= 0;
+                        mx = std::max(mx, conv[k]);
+                    }
+                    if (ok) { prowb[b] = mx + 1; any = true; }
+                }
+                if (any) {
+                    pinf.assign(ld, 0.0);
+                    for (int k = 0; k < N; k++) pinf[k] = rr[k];
+                } else {
+                    prowb.clear();
+                }
+            } else {
             for (int kf = 128; kf < N; kf += 128) {
                 int mx = 0;
                 bool ok = true;
@@ -2116,9 +2141,11 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
                 ptab.clear();
                 kfast = 1 << 30;
             }
+            }
         }
     }
-    const size_t n_pt = ptab.empty() ? 0 : ptab.size() + (size_t)ld;
+    // (the pivot table and pinf, or pinf and the block rows -- ints, in doubles' room)
+    const size_t n_pt = !ptab.empty() ? ptab.size() + (size_t)ld : (!prowb.empty() ? (size_t)ld + prowb.size() : 0);
     // (r5) ny = 16384: e^{-2 pi i m / 8192}, m < 8192, after the pivot table (the two-half transforms)
     const size_t n_t8 = nsg::fps_log2(N) < 0 ? (size_t)N : 0;
     HIPCHK(hipMalloc(&s->fps_mem, (total + n_pt + n_t8) * sizeof(double)));
@@ -2133,7 +2160,7 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
         s->fps_tw8 = s->fps_mem + total + n_pt;
         HIPCHK(hipMemcpy(s->fps_mem + total + n_pt, t8.data(), n_t8 * sizeof(double), hipMemcpyHostToDevice));
     }
-    if (n_pt) {
+    if (n_pt && !ptab.empty()) {
         double* pt = s->fps_mem + total;
         HIPCHK(hipMemcpy(pt, ptab.data(), ptab.size() * sizeof(double), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(pt + ptab.size(), pinf.data(), (size_t)ld * sizeof(double), hipMemcpyHostToDevice));
@@ -2141,6 +2168,13 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
         a.pinf = pt + ptab.size();
         a.prow = prow;
         a.kfast = kfast;
+    } else if (n_pt) {
+        double* pt = s->fps_mem + total;
+        HIPCHK(hipMemcpy(pt, pinf.data(), (size_t)ld * sizeof(double), hipMemcpyHostToDevice));
+        int* pb = reinterpret_cast<int*>(pt + ld);
+        HIPCHK(hipMemcpy(pb, prowb.data(), prowb.size() * sizeof(int), hipMemcpyHostToDevice));
+        a.pinf = pt;
+        a.prowb = pb;
     }
     double* d = s->fps_mem;
     s->fps_tw = d;
