@@ -477,18 +477,22 @@ static int g_phase = 0;
 //            row pipeline after the exchange instead of a whole strip of L rows;
 // d = depth rounded up to even.  Launch strip row k covers rows [ib, min(ib + L, rend)) with
 // ib = rb0 + k L for k < slo, else rb1 + (k - slo) L; its partial slot is (pbase + k) nsj + sj.
+// (r5) rend0: the end of the low runs (rend but in phase 2, where the low edge band [0, d) may be cut into
+// several runs -- plan_rows' esplit)
 struct RowPlan {
-    int L, slo, nrun, rb0, rb1, rend, pbase;
+    int L, slo, nrun, rb0, rb1, rend, pbase, rend0;
     __device__ __forceinline__ void rows(int run, int& ib, int& ie) const {
         ib = run < slo ? rb0 + run * L : rb1 + (run - slo) * L;
-        ie = min(ib + L, rend);
+        ie = min(ib + L, run < slo ? rend0 : rend);
     }
 };
 
 // host side of RowPlan: the strip rows of the current phase (g_phase) for `nxl` rows in strips of
 // `L` (one resident round), reading `depth` rows beyond their own; returns the pass's strip-row
 // count (partial slots / nsj, the same in every phase) and sets the plan's launch subset
-static int plan_rows(int nxl, int L, int depth, RowPlan* p) {
+// (r5) esplit > 0: phase 2 cuts each edge band into runs of esplit rows (K1's deep edge bands are ~22 rows:
+// one run each left 132 waves walking them one row at a time after the exchange -- 31.7 us at 8192 P8)
+static int plan_rows(int nxl, int L, int depth, RowPlan* p, int esplit = 0) {
     const int d = (depth + 1) & ~1, R = nxl - 2 * d;
     p->pbase = 0;
     p->rb1 = 0;
@@ -498,24 +502,26 @@ static int plan_rows(int nxl, int L, int depth, RowPlan* p) {
         p->nrun = g_phase == 1 ? 0 : n;   // (a slab too thin to split: all of it after the exchange)
         p->slo = n;
         p->rb0 = 0;
-        p->rend = nxl;
+        p->rend = p->rend0 = nxl;
         return n;
     }
     const int n1 = (R + L - 1) / L;
+    const int le = esplit > 0 && esplit < d ? esplit : d, m = (d + le - 1) / le;   // runs per edge band
     if (g_phase == 1) {
         p->nrun = p->slo = n1;
         p->rb0 = d;
-        p->rend = nxl - d;
+        p->rend = p->rend0 = nxl - d;
     } else {
-        p->L = d;
-        p->nrun = 2;
-        p->slo = 1;
+        p->L = le;
+        p->nrun = 2 * m;
+        p->slo = m;
         p->rb0 = 0;
+        p->rend0 = d;
         p->rb1 = nxl - d;
         p->rend = nxl;
         p->pbase = n1;
     }
-    return n1 + 2;
+    return n1 + 2 * m;
 }
 
 static int phase_range(int nxl, int rows, int n, int depth, int* lo, int* hi0) {
@@ -1429,6 +1435,9 @@ __device__ __forceinline__ void rhs_ring_body(const Geo& g, const Coef& c, doubl
 }
 
 constexpr int K1_LMAX = 128;      // k_rhs_s: rows per strip at most (one resident round of strips)
+#ifndef K1_ESPLIT
+#define K1_ESPLIT 4               // (r5) k_rhs_s: rows per run of the edge bands after a slab's exchange (0: one run)
+#endif
 constexpr int RC_K1 = 4;          // k_rhs_s: row tables from row ib-4 (the window-fill steps read ib-4 .. )
 template <bool NT, int SK, bool UY = false>
 __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
@@ -1887,7 +1896,14 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
 // come from the adjacent lanes (the outermost lanes' missing neighbours fall outside
 // the written cone of the same 116-column layout).
 constexpr int SW2 = 120;
-constexpr int BT = 32;   // Helmholtz wall bands (k_helm_band): tile size
+// Helmholtz wall bands (k_helm_band): tile size and rows per thread (A/B: make variant DEFS="-DBAND_BT=52 -DBAND_SEG=8")
+#ifndef BAND_BT
+#define BAND_BT 32
+#endif
+#ifndef BAND_SEG
+#define BAND_SEG 4
+#endif
+constexpr int BT = BAND_BT;
 constexpr int SW2X = 116;
 // rows in flight per wave (prefetch depth) per pass type: each row costs 8 VGPRs (phi, b);
 // the Helmholtz pass (136 VGPRs at 3 rows) and FUSE_P (154) stay at 3 waves/SIMD up to 168
@@ -2961,7 +2977,7 @@ constexpr int BAND_NSW = 3;   // sweeps per launch: a 6-cell cone, within the sl
 // every segment on an even row), so there is no divergence.  One barrier per half-sweep: a
 // half-sweep reads only the other colour (stable) and publishes its own cells.
 __global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
-    constexpr int R = 2 * BAND_NSW, E = BT + 2 * R, NP = E / 2, SEG = 4, NSEG = E / SEG;
+    constexpr int R = 2 * BAND_NSW, E = BT + 2 * R, NP = E / 2, SEG = BAND_SEG, NSEG = E / SEG;
     static_assert(E % SEG == 0 && NP * NSEG <= 256, "band tile layout");
     __shared__ double sp[E][E];
     __shared__ double rw[E][3];   // per staged row: cw, ce, cw + ce + bx
@@ -4057,7 +4073,7 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
             // 4096^2 at 2 waves / SIMD then left 128 of 2176 strips to a second round)
             const long nsi = std::max(1L, resident_waves(kk) / A.nsj);
             const int L = std::min(std::max((int)((g.nxl + nsi - 1) / nsi + 1) & ~1, 8), K1_LMAX);
-            A.nstr = A.nsj * plan_rows(g.nxl, L, depth, &A.P);   // u, v rows ib-2 .. ie+1
+            A.nstr = A.nsj * plan_rows(g.nxl, L, depth, &A.P, K1_ESPLIT);   // u, v rows ib-2 .. ie+1
         }
         const bool inner = A.jhi > 2 && A.ihi > A.ilo;
         if (!inner) A.P.nrun = 0;
@@ -4113,7 +4129,7 @@ static int launch_cell_s(CellStreamArgs A, hipStream_t st) {
         const int nsi = (A.g.nxl + L - 1) / L;
         int lo = 0, hi0 = 0;
         const int nrun = phase_range(A.g.nxl, L, nsi, 1, &lo, &hi0);
-        A.P.L = L; A.P.rb0 = 0; A.P.rend = A.g.nxl;
+        A.P.L = L; A.P.rb0 = 0; A.P.rend = A.P.rend0 = A.g.nxl;
         A.P.nrun = nrun;
         A.P.slo = lo;
         A.P.rb1 = hi0 * L;   // launch strip row k >= lo is strip row hi0 + (k - lo)

@@ -80,7 +80,60 @@ __global__ __launch_bounds__(256) void k_4r4w(const double2* __restrict__ u, con
     }
 }
 
+// (r5) K5's stream mix: read phi, u*, v*, write u, v -- 3 reads + 2 writes of 16 B per lane (40 B/cell)
+template <int U, bool NTS>
+__global__ __launch_bounds__(256) void k_3r2w(const double2* __restrict__ p, const double2* __restrict__ us,
+                                              const double2* __restrict__ vs, double2* __restrict__ u,
+                                              double2* __restrict__ v, size_t n2) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i0 = blockIdx.x * 256 + threadIdx.x; i0 < n2; i0 += stride * U) {
+        double2 a[U], b[U], c[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const size_t i = i0 + k * stride;
+            if (i < n2) { a[k] = p[i]; b[k] = us[i]; c[k] = vs[i]; }
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const size_t i = i0 + k * stride;
+            if (i < n2) {
+                const double2 x = make_double2(b[k].x - 0.5 * a[k].x, b[k].y - 0.5 * a[k].y);
+                const double2 y = make_double2(c[k].x - 0.5 * a[k].y, c[k].y - 0.5 * a[k].x);
+                if (NTS) {
+                    __builtin_nontemporal_store(x.x, &u[i].x); __builtin_nontemporal_store(x.y, &u[i].y);
+                    __builtin_nontemporal_store(y.x, &v[i].x); __builtin_nontemporal_store(y.y, &v[i].y);
+                } else { u[i] = x; v[i] = y; }
+            }
+        }
+    }
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "k5") {   // K5's 3-read / 2-write mix at 4096^2 and 8192^2
+        for (int n : {4096, 8192}) {
+            const size_t N = (size_t)n * n;
+            double* f[5];
+            for (auto& x : f) { hipMalloc(&x, N * 8); hipMemset(x, 0, N * 8); }
+            hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+            auto timeit = [&](auto launch, const char* name, int g) {
+                for (int w = 0; w < 5; w++) launch();
+                std::vector<float> ts;
+                for (int it = 0; it < 20; it++) {
+                    hipEventRecord(e0); launch(); hipEventRecord(e1); hipEventSynchronize(e1);
+                    float ms; hipEventElapsedTime(&ms, e0, e1); ts.push_back(ms);
+                }
+                std::sort(ts.begin(), ts.end());
+                printf("n=%d 3R2W %-10s grid=%d median %8.1f us  %7.1f GB/s (40 B/cell)\n", n, name, g, ts[10] * 1e3,
+                       40.0 * N / (ts[10] * 1e-3) / 1e9);
+            };
+            for (int g : {2048, 4096, 8192}) {
+                timeit([&] { hipLaunchKernelGGL((k_3r2w<2, false>), dim3(g), dim3(256), 0, 0, (const double2*)f[0], (const double2*)f[1], (const double2*)f[2], (double2*)f[3], (double2*)f[4], N / 2); }, "plain", g);
+                timeit([&] { hipLaunchKernelGGL((k_3r2w<2, true>), dim3(g), dim3(256), 0, 0, (const double2*)f[0], (const double2*)f[1], (const double2*)f[2], (double2*)f[3], (double2*)f[4], N / 2); }, "ntstore", g);
+            }
+            for (auto x : f) hipFree(x);
+        }
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "k1") {   // K1's 4-read / 4-write mix at 4096^2 and 8192^2
         for (int n : {4096, 8192}) {
             const size_t N = (size_t)n * n;
@@ -107,7 +160,7 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
-    for (int n : {4096, 8192}) {
+    for (int n : {4096, 8192, 16384}) {
         const size_t N = (size_t)n * n;
         double *a, *b, *c;
         hipMalloc(&a, N * 8); hipMalloc(&b, N * 8); hipMalloc(&c, N * 8);
