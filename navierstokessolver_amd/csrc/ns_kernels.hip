@@ -962,6 +962,8 @@ struct StreamArgs {
     // [ib, min(ib + L, rend)) with ib = rb0 + k L for k < slo, else rb1 + (k - slo) L; its
     // residual partials go to slot (pbase + k) nsj + j; nrun strip rows in all
     int slo, nrun, rb0, rb1, rend, pbase;
+    // (r5) the launch rows whose residual is summed (a deep-ghost launch: its slab's own rows; Geo::sr0 / sr1)
+    int sr0, sr1;
     // k_sweep2<..., FUSE_UV>: two fields in one launch (the multi-rank Helmholtz pair pass, u and
     // v): waves [nstr, 2 nstr) take in2 / out2 / b2 and write their partials to part2
     const double* in2;
@@ -2447,7 +2449,7 @@ __device__ __forceinline__ double sweep3_strip(const StreamArgs& a, const double
                 double q0, q1;
                 relax<1>(F1.x, Fm.x, Fp.x, lf, F1.y, B7.x, cw, ce, cs0, cn0, d0, 0.0, alpha, q0);
                 relax<1>(F1.y, Fm.y, Fp.y, F1.x, rt, B7.y, cw, ce, cs1, cn1, d1, 0.0, alpha, q1);
-                res += (o0 ? q0 * q0 : 0.0) + (o1 ? q1 * q1 : 0.0);
+                if (m7 >= a.sr0 && m7 < a.sr1) res += (o0 ? q0 * q0 : 0.0) + (o1 ? q1 * q1 : 0.0);
             }
         }
     };
@@ -4330,6 +4332,8 @@ static StreamArgs stream_args(const Geo& g, const Coef& c, const double* in, dou
     a.nx = g.nx; a.ny = g.ny; a.i0 = g.i0; a.nxl = g.nxl; a.ld = g.ld;
     a.nsj = (g.ny + SW - 1) / SW;
     a.part = part;
+    a.sr0 = g.sr0;
+    a.sr1 = g.sr1;
     a.nt = 1;
     a.ntl = -1;   // per kernel (non-temporal in the prolongation pass only)
     return a;

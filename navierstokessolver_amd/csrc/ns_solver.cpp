@@ -311,10 +311,10 @@ struct ns_solver {
     bool bus = false;
     double* bus_mem = nullptr;
     // r5, multi-rank rectangles on the direct solve: DEEP ghost rows.  K1 computes its rows and deep_e =
-    // 7 + 6 R rows of each neighbour's slab (R: the wall bands' 3-sweep launches), its exchange carrying u,
+    // 8 + 6 R rows of each neighbour's slab (R: the wall bands' 3-sweep launches), its exchange carrying u,
     // v, phi that deep; the band launches then compute 6 rows fewer each and need no exchange, and the
-    // residual 3-sweep pass finds its 7-row cone valid -- one exchange group where r4 had 1 + R + 1
-    // (deep_geo; NSGPU_DEEP=0: the r4 exchanges, A/B).  hp: the finest planes' ghost rows per side
+    // residual 3-sweep pass finds its 7-row cone valid and computes one neighbour row more, which K3 reads --
+    // one exchange group (K1's) where r4 had 1 + R + 1 + 1 (deep_geo; NSGPU_DEEP=0: the r4 exchanges, A/B).  hp: the finest planes' ghost rows per side
     // (HALO, or deep_e + HALO + 2); cu_ext / u_ext: ghost rows of cu, cv / of u, v (the Helmholtz
     // iterates) known valid now
     int hp = nsg::HALO;
@@ -703,10 +703,22 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                     }
                     CHK(t_begin(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]));
                 }
-                // (r5, deep ghost rows: the wall bands left u, v valid deep enough -- no exchange)
+                // (r5, deep ghost rows: the wall bands left u, v valid deep enough -- no exchange; the residual
+                // 3-sweep pass then also computes one row of each neighbour's slab, so that K3 finds u*, v*'s ghost
+                // row valid and needs no exchange either -- its residual summed over the slab's own rows)
                 const bool valid = s->deep && s->u_ext >= hw;
+                const int ex = valid && w == 3 && part && s->u_ext >= hw + 1 ? 1 : 0;
                 nb = valid ? -1 : 0;
                 auto pass = [&]() {
+                    if (w == 3 && ex) {
+                        int lo = 0;
+                        const int ld = s->g.ld;
+                        const nsg::Geo gk = deep_geo(s, ex, &lo);
+                        return nsg::launch_helm_sweep3(gk, s->c, alpha, s->omega_v, shp(s->arr[NS_ARR_U], lo, ld),
+                                                       shp(s->arr[NS_ARR_V], lo, ld), shp(s->arr[NS_ARR_TMPU], lo, ld),
+                                                       shp(s->arr[NS_ARR_TMPV], lo, ld), shp(s->arr[NS_ARR_RU], lo, ld),
+                                                       shp(s->arr[NS_ARR_RV], lo, ld), s->st, 3, part);
+                    }
                     if (w == 3)
                         return nsg::launch_helm_sweep3(s->g, s->c, alpha, s->omega_v, s->arr[NS_ARR_U], s->arr[NS_ARR_V],
                                                        s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], s->arr[NS_ARR_RU],
@@ -716,7 +728,7 @@ int helm_sweeps(ns_solver* s, double alpha, int n, double* part_first, double* p
                                                    s->arr[NS_ARR_RV], part, s->st, 3);
                 };
                 nb = valid ? pass() : overlapped(s, r, nr, pass);
-                s->u_ext = 0;
+                s->u_ext = ex;
                 if (nb < 0) return nb;
                 if (t2) {
                     CHK(t_end(s, s->hev[2 * s->hn], s->hev[2 * s->hn + 1]));
@@ -853,7 +865,7 @@ int helm_band(ns_solver* s, double alpha) {
     if (s->deep && s->u_ext >= s->deep_e && s->in_step) {
         // (r5) deep ghost rows: round k computes deep_e - 6 (k + 1) rows of each neighbour's slab from the
         // rows K1's exchange brought (u, v) and K1 computed (rhs) -- no exchange; the last round leaves
-        // deep_e - 6 R = 7 valid rows for the residual 3-sweep pass
+        // deep_e - 6 R = 8 valid rows for the residual 3-sweep pass (its 7-row cone + the row it computes for K3)
         const int ld = s->g.ld;
         double *RU = s->arr[NS_ARR_RU], *RV = s->arr[NS_ARR_RV];
         int e = s->deep_e;
@@ -2714,7 +2726,9 @@ int divergence_fps(ns_solver* s) {
     };
     const HaloReq r[2] = {{&s->g, s->arr[NS_ARR_U], 1}, {&s->g, s->arr[NS_ARR_V], 1}};
     int nb;
-    if (!comm_on(s) || !s->overlap || !s->cst) {
+    if (s->deep && s->u_ext >= 1 && s->in_step) {
+        nb = launch(0);   // (r5, deep ghost rows: the residual pass computed u*, v*'s ghost row -- no exchange)
+    } else if (!comm_on(s) || !s->overlap || !s->cst) {
         CHK(halo_reqs(s, r, 2, s->st));
         nb = launch(0);
     } else {
@@ -2743,10 +2757,12 @@ int divergence(ns_solver* s) {
     if (s->fps && s->fps_fuse && s->in_step) return divergence_fps(s);
     s->fps_pre = false;
     const HaloReq r[2] = {{&s->g, s->arr[NS_ARR_U], 1}, {&s->g, s->arr[NS_ARR_V], 1}};
-    const int nb = overlapped(s, r, 2, [&]() {
+    auto launch = [&]() {
         return nsg::launch_div(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_RPHI], s->part,
                                s->st);
-    });
+    };
+    // (r5, deep ghost rows: the residual pass computed u*, v*'s ghost row -- no exchange)
+    const int nb = s->deep && s->u_ext >= 1 && s->in_step ? launch() : overlapped(s, r, 2, launch);
     if (nb < 0) return nb;
     return div_mean(s, nb);
 }
@@ -2861,6 +2877,7 @@ int correct(ns_solver* s) {
     s->k5_spec = 0;
     std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
     std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
+    s->u_ext = 0;   // (the corrected u, v: the slab's own rows)
     return 0;
 }
 
@@ -3264,7 +3281,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         // (r5) deep ghost rows (ns_solver::deep): multi-rank rectangles on the direct solve with the wall bands and
         // the residual 3-sweep pass, every rank's slab at least deep_e + 3 rows (one neighbour feeds the exchange)
         const char* de = getenv("NSGPU_DEEP");
-        const int R = std::max(1, s->band_sweeps / 3), E1 = 7 + 6 * R;
+        // (E1 = 8 + 6 R: the residual pass's 7-row cone plus the one row of each neighbour it computes for K3)
+        const int R = std::max(1, s->band_sweeps / 3), E1 = 8 + 6 * R;
         bool ok = p->nranks > 1 && !masked && s->fps && s->helm_band && s->sweep3 && s->sweep3_res && s->triple &&
                   !(de && std::atoi(de) == 0);
         for (int q = 0; q < p->nranks && ok; q++) {
