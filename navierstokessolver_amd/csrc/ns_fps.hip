@@ -737,7 +737,9 @@ __device__ inline double piv_next(const FpsArgs& a, int gi, int k, double mu, do
                                   double pem, double& g) {
     const bool oe = a.outE && gi == a.nx - 1;
     g = (oe ? -0.5 * mu : pw) * rprev;
-    const double p = (oe ? mu : -(pw + pe) + mu) - g * pem;
+    // (r5: an explicit fma -- fps_setup's host recurrences use the same one, so host and device pivots are the
+    // same bits and the block fixed points of FpsArgs::prowb are exact)
+    const double p = fma(-g, pem, oe ? mu : -(pw + pe) + mu);
     return (a.pin && k == 0 && gi == a.nx - 1) ? 0.0 : 1.0 / p;
 }
 

@@ -2060,7 +2060,7 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
         const bool oe = a.outE && gi == g.nx - 1;
         for (int k = 0; k < N; k++) {
             const double gg = (oe ? -0.5 * h[4 * N + k] : pw[gi]) * r[k];
-            const double p = (oe ? h[4 * N + k] : -(pw[gi] + pe[gi]) + h[4 * N + k]) - gg * pem;
+            const double p = std::fma(-gg, pem, oe ? h[4 * N + k] : -(pw[gi] + pe[gi]) + h[4 * N + k]);   // (piv_next's)
             r[k] = (k == 0 && gi == g.nx - 1) ? 0.0 : 1.0 / p;
             if (li >= 0) {
                 crp[(size_t)t * N + k] = r[k];
@@ -2097,15 +2097,22 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
         if (mode != 0 && N > 128 && PRMAX > 64) {
             std::vector<double> rr(N, 0.0);
             std::vector<int> conv(N, -1);
+            std::vector<char> left(N, 0);
             if (mode == 1) ptab.assign((size_t)PRMAX * ld, 0.0);
             for (int gi = 0; gi < PRMAX; gi++) {
                 const double pem = gi > 0 ? pe[gi - 1] : 0.0;
                 for (int k = 0; k < N; k++) {
                     const double gg = pw[gi] * rr[k];
-                    const double pv = -(pw[gi] + pe[gi]) + h[4 * N + k] - gg * pem;
+                    const double pv = std::fma(-gg, pem, -(pw[gi] + pe[gi]) + h[4 * N + k]);
                     const double rn = 1.0 / pv;
-                    if (conv[k] < 0 && gi > 1 && std::fabs(rn - rr[k]) <= 4 * 2.220446049250313e-16 * std::fabs(rn))
-                        conv[k] = gi;
+                    // (mode 2: the exact fixed point -- the recurrence returns the same bits from here on, so the
+                    // skipped divisions change nothing; mode 1: within 4 ulp)
+                    const bool fixed = mode == 2 ? rn == rr[k] : std::fabs(rn - rr[k]) <= 4 * 2.220446049250313e-16 * std::fabs(rn);
+                    if (conv[k] < 0 && !left[k] && gi > 1 && fixed) conv[k] = gi;
+                    if (mode == 2 && conv[k] >= 0 && rn != rr[k]) {   // (left it again -- an oscillation: never fast)
+                        conv[k] = -1;
+                        left[k] = 1;
+                    }
                     rr[k] = rn;
                     if (mode == 1) ptab[(size_t)gi * ld + k] = rn;
                 }
@@ -2215,7 +2222,7 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
             double rp = 0.0;
             for (int gi = 0; gi < nx; gi++) {
                 const double gg = pw[gi] * rp, pem = gi > 0 ? pe[gi - 1] : 0.0;
-                const double p = -(pw[gi] + pe[gi]) + 0.0 - gg * pem;
+                const double p = std::fma(-gg, pem, -(pw[gi] + pe[gi]) + 0.0);
                 rp = r0[gi] = gi == nx - 1 ? 0.0 : 1.0 / p;   // (mode 0's pinned last row, a.pin)
             }
         }
