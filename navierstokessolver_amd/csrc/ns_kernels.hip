@@ -4602,8 +4602,10 @@ int launch_helm_sweep3(const Geo& g, const Coef& c, double alpha, double omega, 
     StreamArgs a = stream_args(g, c, which == 2 ? v : u, which == 2 ? vo : uo, which == 2 ? rv : ru, nullptr, alpha,
                                omega, part, true);
     // the batch's last pass with its output residual (7-row cone: 7 ghost rows on slabs); rows in
-    // flight: 3 (114 vs 118 us at 4096^2 with 2; NSGPU_SD3=2: A/B)
-    static const int sd3 = getenv("NSGPU_SD3") ? std::atoi(getenv("NSGPU_SD3")) : 3;
+    // flight: 3 for one field (114 vs 118 us at 4096^2 with 2), (r5) 2 for the two-field launch (its SD3 = 3
+    // build spills 40 B per lane: 207 -> 191 us, bench 16,434 -> 16,725; profiles/r05/sd3/); NSGPU_SD3: A/B
+    static const int sd3e = getenv("NSGPU_SD3") ? std::atoi(getenv("NSGPU_SD3")) : 0;
+    const int sd3 = sd3e ? sd3e : (which == 3 ? 2 : 3);
     if (part) {
         a.nsj = (g.ny + SW3R - 1) / SW3R;
         int nblk = 0;
