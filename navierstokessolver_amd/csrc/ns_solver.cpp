@@ -1814,8 +1814,13 @@ int allgather(ns_solver* s, const double* mine, double* all, size_t n) {
     if (s->loopback) {
         // (a virtual slab: the same ONE ncclAllGather launch as the real call, on the 1-rank communicator --
         // it fills this rank's slot; the others keep their zeros (r4 issued P - 1 self send / recv pairs,
-        // which cost the slab's stream far more than one collective launch does)
-        NCCLCHK(ncclAllGather(mine, all + r * n, n, ncclDouble, s->comm, s->st));
+        // which cost the slab's stream far more than one collective launch does).  (r5) NSGPU_VIRTUAL_COPY=1:
+        // the slot filled by a device copy instead -- the 1-rank RCCL kernel of a 131 KB allgather runs on one
+        // workgroup for ~60 us, a loopback artefact that tools/slab_projection.py's per-collective cost would
+        // count twice)
+        static const bool vcopy = getenv("NSGPU_VIRTUAL_COPY") && std::atoi(getenv("NSGPU_VIRTUAL_COPY")) != 0;
+        if (vcopy) HIPCHK(hipMemcpyAsync(all + r * n, mine, n * 8, hipMemcpyDeviceToDevice, s->st));
+        else NCCLCHK(ncclAllGather(mine, all + r * n, n, ncclDouble, s->comm, s->st));
         return 0;
     }
     NCCLCHK(ncclAllGather(mine, all, n, ncclDouble, s->comm, s->st));

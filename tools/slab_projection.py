@@ -130,7 +130,11 @@ def main():
             r["projected_speedup"] = base / r["projected_ms_per_step"]
             r["projected_speedup_link"] = base / r["projected_ms_per_step_link"]
         print(json.dumps({"n": a.n, "assumptions": {"allreduce_us": a.allreduce_us, "exchange_us": a.exchange_us,
-                                                    "link_gbs": a.link_gbs},
+                                                    "link_gbs": a.link_gbs,
+                                                    # (r5) the measured share's collectives: RCCL's 1-rank loopback
+                                                    # kernels, or device copies (NSGPU_VIRTUAL_COPY=1)
+                                                    "virtual_collectives": "copy" if os.environ.get(
+                                                        "NSGPU_VIRTUAL_COPY", "0") not in ("", "0") else "rccl-loopback"},
                           "speedup": {r["P"]: round(r["projected_speedup"], 2) for r in rows},
                           "speedup_link_bytes_exposed": {r["P"]: round(r["projected_speedup_link"], 2) for r in rows}}),
               flush=True)
