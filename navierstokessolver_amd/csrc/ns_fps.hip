@@ -1294,6 +1294,8 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
         X[0] = fma(br.x, X[0], bx.x);
         X[1] = fma(br.y, X[1], bx.y);
     }
+    // (r5, a.ghost) the slab's last chunk: X is now the solution at the next slab's first row (the backward carry)
+    if (a.ghost && c == a.nch - 1 && a.i0 + a.nxl < a.nx) st2(f + (size_t)a.nxl * a.ld + k0, X[0], X[1]);
     const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
     const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
     double r[2] = {r0.x, r0.y}, y[2] = {yin.x, yin.y};
@@ -1320,6 +1322,12 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
             X[1] = fma(yv[t].y, rv[t].y, -cr.pe[t] * rv[t].y * X[1]);
             st2(f + (size_t)(li0 + t) * a.ld + k0, X[0], X[1]);
         }
+    }
+    // (r5, a.ghost) the slab's first chunk: the previous slab's last row, one more back-substitution step from
+    // its forward value (the forward carry yin) and pivot (r0: 1 / p of the row before the chunk)
+    if (a.ghost && c == 0 && a.i0 > 0) {
+        const double pe = a.pe[a.i0 - 1];
+        st2(f - (ptrdiff_t)a.ld + k0, fma(yin.x, r0.x, -pe * r0.x * X[0]), fma(yin.y, r0.y, -pe * r0.y * X[1]));
     }
 }
 
@@ -1520,8 +1528,7 @@ int fps_log2(int ny) {
 int fps_log2x(int ny) { return ny == N14 ? 14 : fps_log2(ny); }
 
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
-                   const double* tw, const double* wk, hipStream_t st, int oe_pair, double* scratch, const double* tw8) {
-    (void)scratch;
+                   const double* tw, const double* wk, hipStream_t st, int oe_pair, const double* tw8) {
     if (ny == N14) {   // (r5: two 8192-point transforms per row pair)
         if (!tw8) return -1;
         dct14(inverse, in, shift, out, nrows, ld, tw, tw8, wk, st, oe_pair);

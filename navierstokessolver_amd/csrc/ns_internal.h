@@ -335,6 +335,10 @@ struct FpsArgs {
     // sit at their fixed point (prowb, ld / 128 ints; 1 << 30: never) -- rows before it keep the division, rows
     // after it take pinf.  The table's reads (up to 1024 rows x ld) cost t1b more than the divisions they saved
     const int* prowb = nullptr;
+    // (r5) slabs with deep ghost rows: k_fps_t2b also writes the transformed solution of the neighbours' edge rows
+    // (local rows -1 and nxl, where a neighbour exists) -- the row below from the backward carry, the row above
+    // from the forward carry and the slab's own first row -- so the inverse transform gives K5 phi's ghost rows
+    int ghost = 0;
 };
 // the other ranks' part of a multi-rank scan (k_fps_scan / k_fps_scan_seg): gathered aggregates, P slots of
 // `stride` doubles (E | Pi, or X | R, and forward with the deferred mean (sum b, sum b^2) at 2 ld); a1 / ge1:
@@ -353,11 +357,10 @@ int fps_log2(int ny);
 // tw: ny complex e^{-2 pi i m / ny}, wk: ny complex e^{-i pi k / 2 ny} (interleaved doubles)
 // oe_pair (forward only): the row pair whose second row is a NEUMANN outflow row (transformed as b_{n-1} -
 // b_{n-2} / 2, FpsArgs::outE); -1: none
-// (r5) ny = 16384 (fps_log2x): two launches per direction through `scratch` (a plane of the slab's rows;
-// tw8: the 8192-point twiddles); ny <= 8192: scratch / tw8 unused
+// (r5) ny = 16384 (fps_log2x): each row pair as two 8192-point transforms in one launch (tw8: the 8192-point
+// twiddles); ny <= 8192: tw8 unused
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
-                   const double* tw, const double* wk, hipStream_t st, int oe_pair = -1, double* scratch = nullptr,
-                   const double* tw8 = nullptr);
+                   const double* tw, const double* wk, hipStream_t st, int oe_pair = -1, const double* tw8 = nullptr);
 // (r5) log2(ny) also for ny = 16384 (the two-half transforms of launch_fps_dct), else as fps_log2
 int fps_log2x(int ny);
 // K3 fused into the DCT (k_fps_dct_div): b = Div_V(u*, v*) / dt of the slab's rows -> their DCT-II

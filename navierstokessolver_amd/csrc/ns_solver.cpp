@@ -320,6 +320,7 @@ struct ns_solver {
     int hp = nsg::HALO;
     bool deep = false;
     int deep_e = 0, cu_ext = 0, u_ext = 0;
+    int phi_ext = 0;             // (r5) phi's ghost row valid from the direct solve (deep slabs, k_fps_t2b's ghost rows)
     bool fps_strict = false;     // a check failed or came within 1/100 of rtol: check every solve
     bool hbn_pend = false;       // slabs: K1's ||RHS||^2 partial sums await the Helmholtz check's all-reduce
     // K3 fused into the direct solve's DCT (r4, launch_fps_div; NSGPU_FPS_FUSE=0: K3 + the DCT): inside
@@ -1886,12 +1887,8 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         CHK(ensure_kev(s));
         if (!pre) CHK(t_begin(s, s->kev[2], s->kev[3]));
     }
-    // (r5) ny = 16384: the transforms run as two 8192-point halves through a scratch plane -- TMPU, the
-    // Helmholtz sweeps' ping-pong partner, free between the Helmholtz solves and K5 (which writes it whole)
-    double* scr = s->arr[NS_ARR_TMPU];
     if (!pre && nsg::launch_fps_dct(false, s->arr[NS_ARR_RPHI], oe ? nullptr : s->scal + S_SHIFT, F, g.nxl, g.ny,
-                                    g.ld, s->fps_tw, s->fps_wk, s->st, oe ? g.nxl / 2 - 1 : -1, scr,
-                                    s->fps_tw8) < 0) {
+                                    g.ld, s->fps_tw, s->fps_wk, s->st, oe ? g.nxl / 2 - 1 : -1, s->fps_tw8) < 0) {
         set_err("direct Poisson solve: ny = %d is not a supported power of two", g.ny);
         return NS_EINVAL;
     }
@@ -1911,14 +1908,20 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         s->mean_pend = false;
         nsg::launch_fps_mid(fam, F, s->st);
         CHK(fps_scan(s, true));
-        nsg::launch_fps_t2b(fa, F, s->st);
+        nsg::FpsArgs fa2 = fa;
+        fa2.ghost = s->deep && s->in_step ? 1 : 0;   // (r5: phi's ghost rows from the solve -- K5 exchanges none)
+        nsg::launch_fps_t2b(fa2, F, s->st);
     }
+    // (r5) the inverse transform over the ghost rows t2b wrote too (deep slabs): rows [-glo, nxl + ghi)
+    const int glo = s->fps_passes != 3 && s->deep && s->in_step && g.i0 > 0 ? 1 : 0;
+    const int ghi = s->fps_passes != 3 && s->deep && s->in_step && g.i0 + g.nxl < g.nx ? 1 : 0;
+    s->phi_ext = s->fps_passes != 3 && s->deep && s->in_step ? 1 : 0;
     if (t) {
         HIPCHK(hipEventRecord(s->kev[5], s->st));
         CHK(t_begin(s, s->kev[6], s->kev[7]));
     }
-    nsg::launch_fps_dct(true, F, nullptr, s->arr[NS_ARR_PHI], g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st, -1,
-                        scr, s->fps_tw8);
+    nsg::launch_fps_dct(true, F - (ptrdiff_t)glo * g.ld, nullptr, s->arr[NS_ARR_PHI] - (ptrdiff_t)glo * g.ld,
+                        g.nxl + glo + ghi, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st, -1, s->fps_tw8);
     if (t) CHK(t_end(s, s->kev[6], s->kev[7]));
     auto take_times = [&]() -> int {
         if (!t || !stt) return 0;
@@ -1987,6 +1990,7 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     // the direct solve's round-off (e.g. 1e-12 at 2048^2: 1.25e-12) -- every later solve is checked
     // and refined the same way
     if (s->in_step) s->fps_strict = true;
+    s->phi_ext = 0;   // (the refinement below changes phi's own rows only)
     CHK(halo(s, {s->arr[NS_ARR_RPHI]}, 4));   // (the direct solve read no rhs ghost rows)
     int c = 0;
     // (an outflow side: the BiCGStab solve of the true matrix, from this phi)
@@ -2863,7 +2867,16 @@ int correct_launch(ns_solver* s, double* part2) {
     const ExtrapPlan p = extrap_plan(s, s->cur_cycles);
     const bool guess = s->in_step && s->k5_guess && p.branch >= 1 && p.branch <= 3 && nsg::correct_streams(s->g);
     s->guess_ready = 0;
-    const int nb = overlapped(s, r, 1, [&]() {
+    // (r5, deep slabs: the direct solve wrote phi's ghost rows -- no exchange)
+    const bool have = s->deep && s->phi_ext && s->in_step;
+    const int nb = have ? [&]() {
+        if (guess)
+            return nsg::launch_correct_guess(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
+                                             s->arr[NS_ARR_TMPV], s->arr[NS_ARR_PHI], part2, p.h[0], p.h[1], p.h[2], p.c,
+                                             s->arr[NS_ARR_TMP], s->st);
+        return nsg::launch_correct(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
+                                   s->arr[NS_ARR_TMPV], s->arr[NS_ARR_PHI], part2, s->st);
+    }() : overlapped(s, r, 1, [&]() {
         if (guess)
             return nsg::launch_correct_guess(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
                                              s->arr[NS_ARR_TMPV], s->arr[NS_ARR_PHI], part2, p.h[0], p.h[1], p.h[2], p.c,
@@ -3672,7 +3685,7 @@ int ns_get_array(ns_solver* s, int which, double* host) {
 int ns_set_array(ns_solver* s, int which, const double* host) {
     CHK(check_arr(s, which));
     s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
-    s->cu_ext = s->u_ext = 0;   // (r5: the deep ghost rows are stale now)
+    s->cu_ext = s->u_ext = s->phi_ext = 0;   // (r5: the deep ghost rows are stale now)
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);
     HIPCHK(hipMemcpy2DAsync(s->arr[which], (size_t)s->g.ld * 8, host, (size_t)s->g.ny * 8, (size_t)s->g.ny * 8,
@@ -3726,7 +3739,7 @@ int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* 
                   const double* cv0) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
-    s->cu_ext = s->u_ext = 0;   // (r5: the deep ghost rows are stale now)
+    s->cu_ext = s->u_ext = s->phi_ext = 0;   // (r5: the deep ghost rows are stale now)
     if (u) CHK(set_compact(s, NS_ARR_U, u));
     if (v) CHK(set_compact(s, NS_ARR_V, v));
     if (phi) CHK(set_compact(s, NS_ARR_PHI, phi));
@@ -3738,7 +3751,7 @@ int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* 
 int ns_kernel(ns_solver* s, int which, int iters, double* out) {
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
-    s->cu_ext = s->u_ext = 0;   // (r5: a kernel alone writes the slab's own rows: the deep ghost rows are stale)
+    s->cu_ext = s->u_ext = s->phi_ext = 0;   // (r5: a kernel alone writes the slab's own rows: the deep ghost rows are stale)
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);
     const double alpha = s->dt / (2 * s->re);
