@@ -1270,6 +1270,9 @@ __global__ void __launch_bounds__(64) k_fps_mid(FpsArgs a, const double* __restr
 
 // T2b: the chunk's exact values -- the forward recurrence from its carry-in Y_in (ya), the back
 // substitution from its carry-in X_in (the group's, through the later chunks' (BX, BR)) -- in place
+// (GHOST: the deep slabs' variant with a.ghost's two extra rows -- a separate build, since keeping the carries live
+// to the end of the kernel cost the plain one 52 -> 63 us at 4096^2)
+template <bool GHOST>
 __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __restrict__ f) {
     const int lane = threadIdx.x, w = __builtin_amdgcn_readfirstlane(threadIdx.y);
     const int k0 = 2 * (blockIdx.x * 64 + lane);
@@ -1295,7 +1298,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
         X[1] = fma(br.y, X[1], bx.y);
     }
     // (r5, a.ghost) the slab's last chunk: X is now the solution at the next slab's first row (the backward carry)
-    if (a.ghost && c == a.nch - 1 && a.i0 + a.nxl < a.nx) st2(f + (size_t)a.nxl * a.ld + k0, X[0], X[1]);
+    if (GHOST && c == a.nch - 1 && a.i0 + a.nxl < a.nx) st2(f + (size_t)a.nxl * a.ld + k0, X[0], X[1]);
     const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
     const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
     double r[2] = {r0.x, r0.y}, y[2] = {yin.x, yin.y};
@@ -1325,7 +1328,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
     }
     // (r5, a.ghost) the slab's first chunk: the previous slab's last row, one more back-substitution step from
     // its forward value (the forward carry yin) and pivot (r0: 1 / p of the row before the chunk)
-    if (a.ghost && c == 0 && a.i0 > 0) {
+    if (GHOST && c == 0 && a.i0 > 0) {
         const double pe = a.pe[a.i0 - 1];
         st2(f - (ptrdiff_t)a.ld + k0, fma(yin.x, r0.x, -pe * r0.x * X[0]), fma(yin.y, r0.y, -pe * r0.y * X[1]));
     }
@@ -1592,7 +1595,8 @@ void launch_fps_mid(const FpsArgs& a, const double* f, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_mid, dim3((a.ny + 127) / 128, a.ngrp), dim3(64), 0, st, a, f);
 }
 void launch_fps_t2b(const FpsArgs& a, double* f, hipStream_t st) {
-    hipLaunchKernelGGL(k_fps_t2b, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
+    if (a.ghost) hipLaunchKernelGGL(k_fps_t2b<true>, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
+    else hipLaunchKernelGGL(k_fps_t2b<false>, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
 }
 void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_t3, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
