@@ -1329,8 +1329,10 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
     // (r5, a.ghost) the slab's first chunk: the previous slab's last row, one more back-substitution step from
     // its forward value (the forward carry yin) and pivot (r0: 1 / p of the row before the chunk)
     if (GHOST && c == 0 && a.i0 > 0) {
+        // (the carries loaded again -- kept live through the loop they cost the kernel 10 VGPRs)
+        const double2 yi = ld2(a.ya + k0), rq = ld2(a.rp0 + k0);
         const double pe = a.pe[a.i0 - 1];
-        st2(f - (ptrdiff_t)a.ld + k0, fma(yin.x, r0.x, -pe * r0.x * X[0]), fma(yin.y, r0.y, -pe * r0.y * X[1]));
+        st2(f - (ptrdiff_t)a.ld + k0, fma(yi.x, rq.x, -pe * rq.x * X[0]), fma(yi.y, rq.y, -pe * rq.y * X[1]));
     }
 }
 
