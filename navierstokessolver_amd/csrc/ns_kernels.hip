@@ -1685,6 +1685,13 @@ __device__ __forceinline__ double extrap_comb(double a, double x, double b, doub
     return r;
 }
 
+// K5's u, v stores non-temporal (A/B: make variant DEFS=-DK5_NT=1)
+#ifndef K5_NT
+#define K5_NT 0
+#endif
+#ifndef K5_RCP
+#define K5_RCP 0
+#endif
 // K5's rows in flight (A/B: make variant DEFS=-DK5_SD=n)
 #ifndef K5_SD
 #define K5_SD 4
@@ -1823,13 +1830,15 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                     const double V1 = face_val(pc, pe, hE, fe, pc);
                     const double V2 = face_val(pc, ps, e ? s1 : s0, e ? fs1 : fs0, pc);
                     const double V3 = face_val(pc, pn, e ? n1 : n0, e ? fn1 : fn0, pc);
-                    const double gx = (V1 - V0) / hx, gy = (V3 - V2) / (e ? hy1 : hy0);
+                    // (K5_RCP, A/B: the reciprocal spacings instead of the divisions -- within an ulp of GradP's)
+                    const double gx = K5_RCP ? (V1 - V0) * c.rhx[gi] : (V1 - V0) / hx;
+                    const double gy = K5_RCP ? (V3 - V2) * (e ? c.rhy[k1] : c.rhy[k0]) : (V3 - V2) / (e ? hy1 : hy0);
                     un[e] = (e ? x.y : x.x) - A.dt * gx;
                     vn[e] = (e ? y.y : y.x) - A.dt * gy;
                 }
                 if (wr && v1) {
-                    st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(un[0], un[1]), false);
-                    st_stream(A.o1 + (ptrdiff_t)m * ld + c0, make_double2(vn[0], vn[1]), false);
+                    st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(un[0], un[1]), K5_NT);
+                    st_stream(A.o1 + (ptrdiff_t)m * ld + c0, make_double2(vn[0], vn[1]), K5_NT);
                 } else if (wr) {
                     A.o0[(ptrdiff_t)m * ld + c0] = un[0];
                     A.o1[(ptrdiff_t)m * ld + c0] = vn[0];
