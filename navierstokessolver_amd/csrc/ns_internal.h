@@ -277,6 +277,10 @@ struct KrylovArgs {
 // y = A x with A the reference's Poisson matrix (op 0, NEUMANN outflow rows included) or its
 // Helmholtz matrix I - alpha L_V (op 1), on a rectangle or a masked domain; partials
 // (sum y, sum q*y) per block (q may be null); returns the partial count
+// (r5) one red (par 0) or black (par 1) SOR half-sweep of the Helmholtz matrix I - alpha L_V on x in place, or
+// (par 2) the block partials of ||b - A x||^2 (returns their count); masked domains' Helmholtz solve (one rank)
+int launch_helm_rb_mask(const Geo& g, const Coef& c, double alpha, double omega, double* x, const double* b, int par,
+                        double* part, hipStream_t st);
 // (stop: a KS_STOP slot -- the grid kernels then do nothing once it is set; null: always run)
 int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double* x, double* y, const double* q,
                  double* part, hipStream_t st, const double* stop = nullptr);

@@ -3817,6 +3817,44 @@ __global__ __launch_bounds__(256) void k_apply(Geo g, Coef c, double alpha, cons
     block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
 }
 
+// (r5) the masked domain's Helmholtz solve by red-black SOR (one rank; ns_solver.cpp helm_solve), k_apply<1, T>'s
+// operator: par 0 / 1 relaxes the cells of that colour ((gi + j) parity) in place, x += omega (b - A x) / d, a
+// half-sweep reading only the other colour; par 2 leaves x and writes the block partials of ||b - A x||^2
+template <class T>
+__global__ __launch_bounds__(256) void k_helm_rb_mask(Geo g, Coef c, double alpha, double omega, double* __restrict__ x,
+                                                      const double* __restrict__ b, int par, double* __restrict__ part,
+                                                      int rows) {
+    const int j = blockIdx.x * 64 + threadIdx.x;
+    const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
+    double acc[1] = {0.0};
+    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
+        const int gi = g.i0 + li, ld = g.ld;
+        if (par < 2 && ((gi + j) & 1) != par) continue;
+        const T t(g, li, j);
+        if (!t.cell()) continue;
+        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+        const double xc = x[o], hx = c.hx[gi], hy = c.hy[j];
+        const double w2[4] = {1.0 / (hx * hx), 1.0 / (hx * hx), 1.0 / (hy * hy), 1.0 / (hy * hy)};
+        const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
+        const double pn[4] = {c.pw[gi], c.pe[gi], c.ps[j], c.pn[j]};
+        double s = 0.0, d = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (t.in(di[k], dj[k])) {
+                s += pn[k] * (x[o + di[k] * ld + dj[k]] - xc);
+                d -= pn[k];
+            } else if (!t.edge(k).neu) {
+                s += -2.0 * xc * w2[k];
+                d -= 2.0 * w2[k];
+            }
+        }
+        const double r = b[o] - (xc - alpha * s);
+        if (par < 2) x[o] = xc + omega * r / (1.0 - alpha * d);
+        else acc[0] += r * r;
+    }
+    if (par == 2) block_reduce_sum<1>(acc, part + (blockIdx.x + gridDim.x * blockIdx.y));
+}
+
 // z = q / diag(A) (the Jacobi preconditioner of the masked-domain Krylov solves; the
 // outflow rows' diagonal -(sum p) + 1.5 w, oracle diag_poisson / diag_helmholtz)
 template <int OP, class T>
@@ -4190,6 +4228,14 @@ int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double
     return (int)(cg.x * cg.y);
 }
 
+int launch_helm_rb_mask(const Geo& g, const Coef& c, double alpha, double omega, double* x, const double* b, int par,
+                        double* part, hipStream_t st) {
+    const int rows = cell_rows(g);
+    const dim3 cg = cell_grid(g, rows);
+    if (g.fc) NS_LAUNCH(k_helm_rb_mask<TopoMask>, cg, dim3(64, 4), 0, st, g, c, alpha, omega, x, b, par, part, rows);
+    else NS_LAUNCH(k_helm_rb_mask<TopoRect>, cg, dim3(64, 4), 0, st, g, c, alpha, omega, x, b, par, part, rows);
+    return (int)(cg.x * cg.y);
+}
 void launch_diag_pc(int op, const Geo& g, const Coef& c, double alpha, const double* q, double* z, hipStream_t st,
                     const double* stop) {
     const dim3 cg = cell_grid(g);

@@ -304,6 +304,10 @@ struct ns_solver {
     const double *m0e = nullptr, *m0b = nullptr, *m0g = nullptr, *m0a = nullptr;
     double fps_res = -1.0;       // the last checked solve's relative residual
     int kpred[3] = {1, 1, 1};    // (r5) the last BiCGStab solve's iterations: Poisson, Helmholtz u, v (bicgstab's batch)
+    // (r5) a masked domain's Helmholtz solve on one rank by red-black SOR (NSGPU_MASK_HELM=krylov: BiCGStab); the
+    // sweeps the last step needed (the next step's first batch)
+    bool mask_rb = true;
+    int mask_helm_next = 4;
     // r5, multi-rank rectangles: the Helmholtz check's collective is an allgather of every rank's
     // S_HBNL .. S_MML (bus()): K1's norms and the previous step's K5 min / max ride on it, so neither
     // takes a collective of its own (NSGPU_BUS=0: the per-reduction all-reduces, A/B); bus_mem holds
@@ -920,6 +924,42 @@ int helm_band(ns_solver* s, double alpha) {
 // fewer sweeps than the reference's zero guess.
 int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
     const double alpha = s->dt / (2 * s->re);
+    if (s->g.fc && s->nranks == 1 && s->mask_rb) {
+        // (r5) masked domain, one rank: red-black SOR on I - alpha L_V (strongly diagonally dominant: alpha / h^2 ~ 0.06
+        // at 1024^2), u and v sweep by sweep, the residual of both checked after a batch -- the first batch what
+        // the previous step needed (NSGPU_MASK_HELM=krylov: the BiCGStab of rounds 1-4)
+        CHK(fetch(s));   // ||RHS_u||^2, ||RHS_v||^2
+        const double tol2 = s->rtol * s->rtol, bu = s->hs[S_HBN], bv = s->hs[S_HBN + 1];
+        int sweeps = 0, batch = std::max(1, s->mask_helm_next);
+        double r2u = 0.0, r2v = 0.0;
+        for (;;) {
+            const int n = std::min(batch, s->max_iters - sweeps);
+            for (int k = 0; k < n; k++)
+                for (int f : {NS_ARR_U, NS_ARR_V})
+                    for (int par : {0, 1})
+                        nsg::launch_helm_rb_mask(s->g, s->c, alpha, s->omega_v, s->arr[f], s->arr[f == NS_ARR_U ? NS_ARR_RU : NS_ARR_RV],
+                                                 par, nullptr, s->st);
+            sweeps += n;
+            int nb = 0;
+            for (int f : {NS_ARR_U, NS_ARR_V})
+                nb = nsg::launch_helm_rb_mask(s->g, s->c, alpha, s->omega_v, s->arr[f],
+                                              s->arr[f == NS_ARR_U ? NS_ARR_RU : NS_ARR_RV], 2,
+                                              s->part + (f == NS_ARR_U ? 0 : (size_t)nsg::max_partials(s->g)), s->st);
+            nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
+            nsg::launch_reduce_sum(s->part + nsg::max_partials(s->g), nb, 1, s->scal + S_RES + 1, s->st);
+            CHK(fetch(s));
+            r2u = s->hs[S_RES];
+            r2v = s->hs[S_RES + 1];
+            if (!std::isfinite(r2u) || !std::isfinite(r2v)) { set_err("Helmholtz residual is not finite"); return NS_EDIVERGE; }
+            if ((r2u <= tol2 * bu && r2v <= tol2 * bv) || sweeps >= s->max_iters) break;
+            batch = 2;
+        }
+        *resu = bu > 0 ? std::sqrt(r2u / bu) : std::sqrt(r2u);
+        *resv = bv > 0 ? std::sqrt(r2v / bv) : std::sqrt(r2v);
+        *its = sweeps;
+        s->mask_helm_next = sweeps;
+        return 0;
+    }
     if (s->g.fc) {
         // masked domain: u then v, each a Jacobi-preconditioned BiCGStab on I - alpha L_V
         CHK(fetch(s));   // ||RHS_u||^2, ||RHS_v||^2
@@ -3176,6 +3216,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_FUSE4")) s->fuse4 = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_GIN")) s->gin = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_MASK_HELM")) s->mask_rb = std::strcmp(e, "krylov") != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     if (const char* e = getenv("NSGPU_DIRECT_CELLS")) s->direct_cells = std::max(0L, std::atol(e));
     {
