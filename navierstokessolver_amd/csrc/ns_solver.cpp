@@ -307,7 +307,7 @@ struct ns_solver {
     // (r5) a masked domain's Helmholtz solve on one rank by red-black SOR (NSGPU_MASK_HELM=krylov: BiCGStab); the
     // sweeps the last step needed (the next step's first batch)
     bool mask_rb = true;
-    int mask_helm_next = 4;
+    int mask_helm_next = 4, mask_helm_ok = 0;
     // r5, multi-rank rectangles: the Helmholtz check's collective is an allgather of every rank's
     // S_HBNL .. S_MML (bus()): K1's norms and the previous step's K5 min / max ride on it, so neither
     // takes a collective of its own (NSGPU_BUS=0: the per-reduction all-reduces, A/B); bus_mem holds
@@ -957,7 +957,16 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         *resu = bu > 0 ? std::sqrt(r2u / bu) : std::sqrt(r2u);
         *resv = bv > 0 ? std::sqrt(r2v / bv) : std::sqrt(r2v);
         *its = sweeps;
-        s->mask_helm_next = sweeps;
+        // (the next step's first batch: what this one needed; after 4 steps in a row whose first batch sufficed,
+        // one sweep fewer -- the flow settles and the solves need fewer sweeps than at the start)
+        const bool first_ok = sweeps <= std::max(1, s->mask_helm_next);
+        if (first_ok && ++s->mask_helm_ok >= 4) {
+            s->mask_helm_next = std::max(2, sweeps - 1);
+            s->mask_helm_ok = 0;
+        } else {
+            s->mask_helm_next = sweeps;
+            if (!first_ok) s->mask_helm_ok = 0;
+        }
         return 0;
     }
     if (s->g.fc) {
