@@ -882,6 +882,24 @@ __device__ inline double fps_rank_in(const FpsRank& R, int k, int ld, int ny, bo
     *sft0 = k == 0 ? sft : 0.0;
     double Y = 0.0;
     if (!R.gath) return Y;
+    if (backward && R.bq) {
+        // (r5, one allgather) every rank's forward carry-in, then the backward fold of the ranks after this one
+        constexpr int PMAX = 64;
+        double yin[PMAX];
+        double Yf = 0.0;
+        for (int q = 0; q < R.P && q < PMAX; q++) {
+            yin[q] = Yf;
+            const double E = R.gath[(size_t)q * R.stride + k] - (R.a1 ? *sft0 * R.a1[q] : 0.0);
+            Yf = fma(R.gath[(size_t)q * R.stride + ld + k], Yf, E);
+        }
+        const size_t ox = 2 * (size_t)ld + 8;
+        for (int q = R.P - 1; q > R.r; q--) {
+            const double* sl = R.gath + (size_t)q * R.stride;
+            const double X0 = sl[ox + k] - (R.x1 ? *sft0 * R.x1[q] : 0.0);
+            Y = fma(sl[ox + ld + k], Y, fma(R.bq[(size_t)q * ld + k], yin[q], X0));
+        }
+        return Y;
+    }
     if (!backward) {
         for (int q = 0; q < R.r; q++) {
             const double E = R.gath[(size_t)q * R.stride + k] - (R.a1 ? *sft0 * R.a1[q] : 0.0);
@@ -1246,12 +1264,12 @@ __global__ void __launch_bounds__(64) k_fps_mid(FpsArgs a, const double* __restr
                 bl.x -= sft * a.m0b[c];
             }
             const double2 be = ld2(a.bt + (size_t)c * a.ld + k0), br = ld2(a.bt + (size_t)(a.nch + c) * a.ld + k0);
-            st2(a.ya + (size_t)c * a.ld + k0, Y[0], Y[1]);
+            if (!a.mid_local) st2(a.ya + (size_t)c * a.ld + k0, Y[0], Y[1]);
             BX[w][0] = fma(be.x, Y[0], bl.x);
             BX[w][1] = fma(be.y, Y[1], bl.y);
             BR[w][0] = br.x;
             BR[w][1] = br.y;
-            st2(a.cb + (size_t)c * a.ld + k0, BX[w][0], BX[w][1]);
+            if (!a.mid_local) st2(a.cb + (size_t)c * a.ld + k0, BX[w][0], BX[w][1]);
             Y[0] = fma(pp.x, Y[0], e.x);
             Y[1] = fma(pp.y, Y[1], e.y);
         }

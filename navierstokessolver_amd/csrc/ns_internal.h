@@ -339,6 +339,9 @@ struct FpsArgs {
     // sit at their fixed point (prowb, ld / 128 ints; 1 << 30: never) -- rows before it keep the division, rows
     // after it take pinf.  The table's reads (up to 1024 rows x ld) cost t1b more than the divisions they saved
     const int* prowb = nullptr;
+    // (r5, one allgather per solve) k_fps_mid's first, rank-local pass: only the groups' backward aggregates (the
+    // chunks' carries and BX are formed again after the allgather)
+    int mid_local = 0;
     // (r5) slabs with deep ghost rows: k_fps_t2b also writes the transformed solution of the neighbours' edge rows
     // (local rows -1 and nxl, where a neighbour exists) -- the row below from the backward carry, the row above
     // from the forward carry and the slab's own first row -- so the inverse transform gives K5 phi's ghost rows
@@ -354,6 +357,11 @@ struct FpsRank {
     const double *a1 = nullptr, *ge1 = nullptr;
     double ncells = 0.0;
     double* shift = nullptr;
+    // (r5, one allgather per solve, backward) every rank's slot also holds its backward aggregate with a zero
+    // forward carry-in (X0 at 2 ld + 8, R at 3 ld + 8): the carry-in from the ranks after this one folds X0_p +
+    // B_p Yin_p (- ny mean X1_p for mode 0) with R_p, Yin_p every rank's forward carry-in from the same slots;
+    // bq: B_p (P x ld, host table), x1: X1_p (P, mode 0's response to the constant 1)
+    const double *bq = nullptr, *x1 = nullptr;
 };
 // log2(ny) if ny is a supported power of two, else -1
 int fps_log2(int ny);

@@ -295,6 +295,11 @@ struct ns_solver {
     // allgather per direction and solve) and the carry-in folded from them (ld)
     double *fps_ragg = nullptr, *fps_gath = nullptr;
     size_t fps_n = 0;            // (r5) the allgather's slot: 2 x ld aggregates + (sum b, sum b^2) + padding
+    // (r5) ONE allgather per solve (NSGPU_FPS_ONEGATHER=0: two, A/B): the slot also carries the rank's backward
+    // aggregate with a zero forward carry-in (2 more ld), which is affine in that carry-in (FpsRank::bq); og_b /
+    // og_x1: the host tables B_p (every rank, per mode) and X1_p
+    bool fps_og = false, fps_og_mean = false;
+    const double *og_b = nullptr, *og_x1 = nullptr;
     // r5, multi-rank rectangles on the direct solve: the fused K3's sums are not all-reduced -- they ride
     // on the recurrences' forward allgather (at 2 ld of each rank's slot), and the mean comes off mode 0
     // afterwards, as the linear response of its aggregates to the constant ny * mean (host tables m0: every
@@ -1889,6 +1894,40 @@ int fps_scan(ns_solver* s, bool backward) {
         nsg::launch_fps_scan(s->fa, backward, nsg::FpsRank{}, nullptr, s->st);
         return 0;
     }
+    if (s->fps_og) {
+        // (r5) ONE allgather per solve: forward, the rank-local passes first -- the forward scan (this rank's
+        // (E, P)), k_fps_mid without the chunk stores, the backward scan (its (X0, R) with a zero carry-in) --
+        // then the allgather and the real forward scan; backward, the real scan with FpsRank::bq's carry-in
+        nsg::FpsRank R{s->fps_gath, s->nranks, s->rank, (int)s->fps_n};
+        if (backward) {
+            R.bq = s->og_b;
+            if (s->fps_og_mean) {   // (the mean was deferred in this solve's forward pass: the same correction)
+                R.a1 = s->m0a;
+                R.x1 = s->og_x1;
+                R.ncells = s->ncells;
+            }
+            nsg::launch_fps_scan(s->fa, true, R, nullptr, s->st);
+            return 0;
+        }
+        if (s->mean_pend) {
+            R.a1 = s->m0a;
+            R.ncells = s->ncells;
+        }
+        const size_t ld = s->g.ld;
+        nsg::launch_fps_scan(s->fa, false, nsg::FpsRank{}, s->fps_ragg, s->st);
+        nsg::FpsArgs fl = s->fa;
+        fl.mid_local = 1;
+        nsg::launch_fps_mid(fl, s->arr[NS_ARR_TMP], s->st);
+        nsg::launch_fps_scan(s->fa, true, nsg::FpsRank{}, s->fps_ragg + 2 * ld + 8, s->st);
+        CHK(fps_allgather(s));
+        s->fps_og_mean = s->mean_pend;   // (the backward carry's mode-0 correction needs the same sums)
+        if (s->mean_pend) {
+            R.ge1 = s->m0g;
+            R.shift = s->scal + S_SHIFT;
+        }
+        nsg::launch_fps_scan(s->fa, false, R, nullptr, s->st);
+        return 0;
+    }
     nsg::launch_fps_scan(s->fa, backward, nsg::FpsRank{}, s->fps_ragg, s->st);
     CHK(fps_allgather(s));
     // (the other ranks' carry-in is folded inside the scan; r4 had a k_fps_rank_carry launch per direction)
@@ -2087,8 +2126,14 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     const size_t n_tab = 4 * (size_t)N + (size_t)N, n_rp0 = (size_t)nchp * ld, n_g = (size_t)a.ngrp * ld;
     // multi-rank: the allgather's own slot and every rank's (fps_n each), and the deferred mean's mode-0
     // tables (chunks' E and BXl, groups', ranks' aggregates of the constant 1)
-    s->fps_n = 2 * (size_t)ld + 8;
-    const size_t n_mr = s->nranks > 1 ? (size_t)(1 + s->nranks) * s->fps_n + 2 * (size_t)nchp + a.ngrp + s->nranks : 0;
+    {
+        const char* e = getenv("NSGPU_FPS_ONEGATHER");
+        s->fps_og = s->nranks > 1 && s->nranks <= 64 && s->fps_passes != 3 && !(e && std::atoi(e) == 0);
+    }
+    s->fps_n = (s->fps_og ? 4 : 2) * (size_t)ld + 8;
+    const size_t n_og = s->fps_og ? (size_t)s->nranks * ld + s->nranks : 0;
+    const size_t n_mr = s->nranks > 1 ? (size_t)(1 + s->nranks) * s->fps_n + 2 * (size_t)nchp + a.ngrp + s->nranks + n_og
+                                      : 0;
     const size_t n_bt = 2 * (size_t)nchp * ld;
     const size_t total = n_tab + n_rp0 + n_bt + 6 * n_g + 5 * (size_t)nchp * ld + n_mr + 8;
     std::vector<double> h(n_tab + n_rp0 + n_bt, 0.0);
@@ -2317,6 +2362,47 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
         s->m0g = q + 2 * (size_t)nchp;
         s->m0a = s->m0g + a.ngrp;
         q += m0.size();
+        if (s->fps_og) {
+            // (r5) every rank's backward aggregate (x at its first row, zero carry from the ranks after it) as a
+            // function of its forward carry-in Y: with f = 0, y_i = Y prod(-g), x_i = y_i r_i - pe_i r_i x_{i+1}, so
+            // B_p(k) = sum_i prod_{m <= i}(-g_m) r_i prod_{m < i}(-pe_m r_m) over rank p's rows (piv_next's pivots);
+            // X1_p: mode 0's aggregate of f = 1 from zero (the deferred mean's correction)
+            const int P = s->nranks;
+            std::vector<double> B((size_t)P * ld, 0.0), X1(P, 0.0), rr(N, 0.0), fw(N), bw(N);
+            int rq = 0;
+            int32_t q0 = 0, q1 = 0;
+            ns_slab_range(nx, P, 0, &q0, &q1);
+            double y1 = 0.0, bw1 = 1.0;
+            for (int gi = 0; gi < nx; gi++) {
+                while (gi >= q1) { rq++; ns_slab_range(nx, P, rq, &q0, &q1); }
+                if (gi == q0) {
+                    std::fill(fw.begin(), fw.end(), 1.0);
+                    std::fill(bw.begin(), bw.end(), 1.0);
+                    y1 = 0.0;
+                    bw1 = 1.0;
+                }
+                const double pem = gi > 0 ? pe[gi - 1] : 0.0;
+                double* Bq = B.data() + (size_t)rq * ld;
+                for (int k = 0; k < N; k++) {
+                    const double gg = pw[gi] * rr[k];
+                    const double p = std::fma(-gg, pem, -(pw[gi] + pe[gi]) + h[4 * N + k]);
+                    rr[k] = (k == 0 && gi == nx - 1) ? 0.0 : 1.0 / p;
+                    fw[k] *= -gg;
+                    Bq[k] += fw[k] * rr[k] * bw[k];
+                    bw[k] *= -pe[gi] * rr[k];
+                }
+                // (mode 0, f = 1: y_i = 1 - g_i y_{i-1}, the same back substitution)
+                y1 = std::fma(-(pw[gi] * (gi > 0 ? r0[gi - 1] : 0.0)), y1, 1.0);
+                X1[rq] += y1 * r0[gi] * bw1;
+                bw1 *= -pe[gi] * r0[gi];
+            }
+            HIPCHK(hipMemcpy(q, B.data(), B.size() * sizeof(double), hipMemcpyHostToDevice));
+            s->og_b = q;
+            q += B.size();
+            HIPCHK(hipMemcpy(q, X1.data(), X1.size() * sizeof(double), hipMemcpyHostToDevice));
+            s->og_x1 = q;
+            q += X1.size();
+        }
     }
     a.pw = s->c.pw;
     a.pe = s->c.pe;

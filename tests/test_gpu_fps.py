@@ -305,21 +305,24 @@ def test_direct_solve_check_policy(gpu):
 
 @pytest.mark.parametrize("nproc", [2, 3])
 def test_slab_collective_budget(tmp_path, gpu, monkeypatch, nproc):
-    """r5: a multi-rank direct-solve step takes 3 collectives -- the Helmholtz check's
-    allgather (the scalar bus: K1's ||RHS||^2 and the previous step's K5 min / max ride on it), the
-    recurrences' forward allgather (K3's sums ride on it: the mean comes off mode 0 after it, through the
-    aggregates' linear response to a constant) and the backward one -- plus an all-reduce on a checked
-    solve; r4 took 6 (5 + 1).  Host-transport slabs with async steps (the monitor one call late): the same
-    fields as the per-reduction all-reduces (NSGPU_BUS=0) to 1e-12 and as one rank to 1e-10."""
+    """r5: a multi-rank direct-solve step takes 2 collectives -- the Helmholtz check's
+    allgather (the scalar bus: K1's ||RHS||^2 and the previous step's K5 min / max ride on it) and ONE allgather
+    of the recurrences (K3's sums ride on it: the mean comes off mode 0 after it, through the aggregates'
+    linear response to a constant; every rank's backward aggregate rides on it too, affine in the rank's
+    forward carry-in) -- plus an all-reduce on a checked solve; r4 took 6 (5 + 1).  Host-transport slabs with
+    async steps (the monitor one call late): the same fields as the per-reduction all-reduces and two
+    allgathers (NSGPU_BUS=0, NSGPU_FPS_ONEGATHER=0) to 1e-12 and as one rank to 1e-10."""
     n, steps = 128, 20
     args = ("--xport", "host", "--size", str(n), "--nsteps", str(steps), "--solver", str(gpu.NS_POISSON_MG),
             "--tol", "1e-10", "--async-steps")
     r = _slabs(tmp_path, nproc, *args, port=29781 + nproc)
     monkeypatch.setenv("NSGPU_BUS", "0")
+    monkeypatch.setenv("NSGPU_FPS_ONEGATHER", "0")
     r0 = _slabs(tmp_path, nproc, *args, port=29791 + nproc)
     monkeypatch.delenv("NSGPU_BUS")
+    monkeypatch.delenv("NSGPU_FPS_ONEGATHER")
     coll, coll0 = r["xc"][:, 1], r0["xc"][:, 1]
-    assert np.median(coll) == 3 and coll.max() <= 4, coll
+    assert np.median(coll) == 2 and coll.max() <= 3, coll
     assert np.median(coll0) >= 5, coll0
     gs = gpu.GpuSolver(gpu.rectangle(n, n), 1.0 / (8 * n), 100.0, rtol=1e-10, device=0)
     mm = np.array([[x[k] for k in ("umin", "umax", "vmin", "vmax")] for x in (gs.step() for _ in range(steps))])
