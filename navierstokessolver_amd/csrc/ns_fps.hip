@@ -1621,6 +1621,118 @@ void launch_fps_t2b(const FpsArgs& a, double* f, hipStream_t st) {
 void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_t3, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);
 }
+// ------------------------------------------------ (r5) masked domains: the capacitance solve
+// L_ext (the masked operator on the domain, zero-flux at its inner walls) differs from the bounding box's L_box
+// only across the m interface faces f = (i in the domain, j outside): L_box = L_ext - D_w D^T, d_f = e_i - e_j,
+// D_w's columns w_f d_f.  L_ext x = q is then x = L_box^+ (q - D_w y) with (I + D^T L_box^+ D_w) y = D^T L_box^+ q;
+// the capacitance matrix C is singular along y0 = 1 (the domain's constant), C + 1 1^T / m is not (CapArgs)
+namespace {
+
+// y = Cinv (D^T z): one row per wave; every workgroup gathers the m interface differences into LDS first
+__global__ __launch_bounds__(256) void k_cap_gemv(CapArgs a, const double* __restrict__ z) {
+    extern __shared__ double gl[];
+    for (int f = threadIdx.x; f < a.m; f += 256) gl[f] = z[a.fi[f]] - z[a.fj[f]];
+    __syncthreads();
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= a.m) return;
+    const double* cr = a.cinv + (size_t)row * a.m;
+    double acc = 0.0;
+    for (int k = lane; k < a.m; k += 64) acc = fma(cr[k], gl[k], acc);
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) a.y[row] = acc;
+}
+
+// q -= D_w y at the interface cells (mode 0), or q = 0 at those outside the domain (mode 1: the Krylov planes'
+// invariant -- 0 outside -- restored after the second box solve)
+__global__ __launch_bounds__(256) void k_cap_scatter(CapArgs a, double* __restrict__ q, int mode) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= a.ncell) return;
+    const int4 f4 = a.cf[c];
+    const int fs[4] = {f4.x, f4.y, f4.z, f4.w};
+    if (mode == 1) {
+        if (fs[0] < 0) q[a.co[c]] = 0.0;   // (a cell outside holds only negative references)
+        return;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int v = fs[k];
+        if (v == 0) continue;
+        const int f = (v > 0 ? v : -v) - 1;
+        acc += (v > 0 ? 1.0 : -1.0) * a.w[f] * a.y[f];
+    }
+    q[a.co[c]] -= acc;
+}
+
+// x += z on the domain's cells
+__global__ __launch_bounds__(256) void k_cap_axpy(Geo g, double* __restrict__ x, const double* __restrict__ z) {
+    const int j = blockIdx.x * 64 + threadIdx.x, li = blockIdx.y * 4 + threadIdx.y;
+    if (j >= g.ny || li >= g.nxl) return;
+    const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
+    if (g.fc[o] & FC_IN) x[o] += z[o];
+}
+
+// set-up: the source w_f d_f of column f in the zeroed plane q (the previous column's cleared; f < 0: only that)
+__global__ void k_cap_src(CapArgs a, double* __restrict__ q, int fprev, int f) {
+    if (fprev >= 0) { q[a.fi[fprev]] = 0.0; q[a.fj[fprev]] = 0.0; }
+    if (f >= 0) { q[a.fi[f]] = a.w[f]; q[a.fj[f]] = -a.w[f]; }
+}
+
+// set-up: column f of C + 1 1^T / m from z = L_box^+ (w_f d_f) (row-major in cmat)
+__global__ __launch_bounds__(256) void k_cap_col(CapArgs a, const double* __restrict__ z, int f,
+                                                 double* __restrict__ cmat) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= a.m) return;
+    cmat[(size_t)r * a.m + f] = (r == f ? 1.0 : 0.0) + (z[a.fi[r]] - z[a.fj[r]]) + 1.0 / a.m;
+}
+
+// set-up: Gauss-Jordan inversion in place without pivoting (C + 1 1^T / m is symmetric positive definite for
+// uniform face weights, a diagonal similarity of one otherwise): pivot k's scaled row t and column u ...
+__global__ __launch_bounds__(256) void k_gj_prep(double* __restrict__ A, int m, int k, double* __restrict__ t,
+                                                 double* __restrict__ u, double* __restrict__ flag) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= m) return;
+    const double p = A[(size_t)k * m + k];
+    if (c == 0 && !(p > 0.0 && isfinite(p))) flag[0] = 1.0;
+    t[c] = c == k ? 1.0 / p : A[(size_t)k * m + c] / p;
+    u[c] = A[(size_t)c * m + k];
+}
+// ... then the rank-1 update of every other entry
+__global__ __launch_bounds__(256) void k_gj_step(double* __restrict__ A, int m, int k, const double* __restrict__ t,
+                                                 const double* __restrict__ u) {
+    const int c = blockIdx.x * 64 + threadIdx.x, r = blockIdx.y * 4 + threadIdx.y;
+    if (c >= m || r >= m) return;
+    double& e = A[(size_t)r * m + c];
+    if (r == k) e = t[c];
+    else if (c == k) e = -u[r] * t[k];
+    else e = fma(-u[r], t[c], e);
+}
+
+}  // namespace
+
+void launch_cap_gemv(const CapArgs& a, const double* z, hipStream_t st) {
+    hipLaunchKernelGGL(k_cap_gemv, dim3((a.m + 3) / 4), dim3(256), a.m * sizeof(double), st, a, z);
+}
+void launch_cap_scatter(const CapArgs& a, double* q, int mode, hipStream_t st) {
+    hipLaunchKernelGGL(k_cap_scatter, dim3((a.ncell + 255) / 256), dim3(256), 0, st, a, q, mode);
+}
+void launch_cap_axpy(const Geo& g, double* x, const double* z, hipStream_t st) {
+    hipLaunchKernelGGL(k_cap_axpy, dim3((g.ny + 63) / 64, (g.nxl + 3) / 4), dim3(64, 4), 0, st, g, x, z);
+}
+void launch_cap_src(const CapArgs& a, double* q, int fprev, int f, hipStream_t st) {
+    hipLaunchKernelGGL(k_cap_src, dim3(1), dim3(1), 0, st, a, q, fprev, f);
+}
+void launch_cap_col(const CapArgs& a, const double* z, int f, double* cmat, hipStream_t st) {
+    hipLaunchKernelGGL(k_cap_col, dim3((a.m + 255) / 256), dim3(256), 0, st, a, z, f, cmat);
+}
+void launch_gj_invert(double* A, int m, double* t, double* u, double* flag, hipStream_t st) {
+    for (int k = 0; k < m; k++) {
+        hipLaunchKernelGGL(k_gj_prep, dim3((m + 255) / 256), dim3(256), 0, st, A, m, k, t, u, flag);
+        hipLaunchKernelGGL(k_gj_step, dim3((m + 63) / 64, (m + 3) / 4), dim3(64, 4), 0, st, A, m, k, (const double*)t,
+                           (const double*)u);
+    }
+}
+
 void launch_fps_scan(const FpsArgs& a, bool backward, const FpsRank& R, double* rout, hipStream_t st) {
     if (FPS_SSEG > 1 && a.ngrp >= 2 * FPS_SSEG)
         hipLaunchKernelGGL(k_fps_scan_seg<FPS_SSEG>, dim3((a.ny + 63) / 64), dim3(64, FPS_SSEG), 0, st, a.ngrp, a.ld,

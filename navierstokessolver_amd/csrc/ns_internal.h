@@ -17,6 +17,8 @@ constexpr int HALO = 7;  // ghost rows per side: K1's MUSCL stencil (2), the 2-s
 //   FC_IN set = the cell is in the domain; bits 5k..5k+4 = the boundary edge on face k
 //   (0 W, 1 E, 2 S, 3 N; Cell::edges, Grid.h:33) or FC_INT if the neighbour is in the domain.
 constexpr int FC_IN = 1 << 20;
+// (r5) the cell's neighbours up to 2 away along x and y (K1's MUSCL stencil) are all in the domain
+constexpr int FC_DEEP = 1 << 21;
 constexpr int FC_INT = 31;
 constexpr int MAX_EDGES = 31;
 __host__ __device__ inline int fc_edge(int code, int k) { return (code >> (5 * k)) & 31; }
@@ -49,6 +51,10 @@ struct Geo {
     // the face value) instead of a wall; prolongation extends the correction there oddly
     // (0 on the face) rather than reflecting it
     int dsx = 0;
+    // (r5) masked domains: the slab's domain cells that are not FC_DEEP (plane offsets li * ld + j, ascending) --
+    // K1's LDS tiles take the FC_DEEP cells, a second launch these (launch_rhs)
+    const int* ecell = nullptr;
+    int necell = 0;
 };
 
 // 1-D coefficient tables (global index) built once from hx, hy (ConstructLHS, FluidSolver.cpp:113-131)
@@ -277,10 +283,11 @@ struct KrylovArgs {
 // y = A x with A the reference's Poisson matrix (op 0, NEUMANN outflow rows included) or its
 // Helmholtz matrix I - alpha L_V (op 1), on a rectangle or a masked domain; partials
 // (sum y, sum q*y) per block (q may be null); returns the partial count
-// (r5) one red (par 0) or black (par 1) SOR half-sweep of the Helmholtz matrix I - alpha L_V on x in place, or
-// (par 2) the block partials of ||b - A x||^2 (returns their count); masked domains' Helmholtz solve (one rank)
-int launch_helm_rb_mask(const Geo& g, const Coef& c, double alpha, double omega, double* x, const double* b, int par,
-                        double* part, hipStream_t st);
+// (r5) one red (par 0) or black (par 1) SOR half-sweep of the Helmholtz matrix I - alpha L_V on x in place (and on
+// x2, rhs b2, in the same pass if not null), or (par 2) the block partials of ||b - A x||^2 and ||b2 - A x2||^2 (2
+// per block; returns the block count); masked domains' Helmholtz solve (one rank)
+int launch_helm_rb_mask(const Geo& g, const Coef& c, double alpha, double omega, double* x, const double* b,
+                        double* x2, const double* b2, int par, double* part, hipStream_t st);
 // (stop: a KS_STOP slot -- the grid kernels then do nothing once it is set; null: always run)
 int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double* x, double* y, const double* q,
                  double* part, hipStream_t st, const double* stop = nullptr);
@@ -394,5 +401,24 @@ void launch_fps_t2b(const FpsArgs& a, double* f, hipStream_t st);
 // ranks (R: the fold of their gathered aggregates; default: none, 0); rout (if not null) <- this rank's
 // aggregate
 void launch_fps_scan(const FpsArgs& a, bool backward, const FpsRank& R, double* rout, hipStream_t st);
+
+// (r5) a masked domain's exact Poisson solve by the capacitance matrix of its interface with the bounding box
+// (ns_fps.hip; ns_solver.cpp cap_setup / cap_solve): m faces (fi: the domain cell's plane offset, fj: the outside
+// cell's, w: the face's operator weight), cinv = (C + 1 1^T / m)^-1 (m x m, row-major), y (m); the ncell cells on
+// either side of a face (co: plane offset, cf: up to 4 signed face references +-(f + 1), + on the domain's side,
+// 0: none)
+struct CapArgs {
+    int m = 0, ncell = 0;
+    const int *fi = nullptr, *fj = nullptr, *co = nullptr;
+    const int4* cf = nullptr;
+    const double* w = nullptr;
+    double *cinv = nullptr, *y = nullptr;
+};
+void launch_cap_gemv(const CapArgs& a, const double* z, hipStream_t st);                // y = cinv D^T z
+void launch_cap_scatter(const CapArgs& a, double* q, int mode, hipStream_t st);         // q -= D_w y / q = 0 outside
+void launch_cap_axpy(const Geo& g, double* x, const double* z, hipStream_t st);         // x += z on the domain
+void launch_cap_src(const CapArgs& a, double* q, int fprev, int f, hipStream_t st);     // set-up: column f's source
+void launch_cap_col(const CapArgs& a, const double* z, int f, double* cmat, hipStream_t st);
+void launch_gj_invert(double* A, int m, double* t, double* u, double* flag, hipStream_t st);
 
 }  // namespace nsg

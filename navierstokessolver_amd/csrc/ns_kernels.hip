@@ -172,7 +172,12 @@ struct TopoMask {
     }
     __device__ __forceinline__ TopoMask(const Geo& g_, int li_, int j_) : g(g_), li(li_), j(j_), code(0) { code = at(0, 0); }
     __device__ __forceinline__ bool cell() const { return (code & FC_IN) != 0; }
-    __device__ __forceinline__ bool in(int di, int dj) const { return (at(di, dj) & FC_IN) != 0; }
+    __device__ __forceinline__ bool in(int di, int dj) const {
+        // (r5) a face neighbour from the cell's own code (its face is FC_INT exactly when the neighbour is in the
+        // domain: ns_create checks Grid::inDomain against Cell::edges) -- no load of the neighbour's code
+        if (di * di + dj * dj == 1) return fc_edge(code, di < 0 ? 0 : di > 0 ? 1 : dj < 0 ? 2 : 3) == FC_INT;
+        return (at(di, dj) & FC_IN) != 0;
+    }
     __device__ __forceinline__ double gv(int di, int dj, int k, double q, int d) const {
         const EdgeDev& E = g.et[fc_edge(di == 0 && dj == 0 ? code : at(di, dj), k)];
         return E.neu ? q : (-q + (d == 0 ? E.c0 : E.c1));
@@ -445,7 +450,12 @@ __global__ __launch_bounds__(256) void k_rhs(Geo g, Coef c, double dt, double re
         auto X = [&](int t, int d) { return (t == 0 ? c.hx : t == 1 ? c.rhx : c.rsx)[gi + d]; };
         auto Y = [&](int t, int d) { return (t == 0 ? c.hy : t == 1 ? c.rhy : c.rsy)[j + d]; };
         double cun, cvn, ru_, rv_;
-        rhs_cell<true, T>(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
+        // (r5) a masked domain's cell whose MUSCL stencil lies in the domain (FC_DEEP): the interior arithmetic, no
+        // topology or edge-table reads (the same values: every existence test is true, no ghost is used)
+        if (g.fc && (g.fc[o] & FC_DEEP))
+            rhs_cell<false, TopoInner>(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
+        else
+            rhs_cell<true, T>(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
         cu[o] = cun;
         cv[o] = cvn;
         ru[o] = ru_;
@@ -537,6 +547,11 @@ __device__ __forceinline__ int phase_block(int k, int lo, int hi0) { return k < 
 
 
 constexpr int RT = 16;
+// (r5) MASK: a masked domain's K1 (launch_rhs) -- cells outside the domain skipped (they stay 0), FC_DEEP cells (the
+// MUSCL stencil inside the domain) with the interior arithmetic, the others with the polygon's topology and their
+// wall terms inline; every domain cell's ||RHS||^2 in the partials (no k_rhs_bc pass).  The global-load k_rhs<TopoMask>
+// fetched every u / v value ~13 times through L1 / L2 (105 us at the 1024^2 L-shape)
+template <bool MASK>
 __global__ __launch_bounds__(256) void k_rhs_lds(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
                                                  const double* __restrict__ v, const double* __restrict__ phi,
                                                  double* __restrict__ cu, double* __restrict__ cv,
@@ -623,22 +638,59 @@ __global__ __launch_bounds__(256) void k_rhs_lds(Geo g, Coef c, double dt, doubl
             auto X = [&](int t, int d) { return tx[t][R - 1 + d]; };
             auto Y = [&](int t, int d) { return ty[t][C - 1 + d]; };
             double cun, cvn, ru_, rv_;
-            rhs_cell<false, T>(g, c, dt, re, U, V, X, Y, phi, li, j, scu[R - 2][C - 2], scv[R - 2][C - 2], cun, cvn,
-                               ru_, rv_);
+            if (MASK) {
+                // (the other domain cells: k_rhs_cells' list -- in this loop their topology path, taken by every
+                // wave holding one, cost the whole launch 3.3x: 93 vs 28 us at 1024^2)
+                if (!(g.fc[o] & FC_DEEP)) continue;
+                rhs_cell<false, TopoInner>(g, c, dt, re, U, V, X, Y, phi, li, j, scu[R - 2][C - 2], scv[R - 2][C - 2],
+                                           cun, cvn, ru_, rv_);
+            } else {
+                rhs_cell<false, T>(g, c, dt, re, U, V, X, Y, phi, li, j, scu[R - 2][C - 2], scv[R - 2][C - 2], cun,
+                                   cvn, ru_, rv_);
+            }
             cu[o] = cun;
             cv[o] = cvn;
             ru[o] = ru_;
             rv[o] = rv_;
             const int gi = g.i0 + li;
-            if (gi > 0 && gi < g.nx - 1 && j > 0 && j < g.ny - 1) {   // wall cells: k_rhs_bc
+            if (MASK || (gi > 0 && gi < g.nx - 1 && j > 0 && j < g.ny - 1)) {   // wall cells: k_rhs_bc
                 acc[0] += ru_ * ru_;
                 acc[1] += rv_ * rv_;
             }
         }
     };
-    if (inner) rows(TopoInner(g, 0, 0));
+    if (MASK) rows(TopoInner(g, 0, 0));   // (the topology per cell above)
+    else if (inner) rows(TopoInner(g, 0, 0));
     else rows(TopoRect(g, 0, 0));
     block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * ti));
+}
+
+// (r5) K1 of a masked domain's listed cells (Geo::ecell: the domain cells within 2 of its boundary), one thread
+// each, with the polygon's topology and wall terms (k_rhs<TopoMask>'s cell)
+__global__ __launch_bounds__(256) void k_rhs_cells(Geo g, Coef c, double dt, double re, const double* __restrict__ u,
+                                                   const double* __restrict__ v, const double* __restrict__ phi,
+                                                   double* __restrict__ cu, double* __restrict__ cv,
+                                                   double* __restrict__ ru, double* __restrict__ rv,
+                                                   double* __restrict__ part) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    double acc[2] = {0.0, 0.0};
+    if (k < g.necell) {
+        const int ld = g.ld, o = g.ecell[k], li = o / ld, j = o - li * ld;
+        auto U = [&](int di, int dj) { return ldf(u, ld, li + di, j + dj); };
+        auto V = [&](int di, int dj) { return ldf(v, ld, li + di, j + dj); };
+        const int gi = g.i0 + li;
+        auto X = [&](int t, int d) { return (t == 0 ? c.hx : t == 1 ? c.rhx : c.rsx)[gi + d]; };
+        auto Y = [&](int t, int d) { return (t == 0 ? c.hy : t == 1 ? c.rhy : c.rsy)[j + d]; };
+        double cun, cvn, ru_, rv_;
+        rhs_cell<true, TopoMask>(g, c, dt, re, U, V, X, Y, phi, li, j, cu[o], cv[o], cun, cvn, ru_, rv_);
+        cu[o] = cun;
+        cv[o] = cvn;
+        ru[o] = ru_;
+        rv[o] = rv_;
+        acc[0] = ru_ * ru_;
+        acc[1] = rv_ * rv_;
+    }
+    block_reduce_sum<2>(acc, part + 2 * blockIdx.x);
 }
 
 // the wall cells' ApplyBoundaryConditions terms (rhs_bc) on top of k_rhs_lds's values -- the
@@ -3818,41 +3870,56 @@ __global__ __launch_bounds__(256) void k_apply(Geo g, Coef c, double alpha, cons
 }
 
 // (r5) the masked domain's Helmholtz solve by red-black SOR (one rank; ns_solver.cpp helm_solve), k_apply<1, T>'s
-// operator: par 0 / 1 relaxes the cells of that colour ((gi + j) parity) in place, x += omega (b - A x) / d, a
-// half-sweep reading only the other colour; par 2 leaves x and writes the block partials of ||b - A x||^2
+// operator on x (rhs b) and, if x2 is not null, x2 (rhs b2) in the same pass -- the topology decoded once for u
+// and v: par 0 / 1 relaxes the cells of that colour ((gi + j) parity) in place, x += omega (b - A x) / d, a
+// half-sweep reading only the other colour, one thread per cell OF THAT COLOUR (j = 2 jx + parity); par 2 leaves
+// x and writes the block partials of ||b - A x||^2 (and ||b2 - A x2||^2: 2 per block)
 template <class T>
 __global__ __launch_bounds__(256) void k_helm_rb_mask(Geo g, Coef c, double alpha, double omega, double* __restrict__ x,
-                                                      const double* __restrict__ b, int par, double* __restrict__ part,
+                                                      const double* __restrict__ b, double* __restrict__ x2,
+                                                      const double* __restrict__ b2, int par, double* __restrict__ part,
                                                       int rows) {
-    const int j = blockIdx.x * 64 + threadIdx.x;
+    const int jx = blockIdx.x * 64 + threadIdx.x;
     const int lend = min((int)(blockIdx.y + 1) * 4 * rows, g.nxl);
-    double acc[1] = {0.0};
-    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend && j < g.ny; li += 4) {
+    double acc[2] = {0.0, 0.0};
+    for (int li = blockIdx.y * 4 * rows + threadIdx.y; li < lend; li += 4) {
         const int gi = g.i0 + li, ld = g.ld;
-        if (par < 2 && ((gi + j) & 1) != par) continue;
+        const int j = par < 2 ? 2 * jx + ((par + gi) & 1) : jx;
+        if (j >= g.ny) continue;
         const T t(g, li, j);
         if (!t.cell()) continue;
         const ptrdiff_t o = (ptrdiff_t)li * ld + j;
-        const double xc = x[o], hx = c.hx[gi], hy = c.hy[j];
+        const double hx = c.hx[gi], hy = c.hy[j];
         const double w2[4] = {1.0 / (hx * hx), 1.0 / (hx * hx), 1.0 / (hy * hy), 1.0 / (hy * hy)};
         const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
         const double pn[4] = {c.pw[gi], c.pe[gi], c.ps[j], c.pn[j]};
-        double s = 0.0, d = 0.0;
+        // the stencil as weights: A x = x - alpha (sum_k wk x_nb(k) - wc x_c), wk = 0 where the face has no neighbour
+        double wk[4], wc = 0.0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
+            wk[k] = 0.0;
             if (t.in(di[k], dj[k])) {
-                s += pn[k] * (x[o + di[k] * ld + dj[k]] - xc);
-                d -= pn[k];
+                wk[k] = pn[k];
+                wc += pn[k];
             } else if (!t.edge(k).neu) {
-                s += -2.0 * xc * w2[k];
-                d -= 2.0 * w2[k];
+                wc += 2.0 * w2[k];
             }
         }
-        const double r = b[o] - (xc - alpha * s);
-        if (par < 2) x[o] = xc + omega * r / (1.0 - alpha * d);
-        else acc[0] += r * r;
+        const double dinv = omega / (1.0 + alpha * wc);
+        auto relax = [&](double* __restrict__ xf, const double* __restrict__ bf, double& a) {
+            const double xc = xf[o];
+            double s = -wc * xc;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (wk[k] != 0.0) s = fma(wk[k], xf[o + di[k] * ld + dj[k]], s);
+            const double r = bf[o] - (xc - alpha * s);
+            if (par < 2) xf[o] = fma(dinv, r, xc);
+            else a += r * r;
+        };
+        relax(x, b, acc[0]);
+        if (x2) relax(x2, b2, acc[1]);
     }
-    if (par == 2) block_reduce_sum<1>(acc, part + (blockIdx.x + gridDim.x * blockIdx.y));
+    if (par == 2) block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
 }
 
 // z = q / diag(A) (the Jacobi preconditioner of the masked-domain Krylov solves; the
@@ -4092,11 +4159,23 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
     // (the grid kernels cannot split: the interior phase launches nothing, the edge phase all;
     // K1 updates cu / cv in place, so no cell may run twice)
     if (g.fc) {   // masked domain: the grid kernel with the polygon's topology
-        const int rows = cell_rows(g);
-        const dim3 cg = cell_grid(g, rows);
-        if (g_phase != 1)
-            NS_LAUNCH(k_rhs<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
-        return (int)(cg.x * cg.y);
+        if (e && std::strcmp(e, "global") == 0) {   // (A/B: r1-r4's global-load kernel)
+            const int rows = cell_rows(g);
+            const dim3 cg = cell_grid(g, rows);
+            if (g_phase != 1)
+                NS_LAUNCH(k_rhs<TopoMask>, cg, dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv, part, rows);
+            return (int)(cg.x * cg.y);
+        }
+        // (r5) LDS tiles for the FC_DEEP cells (k_rhs_lds<true>), then the listed others (k_rhs_cells); the whole
+        // slab in one pass (no phase split, as above)
+        const int nti = (g.nxl + RT - 1) / RT, nb = ((g.ny + 63) / 64) * nti, ne = (g.necell + 255) / 256;
+        if (g_phase != 1) {
+            NS_LAUNCH(k_rhs_lds<true>, dim3((g.ny + 63) / 64, nti), dim3(64, 4), 0, st, g, c, dt, re, u, v, phi, cu, cv,
+                      ru, rv, part, nti, nti);
+            if (ne > 0) NS_LAUNCH(k_rhs_cells, dim3(ne), dim3(256), 0, st, g, c, dt, re, u, v, phi, cu, cv, ru, rv,
+                                  part + 2 * nb);
+        }
+        return nb + ne;
     }
     if (!e) {
         // the streaming inner kernel (k_rhs_s) with its wall ring (extra workgroups of the same launch)
@@ -4152,7 +4231,7 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         const int nrun = phase_range(g.nxl, RT, nti, 2, &tlo, &thi0);   // MUSCL: rows li0-2 .. li0+RT+1
         const int nb = ((g.ny + 63) / 64) * nti;
         if (nrun > 0)
-            NS_LAUNCH(k_rhs_lds, dim3((g.ny + 63) / 64, nrun), dim3(64, 4), 0, st, g, c, dt, re, u, v, phi,
+            NS_LAUNCH(k_rhs_lds<false>, dim3((g.ny + 63) / 64, nrun), dim3(64, 4), 0, st, g, c, dt, re, u, v, phi,
                                cu, cv, ru, rv, part, tlo, thi0);
         const int nbc = (2 * g.nxl + 2 * g.ny + 255) / 256;
         // the wall terms read phi's ghost rows: with the edge phase
@@ -4228,12 +4307,13 @@ int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double
     return (int)(cg.x * cg.y);
 }
 
-int launch_helm_rb_mask(const Geo& g, const Coef& c, double alpha, double omega, double* x, const double* b, int par,
-                        double* part, hipStream_t st) {
+int launch_helm_rb_mask(const Geo& g, const Coef& c, double alpha, double omega, double* x, const double* b,
+                        double* x2, const double* b2, int par, double* part, hipStream_t st) {
     const int rows = cell_rows(g);
-    const dim3 cg = cell_grid(g, rows);
-    if (g.fc) NS_LAUNCH(k_helm_rb_mask<TopoMask>, cg, dim3(64, 4), 0, st, g, c, alpha, omega, x, b, par, part, rows);
-    else NS_LAUNCH(k_helm_rb_mask<TopoRect>, cg, dim3(64, 4), 0, st, g, c, alpha, omega, x, b, par, part, rows);
+    dim3 cg = cell_grid(g, rows);
+    if (par < 2) cg.x = ((g.ny + 1) / 2 + 63) / 64;   // (one thread per cell of the colour)
+    if (g.fc) NS_LAUNCH(k_helm_rb_mask<TopoMask>, cg, dim3(64, 4), 0, st, g, c, alpha, omega, x, b, x2, b2, par, part, rows);
+    else NS_LAUNCH(k_helm_rb_mask<TopoRect>, cg, dim3(64, 4), 0, st, g, c, alpha, omega, x, b, x2, b2, par, part, rows);
     return (int)(cg.x * cg.y);
 }
 void launch_diag_pc(int op, const Geo& g, const Coef& c, double alpha, const double* q, double* z, hipStream_t st,

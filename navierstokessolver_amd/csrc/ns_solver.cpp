@@ -17,6 +17,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -231,6 +232,7 @@ struct ns_solver {
     double area = 0.0;           // sum of the domain's cell areas
     double inv_area = 0.0;       // sum of their reciprocals
     int32_t* fc_mem = nullptr;   // masked domain: topology plane (g.fc) and edge table (g.et)
+    int32_t* ecell_mem = nullptr;   // (r5) masked domain: the slab's domain cells that are not FC_DEEP (g.ecell)
     nsg::EdgeDev* et_mem = nullptr;
     ns_host_transport ht{};      // host transport (ht.exchange != NULL) instead of RCCL
     double* stage = nullptr;     // pinned staging for the host transport
@@ -284,6 +286,10 @@ struct ns_solver {
     // (1e-13 .. 1e-12 of ||b|| at 4096^2).  NSGPU_FPS=0: multigrid
     bool fps = false;
     bool fps_pc = false;         // masked domain: the bounding box's direct solve preconditions BiCGStab (NSGPU_FPS_PC=0: V-cycle)
+    // (r5) and, with at most NSGPU_CAP_MAX (4096) interface faces, the exact solve by the capacitance matrix
+    // (cap_setup / cap_solve; NSGPU_CAP=0: BiCGStab preconditioned by the box's solve, A/B)
+    nsg::CapArgs cap{};
+    void* cap_mem = nullptr;
     nsg::FpsArgs fa{};
     double* fps_mem = nullptr;
     const double *fps_tw = nullptr, *fps_wk = nullptr;
@@ -939,19 +945,15 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         double r2u = 0.0, r2v = 0.0;
         for (;;) {
             const int n = std::min(batch, s->max_iters - sweeps);
+            // (u and v in the same launches: the topology decoded once -- 4 -> 2 launches per sweep)
+            double *U = s->arr[NS_ARR_U], *V = s->arr[NS_ARR_V];
+            const double *RU = s->arr[NS_ARR_RU], *RV = s->arr[NS_ARR_RV];
             for (int k = 0; k < n; k++)
-                for (int f : {NS_ARR_U, NS_ARR_V})
-                    for (int par : {0, 1})
-                        nsg::launch_helm_rb_mask(s->g, s->c, alpha, s->omega_v, s->arr[f], s->arr[f == NS_ARR_U ? NS_ARR_RU : NS_ARR_RV],
-                                                 par, nullptr, s->st);
+                for (int par : {0, 1})
+                    nsg::launch_helm_rb_mask(s->g, s->c, alpha, s->omega_v, U, RU, V, RV, par, nullptr, s->st);
             sweeps += n;
-            int nb = 0;
-            for (int f : {NS_ARR_U, NS_ARR_V})
-                nb = nsg::launch_helm_rb_mask(s->g, s->c, alpha, s->omega_v, s->arr[f],
-                                              s->arr[f == NS_ARR_U ? NS_ARR_RU : NS_ARR_RV], 2,
-                                              s->part + (f == NS_ARR_U ? 0 : (size_t)nsg::max_partials(s->g)), s->st);
-            nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
-            nsg::launch_reduce_sum(s->part + nsg::max_partials(s->g), nb, 1, s->scal + S_RES + 1, s->st);
+            const int nb = nsg::launch_helm_rb_mask(s->g, s->c, alpha, s->omega_v, U, RU, V, RV, 2, s->part, s->st);
+            nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_RES, s->st);
             CHK(fetch(s));
             r2u = s->hs[S_RES];
             r2v = s->hs[S_RES + 1];
@@ -1717,6 +1719,108 @@ int fps_precond(ns_solver* s, const double* q, double* z, double* scratch) {
     return 0;
 }
 
+// (r5) z = L_ext^+ q on a masked domain by its capacitance matrix (nsg::CapArgs): two box solves around the
+// interface's dense m x m solve -- z1 = L_box^+ q, y = (C + 1 1^T / m)^-1 D^T z1, z = L_box^+ (q - D_w y).  q is mean-
+// free over the domain and 0 outside it (the residual k_bicg_vec's KV_INIT leaves); it is modified at the
+// interface cells and restored to 0 outside (its domain values are rewritten by the next KV_INIT)
+int cap_solve(ns_solver* s, double* q, double* z) {
+    CHK(fps_precond(s, q, z, s->kv[8]));
+    nsg::launch_cap_gemv(s->cap, z, s->st);
+    nsg::launch_cap_scatter(s->cap, q, 0, s->st);
+    CHK(fps_precond(s, q, z, s->kv[8]));
+    nsg::launch_cap_scatter(s->cap, q, 1, s->st);
+    return 0;
+}
+
+// (r5) the capacitance matrix of a masked domain on one rank whose bounding box has the direct solve: the m
+// faces between a domain cell and a box cell outside it, then C's columns by m box solves of the faces'
+// dipoles w_f d_f (C[g][f] = delta_gf + (D^T L_box^+ w_f d_f)_g, + 1 / m: the regularisation along the domain's
+// constant y0 = 1, C y0 = 0) and its inverse by Gauss-Jordan, all on the device.  Not built (BiCGStab with the box
+// preconditioner stays): m = 0 or > NSGPU_CAP_MAX (4096), NSGPU_CAP=0, a non-positive pivot
+int cap_setup(ns_solver* s, const ns_grid_desc* gd, const double* pw, const double* pe, const double* ps,
+              const double* pn) {
+    const char* ce = getenv("NSGPU_CAP");
+    if (ce && std::atoi(ce) == 0) return 0;
+    const char* cm = getenv("NSGPU_CAP_MAX");
+    const long mmax = cm ? std::atol(cm) : 4096;
+    const nsg::Geo& g = s->g;
+    const int nx = gd->nx, ny = gd->ny;
+    auto inside = [&](int i, int j) { return gd->cell_id[(size_t)i * ny + j] >= 0; };
+    std::vector<int> fi, fj;
+    std::vector<double> w;
+    std::map<int, std::vector<int>> refs;   // plane offset -> signed face references
+    const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < ny; j++) {
+            if (!inside(i, j)) continue;
+            for (int k = 0; k < 4; k++) {
+                const int a = i + di[k], b = j + dj[k];
+                if (a < 0 || a >= nx || b < 0 || b >= ny || inside(a, b)) continue;
+                const int f = (int)fi.size();
+                if ((long)f >= mmax) return 0;
+                const int oi = (i - g.i0) * g.ld + j, oj = (a - g.i0) * g.ld + b;
+                fi.push_back(oi);
+                fj.push_back(oj);
+                // (the coefficient of this face in the domain cell's row; the same in the outside cell's row on the
+                // uniform grids the box's direct solve admits)
+                w.push_back(k == 0 ? pw[i] : k == 1 ? pe[i] : k == 2 ? ps[j] : pn[j]);
+                refs[oi].push_back(f + 1);
+                refs[oj].push_back(-(f + 1));
+            }
+        }
+    const int m = (int)fi.size();
+    if (m == 0) return 0;
+    std::vector<int> co;
+    std::vector<int> cf;
+    for (const auto& kv : refs) {
+        if (kv.second.size() > 4) return 0;   // (a cell has 4 faces)
+        co.push_back(kv.first);
+        for (int k = 0; k < 4; k++) cf.push_back(k < (int)kv.second.size() ? kv.second[k] : 0);
+    }
+    const int nc = (int)co.size();
+    // device: cinv (m^2), y, w, t, u, flag (doubles); fi, fj, co, cf (ints)
+    // (nd even and the int4 table at a multiple of 4 ints: 16-byte aligned)
+    const size_t nd = ((size_t)m * m + 4 * (size_t)m + 9) & ~(size_t)1, o4 = (2 * (size_t)m + nc + 3) & ~(size_t)3;
+    const size_t ni = o4 + 4 * (size_t)nc;
+    HIPCHK(hipMalloc(&s->cap_mem, nd * sizeof(double) + ni * sizeof(int)));
+    double* dm = (double*)s->cap_mem;
+    double *cinv = dm, *y = cinv + (size_t)m * m, *wd = y + m, *t = wd + m, *u = t + m, *flag = u + m;
+    int* im = (int*)(dm + nd);
+    int *dfi = im, *dfj = dfi + m, *dco = dfj + m;
+    int* dcf = im + o4;
+    HIPCHK(hipMemcpy(wd, w.data(), m * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(flag, 0, sizeof(double)));
+    HIPCHK(hipMemcpy(dfi, fi.data(), m * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dfj, fj.data(), m * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dco, co.data(), nc * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dcf, cf.data(), 4 * (size_t)nc * sizeof(int), hipMemcpyHostToDevice));
+    nsg::CapArgs& a = s->cap;
+    a.m = m; a.ncell = nc;
+    a.fi = dfi; a.fj = dfj; a.co = dco; a.cf = (const int4*)dcf; a.w = wd;
+    a.cinv = cinv; a.y = y;
+    // C by columns: the dipole in the (zeroed) plane kv[0], its box solve into kv[6]
+    HIPCHK(hipStreamSynchronize(s->st));   // (the Krylov planes' memset)
+    for (int f = 0; f < m; f++) {
+        nsg::launch_cap_src(a, s->kv[0], f - 1, f, s->st);
+        CHK(fps_precond(s, s->kv[0], s->kv[6], s->kv[8]));
+        nsg::launch_cap_col(a, s->kv[6], f, cinv, s->st);
+    }
+    nsg::launch_cap_src(a, s->kv[0], m - 1, -1, s->st);
+    nsg::launch_gj_invert(cinv, m, t, u, flag, s->st);
+    double fl = 0.0;
+    HIPCHK(hipMemcpyAsync(&fl, flag, sizeof(double), hipMemcpyDeviceToHost, s->st));
+    HIPCHK(hipStreamSynchronize(s->st));
+    if (fl != 0.0) {   // (never seen: the preconditioned BiCGStab instead)
+        if (s->verbose) fprintf(stderr, "nsgpu: capacitance matrix (%d faces) not positive definite: BiCGStab\n", m);
+        s->cap = nsg::CapArgs{};
+        (void)hipFree(s->cap_mem);
+        s->cap_mem = nullptr;
+        return 0;
+    }
+    if (s->verbose) fprintf(stderr, "nsgpu: masked Poisson by the capacitance matrix: %d interface faces, %d cells\n", m, nc);
+    return 0;
+}
+
 // One BiCGStab solve A x = b - shift on this solver's planes (x updated in place).
 //   op 0: the Poisson matrix (NEUMANN outflow rows / a masked domain), solved as
 //         P A x = P (b - shift) with P the mean projection over the domain's cells;
@@ -1796,6 +1900,31 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
     int batch = s->verbose ? 1 : std::max(1, gated ? s->kpred[kind] + 1 : s->kpred[kind] - 1);
     nsg::launch_bicg_start(s->ksc, tol2 * ks.b2, ks.b2, maxit, s->st);
     CHK(init());
+    int its0 = 0;   // (the capacitance solve's refinements before any BiCGStab iteration)
+    if (ks.op == 0 && s->cap.m > 0) {
+        // (r5) a masked domain with its capacitance matrix: x += L_ext^+ r (exact up to round-off), then the
+        // residual -- one host read per refinement; a second one only at rtol near the round-off (~1e-13).
+        // Stagnating after 3: BiCGStab preconditioned by the box's solve from this x
+        for (;;) {
+            CHK(cap_solve(s, a.r, s->kv[6]));
+            nsg::launch_cap_axpy(s->g, a.x, s->kv[6], s->st);
+            CHK(init());
+            its0++;
+            HIPCHK(hipMemcpyAsync(s->scal + S_KRY, d, sizeof(double), hipMemcpyDeviceToDevice, s->st));
+            CHK(fetch(s));
+            const double r2 = s->hs[S_KRY], b2 = ks.b2;
+            *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
+            *its = its0;
+            if (s->verbose)
+                fprintf(stderr, "nsgpu %s (capacitance solve): refinement %d rel. residual %.3e\n", ks.name, its0, *res);
+            if (!std::isfinite(r2) || (b2 > 0 && r2 > 1e16 * b2)) {
+                set_err("%s (capacitance solve) diverged: relative residual %g", ks.name, *res);
+                return NS_EDIVERGE;
+            }
+            if (r2 <= tol2 * b2 || r2 == 0.0) return 0;
+            if (its0 >= 3) break;
+        }
+    }
     int restarts = 0;
     for (;;) {
         for (int q = 0; q < batch; q++) CHK(iteration());
@@ -1824,7 +1953,7 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
         if (s->verbose)
             fprintf(stderr, "nsgpu %s (bicgstab): it %d rel. residual %.3e (alpha %.3e omega %.3e%s)\n", ks.name, it,
                     *res, s->hs[S_KRY + 5], s->hs[S_KRY + 6], brk ? ", breakdown: restart" : "");
-        *its = it;
+        *its = its0 + it;
         if (!stopped) {
             batch = s->verbose ? 1 : (gated ? 2 : 1);
             continue;
@@ -1840,7 +1969,7 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
         CHK(init());
         batch = 1;
     }
-    s->kpred[kind] = *its;
+    s->kpred[kind] = *its - its0;
     return 0;
 }
 
@@ -3216,6 +3345,9 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
                         }
                     }
                 }
+                if (inside(i - 1, j) && inside(i - 2, j) && inside(i + 1, j) && inside(i + 2, j) && inside(i, j - 1) &&
+                    inside(i, j - 2) && inside(i, j + 1) && inside(i, j + 2))
+                    code |= nsg::FC_DEEP;
                 fch[(size_t)(li + nsg::HALO) * g.ld + j] = code;
             }
         }
@@ -3487,6 +3619,18 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
             hipMemcpy(s->et_mem, etab.data(), etab.size() * sizeof(nsg::EdgeDev), hipMemcpyHostToDevice) != hipSuccess) { set_err("topology upload failed"); return fail(NS_EHIP); }
         s->g.fc = s->fc_mem + (size_t)nsg::HALO * g.ld;
         s->g.et = s->et_mem;
+        std::vector<int32_t> ec;
+        for (int li = 0; li < g.nxl; li++)
+            for (int j = 0; j < g.ny; j++) {
+                const int32_t code = fch[(size_t)(li + nsg::HALO) * g.ld + j];
+                if ((code & nsg::FC_IN) && !(code & nsg::FC_DEEP)) ec.push_back(li * g.ld + j);
+            }
+        if (!ec.empty()) {
+            if (hipMalloc(&s->ecell_mem, ec.size() * sizeof(int32_t)) != hipSuccess) { set_err("hipMalloc topology failed"); return fail(NS_ENOMEM); }
+            if (hipMemcpy(s->ecell_mem, ec.data(), ec.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) { set_err("topology upload failed"); return fail(NS_EHIP); }
+            s->g.ecell = s->ecell_mem;
+            s->g.necell = (int)ec.size();
+        }
     }
 
     // coefficient tables (ConstructLHS, FluidSolver.cpp:113-131)
@@ -3568,6 +3712,11 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (hipMalloc(&s->ksc, nsg::KS_NUM * sizeof(double)) != hipSuccess) { set_err("hipMalloc failed"); return fail(NS_ENOMEM); }
         if (hipMemsetAsync(s->ksc, 0, nsg::KS_NUM * sizeof(double), s->st) != hipSuccess) { set_err("memset failed"); return fail(NS_EHIP); }
     }
+    if (s->fps_pc && s->kv[0]) {   // (r5) the masked domain's capacitance matrix
+        const std::vector<double> h = coef_tables(hx0, hy0, g.neu);
+        if (int rc = cap_setup(s, gd, h.data(), h.data() + g.nx, h.data() + 3 * g.nx, h.data() + 3 * g.nx + g.ny))
+            return fail(rc);
+    }
     const int np = nsg::max_partials(g);
     // partials: [0, 4 np) for any kernel's, [4 np, 8 np) for a speculative K5's (correct_launch)
     if (hipMalloc(&s->part, (size_t)np * 8 * sizeof(double)) != hipSuccess) { set_err("hipMalloc partials failed"); return fail(NS_ENOMEM); }
@@ -3624,10 +3773,12 @@ void ns_destroy(ns_solver* s) {
     if (s->cvimg) (void)hipFree(s->cvimg);
     if (s->dmat) (void)hipFree(s->dmat);
     if (s->fps_mem) (void)hipFree(s->fps_mem);
+    if (s->cap_mem) (void)hipFree(s->cap_mem);
     for (auto e : s->kev)
         if (e) (void)hipEventDestroy(e);
     if (s->f32_mem) (void)hipFree(s->f32_mem);
     if (s->fc_mem) (void)hipFree(s->fc_mem);
+    if (s->ecell_mem) (void)hipFree(s->ecell_mem);
     if (s->et_mem) (void)hipFree(s->et_mem);
     if (s->ksc) (void)hipFree(s->ksc);
     if (s->coef) (void)hipFree(s->coef);

@@ -260,6 +260,7 @@ def test_masked_poisson_with_box_direct_preconditioner(gpu, monkeypatch):
     rng = np.random.default_rng(41)
     b = rng.uniform(-1, 1, og.N)
     out = {}
+    monkeypatch.setenv("NSGPU_CAP", "0")   # (the capacitance solve: the next test)
     for pc in ("1", "0"):
         monkeypatch.setenv("NSGPU_FPS_PC", pc)
         gs = gpu.GpuSolver(gpu.polygon(verts, og.hx, og.hy, bc), 1e-3, 100.0, rtol=1e-12)
@@ -276,6 +277,47 @@ def test_masked_poisson_with_box_direct_preconditioner(gpu, monkeypatch):
     xp, _ = og.solve_poisson(b)
     assert rel(out["1"][1], demean(xp)) <= 1e-8
     assert out["1"][0] <= out["0"][0], (out["1"][0], out["0"][0])
+
+
+CAP_SHAPES = {
+    # (the L-shaped cavity; a U-shaped one: a notch from the top, 8 edges, two inner corners more)
+    "lshape": ([(0, 0), (0, 1), (1, 1), (1, 0.5), (0.5, 0.5), (0.5, 0)], [(2, 0.0), (2, 1.0)] + [(2, 0.0)] * 4),
+    "ushape": ([(0, 0), (0, 1), (0.375, 1), (0.375, 0.5), (0.625, 0.5), (0.625, 1), (1, 1), (1, 0)],
+               [(2, 0.0), (2, 1.0)] + [(2, 0.0)] * 6),
+}
+
+
+@pytest.mark.parametrize("shape,nx,ny", [("lshape", 128, 128), ("lshape", 96, 64), ("ushape", 64, 128)])
+def test_masked_poisson_capacitance_solve(gpu, monkeypatch, shape, nx, ny):
+    """(r5) A masked domain on one rank whose bounding box has the direct solve: the exact solve by the capacitance
+    matrix of its interface with the box (ns_solver.cpp cap_setup / cap_solve: two box solves around a dense m x m
+    solve, m the interface faces) -- L-shapes with hx = hy and hx != hy (unequal face weights: the non-symmetric
+    capacitance matrix) and a U-shape.  Residual <= 1e-12 in at most 2 refinements (BiCGStab preconditioned by the
+    box's solve, NSGPU_CAP=0, takes several iterations); phi (modulo its mean) the same as that path's to 1e-9 of
+    its max and the oracle's converged solve to 1e-8."""
+    verts, bc = CAP_SHAPES[shape]
+    og = OGrid(verts, [[0, 1, nx, -1]], [[0, 1, ny, -1]], bc)
+    rng = np.random.default_rng(43)
+    b = rng.uniform(-1, 1, og.N)
+    out = {}
+    for cap in ("1", "0"):
+        monkeypatch.setenv("NSGPU_CAP", cap)
+        gs = gpu.GpuSolver(gpu.polygon(verts, og.hx, og.hy, bc), 1e-3, 100.0, rtol=1e-12)
+        m = gs.grid.mask.ravel()
+        p = np.zeros(m.size)
+        p[m] = b
+        gs.set(gpu.NS_ARR_PHI, np.zeros(m.size))
+        gs.set(gpu.NS_ARR_RPHI, p)
+        its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+        assert res <= 1e-12, (cap, its, res)
+        phi = gs.get(gpu.NS_ARR_PHI).ravel()
+        assert not np.any(phi[~m]), "cells outside the domain must stay 0"
+        out[cap] = (int(its), demean(phi[m]))
+        gs.close()
+    assert out["1"][0] <= 2 < out["0"][0], (out["1"][0], out["0"][0])
+    assert rel(out["1"][1], out["0"][1]) <= 1e-9
+    xp, _ = og.solve_poisson(b)
+    assert rel(out["1"][1], demean(xp)) <= 1e-8
 
 
 def test_direct_solve_check_policy(gpu):
