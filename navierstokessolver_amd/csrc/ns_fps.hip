@@ -1664,12 +1664,21 @@ __global__ __launch_bounds__(256) void k_cap_scatter(CapArgs a, double* __restri
     q[a.co[c]] -= acc;
 }
 
-// x += z on the domain's cells
-__global__ __launch_bounds__(256) void k_cap_axpy(Geo g, double* __restrict__ x, const double* __restrict__ z) {
+// x += z on the domain's cells (set: x = z)
+__global__ __launch_bounds__(256) void k_cap_axpy(Geo g, double* __restrict__ x, const double* __restrict__ z, int set) {
     const int j = blockIdx.x * 64 + threadIdx.x, li = blockIdx.y * 4 + threadIdx.y;
     if (j >= g.ny || li >= g.nxl) return;
     const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
-    if (g.fc[o] & FC_IN) x[o] += z[o];
+    if (g.fc[o] & FC_IN) x[o] = set ? z[o] : x[o] + z[o];
+}
+
+// r = b - *shift on the domain's cells (the first capacitance solve's right-hand side, from x = 0)
+__global__ __launch_bounds__(256) void k_cap_rhs(Geo g, const double* __restrict__ b, const double* __restrict__ shift,
+                                                 double* __restrict__ r) {
+    const int j = blockIdx.x * 64 + threadIdx.x, li = blockIdx.y * 4 + threadIdx.y;
+    if (j >= g.ny || li >= g.nxl) return;
+    const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
+    if (g.fc[o] & FC_IN) r[o] = b[o] - (shift ? shift[0] : 0.0);
 }
 
 // set-up: the source w_f d_f of column f in the zeroed plane q (the previous column's cleared; f < 0: only that)
@@ -1716,8 +1725,11 @@ void launch_cap_gemv(const CapArgs& a, const double* z, hipStream_t st) {
 void launch_cap_scatter(const CapArgs& a, double* q, int mode, hipStream_t st) {
     hipLaunchKernelGGL(k_cap_scatter, dim3((a.ncell + 255) / 256), dim3(256), 0, st, a, q, mode);
 }
-void launch_cap_axpy(const Geo& g, double* x, const double* z, hipStream_t st) {
-    hipLaunchKernelGGL(k_cap_axpy, dim3((g.ny + 63) / 64, (g.nxl + 3) / 4), dim3(64, 4), 0, st, g, x, z);
+void launch_cap_axpy(const Geo& g, double* x, const double* z, int set, hipStream_t st) {
+    hipLaunchKernelGGL(k_cap_axpy, dim3((g.ny + 63) / 64, (g.nxl + 3) / 4), dim3(64, 4), 0, st, g, x, z, set);
+}
+void launch_cap_rhs(const Geo& g, const double* b, const double* shift, double* r, hipStream_t st) {
+    hipLaunchKernelGGL(k_cap_rhs, dim3((g.ny + 63) / 64, (g.nxl + 3) / 4), dim3(64, 4), 0, st, g, b, shift, r);
 }
 void launch_cap_src(const CapArgs& a, double* q, int fprev, int f, hipStream_t st) {
     hipLaunchKernelGGL(k_cap_src, dim3(1), dim3(1), 0, st, a, q, fprev, f);

@@ -288,6 +288,10 @@ struct KrylovArgs {
 // per block; returns the block count); masked domains' Helmholtz solve (one rank)
 int launch_helm_rb_mask(const Geo& g, const Coef& c, double alpha, double omega, double* x, const double* b,
                         double* x2, const double* b2, int par, double* part, hipStream_t st);
+// (r5) one whole red-black sweep of the same operator on u and v (rhs bu, bv) out of place, u, v -> uo, vo (LDS tiles;
+// the values of a red and a black launch of the above); one rank
+void launch_helm_rbt_mask(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                          const double* bu, const double* bv, double* uo, double* vo, hipStream_t st);
 // (stop: a KS_STOP slot -- the grid kernels then do nothing once it is set; null: always run)
 int launch_apply(int op, const Geo& g, const Coef& c, double alpha, const double* x, double* y, const double* q,
                  double* part, hipStream_t st, const double* stop = nullptr);
@@ -416,7 +420,8 @@ struct CapArgs {
 };
 void launch_cap_gemv(const CapArgs& a, const double* z, hipStream_t st);                // y = cinv D^T z
 void launch_cap_scatter(const CapArgs& a, double* q, int mode, hipStream_t st);         // q -= D_w y / q = 0 outside
-void launch_cap_axpy(const Geo& g, double* x, const double* z, hipStream_t st);         // x += z on the domain
+void launch_cap_axpy(const Geo& g, double* x, const double* z, int set, hipStream_t st);  // x += z (set: =) on the domain
+void launch_cap_rhs(const Geo& g, const double* b, const double* shift, double* r, hipStream_t st);   // r = b - shift
 void launch_cap_src(const CapArgs& a, double* q, int fprev, int f, hipStream_t st);     // set-up: column f's source
 void launch_cap_col(const CapArgs& a, const double* z, int f, double* cmat, hipStream_t st);
 void launch_gj_invert(double* A, int m, double* t, double* u, double* flag, hipStream_t st);

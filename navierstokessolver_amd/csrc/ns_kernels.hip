@@ -3922,6 +3922,92 @@ __global__ __launch_bounds__(256) void k_helm_rb_mask(Geo g, Coef c, double alph
     if (par == 2) block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
 }
 
+// (r5) one whole red-black SOR sweep of k_helm_rb_mask's operator on u and v per launch, out of place (u, v ->
+// uo, vo): a tile of RTM x 64 cells staged in LDS with a 2-cell ring; red relaxed over the tile and its 1-cell ring
+// (the ring's red values the tile's black cells need), then black over the tile, from the same old values a
+// red launch and a black launch would read -- the same arithmetic, half the launches and HBM passes
+constexpr int RTM = 16;
+__global__ __launch_bounds__(256) void k_helm_rbt_mask(Geo g, Coef c, double alpha, double omega,
+                                                       const double* __restrict__ u, const double* __restrict__ v,
+                                                       const double* __restrict__ bu, const double* __restrict__ bv,
+                                                       double* __restrict__ uo, double* __restrict__ vo) {
+    constexpr int EI = RTM + 4, EJ = 64 + 4, NQ = (EI * EJ + 255) / 256;
+    __shared__ double su[EI][EJ], sv[EI][EJ];
+    const int li0 = blockIdx.y * RTM, j0 = blockIdx.x * 64, ld = g.ld;
+    const int tid = threadIdx.x + 64 * threadIdx.y;
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const int q = tid + 256 * k;
+        if (q < EI * EJ) {
+            const int r = q / EJ, cc = q - r * EJ;
+            const int li = min(max(li0 - 2 + r, -HALO), g.nxl + HALO - 1);
+            const int j = min(max(j0 - 2 + cc, 0), g.ny - 1);
+            su[r][cc] = ldf(u, ld, li, j);
+            sv[r][cc] = ldf(v, ld, li, j);
+        }
+    }
+    __syncthreads();
+    // relax cell (li, j) at LDS (R, C) of colour par if in the domain (one rank: the ring's cells outside the slab
+    // are outside the box -- their codes are 0)
+    auto relax = [&](int li, int j, int R, int C) {
+        if (j < 0 || j >= g.ny || li < -1 || li > g.nxl) return;
+        const TopoMask t(g, li, j);
+        if (!t.cell()) return;
+        const int gi = g.i0 + li;
+        const double hx = c.hx[gi], hy = c.hy[j];
+        const double w2[4] = {1.0 / (hx * hx), 1.0 / (hx * hx), 1.0 / (hy * hy), 1.0 / (hy * hy)};
+        const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
+        const double pn[4] = {c.pw[gi], c.pe[gi], c.ps[j], c.pn[j]};
+        double wk[4], wc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            wk[k] = 0.0;
+            if (t.in(di[k], dj[k])) {
+                wk[k] = pn[k];
+                wc += pn[k];
+            } else if (!t.edge(k).neu) {
+                wc += 2.0 * w2[k];
+            }
+        }
+        const double dinv = omega / (1.0 + alpha * wc);
+        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+        auto one = [&](double (*sx)[EJ], const double* __restrict__ bf) {
+            const double xc = sx[R][C];
+            double s = -wc * xc;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (wk[k] != 0.0) s = fma(wk[k], sx[R + di[k]][C + dj[k]], s);
+            const double r = bf[o] - (xc - alpha * s);
+            sx[R][C] = fma(dinv, r, xc);
+        };
+        one(su, bu);
+        one(sv, bv);
+    };
+    // red (colour 0) over rows li0 - 1 .. li0 + RTM, columns j0 - 1 .. j0 + 64: (RTM + 2) x 66 cells, half red
+    constexpr int RI = RTM + 2, RJ = 66;
+    for (int q = tid; q < RI * RJ; q += 256) {
+        const int r = q / RJ, cc = q - r * RJ;
+        const int li = li0 - 1 + r, j = j0 - 1 + cc;
+        if (((g.i0 + li + j) & 1) == 0) relax(li, j, r + 1, cc + 1);
+    }
+    __syncthreads();
+    // black over the tile: thread (x, y) walks rows y, y + 4, ... of column j0 + x
+    const int j = j0 + threadIdx.x;
+    for (int r = threadIdx.y; r < RTM; r += 4) {
+        const int li = li0 + r;
+        if (li < g.nxl && ((g.i0 + li + j) & 1) == 1) relax(li, j, r + 2, threadIdx.x + 2);
+    }
+    __syncthreads();
+    for (int r = threadIdx.y; r < RTM; r += 4) {
+        const int li = li0 + r;
+        if (li < g.nxl && j < g.ny) {
+            const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+            uo[o] = su[r + 2][threadIdx.x + 2];
+            vo[o] = sv[r + 2][threadIdx.x + 2];
+        }
+    }
+}
+
 // z = q / diag(A) (the Jacobi preconditioner of the masked-domain Krylov solves; the
 // outflow rows' diagonal -(sum p) + 1.5 w, oracle diag_poisson / diag_helmholtz)
 template <int OP, class T>
@@ -4315,6 +4401,11 @@ int launch_helm_rb_mask(const Geo& g, const Coef& c, double alpha, double omega,
     if (g.fc) NS_LAUNCH(k_helm_rb_mask<TopoMask>, cg, dim3(64, 4), 0, st, g, c, alpha, omega, x, b, x2, b2, par, part, rows);
     else NS_LAUNCH(k_helm_rb_mask<TopoRect>, cg, dim3(64, 4), 0, st, g, c, alpha, omega, x, b, x2, b2, par, part, rows);
     return (int)(cg.x * cg.y);
+}
+void launch_helm_rbt_mask(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                          const double* bu, const double* bv, double* uo, double* vo, hipStream_t st) {
+    NS_LAUNCH(k_helm_rbt_mask, dim3((g.ny + 63) / 64, (g.nxl + RTM - 1) / RTM), dim3(64, 4), 0, st, g, c, alpha, omega,
+              u, v, bu, bv, uo, vo);
 }
 void launch_diag_pc(int op, const Geo& g, const Coef& c, double alpha, const double* q, double* z, hipStream_t st,
                     const double* stop) {

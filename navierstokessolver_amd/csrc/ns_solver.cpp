@@ -317,7 +317,7 @@ struct ns_solver {
     int kpred[3] = {1, 1, 1};    // (r5) the last BiCGStab solve's iterations: Poisson, Helmholtz u, v (bicgstab's batch)
     // (r5) a masked domain's Helmholtz solve on one rank by red-black SOR (NSGPU_MASK_HELM=krylov: BiCGStab); the
     // sweeps the last step needed (the next step's first batch)
-    bool mask_rb = true;
+    bool mask_rb = true, mask_rbt = true;
     int mask_helm_next = 4, mask_helm_ok = 0;
     // r5, multi-rank rectangles: the Helmholtz check's collective is an allgather of every rank's
     // S_HBNL .. S_MML (bus()): K1's norms and the previous step's K5 min / max ride on it, so neither
@@ -948,9 +948,19 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
             // (u and v in the same launches: the topology decoded once -- 4 -> 2 launches per sweep)
             double *U = s->arr[NS_ARR_U], *V = s->arr[NS_ARR_V];
             const double *RU = s->arr[NS_ARR_RU], *RV = s->arr[NS_ARR_RV];
-            for (int k = 0; k < n; k++)
+            // (r5) whole sweeps in LDS tiles, U, V -> TU, TV -> U, V (an odd batch: its first sweep as the two
+            // in-place half-sweeps); NSGPU_MASK_RBT=0: half-sweeps only (A/B)
+            double *TU = s->arr[NS_ARR_TMPU], *TV = s->arr[NS_ARR_TMPV];
+            for (int k = 0; k < n; k++) {
+                if (s->mask_rbt && (n - k) % 2 == 0) {
+                    nsg::launch_helm_rbt_mask(s->g, s->c, alpha, s->omega_v, U, V, RU, RV, TU, TV, s->st);
+                    nsg::launch_helm_rbt_mask(s->g, s->c, alpha, s->omega_v, TU, TV, RU, RV, U, V, s->st);
+                    k++;
+                    continue;
+                }
                 for (int par : {0, 1})
                     nsg::launch_helm_rb_mask(s->g, s->c, alpha, s->omega_v, U, RU, V, RV, par, nullptr, s->st);
+            }
             sweeps += n;
             const int nb = nsg::launch_helm_rb_mask(s->g, s->c, alpha, s->omega_v, U, RU, V, RV, 2, s->part, s->st);
             nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_RES, s->st);
@@ -1899,15 +1909,16 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
     const bool gated = !ks.mg;
     int batch = s->verbose ? 1 : std::max(1, gated ? s->kpred[kind] + 1 : s->kpred[kind] - 1);
     nsg::launch_bicg_start(s->ksc, tol2 * ks.b2, ks.b2, maxit, s->st);
-    CHK(init());
     int its0 = 0;   // (the capacitance solve's refinements before any BiCGStab iteration)
     if (ks.op == 0 && s->cap.m > 0) {
-        // (r5) a masked domain with its capacitance matrix: x += L_ext^+ r (exact up to round-off), then the
-        // residual -- one host read per refinement; a second one only at rtol near the round-off (~1e-13).
-        // Stagnating after 3: BiCGStab preconditioned by the box's solve from this x
+        // (r5) a masked domain with its capacitance matrix: x = L_ext^+ (b - shift) (exact up to round-off; from
+        // x = 0: b - shift is the projected residual, no operator application), then the residual -- one host
+        // read per solve; a refinement x += L_ext^+ r only at rtol near the round-off (~1e-13).  Stagnating after
+        // 3: BiCGStab preconditioned by the box's solve from this x
+        nsg::launch_cap_rhs(s->g, ks.b, ks.shift, a.r, s->st);
         for (;;) {
             CHK(cap_solve(s, a.r, s->kv[6]));
-            nsg::launch_cap_axpy(s->g, a.x, s->kv[6], s->st);
+            nsg::launch_cap_axpy(s->g, a.x, s->kv[6], its0 == 0, s->st);
             CHK(init());
             its0++;
             HIPCHK(hipMemcpyAsync(s->scal + S_KRY, d, sizeof(double), hipMemcpyDeviceToDevice, s->st));
@@ -1924,6 +1935,8 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
             if (r2 <= tol2 * b2 || r2 == 0.0) return 0;
             if (its0 >= 3) break;
         }
+    } else {
+        CHK(init());
     }
     int restarts = 0;
     for (;;) {
@@ -3444,6 +3457,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_GIN")) s->gin = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_MASK_HELM")) s->mask_rb = std::strcmp(e, "krylov") != 0;
+    if (const char* e = getenv("NSGPU_MASK_RBT")) s->mask_rbt = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     if (const char* e = getenv("NSGPU_DIRECT_CELLS")) s->direct_cells = std::max(0L, std::atol(e));
     {

@@ -202,3 +202,22 @@ def test_mask_step_outflow_line_preconditioner(gpu, monkeypatch):
     for a, b in zip(out["line"], out["wall"]):
         np.testing.assert_allclose([a[k] for k in ("umin", "umax", "vmin", "vmax")],
                                    [b[k] for k in ("umin", "umax", "vmin", "vmax")], atol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["lshape", "step", "uchannel"])
+def test_mask_helmholtz_tiled_sweeps_bit_identical(gpu, monkeypatch, name):
+    """(r5) The masked Helmholtz solve's whole red-black sweeps in LDS tiles (k_helm_rbt_mask, u, v -> TMPU, TMPV and
+    back) against the two in-place half-sweep launches per sweep (NSGPU_MASK_RBT=0): the same arithmetic on the same
+    old values, so every field after 6 full steps is bit-identical, and so are the sweep counts."""
+    P = ALL[name]
+    n = max(P["xspec"][-1][2], P["yspec"][-1][2])
+    out = {}
+    for rbt in ("1", "0"):
+        monkeypatch.setenv("NSGPU_MASK_RBT", rbt)
+        og, gs, m = pair(gpu, name, 1.0 / (16 * n), 200.0, rtol=1e-10)
+        st = [gs.step() for _ in range(6)]
+        out[rbt] = ([x["it_u"] for x in st], [a.copy() for a in gs.fields()])
+        gs.close()
+    assert out["1"][0] == out["0"][0]
+    for a, b in zip(out["1"][1], out["0"][1]):
+        np.testing.assert_array_equal(a, b)
