@@ -1631,13 +1631,14 @@ namespace {
 // y = Cinv (D^T z): one row per wave; every workgroup gathers the m interface differences into LDS first
 __global__ __launch_bounds__(256) void k_cap_gemv(CapArgs a, const double* __restrict__ z) {
     extern __shared__ double gl[];
-    for (int f = threadIdx.x; f < a.m; f += 256) gl[f] = z[a.fi[f]] - z[a.fj[f]];
+    const int M = a.m + a.border;
+    for (int f = threadIdx.x; f < M; f += 256) gl[f] = f < a.m ? z[a.fi[f]] - z[a.fj[f]] : 0.0;
     __syncthreads();
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (row >= a.m) return;
-    const double* cr = a.cinv + (size_t)row * a.m;
+    if (row >= M) return;
+    const double* cr = a.cinv + (size_t)row * M;
     double acc = 0.0;
-    for (int k = lane; k < a.m; k += 64) acc = fma(cr[k], gl[k], acc);
+    for (int k = lane; k < M; k += 64) acc = fma(cr[k], gl[k], acc);
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
     if (lane == 0) a.y[row] = acc;
 }
@@ -1664,12 +1665,24 @@ __global__ __launch_bounds__(256) void k_cap_scatter(CapArgs a, double* __restri
     q[a.co[c]] -= acc;
 }
 
-// x += z on the domain's cells (set: x = z)
-__global__ __launch_bounds__(256) void k_cap_axpy(Geo g, double* __restrict__ x, const double* __restrict__ z, int set) {
+// x += z (+ lambda e1, bordered) on the domain's cells (set: x = ...)
+__global__ __launch_bounds__(256) void k_cap_axpy(Geo g, CapArgs a, double* __restrict__ x, const double* __restrict__ z,
+                                                  int set) {
     const int j = blockIdx.x * 64 + threadIdx.x, li = blockIdx.y * 4 + threadIdx.y;
     if (j >= g.ny || li >= g.nxl) return;
     const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
-    if (g.fc[o] & FC_IN) x[o] = set ? z[o] : x[o] + z[o];
+    if (!(g.fc[o] & FC_IN)) return;
+    double d = z[o];
+    if (a.border) d = fma(a.y[a.m], a.e1[o], d);
+    x[o] = set ? d : x[o] + d;
+}
+
+// set-up: q = val on the domain's cells
+__global__ __launch_bounds__(256) void k_cap_fill(Geo g, double* __restrict__ q, double val) {
+    const int j = blockIdx.x * 64 + threadIdx.x, li = blockIdx.y * 4 + threadIdx.y;
+    if (j >= g.ny || li >= g.nxl) return;
+    const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
+    if (g.fc[o] & FC_IN) q[o] = val;
 }
 
 // r = b - *shift on the domain's cells (the first capacitance solve's right-hand side, from x = 0)
@@ -1687,12 +1700,17 @@ __global__ void k_cap_src(CapArgs a, double* __restrict__ q, int fprev, int f) {
     if (f >= 0) { q[a.fi[f]] = a.w[f]; q[a.fj[f]] = -a.w[f]; }
 }
 
-// set-up: column f of C + 1 1^T / m from z = L_box^+ (w_f d_f) (row-major in cmat)
+// set-up: column f of C + 1 1^T / m from z = L_box^+ (w_f d_f) (row-major in cmat); bordered, its row m = 1
+// (y0^T y = 0), and column f = m from z = L_box^+ 1_domain: -D^T z, 0
 __global__ __launch_bounds__(256) void k_cap_col(CapArgs a, const double* __restrict__ z, int f,
                                                  double* __restrict__ cmat) {
-    const int r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= a.m) return;
-    cmat[(size_t)r * a.m + f] = (r == f ? 1.0 : 0.0) + (z[a.fi[r]] - z[a.fj[r]]) + 1.0 / a.m;
+    const int r = blockIdx.x * 256 + threadIdx.x, M = a.m + a.border;
+    if (r >= M) return;
+    double val;
+    if (r == a.m) val = f < a.m ? 1.0 : 0.0;
+    else if (f == a.m) val = -(z[a.fi[r]] - z[a.fj[r]]);
+    else val = (r == f ? 1.0 : 0.0) + (z[a.fi[r]] - z[a.fj[r]]) + 1.0 / a.m;
+    cmat[(size_t)r * M + f] = val;
 }
 
 // set-up: Gauss-Jordan inversion in place without pivoting (C + 1 1^T / m is symmetric positive definite for
@@ -1702,7 +1720,7 @@ __global__ __launch_bounds__(256) void k_gj_prep(double* __restrict__ A, int m, 
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= m) return;
     const double p = A[(size_t)k * m + k];
-    if (c == 0 && !(p > 0.0 && isfinite(p))) flag[0] = 1.0;
+    if (c == 0 && !(p != 0.0 && isfinite(p))) flag[0] = 1.0;
     t[c] = c == k ? 1.0 / p : A[(size_t)k * m + c] / p;
     u[c] = A[(size_t)c * m + k];
 }
@@ -1720,13 +1738,17 @@ __global__ __launch_bounds__(256) void k_gj_step(double* __restrict__ A, int m, 
 }  // namespace
 
 void launch_cap_gemv(const CapArgs& a, const double* z, hipStream_t st) {
-    hipLaunchKernelGGL(k_cap_gemv, dim3((a.m + 3) / 4), dim3(256), a.m * sizeof(double), st, a, z);
+    const int M = a.m + a.border;
+    hipLaunchKernelGGL(k_cap_gemv, dim3((M + 3) / 4), dim3(256), M * sizeof(double), st, a, z);
 }
 void launch_cap_scatter(const CapArgs& a, double* q, int mode, hipStream_t st) {
     hipLaunchKernelGGL(k_cap_scatter, dim3((a.ncell + 255) / 256), dim3(256), 0, st, a, q, mode);
 }
-void launch_cap_axpy(const Geo& g, double* x, const double* z, int set, hipStream_t st) {
-    hipLaunchKernelGGL(k_cap_axpy, dim3((g.ny + 63) / 64, (g.nxl + 3) / 4), dim3(64, 4), 0, st, g, x, z, set);
+void launch_cap_axpy(const Geo& g, const CapArgs& a, double* x, const double* z, int set, hipStream_t st) {
+    hipLaunchKernelGGL(k_cap_axpy, dim3((g.ny + 63) / 64, (g.nxl + 3) / 4), dim3(64, 4), 0, st, g, a, x, z, set);
+}
+void launch_cap_fill(const Geo& g, double* q, double val, hipStream_t st) {
+    hipLaunchKernelGGL(k_cap_fill, dim3((g.ny + 63) / 64, (g.nxl + 3) / 4), dim3(64, 4), 0, st, g, q, val);
 }
 void launch_cap_rhs(const Geo& g, const double* b, const double* shift, double* r, hipStream_t st) {
     hipLaunchKernelGGL(k_cap_rhs, dim3((g.ny + 63) / 64, (g.nxl + 3) / 4), dim3(64, 4), 0, st, g, b, shift, r);
@@ -1735,7 +1757,7 @@ void launch_cap_src(const CapArgs& a, double* q, int fprev, int f, hipStream_t s
     hipLaunchKernelGGL(k_cap_src, dim3(1), dim3(1), 0, st, a, q, fprev, f);
 }
 void launch_cap_col(const CapArgs& a, const double* z, int f, double* cmat, hipStream_t st) {
-    hipLaunchKernelGGL(k_cap_col, dim3((a.m + 255) / 256), dim3(256), 0, st, a, z, f, cmat);
+    hipLaunchKernelGGL(k_cap_col, dim3((a.m + a.border + 255) / 256), dim3(256), 0, st, a, z, f, cmat);
 }
 void launch_gj_invert(double* A, int m, double* t, double* u, double* flag, hipStream_t st) {
     for (int k = 0; k < m; k++) {

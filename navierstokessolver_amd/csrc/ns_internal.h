@@ -411,8 +411,12 @@ void launch_fps_scan(const FpsArgs& a, bool backward, const FpsRank& R, double* 
 // cell's, w: the face's operator weight), cinv = (C + 1 1^T / m)^-1 (m x m, row-major), y (m); the ncell cells on
 // either side of a face (co: plane offset, cf: up to 4 signed face references +-(f + 1), + on the domain's side,
 // 0: none)
+// (r5) border = 1: the box has the E outflow (mode 0 of its solve and of the domain's in the projected sense): the
+// system is bordered by the unknown constant lambda the domain's right-hand side takes (q + lambda 1_domain) and the
+// row y0^T y = 0 -- cinv is (m + 1) x (m + 1), y[m] = lambda, e1 = L_box^+ 1_domain (a plane)
 struct CapArgs {
-    int m = 0, ncell = 0;
+    int m = 0, ncell = 0, border = 0;
+    const double* e1 = nullptr;
     const int *fi = nullptr, *fj = nullptr, *co = nullptr;
     const int4* cf = nullptr;
     const double* w = nullptr;
@@ -420,10 +424,11 @@ struct CapArgs {
 };
 void launch_cap_gemv(const CapArgs& a, const double* z, hipStream_t st);                // y = cinv D^T z
 void launch_cap_scatter(const CapArgs& a, double* q, int mode, hipStream_t st);         // q -= D_w y / q = 0 outside
-void launch_cap_axpy(const Geo& g, double* x, const double* z, int set, hipStream_t st);  // x += z (set: =) on the domain
+void launch_cap_axpy(const Geo& g, const CapArgs& a, double* x, const double* z, int set, hipStream_t st);  // x += z (+ lambda e1)
+void launch_cap_fill(const Geo& g, double* q, double val, hipStream_t st);   // set-up: q = val on the domain
 void launch_cap_rhs(const Geo& g, const double* b, const double* shift, double* r, hipStream_t st);   // r = b - shift
 void launch_cap_src(const CapArgs& a, double* q, int fprev, int f, hipStream_t st);     // set-up: column f's source
-void launch_cap_col(const CapArgs& a, const double* z, int f, double* cmat, hipStream_t st);
+void launch_cap_col(const CapArgs& a, const double* z, int f, double* cmat, hipStream_t st);   // (f = m: the border)
 void launch_gj_invert(double* A, int m, double* t, double* u, double* flag, hipStream_t st);
 
 }  // namespace nsg

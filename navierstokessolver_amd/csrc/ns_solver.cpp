@@ -1716,7 +1716,9 @@ int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch, int* tn = 
 int fps_scan(ns_solver* s, bool backward);
 int fps_precond(ns_solver* s, const double* q, double* z, double* scratch) {
     const nsg::Geo& g = s->g;
-    if (nsg::launch_fps_dct(false, q, nullptr, scratch, g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st) < 0) {
+    // ((r5) a masked domain whose box has the E outflow: its row pair transformed eliminated, as the channel's)
+    if (nsg::launch_fps_dct(false, q, nullptr, scratch, g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st,
+                            s->fa.outE ? g.nxl / 2 - 1 : -1) < 0) {
         set_err("direct Poisson preconditioner: ny = %d is not a supported power of two", g.ny);
         return NS_EINVAL;
     }
@@ -1788,13 +1790,17 @@ int cap_setup(ns_solver* s, const ns_grid_desc* gd, const double* pw, const doub
         for (int k = 0; k < 4; k++) cf.push_back(k < (int)kv.second.size() ? kv.second[k] : 0);
     }
     const int nc = (int)co.size();
-    // device: cinv (m^2), y, w, t, u, flag (doubles); fi, fj, co, cf (ints)
+    // (an E outflow: the bordered system, M = m + 1, and the plane e1 = L_box^+ 1_domain)
+    const int border = s->fa.outE ? 1 : 0, M = m + border;
+    const size_t ne1 = border ? s->plane : 0;
+    // device: cinv (M^2), y, t, u (M each), w (m), flag, e1 (doubles); fi, fj, co, cf (ints)
     // (nd even and the int4 table at a multiple of 4 ints: 16-byte aligned)
-    const size_t nd = ((size_t)m * m + 4 * (size_t)m + 9) & ~(size_t)1, o4 = (2 * (size_t)m + nc + 3) & ~(size_t)3;
+    const size_t nd = ((size_t)M * M + 4 * (size_t)M + ne1 + 9) & ~(size_t)1, o4 = (2 * (size_t)m + nc + 3) & ~(size_t)3;
     const size_t ni = o4 + 4 * (size_t)nc;
     HIPCHK(hipMalloc(&s->cap_mem, nd * sizeof(double) + ni * sizeof(int)));
     double* dm = (double*)s->cap_mem;
-    double *cinv = dm, *y = cinv + (size_t)m * m, *wd = y + m, *t = wd + m, *u = t + m, *flag = u + m;
+    double *cinv = dm, *y = cinv + (size_t)M * M, *wd = y + M, *t = wd + M, *u = t + M, *flag = u + M;
+    double* e1 = border ? flag + 8 + (size_t)s->hp * g.ld : nullptr;
     int* im = (int*)(dm + nd);
     int *dfi = im, *dfj = dfi + m, *dco = dfj + m;
     int* dcf = im + o4;
@@ -1805,7 +1811,7 @@ int cap_setup(ns_solver* s, const ns_grid_desc* gd, const double* pw, const doub
     HIPCHK(hipMemcpy(dco, co.data(), nc * sizeof(int), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dcf, cf.data(), 4 * (size_t)nc * sizeof(int), hipMemcpyHostToDevice));
     nsg::CapArgs& a = s->cap;
-    a.m = m; a.ncell = nc;
+    a.m = m; a.ncell = nc; a.border = border; a.e1 = e1;
     a.fi = dfi; a.fj = dfj; a.co = dco; a.cf = (const int4*)dcf; a.w = wd;
     a.cinv = cinv; a.y = y;
     // C by columns: the dipole in the (zeroed) plane kv[0], its box solve into kv[6]
@@ -1816,7 +1822,13 @@ int cap_setup(ns_solver* s, const ns_grid_desc* gd, const double* pw, const doub
         nsg::launch_cap_col(a, s->kv[6], f, cinv, s->st);
     }
     nsg::launch_cap_src(a, s->kv[0], m - 1, -1, s->st);
-    nsg::launch_gj_invert(cinv, m, t, u, flag, s->st);
+    if (border) {   // the border column from e1 = L_box^+ 1_domain (kv[0] zeroed again after)
+        nsg::launch_cap_fill(g, s->kv[0], 1.0, s->st);
+        CHK(fps_precond(s, s->kv[0], e1, s->kv[8]));
+        nsg::launch_cap_fill(g, s->kv[0], 0.0, s->st);
+        nsg::launch_cap_col(a, e1, m, cinv, s->st);
+    }
+    nsg::launch_gj_invert(cinv, M, t, u, flag, s->st);
     double fl = 0.0;
     HIPCHK(hipMemcpyAsync(&fl, flag, sizeof(double), hipMemcpyDeviceToHost, s->st));
     HIPCHK(hipStreamSynchronize(s->st));
@@ -1827,7 +1839,9 @@ int cap_setup(ns_solver* s, const ns_grid_desc* gd, const double* pw, const doub
         s->cap_mem = nullptr;
         return 0;
     }
-    if (s->verbose) fprintf(stderr, "nsgpu: masked Poisson by the capacitance matrix: %d interface faces, %d cells\n", m, nc);
+    if (s->verbose)
+        fprintf(stderr, "nsgpu: masked Poisson by the capacitance matrix: %d interface faces, %d cells%s\n", m, nc,
+                border ? ", bordered (E outflow)" : "");
     return 0;
 }
 
@@ -1918,7 +1932,7 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
         nsg::launch_cap_rhs(s->g, ks.b, ks.shift, a.r, s->st);
         for (;;) {
             CHK(cap_solve(s, a.r, s->kv[6]));
-            nsg::launch_cap_axpy(s->g, a.x, s->kv[6], its0 == 0, s->st);
+            nsg::launch_cap_axpy(s->g, s->cap, a.x, s->kv[6], its0 == 0, s->st);
             CHK(init());
             its0++;
             HIPCHK(hipMemcpyAsync(s->scal + S_KRY, d, sizeof(double), hipMemcpyDeviceToDevice, s->st));
@@ -3506,8 +3520,27 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (nsg::fps_log2(gd->ny) < 0) s->fps_fuse = false;
         if (s->fps) s->phi_extrap = 0;   // (no initial guess: no history planes)
         const char* fpc = getenv("NSGPU_FPS_PC");
+        // (r5) or a masked domain whose only NEUMANN edge is its box's whole E column (the backward-facing step):
+        // the box's direct solve with the channel's outflow elimination
+        bool mask_oe = false;
+        if (masked && outflow && gd->nx % 2 == 0 && gd->nx >= 4 && !(foe && std::atoi(foe) == 0) &&
+            !(getenv("NSGPU_CAP_OUTFLOW") && std::atoi(getenv("NSGPU_CAP_OUTFLOW")) == 0)) {
+            int en = -1, nne = 0;
+            for (int e = 0; e < gd->n_edges; e++)
+                if (gd->edges[e].type == NS_BC_NEUMANN) { en = e; nne++; }
+            bool whole = nne == 1;
+            for (int j = 0; j < gd->ny && whole; j++) {
+                const size_t c = (size_t)(gd->nx - 1) * gd->ny + j;
+                whole = gd->cell_id[c] >= 0 && gd->face_edge[4 * c + 1] == en;
+            }
+            long faces = 0;
+            for (size_t c = 0; c < (size_t)gd->nx * gd->ny && whole; c++)
+                for (int f = 0; f < 4; f++) faces += gd->face_edge[4 * c + f] == en;
+            mask_oe = whole && faces == gd->ny;
+        }
         s->fps_pc = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !(fpc && std::atoi(fpc) == 0) &&
-                    masked && !outflow && yuni && p->nranks == 1 && nsg::fps_log2(gd->ny) >= 0;
+                    masked && (!outflow || mask_oe) && yuni && p->nranks == 1 && nsg::fps_log2(gd->ny) >= 0;
+        if (s->fps_pc && outflow) s->fa.outE = 1;
     }
 
     auto fail = [&](int rc) { ns_destroy(s); return rc; };

@@ -23,4 +23,7 @@ UCHAN = dict(vertices=[(0, 0), (0, 1), (1.5, 1), (1.5, 0), (1, 0), (1, 0.5), (0.
                  (INLET, 1.0)])
 # the L-shaped cavity on a stretched grid (walls only: the area-consistent Poisson rhs)
 LSHAPE_S = dict(LSHAPE, xspec=[[0, 0.5, 12, 1.04], [0.5, 1, 12, 0.96]], yspec=[[0, 0.5, 10, 0.95], [0.5, 1, 14, -1]])
-ALL = {"step": STEP, "lshape": LSHAPE, "split": SPLIT, "uchannel": UCHAN, "lshape_s": LSHAPE_S}
+# (r5) the backward-facing step on a power-of-two box (64 x 32): its bounding box has the direct solve with the
+# outflow elimination, so the GPU's Poisson solve is the bordered capacitance solve
+STEP_P2 = dict(STEP, xspec=[[0, 2, 64, -1]], yspec=[[0, 1, 32, -1]])
+ALL = {"step": STEP, "lshape": LSHAPE, "split": SPLIT, "uchannel": UCHAN, "lshape_s": LSHAPE_S, "step_p2": STEP_P2}

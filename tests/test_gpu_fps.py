@@ -280,23 +280,29 @@ def test_masked_poisson_with_box_direct_preconditioner(gpu, monkeypatch):
 
 
 CAP_SHAPES = {
-    # (the L-shaped cavity; a U-shaped one: a notch from the top, 8 edges, two inner corners more)
-    "lshape": ([(0, 0), (0, 1), (1, 1), (1, 0.5), (0.5, 0.5), (0.5, 0)], [(2, 0.0), (2, 1.0)] + [(2, 0.0)] * 4),
+    # (vertices, edge BCs, box length along x) -- the L-shaped cavity; a U-shaped one (a notch from the top, 8
+    # edges, two inner corners more); the backward-facing step (inlet W, outflow on the box's whole E column: the
+    # box's solve with the outflow elimination, the bordered capacitance system)
+    "lshape": ([(0, 0), (0, 1), (1, 1), (1, 0.5), (0.5, 0.5), (0.5, 0)], [(2, 0.0), (2, 1.0)] + [(2, 0.0)] * 4, 1),
     "ushape": ([(0, 0), (0, 1), (0.375, 1), (0.375, 0.5), (0.625, 0.5), (0.625, 1), (1, 1), (1, 0)],
-               [(2, 0.0), (2, 1.0)] + [(2, 0.0)] * 6),
+               [(2, 0.0), (2, 1.0)] + [(2, 0.0)] * 6, 1),
+    "step": ([(0, 0.5), (0, 1), (2, 1), (2, 0), (0.5, 0), (0.5, 0.5)],
+             [(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0), (2, 0.0), (2, 0.0)], 2),
 }
 
 
-@pytest.mark.parametrize("shape,nx,ny", [("lshape", 128, 128), ("lshape", 96, 64), ("ushape", 64, 128)])
+@pytest.mark.parametrize("shape,nx,ny", [("lshape", 128, 128), ("lshape", 96, 64), ("ushape", 64, 128),
+                                         ("step", 128, 64), ("step", 256, 64)])
 def test_masked_poisson_capacitance_solve(gpu, monkeypatch, shape, nx, ny):
     """(r5) A masked domain on one rank whose bounding box has the direct solve: the exact solve by the capacitance
     matrix of its interface with the box (ns_solver.cpp cap_setup / cap_solve: two box solves around a dense m x m
     solve, m the interface faces) -- L-shapes with hx = hy and hx != hy (unequal face weights: the non-symmetric
-    capacitance matrix) and a U-shape.  Residual <= 1e-12 in at most 2 refinements (BiCGStab preconditioned by the
-    box's solve, NSGPU_CAP=0, takes several iterations); phi (modulo its mean) the same as that path's to 1e-9 of
-    its max and the oracle's converged solve to 1e-8."""
-    verts, bc = CAP_SHAPES[shape]
-    og = OGrid(verts, [[0, 1, nx, -1]], [[0, 1, ny, -1]], bc)
+    capacitance matrix), a U-shape, and backward-facing steps (an E outflow: mode 0 in the projected sense, the
+    system bordered by the domain's constant).  Residual <= 1e-12 in at most 2 refinements (BiCGStab preconditioned
+    by the box's solve, NSGPU_CAP=0, takes several iterations); phi (modulo its mean) the same as that path's to
+    1e-9 of its max and the oracle's converged solve to 1e-8."""
+    verts, bc, lx = CAP_SHAPES[shape]
+    og = OGrid(verts, [[0, lx, nx, -1]], [[0, 1, ny, -1]], bc)
     rng = np.random.default_rng(43)
     b = rng.uniform(-1, 1, og.N)
     out = {}

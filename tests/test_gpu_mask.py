@@ -100,7 +100,7 @@ def test_mask_converged_solves(gpu, name):
 
 @pytest.mark.parametrize("rtol", [1e-8, 1e-11])
 @pytest.mark.parametrize("name,steps,re", [("step", 15, 100.0), ("lshape", 12, 400.0), ("split", 10, 100.0),
-                                           ("uchannel", 10, 100.0), ("lshape_s", 10, 200.0)])
+                                           ("uchannel", 10, 100.0), ("lshape_s", 10, 200.0), ("step_p2", 12, 100.0)])
 def test_mask_full_steps_vs_oracle(gpu, name, steps, re, rtol):
     """Full steps on the polygons against the oracle (rtol 1e-13).  At the reference's rtol 1e-8:
     u, v <= 1e-6 (the parity bar) and phi (modulo its mean, relative L2) <= 1e-4 -- phi is the
@@ -185,20 +185,31 @@ def test_mask_step_outflow_line_preconditioner(gpu, monkeypatch):
     outflow on the whole E column, Re 1000) from rest: its only NEUMANN edge is the bounding
     box's E column, so the box hierarchy takes the outflow line closure -- Poisson
     BiCGStab <= 15 iterations per step where the wall closure (NSGPU_OUTFLOW_PC=wall) needs
-    ~35 -- and both runs take the same steps (monitor to 1e-6, the solves' rtol 1e-8)."""
+    ~35 -- and both runs take the same steps (monitor to 1e-6, the solves' rtol 1e-8).  (r5) Both with
+    NSGPU_FPS_PC=0: by default the step's Poisson solve is the bordered capacitance solve around the box's
+    direct solve with the outflow elimination -- one iteration per step, the same steps too."""
     n = 512
     hs = 2.0 / n
     verts = [(0, 0.5), (0, 1), (2, 1), (2, 0), (0.5, 0), (0.5, 0.5)]
     bc = [(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0), (2, 0.0), (2, 0.0)]
     out = {}
-    for pc in ("line", "wall"):
-        monkeypatch.setenv("NSGPU_OUTFLOW_PC", pc)
+    for pc in ("line", "wall", "cap"):
+        if pc == "cap":
+            monkeypatch.delenv("NSGPU_OUTFLOW_PC")
+            monkeypatch.delenv("NSGPU_FPS_PC")
+        else:
+            monkeypatch.setenv("NSGPU_OUTFLOW_PC", pc)
+            monkeypatch.setenv("NSGPU_FPS_PC", "0")
         gs = gpu.GpuSolver(gpu.polygon(verts, np.full(n, hs), np.full(n // 2, hs), bc), hs / 8, 1000.0)
         st = [gs.step() for _ in range(6)]
         gs.close()
         out[pc] = st
     its = {k: [x["it_phi"] for x in v] for k, v in out.items()}
     assert np.mean(its["line"]) <= 15 and np.mean(its["line"]) < 0.6 * np.mean(its["wall"]), its
+    assert its["cap"] == [1] * 6, its
+    for a, b in zip(out["line"], out["cap"]):
+        np.testing.assert_allclose([a["umin"], a["umax"], a["vmin"], a["vmax"]],
+                                   [b["umin"], b["umax"], b["vmin"], b["vmax"]], atol=1e-6)
     for a, b in zip(out["line"], out["wall"]):
         np.testing.assert_allclose([a[k] for k in ("umin", "umax", "vmin", "vmax")],
                                    [b[k] for k in ("umin", "umax", "vmin", "vmax")], atol=1e-6)
