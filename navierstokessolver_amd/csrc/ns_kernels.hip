@@ -3926,7 +3926,7 @@ __global__ __launch_bounds__(256) void k_helm_rb_mask(Geo g, Coef c, double alph
 // uo, vo): a tile of RTM x 64 cells staged in LDS with a 2-cell ring; red relaxed over the tile and its 1-cell ring
 // (the ring's red values the tile's black cells need), then black over the tile, from the same old values a
 // red launch and a black launch would read -- the same arithmetic, half the launches and HBM passes
-constexpr int RTM = 16;
+constexpr int RTM = 8;
 __global__ __launch_bounds__(256) void k_helm_rbt_mask(Geo g, Coef c, double alpha, double omega,
                                                        const double* __restrict__ u, const double* __restrict__ v,
                                                        const double* __restrict__ bu, const double* __restrict__ bv,
@@ -3946,57 +3946,79 @@ __global__ __launch_bounds__(256) void k_helm_rbt_mask(Geo g, Coef c, double alp
             sv[r][cc] = ldf(v, ld, li, j);
         }
     }
+    // the 1-cell ring's codes and the tile's spacing / coefficient tables in LDS too
+    constexpr int RI = RTM + 2, RJ = 66, NB = (RI * RJ + 255) / 256;
+    __shared__ int scode[RI][RJ];
+    __shared__ double trow[3][RI], tcol[3][RJ];   // hx, pw, pe of rows li0 - 1 ..; hy, ps, pn of columns j0 - 1 ..
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+        const int q = tid + 256 * k;
+        if (q < RI * RJ) {
+            const int r = q / RJ, cc = q - r * RJ, li = li0 - 1 + r, j = j0 - 1 + cc;
+            // (one rank: ring cells outside the slab are outside the box -- code 0)
+            const bool ok = j >= 0 && j < g.ny && li >= -1 && li <= g.nxl;
+            const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+            scode[r][cc] = ok ? g.fc[o] : 0;
+        }
+    }
+    if (tid < RI) {
+        const int gi = min(max(g.i0 + li0 - 1 + tid, 0), g.nx - 1);
+        trow[0][tid] = c.hx[gi]; trow[1][tid] = c.pw[gi]; trow[2][tid] = c.pe[gi];
+    } else if (tid >= 64 && tid < 64 + RJ) {
+        const int k = tid - 64, j = min(max(j0 - 1 + k, 0), g.ny - 1);
+        tcol[0][k] = c.hy[j]; tcol[1][k] = c.ps[j]; tcol[2][k] = c.pn[j];
+    }
     __syncthreads();
-    // relax cell (li, j) at LDS (R, C) of colour par if in the domain (one rank: the ring's cells outside the slab
-    // are outside the box -- their codes are 0)
-    auto relax = [&](int li, int j, int R, int C) {
-        if (j < 0 || j >= g.ny || li < -1 || li > g.nxl) return;
-        const TopoMask t(g, li, j);
-        if (!t.cell()) return;
-        const int gi = g.i0 + li;
-        const double hx = c.hx[gi], hy = c.hy[j];
+    // relax the cell at ring coordinates (r1, c1) (LDS su / sv at (r1 + 1, c1 + 1)) if in the domain: k_helm_rb_mask's
+    // arithmetic in its order
+    auto relax = [&](int r1, int c1) {
+        const int code = scode[r1][c1];
+        if (!(code & FC_IN)) return;
+        const double hx = trow[0][r1], hy = tcol[0][c1];
         const double w2[4] = {1.0 / (hx * hx), 1.0 / (hx * hx), 1.0 / (hy * hy), 1.0 / (hy * hy)};
         const int di[4] = {-1, 1, 0, 0}, dj[4] = {0, 0, -1, 1};
-        const double pn[4] = {c.pw[gi], c.pe[gi], c.ps[j], c.pn[j]};
+        const double pn[4] = {trow[1][r1], trow[2][r1], tcol[1][c1], tcol[2][c1]};
         double wk[4], wc = 0.0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             wk[k] = 0.0;
-            if (t.in(di[k], dj[k])) {
+            if (fc_edge(code, k) == FC_INT) {
                 wk[k] = pn[k];
                 wc += pn[k];
-            } else if (!t.edge(k).neu) {
+            } else if (!g.et[fc_edge(code, k)].neu) {
                 wc += 2.0 * w2[k];
             }
         }
         const double dinv = omega / (1.0 + alpha * wc);
-        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
-        auto one = [&](double (*sx)[EJ], const double* __restrict__ bf) {
+        const int R = r1 + 1, C = c1 + 1;
+        auto one = [&](double (*sx)[EJ], double b) {
             const double xc = sx[R][C];
             double s = -wc * xc;
 #pragma unroll
             for (int k = 0; k < 4; k++)
                 if (wk[k] != 0.0) s = fma(wk[k], sx[R + di[k]][C + dj[k]], s);
-            const double r = bf[o] - (xc - alpha * s);
+            const double r = b - (xc - alpha * s);
             sx[R][C] = fma(dinv, r, xc);
         };
-        one(su, bu);
-        one(sv, bv);
+        // (the right-hand sides from global memory: staged too, the tile's 47 KB of LDS left 3 workgroups per CU and
+        // the launch two rounds of them -- 26 us at 1024^2)
+        const ptrdiff_t o = (ptrdiff_t)(li0 - 1 + r1) * ld + (j0 - 1 + c1);
+        one(su, bu[o]);
+        one(sv, bv[o]);
     };
-    // red (colour 0) over rows li0 - 1 .. li0 + RTM, columns j0 - 1 .. j0 + 64: (RTM + 2) x 66 cells, half red
-    constexpr int RI = RTM + 2, RJ = 66;
-    for (int q = tid; q < RI * RJ; q += 256) {
-        const int r = q / RJ, cc = q - r * RJ;
-        const int li = li0 - 1 + r, j = j0 - 1 + cc;
-        if (((g.i0 + li + j) & 1) == 0) relax(li, j, r + 1, cc + 1);
+    // red (colour 0) over rows li0 - 1 .. li0 + RTM, columns j0 - 1 .. j0 + 64: 33 red cells in each ring row, one
+    // per thread
+    for (int q = tid; q < RI * 33; q += 256) {
+        const int r1 = q / 33, k = q - r1 * 33;
+        relax(r1, 2 * k + ((g.i0 + li0 - 1 + r1 + j0 - 1) & 1));
     }
     __syncthreads();
-    // black over the tile: thread (x, y) walks rows y, y + 4, ... of column j0 + x
-    const int j = j0 + threadIdx.x;
-    for (int r = threadIdx.y; r < RTM; r += 4) {
-        const int li = li0 + r;
-        if (li < g.nxl && ((g.i0 + li + j) & 1) == 1) relax(li, j, r + 2, threadIdx.x + 2);
+    // black (colour 1) over the tile: 32 in each row
+    for (int q = tid; q < RTM * 32; q += 256) {
+        const int r = q >> 5, k = q & 31;
+        if (li0 + r < g.nxl) relax(r + 1, 2 * k + ((g.i0 + li0 + r + j0 + 1) & 1) + 1);
     }
+    const int j = j0 + threadIdx.x;
     __syncthreads();
     for (int r = threadIdx.y; r < RTM; r += 4) {
         const int li = li0 + r;

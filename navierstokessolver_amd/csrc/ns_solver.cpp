@@ -939,8 +939,9 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         // (r5) masked domain, one rank: red-black SOR on I - alpha L_V (strongly diagonally dominant: alpha / h^2 ~ 0.06
         // at 1024^2), u and v sweep by sweep, the residual of both checked after a batch -- the first batch what
         // the previous step needed (NSGPU_MASK_HELM=krylov: the BiCGStab of rounds 1-4)
-        CHK(fetch(s));   // ||RHS_u||^2, ||RHS_v||^2
-        const double tol2 = s->rtol * s->rtol, bu = s->hs[S_HBN], bv = s->hs[S_HBN + 1];
+        // (||RHS_u||^2, ||RHS_v||^2 come with the first batch's residuals: no host read before it)
+        const double tol2 = s->rtol * s->rtol;
+        double bu = 0.0, bv = 0.0;
         int sweeps = 0, batch = std::max(1, s->mask_helm_next);
         double r2u = 0.0, r2v = 0.0;
         for (;;) {
@@ -965,6 +966,8 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
             const int nb = nsg::launch_helm_rb_mask(s->g, s->c, alpha, s->omega_v, U, RU, V, RV, 2, s->part, s->st);
             nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_RES, s->st);
             CHK(fetch(s));
+            bu = s->hs[S_HBN];
+            bv = s->hs[S_HBN + 1];
             r2u = s->hs[S_RES];
             r2v = s->hs[S_RES + 1];
             if (!std::isfinite(r2u) || !std::isfinite(r2v)) { set_err("Helmholtz residual is not finite"); return NS_EDIVERGE; }
@@ -1922,7 +1925,8 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
     const int kind = ks.op == 0 ? 0 : (ks.x == s->arr[NS_ARR_U] ? 1 : 2);
     const bool gated = !ks.mg;
     int batch = s->verbose ? 1 : std::max(1, gated ? s->kpred[kind] + 1 : s->kpred[kind] - 1);
-    nsg::launch_bicg_start(s->ksc, tol2 * ks.b2, ks.b2, maxit, s->st);
+    double kb2 = ks.b2;   // (< 0: not read yet -- the capacitance solve reads it with its residual)
+    nsg::launch_bicg_start(s->ksc, tol2 * kb2, kb2, maxit, s->st);
     int its0 = 0;   // (the capacitance solve's refinements before any BiCGStab iteration)
     if (ks.op == 0 && s->cap.m > 0) {
         // (r5) a masked domain with its capacitance matrix: x = L_ext^+ (b - shift) (exact up to round-off; from
@@ -1937,7 +1941,8 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
             its0++;
             HIPCHK(hipMemcpyAsync(s->scal + S_KRY, d, sizeof(double), hipMemcpyDeviceToDevice, s->st));
             CHK(fetch(s));
-            const double r2 = s->hs[S_KRY], b2 = ks.b2;
+            if (kb2 < 0) kb2 = s->hs[S_SHIFT + 1];   // (||b - mean||^2, from K3's reductions)
+            const double r2 = s->hs[S_KRY], b2 = kb2;
             *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
             *its = its0;
             if (s->verbose)
@@ -1947,7 +1952,10 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
                 return NS_EDIVERGE;
             }
             if (r2 <= tol2 * b2 || r2 == 0.0) return 0;
-            if (its0 >= 3) break;
+            if (its0 >= 3) {   // (BiCGStab from this x: its threshold with b2 known now)
+                nsg::launch_bicg_start(s->ksc, tol2 * kb2, kb2, maxit, s->st);
+                break;
+            }
         }
     } else {
         CHK(init());
@@ -1975,7 +1983,7 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
         tn = 0;
         const bool stopped = s->hs[S_KRY] != 0.0, brk = s->hs[S_KRY + 1] != 0.0;
         const int it = (int)s->hs[S_KRY + 2];
-        const double r2 = stopped ? s->hs[S_KRY + 3] : s->hs[S_KRY + 4], b2 = ks.b2;
+        const double r2 = stopped ? s->hs[S_KRY + 3] : s->hs[S_KRY + 4], b2 = kb2;
         *res = b2 > 0 ? std::sqrt(r2 / b2) : std::sqrt(r2);
         if (s->verbose)
             fprintf(stderr, "nsgpu %s (bicgstab): it %d rel. residual %.3e (alpha %.3e omega %.3e%s)\n", ks.name, it,
@@ -2246,9 +2254,11 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
 }
 
 int pois_solve_krylov(ns_solver* s, int* its, double* res, ns_stats* stt) {
-    CHK(fetch(s));   // ||b - mean||^2 for the relative test
+    // ||b - mean||^2 for the relative test (r5: the capacitance solve reads it with its residual, b2 = -1 here)
+    if (!s->cap.m) CHK(fetch(s));
     const KrylovSolve ks{0, 0.0, s->krylov_mg, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI],
-                         s->scal + (s->consist ? S_KSHIFT : S_SHIFT), s->hs[S_SHIFT + 1], "poisson", stt};
+                         s->scal + (s->consist ? S_KSHIFT : S_SHIFT), s->cap.m ? -1.0 : s->hs[S_SHIFT + 1], "poisson",
+                         stt};
     const int rc = bicgstab(s, ks, its, res);
     if (stt) stt->n_checks += *its + 1;
     // (last_cycles / cur_cycles -1: the quadratic guess -- the channel's BiCGStab took 5.1

@@ -20,7 +20,11 @@ def run(name, grid, dt, re, warm=5, steps=10):
 
 
 def _run(name, grid, dt, re, warm, steps):
+    torch.cuda.synchronize()
+    tc = time.perf_counter()
     s = nsa.GpuSolver(grid, dt, re, device=0)
+    torch.cuda.synchronize()
+    tc = time.perf_counter() - tc   # (ns_create: a masked domain's capacitance matrix is built here)
     for _ in range(warm):
         s.step()
     torch.cuda.synchronize()
@@ -31,7 +35,7 @@ def _run(name, grid, dt, re, warm, steps):
     cells = int(grid.mask.sum())
     print(f"{name}: {cells} cells, {el / steps * 1e3:.2f} ms/step, {cells * steps / el / 1e6:.0f} MLUPS, "
           f"poisson its/step {np.mean([x['it_phi'] for x in st]):.1f}, helmholtz its/step "
-          f"{np.mean([x['it_u'] for x in st]):.1f}", flush=True)
+          f"{np.mean([x['it_u'] for x in st]):.1f}, set-up {tc:.2f} s", flush=True)
     s.close()
 
 
