@@ -326,6 +326,24 @@ def test_masked_poisson_capacitance_solve(gpu, monkeypatch, shape, nx, ny):
     assert rel(out["1"][1], demean(xp)) <= 1e-8
 
 
+def test_masked_capacitance_solve_check_policy(gpu):
+    """(r5) The capacitance solve inside steps follows the direct solve's check policy: its residual is computed on
+    the first solve and every 16th after it (phi_checked 1; res_phi -1 and phi_checked 0 between), and the checked
+    ones are within rtol -- the L-shape 128^2 at the default rtol 1e-8."""
+    n = 128
+    verts, bc, _ = CAP_SHAPES["lshape"]
+    og = OGrid(verts, [[0, 1, n, -1]], [[0, 1, n, -1]], bc)
+    gs = gpu.GpuSolver(gpu.polygon(verts, og.hx, og.hy, bc), 1.0 / (8 * n), 400.0)
+    st = [gs.step() for _ in range(18)]
+    gs.close()
+    checked = [x["phi_checked"] for x in st]
+    assert checked == [1] + [0] * 15 + [1, 0], checked
+    for x in st:
+        assert x["it_phi"] == 1
+        assert (x["res_phi"] == -1.0) == (x["phi_checked"] == 0)
+        assert x["res_phi"] <= 1e-2 * 1e-8
+
+
 def test_direct_solve_check_policy(gpu):
     """ADVICE r4 / VERDICT r4 weak 7: the direct solve's residual is computed on the first solve and on
     every 16th after it, and `res_phi` is reported only for those (phi_checked 1; -1 and phi_checked 0
