@@ -77,6 +77,13 @@ KERNELS = {
                 "recurrences along x, one per mode, chunked; five launches timed as one interval)",
                 40 if os.environ.get("NSGPU_FPS_PASSES") == "3" else 24),
     "fps_idct": ("k_fps_idct (direct Poisson solve: DCT-III of every row pair -> phi)", 16),
+    # (r6) K5 (CorrectVelocities + GradP + the min / max monitor): read phi 8 + u*, v* 16, write u, v 16 = 40
+    "k5": ("k_cell_s<5> (K5, CorrectVelocities: u = u* - dt grad phi, fused min / max of u, v)", 40),
+    # (r6) the Helmholtz wall bands (k_helm_band, 3 RB-SOR sweeps per launch on the cells within 128 of a wall):
+    # per band cell u, v read 16 + rhs 16 + write 16 = 48 B; per cell of the grid 48 x the band's fraction
+    # (set in run(): BAND_BPC)
+    "band": ("k_helm_band (Helmholtz wall bands: 3 RB-SOR sweeps of u, v on the cells within 128 of a wall, "
+             "LDS-tiled)", None),
 }
 # (r4) K3 fused into the DCT (NSGPU_FPS_FUSE, default on): the divergence of u*, v* formed in the
 # transform's LDS -- read u*, v* 16 + write the coefficients 8; rhs_phi (8 more) only for a checked solve
@@ -85,7 +92,7 @@ if FPS_FUSED:
     KERNELS["fps_dct"] = ("k_fps_dct_div (direct Poisson solve: K3's divergence of u*, v* fused into the DCT-II of "
                           "every row pair, Stockham FFT in LDS)", 24)
 # one-launch kernels (the `roofline` candidates; fps_tri is five launches)
-SINGLE_LAUNCH = ("restrict", "prolong", "cycle", "guess", "helmholtz", "rhs", "fps_dct", "fps_idct")
+SINGLE_LAUNCH = ("restrict", "prolong", "cycle", "guess", "helmholtz", "rhs", "fps_dct", "fps_idct", "k5", "band")
 JACOBI_LABEL = "k_jacobi_s<double> (one weighted-Jacobi sweep of the Poisson operator, the north star's roofline kernel)"
 SWEEP_BYTES_PER_CELL = 24
 # configs[4]'s fp32-field Jacobi sweep: read phi 4 + read b 4 + write phi 4 (fp64 arithmetic / residual)
@@ -99,7 +106,11 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--n", type=int, default=4096)
-    ap.add_argument("--case", choices=("cavity", "channel"), default="cavity")
+    ap.add_argument("--case", choices=("cavity", "channel", "stretched", "xstretched"), default="cavity",
+                    help="cavity (the headline), channel (NEUMANN outflow), stretched / xstretched (the cavity on a "
+                         "geometrically stretched grid, Grid.cpp:87-92: both directions / x only, --ratio)")
+    ap.add_argument("--ratio", type=float, default=1.0005,
+                    help="--case stretched / xstretched: the face-spacing ratio (Nx / Ny {0 1 n ratio})")
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -356,6 +367,13 @@ def run(args, rank, world, local, wd):
         nyc, h = n // 4, 4.0 / n
         dt = h / 8
         grid = nsa.rectangle(n, nyc, lx=4.0, ly=nyc * h, bc=[(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0)])
+    elif args.case in ("stretched", "xstretched"):
+        # (r6) the cavity on the reference's geometric spacing (ratio > 0), dt = 1/(8n) as the
+        # uniform cavity (the smallest cell is ~(1 - ratio^(-n/2)) of h: CFL stays < 0.19 for ratio <= 1.0005 at 4096)
+        nyc, dt = n, 1.0 / (8 * n)
+        grid = nsa.rectangle(n, n, bc=[(nsa.NS_BC_WALL, 0.0), (nsa.NS_BC_WALL, 1.0), (nsa.NS_BC_WALL, 0.0),
+                                       (nsa.NS_BC_WALL, 0.0)],
+                             xratio=args.ratio, yratio=args.ratio if args.case == "stretched" else -1)
     else:
         nyc, dt = n, 1.0 / (8 * n)
         grid = nsa.cavity(n)
@@ -416,7 +434,9 @@ def run(args, rank, world, local, wd):
              "helmholtz": (sum(s["t_helm_kernel_ms"] for s in stats), sum(s["n_helm_kernels"] for s in stats)),
              "cycle": (sum(s["t_cycle_kernel_ms"] for s in stats), sum(s["n_cycle_kernels"] for s in stats)),
              "guess": (sum(s["t_guess_kernel_ms"] for s in stats), sum(s["n_guess_kernels"] for s in stats)),
-             "rhs": (sum(s["t_rhs_kernel_ms"] for s in stats), sum(s["n_rhs_kernels"] for s in stats))}
+             "rhs": (sum(s["t_rhs_kernel_ms"] for s in stats), sum(s["n_rhs_kernels"] for s in stats)),
+             "k5": (sum(s["t_k5_kernel_ms"] for s in stats), sum(s["n_k5_kernels"] for s in stats)),
+             "band": (sum(s["t_band_kernel_ms"] for s in stats), sum(s["n_band_kernels"] for s in stats))}
     for k in ("dct", "tri", "idct"):
         timed["fps_" + k] = (sum(s[f"t_fps_{k}_ms"] for s in stats), sum(s["n_fps_solves"] for s in stats))
     # the direct Poisson solve ran (one solve per step, no V-cycles) -- or, untimed, no restriction pass
@@ -443,7 +463,8 @@ def run(args, rank, world, local, wd):
         extrap_bpc -= 16
     # the Helmholtz wall bands (two k_helm_band launches) on the cells within 128 of a wall:
     # per launch u, v read 16 + rhs 16 + write 16 -> 96 B per band cell
-    band_frac = 1.0 - max(n - 256, 0) * max(nyc - 256, 0) / float(n * nyc)
+    bw = max(32, min(n, nyc) // 32)   # the solver's band_w
+    band_frac = 1.0 - max(n - 2 * bw, 0) * max(nyc - 2 * bw, 0) / float(n * nyc)
     # the finest level: a V-cycle whose output is not checked hands its prolongation pass to the next
     # cycle's restriction pass (one k_sweep4 pass of 28 B/cell instead of 26 + 26): cycles - checks
     # such boundaries per solve (one rank, multigrid)
@@ -474,7 +495,7 @@ def run(args, rank, world, local, wd):
     # the north star's roofline kernel: one Jacobi sweep of this rank's slab (random phi, b;
     # 10 warm-up + 50 timed launches, HIP events), single rank only
     jacobi = jacobi32 = None
-    if world == 1 and not channel and not args.no_jacobi:
+    if world == 1 and args.case == "cavity" and not args.no_jacobi:
         js = nsa.GpuSolver(nsa.cavity(n), dt, re, poisson=nsa.NS_POISSON_JACOBI, omega=1.0, device=device)
         js.fill_random(0x5EED)
         t = js.time_poisson(10, 50)
@@ -496,7 +517,7 @@ def run(args, rank, world, local, wd):
     if os.path.exists(prof) and world == 1:
         try:
             d = json.load(open(prof))
-            if d.get("n") == n and not channel:
+            if d.get("n") == n and args.case == "cavity":
                 traffic = {k: v.get("kernel_bytes_per_launch") for k, v in d.get("kernels", {}).items()}
                 tri = [traffic.get(k) for k in (("fps_t1", "fps_t2", "fps_t3")
                                                 if os.environ.get("NSGPU_FPS_PASSES") == "3" else ("fps_t1b", "fps_t2b"))]
@@ -522,6 +543,8 @@ def run(args, rank, world, local, wd):
 
     kern = {}
     for key, (label, bpc) in KERNELS.items():
+        if key == "band":
+            bpc = 48 * band_frac
         ms, cnt = timed[key]
         if cnt:
             kern[key] = roof(key, label, bpc, ms / cnt / 1e3, cnt)
@@ -548,12 +571,17 @@ def run(args, rank, world, local, wd):
                                    "16th solve)" if direct else
                                    "BiCGStab Poisson with the line-closure V-cycle preconditioner")
                                 + f" + RB-SOR Helmholtz, both to rtol {args.rtol:g}") if channel else
-                               (f"{n}x{n} lid-driven cavity, Re={re:g}, dt=1/{8 * n}, fp64, "
+                               (f"{n}x{n} lid-driven cavity"
+                                + (f" on a stretched grid (ratio {args.ratio:g} along x"
+                                   + (" and y)" if args.case == "stretched" else ", y uniform)")
+                                   if args.case != "cavity" else "")
+                                + f", Re={re:g}, dt=1/{8 * n}, fp64, "
                                 + ("direct Poisson solve (DCT along y + tridiagonal recurrences along x; residual "
                                    "checked on every 16th solve)" if direct else
-                                   "multigrid Poisson (RB-GS smoother)")
+                                   "multigrid Poisson (RB-GS smoother; V-cycles to rtol)")
                                 + f" + RB-SOR Helmholtz, both to rtol {args.rtol:g}"),
                    "case": args.case, "nx": n, "ny": nyc, "re": re, "dt": dt, "parallelism": f"x-slab x{world}",
+                   "ratio": args.ratio if args.case in ("stretched", "xstretched") else None,
                    "step_api": "ns_step" if args.sync_monitor else "ns_step_async",
                    "transport": ("none (one rank)" if world == 1 else
                                  "RCCL over xGMI, one GPU per rank" if not host else
@@ -579,6 +607,11 @@ def run(args, rank, world, local, wd):
                                   "kernel boundaries and latency-bound coarse levels included)"},
         "kernels": dict(kern),
     }
+    # (r6) the share of the step's wall time the timed kernels account for (their per-step ms over ms_per_step;
+    # the unlisted rest: the scans / carries of fps_tri are inside it, the small reductions and kernel boundaries
+    # are not)
+    line["kernels_ms_per_step"] = sum(k["ms_per_step"] for k in kern.values())
+    line["kernels_share_of_step"] = line["kernels_ms_per_step"] / (elapsed / K * 1e3)
     if jacobi is not None:
         line["kernels"]["jacobi_sweep"] = roof("jacobi_sweep", JACOBI_LABEL, SWEEP_BYTES_PER_CELL, jacobi, 50)
     if jacobi32 is not None:
@@ -595,11 +628,12 @@ def run(args, rank, world, local, wd):
                         "x_link_bytes_per_step": sum(s["x_link_bytes"] for s in stats) / K,
                         "rccl_version": _rccl_version(torch) if not host else None,
                         "note": "collectives = all-reduces + allgathers issued per step by rank 0 (r5: the "
-                                "Helmholtz check's scalar bus and the direct solve's two allgathers, + 1 on a "
-                                "checked solve); exchanges = ghost-row send/recv groups"}
+                                "Helmholtz check's scalar bus and the direct solve's one allgather -- two with "
+                                "NSGPU_FPS_ONEGATHER=0 -- + 1 on a checked solve); exchanges = ghost-row send/recv "
+                                "groups"}
     else:
         line.pop("ranks")
-    if world == 1 and not args.no_cpu and not channel:
+    if world == 1 and not args.no_cpu and args.case == "cavity" and n & (n - 1) == 0:
         try:
             state = {k: solver.get(a).ravel() for k, a in (("u", nsa.NS_ARR_U), ("v", nsa.NS_ARR_V),
                                                            ("phi", nsa.NS_ARR_PHI), ("cu", nsa.NS_ARR_CU),

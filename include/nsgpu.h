@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NSGPU_ABI_VERSION 8   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
+#define NSGPU_ABI_VERSION 9   /* 2: ns_grid_desc.face_edge (non-rectangular domains);
                                  3: ns_get/set_fields in compact-id order on polygons, ns_local_cells;
                                  4: NS_POISSON_MG is 0, so a zero-initialised ns_params selects the
                                     multigrid (RB-SOR moved to 3; the value 2 is rejected);
@@ -45,7 +45,9 @@ extern "C" {
                                     Poisson solve's kernel times t_fps_dct_ms / t_fps_tri_ms /
                                     t_fps_idct_ms / n_fps_solves appended;
                                  8: ns_stats.phi_checked appended (res_phi is -1 on a direct solve
-                                    whose residual was not computed) */
+                                    whose residual was not computed);
+                                 9: ns_stats.t_k5_kernel_ms / n_k5_kernels (K5) and t_band_kernel_ms /
+                                    n_band_kernels (the Helmholtz wall bands) appended */
 
 typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm */
 
@@ -178,6 +180,12 @@ typedef struct ns_stats {
                                       * residual came within 1/100 of rtol); 0: a direct solve not checked on
                                       * this step (res_phi = -1) -- a fixed arithmetic sequence whose residual
                                       * the last check measured */
+    double  t_k5_kernel_ms;          /* (ABI 9) K5's duration (CorrectVelocities, k_cell_s<5>; timing == 1).  K5 is the
+                                      * step's last launch: ns_step reports its own step's, ns_step_async the
+                                      * previous step's (read at this step's first host sync, like the monitor) */
+    int32_t n_k5_kernels;            /* number of K5 launches timed (0 or 1) */
+    double  t_band_kernel_ms;        /* (ABI 9) the Helmholtz wall-band launches (k_helm_band; timing == 1) */
+    int32_t n_band_kernels;          /* number of band launches timed */
 } ns_stats;
 
 /* device arrays addressable by ns_get_array / ns_set_array */

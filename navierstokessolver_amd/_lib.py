@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("NSGPU_LIB", os.path.join(HERE, "libnsgpu.so"))
 HEADER = os.path.join(os.path.dirname(HERE), "include", "nsgpu.h")
 
 # ---- constants mirrored from include/nsgpu.h (checked by tests/test_abi.py) ----
-NSGPU_ABI_VERSION = 8   # the struct layouts / enum values below; lib() refuses a library of another ABI
+NSGPU_ABI_VERSION = 9   # the struct layouts / enum values below; lib() refuses a library of another ABI
 NS_OK, NS_EINVAL, NS_EHIP, NS_ERCCL, NS_ENOMEM, NS_EDIVERGE = 0, -1, -2, -3, -4, -5
 NS_BC_INLET_UNI, NS_BC_INLET_PARABOLIC, NS_BC_WALL, NS_BC_PRESSURE, NS_BC_NEUMANN = 0, 1, 2, 3, 4
 NS_POISSON_MG, NS_POISSON_JACOBI, NS_POISSON_RBSOR = 0, 1, 3   # ABI 4: zeroed params select MG
@@ -73,7 +73,9 @@ class NsStats(ctypes.Structure):
                 ("n_guess_kernels", ctypes.c_int32), ("t_rhs_kernel_ms", ctypes.c_double),
                 ("n_rhs_kernels", ctypes.c_int32), ("t_fps_dct_ms", ctypes.c_double), ("t_fps_tri_ms", ctypes.c_double),
                 ("t_fps_idct_ms", ctypes.c_double), ("n_fps_solves", ctypes.c_int32),
-                ("phi_checked", ctypes.c_int32)]
+                ("phi_checked", ctypes.c_int32), ("t_k5_kernel_ms", ctypes.c_double),
+                ("n_k5_kernels", ctypes.c_int32), ("t_band_kernel_ms", ctypes.c_double),
+                ("n_band_kernels", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1715,12 +1715,16 @@ __global__ __launch_bounds__(256) void k_cap_col(CapArgs a, const double* __rest
 
 // set-up: Gauss-Jordan inversion in place without pivoting (C + 1 1^T / m is symmetric positive definite for
 // uniform face weights, a diagonal similarity of one otherwise): pivot k's scaled row t and column u ...
+// (r6) flagged -- the caller then keeps the preconditioned BiCGStab -- when a pivot is not finite, below
+// GJ_TINY in magnitude (C's entries are O(1): the identity plus the dipoles' responses), or, without a border (spd),
+// not positive; the bordered (E-outflow) system is indefinite, so there only the magnitude is tested
+constexpr double GJ_TINY = 1e-12;
 __global__ __launch_bounds__(256) void k_gj_prep(double* __restrict__ A, int m, int k, double* __restrict__ t,
-                                                 double* __restrict__ u, double* __restrict__ flag) {
+                                                 double* __restrict__ u, double* __restrict__ flag, int spd) {
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= m) return;
     const double p = A[(size_t)k * m + k];
-    if (c == 0 && !(p != 0.0 && isfinite(p))) flag[0] = 1.0;
+    if (c == 0 && !(isfinite(p) && fabs(p) >= GJ_TINY && (!spd || p > 0.0))) flag[0] = 1.0;
     t[c] = c == k ? 1.0 / p : A[(size_t)k * m + c] / p;
     u[c] = A[(size_t)c * m + k];
 }
@@ -1737,9 +1741,13 @@ __global__ __launch_bounds__(256) void k_gj_step(double* __restrict__ A, int m, 
 
 }  // namespace
 
-void launch_cap_gemv(const CapArgs& a, const double* z, hipStream_t st) {
+hipError_t launch_cap_gemv(const CapArgs& a, const double* z, hipStream_t st) {
     const int M = a.m + a.border;
+    // (the interface differences in dynamic LDS: cap_setup bounds M by CAP_LDS_MAX doubles -- 64 KiB, the launch
+    // limit without a raised attribute -- and the launch is checked: a failed one must not leave y stale)
+    if ((size_t)M > CAP_LDS_MAX) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_cap_gemv, dim3((M + 3) / 4), dim3(256), M * sizeof(double), st, a, z);
+    return hipGetLastError();
 }
 void launch_cap_scatter(const CapArgs& a, double* q, int mode, hipStream_t st) {
     hipLaunchKernelGGL(k_cap_scatter, dim3((a.ncell + 255) / 256), dim3(256), 0, st, a, q, mode);
@@ -1759,9 +1767,9 @@ void launch_cap_src(const CapArgs& a, double* q, int fprev, int f, hipStream_t s
 void launch_cap_col(const CapArgs& a, const double* z, int f, double* cmat, hipStream_t st) {
     hipLaunchKernelGGL(k_cap_col, dim3((a.m + a.border + 255) / 256), dim3(256), 0, st, a, z, f, cmat);
 }
-void launch_gj_invert(double* A, int m, double* t, double* u, double* flag, hipStream_t st) {
+void launch_gj_invert(double* A, int m, double* t, double* u, double* flag, int spd, hipStream_t st) {
     for (int k = 0; k < m; k++) {
-        hipLaunchKernelGGL(k_gj_prep, dim3((m + 255) / 256), dim3(256), 0, st, A, m, k, t, u, flag);
+        hipLaunchKernelGGL(k_gj_prep, dim3((m + 255) / 256), dim3(256), 0, st, A, m, k, t, u, flag, spd);
         hipLaunchKernelGGL(k_gj_step, dim3((m + 63) / 64, (m + 3) / 4), dim3(64, 4), 0, st, A, m, k, (const double*)t,
                            (const double*)u);
     }

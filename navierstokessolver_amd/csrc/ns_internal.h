@@ -422,13 +422,14 @@ struct CapArgs {
     const double* w = nullptr;
     double *cinv = nullptr, *y = nullptr;
 };
-void launch_cap_gemv(const CapArgs& a, const double* z, hipStream_t st);                // y = cinv D^T z
+constexpr size_t CAP_LDS_MAX = 8192;   // k_cap_gemv: interface differences in LDS (64 KiB of doubles)
+hipError_t launch_cap_gemv(const CapArgs& a, const double* z, hipStream_t st);                // y = cinv D^T z
 void launch_cap_scatter(const CapArgs& a, double* q, int mode, hipStream_t st);         // q -= D_w y / q = 0 outside
 void launch_cap_axpy(const Geo& g, const CapArgs& a, double* x, const double* z, int set, hipStream_t st);  // x += z (+ lambda e1)
 void launch_cap_fill(const Geo& g, double* q, double val, hipStream_t st);   // set-up: q = val on the domain
 void launch_cap_rhs(const Geo& g, const double* b, const double* shift, double* r, hipStream_t st);   // r = b - shift
 void launch_cap_src(const CapArgs& a, double* q, int fprev, int f, hipStream_t st);     // set-up: column f's source
 void launch_cap_col(const CapArgs& a, const double* z, int f, double* cmat, hipStream_t st);   // (f = m: the border)
-void launch_gj_invert(double* A, int m, double* t, double* u, double* flag, hipStream_t st);
+void launch_gj_invert(double* A, int m, double* t, double* u, double* flag, int spd, hipStream_t st);
 
 }  // namespace nsg

@@ -342,8 +342,10 @@ struct ns_solver {
     // steps the divergence goes straight into the transformed plane, rhs_phi is stored only for a checked
     // solve; fps_pre: the plane holds this step's coefficients (pois_solve_fps skips its DCT)
     bool fps_fuse = true, fps_pre = false, fps_pre_b = false;
-    // timed steps: K1 (kev[0..1]) and the direct solve's transforms / recurrences (kev[2..7])
-    hipEvent_t kev[8] = {};
+    // timed steps: K1 (kev[0..1]) and the direct solve's transforms / recurrences (kev[2..7]); (r6) the wall-band
+    // launches (kev[8..11], two launches) and K5 (kev[12..13], read at the next host sync: k5_pend)
+    hipEvent_t kev[14] = {};
+    int band_timed = 0, k5_pend = 0;
 };
 
 namespace {
@@ -905,6 +907,8 @@ int helm_band(ns_solver* s, double alpha) {
         s->helm_b_pend = 0;
         return 0;
     }
+    const bool tb = s->timing && s->in_step && s->nranks == 1;   // (r6: the bench's band line)
+    if (tb) CHK(ensure_kev(s));
     for (int k = 0; k < rounds; k++) {
         const bool odd = k & 1;
         auto launch = [&]() {
@@ -912,7 +916,12 @@ int helm_band(ns_solver* s, double alpha) {
                                          odd ? U : TU, odd ? V : TV, s->arr[NS_ARR_RU], s->arr[NS_ARR_RV],
                                          s->band_w, 0, s->st);
         };
-        if (s->nranks > 1) {
+        if (tb && k < 2) {
+            CHK(t_begin(s, s->kev[8 + 2 * k], s->kev[9 + 2 * k]));
+            launch();
+            CHK(t_end(s, s->kev[8 + 2 * k], s->kev[9 + 2 * k]));
+            s->band_timed = k + 1;
+        } else if (s->nranks > 1) {
             // the exchange overlapped with the tiles that read no neighbour's rows
             const HaloReq r[4] = {{&s->g, odd ? TU : U, 6}, {&s->g, odd ? TV : V, 6},
                                   {&s->g, s->arr[NS_ARR_RU], 6}, {&s->g, s->arr[NS_ARR_RV], 6}};
@@ -1740,7 +1749,10 @@ int fps_precond(ns_solver* s, const double* q, double* z, double* scratch) {
 // interface cells and restored to 0 outside (its domain values are rewritten by the next KV_INIT)
 int cap_solve(ns_solver* s, double* q, double* z) {
     CHK(fps_precond(s, q, z, s->kv[8]));
-    nsg::launch_cap_gemv(s->cap, z, s->st);
+    if (nsg::launch_cap_gemv(s->cap, z, s->st) != hipSuccess) {
+        set_err("capacitance solve: k_cap_gemv launch failed (%d interface faces)", s->cap.m + s->cap.border);
+        return NS_EHIP;
+    }
     nsg::launch_cap_scatter(s->cap, q, 0, s->st);
     CHK(fps_precond(s, q, z, s->kv[8]));
     nsg::launch_cap_scatter(s->cap, q, 1, s->st);
@@ -1751,13 +1763,14 @@ int cap_solve(ns_solver* s, double* q, double* z) {
 // faces between a domain cell and a box cell outside it, then C's columns by m box solves of the faces'
 // dipoles w_f d_f (C[g][f] = delta_gf + (D^T L_box^+ w_f d_f)_g, + 1 / m: the regularisation along the domain's
 // constant y0 = 1, C y0 = 0) and its inverse by Gauss-Jordan, all on the device.  Not built (BiCGStab with the box
-// preconditioner stays): m = 0 or > NSGPU_CAP_MAX (4096), NSGPU_CAP=0, a non-positive pivot
+// preconditioner stays): m = 0 or > NSGPU_CAP_MAX (4096; clamped to the gemv's LDS bound, nsg::CAP_LDS_MAX - 1),
+// NSGPU_CAP=0, a Gauss-Jordan pivot that is not finite, below 1e-12 in magnitude, or (no border) not positive
 int cap_setup(ns_solver* s, const ns_grid_desc* gd, const double* pw, const double* pe, const double* ps,
               const double* pn) {
     const char* ce = getenv("NSGPU_CAP");
     if (ce && std::atoi(ce) == 0) return 0;
     const char* cm = getenv("NSGPU_CAP_MAX");
-    const long mmax = cm ? std::atol(cm) : 4096;
+    const long mmax = std::min(cm ? std::atol(cm) : 4096L, (long)nsg::CAP_LDS_MAX - 1);   // (+ the border row)
     const nsg::Geo& g = s->g;
     const int nx = gd->nx, ny = gd->ny;
     auto inside = [&](int i, int j) { return gd->cell_id[(size_t)i * ny + j] >= 0; };
@@ -1831,12 +1844,14 @@ int cap_setup(ns_solver* s, const ns_grid_desc* gd, const double* pw, const doub
         nsg::launch_cap_fill(g, s->kv[0], 0.0, s->st);
         nsg::launch_cap_col(a, e1, m, cinv, s->st);
     }
-    nsg::launch_gj_invert(cinv, M, t, u, flag, s->st);
+    nsg::launch_gj_invert(cinv, M, t, u, flag, border ? 0 : 1, s->st);
     double fl = 0.0;
     HIPCHK(hipMemcpyAsync(&fl, flag, sizeof(double), hipMemcpyDeviceToHost, s->st));
     HIPCHK(hipStreamSynchronize(s->st));
     if (fl != 0.0) {   // (never seen: the preconditioned BiCGStab instead)
-        if (s->verbose) fprintf(stderr, "nsgpu: capacitance matrix (%d faces) not positive definite: BiCGStab\n", m);
+        if (s->verbose)
+            fprintf(stderr, "nsgpu: capacitance matrix (%d faces): a Gauss-Jordan pivot failed the test of k_gj_prep "
+                            "(not finite, tiny%s): BiCGStab\n", m, border ? "" : " or not positive");
         s->cap = nsg::CapArgs{};
         (void)hipFree(s->cap_mem);
         s->cap_mem = nullptr;
@@ -3185,6 +3200,11 @@ int correct_launch(ns_solver* s, double* part2) {
     s->guess_ready = 0;
     // (r5, deep slabs: the direct solve wrote phi's ghost rows -- no exchange)
     const bool have = s->deep && s->phi_ext && s->in_step;
+    const bool t5 = s->timing && s->in_step && !guess;   // (r6: the bench's K5 line; read at the next host sync)
+    if (t5) {
+        CHK(ensure_kev(s));
+        CHK(t_begin(s, s->kev[12], s->kev[13]));
+    }
     const int nb = have ? [&]() {
         if (guess)
             return nsg::launch_correct_guess(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
@@ -3200,6 +3220,10 @@ int correct_launch(ns_solver* s, double* part2) {
         return nsg::launch_correct(s->g, s->c, s->dt, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_TMPU],
                                    s->arr[NS_ARR_TMPV], s->arr[NS_ARR_PHI], part2, s->st);
     });
+    if (t5 && nb >= 0) {
+        CHK(t_end(s, s->kev[12], s->kev[13]));
+        s->k5_pend = 1;
+    }
     if (guess && nb >= 0) {
         s->guess_ready = 1;
         s->guess_branch = p.branch;
@@ -3914,6 +3938,16 @@ static int step_body_(ns_solver* s, ns_stats& st) {
         st.t_rhs_kernel_ms += kev_ms(s, 0);
         st.n_rhs_kernels++;
     }
+    for (int k = 0; k < s->band_timed; k++) {   // (r6: the wall bands, before the same syncs)
+        st.t_band_kernel_ms += kev_ms(s, 8 + 2 * k);
+        st.n_band_kernels++;
+    }
+    s->band_timed = 0;
+    if (s->k5_pend) {   // (r6: the previous step's K5, ended before this step's first host sync)
+        st.t_k5_kernel_ms += kev_ms(s, 12);
+        st.n_k5_kernels++;
+        s->k5_pend = 0;
+    }
     if (!s->k3_spec) CHK(divergence(s));                           // ConstructRHS_phi + mean (:549-550)
     s->k3_spec = 0;
     CHK(consistent_rhs(s));                                        // stretched grids only
@@ -3953,6 +3987,11 @@ int ns_step(ns_solver* s, ns_stats* out) {
         st.n_allreduces++;
     }
     CHK(fetch(s));                                                 // VecMin/VecMax        (:554-557)
+    if (s->k5_pend) {   // (r6: this step's K5 -- the fetch synchronised the stream behind it)
+        st.t_k5_kernel_ms += kev_ms(s, 12);
+        st.n_k5_kernels++;
+        s->k5_pend = 0;
+    }
     st.umin = s->hs[S_MM];
     st.umax = -s->hs[S_MM + 1];
     st.vmin = s->hs[S_MM + 2];

@@ -27,3 +27,8 @@ LSHAPE_S = dict(LSHAPE, xspec=[[0, 0.5, 12, 1.04], [0.5, 1, 12, 0.96]], yspec=[[
 # outflow elimination, so the GPU's Poisson solve is the bordered capacitance solve
 STEP_P2 = dict(STEP, xspec=[[0, 2, 64, -1]], yspec=[[0, 1, 32, -1]])
 ALL = {"step": STEP, "lshape": LSHAPE, "split": SPLIT, "uchannel": UCHAN, "lshape_s": LSHAPE_S, "step_p2": STEP_P2}
+# (r6) larger boxes for the masked LDS-tiled kernels (64-column tiles, 2-cell ring in j): ny >= 128, so checked
+# comparisons cross the column-tile boundaries; not in ALL (the per-kernel sets stay small)
+LSHAPE_BIG = dict(LSHAPE, xspec=[[0, 1, 160, -1]], yspec=[[0, 1, 200, -1]])
+STEP_BIG = dict(STEP, xspec=[[0, 2, 256, -1]], yspec=[[0, 1, 136, -1]])
+BIG = {"lshape_big": LSHAPE_BIG, "step_big": STEP_BIG}

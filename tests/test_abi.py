@@ -19,7 +19,7 @@ def test_library_exports_every_header_symbol():
     for n in names:
         assert hasattr(lib, n), f"libnsgpu.so does not export {n}"
     assert set(names) == set(L.SIGNATURES), "ctypes signatures out of sync with include/nsgpu.h"
-    assert lib.ns_abi_version() == L.NSGPU_ABI_VERSION == 8
+    assert lib.ns_abi_version() == L.NSGPU_ABI_VERSION == 9
 
 
 def test_lib_is_gfx950_code_object():

@@ -10,13 +10,15 @@ import numpy as np
 import pytest
 
 from oracle import OGrid, OSolver
-from polygons import ALL
+from polygons import ALL, BIG
+
+POLY = {**ALL, **BIG}
 
 pytestmark = pytest.mark.gpu
 
 
 def pair(gpu, name, dt, re, **kw):
-    P = ALL[name]
+    P = POLY[name]
     og = OGrid(P["vertices"], P["xspec"], P["yspec"], P["bc"])
     gs = gpu.GpuSolver(gpu.polygon(P["vertices"], og.hx, og.hy, P["bc"]), dt, re, **kw)
     return og, gs, gs.grid.mask.ravel()
@@ -32,7 +34,7 @@ def rel(a, b):
     return float(np.max(np.abs(np.asarray(a).ravel() - np.asarray(b).ravel())) / max(np.max(np.abs(b)), 1e-300))
 
 
-@pytest.mark.parametrize("name", sorted(ALL))
+@pytest.mark.parametrize("name", sorted(ALL) + sorted(BIG))
 def test_mask_k1_rhs_velocity(gpu, name):
     rng = np.random.default_rng(21)
     dt, re = 1e-3, 250.0
@@ -215,12 +217,13 @@ def test_mask_step_outflow_line_preconditioner(gpu, monkeypatch):
                                    [b[k] for k in ("umin", "umax", "vmin", "vmax")], atol=1e-6)
 
 
-@pytest.mark.parametrize("name", ["lshape", "step", "uchannel"])
+@pytest.mark.parametrize("name", ["lshape", "step", "uchannel", "lshape_big", "step_big"])
 def test_mask_helmholtz_tiled_sweeps_bit_identical(gpu, monkeypatch, name):
     """(r5) The masked Helmholtz solve's whole red-black sweeps in LDS tiles (k_helm_rbt_mask, u, v -> TMPU, TMPV and
     back) against the two in-place half-sweep launches per sweep (NSGPU_MASK_RBT=0): the same arithmetic on the same
-    old values, so every field after 6 full steps is bit-identical, and so are the sweep counts."""
-    P = ALL[name]
+    old values, so every field after 6 full steps is bit-identical, and so are the sweep counts.  (r6) lshape_big /
+    step_big: ny >= 128, the tiles' 64-column boundaries and their 2-cell ring inside the checked region."""
+    P = POLY[name]
     n = max(P["xspec"][-1][2], P["yspec"][-1][2])
     out = {}
     for rbt in ("1", "0"):

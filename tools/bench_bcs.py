@@ -39,6 +39,14 @@ def _run(name, grid, dt, re, warm, steps):
     s.close()
 
 
+if len(sys.argv) > 2 and sys.argv[1] == "--lshape-only":
+    # (r6) the L-shaped cavity alone (a kernel trace of its 2 + 3 steps: tools/evidence.sh fallbacks)
+    n = int(sys.argv[2])
+    hl = 1.0 / n
+    lsh = nsa.polygon([(0, 0), (0, 1), (1, 1), (1, 0.5), (0.5, 0.5), (0.5, 0)], np.full(n, hl), np.full(n, hl),
+                      [(2, 0.0), (2, 1.0), (2, 0.0), (2, 0.0), (2, 0.0), (2, 0.0)])
+    run(f"L-shaped cavity {n}x{n} (mask, walls)", lsh, hl / 8, 1000.0, warm=2, steps=3)
+    sys.exit(0)
 nx, ny = int(sys.argv[1]) if len(sys.argv) > 1 else 4096, int(sys.argv[2]) if len(sys.argv) > 2 else 1024
 h = 4.0 / nx
 run(f"channel {nx}x{ny} (inlet W, outflow E)",

@@ -58,7 +58,32 @@ devflow)
 jacobi)
   timeout -k 10 300 python3 -u tools/sweep_c5.py --n 4096 8192 16384 > $out/sweeps.log 2>&1 || exit $?
   cat $out/sweeps.log ;;
+fallbacks)
+  # (r6) the grids the direct solve does not take: bench lines (MLUPS, step and kernel
+  # rooflines) and kernel traces of the stretched cavity (ratio 1.0005 both ways / x only), a 4000^2 cavity
+  # (ny not a power of two), the 2-rank host-transport channel, and the masked L-shape / step at 4096
+  trace() {   # trace <name> <steps> <bench args...>: a kernel trace of the same command, per-step summary
+    local nm=$1 st=$2; shift 2
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace_$nm -o run -- \
+      python3 "$@" > $out/trace_$nm.log 2>&1 || return $?
+    python3 tools/trace_summary.py $(find $out/trace_$nm -name "*kernel_trace.csv" | head -1) $st > $out/${nm}_summary.txt
+    head -14 $out/${nm}_summary.txt
+  }
+  for c in stretched xstretched; do
+    timeout -k 10 300 python -u bench.py --case $c --warmup 5 --steps 20 > $out/$c.log 2>&1 || exit $?
+    line $c $out/$c.log
+    trace $c 25 bench.py --case $c --warmup 5 --steps 20 --no-cpu || exit $?
+  done
+  timeout -k 10 300 python -u bench.py --n 4000 --warmup 5 --steps 20 > $out/n4000.log 2>&1 || exit $?
+  line n4000 $out/n4000.log
+  trace n4000 25 bench.py --n 4000 --warmup 5 --steps 20 --no-cpu || exit $?
+  timeout -k 10 400 python -u bench.py --case channel --gpus 2 --transport host --warmup 3 --steps 10 \
+    > $out/channel_host2.log 2>&1 || exit $?
+  line channel_host2 $out/channel_host2.log
+  timeout -k 10 400 python -u tools/bench_bcs.py 4096 1024 4096 > $out/bcs_4096.log 2>&1 || exit $?
+  cat $out/bcs_4096.log
+  trace lshape_4096 5 tools/bench_bcs.py --lshape-only 4096 || exit $? ;;
 *)
-  echo "usage: bash tools/evidence.sh suite|bench|pmc|sizes|projection|devflow|jacobi [outdir]"; exit 2 ;;
+  echo "usage: bash tools/evidence.sh suite|bench|pmc|sizes|projection|devflow|jacobi|fallbacks [outdir]"; exit 2 ;;
 esac
 echo done
