@@ -480,10 +480,16 @@ def run(args, rank, world, local, wd):
         # (fused K3: no K3 pass (24), the DCT reads u*, v* (24 instead of 16) and stores rhs_phi for the
         # checked solves, 8 more there)
         checks = sum(int(s["n_checks"]) for s in stats)
-        fps_bpc = KERNELS["fps_dct"][1] + KERNELS["fps_tri"][1] + 16
+        fused = FPS_FUSED and args.case != "xstretched"
+        if not fused and FPS_FUSED:
+            # (r6: an x-stretched grid takes the direct solve unfused -- K3 (24), the consistent rhs's two passes
+            # (area sum 8 + fix 16), then the plain DCT of rhs_phi (16))
+            KERNELS["fps_dct"] = ("k_fps_dct (direct Poisson solve: DCT-II of every row pair of the consistent "
+                                  "rhs_phi - mean, Stockham FFT in LDS)", 16)
+        fps_bpc = KERNELS["fps_dct"][1] + KERNELS["fps_tri"][1] + 16 + (0 if fused or not FPS_FUSED else 24 + 24)
         # (the channel's checked residual is the outflow operator's: apply 16 + b - y 24 + sums 8 = 48, vs 16)
         step_bpc = (64 + (0 if FPS_FUSED else 24) + 40 + 2 * 24 * hpasses / K + 96 * band_frac + fps_bpc * cycles / K
-                    + ((48 if channel else 16) + (8 if FPS_FUSED else 0)) * checks / K)
+                    + ((48 if channel else 16) + (8 if fused else 0)) * checks / K)
     if channel and not direct:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications
         # of (line extension 8 + FUSE_R 28 + FUSE_P 26, x 4/3 for the coarser levels) = 80 each,

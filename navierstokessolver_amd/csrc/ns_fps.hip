@@ -776,7 +776,7 @@ __device__ inline void piv_pair(const FpsArgs& a, bool fast, double2 pinf, int g
 // *a.s0 for t2b (which overwrites the plane)
 __device__ inline double mode0_shift(const FpsArgs& a, int k0, const double* f = nullptr) {
     if (k0 != 0) return 0.0;
-    if (a.outE) return f ? 2.0 * f[(size_t)(a.nxl - 1) * a.ld] : *a.s0;
+    if (a.outE) return f && !a.s0_given ? 2.0 * f[(size_t)(a.nxl - 1) * a.ld] : *a.s0;
     return a.sh0 ? a.ny * *a.sh0 : 0.0;
 }
 __device__ inline double2 ldf0(const FpsArgs& a, const double* f, int li, int k0, double s0) {
@@ -1245,7 +1245,7 @@ __global__ void __launch_bounds__(64) k_fps_mid(FpsArgs a, const double* __restr
     const int k0 = 2 * (blockIdx.x * 64 + threadIdx.x);
     const int grp = blockIdx.y;
     if (k0 >= a.ny) return;
-    if (a.outE && k0 == 0 && grp == 0) *a.s0 = mode0_shift(a, 0, f);   // (t2b overwrites the plane)
+    if (a.outE && !a.s0_given && k0 == 0 && grp == 0) *a.s0 = mode0_shift(a, 0, f);   // (t2b overwrites the plane)
     const double2 y0 = ld2(a.gc + (size_t)grp * a.ld + k0);
     double Y[2] = {y0.x, y0.y};
     double BX[FPS_G][2], BR[FPS_G][2];
@@ -1613,6 +1613,14 @@ void launch_fps_t1b(const FpsArgs& a, const double* f, hipStream_t st) {
 }
 void launch_fps_mid(const FpsArgs& a, const double* f, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_mid, dim3((a.ny + 127) / 128, a.ngrp), dim3(64), 0, st, a, f);
+}
+namespace {
+__global__ void k_fps_oe_s0(const double* __restrict__ f, int row, int ld, int last, double* __restrict__ out) {
+    if (threadIdx.x == 0) out[0] = last ? 2.0 * f[(size_t)row * ld] : 0.0;
+}
+}  // namespace
+void launch_fps_oe_s0(const double* f, int row, int ld, int last, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_fps_oe_s0, dim3(1), dim3(64), 0, st, f, row, ld, last, out);
 }
 void launch_fps_t2b(const FpsArgs& a, double* f, hipStream_t st) {
     if (a.ghost) hipLaunchKernelGGL(k_fps_t2b<true>, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);

@@ -341,6 +341,9 @@ struct FpsArgs {
     // form (piv_next), mode 0 solved in the projected sense with the shift k_fps_mid keeps in *s0
     int outE = 0;
     double* s0 = nullptr;
+    // (r6) slabs: *s0 is given before t1b (the last rank's outflow row, all-reduced: launch_fps_oe_s0) -- every
+    // kernel reads it there, none derives it from its own (not the outflow) last row
+    int s0_given = 0;
     // r5: the pivots tabled (t1b / t2b without the fp64 division chain): for the modes k >= kfast (a multiple
     // of 128: whole waves) 1 / p of global rows < prow (ptab, prow x ld) and the converged value (pinf, ld);
     // ptab null: none
@@ -401,6 +404,9 @@ void launch_fps_t3(const FpsArgs& a, double* f, hipStream_t st);
 void launch_fps_t1b(const FpsArgs& a, const double* f, hipStream_t st);
 void launch_fps_mid(const FpsArgs& a, const double* f, hipStream_t st);
 void launch_fps_t2b(const FpsArgs& a, double* f, hipStream_t st);
+// (r6) slabs with an E outflow: out = 2 f'_{n-1} (mode 0 of the outflow row's eliminated coefficients) on the rank that
+// holds that row (last != 0), 0 on the others -- all-reduced (sum) into mode 0's projected shift
+void launch_fps_oe_s0(const double* f, int row, int ld, int last, double* out, hipStream_t st);
 // group scan (forward: ga -> gc ascending; backward: gb -> gx descending) from the carry-in of the other
 // ranks (R: the fold of their gathered aggregates; default: none, 0); rout (if not null) <- this rank's
 // aggregate

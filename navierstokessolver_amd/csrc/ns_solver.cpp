@@ -78,7 +78,8 @@ enum {
     S_AUXL = 22,    // 2
     S_MML = 24,     // 4
     S_KRY = 28,     // 7: (r5) a BiCGStab batch's verdict for the host (KS_STOP, KS_BRK, KS_IT, KS_R2, r.r, alpha, omega)
-    S_NUM = 35
+    S_OE = 35,      // 1: (r6) slabs with an E outflow: mode 0's projected shift 2 f'_{n-1}, all-reduced
+    S_NUM = 36
 };
 constexpr int BUS_NV = 10, BUS_NSUM = 6;
 
@@ -229,6 +230,7 @@ struct ns_solver {
     // on the finest level, is the side's 1-D line solve (launch_line_solve); -1 = walls
     int out_side = -1;
     bool consist = false;        // stretched grid, no outflow: consistent_rhs() before every Poisson solve
+    bool fps_xuni = true;        // (r6) the direct solve's hx is uniform (false: x-stretched, unfused, no pivot fixed points)
     double area = 0.0;           // sum of the domain's cell areas
     double inv_area = 0.0;       // sum of their reciprocals
     int32_t* fc_mem = nullptr;   // masked domain: topology plane (g.fc) and edge table (g.et)
@@ -2168,14 +2170,26 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         CHK(ensure_kev(s));
         if (!pre) CHK(t_begin(s, s->kev[2], s->kev[3]));
     }
+    // (the outflow row pair: the last rank's last local pair -- r6, slabs)
+    const int oe_pair = oe && g.i0 + g.nxl == g.nx ? g.nxl / 2 - 1 : -1;
     if (!pre && nsg::launch_fps_dct(false, s->arr[NS_ARR_RPHI], oe ? nullptr : s->scal + S_SHIFT, F, g.nxl, g.ny,
-                                    g.ld, s->fps_tw, s->fps_wk, s->st, oe ? g.nxl / 2 - 1 : -1, s->fps_tw8) < 0) {
+                                    g.ld, s->fps_tw, s->fps_wk, s->st, oe_pair, s->fps_tw8) < 0) {
         set_err("direct Poisson solve: ny = %d is not a supported power of two", g.ny);
         return NS_EINVAL;
     }
     if (t) {
         if (!pre) CHK(t_end(s, s->kev[2], s->kev[3]));
         HIPCHK(hipEventRecord(s->kev[4], s->st));
+    }
+    if (oe && s->nranks > 1) {
+        // (r6) slabs: the outflow row lives on the last rank -- its mode-0 shift 2 f'_{n-1} comes to every rank by one
+        // scalar all-reduce before the recurrences, which then read it instead of their own last row
+        nsg::launch_fps_oe_s0(F, g.nxl - 1, g.ld, g.i0 + g.nxl == g.nx ? 1 : 0, s->scal + S_OE, s->st);
+        CHK(allreduce(s, s->scal + S_OE, 1, ncclSum));
+        for (nsg::FpsArgs* q : {&fa, &fa1, &fam}) {
+            q->s0 = s->scal + S_OE;
+            q->s0_given = 1;
+        }
     }
     if (s->fps_passes == 3) {   // (A/B: round 4's first form)
         nsg::launch_fps_t1(fa, F, s->st);
@@ -2235,6 +2249,7 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         nsg::launch_axpby(g, 1.0, s->arr[NS_ARR_RPHI], -1.0, y, y, s->st);
         const int nb = nsg::launch_sums(g, y, s->part, s->st);
         nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_AUX + 2, s->st);
+        CHK(allreduce(s, s->scal + S_AUX + 2, 2, ncclSum));   // (r6: slabs; one rank: no-op)
         nsg::launch_finish_mean(s->scal + S_AUX + 2, s->ncells, s->scal + S_AUX, s->st);
         HIPCHK(hipMemcpyAsync(s->scal + S_RES, s->scal + S_AUX + 1, sizeof(double), hipMemcpyDeviceToDevice, s->st));
     } else {
@@ -2391,7 +2406,7 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     {
         // NSGPU_FPS_PTAB: 0 divisions everywhere, 1 the table (A/B), 2 (default) per 128-mode block its fixed-point row
         const char* pe_env = getenv("NSGPU_FPS_PTAB");
-        const int mode = pe_env ? std::atoi(pe_env) : 2;
+        const int mode = !s->fps_xuni ? 0 : pe_env ? std::atoi(pe_env) : 2;   // (r6: stretched hx -- no fixed point)
         const int PRMAX = std::min(g.nx - 1, mode == 1 ? 1024 : 4096);
         if (mode != 0 && N > 128 && PRMAX > 64) {
             std::vector<double> rr(N, 0.0);
@@ -2579,9 +2594,10 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
                 }
                 const double pem = gi > 0 ? pe[gi - 1] : 0.0;
                 double* Bq = B.data() + (size_t)rq * ld;
+                const bool oe = a.outE && gi == nx - 1;   // (r6: the eliminated outflow row, piv_next)
                 for (int k = 0; k < N; k++) {
-                    const double gg = pw[gi] * rr[k];
-                    const double p = std::fma(-gg, pem, -(pw[gi] + pe[gi]) + h[4 * N + k]);
+                    const double gg = (oe ? -0.5 * h[4 * N + k] : pw[gi]) * rr[k];
+                    const double p = std::fma(-gg, pem, oe ? h[4 * N + k] : -(pw[gi] + pe[gi]) + h[4 * N + k]);
                     rr[k] = (k == 0 && gi == nx - 1) ? 0.0 : 1.0 / p;
                     fw[k] *= -gg;
                     Bq[k] += fw[k] * rr[k] * bw[k];
@@ -3546,19 +3562,25 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
                 }
         s->area = a;
         s->inv_area = ia;
-        // the direct Poisson solve: a rectangle without an outflow side, uniform spacings (the DCT
-        // needs hy uniform; hx uniform keeps b - plain mean consistent, as the oracle's og_fps_ok
-        // assumes), ny a power of two
-        bool yuni = true;
+        // the direct Poisson solve: a rectangle without an outflow side, uniform hy (the DCT's premise), ny a power
+        // of two.  (r6) hx may be stretched (Grid.cpp:87-92): Lx's per-row coefficients enter Thomas' recurrences
+        // as they are (ns_fps.hip piv_next), and consistent_rhs makes b - plain mean area-consistent first (mode
+        // 0's singular system along x); the fused K3 form (uniform face weights) and the pivot fixed points
+        // (uniform interior rows) stay off there
+        bool yuni = true, xuni = true;
         for (int j = 1; j < gd->ny; j++) yuni &= gd->hy[j] == gd->hy[0];
-        for (int i = 1; i < gd->nx; i++) yuni &= gd->hx[i] == gd->hx[0];
+        for (int i = 1; i < gd->nx; i++) xuni &= gd->hx[i] == gd->hx[0];
         const char* fe = getenv("NSGPU_FPS");
         // (r5) or a rectangle whose only NEUMANN side is E, on one rank with nx even (the outflow row is
         // the second row of the last row pair, the elimination of ns_fps.hip's piv_next): the channel
         const int nneu_r = masked ? 0 : g.neu[0] + g.neu[1] + g.neu[2] + g.neu[3];
         const char* foe = getenv("NSGPU_FPS_OUTFLOW");
-        const bool out_ok = nneu_r == 1 && g.neu[1] && p->nranks == 1 && gd->nx % 2 == 0 && gd->nx >= 4 &&
-                            !(foe && std::atoi(foe) == 0);
+        // (r6) on slabs too: the outflow row pair is the last rank's last local pair (its row count even, >= 4), the
+        // mode-0 shift reaches the other ranks by one scalar all-reduce (pois_solve_fps)
+        int32_t lq0 = 0, lq1 = gd->nx;
+        if (p->nranks > 1) ns_slab_range(gd->nx, p->nranks, p->nranks - 1, &lq0, &lq1);
+        const bool out_ok = nneu_r == 1 && g.neu[1] && gd->nx % 2 == 0 && gd->nx >= 4 && (lq1 - lq0) % 2 == 0 &&
+                            lq1 - lq0 >= 4 && !(foe && std::atoi(foe) == 0) && xuni;   // (the elimination: uniform hx)
         s->fps = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !masked && (!outflow || out_ok) &&
                  yuni && nsg::fps_log2x(gd->ny) >= 0;
         s->fa.outE = s->fps && outflow ? 1 : 0;
@@ -3567,6 +3589,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (const char* e = getenv("NSGPU_FPS_FUSE")) s->fps_fuse = std::atoi(e) != 0;
         // (r5) ny = 16384 (configs[4]): the two-half transforms have no fused K3 form -- K3, then the DCT
         if (nsg::fps_log2(gd->ny) < 0) s->fps_fuse = false;
+        s->fps_xuni = xuni;
+        if (!xuni) s->fps_fuse = false;   // (r6: K3's general face weights, then the DCT of the consistent rhs)
         if (s->fps) s->phi_extrap = 0;   // (no initial guess: no history planes)
         const char* fpc = getenv("NSGPU_FPS_PC");
         // (r5) or a masked domain whose only NEUMANN edge is its box's whole E column (the backward-facing step):
@@ -3588,7 +3612,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
             mask_oe = whole && faces == gd->ny;
         }
         s->fps_pc = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !(fpc && std::atoi(fpc) == 0) &&
-                    masked && (!outflow || mask_oe) && yuni && p->nranks == 1 && nsg::fps_log2(gd->ny) >= 0;
+                    masked && (!outflow || mask_oe) && yuni && xuni && p->nranks == 1 && nsg::fps_log2(gd->ny) >= 0;
         if (s->fps_pc && outflow) s->fa.outE = 1;
     }
 
@@ -3829,7 +3853,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
             return fail(NS_ENOMEM);
         }
         const char* de = getenv("NSGPU_FPS_DEFER");
-        s->fps_defer = s->bus && s->fps && s->fps_fuse && s->m0e && !(de && std::atoi(de) == 0);
+        // (r6: not with an outflow side -- its mode 0 takes the projected shift, the mean never enters)
+    s->fps_defer = s->bus && s->fps && s->fps_fuse && s->m0e && !s->fa.outE && !(de && std::atoi(de) == 0);
     }
 
     if (s->loopback) {

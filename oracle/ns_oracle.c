@@ -1322,9 +1322,10 @@ int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre
  * runs the plain sequential recurrences and a textbook radix-2 FFT: it checks the GPU's chunked
  * scans and Stockham transforms, not their arithmetic order (agreement ~1e-13, not bitwise). */
 
+/* (r6) hy uniform: Ly's eigenvectors are the DCT-II basis whatever hx (L = Lx (x) I + I (x) Ly with Lx's per-row
+ * coefficients pcoef -- ConstructLHS, FluidSolver.cpp:113-131, on Grid.cpp:87-92's stretched faces) */
 int og_fps_ok(const og_grid* g) {
     if (!rect_dirichlet(g)) return 0;
-    for (int i = 1; i < g->nx; i++) if (g->hx[i] != g->hx[0]) return 0;
     for (int j = 1; j < g->ny; j++) if (g->hy[j] != g->hy[0]) return 0;
     return g->ny >= 16 && g->ny <= 16384 && (g->ny & (g->ny - 1)) == 0 && g->nx >= 2;
 }
@@ -1354,13 +1355,26 @@ static void fft_inplace(int n, double* re, double* im, const double* cw, const d
 }
 
 int og_fps_solve(const og_grid* g, double* rhs, double* x) {
-    if (!og_fps_ok(g)) { set_err("the direct solve needs a uniform rectangle with zero-flux faces, ny = 2^p in [16, 16384]"); return -1; }
+    if (!og_fps_ok(g)) { set_err("the direct solve needs a rectangle with zero-flux faces, uniform hy, ny = 2^p in [16, 16384]"); return -1; }
     const int nx = g->nx, N = g->ny;
     const size_t n = (size_t)nx * N;
     double m = 0.0;
     for (size_t c = 0; c < n; c++) m += rhs[c];
     m /= (double)n;
     for (size_t c = 0; c < n; c++) rhs[c] -= m;
+    /* (r6) stretched along x: MatNullSpaceRemove's plain mean (FluidSolver.cpp:550) leaves sum A b != 0, the
+     * system inconsistent; the area projection b_c -= (sum A b / N) / A_c (the Krylov solves' converged
+     * solution, the GPU's k_area_fix) makes mode 0's singular system along x solvable */
+    int xuni = 1;
+    for (int i = 1; i < nx; i++) xuni &= g->hx[i] == g->hx[0];
+    if (!xuni) {
+        double sab = 0.0;
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < N; j++) sab += g->hx[i] * g->hy[j] * rhs[(size_t)i * N + j];
+        const double mm = sab / (double)n;
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < N; j++) rhs[(size_t)i * N + j] -= mm / (g->hx[i] * g->hy[j]);
+    }
     const double PI = 3.14159265358979323846;
     double* cw = malloc(sizeof(double) * N); double* sw = malloc(sizeof(double) * N);
     double* ck = malloc(sizeof(double) * N); double* sk = malloc(sizeof(double) * N);

@@ -123,9 +123,10 @@ int og_mg_solve(const og_grid* g, double* rhs, double* x, double rtol, int pre, 
 int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre, int post, int maxcycles,
                   double omega);
 
-/* ---- the GPU's direct Poisson solve (ns_fps.hip, r4), restated: a uniform rectangle with
- *      zero-flux faces, ny = 2^p in [16, 16384] (og_fps_ok); DCT-II along y, one Thomas solve per
- *      mode along x (mode 0's last unknown pinned to 0), DCT-III.  rhs is mean-removed in place;
+/* ---- the GPU's direct Poisson solve (ns_fps.hip, r4), restated: a rectangle with zero-flux faces,
+ *      uniform hy (r6: any hx -- Thomas' coefficients are per row), ny = 2^p in [16, 16384] (og_fps_ok);
+ *      DCT-II along y, one Thomas solve per mode along x (mode 0's last unknown pinned to 0), DCT-III.
+ *      rhs is mean-removed in place (and, hx stretched, area-projected: b_c -= (sum A b / N) / A_c);
  *      returns 1 (one "iteration") or -1 ---- */
 int og_fps_ok(const og_grid* g);
 int og_fps_solve(const og_grid* g, double* rhs, double* x);

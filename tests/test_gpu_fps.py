@@ -68,6 +68,34 @@ def test_direct_solve_matches_oracle(gpu, nx, ny):
         assert rel(g, demean(xk)) <= 1e-8
 
 
+@pytest.mark.parametrize("nx,ny,xr", [(64, 64, 1.03), (300, 256, 0.995), (1001, 512, 1.0005), (130, 4096, 1.002)])
+def test_direct_solve_x_stretched_matches_oracle(gpu, nx, ny, xr):
+    """(r6) hx stretched (Grid.cpp:87-92: Nx { 0 l n ratio }), hy uniform: the direct solve
+    applies -- Thomas' recurrences take Lx's per-row coefficients as they are, the rhs is first made
+    area-consistent (the reference's plain mean removal, FluidSolver.cpp:550, leaves the stretched system
+    inconsistent; the GPU's consistent_rhs, the oracle's og_fps_solve) -- one 'iteration', residual <= 1e-11 of the
+    consistent rhs, phi (modulo its mean) within 1e-10 of the oracle's restatement."""
+    rng = np.random.default_rng(nx * 3 + ny)
+    og = OGrid.rectangle(nx, ny, lx=nx / ny, xratio=xr)
+    assert og.fps_ok()
+    gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny, xratio=xr), 1e-3, 100.0, rtol=1e-11)
+    b = rng.uniform(-100, 100, nx * ny)
+    gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny))
+    gs.set(gpu.NS_ARR_RPHI, b)
+    its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+    assert its == 1 and 0.0 <= res <= 1e-11, (its, res)
+    g = demean(gs.get(gpu.NS_ARR_PHI))
+    x = demean(og.fps_solve(b))
+    assert rel(g, x) <= 1e-10, rel(g, x)
+    hx = gs.grid.hx
+    A = np.outer(hx, np.full(ny, 1.0 / ny)).ravel()
+    bb = b - b.mean()
+    bc = bb - (np.sum(A * bb) / (nx * ny)) / A
+    r = og.apply_poisson(g) - bc
+    assert np.linalg.norm(r) <= 1e-11 * np.linalg.norm(bc)
+    gs.close()
+
+
 def test_direct_solve_is_deterministic(gpu):
     n = 512
     out = []
@@ -470,6 +498,28 @@ def test_outflow_channel_steps_direct_vs_krylov(gpu, monkeypatch):
     (u0, v0, _), st0 = out["0"]
     assert all(x["it_phi"] == 1 for x in st1) and all(x["it_phi"] > 1 for x in st0)
     assert np.max(np.abs(u1 - u0)) <= 1e-8 and np.max(np.abs(v1 - v0)) <= 1e-8
+
+
+@pytest.mark.parametrize("n,ny,nproc", [(128, 64, 2), (200, 64, 3), (256, 128, 4)])
+def test_outflow_direct_solve_on_slabs_matches_one_rank(tmp_path, gpu, n, ny, nproc):
+    """(r6) The NEUMANN-outflow channel's direct solve on x-slabs (host transport, every rank on
+    the one GPU): the outflow row (FluidSolver.cpp:98-101) is eliminated on the last rank, whose last local row pair
+    holds it; mode 0's projected shift 2 f'_{n-1} reaches the other ranks by one scalar all-reduce before the
+    recurrences.  The gathered steps equal one rank's: u, v and the monitor to 1e-10, phi (modulo its mean) to 1e-9
+    of its max, one Poisson 'iteration' per step on every rank (200 / 3: slabs of 67 / 67 / 66 rows)."""
+    steps, tol = 6, 1e-10
+    spec = ",".join(f"{t}:{i}" for t, i in BC_CHANNEL)
+    r = _slabs(tmp_path, nproc, "--xport", "host", "--size", str(n), "--size-y", str(ny), "--nsteps", str(steps),
+               "--solver", str(gpu.NS_POISSON_MG), "--tol", str(tol), "--bc", spec, port=29861 + nproc)
+    gs = gpu.GpuSolver(gpu.rectangle(n, ny, bc=BC_CHANNEL), 1.0 / (8 * n), 100.0, rtol=tol, device=0)
+    mm = np.array([list(gs.step().values())[:7] for _ in range(steps)])
+    u, v, phi = gs.fields()
+    gs.close()
+    assert np.all(r["mm"][:, 6] == 1) and np.all(mm[:, 6] == 1), (r["mm"][:, 6], mm[:, 6])
+    assert np.max(np.abs(r["u"] - u)) <= 1e-10
+    assert np.max(np.abs(r["v"] - v)) <= 1e-10
+    assert rel(demean(r["phi"]), demean(phi)) <= 1e-9
+    np.testing.assert_allclose(r["mm"][:, :4], mm[:, :4], atol=1e-10)
 
 
 # (the direct solve needs ny = 2^p: 256 on 3 ranks -- slabs of 88 / 84 / 84 rows)

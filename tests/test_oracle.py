@@ -193,8 +193,42 @@ def test_direct_poisson_restatement(nx, ny):
     assert np.max(np.abs(d)) <= 1e-11 * np.max(np.abs(xs))
 
 
-def test_direct_poisson_applies_only_to_uniform_walled_rectangles():
+@pytest.mark.parametrize("nx,ny,xr", [(40, 64, 1.03), (33, 16, 0.96), (24, 32, 1.1)])
+def test_direct_poisson_restatement_x_stretched(nx, ny, xr):
+    """(r6) hx stretched (Grid.cpp:87-92), hy uniform: og_fps_solve's per-row Thomas coefficients + the area
+    projection of the plain-mean rhs (b_c -= (sum A b / N) / A_c: the reference's MatNullSpaceRemove leaves the
+    stretched system inconsistent, FluidSolver.cpp:550) against an independent sparse LU of the reference's
+    matrix on that consistent rhs: phi modulo its mean to 1e-11 of max|phi|, relative residual <= 1e-12."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spl
+    og = OGrid.rectangle(nx, ny, lx=nx / ny, xratio=xr)
+    assert og.fps_ok()
+    hx = np.diff(np.concatenate([[0.0], np.cumsum(_spacing(nx / ny, nx, xr))]))
+    A = np.outer(hx, np.full(ny, 1.0 / ny)).ravel()
+    rng = np.random.default_rng(nx + ny + 1)
+    b = rng.uniform(-1, 1, og.N)
+    x = og.fps_solve(b)
+    bb = b - b.mean()
+    bc = bb - (np.sum(A * bb) / og.N) / A
+    assert abs(np.sum(A * bc)) <= 1e-13 * np.sum(np.abs(A * bc))
+    r = og.apply_poisson(x) - bc
+    assert np.linalg.norm(r) <= 1e-12 * np.linalg.norm(bc)
+    cols = [og.apply_poisson(e) for e in np.eye(og.N)]
+    M = sp.csc_matrix(np.array(cols).T)[1:, 1:]   # x_0 = 0 (consistent: the dropped row is implied)
+    xs = np.concatenate([[0.0], spl.spsolve(M.tocsc(), bc[1:])])
+    d = (x - x.mean()) - (xs - xs.mean())
+    assert np.max(np.abs(d)) <= 1e-11 * np.max(np.abs(xs))
+
+
+def _spacing(length, n, ratio):
+    """GenerateFaces' geometric spacing (Grid.cpp:87-92)."""
+    h = length * (ratio - 1) / (ratio ** n - 1)
+    return np.array([h * ratio ** k for k in range(n)])
+
+
+def test_direct_poisson_applies_only_to_walled_rectangles_with_uniform_hy():
     assert not OGrid.rectangle(64, 48).fps_ok()                     # ny not a power of two
-    assert not OGrid.rectangle(64, 64, xratio=1.01).fps_ok()        # stretched
+    assert not OGrid.rectangle(64, 64, yratio=1.01).fps_ok()        # stretched along y
+    assert OGrid.rectangle(64, 64, xratio=1.01).fps_ok()            # (r6) stretched along x only
     assert not OGrid.rectangle(64, 64, bc=[(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0)]).fps_ok()   # outflow
     assert OGrid.rectangle(64, 64, bc=[(0, 1.0), (2, 0.0), (0, 1.0), (2, 0.5)]).fps_ok()       # inlets
