@@ -497,6 +497,11 @@ def run(args, rank, world, local, wd):
         # KV_INIT) 64; no phi extrapolation
         step_bpc = 64 + 24 + 40 + 64 + 2 * 24 * hpasses / K + 352 * cycles / K
     value = cells * K / elapsed / 1e6
+    # (r6) ns_step_async with K5 deferred into the next step's K1 (every timed step's K1 applied the previous step's
+    # correction; the last step's K5 runs once inside the timed region, in solver.monitor())
+    deferred = bool(stats) and all(int(s.get("k5_deferred", 0)) for s in stats)
+    if deferred:
+        step_bpc += 88 - 64 - 40 + 40.0 / K
 
     # the north star's roofline kernel: one Jacobi sweep of this rank's slab (random phi, b;
     # 10 warm-up + 50 timed launches, HIP events), single rank only
@@ -551,6 +556,11 @@ def run(args, rank, world, local, wd):
     for key, (label, bpc) in KERNELS.items():
         if key == "band":
             bpc = 48 * band_frac
+        if key == "rhs" and deferred:
+            # (r6) K1 with the previous step's K5 folded in (k_rhs_sc): read u*, v*, phi^n, cu, cv 40 + write u, v,
+            # cu, cv, ru, rv 48
+            label, bpc = ("k_rhs_sc (K1 + the previous step's K5 folded in: CorrectVelocities on the fly, then "
+                          "ConstructRHS_V: AB2 MUSCL/Rusanov convection + CN-explicit diffusion + wall terms)", 88)
         ms, cnt = timed[key]
         if cnt:
             kern[key] = roof(key, label, bpc, ms / cnt / 1e3, cnt)

@@ -46,8 +46,8 @@ extern "C" {
                                     t_fps_idct_ms / n_fps_solves appended;
                                  8: ns_stats.phi_checked appended (res_phi is -1 on a direct solve
                                     whose residual was not computed);
-                                 9: ns_stats.t_k5_kernel_ms / n_k5_kernels (K5) and t_band_kernel_ms /
-                                    n_band_kernels (the Helmholtz wall bands) appended */
+                                 9: ns_stats.t_k5_kernel_ms / n_k5_kernels (K5), t_band_kernel_ms /
+                                    n_band_kernels (the Helmholtz wall bands) and k5_deferred appended */
 
 typedef struct ns_solver ns_solver;  /* opaque: device memory, stream, RCCL comm */
 
@@ -186,6 +186,9 @@ typedef struct ns_stats {
     int32_t n_k5_kernels;            /* number of K5 launches timed (0 or 1) */
     double  t_band_kernel_ms;        /* (ABI 9) the Helmholtz wall-band launches (k_helm_band; timing == 1) */
     int32_t n_band_kernels;          /* number of band launches timed */
+    int32_t k5_deferred;             /* (ABI 9) 1: this step's K1 applied the previous ns_step_async step's
+                                      * CorrectVelocities on the fly (k_rhs_sc: K5 folded into K1, 88 B/cell;
+                                      * the async step ends after its Poisson solve) */
 } ns_stats;
 
 /* device arrays addressable by ns_get_array / ns_set_array */

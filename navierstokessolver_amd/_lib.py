@@ -75,7 +75,7 @@ class NsStats(ctypes.Structure):
                 ("t_fps_idct_ms", ctypes.c_double), ("n_fps_solves", ctypes.c_int32),
                 ("phi_checked", ctypes.c_int32), ("t_k5_kernel_ms", ctypes.c_double),
                 ("n_k5_kernels", ctypes.c_int32), ("t_band_kernel_ms", ctypes.c_double),
-                ("n_band_kernels", ctypes.c_int32)]
+                ("n_band_kernels", ctypes.c_int32), ("k5_deferred", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

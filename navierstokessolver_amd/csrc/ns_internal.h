@@ -81,9 +81,12 @@ struct Partials {
 // K1: rhs_velocity (ConstructRHS_V); partials (sum ru^2, sum rv^2) per block
 // depth: the rows beyond a strip it reads (2: MUSCL), which the exchange / compute overlap's phases split by
 // (a deep-ghost launch passes its extension + 2: its extension rows wait for the exchange too)
+// (r6) uo / vo / mm: the previous step's CorrectVelocities folded in (ns_solver's deferred K5, ns_step_async): u, v
+// are u*, v*, phi is phi^n; the corrected u, v of every cell go to uo, vo and their min / max partials (4 per
+// block, the same count as the return value) to mm.  Streaming kernel only (-1 otherwise)
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
                const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st,
-               int depth = 2);
+               int depth = 2, double* uo = nullptr, double* vo = nullptr, double* mm = nullptr);
 // K2: fused red-black SOR sweep of (I - a L_V) on u and v, (u,v) -> (uo,vo);
 //     residual^2 partials of the input if part != null: u at part[0..n), v at part[n..2n), n returned
 int launch_helm_sweep(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,

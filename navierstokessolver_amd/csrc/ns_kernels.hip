@@ -1425,6 +1425,35 @@ __global__ __launch_bounds__(256) void k_to_f64(const float* __restrict__ src, d
 // ApplyBoundaryConditions terms included.  u, v rows ib-2 .. ie+1 are read (2 ghost rows), cu0 /
 // cv0 at the output rows (updated in place: each lane reads its cells' old values before it
 // stores them), stores through buffer resources (dropped offsets for unwritten lanes / rows).
+// (r6) CorrectVelocities + GradP of one cell (FluidSolver.cpp:420-456, 512-534): u = u* - dt dphi/dx, v = v* - dt
+// dphi/dy from the face values of phi (the wall / inlet ghost phi itself: 0.5 (p + p)).  Explicit fmas and one
+// expression for every caller -- K5 (k_cell_s<5>), K1's deferred correction (k_rhs_s CORR) and its wall ring --
+// so a deferred correction gives K5's bits
+__device__ __forceinline__ double fvp(double q, double qn, bool has, double r) {
+    return has ? fma(qn, r, q * (1.0 - r)) : 0.5 * (q + q);
+}
+__device__ __forceinline__ void corr1(double us, double vs, double pc, double pw, double pe, double ps, double pn,
+                                      bool hW, bool hE, bool hS, bool hN, double fw, double fe, double fs, double fn,
+                                      double hx, double hy, double dt, double& u, double& v) {
+    const double V0 = fvp(pc, pw, hW, fw), V1 = fvp(pc, pe, hE, fe);
+    const double V2 = fvp(pc, ps, hS, fs), V3 = fvp(pc, pn, hN, fn);
+    u = fma(-dt, (V1 - V0) / hx, us);
+    v = fma(-dt, (V3 - V2) / hy, vs);
+}
+// the same at cell (li, j) from global loads (K1's wall ring; a rectangle without NEUMANN sides)
+__device__ __forceinline__ void corr_at(const Geo& g, const Coef& c, double dt, const double* __restrict__ us,
+                                        const double* __restrict__ vs, const double* __restrict__ phi, int li, int j,
+                                        double& u, double& v) {
+    const int gi = g.i0 + li, ld = g.ld;
+    const bool hW = gi > 0, hE = gi < g.nx - 1, hS = j > 0, hN = j < g.ny - 1;
+    const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+    const double pc = phi[o];
+    const double pw = hW ? phi[o - ld] : pc, pe = hE ? phi[o + ld] : pc;
+    const double ps = hS ? phi[o - 1] : pc, pn = hN ? phi[o + 1] : pc;
+    corr1(us[o], vs[o], pc, pw, pe, ps, pn, hW, hE, hS, hN, c.fwx[gi], c.fex[gi], c.fsy[j], c.fny[j], c.hx[gi],
+          c.hy[j], dt, u, v);
+}
+
 // the ring of k_rhs_s (below): the slab's cells within two rows of the W / E walls (whole rows),
 // and on the other rows the columns 0, 1 and [jhi, ny).  Thread k: the whole wall rows first
 // (nfull of them, from local row fr[q]), then (ncol columns) x the other rows.
@@ -1447,15 +1476,22 @@ struct RhsStreamArgs {
     int nsblk;                    // workgroups of strips; those past it take the ring (nring of them)
     int nring, nstr;              // ring workgroups of this launch, the pass's strip count (partial offset)
     RhsRingArgs R;
+    // (r6) CORR: the previous step's CorrectVelocities folded in -- u, v above are u*, v*, phi is phi^n: every u, v
+    // value the stencil reads is corrected on the fly (corr1, K5's arithmetic), the written cells' corrected u, v
+    // go to uo, vo and their min / max to mm (4 per strip, then 4 per ring block)
+    double *uo, *vo, *mm;
 };
+template <bool CORR = false>
 __device__ __forceinline__ void rhs_ring_body(const Geo& g, const Coef& c, double dt, double re,
                                               const double* __restrict__ u, const double* __restrict__ v,
                                               const double* __restrict__ phi, double* __restrict__ cu,
                                               double* __restrict__ cv, double* __restrict__ ru,
                                               double* __restrict__ rv, double* __restrict__ part, const RhsRingArgs& R,
-                                              int blk) {
+                                              int blk, double* __restrict__ uo = nullptr, double* __restrict__ vo = nullptr,
+                                              double* __restrict__ mm = nullptr) {
     const int k = blk * 256 + threadIdx.x;
     double acc[2] = {0.0, 0.0};
+    double amm[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
     if (k < R.n) {
         int li, j;
         const int nf = R.nfull * g.ny;
@@ -1470,8 +1506,19 @@ __device__ __forceinline__ void rhs_ring_body(const Geo& g, const Coef& c, doubl
         }
         const int ld = g.ld, gi = g.i0 + li;
         const ptrdiff_t o = (ptrdiff_t)li * ld + j;
-        auto U = [&](int di, int dj) { return ldf(u, ld, li + di, j + dj); };
-        auto V = [&](int di, int dj) { return ldf(v, ld, li + di, j + dj); };
+        // (CORR: the stencil's u, v corrected from u*, v* and phi^n on the fly, each value by corr_at)
+        auto U = [&](int di, int dj) {
+            if (!CORR) return ldf(u, ld, li + di, j + dj);
+            double a, b;
+            corr_at(g, c, dt, u, v, phi, li + di, j + dj, a, b);
+            return a;
+        };
+        auto V = [&](int di, int dj) {
+            if (!CORR) return ldf(v, ld, li + di, j + dj);
+            double a, b;
+            corr_at(g, c, dt, u, v, phi, li + di, j + dj, a, b);
+            return b;
+        };
         auto X = [&](int t, int d) { return (t == 0 ? c.hx : t == 1 ? c.rhx : c.rsx)[gi + d]; };
         auto Y = [&](int t, int d) { return (t == 0 ? c.hy : t == 1 ? c.rhy : c.rsy)[j + d]; };
         double cun, cvn, ru_, rv_;
@@ -1484,8 +1531,19 @@ __device__ __forceinline__ void rhs_ring_body(const Geo& g, const Coef& c, doubl
             acc[0] = ru_ * ru_;
             acc[1] = rv_ * rv_;
         }
+        if (CORR) {
+            double un, vn;
+            corr_at(g, c, dt, u, v, phi, li, j, un, vn);
+            uo[o] = un;
+            vo[o] = vn;
+            amm[0] = un != un ? -INFINITY : un;
+            amm[1] = un != un ? -INFINITY : -un;
+            amm[2] = vn != vn ? -INFINITY : vn;
+            amm[3] = vn != vn ? -INFINITY : -vn;
+        }
     }
     block_reduce_sum<2>(acc, part + 2 * blk);
+    if (CORR) block_reduce_min<4>(amm, mm + 4 * blk);
 }
 
 constexpr int K1_LMAX = 128;      // k_rhs_s: rows per strip at most (one resident round of strips)
@@ -1493,13 +1551,13 @@ constexpr int K1_LMAX = 128;      // k_rhs_s: rows per strip at most (one reside
 #define K1_ESPLIT 4               // (r5) k_rhs_s: rows per run of the edge bands after a slab's exchange (0: one run)
 #endif
 constexpr int RC_K1 = 4;          // k_rhs_s: row tables from row ib-4 (the window-fill steps read ib-4 .. )
-template <bool NT, int SK, bool UY = false>
+template <bool NT, int SK, bool UY = false, bool CORR = false>
 __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
     const Geo& g = A.g;
     const Coef& c = A.c;
     if ((int)blockIdx.x >= A.nsblk) {   // the wall ring's workgroups, beside the strips (block-uniform)
-        rhs_ring_body(g, c, A.dt, A.re, A.u, A.v, A.phi, A.cu, A.cv, A.ru, A.rv, A.part + 2 * A.nstr, A.R,
-                      (int)blockIdx.x - A.nsblk);
+        rhs_ring_body<CORR>(g, c, A.dt, A.re, A.u, A.v, A.phi, A.cu, A.cv, A.ru, A.rv, A.part + 2 * A.nstr, A.R,
+                            (int)blockIdx.x - A.nsblk, A.uo, A.vo, CORR ? A.mm + 4 * A.nstr : nullptr);
         return;
     }
     __shared__ double rcs[4][K1_LMAX + 2 * RC_K1 + 2][4];   // per row: hx, 1/hx, 2/(h_{i-1}+h_i), 2/(h_i+h_{i+1})
@@ -1522,6 +1580,7 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
     }
     __syncthreads();
     double acc0 = 0.0, acc1 = 0.0;
+    double amm[4] = {INFINITY, INFINITY, INFINITY, INFINITY};   // (CORR: umin, -umax, vmin, -vmax)
     if (w < nstr) {
         const int ny = g.ny, ld = g.ld;
         const int jb = sj * SW;
@@ -1545,13 +1604,42 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
         const __amdgpu_buffer_rsrc_t brv = __builtin_amdgcn_make_buffer_rsrc(A.rv, (short)0, 0x7FFFFFF0, 0x00020000);
         // one row of u, v (row r) and of cu0, cv0 (row r-2, the output row of that step)
         // SK rows in flight, 4 double2 each (u, v, cu0, cv0)
-        double2 QU[SK], QV[SK], QC[SK], QD[SK];
-        auto load = [&](int r, double2& qu, double2& qv, double2& qc, double2& qd) {
+        // (CORR: + phi^n's row r+1, and for the wave's edge lanes the phi value beyond their outer column -- lane 0
+        // column c0 - 1, lane 63 column c1 + 1 -- the correction's y-neighbour no lane holds)
+        const int ce = lane == 0 ? max(c0 - 1, 0) : min(c0 + 2, ny - 1);
+        double2 QU[SK], QV[SK], QC[SK], QD[SK], QP[CORR ? SK : 1];
+        double QE[CORR ? SK : 1];
+        auto load = [&](int r, double2& qu, double2& qv, double2& qc, double2& qd, double2& qp, double& qe) {
             const int lr = min(max(r, rlo), rhi), lo = min(max(r - 2, 0), g.nxl - 1);
             qu = *reinterpret_cast<const double2*>(A.u + (ptrdiff_t)lr * ld + lc);
             qv = *reinterpret_cast<const double2*>(A.v + (ptrdiff_t)lr * ld + lc);
             qc = *reinterpret_cast<const double2*>(A.cu + (ptrdiff_t)lo * ld + lc);
             qd = *reinterpret_cast<const double2*>(A.cv + (ptrdiff_t)lo * ld + lc);
+            if (CORR) {
+                const int lp = min(max(r + 1, rlo), rhi);
+                qp = *reinterpret_cast<const double2*>(A.phi + (ptrdiff_t)lp * ld + lc);
+                if (lane == 0 || lane == 63) qe = A.phi[(ptrdiff_t)lp * ld + ce];
+            }
+        };
+        // CORR: phi^n rows r-1 .. r+1 (PH0..PH2) and the edge lanes' outer values of rows r, r+1 (E1, E2); the
+        // correction's column constants (hy uniform on the direct-solve grids that defer K5: GradP's face weights
+        // there are 0.5 exactly, fsy / fny's values)
+        double2 PH0 = {0, 0}, PH1 = {0, 0}, PH2 = {0, 0};
+        double E1 = 0.0, E2 = 0.0;
+        const bool cs0 = c0 > 0, cn0 = c0 < ny - 1, cs1 = c0 + 1 > 0, cn1 = c0 + 1 < ny - 1;
+        auto corr_row = [&](double2& qu, double2& qv, int r) {
+            const int gi = g.i0 + min(max(r, rlo), rhi);
+            const int gq = min(max(gi, 0), g.nx - 1);
+            const bool hW = gi > 0, hE = gi < g.nx - 1;
+            const double fw = c.fwx[gq], fe = c.fex[gq], hx = c.hx[gq], hy = c.hy[0];
+            double pl = lane_up1(PH1.y), pr = lane_dn1(PH1.x);
+            if (lane == 0) pl = E1;
+            if (lane == 63) pr = E1;
+            double2 un, vn;
+            corr1(qu.x, qv.x, PH1.x, PH0.x, PH2.x, pl, PH1.y, hW, hE, cs0, cn0, fw, fe, 0.5, 0.5, hx, hy, dt, un.x, vn.x);
+            corr1(qu.y, qv.y, PH1.y, PH0.y, PH2.y, PH1.x, pr, hW, hE, cs1, cn1, fw, fe, 0.5, 0.5, hx, hy, dt, un.y, vn.y);
+            qu = un;
+            qv = vn;
         };
         // window rows r-3 .. r; x-slopes of rows r-2 (SP*) and r-1 (SC*); the x-face (r-3 | r-2)'s fluxes
         double2 U0 = {0, 0}, U1 = {0, 0}, U2 = {0, 0}, U3 = {0, 0};
@@ -1561,7 +1649,35 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
         auto xslope = [&](double qm, double qc, double qp, const double* rw) {
             return minmode_nd((qp - qc) * rw[3], (qc - qm) * rw[2]);
         };
-        auto step = [&](const double2 qu, const double2 qv, const double2 cu0, const double2 cv0, int r) {
+        auto step = [&](double2 qu, double2 qv, const double2 cu0, const double2 cv0, const double2 qp, const double qe,
+                        int r) {
+            if (CORR) {
+                // row r's u, v from u*, v* and phi^n rows r-1 .. r+1 (r5's K5 of the previous step, folded in);
+                // the strip's own cells of row r store them, with their min / max
+                PH0 = PH1; PH1 = PH2; PH2 = qp;
+                E1 = E2; E2 = qe;
+                corr_row(qu, qv, r);
+                const bool lr = r >= ib && r < ie && r >= A.ilo && r < A.ihi && wr;
+                const unsigned off = lr ? ((unsigned)r * (unsigned)ld + (unsigned)c0) * 8u : OOB;
+                const __amdgpu_buffer_rsrc_t buo = __builtin_amdgcn_make_buffer_rsrc(A.uo, (short)0, 0x7FFFFFF0, 0x00020000);
+                const __amdgpu_buffer_rsrc_t bvo = __builtin_amdgcn_make_buffer_rsrc(A.vo, (short)0, 0x7FFFFFF0, 0x00020000);
+                const nsu4 du = {(unsigned)__double2loint(qu.x), (unsigned)__double2hiint(qu.x),
+                                 (unsigned)__double2loint(qu.y), (unsigned)__double2hiint(qu.y)};
+                const nsu4 dv = {(unsigned)__double2loint(qv.x), (unsigned)__double2hiint(qv.x),
+                                 (unsigned)__double2loint(qv.y), (unsigned)__double2hiint(qv.y)};
+                __builtin_amdgcn_raw_buffer_store_b128(du, buo, (int)off, 0, NT ? 2 : 0);
+                __builtin_amdgcn_raw_buffer_store_b128(dv, bvo, (int)off, 0, NT ? 2 : 0);
+                if (lr) {
+#pragma unroll
+                    for (int e = 0; e < 2; e++) {
+                        const double un = e ? qu.y : qu.x, vn = e ? qv.y : qv.x;
+                        amm[0] = fmin(amm[0], un != un ? -INFINITY : un);
+                        amm[1] = fmin(amm[1], un != un ? -INFINITY : -un);
+                        amm[2] = fmin(amm[2], vn != vn ? -INFINITY : vn);
+                        amm[3] = fmin(amm[3], vn != vn ? -INFINITY : -vn);
+                    }
+                }
+            }
             U0 = U1; U1 = U2; U2 = U3; U3 = vcopy(qu);
             V0 = V1; V1 = V2; V2 = V3; V3 = vcopy(qv);
             const double* rm = rc[r - 2 - ib + RC_K1];   // output row m = r-2
@@ -1655,18 +1771,34 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
         };
         // rows ib-2 .. ie+1 (the first two steps only fill the window; row ib-1's slope needs ib)
         const int r0 = ib - 2, r1 = ie + 1;
+        if (CORR) {   // phi^n rows r0 - 1, r0 (the window's first two rows) and row r0's edge value
+            const int la = min(max(r0 - 1, rlo), rhi), lb = min(max(r0, rlo), rhi);
+            PH1 = *reinterpret_cast<const double2*>(A.phi + (ptrdiff_t)la * ld + lc);
+            PH2 = *reinterpret_cast<const double2*>(A.phi + (ptrdiff_t)lb * ld + lc);
+            if (lane == 0 || lane == 63) E2 = A.phi[(ptrdiff_t)lb * ld + ce];
+        }
 #pragma unroll
         for (int q = 0; q < SK; q++) {
-            load(r0 + q, QU[q], QV[q], QC[q], QD[q]);
+            load(r0 + q, QU[q], QV[q], QC[q], QD[q], QP[CORR ? q : 0], QE[CORR ? q : 0]);
             asm volatile("" ::: "memory");
         }
         for (int r = r0; r <= r1; r += SK) {
 #pragma unroll
             for (int q = 0; q < SK; q++) {
-                step(QU[q], QV[q], QC[q], QD[q], r + q);   // (rows past r1: computed, not stored)
-                load(r + q + SK, QU[q], QV[q], QC[q], QD[q]);
+                // (rows past r1: computed, not stored)
+                step(QU[q], QV[q], QC[q], QD[q], QP[CORR ? q : 0], QE[CORR ? q : 0], r + q);
+                load(r + q + SK, QU[q], QV[q], QC[q], QD[q], QP[CORR ? q : 0], QE[CORR ? q : 0]);
             }
         }
+    }
+    if (CORR) {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) amm[k] = fmin(amm[k], __shfl_xor(amm[k], off, 64));
+        if (lane == 0 && w < nstr)
+#pragma unroll
+            for (int k = 0; k < 4; k++) A.mm[4 * wid + k] = amm[k];
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -1682,6 +1814,9 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
 // lane.  NSGPU_K1S picks the variant (A/B): 3 = k_rhs_s3, 23 / 24 = 2 waves with 3 / 4 rows in flight
 template <bool NT, int SK>
 __global__ __launch_bounds__(256) void k_rhs_s(RhsStreamArgs A) { rhs_s_body<NT, SK>(A); }
+// (r6) K1 with the previous step's K5 folded in (CORR)
+template <bool NT, int SK>
+__global__ __launch_bounds__(256) void k_rhs_sc(RhsStreamArgs A) { rhs_s_body<NT, SK, false, true>(A); }
 template <bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_rhs_s3(RhsStreamArgs A) {
     rhs_s_body<NT, 2>(A);
@@ -1740,9 +1875,6 @@ __device__ __forceinline__ double extrap_comb(double a, double x, double b, doub
 // K5's u, v stores non-temporal (A/B: make variant DEFS=-DK5_NT=1)
 #ifndef K5_NT
 #define K5_NT 0
-#endif
-#ifndef K5_RCP
-#define K5_RCP 0
 #endif
 // K5's rows in flight (A/B: make variant DEFS=-DK5_SD=n)
 #ifndef K5_SD
@@ -1878,15 +2010,9 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                 for (int e = 0; e < 2; e++) {
                     const double pc = e ? W1.y : W1.x, pw = e ? W0.y : W0.x, pe = e ? W2.y : W2.x;
                     const double ps = e ? W1.x : ps0, pn = e ? pn1 : W1.y;
-                    const double V0 = face_val(pc, pw, hW, fw, pc);
-                    const double V1 = face_val(pc, pe, hE, fe, pc);
-                    const double V2 = face_val(pc, ps, e ? s1 : s0, e ? fs1 : fs0, pc);
-                    const double V3 = face_val(pc, pn, e ? n1 : n0, e ? fn1 : fn0, pc);
-                    // (K5_RCP, A/B: the reciprocal spacings instead of the divisions -- within an ulp of GradP's)
-                    const double gx = K5_RCP ? (V1 - V0) * c.rhx[gi] : (V1 - V0) / hx;
-                    const double gy = K5_RCP ? (V3 - V2) * (e ? c.rhy[k1] : c.rhy[k0]) : (V3 - V2) / (e ? hy1 : hy0);
-                    un[e] = (e ? x.y : x.x) - A.dt * gx;
-                    vn[e] = (e ? y.y : y.x) - A.dt * gy;
+                    // (r6: corr1, the expression K1's deferred correction shares)
+                    corr1(e ? x.y : x.x, e ? y.y : y.x, pc, pw, pe, ps, pn, hW, hE, e ? s1 : s0, e ? n1 : n0, fw, fe,
+                          e ? fs1 : fs0, e ? fn1 : fn0, hx, e ? hy1 : hy0, A.dt, un[e], vn[e]);
                 }
                 if (wr && v1) {
                     st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(un[0], un[1]), K5_NT);
@@ -4267,8 +4393,11 @@ static int strip_rows(int nxl, long nsj, long cap, int lmin, int lmax = 64);
 
 int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* u, const double* v,
                const double* phi, double* cu, double* cv, double* ru, double* rv, double* part, hipStream_t st,
-               int depth) {
+               int depth, double* uo, double* vo, double* mm) {
     const char* e = getenv("NSGPU_RHS");   // NSGPU_RHS=global: the global-load K1 (A/B)
+    // (r6) uo: the previous step's correction folded in (k_rhs_sc) -- the streaming kernel only, rectangles without
+    // NEUMANN sides, hy uniform (the solver asks for it only there)
+    if (uo && (e || g.fc || !c.yuni || g.neu[0] || g.neu[1] || g.neu[2] || g.neu[3])) return -1;
     // (the grid kernels cannot split: the interior phase launches nothing, the edge phase all;
     // K1 updates cu / cv in place, so no cell may run twice)
     if (g.fc) {   // masked domain: the grid kernel with the polygon's topology
@@ -4295,6 +4424,7 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         RhsStreamArgs A{};
         A.g = g; A.c = c; A.dt = dt; A.re = re; A.u = u; A.v = v; A.phi = phi; A.cu = cu; A.cv = cv; A.ru = ru;
         A.rv = rv; A.part = part;
+        A.uo = uo; A.vo = vo; A.mm = mm;
         A.jhi = std::max(2, (g.ny - 2) & ~1);
         A.ilo = std::max(0, std::min(2 - g.i0, g.nxl));
         A.ihi = std::max(A.ilo, std::min(g.nx - 2 - g.i0, g.nxl));
@@ -4306,7 +4436,8 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         // 243-246 us vs k_rhs_s's 230 us; profiles/r05/k1_waves.log): K1 moves its bytes at ~0.8 of the
         // measured HBM copy rate already (4 streams read, 4 written), more waves only shorten the strips
         const bool uy = c.yuni && (kv == 32 || kv == 33);
-        const void* kk = uy ? (kv == 33 ? (const void*)k_rhs_su<true, 3> : (const void*)k_rhs_su<true, 2>)
+        const void* kk = uo ? (const void*)k_rhs_sc<true, 2>
+                       : uy ? (kv == 33 ? (const void*)k_rhs_su<true, 3> : (const void*)k_rhs_su<true, 2>)
                        : kv == 3 ? (const void*)k_rhs_s3<true>
                        : kv == 24 ? (const void*)k_rhs_s<true, 4> : (const void*)k_rhs_s<true, 2>;
         {
@@ -4330,8 +4461,14 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
         // the ring reads phi's and u, v's ghost rows (wall terms, MUSCL): with the edge phase
         A.nring = g_phase != 1 ? nring : 0;
         A.nsblk = (A.nsj * A.P.nrun + 3) / 4;
-        if (!inner && g_phase != 1)
+        if (!inner && g_phase != 1) {
             (void)hipMemsetAsync(part, 0, 2 * sizeof(double) * A.nstr, st);   // (no inner cells: zero partials)
+            if (mm) {   // (min / max partials of no cell: +inf)
+                static const std::vector<double> inf(4 * 4096, INFINITY);
+                if (4 * (size_t)A.nstr > inf.size()) return -1;
+                (void)hipMemcpyAsync(mm, inf.data(), 4 * sizeof(double) * A.nstr, hipMemcpyHostToDevice, st);
+            }
+        }
         if (A.nsblk + A.nring > 0) {
             void* args[] = {&A};
             if (launch_raw(kk, dim3(A.nsblk + A.nring), dim3(256), args, 0, st) != hipSuccess) return -1;

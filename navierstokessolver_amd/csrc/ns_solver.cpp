@@ -348,6 +348,11 @@ struct ns_solver {
     // launches (kev[8..11], two launches) and K5 (kev[12..13], read at the next host sync: k5_pend)
     hipEvent_t kev[14] = {};
     int band_timed = 0, k5_pend = 0;
+    // (r6) the deferred correction: an ns_step_async step ends after its Poisson solve (U, V = u*, v*, PHI = phi^n)
+    // and the next step's K1 applies CorrectVelocities on the fly (k_rhs_sc: K5 folded into K1 -- one HBM pass
+    // of 40 B/cell less); any other entry point that reads or writes the fields runs K5 first (materialize)
+    bool k5_defer_ok = false;    // one rank, rectangle, no NEUMANN side, the direct solve, hy uniform, streaming K1
+    int corr_pend = 0, defer_now = 0, corr_k1 = 0;   // corr_k1: this step's K1 applied a deferred correction
 };
 
 namespace {
@@ -1568,7 +1573,7 @@ int pois_solve_mg(ns_solver* s, int* its, double* res, ns_stats* stt) {
     double prev_rr = -1.0;
     if (s->rp_c >= 0) next_chk = s->rp_c;   // virtual slab: the replayed cycle count, one check
     // speculate at the first check when the last four solves all converged by then
-    const bool spec_ok = s->speculate && s->in_step && s->mg_predict && s->rp_c < 0 && next_chk > 0;
+    const bool spec_ok = s->speculate && s->in_step && !s->defer_now && s->mg_predict && s->rp_c < 0 && next_chk > 0;
     auto check = [&](int nb) -> int {
         const int cycles = cyc + 1;   // complete cycles (this check ends one)
         if (!(cycles >= next_chk || cycles >= maxc)) return 0;
@@ -2258,7 +2263,7 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         nsg::launch_reduce_sum(s->part, nb, 1, s->scal + S_RES, s->st);
         CHK(allreduce(s, s->scal + S_RES, 1, ncclSum));
     }
-    const bool spec = s->speculate && s->in_step;
+    const bool spec = s->speculate && s->in_step && !s->defer_now;
     if (spec) {
         CHK(fetch_begin(s));
         CHK(correct_launch(s, s->part + 4 * (size_t)nsg::max_partials(s->g)));
@@ -3179,6 +3184,20 @@ int rhs(ns_solver* s, bool defer_norm = false) {
         });
         s->cu_ext = e;
         s->u_ext = e + 2;
+    } else if (s->corr_pend && s->in_step) {
+        // (r6) the previous step's CorrectVelocities folded in: U, V hold u*, v*, PHI phi^n; the corrected u, v go to
+        // the ping-pong partners (swapped below) and their min / max -- the previous step's monitor -- to S_MM
+        double* mm = s->part + 4 * (size_t)nsg::max_partials(s->g);
+        nb = nsg::launch_rhs(s->g, s->c, s->dt, s->re, s->arr[NS_ARR_U], s->arr[NS_ARR_V], s->arr[NS_ARR_PHI],
+                             s->arr[NS_ARR_CU], s->arr[NS_ARR_CV], s->arr[NS_ARR_RU], s->arr[NS_ARR_RV], s->part, s->st,
+                             2, s->arr[NS_ARR_TMPU], s->arr[NS_ARR_TMPV], mm);
+        if (nb < 0) { set_err("K1 with the deferred correction: launch refused"); return NS_EHIP; }
+        std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
+        std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
+        s->corr_pend = 0;
+        s->corr_k1 = 1;
+        nsg::launch_reduce_min(mm, nb, 4, s->scal + S_MM, s->st);
+        s->cu_ext = 0;
     } else {
         const HaloReq r[3] = {{&s->g, s->arr[NS_ARR_U], 2}, {&s->g, s->arr[NS_ARR_V], 2}, {&s->g, s->arr[NS_ARR_PHI], 1}};
         nb = overlapped(s, r, 3, [&]() {
@@ -3254,12 +3273,26 @@ int correct_launch(ns_solver* s, double* part2) {
 }
 
 int correct(ns_solver* s) {
+    if (s->defer_now && s->in_step) {   // (r6: the next step's K1 applies it -- or materialize())
+        s->corr_pend = 1;
+        s->u_ext = 0;
+        return 0;
+    }
     if (!s->k5_spec) CHK(correct_launch(s, s->part));
     s->k5_spec = 0;
     std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
     std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
     s->u_ext = 0;   // (the corrected u, v: the slab's own rows)
     return 0;
+}
+
+// (r6) a deferred correction applied now (K5 as in a synchronous step): before any entry point that reads or writes
+// the fields, the monitor, or runs kernels on them
+int materialize(ns_solver* s) {
+    if (!s->corr_pend) return 0;
+    s->corr_pend = 0;
+    HIPCHK(hipSetDevice(s->device));
+    return correct(s);
 }
 
 int check_arr(ns_solver* s, int which) {
@@ -3855,6 +3888,14 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         const char* de = getenv("NSGPU_FPS_DEFER");
         // (r6: not with an outflow side -- its mode 0 takes the projected shift, the mean never enters)
     s->fps_defer = s->bus && s->fps && s->fps_fuse && s->m0e && !s->fa.outE && !(de && std::atoi(de) == 0);
+    {
+        // (r6) K5 deferred into the next async step's K1 (k_rhs_sc): one rank, a rectangle without NEUMANN sides (the
+        // streaming K5's domain), the direct solve (no phi-history guess formed by K5), hy uniform (K1's correction
+        // takes GradP's y face weights as 0.5); NSGPU_K5_DEFER=0: K5 at every step's end (A/B)
+        const char* kd = getenv("NSGPU_K5_DEFER");
+        s->k5_defer_ok = !comm_on(s) && !s->g.fc && s->fps && s->c.yuni && !getenv("NSGPU_RHS") && !s->tiled &&
+                         nsg::correct_streams(s->g) && !(kd && std::atoi(kd) == 0);
+    }
     }
 
     if (s->loopback) {
@@ -3929,8 +3970,10 @@ static int step_body(ns_solver* s, ns_stats& st) {
         s->rp_c = r.second;
     }
     s->in_step = 1;
+    s->corr_k1 = 0;
     const int rc = step_body_(s, st);
     s->in_step = 0;
+    st.k5_deferred = s->corr_k1;
     st.n_exchanges = s->n_xchg;
     st.n_allreduces = s->n_allred;
     st.x_link_bytes = s->x_link;
@@ -4006,6 +4049,7 @@ int ns_step(ns_solver* s, ns_stats* out) {
     nsg::set_compute_cus(s->compute_cus);
     if (s->mm_pending) HIPCHK(hipEventSynchronize(s->mev));   // (an ns_step_async before: its copy lands first)
     s->mm_pending = 0;
+    CHK(materialize(s));   // (r6: an ns_step_async before left its correction to this step: K5 first, as ns_step does)
     CHK(step_body(s, st));
     if (s->bus) {   // (r5: K5's min / max went to S_MML; fold them now -- the sync step reports its own)
         CHK(bus(s));
@@ -4038,6 +4082,25 @@ int ns_step_async(ns_solver* s, ns_stats* out) {
         HIPCHK(hipHostMalloc(&s->mm_host, 4 * sizeof(double), hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&s->mev, hipEventDisableTiming));
         for (int k = 0; k < 4; k++) s->mm_host[k] = std::numeric_limits<double>::quiet_NaN();
+    }
+    if (s->k5_defer_ok) {
+        // (r6) K5 deferred into the next step's K1: this step's K1 corrects the previous step's u*, v* (if one is
+        // pending) and reduces its min / max into S_MM before the Helmholtz check, whose host read brings them --
+        // the previous step's monitor, as before; this step's correction waits in U, V, PHI
+        // (the previous async step's monitor: in S_MM from this step's K1, or from a K5 a field read ran since)
+        const bool had = s->mm_pending != 0;
+        s->defer_now = 1;
+        const int rc = step_body(s, st);
+        s->defer_now = 0;
+        CHK(rc);
+        const double nan = std::numeric_limits<double>::quiet_NaN();
+        st.umin = had ? s->hs[S_MM] : nan;
+        st.umax = had ? -s->hs[S_MM + 1] : nan;
+        st.vmin = had ? s->hs[S_MM + 2] : nan;
+        st.vmax = had ? -s->hs[S_MM + 3] : nan;
+        s->mm_pending = 1;
+        if (out) *out = st;
+        return had ? check_monitor(st) : 0;
     }
     CHK(step_body(s, st));   // (its residual checks synchronised the stream: the previous copy has landed)
     const bool prev = s->mm_pending != 0;
@@ -4072,6 +4135,15 @@ int ns_monitor(ns_solver* s, double* mm) {
     nsg::set_compute_cus(s->compute_cus);
     ns_stats st{};
     s->mm_pending = 0;
+    if (s->k5_defer_ok) {   // (r6: the latest step's correction deferred -- K5 now -- or applied by a field read: S_MM)
+        CHK(materialize(s));
+        CHK(fetch(s));
+        st.umin = mm[0] = s->hs[S_MM];
+        st.umax = mm[1] = -s->hs[S_MM + 1];
+        st.vmin = mm[2] = s->hs[S_MM + 2];
+        st.vmax = mm[3] = -s->hs[S_MM + 3];
+        return check_monitor(st);
+    }
     if (s->bus) {   // (r5: the latest step's min / max still wait in S_MML -- every rank calls this)
         CHK(bus(s));
         CHK(fetch(s));
@@ -4097,6 +4169,7 @@ int ns_set_timing(ns_solver* s, int on) {
 
 int ns_get_array(ns_solver* s, int which, double* host) {
     CHK(check_arr(s, which));
+    CHK(materialize(s));
     HIPCHK(hipSetDevice(s->device));
     nsg::set_compute_cus(s->compute_cus);
     HIPCHK(hipMemcpy2DAsync(host, (size_t)s->g.ny * 8, s->arr[which], (size_t)s->g.ld * 8, (size_t)s->g.ny * 8,
@@ -4107,6 +4180,7 @@ int ns_get_array(ns_solver* s, int which, double* host) {
 
 int ns_set_array(ns_solver* s, int which, const double* host) {
     CHK(check_arr(s, which));
+    CHK(materialize(s));
     s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     s->cu_ext = s->u_ext = s->phi_ext = 0;   // (r5: the deep ghost rows are stale now)
     HIPCHK(hipSetDevice(s->device));
@@ -4172,6 +4246,7 @@ int ns_set_fields(ns_solver* s, const double* u, const double* v, const double* 
 }
 
 int ns_kernel(ns_solver* s, int which, int iters, double* out) {
+    if (s && s->corr_pend) CHK(materialize(s));   // (r6: a deferred correction first)
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     s->cu_ext = s->u_ext = s->phi_ext = 0;   // (r5: a kernel alone writes the slab's own rows: the deep ghost rows are stale)
@@ -4308,6 +4383,7 @@ int ns_kernel(ns_solver* s, int which, int iters, double* out) {
 }
 
 int ns_mg_transfer(ns_solver* s, int op, double* coarse) {
+    if (s && s->corr_pend) CHK(materialize(s));   // (r6: a deferred correction first)
     if (!s || !coarse || s->poisson != NS_POISSON_MG || s->lv.size() < 2) {
         set_err("ns_mg_transfer needs a multigrid solver with at least two levels");
         return NS_EINVAL;
@@ -4341,6 +4417,7 @@ int ns_mg_transfer(ns_solver* s, int op, double* coarse) {
 }
 
 int ns_fill_random(ns_solver* s, uint64_t seed) {
+    if (s && s->corr_pend) CHK(materialize(s));   // (r6: a deferred correction first)
     if (!s) { set_err("null solver"); return NS_EINVAL; }
     s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     if (s->g.fc) { set_err("ns_fill_random (the sweep benchmark input) is rectangle-only"); return NS_EINVAL; }
@@ -4354,6 +4431,7 @@ int ns_fill_random(ns_solver* s, uint64_t seed) {
 }
 
 int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
+    if (s && s->corr_pend) CHK(materialize(s));   // (r6: a deferred correction first)
     if (!s || iters <= 0) { set_err("bad arguments"); return NS_EINVAL; }
     s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     if (s->kv[0]) { set_err("ns_time_poisson times the rectangle's sweeps (no NEUMANN side, no mask)"); return NS_EINVAL; }
@@ -4394,6 +4472,7 @@ int ns_time_poisson(ns_solver* s, int warmup, int iters, double* out) {
 }
 
 int ns_time_poisson_fp32(ns_solver* s, int warmup, int iters, double* out) {
+    if (s && s->corr_pend) CHK(materialize(s));   // (r6: a deferred correction first)
     if (!s || iters <= 0) { set_err("bad arguments"); return NS_EINVAL; }
     s->guess_ready = 0;   // (TMP / the phi planes may change: the next step forms its guess itself)
     if (s->kv[0]) { set_err("ns_time_poisson_fp32 times the rectangle's sweeps (no NEUMANN side, no mask)"); return NS_EINVAL; }

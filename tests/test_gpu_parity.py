@@ -677,6 +677,38 @@ def test_step_async_equals_step(gpu):
     assert a.step()["umax"] == b.step()["umax"]
 
 
+@pytest.mark.parametrize("n", [96, 512])
+def test_deferred_correction_is_bit_identical(gpu, monkeypatch, n):
+    """(r6) ns_step_async defers CorrectVelocities (FluidSolver.cpp:512-534) into the next step's K1 (k_rhs_sc:
+    u = u* - dt grad phi formed on the fly from u*, v*, phi^n with K5's own arithmetic, corr1), so an async step
+    ends after its Poisson solve; reading the fields, the monitor or a synchronous step applies a pending
+    correction first (K5).  Against NSGPU_K5_DEFER=0 (K5 at every step's end): the same monitors, sweep counts and
+    fields bit for bit -- also across a mid-run field read and an async -> sync -> async switch."""
+    dt, re = 1.0 / (8 * n), 400.0
+    out = {}
+    for d in ("1", "0"):
+        monkeypatch.setenv("NSGPU_K5_DEFER", d)
+        gs = gpu.GpuSolver(gpu.cavity(n), dt, re)
+        st = [gs.step_async() for _ in range(4)]
+        mid = [a.copy() for a in gs.fields()]          # (a pending correction applied here)
+        st += [gs.step_async() for _ in range(3)]
+        st += [gs.step()]                              # (async -> sync)
+        st += [gs.step_async() for _ in range(3)]
+        last = gs.monitor()
+        out[d] = (st, mid, [a.copy() for a in gs.fields()], last)
+        gs.close()
+    (sa, ma, fa, la), (sb, mb, fb, lb) = out["1"], out["0"]
+    key = ("umin", "umax", "vmin", "vmax", "it_u", "it_phi")
+    for x, y in zip(sa, sb):
+        assert all((np.isnan(x[k]) and np.isnan(y[k])) or x[k] == y[k] for k in key), (x, y)
+    assert la == lb
+    for x, y in zip(ma + fa, mb + fb):
+        assert np.array_equal(x, y)
+    # the deferral ran: every async step after the first of a run folded its predecessor's K5 into K1
+    assert [x["k5_deferred"] for x in sa] == [0, 1, 1, 1, 0, 1, 1, 0, 0, 1, 1], [x["k5_deferred"] for x in sa]
+    assert all(x["k5_deferred"] == 0 for x in sb)
+
+
 def test_known_answer_trace_128_async(gpu):
     """The reference's printed 128^2 monitor through ns_step_async (one step late)."""
     n = 128
