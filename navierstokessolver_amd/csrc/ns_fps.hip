@@ -1543,6 +1543,185 @@ void dct14(bool inverse, const double* in, const double* shift, double* out, int
 
 }  // namespace
 
+// ---- (r6) any even ny in [16, 8192] whose prime factors are 2, 3, 5, 7 (3072, 3000, 1000, ...):
+// the same two transforms -- two rows per complex N-point FFT, Makhoul's reordering, the k_fps_dct / k_fps_idct
+// pre- and post-processing -- through a mixed-radix Stockham FFT in LDS (radices 8, 4, 2 for the power of two,
+// then 3, 5, 7), one stage per barrier pair: each thread reads its butterflies' R inputs, the block synchronises,
+// then writes.  Twiddles w^r = e^{-2 pi i r k / (Ns R)} from the N-entry table (Ns R divides N); the odd radices'
+// DFTs by their constant tables (O(R^2), R <= 7).  Not the power-of-two kernels' register-fed fast path: the
+// general grids' direct solve, not the headline's
+namespace {
+constexpr int GT = 512;   // threads per workgroup: at most 8 butterflies of radix 2 per thread at N = 8192
+struct GenFft {
+    int N, nst;
+    int rad[24];
+};
+__device__ constexpr double C3[3] = {1.0, -0.5, -0.5};
+__device__ constexpr double S3[3] = {0.0, 0.86602540378443864676, -0.86602540378443864676};
+__device__ constexpr double C5[5] = {1.0, 0.30901699437494742410, -0.80901699437494742410, -0.80901699437494742410,
+                                     0.30901699437494742410};
+__device__ constexpr double S5[5] = {0.0, 0.95105651629515357212, 0.58778525229247312917, -0.58778525229247312917,
+                                     -0.95105651629515357212};
+__device__ constexpr double C7[7] = {1.0, 0.62348980185873353053, -0.22252093395631440429, -0.90096886790241912624,
+                                     -0.90096886790241912624, -0.22252093395631440429, 0.62348980185873353053};
+__device__ constexpr double S7[7] = {0.0, 0.78183148246802980871, 0.97492791218182360702, 0.43388373911755812048,
+                                     -0.43388373911755812048, -0.97492791218182360702, -0.78183148246802980871};
+// X_k = sum_n v_n e^{-2 pi i n k / R}
+template <int R>
+__device__ inline void dftg(cplx* v) {
+    if constexpr (R == 2 || R == 4 || R == 8) {
+        dft<R>(v);
+    } else {
+        const double* C = R == 3 ? C3 : R == 5 ? C5 : C7;
+        const double* S = R == 3 ? S3 : R == 5 ? S5 : S7;
+        cplx x[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            cplx a = v[0];
+#pragma unroll
+            for (int n = 1; n < R; n++) {
+                const int m = (n * k) % R;
+                a = cadd(a, cmul(v[n], cplx{C[m], -S[m]}));
+            }
+            x[k] = a;
+        }
+#pragma unroll
+        for (int k = 0; k < R; k++) v[k] = x[k];
+    }
+}
+template <int R>
+__device__ inline void stage_g(cplx* z, const cplx* __restrict__ tw, int N, int Ns) {
+    constexpr int MB = (8192 / R + GT - 1) / GT;
+    const int NB = N / R, tid = threadIdx.x;
+    cplx v[MB][R];
+#pragma unroll
+    for (int b = 0; b < MB; b++) {
+        const int jb = tid + b * GT;
+        if (jb < NB)
+#pragma unroll
+            for (int r = 0; r < R; r++) v[b][r] = z[jb + r * NB];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < MB; b++) {
+        const int jb = tid + b * GT;
+        if (jb < NB) {
+            const int k = jb % Ns;
+            if (Ns > 1) {
+                const cplx w = tw[k * (N / (Ns * R))];
+                cplx wr = w;
+#pragma unroll
+                for (int r = 1; r < R; r++) {
+                    v[b][r] = cmul(v[b][r], wr);
+                    if (r + 1 < R) wr = cmul(wr, w);
+                }
+            }
+            dftg<R>(v[b]);
+            const int d = (jb - k) * R + k;
+#pragma unroll
+            for (int r = 0; r < R; r++) z[d + r * Ns] = v[b][r];
+        }
+    }
+    __syncthreads();
+}
+__device__ inline void fft_g(cplx* z, const cplx* __restrict__ tw, const GenFft& P) {
+    int Ns = 1;
+    for (int s = 0; s < P.nst; s++) {
+        switch (P.rad[s]) {
+        case 8: stage_g<8>(z, tw, P.N, Ns); break;
+        case 4: stage_g<4>(z, tw, P.N, Ns); break;
+        case 2: stage_g<2>(z, tw, P.N, Ns); break;
+        case 3: stage_g<3>(z, tw, P.N, Ns); break;
+        case 5: stage_g<5>(z, tw, P.N, Ns); break;
+        default: stage_g<7>(z, tw, P.N, Ns); break;
+        }
+        Ns *= P.rad[s];
+    }
+}
+// DCT-II of row pairs (k_fps_dct's arithmetic, any N of the plan)
+__global__ void __launch_bounds__(GT) k_fps_dctg(const double* __restrict__ in, const double* shiftp,
+                                                 double* __restrict__ out, int nrows, int ld, const cplx* __restrict__ tw,
+                                                 const cplx* __restrict__ wk, int oe_pair, GenFft P) {
+    extern __shared__ cplx z[];
+    const int N = P.N, tid = threadIdx.x, npairs = (nrows + 1) / 2;
+    const double sh = shiftp ? *shiftp : 0.0;
+    for (int p = blockIdx.x; p < npairs; p += gridDim.x) {
+        const int r0 = 2 * p;
+        const bool two = r0 + 1 < nrows;
+        const double* a = in + (size_t)r0 * ld;
+        const double lam = p == oe_pair ? 0.5 : 0.0;
+        for (int j = tid; j < N; j += GT) {
+            const int n = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
+            const double xa = a[j] - sh;
+            z[n] = cplx{xa, two ? a[ld + j] - sh - lam * xa : 0.0};
+        }
+        __syncthreads();
+        fft_g(z, tw, P);
+        double* oa = out + (size_t)r0 * ld;
+        double* ob = oa + ld;
+        for (int k = tid; k < N; k += GT) {
+            const cplx Zk = z[k], Zn = z[k ? N - k : 0];
+            const cplx Va{0.5 * (Zk.x + Zn.x), 0.5 * (Zk.y - Zn.y)};
+            const cplx Vb{0.5 * (Zk.y + Zn.y), 0.5 * (Zn.x - Zk.x)};
+            const cplx w = wk[k];
+            oa[k] = fma(w.x, Va.x, -w.y * Va.y);
+            if (two) ob[k] = fma(w.x, Vb.x, -w.y * Vb.y);
+        }
+        __syncthreads();
+    }
+}
+// DCT-III of row pairs (k_fps_idct's arithmetic)
+__global__ void __launch_bounds__(GT) k_fps_idctg(const double* __restrict__ in, double* __restrict__ out, int nrows,
+                                                  int ld, const cplx* __restrict__ tw, const cplx* __restrict__ wk,
+                                                  GenFft P) {
+    extern __shared__ cplx z[];
+    const int N = P.N, tid = threadIdx.x, npairs = (nrows + 1) / 2;
+    const double rn = 1.0 / N;
+    for (int p = blockIdx.x; p < npairs; p += gridDim.x) {
+        const int r0 = 2 * p;
+        const bool two = r0 + 1 < nrows;
+        const double* a = in + (size_t)r0 * ld;
+        for (int k = tid; k < N; k += GT) {
+            const double xa = a[k], xb = two ? a[ld + k] : 0.0;
+            const double ya = k ? a[N - k] : 0.0, yb = two && k ? a[ld + N - k] : 0.0;
+            const cplx w = wk[k];
+            const double c = w.x, sn = -w.y;
+            const cplx Va{fma(c, xa, sn * ya), fma(sn, xa, -c * ya)};
+            const cplx Vb{fma(c, xb, sn * yb), fma(sn, xb, -c * yb)};
+            z[k] = cplx{Va.x - Vb.y, -(Va.y + Vb.x)};
+        }
+        __syncthreads();
+        fft_g(z, tw, P);
+        double* oa = out + (size_t)r0 * ld;
+        double* ob = oa + ld;
+        for (int j = tid; j < N; j += GT) {
+            const int n = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
+            const cplx y = z[n];
+            oa[j] = y.x * rn;
+            if (two) ob[j] = -y.y * rn;
+        }
+        __syncthreads();
+    }
+}
+// the radix plan of N (radices 8 / 4 / 2 first, then 3, 5, 7); false if N has another prime factor
+bool gen_plan(int N, GenFft& P) {
+    P.N = N;
+    P.nst = 0;
+    int m = N;
+    while (m % 8 == 0) { P.rad[P.nst++] = 8; m /= 8; }
+    if (m % 4 == 0) { P.rad[P.nst++] = 4; m /= 4; }
+    if (m % 2 == 0) { P.rad[P.nst++] = 2; m /= 2; }
+    for (int q : {3, 5, 7})
+        while (m % q == 0 && P.nst < 24) { P.rad[P.nst++] = q; m /= q; }
+    return m == 1;
+}
+}  // namespace
+
+bool fps_gen_ok(int ny) {
+    GenFft P;
+    return ny >= 16 && ny <= 8192 && ny % 2 == 0 && fps_log2(ny) < 0 && gen_plan(ny, P);
+}
+
 int fps_log2(int ny) {
     int l = 0;
     while ((1 << l) < ny) l++;
@@ -1555,6 +1734,22 @@ int launch_fps_dct(bool inverse, const double* in, const double* shift, double* 
     if (ny == N14) {   // (r5: two 8192-point transforms per row pair)
         if (!tw8) return -1;
         dct14(inverse, in, shift, out, nrows, ld, tw, tw8, wk, st, oe_pair);
+        return 0;
+    }
+    if (fps_gen_ok(ny)) {   // (r6) the mixed-radix transforms
+        GenFft P;
+        gen_plan(ny, P);
+        const int npairs = (nrows + 1) / 2, lds = ny * (int)sizeof(cplx);
+        const int nb = std::max(1, std::min(npairs, 1024));
+        if (inverse) {
+            lds_attr_once((const void*)k_fps_idctg, lds);
+            hipLaunchKernelGGL(k_fps_idctg, dim3(nb), dim3(GT), lds, st, in, out, nrows, ld, (const cplx*)tw,
+                               (const cplx*)wk, P);
+        } else {
+            lds_attr_once((const void*)k_fps_dctg, lds);
+            hipLaunchKernelGGL(k_fps_dctg, dim3(nb), dim3(GT), lds, st, in, shift, out, nrows, ld, (const cplx*)tw,
+                               (const cplx*)wk, oe_pair, P);
+        }
         return 0;
     }
     switch (fps_log2(ny)) {

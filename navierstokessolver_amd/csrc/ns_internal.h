@@ -392,6 +392,8 @@ int launch_fps_dct(bool inverse, const double* in, const double* shift, double* 
                    const double* tw, const double* wk, hipStream_t st, int oe_pair = -1, const double* tw8 = nullptr);
 // (r5) log2(ny) also for ny = 16384 (the two-half transforms of launch_fps_dct), else as fps_log2
 int fps_log2x(int ny);
+// (r6) ny the mixed-radix transforms take (even, 16 .. 8192, prime factors 2, 3, 5, 7; not a power of two)
+bool fps_gen_ok(int ny);
 // K3 fused into the DCT (k_fps_dct_div): b = Div_V(u*, v*) / dt of the slab's rows -> their DCT-II
 // coefficients in out (of b itself: FpsArgs::sh0 takes the mean off later), b stored too if not null,
 // (sum b, sum b^2) per row pair p at part + 2 p.  phase 0: every row pair; 1: those whose rows need no

@@ -3615,7 +3615,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         const bool out_ok = nneu_r == 1 && g.neu[1] && gd->nx % 2 == 0 && gd->nx >= 4 && (lq1 - lq0) % 2 == 0 &&
                             lq1 - lq0 >= 4 && !(foe && std::atoi(foe) == 0) && xuni;   // (the elimination: uniform hx)
         s->fps = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !masked && (!outflow || out_ok) &&
-                 yuni && nsg::fps_log2x(gd->ny) >= 0;
+                 yuni && (nsg::fps_log2x(gd->ny) >= 0 || nsg::fps_gen_ok(gd->ny));   // (r6: mixed radix)
         s->fa.outE = s->fps && outflow ? 1 : 0;
         if (const char* e = getenv("NSGPU_FPS_CHECK")) s->fps_check = std::max(0, std::atoi(e));
         if (const char* e = getenv("NSGPU_FPS_PASSES")) s->fps_passes = std::atoi(e) == 3 && !s->fa.outE ? 3 : 2;

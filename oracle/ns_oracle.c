@@ -1327,7 +1327,32 @@ int og_mg_solve_w(const og_grid* g, double* rhs, double* x, double rtol, int pre
 int og_fps_ok(const og_grid* g) {
     if (!rect_dirichlet(g)) return 0;
     for (int j = 1; j < g->ny; j++) if (g->hy[j] != g->hy[0]) return 0;
-    return g->ny >= 16 && g->ny <= 16384 && (g->ny & (g->ny - 1)) == 0 && g->nx >= 2;
+    /* (r6) any even ny in [16, 8192] with prime factors 2, 3, 5, 7 too -- the GPU's mixed-radix transforms
+     * (ns_fps.hip fps_gen_ok); restated here with a plain O(N^2) DFT */
+    int m = g->ny;
+    if (m % 2 == 0 && m <= 8192)
+        for (int q = 2; q <= 7; q++)
+            while (m % q == 0) m /= q;
+    const int gen = g->ny % 2 == 0 && g->ny <= 8192 && m == 1;
+    return g->ny >= 16 && g->ny <= 16384 && ((g->ny & (g->ny - 1)) == 0 || gen) && g->nx >= 2;
+}
+
+/* in-place forward DFT of any n (the plain O(n^2) sum; cw / sw: cos / sin (2 pi m / n), m < n) */
+static void dft_plain(int n, double* re, double* im, const double* cw, const double* sw) {
+    double* xr = malloc(sizeof(double) * n);
+    double* xi = malloc(sizeof(double) * n);
+    for (int k = 0; k < n; k++) {
+        double ar = 0.0, ai = 0.0;
+        for (int j = 0; j < n; j++) {
+            const int m = (int)(((long)j * k) % n);
+            const double c = cw[m], s = -sw[m];   /* e^{-2 pi i j k / n} */
+            ar += re[j] * c - im[j] * s;
+            ai += re[j] * s + im[j] * c;
+        }
+        xr[k] = ar; xi[k] = ai;
+    }
+    for (int k = 0; k < n; k++) { re[k] = xr[k]; im[k] = xi[k]; }
+    free(xr); free(xi);
 }
 
 /* in-place forward DFT of n = 2^p complex points (iterative radix-2, bit-reversed input order) */
@@ -1394,7 +1419,7 @@ int og_fps_solve(const og_grid* g, double* rhs, double* x) {
             const int q = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);
             re[q] = r[j]; im[q] = 0.0;
         }
-        fft_inplace(N, re, im, cw, sw);
+        if (N & (N - 1)) dft_plain(N, re, im, cw, sw); else fft_inplace(N, re, im, cw, sw);
         for (int k = 0; k < N; k++) F[(size_t)i * N + k] = ck[k] * re[k] + sk[k] * im[k];
     }
     /* Thomas per mode along x: a_i = cw_i, c_i = ce_i, d_i = -(cw_i + ce_i) + mu_k */
@@ -1429,7 +1454,7 @@ int og_fps_solve(const og_grid* g, double* rhs, double* x) {
             re[k] = ck[k] * a + sk[k] * b;
             im[k] = -(sk[k] * a - ck[k] * b);
         }
-        fft_inplace(N, re, im, cw, sw);
+        if (N & (N - 1)) dft_plain(N, re, im, cw, sw); else fft_inplace(N, re, im, cw, sw);
         double* o = x + (size_t)i * N;
         for (int j = 0; j < N; j++) {
             const int q = (j & 1) ? N - 1 - (j >> 1) : (j >> 1);

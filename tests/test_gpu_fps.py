@@ -40,9 +40,11 @@ def demean(x):
 # (r5) ny = 16384 (configs[4]'s grid): the two-half transforms through the scratch plane, an odd nx among them
 SIZES = [(64, 64), (96, 128), (40, 256), (37, 64), (1001, 512), (16, 16), (130, 32), (300, 4096), (128, 8192),
          (64, 16384), (37, 16384)]
+# (r6) ny not a power of two: the mixed-radix transforms (radices 8 / 4 / 2, 3, 5, 7)
+SIZES_MIXED = [(64, 3072), (40, 3000), (33, 1000), (96, 24), (130, 6144), (17, 210), (256, 1536)]
 
 
-@pytest.mark.parametrize("nx,ny", SIZES)
+@pytest.mark.parametrize("nx,ny", SIZES + SIZES_MIXED)
 def test_direct_solve_matches_oracle(gpu, nx, ny):
     rng = np.random.default_rng(nx * 7 + ny)
     og = OGrid.rectangle(nx, ny, lx=nx / ny)

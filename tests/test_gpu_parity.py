@@ -261,7 +261,7 @@ def test_stretched_full_steps_vs_oracle(gpu, nx, ny, xr, yr, bc):
     dt = 1.0 / (16 * max(nx, ny))
     og, gs = pair(gpu, nx, ny, dt, 200.0, bc, xr, yr)
     osv = OSolver(og, dt, 200.0, rtol=1e-13)
-    direct = yr == -1 and ny & (ny - 1) == 0 and bc != BC_CHANNEL
+    direct = yr == -1 and bc != BC_CHANNEL and OGrid.rectangle(nx, ny, bc=bc, xratio=xr).fps_ok()
     for _ in range(10):
         st = gs.step()
         mm, _ = osv.step()

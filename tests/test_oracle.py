@@ -169,7 +169,7 @@ def test_multigrid_checks_the_cycle_output():
     assert cm == cyc - 1 and (cyc == 1 or rel(xm) > rtol)
 
 
-@pytest.mark.parametrize("nx,ny", [(40, 64), (33, 16), (24, 32)])
+@pytest.mark.parametrize("nx,ny", [(40, 64), (33, 16), (24, 32), (20, 48), (16, 60), (12, 70)])
 def test_direct_poisson_restatement(nx, ny):
     """og_fps_solve (the GPU's direct Poisson solve restated: DCT-II along y, Thomas along x with mode
     0 pinned, DCT-III) against an independent sparse LU of the reference's matrix (ConstructLHS,
@@ -227,7 +227,9 @@ def _spacing(length, n, ratio):
 
 
 def test_direct_poisson_applies_only_to_walled_rectangles_with_uniform_hy():
-    assert not OGrid.rectangle(64, 48).fps_ok()                     # ny not a power of two
+    assert not OGrid.rectangle(64, 44).fps_ok()                     # ny with a prime factor > 7
+    assert not OGrid.rectangle(64, 45).fps_ok()                     # ny odd
+    assert OGrid.rectangle(64, 48).fps_ok()                         # (r6) 2^4 * 3: the mixed-radix transforms
     assert not OGrid.rectangle(64, 64, yratio=1.01).fps_ok()        # stretched along y
     assert OGrid.rectangle(64, 64, xratio=1.01).fps_ok()            # (r6) stretched along x only
     assert not OGrid.rectangle(64, 64, bc=[(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0)]).fps_ok()   # outflow
