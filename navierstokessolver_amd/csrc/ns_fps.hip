@@ -777,7 +777,7 @@ __device__ inline void piv_pair(const FpsArgs& a, bool fast, double2 pinf, int g
 __device__ inline double mode0_shift(const FpsArgs& a, int k0, const double* f = nullptr) {
     if (k0 != 0) return 0.0;
     if (a.outE) return f && !a.s0_given ? 2.0 * f[(size_t)(a.nxl - 1) * a.ld] : *a.s0;
-    return a.sh0 ? a.ny * *a.sh0 : 0.0;
+    return a.sh0 ? (a.sh0s != 0.0 ? a.sh0s : (double)a.ny) * *a.sh0 : 0.0;
 }
 __device__ inline double2 ldf0(const FpsArgs& a, const double* f, int li, int k0, double s0) {
     double2 x = ld2(f + (size_t)li * a.ld + k0);
@@ -1716,6 +1716,31 @@ bool gen_plan(int N, GenFft& P) {
     return m == 1;
 }
 }  // namespace
+
+namespace {
+__global__ __launch_bounds__(256) void k_dense_mats(const double* __restrict__ C, const double* __restrict__ shy,
+                                                    double rsum, int N, double* __restrict__ F, double* __restrict__ G) {
+    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (size_t)N * N) return;
+    const int j = (int)(t % N), k = (int)(t / N);   // column k of F^T / G: element (j, k)
+    const double sq = shy[j];
+    double f, gv;
+    if (k == 0) {
+        f = sq * sq * rsum;
+        gv = rsum;
+    } else {
+        const double q = C[(size_t)(N - 1 - k) * N + j];
+        f = q * sq;
+        gv = q / sq;
+    }
+    F[(size_t)j * N + k] = f;     // F(k, j), column-major
+    G[(size_t)k * N + j] = gv;    // G(j, k)
+}
+}  // namespace
+void launch_dense_mats(const double* C, const double* shy, double rsum, int N, double* F, double* G, hipStream_t st) {
+    const size_t n = (size_t)N * N;
+    hipLaunchKernelGGL(k_dense_mats, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, C, shy, rsum, N, F, G);
+}
 
 bool fps_gen_ok(int ny) {
     GenFft P;

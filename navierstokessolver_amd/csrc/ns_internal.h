@@ -335,7 +335,8 @@ struct FpsArgs {
     double* cb;                    // backward chunk aggregates (2 x nch x ld)
     const double* bt;              // two-pass recurrences: per chunk beta (d BX / d Y_in) and BR (2 x nch x ld, host)
     double* ya;                    // two-pass recurrences: every chunk's forward carry-in (nch x ld)
-    const double* sh0 = nullptr;   // fused K3 (launch_fps_div): the mean, taken off mode 0 as ny * mean
+    const double* sh0 = nullptr;   // fused K3 (launch_fps_div): the mean, taken off mode 0 as sh0s * mean
+    double sh0s = 0.0;             // (r6) mode 0's transform of the constant 1: ny (the DCT), sqrt(sum hy) (dense)
     // r5, multi-rank, the mean deferred to the forward allgather: k_fps_mid corrects mode 0's chunk aggregates
     // (E, BXl from b's raw coefficients) by the response to the constant ny * *m0s -- m0e / m0b: every local
     // chunk's forward end value / local back substitution of the constant 1 (host tables)
@@ -394,6 +395,11 @@ int launch_fps_dct(bool inverse, const double* in, const double* shift, double* 
 int fps_log2x(int ny);
 // (r6) ny the mixed-radix transforms take (even, 16 .. 8192, prime factors 2, 3, 5, 7; not a power of two)
 bool fps_gen_ok(int ny);
+// (r6) the dense y transforms' matrices (column-major N x N) from the tridiagonal eigenvectors C (column k = the
+// eigenvector of the k-th smallest eigenvalue) and sqrt(hy): F(k, j) = q_{N-1-k}[j] sqrt(hy_j), G(j, k) =
+// q_{N-1-k}[j] / sqrt(hy_j) -- mode 0 (the zero eigenvalue) set exactly: F(0, j) = hy_j / sqrt(sum hy), G(j, 0) =
+// 1 / sqrt(sum hy)
+void launch_dense_mats(const double* C, const double* shy, double rsum, int N, double* F, double* G, hipStream_t st);
 // K3 fused into the DCT (k_fps_dct_div): b = Div_V(u*, v*) / dt of the slab's rows -> their DCT-II
 // coefficients in out (of b itself: FpsArgs::sh0 takes the mean off later), b stored too if not null,
 // (sum b, sum b^2) per row pair p at part + 2 p.  phase 0: every row pair; 1: those whose rows need no

@@ -3786,42 +3786,19 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
 
 
 // ---------------------------------------------------------------- reductions
-// (r6) one pass over the partials: every thread sums its strided share of all nv (<= 4) values in registers
-// (ascending k), each wave folds its lanes by an xor-shuffle tree, and one thread adds the 16 waves' sums in wave
-// order -- ONE barrier.  Rounds 1-5 ran a 10-barrier LDS tree per value: 4.4-6.4 us per single-workgroup launch,
-// ~20 us per step over the four of them (rocprofv3, profiles/r05/final).  A fixed order: deterministic.
-// Value v of partial k at p[k * ks + v * vs]
-__device__ __forceinline__ void red_sum4(const double* __restrict__ p, int n, int nv, int ks, int vs, double (&r)[4]) {
-    __shared__ double sh[16][4];
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-    for (int k = threadIdx.x; k < n; k += 1024)
-#pragma unroll
-        for (int v = 0; v < 4; v++)
-            if (v < nv) a[v] += p[(size_t)k * ks + (size_t)v * vs];
-#pragma unroll
-    for (int v = 0; v < 4; v++)
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) a[v] += __shfl_xor(a[v], off, 64);
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0)
-#pragma unroll
-        for (int v = 0; v < 4; v++) sh[wv][v] = a[v];
-    __syncthreads();
-#pragma unroll
-    for (int v = 0; v < 4; v++) {
-        double t = sh[0][v];
-        for (int w = 1; w < 16; w++) t += sh[w][v];
-        r[v] = t;
-    }
-}
 __global__ __launch_bounds__(1024) void k_reduce_sum(const double* __restrict__ p, int n, int nv,
                                                      double* __restrict__ out) {
-    // (nv > 4: four values per pass)
-    for (int v0 = 0; v0 < nv; v0 += 4) {
-        double r[4];
-        red_sum4(p + v0, n, min(4, nv - v0), nv, 1, r);
-        if ((int)threadIdx.x < min(4, nv - v0)) out[v0 + threadIdx.x] = r[threadIdx.x];
+    __shared__ double sh[1024];
+    for (int v = 0; v < nv; v++) {
+        double s = 0.0;
+        for (int k = threadIdx.x; k < n; k += 1024) s += p[(size_t)k * nv + v];
+        sh[threadIdx.x] = s;
+        __syncthreads();
+        for (int w = 512; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[v] = sh[0];
         __syncthreads();
     }
 }
@@ -3830,10 +3807,18 @@ __global__ __launch_bounds__(1024) void k_reduce_sum(const double* __restrict__ 
 // summed exactly as k_reduce_sum (nv = 1) sums it
 __global__ __launch_bounds__(1024) void k_reduce_sum_segs(const double* __restrict__ p, int n, int nseg,
                                                           double* __restrict__ out) {
-    for (int g0 = 0; g0 < nseg; g0 += 4) {
-        double r[4];
-        red_sum4(p + (size_t)g0 * n, n, min(4, nseg - g0), 1, n, r);
-        if ((int)threadIdx.x < min(4, nseg - g0)) out[g0 + threadIdx.x] = r[threadIdx.x];
+    __shared__ double sh[1024];
+    for (int g = 0; g < nseg; g++) {
+        const double* q = p + (size_t)g * n;
+        double s = 0.0;
+        for (int k = threadIdx.x; k < n; k += 1024) s += q[k];
+        sh[threadIdx.x] = s;
+        __syncthreads();
+        for (int w = 512; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[g] = sh[0];
         __syncthreads();
     }
 }
@@ -3844,7 +3829,6 @@ __global__ __launch_bounds__(1024) void k_reduce_min(const double* __restrict__ 
     // results through LDS (2 barriers instead of 11 per value; fmin is order-independent)
     __shared__ double sh[16][4];
     double m[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
-#pragma unroll 4
     for (int k = threadIdx.x; k < n; k += 1024)
 #pragma unroll
         for (int v = 0; v < 4; v++)
@@ -3870,12 +3854,23 @@ __global__ __launch_bounds__(1024) void k_reduce_min(const double* __restrict__ 
 __global__ __launch_bounds__(1024) void k_reduce_sum_mean(const double* __restrict__ p, int n,
                                                           double* __restrict__ sums, double nc,
                                                           double* __restrict__ out) {
-    double r[4];
-    red_sum4(p, n, 2, 2, 1, r);
+    __shared__ double sh[1024];
+    double r[2];
+    for (int v = 0; v < 2; v++) {
+        double s = 0.0;
+        for (int k = threadIdx.x; k < n; k += 1024) s += p[(size_t)k * 2 + v];
+        sh[threadIdx.x] = s;
+        __syncthreads();
+        for (int w = 512; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+            __syncthreads();
+        }
+        r[v] = sh[0];
+        if (threadIdx.x == 0) sums[v] = sh[0];
+        __syncthreads();
+    }
     if (threadIdx.x == 0) {
         const double s = r[0], s2 = r[1];
-        sums[0] = s;
-        sums[1] = s2;
         out[0] = s / nc;
         out[1] = fmax(s2 - s * s / nc, 0.0);
     }

@@ -10,6 +10,9 @@
 // FluidSolver.cpp:61-82) are replaced by red-black SOR sweeps run to the same
 // relative-residual tolerance, checked every few sweeps from a fused residual.
 #include <rccl/rccl.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+#include <dlfcn.h>
 #include <limits>
 
 #include <algorithm>
@@ -231,6 +234,11 @@ struct ns_solver {
     int out_side = -1;
     bool consist = false;        // stretched grid, no outflow: consistent_rhs() before every Poisson solve
     bool fps_xuni = true;        // (r6) the direct solve's hx is uniform (false: x-stretched, unfused, no pivot fixed points)
+    // (r6) the dense y transforms (hy stretched, or an ny no FFT plan takes): Ly's eigenvectors through rocSOLVER's
+    // tridiagonal eigensolver at create, the transforms as rocBLAS GEMMs (F: forward, G: inverse, N x N each)
+    bool fps_dense = false;
+    rocblas_handle rb = nullptr;
+    double *dense_mem = nullptr, *dF = nullptr, *dG = nullptr;
     double area = 0.0;           // sum of the domain's cell areas
     double inv_area = 0.0;       // sum of their reciprocals
     int32_t* fc_mem = nullptr;   // masked domain: topology plane (g.fc) and edge table (g.et)
@@ -2142,6 +2150,34 @@ int fps_scan(ns_solver* s, bool backward) {
     return 0;
 }
 
+// (r6) rocBLAS / rocSOLVER for the dense y transforms, loaded on first use (dlopen): the common grids never map the
+// libraries (their code objects would add ~20 MB to every process that loads libnsgpu.so)
+struct DenseLib {
+    bool tried = false, ok = false;
+    decltype(&rocblas_create_handle) create = nullptr;
+    decltype(&rocblas_destroy_handle) destroy = nullptr;
+    decltype(&rocblas_set_stream) set_stream = nullptr;
+    decltype(&rocblas_dgemm) dgemm = nullptr;
+    decltype(&rocsolver_dstedc) dstedc = nullptr;
+};
+DenseLib& dense_lib() {
+    static DenseLib L;
+    if (L.tried) return L;
+    L.tried = true;
+    void* hb = dlopen("librocblas.so.5", RTLD_NOW | RTLD_GLOBAL);
+    if (!hb) hb = dlopen("/opt/rocm/lib/librocblas.so", RTLD_NOW | RTLD_GLOBAL);
+    void* hs = dlopen("librocsolver.so.0", RTLD_NOW | RTLD_GLOBAL);
+    if (!hs) hs = dlopen("/opt/rocm/lib/librocsolver.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!hb || !hs) return L;
+    L.create = (decltype(L.create))dlsym(hb, "rocblas_create_handle");
+    L.destroy = (decltype(L.destroy))dlsym(hb, "rocblas_destroy_handle");
+    L.set_stream = (decltype(L.set_stream))dlsym(hb, "rocblas_set_stream");
+    L.dgemm = (decltype(L.dgemm))dlsym(hb, "rocblas_dgemm");
+    L.dstedc = (decltype(L.dstedc))dlsym(hs, "rocsolver_dstedc");
+    L.ok = L.create && L.destroy && L.set_stream && L.dgemm && L.dstedc;
+    return L;
+}
+
 // the direct solve (ns_fps.hip): RPHI - shift -> PHI through the transformed plane in TMP; one
 // "iteration".  A checked solve computes its residual; speculating, K5 is enqueued before the host
 // reads it (as after a predicted multigrid check).  A residual above rtol (never seen: ~1e-14)
@@ -2173,17 +2209,29 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     }
     if (t) {
         CHK(ensure_kev(s));
-        if (!pre) CHK(t_begin(s, s->kev[2], s->kev[3]));
+        if (!pre && !s->fps_dense) CHK(t_begin(s, s->kev[2], s->kev[3]));
     }
     // (the outflow row pair: the last rank's last local pair -- r6, slabs)
     const int oe_pair = oe && g.i0 + g.nxl == g.nx ? g.nxl / 2 - 1 : -1;
-    if (!pre && nsg::launch_fps_dct(false, s->arr[NS_ARR_RPHI], oe ? nullptr : s->scal + S_SHIFT, F, g.nxl, g.ny,
-                                    g.ld, s->fps_tw, s->fps_wk, s->st, oe_pair, s->fps_tw8) < 0) {
+    if (s->fps_dense) {
+        // (r6) the dense forward transform: F^T = F (N x N) b^T, one GEMM over the slab's rows (rocBLAS, column-major:
+        // the row-major plane is its transpose); the mean comes off mode 0 in the recurrences (sh0, scale sh0s)
+        if (t) HIPCHK(hipEventRecord(s->kev[2], s->st));
+        const double one = 1.0, zero = 0.0;
+        if (dense_lib().dgemm(s->rb, rocblas_operation_none, rocblas_operation_none, g.ny, g.nxl, g.ny, &one, s->dF, g.ny,
+                          s->arr[NS_ARR_RPHI], g.ld, &zero, F, g.ld) != rocblas_status_success) {
+            set_err("direct Poisson solve: the dense forward transform (rocblas_dgemm) failed");
+            return NS_EHIP;
+        }
+        if (t) HIPCHK(hipEventRecord(s->kev[3], s->st));
+        fa.sh0 = fa1.sh0 = fam.sh0 = s->scal + S_SHIFT;
+    } else if (!pre && nsg::launch_fps_dct(false, s->arr[NS_ARR_RPHI], oe ? nullptr : s->scal + S_SHIFT, F, g.nxl, g.ny,
+                                           g.ld, s->fps_tw, s->fps_wk, s->st, oe_pair, s->fps_tw8) < 0) {
         set_err("direct Poisson solve: ny = %d is not a supported power of two", g.ny);
         return NS_EINVAL;
     }
     if (t) {
-        if (!pre) CHK(t_end(s, s->kev[2], s->kev[3]));
+        if (!pre && !s->fps_dense) CHK(t_end(s, s->kev[2], s->kev[3]));
         HIPCHK(hipEventRecord(s->kev[4], s->st));
     }
     if (oe && s->nranks > 1) {
@@ -2218,11 +2266,25 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
     s->phi_ext = s->fps_passes != 3 && s->deep && s->in_step ? 1 : 0;
     if (t) {
         HIPCHK(hipEventRecord(s->kev[5], s->st));
-        CHK(t_begin(s, s->kev[6], s->kev[7]));
+        if (s->fps_dense) HIPCHK(hipEventRecord(s->kev[6], s->st));
+        else CHK(t_begin(s, s->kev[6], s->kev[7]));
     }
-    nsg::launch_fps_dct(true, F - (ptrdiff_t)glo * g.ld, nullptr, s->arr[NS_ARR_PHI] - (ptrdiff_t)glo * g.ld,
-                        g.nxl + glo + ghi, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st, -1, s->fps_tw8);
-    if (t) CHK(t_end(s, s->kev[6], s->kev[7]));
+    if (s->fps_dense) {   // (r6) phi^T = G (N x N) x^T over the rows the solve wrote
+        const double one = 1.0, zero = 0.0;
+        if (dense_lib().dgemm(s->rb, rocblas_operation_none, rocblas_operation_none, g.ny, g.nxl + glo + ghi, g.ny, &one,
+                          s->dG, g.ny, F - (ptrdiff_t)glo * g.ld, g.ld, &zero,
+                          s->arr[NS_ARR_PHI] - (ptrdiff_t)glo * g.ld, g.ld) != rocblas_status_success) {
+            set_err("direct Poisson solve: the dense inverse transform (rocblas_dgemm) failed");
+            return NS_EHIP;
+        }
+    } else {
+        nsg::launch_fps_dct(true, F - (ptrdiff_t)glo * g.ld, nullptr, s->arr[NS_ARR_PHI] - (ptrdiff_t)glo * g.ld,
+                            g.nxl + glo + ghi, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st, -1, s->fps_tw8);
+    }
+    if (t) {
+        if (s->fps_dense) HIPCHK(hipEventRecord(s->kev[7], s->st));
+        else CHK(t_end(s, s->kev[6], s->kev[7]));
+    }
     auto take_times = [&]() -> int {
         if (!t || !stt) return 0;
         HIPCHK(hipEventSynchronize(s->kev[7]));
@@ -2364,6 +2426,50 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
         const double sn = std::sin(u);
         h[4 * N + m] = -4.0 / (hy[0] * hy[0]) * sn * sn;   // -(2/hy^2)(1 - cos(pi m / N))
     }
+    if (s->fps_dense) {
+        // (r6) Ly's eigen-decomposition (the Poisson operator along y, ConstructLHS FluidSolver.cpp:113-131: zero-flux
+        // faces, 2 / (h (h + h_nb)) toward each neighbour): S = H^1/2 Ly H^-1/2 is symmetric tridiagonal (diagonal
+        // -(ps + pn), off-diagonal sqrt(pn_j ps_j+1)); rocSOLVER's divide and conquer gives its eigenpairs, the
+        // transforms F = Q^T H^1/2, G = H^-1/2 Q (mode 0 = the zero eigenvalue, its vector H^1/2 1 set exactly)
+        std::vector<double> dg(N), of(std::max(N - 1, 1), 0.0), shy(N);
+        double sumhy = 0.0;
+        for (int j = 0; j < N; j++) {
+            const double ps = j > 0 ? 2.0 / (hy[j] * (hy[j] + hy[j - 1])) : 0.0;
+            const double pn = j < N - 1 ? 2.0 / (hy[j] * (hy[j] + hy[j + 1])) : 0.0;
+            dg[j] = -(ps + pn);
+            if (j < N - 1) of[j] = std::sqrt(pn * (2.0 / (hy[j + 1] * (hy[j + 1] + hy[j]))));
+            shy[j] = std::sqrt(hy[j]);
+            sumhy += hy[j];
+        }
+        DenseLib& DL = dense_lib();
+        if (!DL.ok) { set_err("the dense y transforms need librocblas / librocsolver (dlopen failed)"); return NS_EINVAL; }
+        if (DL.create(&s->rb) != rocblas_status_success) { set_err("rocblas_create_handle failed"); return NS_EHIP; }
+        if (DL.set_stream(s->rb, s->st) != rocblas_status_success) { set_err("rocblas_set_stream failed"); return NS_EHIP; }
+        const size_t nn = (size_t)N * N;
+        HIPCHK(hipMalloc(&s->dense_mem, (3 * nn + 3 * (size_t)N + 8) * sizeof(double)));
+        s->dF = s->dense_mem;
+        s->dG = s->dF + nn;
+        double *dC = s->dG + nn, *dD = dC + nn, *dE = dD + N, *dS = dE + N;
+        rocblas_int* dinfo = reinterpret_cast<rocblas_int*>(dS + N);
+        HIPCHK(hipMemcpy(dD, dg.data(), N * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(dE, of.data(), std::max(N - 1, 1) * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(dS, shy.data(), N * sizeof(double), hipMemcpyHostToDevice));
+        if (DL.dstedc(s->rb, rocblas_evect_tridiagonal, N, dD, dE, dC, N, dinfo) != rocblas_status_success) {
+            set_err("rocsolver_dstedc failed (ny = %d)", N);
+            return NS_EHIP;
+        }
+        rocblas_int info = 0;
+        std::vector<double> lam(N);
+        HIPCHK(hipMemcpyAsync(&info, dinfo, sizeof(info), hipMemcpyDeviceToHost, s->st));
+        HIPCHK(hipMemcpyAsync(lam.data(), dD, N * sizeof(double), hipMemcpyDeviceToHost, s->st));
+        HIPCHK(hipStreamSynchronize(s->st));
+        if (info != 0) { set_err("rocsolver_dstedc: info %d (ny = %d)", (int)info, N); return NS_EHIP; }
+        // mode k: the (N - 1 - k)-th smallest eigenvalue (ascending from rocSOLVER): mode 0 the zero one
+        for (int k = 0; k < N; k++) h[4 * N + k] = k == 0 ? 0.0 : lam[N - 1 - k];
+        nsg::launch_dense_mats(dC, dS, 1.0 / std::sqrt(sumhy), N, s->dF, s->dG, s->st);
+        HIPCHK(hipStreamSynchronize(s->st));
+        a.sh0s = std::sqrt(sumhy);   // (mode 0 of the constant 1: sum_j hy_j / sqrt(sum hy))
+    }
     double* rp0 = h.data() + n_tab;
     double* bt = rp0 + n_rp0;   // per chunk: beta (the local back substitution over pi) and BR
     std::vector<double> r(N, 0.0);   // 1 / p of the previous row, per mode
@@ -2411,7 +2517,7 @@ int fps_setup(ns_solver* s, const std::vector<double>& hy, const double* pw, con
     {
         // NSGPU_FPS_PTAB: 0 divisions everywhere, 1 the table (A/B), 2 (default) per 128-mode block its fixed-point row
         const char* pe_env = getenv("NSGPU_FPS_PTAB");
-        const int mode = !s->fps_xuni ? 0 : pe_env ? std::atoi(pe_env) : 2;   // (r6: stretched hx -- no fixed point)
+        const int mode = !s->fps_xuni || s->fps_dense ? 0 : pe_env ? std::atoi(pe_env) : 2;   // (r6: stretched -- none)
         const int PRMAX = std::min(g.nx - 1, mode == 1 ? 1024 : 4096);
         if (mode != 0 && N > 128 && PRMAX > 64) {
             std::vector<double> rr(N, 0.0);
@@ -3614,8 +3720,15 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (p->nranks > 1) ns_slab_range(gd->nx, p->nranks, p->nranks - 1, &lq0, &lq1);
         const bool out_ok = nneu_r == 1 && g.neu[1] && gd->nx % 2 == 0 && gd->nx >= 4 && (lq1 - lq0) % 2 == 0 &&
                             lq1 - lq0 >= 4 && !(foe && std::atoi(foe) == 0) && xuni;   // (the elimination: uniform hx)
-        s->fps = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !masked && (!outflow || out_ok) &&
-                 yuni && (nsg::fps_log2x(gd->ny) >= 0 || nsg::fps_gen_ok(gd->ny));   // (r6: mixed radix)
+        // (r6) the transforms along y: the FFT (hy uniform, ny a power of two or of 2, 3, 5, 7) or the dense
+        // eigenvector transforms (hy stretched, Grid.cpp:87-92, or another ny <= 4096; walls / inlets only)
+        const bool fft = yuni && (nsg::fps_log2x(gd->ny) >= 0 || nsg::fps_gen_ok(gd->ny));
+        const char* fdn = getenv("NSGPU_FPS_DENSE");
+        const bool dense = !fft && !outflow && gd->ny >= 2 && gd->ny <= (yuni ? 4096 : 8192) &&
+                           !(fdn && std::atoi(fdn) == 0);
+        s->fps = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !masked &&
+                 (fft ? (!outflow || out_ok) : dense);
+        s->fps_dense = s->fps && !fft;
         s->fa.outE = s->fps && outflow ? 1 : 0;
         if (const char* e = getenv("NSGPU_FPS_CHECK")) s->fps_check = std::max(0, std::atoi(e));
         if (const char* e = getenv("NSGPU_FPS_PASSES")) s->fps_passes = std::atoi(e) == 3 && !s->fa.outE ? 3 : 2;
@@ -3623,7 +3736,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         // (r5) ny = 16384 (configs[4]): the two-half transforms have no fused K3 form -- K3, then the DCT
         if (nsg::fps_log2(gd->ny) < 0) s->fps_fuse = false;
         s->fps_xuni = xuni;
-        if (!xuni) s->fps_fuse = false;   // (r6: K3's general face weights, then the DCT of the consistent rhs)
+        if (!xuni || s->fps_dense) s->fps_fuse = false;   // (r6: K3's general face weights, then the transform)
         if (s->fps) s->phi_extrap = 0;   // (no initial guess: no history planes)
         const char* fpc = getenv("NSGPU_FPS_PC");
         // (r5) or a masked domain whose only NEUMANN edge is its box's whole E column (the backward-facing step):
@@ -3935,6 +4048,8 @@ void ns_destroy(ns_solver* s) {
     if (s->cvimg) (void)hipFree(s->cvimg);
     if (s->dmat) (void)hipFree(s->dmat);
     if (s->fps_mem) (void)hipFree(s->fps_mem);
+    if (s->dense_mem) (void)hipFree(s->dense_mem);
+    if (s->rb) (void)dense_lib().destroy(s->rb);
     if (s->cap_mem) (void)hipFree(s->cap_mem);
     for (auto e : s->kev)
         if (e) (void)hipEventDestroy(e);

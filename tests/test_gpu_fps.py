@@ -98,6 +98,34 @@ def test_direct_solve_x_stretched_matches_oracle(gpu, nx, ny, xr):
     gs.close()
 
 
+@pytest.mark.parametrize("nx,ny,xr,yr", [(64, 64, -1, 1.03), (100, 96, 1.02, 0.98), (33, 44, -1, -1), (48, 22, 1.05, -1),
+                                        (256, 512, 1.001, 1.0005), (40, 2048, -1, 1.0002)])
+def test_direct_solve_dense_matches_krylov(gpu, nx, ny, xr, yr):
+    """(r6) Every other walled rectangle the reference's Grid accepts: hy stretched (Grid.cpp:87-92) or an ny no FFT
+    plan takes (44 = 4 x 11, 22) -- the transforms along y are Ly's eigenvectors (rocSOLVER's tridiagonal eigensolver
+    at ns_create, the transforms as two rocBLAS GEMMs per solve), Thomas along x as before.  One 'iteration',
+    residual <= 1e-11 of the area-consistent rhs, phi (modulo its mean) within 1e-8 of the oracle's Krylov solve of
+    the reference's matrix (its area-projected solution, FluidSolver.cpp:550-551) at rtol 1e-13."""
+    rng = np.random.default_rng(nx + 5 * ny)
+    og = OGrid.rectangle(nx, ny, lx=nx / ny, xratio=xr, yratio=yr)
+    gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny, xratio=xr, yratio=yr), 1e-3, 100.0, rtol=1e-11)
+    b = rng.uniform(-100, 100, nx * ny)
+    gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny))
+    gs.set(gpu.NS_ARR_RPHI, b)
+    its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+    assert its == 1 and 0.0 <= res <= 1e-11, (its, res)
+    g = demean(gs.get(gpu.NS_ARR_PHI))
+    A = np.outer(gs.grid.hx, gs.grid.hy).ravel()
+    bb = b - b.mean()
+    bc = bb - (np.sum(A * bb) / (nx * ny)) / A
+    r = og.apply_poisson(g) - bc
+    assert np.linalg.norm(r) <= 1e-11 * np.linalg.norm(bc)
+    if nx * ny <= 70000:
+        xk, _ = og.solve_poisson(b)
+        assert rel(g, demean(xk)) <= 1e-8, rel(g, demean(xk))
+    gs.close()
+
+
 def test_direct_solve_is_deterministic(gpu):
     n = 512
     out = []

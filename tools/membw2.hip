@@ -108,7 +108,107 @@ __global__ __launch_bounds__(256) void k_3r2w(const double2* __restrict__ p, con
     }
 }
 
+// (r6) the guide's copy pattern (MI355X_MICROARCH.md: 6.29 TB/s "float4 copy"): one 16-B
+// element per thread, a grid of n / 256 workgroups (no grid-stride loop), plain and non-temporal stores
+template <bool NTS>
+__global__ __launch_bounds__(256) void k_copy1(const double2* __restrict__ a, double2* __restrict__ c, size_t n2) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n2) {
+        const double2 x = a[i];
+        if (NTS) { __builtin_nontemporal_store(x.x, &c[i].x); __builtin_nontemporal_store(x.y, &c[i].y); }
+        else c[i] = x;
+    }
+}
+// (r6) K1 with K5 folded in (k_rhs_sc): read u*, v*, phi, cu, cv, write u, v, cu, cv, ru, rv -- 5 reads + 6 writes of
+// 16 B per lane (88 B/cell), non-temporal stores like the kernel
+template <int U>
+__global__ __launch_bounds__(256) void k_5r6w(const double2* __restrict__ us, const double2* __restrict__ vs,
+                                              const double2* __restrict__ ph, double2* cu, double2* cv,
+                                              double2* __restrict__ u, double2* __restrict__ v, double2* __restrict__ ru,
+                                              double2* __restrict__ rv, size_t n2) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i0 = blockIdx.x * 256 + threadIdx.x; i0 < n2; i0 += stride * U) {
+        double2 a[U], b[U], c[U], d[U], e[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const size_t i = i0 + k * stride;
+            if (i < n2) { a[k] = us[i]; b[k] = vs[i]; c[k] = ph[i]; d[k] = cu[i]; e[k] = cv[i]; }
+        }
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const size_t i = i0 + k * stride;
+            if (i < n2) {
+                auto st = [](double2* p, double x, double y) {
+                    __builtin_nontemporal_store(x, &p->x); __builtin_nontemporal_store(y, &p->y);
+                };
+                st(&u[i], a[k].x - c[k].x, a[k].y - c[k].y);
+                st(&v[i], b[k].x - c[k].y, b[k].y - c[k].x);
+                st(&cu[i], a[k].x + d[k].x, a[k].y + d[k].y);
+                st(&cv[i], b[k].x + e[k].x, b[k].y + e[k].y);
+                st(&ru[i], a[k].x - e[k].x, a[k].y - e[k].y);
+                st(&rv[i], b[k].x - d[k].x, b[k].y - d[k].y);
+            }
+        }
+    }
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "copy") {   // (r6) copy ceilings at 4096^2, 8192^2, 16384^2
+        for (int n : {4096, 8192, 16384}) {
+            const size_t N = (size_t)n * n;
+            double *a, *c;
+            hipMalloc(&a, N * 8); hipMalloc(&c, N * 8);
+            hipMemset(a, 0, N * 8); hipMemset(c, 0, N * 8);
+            hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+            auto timeit = [&](auto launch, const std::string& name) {
+                for (int w = 0; w < 5; w++) launch();
+                std::vector<float> ts;
+                for (int it = 0; it < 20; it++) {
+                    hipEventRecord(e0); launch(); hipEventRecord(e1); hipEventSynchronize(e1);
+                    float ms; hipEventElapsedTime(&ms, e0, e1); ts.push_back(ms);
+                }
+                std::sort(ts.begin(), ts.end());
+                printf("n=%d %-34s median %8.1f us  %7.1f GB/s (16 B/cell)\n", n, name.c_str(), ts[10] * 1e3,
+                       16.0 * N / (ts[10] * 1e-3) / 1e9);
+            };
+            const unsigned g1 = (unsigned)((N / 2 + 255) / 256);
+            timeit([&] { hipLaunchKernelGGL((k_copy1<false>), dim3(g1), dim3(256), 0, 0, (const double2*)a, (double2*)c, N / 2); }, "copy one/thread");
+            timeit([&] { hipLaunchKernelGGL((k_copy1<true>), dim3(g1), dim3(256), 0, 0, (const double2*)a, (double2*)c, N / 2); }, "copy one/thread ntstore");
+            for (int g : {2048, 8192, 32768}) {
+                auto G = std::to_string(g);
+                timeit([&] { hipLaunchKernelGGL((k_copy<1>), dim3(g), dim3(256), 0, 0, (const double2*)a, (double2*)c, N / 2); }, "copy U1 grid=" + G);
+                timeit([&] { hipLaunchKernelGGL((k_copy<4>), dim3(g), dim3(256), 0, 0, (const double2*)a, (double2*)c, N / 2); }, "copy U4 grid=" + G);
+            }
+            hipFree(a); hipFree(c);
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "k1c") {   // (r6) K1 + K5's 5-read / 6-write mix
+        for (int n : {4096, 8192}) {
+            const size_t N = (size_t)n * n;
+            double* f[9];
+            for (auto& x : f) { hipMalloc(&x, N * 8); hipMemset(x, 0, N * 8); }
+            hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+            for (int g : {2048, 4096, 8192}) {
+                auto launch = [&] {
+                    hipLaunchKernelGGL((k_5r6w<2>), dim3(g), dim3(256), 0, 0, (const double2*)f[0], (const double2*)f[1],
+                                       (const double2*)f[2], (double2*)f[3], (double2*)f[4], (double2*)f[5], (double2*)f[6],
+                                       (double2*)f[7], (double2*)f[8], N / 2);
+                };
+                for (int w = 0; w < 5; w++) launch();
+                std::vector<float> ts;
+                for (int it = 0; it < 20; it++) {
+                    hipEventRecord(e0); launch(); hipEventRecord(e1); hipEventSynchronize(e1);
+                    float ms; hipEventElapsedTime(&ms, e0, e1); ts.push_back(ms);
+                }
+                std::sort(ts.begin(), ts.end());
+                printf("n=%d 5R6W (K1+K5 mix, nt stores) grid=%d median %8.1f us  %7.1f GB/s (88 B/cell)\n", n, g,
+                       ts[10] * 1e3, 88.0 * N / (ts[10] * 1e-3) / 1e9);
+            }
+            for (auto x : f) hipFree(x);
+        }
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "k5") {   // K5's 3-read / 2-write mix at 4096^2 and 8192^2
         for (int n : {4096, 8192}) {
             const size_t N = (size_t)n * n;
