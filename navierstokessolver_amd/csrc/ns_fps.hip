@@ -1766,14 +1766,24 @@ int launch_fps_dct(bool inverse, const double* in, const double* shift, double* 
         gen_plan(ny, P);
         const int npairs = (nrows + 1) / 2, lds = ny * (int)sizeof(cplx);
         const int nb = std::max(1, std::min(npairs, 1024));
+        hipEvent_t ea, eb;
+        const bool tm = take_launch_timing(ea, eb);   // (the solve's dispatch-stamped transform timing)
         if (inverse) {
             lds_attr_once((const void*)k_fps_idctg, lds);
-            hipLaunchKernelGGL(k_fps_idctg, dim3(nb), dim3(GT), lds, st, in, out, nrows, ld, (const cplx*)tw,
-                               (const cplx*)wk, P);
+            if (tm)
+                hipExtLaunchKernelGGL(k_fps_idctg, dim3(nb), dim3(GT), lds, st, ea, eb, 0, in, out, nrows, ld,
+                                      (const cplx*)tw, (const cplx*)wk, P);
+            else
+                hipLaunchKernelGGL(k_fps_idctg, dim3(nb), dim3(GT), lds, st, in, out, nrows, ld, (const cplx*)tw,
+                                   (const cplx*)wk, P);
         } else {
             lds_attr_once((const void*)k_fps_dctg, lds);
-            hipLaunchKernelGGL(k_fps_dctg, dim3(nb), dim3(GT), lds, st, in, shift, out, nrows, ld, (const cplx*)tw,
-                               (const cplx*)wk, oe_pair, P);
+            if (tm)
+                hipExtLaunchKernelGGL(k_fps_dctg, dim3(nb), dim3(GT), lds, st, ea, eb, 0, in, shift, out, nrows, ld,
+                                      (const cplx*)tw, (const cplx*)wk, oe_pair, P);
+            else
+                hipLaunchKernelGGL(k_fps_dctg, dim3(nb), dim3(GT), lds, st, in, shift, out, nrows, ld, (const cplx*)tw,
+                                   (const cplx*)wk, oe_pair, P);
         }
         return 0;
     }

@@ -152,7 +152,60 @@ __global__ __launch_bounds__(256) void k_5r6w(const double2* __restrict__ us, co
     }
 }
 
+// (r6) the strip walk of the streaming kernels (K1 / K5 / the sweeps): each wave owns a 64-lane x 16-B column strip
+// (1 KiB of a row) and walks L rows with SK rows in flight; the workgroup's 4 waves take 4 adjacent strips (4 KiB of
+// each row) -- a copy in that order, against the one-shot copy above
+template <int SK>
+__global__ __launch_bounds__(256) void k_strip_copy(const double2* __restrict__ a, double2* __restrict__ c, int ld2,
+                                                    int nsj, int L, int rows) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nwj = nsj / 4;
+    const int run = blockIdx.x / nwj, sj = (blockIdx.x % nwj) * 4 + wave;
+    const size_t col = (size_t)sj * 64 + lane;
+    const int r0 = run * L, r1 = min(r0 + L, rows);
+    double2 q[SK];
+#pragma unroll
+    for (int k = 0; k < SK; k++) q[k] = r0 + k < r1 ? a[(size_t)(r0 + k) * ld2 + col] : make_double2(0, 0);
+    for (int r = r0; r < r1; r += SK) {
+#pragma unroll
+        for (int k = 0; k < SK; k++) {
+            if (r + k < r1) c[(size_t)(r + k) * ld2 + col] = q[k];
+            if (r + k + SK < r1) q[k] = a[(size_t)(r + k + SK) * ld2 + col];
+        }
+    }
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "strip") {   // (r6) strip-walk copies at 4096^2 .. 16384^2
+        for (int n : {4096, 8192, 16384}) {
+            const size_t N = (size_t)n * n;
+            double *a, *c;
+            hipMalloc(&a, N * 8); hipMalloc(&c, N * 8);
+            hipMemset(a, 0, N * 8); hipMemset(c, 0, N * 8);
+            hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+            auto timeit = [&](auto launch, const std::string& name) {
+                for (int w = 0; w < 5; w++) launch();
+                std::vector<float> ts;
+                for (int it = 0; it < 20; it++) {
+                    hipEventRecord(e0); launch(); hipEventRecord(e1); hipEventSynchronize(e1);
+                    float ms; hipEventElapsedTime(&ms, e0, e1); ts.push_back(ms);
+                }
+                std::sort(ts.begin(), ts.end());
+                printf("n=%d %-34s median %8.1f us  %7.1f GB/s (16 B/cell)\n", n, name.c_str(), ts[10] * 1e3,
+                       16.0 * N / (ts[10] * 1e-3) / 1e9);
+            };
+            const int ld2 = n / 2, nsj = ld2 / 64;
+            const unsigned g1 = (unsigned)((N / 2 + 255) / 256);
+            timeit([&] { hipLaunchKernelGGL((k_copy1<false>), dim3(g1), dim3(256), 0, 0, (const double2*)a, (double2*)c, N / 2); }, "copy one/thread");
+            for (int L : {16, 64, 256}) {
+                const int nb = (nsj / 4) * ((n + L - 1) / L);
+                timeit([&] { hipLaunchKernelGGL((k_strip_copy<2>), dim3(nb), dim3(256), 0, 0, (const double2*)a, (double2*)c, ld2, nsj, L, n); }, "strip SK2 L=" + std::to_string(L));
+                timeit([&] { hipLaunchKernelGGL((k_strip_copy<4>), dim3(nb), dim3(256), 0, 0, (const double2*)a, (double2*)c, ld2, nsj, L, n); }, "strip SK4 L=" + std::to_string(L));
+            }
+            hipFree(a); hipFree(c);
+        }
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "copy") {   // (r6) copy ceilings at 4096^2, 8192^2, 16384^2
         for (int n : {4096, 8192, 16384}) {
             const size_t N = (size_t)n * n;
