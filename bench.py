@@ -464,14 +464,21 @@ def run(args, rank, world, local, wd):
     # the Helmholtz wall bands (two k_helm_band launches) on the cells within 128 of a wall:
     # per launch u, v read 16 + rhs 16 + write 16 -> 96 B per band cell
     bw = max(32, min(n, nyc) // 32)   # the solver's band_w
+    if min(n, nyc) > 4096:
+        bw = 3 * min(n, nyc) // 64
     band_frac = 1.0 - max(n - 2 * bw, 0) * max(nyc - 2 * bw, 0) / float(n * nyc)
+    # (r6) one rank, 6 band sweeps (<= 4096): ONE k_helm_band6 launch (48 B per band cell) + the band cells'
+    # copy-back (32 B), timed as one interval -- 80 B per band cell per step instead of 2 x 48
+    band6 = (world == 1 and min(n, nyc) <= 4096 and os.environ.get("NSGPU_BAND6", "1") != "0"
+             and os.environ.get("NSGPU_BAND_SWEEPS", "6") == "6")
+    band_bpc = (80 if band6 else 96) * band_frac
     # the finest level: a V-cycle whose output is not checked hands its prolongation pass to the next
     # cycle's restriction pass (one k_sweep4 pass of 28 B/cell instead of 26 + 26): cycles - checks
     # such boundaries per solve (one rank, multigrid)
     fused = sum(max(0, int(s["it_phi"]) - int(s["n_checks"])) for s in stats) if (world == 1 and not channel) else 0
     if not any(s["n_cycle_kernels"] for s in stats) and args.time_every:
         fused = 0   # (NSGPU_FUSE4=0: no boundary pass was timed, none ran)
-    step_bpc = (64 + 24 + 40 + extrap_bpc + 2 * 24 * hpasses / K + 96 * band_frac
+    step_bpc = (64 + 24 + 40 + extrap_bpc + 2 * 24 * hpasses / K + band_bpc
                 + (52 * (cycles - fused) + 28 * fused) / K + 52 * cycles / K / 3.0)
     if direct:
         # the direct solve: 56 B/cell (fps_* above; 72 in the three-pass form; 64 with K3 fused) per solve, plus its
@@ -488,7 +495,7 @@ def run(args, rank, world, local, wd):
                                   "rhs_phi - mean, Stockham FFT in LDS)", 16)
         fps_bpc = KERNELS["fps_dct"][1] + KERNELS["fps_tri"][1] + 16 + (0 if fused or not FPS_FUSED else 24 + 24)
         # (the channel's checked residual is the outflow operator's: apply 16 + b - y 24 + sums 8 = 48, vs 16)
-        step_bpc = (64 + (0 if FPS_FUSED else 24) + 40 + 2 * 24 * hpasses / K + 96 * band_frac + fps_bpc * cycles / K
+        step_bpc = (64 + (0 if FPS_FUSED else 24) + 40 + 2 * 24 * hpasses / K + band_bpc + fps_bpc * cycles / K
                     + ((48 if channel else 16) + (8 if fused else 0)) * checks / K)
     if channel and not direct:
         # BiCGStab iteration (`cycles` = iterations): KV_P 32, two preconditioner applications
@@ -561,6 +568,10 @@ def run(args, rank, world, local, wd):
     for key, (label, bpc) in KERNELS.items():
         if key == "band":
             bpc = 48 * band_frac
+            if band6:
+                label, bpc = ("k_helm_band6 + k_band_copy (Helmholtz wall bands: 6 RB-SOR sweeps of u, v on the cells "
+                              "near a wall in one launch of 64 x 64 tiles with their 12-cell cone in LDS, then the "
+                              "band cells' copy-back)", band_bpc)
         if key == "rhs" and deferred:
             # (r6) K1 with the previous step's K5 folded in (k_rhs_sc): read u*, v*, phi^n, cu, cv 40 + write u, v,
             # cu, cv, ru, rv 48

@@ -1360,7 +1360,9 @@ void dct_pair(bool inverse, const double* in, const double* shift, double* out, 
     constexpr int T = Fft<LOGN>::T;
     const size_t lds = sizeof(cplx) * (size_t)FftLds<LOGN>::n;
     // (two workgroups per CU fit the LDS: one persistent round)
-    const dim3 grid(std::min((nrows + 1) / 2, 2 * device_cus()));
+    // (r6, A/B) NSGPU_FPS_GRID: workgroups per launch (0: one persistent round, two per CU)
+    static const int fg = getenv("NSGPU_FPS_GRID") ? std::atoi(getenv("NSGPU_FPS_GRID")) : 0;
+    const dim3 grid(std::min((nrows + 1) / 2, fg > 0 ? fg : 2 * device_cus()));
     if (inverse) {
         lds_attr_once((const void*)k_fps_idct<LOGN>, (int)lds);
         hipEvent_t a, b;
@@ -1387,7 +1389,8 @@ int div_pair(const FpsDivArgs& a0, hipStream_t st) {
     constexpr int T = Fft<LOGN>::T;
     const size_t lds = sizeof(cplx) * (size_t)FftLds<LOGN>::n;
     lds_attr_once((const void*)k_fps_dct_div<LOGN>, (int)lds);
-    const dim3 grid(std::min(a0.cnt, 2 * device_cus()));
+    static const int fg = getenv("NSGPU_FPS_GRID") ? std::atoi(getenv("NSGPU_FPS_GRID")) : 0;
+    const dim3 grid(std::min(a0.cnt, fg > 0 ? fg : 2 * device_cus()));
     hipEvent_t a, b;
     if (take_launch_timing(a, b)) hipExtLaunchKernelGGL(k_fps_dct_div<LOGN>, grid, dim3(T), lds, st, a, b, 0, a0);
     else hipLaunchKernelGGL(k_fps_dct_div<LOGN>, grid, dim3(T), lds, st, a0);

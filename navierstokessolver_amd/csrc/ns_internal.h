@@ -19,6 +19,9 @@ constexpr int HALO = 7;  // ghost rows per side: K1's MUSCL stencil (2), the 2-s
 constexpr int FC_IN = 1 << 20;
 // (r5) the cell's neighbours up to 2 away along x and y (K1's MUSCL stencil) are all in the domain
 constexpr int FC_DEEP = 1 << 21;
+// (r6) FC_BAND: the cell lies within the wall-band width of a boundary face along its row or column (one rank;
+// the masked Helmholtz solve's wall bands)
+constexpr int FC_BAND = 1 << 22;
 constexpr int FC_INT = 31;
 constexpr int MAX_EDGES = 31;
 __host__ __device__ inline int fc_edge(int code, int k) { return (code >> (5 * k)) & 31; }
@@ -293,6 +296,16 @@ int launch_helm_rb_mask(const Geo& g, const Coef& c, double alpha, double omega,
                         double* x2, const double* b2, int par, double* part, hipStream_t st);
 // (r5) one whole red-black sweep of the same operator on u and v (rhs bu, bv) out of place, u, v -> uo, vo (LDS tiles;
 // the values of a red and a black launch of the above); one rank
+// (r6) nsw (1..4) whole red-black SOR sweeps of the masked Helmholtz operator on u, v in one launch (LDS temporal
+// blocking), u, v -> uo, vo; part: per-workgroup residuals of both fields after the last sweep (2 each; the
+// workgroup count is returned); one rank; < 0 when not applicable
+// tiles != null: the wall bands (FC_BAND cells only, 3 sweeps, one workgroup per (li0, j0) pair of `tiles`: the
+// MT_TI x MT_TJ tiles holding a band cell), band cells read from qbu / qbv, only they written
+constexpr int MT_TI = 32, MT_TJ = 64;
+int launch_helm_mt_mask(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                        const double* bu, const double* bv, double* uo, double* vo, int nsw, double* part,
+                        hipStream_t st, const double* qbu = nullptr, const double* qbv = nullptr,
+                        const int* tiles = nullptr, int ntiles = 0);
 void launch_helm_rbt_mask(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
                           const double* bu, const double* bv, double* uo, double* vo, hipStream_t st);
 // (stop: a KS_STOP slot -- the grid kernels then do nothing once it is set; null: always run)

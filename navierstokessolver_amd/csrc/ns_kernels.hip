@@ -3165,21 +3165,25 @@ constexpr int BAND_NSW = 3;   // sweeps per launch: a 6-cell cone, within the sl
 // (par + gi + j0) parity: uniform over the workgroup (every pair starts on an even column,
 // every segment on an even row), so there is no divergence.  One barrier per half-sweep: a
 // half-sweep reads only the other colour (stable) and publishes its own cells.
-__global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
-    constexpr int R = 2 * BAND_NSW, E = BT + 2 * R, NP = E / 2, SEG = BAND_SEG, NSEG = E / SEG;
-    static_assert(E % SEG == 0 && NP * NSEG <= 256, "band tile layout");
-    __shared__ double sp[E][E];
-    __shared__ double rw[E][3];   // per staged row: cw, ce, cw + ce + bx
-    __shared__ double cl[E][3];   // per staged column: cs, cn, cs + cn + by
+// (BTT tile, NSW sweeps, SEGT rows per thread, NTH threads; REGC: the row coefficients in
+// registers -- off for the 6-sweep tile, whose 512 threads must fit 128 VGPRs for 2 workgroups a CU)
+template <int BTT, int NSW, int SEGT, int NTH, bool REGC>
+__device__ __forceinline__ void helm_band_body(const BandArgs& a, double* smem) {
+    constexpr int R = 2 * NSW, E = BTT + 2 * R, NP = E / 2, SEG = SEGT, NSEG = E / SEG;
+    constexpr int CO = (E + 63) / 64 * 64;   // the column tables' loaders: threads CO .. CO + E - 1
+    static_assert(E % SEG == 0 && NP * NSEG <= NTH && CO + E <= NTH, "band tile layout");
+    double (*sp)[E] = reinterpret_cast<double (*)[E]>(smem);
+    double (*rw)[3] = reinterpret_cast<double (*)[3]>(smem + E * E);           // per staged row: cw, ce, cw + ce + bx
+    double (*cl)[3] = reinterpret_cast<double (*)[3]>(smem + E * E + 3 * E);   // per staged column: cs, cn, cs + cn + by
     int ti, tj;
     band_tile(blockIdx.x, a, ti, tj);
     const int f = blockIdx.y;
     const double* q = a.q[f];
     const double* qb = a.qb[f];
     const double* b = a.b[f];
-    const int li0 = ti * BT, j0 = tj * BT, ld = a.ld, ny = a.ny, nx = a.nx;
+    const int li0 = ti * BTT, j0 = tj * BTT, ld = a.ld, ny = a.ny, nx = a.nx;
     if (a.phase) {   // (workgroup-uniform) does the staged region reach a neighbour rank's rows?
-        const bool touch = (a.i0 > 0 && li0 - R < 0) || (a.i0 + a.nxl < nx && li0 + BT + R > a.nxl);
+        const bool touch = (a.i0 > 0 && li0 - R < 0) || (a.i0 + a.nxl < nx && li0 + BTT + R > a.nxl);
         if (touch != (a.phase == 2)) return;
     }
     const int rlo = -HALO, rhi = a.nxl + HALO - 1;
@@ -3211,8 +3215,8 @@ __global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
         const int gi = min(max(gib + t, 0), nx - 1);
         const double cw = a.cw[gi], ce = a.ce[gi];
         rw[t][0] = cw; rw[t][1] = ce; rw[t][2] = cw + ce + a.bx[gi];
-    } else if (t >= 64 && t < 64 + E) {
-        const int k = t - 64;
+    } else if (t >= CO && t < CO + E) {
+        const int k = t - CO;
         const int j = min(max(jb + k, 0), ny - 1);
         const double cs = a.cs[j], cn = a.cn[j];
         cl[k][0] = cs; cl[k][1] = cn; cl[k][2] = cs + cn + a.by[j];
@@ -3224,19 +3228,23 @@ __global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
     __syncthreads();
     const double alpha = a.alpha, omega = a.omega;
     // this thread's coefficients and relaxation weights (0 on held cells)
-    double2 w[SEG];
-    double rcw[SEG], rce[SEG], rd[SEG];
+    // (!REGC: the weights are formed at each update instead -- same expression, same value)
+    constexpr int NW = REGC ? SEG : 1;
+    double2 w[NW];
+    double rcw[NW], rce[NW], rd[NW];
     const double ccs0 = cl[c0][0], ccn0 = cl[c0][1], ccd0 = cl[c0][2];
     const double ccs1 = cl[c0 + 1][0], ccn1 = cl[c0 + 1][1], ccd1 = cl[c0 + 1][2];
+    if constexpr (REGC) {
 #pragma unroll
-    for (int s = 0; s < SEG; s++) {
-        const int r = r0 + s, gi = gib + r;
-        rcw[s] = rw[r][0]; rce[s] = rw[r][1]; rd[s] = rw[r][2];
-        w[s].x = (jin[0] && in_band(gi, jj[0], nx, ny, a.bw)) ? omega * rcp_nr(diag<1>(rd[s], ccd0, alpha)) : 0.0;
-        w[s].y = (jin[1] && in_band(gi, jj[1], nx, ny, a.bw)) ? omega * rcp_nr(diag<1>(rd[s], ccd1, alpha)) : 0.0;
+        for (int s = 0; s < NW; s++) {
+            const int r = r0 + s, gi = gib + r;
+            rcw[s] = rw[r][0]; rce[s] = rw[r][1]; rd[s] = rw[r][2];
+            w[s].x = (jin[0] && in_band(gi, jj[0], nx, ny, a.bw)) ? omega * rcp_nr(diag<1>(rd[s], ccd0, alpha)) : 0.0;
+            w[s].y = (jin[1] && in_band(gi, jj[1], nx, ny, a.bw)) ? omega * rcp_nr(diag<1>(rd[s], ccd1, alpha)) : 0.0;
+        }
     }
     const int cpar = (gib + jb) & 1;   // colour parity of staged (0, 0)
-    for (int h = 0; h < 2 * BAND_NSW; h++) {
+    for (int h = 0; h < 2 * NSW; h++) {
         const int par = h & 1;                   // red ((gi + j) even), black, ...
         const int lo = h + 1, hi = E - 2 - h;    // the half-sweep's region: [lo, hi]^2
         if (act) {
@@ -3251,15 +3259,25 @@ __global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
                 const double xm = s > 0 ? (e ? v[s - 1].y : v[s - 1].x) : sp[r - 1][cc];
                 const double xp = s < SEG - 1 ? (e ? v[s + 1].y : v[s + 1].x) : sp[r + 1][cc];
                 double rr;
+                const int sr = REGC ? s : 0;
+                const double cws = REGC ? rcw[sr] : rw[r][0], ces = REGC ? rce[sr] : rw[r][1];
+                const double rds = REGC ? rd[sr] : rw[r][2];
+                double wc;
+                if constexpr (REGC) {
+                    wc = e ? w[sr].y : w[sr].x;
+                } else {
+                    wc = ((e ? jin[1] : jin[0]) && in_band(gib + r, e ? jj[1] : jj[0], nx, ny, a.bw))
+                             ? omega * rcp_nr(diag<1>(rds, e ? ccd1 : ccd0, alpha)) : 0.0;
+                }
                 if (e == 0) {
                     const double ym = sp[r][cc - 1], yp = v[s].y;
-                    v[s].x = relax<1>(v[s].x, xm, xp, ym, yp, bq[s].x, rcw[s], rce[s], ccs0, ccn0,
-                                      diag<1>(rd[s], ccd0, alpha), w[s].x, alpha, rr);
+                    v[s].x = relax<1>(v[s].x, xm, xp, ym, yp, bq[s].x, cws, ces, ccs0, ccn0,
+                                      diag<1>(rds, ccd0, alpha), wc, alpha, rr);
                     sp[r][cc] = v[s].x;
                 } else {
                     const double ym = v[s].x, yp = sp[r][cc + 1];
-                    v[s].y = relax<1>(v[s].y, xm, xp, ym, yp, bq[s].y, rcw[s], rce[s], ccs1, ccn1,
-                                      diag<1>(rd[s], ccd1, alpha), w[s].y, alpha, rr);
+                    v[s].y = relax<1>(v[s].y, xm, xp, ym, yp, bq[s].y, cws, ces, ccs1, ccn1,
+                                      diag<1>(rds, ccd1, alpha), wc, alpha, rr);
                     sp[r][cc] = v[s].y;
                 }
             }
@@ -3271,24 +3289,41 @@ __global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
 #pragma unroll
         for (int s = 0; s < SEG; s++) {
             const int r = r0 + s, li = li0 + r - R;
-            if (r < R || r >= R + BT || li >= a.nxl) continue;
+            if (r < R || r >= R + BTT || li >= a.nxl) continue;
 #pragma unroll
             for (int e = 0; e < 2; e++) {
                 const int cc = c0 + e, j = jb + cc;
-                if (cc < R || cc >= R + BT || j >= ny || !in_band(a.i0 + li, j, nx, ny, a.bw)) continue;
+                if (cc < R || cc >= R + BTT || j >= ny || !in_band(a.i0 + li, j, nx, ny, a.bw)) continue;
                 out[(ptrdiff_t)li * ld + j] = e ? v[s].y : v[s].x;
             }
         }
     }
 }
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_helm_band(BandArgs a) {
+    constexpr int E = BT + 4 * BAND_NSW;
+    __shared__ double smem[E * E + 6 * E];
+    helm_band_body<BT, BAND_NSW, BAND_SEG, 256, true>(a, smem);
+}
+// (r6) one rank: all 6 sweeps in ONE launch -- 64 x 64 tiles and their 12-cell cone (88 x 88
+// staged, 66 KB of LDS: 2 workgroups a CU), the same (88/64)^2 read amplification as a 3-sweep
+// 32 x 32 launch, so half the band traffic; the band cells land in `out` (the scratch plane) and
+// k_band_copy brings them back.  Identical arithmetic (each band cell's value after 6 sweeps does
+// not depend on the tiling).
+constexpr int BAND6_BT = 64, BAND6_E = BAND6_BT + 24;
+constexpr int BAND6_LDS = (BAND6_E * BAND6_E + 6 * BAND6_E) * 8;
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_helm_band6(BandArgs a) {
+    extern __shared__ double smem6[];
+    helm_band_body<BAND6_BT, 6, 8, 512, false>(a, smem6);
+}
 
 // the band cells of each tile: qb -> out (an odd number of band launches ends in the scratch plane)
+template <int BTT>
 __global__ __launch_bounds__(256) void k_band_copy(BandArgs a) {
     int ti, tj;
     band_tile(blockIdx.x, a, ti, tj);
     const int f = blockIdx.y;
-    for (int t = threadIdx.x; t < BT * BT; t += 256) {
-        const int li = ti * BT + t / BT, j = tj * BT + t % BT;
+    for (int t = threadIdx.x; t < BTT * BTT; t += 256) {
+        const int li = ti * BTT + t / BTT, j = tj * BTT + t % BTT;
         if (li >= a.nxl || j >= a.ny || !in_band(a.i0 + li, j, a.nx, a.ny, a.bw)) continue;
         const ptrdiff_t o = (ptrdiff_t)li * a.ld + j;
         a.out[f][o] = a.qb[f][o];
@@ -4156,6 +4191,142 @@ __global__ __launch_bounds__(256) void k_helm_rbt_mask(Geo g, Coef c, double alp
     }
 }
 
+// (r6) NSW whole red-black SOR sweeps of k_helm_rb_mask's operator on u and v in ONE launch (temporal blocking,
+// k_helm_band's idea on the masked domain): a TI x 64 tile is staged with its R-cell cone (R = 2 NSW, + 1 with
+// the residual) -- u, v and the cell codes in LDS, the right-hand sides read from global memory (L2) -- each
+// half-sweep relaxes one colour over a region one ring smaller, so the tile's cells come out exactly as after NSW
+// global sweeps, in the same arithmetic order as k_helm_rb_mask / k_helm_rbt_mask (bit-identical fields).  RES:
+// the tile's residuals of both fields after the last sweep (k_helm_rb_mask par 2's expression) into part --
+// the batch's check without a pass of its own.  One rank (the cone reaches R > HALO rows past the tile).
+// Per NSW sweeps: u, v, code read ~(1 + 2R/TI)(1 + 2R/64) x 20 B + b 16 + write 16 -- against 52 B per sweep.
+template <int NSW>
+struct MtTile {
+    static constexpr int TI = MT_TI, TJ = MT_TJ, NTH = 1024;
+};
+// BAND (r6, the wall bands of a masked domain): only the cells flagged FC_BAND (within the band width of a
+// boundary face along a row or column) are relaxed, the rest held; one workgroup per tile of the list `tiles`;
+// band cells read from qbu / qbv, the others from u / v, and only band cells written (k_helm_band's scheme: two
+// launches U -> TU, then (U, TU) -> U, no tile writes what another reads, no copy-back)
+template <int NSW, bool RES, bool BAND>
+__global__ __launch_bounds__(1024) void k_helm_mt_mask(Geo g, Coef c, double alpha, double omega,
+                                                       const double* __restrict__ u, const double* __restrict__ v,
+                                                       const double* __restrict__ qbu, const double* __restrict__ qbv,
+                                                       const double* __restrict__ bu, const double* __restrict__ bv,
+                                                       double* __restrict__ uo, double* __restrict__ vo,
+                                                       double* __restrict__ part, const int2* __restrict__ tiles) {
+    constexpr int TI = MtTile<NSW>::TI, TJ = MtTile<NSW>::TJ, NTH = MtTile<NSW>::NTH;
+    constexpr int R = 2 * NSW + (RES ? 1 : 0), EI = TI + 2 * R, EJ = TJ + 2 * R, NE = EI * EJ;
+    // LDS: u, v, the cell's diagonal weight sum wc and omega / (1 + alpha wc) (formed once per staged cell, not
+    // once per relaxation), the codes, and per row hx, pw, pe, 1 / hx^2, per column hy, ps, pn, 1 / hy^2
+    extern __shared__ double smt[];
+    double* su = smt;
+    double* sv = smt + NE;
+    double* swc = smt + 2 * NE;
+    double* sdi = smt + 3 * NE;
+    double* trow = smt + 4 * NE;            // [4][EI]
+    double* tcol = trow + 4 * EI;           // [4][EJ]
+    int* sc = reinterpret_cast<int*>(tcol + 4 * EJ);
+    int li0 = blockIdx.y * TI, j0 = blockIdx.x * TJ;
+    if (BAND) {
+        const int2 t = tiles[blockIdx.x];
+        li0 = t.x;
+        j0 = t.y;
+    }
+    const int ld = g.ld;
+    const int tid = threadIdx.x;
+    // the cells this launch relaxes
+    auto live = [](int code) { return (code & FC_IN) && (!BAND || (code & FC_BAND)); };
+    for (int q = tid; q < NE; q += NTH) {
+        const int r = q / EJ, cc = q - r * EJ;
+        const int li = li0 - R + r, j = j0 - R + cc;
+        const bool in = li >= 0 && li < g.nxl && j >= 0 && j < g.ny;
+        const ptrdiff_t o = (ptrdiff_t)min(max(li, -HALO), g.nxl + HALO - 1) * ld + min(max(j, 0), g.ny - 1);
+        const int code = in ? g.fc[o] : 0;   // (one rank: cells off the slab are off the box)
+        const bool fb = BAND && (code & FC_BAND);
+        su[q] = (fb ? qbu : u)[o];
+        sv[q] = (fb ? qbv : v)[o];
+        sc[q] = code;
+    }
+    if (tid < EI) {
+        const int gi = min(max(g.i0 + li0 - R + tid, 0), g.nx - 1);
+        const double hx = c.hx[gi];
+        trow[tid] = hx; trow[EI + tid] = c.pw[gi]; trow[2 * EI + tid] = c.pe[gi]; trow[3 * EI + tid] = 1.0 / (hx * hx);
+    } else if (tid >= 128 && tid < 128 + EJ) {
+        const int k = tid - 128, j = min(max(j0 - R + k, 0), g.ny - 1);
+        const double hy = c.hy[j];
+        tcol[k] = hy; tcol[EJ + k] = c.ps[j]; tcol[2 * EJ + k] = c.pn[j]; tcol[3 * EJ + k] = 1.0 / (hy * hy);
+    }
+    __syncthreads();
+    // k_helm_rb_mask's weights in its order: the off-diagonal of face k is its coefficient when the face is
+    // interior, else 0 (a wall's 2 / h^2 goes to the diagonal unless NEUMANN)
+    auto pn_of = [&](int k, int r, int cc) {
+        return k == 0 ? trow[EI + r] : k == 1 ? trow[2 * EI + r] : k == 2 ? tcol[EJ + cc] : tcol[2 * EJ + cc];
+    };
+    for (int q = tid; q < NE; q += NTH) {
+        const int code = sc[q];
+        if (!live(code)) continue;
+        const int r = q / EJ, cc = q - r * EJ;
+        const double w2[4] = {trow[3 * EI + r], trow[3 * EI + r], tcol[3 * EJ + cc], tcol[3 * EJ + cc]};
+        double wc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (fc_edge(code, k) == FC_INT) wc += pn_of(k, r, cc);
+            else if (!g.et[fc_edge(code, k)].neu) wc += 2.0 * w2[k];
+        }
+        swc[q] = wc;
+        sdi[q] = omega / (1.0 + alpha * wc);
+    }
+    __syncthreads();
+    // the residual b - (I - alpha L_V) x at staged cell x (row r, column cc)
+    auto resid = [&](const double* sx, int x, int code, int r, int cc, double b) {
+        const double xc = sx[x];
+        double s = -swc[x] * xc;
+        const int nb[4] = {x - EJ, x + EJ, x - 1, x + 1};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (fc_edge(code, k) == FC_INT) s = fma(pn_of(k, r, cc), sx[nb[k]], s);
+        return b - (xc - alpha * s);
+    };
+    const int base = (g.i0 + li0 - R + j0 - R) & 1;   // colour of staged (0, 0)
+    for (int h = 0; h < 2 * NSW; h++) {
+        const int par = h & 1, lo = h + 1, hr = EI - 2 - h, hc = EJ - 2 - h;
+        const int npr = (hc - lo) / 2 + 1, cnt = (hr - lo + 1) * npr;
+        for (int q = tid; q < cnt; q += NTH) {
+            const int rq = q / npr, k = q - rq * npr, r = lo + rq;
+            const int cc = lo + ((par + base + r + lo) & 1) + 2 * k;
+            if (cc > hc) continue;
+            const int x = r * EJ + cc, code = sc[x];
+            if (!live(code)) continue;
+            const ptrdiff_t o = (ptrdiff_t)(li0 - R + r) * ld + (j0 - R + cc);
+            const double di = sdi[x], xu = su[x], xv = sv[x];
+            const double ru = resid(su, x, code, r, cc, bu[o]), rv = resid(sv, x, code, r, cc, bv[o]);
+            su[x] = fma(di, ru, xu);
+            sv[x] = fma(di, rv, xv);
+        }
+        __syncthreads();
+    }
+    double acc[2] = {0.0, 0.0};
+    for (int q = tid; q < TI * TJ; q += NTH) {
+        const int r = q / TJ, cc = q - r * TJ, li = li0 + r, j = j0 + cc;
+        if (li >= g.nxl || j >= g.ny) continue;
+        const int x = (r + R) * EJ + cc + R;
+        const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+        if (BAND && !live(sc[x])) continue;
+        uo[o] = su[x];
+        vo[o] = sv[x];
+        if (RES) {
+            const int code = sc[x];
+            if (code & FC_IN) {
+                const double ru = resid(su, x, code, r + R, cc + R, bu[o]);
+                const double rv = resid(sv, x, code, r + R, cc + R, bv[o]);
+                acc[0] += ru * ru;
+                acc[1] += rv * rv;
+            }
+        }
+    }
+    if (RES) block_reduce_sum<2>(acc, part + 2 * (blockIdx.x + gridDim.x * blockIdx.y));
+}
+
 // z = q / diag(A) (the Jacobi preconditioner of the masked-domain Krylov solves; the
 // outflow rows' diagonal -(sum p) + 1.5 w, oracle diag_poisson / diag_helmholtz)
 template <int OP, class T>
@@ -4439,7 +4610,10 @@ int launch_rhs(const Geo& g, const Coef& c, double dt, double re, const double* 
             // the fewest rows that keep every strip in ONE resident round (strip_rows caps at 64:
             // 4096^2 at 2 waves / SIMD then left 128 of 2176 strips to a second round)
             const long nsi = std::max(1L, resident_waves(kk) / A.nsj);
-            const int L = std::min(std::max((int)((g.nxl + nsi - 1) / nsi + 1) & ~1, 8), K1_LMAX);
+            int L = std::min(std::max((int)((g.nxl + nsi - 1) / nsi + 1) & ~1, 8), K1_LMAX);
+            // (r6, A/B) NSGPU_K1_L: rows per strip (several resident rounds of shorter strips)
+            static const int k1l = getenv("NSGPU_K1_L") ? std::atoi(getenv("NSGPU_K1_L")) : 0;
+            if (k1l >= 4) L = std::min(k1l & ~1, K1_LMAX);
             A.nstr = A.nsj * plan_rows(g.nxl, L, depth, &A.P, K1_ESPLIT);   // u, v rows ib-2 .. ie+1
         }
         const bool inner = A.jhi > 2 && A.ihi > A.ilo;
@@ -4565,6 +4739,46 @@ void launch_helm_rbt_mask(const Geo& g, const Coef& c, double alpha, double omeg
                           const double* bu, const double* bv, double* uo, double* vo, hipStream_t st) {
     NS_LAUNCH(k_helm_rbt_mask, dim3((g.ny + 63) / 64, (g.nxl + RTM - 1) / RTM), dim3(64, 4), 0, st, g, c, alpha, omega,
               u, v, bu, bv, uo, vo);
+}
+// (r6) nsw (1..4) whole sweeps in one launch (k_helm_mt_mask), u, v -> uo, vo; part != null: the residuals of
+// both fields after the last sweep, per workgroup (2 per workgroup); returns the workgroups (< 0: no such build)
+template <int NSW, bool RES, bool BAND>
+static int mt_launch(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                     const double* qbu, const double* qbv, const double* bu, const double* bv, double* uo, double* vo,
+                     double* part, const int2* tiles, int ntiles, hipStream_t st) {
+    constexpr int TI = MtTile<NSW>::TI, TJ = MtTile<NSW>::TJ, R = 2 * NSW + (RES ? 1 : 0);
+    constexpr int EI = TI + 2 * R, EJ = TJ + 2 * R;
+    constexpr int lds = (4 * EI * EJ + 4 * (EI + EJ)) * 8 + EI * EJ * 4;
+    static_assert(EI <= 128 && EJ <= 128 && lds <= 160 * 1024, "table loaders / LDS");
+    lds_attr_once((const void*)k_helm_mt_mask<NSW, RES, BAND>, lds);
+    const dim3 grid = BAND ? dim3(ntiles) : dim3((g.ny + TJ - 1) / TJ, (g.nxl + TI - 1) / TI);
+    if (grid.x * grid.y == 0) return 0;
+    NS_LAUNCH((k_helm_mt_mask<NSW, RES, BAND>), grid, dim3(MtTile<NSW>::NTH), lds, st, g, c, alpha, omega, u, v, qbu,
+              qbv, bu, bv, uo, vo, part, tiles);
+    return (int)(grid.x * grid.y);
+}
+int launch_helm_mt_mask(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
+                        const double* bu, const double* bv, double* uo, double* vo, int nsw, double* part,
+                        hipStream_t st, const double* qbu, const double* qbv, const int* tiles, int ntiles) {
+    if (!g.fc || g.nxl != g.nx) return -1;
+    const int2* tl = reinterpret_cast<const int2*>(tiles);
+    if (tiles) {   // the wall bands: 3 sweeps per launch, no residual
+        if (nsw != 3 || part) return -1;
+        return mt_launch<3, false, true>(g, c, alpha, omega, u, v, qbu, qbv, bu, bv, uo, vo, nullptr, tl, ntiles, st);
+    }
+    switch (nsw * 2 + (part ? 1 : 0)) {
+#define NS_MT(K, RS) return mt_launch<K, RS, false>(g, c, alpha, omega, u, v, u, v, bu, bv, uo, vo, part, nullptr, 0, st)
+        case 2: NS_MT(1, false);
+        case 3: NS_MT(1, true);
+        case 4: NS_MT(2, false);
+        case 5: NS_MT(2, true);
+        case 6: NS_MT(3, false);
+        case 7: NS_MT(3, true);
+        case 8: NS_MT(4, false);
+        case 9: NS_MT(4, true);
+#undef NS_MT
+        default: return -1;
+    }
 }
 void launch_diag_pc(int op, const Geo& g, const Coef& c, double alpha, const double* q, double* z, hipStream_t st,
                     const double* stop) {
@@ -4950,9 +5164,13 @@ int launch_pois_rbsor2(const Geo& g, const Coef& c, double omega, const double* 
 // one launch of the Helmholtz wall-band relaxation (k_helm_band: 3 RB-SOR sweeps of u and v on
 // the cells within bw of a wall), band cells read from qu / qv (the rest from u / v), written to
 // ou / ov; copy != 0: the band cells qu / qv -> ou / ov instead (k_band_copy).  Returns the tiles.
+// copy 2: the 6-sweep one-launch tile (k_helm_band6, one rank: its cone is 12 rows); copy 3: the
+// copy-back with that launch's tiles (k_band_copy<64>)
 int launch_helm_band(const Geo& g, const Coef& c, double alpha, double omega, const double* u, const double* v,
                      const double* qu, const double* qv, double* ou, double* ov, const double* ru, const double* rv,
                      int bw, int copy, hipStream_t st) {
+    const int BT = copy >= 2 ? BAND6_BT : nsg::BT;
+    if (copy >= 2 && (g.nxl != g.nx || g_phase)) return -1;
     BandArgs a{};
     a.q[0] = u; a.q[1] = v; a.qb[0] = qu; a.qb[1] = qv; a.out[0] = ou; a.out[1] = ov; a.b[0] = ru; a.b[1] = rv;
     a.cw = c.pw; a.ce = c.pe; a.bx = c.bx; a.cs = c.ps; a.cn = c.pn; a.by = c.by;
@@ -4975,8 +5193,16 @@ int launch_helm_band(const Geo& g, const Coef& c, double alpha, double omega, co
     a.ncr = std::max((g.ny - bw) / BT, a.ncl);
     const int n = (a.fa + a.nti - a.fb) * a.ntj + (a.fb - a.fa) * (a.ncl + a.ntj - a.ncr);
     if (n <= 0) return 0;
-    if (copy) NS_LAUNCH(k_band_copy, dim3(n, 2), dim3(256), 0, st, a);
-    else NS_LAUNCH(k_helm_band, dim3(n, 2), dim3(256), 0, st, a);
+    if (copy == 2) {
+        lds_attr_once((const void*)k_helm_band6, BAND6_LDS);
+        NS_LAUNCH(k_helm_band6, dim3(n, 2), dim3(512), BAND6_LDS, st, a);
+    } else if (copy == 3) {
+        NS_LAUNCH(k_band_copy<BAND6_BT>, dim3(n, 2), dim3(256), 0, st, a);
+    } else if (copy) {
+        NS_LAUNCH(k_band_copy<nsg::BT>, dim3(n, 2), dim3(256), 0, st, a);
+    } else {
+        NS_LAUNCH(k_helm_band, dim3(n, 2), dim3(256), 0, st, a);
+    }
     return n;
 }
 

@@ -146,6 +146,7 @@ struct ns_solver {
     bool triple = true;          // 3-sweep passes allowed on this decomposition (slabs >= 2*HALO rows)
     bool sweep3 = true;          // single rank: odd Helmholtz batches start with a 3-sweep pass (k_sweep3)
     bool helm_band = true;       // Helmholtz: wall-band relaxation before the global passes (k_helm_band)
+    bool band6 = true;           // (r6) one rank, 6 band sweeps: one k_helm_band6 launch + copy-back (NSGPU_BAND6=0: 2 x 3)
     int band_w = 128, band_sweeps = 6;   // its width (cells from a wall: min(nx, ny) / 32) and RB-SOR sweeps (a multiple of 3)
     bool sweep3_res = true;      // one rank: a Helmholtz batch may end on a 3-sweep pass with its residual
     int helm_uv = 1;             // NSGPU_HELM_UV=0: one rank's 3-sweep batch as two one-field launches (A/B)
@@ -242,6 +243,8 @@ struct ns_solver {
     double area = 0.0;           // sum of the domain's cell areas
     double inv_area = 0.0;       // sum of their reciprocals
     int32_t* fc_mem = nullptr;   // masked domain: topology plane (g.fc) and edge table (g.et)
+    int32_t* mband_tiles = nullptr;   // (r6) masked, one rank: the (li0, j0) of the mt tiles holding a wall-band cell
+    int mband_n = 0;
     int32_t* ecell_mem = nullptr;   // (r5) masked domain: the slab's domain cells that are not FC_DEEP (g.ecell)
     nsg::EdgeDev* et_mem = nullptr;
     ns_host_transport ht{};      // host transport (ht.exchange != NULL) instead of RCCL
@@ -328,6 +331,8 @@ struct ns_solver {
     // (r5) a masked domain's Helmholtz solve on one rank by red-black SOR (NSGPU_MASK_HELM=krylov: BiCGStab); the
     // sweeps the last step needed (the next step's first batch)
     bool mask_rb = true, mask_rbt = true;
+    bool mask_mt = true;   // (r6) masked Helmholtz: up to 4 sweeps per launch + the residual in the last (NSGPU_MASK_MT=0: rbt)
+    int mask_band = 6;     // (r6) masked Helmholtz: wall-band sweeps before the global ones (NSGPU_MASK_BAND; 0 off, multiple of 6)
     int mask_helm_next = 4, mask_helm_ok = 0;
     // r5, multi-rank rectangles: the Helmholtz check's collective is an allgather of every rank's
     // S_HBNL .. S_MML (bus()): K1's norms and the previous step's K5 min / max ride on it, so neither
@@ -924,6 +929,24 @@ int helm_band(ns_solver* s, double alpha) {
     }
     const bool tb = s->timing && s->in_step && s->nranks == 1;   // (r6: the bench's band line)
     if (tb) CHK(ensure_kev(s));
+    if (s->band6 && s->nranks == 1 && rounds == 2) {
+        // (r6) one rank, 6 sweeps: ONE launch of 64 x 64 tiles with their 12-cell cone (k_helm_band6) into the
+        // scratch planes, then the band cells' copy-back -- 80 B per band cell instead of 2 x 48 (one timed
+        // interval: the bench's band line is the pair)
+        if (tb) CHK(t_begin(s, s->kev[8], s->kev[9]));
+        const int n = nsg::launch_helm_band(s->g, s->c, alpha, s->omega_v, U, V, U, V, TU, TV, s->arr[NS_ARR_RU],
+                                            s->arr[NS_ARR_RV], s->band_w, 2, s->st);
+        if (n >= 0) {
+            nsg::launch_helm_band(s->g, s->c, alpha, s->omega_v, U, V, TU, TV, U, V, s->arr[NS_ARR_RU],
+                                  s->arr[NS_ARR_RV], s->band_w, 3, s->st);
+            if (tb) {
+                CHK(t_end(s, s->kev[8], s->kev[9]));
+                s->band_timed = 1;
+            }
+            return 0;
+        }
+        if (tb) CHK(t_end(s, s->kev[8], s->kev[9]));   // (unsupported here: the launches of 3 below)
+    }
     for (int k = 0; k < rounds; k++) {
         const bool odd = k & 1;
         auto launch = [&]() {
@@ -968,6 +991,20 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
         double bu = 0.0, bv = 0.0;
         int sweeps = 0, batch = std::max(1, s->mask_helm_next);
         double r2u = 0.0, r2v = 0.0;
+        if (s->mask_mt && s->mask_band > 0 && s->mband_n > 0) {
+            // (r6) the wall bands first (the residual of the guess u^n lives there, as on the rectangle): launches
+            // of 3 sweeps on the FC_BAND cells, U -> TU, then (U, TU) -> U (an even count: the band ends in U)
+            const double *RU = s->arr[NS_ARR_RU], *RV = s->arr[NS_ARR_RV];
+            const int nl = s->mask_band / 3;
+            for (int l = 0; l < nl; l++) {
+                double *U = s->arr[NS_ARR_U], *V = s->arr[NS_ARR_V], *TU = s->arr[NS_ARR_TMPU], *TV = s->arr[NS_ARR_TMPV];
+                const bool odd = l & 1;
+                const int rc = nsg::launch_helm_mt_mask(s->g, s->c, alpha, s->omega_v, U, V, RU, RV, odd ? U : TU,
+                                                        odd ? V : TV, 3, nullptr, s->st, odd ? TU : U, odd ? TV : V,
+                                                        s->mband_tiles, s->mband_n);
+                if (rc < 0) { set_err("masked wall-band launch failed"); return NS_EINVAL; }
+            }
+        }
         for (;;) {
             const int n = std::min(batch, s->max_iters - sweeps);
             // (u and v in the same launches: the topology decoded once -- 4 -> 2 launches per sweep)
@@ -976,6 +1013,36 @@ int helm_solve(ns_solver* s, int* its, double* resu, double* resv) {
             // (r5) whole sweeps in LDS tiles, U, V -> TU, TV -> U, V (an odd batch: its first sweep as the two
             // in-place half-sweeps); NSGPU_MASK_RBT=0: half-sweeps only (A/B)
             double *TU = s->arr[NS_ARR_TMPU], *TV = s->arr[NS_ARR_TMPV];
+            if (s->mask_mt) {
+                // (r6) up to 4 sweeps per launch (k_helm_mt_mask: LDS temporal blocking), U, V <-> TU, TV, the
+                // batch's last launch with the residuals of both fields -- no pass of its own
+                const int nl = (n + 3) / 4;
+                int left = n, nb = -1;
+                bool in_t = false;
+                for (int l = 0; l < nl; l++) {
+                    const int k = (left + (nl - l) - 1) / (nl - l);
+                    nb = nsg::launch_helm_mt_mask(s->g, s->c, alpha, s->omega_v, in_t ? TU : U, in_t ? TV : V, RU, RV,
+                                                  in_t ? U : TU, in_t ? V : TV, k, left == k ? s->part : nullptr, s->st);
+                    if (nb < 0) { set_err("masked Helmholtz tile launch failed"); return NS_EINVAL; }
+                    in_t = !in_t;
+                    left -= k;
+                }
+                if (in_t) {
+                    std::swap(s->arr[NS_ARR_U], s->arr[NS_ARR_TMPU]);
+                    std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
+                }
+                sweeps += n;
+                nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_RES, s->st);
+                CHK(fetch(s));
+                bu = s->hs[S_HBN];
+                bv = s->hs[S_HBN + 1];
+                r2u = s->hs[S_RES];
+                r2v = s->hs[S_RES + 1];
+                if (!std::isfinite(r2u) || !std::isfinite(r2v)) { set_err("Helmholtz residual is not finite"); return NS_EDIVERGE; }
+                if ((r2u <= tol2 * bu && r2v <= tol2 * bv) || sweeps >= s->max_iters) break;
+                batch = 2;
+                continue;
+            }
             for (int k = 0; k < n; k++) {
                 if (s->mask_rbt && (n - k) % 2 == 0) {
                     nsg::launch_helm_rbt_mask(s->g, s->c, alpha, s->omega_v, U, V, RU, RV, TU, TV, s->st);
@@ -3584,6 +3651,56 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         }
     }
 
+    // (r6) the masked domain's wall bands (one rank): FC_BAND on the cells within mbw of a boundary face along
+    // their row or column (on a rectangle exactly the box bands of helm_band), and the mt kernel's tiles holding one
+    std::vector<int32_t> mband;
+    if (masked && g.nxl == gd->nx) {
+        const int nx = gd->nx, ny = gd->ny, ldh = g.ld;
+        const int mbw = std::min(nx, ny) > 4096 ? 3 * std::min(nx, ny) / 64 : std::max(32, std::min(nx, ny) / 32);
+        auto code_at = [&](int i, int j) -> int32_t& { return fch[(size_t)(i + nsg::HALO) * ldh + j]; };
+        auto bnd = [&](int i, int j) {   // a domain cell with a face that is not interior
+            const int32_t c = code_at(i, j);
+            if (!(c & nsg::FC_IN)) return false;
+            for (int k = 0; k < 4; k++)
+                if (nsg::fc_edge(c, k) != nsg::FC_INT) return true;
+            return false;
+        };
+        const int BIG = 1 << 29;
+        std::vector<int> dr((size_t)nx * ny, BIG);   // distance along the row / column to a boundary cell
+        for (int i = 0; i < nx; i++) {
+            int last = -BIG;
+            for (int j = 0; j < ny; j++) { if (bnd(i, j)) last = j; dr[(size_t)i * ny + j] = j - last; }
+            last = BIG;
+            for (int j = ny - 1; j >= 0; j--) {
+                if (bnd(i, j)) last = j;
+                dr[(size_t)i * ny + j] = std::min(dr[(size_t)i * ny + j], last - j);
+            }
+        }
+        for (int j = 0; j < ny; j++) {
+            int last = -BIG;
+            for (int i = 0; i < nx; i++) {
+                if (bnd(i, j)) last = i;
+                dr[(size_t)i * ny + j] = std::min(dr[(size_t)i * ny + j], i - last);
+            }
+            last = BIG;
+            for (int i = nx - 1; i >= 0; i--) {
+                if (bnd(i, j)) last = i;
+                dr[(size_t)i * ny + j] = std::min(dr[(size_t)i * ny + j], last - i);
+            }
+        }
+        const int nti = (nx + nsg::MT_TI - 1) / nsg::MT_TI, ntj = (ny + nsg::MT_TJ - 1) / nsg::MT_TJ;
+        std::vector<char> tb((size_t)nti * ntj, 0);
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < ny; j++)
+                if ((code_at(i, j) & nsg::FC_IN) && dr[(size_t)i * ny + j] < mbw) {
+                    code_at(i, j) |= nsg::FC_BAND;
+                    tb[(size_t)(i / nsg::MT_TI) * ntj + j / nsg::MT_TJ] = 1;
+                }
+        for (int a = 0; a < nti; a++)
+            for (int b = 0; b < ntj; b++)
+                if (tb[(size_t)a * ntj + b]) { mband.push_back(a * nsg::MT_TI); mband.push_back(b * nsg::MT_TJ); }
+    }
+
     ns_solver* s = new ns_solver();
     s->g = g;
     if (masked) {
@@ -3653,6 +3770,7 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     }
     if (const char* e = getenv("NSGPU_BAND_W")) s->band_w = std::max(1, std::atoi(e));   // A/B: band width
     if (const char* e = getenv("NSGPU_BAND_SWEEPS")) s->band_sweeps = std::max(3, std::atoi(e) / 3 * 3);
+    if (const char* e = getenv("NSGPU_BAND6")) s->band6 = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_SWEEP3_RES")) s->sweep3_res = std::atoi(e) != 0;   // A/B: batches end on pairs
     if (const char* e = getenv("NSGPU_HELM_UV")) s->helm_uv = std::atoi(e);
     // the 3-sweep pass reads HALO ghost rows, which one neighbour feeds only from slabs of
@@ -3676,6 +3794,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     if (const char* e = getenv("NSGPU_VERBOSE")) s->verbose = std::atoi(e) != 0;
     if (const char* e = getenv("NSGPU_MASK_HELM")) s->mask_rb = std::strcmp(e, "krylov") != 0;
     if (const char* e = getenv("NSGPU_MASK_RBT")) s->mask_rbt = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_MASK_MT")) s->mask_mt = std::atoi(e) != 0;
+    if (const char* e = getenv("NSGPU_MASK_BAND")) s->mask_band = std::max(0, std::atoi(e) / 6 * 6);
     if (const char* e = getenv("NSGPU_PAIR_MIN_CELLS")) s->pair_min_cells = std::atol(e);
     if (const char* e = getenv("NSGPU_DIRECT_CELLS")) s->direct_cells = std::max(0L, std::atol(e));
     {
@@ -3885,6 +4005,11 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
             hipMemcpy(s->et_mem, etab.data(), etab.size() * sizeof(nsg::EdgeDev), hipMemcpyHostToDevice) != hipSuccess) { set_err("topology upload failed"); return fail(NS_EHIP); }
         s->g.fc = s->fc_mem + (size_t)nsg::HALO * g.ld;
         s->g.et = s->et_mem;
+        if (!mband.empty()) {
+            if (hipMalloc(&s->mband_tiles, mband.size() * sizeof(int32_t)) != hipSuccess) { set_err("hipMalloc topology failed"); return fail(NS_ENOMEM); }
+            if (hipMemcpy(s->mband_tiles, mband.data(), mband.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) { set_err("topology upload failed"); return fail(NS_EHIP); }
+            s->mband_n = (int)(mband.size() / 2);
+        }
         std::vector<int32_t> ec;
         for (int li = 0; li < g.nxl; li++)
             for (int j = 0; j < g.ny; j++) {
@@ -4055,6 +4180,7 @@ void ns_destroy(ns_solver* s) {
         if (e) (void)hipEventDestroy(e);
     if (s->f32_mem) (void)hipFree(s->f32_mem);
     if (s->fc_mem) (void)hipFree(s->fc_mem);
+    if (s->mband_tiles) (void)hipFree(s->mband_tiles);
     if (s->ecell_mem) (void)hipFree(s->ecell_mem);
     if (s->et_mem) (void)hipFree(s->et_mem);
     if (s->ksc) (void)hipFree(s->ksc);

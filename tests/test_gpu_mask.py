@@ -222,16 +222,46 @@ def test_mask_helmholtz_tiled_sweeps_bit_identical(gpu, monkeypatch, name):
     """(r5) The masked Helmholtz solve's whole red-black sweeps in LDS tiles (k_helm_rbt_mask, u, v -> TMPU, TMPV and
     back) against the two in-place half-sweep launches per sweep (NSGPU_MASK_RBT=0): the same arithmetic on the same
     old values, so every field after 6 full steps is bit-identical, and so are the sweep counts.  (r6) lshape_big /
-    step_big: ny >= 128, the tiles' 64-column boundaries and their 2-cell ring inside the checked region."""
+    step_big: ny >= 128, the tiles' 64-column boundaries and their 2-cell ring inside the checked region.  (r6) And
+    the default, up to 4 whole sweeps per launch with the batch's residual in its last launch (k_helm_mt_mask, LDS
+    temporal blocking with a 2 NSW (+1)-cell cone): the same fields bit for bit (NSGPU_MASK_MT=0: the two above;
+    the wall bands off, NSGPU_MASK_BAND=0, since they change the global sweeps' start)."""
     P = POLY[name]
     n = max(P["xspec"][-1][2], P["yspec"][-1][2])
     out = {}
-    for rbt in ("1", "0"):
+    monkeypatch.setenv("NSGPU_MASK_BAND", "0")
+    for mt, rbt in (("1", "1"), ("0", "1"), ("0", "0")):
+        monkeypatch.setenv("NSGPU_MASK_MT", mt)
         monkeypatch.setenv("NSGPU_MASK_RBT", rbt)
         og, gs, m = pair(gpu, name, 1.0 / (16 * n), 200.0, rtol=1e-10)
         st = [gs.step() for _ in range(6)]
-        out[rbt] = ([x["it_u"] for x in st], [a.copy() for a in gs.fields()])
+        out[mt + rbt] = ([x["it_u"] for x in st], [a.copy() for a in gs.fields()])
         gs.close()
-    assert out["1"][0] == out["0"][0]
-    for a, b in zip(out["1"][1], out["0"][1]):
-        np.testing.assert_array_equal(a, b)
+    for k in ("11", "01"):
+        assert out[k][0] == out["00"][0], (k, out[k][0], out["00"][0])
+        for a, b in zip(out[k][1], out["00"][1]):
+            np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["lshape_big", "step_big", "uchannel"])
+def test_mask_wall_bands(gpu, monkeypatch, name):
+    """(r6) The masked Helmholtz solve's wall bands (FC_BAND: the cells within the band width of a boundary face
+    along their row or column; 6 RB-SOR sweeps on them in two k_helm_mt_mask<3, BAND> launches before the global
+    sweeps, the rest held): the solve converges to the same solution -- every step's velocity within the
+    solves' rtol (1e-10 here) of the run without bands -- in no more global sweeps."""
+    P = POLY[name]
+    n = max(P["xspec"][-1][2], P["yspec"][-1][2])
+    out = {}
+    for band in ("6", "0"):
+        monkeypatch.setenv("NSGPU_MASK_BAND", band)
+        og, gs, m = pair(gpu, name, 1.0 / (16 * n), 200.0, rtol=1e-10)
+        st = [gs.step() for _ in range(6)]
+        out[band] = ([x["it_u"] for x in st], [a.copy() for a in gs.fields()], st)
+        gs.close()
+    assert sum(out["6"][0]) <= sum(out["0"][0]), (out["6"][0], out["0"][0])
+    for a, b in zip(out["6"][2], out["0"][2]):
+        np.testing.assert_allclose([a[k] for k in ("umin", "umax", "vmin", "vmax")],
+                                   [b[k] for k in ("umin", "umax", "vmin", "vmax")], atol=1e-9)
+    u6, v6 = out["6"][1][0], out["6"][1][1]
+    u0, v0 = out["0"][1][0], out["0"][1][1]
+    assert float(np.max(np.abs(u6 - u0))) <= 1e-8 and float(np.max(np.abs(v6 - v0))) <= 1e-8

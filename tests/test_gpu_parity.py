@@ -709,6 +709,28 @@ def test_deferred_correction_is_bit_identical(gpu, monkeypatch, n):
     assert all(x["k5_deferred"] == 0 for x in sb)
 
 
+@pytest.mark.parametrize("nx,ny", [(96, 96), (200, 136), (512, 512), (130, 1000)])
+def test_band6_is_bit_identical(gpu, monkeypatch, nx, ny):
+    """(r6) one rank's 6 wall-band sweeps in ONE launch (k_helm_band6: 64 x 64 tiles, their 12-cell cone staged in
+    LDS, the band cells copied back) against two launches of 3 sweeps on 32 x 32 tiles (NSGPU_BAND6=0): a band
+    cell's value after 6 RB-SOR sweeps does not depend on the tiling, so the monitors, sweep counts and fields
+    agree bit for bit -- grids that are no multiple of 64, bands wider than half a tile row."""
+    dt, re = 1.0 / (8 * max(nx, ny)), 400.0
+    out = {}
+    for d in ("1", "0"):
+        monkeypatch.setenv("NSGPU_BAND6", d)
+        gs = gpu.GpuSolver(gpu.rectangle(nx, ny), dt, re)
+        st = [gs.step() for _ in range(5)]
+        out[d] = (st, [a.copy() for a in gs.fields()])
+        gs.close()
+    (sa, fa), (sb, fb) = out["1"], out["0"]
+    key = ("umin", "umax", "vmin", "vmax", "it_u", "it_phi")
+    for x, y in zip(sa, sb):
+        assert all(x[k] == y[k] for k in key), (x, y)
+    for x, y in zip(fa, fb):
+        assert np.array_equal(x, y)
+
+
 def test_known_answer_trace_128_async(gpu):
     """The reference's printed 128^2 monitor through ns_step_async (one step late)."""
     n = 128

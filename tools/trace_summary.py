@@ -1,13 +1,16 @@
 """Per-kernel, per-grid-size time from a rocprofv3 kernel trace (csv).
 python tools/trace_summary.py <kernel_trace.csv> [steps] [first-kernel]
 first-kernel: count only from the first launch whose name contains it (e.g. k_rhs: the first time
-step), so one-time set-up work -- RCCL's communicator init (~260 copies and ~520 fills,
+step; k_rhs@5: the sixth, after 5 warm-up steps), so one-time set-up work -- RCCL's communicator init (~260 copies and ~520 fills,
 tools/rccl_loopback_probe.cpp), solver creation -- is not divided over the steps."""
 import csv, sys, collections
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
 if len(sys.argv) > 3:
-    k0 = next((i for i, r in enumerate(rows) if sys.argv[3] in r["Kernel_Name"]), 0)
+    # name@K: from the K-th (0-based) launch whose name contains `name` (skip K warm-up steps)
+    key, _, nth = sys.argv[3].partition("@")
+    hits = [i for i, r in enumerate(rows) if key in r["Kernel_Name"]]
+    k0 = hits[min(int(nth or 0), len(hits) - 1)] if hits else 0
     rows = rows[k0:]
 agg = collections.defaultdict(lambda: [0, 0.0])
 def g(r, k):
