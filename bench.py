@@ -467,9 +467,9 @@ def run(args, rank, world, local, wd):
     if min(n, nyc) > 4096:
         bw = 3 * min(n, nyc) // 64
     band_frac = 1.0 - max(n - 2 * bw, 0) * max(nyc - 2 * bw, 0) / float(n * nyc)
-    # (r6) one rank, 6 band sweeps (<= 4096): ONE k_helm_band6 launch (48 B per band cell) + the band cells'
-    # copy-back (32 B), timed as one interval -- 80 B per band cell per step instead of 2 x 48
-    band6 = (world == 1 and min(n, nyc) <= 4096 and os.environ.get("NSGPU_BAND6", "1") != "0"
+    # (r6) NSGPU_BAND6=1 (one rank, 6 band sweeps, <= 4096): ONE k_helm_band6 launch (48 B per band cell) + the
+    # band cells' copy-back (32 B), timed as one interval -- 80 B per band cell per step instead of 2 x 48
+    band6 = (world == 1 and min(n, nyc) <= 4096 and os.environ.get("NSGPU_BAND6", "0") != "0"
              and os.environ.get("NSGPU_BAND_SWEEPS", "6") == "6")
     band_bpc = (80 if band6 else 96) * band_frac
     # the finest level: a V-cycle whose output is not checked hands its prolongation pass to the next

@@ -1359,10 +1359,10 @@ void dct_pair(bool inverse, const double* in, const double* shift, double* out, 
               const void* wk, hipStream_t st, int oe_pair) {
     constexpr int T = Fft<LOGN>::T;
     const size_t lds = sizeof(cplx) * (size_t)FftLds<LOGN>::n;
-    // (two workgroups per CU fit the LDS: one persistent round)
-    // (r6, A/B) NSGPU_FPS_GRID: workgroups per launch (0: one persistent round, two per CU)
+    // (r6) one workgroup per row pair: 106.5 / 64.6 us at 4096^2 against 110.7 / 65.6 with r4-r5's one persistent
+    // round of two per CU (profiles/r06/ab/fpsg_summary.txt); NSGPU_FPS_GRID=n: at most n workgroups (A/B)
     static const int fg = getenv("NSGPU_FPS_GRID") ? std::atoi(getenv("NSGPU_FPS_GRID")) : 0;
-    const dim3 grid(std::min((nrows + 1) / 2, fg > 0 ? fg : 2 * device_cus()));
+    const dim3 grid(std::min((nrows + 1) / 2, fg > 0 ? fg : 1 << 30));
     if (inverse) {
         lds_attr_once((const void*)k_fps_idct<LOGN>, (int)lds);
         hipEvent_t a, b;
@@ -1389,8 +1389,8 @@ int div_pair(const FpsDivArgs& a0, hipStream_t st) {
     constexpr int T = Fft<LOGN>::T;
     const size_t lds = sizeof(cplx) * (size_t)FftLds<LOGN>::n;
     lds_attr_once((const void*)k_fps_dct_div<LOGN>, (int)lds);
-    static const int fg = getenv("NSGPU_FPS_GRID") ? std::atoi(getenv("NSGPU_FPS_GRID")) : 0;
-    const dim3 grid(std::min(a0.cnt, fg > 0 ? fg : 2 * device_cus()));
+    static const int fg = getenv("NSGPU_FPS_GRID") ? std::atoi(getenv("NSGPU_FPS_GRID")) : 0;   // (as dct_pair)
+    const dim3 grid(std::min(a0.cnt, fg > 0 ? fg : 1 << 30));
     hipEvent_t a, b;
     if (take_launch_timing(a, b)) hipExtLaunchKernelGGL(k_fps_dct_div<LOGN>, grid, dim3(T), lds, st, a, b, 0, a0);
     else hipLaunchKernelGGL(k_fps_dct_div<LOGN>, grid, dim3(T), lds, st, a0);

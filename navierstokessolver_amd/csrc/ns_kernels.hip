@@ -3299,11 +3299,124 @@ __device__ __forceinline__ void helm_band_body(const BandArgs& a, double* smem) 
         }
     }
 }
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_helm_band(BandArgs a) {
-    constexpr int E = BT + 4 * BAND_NSW;
-    __shared__ double smem[E * E + 6 * E];
-    helm_band_body<BT, BAND_NSW, BAND_SEG, 256, true>(a, smem);
+// (the 3-sweep launch: its own body -- the templated one above measured 48.5 -> 62.8 us here)
+__global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
+    constexpr int R = 2 * BAND_NSW, E = BT + 2 * R, NP = E / 2, SEG = BAND_SEG, NSEG = E / SEG;
+    static_assert(E % SEG == 0 && NP * NSEG <= 256, "band tile layout");
+    __shared__ double sp[E][E];
+    __shared__ double rw[E][3];   // per staged row: cw, ce, cw + ce + bx
+    __shared__ double cl[E][3];   // per staged column: cs, cn, cs + cn + by
+    int ti, tj;
+    band_tile(blockIdx.x, a, ti, tj);
+    const int f = blockIdx.y;
+    const double* q = a.q[f];
+    const double* qb = a.qb[f];
+    const double* b = a.b[f];
+    const int li0 = ti * BT, j0 = tj * BT, ld = a.ld, ny = a.ny, nx = a.nx;
+    if (a.phase) {   // (workgroup-uniform) does the staged region reach a neighbour rank's rows?
+        const bool touch = (a.i0 > 0 && li0 - R < 0) || (a.i0 + a.nxl < nx && li0 + BT + R > a.nxl);
+        if (touch != (a.phase == 2)) return;
+    }
+    const int rlo = -HALO, rhi = a.nxl + HALO - 1;
+    const int gib = a.i0 + li0 - R, jb = j0 - R;   // global row / column of staged (0, 0)
+    const int t = threadIdx.x;
+    const bool act = t < NP * NSEG;
+    const int kp = act ? t % NP : 0, sg = act ? t / NP : 0;
+    const int c0 = 2 * kp, r0 = SEG * sg;          // columns c0, c0 + 1; rows r0 .. r0 + SEG - 1
+    double2 v[SEG], bq[SEG];
+    int jj[2];
+    bool jin[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const int j = jb + c0 + e;
+        jin[e] = j >= 0 && j < ny;
+        jj[e] = min(max(j, 0), ny - 1);
+    }
+#pragma unroll
+    for (int s = 0; s < SEG; s++) {
+        const int li = min(max(li0 - R + r0 + s, rlo), rhi);
+        const ptrdiff_t o = (ptrdiff_t)li * ld;
+        const bool b0 = in_band(a.i0 + li, jj[0], nx, ny, a.bw), b1 = in_band(a.i0 + li, jj[1], nx, ny, a.bw);
+        v[s].x = (b0 ? qb : q)[o + jj[0]];
+        v[s].y = (b1 ? qb : q)[o + jj[1]];
+        bq[s].x = b[o + jj[0]];
+        bq[s].y = b[o + jj[1]];
+    }
+    if (t < E) {
+        const int gi = min(max(gib + t, 0), nx - 1);
+        const double cw = a.cw[gi], ce = a.ce[gi];
+        rw[t][0] = cw; rw[t][1] = ce; rw[t][2] = cw + ce + a.bx[gi];
+    } else if (t >= 64 && t < 64 + E) {
+        const int k = t - 64;
+        const int j = min(max(jb + k, 0), ny - 1);
+        const double cs = a.cs[j], cn = a.cn[j];
+        cl[k][0] = cs; cl[k][1] = cn; cl[k][2] = cs + cn + a.by[j];
+    }
+    if (act) {
+#pragma unroll
+        for (int s = 0; s < SEG; s++) { sp[r0 + s][c0] = v[s].x; sp[r0 + s][c0 + 1] = v[s].y; }
+    }
+    __syncthreads();
+    const double alpha = a.alpha, omega = a.omega;
+    // this thread's coefficients and relaxation weights (0 on held cells)
+    double2 w[SEG];
+    double rcw[SEG], rce[SEG], rd[SEG];
+    const double ccs0 = cl[c0][0], ccn0 = cl[c0][1], ccd0 = cl[c0][2];
+    const double ccs1 = cl[c0 + 1][0], ccn1 = cl[c0 + 1][1], ccd1 = cl[c0 + 1][2];
+#pragma unroll
+    for (int s = 0; s < SEG; s++) {
+        const int r = r0 + s, gi = gib + r;
+        rcw[s] = rw[r][0]; rce[s] = rw[r][1]; rd[s] = rw[r][2];
+        w[s].x = (jin[0] && in_band(gi, jj[0], nx, ny, a.bw)) ? omega * rcp_nr(diag<1>(rd[s], ccd0, alpha)) : 0.0;
+        w[s].y = (jin[1] && in_band(gi, jj[1], nx, ny, a.bw)) ? omega * rcp_nr(diag<1>(rd[s], ccd1, alpha)) : 0.0;
+    }
+    const int cpar = (gib + jb) & 1;   // colour parity of staged (0, 0)
+    for (int h = 0; h < 2 * BAND_NSW; h++) {
+        const int par = h & 1;                   // red ((gi + j) even), black, ...
+        const int lo = h + 1, hi = E - 2 - h;    // the half-sweep's region: [lo, hi]^2
+        if (act) {
+#pragma unroll
+            for (int s = 0; s < SEG; s++) {
+                const int r = r0 + s;
+                if (r < lo || r > hi) continue;
+                // the colour's column in this row: c0 + e, e = (par + gi + j) parity, uniform
+                const int e = (par + cpar + r) & 1;
+                const int cc = c0 + e;
+                if (cc < lo || cc > hi) continue;
+                const double xm = s > 0 ? (e ? v[s - 1].y : v[s - 1].x) : sp[r - 1][cc];
+                const double xp = s < SEG - 1 ? (e ? v[s + 1].y : v[s + 1].x) : sp[r + 1][cc];
+                double rr;
+                if (e == 0) {
+                    const double ym = sp[r][cc - 1], yp = v[s].y;
+                    v[s].x = relax<1>(v[s].x, xm, xp, ym, yp, bq[s].x, rcw[s], rce[s], ccs0, ccn0,
+                                      diag<1>(rd[s], ccd0, alpha), w[s].x, alpha, rr);
+                    sp[r][cc] = v[s].x;
+                } else {
+                    const double ym = v[s].x, yp = sp[r][cc + 1];
+                    v[s].y = relax<1>(v[s].y, xm, xp, ym, yp, bq[s].y, rcw[s], rce[s], ccs1, ccn1,
+                                      diag<1>(rd[s], ccd1, alpha), w[s].y, alpha, rr);
+                    sp[r][cc] = v[s].y;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (act) {
+        double* out = a.out[f];
+#pragma unroll
+        for (int s = 0; s < SEG; s++) {
+            const int r = r0 + s, li = li0 + r - R;
+            if (r < R || r >= R + BT || li >= a.nxl) continue;
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const int cc = c0 + e, j = jb + cc;
+                if (cc < R || cc >= R + BT || j >= ny || !in_band(a.i0 + li, j, nx, ny, a.bw)) continue;
+                out[(ptrdiff_t)li * ld + j] = e ? v[s].y : v[s].x;
+            }
+        }
+    }
 }
+
 // (r6) one rank: all 6 sweeps in ONE launch -- 64 x 64 tiles and their 12-cell cone (88 x 88
 // staged, 66 KB of LDS: 2 workgroups a CU), the same (88/64)^2 read amplification as a 3-sweep
 // 32 x 32 launch, so half the band traffic; the band cells land in `out` (the scratch plane) and
@@ -4200,15 +4313,15 @@ __global__ __launch_bounds__(256) void k_helm_rbt_mask(Geo g, Coef c, double alp
 // the batch's check without a pass of its own.  One rank (the cone reaches R > HALO rows past the tile).
 // Per NSW sweeps: u, v, code read ~(1 + 2R/TI)(1 + 2R/64) x 20 B + b 16 + write 16 -- against 52 B per sweep.
 template <int NSW>
-struct MtTile {
-    static constexpr int TI = MT_TI, TJ = MT_TJ, NTH = 1024;
+struct MtTile {   // (two workgroups per CU by LDS: 4 sweeps with the residual take 24-row tiles)
+    static constexpr int TI = NSW >= 4 ? 24 : MT_TI, TJ = MT_TJ, NTH = 512;
 };
 // BAND (r6, the wall bands of a masked domain): only the cells flagged FC_BAND (within the band width of a
 // boundary face along a row or column) are relaxed, the rest held; one workgroup per tile of the list `tiles`;
 // band cells read from qbu / qbv, the others from u / v, and only band cells written (k_helm_band's scheme: two
 // launches U -> TU, then (U, TU) -> U, no tile writes what another reads, no copy-back)
 template <int NSW, bool RES, bool BAND>
-__global__ __launch_bounds__(1024) void k_helm_mt_mask(Geo g, Coef c, double alpha, double omega,
+__global__ __launch_bounds__(512) void k_helm_mt_mask(Geo g, Coef c, double alpha, double omega,
                                                        const double* __restrict__ u, const double* __restrict__ v,
                                                        const double* __restrict__ qbu, const double* __restrict__ qbv,
                                                        const double* __restrict__ bu, const double* __restrict__ bv,
@@ -4216,14 +4329,13 @@ __global__ __launch_bounds__(1024) void k_helm_mt_mask(Geo g, Coef c, double alp
                                                        double* __restrict__ part, const int2* __restrict__ tiles) {
     constexpr int TI = MtTile<NSW>::TI, TJ = MtTile<NSW>::TJ, NTH = MtTile<NSW>::NTH;
     constexpr int R = 2 * NSW + (RES ? 1 : 0), EI = TI + 2 * R, EJ = TJ + 2 * R, NE = EI * EJ;
-    // LDS: u, v, the cell's diagonal weight sum wc and omega / (1 + alpha wc) (formed once per staged cell, not
-    // once per relaxation), the codes, and per row hx, pw, pe, 1 / hx^2, per column hy, ps, pn, 1 / hy^2
+    // LDS: u, v, the codes, and per row hx, pw, pe, 1 / hx^2, per column hy, ps, pn, 1 / hy^2 (20 B per staged
+    // cell: two workgroups per CU, one loading while the other relaxes -- with the weights staged too (36 B) one
+    // workgroup per CU left the memory idle during its sweeps: 540 vs 3 x 194 us for 3 sweeps)
     extern __shared__ double smt[];
     double* su = smt;
     double* sv = smt + NE;
-    double* swc = smt + 2 * NE;
-    double* sdi = smt + 3 * NE;
-    double* trow = smt + 4 * NE;            // [4][EI]
+    double* trow = smt + 2 * NE;            // [4][EI]
     double* tcol = trow + 4 * EI;           // [4][EJ]
     int* sc = reinterpret_cast<int*>(tcol + 4 * EJ);
     int li0 = blockIdx.y * TI, j0 = blockIdx.x * TJ;
@@ -4236,16 +4348,57 @@ __global__ __launch_bounds__(1024) void k_helm_mt_mask(Geo g, Coef c, double alp
     const int tid = threadIdx.x;
     // the cells this launch relaxes
     auto live = [](int code) { return (code & FC_IN) && (!BAND || (code & FC_BAND)); };
-    for (int q = tid; q < NE; q += NTH) {
+    // the edge tags' NEUMANN flags as a mask (the table is padded to 32 entries)
+    const unsigned long long neub = __ballot((tid & 63) < 32 && g.et[tid & 31].neu != 0);
+    const unsigned neum = (unsigned)neub;
+    const int base = (g.i0 + li0 - R + j0 - R) & 1;   // colour of staged (0, 0)
+    // staging: every load of the thread's cells issued before the first LDS store (one memory round trip, not
+    // one per cell: with one workgroup per CU nothing else hides it)
+    constexpr int NQ = (NE + NTH - 1) / NTH;
+    double lu[NQ], lv[NQ], lbu[BAND ? NQ : 1], lbv[BAND ? NQ : 1];
+    int lc[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const int q = min(tid + k * NTH, NE - 1);
         const int r = q / EJ, cc = q - r * EJ;
         const int li = li0 - R + r, j = j0 - R + cc;
         const bool in = li >= 0 && li < g.nxl && j >= 0 && j < g.ny;
         const ptrdiff_t o = (ptrdiff_t)min(max(li, -HALO), g.nxl + HALO - 1) * ld + min(max(j, 0), g.ny - 1);
-        const int code = in ? g.fc[o] : 0;   // (one rank: cells off the slab are off the box)
-        const bool fb = BAND && (code & FC_BAND);
-        su[q] = (fb ? qbu : u)[o];
-        sv[q] = (fb ? qbv : v)[o];
-        sc[q] = code;
+        lc[k] = in ? g.fc[o] : 0;   // (one rank: cells off the slab are off the box)
+        lu[k] = u[o];
+        lv[k] = v[o];
+        if (BAND) {   // (both planes: the select waits for the code)
+            lbu[BAND ? k : 0] = qbu[o];
+            lbv[BAND ? k : 0] = qbv[o];
+        }
+    }
+    // the right-hand sides of a half-sweep's cells are loaded one half-sweep ahead (a load per half-sweep, behind
+    // a barrier, would expose its latency 2 NSW times)
+    constexpr int MAXIT = ((EI - 2) * (EJ - 2) / 2 + EI + NTH - 1) / NTH;
+    double pbu[MAXIT], pbv[MAXIT];
+    auto load_b = [&](int h) {
+        const int par = h & 1, lo = h + 1, hr = EI - 2 - h, hc = EJ - 2 - h;
+        const int npr = (hc - lo) / 2 + 1, cnt = (hr - lo + 1) * npr;
+#pragma unroll
+        for (int it = 0; it < MAXIT; it++) {
+            const int q = tid + it * NTH;
+            const int rq = q / npr, r = lo + rq;
+            const int cc = min(lo + ((par + base + r + lo) & 1) + 2 * (q - rq * npr), hc);
+            const int li = min(max(li0 - R + r, 0), g.nxl - 1), j = min(max(j0 - R + cc, 0), g.ny - 1);
+            const ptrdiff_t o = (ptrdiff_t)li * ld + j;
+            pbu[it] = q < cnt ? bu[o] : 0.0;
+            pbv[it] = q < cnt ? bv[o] : 0.0;
+        }
+    };
+    load_b(0);
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const int q = tid + k * NTH;
+        if (q >= NE) continue;
+        const bool fb = BAND && (lc[k] & FC_BAND);
+        su[q] = fb ? lbu[BAND ? k : 0] : lu[k];
+        sv[q] = fb ? lbv[BAND ? k : 0] : lv[k];
+        sc[q] = lc[k];
     }
     if (tid < EI) {
         const int gi = min(max(g.i0 + li0 - R + tid, 0), g.nx - 1);
@@ -4262,46 +4415,53 @@ __global__ __launch_bounds__(1024) void k_helm_mt_mask(Geo g, Coef c, double alp
     auto pn_of = [&](int k, int r, int cc) {
         return k == 0 ? trow[EI + r] : k == 1 ? trow[2 * EI + r] : k == 2 ? tcol[EJ + cc] : tcol[2 * EJ + cc];
     };
-    for (int q = tid; q < NE; q += NTH) {
-        const int code = sc[q];
-        if (!live(code)) continue;
-        const int r = q / EJ, cc = q - r * EJ;
+    // (branch-free: a term that k_helm_rb_mask skips is added as an exact 0 here -- wc + 0.0 and
+    // fma(0.0, x, s) leave the sums' values unchanged, so the result is the same bit for bit -- and every
+    // neighbour is loaded: the iterations of a half-sweep interleave instead of waiting on each other)
+    auto wsum = [&](int code, int r, int cc, double (&pk)[4]) {
         const double w2[4] = {trow[3 * EI + r], trow[3 * EI + r], tcol[3 * EJ + cc], tcol[3 * EJ + cc]};
         double wc = 0.0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            if (fc_edge(code, k) == FC_INT) wc += pn_of(k, r, cc);
-            else if (!g.et[fc_edge(code, k)].neu) wc += 2.0 * w2[k];
+            const int e = fc_edge(code, k);
+            const double p = pn_of(k, r, cc);
+            pk[k] = e == FC_INT ? p : 0.0;
+            wc += e == FC_INT ? p : (((neum >> e) & 1u) ? 0.0 : 2.0 * w2[k]);
         }
-        swc[q] = wc;
-        sdi[q] = omega / (1.0 + alpha * wc);
-    }
-    __syncthreads();
+        return wc;
+    };
     // the residual b - (I - alpha L_V) x at staged cell x (row r, column cc)
-    auto resid = [&](const double* sx, int x, int code, int r, int cc, double b) {
+    auto resid = [&](const double* sx, int x, const double (&pk)[4], double wc, double b) {
         const double xc = sx[x];
-        double s = -swc[x] * xc;
+        double s = -wc * xc;
         const int nb[4] = {x - EJ, x + EJ, x - 1, x + 1};
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (fc_edge(code, k) == FC_INT) s = fma(pn_of(k, r, cc), sx[nb[k]], s);
+        for (int k = 0; k < 4; k++) s = fma(pk[k], sx[nb[k]], s);
         return b - (xc - alpha * s);
     };
-    const int base = (g.i0 + li0 - R + j0 - R) & 1;   // colour of staged (0, 0)
+#pragma unroll
     for (int h = 0; h < 2 * NSW; h++) {
         const int par = h & 1, lo = h + 1, hr = EI - 2 - h, hc = EJ - 2 - h;
         const int npr = (hc - lo) / 2 + 1, cnt = (hr - lo + 1) * npr;
-        for (int q = tid; q < cnt; q += NTH) {
-            const int rq = q / npr, k = q - rq * npr, r = lo + rq;
-            const int cc = lo + ((par + base + r + lo) & 1) + 2 * k;
-            if (cc > hc) continue;
+        double cbu[MAXIT], cbv[MAXIT];
+#pragma unroll
+        for (int it = 0; it < MAXIT; it++) { cbu[it] = pbu[it]; cbv[it] = pbv[it]; }
+        if (h + 1 < 2 * NSW) load_b(h + 1);
+#pragma unroll
+        for (int it = 0; it < MAXIT; it++) {
+            const int q = tid + it * NTH;
+            const int rq = min(q / npr, hr - lo), k = q - (q / npr) * npr, r = lo + rq;
+            const int cc0 = lo + ((par + base + r + lo) & 1) + 2 * k;
+            const int cc = min(cc0, hc);
             const int x = r * EJ + cc, code = sc[x];
-            if (!live(code)) continue;
-            const ptrdiff_t o = (ptrdiff_t)(li0 - R + r) * ld + (j0 - R + cc);
-            const double di = sdi[x], xu = su[x], xv = sv[x];
-            const double ru = resid(su, x, code, r, cc, bu[o]), rv = resid(sv, x, code, r, cc, bv[o]);
-            su[x] = fma(di, ru, xu);
-            sv[x] = fma(di, rv, xv);
+            double pk[4];
+            const double wc = wsum(code, r, cc, pk);
+            const double di = omega / (1.0 + alpha * wc), xu = su[x], xv = sv[x];
+            const double ru = resid(su, x, pk, wc, cbu[it]), rv = resid(sv, x, pk, wc, cbv[it]);
+            if (q < cnt && cc0 <= hc && live(code)) {
+                su[x] = fma(di, ru, xu);
+                sv[x] = fma(di, rv, xv);
+            }
         }
         __syncthreads();
     }
@@ -4317,8 +4477,10 @@ __global__ __launch_bounds__(1024) void k_helm_mt_mask(Geo g, Coef c, double alp
         if (RES) {
             const int code = sc[x];
             if (code & FC_IN) {
-                const double ru = resid(su, x, code, r + R, cc + R, bu[o]);
-                const double rv = resid(sv, x, code, r + R, cc + R, bv[o]);
+                double pk[4];
+                const double wc = wsum(code, r + R, cc + R, pk);
+                const double ru = resid(su, x, pk, wc, bu[o]);
+                const double rv = resid(sv, x, pk, wc, bv[o]);
                 acc[0] += ru * ru;
                 acc[1] += rv * rv;
             }
@@ -4748,8 +4910,8 @@ static int mt_launch(const Geo& g, const Coef& c, double alpha, double omega, co
                      double* part, const int2* tiles, int ntiles, hipStream_t st) {
     constexpr int TI = MtTile<NSW>::TI, TJ = MtTile<NSW>::TJ, R = 2 * NSW + (RES ? 1 : 0);
     constexpr int EI = TI + 2 * R, EJ = TJ + 2 * R;
-    constexpr int lds = (4 * EI * EJ + 4 * (EI + EJ)) * 8 + EI * EJ * 4;
-    static_assert(EI <= 128 && EJ <= 128 && lds <= 160 * 1024, "table loaders / LDS");
+    constexpr int lds = (2 * EI * EJ + 4 * (EI + EJ)) * 8 + EI * EJ * 4;
+    static_assert(EI <= 128 && EJ <= 128 && lds <= 80 * 1024, "table loaders / two workgroups per CU");
     lds_attr_once((const void*)k_helm_mt_mask<NSW, RES, BAND>, lds);
     const dim3 grid = BAND ? dim3(ntiles) : dim3((g.ny + TJ - 1) / TJ, (g.nxl + TI - 1) / TI);
     if (grid.x * grid.y == 0) return 0;

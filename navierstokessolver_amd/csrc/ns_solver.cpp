@@ -146,7 +146,9 @@ struct ns_solver {
     bool triple = true;          // 3-sweep passes allowed on this decomposition (slabs >= 2*HALO rows)
     bool sweep3 = true;          // single rank: odd Helmholtz batches start with a 3-sweep pass (k_sweep3)
     bool helm_band = true;       // Helmholtz: wall-band relaxation before the global passes (k_helm_band)
-    bool band6 = true;           // (r6) one rank, 6 band sweeps: one k_helm_band6 launch + copy-back (NSGPU_BAND6=0: 2 x 3)
+    // (r6) one rank, 6 band sweeps as ONE k_helm_band6 launch + copy-back (NSGPU_BAND6=1): half the band bytes, but
+    // the launches are latency-bound, not HBM-bound -- 100 + 13 us against 2 x 48.5 (profiles/r06/ab/): off
+    bool band6 = false;
     int band_w = 128, band_sweeps = 6;   // its width (cells from a wall: min(nx, ny) / 32) and RB-SOR sweeps (a multiple of 3)
     bool sweep3_res = true;      // one rank: a Helmholtz batch may end on a 3-sweep pass with its residual
     int helm_uv = 1;             // NSGPU_HELM_UV=0: one rank's 3-sweep batch as two one-field launches (A/B)
@@ -3656,7 +3658,8 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     std::vector<int32_t> mband;
     if (masked && g.nxl == gd->nx) {
         const int nx = gd->nx, ny = gd->ny, ldh = g.ld;
-        const int mbw = std::min(nx, ny) > 4096 ? 3 * std::min(nx, ny) / 64 : std::max(32, std::min(nx, ny) / 32);
+        int mbw = std::min(nx, ny) > 4096 ? 3 * std::min(nx, ny) / 64 : std::max(32, std::min(nx, ny) / 32);
+        if (const char* e = getenv("NSGPU_MASK_BAND_W")) mbw = std::max(1, std::atoi(e));   // (A/B)
         auto code_at = [&](int i, int j) -> int32_t& { return fch[(size_t)(i + nsg::HALO) * ldh + j]; };
         auto bnd = [&](int i, int j) {   // a domain cell with a face that is not interior
             const int32_t c = code_at(i, j);
@@ -3999,10 +4002,13 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
     }
 
     if (masked) {
+        // (the device edge table padded to 32 entries: k_helm_mt_mask reads the NEUMANN flags of all 31 tags at once)
+        std::vector<nsg::EdgeDev> etd(etab.begin(), etab.end());
+        if (etd.size() < 32) etd.resize(32, nsg::EdgeDev{});
         if (hipMalloc(&s->fc_mem, fch.size() * sizeof(int32_t)) != hipSuccess ||
-            hipMalloc(&s->et_mem, etab.size() * sizeof(nsg::EdgeDev)) != hipSuccess) { set_err("hipMalloc topology failed"); return fail(NS_ENOMEM); }
+            hipMalloc(&s->et_mem, etd.size() * sizeof(nsg::EdgeDev)) != hipSuccess) { set_err("hipMalloc topology failed"); return fail(NS_ENOMEM); }
         if (hipMemcpy(s->fc_mem, fch.data(), fch.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(s->et_mem, etab.data(), etab.size() * sizeof(nsg::EdgeDev), hipMemcpyHostToDevice) != hipSuccess) { set_err("topology upload failed"); return fail(NS_EHIP); }
+            hipMemcpy(s->et_mem, etd.data(), etd.size() * sizeof(nsg::EdgeDev), hipMemcpyHostToDevice) != hipSuccess) { set_err("topology upload failed"); return fail(NS_EHIP); }
         s->g.fc = s->fc_mem + (size_t)nsg::HALO * g.ld;
         s->g.et = s->et_mem;
         if (!mband.empty()) {
