@@ -557,8 +557,9 @@ def run(args, rank, world, local, wd):
 
     def roof(key, label, bpc, avg_s, launches):
         achieved = bpc * local_cells / avg_s / 1e9
+        tkey = "rhs_sc" if (key == "rhs" and deferred) else key   # (r6: K1 with the deferred K5 folded in)
         r = {"bound": "hbm", "kernel": label, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get(key), "avg_kernel_us": avg_s * 1e6,
+             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get(tkey), "avg_kernel_us": avg_s * 1e6,
              "launches_timed": launches, "bytes_per_launch": bpc * local_cells, "bytes_per_cell": bpc}
         if r["traffic"] is not None:
             r["traffic_source"] = tsrc

@@ -784,6 +784,56 @@ __global__ __launch_bounds__(256) void k_correct(Geo g, Coef c, double dt, const
     block_reduce_min<4>(acc, part + 4 * (blockIdx.x + gridDim.x * blockIdx.y));
 }
 
+// (r6) K3 / K5 of a masked domain's listed cells (Geo::ecell: the domain cells that are not FC_DEEP), one thread
+// each, k_div<TopoMask> / k_correct<TopoMask>'s arithmetic; the FC_DEEP cells are k_cell_s's
+__global__ __launch_bounds__(256) void k_div_cells(Geo g, Coef c, double dt, const double* __restrict__ u,
+                                                   const double* __restrict__ v, double* __restrict__ rp,
+                                                   double* __restrict__ part) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    double acc[2] = {0.0, 0.0};
+    if (k < g.necell) {
+        const int ld = g.ld, o = g.ecell[k], li = o / ld, j = o - li * ld;
+        const TopoMask t(g, li, j);
+        const int gi = g.i0 + li;
+        const double uc = ldf(u, ld, li, j), vc = ldf(v, ld, li, j);
+        const double hx = c.hx[gi], hy = c.hy[j];
+        double V0, V1, V2, V3, r;
+        if (t.in(-1, 0)) { r = hx / (c.hx[gi - 1] + hx); V0 = ldf(u, ld, li - 1, j) * r + uc * (1 - r); }
+        else V0 = 0.5 * (uc + t.gv(0, 0, 0, uc, 0));
+        if (t.in(1, 0)) { r = hx / (c.hx[gi + 1] + hx); V1 = ldf(u, ld, li + 1, j) * r + uc * (1 - r); }
+        else V1 = 0.5 * (uc + t.gv(0, 0, 1, uc, 0));
+        if (t.in(0, -1)) { r = hy / (c.hy[j - 1] + hy); V2 = ldf(v, ld, li, j - 1) * r + vc * (1 - r); }
+        else V2 = 0.5 * (vc + t.gv(0, 0, 2, vc, 1));
+        if (t.in(0, 1)) { r = hy / (c.hy[j + 1] + hy); V3 = ldf(v, ld, li, j + 1) * r + vc * (1 - r); }
+        else V3 = 0.5 * (vc + t.gv(0, 0, 3, vc, 1));
+        const double val = ((V1 - V0) / hx + (V3 - V2) / hy) / dt;
+        rp[o] = val;
+        acc[0] = val;
+        acc[1] = val * val;
+    }
+    block_reduce_sum<2>(acc, part + 2 * blockIdx.x);
+}
+__global__ __launch_bounds__(256) void k_correct_cells(Geo g, Coef c, double dt, const double* __restrict__ us,
+                                                       const double* __restrict__ vs, double* __restrict__ u,
+                                                       double* __restrict__ v, const double* __restrict__ phi,
+                                                       double* __restrict__ part) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    double acc[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+    if (k < g.necell) {
+        const int ld = g.ld, o = g.ecell[k], li = o / ld, j = o - li * ld;
+        double gx, gy;
+        grad_phi<TopoMask>(g, c, phi, li, j, gx, gy);
+        const double un = us[o] - dt * gx, vn = vs[o] - dt * gy;
+        u[o] = un;
+        v[o] = vn;
+        acc[0] = un != un ? -INFINITY : un;
+        acc[1] = un != un ? -INFINITY : -un;
+        acc[2] = vn != vn ? -INFINITY : vn;
+        acc[3] = vn != vn ? -INFINITY : -vn;
+    }
+    block_reduce_min<4>(acc, part + 4 * blockIdx.x);
+}
+
 // ------------------------------------------------------- K2 / K4: fused red-black sweep
 // One workgroup owns a TI x TJ tile.  It stages the tile plus a 2-cell ring of
 // the OLD iterate (and a 1-cell ring of the rhs) in LDS, updates the red cells
@@ -1856,6 +1906,9 @@ struct CellStreamArgs {
     const double *h1, *h2, *h3;
     double* gout;
     double gc0, gc1, gc2, gc3;
+    // (r6) a masked domain (K3 / K5, one rank): only the FC_DEEP cells -- every face interior, so the rectangle's
+    // interior arithmetic -- are written and reduced; the rest (Geo::ecell) take k_div_cells / k_correct_cells
+    const int32_t* fc;
 };
 
 // one face value along a line: interior r-weighted interpolation, or the wall's (q + ghost)/2
@@ -1924,9 +1977,12 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
         double2 Q[SDK], X[SDK], Y[SDK];
         constexpr int SH = K == 6 ? SDK : 1;   // K6: the history planes' rows, prefetched alike
         double2 H1[SH], H2[SH], H3[SH];
-        auto load = [&](int r, double2& q, double2& x, double2& y, double2& h1, double2& h2, double2& h3) {
+        constexpr int SM = (K == 3 || K == 5) ? SDK : 1;   // (masked K3 / K5: the codes' rows)
+        int2 CD[SM];
+        auto load = [&](int r, double2& q, double2& x, double2& y, double2& h1, double2& h2, double2& h3, int2& cd) {
             const int lw = min(max(r, max(ib - 1, rlo)), min(ie, rhi));
             const int lr = min(max(r - 1, ib), ie - 1);
+            if ((K == 3 || K == 5) && A.fc) cd = *reinterpret_cast<const int2*>(A.fc + (ptrdiff_t)lr * ld + lc);
             q = *reinterpret_cast<const double2*>(A.a0 + (ptrdiff_t)lw * ld + lc);
             if (K == 3 || (K == 7 && A.a1)) {
                 x = *reinterpret_cast<const double2*>(A.a1 + (ptrdiff_t)lr * ld + lc);
@@ -1941,10 +1997,13 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
             }
         };
         auto step = [&](const double2 q, const double2 x, const double2 y, const double2 h1, const double2 h2,
-                        const double2 h3, int r) {
+                        const double2 h3, const int2 cd, int r) {
             W0 = W1; W1 = W2; W2 = q;
             const int m = r - 1;
             if (m < ib || m >= ie) return;
+            // (masked: the FC_DEEP cells only)
+            const bool d0 = !((K == 3 || K == 5) && A.fc) || (cd.x & FC_DEEP) != 0;
+            const bool d1 = !((K == 3 || K == 5) && A.fc) || (cd.y & FC_DEEP) != 0;
             const int gi = g.i0 + m;
             const bool hW = gi > 0, hE = gi < g.nx - 1;
             const double hx = c.hx[gi], fw = c.fwx[gi], fe = c.fex[gi];
@@ -1964,11 +2023,14 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                     val[e] = ((V1 - V0) / hx + (V3 - V2) / (e ? hy1 : hy0)) / A.dt;
                 }
                 if (wr) {   // (an odd ny's last pair: column ny is row padding, left untouched)
-                    if (v1) st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(val[0], val[1]), false);
-                    else A.o0[(ptrdiff_t)m * ld + c0] = val[0];
+                    if (v1 && d0 && d1) st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(val[0], val[1]), false);
+                    else {
+                        if (d0) A.o0[(ptrdiff_t)m * ld + c0] = val[0];
+                        if (v1 && d1) A.o0[(ptrdiff_t)m * ld + c1] = val[1];
+                    }
                 }
-                if (o0) { acc[0] += val[0]; acc[1] += val[0] * val[0]; }
-                if (o1) { acc[0] += val[1]; acc[1] += val[1] * val[1]; }
+                if (o0 && d0) { acc[0] += val[0]; acc[1] += val[0] * val[0]; }
+                if (o1 && d1) { acc[0] += val[1]; acc[1] += val[1] * val[1]; }
             } else if (K == 7) {
                 // k_apply<0, TopoRect>'s sum in its order (W, E, S, N): pn (x_nb - x_c), 0 across a
                 // wall / inlet face, (ghost - x_c) / h^2 across a NEUMANN one, ghost = 2.5 x_c -
@@ -2014,12 +2076,18 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                     corr1(e ? x.y : x.x, e ? y.y : y.x, pc, pw, pe, ps, pn, hW, hE, e ? s1 : s0, e ? n1 : n0, fw, fe,
                           e ? fs1 : fs0, e ? fn1 : fn0, hx, e ? hy1 : hy0, A.dt, un[e], vn[e]);
                 }
-                if (wr && v1) {
+                if (wr && v1 && d0 && d1) {
                     st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(un[0], un[1]), K5_NT);
                     st_stream(A.o1 + (ptrdiff_t)m * ld + c0, make_double2(vn[0], vn[1]), K5_NT);
                 } else if (wr) {
-                    A.o0[(ptrdiff_t)m * ld + c0] = un[0];
-                    A.o1[(ptrdiff_t)m * ld + c0] = vn[0];
+                    if (d0) {
+                        A.o0[(ptrdiff_t)m * ld + c0] = un[0];
+                        A.o1[(ptrdiff_t)m * ld + c0] = vn[0];
+                    }
+                    if (v1 && d1) {
+                        A.o0[(ptrdiff_t)m * ld + c1] = un[1];
+                        A.o1[(ptrdiff_t)m * ld + c1] = vn[1];
+                    }
                 }
                 if (K == 6) {
                     // the next step's Poisson guess from this step's phi (the window's row m) and the
@@ -2031,7 +2099,7 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                 }
 #pragma unroll
                 for (int e = 0; e < 2; e++) {
-                    if (!(e ? o1 : o0)) continue;
+                    if (!(e ? o1 && d1 : o0 && d0)) continue;
                     // NaN-propagating min so a blown-up step is visible in the stats
                     acc[0] = fmin(acc[0], un[e] != un[e] ? -INFINITY : un[e]);
                     acc[1] = fmin(acc[1], un[e] != un[e] ? -INFINITY : -un[e]);
@@ -2042,12 +2110,12 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
         };
         const int r0 = ib - 1, r1 = ie;
 #pragma unroll
-        for (int q = 0; q < SDK; q++) load(r0 + q, Q[q], X[q], Y[q], H1[q % SH], H2[q % SH], H3[q % SH]);
+        for (int q = 0; q < SDK; q++) load(r0 + q, Q[q], X[q], Y[q], H1[q % SH], H2[q % SH], H3[q % SH], CD[q % SM]);
         for (int r = r0; r <= r1; r += SDK) {
 #pragma unroll
             for (int q = 0; q < SDK; q++) {
-                if (r + q <= r1) step(Q[q], X[q], Y[q], H1[q % SH], H2[q % SH], H3[q % SH], r + q);
-                load(r + q + SDK, Q[q], X[q], Y[q], H1[q % SH], H2[q % SH], H3[q % SH]);
+                if (r + q <= r1) step(Q[q], X[q], Y[q], H1[q % SH], H2[q % SH], H3[q % SH], CD[q % SM], r + q);
+                load(r + q + SDK, Q[q], X[q], Y[q], H1[q % SH], H2[q % SH], H3[q % SH], CD[q % SM]);
             }
         }
     }
@@ -4662,6 +4730,8 @@ static inline dim3 cell_grid(const Geo& g) { return dim3((g.ny + 63) / 64, (g.nx
 // partial) per 64 x 4*rows cells instead of per 256; still >= 2048 blocks per launch
 static inline int cell_rows(const Geo& g) {
     const long blocks = (long)((g.ny + 63) / 64) * ((g.nxl + 3) / 4);
+    static const int ov = getenv("NSGPU_CELL_ROWS") ? std::atoi(getenv("NSGPU_CELL_ROWS")) : 0;   // (A/B)
+    if (ov > 0) return std::min(ov, 16);
     return (int)std::min(16L, std::max(1L, blocks / 2048));
 }
 static inline dim3 cell_grid(const Geo& g, int rows) {
@@ -4856,12 +4926,28 @@ static bool cell_streaming() {
     return !(e && std::strcmp(e, "grid") == 0);
 }
 
+// (r6) a masked domain on one rank: the streaming K3 / K5 on its FC_DEEP cells + the listed cells (NSGPU_MASK_CELL=0:
+// the thread-per-cell k_div / k_correct<TopoMask>)
+static bool mask_cell_streams(const Geo& g) {
+    const char* e = getenv("NSGPU_MASK_CELL");   // (read per launch: the tests switch it)
+    const bool on = !(e && std::atoi(e) == 0);
+    return on && g.fc && g.ecell && g.nxl == g.nx && g_phase == 0 && cell_streaming();
+}
+
 int launch_div(const Geo& g, const Coef& c, double dt, const double* u, const double* v, double* rp, double* part,
                hipStream_t st) {
     if (cell_streaming() && !g.fc) {
         CellStreamArgs A{};
         A.g = g; A.c = c; A.dt = dt; A.a0 = u; A.a1 = v; A.o0 = rp; A.part = part;
         return launch_cell_s<3>(A, st);
+    }
+    if (mask_cell_streams(g)) {
+        CellStreamArgs A{};
+        A.g = g; A.c = c; A.dt = dt; A.a0 = u; A.a1 = v; A.o0 = rp; A.part = part; A.fc = g.fc;
+        const int n1 = launch_cell_s<3>(A, st);
+        const int n2 = (g.necell + 255) / 256;
+        NS_LAUNCH(k_div_cells, dim3(n2), dim3(256), 0, st, g, c, dt, u, v, rp, part + 2 * n1);
+        return n1 + n2;
     }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);
@@ -4994,6 +5080,14 @@ int launch_correct(const Geo& g, const Coef& c, double dt, const double* us, con
         CellStreamArgs A{};
         A.g = g; A.c = c; A.dt = dt; A.a0 = phi; A.a1 = us; A.a2 = vs; A.o0 = u; A.o1 = v; A.part = part;
         return launch_cell_s<5>(A, st);
+    }
+    if (mask_cell_streams(g)) {
+        CellStreamArgs A{};
+        A.g = g; A.c = c; A.dt = dt; A.a0 = phi; A.a1 = us; A.a2 = vs; A.o0 = u; A.o1 = v; A.part = part; A.fc = g.fc;
+        const int n1 = launch_cell_s<5>(A, st);
+        const int n2 = (g.necell + 255) / 256;
+        NS_LAUNCH(k_correct_cells, dim3(n2), dim3(256), 0, st, g, c, dt, us, vs, u, v, phi, part + 4 * n1);
+        return n1 + n2;
     }
     const int rows = cell_rows(g);
     const dim3 cg = cell_grid(g, rows);

@@ -3883,6 +3883,10 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         s->fps_pc = p->poisson == NS_POISSON_MG && !(fe && std::atoi(fe) == 0) && !(fpc && std::atoi(fpc) == 0) &&
                     masked && (!outflow || mask_oe) && yuni && xuni && p->nranks == 1 && nsg::fps_log2(gd->ny) >= 0;
         if (s->fps_pc && outflow) s->fa.outE = 1;
+        // (r6) the capacitance solve (cap_setup, unless NSGPU_CAP=0) is exact: BiCGStab takes one iteration from
+        // any start, so no phi extrapolation (its k_axpby pass, 87 us at 4096^2, and its four history planes)
+        const char* cpe = getenv("NSGPU_CAP");
+        if (s->fps_pc && !(cpe && std::atoi(cpe) == 0)) s->phi_extrap = 0;
     }
 
     auto fail = [&](int rc) { ns_destroy(s); return rc; };

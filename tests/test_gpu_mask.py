@@ -54,8 +54,13 @@ def test_mask_k1_rhs_velocity(gpu, name):
     assert abs(sums[0] - np.sum(ru * ru)) <= 1e-11 * np.sum(ru * ru)
 
 
-@pytest.mark.parametrize("name", sorted(ALL))
-def test_mask_k3_k5(gpu, name):
+@pytest.mark.parametrize("cells", ["1", "0"])
+@pytest.mark.parametrize("name", sorted(ALL) + sorted(BIG))
+def test_mask_k3_k5(gpu, monkeypatch, name, cells):
+    """K3 / K5 on the polygons against the oracle (1e-12).  (r6) cells=1, the default on one rank: the streaming
+    k_cell_s<3 / 5> on the FC_DEEP cells + k_div_cells / k_correct_cells on the rest; 0: the thread-per-cell
+    k_div / k_correct<TopoMask> (NSGPU_MASK_CELL=0).  Cells outside the domain are never written."""
+    monkeypatch.setenv("NSGPU_MASK_CELL", cells)
     rng = np.random.default_rng(22)
     dt = 1.0 / 512
     og, gs, m = pair(gpu, name, dt, 100.0)
@@ -72,6 +77,7 @@ def test_mask_k3_k5(gpu, name):
     eu, ev = rel(gs.get(gpu.NS_ARR_U).ravel()[m], u), rel(gs.get(gpu.NS_ARR_V).ravel()[m], v)
     assert eu <= 1e-12 and ev <= 1e-12, (eu, ev)
     np.testing.assert_allclose(mm[:4], [u.min(), u.max(), v.min(), v.max()], rtol=1e-12, atol=1e-15)
+    assert not np.any(gs.get(gpu.NS_ARR_U).ravel()[~m]) and not np.any(gs.get(gpu.NS_ARR_RPHI).ravel()[~m])
 
 
 @pytest.mark.parametrize("name", sorted(ALL))
@@ -116,10 +122,15 @@ def test_mask_full_steps_vs_oracle(gpu, name, steps, re, rtol):
     og, gs, m = pair(gpu, name, dt, re, rtol=rtol)
     osv = OSolver(og, dt, re, rtol=1e-13)
     tu, tp = (1e-6, 1e-4) if rtol >= 1e-8 else (1e-9, 1e-7)
+    its = []
     for _ in range(steps):
         st = gs.step()
+        its.append(int(st["it_phi"]))
         mm, _ = osv.step()
         np.testing.assert_allclose([st["umin"], st["umax"], st["vmin"], st["vmax"]], mm, atol=tu)
+    if rtol >= 1e-8 and all(k == 1 for k in its):
+        # (r6) the capacitance solve (one exact iteration per step): phi's bar tightened 1e-4 -> 1e-5
+        tp = 1e-5
     ref = osv.get()
     u, v, phi = (a.ravel() for a in gs.fields())
     du, dv = float(np.max(np.abs(u[m] - ref["u"]))), float(np.max(np.abs(v[m] - ref["v"])))
