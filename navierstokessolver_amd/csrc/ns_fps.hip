@@ -569,7 +569,8 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
 template <int LOGN>
 __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const double* __restrict__ in, double* __restrict__ out,
                                                             int nrows, int ld, const cplx* __restrict__ tw,
-                                                            const cplx* __restrict__ wk) {
+                                                            const cplx* __restrict__ wk,
+                                                            const int32_t* __restrict__ fcm) {
     constexpr int N = Fft<LOGN>::N, T = Fft<LOGN>::T;
     constexpr int PT = (N + T - 1) / T;
     extern __shared__ cplx z[];
@@ -637,6 +638,17 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
                 for (int q = 0; q < 8; q++) {
                     const int m = tid + q * T;   // columns 2m (v_m) and 2m + 1 (v_{N-1-m})
                     const cplx e = z[pz(m)], o = z[pz(N - 1 - m)];
+                    if (fcm) {   // (r6, a masked domain's solution: its cells only, the rest of `out` kept)
+                        const int2 ca = *reinterpret_cast<const int2*>(fcm + (size_t)r0 * ld + 2 * m);
+                        if (ca.x & FC_IN) oa[2 * m] = e.x * rn;
+                        if (ca.y & FC_IN) oa[2 * m + 1] = o.x * rn;
+                        if (two) {
+                            const int2 cb = *reinterpret_cast<const int2*>(fcm + (size_t)(r0 + 1) * ld + 2 * m);
+                            if (cb.x & FC_IN) ob[2 * m] = -e.y * rn;
+                            if (cb.y & FC_IN) ob[2 * m + 1] = -o.y * rn;
+                        }
+                        continue;
+                    }
                     st2(oa + 2 * m, e.x * rn, o.x * rn);
                     if (two) st2(ob + 2 * m, -e.y * rn, -o.y * rn);
                 }
@@ -1356,7 +1368,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
 
 template <int LOGN>
 void dct_pair(bool inverse, const double* in, const double* shift, double* out, int nrows, int ld, const void* tw,
-              const void* wk, hipStream_t st, int oe_pair) {
+              const void* wk, hipStream_t st, int oe_pair, const int32_t* fcm = nullptr) {
     constexpr int T = Fft<LOGN>::T;
     const size_t lds = sizeof(cplx) * (size_t)FftLds<LOGN>::n;
     // (r6) one workgroup per row pair: 106.5 / 64.6 us at 4096^2 against 110.7 / 65.6 with r4-r5's one persistent
@@ -1368,10 +1380,10 @@ void dct_pair(bool inverse, const double* in, const double* shift, double* out, 
         hipEvent_t a, b;
         if (take_launch_timing(a, b))
             hipExtLaunchKernelGGL(k_fps_idct<LOGN>, grid, dim3(T), lds, st, a, b, 0, in, out, nrows, ld,
-                                  (const cplx*)tw, (const cplx*)wk);
+                                  (const cplx*)tw, (const cplx*)wk, fcm);
         else
             hipLaunchKernelGGL(k_fps_idct<LOGN>, grid, dim3(T), lds, st, in, out, nrows, ld, (const cplx*)tw,
-                               (const cplx*)wk);
+                               (const cplx*)wk, fcm);
     } else {
         lds_attr_once((const void*)k_fps_dct<LOGN>, (int)lds);
         hipEvent_t a, b;
@@ -1756,6 +1768,25 @@ int fps_log2(int ny) {
     return (1 << l) == ny && l >= FPS_LOGN_MIN && l <= FPS_LOGN_MAX ? l : -1;
 }
 int fps_log2x(int ny) { return ny == N14 ? 14 : fps_log2(ny); }
+
+// (r6) the inverse transform storing only a masked domain's cells (the register-fed transforms: 1024 <= ny <= 8192,
+// a power of two); false where that build is not there
+bool fps_idct_mask_ok(int ny) {
+    const int l = fps_log2(ny);
+    return FPS_REGIO && FPS_LR == 4 && FPS_ISTAGE && l >= 10 && l <= 13;
+}
+int launch_fps_idct_masked(const double* in, double* out, int nrows, int ny, int ld, const double* tw, const double* wk,
+                           hipStream_t st, const int32_t* fcm) {
+    if (!fps_idct_mask_ok(ny)) return -1;
+    switch (fps_log2(ny)) {
+    case 10: dct_pair<10>(true, in, nullptr, out, nrows, ld, tw, wk, st, -1, fcm); break;
+    case 11: dct_pair<11>(true, in, nullptr, out, nrows, ld, tw, wk, st, -1, fcm); break;
+    case 12: dct_pair<12>(true, in, nullptr, out, nrows, ld, tw, wk, st, -1, fcm); break;
+    case 13: dct_pair<13>(true, in, nullptr, out, nrows, ld, tw, wk, st, -1, fcm); break;
+    default: return -1;
+    }
+    return 0;
+}
 
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
                    const double* tw, const double* wk, hipStream_t st, int oe_pair, const double* tw8) {

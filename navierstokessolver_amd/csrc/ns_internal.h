@@ -402,6 +402,11 @@ int fps_log2(int ny);
 // b_{n-2} / 2, FpsArgs::outE); -1: none
 // (r5) ny = 16384 (fps_log2x): each row pair as two 8192-point transforms in one launch (tw8: the 8192-point
 // twiddles); ny <= 8192: tw8 unused
+// (r6) the inverse transform writing only the FC_IN cells of `fcm` (a masked domain's solution into phi, the rest
+// of `out` untouched); -1 where unsupported (fps_idct_mask_ok)
+bool fps_idct_mask_ok(int ny);
+int launch_fps_idct_masked(const double* in, double* out, int nrows, int ny, int ld, const double* tw, const double* wk,
+                           hipStream_t st, const int32_t* fcm);
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
                    const double* tw, const double* wk, hipStream_t st, int oe_pair = -1, const double* tw8 = nullptr);
 // (r5) log2(ny) also for ny = 16384 (the two-half transforms of launch_fps_dct), else as fps_log2

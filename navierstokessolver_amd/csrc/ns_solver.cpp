@@ -1810,7 +1810,7 @@ int mg_precond(ns_solver* s, double* q, double*& z, double*& scratch, int* tn = 
 // applies the mean projection P to r, v and t (KV_INIT / KV_V / KV_T), so p and s -- the vectors handed
 // here -- inherit both properties
 int fps_scan(ns_solver* s, bool backward);
-int fps_precond(ns_solver* s, const double* q, double* z, double* scratch) {
+int fps_precond(ns_solver* s, const double* q, double* z, double* scratch, const int32_t* omask = nullptr) {
     const nsg::Geo& g = s->g;
     // ((r5) a masked domain whose box has the E outflow: its row pair transformed eliminated, as the channel's)
     if (nsg::launch_fps_dct(false, q, nullptr, scratch, g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st,
@@ -1823,6 +1823,13 @@ int fps_precond(ns_solver* s, const double* q, double* z, double* scratch) {
     nsg::launch_fps_mid(s->fa, scratch, s->st);
     CHK(fps_scan(s, true));
     nsg::launch_fps_t2b(s->fa, scratch, s->st);
+    if (omask) {   // (r6: z's masked-domain cells only)
+        if (nsg::launch_fps_idct_masked(scratch, z, g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st, omask) < 0) {
+            set_err("direct Poisson preconditioner: no masked inverse transform for ny = %d", g.ny);
+            return NS_EINVAL;
+        }
+        return 0;
+    }
     nsg::launch_fps_dct(true, scratch, nullptr, z, g.nxl, g.ny, g.ld, s->fps_tw, s->fps_wk, s->st);
     return 0;
 }
@@ -1831,14 +1838,17 @@ int fps_precond(ns_solver* s, const double* q, double* z, double* scratch) {
 // interface's dense m x m solve -- z1 = L_box^+ q, y = (C + 1 1^T / m)^-1 D^T z1, z = L_box^+ (q - D_w y).  q is mean-
 // free over the domain and 0 outside it (the residual k_bicg_vec's KV_INIT leaves); it is modified at the
 // interface cells and restored to 0 outside (its domain values are rewritten by the next KV_INIT)
-int cap_solve(ns_solver* s, double* q, double* z) {
+// (r6) xout: the second box solve writes the solution's domain cells straight into xout (its other cells kept) --
+// the x = z pass of a solve from zero (k_cap_axpy, 57 us at 4096^2) not needed
+int cap_solve(ns_solver* s, double* q, double* z, double* xout = nullptr) {
     CHK(fps_precond(s, q, z, s->kv[8]));
     if (nsg::launch_cap_gemv(s->cap, z, s->st) != hipSuccess) {
         set_err("capacitance solve: k_cap_gemv launch failed (%d interface faces)", s->cap.m + s->cap.border);
         return NS_EHIP;
     }
     nsg::launch_cap_scatter(s->cap, q, 0, s->st);
-    CHK(fps_precond(s, q, z, s->kv[8]));
+    if (xout) CHK(fps_precond(s, q, xout, s->kv[8], s->g.fc));
+    else CHK(fps_precond(s, q, z, s->kv[8]));
     nsg::launch_cap_scatter(s->cap, q, 1, s->st);
     return 0;
 }
@@ -2039,8 +2049,14 @@ int bicgstab(ns_solver* s, const KrylovSolve& ks, int* its, double* res) {
         const bool check = !s->in_step || fps_checks_next(s);
         if (s->in_step) s->fps_solves++;
         for (;;) {
-            CHK(cap_solve(s, a.r, s->kv[6]));
-            nsg::launch_cap_axpy(s->g, s->cap, a.x, s->kv[6], its0 == 0, s->st);
+            // (the first from x = 0 without a border row: the solution's domain cells written straight into x)
+            const bool direct_x = its0 == 0 && !s->cap.border && nsg::fps_idct_mask_ok(s->g.ny) && !s->fa.outE;
+            if (direct_x) {
+                CHK(cap_solve(s, a.r, s->kv[6], a.x));
+            } else {
+                CHK(cap_solve(s, a.r, s->kv[6]));
+                nsg::launch_cap_axpy(s->g, s->cap, a.x, s->kv[6], its0 == 0, s->st);
+            }
             if (!check) {
                 *its = 1;
                 *res = -1.0;
