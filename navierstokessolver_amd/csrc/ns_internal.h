@@ -173,6 +173,9 @@ void launch_reduce_sum(const double* p, int n, int nv, double* out, hipStream_t 
 // nseg contiguous segments of n partials -> out[0..nseg) (k_reduce_sum's order per segment)
 void launch_reduce_sum_segs(const double* p, int n, int nseg, double* out, hipStream_t st);
 // min/max: partials are (umin, -umax, vmin, -vmax) per block -> out[4] = mins of each
+// (r6) launch_reduce_sum (ps) and launch_reduce_min (pm) in one launch
+void launch_reduce_sum_min(const double* ps, int ns, int nvs, double* outs, const double* pm, int nm, int nvm,
+                           double* outm, hipStream_t st);
 void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t st);
 // Poisson prep: from sums (S, S2) and N -> shift = S/N, out[1] = S2 - S^2/N (= ||b||^2)
 // one rank: launch_reduce_sum (nv = 2) + launch_finish_mean in one launch

@@ -4002,9 +4002,8 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
 
 
 // ---------------------------------------------------------------- reductions
-__global__ __launch_bounds__(1024) void k_reduce_sum(const double* __restrict__ p, int n, int nv,
-                                                     double* __restrict__ out) {
-    __shared__ double sh[1024];
+__device__ __forceinline__ void reduce_sum_body(const double* __restrict__ p, int n, int nv, double* __restrict__ out,
+                                                double* sh) {
     for (int v = 0; v < nv; v++) {
         double s = 0.0;
         for (int k = threadIdx.x; k < n; k += 1024) s += p[(size_t)k * nv + v];
@@ -4017,6 +4016,11 @@ __global__ __launch_bounds__(1024) void k_reduce_sum(const double* __restrict__ 
         if (threadIdx.x == 0) out[v] = sh[0];
         __syncthreads();
     }
+}
+__global__ __launch_bounds__(1024) void k_reduce_sum(const double* __restrict__ p, int n, int nv,
+                                                     double* __restrict__ out) {
+    __shared__ double sh[1024];
+    reduce_sum_body(p, n, nv, out, sh);
 }
 
 // nseg contiguous segments of n partials -> out[seg]: one launch instead of nseg, each segment
@@ -4039,11 +4043,10 @@ __global__ __launch_bounds__(1024) void k_reduce_sum_segs(const double* __restri
     }
 }
 
-__global__ __launch_bounds__(1024) void k_reduce_min(const double* __restrict__ p, int n, int nv,
-                                                     double* __restrict__ out) {
+__device__ __forceinline__ void reduce_min_body(const double* __restrict__ p, int n, int nv, double* __restrict__ out,
+                                                double (*sh)[4]) {
     // all nv (<= 4) minima in one pass: per-thread registers, a wave's shuffles, the 16 waves'
     // results through LDS (2 barriers instead of 11 per value; fmin is order-independent)
-    __shared__ double sh[16][4];
     double m[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
     for (int k = threadIdx.x; k < n; k += 1024)
 #pragma unroll
@@ -4063,6 +4066,19 @@ __global__ __launch_bounds__(1024) void k_reduce_min(const double* __restrict__ 
         for (int w = 1; w < 16; w++) r = fmin(r, sh[w][threadIdx.x]);
         out[threadIdx.x] = r;
     }
+}
+__global__ __launch_bounds__(1024) void k_reduce_min(const double* __restrict__ p, int n, int nv,
+                                                     double* __restrict__ out) {
+    __shared__ double sh[16][4];
+    reduce_min_body(p, n, nv, out, sh);
+}
+// (r6) k_reduce_sum and k_reduce_min of two partial sets in one launch (workgroup 0 / 1): K1' leaves both
+__global__ __launch_bounds__(1024) void k_reduce_sum_min(const double* __restrict__ ps, int ns, int nvs,
+                                                         double* __restrict__ outs, const double* __restrict__ pm,
+                                                         int nm, int nvm, double* __restrict__ outm) {
+    __shared__ double sh[1024];
+    if (blockIdx.x == 0) reduce_sum_body(ps, ns, nvs, outs, sh);
+    else reduce_min_body(pm, nm, nvm, outm, reinterpret_cast<double (*)[4]>(sh));
 }
 
 // one rank: k_reduce_sum of the (sum, sum^2) partials and k_finish_mean in one launch (no
@@ -6031,6 +6047,10 @@ void launch_reduce_sum_segs(const double* p, int n, int nseg, double* out, hipSt
 }
 void launch_reduce_min(const double* p, int n, int nv, double* out, hipStream_t st) {
     NS_LAUNCH(k_reduce_min, dim3(1), dim3(1024), 0, st, p, n, nv, out);
+}
+void launch_reduce_sum_min(const double* ps, int ns, int nvs, double* outs, const double* pm, int nm, int nvm,
+                           double* outm, hipStream_t st) {
+    NS_LAUNCH(k_reduce_sum_min, dim3(2), dim3(1024), 0, st, ps, ns, nvs, outs, pm, nm, nvm, outm);
 }
 void launch_reduce_sum_mean(const double* p, int n, double* sums, double ncells, double* out, hipStream_t st) {
     NS_LAUNCH(k_reduce_sum_mean, dim3(1), dim3(1024), 0, st, p, n, sums, ncells, out);

@@ -3387,8 +3387,12 @@ int rhs(ns_solver* s, bool defer_norm = false) {
         std::swap(s->arr[NS_ARR_V], s->arr[NS_ARR_TMPV]);
         s->corr_pend = 0;
         s->corr_k1 = 1;
-        nsg::launch_reduce_min(mm, nb, 4, s->scal + S_MM, s->st);
         s->cu_ext = 0;
+        if (nb < 0) return nb;
+        if (t) CHK(t_end(s, s->kev[0], s->kev[1]));
+        // (the min / max and ||RHS||^2 partials in one launch; one rank: no bus, no all-reduce)
+        nsg::launch_reduce_sum_min(s->part, nb, 2, s->scal + S_HBN, mm, nb, 4, s->scal + S_MM, s->st);
+        return 0;
     } else {
         const HaloReq r[3] = {{&s->g, s->arr[NS_ARR_U], 2}, {&s->g, s->arr[NS_ARR_V], 2}, {&s->g, s->arr[NS_ARR_PHI], 1}};
         nb = overlapped(s, r, 3, [&]() {
