@@ -801,15 +801,42 @@ __device__ inline double2 ldf0(const FpsArgs& a, const double* f, int li, int k0
 // dependent chain of divisions; one row in flight at a time left the passes at 3 TB/s)
 struct ChunkRows {
     double pw[FPS_M], pe[FPS_M], pem[FPS_M];
+    // (r6) branch-free, rows past the chunk's end clamped onto its last (their values unused): a per-row
+    // `t < rows` branch serialised the loads -- one scalar round trip per row
     __device__ inline void load(const FpsArgs& a, int li0, int rows) {
+        (void)rows;
 #pragma unroll
         for (int t = 0; t < FPS_M; t++) {
-            if (t < rows) {
-                const int gi = a.i0 + li0 + t;
-                pw[t] = a.pw[gi];
-                pe[t] = a.pe[gi];
-                pem[t] = gi > 0 ? a.pe[gi - 1] : 0.0;
-            }
+            const int gi = a.i0 + min(li0 + t, a.nxl - 1);
+            pw[t] = a.pw[gi];
+            pe[t] = a.pe[gi];
+            const double pm = a.pe[max(gi - 1, 0)];
+            pem[t] = gi > 0 ? pm : 0.0;
+        }
+    }
+    // (r6) the same values by ONE vector load per wave -- lanes 0-15 pw, 16-31 pe, 32-47 the row before's pe --
+    // and lane reads into scalars: 48 scalar loads waited in small groups cost k_fps_t1b ~9 us.  Every lane of
+    // the wave must run it (call before any divergent branch)
+    __device__ inline void load_wave(const FpsArgs& a, int li0) {
+        if constexpr (3 * FPS_M > 64) {   // (a taller chunk, FPS_ROWS A/B builds: the scalar loads)
+            load(a, li0, FPS_M);
+            return;
+        }
+        const int lane = threadIdx.x & 63, t = lane % FPS_M, kind = lane / FPS_M;
+        const int gi = a.i0 + min(li0 + t, a.nxl - 1);
+        const int gk = kind == 2 ? max(gi - 1, 0) : gi;
+        const double* src = kind == 0 ? a.pw : a.pe;
+        double v = kind < 3 ? src[gk] : 0.0;
+        if (kind == 2 && gi == 0) v = 0.0;
+        const int lo = __double2loint(v), hi = __double2hiint(v);
+        auto rd = [&](int l) {
+            return __hiloint2double(__builtin_amdgcn_readlane(hi, l), __builtin_amdgcn_readlane(lo, l));
+        };
+#pragma unroll
+        for (int q = 0; q < FPS_M; q++) {
+            pw[q] = rd(q);
+            pe[q] = rd(FPS_M + q);
+            pem[q] = rd(2 * FPS_M + q);
         }
     }
 };
@@ -1059,7 +1086,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2(FpsArgs a, double* __rest
         double2 yv[FPS_M];   // f, then the exact forward values in place
 #pragma unroll
         for (int t = 0; t < FPS_M; t++)
-            if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0, s0);
+            yv[t] = ldf0(a, f, min(li0 + t, a.nxl - 1), k0, s0);   // (r6: unconditional, clamped: pipelined)
         const double2 y0 = ld2(a.gc + (size_t)grp * a.ld + k0);
         double y[2] = {y0.x, y0.y};
         for (int q = grp * FPS_G; q < c; q++) {
@@ -1194,16 +1221,16 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t1b(FpsArgs a, const double*
     const int li0 = c * FPS_M;
     const int rows = k0 < a.ny ? min(FPS_M, a.nxl - li0) : 0;
     double E[2] = {0.0, 0.0}, P[2] = {1.0, 1.0};
+    ChunkRows cr;
+    cr.load_wave(a, li0);   // (every lane, before the divergent branch)
     if (rows > 0) {
         const double mu[2] = {a.mu[k0], a.mu[k0 + 1]};
         const double2 r0 = ld2(a.rp0 + (size_t)c * a.ld + k0);
         const double s0 = mode0_shift(a, k0, f);
-        ChunkRows cr;
-        cr.load(a, li0, rows);
         double2 yv[FPS_M], rv[FPS_M];
 #pragma unroll
         for (int t = 0; t < FPS_M; t++)
-            if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0, s0);
+            yv[t] = ldf0(a, f, min(li0 + t, a.nxl - 1), k0, s0);   // (r6: unconditional, clamped: pipelined)
         double r[2] = {r0.x, r0.y};
         const int pb = fps_prow_block(a);
         const bool fast = pb < a.nx;
@@ -1261,21 +1288,33 @@ __global__ void __launch_bounds__(64) k_fps_mid(FpsArgs a, const double* __restr
     const double2 y0 = ld2(a.gc + (size_t)grp * a.ld + k0);
     double Y[2] = {y0.x, y0.y};
     double BX[FPS_G][2], BR[FPS_G][2];
+    // (r6) every chunk's loads first (clamped chunk index): inside the uniform `c < nch` branch below they were
+    // issued chunk by chunk behind the carry's dependent chain
+    double2 le[FPS_G], lp[FPS_G], lb[FPS_G], lbe[FPS_G], lbr[FPS_G];
+#pragma unroll
+    for (int w = 0; w < FPS_G; w++) {
+        const int c = min(grp * FPS_G + w, a.nch - 1);
+        le[w] = ld2(a.ca + (size_t)c * a.ld + k0);
+        lp[w] = ld2(a.ca + (size_t)(a.nch + c) * a.ld + k0);
+        lb[w] = ld2(a.cb + (size_t)c * a.ld + k0);
+        lbe[w] = ld2(a.bt + (size_t)c * a.ld + k0);
+        lbr[w] = ld2(a.bt + (size_t)(a.nch + c) * a.ld + k0);
+    }
 #pragma unroll
     for (int w = 0; w < FPS_G; w++) {
         const int c = grp * FPS_G + w;
         BX[w][0] = BX[w][1] = 0.0;
         BR[w][0] = BR[w][1] = 1.0;
         if (c < a.nch) {
-            double2 e = ld2(a.ca + (size_t)c * a.ld + k0);
-            const double2 pp = ld2(a.ca + (size_t)(a.nch + c) * a.ld + k0);
-            double2 bl = ld2(a.cb + (size_t)c * a.ld + k0);
+            double2 e = le[w];
+            const double2 pp = lp[w];
+            double2 bl = lb[w];
             if (a.m0e && k0 == 0) {   // (r5, the deferred mean: t1b's mode 0 saw b's raw coefficients)
                 const double sft = a.ny * *a.m0s;
                 e.x -= sft * a.m0e[c];
                 bl.x -= sft * a.m0b[c];
             }
-            const double2 be = ld2(a.bt + (size_t)c * a.ld + k0), br = ld2(a.bt + (size_t)(a.nch + c) * a.ld + k0);
+            const double2 be = lbe[w], br = lbr[w];
             if (!a.mid_local) st2(a.ya + (size_t)c * a.ld + k0, Y[0], Y[1]);
             BX[w][0] = fma(be.x, Y[0], bl.x);
             BX[w][1] = fma(be.y, Y[1], bl.y);
@@ -1309,14 +1348,14 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
     const int grp = blockIdx.y, c = grp * FPS_G + w;
     const int li0 = c * FPS_M;
     const int rows = k0 < a.ny ? min(FPS_M, a.nxl - li0) : 0;
+    ChunkRows cr;
+    cr.load_wave(a, li0);   // (every lane, before the divergent return)
     if (rows <= 0) return;
     const double s0 = mode0_shift(a, k0);
-    ChunkRows cr;
-    cr.load(a, li0, rows);
     double2 yv[FPS_M];
 #pragma unroll
     for (int t = 0; t < FPS_M; t++)
-        if (t < rows) yv[t] = ldf0(a, f, li0 + t, k0, s0);
+        yv[t] = ldf0(a, f, min(li0 + t, a.nxl - 1), k0, s0);   // (r6: unconditional, clamped: pipelined)
     const double2 yin = ld2(a.ya + (size_t)c * a.ld + k0);
     const double2 x0 = ld2(a.gx + (size_t)grp * a.ld + k0);
     double X[2] = {x0.x, x0.y};

@@ -1610,11 +1610,14 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
                             (int)blockIdx.x - A.nsblk, A.uo, A.vo, CORR ? A.mm + 4 * A.nstr : nullptr);
         return;
     }
-    __shared__ double rcs[4][K1_LMAX + 2 * RC_K1 + 2][4];   // per row: hx, 1/hx, 2/(h_{i-1}+h_i), 2/(h_i+h_{i+1})
+    // per row: hx, 1/hx, 2/(h_{i-1}+h_i), 2/(h_i+h_{i+1}); (r6, CORR) + GradP's face weights fwx, fex -- read per row by
+    // the folded correction, as global (scalar) loads they put a memory round trip into every row step
+    constexpr int RCW = CORR ? 6 : 4;
+    __shared__ double rcs[4][K1_LMAX + 2 * RC_K1 + 2][RCW];
     const int lane = threadIdx.x & 63;
     const int nstr = A.nsj * A.P.nrun;
     const int w = xcd_swizzle(blockIdx.x, A.nsblk) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    double (*rc)[4] = rcs[threadIdx.x >> 6];
+    double (*rc)[RCW] = rcs[threadIdx.x >> 6];
     const int run = w / A.nsj, sj = w - run * A.nsj;
     const int wid = (A.P.pbase + run) * A.nsj + sj;
     int ib, ie;
@@ -1626,6 +1629,10 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
             rc[t][1] = c.rhx[gi];
             rc[t][2] = c.rsx[gi];
             rc[t][3] = c.rsx[gi + 1];
+            if constexpr (CORR) {
+                rc[t][4] = c.fwx[gi];
+                rc[t][5] = c.fex[gi];
+            }
         }
     }
     __syncthreads();
@@ -1677,11 +1684,13 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
         double2 PH0 = {0, 0}, PH1 = {0, 0}, PH2 = {0, 0};
         double E1 = 0.0, E2 = 0.0;
         const bool cs0 = c0 > 0, cn0 = c0 < ny - 1, cs1 = c0 + 1 > 0, cn1 = c0 + 1 < ny - 1;
+        const double hyc = c.hy[0];
         auto corr_row = [&](double2& qu, double2& qv, int r) {
             const int gi = g.i0 + min(max(r, rlo), rhi);
-            const int gq = min(max(gi, 0), g.nx - 1);
             const bool hW = gi > 0, hE = gi < g.nx - 1;
-            const double fw = c.fwx[gq], fe = c.fex[gq], hx = c.hx[gq], hy = c.hy[0];
+            // (the row table: row r is entry r - ib + RC_K1, the same clamped row)
+            const double* rq = rc[r - ib + RC_K1];
+            const double fw = rq[CORR ? 4 : 0], fe = rq[CORR ? 5 : 0], hx = rq[0], hy = hyc;
             double pl = lane_up1(PH1.y), pr = lane_dn1(PH1.x);
             if (lane == 0) pl = E1;
             if (lane == 63) pr = E1;
