@@ -634,23 +634,31 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_idct(const doubl
 #pragma unroll
                 for (int r = 0; r < 16; r++) z[pz(tid + r * T)] = v[r];
                 __syncthreads();
+                if (fcm) {   // (r6, a masked domain's solution: its cells only, the rest of `out` kept; codes loaded first)
+                    int2 ca[8], cb[8];
 #pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const int m = tid + q * T;   // columns 2m (v_m) and 2m + 1 (v_{N-1-m})
-                    const cplx e = z[pz(m)], o = z[pz(N - 1 - m)];
-                    if (fcm) {   // (r6, a masked domain's solution: its cells only, the rest of `out` kept)
-                        const int2 ca = *reinterpret_cast<const int2*>(fcm + (size_t)r0 * ld + 2 * m);
-                        if (ca.x & FC_IN) oa[2 * m] = e.x * rn;
-                        if (ca.y & FC_IN) oa[2 * m + 1] = o.x * rn;
-                        if (two) {
-                            const int2 cb = *reinterpret_cast<const int2*>(fcm + (size_t)(r0 + 1) * ld + 2 * m);
-                            if (cb.x & FC_IN) ob[2 * m] = -e.y * rn;
-                            if (cb.y & FC_IN) ob[2 * m + 1] = -o.y * rn;
-                        }
-                        continue;
+                    for (int q = 0; q < 8; q++) {
+                        const int m = tid + q * T;
+                        ca[q] = *reinterpret_cast<const int2*>(fcm + (size_t)r0 * ld + 2 * m);
+                        cb[q] = *reinterpret_cast<const int2*>(fcm + (size_t)(two ? r0 + 1 : r0) * ld + 2 * m);
                     }
-                    st2(oa + 2 * m, e.x * rn, o.x * rn);
-                    if (two) st2(ob + 2 * m, -e.y * rn, -o.y * rn);
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const int m = tid + q * T;
+                        const cplx e = z[pz(m)], o = z[pz(N - 1 - m)];
+                        if (ca[q].x & FC_IN) oa[2 * m] = e.x * rn;
+                        if (ca[q].y & FC_IN) oa[2 * m + 1] = o.x * rn;
+                        if (two && (cb[q].x & FC_IN)) ob[2 * m] = -e.y * rn;
+                        if (two && (cb[q].y & FC_IN)) ob[2 * m + 1] = -o.y * rn;
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const int m = tid + q * T;   // columns 2m (v_m) and 2m + 1 (v_{N-1-m})
+                        const cplx e = z[pz(m)], o = z[pz(N - 1 - m)];
+                        st2(oa + 2 * m, e.x * rn, o.x * rn);
+                        if (two) st2(ob + 2 * m, -e.y * rn, -o.y * rn);
+                    }
                 }
             } else {
 #pragma unroll

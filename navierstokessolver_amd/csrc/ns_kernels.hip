@@ -1605,18 +1605,22 @@ template <bool NT, int SK, bool UY = false, bool CORR = false>
 __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
     const Geo& g = A.g;
     const Coef& c = A.c;
-    if ((int)blockIdx.x >= A.nsblk) {   // the wall ring's workgroups, beside the strips (block-uniform)
+    // the wall ring's workgroups, after the strips' (block-uniform).  (r6: the ring's workgroups first measured
+    // 12 us slower, 305.5 vs 293.3 us on one box -- they then hold resident slots the strips' one round needs;
+    // without the ring -- a timing probe, wrong results -- K1' took 331 vs 338 us: the ring is ~7 us of it)
+    if ((int)blockIdx.x >= A.nsblk) {
         rhs_ring_body<CORR>(g, c, A.dt, A.re, A.u, A.v, A.phi, A.cu, A.cv, A.ru, A.rv, A.part + 2 * A.nstr, A.R,
                             (int)blockIdx.x - A.nsblk, A.uo, A.vo, CORR ? A.mm + 4 * A.nstr : nullptr);
         return;
     }
+    const int sbx = (int)blockIdx.x;
     // per row: hx, 1/hx, 2/(h_{i-1}+h_i), 2/(h_i+h_{i+1}); (r6, CORR) + GradP's face weights fwx, fex -- read per row by
     // the folded correction, as global (scalar) loads they put a memory round trip into every row step
     constexpr int RCW = CORR ? 6 : 4;
     __shared__ double rcs[4][K1_LMAX + 2 * RC_K1 + 2][RCW];
     const int lane = threadIdx.x & 63;
     const int nstr = A.nsj * A.P.nrun;
-    const int w = xcd_swizzle(blockIdx.x, A.nsblk) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = xcd_swizzle(sbx, A.nsblk) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double (*rc)[RCW] = rcs[threadIdx.x >> 6];
     const int run = w / A.nsj, sj = w - run * A.nsj;
     const int wid = (A.P.pbase + run) * A.nsj + sj;
