@@ -3246,9 +3246,9 @@ constexpr int BAND_NSW = 3;   // sweeps per launch: a 6-cell cone, within the sl
 // (par + gi + j0) parity: uniform over the workgroup (every pair starts on an even column,
 // every segment on an even row), so there is no divergence.  One barrier per half-sweep: a
 // half-sweep reads only the other colour (stable) and publishes its own cells.
-// (BTT tile, NSW sweeps, SEGT rows per thread, NTH threads; REGC: the row coefficients in
-// registers -- off for the 6-sweep tile, whose 512 threads must fit 128 VGPRs for 2 workgroups a CU)
-template <int BTT, int NSW, int SEGT, int NTH, bool REGC>
+// (r6, k_helm_band6's body: BTT tile, NSW sweeps, SEGT rows per thread, NTH threads; the relaxation weights
+// formed at each update -- the 512 threads must fit 128 VGPRs for 2 workgroups a CU)
+template <int BTT, int NSW, int SEGT, int NTH>
 __device__ __forceinline__ void helm_band_body(const BandArgs& a, double* smem) {
     constexpr int R = 2 * NSW, E = BTT + 2 * R, NP = E / 2, SEG = SEGT, NSEG = E / SEG;
     constexpr int CO = (E + 63) / 64 * 64;   // the column tables' loaders: threads CO .. CO + E - 1
@@ -3308,22 +3308,10 @@ __device__ __forceinline__ void helm_band_body(const BandArgs& a, double* smem) 
     }
     __syncthreads();
     const double alpha = a.alpha, omega = a.omega;
-    // this thread's coefficients and relaxation weights (0 on held cells)
-    // (!REGC: the weights are formed at each update instead -- same expression, same value)
-    constexpr int NW = REGC ? SEG : 1;
-    double2 w[NW];
-    double rcw[NW], rce[NW], rd[NW];
+    // this thread's column coefficients; the row's and the relaxation weight (0 on held cells: k_helm_band's
+    // expression) at each update
     const double ccs0 = cl[c0][0], ccn0 = cl[c0][1], ccd0 = cl[c0][2];
     const double ccs1 = cl[c0 + 1][0], ccn1 = cl[c0 + 1][1], ccd1 = cl[c0 + 1][2];
-    if constexpr (REGC) {
-#pragma unroll
-        for (int s = 0; s < NW; s++) {
-            const int r = r0 + s, gi = gib + r;
-            rcw[s] = rw[r][0]; rce[s] = rw[r][1]; rd[s] = rw[r][2];
-            w[s].x = (jin[0] && in_band(gi, jj[0], nx, ny, a.bw)) ? omega * rcp_nr(diag<1>(rd[s], ccd0, alpha)) : 0.0;
-            w[s].y = (jin[1] && in_band(gi, jj[1], nx, ny, a.bw)) ? omega * rcp_nr(diag<1>(rd[s], ccd1, alpha)) : 0.0;
-        }
-    }
     const int cpar = (gib + jb) & 1;   // colour parity of staged (0, 0)
     for (int h = 0; h < 2 * NSW; h++) {
         const int par = h & 1;                   // red ((gi + j) even), black, ...
@@ -3340,16 +3328,9 @@ __device__ __forceinline__ void helm_band_body(const BandArgs& a, double* smem) 
                 const double xm = s > 0 ? (e ? v[s - 1].y : v[s - 1].x) : sp[r - 1][cc];
                 const double xp = s < SEG - 1 ? (e ? v[s + 1].y : v[s + 1].x) : sp[r + 1][cc];
                 double rr;
-                const int sr = REGC ? s : 0;
-                const double cws = REGC ? rcw[sr] : rw[r][0], ces = REGC ? rce[sr] : rw[r][1];
-                const double rds = REGC ? rd[sr] : rw[r][2];
-                double wc;
-                if constexpr (REGC) {
-                    wc = e ? w[sr].y : w[sr].x;
-                } else {
-                    wc = ((e ? jin[1] : jin[0]) && in_band(gib + r, e ? jj[1] : jj[0], nx, ny, a.bw))
-                             ? omega * rcp_nr(diag<1>(rds, e ? ccd1 : ccd0, alpha)) : 0.0;
-                }
+                const double cws = rw[r][0], ces = rw[r][1], rds = rw[r][2];
+                const double wc = ((e ? jin[1] : jin[0]) && in_band(gib + r, e ? jj[1] : jj[0], nx, ny, a.bw))
+                                      ? omega * rcp_nr(diag<1>(rds, e ? ccd1 : ccd0, alpha)) : 0.0;
                 if (e == 0) {
                     const double ym = sp[r][cc - 1], yp = v[s].y;
                     v[s].x = relax<1>(v[s].x, xm, xp, ym, yp, bq[s].x, cws, ces, ccs0, ccn0,
@@ -3507,7 +3488,7 @@ constexpr int BAND6_BT = 64, BAND6_E = BAND6_BT + 24;
 constexpr int BAND6_LDS = (BAND6_E * BAND6_E + 6 * BAND6_E) * 8;
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_helm_band6(BandArgs a) {
     extern __shared__ double smem6[];
-    helm_band_body<BAND6_BT, 6, 8, 512, false>(a, smem6);
+    helm_band_body<BAND6_BT, 6, 8, 512>(a, smem6);
 }
 
 // the band cells of each tile: qb -> out (an odd number of band launches ends in the scratch plane)
@@ -4759,8 +4740,6 @@ static inline dim3 cell_grid(const Geo& g) { return dim3((g.ny + 63) / 64, (g.nx
 // partial) per 64 x 4*rows cells instead of per 256; still >= 2048 blocks per launch
 static inline int cell_rows(const Geo& g) {
     const long blocks = (long)((g.ny + 63) / 64) * ((g.nxl + 3) / 4);
-    static const int ov = getenv("NSGPU_CELL_ROWS") ? std::atoi(getenv("NSGPU_CELL_ROWS")) : 0;   // (A/B)
-    if (ov > 0) return std::min(ov, 16);
     return (int)std::min(16L, std::max(1L, blocks / 2048));
 }
 static inline dim3 cell_grid(const Geo& g, int rows) {
