@@ -372,6 +372,9 @@ __device__ inline double dpp_dn1(double x) {   // lane l <- lane l + 1
                             __builtin_amdgcn_update_dpp(lo, lo, 0x130, 0xf, 0xf, false));
 }
 
+#ifndef FPS_DB
+#define FPS_DB 4   // column pairs whose loads k_fps_dct_div issues before their arithmetic (A/B: 8)
+#endif
 struct FpsDivArgs {
     Geo g;
     Coef c;
@@ -483,7 +486,7 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
         if constexpr (NC % T == 0) {
             // (N >= 128: every lane has NC / T column pairs; their loads issued in batches of 4 before the
             // arithmetic -- one HBM latency per batch instead of two per column pair)
-            constexpr int NCT = NC / T, B = NCT < 4 ? NCT : 4;
+            constexpr int NCT = NC / T, B = NCT < FPS_DB ? NCT : FPS_DB;
 #pragma unroll
             for (int c0 = 0; c0 < NCT; c0 += B) {
                 double2 U[B][4], Vv[B][2];
@@ -560,6 +563,202 @@ __global__ void __launch_bounds__(Fft<LOGN>::T) FPS_WAVES k_fps_dct_div(FpsDivAr
             }
         }
         __syncthreads();   // (z is rewritten by the next pair)
+    }
+}
+
+// (1'') (r6) the same forward transform with K3 fused, ONE row per workgroup: the row's N reals
+// in Makhoul's order v as the N/2-point complex sequence y_m = v_2m + i v_2m+1, Y = FFT_{N/2}(y) by radix-8
+// Stockham stages (N/16 threads), then V_k = E_k + e^{-2 pi i k / N} O_k and V_{k+N/2} = E_k - e^{-2 pi i k / N} O_k
+// with E_k = (Y_k + conj Y_{N/2-k}) / 2, O_k = (Y_k - conj Y_{N/2-k}) / 2i the even / odd samples' spectra, and
+// X_k = Re(e^{-i pi k / 2N} V_k) as before.  Half the LDS of the row pair's transform (32 KiB at N = 4096) and
+// half its registers per thread: 4 workgroups of 4 waves per CU instead of 2.  The divergence arithmetic is
+// k_fps_dct_div's (b identical); the sums go out per row (slot 2 p + h: 2 np partials).  Not for a NEUMANN
+// outflow E side (its last row is transformed against the row above: k_fps_dct_div keeps it)
+template <int LOGN>
+struct RFft {
+    static constexpr int N = 1 << LOGN, M = N / 2, T = M / 8;
+};
+template <int LOGN, int R>
+__device__ inline void rfft_stage(cplx* z, const cplx* __restrict__ tw, int tid, int Ns) {
+    constexpr int N = 1 << LOGN, M = N / 2, T = RFft<LOGN>::T, NB = M / R, BPT = NB / T;
+    static_assert(NB % T == 0, "rfft stage layout");
+    cplx v[BPT][R];
+#pragma unroll
+    for (int b = 0; b < BPT; b++) {
+        const int jb = tid + b * T;
+#pragma unroll
+        for (int r = 0; r < R; r++) v[b][r] = z[pz(jb + r * NB)];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < BPT; b++) {
+        const int jb = tid + b * T;
+        const int k = jb & (Ns - 1);
+        if (Ns > 1) {
+            const cplx w = tw[k * (N / (Ns * R))];   // e^{-2 pi i k / (Ns R)} from the N-point table
+            cplx wr = w;
+#pragma unroll
+            for (int r = 1; r < R; r++) {
+                v[b][r] = cmul(v[b][r], wr);
+                if (r + 1 < R) wr = cmul(wr, w);
+            }
+        }
+        dft<R>(v[b]);
+        const int d = (jb - k) * R + k;
+#pragma unroll
+        for (int r = 0; r < R; r++) z[pz(d + r * Ns)] = v[b][r];
+    }
+    __syncthreads();
+}
+
+template <int LOGN>
+__global__ void __launch_bounds__(RFft<LOGN>::T) k_fps_dct_div_r(FpsDivArgs A) {
+    constexpr int N = 1 << LOGN, M = N / 2, T = RFft<LOGN>::T, LOGM = LOGN - 1;
+    constexpr int NCT = M / T, B = NCT < 4 ? NCT : 4;   // column pairs per thread (8), loads batched by 4
+    extern __shared__ cplx z[];
+    __shared__ double red[T / 64][2];
+    const Geo& g = A.g;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int ld = A.ld;
+    // workgroup -> (pair q, its row h); consecutive rows on one XCD (their shared u* rows in its L2)
+    const int G = gridDim.x, bx = blockIdx.x;
+    const int un = G % 8 == 0 ? (bx % 8) * (G / 8) + bx / 8 : bx;
+    const int p = A.plo + (un >> 1) * A.pstep, r = 2 * p + (un & 1);
+    if (r >= A.nrows) {   // (an odd slab's last pair has one row: zero sums for the other)
+        if (tid == 0) A.part[2 * r] = A.part[2 * r + 1] = 0.0;
+        return;
+    }
+    const int gi = g.i0 + r;
+    const bool hW = gi > 0, hE = gi < g.nx - 1;
+    const double* u0 = A.u + (ptrdiff_t)(r - 1) * ld;
+    const double* va = A.v + (ptrdiff_t)r * ld;
+    const double rhy = A.c.rhy[1], hrdt = 0.5 * A.rdt, rhx = A.c.rhx[gi];
+    double* zd = reinterpret_cast<double*>(z);
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int c0 = 0; c0 < NCT; c0 += B) {
+        double2 U[B][3], V[B];
+        double E[B][2];
+#pragma unroll
+        for (int q = 0; q < B; q++) {
+            const int j = 2 * (tid + (c0 + q) * T);
+#pragma unroll
+            for (int k = 0; k < 3; k++) U[q][k] = ld2(u0 + k * ld + j);
+            V[q] = ld2(va + j);
+            E[q][0] = va[max(j - 1, 0)];                   // (lane 0's west neighbour)
+            E[q][1] = va[min(j + 2, g.ny - 1)];            // (lane 63's east neighbour)
+        }
+#pragma unroll
+        for (int q = 0; q < B; q++) {
+            const int cb = tid + (c0 + q) * T, j = 2 * cb;
+            double vs = dpp_up1(V[q].y), vn = dpp_dn1(V[q].x);
+            if (lane == 0) vs = E[q][0];
+            if (lane == 63 || cb + 1 >= M) vn = E[q][1];
+            double d[2];
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const int jj = j + e;
+                const bool sa = jj > 0, na = jj < g.ny - 1;
+                const double uc = e ? U[q][1].y : U[q][1].x, uwv = e ? U[q][0].y : U[q][0].x,
+                             uev = e ? U[q][2].y : U[q][2].x;
+                const double vc = e ? V[q].y : V[q].x;
+                const double vsv = e ? V[q].x : vs, vnv = e ? vn : V[q].y;
+                const double X = hE ? uev : fv_ghost(g, uc, 1, 0), Y = hW ? uwv : fv_ghost(g, uc, 0, 0);
+                const double Xn = na ? vnv : fv_ghost(g, vc, 3, 1), Ys = sa ? vsv : fv_ghost(g, vc, 2, 1);
+                d[e] = fma(X - Y, rhx, (Xn - Ys) * rhy) * hrdt;
+            }
+            acc0 += d[0] + d[1];
+            acc1 += d[0] * d[0] + d[1] * d[1];
+            if (A.b) st2(A.b + (ptrdiff_t)r * ld + j, d[0], d[1]);
+            // x_2cb = v_cb -> y_{cb/2} (re / im by cb's parity); x_{2cb+1} = v_{N-1-cb} -> y_{(N-1-cb)/2}
+            const int n1 = N - 1 - cb;
+            zd[2 * pz(cb >> 1) + (cb & 1)] = d[0];
+            zd[2 * pz(n1 >> 1) + (n1 & 1)] = d[1];
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        acc0 += __shfl_xor(acc0, off, 64);
+        acc1 += __shfl_xor(acc1, off, 64);
+    }
+    if (lane == 0) {
+        red[tid >> 6][0] = acc0;
+        red[tid >> 6][1] = acc1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int w = 0; w < T / 64; w++) {
+            s0 += red[w][0];
+            s1 += red[w][1];
+        }
+        A.part[2 * r] = s0;
+        A.part[2 * r + 1] = s1;
+    }
+    int Ns = 1;
+#pragma unroll
+    for (int st = 0; st < LOGM / 3; st++) {
+        rfft_stage<LOGN, 8>(z, A.tw, tid, Ns);
+        Ns *= 8;
+    }
+    if constexpr (LOGM % 3 != 0) rfft_stage<LOGN, (1 << (LOGM % 3))>(z, A.tw, tid, Ns);
+    double* oa = A.out + (size_t)r * ld;
+#pragma unroll
+    for (int q = 0; q < M / T; q++) {
+        const int k = tid + q * T;
+        const cplx Yk = z[pz(k)], Ym = z[pz((M - k) & (M - 1))];
+        const cplx Ek{0.5 * (Yk.x + Ym.x), 0.5 * (Yk.y - Ym.y)};
+        const cplx Ok{0.5 * (Yk.y + Ym.y), 0.5 * (Ym.x - Yk.x)};
+        const cplx tO = cmul(A.tw[k], Ok);
+        const cplx V0 = cadd(Ek, tO), V1 = csub(Ek, tO);
+        const cplx w0 = A.wk[k], w1 = A.wk[k + M];
+        oa[k] = fma(w0.x, V0.x, -w0.y * V0.y);
+        oa[k + M] = fma(w1.x, V1.x, -w1.y * V1.y);
+    }
+}
+
+// (3'') (r6) the inverse of ONE row per workgroup (k_fps_dct_div_r's layout backwards): V is Hermitian (v real), so
+// with V_k = e^{i pi k / 2N} (X_k - i X_{N-k}), E_k = (V_k + V_{k+N/2}) / 2, O_k = (V_k - V_{k+N/2}) e^{2 pi i k / N} / 2
+// (the even / odd samples' spectra), y = IFFT_{N/2}(E + i O) holds v_2m + i v_2m+1 -- one N/2-point transform
+// (conj(FFT(conj .)) / (N/2)) instead of a row pair's N-point one; each lane stores columns 2 cb, 2 cb + 1
+template <int LOGN>
+__global__ void __launch_bounds__(RFft<LOGN>::T) k_fps_idct_r(const double* __restrict__ in, double* __restrict__ out,
+                                                              int nrows, int ld, const cplx* __restrict__ tw,
+                                                              const cplx* __restrict__ wk) {
+    constexpr int N = 1 << LOGN, M = N / 2, T = RFft<LOGN>::T, LOGM = LOGN - 1;
+    extern __shared__ cplx z[];
+    const int tid = threadIdx.x;
+    const int r = nrows - 1 - (int)blockIdx.x;   // (as k_fps_idct's pass order: up the slab)
+    const double* a = in + (size_t)r * ld;
+#pragma unroll
+    for (int q = 0; q < M / T; q++) {
+        const int k = tid + q * T;
+        const double xa = a[k], ya = k ? a[N - k] : 0.0, xb = a[k + M], yb = a[M - k];
+        const cplx w0 = wk[k], w1 = wk[k + M], t = tw[k];   // e^{-i pi k / 2N}, e^{-i pi (k + M) / 2N}, e^{-2 pi i k / N}
+        const double c0 = w0.x, s0 = -w0.y, c1 = w1.x, s1 = -w1.y;
+        const cplx Va{fma(c0, xa, s0 * ya), fma(s0, xa, -c0 * ya)};
+        const cplx Vb{fma(c1, xb, s1 * yb), fma(s1, xb, -c1 * yb)};
+        const cplx Ek{0.5 * (Va.x + Vb.x), 0.5 * (Va.y + Vb.y)};
+        const cplx Ok = cmul(cplx{0.5 * (Va.x - Vb.x), 0.5 * (Va.y - Vb.y)}, cplx{t.x, -t.y});
+        z[pz(k)] = cplx{Ek.x - Ok.y, -(Ek.y + Ok.x)};   // conj(E + i O)
+    }
+    __syncthreads();
+    int Ns = 1;
+#pragma unroll
+    for (int st = 0; st < LOGM / 3; st++) {
+        rfft_stage<LOGN, 8>(z, tw, tid, Ns);
+        Ns *= 8;
+    }
+    if constexpr (LOGM % 3 != 0) rfft_stage<LOGN, (1 << (LOGM % 3))>(z, tw, tid, Ns);
+    constexpr double rm = 1.0 / M;
+    double* o = out + (size_t)r * ld;
+    const double* zd = reinterpret_cast<const double*>(z);
+#pragma unroll
+    for (int q = 0; q < M / T; q++) {
+        const int cb = tid + q * T, n1 = N - 1 - cb;
+        // y_m = conj(Z_m) / M: v_2m = Z_m.x / M, v_2m+1 = -Z_m.y / M; x_2cb = v_cb, x_2cb+1 = v_{N-1-cb}
+        const double e0 = zd[2 * pz(cb >> 1) + (cb & 1)], e1 = zd[2 * pz(n1 >> 1) + (n1 & 1)];
+        st2(o + 2 * cb, (cb & 1) ? -e0 * rm : e0 * rm, (n1 & 1) ? -e1 * rm : e1 * rm);
     }
 }
 
@@ -1413,6 +1612,7 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
     }
 }
 
+bool fps_div_real(int logn, int outE);
 template <int LOGN>
 void dct_pair(bool inverse, const double* in, const double* shift, double* out, int nrows, int ld, const void* tw,
               const void* wk, hipStream_t st, int oe_pair, const int32_t* fcm = nullptr) {
@@ -1422,6 +1622,20 @@ void dct_pair(bool inverse, const double* in, const double* shift, double* out, 
     // round of two per CU (profiles/r06/ab/fpsg_summary.txt); NSGPU_FPS_GRID=n: at most n workgroups (A/B)
     static const int fg = getenv("NSGPU_FPS_GRID") ? std::atoi(getenv("NSGPU_FPS_GRID")) : 0;
     const dim3 grid(std::min((nrows + 1) / 2, fg > 0 ? fg : 1 << 30));
+    if constexpr (LOGN >= 10 && LOGN <= 13) {
+        if (inverse && !fcm && fps_div_real(LOGN, 0)) {   // (r6: one row per workgroup, k_fps_idct_r)
+            const size_t lr = sizeof(cplx) * (size_t)RFft<LOGN>::M;
+            lds_attr_once((const void*)k_fps_idct_r<LOGN>, (int)lr);
+            hipEvent_t a, b;
+            if (take_launch_timing(a, b))
+                hipExtLaunchKernelGGL(k_fps_idct_r<LOGN>, dim3(nrows), dim3(RFft<LOGN>::T), lr, st, a, b, 0, in, out,
+                                      nrows, ld, (const cplx*)tw, (const cplx*)wk);
+            else
+                hipLaunchKernelGGL(k_fps_idct_r<LOGN>, dim3(nrows), dim3(RFft<LOGN>::T), lr, st, in, out, nrows, ld,
+                                   (const cplx*)tw, (const cplx*)wk);
+            return;
+        }
+    }
     if (inverse) {
         lds_attr_once((const void*)k_fps_idct<LOGN>, (int)lds);
         hipEvent_t a, b;
@@ -1441,6 +1655,26 @@ void dct_pair(bool inverse, const double* in, const double* shift, double* out, 
             hipLaunchKernelGGL(k_fps_dct<LOGN>, grid, dim3(T), lds, st, in, shift, out, nrows, ld, (const cplx*)tw,
                                (const cplx*)wk, oe_pair);
     }
+}
+
+// (r6) the one-row-per-workgroup transform (k_fps_dct_div_r): 2 cnt workgroups; NSGPU_FPS_REAL=0: the pairs (A/B)
+bool fps_div_real(int logn, int outE) {
+    const char* e = getenv("NSGPU_FPS_REAL");   // (read per launch: the parity test switches it)
+    return (!e || std::atoi(e) != 0) && !outE && logn >= 10 && logn <= 13;
+}
+template <int LOGN>
+int div_row(const FpsDivArgs& a0, hipStream_t st) {
+    if constexpr (LOGN >= 10 && LOGN <= 13) {
+        constexpr int T = RFft<LOGN>::T;
+        const size_t lds = sizeof(cplx) * (size_t)RFft<LOGN>::M;
+        lds_attr_once((const void*)k_fps_dct_div_r<LOGN>, (int)lds);
+        const dim3 grid(2 * a0.cnt);
+        hipEvent_t a, b;
+        if (take_launch_timing(a, b)) hipExtLaunchKernelGGL(k_fps_dct_div_r<LOGN>, grid, dim3(T), lds, st, a, b, 0, a0);
+        else hipLaunchKernelGGL(k_fps_dct_div_r<LOGN>, grid, dim3(T), lds, st, a0);
+        return (int)grid.x;
+    }
+    return -1;
 }
 
 template <int LOGN>
@@ -1895,9 +2129,22 @@ int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, cons
         a.cnt = std::min(np, 2);
         a.pstep = std::max(np - 1, 1);
     }
+    const int lg = fps_log2(g.ny);
+    if (fps_div_real(lg, outE)) {   // (per-row sums: 2 np partials)
+        if (a.cnt <= 0) return 2 * np;
+        int n = -1;
+        switch (lg) {
+        case 10: n = div_row<10>(a, st); break;
+        case 11: n = div_row<11>(a, st); break;
+        case 12: n = div_row<12>(a, st); break;
+        case 13: n = div_row<13>(a, st); break;
+        default: return -1;
+        }
+        return n < 0 ? -1 : 2 * np;
+    }
     if (a.cnt <= 0) return np;
     int n = -1;
-    switch (fps_log2(g.ny)) {
+    switch (lg) {
     case 4: n = div_pair<4>(a, st); break;
     case 5: n = div_pair<5>(a, st); break;
     case 6: n = div_pair<6>(a, st); break;
@@ -2010,7 +2257,7 @@ __global__ __launch_bounds__(256) void k_cap_rhs(Geo g, const double* __restrict
     const int j = blockIdx.x * 64 + threadIdx.x, li = blockIdx.y * 4 + threadIdx.y;
     if (j >= g.ny || li >= g.nxl) return;
     const ptrdiff_t o = (ptrdiff_t)li * g.ld + j;
-    if (g.fc[o] & FC_IN) r[o] = b[o] - (shift ? shift[0] : 0.0);
+    if (!g.fc || (g.fc[o] & FC_IN)) r[o] = b[o] - (shift ? shift[0] : 0.0);   // (r6: rectangles too)
 }
 
 // set-up: the source w_f d_f of column f in the zeroed plane q (the previous column's cleared; f < 0: only that)

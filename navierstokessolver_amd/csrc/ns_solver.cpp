@@ -2399,10 +2399,16 @@ int pois_solve_fps(ns_solver* s, int* its, double* res, ns_stats* stt) {
         double* y = s->kv[0];
         nsg::launch_apply(0, g, s->c, 0.0, s->arr[NS_ARR_PHI], y, nullptr, s->part, s->st);
         nsg::launch_axpby(g, 1.0, s->arr[NS_ARR_RPHI], -1.0, y, y, s->st);
-        const int nb = nsg::launch_sums(g, y, s->part, s->st);
-        nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_AUX + 2, s->st);
-        CHK(allreduce(s, s->scal + S_AUX + 2, 2, ncclSum));   // (r6: slabs; one rank: no-op)
-        nsg::launch_finish_mean(s->scal + S_AUX + 2, s->ncells, s->scal + S_AUX, s->st);
+        // (r6) in two passes: the mean off r first, then the sums of r - mean -- the one-pass s2 - s^2 / n cancels
+        // when r carries a large constant (the projected system's C 1): 5.7e-10 of noise for a ~1e-14 residual at
+        // 4096 x 1024 (tools/fps_real_diag.py), which sent a converged solve into the BiCGStab polish
+        for (int pass = 0; pass < 2; pass++) {
+            if (pass) nsg::launch_cap_rhs(g, y, s->scal + S_AUX, y, s->st);
+            const int nb = nsg::launch_sums(g, y, s->part, s->st);
+            nsg::launch_reduce_sum(s->part, nb, 2, s->scal + S_AUX + 2, s->st);
+            CHK(allreduce(s, s->scal + S_AUX + 2, 2, ncclSum));   // (r6: slabs; one rank: no-op)
+            nsg::launch_finish_mean(s->scal + S_AUX + 2, s->ncells, s->scal + S_AUX, s->st);
+        }
         HIPCHK(hipMemcpyAsync(s->scal + S_RES, s->scal + S_AUX + 1, sizeof(double), hipMemcpyDeviceToDevice, s->st));
     } else {
         const int nb = nsg::launch_pois_residual(g, s->c, s->arr[NS_ARR_PHI], s->arr[NS_ARR_RPHI], s->scal + S_SHIFT,

@@ -281,6 +281,36 @@ def test_fused_divergence_equals_k3(gpu, monkeypatch, nx, ny):
     assert rel(out["11"][4], ref[4]) <= 1e-11, rel(out["11"][4], ref[4])
 
 
+@pytest.mark.parametrize("nx,ny", [(37, 1024), (300, 2048), (130, 4096), (64, 8192)])
+def test_row_transforms_match_pair_transforms(gpu, monkeypatch, nx, ny):
+    """r6: the one-row real-input transforms (k_fps_dct_div_r: N/2-point FFT of y_m = v_2m +
+    i v_2m+1 with the even / odd split; k_fps_idct_r backwards; default for 1024 <= ny <= 8192) against the
+    row-pair transforms (NSGPU_FPS_REAL=0): a standalone solve's phi (modulo its mean) to 1e-12 of its max, and
+    4 steps (the fused divergence + the inverse inside them) -- u, v to 1e-12, the monitor to 1e-12; both
+    solves' own residual <= 1e-10 (the pair transforms reach 5.2e-11 at 64 x 8192, the row ones 2-3e-11 there:
+    tools/fps_real_diag.py).  An odd nx: the last pair's one row."""
+    out = {}
+    for real in ("0", "1"):
+        monkeypatch.setenv("NSGPU_FPS_REAL", real)
+        gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny), 1.0 / (8 * max(nx, ny)), 1000.0, rtol=1e-10)
+        b = np.random.default_rng(nx + ny).uniform(-1, 1, nx * ny)
+        gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny))
+        gs.set(gpu.NS_ARR_RPHI, b)
+        its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
+        assert its == 1 and res <= 1e-10, (real, its, res)
+        phi = demean(gs.get(gpu.NS_ARR_PHI))
+        gs.close()
+        gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny), 1.0 / (8 * max(nx, ny)), 1000.0, rtol=1e-10)
+        mm = np.array([[st[k] for k in ("umin", "umax", "vmin", "vmax")] for st in (gs.step() for _ in range(4))])
+        u, v, _ = gs.fields()
+        out[real] = (phi, mm, u.ravel(), v.ravel())
+        gs.close()
+    assert rel(out["1"][0], out["0"][0]) <= 1e-12, rel(out["1"][0], out["0"][0])
+    np.testing.assert_allclose(out["1"][1], out["0"][1], atol=1e-12)
+    assert np.max(np.abs(out["1"][2] - out["0"][2])) <= 1e-12
+    assert np.max(np.abs(out["1"][3] - out["0"][3])) <= 1e-12
+
+
 def test_direct_solve_steps_vs_reference_krylov_256(gpu):
     """The GPU's default step (direct Poisson solve, RB-SOR Helmholtz) against the oracle's
     reference-faithful algorithm (OSolver's default: the Krylov solves of the reference's assembled
@@ -473,18 +503,18 @@ def test_outflow_direct_solve_matches_oracle(gpu, nx, ny):
     (2.5 / -2 / 0.5 ghost, FluidSolver.cpp:98-101) eliminated into tridiagonal form per mode, mode 0 in
     the BiCGStab path's projected sense (A x = b + C 1) -- against the oracle's banded-LU solve of the same
     mean-projected system (phi modulo its mean, <= 1e-10 of max|phi|) and its own projected residual
-    ||P (b - A phi)|| <= 1e-11 ||b - mean b|| (the library's check); re-evaluated by the oracle's operator
-    on the host <= 1e-10 (that evaluation's own round-off, ~||A|| ||phi|| eps, reaches 2e-11 at 512 x 64);
-    one 'iteration'."""
+    ||P (b - A phi)|| <= 1e-10 ||b - mean b|| (the library's check -- r6: the projection in two passes; the one-pass
+    s2 - s^2 / n had cancelled to 0 and hidden the solve's ~1e-11 here); re-evaluated by the oracle's operator on
+    the host <= 1e-10; one 'iteration'."""
     rng = np.random.default_rng(nx * 5 + ny)
     h = 4.0 / nx
     og = OGrid.rectangle(nx, ny, lx=4.0, ly=ny * h, bc=BC_CHANNEL)
-    gs = _channel(gpu, nx, ny, rtol=1e-11)
+    gs = _channel(gpu, nx, ny, rtol=1e-10)
     b = rng.uniform(-100, 100, nx * ny)
     gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny))
     gs.set(gpu.NS_ARR_RPHI, b)
     its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
-    assert its == 1 and res <= 1e-11, (its, res)
+    assert its == 1 and res <= 1e-10, (its, res)
     g = demean(gs.get(gpu.NS_ARR_PHI))
     gs.close()
     xk, _ = og.solve_poisson(b)
@@ -495,19 +525,21 @@ def test_outflow_direct_solve_matches_oracle(gpu, nx, ny):
 
 
 def test_outflow_direct_solve_equals_krylov_at_size(gpu, monkeypatch):
-    """The bench's channel grid (4096 x 1024): the direct solve against the GPU's BiCGStab path
-    (NSGPU_FPS_OUTFLOW=0, line-closure V-cycle preconditioner) run to rtol 1e-12 on the same rhs:
-    phi modulo its mean <= 1e-9 of its max."""
+    """The bench's channel grid (4096 x 1024): the direct solve (one 'iteration', its own projected residual
+    2.1e-10 here -- r6's two-pass check, tools/fps_real_diag.py -- so at rtol 1e-9) against the GPU's BiCGStab
+    path (NSGPU_FPS_OUTFLOW=0, line-closure V-cycle preconditioner) run to rtol 1e-12 on the same rhs: phi
+    modulo its mean <= 1e-9 of its max."""
     nx, ny = 4096, 1024
     b = np.random.default_rng(3).uniform(-1, 1, nx * ny)
     sol = {}
     for fo in ("1", "0"):
         monkeypatch.setenv("NSGPU_FPS_OUTFLOW", fo)
-        gs = _channel(gpu, nx, ny, rtol=1e-12)
+        rt = 1e-9 if fo == "1" else 1e-12
+        gs = _channel(gpu, nx, ny, rtol=rt)
         gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny))
         gs.set(gpu.NS_ARR_RPHI, b)
         its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
-        assert res <= 1e-12 and ((its == 1) == (fo == "1")), (fo, its, res)
+        assert res <= rt and ((its == 1) == (fo == "1")), (fo, its, res)
         sol[fo] = demean(gs.get(gpu.NS_ARR_PHI))
         gs.close()
     assert rel(sol["1"], sol["0"]) <= 1e-9, rel(sol["1"], sol["0"])
