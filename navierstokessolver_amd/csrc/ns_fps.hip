@@ -1614,6 +1614,18 @@ __global__ void __launch_bounds__(64 * FPS_G) k_fps_t2b(FpsArgs a, double* __res
 
 bool fps_div_real(int logn, int outE);
 template <int LOGN>
+void idct_row(const double* in, double* out, int nrows, int ld, const void* tw, const void* wk, hipStream_t st) {
+    const size_t lr = sizeof(cplx) * (size_t)RFft<LOGN>::M;
+    lds_attr_once((const void*)k_fps_idct_r<LOGN>, (int)lr);
+    hipEvent_t a, b;
+    if (take_launch_timing(a, b))
+        hipExtLaunchKernelGGL(k_fps_idct_r<LOGN>, dim3(nrows), dim3(RFft<LOGN>::T), lr, st, a, b, 0, in, out, nrows,
+                              ld, (const cplx*)tw, (const cplx*)wk);
+    else
+        hipLaunchKernelGGL(k_fps_idct_r<LOGN>, dim3(nrows), dim3(RFft<LOGN>::T), lr, st, in, out, nrows, ld,
+                           (const cplx*)tw, (const cplx*)wk);
+}
+template <int LOGN>
 void dct_pair(bool inverse, const double* in, const double* shift, double* out, int nrows, int ld, const void* tw,
               const void* wk, hipStream_t st, int oe_pair, const int32_t* fcm = nullptr) {
     constexpr int T = Fft<LOGN>::T;
@@ -1624,15 +1636,7 @@ void dct_pair(bool inverse, const double* in, const double* shift, double* out, 
     const dim3 grid(std::min((nrows + 1) / 2, fg > 0 ? fg : 1 << 30));
     if constexpr (LOGN >= 10 && LOGN <= 13) {
         if (inverse && !fcm && fps_div_real(LOGN, 0)) {   // (r6: one row per workgroup, k_fps_idct_r)
-            const size_t lr = sizeof(cplx) * (size_t)RFft<LOGN>::M;
-            lds_attr_once((const void*)k_fps_idct_r<LOGN>, (int)lr);
-            hipEvent_t a, b;
-            if (take_launch_timing(a, b))
-                hipExtLaunchKernelGGL(k_fps_idct_r<LOGN>, dim3(nrows), dim3(RFft<LOGN>::T), lr, st, a, b, 0, in, out,
-                                      nrows, ld, (const cplx*)tw, (const cplx*)wk);
-            else
-                hipLaunchKernelGGL(k_fps_idct_r<LOGN>, dim3(nrows), dim3(RFft<LOGN>::T), lr, st, in, out, nrows, ld,
-                                   (const cplx*)tw, (const cplx*)wk);
+            idct_row<LOGN>(in, out, nrows, ld, tw, wk, st);
             return;
         }
     }
@@ -1660,11 +1664,11 @@ void dct_pair(bool inverse, const double* in, const double* shift, double* out, 
 // (r6) the one-row-per-workgroup transform (k_fps_dct_div_r): 2 cnt workgroups; NSGPU_FPS_REAL=0: the pairs (A/B)
 bool fps_div_real(int logn, int outE) {
     const char* e = getenv("NSGPU_FPS_REAL");   // (read per launch: the parity test switches it)
-    return (!e || std::atoi(e) != 0) && !outE && logn >= 10 && logn <= 13;
+    return (!e || std::atoi(e) != 0) && !outE && logn >= 10 && logn <= 14;
 }
 template <int LOGN>
 int div_row(const FpsDivArgs& a0, hipStream_t st) {
-    if constexpr (LOGN >= 10 && LOGN <= 13) {
+    if constexpr (LOGN >= 10 && LOGN <= 14) {
         constexpr int T = RFft<LOGN>::T;
         const size_t lds = sizeof(cplx) * (size_t)RFft<LOGN>::M;
         lds_attr_once((const void*)k_fps_dct_div_r<LOGN>, (int)lds);
@@ -2071,6 +2075,10 @@ int launch_fps_idct_masked(const double* in, double* out, int nrows, int ny, int
 
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,
                    const double* tw, const double* wk, hipStream_t st, int oe_pair, const double* tw8) {
+    if (ny == N14 && inverse && fps_div_real(14, 0)) {   // (r6: one row per workgroup, 1024 threads)
+        idct_row<14>(in, out, nrows, ld, tw, wk, st);
+        return 0;
+    }
     if (ny == N14) {   // (r5: two 8192-point transforms per row pair)
         if (!tw8) return -1;
         dct14(inverse, in, shift, out, nrows, ld, tw, tw8, wk, st, oe_pair);
@@ -2129,7 +2137,7 @@ int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, cons
         a.cnt = std::min(np, 2);
         a.pstep = std::max(np - 1, 1);
     }
-    const int lg = fps_log2(g.ny);
+    const int lg = g.ny == (1 << 14) ? 14 : fps_log2(g.ny);
     if (fps_div_real(lg, outE)) {   // (per-row sums: 2 np partials)
         if (a.cnt <= 0) return 2 * np;
         int n = -1;
@@ -2138,6 +2146,7 @@ int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, cons
         case 11: n = div_row<11>(a, st); break;
         case 12: n = div_row<12>(a, st); break;
         case 13: n = div_row<13>(a, st); break;
+        case 14: n = div_row<14>(a, st); break;   // (ny = 16384: 128 KiB, one workgroup of 1024 threads per CU)
         default: return -1;
         }
         return n < 0 ? -1 : 2 * np;
@@ -2159,6 +2168,10 @@ int launch_fps_div(const Geo& g, const Coef& c, double dt, const double* u, cons
     }
     return n < 0 ? -1 : np;
 }
+
+// whether the step's divergence can go into the forward transform (launch_fps_div): the row pairs for ny = 2^p <= 8192,
+// the one-row transforms (r6) up to 16384
+bool fps_fuse_ok(int ny, int outE) { return ny == (1 << 14) ? fps_div_real(14, outE) : fps_log2(ny) >= 0; }
 
 void launch_fps_t1(const FpsArgs& a, const double* f, hipStream_t st) {
     hipLaunchKernelGGL(k_fps_t1, dim3((a.ny + 127) / 128, a.ngrp), dim3(64, FPS_G), 0, st, a, f);

@@ -408,6 +408,7 @@ int fps_log2(int ny);
 // (r6) the inverse transform writing only the FC_IN cells of `fcm` (a masked domain's solution into phi, the rest
 // of `out` untouched); -1 where unsupported (fps_idct_mask_ok)
 bool fps_idct_mask_ok(int ny);
+bool fps_fuse_ok(int ny, int outE);   // (r6) the divergence fused into the forward transform (launch_fps_div)
 int launch_fps_idct_masked(const double* in, double* out, int nrows, int ny, int ld, const double* tw, const double* wk,
                            hipStream_t st, const int32_t* fcm);
 int launch_fps_dct(bool inverse, const double* in, const double* shift, double* out, int nrows, int ny, int ld,

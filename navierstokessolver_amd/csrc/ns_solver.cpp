@@ -3882,8 +3882,9 @@ int ns_create(const ns_grid_desc* gd, const ns_params* p, ns_solver** out) {
         if (const char* e = getenv("NSGPU_FPS_CHECK")) s->fps_check = std::max(0, std::atoi(e));
         if (const char* e = getenv("NSGPU_FPS_PASSES")) s->fps_passes = std::atoi(e) == 3 && !s->fa.outE ? 3 : 2;
         if (const char* e = getenv("NSGPU_FPS_FUSE")) s->fps_fuse = std::atoi(e) != 0;
-        // (r5) ny = 16384 (configs[4]): the two-half transforms have no fused K3 form -- K3, then the DCT
-        if (nsg::fps_log2(gd->ny) < 0) s->fps_fuse = false;
+        // (r5) ny = 16384 (configs[4]): the two-half transforms have no fused K3 form -- K3, then the DCT; (r6) the
+        // one-row transform has (fps_fuse_ok)
+        if (!nsg::fps_fuse_ok(gd->ny, s->fa.outE)) s->fps_fuse = false;
         s->fps_xuni = xuni;
         if (!xuni || s->fps_dense) s->fps_fuse = false;   // (r6: K3's general face weights, then the transform)
         if (s->fps) s->phi_extrap = 0;   // (no initial guess: no history planes)

@@ -281,23 +281,25 @@ def test_fused_divergence_equals_k3(gpu, monkeypatch, nx, ny):
     assert rel(out["11"][4], ref[4]) <= 1e-11, rel(out["11"][4], ref[4])
 
 
-@pytest.mark.parametrize("nx,ny", [(37, 1024), (300, 2048), (130, 4096), (64, 8192)])
+@pytest.mark.parametrize("nx,ny", [(37, 1024), (300, 2048), (130, 4096), (64, 8192), (33, 16384)])
 def test_row_transforms_match_pair_transforms(gpu, monkeypatch, nx, ny):
     """r6: the one-row real-input transforms (k_fps_dct_div_r: N/2-point FFT of y_m = v_2m +
-    i v_2m+1 with the even / odd split; k_fps_idct_r backwards; default for 1024 <= ny <= 8192) against the
-    row-pair transforms (NSGPU_FPS_REAL=0): a standalone solve's phi (modulo its mean) to 1e-12 of its max, and
+    i v_2m+1 with the even / odd split; k_fps_idct_r backwards; default for 1024 <= ny <= 16384 -- at 16384 with
+    the divergence fused, which the two-half transforms had not) against the row-pair transforms
+    (NSGPU_FPS_REAL=0): a standalone solve's phi (modulo its mean) to 1e-12 of its max, and
     4 steps (the fused divergence + the inverse inside them) -- u, v to 1e-12, the monitor to 1e-12; both
     solves' own residual <= 1e-10 (the pair transforms reach 5.2e-11 at 64 x 8192, the row ones 2-3e-11 there:
-    tools/fps_real_diag.py).  An odd nx: the last pair's one row."""
+    tools/fps_real_diag.py; 16384: <= 2e-9, the two-half transforms' 1.2e-9 at 33 x 16384).  An odd nx: the last
+    pair's one row."""
     out = {}
     for real in ("0", "1"):
         monkeypatch.setenv("NSGPU_FPS_REAL", real)
-        gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny), 1.0 / (8 * max(nx, ny)), 1000.0, rtol=1e-10)
+        gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny), 1.0 / (8 * max(nx, ny)), 1000.0, rtol=1e-8)
         b = np.random.default_rng(nx + ny).uniform(-1, 1, nx * ny)
         gs.set(gpu.NS_ARR_PHI, np.zeros(nx * ny))
         gs.set(gpu.NS_ARR_RPHI, b)
         its, res = gs.kernel(gpu.NS_K_POIS_SOLVE)[:2]
-        assert its == 1 and res <= 1e-10, (real, its, res)
+        assert its == 1 and res <= (1e-10 if ny <= 8192 else 2e-9), (real, its, res)
         phi = demean(gs.get(gpu.NS_ARR_PHI))
         gs.close()
         gs = gpu.GpuSolver(gpu.rectangle(nx, ny, lx=nx / ny), 1.0 / (8 * max(nx, ny)), 1000.0, rtol=1e-10)

@@ -10,7 +10,7 @@ import navierstokessolver_amd as gpu  # noqa: E402
 
 CAV = [(2, 0.0), (2, 1.0), (2, 0.0), (2, 0.0)]
 CHAN = [(0, 1.0), (2, 0.0), (4, 0.0), (2, 0.0)]
-for nx, ny, bc in ((300, 4096, CAV), (1024, 1024, CAV), (4096, 4096, CAV), (128, 8192, CAV), (4096, 1024, CHAN),
+for nx, ny, bc in ((300, 4096, CAV), (1024, 1024, CAV), (4096, 4096, CAV), (128, 8192, CAV), (33, 16384, CAV), (4096, 1024, CHAN),
                    (512, 1024, CHAN)):
     h = 4.0 / nx if bc is CHAN else 1.0 / nx
     g = gpu.rectangle(nx, ny, lx=nx * h, ly=ny * h, bc=bc)
