@@ -578,8 +578,32 @@ template <int LOGN>
 struct RFft {
     static constexpr int N = 1 << LOGN, M = N / 2, T = M / 8;
 };
+#ifndef FPS_RTW
+#define FPS_RTW 1   // the row transforms' stage twiddles loaded up front (RTw), the split's formed by products (A/B: 0)
+// (N <= 8192; at 16384 -- 1024 threads, one workgroup per CU -- they measured slower: 2346 vs 2219 us forward)
+#endif
+// every radix-8 stage's twiddle of this thread's butterfly and the last (radix 2 / 4) stage's, loaded before the row:
+// their latency behind its loads instead of one global round trip per stage between two barriers
+template <int LOGN>
+struct RTw {
+    static constexpr int N = 1 << LOGN, M = N / 2, T = RFft<LOGN>::T, LOGM = LOGN - 1, NS8 = LOGM / 3,
+                         RL = 1 << (LOGM % 3), BL = RL > 1 ? (M / RL) / T : 1;
+    cplx w8[NS8], wl[BL];
+    __device__ inline void load(const cplx* __restrict__ tw, int tid) {
+        int Ns = 1;
+#pragma unroll
+        for (int st = 0; st < NS8; st++) {
+            w8[st] = tw[(tid & (Ns - 1)) * (N / (Ns * 8))];
+            Ns *= 8;
+        }
+        if constexpr (RL > 1) {
+#pragma unroll
+            for (int b = 0; b < BL; b++) wl[b] = tw[((tid + b * T) & (Ns - 1)) * (N / (Ns * RL))];
+        }
+    }
+};
 template <int LOGN, int R>
-__device__ inline void rfft_stage(cplx* z, const cplx* __restrict__ tw, int tid, int Ns) {
+__device__ inline void rfft_stage(cplx* z, const cplx* __restrict__ tw, int tid, int Ns, const cplx* wp = nullptr) {
     constexpr int N = 1 << LOGN, M = N / 2, T = RFft<LOGN>::T, NB = M / R, BPT = NB / T;
     static_assert(NB % T == 0, "rfft stage layout");
     cplx v[BPT][R];
@@ -595,7 +619,7 @@ __device__ inline void rfft_stage(cplx* z, const cplx* __restrict__ tw, int tid,
         const int jb = tid + b * T;
         const int k = jb & (Ns - 1);
         if (Ns > 1) {
-            const cplx w = tw[k * (N / (Ns * R))];   // e^{-2 pi i k / (Ns R)} from the N-point table
+            const cplx w = wp ? wp[b] : tw[k * (N / (Ns * R))];   // e^{-2 pi i k / (Ns R)}: the N-point table
             cplx wr = w;
 #pragma unroll
             for (int r = 1; r < R; r++) {
@@ -676,6 +700,15 @@ __global__ void __launch_bounds__(RFft<LOGN>::T) k_fps_dct_div_r(FpsDivArgs A) {
             zd[2 * pz(n1 >> 1) + (n1 & 1)] = d[1];
         }
     }
+    // (the transform's twiddles now, after the row's registers are free: all stages' in one round trip, behind the
+    // partial sums' barrier)
+    RTw<LOGN> W;
+    cplx t0{1.0, 0.0}, w0s{1.0, 0.0};
+    if constexpr (FPS_RTW && LOGN <= 13) {
+        W.load(A.tw, tid);
+        t0 = A.tw[tid];    // the split's e^{-2 pi i k / N}, e^{-i pi k / 2N} at k = tid; k = tid + q T by products
+        w0s = A.wk[tid];
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         acc0 += __shfl_xor(acc0, off, 64);
@@ -698,10 +731,10 @@ __global__ void __launch_bounds__(RFft<LOGN>::T) k_fps_dct_div_r(FpsDivArgs A) {
     int Ns = 1;
 #pragma unroll
     for (int st = 0; st < LOGM / 3; st++) {
-        rfft_stage<LOGN, 8>(z, A.tw, tid, Ns);
+        rfft_stage<LOGN, 8>(z, A.tw, tid, Ns, (FPS_RTW && LOGN <= 13) ? &W.w8[st] : nullptr);
         Ns *= 8;
     }
-    if constexpr (LOGM % 3 != 0) rfft_stage<LOGN, (1 << (LOGM % 3))>(z, A.tw, tid, Ns);
+    if constexpr (LOGM % 3 != 0) rfft_stage<LOGN, (1 << (LOGM % 3))>(z, A.tw, tid, Ns, (FPS_RTW && LOGN <= 13) ? W.wl : nullptr);
     double* oa = A.out + (size_t)r * ld;
 #pragma unroll
     for (int q = 0; q < M / T; q++) {
@@ -709,9 +742,13 @@ __global__ void __launch_bounds__(RFft<LOGN>::T) k_fps_dct_div_r(FpsDivArgs A) {
         const cplx Yk = z[pz(k)], Ym = z[pz((M - k) & (M - 1))];
         const cplx Ek{0.5 * (Yk.x + Ym.x), 0.5 * (Yk.y - Ym.y)};
         const cplx Ok{0.5 * (Yk.y + Ym.y), 0.5 * (Ym.x - Yk.x)};
-        const cplx tO = cmul(A.tw[k], Ok);
+        // (FPS_RTW: e^{-2 pi i k / N} = tw[tid] tw[q T], e^{-i pi k / 2N} = wk[tid] wk[q T], e^{-i pi (k + M) / 2N} =
+        // that times wk[M] -- the uniform factors are scalar loads; one rounding more than the table)
+        const cplx tk = (FPS_RTW && LOGN <= 13) ? (q ? cmul(t0, A.tw[q * T]) : t0) : A.tw[k];
+        const cplx tO = cmul(tk, Ok);
         const cplx V0 = cadd(Ek, tO), V1 = csub(Ek, tO);
-        const cplx w0 = A.wk[k], w1 = A.wk[k + M];
+        const cplx w0 = (FPS_RTW && LOGN <= 13) ? (q ? cmul(w0s, A.wk[q * T]) : w0s) : A.wk[k];
+        const cplx w1 = (FPS_RTW && LOGN <= 13) ? cmul(w0, A.wk[M]) : A.wk[k + M];
         oa[k] = fma(w0.x, V0.x, -w0.y * V0.y);
         oa[k + M] = fma(w1.x, V1.x, -w1.y * V1.y);
     }
@@ -730,6 +767,8 @@ __global__ void __launch_bounds__(RFft<LOGN>::T) k_fps_idct_r(const double* __re
     const int tid = threadIdx.x;
     const int r = nrows - 1 - (int)blockIdx.x;   // (as k_fps_idct's pass order: up the slab)
     const double* a = in + (size_t)r * ld;
+    RTw<LOGN> W;
+    if constexpr (FPS_RTW && LOGN <= 13) W.load(tw, tid);
 #pragma unroll
     for (int q = 0; q < M / T; q++) {
         const int k = tid + q * T;
@@ -746,10 +785,10 @@ __global__ void __launch_bounds__(RFft<LOGN>::T) k_fps_idct_r(const double* __re
     int Ns = 1;
 #pragma unroll
     for (int st = 0; st < LOGM / 3; st++) {
-        rfft_stage<LOGN, 8>(z, tw, tid, Ns);
+        rfft_stage<LOGN, 8>(z, tw, tid, Ns, (FPS_RTW && LOGN <= 13) ? &W.w8[st] : nullptr);
         Ns *= 8;
     }
-    if constexpr (LOGM % 3 != 0) rfft_stage<LOGN, (1 << (LOGM % 3))>(z, tw, tid, Ns);
+    if constexpr (LOGM % 3 != 0) rfft_stage<LOGN, (1 << (LOGM % 3))>(z, tw, tid, Ns, (FPS_RTW && LOGN <= 13) ? W.wl : nullptr);
     constexpr double rm = 1.0 / M;
     double* o = out + (size_t)r * ld;
     const double* zd = reinterpret_cast<const double*>(z);

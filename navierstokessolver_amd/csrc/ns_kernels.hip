@@ -3996,19 +3996,29 @@ __global__ __launch_bounds__(CV_THREADS) void k_coarse_vcycle(Geo g, const doubl
 
 
 // ---------------------------------------------------------------- reductions
+// the 1024 threads' tree sum sh[t] += sh[t + w], w = 512 ... 1, in that pairing: the four levels across waves through
+// the LDS, the last six inside wave 0 by shuffles (the same additions in the same order -- bit-identical to the
+// all-LDS tree -- with 6 barriers fewer per value).  Thread 0's return value is the sum; the LDS can take the next
+// value at once (wave 0 reads only sh[0, 64), which no other wave writes)
+__device__ __forceinline__ double tree_sum_1024(double s, double* sh) {
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 512; w >= 64; w >>= 1) {
+        if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+        __syncthreads();
+    }
+    double x = threadIdx.x < 64 ? sh[threadIdx.x] : 0.0;
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) x += __shfl_down(x, w, 64);
+    return x;
+}
 __device__ __forceinline__ void reduce_sum_body(const double* __restrict__ p, int n, int nv, double* __restrict__ out,
                                                 double* sh) {
     for (int v = 0; v < nv; v++) {
         double s = 0.0;
         for (int k = threadIdx.x; k < n; k += 1024) s += p[(size_t)k * nv + v];
-        sh[threadIdx.x] = s;
-        __syncthreads();
-        for (int w = 512; w > 0; w >>= 1) {
-            if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) out[v] = sh[0];
-        __syncthreads();
+        s = tree_sum_1024(s, sh);
+        if (threadIdx.x == 0) out[v] = s;
     }
 }
 __global__ __launch_bounds__(1024) void k_reduce_sum(const double* __restrict__ p, int n, int nv,
@@ -4026,14 +4036,8 @@ __global__ __launch_bounds__(1024) void k_reduce_sum_segs(const double* __restri
         const double* q = p + (size_t)g * n;
         double s = 0.0;
         for (int k = threadIdx.x; k < n; k += 1024) s += q[k];
-        sh[threadIdx.x] = s;
-        __syncthreads();
-        for (int w = 512; w > 0; w >>= 1) {
-            if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) out[g] = sh[0];
-        __syncthreads();
+        s = tree_sum_1024(s, sh);
+        if (threadIdx.x == 0) out[g] = s;
     }
 }
 
@@ -4085,15 +4089,8 @@ __global__ __launch_bounds__(1024) void k_reduce_sum_mean(const double* __restri
     for (int v = 0; v < 2; v++) {
         double s = 0.0;
         for (int k = threadIdx.x; k < n; k += 1024) s += p[(size_t)k * 2 + v];
-        sh[threadIdx.x] = s;
-        __syncthreads();
-        for (int w = 512; w > 0; w >>= 1) {
-            if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
-            __syncthreads();
-        }
-        r[v] = sh[0];
-        if (threadIdx.x == 0) sums[v] = sh[0];
-        __syncthreads();
+        r[v] = tree_sum_1024(s, sh);   // (thread 0's is the sum)
+        if (threadIdx.x == 0) sums[v] = r[v];
     }
     if (threadIdx.x == 0) {
         const double s = r[0], s2 = r[1];
