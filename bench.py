@@ -76,7 +76,8 @@ KERNELS = {
     "fps_tri": ("k_fps_t1b + scan + k_fps_mid + scan + k_fps_t2b (direct Poisson solve: the tridiagonal "
                 "recurrences along x, one per mode, chunked; five launches timed as one interval)",
                 40 if os.environ.get("NSGPU_FPS_PASSES") == "3" else 24),
-    "fps_idct": ("k_fps_idct (direct Poisson solve: DCT-III of every row pair -> phi)", 16),
+    "fps_idct": ("k_fps_idct_r (direct Poisson solve: DCT-III of every row -> phi, one row per workgroup as an "
+                 "N/2-point complex FFT; k_fps_idct's row pairs outside 1024 <= ny <= 16384)", 16),
     # (r6) K5 (CorrectVelocities + GradP + the min / max monitor): read phi 8 + u*, v* 16, write u, v 16 = 40
     "k5": ("k_cell_s<5> (K5, CorrectVelocities: u = u* - dt grad phi, fused min / max of u, v)", 40),
     # (r6) the Helmholtz wall bands (k_helm_band, 3 RB-SOR sweeps per launch on the cells within 128 of a wall):
@@ -89,8 +90,9 @@ KERNELS = {
 # transform's LDS -- read u*, v* 16 + write the coefficients 8; rhs_phi (8 more) only for a checked solve
 FPS_FUSED = os.environ.get("NSGPU_FPS_FUSE", "1") != "0"
 if FPS_FUSED:
-    KERNELS["fps_dct"] = ("k_fps_dct_div (direct Poisson solve: K3's divergence of u*, v* fused into the DCT-II of "
-                          "every row pair, Stockham FFT in LDS)", 24)
+    KERNELS["fps_dct"] = ("k_fps_dct_div_r (direct Poisson solve: K3's divergence of u*, v* fused into the DCT-II of "
+                          "every row, one row per workgroup -- its N reals as an N/2-point complex FFT, radix-8 "
+                          "Stockham in LDS; k_fps_dct_div's row pairs outside 1024 <= ny <= 16384)", 24)
 # one-launch kernels (the `roofline` candidates; fps_tri is five launches)
 SINGLE_LAUNCH = ("restrict", "prolong", "cycle", "guess", "helmholtz", "rhs", "fps_dct", "fps_idct", "k5", "band")
 JACOBI_LABEL = "k_jacobi_s<double> (one weighted-Jacobi sweep of the Poisson operator, the north star's roofline kernel)"

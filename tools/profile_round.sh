@@ -19,7 +19,7 @@ python3 tools/pmc_summarize.py 4096 $out/fetch $out/write $out/pmc_traffic.json 
   'jacobi_sweep=k_jacobi_s<double=24' 'jacobi_sweep_fp32=k_jacobi_s<float=12' \
   'helmholtz=k_sweep3<(0|3), true=48' 'rhs=k_rhs_s<=64' 'rhs_sc=k_rhs_sc<=88' 'band=k_helm_band=5.8125' \
   'k5=k_cell_s<(5|6)>=40' 'k3=k_cell_s<3>=24' \
-  'fps_dct=k_fps_dct<=16' 'fps_dct_div=k_fps_dct_div<=24' 'fps_idct=k_fps_idct<=16' 'fps_t1b=k_fps_t1b=8' 'fps_t2b=k_fps_t2b=16' 'fps_mid=k_fps_mid=0.5'
+  'fps_dct=k_fps_dct<=16' 'fps_dct_div=k_fps_dct_div(_r)?<=24' 'fps_idct=k_fps_idct(_r)?<=16' 'fps_t1b=k_fps_t1b=8' 'fps_t2b=k_fps_t2b=16' 'fps_mid=k_fps_mid=0.5'
 # (one rank's Helmholtz residual pass is the two-field launch k_sweep3<FUSE_UV = 3>: 2 x 24 B/cell; the
 # bench's helmholtz roofline is per component, so the entry is halved)
 python3 - $out/pmc_traffic.json <<'PY'
@@ -33,4 +33,4 @@ json.dump(d, open(sys.argv[1], "w"), indent=1)
 PY
 python3 tools/pmc_summarize.py --valu 4096 $out/valu $out/valu_per_cell.json 'rhs=k_rhs_s<' 'helmholtz=k_sweep3<(0|3), true' \
   'restrict=k_sweep2<0, false, 1' 'prolong=k_sweep2<0, (true|false), 2' 'cycle=k_sweep4' 'k5=k_cell_s<(5|6)>' 'k3=k_cell_s<3>' \
-  'fps_dct=k_fps_dct<' 'fps_dct_div=k_fps_dct_div<' 'fps_idct=k_fps_idct<' 'fps_t1b=k_fps_t1b' 'fps_t2b=k_fps_t2b' 'fps_mid=k_fps_mid'
+  'fps_dct=k_fps_dct<' 'fps_dct_div=k_fps_dct_div(_r)?<' 'fps_idct=k_fps_idct(_r)?<' 'fps_t1b=k_fps_t1b' 'fps_t2b=k_fps_t2b' 'fps_mid=k_fps_mid'
