@@ -578,6 +578,12 @@ template <int LOGN>
 struct RFft {
     static constexpr int N = 1 << LOGN, M = N / 2, T = M / 8;
 };
+#ifndef FPS_RB
+#define FPS_RB 4   // k_fps_dct_div_r: column pairs whose loads are issued before their arithmetic (A/B: 8)
+#endif
+#ifndef FPS_RE
+#define FPS_RE 0   // k_fps_dct_div_r: the wave-edge neighbours loaded by the edge lanes only (A/B: 1)
+#endif
 #ifndef FPS_RTW
 #define FPS_RTW 1   // the row transforms' stage twiddles loaded up front (RTw), the split's formed by products (A/B: 0)
 // (N <= 8192; at 16384 -- 1024 threads, one workgroup per CU -- they measured slower: 2346 vs 2219 us forward)
@@ -638,7 +644,7 @@ __device__ inline void rfft_stage(cplx* z, const cplx* __restrict__ tw, int tid,
 template <int LOGN>
 __global__ void __launch_bounds__(RFft<LOGN>::T) k_fps_dct_div_r(FpsDivArgs A) {
     constexpr int N = 1 << LOGN, M = N / 2, T = RFft<LOGN>::T, LOGM = LOGN - 1;
-    constexpr int NCT = M / T, B = NCT < 4 ? NCT : 4;   // column pairs per thread (8), loads batched by 4
+    constexpr int NCT = M / T, B = NCT < FPS_RB ? NCT : FPS_RB;   // column pairs per thread (8), loads batched by 4
     extern __shared__ cplx z[];
     __shared__ double red[T / 64][2];
     const Geo& g = A.g;
@@ -669,8 +675,8 @@ __global__ void __launch_bounds__(RFft<LOGN>::T) k_fps_dct_div_r(FpsDivArgs A) {
 #pragma unroll
             for (int k = 0; k < 3; k++) U[q][k] = ld2(u0 + k * ld + j);
             V[q] = ld2(va + j);
-            E[q][0] = va[max(j - 1, 0)];                   // (lane 0's west neighbour)
-            E[q][1] = va[min(j + 2, g.ny - 1)];            // (lane 63's east neighbour)
+            if (FPS_RE == 0 || lane == 0) E[q][0] = va[max(j - 1, 0)];                      // (lane 0's west neighbour)
+            if (FPS_RE == 0 || lane == 63 || j + 2 >= N) E[q][1] = va[min(j + 2, g.ny - 1)];   // (lane 63's east one)
         }
 #pragma unroll
         for (int q = 0; q < B; q++) {

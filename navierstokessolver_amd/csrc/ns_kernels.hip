@@ -3238,6 +3238,9 @@ __device__ __forceinline__ bool in_band(int gi, int j, int nx, int ny, int bw) {
     return gi >= 0 && gi < nx && (gi < bw || gi >= nx - bw || j < bw || j >= ny - bw);
 }
 
+#ifndef BAND_TBL_FIRST
+#define BAND_TBL_FIRST 1   // k_helm_band: the coefficient tables loaded before the tile, unconditionally (A/B: 0)
+#endif
 constexpr int BAND_NSW = 3;   // sweeps per launch: a 6-cell cone, within the slabs' 6 ghost rows
 // Thread layout: the staged E x E region (E = BT + 12 = 44) is cut into 22 column pairs x 11
 // segments of 4 rows; a thread keeps its 8 cells (value, rhs, weight) in registers and meets
@@ -3385,6 +3388,20 @@ __global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
     const bool act = t < NP * NSEG;
     const int kp = act ? t % NP : 0, sg = act ? t / NP : 0;
     const int c0 = 2 * kp, r0 = SEG * sg;          // columns c0, c0 + 1; rows r0 .. r0 + SEG - 1
+    // (r6) the coefficient tables' loads first, unconditional in waves 0 (rows) and 1 (columns), so that they fly
+    // with the tile's: in the branches below they had waited for the tile's loads and then one another (the ISA's
+    // load / s_waitcnt vmcnt(0) pairs), two round trips more before the first barrier
+#if BAND_TBL_FIRST
+    double tb0 = 0.0, tb1 = 0.0, tb2 = 0.0;
+    if (t < 128) {   // (wave-uniform)
+        const bool rowt = t < 64;
+        const int k = t & 63;
+        const int ix = rowt ? min(max(gib + k, 0), nx - 1) : min(max(jb + k, 0), ny - 1);
+        tb0 = (rowt ? a.cw : a.cs)[ix];
+        tb1 = (rowt ? a.ce : a.cn)[ix];
+        tb2 = (rowt ? a.bx : a.by)[ix];
+    }
+#endif
     double2 v[SEG], bq[SEG];
     int jj[2];
     bool jin[2];
@@ -3404,6 +3421,13 @@ __global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
         bq[s].x = b[o + jj[0]];
         bq[s].y = b[o + jj[1]];
     }
+#if BAND_TBL_FIRST
+    if (t < E) {
+        rw[t][0] = tb0; rw[t][1] = tb1; rw[t][2] = tb0 + tb1 + tb2;
+    } else if (t >= 64 && t < 64 + E) {
+        cl[t - 64][0] = tb0; cl[t - 64][1] = tb1; cl[t - 64][2] = tb0 + tb1 + tb2;
+    }
+#else
     if (t < E) {
         const int gi = min(max(gib + t, 0), nx - 1);
         const double cw = a.cw[gi], ce = a.ce[gi];
@@ -3414,6 +3438,7 @@ __global__ __launch_bounds__(256) void k_helm_band(BandArgs a) {
         const double cs = a.cs[j], cn = a.cn[j];
         cl[k][0] = cs; cl[k][1] = cn; cl[k][2] = cs + cn + a.by[j];
     }
+#endif
     if (act) {
 #pragma unroll
         for (int s = 0; s < SEG; s++) { sp[r0 + s][c0] = v[s].x; sp[r0 + s][c0 + 1] = v[s].y; }
