@@ -1482,13 +1482,20 @@ __global__ __launch_bounds__(256) void k_to_f64(const float* __restrict__ src, d
 __device__ __forceinline__ double fvp(double q, double qn, bool has, double r) {
     return has ? fma(qn, r, q * (1.0 - r)) : 0.5 * (q + q);
 }
+// (r6, A/B) hx, hy: CORR_H(1 / h, h) -- CORR_RCP=1 takes the reciprocal tables' 1 / hx, 1 / hy, a product instead of
+// the IEEE division (four per cell pair); measured no faster (K1' 342 vs 343 us, K5 140 vs 137), so the default keeps
+// the division and its bits
+#ifndef CORR_RCP
+#define CORR_RCP 0
+#endif
+#define CORR_H(r, h) (CORR_RCP ? (r) : (h))
 __device__ __forceinline__ void corr1(double us, double vs, double pc, double pw, double pe, double ps, double pn,
                                       bool hW, bool hE, bool hS, bool hN, double fw, double fe, double fs, double fn,
                                       double hx, double hy, double dt, double& u, double& v) {
     const double V0 = fvp(pc, pw, hW, fw), V1 = fvp(pc, pe, hE, fe);
     const double V2 = fvp(pc, ps, hS, fs), V3 = fvp(pc, pn, hN, fn);
-    u = fma(-dt, (V1 - V0) / hx, us);
-    v = fma(-dt, (V3 - V2) / hy, vs);
+    u = fma(-dt, CORR_RCP ? (V1 - V0) * hx : (V1 - V0) / hx, us);
+    v = fma(-dt, CORR_RCP ? (V3 - V2) * hy : (V3 - V2) / hy, vs);
 }
 // the same at cell (li, j) from global loads (K1's wall ring; a rectangle without NEUMANN sides)
 __device__ __forceinline__ void corr_at(const Geo& g, const Coef& c, double dt, const double* __restrict__ us,
@@ -1500,8 +1507,8 @@ __device__ __forceinline__ void corr_at(const Geo& g, const Coef& c, double dt, 
     const double pc = phi[o];
     const double pw = hW ? phi[o - ld] : pc, pe = hE ? phi[o + ld] : pc;
     const double ps = hS ? phi[o - 1] : pc, pn = hN ? phi[o + 1] : pc;
-    corr1(us[o], vs[o], pc, pw, pe, ps, pn, hW, hE, hS, hN, c.fwx[gi], c.fex[gi], c.fsy[j], c.fny[j], c.hx[gi],
-          c.hy[j], dt, u, v);
+    corr1(us[o], vs[o], pc, pw, pe, ps, pn, hW, hE, hS, hN, c.fwx[gi], c.fex[gi], c.fsy[j], c.fny[j],
+          CORR_H(c.rhx[gi], c.hx[gi]), CORR_H(c.rhy[j], c.hy[j]), dt, u, v);
 }
 
 // the ring of k_rhs_s (below): the slab's cells within two rows of the W / E walls (whole rows),
@@ -1596,6 +1603,14 @@ __device__ __forceinline__ void rhs_ring_body(const Geo& g, const Coef& c, doubl
     if (CORR) block_reduce_min<4>(amm, mm + 4 * blk);
 }
 
+// (r6, A/B, measured and not kept: K1' 342-347 us with both against 338 without, same box,
+// profiles/r06/ab/k1_loop_*_summary.txt -- the drain is not what bounds K1', its bytes are)
+#ifndef K1_UR6
+#define K1_UR6 0
+#endif
+#ifndef K1_QE_ALL
+#define K1_QE_ALL 0
+#endif
 constexpr int K1_LMAX = 128;      // k_rhs_s: rows per strip at most (one resident round of strips)
 #ifndef K1_ESPLIT
 #define K1_ESPLIT 4               // (r5) k_rhs_s: rows per run of the edge bands after a slab's exchange (0: one run)
@@ -1679,7 +1694,9 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
             if (CORR) {
                 const int lp = min(max(r + 1, rlo), rhi);
                 qp = *reinterpret_cast<const double2*>(A.phi + (ptrdiff_t)lp * ld + lc);
-                if (lane == 0 || lane == 63) qe = A.phi[(ptrdiff_t)lp * ld + ce];
+                // (r6, A/B K1_QE_ALL=1: every lane loads -- the branch-free form; with K1_UR6 it removes the loop head's
+                // s_waitcnt vmcnt(0), which measured no faster)
+                if (K1_QE_ALL || lane == 0 || lane == 63) qe = A.phi[(ptrdiff_t)lp * ld + ce];
             }
         };
         // CORR: phi^n rows r-1 .. r+1 (PH0..PH2) and the edge lanes' outer values of rows r, r+1 (E1, E2); the
@@ -1688,13 +1705,13 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
         double2 PH0 = {0, 0}, PH1 = {0, 0}, PH2 = {0, 0};
         double E1 = 0.0, E2 = 0.0;
         const bool cs0 = c0 > 0, cn0 = c0 < ny - 1, cs1 = c0 + 1 > 0, cn1 = c0 + 1 < ny - 1;
-        const double hyc = c.hy[0];
+        const double hyc = CORR_H(c.rhy[0], c.hy[0]);
         auto corr_row = [&](double2& qu, double2& qv, int r) {
             const int gi = g.i0 + min(max(r, rlo), rhi);
             const bool hW = gi > 0, hE = gi < g.nx - 1;
             // (the row table: row r is entry r - ib + RC_K1, the same clamped row)
             const double* rq = rc[r - ib + RC_K1];
-            const double fw = rq[CORR ? 4 : 0], fe = rq[CORR ? 5 : 0], hx = rq[0], hy = hyc;
+            const double fw = rq[CORR ? 4 : 0], fe = rq[CORR ? 5 : 0], hx = CORR_H(rq[1], rq[0]), hy = hyc;
             double pl = lane_up1(PH1.y), pr = lane_dn1(PH1.x);
             if (lane == 0) pl = E1;
             if (lane == 63) pr = E1;
@@ -1845,12 +1862,19 @@ __device__ __forceinline__ void rhs_s_body(const RhsStreamArgs& A) {
             load(r0 + q, QU[q], QV[q], QC[q], QD[q], QP[CORR ? q : 0], QE[CORR ? q : 0]);
             asm volatile("" ::: "memory");
         }
-        for (int r = r0; r <= r1; r += SK) {
+        // (r6, A/B K1_UR6=1, CORR) 3 SK rows per iteration: the correction's phi rows rotate with period 3 (PH0 <- PH1
+        // <- PH2 <- qp), so a 2-row body ends on register copies of the rows just loaded -- an s_waitcnt vmcnt(0) at the
+        // loop head that drains the row pipeline every two rows; 6 rows bring every register home.  Not the default:
+        // K1' measured 342-347 us with it against 338 without (same box) -- the row loop is bandwidth-bound, not
+        // drain-bound
+        constexpr int UR = CORR && K1_UR6 ? 3 * SK : SK;
+        for (int r = r0; r <= r1; r += UR) {
 #pragma unroll
-            for (int q = 0; q < SK; q++) {
+            for (int q = 0; q < UR; q++) {
                 // (rows past r1: computed, not stored)
-                step(QU[q], QV[q], QC[q], QD[q], QP[CORR ? q : 0], QE[CORR ? q : 0], r + q);
-                load(r + q + SK, QU[q], QV[q], QC[q], QD[q], QP[CORR ? q : 0], QE[CORR ? q : 0]);
+                const int k = q % SK;
+                step(QU[k], QV[k], QC[k], QD[k], QP[CORR ? k : 0], QE[CORR ? k : 0], r + q);
+                load(r + q + SK, QU[k], QV[k], QC[k], QD[k], QP[CORR ? k : 0], QE[CORR ? k : 0]);
             }
         }
     }
@@ -2087,7 +2111,8 @@ __global__ __launch_bounds__(256) void k_cell_s(CellStreamArgs A) {
                     const double ps = e ? W1.x : ps0, pn = e ? pn1 : W1.y;
                     // (r6: corr1, the expression K1's deferred correction shares)
                     corr1(e ? x.y : x.x, e ? y.y : y.x, pc, pw, pe, ps, pn, hW, hE, e ? s1 : s0, e ? n1 : n0, fw, fe,
-                          e ? fs1 : fs0, e ? fn1 : fn0, hx, e ? hy1 : hy0, A.dt, un[e], vn[e]);
+                          e ? fs1 : fs0, e ? fn1 : fn0, CORR_H(c.rhx[gi], hx), CORR_H(e ? c.rhy[k1] : c.rhy[k0], e ? hy1 : hy0),
+                          A.dt, un[e], vn[e]);
                 }
                 if (wr && v1 && d0 && d1) {
                     st_stream(A.o0 + (ptrdiff_t)m * ld + c0, make_double2(un[0], un[1]), K5_NT);
