@@ -1269,10 +1269,11 @@ __global__ void __launch_bounds__(64 * S) k_fps_scan_seg(int ngrp, int ld, int n
         for (int qb = q0; qb < q1; qb += B) {
             double E[B], P[B];
 #pragma unroll
-            for (int t = 0; t < B; t++) {
-                const int q = qb + t;
-                E[t] = q < q1 ? ge(q) : 0.0;
-                P[t] = q < q1 ? agg[(size_t)(ngrp + gq(q)) * ld + k] : 1.0;
+            for (int t = 0; t < B; t++) {   // (r6: clamped loads, then the select -- no branch around them)
+                const int q = qb + t, qc = min(q, q1 - 1);
+                const double e = ge(qc), pv = agg[(size_t)(ngrp + gq(qc)) * ld + k];
+                E[t] = q < q1 ? e : 0.0;
+                P[t] = q < q1 ? pv : 1.0;
             }
 #pragma unroll
             for (int t = 0; t < B; t++) {
@@ -1303,10 +1304,11 @@ __global__ void __launch_bounds__(64 * S) k_fps_scan_seg(int ngrp, int ld, int n
         for (int qb = q0; qb < q1; qb += B) {
             double E[B], P[B];
 #pragma unroll
-            for (int t = 0; t < B; t++) {
-                const int q = qb + t;
-                E[t] = q < q1 ? ge(q) : 0.0;
-                P[t] = q < q1 ? agg[(size_t)(ngrp + gq(q)) * ld + k] : 1.0;
+            for (int t = 0; t < B; t++) {   // (r6: clamped loads, then the select -- no branch around them)
+                const int q = qb + t, qc = min(q, q1 - 1);
+                const double e = ge(qc), pv = agg[(size_t)(ngrp + gq(qc)) * ld + k];
+                E[t] = q < q1 ? e : 0.0;
+                P[t] = q < q1 ? pv : 1.0;
             }
 #pragma unroll
             for (int t = 0; t < B; t++) {
